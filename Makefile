@@ -1,0 +1,43 @@
+# Build of the MI355X IPv4 fast path (gfx950) and of the test oracle.
+# Everything is built in-tree so the shared objects travel to the GPU box.
+HIPCC ?= /opt/rocm/bin/hipcc
+CC ?= gcc
+ARCH ?= gfx950
+# host code built here runs on the GPU box's host too: portable x86-64-v3
+CFLAGS_HOST = -O3 -march=x86-64-v3 -fPIC -Wall -Wextra -Wno-unused-parameter
+HIPFLAGS = -x hip --offload-arch=$(ARCH) -O3 -fPIC -Wall -Wno-unused-value -Wno-unused-result -std=c++17
+
+CSRC = grout_amd/csrc
+BUILD = build
+LIB_HIP = grout_amd/libgrout_hip.so
+LIB_HOST = grout_amd/libgrout_host.so
+LIB_ORACLE = oracle/liboracle.so
+HDRS = include/grout_hip.h $(CSRC)/fwd4_kernel.h $(CSRC)/fib4.h
+
+all: $(LIB_HIP) $(LIB_HOST) $(LIB_ORACLE)
+
+$(BUILD)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(BUILD)/gr_hip.o: $(CSRC)/gr_hip.cpp $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(BUILD)/fib4.o: $(CSRC)/fib4.c $(CSRC)/fib4.h
+	@mkdir -p $(BUILD)
+	$(CC) $(CFLAGS_HOST) -c -o $@ $<
+
+$(LIB_HIP): $(BUILD)/fwd4_kernel.o $(BUILD)/gr_hip.o $(BUILD)/fib4.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+$(LIB_HOST): $(CSRC)/fib4.c $(CSRC)/synth.c $(CSRC)/fib4.h $(CSRC)/synth.h include/grout_hip.h
+	$(CC) $(CFLAGS_HOST) -shared -o $@ $(CSRC)/fib4.c $(CSRC)/synth.c
+
+$(LIB_ORACLE): oracle/oracle.c oracle/oracle.h include/grout_hip.h
+	$(CC) $(CFLAGS_HOST) -pthread -shared -o $@ oracle/oracle.c
+
+clean:
+	rm -rf $(BUILD) $(LIB_HIP) $(LIB_HOST) $(LIB_ORACLE)
+
+.PHONY: all clean

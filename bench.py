@@ -1,0 +1,231 @@
+# SPDX-License-Identifier: BSD-3-Clause
+"""Headline benchmark: Mpps of IPv4 forwarding, 64 B packets, ~1M-route FIB,
+device-resident, per MI355X (BASELINE.json `metric`, config 3).
+
+A step is one pass of the fused forwarding kernel over one batch of
+synthetic packets already resident in HBM (default 2^24 packets, 64-byte
+slots): iface_input .. iface_output for every packet, header lines written
+out of place so every step sees the same input. Multi-GPU runs are replicas
+(one independent RX stream and FIB replica per GPU, no collective on the data
+path; torch.distributed is used only for the barrier and the max-over-ranks
+clock), so scaling is weak.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+B_PKT = 64 + 8 + 4 + 64 + 8  # algorithmic HBM bytes per packet
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=1 << 24, help="packets per step per GPU")
+    p.add_argument("--workload", default="fullview64", choices=["fullview64", "single64", "imix"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-host-path", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=6.0, help="wall time of the CPU baseline sample")
+    p.add_argument("--cpu-threads", type=int, default=16, help="host cores of the box share (16)")
+    return p.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from grout_amd import abi
+    from grout_amd import synth as S
+    from grout_amd import topology as T
+    from grout_amd.fwd import FastPath
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    # ---- control plane: topology + FIB replica on this GPU
+    t0 = time.time()
+    if args.workload == "single64":
+        topo = T.config_single_route()
+        routes, dst_range = None, (T.ip4("16.1.0.0"), T.ip4("16.1.255.255"))
+        workload = "config2: 64B synthetic burst, 1-route FIB"
+    else:
+        topo = T.config_fullview()
+        routes, dst_range = topo.route_array(), None
+        workload = ("config3: 64B synthetic burst, 1M-route full-view FIB (fib_inject)" if args.workload == "fullview64"
+                    else "config4: IMIX 64/570/1518 synthetic burst, full-view FIB, header lines staged")
+    fp = FastPath(local)
+    fp.load(topo)
+    info = fp.fib_info(T.VRF_MAIN)
+    log(f"[rank {rank}] topology + FIB loaded in {time.time() - t0:.1f}s: {info}")
+
+    # ---- synthetic RX stream of this GPU (seed 0x67721000 + g)
+    n = args.batch
+    seed = S.SEED_GPU_BASE + rank
+    imix = args.workload == "imix"
+    t0 = time.time()
+    frames, meta = S.stream(n, seed, routes=routes, dst_range=dst_range, imix=imix, lines_only=imix)
+    d_in = torch.from_numpy(frames.reshape(-1)).to(dev)
+    d_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
+    d_out = torch.empty(n * abi.LINE, dtype=torch.uint8, device=dev)
+    d_v = torch.empty(n * 8, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] {n} packets generated and resident in {time.time() - t0:.1f}s")
+
+    q = fp.queue(torch.cuda.current_stream(dev).cuda_stream)
+
+    def step():
+        q.submit(d_in, d_out, d_meta, d_v, n, in_stride=abi.LINE, out_stride=abi.LINE, lines_only=imix)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms, kcount = q.kernel_ms(args.steps)
+    tmax = elapsed
+    if world > 1:
+        x = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        tmax = float(x.item())
+
+    edges = torch.bincount(d_v.view(n, 8)[:, 0].long(), minlength=abi.E_COUNT).cpu().numpy()
+    fwd_frac = float(edges[abi.EDGE["port_output"]]) / n
+    value = world * n * args.steps / tmax / 1e6
+    avg_kernel_s = kern_ms / max(kcount, 1) / 1e3
+    achieved = n * B_PKT / avg_kernel_s / 1e9
+
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tf):
+        try:
+            pm = json.load(open(tf))
+            if pm.get("workload") == args.workload and pm.get("batch") == n:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    result = {
+        "metric": "Mpps IPv4 forward, 64B pkts, ~1M-route FIB (device-resident), 1/8 GPU",
+        "value": round(value, 1),
+        "unit": "Mpps",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(tmax / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8/u32 integer",
+        "data": "synthetic (fib_inject route set, seeded 64B UDP stream per GPU)",
+        "config": {
+            "workload": workload,
+            "batch_pkts_per_gpu": n,
+            "routes": int(info["routes"]),
+            "tbl8_groups_used": int(info["tbl8_used"]),
+            "parallelism": f"replicas x{world} (one RX stream + FIB replica per GPU, no collective)",
+            "forwarded_frac": round(fwd_frac, 6),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "bytes_per_pkt": B_PKT,
+            "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),
+        },
+    }
+    if args.workload != "fullview64":
+        result["metric"] = result["metric"] + f" [non-headline workload: {args.workload}]"
+
+    # ---- host-memory path (PCIe-inclusive): reported, never `value`
+    if rank == 0 and world == 1 and not args.no_host_path:
+        hn = min(n, 1 << 23)
+        lines = torch.from_numpy(frames[:hn].reshape(-1)[: hn * abi.LINE]).pin_memory()
+        hmeta = torch.from_numpy(meta[:hn].view(np.uint8)).pin_memory()
+        hout = torch.empty(hn * abi.LINE, dtype=torch.uint8).pin_memory()
+        hv = torch.empty(hn * 8, dtype=torch.uint8).pin_memory()
+        hq = fp.queue()
+        import ctypes
+        fn = fp.lib.gr_hip_fwd4_host
+        fn(hq._h, lines.data_ptr(), hmeta.data_ptr(), hn, hout.data_ptr(), hv.data_ptr())
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r = fn(hq._h, lines.data_ptr(), hmeta.data_ptr(), hn, hout.data_ptr(), hv.data_ptr())
+            abi.check("gr_hip_fwd4_host", r)
+        ht = (time.perf_counter() - t0) / reps
+        hq.close()
+        del ctypes
+        result["host_path"] = {
+            "mpps": round(hn / ht / 1e6, 1),
+            "pkts": hn,
+            "h2d_bytes_per_pkt": abi.LINE + 8,
+            "d2h_bytes_per_pkt": abi.LINE + 8,
+            "note": "header lines + metadata from pinned host memory, chunked H2D/kernel/D2H on 3 streams",
+        }
+
+    # ---- CPU baseline: the oracle restatement on this host's cores
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle
+        o = oracle.Oracle(topo)
+        cf, cm = frames[: 1 << 20].copy(), meta[: 1 << 20].copy()
+        m1, _ = o.bench(cf, cm, 1, 2_000_000)
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        per_thread = int(m1 * 1e6 * args.cpu_seconds)
+        mN, _fwd = o.bench(cf, cm, threads, per_thread)
+        result["cpu_baseline"] = {
+            "value": round(mN, 2),
+            "unit": "Mpps",
+            "cores": threads,
+            "kind": "port",
+            "single_core_mpps": round(m1, 2),
+            "sample": (f"oracle C restatement of grout's node chain (bursts of 64, DIR24_8 8-byte "
+                       f"entries), {threads} pinned threads x {per_thread} packets of the same "
+                       f"1M-packet prefix of this stream"),
+        }
+        o.close()
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    q.close()
+    fp.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,522 @@
+// SPDX-License-Identifier: BSD-3-Clause
+//
+// fwd4_kernel.hip -- the fused IPv4 forwarding kernel for gfx950 (MI355X).
+//
+// One lane per packet. A 256-thread workgroup (4 wave64s) owns a tile of 256
+// packets: their 64-byte header lines are staged into LDS with coalesced
+// 16-byte loads (4 lanes per line), each lane then walks its packet through
+//   iface_input (iface_input.c:52-112) -> eth_input (eth_input.c:35-88)
+//   -> ip_input (ip_input.c:47-197) with the DIR24_8 lookup of fib4_lookup
+//      (route.c:147-167) and group resolution (nexthop.h:89-96)
+//   -> ip_forward (ip_forward.c:14-41) -> ip_output (ip_output.c:122-223)
+//   -> eth_output (eth_output.c:28-77) -> iface_output (iface_output.c:198-255)
+// entirely in registers, and the rewritten lines leave through LDS with
+// coalesced 16-byte stores. Per-iface rx/tx counters are reduced per wave
+// (ballot), per workgroup (LDS slot table) and flushed once per workgroup to
+// a sharded global table. The grid is persistent (<= 8 workgroups per CU) and
+// strides over tiles. No MFMA: this is HBM-bound integer work.
+#include <hip/hip_runtime.h>
+
+#include "fwd4_kernel.h"
+
+#define CHAIN GR_HIP_EDGE_CHAIN
+
+struct ifv { // fields of struct gr_hip_iface the path reads
+	uint32_t id, type, mode, flags, mtu, vrf_id, vlan_id, parent_id;
+	uint32_t mac_lo, mac_hi; // bytes 0-3, 4-5
+	bool mac_ok;
+	bool ok;
+};
+
+// iface_from_id (iface.c:459-466) on the device mirror.
+__device__ __forceinline__ ifv load_iface(const fwd4_params &P, uint32_t id) {
+	ifv r;
+	r.ok = false;
+	if (id == 0 || id >= P.max_ifaces)
+		return r;
+	const uint4 *p = reinterpret_cast<const uint4 *>(P.ifaces + id);
+	uint4 a = p[0];
+	uint2 b = reinterpret_cast<const uint2 *>(p + 1)[0];
+	r.id = a.x & 0xffff;
+	r.ok = r.id == id;
+	r.type = (a.x >> 16) & 0xff;
+	r.mode = a.x >> 24;
+	r.flags = a.y & 0xffff;
+	r.mtu = a.y >> 16;
+	r.vrf_id = a.z & 0xffff;
+	r.vlan_id = a.w & 0xffff;
+	r.parent_id = a.w >> 16;
+	r.mac_lo = b.x;
+	r.mac_hi = b.y & 0xffff;
+	r.mac_ok = ((b.y >> 16) & 0xff) != 0;
+	return r;
+}
+
+struct nhv { // fields of struct gr_hip_nh
+	uint32_t type, state, flags, iface_id, ipv4, mac_lo, mac_hi;
+	uint32_t reta_size, reta_off, single, n_members;
+};
+
+__device__ __forceinline__ nhv load_nh(const fwd4_params &P, uint32_t slot) {
+	const uint4 *p = reinterpret_cast<const uint4 *>(P.nh + slot);
+	uint4 a = p[0];
+	nhv r;
+	r.type = a.x & 0xff;
+	r.state = (a.x >> 8) & 0xff;
+	r.flags = (a.x >> 16) & 0xff;
+	r.iface_id = a.y & 0xffff;
+	r.ipv4 = a.z;
+	r.mac_lo = a.w;
+	uint4 b = p[1];
+	r.mac_hi = b.x & 0xffff;
+	r.reta_size = b.x >> 16;
+	r.reta_off = b.y;
+	r.single = b.z;
+	r.n_members = b.w & 0xffff;
+	return r;
+}
+
+// VLAN sub-interface demux, vlan_get_iface (vlan.c:27-34): open addressing
+// on (parent << 16 | vlan) + 1.
+__device__ __forceinline__ uint32_t vlan_lookup(const fwd4_params &P, uint32_t parent, uint32_t vid) {
+	if (P.vlan_keys == nullptr)
+		return 0;
+	uint32_t key = ((parent << 16) | vid) + 1;
+	uint32_t h = (key * 0x9e3779b1u) & P.vlan_mask;
+	for (uint32_t i = 0; i <= P.vlan_mask; i++) {
+		uint32_t k = P.vlan_keys[h];
+		if (k == key)
+			return P.vlan_vals[h];
+		if (k == 0)
+			return 0;
+		h = (h + 1) & P.vlan_mask;
+	}
+	return 0;
+}
+
+struct stat_slot {
+	uint32_t key; // ((kind << 16) | iface) + 1, 0 = free
+	uint32_t pkts;
+	unsigned long long bytes;
+};
+
+// One lane (the wave leader of a key) adds a wave's contribution.
+__device__ __forceinline__ void slot_add(
+	stat_slot *slots,
+	const fwd4_params &P,
+	uint32_t key,
+	uint32_t pkts,
+	uint32_t bytes
+) {
+	uint32_t h = (key * 0x9e3779b1u) >> 27; // 32 slots
+	for (uint32_t i = 0; i < FWD4_STAT_SLOTS; i++) {
+		uint32_t s = (h + i) & (FWD4_STAT_SLOTS - 1);
+		uint32_t old = atomicCAS(&slots[s].key, 0u, key);
+		if (old == 0 || old == key) {
+			atomicAdd(&slots[s].pkts, pkts);
+			atomicAdd(&slots[s].bytes, (unsigned long long)bytes);
+			return;
+		}
+	}
+	// table full: straight to the global shard
+	uint32_t kind = (key - 1) >> 16, iface = (key - 1) & 0xffff;
+	gr_hip_iface_stats *st = P.stats + (size_t)(blockIdx.x % FWD4_STAT_SHARDS) * P.max_ifaces + iface;
+	unsigned long long *c = reinterpret_cast<unsigned long long *>(kind ? &st->tx_packets : &st->rx_packets);
+	atomicAdd(c, (unsigned long long)pkts);
+	atomicAdd(c + 1, (unsigned long long)bytes);
+}
+
+// Wave-aggregate one counter key per lane (0 = nothing) into the LDS slots.
+__device__ __forceinline__ void wave_count(stat_slot *slots, const fwd4_params &P, uint32_t key, uint32_t len) {
+	const int lane = threadIdx.x & 63;
+	for (;;) {
+		unsigned long long act = __ballot(key != 0);
+		if (act == 0)
+			break;
+		int lead = __ffsll((long long)act) - 1;
+		uint32_t k = __shfl(key, lead, 64);
+		bool same = key == k;
+		unsigned long long sm = __ballot(same);
+		uint32_t b = same ? len : 0;
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1)
+			b += __shfl_xor(b, o, 64);
+		if (lane == lead)
+			slot_add(slots, P, k, (uint32_t)__popcll(sm), b);
+		if (same)
+			key = 0;
+	}
+}
+
+__device__ __forceinline__ uint32_t lo16(uint32_t x) {
+	return x & 0xffff;
+}
+__device__ __forceinline__ uint32_t hi16(uint32_t x) {
+	return x >> 16;
+}
+__device__ __forceinline__ uint32_t bswap16(uint32_t x) {
+	return ((x & 0xff) << 8) | ((x >> 8) & 0xff);
+}
+
+struct result {
+	uint32_t edge, domain, iface, nh;
+	uint32_t rx_if, rx_par, tx_if, tx_par; // counter keys (0 = none)
+};
+
+// The node chain for one packet. w[] is the 64-byte line (little-endian
+// words: byte j is (w[j/4] >> 8*(j%4)) & 0xff), modified in place.
+__device__ __forceinline__ result process(
+	const fwd4_params &P,
+	uint32_t (&w)[16],
+	const gr_hip_pkt_meta &m,
+	const uint8_t *frame
+) {
+	result r = {GR_HIP_E_PUNT, 0, m.iface, 0, 0, 0, 0, 0};
+	const fwd4_edges &E = P.edges;
+
+	// ---- iface_input (iface_input.c:52-112)
+	ifv cur = load_iface(P, m.iface);
+	if (!cur.ok)
+		return r; // port_rx always sets a valid iface: not grout's case, punt
+	uint32_t vlan = m.vlan_ck & 0xfff;
+	if (vlan != 0 && cur.mode == GR_HIP_IFACE_MODE_VRF) { // :74-86
+		uint32_t vid = vlan_lookup(P, cur.id, vlan);
+		ifv v = load_iface(P, vid);
+		if (!v.ok) {
+			r.edge = GR_HIP_E_IFACE_INPUT_UNKNOWN_VLAN;
+			return r;
+		}
+		cur = v;
+	}
+	r.iface = cur.id;
+	if (!(cur.flags & GR_HIP_IFACE_F_UP)) { // :88-91
+		r.edge = GR_HIP_E_IFACE_INPUT_ADMIN_DOWN;
+		return r;
+	}
+	r.rx_if = cur.id; // IFACE_STATS_INC :93-95
+	r.rx_par = m.iface != cur.id ? m.iface : 0;
+	uint32_t e = cur.mode < GR_HIP_IFACE_MODE_COUNT ? E.mode[cur.mode] : GR_HIP_E_IFACE_MODE_UNKNOWN;
+	if (e != CHAIN) {
+		r.edge = e;
+		return r;
+	}
+
+	// ---- eth_input (eth_input.c:35-88)
+	uint32_t type_raw = lo16(w[3]); // as stored (big endian)
+	uint32_t type = bswap16(type_raw);
+	if (type < 1536 || type == 0x8870) { // snap.h:11-12
+		r.edge = GR_HIP_E_SNAP_INPUT;
+		return r;
+	}
+	if (!cur.mac_ok) { // iface_get_eth_addr() < 0
+		r.edge = GR_HIP_E_ETH_INPUT_INVALID_IFACE;
+		return r;
+	}
+	if (w[0] & 1) { // rte_is_multicast_ether_addr
+		bool bc = w[0] == 0xffffffffu && lo16(w[1]) == 0xffff;
+		r.domain = bc ? GR_HIP_ETH_DOMAIN_BROADCAST : GR_HIP_ETH_DOMAIN_MULTICAST;
+	} else if (w[0] == cur.mac_lo && lo16(w[1]) == cur.mac_hi) {
+		r.domain = GR_HIP_ETH_DOMAIN_LOCAL;
+	} else {
+		r.domain = GR_HIP_ETH_DOMAIN_OTHER;
+	}
+	uint32_t data_len = m.pkt_len >= 14 ? m.pkt_len - 14u : m.pkt_len; // rte_pktmbuf_adj
+	e = GR_HIP_E_ETH_INPUT_UNKNOWN_TYPE;
+	for (uint32_t i = 0; i < E.n_eth_types; i++) // l2l3_edges[ether_type]
+		if (E.eth_type_be[i] == type_raw)
+			e = E.eth_type_edge[i];
+	if (e != CHAIN) {
+		r.edge = e;
+		return r;
+	}
+
+	// ---- ip_input (ip_input.c:58-187); the IPv4 header starts at byte 14
+	const uint32_t vihl = (w[3] >> 16) & 0xff;
+	const uint32_t ihl = vihl & 0xf;
+	if (data_len < 20) { // (1) :70-77
+		r.edge = GR_HIP_E_IP_INPUT_BAD_LENGTH;
+		return r;
+	}
+	const uint32_t ck = (m.vlan_ck >> 12) & 3;
+	if (ck == GR_HIP_CKSUM_UNKNOWN) { // (2) :80-88, rte_ipv4_cksum
+		uint32_t hl = ihl * 4;
+		if (14 + hl > P.readable) {
+			r.edge = GR_HIP_E_PUNT; // header bytes not present: CPU path
+			r.rx_if = r.rx_par = 0;
+			r.domain = 0;
+			r.iface = m.iface;
+			return r;
+		}
+		// rte_raw_cksum over hl bytes: 16-bit LE words at offsets 14, 16, ...
+		uint32_t sum = 0;
+		if (ihl != 0) {
+			sum = hi16(w[3]);
+#pragma unroll
+			for (uint32_t j = 4; j < 16; j++) {
+				uint32_t full = lo16(w[j]) + hi16(w[j]);
+				sum += (j <= 2 + ihl) ? full : (j == 3 + ihl ? lo16(w[j]) : 0u);
+			}
+			if (ihl > 12) { // options reach past the line: bytes 64..73
+				uint4 x = *reinterpret_cast<const uint4 *>(frame + 64);
+				uint32_t xw[3] = {x.x, x.y, x.z};
+#pragma unroll
+				for (uint32_t j = 16; j < 19; j++) {
+					uint32_t v = xw[j - 16];
+					uint32_t full = lo16(v) + hi16(v);
+					sum += (j <= 2 + ihl) ? full : (j == 3 + ihl ? lo16(v) : 0u);
+				}
+			}
+		}
+		sum = (sum & 0xffff) + (sum >> 16);
+		sum = (sum & 0xffff) + (sum >> 16);
+		if (sum != 0xffff) { // (uint16_t)~sum != 0
+			r.edge = GR_HIP_E_IP_INPUT_BAD_CHECKSUM;
+			return r;
+		}
+	} else if (ck == GR_HIP_CKSUM_BAD) { // :89-91
+		r.edge = GR_HIP_E_IP_INPUT_BAD_CHECKSUM;
+		return r;
+	}
+	const uint32_t dst = hi16(w[7]) | (lo16(w[8]) << 16); // network order, as stored
+	if (dst == 0) { // :94-97
+		r.edge = GR_HIP_E_IP_INPUT_BAD_ADDRESS;
+		return r;
+	}
+	if ((vihl >> 4) != 4) { // (3) :102-105
+		r.edge = GR_HIP_E_IP_INPUT_BAD_VERSION;
+		return r;
+	}
+	if (ihl * 4 < 20) { // (4) :109-112
+		r.edge = GR_HIP_E_IP_INPUT_BAD_LENGTH;
+		return r;
+	}
+	if (bswap16(lo16(w[4])) < 20) { // (5) :117-120
+		r.edge = GR_HIP_E_IP_INPUT_BAD_LENGTH;
+		return r;
+	}
+	if (r.domain != GR_HIP_ETH_DOMAIN_LOCAL) { // :122-137 (LOOPBACK never from a port)
+		bool mc = r.domain == GR_HIP_ETH_DOMAIN_BROADCAST || r.domain == GR_HIP_ETH_DOMAIN_MULTICAST;
+		r.edge = mc ? GR_HIP_E_IP_INPUT_LOCAL : GR_HIP_E_IP_INPUT_OTHER_HOST;
+		return r;
+	}
+	const uint32_t d0 = dst & 0xff;
+	if (dst == 0xffffffffu || (d0 >= 224 && d0 <= 239)) { // :139-142
+		r.edge = GR_HIP_E_IP_INPUT_LOCAL;
+		return r;
+	}
+	// fib4_lookup (route.c:147-167): VRF iface (vrf.c:51-57), DIR24_8
+	uint32_t slot = 0;
+	{
+		ifv vrf = load_iface(P, cur.vrf_id);
+		if (vrf.ok && vrf.type == GR_HIP_IFACE_TYPE_VRF) {
+			fwd4_fib f = P.fibs[cur.vrf_id];
+			if (f.tbl24 != nullptr) {
+				uint32_t ip = __builtin_bswap32(dst);
+				uint32_t ent = f.tbl24[ip >> 8];
+				if (ent & 0x80000000u)
+					ent = f.tbl8[(size_t)(ent & 0x7fffffffu) * 256 + (ip & 0xff)];
+				slot = ent;
+			}
+		}
+	}
+	if (slot == 0 || slot > P.max_nh) {
+		r.edge = GR_HIP_E_IP_ERROR_DEST_UNREACH; // NO_ROUTE :150-153
+		return r;
+	}
+	nhv nh = load_nh(P, slot);
+	if (nh.type == GR_HIP_NH_T_GROUP) { // nexthop_group_get_nh, nexthop.h:89-96
+		if (nh.n_members == 1) {
+			slot = nh.single;
+		} else if (nh.n_members == 0) {
+			slot = 0;
+		} else {
+			uint32_t i = nh.reta_off + (m.rss & (nh.reta_size - 1));
+			slot = i < P.reta_cap ? P.reta[i] : 0;
+		}
+		if (slot == 0 || slot > P.max_nh) {
+			r.edge = GR_HIP_E_IP_ERROR_DEST_UNREACH;
+			return r;
+		}
+		nh = load_nh(P, slot);
+	}
+	r.nh = slot; // l3_mbuf_data(mbuf)->nh :156
+	e = nh.type < 8 ? E.in_nh[nh.type] : CHAIN;
+	if (e != CHAIN) {
+		r.edge = e;
+		return r;
+	}
+	if (nh.type == GR_HIP_NH_T_L3 && (nh.flags & GR_HIP_NH_F_LOCAL) && dst == nh.ipv4) { // :166-187
+		r.edge = (cur.flags & GR_HIP_IFACE_F_SNAT_DYNAMIC) ? GR_HIP_E_IP_INPUT_LOCAL_CT
+		                                                  : GR_HIP_E_IP_INPUT_LOCAL;
+		return r;
+	}
+
+	// ---- ip_forward (ip_forward.c:21-33)
+	uint32_t ttl = (w[5] >> 16) & 0xff;
+	if (ttl <= 1) {
+		r.edge = GR_HIP_E_IP_ERROR_TTL_EXCEEDED;
+		return r;
+	}
+	w[5] = (w[5] & 0xff00ffffu) | ((ttl - 1) << 16);
+	uint32_t c = lo16(w[6]) + 1; // host-order u16 + RTE_BE16(0x0100)
+	c += c >= 0xffff;
+	w[6] = (w[6] & 0xffff0000u) | (c & 0xffff);
+
+	// ---- ip_output (ip_output.c:135-213)
+	e = nh.type < 8 ? E.out_nh[nh.type] : CHAIN;
+	if (e != CHAIN) {
+		r.edge = e;
+		return r;
+	}
+	ifv oif = load_iface(P, nh.iface_id);
+	if (!oif.ok) { // :151-155
+		r.edge = GR_HIP_E_IP_OUTPUT_ERROR;
+		return r;
+	}
+	r.iface = oif.id; // :157
+	if (data_len > oif.mtu) { // :159-166, DF = BE 0x4000 -> byte 20 & 0x40
+		r.edge = (w[5] & 0x40) ? GR_HIP_E_IP_ERROR_FRAG_NEEDED : GR_HIP_E_IP_FRAGMENT;
+		return r;
+	}
+	e = oif.type < 8 ? E.out_iface[oif.type] : CHAIN; // :170
+	if (oif.flags & (GR_HIP_IFACE_F_SNAT_STATIC | GR_HIP_IFACE_F_SNAT_DYNAMIC)) {
+		r.edge = GR_HIP_E_IP_OUTPUT_SNAT; // snat44_process :172-179
+		return r;
+	}
+	if (e != CHAIN) {
+		r.edge = e;
+		return r;
+	}
+	if (nh.state != GR_HIP_NH_S_REACHABLE || ((nh.flags & GR_HIP_NH_F_LINK) && dst != nh.ipv4)) {
+		r.edge = GR_HIP_E_IP_HOLD; // :186-198
+		return r;
+	}
+
+	// ---- eth_output (eth_output.c:297-316): dst = nh mac, src = iface mac
+	w[0] = nh.mac_lo;
+	w[1] = (w[1] & 0xffff0000u) | nh.mac_hi;
+	if (!oif.mac_ok) {
+		r.edge = GR_HIP_E_ETH_OUTPUT_NO_MAC;
+		return r;
+	}
+	w[1] = lo16(w[1]) | (oif.mac_lo << 16);
+	w[2] = (oif.mac_lo >> 16) | (oif.mac_hi << 16);
+	w[3] = (w[3] & 0xffff0000u) | 0x0008u; // RTE_BE16(RTE_ETHER_TYPE_IPV4)
+
+	// ---- iface_output (iface_output.c:213-246)
+	ifv out = oif;
+	bool vlan_if = oif.type == GR_HIP_IFACE_TYPE_VLAN;
+	if (vlan_if) {
+		out = load_iface(P, oif.parent_id);
+		if (!out.ok) {
+			r.edge = GR_HIP_E_IFACE_OUTPUT_VLAN_NO_PARENT;
+			return r;
+		}
+	}
+	if (!(oif.flags & GR_HIP_IFACE_F_UP)) {
+		r.edge = GR_HIP_E_IFACE_OUTPUT_ADMIN_DOWN;
+		return r;
+	}
+	r.tx_if = oif.id;
+	r.tx_par = vlan_if ? out.id : 0;
+	r.iface = out.id;
+	r.edge = out.type < 8 ? E.iout_type[out.type] : GR_HIP_E_IFACE_OUTPUT_INVAL_TYPE;
+	return r;
+}
+
+extern "C" __global__ void __launch_bounds__(FWD4_BLOCK)
+gr_fwd4_kernel(const fwd4_params P) {
+	__shared__ __attribute__((aligned(16))) uint8_t lines[FWD4_BLOCK * FWD4_ROW];
+	__shared__ stat_slot slots[FWD4_STAT_SLOTS];
+	const uint32_t tid = threadIdx.x;
+
+	if (tid < FWD4_STAT_SLOTS) {
+		slots[tid].key = 0;
+		slots[tid].pkts = 0;
+		slots[tid].bytes = 0;
+	}
+
+	const uint32_t n_tiles = (P.n + FWD4_BLOCK - 1) / FWD4_BLOCK;
+	for (uint32_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+		const uint32_t base = tile * FWD4_BLOCK;
+		const uint32_t cnt = min((uint32_t)FWD4_BLOCK, P.n - base);
+
+		// stage: 4 lanes per 64-byte line, 16 bytes each (coalesced)
+#pragma unroll
+		for (uint32_t k = 0; k < 4; k++) {
+			uint32_t c = k * FWD4_BLOCK + tid;
+			uint32_t p = c >> 2, part = c & 3;
+			if (p < cnt) {
+				const uint4 *src = reinterpret_cast<const uint4 *>(
+					P.in + (size_t)(base + p) * P.in_stride + part * 16);
+				*reinterpret_cast<uint4 *>(&lines[p * FWD4_ROW + part * 16]) = *src;
+			}
+		}
+		gr_hip_pkt_meta m = {0, 0, 0, 0};
+		if (tid < cnt)
+			m = P.meta[base + tid];
+		__syncthreads();
+
+		result r = {0, 0, 0, 0, 0, 0, 0, 0};
+		if (tid < cnt) {
+			uint32_t w[16];
+			uint4 *row = reinterpret_cast<uint4 *>(&lines[tid * FWD4_ROW]);
+#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				uint4 x = row[k];
+				w[4 * k] = x.x;
+				w[4 * k + 1] = x.y;
+				w[4 * k + 2] = x.z;
+				w[4 * k + 3] = x.w;
+			}
+			const uint8_t *frame = P.in + (size_t)(base + tid) * P.in_stride;
+			r = process(P, w, m, frame);
+#pragma unroll
+			for (int k = 0; k < 4; k++)
+				row[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+			gr_hip_verdict v;
+			v.edge = (uint8_t)r.edge;
+			v.domain = (uint8_t)r.domain;
+			v.iface = (uint16_t)r.iface;
+			v.nh = r.nh;
+			P.verdicts[base + tid] = v;
+		}
+		// counters (every lane of the wave takes part in the ballots)
+		if (P.stats != nullptr) {
+			uint32_t len = m.pkt_len;
+			wave_count(slots, P, r.rx_if ? r.rx_if + 1 : 0, len);
+			wave_count(slots, P, r.rx_par ? r.rx_par + 1 : 0, len);
+			wave_count(slots, P, r.tx_if ? (r.tx_if | 0x10000u) + 1 : 0, len);
+			wave_count(slots, P, r.tx_par ? (r.tx_par | 0x10000u) + 1 : 0, len);
+		}
+		__syncthreads();
+
+		// write back: same coalesced mapping
+#pragma unroll
+		for (uint32_t k = 0; k < 4; k++) {
+			uint32_t c = k * FWD4_BLOCK + tid;
+			uint32_t p = c >> 2, part = c & 3;
+			if (p < cnt) {
+				uint4 *dst = reinterpret_cast<uint4 *>(
+					P.out + (size_t)(base + p) * P.out_stride + part * 16);
+				*dst = *reinterpret_cast<const uint4 *>(&lines[p * FWD4_ROW + part * 16]);
+			}
+		}
+		__syncthreads();
+	}
+
+	if (P.stats != nullptr && tid < FWD4_STAT_SLOTS && slots[tid].key != 0) {
+		uint32_t key = slots[tid].key - 1;
+		uint32_t kind = key >> 16, iface = key & 0xffff;
+		gr_hip_iface_stats *st =
+			P.stats + (size_t)(blockIdx.x % FWD4_STAT_SHARDS) * P.max_ifaces + iface;
+		unsigned long long *c = reinterpret_cast<unsigned long long *>(kind ? &st->tx_packets : &st->rx_packets);
+		atomicAdd(c, (unsigned long long)slots[tid].pkts);
+		atomicAdd(c + 1, slots[tid].bytes);
+	}
+}
+
+extern "C" hipError_t gr_fwd4_launch(const fwd4_params *P, uint32_t grid, hipStream_t s) {
+	hipLaunchKernelGGL(gr_fwd4_kernel, dim3(grid), dim3(FWD4_BLOCK), 0, s, *P);
+	return hipGetLastError();
+}

@@ -1,0 +1,879 @@
+// SPDX-License-Identifier: BSD-3-Clause
+//
+// gr_hip.cpp -- implementation of the C ABI declared in include/grout_hip.h:
+// device mirrors of grout's iface / nexthop objects, per-VRF device FIBs fed
+// by the host RIB (fib4.c), queues (one HIP stream each, the analogue of one
+// grout worker / RX queue) and the launches of the fused kernel.
+//
+// Control-plane updates are stream ordered: a control stream first waits for
+// every queue's submitted work, then copies, then the caller returns once the
+// copies are done. Submits issued after the call see the new state; in-flight
+// kernels never see a half-updated table. That is the role of the RCU QSBR
+// synchronisation grout performs around FIB changes (route.c:87-95,740-771).
+#include <hip/hip_runtime.h>
+
+#include "fib4.h"
+#include "fwd4_kernel.h"
+
+#include <algorithm>
+#include <errno.h>
+#include <mutex>
+#include <new>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+extern "C" hipError_t gr_fwd4_launch(const fwd4_params *P, uint32_t grid, hipStream_t s);
+
+#define HCK(expr)                                                                                  \
+	do {                                                                                       \
+		hipError_t e__ = (expr);                                                           \
+		if (e__ != hipSuccess) {                                                           \
+			(void)hipGetLastError();                                                   \
+			return e__ == hipErrorOutOfMemory ? -ENOMEM : -EIO;                        \
+		}                                                                                  \
+	} while (0)
+
+namespace {
+
+constexpr uint32_t N_TIMED = 64;
+constexpr uint32_t HOST_SLOTS = 3;
+constexpr uint32_t HOST_CHUNK = 1u << 18; // packets per host-mode chunk
+
+struct vrf_fib {
+	gr_fib4 *rib = nullptr;
+	uint32_t *d24 = nullptr;
+	uint32_t *d8 = nullptr;
+	uint32_t num_tbl8 = 0;
+	bool uploaded = false; // tbl24 uploaded at least once
+};
+
+struct host_slot {
+	hipStream_t s = nullptr;
+	uint8_t *in = nullptr, *out = nullptr;
+	gr_hip_pkt_meta *meta = nullptr;
+	gr_hip_verdict *v = nullptr;
+};
+
+} // namespace
+
+struct gr_hip_queue {
+	gr_hip_ctx *ctx;
+	hipStream_t s;
+	bool own_stream;
+	hipEvent_t ev0[N_TIMED], ev1[N_TIMED];
+	uint64_t n_launch;
+	hipEvent_t quiesce;
+	gr_hip_iface_stats *d_stats; // [FWD4_STAT_SHARDS][max_ifaces]
+	host_slot hs[HOST_SLOTS];
+};
+
+struct gr_hip_ctx {
+	int dev;
+	uint32_t max_ifaces, max_nh;
+	int n_cu;
+	std::mutex mu;
+	hipStream_t ctl;
+	std::vector<gr_hip_iface> ifaces;
+	std::vector<gr_hip_nh> nh;
+	std::vector<uint32_t> reta;
+	std::vector<vrf_fib> vrfs;
+	std::vector<fwd4_fib> fibs;
+	gr_hip_iface *d_ifaces;
+	gr_hip_nh *d_nh;
+	uint32_t *d_reta;
+	uint32_t d_reta_cap;
+	fwd4_fib *d_fibs;
+	uint32_t *d_vlan_keys;
+	uint16_t *d_vlan_vals;
+	uint32_t vlan_cap;
+	fwd4_edges edges;
+	std::vector<gr_hip_queue *> queues;
+};
+
+// ---------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------
+
+// Make the control stream wait for everything submitted on every queue.
+static int quiesce(gr_hip_ctx *c) {
+	for (gr_hip_queue *q : c->queues) {
+		HCK(hipEventRecord(q->quiesce, q->s));
+		HCK(hipStreamWaitEvent(c->ctl, q->quiesce, 0));
+	}
+	return 0;
+}
+
+static int h2d(gr_hip_ctx *c, void *dst, const void *src, size_t n) {
+	if (n == 0)
+		return 0;
+	HCK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->ctl));
+	return 0;
+}
+
+static int ctl_sync(gr_hip_ctx *c) {
+	HCK(hipStreamSynchronize(c->ctl));
+	return 0;
+}
+
+static void set_default_edges(fwd4_edges *E) {
+	// grout's default module set: ip_input.c:200-203, arp_input.c:62,
+	// ip6_input.c:161, lacp_input.c:66-68, eth_input.c:115, xconnect.c:65,
+	// bridge_input.c:124-125, vxlan_output.c:138, bond_output.c:250,
+	// port_output.c:51, xvrf.c:63, ipip/datapath_out.c:91,
+	// srv6_output.c:152, dnat44_static.c:102
+	memset(E, 0, sizeof(*E));
+	auto be = [](uint16_t h) { return (uint16_t)((h >> 8) | (h << 8)); };
+	const struct {
+		uint16_t t;
+		uint8_t e;
+	} types[] = {
+		{0x0800, GR_HIP_EDGE_CHAIN},
+		{0x0806, GR_HIP_E_ARP_INPUT},
+		{0x86dd, GR_HIP_E_IP6_INPUT},
+		{0x8809, GR_HIP_E_LACP_INPUT},
+	};
+	for (auto &t : types) {
+		E->eth_type_be[E->n_eth_types] = be(t.t);
+		E->eth_type_edge[E->n_eth_types] = t.e;
+		E->n_eth_types++;
+	}
+	E->mode[GR_HIP_IFACE_MODE_VRF] = GR_HIP_EDGE_CHAIN;
+	E->mode[GR_HIP_IFACE_MODE_XC] = GR_HIP_E_XCONNECT;
+	E->mode[GR_HIP_IFACE_MODE_BOND] = GR_HIP_EDGE_CHAIN;
+	E->mode[GR_HIP_IFACE_MODE_BRIDGE] = GR_HIP_E_BRIDGE_INPUT;
+	for (int i = 0; i < 8; i++) {
+		E->in_nh[i] = GR_HIP_EDGE_CHAIN;
+		E->out_nh[i] = GR_HIP_EDGE_CHAIN;
+		E->out_iface[i] = GR_HIP_EDGE_CHAIN;
+		E->iout_type[i] = GR_HIP_E_IFACE_OUTPUT_INVAL_TYPE;
+	}
+	E->in_nh[GR_HIP_NH_T_BLACKHOLE] = GR_HIP_E_IP_BLACKHOLE;
+	E->in_nh[GR_HIP_NH_T_REJECT] = GR_HIP_E_IP_ERROR_DEST_UNREACH;
+	E->in_nh[GR_HIP_NH_T_DNAT] = GR_HIP_E_DNAT44_STATIC;
+	E->out_nh[GR_HIP_NH_T_SR6_OUTPUT] = GR_HIP_E_SR6_OUTPUT;
+	E->out_iface[GR_HIP_IFACE_TYPE_VRF] = GR_HIP_E_XVRF;
+	E->out_iface[GR_HIP_IFACE_TYPE_IPIP] = GR_HIP_E_IPIP_OUTPUT;
+	E->iout_type[GR_HIP_IFACE_TYPE_PORT] = GR_HIP_E_PORT_OUTPUT;
+	E->iout_type[GR_HIP_IFACE_TYPE_BOND] = GR_HIP_E_BOND_OUTPUT;
+	E->iout_type[GR_HIP_IFACE_TYPE_VXLAN] = GR_HIP_E_VXLAN_OUTPUT;
+	E->iout_type[GR_HIP_IFACE_TYPE_BRIDGE] = GR_HIP_E_BRIDGE_INPUT;
+}
+
+// ---------------------------------------------------------------------------
+// lifetime
+// ---------------------------------------------------------------------------
+
+extern "C" int gr_hip_abi_version(void) {
+	return GR_HIP_ABI_VERSION;
+}
+
+extern "C" const char *gr_hip_strerror(int err) {
+	return strerror(err < 0 ? -err : err);
+}
+
+extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, gr_hip_ctx_t **out) {
+	if (out == nullptr || max_ifaces < 2 || max_ifaces > 65535 || max_nexthops == 0
+	    || max_nexthops > GR_HIP_MAX_NEXTHOPS)
+		return -EINVAL;
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+		(void)hipGetLastError();
+		return -ENODEV;
+	}
+	if (dev < 0 || dev >= ndev)
+		return -ENODEV;
+	HCK(hipSetDevice(dev));
+	gr_hip_ctx *c = new (std::nothrow) gr_hip_ctx();
+	if (c == nullptr)
+		return -ENOMEM;
+	c->dev = dev;
+	c->max_ifaces = max_ifaces;
+	c->max_nh = max_nexthops;
+	hipDeviceProp_t prop;
+	if (hipGetDeviceProperties(&prop, dev) != hipSuccess) {
+		delete c;
+		return -EIO;
+	}
+	c->n_cu = prop.multiProcessorCount;
+	c->ifaces.assign(max_ifaces, gr_hip_iface {});
+	c->nh.assign((size_t)max_nexthops + 1, gr_hip_nh {});
+	c->vrfs.assign(max_ifaces, vrf_fib {});
+	c->fibs.assign(max_ifaces, fwd4_fib {nullptr, nullptr});
+	set_default_edges(&c->edges);
+	c->d_reta = nullptr;
+	c->d_reta_cap = 0;
+	c->d_vlan_keys = nullptr;
+	c->d_vlan_vals = nullptr;
+	c->vlan_cap = 0;
+	int ret = -ENOMEM;
+	if (hipStreamCreateWithFlags(&c->ctl, hipStreamNonBlocking) != hipSuccess)
+		goto fail;
+	if (hipMalloc(&c->d_ifaces, sizeof(gr_hip_iface) * max_ifaces) != hipSuccess)
+		goto fail;
+	if (hipMalloc(&c->d_nh, sizeof(gr_hip_nh) * ((size_t)max_nexthops + 1)) != hipSuccess)
+		goto fail;
+	if (hipMalloc(&c->d_fibs, sizeof(fwd4_fib) * max_ifaces) != hipSuccess)
+		goto fail;
+	if (hipMemset(c->d_ifaces, 0, sizeof(gr_hip_iface) * max_ifaces) != hipSuccess
+	    || hipMemset(c->d_nh, 0, sizeof(gr_hip_nh) * ((size_t)max_nexthops + 1)) != hipSuccess
+	    || hipMemset(c->d_fibs, 0, sizeof(fwd4_fib) * max_ifaces) != hipSuccess)
+		goto fail;
+	*out = c;
+	return 0;
+fail:
+	(void)hipGetLastError();
+	gr_hip_fini(c);
+	return ret;
+}
+
+extern "C" int gr_hip_fini(gr_hip_ctx_t *c) {
+	if (c == nullptr)
+		return -EINVAL;
+	hipSetDevice(c->dev);
+	while (!c->queues.empty())
+		gr_hip_queue_destroy(c->queues.back());
+	for (vrf_fib &v : c->vrfs) {
+		gr_fib4_free(v.rib);
+		hipFree(v.d24);
+		hipFree(v.d8);
+	}
+	hipFree(c->d_ifaces);
+	hipFree(c->d_nh);
+	hipFree(c->d_fibs);
+	hipFree(c->d_reta);
+	hipFree(c->d_vlan_keys);
+	hipFree(c->d_vlan_vals);
+	if (c->ctl)
+		hipStreamDestroy(c->ctl);
+	(void)hipGetLastError();
+	delete c;
+	return 0;
+}
+
+// ---------------------------------------------------------------------------
+// edges
+// ---------------------------------------------------------------------------
+
+static bool edge_ok(uint8_t e) {
+	return e == GR_HIP_EDGE_CHAIN || e < GR_HIP_E_COUNT;
+}
+
+extern "C" int gr_hip_edges_eth_type(gr_hip_ctx_t *c, uint16_t be_type, uint8_t edge) {
+	if (c == nullptr || !edge_ok(edge))
+		return -EINVAL;
+	std::lock_guard<std::mutex> l(c->mu);
+	fwd4_edges &E = c->edges;
+	for (uint32_t i = 0; i < E.n_eth_types; i++) {
+		if (E.eth_type_be[i] == be_type) {
+			E.eth_type_edge[i] = edge;
+			return 0;
+		}
+	}
+	if (E.n_eth_types >= FWD4_MAX_ETH_TYPES)
+		return -ENOSPC;
+	E.eth_type_be[E.n_eth_types] = be_type;
+	E.eth_type_edge[E.n_eth_types] = edge;
+	E.n_eth_types++;
+	return 0;
+}
+
+#define EDGE_SETTER(fn, field, limit)                                                              \
+	extern "C" int fn(gr_hip_ctx_t *c, uint8_t key, uint8_t edge) {                            \
+		if (c == nullptr || key >= (limit) || !edge_ok(edge))                              \
+			return -EINVAL;                                                            \
+		std::lock_guard<std::mutex> l(c->mu);                                              \
+		c->edges.field[key] = edge;                                                        \
+		return 0;                                                                          \
+	}
+EDGE_SETTER(gr_hip_edges_iface_mode, mode, GR_HIP_IFACE_MODE_COUNT)
+EDGE_SETTER(gr_hip_edges_ip_input_nh_type, in_nh, 8)
+EDGE_SETTER(gr_hip_edges_ip_output_nh_type, out_nh, 8)
+EDGE_SETTER(gr_hip_edges_ip_output_iface_type, out_iface, 8)
+EDGE_SETTER(gr_hip_edges_iface_output_type, iout_type, 8)
+
+// ---------------------------------------------------------------------------
+// mirrors
+// ---------------------------------------------------------------------------
+
+static int upload_vlans(gr_hip_ctx *c) {
+	uint32_t n = 0;
+	for (const gr_hip_iface &i : c->ifaces)
+		n += i.id != 0 && i.type == GR_HIP_IFACE_TYPE_VLAN;
+	uint32_t cap = 16;
+	while (cap < 2 * n)
+		cap *= 2;
+	std::vector<uint32_t> keys(cap, 0);
+	std::vector<uint16_t> vals(cap, 0);
+	for (const gr_hip_iface &i : c->ifaces) {
+		if (i.id == 0 || i.type != GR_HIP_IFACE_TYPE_VLAN)
+			continue;
+		uint32_t key = (((uint32_t)i.parent_id << 16) | i.vlan_id) + 1;
+		uint32_t h = (key * 0x9e3779b1u) & (cap - 1);
+		while (keys[h] != 0 && keys[h] != key)
+			h = (h + 1) & (cap - 1);
+		keys[h] = key;
+		vals[h] = i.id;
+	}
+	if (cap != c->vlan_cap) {
+		hipFree(c->d_vlan_keys);
+		hipFree(c->d_vlan_vals);
+		c->d_vlan_keys = nullptr;
+		c->d_vlan_vals = nullptr;
+		c->vlan_cap = 0;
+		HCK(hipMalloc(&c->d_vlan_keys, cap * sizeof(uint32_t)));
+		HCK(hipMalloc(&c->d_vlan_vals, cap * sizeof(uint16_t)));
+		c->vlan_cap = cap;
+	}
+	int r = h2d(c, c->d_vlan_keys, keys.data(), cap * sizeof(uint32_t));
+	if (r == 0)
+		r = h2d(c, c->d_vlan_vals, vals.data(), cap * sizeof(uint16_t));
+	if (r == 0)
+		r = ctl_sync(c); // the vectors go out of scope
+	return r;
+}
+
+extern "C" int gr_hip_iface_set(gr_hip_ctx_t *c, const struct gr_hip_iface *ifs, uint32_t n) {
+	if (c == nullptr || (ifs == nullptr && n))
+		return -EINVAL;
+	for (uint32_t i = 0; i < n; i++)
+		if (ifs[i].id == 0 || ifs[i].id >= c->max_ifaces)
+			return -EINVAL;
+	std::lock_guard<std::mutex> l(c->mu);
+	hipSetDevice(c->dev);
+	bool vlans = false;
+	for (uint32_t i = 0; i < n; i++) {
+		vlans |= ifs[i].type == GR_HIP_IFACE_TYPE_VLAN
+			|| c->ifaces[ifs[i].id].type == GR_HIP_IFACE_TYPE_VLAN;
+		c->ifaces[ifs[i].id] = ifs[i];
+	}
+	int r = quiesce(c);
+	if (r == 0)
+		r = h2d(c, c->d_ifaces, c->ifaces.data(), sizeof(gr_hip_iface) * c->max_ifaces);
+	if (r == 0)
+		r = ctl_sync(c);
+	if (r == 0 && (vlans || c->vlan_cap == 0))
+		r = upload_vlans(c);
+	return r;
+}
+
+extern "C" int gr_hip_iface_del(gr_hip_ctx_t *c, uint16_t id) {
+	if (c == nullptr || id == 0 || id >= c->max_ifaces)
+		return -EINVAL;
+	std::lock_guard<std::mutex> l(c->mu);
+	hipSetDevice(c->dev);
+	bool vlan = c->ifaces[id].type == GR_HIP_IFACE_TYPE_VLAN;
+	c->ifaces[id] = gr_hip_iface {};
+	int r = quiesce(c);
+	if (r == 0)
+		r = h2d(c, c->d_ifaces + id, &c->ifaces[id], sizeof(gr_hip_iface));
+	if (r == 0)
+		r = ctl_sync(c);
+	if (r == 0 && vlan)
+		r = upload_vlans(c);
+	return r;
+}
+
+extern "C" int gr_hip_nh_set(gr_hip_ctx_t *c, uint32_t first, const struct gr_hip_nh *nh, uint32_t n) {
+	if (c == nullptr || first == 0 || (nh == nullptr && n)
+	    || (uint64_t)first + n > (uint64_t)c->max_nh + 1)
+		return -EINVAL;
+	std::lock_guard<std::mutex> l(c->mu);
+	hipSetDevice(c->dev);
+	memcpy(&c->nh[first], nh, (size_t)n * sizeof(*nh));
+	int r = quiesce(c);
+	if (r == 0)
+		r = h2d(c, c->d_nh + first, &c->nh[first], (size_t)n * sizeof(*nh));
+	if (r == 0)
+		r = ctl_sync(c);
+	return r;
+}
+
+extern "C" int gr_hip_reta_set(gr_hip_ctx_t *c, uint32_t first, const uint32_t *slots, uint32_t n) {
+	if (c == nullptr || (slots == nullptr && n) || (uint64_t)first + n > (1ull << 31))
+		return -EINVAL;
+	std::lock_guard<std::mutex> l(c->mu);
+	hipSetDevice(c->dev);
+	if ((uint64_t)first + n > c->reta.size())
+		c->reta.resize((size_t)first + n, 0);
+	memcpy(&c->reta[first], slots, (size_t)n * sizeof(*slots));
+	int r = quiesce(c);
+	if (r != 0)
+		return r;
+	if (c->reta.size() > c->d_reta_cap) {
+		uint32_t cap = c->d_reta_cap ? c->d_reta_cap : 4096;
+		while (cap < c->reta.size())
+			cap *= 2;
+		uint32_t *d = nullptr;
+		HCK(hipStreamSynchronize(c->ctl));
+		HCK(hipMalloc(&d, (size_t)cap * sizeof(uint32_t)));
+		HCK(hipMemset(d, 0, (size_t)cap * sizeof(uint32_t)));
+		hipFree(c->d_reta);
+		c->d_reta = d;
+		c->d_reta_cap = cap;
+		r = h2d(c, c->d_reta, c->reta.data(), c->reta.size() * sizeof(uint32_t));
+	} else {
+		r = h2d(c, c->d_reta + first, &c->reta[first], (size_t)n * sizeof(uint32_t));
+	}
+	if (r == 0)
+		r = ctl_sync(c);
+	return r;
+}
+
+// ---------------------------------------------------------------------------
+// FIB
+// ---------------------------------------------------------------------------
+
+extern "C" int gr_hip_fib4_create(gr_hip_ctx_t *c, uint16_t vrf, uint32_t max_routes, uint32_t num_tbl8) {
+	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
+		return -EINVAL;
+	std::lock_guard<std::mutex> l(c->mu);
+	hipSetDevice(c->dev);
+	vrf_fib &v = c->vrfs[vrf];
+	if (v.rib != nullptr)
+		return -EEXIST;
+	if (num_tbl8 == 0) // fib4_auto_tbl8, route.c:38-41
+		num_tbl8 = max_routes / 500 < 256 ? 256 : max_routes / 500;
+	v.rib = gr_fib4_new(max_routes, num_tbl8);
+	if (v.rib == nullptr)
+		return -ENOMEM;
+	v.num_tbl8 = num_tbl8;
+	if (hipMalloc(&v.d24, sizeof(uint32_t) * GR_FIB4_TBL24_ENTRIES) != hipSuccess
+	    || hipMalloc(&v.d8, sizeof(uint32_t) * 256 * (size_t)num_tbl8) != hipSuccess
+	    || hipMemset(v.d24, 0, sizeof(uint32_t) * GR_FIB4_TBL24_ENTRIES) != hipSuccess
+	    || hipMemset(v.d8, 0, sizeof(uint32_t) * 256 * (size_t)num_tbl8) != hipSuccess) {
+		(void)hipGetLastError();
+		hipFree(v.d24);
+		hipFree(v.d8);
+		gr_fib4_free(v.rib);
+		v = vrf_fib {};
+		return -ENOMEM;
+	}
+	gr_fib4_dirty_clear(v.rib);
+	c->fibs[vrf] = fwd4_fib {v.d24, v.d8};
+	int r = quiesce(c);
+	if (r == 0)
+		r = h2d(c, c->d_fibs + vrf, &c->fibs[vrf], sizeof(fwd4_fib));
+	if (r == 0)
+		r = ctl_sync(c);
+	return r;
+}
+
+extern "C" int gr_hip_fib4_destroy(gr_hip_ctx_t *c, uint16_t vrf) {
+	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
+		return -EINVAL;
+	std::lock_guard<std::mutex> l(c->mu);
+	hipSetDevice(c->dev);
+	vrf_fib &v = c->vrfs[vrf];
+	if (v.rib == nullptr)
+		return -ENOENT;
+	c->fibs[vrf] = fwd4_fib {nullptr, nullptr};
+	int r = quiesce(c);
+	if (r == 0)
+		r = h2d(c, c->d_fibs + vrf, &c->fibs[vrf], sizeof(fwd4_fib));
+	if (r == 0)
+		r = ctl_sync(c);
+	if (r != 0)
+		return r;
+	hipFree(v.d24);
+	hipFree(v.d8);
+	gr_fib4_free(v.rib);
+	v = vrf_fib {};
+	return 0;
+}
+
+extern "C" int gr_hip_route4_add(gr_hip_ctx_t *c, const struct gr_hip_route4 *rt, uint32_t n, int replace) {
+	if (c == nullptr || (rt == nullptr && n))
+		return -EINVAL;
+	std::lock_guard<std::mutex> l(c->mu);
+	for (uint32_t i = 0; i < n; i++) {
+		if (rt[i].vrf_id == 0 || rt[i].vrf_id >= c->max_ifaces || rt[i].nh == 0
+		    || rt[i].nh > c->max_nh)
+			return -EINVAL;
+		vrf_fib &v = c->vrfs[rt[i].vrf_id];
+		if (v.rib == nullptr)
+			return -ENONET;
+		int r = gr_fib4_add(v.rib, __builtin_bswap32(rt[i].ip), rt[i].prefixlen, rt[i].nh, replace);
+		if (r < 0)
+			return r;
+	}
+	return 0;
+}
+
+extern "C" int gr_hip_route4_del(gr_hip_ctx_t *c, uint16_t vrf, uint32_t ip, uint8_t len) {
+	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
+		return -EINVAL;
+	std::lock_guard<std::mutex> l(c->mu);
+	vrf_fib &v = c->vrfs[vrf];
+	if (v.rib == nullptr)
+		return -ENONET;
+	return gr_fib4_del(v.rib, __builtin_bswap32(ip), len);
+}
+
+extern "C" int gr_hip_fib4_commit(gr_hip_ctx_t *c, uint16_t vrf) {
+	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
+		return -EINVAL;
+	std::lock_guard<std::mutex> l(c->mu);
+	hipSetDevice(c->dev);
+	vrf_fib &v = c->vrfs[vrf];
+	if (v.rib == nullptr)
+		return -ENONET;
+	uint32_t lo, hi;
+	gr_fib4_dirty_tbl24(v.rib, &lo, &hi);
+	std::vector<uint32_t> groups(v.num_tbl8);
+	int ng = gr_fib4_dirty_tbl8(v.rib, groups.data(), v.num_tbl8);
+	int r = quiesce(c);
+	if (r != 0)
+		return r;
+	const uint32_t *t24 = gr_fib4_tbl24(v.rib);
+	const uint32_t *t8 = gr_fib4_tbl8(v.rib);
+	if (lo < hi)
+		r = h2d(c, v.d24 + lo, t24 + lo, (size_t)(hi - lo) * sizeof(uint32_t));
+	if (r == 0 && ng < 0) {
+		r = h2d(c, v.d8, t8, sizeof(uint32_t) * 256 * (size_t)v.num_tbl8);
+	} else if (r == 0 && ng > 0) {
+		// coalesce runs of consecutive groups
+		std::vector<uint32_t> gs(groups.begin(), groups.begin() + ng);
+		std::sort(gs.begin(), gs.end());
+		for (size_t i = 0; i < gs.size() && r == 0;) {
+			size_t j = i + 1;
+			while (j < gs.size() && gs[j] == gs[j - 1] + 1)
+				j++;
+			r = h2d(c, v.d8 + (size_t)gs[i] * 256, t8 + (size_t)gs[i] * 256,
+				(j - i) * 256 * sizeof(uint32_t));
+			i = j;
+		}
+	}
+	if (r == 0)
+		r = ctl_sync(c);
+	if (r == 0) {
+		gr_fib4_dirty_clear(v.rib);
+		v.uploaded = true;
+	}
+	return r;
+}
+
+extern "C" int gr_hip_fib4_lookup_host(gr_hip_ctx_t *c, uint16_t vrf, uint32_t ip_be, uint32_t *nh) {
+	if (c == nullptr || nh == nullptr || vrf == 0 || vrf >= c->max_ifaces)
+		return -EINVAL;
+	std::lock_guard<std::mutex> l(c->mu);
+	vrf_fib &v = c->vrfs[vrf];
+	if (v.rib == nullptr)
+		return -ENONET;
+	*nh = gr_fib4_lookup(v.rib, __builtin_bswap32(ip_be));
+	return 0;
+}
+
+extern "C" int gr_hip_fib4_info(gr_hip_ctx_t *c, uint16_t vrf, uint32_t *n_routes, uint32_t *tbl8_used, uint64_t *bytes) {
+	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
+		return -EINVAL;
+	std::lock_guard<std::mutex> l(c->mu);
+	vrf_fib &v = c->vrfs[vrf];
+	if (v.rib == nullptr)
+		return -ENONET;
+	if (n_routes)
+		*n_routes = gr_fib4_n_routes(v.rib);
+	if (tbl8_used)
+		*tbl8_used = gr_fib4_tbl8_used(v.rib);
+	if (bytes)
+		*bytes = sizeof(uint32_t) * ((uint64_t)GR_FIB4_TBL24_ENTRIES + 256ull * v.num_tbl8);
+	return 0;
+}
+
+// ---------------------------------------------------------------------------
+// queues and submits
+// ---------------------------------------------------------------------------
+
+extern "C" int gr_hip_queue_create(gr_hip_ctx_t *c, void *stream, gr_hip_queue_t **out) {
+	if (c == nullptr || out == nullptr)
+		return -EINVAL;
+	std::lock_guard<std::mutex> l(c->mu);
+	hipSetDevice(c->dev);
+	gr_hip_queue *q = new (std::nothrow) gr_hip_queue();
+	if (q == nullptr)
+		return -ENOMEM;
+	q->ctx = c;
+	q->own_stream = stream == nullptr;
+	if (stream == nullptr) {
+		if (hipStreamCreateWithFlags(&q->s, hipStreamNonBlocking) != hipSuccess) {
+			delete q;
+			return -EIO;
+		}
+	} else {
+		q->s = (hipStream_t)stream;
+	}
+	for (uint32_t i = 0; i < N_TIMED; i++) {
+		hipEventCreate(&q->ev0[i]);
+		hipEventCreate(&q->ev1[i]);
+	}
+	hipEventCreateWithFlags(&q->quiesce, hipEventDisableTiming);
+	size_t sb = sizeof(gr_hip_iface_stats) * FWD4_STAT_SHARDS * c->max_ifaces;
+	if (hipMalloc(&q->d_stats, sb) != hipSuccess || hipMemset(q->d_stats, 0, sb) != hipSuccess) {
+		(void)hipGetLastError();
+		q->d_stats = nullptr;
+	}
+	c->queues.push_back(q);
+	*out = q;
+	return 0;
+}
+
+extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
+	if (q == nullptr)
+		return -EINVAL;
+	gr_hip_ctx *c = q->ctx;
+	hipSetDevice(c->dev);
+	hipStreamSynchronize(q->s);
+	for (host_slot &h : q->hs) {
+		if (h.s) {
+			hipStreamSynchronize(h.s);
+			hipStreamDestroy(h.s);
+		}
+		hipFree(h.in);
+		hipFree(h.out);
+		hipFree(h.meta);
+		hipFree(h.v);
+	}
+	for (uint32_t i = 0; i < N_TIMED; i++) {
+		hipEventDestroy(q->ev0[i]);
+		hipEventDestroy(q->ev1[i]);
+	}
+	hipEventDestroy(q->quiesce);
+	hipFree(q->d_stats);
+	if (q->own_stream)
+		hipStreamDestroy(q->s);
+	(void)hipGetLastError();
+	for (size_t i = 0; i < c->queues.size(); i++) {
+		if (c->queues[i] == q) {
+			c->queues.erase(c->queues.begin() + (long)i);
+			break;
+		}
+	}
+	delete q;
+	return 0;
+}
+
+extern "C" void *gr_hip_queue_stream(gr_hip_queue_t *q) {
+	return q ? (void *)q->s : nullptr;
+}
+
+static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool timed) {
+	gr_hip_ctx *c = q->ctx;
+	fwd4_params P;
+	memset(&P, 0, sizeof(P));
+	P.in = static_cast<const uint8_t *>(b->in_frames);
+	P.out = static_cast<uint8_t *>(b->out_lines);
+	P.meta = b->meta;
+	P.verdicts = b->verdicts;
+	P.n = b->n;
+	P.in_stride = b->in_stride;
+	P.out_stride = b->out_stride;
+	P.readable = (b->flags & GR_HIP_BATCH_F_LINES_ONLY) ? GR_HIP_LINE : b->in_stride;
+	P.ifaces = c->d_ifaces;
+	P.nh = c->d_nh;
+	P.reta = c->d_reta;
+	P.reta_cap = c->d_reta ? (uint32_t)c->reta.size() : 0;
+	P.fibs = c->d_fibs;
+	P.vlan_keys = c->d_vlan_keys;
+	P.vlan_vals = c->d_vlan_vals;
+	P.vlan_mask = c->vlan_cap ? c->vlan_cap - 1 : 0;
+	P.stats = q->d_stats;
+	P.max_ifaces = c->max_ifaces;
+	P.max_nh = c->max_nh;
+	P.edges = c->edges;
+	uint32_t tiles = (b->n + FWD4_BLOCK - 1) / FWD4_BLOCK;
+	uint32_t grid = (uint32_t)c->n_cu * 8;
+	if (grid > tiles)
+		grid = tiles;
+	uint32_t slot = (uint32_t)(q->n_launch % N_TIMED);
+	if (timed)
+		HCK(hipEventRecord(q->ev0[slot], s));
+	HCK(gr_fwd4_launch(&P, grid, s));
+	if (timed) {
+		HCK(hipEventRecord(q->ev1[slot], s));
+		q->n_launch++;
+	}
+	return 0;
+}
+
+static int batch_ok(const gr_hip_batch *b) {
+	if (b == nullptr)
+		return -EINVAL;
+	if (b->n == 0)
+		return 0;
+	if (!b->in_frames || !b->out_lines || !b->meta || !b->verdicts)
+		return -EINVAL;
+	if (b->in_stride < GR_HIP_LINE || b->out_stride < GR_HIP_LINE || (b->in_stride & 15)
+	    || (b->out_stride & 15) || ((uintptr_t)b->in_frames & 15) || ((uintptr_t)b->out_lines & 15)
+	    || ((uintptr_t)b->meta & 7) || ((uintptr_t)b->verdicts & 7))
+		return -EINVAL;
+	if (b->n > (1u << 31))
+		return -E2BIG;
+	return 1;
+}
+
+extern "C" int gr_hip_fwd4_submit(gr_hip_queue_t *q, const struct gr_hip_batch *b) {
+	if (q == nullptr)
+		return -EINVAL;
+	int ok = batch_ok(b);
+	if (ok <= 0)
+		return ok;
+	return launch(q, q->s, b, true);
+}
+
+extern "C" int gr_hip_queue_sync(gr_hip_queue_t *q) {
+	if (q == nullptr)
+		return -EINVAL;
+	HCK(hipStreamSynchronize(q->s));
+	return 0;
+}
+
+extern "C" int gr_hip_queue_kernel_ms(gr_hip_queue_t *q, uint32_t n, float *ms, uint32_t *count) {
+	if (q == nullptr || ms == nullptr)
+		return -EINVAL;
+	uint64_t avail = q->n_launch < N_TIMED ? q->n_launch : N_TIMED;
+	if (n > avail)
+		n = (uint32_t)avail;
+	float total = 0;
+	for (uint32_t k = 0; k < n; k++) {
+		uint32_t slot = (uint32_t)((q->n_launch - 1 - k) % N_TIMED);
+		HCK(hipEventSynchronize(q->ev1[slot]));
+		float t = 0;
+		HCK(hipEventElapsedTime(&t, q->ev0[slot], q->ev1[slot]));
+		total += t;
+	}
+	*ms = total;
+	if (count)
+		*count = n;
+	return 0;
+}
+
+extern "C" int gr_hip_fwd4_host(
+	gr_hip_queue_t *q,
+	const void *lines,
+	const struct gr_hip_pkt_meta *meta,
+	uint32_t n,
+	void *out_lines,
+	struct gr_hip_verdict *verdicts
+) {
+	if (q == nullptr)
+		return -EINVAL;
+	if (n == 0)
+		return 0;
+	if (!lines || !meta || !out_lines || !verdicts)
+		return -EINVAL;
+	gr_hip_ctx *c = q->ctx;
+	hipSetDevice(c->dev);
+	for (host_slot &h : q->hs) {
+		if (h.s != nullptr)
+			continue;
+		HCK(hipStreamCreateWithFlags(&h.s, hipStreamNonBlocking));
+		HCK(hipMalloc(&h.in, (size_t)HOST_CHUNK * GR_HIP_LINE));
+		HCK(hipMalloc(&h.out, (size_t)HOST_CHUNK * GR_HIP_LINE));
+		HCK(hipMalloc(&h.meta, (size_t)HOST_CHUNK * sizeof(gr_hip_pkt_meta)));
+		HCK(hipMalloc(&h.v, (size_t)HOST_CHUNK * sizeof(gr_hip_verdict)));
+	}
+	// the chunks follow everything already submitted on the queue
+	HCK(hipEventRecord(q->quiesce, q->s));
+	for (host_slot &h : q->hs)
+		HCK(hipStreamWaitEvent(h.s, q->quiesce, 0));
+	const uint8_t *in = static_cast<const uint8_t *>(lines);
+	uint8_t *out = static_cast<uint8_t *>(out_lines);
+	uint32_t k = 0;
+	for (uint32_t off = 0; off < n; off += HOST_CHUNK, k++) {
+		host_slot &h = q->hs[k % HOST_SLOTS];
+		uint32_t cnt = n - off < HOST_CHUNK ? n - off : HOST_CHUNK;
+		HCK(hipMemcpyAsync(h.in, in + (size_t)off * GR_HIP_LINE, (size_t)cnt * GR_HIP_LINE,
+				   hipMemcpyHostToDevice, h.s));
+		HCK(hipMemcpyAsync(h.meta, meta + off, (size_t)cnt * sizeof(*meta), hipMemcpyHostToDevice, h.s));
+		gr_hip_batch b = {h.in, h.out, h.meta, h.v, cnt, GR_HIP_LINE, GR_HIP_LINE, GR_HIP_BATCH_F_LINES_ONLY};
+		int r = launch(q, h.s, &b, false);
+		if (r < 0)
+			return r;
+		HCK(hipMemcpyAsync(out + (size_t)off * GR_HIP_LINE, h.out, (size_t)cnt * GR_HIP_LINE,
+				   hipMemcpyDeviceToHost, h.s));
+		HCK(hipMemcpyAsync(verdicts + off, h.v, (size_t)cnt * sizeof(*verdicts), hipMemcpyDeviceToHost, h.s));
+	}
+	for (host_slot &h : q->hs) {
+		HCK(hipStreamSynchronize(h.s));
+	}
+	return 0;
+}
+
+extern "C" int gr_hip_queue_stats(gr_hip_queue_t *q, struct gr_hip_iface_stats *st, uint32_t max, int reset) {
+	if (q == nullptr || (st == nullptr && max))
+		return -EINVAL;
+	gr_hip_ctx *c = q->ctx;
+	if (q->d_stats == nullptr)
+		return -ENOMEM;
+	hipSetDevice(c->dev);
+	std::vector<gr_hip_iface_stats> all((size_t)FWD4_STAT_SHARDS * c->max_ifaces);
+	HCK(hipStreamSynchronize(q->s));
+	for (host_slot &h : q->hs)
+		if (h.s)
+			HCK(hipStreamSynchronize(h.s));
+	HCK(hipMemcpy(all.data(), q->d_stats, all.size() * sizeof(gr_hip_iface_stats), hipMemcpyDeviceToHost));
+	uint32_t m = max < c->max_ifaces ? max : c->max_ifaces;
+	memset(st, 0, (size_t)max * sizeof(*st));
+	for (uint32_t s = 0; s < FWD4_STAT_SHARDS; s++) {
+		for (uint32_t i = 0; i < m; i++) {
+			const gr_hip_iface_stats &x = all[(size_t)s * c->max_ifaces + i];
+			st[i].rx_packets += x.rx_packets;
+			st[i].rx_bytes += x.rx_bytes;
+			st[i].tx_packets += x.tx_packets;
+			st[i].tx_bytes += x.tx_bytes;
+		}
+	}
+	if (reset)
+		HCK(hipMemset(q->d_stats, 0, all.size() * sizeof(gr_hip_iface_stats)));
+	return 0;
+}
+
+// ---------------------------------------------------------------------------
+// memory helpers
+// ---------------------------------------------------------------------------
+
+extern "C" int gr_hip_dev_alloc(gr_hip_ctx_t *c, size_t bytes, void **p) {
+	if (c == nullptr || p == nullptr)
+		return -EINVAL;
+	hipSetDevice(c->dev);
+	HCK(hipMalloc(p, bytes));
+	return 0;
+}
+
+extern "C" int gr_hip_dev_free(gr_hip_ctx_t *c, void *p) {
+	if (c == nullptr)
+		return -EINVAL;
+	HCK(hipFree(p));
+	return 0;
+}
+
+extern "C" int gr_hip_host_alloc(gr_hip_ctx_t *c, size_t bytes, void **p) {
+	if (c == nullptr || p == nullptr)
+		return -EINVAL;
+	hipSetDevice(c->dev);
+	HCK(hipHostMalloc(p, bytes, hipHostMallocDefault));
+	return 0;
+}
+
+extern "C" int gr_hip_host_free(gr_hip_ctx_t *c, void *p) {
+	if (c == nullptr)
+		return -EINVAL;
+	HCK(hipHostFree(p));
+	return 0;
+}
+
+extern "C" int gr_hip_memcpy_h2d(gr_hip_ctx_t *c, void *dst, const void *src, size_t n) {
+	if (c == nullptr)
+		return -EINVAL;
+	hipSetDevice(c->dev);
+	HCK(hipMemcpy(dst, src, n, hipMemcpyHostToDevice));
+	return 0;
+}
+
+extern "C" int gr_hip_memcpy_d2h(gr_hip_ctx_t *c, void *dst, const void *src, size_t n) {
+	if (c == nullptr)
+		return -EINVAL;
+	hipSetDevice(c->dev);
+	HCK(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
+	return 0;
+}

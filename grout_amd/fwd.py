@@ -1,0 +1,154 @@
+# SPDX-License-Identifier: BSD-3-Clause
+"""Python handle on the HIP fast path (thin layer over include/grout_hip.h).
+
+Mirrors the way grout's control plane drives the datapath: objects are
+pushed with iface/nexthop/route calls (modules/infra/control/*.c,
+modules/ip/control/route.c) and packets are handed over in batches per
+queue (one queue per RX queue / worker, modules/infra/control/worker.c).
+Every call goes to libgrout_hip.so; there is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+
+from . import abi
+from .abi import check, ptr
+
+
+class FastPath:
+    def __init__(self, dev=0, max_ifaces=1024, max_nexthops=1 << 17):
+        self.lib = abi.hip()
+        h = ctypes.c_void_p()
+        check("gr_hip_init", self.lib.gr_hip_init(dev, max_ifaces, max_nexthops, ctypes.byref(h)))
+        self.h = h
+        self.max_ifaces = max_ifaces
+        self.max_nexthops = max_nexthops
+        self.queues = []
+
+    def close(self):
+        if self.h:
+            for q in self.queues:
+                q._h = None
+            self.lib.gr_hip_fini(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- objects -------------------------------------------------------------
+    def set_ifaces(self, ifaces):
+        a = np.ascontiguousarray(ifaces[ifaces["id"] != 0], dtype=abi.IFACE_DT)
+        check("gr_hip_iface_set", self.lib.gr_hip_iface_set(self.h, ptr(a), len(a)))
+
+    def del_iface(self, iface_id):
+        check("gr_hip_iface_del", self.lib.gr_hip_iface_del(self.h, iface_id))
+
+    def set_nexthops(self, nh, first=1):
+        a = np.ascontiguousarray(nh, dtype=abi.NH_DT)
+        check("gr_hip_nh_set", self.lib.gr_hip_nh_set(self.h, first, ptr(a), len(a)))
+
+    def set_reta(self, reta, first=0):
+        a = np.ascontiguousarray(reta, dtype=np.uint32)
+        if len(a):
+            check("gr_hip_reta_set", self.lib.gr_hip_reta_set(self.h, first, ptr(a), len(a)))
+
+    def fib_create(self, vrf_id, max_routes=1 << 16, num_tbl8=0):
+        check("gr_hip_fib4_create", self.lib.gr_hip_fib4_create(self.h, vrf_id, max_routes, num_tbl8))
+
+    def fib_destroy(self, vrf_id):
+        check("gr_hip_fib4_destroy", self.lib.gr_hip_fib4_destroy(self.h, vrf_id))
+
+    def route_add(self, routes, replace=False):
+        a = np.ascontiguousarray(routes, dtype=abi.ROUTE_DT)
+        check("gr_hip_route4_add", self.lib.gr_hip_route4_add(self.h, ptr(a), len(a), 1 if replace else 0))
+
+    def route_del(self, vrf_id, ip_host, prefixlen):
+        import socket
+        import struct
+        be = struct.unpack("<I", socket.inet_aton(socket.inet_ntoa(struct.pack(">I", ip_host))))[0]
+        check("gr_hip_route4_del", self.lib.gr_hip_route4_del(self.h, vrf_id, be, prefixlen))
+
+    def fib_commit(self, vrf_id):
+        check("gr_hip_fib4_commit", self.lib.gr_hip_fib4_commit(self.h, vrf_id))
+
+    def fib_lookup(self, vrf_id, ip_host):
+        out = ctypes.c_uint32()
+        be = int.from_bytes(ip_host.to_bytes(4, "big"), "little")
+        check("gr_hip_fib4_lookup_host", self.lib.gr_hip_fib4_lookup_host(self.h, vrf_id, be, ctypes.byref(out)))
+        return out.value
+
+    def fib_info(self, vrf_id):
+        n, u, b = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint64()
+        check("gr_hip_fib4_info", self.lib.gr_hip_fib4_info(self.h, vrf_id, ctypes.byref(n), ctypes.byref(u), ctypes.byref(b)))
+        return dict(routes=n.value, tbl8_used=u.value, dev_bytes=b.value)
+
+    def load(self, topo):
+        """Push a grout_amd.topology.Topology (ifaces, nexthops, reta, FIBs)."""
+        self.set_ifaces(topo.ifaces)
+        if topo.n_nh:
+            self.set_nexthops(topo.nh[1:topo.n_nh + 1], first=1)
+        self.set_reta(topo.reta)
+        routes = topo.route_array()
+        for vrf_id, (max_routes, num_tbl8) in topo.fibs.items():
+            self.fib_create(vrf_id, max_routes, num_tbl8)
+        if len(routes):
+            self.route_add(routes)
+        for vrf_id in topo.fibs:
+            self.fib_commit(vrf_id)
+
+    def queue(self, stream=None):
+        q = Queue(self, stream)
+        self.queues.append(q)
+        return q
+
+
+class Queue:
+    def __init__(self, fp, stream=None):
+        self.fp = fp
+        self.lib = fp.lib
+        h = ctypes.c_void_p()
+        check("gr_hip_queue_create", self.lib.gr_hip_queue_create(fp.h, stream, ctypes.byref(h)))
+        self._h = h
+
+    @property
+    def stream(self):
+        return self.lib.gr_hip_queue_stream(self._h)
+
+    def submit(self, in_frames, out_lines, meta, verdicts, n, in_stride=64, out_stride=64, lines_only=False):
+        """Enqueue the fused kernel on device buffers (torch tensors / pointers)."""
+        b = abi.Batch(ptr(in_frames), ptr(out_lines), ptr(meta), ptr(verdicts), n, in_stride,
+                      out_stride, abi.BATCH_F_LINES_ONLY if lines_only else 0)
+        check("gr_hip_fwd4_submit", self.lib.gr_hip_fwd4_submit(self._h, ctypes.byref(b)))
+
+    def sync(self):
+        check("gr_hip_queue_sync", self.lib.gr_hip_queue_sync(self._h))
+
+    def kernel_ms(self, n):
+        ms, cnt = ctypes.c_float(), ctypes.c_uint32()
+        check("gr_hip_queue_kernel_ms", self.lib.gr_hip_queue_kernel_ms(self._h, n, ctypes.byref(ms), ctypes.byref(cnt)))
+        return ms.value, cnt.value
+
+    def forward_host(self, lines, meta, out_lines=None, verdicts=None):
+        """Host-memory path: header lines + metadata in host memory."""
+        n = len(meta)
+        lines = np.ascontiguousarray(lines)
+        meta = np.ascontiguousarray(meta, dtype=abi.META_DT)
+        if out_lines is None:
+            out_lines = np.empty((n, abi.LINE), dtype=np.uint8)
+        if verdicts is None:
+            verdicts = np.empty(n, dtype=abi.VERDICT_DT)
+        check("gr_hip_fwd4_host", self.lib.gr_hip_fwd4_host(self._h, ptr(lines), ptr(meta), n, ptr(out_lines), ptr(verdicts)))
+        return out_lines, verdicts
+
+    def stats(self, reset=False):
+        st = np.zeros(self.fp.max_ifaces, dtype=abi.STATS_DT)
+        check("gr_hip_queue_stats", self.lib.gr_hip_queue_stats(self._h, ptr(st), len(st), 1 if reset else 0))
+        return st
+
+    def close(self):
+        if self._h:
+            self.lib.gr_hip_queue_destroy(self._h)
+            self._h = None

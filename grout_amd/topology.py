@@ -1,0 +1,231 @@
+# SPDX-License-Identifier: BSD-3-Clause
+"""Control-plane objects for the fast path, built with grout's semantics.
+
+A Topology holds the iface table, the nexthop slots, the ECMP reta and the
+routes exactly as grout's control plane would leave them for the datapath:
+
+* add_port / add_vrf / add_vlan: struct iface (modules/infra/control/iface.h:
+  20-35); VRF id 1 is the default VRF (gr_infra.h:51).
+* add_address: addr4_add (modules/ip/control/address.c:60-115) -- one L3
+  nexthop flagged LOCAL|LINK, REACHABLE, carrying the iface MAC, and a route
+  on the address prefix (host bits masked by the FIB).
+* add_nexthop: a gr_nexthop_info_l3 (gr_nexthop.h:93-105); a MAC makes it
+  REACHABLE (l3_nexthop.c:244-250), no address makes it a LINK nexthop
+  (l3_nexthop.c:232-236).
+* add_group: GR_NH_T_GROUP with a power-of-two reta (nexthop.h:80-96).
+* add_route: gr_ip4_route_add_req (modules/ip/api/gr_ip4.h:47-56).
+
+The same arrays feed the HIP library (grout_amd.fwd) and the test oracle.
+"""
+import ipaddress
+
+import numpy as np
+
+from . import abi
+
+
+def ip4(s):
+    """'a.b.c.d' -> host-order int."""
+    return int(ipaddress.IPv4Address(s))
+
+
+def mac_bytes(m):
+    if isinstance(m, (bytes, bytearray)):
+        return bytes(m)
+    return bytes(int(x, 16) for x in m.split(":"))
+
+
+class Topology:
+    def __init__(self, max_ifaces=1024, max_nexthops=1 << 17):
+        self.max_ifaces = max_ifaces
+        self.max_nexthops = max_nexthops
+        self.ifaces = np.zeros(max_ifaces, dtype=abi.IFACE_DT)
+        self.nh = np.zeros(max_nexthops + 1, dtype=abi.NH_DT)  # slot 0 = NULL
+        self.n_nh = 0  # highest slot used
+        self.reta = np.zeros(0, dtype=np.uint32)
+        self.routes = []  # list of ROUTE_DT arrays
+        self.fibs = {}  # vrf_id -> (max_routes, num_tbl8)
+
+    # -- interfaces ---------------------------------------------------------
+    def _iface(self, iface_id, itype, mode, flags, mtu, vrf_id, mac, **kw):
+        if not 0 < iface_id < self.max_ifaces:
+            raise ValueError("iface id")
+        r = self.ifaces[iface_id]
+        r["id"] = iface_id
+        r["type"] = abi.IFACE_TYPE[itype]
+        r["mode"] = abi.IFACE_MODE[mode] if isinstance(mode, str) else mode
+        r["flags"] = flags
+        r["mtu"] = mtu
+        r["vrf_id"] = vrf_id
+        if mac is not None:
+            r["mac"] = np.frombuffer(mac_bytes(mac), np.uint8)
+            r["mac_ok"] = 1
+        else:
+            r["mac"] = 0
+            r["mac_ok"] = 0
+        for k, v in kw.items():
+            r[k] = v
+        return iface_id
+
+    def add_vrf(self, vrf_id=1, mac=None, max_routes=1 << 16, num_tbl8=0):
+        """A VRF iface and its IPv4 FIB (vrf.c, route.c:100-122)."""
+        self._iface(vrf_id, "VRF", "VRF", abi.IFACE_F_UP, 1500, vrf_id, mac)
+        self.fibs[vrf_id] = (max_routes, num_tbl8)
+        return vrf_id
+
+    def add_port(self, iface_id, port_id, mac, vrf_id=1, mtu=1500, up=True, mode="VRF", flags=0):
+        f = (abi.IFACE_F_UP if up else 0) | flags
+        return self._iface(iface_id, "PORT", mode, f, mtu, vrf_id, mac, port_id=port_id)
+
+    def add_vlan(self, iface_id, parent_id, vlan_id, mac=None, vrf_id=1, mtu=1500, up=True, flags=0):
+        if mac is None:  # iface_vlan_get_eth_addr falls back to the parent (vlan.c:174-190)
+            p = self.ifaces[parent_id]
+            mac = bytes(p["mac"]) if p["mac_ok"] else None
+        f = (abi.IFACE_F_UP if up else 0) | flags
+        return self._iface(iface_id, "VLAN", "VRF", f, mtu, vrf_id, mac,
+                           vlan_id=vlan_id, parent_id=parent_id)
+
+    def add_iface(self, iface_id, itype, mac=None, vrf_id=1, mode="VRF", mtu=1500, up=True, flags=0, **kw):
+        f = (abi.IFACE_F_UP if up else 0) | flags
+        return self._iface(iface_id, itype, mode, f, mtu, vrf_id, mac, **kw)
+
+    def iface_mac(self, iface_id):
+        r = self.ifaces[iface_id]
+        return bytes(r["mac"]) if r["mac_ok"] else None
+
+    # -- nexthops -----------------------------------------------------------
+    def _slot(self, slot):
+        if slot is None:
+            slot = self.n_nh + 1
+        if not 0 < slot <= self.max_nexthops:
+            raise ValueError("nexthop slot")
+        self.n_nh = max(self.n_nh, slot)
+        return slot
+
+    def add_nexthop(self, iface_id, ipv4=None, mac=None, nh_type="L3", state=None, flags=0,
+                    vrf_id=None, slot=None):
+        slot = self._slot(slot)
+        r = self.nh[slot]
+        r["type"] = abi.NH_T[nh_type]
+        r["iface_id"] = iface_id
+        r["vrf_id"] = vrf_id if vrf_id is not None else (self.ifaces[iface_id]["vrf_id"] if iface_id else 1)
+        if nh_type == "L3":
+            if ipv4 is None:
+                r["af"] = abi.AF_UNSPEC
+                flags |= abi.NH_F_LINK
+            else:
+                r["af"] = abi.AF_IP4
+                r["ipv4"] = ip4(ipv4) if isinstance(ipv4, str) else ipv4
+            if mac is not None:
+                r["mac"] = np.frombuffer(mac_bytes(mac), np.uint8)
+                if state is None:
+                    state = abi.NH_S["REACHABLE"]
+        r["flags"] = flags
+        r["state"] = state if state is not None else abi.NH_S["NEW"]
+        return slot
+
+    def add_address(self, iface_id, cidr):
+        """addr4_add: LOCAL|LINK nexthop + route on the address prefix."""
+        net = ipaddress.IPv4Interface(cidr)
+        slot = self.add_nexthop(iface_id, str(net.ip), self.iface_mac(iface_id),
+                                flags=abi.NH_F_LOCAL | abi.NH_F_LINK,
+                                state=abi.NH_S["REACHABLE"])
+        self.add_route(self.ifaces[iface_id]["vrf_id"], f"{net.ip}/{net.network.prefixlen}", slot)
+        return slot
+
+    def add_group(self, members, reta_size=None, slot=None):
+        """GR_NH_T_GROUP: members spread round-robin over a power-of-two reta."""
+        slot = self._slot(slot)
+        r = self.nh[slot]
+        r["type"] = abi.NH_T["GROUP"]
+        r["n_members"] = len(members)
+        r["single"] = members[0] if len(members) == 1 else 0
+        if reta_size is None:
+            reta_size = 1
+            while reta_size < 4 * max(1, len(members)):
+                reta_size *= 2
+        if reta_size & (reta_size - 1):
+            raise ValueError("reta size must be a power of two")
+        r["reta_size"] = reta_size
+        r["reta_off"] = len(self.reta)
+        fill = np.array([members[i % len(members)] for i in range(reta_size)] if members else
+                        [0] * reta_size, dtype=np.uint32)
+        self.reta = np.concatenate([self.reta, fill])
+        return slot
+
+    # -- routes ---------------------------------------------------------------
+    def add_route(self, vrf_id, cidr, nh_slot):
+        net = ipaddress.IPv4Network(cidr, strict=False)
+        a = np.zeros(1, dtype=abi.ROUTE_DT)
+        a["ip"] = int(net.network_address)
+        a["prefixlen"] = net.prefixlen
+        a["vrf_id"] = vrf_id
+        a["nh"] = nh_slot
+        self.routes.append(a)
+
+    def add_routes(self, arr):
+        self.routes.append(np.ascontiguousarray(arr, dtype=abi.ROUTE_DT))
+
+    def route_array(self):
+        if not self.routes:
+            return np.zeros(0, dtype=abi.ROUTE_DT)
+        # np.concatenate normalises byte order: convert back to the C layout
+        return np.concatenate(self.routes).astype(abi.ROUTE_DT)
+
+    def live_ifaces(self):
+        return self.ifaces[self.ifaces["id"] != 0]
+
+
+# ---------------------------------------------------------------------------
+# the BASELINE topologies
+# ---------------------------------------------------------------------------
+PORT_MAC = ["02:00:00:00:00:0%d" % p for p in range(4)]
+SRC_MAC = "02:00:00:ff:ff:ff"
+VRF_MAIN = 1
+PORT_IFACE = [2, 3, 4, 5]  # p0..p3
+N_FULLVIEW_NH = 2048
+
+
+def base_ports(max_routes=1 << 16, num_tbl8=0, max_nexthops=1 << 17):
+    t = Topology(max_nexthops=max_nexthops)
+    t.add_vrf(VRF_MAIN, max_routes=max_routes, num_tbl8=num_tbl8)
+    for p in range(4):
+        t.add_port(PORT_IFACE[p], p, PORT_MAC[p])
+    return t
+
+
+def config_single_route():
+    """smoke/ip_forward_test.sh:7-13 with nexthop 45 resolved (config 2)."""
+    t = base_ports()
+    t.add_address(PORT_IFACE[0], "172.16.0.1/24")
+    t.add_address(PORT_IFACE[1], "172.16.1.1/24")
+    gw = t.add_nexthop(PORT_IFACE[0], "172.16.0.2")  # 16.0.0.0/16 via 172.16.0.2 (unresolved)
+    t.add_route(VRF_MAIN, "16.0.0.0/16", gw)
+    nh45 = t.add_nexthop(PORT_IFACE[1], "172.16.1.2", "02:00:00:01:00:2d")
+    t.add_route(VRF_MAIN, "16.1.0.0/16", nh45)
+    return t
+
+
+def fullview_nexthops(t, n_nh=N_FULLVIEW_NH):
+    """nh j -> {p(1+(j-1)%3), 100.64.(j>>8).(j&255), 02:00:00:01:(j>>8):(j&255)}."""
+    first = t.n_nh + 1
+    for j in range(1, n_nh + 1):
+        port = 1 + (j - 1) % 3
+        t.add_nexthop(PORT_IFACE[port], f"100.64.{j >> 8}.{j & 255}",
+                      "02:00:00:01:%02x:%02x" % (j >> 8, j & 255), slot=first + j - 1)
+    return first
+
+
+def config_fullview(count=1_000_000):
+    """fib_inject -4 -n count over 2048 REACHABLE nexthops (configs 3-5)."""
+    import ctypes
+    t = base_ports(max_routes=count + 10)
+    first = fullview_nexthops(t)
+    routes = np.zeros(count, dtype=abi.ROUTE_DT)
+    abi.check("gr_synth_fullview_routes",
+              abi.host().gr_synth_fullview_routes(count, VRF_MAIN, first, N_FULLVIEW_NH,
+                                                  routes.ctypes.data))
+    t.add_routes(routes)
+    t.add_address(PORT_IFACE[0], "172.16.0.1/24")
+    del ctypes
+    return t

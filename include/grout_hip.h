@@ -1,0 +1,372 @@
+// SPDX-License-Identifier: BSD-3-Clause
+//
+// grout_hip.h -- C ABI of the MI355X-native IPv4 forwarding fast path.
+//
+// This is the only interface host C code (grout's datapath, a DPDK worker, or a
+// ctypes test) uses to reach the GPU. Plain pointers and sizes, no C++ or torch
+// types, never throws, never exits: every entry point returns 0 or -errno, the
+// convention of grout's control plane (e.g. modules/ip/control/route.c:58,157).
+//
+// What it replaces in the reference (DPDK/grout, paths relative to its root):
+//   * the per-burst walk  iface_input -> eth_input -> ip_input (+ fib4_lookup)
+//     -> ip_forward -> ip_output -> eth_output -> iface_output
+//     (modules/infra/datapath/iface_input.c:52-112, eth_input.c:35-88,
+//      modules/ip/datapath/ip_input.c:47-197, modules/ip/control/route.c:147-167,
+//      modules/ip/datapath/ip_forward.c:14-41, ip_output.c:63-163,
+//      modules/infra/datapath/eth_output.c:28-77, iface_output.c:60-117)
+//     is gr_hip_fwd4_submit(): one fused HIP kernel, one lane per packet.
+//   * the DIR24_8 FIB that route.c:63-98 creates through DPDK rte_fib, and the
+//     rte_fib_add() calls of rib4_insert_or_replace (route.c:212-275), are the
+//     gr_hip_route4_* / gr_hip_fib4_commit entry points (device-resident tables).
+//   * the nexthop / iface objects the nodes dereference (nexthop.h:22-54,
+//     iface.h:20-35) are mirrored with gr_hip_nh_set / gr_hip_iface_set
+//     (hook: GR_EVENT_NEXTHOP_UPDATE, modules/infra/control/nexthop.c:385).
+//   * the dynamic edge registrations (gr_eth_input_add_type eth_input.c:26,
+//     ip_input_register_nexthop_type ip_input.c:36, ip_output_register_*
+//     ip_output.c:94,106, iface_input_mode_register iface_input.c:22,
+//     iface_output_type_register iface_output.c:25) are gr_hip_edges_*.
+//
+// Every per-packet output ("verdict") names the grout node the packet must be
+// handed to next, i.e. one of the next_nodes of the replaced sub-graph
+// (SURVEY.md Appendix A), together with the mbuf private data grout would have
+// left for that node.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GR_HIP_ABI_VERSION 1
+
+// ---------------------------------------------------------------------------
+// Values mirrored from grout's public API (identical numbering).
+// ---------------------------------------------------------------------------
+
+// gr_iface_type_t, modules/infra/api/gr_infra.h:18-28
+enum {
+	GR_HIP_IFACE_TYPE_UNDEF = 0,
+	GR_HIP_IFACE_TYPE_VRF,
+	GR_HIP_IFACE_TYPE_PORT,
+	GR_HIP_IFACE_TYPE_VLAN,
+	GR_HIP_IFACE_TYPE_IPIP,
+	GR_HIP_IFACE_TYPE_BOND,
+	GR_HIP_IFACE_TYPE_BRIDGE,
+	GR_HIP_IFACE_TYPE_VXLAN,
+	GR_HIP_IFACE_TYPE_COUNT,
+};
+
+// gr_iface_flags_t, gr_infra.h:31-37
+#define GR_HIP_IFACE_F_UP 0x0001
+#define GR_HIP_IFACE_F_PROMISC 0x0002
+#define GR_HIP_IFACE_F_PACKET_TRACE 0x0004
+#define GR_HIP_IFACE_F_SNAT_STATIC 0x0008
+#define GR_HIP_IFACE_F_SNAT_DYNAMIC 0x0010
+
+// gr_iface_mode_t, gr_infra.h:56-61
+enum {
+	GR_HIP_IFACE_MODE_VRF = 0,
+	GR_HIP_IFACE_MODE_XC,
+	GR_HIP_IFACE_MODE_BOND,
+	GR_HIP_IFACE_MODE_BRIDGE,
+	GR_HIP_IFACE_MODE_COUNT,
+};
+
+// gr_nh_state_t / gr_nh_flags_t / gr_nh_type_t, modules/infra/api/gr_nexthop.h:12-40
+enum {
+	GR_HIP_NH_S_NEW = 0,
+	GR_HIP_NH_S_PENDING,
+	GR_HIP_NH_S_REACHABLE,
+	GR_HIP_NH_S_STALE,
+	GR_HIP_NH_S_FAILED,
+};
+#define GR_HIP_NH_F_LOCAL 0x01
+#define GR_HIP_NH_F_GATEWAY 0x02
+#define GR_HIP_NH_F_LINK 0x04
+#define GR_HIP_NH_F_MCAST 0x08
+enum {
+	GR_HIP_NH_T_L3 = 1,
+	GR_HIP_NH_T_SR6_OUTPUT,
+	GR_HIP_NH_T_SR6_LOCAL,
+	GR_HIP_NH_T_DNAT,
+	GR_HIP_NH_T_BLACKHOLE,
+	GR_HIP_NH_T_REJECT,
+	GR_HIP_NH_T_GROUP,
+	GR_HIP_NH_T_COUNT,
+};
+
+// eth_domain_t, modules/infra/datapath/eth.h:13-20
+enum {
+	GR_HIP_ETH_DOMAIN_UNKNOWN = 0,
+	GR_HIP_ETH_DOMAIN_LOOPBACK,
+	GR_HIP_ETH_DOMAIN_LOCAL,
+	GR_HIP_ETH_DOMAIN_BROADCAST,
+	GR_HIP_ETH_DOMAIN_MULTICAST,
+	GR_HIP_ETH_DOMAIN_OTHER,
+};
+
+// addr_family_t (api/gr_net_types.h): GR_AF_UNSPEC / GR_AF_IP4 / GR_AF_IP6
+#define GR_HIP_AF_UNSPEC 0
+#define GR_HIP_AF_IP4 1
+#define GR_HIP_AF_IP6 2
+
+// RTE_MBUF_F_RX_IP_CKSUM_* status reduced to what ip_input.c:80-92 tests.
+#define GR_HIP_CKSUM_UNKNOWN 0 // UNKNOWN or NONE: verify in software
+#define GR_HIP_CKSUM_BAD 1
+#define GR_HIP_CKSUM_GOOD 2
+
+#define GR_HIP_IFACE_ID_UNDEF 0 // gr_infra.h:45
+#define GR_HIP_MAX_IFACES 1024 // default GROUT_MAX_IFACES, main/config.c:276
+#define GR_HIP_MAX_NEXTHOPS ((1u << 24) - 1) // nh slot must fit 24 bits
+#define GR_HIP_MAX_NH_GROUP_RETA 4096 // MAX_NH_GROUP_RETA_SIZE, nexthop.h:80
+
+// ---------------------------------------------------------------------------
+// Terminal edges: the next node of the replaced sub-graph a packet goes to.
+// Each value is named after the grout node.
+// ---------------------------------------------------------------------------
+enum gr_hip_edge {
+	GR_HIP_E_PUNT = 0, // not handled on the GPU: run grout's CPU iface_input
+	// iface_input (iface_input.c:13-18, mode edges :20-28)
+	GR_HIP_E_IFACE_MODE_UNKNOWN, // "iface_mode_unknown" (drop)
+	GR_HIP_E_IFACE_INPUT_ADMIN_DOWN, // "iface_input_admin_down" (drop)
+	GR_HIP_E_IFACE_INPUT_UNKNOWN_VLAN, // "iface_input_unknown_vlan" (drop)
+	GR_HIP_E_XCONNECT, // "xconnect" (mode XC)
+	GR_HIP_E_BRIDGE_INPUT, // "bridge_input" (mode BRIDGE; iface_output BRIDGE)
+	// eth_input (eth_input.c:17-22, l2l3 edges :24-32)
+	GR_HIP_E_ETH_INPUT_UNKNOWN_TYPE, // "eth_input_unknown_type" (drop)
+	GR_HIP_E_ETH_INPUT_INVALID_IFACE, // "eth_input_invalid_iface" (drop)
+	GR_HIP_E_SNAP_INPUT, // "snap_input"
+	GR_HIP_E_ARP_INPUT, // "arp_input"
+	GR_HIP_E_IP6_INPUT, // "ip6_input"
+	GR_HIP_E_LACP_INPUT, // "lacp_input"
+	// ip_input (ip_input.c:20-32, nh type edges :34-44)
+	GR_HIP_E_IP_INPUT_LOCAL, // "ip_input_local"
+	GR_HIP_E_IP_INPUT_LOCAL_CT, // local dst on a SNAT_DYNAMIC iface: grout's
+	                            // conntrack picks "ip_input_local" or
+	                            // "dnat44_dynamic" (ip_input.c:170-185)
+	GR_HIP_E_IP_ERROR_DEST_UNREACH, // "ip_error_dest_unreach"
+	GR_HIP_E_IP_INPUT_BAD_CHECKSUM, // "ip_input_bad_checksum" (drop)
+	GR_HIP_E_IP_INPUT_BAD_ADDRESS, // "ip_input_bad_address" (drop)
+	GR_HIP_E_IP_INPUT_BAD_LENGTH, // "ip_input_bad_length" (drop)
+	GR_HIP_E_IP_INPUT_BAD_VERSION, // "ip_input_bad_version" (drop)
+	GR_HIP_E_IP_INPUT_OTHER_HOST, // "ip_input_other_host" (drop)
+	GR_HIP_E_IP_BLACKHOLE, // "ip_blackhole" (drop)
+	GR_HIP_E_DNAT44_STATIC, // "dnat44_static"
+	// ip_forward (ip_forward.c:7-11)
+	GR_HIP_E_IP_ERROR_TTL_EXCEEDED, // "ip_error_ttl_exceeded"
+	// ip_output (ip_output.c:81-90, type edges :92-114)
+	GR_HIP_E_IP_HOLD, // "ip_hold"
+	GR_HIP_E_IP_OUTPUT_ERROR, // "ip_output_error" (drop)
+	GR_HIP_E_IP_FRAGMENT, // "ip_fragment"
+	GR_HIP_E_IP_ERROR_FRAG_NEEDED, // "ip_error_frag_needed"
+	GR_HIP_E_SR6_OUTPUT, // "sr6_output"
+	GR_HIP_E_XVRF, // "xvrf"
+	GR_HIP_E_IPIP_OUTPUT, // "ipip_output"
+	GR_HIP_E_IP_OUTPUT_SNAT, // egress iface has SNAT flags: grout's
+	                         // snat44_process (nat_datapath.h:57-67) then the
+	                         // rest of ip_output run on the CPU
+	// eth_output (eth_output.c:14-19)
+	GR_HIP_E_ETH_OUTPUT_NO_MAC, // "eth_output_no_mac" (drop)
+	// iface_output (iface_output.c:16-21, type edges :23-33)
+	GR_HIP_E_IFACE_OUTPUT_INVAL_TYPE, // "iface_output_inval_type" (drop)
+	GR_HIP_E_IFACE_OUTPUT_ADMIN_DOWN, // "iface_output_admin_down" (drop)
+	GR_HIP_E_IFACE_OUTPUT_VLAN_NO_PARENT, // "iface_output_vlan_no_parent" (drop)
+	GR_HIP_E_BOND_OUTPUT, // "bond_output"
+	GR_HIP_E_VXLAN_OUTPUT, // "vxlan_output"
+	GR_HIP_E_PORT_OUTPUT, // "port_output": the forwarded case
+	GR_HIP_E_COUNT,
+};
+// Registration value meaning "the next node of the chain" (eth_input for an
+// iface mode, ip_input for an ether type, ip_forward for an ip_input nexthop
+// type, eth_output for an ip_output type): never appears in a verdict.
+#define GR_HIP_EDGE_CHAIN 0xff
+
+// ---------------------------------------------------------------------------
+// Control-plane mirrors (host -> device).
+// ---------------------------------------------------------------------------
+
+// Device mirror of struct iface (iface.h:20-35 + __gr_iface_base
+// gr_infra.h:73-87 + the per-type info the datapath reads). 32 bytes.
+struct gr_hip_iface {
+	uint16_t id; // == index in the table; 0 = slot unused
+	uint8_t type; // GR_HIP_IFACE_TYPE_*
+	uint8_t mode; // GR_HIP_IFACE_MODE_*
+	uint16_t flags; // GR_HIP_IFACE_F_*
+	uint16_t mtu; // iface->mtu (default 1500, iface.c:618)
+	uint16_t vrf_id; // L3 domain (GR_IFACE_MODE_VRF)
+	uint16_t port_id; // PORT: iface_info_port(iface)->port_id (port.h:17-30)
+	uint16_t vlan_id; // VLAN: iface_info_vlan(iface)->vlan_id
+	uint16_t parent_id; // VLAN: iface_info_vlan(iface)->parent_id
+	uint8_t mac[6]; // result of iface_get_eth_addr() (iface.c:475-487)
+	uint8_t mac_ok; // 1 if iface_get_eth_addr() succeeded
+	uint8_t _pad0;
+	uint32_t _pad1[2];
+};
+
+// Device mirror of struct nexthop (nexthop.h:22-31) with the L3 info
+// (nexthop.h:41-54, gr_nexthop.h:93-105) or the group info (nexthop.h:80-96).
+// 32 bytes. A nexthop is identified by its slot index (1..); slot 0 is "no
+// nexthop" (NULL), like the FIB value 0 in route.c:65,156.
+struct gr_hip_nh {
+	uint8_t type; // GR_HIP_NH_T_*
+	uint8_t state; // GR_HIP_NH_S_* (L3)
+	uint8_t flags; // GR_HIP_NH_F_* (L3)
+	uint8_t af; // GR_HIP_AF_* (L3)
+	uint16_t iface_id;
+	uint16_t vrf_id;
+	uint32_t ipv4; // network byte order, as ip4_addr_t
+	uint8_t mac[6]; // L3
+	uint16_t reta_size; // GROUP: power of two
+	uint32_t reta_off; // GROUP: first slot of its reta in the reta table
+	uint32_t single; // GROUP: nhg->nh shortcut used when n_members == 1
+	uint16_t n_members; // GROUP
+	uint16_t _pad0;
+};
+
+// One IPv4 route, as gr_ip4_route_add_req (modules/ip/api/gr_ip4.h:47-56).
+struct gr_hip_route4 {
+	uint32_t ip; // network byte order; host bits are ignored (masked)
+	uint8_t prefixlen; // 0..32
+	uint8_t _pad0;
+	uint16_t vrf_id;
+	uint32_t nh; // nexthop slot (1..)
+};
+
+// ---------------------------------------------------------------------------
+// Per-packet data exchanged with the kernel.
+// ---------------------------------------------------------------------------
+
+// Input metadata, 8 bytes per packet: what port_rx leaves in the mbuf and its
+// private data (port_rx.c:281-316, rxtx.h:154-157) and what ip_input reads
+// from rte_mbuf (ip_input.c:70-92,147).
+struct gr_hip_pkt_meta {
+	uint16_t iface; // iface_mbuf_data.iface (RX port iface id)
+	uint16_t vlan_ck; // bits 0-11: iface_mbuf_data.vlan_id;
+	                  // bits 12-13: GR_HIP_CKSUM_* from ol_flags
+	uint16_t pkt_len; // rte_pktmbuf_pkt_len == data_len (single segment)
+	uint16_t rss; // low 16 bits of m->hash.rss (reta_size <= 4096)
+};
+
+// Output verdict, 8 bytes per packet.
+struct gr_hip_verdict {
+	uint8_t edge; // enum gr_hip_edge
+	uint8_t domain; // eth_input_mbuf_data.domain as left by eth_input
+	uint16_t iface; // mbuf_data(m)->iface at that edge (ingress iface
+	                // before ip_output, egress after it, the port after
+	                // iface_output)
+	uint32_t nh; // l3_mbuf_data.nh slot (0 = NULL)
+};
+
+#define GR_HIP_LINE 64 // bytes of frame header staged per packet
+
+// A batch of packets, device-resident.
+//   frame i:   in_frames + i * in_stride   (Ethernet header at offset 0; the
+//              whole pkt_len bytes are readable, in_stride >= 64, % 16 == 0)
+//   output i:  out_lines + i * out_stride  (the first 64 bytes of the frame as
+//              grout leaves them at the verdict's edge; out_lines may equal
+//              in_frames with out_stride == in_stride for in-place rewrite)
+struct gr_hip_batch {
+	const void *in_frames;
+	void *out_lines;
+	const struct gr_hip_pkt_meta *meta;
+	struct gr_hip_verdict *verdicts;
+	uint32_t n;
+	uint32_t in_stride;
+	uint32_t out_stride;
+	uint32_t flags; // GR_HIP_BATCH_F_*
+};
+// Only the first 64 bytes of each frame are present (header-only staging from
+// host mbufs): packets whose IPv4 header does not fit get GR_HIP_E_PUNT.
+#define GR_HIP_BATCH_F_LINES_ONLY 0x1
+
+// Per-iface counters of one queue (iface.h:105-119 subset the path touches).
+struct gr_hip_iface_stats {
+	uint64_t rx_packets;
+	uint64_t rx_bytes;
+	uint64_t tx_packets;
+	uint64_t tx_bytes;
+};
+
+// ---------------------------------------------------------------------------
+// Entry points. All return 0 or -errno unless stated otherwise.
+// ---------------------------------------------------------------------------
+typedef struct gr_hip_ctx gr_hip_ctx_t;
+typedef struct gr_hip_queue gr_hip_queue_t;
+
+// Library / device lifetime. dev = HIP device ordinal.
+int gr_hip_abi_version(void);
+int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, gr_hip_ctx_t **out);
+int gr_hip_fini(gr_hip_ctx_t *ctx);
+const char *gr_hip_strerror(int err);
+
+// Edge registrations (defaults = grout's default module set, applied by init).
+int gr_hip_edges_eth_type(gr_hip_ctx_t *, uint16_t be_ether_type, uint8_t edge);
+int gr_hip_edges_iface_mode(gr_hip_ctx_t *, uint8_t mode, uint8_t edge);
+int gr_hip_edges_ip_input_nh_type(gr_hip_ctx_t *, uint8_t nh_type, uint8_t edge);
+int gr_hip_edges_ip_output_nh_type(gr_hip_ctx_t *, uint8_t nh_type, uint8_t edge);
+int gr_hip_edges_ip_output_iface_type(gr_hip_ctx_t *, uint8_t iface_type, uint8_t edge);
+int gr_hip_edges_iface_output_type(gr_hip_ctx_t *, uint8_t iface_type, uint8_t edge);
+
+// Object mirrors. Changes become visible to submits issued after the call.
+int gr_hip_iface_set(gr_hip_ctx_t *, const struct gr_hip_iface *ifaces, uint32_t n);
+int gr_hip_iface_del(gr_hip_ctx_t *, uint16_t iface_id);
+int gr_hip_nh_set(gr_hip_ctx_t *, uint32_t first_slot, const struct gr_hip_nh *nh, uint32_t n);
+int gr_hip_reta_set(gr_hip_ctx_t *, uint32_t first, const uint32_t *slots, uint32_t n);
+
+// RIB + device FIB (DIR24_8-equivalent, 4-byte entries). Routes are staged in
+// the host RIB; gr_hip_fib4_commit() makes them visible to later submits
+// (stream-ordered swap, the rte_rcu_qsbr_synchronize analogue of route.c:764).
+int gr_hip_fib4_create(gr_hip_ctx_t *, uint16_t vrf_id, uint32_t max_routes, uint32_t num_tbl8);
+int gr_hip_fib4_destroy(gr_hip_ctx_t *, uint16_t vrf_id);
+int gr_hip_route4_add(gr_hip_ctx_t *, const struct gr_hip_route4 *routes, uint32_t n, int replace);
+int gr_hip_route4_del(gr_hip_ctx_t *, uint16_t vrf_id, uint32_t ip, uint8_t prefixlen);
+int gr_hip_fib4_commit(gr_hip_ctx_t *, uint16_t vrf_id);
+// Host-side lookup in the committed tables (control-plane helper, route.c:183).
+int gr_hip_fib4_lookup_host(gr_hip_ctx_t *, uint16_t vrf_id, uint32_t ip_be, uint32_t *nh);
+// Device table geometry: tbl8 groups in use, bytes of device memory.
+int gr_hip_fib4_info(gr_hip_ctx_t *, uint16_t vrf_id, uint32_t *n_routes, uint32_t *tbl8_used, uint64_t *dev_bytes);
+
+// Queues: one per RX queue / worker; each owns a HIP stream. stream == NULL
+// creates a private non-blocking stream, else the given hipStream_t is used.
+int gr_hip_queue_create(gr_hip_ctx_t *, void *stream, gr_hip_queue_t **out);
+int gr_hip_queue_destroy(gr_hip_queue_t *);
+void *gr_hip_queue_stream(gr_hip_queue_t *);
+
+// Device-resident fast path: enqueue the fused kernel on the queue's stream.
+int gr_hip_fwd4_submit(gr_hip_queue_t *, const struct gr_hip_batch *);
+// Wait until everything submitted on the queue is done.
+int gr_hip_queue_sync(gr_hip_queue_t *);
+// Device time in ms of the last `n` submits (HIP events around each launch,
+// ring of 64). Returns the sum; *count receives how many were measured.
+int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *count);
+
+// Host-memory path (header-only staging): copy `n` 64-byte header lines and
+// metadata from host memory, run the kernel, copy lines and verdicts back.
+// Pinned staging inside the queue, double-buffered; completes before return.
+int gr_hip_fwd4_host(
+	gr_hip_queue_t *,
+	const void *lines,
+	const struct gr_hip_pkt_meta *meta,
+	uint32_t n,
+	void *out_lines,
+	struct gr_hip_verdict *verdicts
+);
+
+// Per-iface counters accumulated by the queue's kernels (rx in iface_input,
+// tx in iface_output). `stats` receives max_ifaces entries.
+int gr_hip_queue_stats(gr_hip_queue_t *, struct gr_hip_iface_stats *stats, uint32_t max_ifaces, int reset);
+
+// Device / pinned host memory helpers for C callers without a framework
+// allocator (pinned buffers make gr_hip_fwd4_host copies asynchronous).
+int gr_hip_host_alloc(gr_hip_ctx_t *, size_t bytes, void **ptr);
+int gr_hip_host_free(gr_hip_ctx_t *, void *ptr);
+int gr_hip_dev_alloc(gr_hip_ctx_t *, size_t bytes, void **dptr);
+int gr_hip_dev_free(gr_hip_ctx_t *, void *dptr);
+int gr_hip_memcpy_h2d(gr_hip_ctx_t *, void *dst, const void *src, size_t bytes);
+int gr_hip_memcpy_d2h(gr_hip_ctx_t *, void *dst, const void *src, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif

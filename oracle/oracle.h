@@ -1,0 +1,95 @@
+// SPDX-License-Identifier: BSD-3-Clause
+//
+// oracle.h -- TEST INFRASTRUCTURE ONLY. Not part of the product.
+//
+// A CPU restatement, in plain C, of grout's IPv4 forwarding node chain:
+// iface_input -> eth_input -> ip_input (+ fib4_lookup) -> ip_forward ->
+// ip_output -> eth_output -> iface_output, run through a minimal rte_graph-like
+// burst walk (bursts of 64, modules/infra/control/graph.c:88-91). Every
+// function in oracle.c cites the reference file:line it follows.
+//
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+// this library, and only as the checker / CPU baseline. The product
+// (grout_amd/) never links or calls it.
+//
+// Parity pinning: the reference cannot be built here (DPDK >= 25.11 is fetched
+// over the network). The restatement is pinned by the
+// known-answer cases of the reference's only hot-path unit test
+// (modules/ip/datapath/ip_input.c:302-383, restated in tests/test_oracle_kat.py),
+// by hand-derived cases of ip_forward's checksum arithmetic, and by a
+// brute-force longest-prefix match cross-check of both of its LPMs. FIB parity
+// against DPDK's rte_fib itself is therefore partial (no reference test pins it).
+#pragma once
+
+#include "../include/grout_hip.h"
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct or_topo or_topo_t;
+
+or_topo_t *or_topo_new(uint32_t max_ifaces, uint32_t max_nexthops);
+void or_topo_free(or_topo_t *);
+
+// Same registration surface as grout (eth_input.c:26, ip_input.c:36, ...);
+// or_topo_new() applies grout's default module set.
+int or_edge_eth_type(or_topo_t *, uint16_t be_type, uint8_t edge);
+int or_edge_iface_mode(or_topo_t *, uint8_t mode, uint8_t edge);
+int or_edge_ip_input_nh_type(or_topo_t *, uint8_t nh_type, uint8_t edge);
+int or_edge_ip_output_nh_type(or_topo_t *, uint8_t nh_type, uint8_t edge);
+int or_edge_ip_output_iface_type(or_topo_t *, uint8_t iface_type, uint8_t edge);
+int or_edge_iface_output_type(or_topo_t *, uint8_t iface_type, uint8_t edge);
+
+int or_iface_set(or_topo_t *, const struct gr_hip_iface *, uint32_t n);
+int or_nh_set(or_topo_t *, uint32_t first_slot, const struct gr_hip_nh *, uint32_t n);
+int or_reta_set(or_topo_t *, uint32_t first, const uint32_t *slots, uint32_t n);
+
+// RIB: per-VRF exact-prefix hash tables (one per prefix length).
+int or_fib_create(or_topo_t *, uint16_t vrf_id, uint32_t num_tbl8);
+int or_route_add(or_topo_t *, const struct gr_hip_route4 *, uint32_t n, int replace);
+int or_route_del(or_topo_t *, uint16_t vrf_id, uint32_t ip_be, uint8_t prefixlen);
+// Build the DIR24_8 restatement (DPDK lib/fib/dir24_8, 8-byte entries).
+int or_fib_build(or_topo_t *, uint16_t vrf_id);
+
+// LPM: hash-per-length probe (truth) and DIR24_8 restatement. ip host order.
+// Return the nexthop slot, 0 = no route.
+uint32_t or_lpm_hash(const or_topo_t *, uint16_t vrf_id, uint32_t ip);
+uint32_t or_lpm_dir24(const or_topo_t *, uint16_t vrf_id, uint32_t ip);
+// Brute force over every installed route (small tables only).
+uint32_t or_lpm_brute(const or_topo_t *, uint16_t vrf_id, uint32_t ip);
+
+// Run n packets through the node chain. Same buffer contract as
+// struct gr_hip_batch (grout_hip.h). stats: max_ifaces entries, accumulated.
+int or_process(
+	or_topo_t *,
+	const void *in_frames,
+	uint32_t in_stride,
+	const struct gr_hip_pkt_meta *meta,
+	uint32_t n,
+	void *out_lines,
+	uint32_t out_stride,
+	struct gr_hip_verdict *verdicts,
+	struct gr_hip_iface_stats *stats,
+	uint32_t flags
+);
+
+// CPU baseline: `threads` pthreads, each walks its own copy of the packet
+// stream in bursts of 64 until it has processed `pkts_per_thread` packets.
+// Returns the aggregate Mpps (wall clock, CLOCK_MONOTONIC).
+double or_bench(
+	or_topo_t *,
+	const void *in_frames,
+	uint32_t in_stride,
+	const struct gr_hip_pkt_meta *meta,
+	uint32_t n,
+	int threads,
+	uint64_t pkts_per_thread,
+	uint64_t *forwarded
+);
+
+#ifdef __cplusplus
+}
+#endif

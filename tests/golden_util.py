@@ -1,0 +1,73 @@
+# SPDX-License-Identifier: BSD-3-Clause
+"""Helpers shared by the golden and GPU parity tests."""
+import functools
+import os
+
+import numpy as np
+
+import scenarios as SC
+from grout_amd import abi
+from grout_amd import topology as T
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+
+
+@functools.lru_cache(maxsize=None)
+def _fullview():
+    return T.config_fullview()
+
+
+def topo_for(name):
+    if name == "corpus":
+        return SC.corpus_topology()[0]
+    if name == "single":
+        return T.config_single_route()
+    return _fullview()
+
+
+_loaded = {}
+
+
+def fresh_fastpath_state(fp, topo):
+    """(Re)load topo into the shared FastPath: clear the old objects first."""
+    key = id(topo)
+    if _loaded.get("key") == key:
+        return
+    _loaded.pop("topo", None)
+    # wipe previous state: FIBs, ifaces, nexthops
+    for vrf in list(_loaded.get("fibs", [])):
+        fp.fib_destroy(vrf)
+    for i in _loaded.get("ifaces", []):
+        fp.del_iface(int(i))
+    fp.set_nexthops(np.zeros(fp.max_nexthops, dtype=abi.NH_DT), first=1)
+    fp.load(topo)
+    _loaded.update(key=key, fibs=list(topo.fibs), ifaces=list(topo.live_ifaces()["id"]), topo=topo)
+
+
+def run_gpu(fp, topo, frames, meta, lines_only=False, inplace=False, q=None):
+    """Device-resident path through the C ABI; returns (lines, verdicts, stats)."""
+    import torch
+    fresh_fastpath_state(fp, topo)
+    dev = torch.device("cuda")
+    if q is None:
+        if "q" not in _loaded:
+            _loaded["q"] = fp.queue(torch.cuda.current_stream().cuda_stream)
+        q = _loaded["q"]
+    n = len(meta)
+    stride = frames.shape[1]
+    fin = torch.from_numpy(np.ascontiguousarray(frames).reshape(-1)).to(dev)
+    me = torch.from_numpy(np.ascontiguousarray(meta).view(np.uint8)).to(dev)
+    out = fin if inplace else torch.zeros(n * abi.LINE, dtype=torch.uint8, device=dev)
+    v = torch.zeros(n * 8, dtype=torch.uint8, device=dev)
+    q.stats(reset=True)
+    q.submit(fin, out, me, v, n, in_stride=stride, out_stride=stride if inplace else abi.LINE,
+             lines_only=lines_only)
+    q.sync()
+    lines = out.cpu().numpy().reshape(n, -1)[:, :abi.LINE].copy()
+    verdicts = v.cpu().numpy().view(abi.VERDICT_DT).copy()
+    st = q.stats(reset=True)
+    return lines, verdicts, st

@@ -1,0 +1,191 @@
+# SPDX-License-Identifier: BSD-3-Clause
+"""Parity of the HIP fast path (through the C ABI) with the oracle.
+
+Bit-exact on integer/byte work: verdict (edge, domain, iface, nexthop),
+the 64-byte header line each packet leaves with, and the per-iface rx/tx
+counters, on the same seeded inputs -- from the exception corpus up to the
+BASELINE full size (16M packets over the 1M-route view)."""
+import numpy as np
+import pytest
+
+import oracle
+import scenarios as SC
+from golden_util import _fullview, fresh_fastpath_state, run_gpu
+from grout_amd import abi
+from grout_amd import synth as S
+from grout_amd import topology as T
+
+pytestmark = pytest.mark.gpu
+
+
+def compare(o_res, g_res, labels=None):
+    out_o, v_o, st_o = o_res
+    out_g, v_g, st_g = g_res
+    bad = np.nonzero(v_o != v_g)[0]
+    assert len(bad) == 0, [((labels[i] if labels else i), v_o[i], v_g[i]) for i in bad[:8]]
+    badl = np.nonzero((out_o != out_g).any(axis=1))[0]
+    assert len(badl) == 0, [(labels[i] if labels else i) for i in badl[:8]]
+    assert np.array_equal(st_o, st_g)
+
+
+def test_corpus_full_frames(fastpath):
+    t, _ = SC.corpus_topology()
+    fr, me, lab = SC.corpus_arrays()
+    compare(oracle.Oracle(t).process(fr, me), run_gpu(fastpath, t, fr, me), lab)
+
+
+def test_corpus_lines_only(fastpath):
+    """Header-only staging: IHL > 12 packets must be punted, others equal."""
+    t, _ = SC.corpus_topology()
+    fr, me, lab = SC.corpus_arrays()
+    fr64 = np.ascontiguousarray(fr[:, :64])
+    o = oracle.Oracle(t).process(fr64, me, lines_only=True)
+    g = run_gpu(fastpath, t, fr64, me, lines_only=True)
+    compare(o, g, lab)
+    punted = {lab[i] for i in np.nonzero(g[1]["edge"] == abi.EDGE["punt"])[0]}
+    assert {"ihl 13 opts", "ihl 15 opts", "ihl 15 bad"} <= punted
+
+
+def test_corpus_stride64_full_mode(fastpath):
+    t, _ = SC.corpus_topology()
+    fr, me, lab = SC.corpus_arrays()
+    fr64 = np.ascontiguousarray(fr[:, :64])
+    compare(oracle.Oracle(t).process(fr64, me), run_gpu(fastpath, t, fr64, me), lab)
+
+
+def test_corpus_in_place(fastpath):
+    t, _ = SC.corpus_topology()
+    fr, me, lab = SC.corpus_arrays()
+    compare(oracle.Oracle(t).process(fr, me), run_gpu(fastpath, t, fr, me, inplace=True), lab)
+
+
+def test_single_route_stream(fastpath):
+    t = T.config_single_route()
+    fr, me = S.stream(1 << 20, S.SEED_SINGLE, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    o = oracle.Oracle(t).process(fr, me)
+    assert (o[1]["edge"] == abi.EDGE["port_output"]).all()
+    compare(o, run_gpu(fastpath, t, fr, me))
+
+
+def test_fullview_full_size(fastpath):
+    """BASELINE config 3 at full size: 16M x 64 B over the 1M-route FIB."""
+    t = _fullview()
+    fr, me = S.stream(1 << 24, S.SEED_FULLVIEW, routes=t.route_array())
+    o = oracle.Oracle(t).process(fr, me)
+    g = run_gpu(fastpath, t, fr, me)
+    compare(o, g)
+    assert (g[1]["edge"] == abi.EDGE["port_output"]).mean() > 0.99
+
+
+def test_fullview_random_dst(fastpath):
+    """Uniformly random destinations: misses, tbl8 hits, /32s."""
+    t = _fullview()
+    fr, me = S.stream(1 << 20, 0xD57, dst_range=(0, (1 << 32) - 1))
+    compare(oracle.Oracle(t).process(fr, me), run_gpu(fastpath, t, fr, me))
+
+
+def test_imix_full_frames(fastpath):
+    """BASELINE config 4: IMIX frames in 2048-byte mbuf-like slots."""
+    t = _fullview()
+    fr, me = S.stream(1 << 17, S.SEED_IMIX, routes=t.route_array(), imix=True, stride=2048)
+    compare(oracle.Oracle(t).process(fr, me), run_gpu(fastpath, t, fr, me))
+
+
+def test_host_memory_path(fastpath):
+    """gr_hip_fwd4_host: header lines in host memory, chunked H2D/D2H."""
+    t = _fullview()
+    fresh_fastpath_state(fastpath, t)
+    fr, me = S.stream(600_000, S.SEED_IMIX, routes=t.route_array(), imix=True, lines_only=True)
+    o = oracle.Oracle(t).process(fr, me, lines_only=True)
+    q = fastpath.queue()
+    q.stats(reset=True)
+    lines, v = q.forward_host(fr, me)
+    st = q.stats(reset=True)
+    q.close()
+    compare(o, (lines, v, st))
+
+
+def test_live_fib_updates(fastpath):
+    """Routes added / replaced / deleted after the first commit."""
+    t, nh = SC.corpus_topology()
+    fr, me, lab = SC.corpus_arrays()
+    run_gpu(fastpath, t, fr, me)  # loads t
+    changes = [("add", "200.1.0.0/16", nh["fwd"]), ("add", "16.1.0.0/17", nh["fwd2"]),
+               ("del", "10.90.1.7/32", None), ("add", "10.66.1.0/24", nh["fwd"]),
+               ("add", "0.0.0.0/0", nh["fwd3"]), ("del", "10.70.0.0/16", None)]
+    o = oracle.Oracle(t, build_dir24=False)
+    for op, cidr, slot in changes:
+        net = T.ipaddress.IPv4Network(cidr)
+        if op == "add":
+            r = np.zeros(1, dtype=abi.ROUTE_DT)
+            r["ip"], r["prefixlen"], r["vrf_id"], r["nh"] = int(net.network_address), net.prefixlen, 1, slot
+            fastpath.route_add(r)
+            assert o.L.or_route_add(o.h, r.ctypes.data, 1, 0) == 0
+        else:
+            fastpath.route_del(1, int(net.network_address), net.prefixlen)
+            be = int.from_bytes(int(net.network_address).to_bytes(4, "big"), "little")
+            assert o.L.or_route_del(o.h, 1, be, net.prefixlen) == 0
+    fastpath.fib_commit(1)
+    o.L.or_fib_build(o.h, 1)
+    compare(o.process(fr, me), run_gpu(fastpath, t, fr, me), lab)
+    # control-plane lookup agrees too
+    for d in ["200.1.2.3", "16.1.0.1", "16.1.200.1", "10.90.1.7", "10.66.1.9", "1.2.3.4"]:
+        assert fastpath.fib_lookup(1, T.ip4(d)) == o.lpm(1, T.ip4(d), "dir24")
+    fresh_fastpath_state(fastpath, T.config_single_route())  # drop the modified state
+
+
+def test_edge_registration(fastpath):
+    """gr_hip_edges_* re-route like grout's *_register hooks."""
+    t, _ = SC.corpus_topology()
+    fr, me, lab = SC.corpus_arrays()
+    run_gpu(fastpath, t, fr, me)
+    L, h = fastpath.lib, fastpath.h
+    o = oracle.Oracle(t)
+    # an extra ether type, blackhole treated as forward, XC mode into eth_input
+    for fn, ofn, key, e in [("gr_hip_edges_eth_type", "eth_type", 0x3412, abi.EDGE["ip6_input"]),
+                            ("gr_hip_edges_ip_input_nh_type", "ip_input_nh_type", abi.NH_T["BLACKHOLE"], abi.EDGE_CHAIN),
+                            ("gr_hip_edges_iface_mode", "iface_mode", abi.IFACE_MODE["XC"], abi.EDGE_CHAIN),
+                            ("gr_hip_edges_iface_output_type", "iface_output_type", abi.IFACE_TYPE["BOND"], abi.EDGE["port_output"])]:
+        assert getattr(L, fn)(h, key, e) == 0
+        o.edge(ofn, key, e)
+    try:
+        compare(o.process(fr, me), run_gpu(fastpath, t, fr, me), lab)
+    finally:
+        assert L.gr_hip_edges_eth_type(h, 0x3412, abi.EDGE["eth_input_unknown_type"]) == 0
+        assert L.gr_hip_edges_ip_input_nh_type(h, abi.NH_T["BLACKHOLE"], abi.EDGE["ip_blackhole"]) == 0
+        assert L.gr_hip_edges_iface_mode(h, abi.IFACE_MODE["XC"], abi.EDGE["xconnect"]) == 0
+        assert L.gr_hip_edges_iface_output_type(h, abi.IFACE_TYPE["BOND"], abi.EDGE["bond_output"]) == 0
+
+
+def test_empty_and_ragged_batches(fastpath):
+    t = T.config_single_route()
+    fresh_fastpath_state(fastpath, t)
+    for n in [1, 63, 255, 257, 1000]:
+        fr, me = S.stream(n, S.SEED_SINGLE + n, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+        compare(oracle.Oracle(t).process(fr, me), run_gpu(fastpath, t, fr, me))
+    q = fastpath.queue()
+    q.submit(0, 0, 0, 0, 0)  # n == 0 is a no-op
+    q.sync()
+    with pytest.raises(abi.GrHipError):
+        q.submit(16, 32, 8, 8, 10, in_stride=40)  # stride not a multiple of 16
+    q.close()
+
+
+def test_kernel_timing_api(fastpath):
+    import torch
+    t = T.config_single_route()
+    fresh_fastpath_state(fastpath, t)
+    fr, me = S.stream(1 << 16, 1, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    q = fastpath.queue()
+    dev = torch.device("cuda")
+    fin = torch.from_numpy(fr.reshape(-1)).to(dev)
+    mt = torch.from_numpy(me.view(np.uint8)).to(dev)
+    out = torch.empty_like(fin)
+    v = torch.empty(len(me) * 8, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        q.submit(fin, out, mt, v, len(me))
+    q.sync()
+    ms, cnt = q.kernel_ms(3)
+    assert cnt == 3 and ms > 0
+    q.close()
