@@ -129,6 +129,7 @@ HIP_API = {
     "gr_hip_fwd4_submit": (_I, [_P, ctypes.POINTER(Batch)]),
     "gr_hip_queue_sync": (_I, [_P]),
     "gr_hip_queue_kernel_ms": (_I, [_P, _U32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(_U32)]),
+    "gr_hip_tune": (_I, [_P, ctypes.c_char_p, _I]),
     "gr_hip_fwd4_host": (_I, [_P, _P, _P, _U32, _P, _P]),
     "gr_hip_queue_stats": (_I, [_P, _P, _U32, _I]),
     "gr_hip_host_alloc": (_I, [_P, ctypes.c_size_t, PP]),
@@ -174,9 +175,20 @@ _host = None
 
 
 def hip():
-    """The HIP fast-path library. Raises if it is not built: no fallback."""
+    """The HIP fast-path library. Raises if it is not built: no fallback.
+
+    When PyTorch is importable it is imported first: its bundled HIP runtime
+    carries the same SONAME (libamdhip64.so.7) as /opt/rocm's, so the library
+    then binds to it and the process runs ONE HIP runtime, whose device
+    pointers and streams torch tensors also use. Without torch the library
+    uses /opt/rocm/lib/libamdhip64.so.7 directly.
+    """
     global _hip
     if _hip is None:
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         _hip = _bind(LIB_HIP, HIP_API, "HIP extension libgrout_hip.so")
     return _hip
 

@@ -30,25 +30,39 @@ struct fwd4_edges {
 	uint8_t iout_type[8]; // iface_output iface type -> edge
 };
 
-struct fwd4_params {
-	const uint8_t *in;
-	uint8_t *out;
-	const struct gr_hip_pkt_meta *meta;
-	struct gr_hip_verdict *verdicts;
-	uint32_t n;
-	uint32_t in_stride;
-	uint32_t out_stride;
-	uint32_t readable; // frame bytes present per packet (64 or in_stride)
+// Device-resident per-context tables (updated by the control plane under
+// quiesce, read by every launch through one pointer: scalar loads).
+struct fwd4_tables {
 	const struct gr_hip_iface *ifaces;
 	const struct gr_hip_nh *nh;
 	const uint32_t *reta;
 	const struct fwd4_fib *fibs;
 	const uint32_t *vlan_keys; // (parent << 16 | vlan_id) + 1, 0 = empty
 	const uint16_t *vlan_vals;
-	struct gr_hip_iface_stats *stats; // [FWD4_STAT_SHARDS][max_ifaces]
 	uint32_t reta_cap;
 	uint32_t vlan_mask; // capacity - 1
 	uint32_t max_ifaces;
 	uint32_t max_nh;
 	struct fwd4_edges edges;
+};
+
+// Per-launch kernel arguments.
+struct fwd4_params {
+	const uint8_t *in;
+	uint8_t *out;
+	const struct gr_hip_pkt_meta *meta;
+	struct gr_hip_verdict *verdicts;
+	struct gr_hip_iface_stats *stats; // [FWD4_STAT_SHARDS][max_ifaces]
+	const struct fwd4_tables *T;
+	uint32_t n;
+	uint32_t in_stride;
+	uint32_t out_stride;
+	uint32_t readable; // frame bytes present per packet (64 or in_stride)
+};
+
+// Kernel variants (gr_hip_tune "staging"): how header lines move between
+// HBM and registers.
+enum {
+	FWD4_STAGE_LDS = 0, // coalesced 16 B/lane loads -> LDS -> per-lane rows
+	FWD4_STAGE_DIRECT = 1, // each lane loads / stores its own 64 B line
 };

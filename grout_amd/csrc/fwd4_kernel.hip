@@ -21,6 +21,21 @@
 
 #define CHAIN GR_HIP_EDGE_CHAIN
 
+// What process() reads: table pointers (loaded once from the device-resident
+// fwd4_tables) and the edge tables, copied into LDS once per workgroup so
+// they cost no scalar registers.
+struct kctx {
+	const gr_hip_iface *ifaces;
+	const gr_hip_nh *nh;
+	const uint32_t *reta;
+	const fwd4_fib *fibs;
+	const uint32_t *vlan_keys;
+	const uint16_t *vlan_vals;
+	uint32_t reta_cap, vlan_mask, max_ifaces, max_nh, readable;
+	const fwd4_edges *edges; // LDS copy
+	gr_hip_iface_stats *stats;
+};
+
 struct ifv { // fields of struct gr_hip_iface the path reads
 	uint32_t id, type, mode, flags, mtu, vrf_id, vlan_id, parent_id;
 	uint32_t mac_lo, mac_hi; // bytes 0-3, 4-5
@@ -29,7 +44,7 @@ struct ifv { // fields of struct gr_hip_iface the path reads
 };
 
 // iface_from_id (iface.c:459-466) on the device mirror.
-__device__ __forceinline__ ifv load_iface(const fwd4_params &P, uint32_t id) {
+__device__ __forceinline__ ifv load_iface(const kctx &P, uint32_t id) {
 	ifv r;
 	r.ok = false;
 	if (id == 0 || id >= P.max_ifaces)
@@ -57,7 +72,7 @@ struct nhv { // fields of struct gr_hip_nh
 	uint32_t reta_size, reta_off, single, n_members;
 };
 
-__device__ __forceinline__ nhv load_nh(const fwd4_params &P, uint32_t slot) {
+__device__ __forceinline__ nhv load_nh(const kctx &P, uint32_t slot) {
 	const uint4 *p = reinterpret_cast<const uint4 *>(P.nh + slot);
 	uint4 a = p[0];
 	nhv r;
@@ -78,7 +93,7 @@ __device__ __forceinline__ nhv load_nh(const fwd4_params &P, uint32_t slot) {
 
 // VLAN sub-interface demux, vlan_get_iface (vlan.c:27-34): open addressing
 // on (parent << 16 | vlan) + 1.
-__device__ __forceinline__ uint32_t vlan_lookup(const fwd4_params &P, uint32_t parent, uint32_t vid) {
+__device__ __forceinline__ uint32_t vlan_lookup(const kctx &P, uint32_t parent, uint32_t vid) {
 	if (P.vlan_keys == nullptr)
 		return 0;
 	uint32_t key = ((parent << 16) | vid) + 1;
@@ -101,14 +116,15 @@ struct stat_slot {
 };
 
 // One lane (the wave leader of a key) adds a wave's contribution.
-__device__ __forceinline__ void slot_add(
+__device__ __noinline__ void slot_add(
 	stat_slot *slots,
-	const fwd4_params &P,
+	const kctx &P,
 	uint32_t key,
 	uint32_t pkts,
 	uint32_t bytes
 ) {
 	uint32_t h = (key * 0x9e3779b1u) >> 27; // 32 slots
+#pragma unroll 1
 	for (uint32_t i = 0; i < FWD4_STAT_SLOTS; i++) {
 		uint32_t s = (h + i) & (FWD4_STAT_SLOTS - 1);
 		uint32_t old = atomicCAS(&slots[s].key, 0u, key);
@@ -127,7 +143,7 @@ __device__ __forceinline__ void slot_add(
 }
 
 // Wave-aggregate one counter key per lane (0 = nothing) into the LDS slots.
-__device__ __forceinline__ void wave_count(stat_slot *slots, const fwd4_params &P, uint32_t key, uint32_t len) {
+__device__ __forceinline__ void wave_count(stat_slot *slots, const kctx &P, uint32_t key, uint32_t len) {
 	const int lane = threadIdx.x & 63;
 	for (;;) {
 		unsigned long long act = __ballot(key != 0);
@@ -166,13 +182,13 @@ struct result {
 // The node chain for one packet. w[] is the 64-byte line (little-endian
 // words: byte j is (w[j/4] >> 8*(j%4)) & 0xff), modified in place.
 __device__ __forceinline__ result process(
-	const fwd4_params &P,
+	const kctx &P,
 	uint32_t (&w)[16],
 	const gr_hip_pkt_meta &m,
 	const uint8_t *frame
 ) {
 	result r = {GR_HIP_E_PUNT, 0, m.iface, 0, 0, 0, 0, 0};
-	const fwd4_edges &E = P.edges;
+	const fwd4_edges &E = *P.edges;
 
 	// ---- iface_input (iface_input.c:52-112)
 	ifv cur = load_iface(P, m.iface);
@@ -424,99 +440,170 @@ __device__ __forceinline__ result process(
 	return r;
 }
 
-extern "C" __global__ void __launch_bounds__(FWD4_BLOCK)
-gr_fwd4_kernel(const fwd4_params P) {
-	__shared__ __attribute__((aligned(16))) uint8_t lines[FWD4_BLOCK * FWD4_ROW];
+template <int STAGE, bool STATS>
+__global__ void __launch_bounds__(FWD4_BLOCK) gr_fwd4_kernel(const fwd4_params A) {
+	__shared__ __attribute__((aligned(16))) uint8_t lines[STAGE == FWD4_STAGE_LDS ? FWD4_BLOCK * FWD4_ROW : 16];
 	__shared__ stat_slot slots[FWD4_STAT_SLOTS];
+	__shared__ fwd4_edges edges;
 	const uint32_t tid = threadIdx.x;
+	const fwd4_tables *T = A.T;
 
-	if (tid < FWD4_STAT_SLOTS) {
+	if (tid < sizeof(fwd4_edges))
+		reinterpret_cast<uint8_t *>(&edges)[tid] = reinterpret_cast<const uint8_t *>(&T->edges)[tid];
+	if (STATS && tid < FWD4_STAT_SLOTS) {
 		slots[tid].key = 0;
 		slots[tid].pkts = 0;
 		slots[tid].bytes = 0;
 	}
+	kctx P;
+	P.ifaces = T->ifaces;
+	P.nh = T->nh;
+	P.reta = T->reta;
+	P.fibs = T->fibs;
+	P.vlan_keys = T->vlan_keys;
+	P.vlan_vals = T->vlan_vals;
+	P.reta_cap = T->reta_cap;
+	P.vlan_mask = T->vlan_mask;
+	P.max_ifaces = T->max_ifaces;
+	P.max_nh = T->max_nh;
+	P.readable = A.readable;
+	P.edges = &edges;
+	P.stats = A.stats;
+	__syncthreads();
 
-	const uint32_t n_tiles = (P.n + FWD4_BLOCK - 1) / FWD4_BLOCK;
+	const uint32_t n_tiles = (A.n + FWD4_BLOCK - 1) / FWD4_BLOCK;
 	for (uint32_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
 		const uint32_t base = tile * FWD4_BLOCK;
-		const uint32_t cnt = min((uint32_t)FWD4_BLOCK, P.n - base);
-
-		// stage: 4 lanes per 64-byte line, 16 bytes each (coalesced)
-#pragma unroll
-		for (uint32_t k = 0; k < 4; k++) {
-			uint32_t c = k * FWD4_BLOCK + tid;
-			uint32_t p = c >> 2, part = c & 3;
-			if (p < cnt) {
-				const uint4 *src = reinterpret_cast<const uint4 *>(
-					P.in + (size_t)(base + p) * P.in_stride + part * 16);
-				*reinterpret_cast<uint4 *>(&lines[p * FWD4_ROW + part * 16]) = *src;
-			}
-		}
+		const uint32_t cnt = min((uint32_t)FWD4_BLOCK, A.n - base);
+		const bool live = tid < cnt;
+		uint32_t w[16];
 		gr_hip_pkt_meta m = {0, 0, 0, 0};
-		if (tid < cnt)
-			m = P.meta[base + tid];
-		__syncthreads();
+		if (live)
+			m = A.meta[base + tid];
 
-		result r = {0, 0, 0, 0, 0, 0, 0, 0};
-		if (tid < cnt) {
-			uint32_t w[16];
-			uint4 *row = reinterpret_cast<uint4 *>(&lines[tid * FWD4_ROW]);
+		if (STAGE == FWD4_STAGE_LDS) {
+			// 4 lanes per 64-byte line, 16 bytes each (coalesced)
+#pragma unroll
+			for (uint32_t k = 0; k < 4; k++) {
+				uint32_t c = k * FWD4_BLOCK + tid;
+				uint32_t p = c >> 2, part = c & 3;
+				if (p < cnt) {
+					const uint4 *src = reinterpret_cast<const uint4 *>(
+						A.in + (size_t)(base + p) * A.in_stride + part * 16);
+					*reinterpret_cast<uint4 *>(&lines[p * FWD4_ROW + part * 16]) = *src;
+				}
+			}
+			__syncthreads();
+			if (live) {
+				const uint4 *row = reinterpret_cast<const uint4 *>(&lines[tid * FWD4_ROW]);
+#pragma unroll
+				for (int k = 0; k < 4; k++) {
+					uint4 x = row[k];
+					w[4 * k] = x.x;
+					w[4 * k + 1] = x.y;
+					w[4 * k + 2] = x.z;
+					w[4 * k + 3] = x.w;
+				}
+			}
+		} else if (live) {
+			const uint4 *src = reinterpret_cast<const uint4 *>(A.in + (size_t)(base + tid) * A.in_stride);
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
-				uint4 x = row[k];
+				uint4 x = src[k];
 				w[4 * k] = x.x;
 				w[4 * k + 1] = x.y;
 				w[4 * k + 2] = x.z;
 				w[4 * k + 3] = x.w;
 			}
-			const uint8_t *frame = P.in + (size_t)(base + tid) * P.in_stride;
+		}
+
+		result r = {0, 0, 0, 0, 0, 0, 0, 0};
+		if (live) {
+			const uint8_t *frame = A.in + (size_t)(base + tid) * A.in_stride;
 			r = process(P, w, m, frame);
-#pragma unroll
-			for (int k = 0; k < 4; k++)
-				row[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
 			gr_hip_verdict v;
 			v.edge = (uint8_t)r.edge;
 			v.domain = (uint8_t)r.domain;
 			v.iface = (uint16_t)r.iface;
 			v.nh = r.nh;
-			P.verdicts[base + tid] = v;
+			A.verdicts[base + tid] = v;
+			if (STAGE == FWD4_STAGE_DIRECT) {
+				uint4 *dst = reinterpret_cast<uint4 *>(A.out + (size_t)(base + tid) * A.out_stride);
+#pragma unroll
+				for (int k = 0; k < 4; k++)
+					dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+			} else {
+				uint4 *row = reinterpret_cast<uint4 *>(&lines[tid * FWD4_ROW]);
+#pragma unroll
+				for (int k = 0; k < 4; k++)
+					row[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+			}
 		}
-		// counters (every lane of the wave takes part in the ballots)
-		if (P.stats != nullptr) {
+		if (STATS) { // every lane of the wave takes part in the ballots
 			uint32_t len = m.pkt_len;
 			wave_count(slots, P, r.rx_if ? r.rx_if + 1 : 0, len);
 			wave_count(slots, P, r.rx_par ? r.rx_par + 1 : 0, len);
 			wave_count(slots, P, r.tx_if ? (r.tx_if | 0x10000u) + 1 : 0, len);
 			wave_count(slots, P, r.tx_par ? (r.tx_par | 0x10000u) + 1 : 0, len);
 		}
-		__syncthreads();
-
-		// write back: same coalesced mapping
+		if (STAGE == FWD4_STAGE_LDS) {
+			__syncthreads();
 #pragma unroll
-		for (uint32_t k = 0; k < 4; k++) {
-			uint32_t c = k * FWD4_BLOCK + tid;
-			uint32_t p = c >> 2, part = c & 3;
-			if (p < cnt) {
-				uint4 *dst = reinterpret_cast<uint4 *>(
-					P.out + (size_t)(base + p) * P.out_stride + part * 16);
-				*dst = *reinterpret_cast<const uint4 *>(&lines[p * FWD4_ROW + part * 16]);
+			for (uint32_t k = 0; k < 4; k++) {
+				uint32_t c = k * FWD4_BLOCK + tid;
+				uint32_t p = c >> 2, part = c & 3;
+				if (p < cnt) {
+					uint4 *dst = reinterpret_cast<uint4 *>(
+						A.out + (size_t)(base + p) * A.out_stride + part * 16);
+					*dst = *reinterpret_cast<const uint4 *>(&lines[p * FWD4_ROW + part * 16]);
+				}
 			}
+			__syncthreads();
 		}
-		__syncthreads();
 	}
 
-	if (P.stats != nullptr && tid < FWD4_STAT_SLOTS && slots[tid].key != 0) {
-		uint32_t key = slots[tid].key - 1;
-		uint32_t kind = key >> 16, iface = key & 0xffff;
-		gr_hip_iface_stats *st =
-			P.stats + (size_t)(blockIdx.x % FWD4_STAT_SHARDS) * P.max_ifaces + iface;
-		unsigned long long *c = reinterpret_cast<unsigned long long *>(kind ? &st->tx_packets : &st->rx_packets);
-		atomicAdd(c, (unsigned long long)slots[tid].pkts);
-		atomicAdd(c + 1, slots[tid].bytes);
+	if (STATS) {
+		__syncthreads();
+		if (tid < FWD4_STAT_SLOTS && slots[tid].key != 0) {
+			uint32_t key = slots[tid].key - 1;
+			uint32_t kind = key >> 16, iface = key & 0xffff;
+			gr_hip_iface_stats *st =
+				A.stats + (size_t)(blockIdx.x % FWD4_STAT_SHARDS) * P.max_ifaces + iface;
+			unsigned long long *c =
+				reinterpret_cast<unsigned long long *>(kind ? &st->tx_packets : &st->rx_packets);
+			atomicAdd(c, (unsigned long long)slots[tid].pkts);
+			atomicAdd(c + 1, slots[tid].bytes);
+		}
 	}
 }
 
-extern "C" hipError_t gr_fwd4_launch(const fwd4_params *P, uint32_t grid, hipStream_t s) {
-	hipLaunchKernelGGL(gr_fwd4_kernel, dim3(grid), dim3(FWD4_BLOCK), 0, s, *P);
+template <int STAGE, bool STATS>
+static hipError_t launch_one(const fwd4_params *A, uint32_t grid, hipStream_t s) {
+	hipLaunchKernelGGL((gr_fwd4_kernel<STAGE, STATS>), dim3(grid), dim3(FWD4_BLOCK), 0, s, *A);
 	return hipGetLastError();
+}
+
+template <int STAGE, bool STATS>
+static int occ_one() {
+	int b = 0;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gr_fwd4_kernel<STAGE, STATS>, FWD4_BLOCK, 0) != hipSuccess) {
+		(void)hipGetLastError();
+		return 0;
+	}
+	return b;
+}
+
+// stage: FWD4_STAGE_*; stats: counters on/off (off only for measurements).
+extern "C" hipError_t gr_fwd4_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int stage, int stats) {
+	if (stage == FWD4_STAGE_DIRECT)
+		return stats ? launch_one<FWD4_STAGE_DIRECT, true>(A, grid, s)
+			     : launch_one<FWD4_STAGE_DIRECT, false>(A, grid, s);
+	return stats ? launch_one<FWD4_STAGE_LDS, true>(A, grid, s) : launch_one<FWD4_STAGE_LDS, false>(A, grid, s);
+}
+
+// Resident workgroups per CU of a variant (sizes the persistent grid).
+extern "C" int gr_fwd4_occupancy(int stage, int stats) {
+	if (stage == FWD4_STAGE_DIRECT)
+		return stats ? occ_one<FWD4_STAGE_DIRECT, true>() : occ_one<FWD4_STAGE_DIRECT, false>();
+	return stats ? occ_one<FWD4_STAGE_LDS, true>() : occ_one<FWD4_STAGE_LDS, false>();
 }

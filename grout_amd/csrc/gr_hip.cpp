@@ -23,7 +23,8 @@
 #include <string.h>
 #include <vector>
 
-extern "C" hipError_t gr_fwd4_launch(const fwd4_params *P, uint32_t grid, hipStream_t s);
+extern "C" hipError_t gr_fwd4_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int stage, int stats);
+extern "C" int gr_fwd4_occupancy(int stage, int stats);
 
 #define HCK(expr)                                                                                  \
 	do {                                                                                       \
@@ -88,7 +89,13 @@ struct gr_hip_ctx {
 	uint16_t *d_vlan_vals;
 	uint32_t vlan_cap;
 	fwd4_edges edges;
+	fwd4_tables *d_tables; // device copy of what every launch reads
 	std::vector<gr_hip_queue *> queues;
+	// tuning knobs (gr_hip_tune)
+	int stage; // FWD4_STAGE_*
+	int stats_on;
+	int wg_per_cu; // 0 = occupancy of the variant
+	int occ[2][2];
 };
 
 // ---------------------------------------------------------------------------
@@ -112,6 +119,27 @@ static int h2d(gr_hip_ctx *c, void *dst, const void *src, size_t n) {
 }
 
 static int ctl_sync(gr_hip_ctx *c) {
+	HCK(hipStreamSynchronize(c->ctl));
+	return 0;
+}
+
+// Refresh the device-resident fwd4_tables (caller holds c->mu and has
+// quiesced the queues); completes before returning.
+static int upload_tables(gr_hip_ctx *c) {
+	fwd4_tables t;
+	memset(&t, 0, sizeof(t));
+	t.ifaces = c->d_ifaces;
+	t.nh = c->d_nh;
+	t.reta = c->d_reta;
+	t.fibs = c->d_fibs;
+	t.vlan_keys = c->d_vlan_keys;
+	t.vlan_vals = c->d_vlan_vals;
+	t.reta_cap = c->d_reta ? (uint32_t)c->reta.size() : 0;
+	t.vlan_mask = c->vlan_cap ? c->vlan_cap - 1 : 0;
+	t.max_ifaces = c->max_ifaces;
+	t.max_nh = c->max_nh;
+	t.edges = c->edges;
+	HCK(hipMemcpyAsync(c->d_tables, &t, sizeof(t), hipMemcpyHostToDevice, c->ctl));
 	HCK(hipStreamSynchronize(c->ctl));
 	return 0;
 }
@@ -215,9 +243,20 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 		goto fail;
 	if (hipMalloc(&c->d_fibs, sizeof(fwd4_fib) * max_ifaces) != hipSuccess)
 		goto fail;
+	if (hipMalloc(&c->d_tables, sizeof(fwd4_tables)) != hipSuccess)
+		goto fail;
 	if (hipMemset(c->d_ifaces, 0, sizeof(gr_hip_iface) * max_ifaces) != hipSuccess
 	    || hipMemset(c->d_nh, 0, sizeof(gr_hip_nh) * ((size_t)max_nexthops + 1)) != hipSuccess
 	    || hipMemset(c->d_fibs, 0, sizeof(fwd4_fib) * max_ifaces) != hipSuccess)
+		goto fail;
+	c->stage = FWD4_STAGE_LDS;
+	c->stats_on = 1;
+	c->wg_per_cu = 0;
+	for (int a = 0; a < 2; a++)
+		for (int b = 0; b < 2; b++)
+			c->occ[a][b] = gr_fwd4_occupancy(a, b);
+	ret = -EIO;
+	if (upload_tables(c) != 0)
 		goto fail;
 	*out = c;
 	return 0;
@@ -244,6 +283,7 @@ extern "C" int gr_hip_fini(gr_hip_ctx_t *c) {
 	hipFree(c->d_reta);
 	hipFree(c->d_vlan_keys);
 	hipFree(c->d_vlan_vals);
+	hipFree(c->d_tables);
 	if (c->ctl)
 		hipStreamDestroy(c->ctl);
 	(void)hipGetLastError();
@@ -267,7 +307,9 @@ extern "C" int gr_hip_edges_eth_type(gr_hip_ctx_t *c, uint16_t be_type, uint8_t 
 	for (uint32_t i = 0; i < E.n_eth_types; i++) {
 		if (E.eth_type_be[i] == be_type) {
 			E.eth_type_edge[i] = edge;
-			return 0;
+			hipSetDevice(c->dev);
+			int r = quiesce(c);
+			return r ? r : upload_tables(c);
 		}
 	}
 	if (E.n_eth_types >= FWD4_MAX_ETH_TYPES)
@@ -275,7 +317,9 @@ extern "C" int gr_hip_edges_eth_type(gr_hip_ctx_t *c, uint16_t be_type, uint8_t 
 	E.eth_type_be[E.n_eth_types] = be_type;
 	E.eth_type_edge[E.n_eth_types] = edge;
 	E.n_eth_types++;
-	return 0;
+	hipSetDevice(c->dev);
+	int r = quiesce(c);
+	return r ? r : upload_tables(c);
 }
 
 #define EDGE_SETTER(fn, field, limit)                                                              \
@@ -284,7 +328,9 @@ extern "C" int gr_hip_edges_eth_type(gr_hip_ctx_t *c, uint16_t be_type, uint8_t 
 			return -EINVAL;                                                            \
 		std::lock_guard<std::mutex> l(c->mu);                                              \
 		c->edges.field[key] = edge;                                                        \
-		return 0;                                                                          \
+		hipSetDevice(c->dev);                                                              \
+		int r = quiesce(c);                                                                \
+		return r ? r : upload_tables(c);                                                   \
 	}
 EDGE_SETTER(gr_hip_edges_iface_mode, mode, GR_HIP_IFACE_MODE_COUNT)
 EDGE_SETTER(gr_hip_edges_ip_input_nh_type, in_nh, 8)
@@ -330,6 +376,8 @@ static int upload_vlans(gr_hip_ctx *c) {
 		r = h2d(c, c->d_vlan_vals, vals.data(), cap * sizeof(uint16_t));
 	if (r == 0)
 		r = ctl_sync(c); // the vectors go out of scope
+	if (r == 0)
+		r = upload_tables(c);
 	return r;
 }
 
@@ -417,6 +465,8 @@ extern "C" int gr_hip_reta_set(gr_hip_ctx_t *c, uint32_t first, const uint32_t *
 	}
 	if (r == 0)
 		r = ctl_sync(c);
+	if (r == 0)
+		r = upload_tables(c);
 	return r;
 }
 
@@ -658,39 +708,54 @@ extern "C" void *gr_hip_queue_stream(gr_hip_queue_t *q) {
 
 static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool timed) {
 	gr_hip_ctx *c = q->ctx;
-	fwd4_params P;
-	memset(&P, 0, sizeof(P));
-	P.in = static_cast<const uint8_t *>(b->in_frames);
-	P.out = static_cast<uint8_t *>(b->out_lines);
-	P.meta = b->meta;
-	P.verdicts = b->verdicts;
-	P.n = b->n;
-	P.in_stride = b->in_stride;
-	P.out_stride = b->out_stride;
-	P.readable = (b->flags & GR_HIP_BATCH_F_LINES_ONLY) ? GR_HIP_LINE : b->in_stride;
-	P.ifaces = c->d_ifaces;
-	P.nh = c->d_nh;
-	P.reta = c->d_reta;
-	P.reta_cap = c->d_reta ? (uint32_t)c->reta.size() : 0;
-	P.fibs = c->d_fibs;
-	P.vlan_keys = c->d_vlan_keys;
-	P.vlan_vals = c->d_vlan_vals;
-	P.vlan_mask = c->vlan_cap ? c->vlan_cap - 1 : 0;
-	P.stats = q->d_stats;
-	P.max_ifaces = c->max_ifaces;
-	P.max_nh = c->max_nh;
-	P.edges = c->edges;
+	fwd4_params A;
+	A.in = static_cast<const uint8_t *>(b->in_frames);
+	A.out = static_cast<uint8_t *>(b->out_lines);
+	A.meta = b->meta;
+	A.verdicts = b->verdicts;
+	A.stats = q->d_stats;
+	A.T = c->d_tables;
+	A.n = b->n;
+	A.in_stride = b->in_stride;
+	A.out_stride = b->out_stride;
+	A.readable = (b->flags & GR_HIP_BATCH_F_LINES_ONLY) ? GR_HIP_LINE : b->in_stride;
+	int stats = c->stats_on && q->d_stats != nullptr;
+	uint32_t per_cu = c->wg_per_cu > 0 ? (uint32_t)c->wg_per_cu : (uint32_t)c->occ[c->stage][stats];
+	if (per_cu == 0)
+		per_cu = 4;
 	uint32_t tiles = (b->n + FWD4_BLOCK - 1) / FWD4_BLOCK;
-	uint32_t grid = (uint32_t)c->n_cu * 8;
+	uint32_t grid = (uint32_t)c->n_cu * per_cu;
 	if (grid > tiles)
 		grid = tiles;
 	uint32_t slot = (uint32_t)(q->n_launch % N_TIMED);
 	if (timed)
 		HCK(hipEventRecord(q->ev0[slot], s));
-	HCK(gr_fwd4_launch(&P, grid, s));
+	HCK(gr_fwd4_launch(&A, grid, s, c->stage, stats));
 	if (timed) {
 		HCK(hipEventRecord(q->ev1[slot], s));
 		q->n_launch++;
+	}
+	return 0;
+}
+
+extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
+	if (c == nullptr || key == nullptr)
+		return -EINVAL;
+	std::lock_guard<std::mutex> l(c->mu);
+	if (strcmp(key, "staging") == 0) {
+		if (value != FWD4_STAGE_LDS && value != FWD4_STAGE_DIRECT)
+			return -EINVAL;
+		c->stage = value;
+	} else if (strcmp(key, "stats") == 0) {
+		c->stats_on = value != 0;
+	} else if (strcmp(key, "wg_per_cu") == 0) {
+		if (value < 0 || value > 32)
+			return -EINVAL;
+		c->wg_per_cu = value;
+	} else if (strcmp(key, "occupancy") == 0) { // read-only: WGs/CU of the current variant
+		return c->occ[c->stage][c->stats_on];
+	} else {
+		return -ENOENT;
 	}
 	return 0;
 }

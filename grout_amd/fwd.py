@@ -66,9 +66,7 @@ class FastPath:
         check("gr_hip_route4_add", self.lib.gr_hip_route4_add(self.h, ptr(a), len(a), 1 if replace else 0))
 
     def route_del(self, vrf_id, ip_host, prefixlen):
-        import socket
-        import struct
-        be = struct.unpack("<I", socket.inet_aton(socket.inet_ntoa(struct.pack(">I", ip_host))))[0]
+        be = int.from_bytes(int(ip_host).to_bytes(4, "big"), "little")
         check("gr_hip_route4_del", self.lib.gr_hip_route4_del(self.h, vrf_id, be, prefixlen))
 
     def fib_commit(self, vrf_id):
@@ -84,6 +82,9 @@ class FastPath:
         n, u, b = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint64()
         check("gr_hip_fib4_info", self.lib.gr_hip_fib4_info(self.h, vrf_id, ctypes.byref(n), ctypes.byref(u), ctypes.byref(b)))
         return dict(routes=n.value, tbl8_used=u.value, dev_bytes=b.value)
+
+    def tune(self, key, value=0):
+        return check("gr_hip_tune", self.lib.gr_hip_tune(self.h, key.encode(), value))
 
     def load(self, topo):
         """Push a grout_amd.topology.Topology (ifaces, nexthops, reta, FIBs)."""

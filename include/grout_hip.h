@@ -342,6 +342,14 @@ int gr_hip_queue_sync(gr_hip_queue_t *);
 // ring of 64). Returns the sum; *count receives how many were measured.
 int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *count);
 
+// Tuning knobs, for measurements (A/B in one process). Keys:
+//   "staging"   0 = LDS-staged coalesced lines (default), 1 = per-lane lines
+//   "stats"     1 = per-iface counters (default; grout always counts), 0 = off
+//   "wg_per_cu" persistent workgroups per CU, 0 = occupancy of the variant
+//   "occupancy" (read) resident workgroups per CU of the current variant
+// Returns 0 (or the value read), -EINVAL, or -ENOENT for an unknown key.
+int gr_hip_tune(gr_hip_ctx_t *, const char *key, int value);
+
 // Host-memory path (header-only staging): copy `n` 64-byte header lines and
 // metadata from host memory, run the kernel, copy lines and verdicts back.
 // Pinned staging inside the queue, double-buffered; completes before return.

@@ -189,3 +189,31 @@ def test_kernel_timing_api(fastpath):
     ms, cnt = q.kernel_ms(3)
     assert cnt == 3 and ms > 0
     q.close()
+
+
+@pytest.mark.parametrize("staging,stats", [(1, 1), (1, 0), (0, 0)])
+def test_kernel_variants(fastpath, staging, stats):
+    """Every tuning variant (gr_hip_tune) forwards bit-exact."""
+    t, _ = SC.corpus_topology()
+    fr, me, lab = SC.corpus_arrays()
+    o = oracle.Oracle(t).process(fr, me)
+    fastpath.tune("staging", staging)
+    fastpath.tune("stats", stats)
+    try:
+        g = run_gpu(fastpath, t, fr, me)
+    finally:
+        fastpath.tune("staging", 0)
+        fastpath.tune("stats", 1)
+    if stats:
+        compare(o, g, lab)
+    else:
+        compare((o[0], o[1], g[2]), g, lab)
+        assert not g[2]["rx_packets"].any()
+    tf = _fullview()
+    fr, me = S.stream(1 << 20, 0xAB + staging, routes=tf.route_array())
+    o = oracle.Oracle(tf).process(fr, me)
+    fastpath.tune("staging", staging)
+    try:
+        compare(o, run_gpu(fastpath, tf, fr, me))
+    finally:
+        fastpath.tune("staging", 0)

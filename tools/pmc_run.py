@@ -1,0 +1,59 @@
+# SPDX-License-Identifier: BSD-3-Clause
+"""Minimal runner for rocprofv3 --pmc passes: the headline workload
+(1M-route view, 2^24 x 64 B) launched `--reps` times, plus one 1 GiB
+device-to-device copy as the byte-count calibration for FETCH/WRITE_SIZE.
+
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d OUT -o run -- \
+        python3 tools/pmc_run.py
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1 << 24)
+    ap.add_argument("--staging", type=int, default=None)
+    args = ap.parse_args()
+    import torch
+
+    from grout_amd import abi
+    from grout_amd import synth as S
+    from grout_amd import topology as T
+    from grout_amd.fwd import FastPath
+
+    dev = torch.device("cuda", 0)
+    topo = T.config_fullview()
+    fp = FastPath(0)
+    fp.load(topo)
+    if args.staging is not None:
+        fp.tune("staging", args.staging)
+    n = args.batch
+    frames, meta = S.stream(n, S.SEED_GPU_BASE, routes=topo.route_array())
+    d_in = torch.from_numpy(frames.reshape(-1)).to(dev)
+    d_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
+    d_out = torch.empty_like(d_in)
+    d_v = torch.empty(n * 8, dtype=torch.uint8, device=dev)
+    q = fp.queue(torch.cuda.current_stream(dev).cuda_stream)
+    for _ in range(args.reps):
+        q.submit(d_in, d_out, d_meta, d_v, n)
+    torch.cuda.synchronize()
+    # calibration: 1 GiB read + 1 GiB written by a streaming copy kernel
+    a = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    print("pmc_run done", n, args.reps)
+    q.close()
+    fp.close()
+    del abi
+
+
+if __name__ == "__main__":
+    main()
