@@ -14,11 +14,6 @@
 #define FWD4_STAT_SHARDS 64 // global counter shards (block % shards)
 #define FWD4_MAX_ETH_TYPES 16
 
-struct fwd4_fib { // one per VRF id
-	const uint32_t *tbl24; // NULL: no FIB for this VRF
-	const uint32_t *tbl8;
-};
-
 struct fwd4_edges {
 	uint16_t eth_type_be[FWD4_MAX_ETH_TYPES]; // registered types (raw BE value)
 	uint8_t eth_type_edge[FWD4_MAX_ETH_TYPES];
@@ -30,13 +25,56 @@ struct fwd4_edges {
 	uint8_t iout_type[8]; // iface_output iface type -> edge
 };
 
+// Per-iface RX view, 32 bytes: what iface_input and eth_input need from an
+// ingress iface, and the FIB of its VRF (get_fib, route.c:51-61), resolved
+// by the control plane when ifaces, VRFs or edge registrations change.
+#define FWD4_RX_MAC_OK 0x01 // iface_get_eth_addr() succeeds
+#define FWD4_RX_SNAT_DYN 0x02 // GR_IFACE_F_SNAT_DYNAMIC
+#define FWD4_RX_VLAN_DEMUX 0x04 // mode VRF: tagged packets look up a sub-iface
+struct fwd4_rx {
+	uint16_t id; // 0: no such iface
+	uint8_t e_in; // iface_input edge: ADMIN_DOWN, mode edge or CHAIN (eth_input)
+	uint8_t flags; // FWD4_RX_*
+	uint8_t mac[6];
+	uint8_t _pad[6];
+	const uint32_t *tbl24; // NULL: no FIB (no route)
+	const uint32_t *tbl8;
+};
+
+// Per-nexthop adjacency, 64 bytes: the nexthop fields ip_input reads plus
+// the outcome of ip_output -> eth_output -> iface_output for that nexthop,
+// precomputed from the iface mirror (everything but the packet-dependent
+// MTU/DF and LINK destination checks). Recomputed on nexthop, iface and
+// edge-registration changes.
+#define FWD4_ADJ_LOCAL 0x01 // L3 nexthop flagged LOCAL (ip_input.c:166-168)
+#define FWD4_ADJ_LINK 0x02 // flagged LINK (ip_output.c:187)
+struct fwd4_adj {
+	uint8_t type; // GR_HIP_NH_T_*
+	uint8_t e_in; // ip_input nh type edge (CHAIN = ip_forward)
+	uint8_t flags; // FWD4_ADJ_*
+	uint8_t e_pre; // ip_output before the MTU check (nh type edge, ERROR) or CHAIN
+	uint8_t e_mid; // after it: SNAT, iface type edge, HOLD (state) or CHAIN
+	uint8_t e_post; // eth_output / iface_output outcome
+	uint16_t oif; // mbuf_data(m)->iface set by ip_output
+	uint16_t mtu; // of oif
+	uint16_t post_iface; // priv iface at e_post
+	uint32_t ipv4; // network order
+	uint16_t tx_if, tx_par; // iface_output counter keys (0 = not counted)
+	uint8_t dmac[6]; // nexthop MAC
+	uint8_t smac[6]; // oif MAC
+	uint16_t n_members; // GROUP
+	uint16_t reta_size;
+	uint32_t reta_off;
+	uint32_t single;
+	uint32_t _pad[5];
+};
+
 // Device-resident per-context tables (updated by the control plane under
-// quiesce, read by every launch through one pointer: scalar loads).
+// quiesce, read by every launch through one pointer).
 struct fwd4_tables {
-	const struct gr_hip_iface *ifaces;
-	const struct gr_hip_nh *nh;
+	const struct fwd4_rx *rx; // [max_ifaces]
+	const struct fwd4_adj *adj; // [max_nh + 1]
 	const uint32_t *reta;
-	const struct fwd4_fib *fibs;
 	const uint32_t *vlan_keys; // (parent << 16 | vlan_id) + 1, 0 = empty
 	const uint16_t *vlan_vals;
 	uint32_t reta_cap;

@@ -21,14 +21,12 @@
 
 #define CHAIN GR_HIP_EDGE_CHAIN
 
-// What process() reads: table pointers (loaded once from the device-resident
-// fwd4_tables) and the edge tables, copied into LDS once per workgroup so
-// they cost no scalar registers.
+// What process() reads: table pointers (loaded once per workgroup from the
+// device-resident fwd4_tables) and the ether type table, copied into LDS.
 struct kctx {
-	const gr_hip_iface *ifaces;
-	const gr_hip_nh *nh;
+	const fwd4_rx *rx;
+	const fwd4_adj *adj;
 	const uint32_t *reta;
-	const fwd4_fib *fibs;
 	const uint32_t *vlan_keys;
 	const uint16_t *vlan_vals;
 	uint32_t reta_cap, vlan_mask, max_ifaces, max_nh, readable;
@@ -36,58 +34,60 @@ struct kctx {
 	gr_hip_iface_stats *stats;
 };
 
-struct ifv { // fields of struct gr_hip_iface the path reads
-	uint32_t id, type, mode, flags, mtu, vrf_id, vlan_id, parent_id;
-	uint32_t mac_lo, mac_hi; // bytes 0-3, 4-5
-	bool mac_ok;
-	bool ok;
+struct rxv {
+	uint32_t id, e_in, flags, mac_lo, mac_hi;
+	const uint32_t *tbl24, *tbl8;
 };
 
-// iface_from_id (iface.c:459-466) on the device mirror.
-__device__ __forceinline__ ifv load_iface(const kctx &P, uint32_t id) {
-	ifv r;
-	r.ok = false;
+// The RX view of an iface (iface_from_id, iface.c:459-466 + get_fib).
+__device__ __forceinline__ rxv load_rx(const kctx &P, uint32_t id) {
+	rxv r;
+	r.id = 0;
 	if (id == 0 || id >= P.max_ifaces)
 		return r;
-	const uint4 *p = reinterpret_cast<const uint4 *>(P.ifaces + id);
+	const uint4 *p = reinterpret_cast<const uint4 *>(P.rx + id);
 	uint4 a = p[0];
-	uint2 b = reinterpret_cast<const uint2 *>(p + 1)[0];
+	uint4 b = p[1];
 	r.id = a.x & 0xffff;
-	r.ok = r.id == id;
-	r.type = (a.x >> 16) & 0xff;
-	r.mode = a.x >> 24;
-	r.flags = a.y & 0xffff;
-	r.mtu = a.y >> 16;
-	r.vrf_id = a.z & 0xffff;
-	r.vlan_id = a.w & 0xffff;
-	r.parent_id = a.w >> 16;
-	r.mac_lo = b.x;
-	r.mac_hi = b.y & 0xffff;
-	r.mac_ok = ((b.y >> 16) & 0xff) != 0;
+	r.e_in = (a.x >> 16) & 0xff;
+	r.flags = a.x >> 24;
+	r.mac_lo = a.y;
+	r.mac_hi = a.z & 0xffff;
+	r.tbl24 = reinterpret_cast<const uint32_t *>(((uint64_t)b.y << 32) | b.x);
+	r.tbl8 = reinterpret_cast<const uint32_t *>(((uint64_t)b.w << 32) | b.z);
 	return r;
 }
 
-struct nhv { // fields of struct gr_hip_nh
-	uint32_t type, state, flags, iface_id, ipv4, mac_lo, mac_hi;
-	uint32_t reta_size, reta_off, single, n_members;
+struct adjv {
+	uint32_t type, e_in, flags, e_pre, e_mid, e_post, oif, mtu, post_iface, ipv4, tx_if, tx_par;
+	uint32_t dmac_lo, dmac_hi, smac_lo, smac_hi; // bytes 0-3 / 4-5
+	uint32_t n_members, reta_size, reta_off, single;
 };
 
-__device__ __forceinline__ nhv load_nh(const kctx &P, uint32_t slot) {
-	const uint4 *p = reinterpret_cast<const uint4 *>(P.nh + slot);
-	uint4 a = p[0];
-	nhv r;
+__device__ __forceinline__ adjv load_adj(const kctx &P, uint32_t slot) {
+	const uint4 *p = reinterpret_cast<const uint4 *>(P.adj + slot);
+	uint4 a = p[0], b = p[1], c = p[2];
+	adjv r;
 	r.type = a.x & 0xff;
-	r.state = (a.x >> 8) & 0xff;
+	r.e_in = (a.x >> 8) & 0xff;
 	r.flags = (a.x >> 16) & 0xff;
-	r.iface_id = a.y & 0xffff;
-	r.ipv4 = a.z;
-	r.mac_lo = a.w;
-	uint4 b = p[1];
-	r.mac_hi = b.x & 0xffff;
-	r.reta_size = b.x >> 16;
-	r.reta_off = b.y;
-	r.single = b.z;
-	r.n_members = b.w & 0xffff;
+	r.e_pre = a.x >> 24;
+	r.e_mid = a.y & 0xff;
+	r.e_post = (a.y >> 8) & 0xff;
+	r.oif = a.y >> 16;
+	r.mtu = a.z & 0xffff;
+	r.post_iface = a.z >> 16;
+	r.ipv4 = a.w;
+	r.tx_if = b.x & 0xffff;
+	r.tx_par = b.x >> 16;
+	r.dmac_lo = b.y; // bytes 20-23
+	r.dmac_hi = b.z & 0xffff; // 24-25
+	r.smac_lo = (b.z >> 16) | (b.w << 16); // 26-29
+	r.smac_hi = b.w >> 16; // 30-31
+	r.n_members = c.x & 0xffff;
+	r.reta_size = c.x >> 16;
+	r.reta_off = c.y;
+	r.single = c.z;
 	return r;
 }
 
@@ -116,13 +116,7 @@ struct stat_slot {
 };
 
 // One lane (the wave leader of a key) adds a wave's contribution.
-__device__ __noinline__ void slot_add(
-	stat_slot *slots,
-	const kctx &P,
-	uint32_t key,
-	uint32_t pkts,
-	uint32_t bytes
-) {
+__device__ __noinline__ void slot_add(stat_slot *slots, const kctx &P, uint32_t key, uint32_t pkts, uint32_t bytes) {
 	uint32_t h = (key * 0x9e3779b1u) >> 27; // 32 slots
 #pragma unroll 1
 	for (uint32_t i = 0; i < FWD4_STAT_SLOTS; i++) {
@@ -181,63 +175,56 @@ struct result {
 
 // The node chain for one packet. w[] is the 64-byte line (little-endian
 // words: byte j is (w[j/4] >> 8*(j%4)) & 0xff), modified in place.
-__device__ __forceinline__ result process(
-	const kctx &P,
-	uint32_t (&w)[16],
-	const gr_hip_pkt_meta &m,
-	const uint8_t *frame
-) {
+__device__ __forceinline__ result process(const kctx &P, uint32_t (&w)[16], const gr_hip_pkt_meta &m, const uint8_t *frame) {
 	result r = {GR_HIP_E_PUNT, 0, m.iface, 0, 0, 0, 0, 0};
-	const fwd4_edges &E = *P.edges;
 
 	// ---- iface_input (iface_input.c:52-112)
-	ifv cur = load_iface(P, m.iface);
-	if (!cur.ok)
+	rxv rx = load_rx(P, m.iface);
+	if (rx.id == 0)
 		return r; // port_rx always sets a valid iface: not grout's case, punt
-	uint32_t vlan = m.vlan_ck & 0xfff;
-	if (vlan != 0 && cur.mode == GR_HIP_IFACE_MODE_VRF) { // :74-86
-		uint32_t vid = vlan_lookup(P, cur.id, vlan);
-		ifv v = load_iface(P, vid);
-		if (!v.ok) {
+	const uint32_t vlan = m.vlan_ck & 0xfff;
+	if (vlan != 0 && (rx.flags & FWD4_RX_VLAN_DEMUX)) { // :74-86
+		rxv v = load_rx(P, vlan_lookup(P, rx.id, vlan));
+		if (v.id == 0) {
 			r.edge = GR_HIP_E_IFACE_INPUT_UNKNOWN_VLAN;
 			return r;
 		}
-		cur = v;
+		rx = v;
 	}
-	r.iface = cur.id;
-	if (!(cur.flags & GR_HIP_IFACE_F_UP)) { // :88-91
-		r.edge = GR_HIP_E_IFACE_INPUT_ADMIN_DOWN;
+	r.iface = rx.id;
+	if (rx.e_in != CHAIN) { // admin down :88-91, or the mode edge :97
+		r.edge = rx.e_in;
+		if (rx.e_in != GR_HIP_E_IFACE_INPUT_ADMIN_DOWN) {
+			r.rx_if = rx.id;
+			r.rx_par = m.iface != rx.id ? m.iface : 0;
+		}
 		return r;
 	}
-	r.rx_if = cur.id; // IFACE_STATS_INC :93-95
-	r.rx_par = m.iface != cur.id ? m.iface : 0;
-	uint32_t e = cur.mode < GR_HIP_IFACE_MODE_COUNT ? E.mode[cur.mode] : GR_HIP_E_IFACE_MODE_UNKNOWN;
-	if (e != CHAIN) {
-		r.edge = e;
-		return r;
-	}
+	r.rx_if = rx.id; // IFACE_STATS_INC :93-95
+	r.rx_par = m.iface != rx.id ? m.iface : 0;
 
 	// ---- eth_input (eth_input.c:35-88)
-	uint32_t type_raw = lo16(w[3]); // as stored (big endian)
-	uint32_t type = bswap16(type_raw);
+	const uint32_t type_raw = lo16(w[3]); // as stored (big endian)
+	const uint32_t type = bswap16(type_raw);
 	if (type < 1536 || type == 0x8870) { // snap.h:11-12
 		r.edge = GR_HIP_E_SNAP_INPUT;
 		return r;
 	}
-	if (!cur.mac_ok) { // iface_get_eth_addr() < 0
+	if (!(rx.flags & FWD4_RX_MAC_OK)) { // iface_get_eth_addr() < 0
 		r.edge = GR_HIP_E_ETH_INPUT_INVALID_IFACE;
 		return r;
 	}
 	if (w[0] & 1) { // rte_is_multicast_ether_addr
 		bool bc = w[0] == 0xffffffffu && lo16(w[1]) == 0xffff;
 		r.domain = bc ? GR_HIP_ETH_DOMAIN_BROADCAST : GR_HIP_ETH_DOMAIN_MULTICAST;
-	} else if (w[0] == cur.mac_lo && lo16(w[1]) == cur.mac_hi) {
+	} else if (w[0] == rx.mac_lo && lo16(w[1]) == rx.mac_hi) {
 		r.domain = GR_HIP_ETH_DOMAIN_LOCAL;
 	} else {
 		r.domain = GR_HIP_ETH_DOMAIN_OTHER;
 	}
-	uint32_t data_len = m.pkt_len >= 14 ? m.pkt_len - 14u : m.pkt_len; // rte_pktmbuf_adj
-	e = GR_HIP_E_ETH_INPUT_UNKNOWN_TYPE;
+	const uint32_t data_len = m.pkt_len >= 14 ? m.pkt_len - 14u : m.pkt_len; // rte_pktmbuf_adj
+	uint32_t e = GR_HIP_E_ETH_INPUT_UNKNOWN_TYPE;
+	const fwd4_edges &E = *P.edges;
 	for (uint32_t i = 0; i < E.n_eth_types; i++) // l2l3_edges[ether_type]
 		if (E.eth_type_be[i] == type_raw)
 			e = E.eth_type_edge[i];
@@ -255,7 +242,7 @@ __device__ __forceinline__ result process(
 	}
 	const uint32_t ck = (m.vlan_ck >> 12) & 3;
 	if (ck == GR_HIP_CKSUM_UNKNOWN) { // (2) :80-88, rte_ipv4_cksum
-		uint32_t hl = ihl * 4;
+		const uint32_t hl = ihl * 4;
 		if (14 + hl > P.readable) {
 			r.edge = GR_HIP_E_PUNT; // header bytes not present: CPU path
 			r.rx_if = r.rx_par = 0;
@@ -320,55 +307,47 @@ __device__ __forceinline__ result process(
 		r.edge = GR_HIP_E_IP_INPUT_LOCAL;
 		return r;
 	}
-	// fib4_lookup (route.c:147-167): VRF iface (vrf.c:51-57), DIR24_8
+	// fib4_lookup (route.c:147-167): DIR24_8 of the iface's VRF
 	uint32_t slot = 0;
-	{
-		ifv vrf = load_iface(P, cur.vrf_id);
-		if (vrf.ok && vrf.type == GR_HIP_IFACE_TYPE_VRF) {
-			fwd4_fib f = P.fibs[cur.vrf_id];
-			if (f.tbl24 != nullptr) {
-				uint32_t ip = __builtin_bswap32(dst);
-				uint32_t ent = f.tbl24[ip >> 8];
-				if (ent & 0x80000000u)
-					ent = f.tbl8[(size_t)(ent & 0x7fffffffu) * 256 + (ip & 0xff)];
-				slot = ent;
-			}
-		}
+	if (rx.tbl24 != nullptr) {
+		const uint32_t ip = __builtin_bswap32(dst);
+		uint32_t ent = rx.tbl24[ip >> 8];
+		if (ent & 0x80000000u)
+			ent = rx.tbl8[(size_t)(ent & 0x7fffffffu) * 256 + (ip & 0xff)];
+		slot = ent;
 	}
 	if (slot == 0 || slot > P.max_nh) {
 		r.edge = GR_HIP_E_IP_ERROR_DEST_UNREACH; // NO_ROUTE :150-153
 		return r;
 	}
-	nhv nh = load_nh(P, slot);
-	if (nh.type == GR_HIP_NH_T_GROUP) { // nexthop_group_get_nh, nexthop.h:89-96
-		if (nh.n_members == 1) {
-			slot = nh.single;
-		} else if (nh.n_members == 0) {
+	adjv a = load_adj(P, slot);
+	if (a.type == GR_HIP_NH_T_GROUP) { // nexthop_group_get_nh, nexthop.h:89-96
+		if (a.n_members == 1) {
+			slot = a.single;
+		} else if (a.n_members == 0) {
 			slot = 0;
 		} else {
-			uint32_t i = nh.reta_off + (m.rss & (nh.reta_size - 1));
+			uint32_t i = a.reta_off + (m.rss & (a.reta_size - 1));
 			slot = i < P.reta_cap ? P.reta[i] : 0;
 		}
 		if (slot == 0 || slot > P.max_nh) {
 			r.edge = GR_HIP_E_IP_ERROR_DEST_UNREACH;
 			return r;
 		}
-		nh = load_nh(P, slot);
+		a = load_adj(P, slot);
 	}
 	r.nh = slot; // l3_mbuf_data(mbuf)->nh :156
-	e = nh.type < 8 ? E.in_nh[nh.type] : CHAIN;
-	if (e != CHAIN) {
-		r.edge = e;
+	if (a.e_in != CHAIN) { // nh_type_edges :158-160
+		r.edge = a.e_in;
 		return r;
 	}
-	if (nh.type == GR_HIP_NH_T_L3 && (nh.flags & GR_HIP_NH_F_LOCAL) && dst == nh.ipv4) { // :166-187
-		r.edge = (cur.flags & GR_HIP_IFACE_F_SNAT_DYNAMIC) ? GR_HIP_E_IP_INPUT_LOCAL_CT
-		                                                  : GR_HIP_E_IP_INPUT_LOCAL;
+	if ((a.flags & FWD4_ADJ_LOCAL) && dst == a.ipv4) { // :166-187
+		r.edge = (rx.flags & FWD4_RX_SNAT_DYN) ? GR_HIP_E_IP_INPUT_LOCAL_CT : GR_HIP_E_IP_INPUT_LOCAL;
 		return r;
 	}
 
 	// ---- ip_forward (ip_forward.c:21-33)
-	uint32_t ttl = (w[5] >> 16) & 0xff;
+	const uint32_t ttl = (w[5] >> 16) & 0xff;
 	if (ttl <= 1) {
 		r.edge = GR_HIP_E_IP_ERROR_TTL_EXCEEDED;
 		return r;
@@ -378,65 +357,37 @@ __device__ __forceinline__ result process(
 	c += c >= 0xffff;
 	w[6] = (w[6] & 0xffff0000u) | (c & 0xffff);
 
-	// ---- ip_output (ip_output.c:135-213)
-	e = nh.type < 8 ? E.out_nh[nh.type] : CHAIN;
-	if (e != CHAIN) {
-		r.edge = e;
+	// ---- ip_output (ip_output.c:135-213), adjacency resolved ahead of time
+	if (a.e_pre != CHAIN) { // nh type edge :147-149, no iface :151-155
+		r.edge = a.e_pre;
 		return r;
 	}
-	ifv oif = load_iface(P, nh.iface_id);
-	if (!oif.ok) { // :151-155
-		r.edge = GR_HIP_E_IP_OUTPUT_ERROR;
-		return r;
-	}
-	r.iface = oif.id; // :157
-	if (data_len > oif.mtu) { // :159-166, DF = BE 0x4000 -> byte 20 & 0x40
+	r.iface = a.oif; // :157
+	if (data_len > a.mtu) { // :159-166, DF = BE 0x4000 -> byte 20 & 0x40
 		r.edge = (w[5] & 0x40) ? GR_HIP_E_IP_ERROR_FRAG_NEEDED : GR_HIP_E_IP_FRAGMENT;
 		return r;
 	}
-	e = oif.type < 8 ? E.out_iface[oif.type] : CHAIN; // :170
-	if (oif.flags & (GR_HIP_IFACE_F_SNAT_STATIC | GR_HIP_IFACE_F_SNAT_DYNAMIC)) {
-		r.edge = GR_HIP_E_IP_OUTPUT_SNAT; // snat44_process :172-179
+	if (a.e_mid != CHAIN) { // SNAT :172-179, iface type edge :170,181, state :186
+		r.edge = a.e_mid;
 		return r;
 	}
-	if (e != CHAIN) {
-		r.edge = e;
-		return r;
-	}
-	if (nh.state != GR_HIP_NH_S_REACHABLE || ((nh.flags & GR_HIP_NH_F_LINK) && dst != nh.ipv4)) {
-		r.edge = GR_HIP_E_IP_HOLD; // :186-198
+	if ((a.flags & FWD4_ADJ_LINK) && dst != a.ipv4) { // :187
+		r.edge = GR_HIP_E_IP_HOLD;
 		return r;
 	}
 
-	// ---- eth_output (eth_output.c:297-316): dst = nh mac, src = iface mac
-	w[0] = nh.mac_lo;
-	w[1] = (w[1] & 0xffff0000u) | nh.mac_hi;
-	if (!oif.mac_ok) {
-		r.edge = GR_HIP_E_ETH_OUTPUT_NO_MAC;
+	// ---- eth_output (eth_output.c:297-316) + iface_output (iface_output.c:213-246)
+	w[0] = a.dmac_lo;
+	w[1] = (w[1] & 0xffff0000u) | a.dmac_hi;
+	r.edge = a.e_post;
+	if (a.e_post == GR_HIP_E_ETH_OUTPUT_NO_MAC)
 		return r;
-	}
-	w[1] = lo16(w[1]) | (oif.mac_lo << 16);
-	w[2] = (oif.mac_lo >> 16) | (oif.mac_hi << 16);
+	w[1] = lo16(w[1]) | (a.smac_lo << 16);
+	w[2] = (a.smac_lo >> 16) | (a.smac_hi << 16);
 	w[3] = (w[3] & 0xffff0000u) | 0x0008u; // RTE_BE16(RTE_ETHER_TYPE_IPV4)
-
-	// ---- iface_output (iface_output.c:213-246)
-	ifv out = oif;
-	bool vlan_if = oif.type == GR_HIP_IFACE_TYPE_VLAN;
-	if (vlan_if) {
-		out = load_iface(P, oif.parent_id);
-		if (!out.ok) {
-			r.edge = GR_HIP_E_IFACE_OUTPUT_VLAN_NO_PARENT;
-			return r;
-		}
-	}
-	if (!(oif.flags & GR_HIP_IFACE_F_UP)) {
-		r.edge = GR_HIP_E_IFACE_OUTPUT_ADMIN_DOWN;
-		return r;
-	}
-	r.tx_if = oif.id;
-	r.tx_par = vlan_if ? out.id : 0;
-	r.iface = out.id;
-	r.edge = out.type < 8 ? E.iout_type[out.type] : GR_HIP_E_IFACE_OUTPUT_INVAL_TYPE;
+	r.iface = a.post_iface;
+	r.tx_if = a.tx_if;
+	r.tx_par = a.tx_par;
 	return r;
 }
 
@@ -456,10 +407,9 @@ __global__ void __launch_bounds__(FWD4_BLOCK) gr_fwd4_kernel(const fwd4_params A
 		slots[tid].bytes = 0;
 	}
 	kctx P;
-	P.ifaces = T->ifaces;
-	P.nh = T->nh;
+	P.rx = T->rx;
+	P.adj = T->adj;
 	P.reta = T->reta;
-	P.fibs = T->fibs;
 	P.vlan_keys = T->vlan_keys;
 	P.vlan_vals = T->vlan_vals;
 	P.reta_cap = T->reta_cap;

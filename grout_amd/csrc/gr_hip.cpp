@@ -79,12 +79,13 @@ struct gr_hip_ctx {
 	std::vector<gr_hip_nh> nh;
 	std::vector<uint32_t> reta;
 	std::vector<vrf_fib> vrfs;
-	std::vector<fwd4_fib> fibs;
-	gr_hip_iface *d_ifaces;
-	gr_hip_nh *d_nh;
+	std::vector<fwd4_rx> rx; // host images of the device views
+	std::vector<fwd4_adj> adj;
+	uint32_t nh_hi; // highest nexthop slot ever set
+	fwd4_rx *d_rx;
+	fwd4_adj *d_adj;
 	uint32_t *d_reta;
 	uint32_t d_reta_cap;
-	fwd4_fib *d_fibs;
 	uint32_t *d_vlan_keys;
 	uint16_t *d_vlan_vals;
 	uint32_t vlan_cap;
@@ -123,15 +124,131 @@ static int ctl_sync(gr_hip_ctx *c) {
 	return 0;
 }
 
+static const gr_hip_iface *iface_get(const gr_hip_ctx *c, uint32_t id) {
+	if (id == GR_HIP_IFACE_ID_UNDEF || id >= c->max_ifaces || c->ifaces[id].id != id)
+		return nullptr; // iface_from_id, iface.c:459-466
+	return &c->ifaces[id];
+}
+
+// RX view of iface `id`: iface_input's admin/mode edge (iface_input.c:88-97),
+// eth_input's MAC (eth_input.c:62-68) and the VRF FIB (route.c:51-61).
+static fwd4_rx make_rx(const gr_hip_ctx *c, uint32_t id) {
+	fwd4_rx r;
+	memset(&r, 0, sizeof(r));
+	const gr_hip_iface *i = iface_get(c, id);
+	if (i == nullptr)
+		return r;
+	r.id = (uint16_t)id;
+	if (!(i->flags & GR_HIP_IFACE_F_UP))
+		r.e_in = GR_HIP_E_IFACE_INPUT_ADMIN_DOWN;
+	else
+		r.e_in = i->mode < GR_HIP_IFACE_MODE_COUNT ? c->edges.mode[i->mode] : GR_HIP_E_IFACE_MODE_UNKNOWN;
+	r.flags = (i->mac_ok ? FWD4_RX_MAC_OK : 0) | ((i->flags & GR_HIP_IFACE_F_SNAT_DYNAMIC) ? FWD4_RX_SNAT_DYN : 0)
+		| (i->mode == GR_HIP_IFACE_MODE_VRF ? FWD4_RX_VLAN_DEMUX : 0);
+	memcpy(r.mac, i->mac, 6);
+	const gr_hip_iface *vrf = iface_get(c, i->vrf_id);
+	if (vrf != nullptr && vrf->type == GR_HIP_IFACE_TYPE_VRF && c->vrfs[i->vrf_id].rib != nullptr) {
+		r.tbl24 = c->vrfs[i->vrf_id].d24;
+		r.tbl8 = c->vrfs[i->vrf_id].d8;
+	}
+	return r;
+}
+
+// Adjacency of nexthop `slot`: the ip_input view (ip_input.c:156-187) and
+// ip_output -> eth_output -> iface_output resolved for that nexthop
+// (ip_output.c:147-213, eth_output.c:297-316, iface_output.c:213-246),
+// leaving the packet-dependent MTU/DF and LINK destination checks.
+static fwd4_adj make_adj(const gr_hip_ctx *c, uint32_t slot) {
+	const fwd4_edges &E = c->edges;
+	const gr_hip_nh &nh = c->nh[slot];
+	fwd4_adj a;
+	memset(&a, 0, sizeof(a));
+	a.type = nh.type;
+	a.e_in = nh.type < 8 ? E.in_nh[nh.type] : GR_HIP_EDGE_CHAIN;
+	a.flags = ((nh.type == GR_HIP_NH_T_L3 && (nh.flags & GR_HIP_NH_F_LOCAL)) ? FWD4_ADJ_LOCAL : 0)
+		| ((nh.flags & GR_HIP_NH_F_LINK) ? FWD4_ADJ_LINK : 0);
+	a.ipv4 = nh.ipv4;
+	a.n_members = nh.n_members;
+	a.reta_size = nh.reta_size;
+	a.reta_off = nh.reta_off;
+	a.single = nh.single;
+	a.e_mid = a.e_post = GR_HIP_EDGE_CHAIN;
+	uint8_t e = nh.type < 8 ? E.out_nh[nh.type] : GR_HIP_EDGE_CHAIN;
+	if (e != GR_HIP_EDGE_CHAIN) {
+		a.e_pre = e;
+		return a;
+	}
+	const gr_hip_iface *oif = iface_get(c, nh.iface_id);
+	if (oif == nullptr) {
+		a.e_pre = GR_HIP_E_IP_OUTPUT_ERROR;
+		return a;
+	}
+	a.e_pre = GR_HIP_EDGE_CHAIN;
+	a.oif = oif->id;
+	a.mtu = oif->mtu;
+	e = oif->type < 8 ? E.out_iface[oif->type] : GR_HIP_EDGE_CHAIN;
+	if (oif->flags & (GR_HIP_IFACE_F_SNAT_STATIC | GR_HIP_IFACE_F_SNAT_DYNAMIC))
+		a.e_mid = GR_HIP_E_IP_OUTPUT_SNAT;
+	else if (e != GR_HIP_EDGE_CHAIN)
+		a.e_mid = e;
+	else if (nh.state != GR_HIP_NH_S_REACHABLE)
+		a.e_mid = GR_HIP_E_IP_HOLD;
+	memcpy(a.dmac, nh.mac, 6);
+	a.post_iface = oif->id;
+	if (!oif->mac_ok) {
+		a.e_post = GR_HIP_E_ETH_OUTPUT_NO_MAC;
+		return a;
+	}
+	memcpy(a.smac, oif->mac, 6);
+	const gr_hip_iface *out = oif;
+	if (oif->type == GR_HIP_IFACE_TYPE_VLAN) {
+		out = iface_get(c, oif->parent_id);
+		if (out == nullptr) {
+			a.e_post = GR_HIP_E_IFACE_OUTPUT_VLAN_NO_PARENT;
+			return a;
+		}
+	}
+	if (!(oif->flags & GR_HIP_IFACE_F_UP)) {
+		a.e_post = GR_HIP_E_IFACE_OUTPUT_ADMIN_DOWN;
+		return a;
+	}
+	a.tx_if = oif->id;
+	a.tx_par = out != oif ? out->id : 0;
+	a.post_iface = out->id;
+	a.e_post = out->type < 8 ? E.iout_type[out->type] : GR_HIP_E_IFACE_OUTPUT_INVAL_TYPE;
+	return a;
+}
+
+// Recompute and upload the RX views (all) and adjacencies [first, first+n)
+// (n == 0: every slot up to nh_hi). Caller holds c->mu and has quiesced.
+static int upload_views(gr_hip_ctx *c, bool rx, uint32_t first, uint32_t n, bool adj) {
+	if (rx) {
+		for (uint32_t i = 0; i < c->max_ifaces; i++)
+			c->rx[i] = make_rx(c, i);
+		HCK(hipMemcpyAsync(c->d_rx, c->rx.data(), sizeof(fwd4_rx) * c->max_ifaces, hipMemcpyHostToDevice, c->ctl));
+	}
+	if (adj) {
+		if (n == 0) {
+			first = 1;
+			n = c->nh_hi;
+		}
+		for (uint32_t i = first; i < first + n; i++)
+			c->adj[i] = make_adj(c, i);
+		if (n)
+			HCK(hipMemcpyAsync(c->d_adj + first, &c->adj[first], sizeof(fwd4_adj) * n, hipMemcpyHostToDevice, c->ctl));
+	}
+	HCK(hipStreamSynchronize(c->ctl));
+	return 0;
+}
+
 // Refresh the device-resident fwd4_tables (caller holds c->mu and has
 // quiesced the queues); completes before returning.
 static int upload_tables(gr_hip_ctx *c) {
 	fwd4_tables t;
 	memset(&t, 0, sizeof(t));
-	t.ifaces = c->d_ifaces;
-	t.nh = c->d_nh;
+	t.rx = c->d_rx;
+	t.adj = c->d_adj;
 	t.reta = c->d_reta;
-	t.fibs = c->d_fibs;
 	t.vlan_keys = c->d_vlan_keys;
 	t.vlan_vals = c->d_vlan_vals;
 	t.reta_cap = c->d_reta ? (uint32_t)c->reta.size() : 0;
@@ -227,7 +344,9 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->ifaces.assign(max_ifaces, gr_hip_iface {});
 	c->nh.assign((size_t)max_nexthops + 1, gr_hip_nh {});
 	c->vrfs.assign(max_ifaces, vrf_fib {});
-	c->fibs.assign(max_ifaces, fwd4_fib {nullptr, nullptr});
+	c->rx.assign(max_ifaces, fwd4_rx {});
+	c->adj.assign((size_t)max_nexthops + 1, fwd4_adj {});
+	c->nh_hi = 0;
 	set_default_edges(&c->edges);
 	c->d_reta = nullptr;
 	c->d_reta_cap = 0;
@@ -237,17 +356,16 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	int ret = -ENOMEM;
 	if (hipStreamCreateWithFlags(&c->ctl, hipStreamNonBlocking) != hipSuccess)
 		goto fail;
-	if (hipMalloc(&c->d_ifaces, sizeof(gr_hip_iface) * max_ifaces) != hipSuccess)
+	if (hipMalloc(&c->d_rx, sizeof(fwd4_rx) * max_ifaces) != hipSuccess)
 		goto fail;
-	if (hipMalloc(&c->d_nh, sizeof(gr_hip_nh) * ((size_t)max_nexthops + 1)) != hipSuccess)
-		goto fail;
-	if (hipMalloc(&c->d_fibs, sizeof(fwd4_fib) * max_ifaces) != hipSuccess)
+	if (hipMalloc(&c->d_adj, sizeof(fwd4_adj) * ((size_t)max_nexthops + 1)) != hipSuccess)
 		goto fail;
 	if (hipMalloc(&c->d_tables, sizeof(fwd4_tables)) != hipSuccess)
 		goto fail;
-	if (hipMemset(c->d_ifaces, 0, sizeof(gr_hip_iface) * max_ifaces) != hipSuccess
-	    || hipMemset(c->d_nh, 0, sizeof(gr_hip_nh) * ((size_t)max_nexthops + 1)) != hipSuccess
-	    || hipMemset(c->d_fibs, 0, sizeof(fwd4_fib) * max_ifaces) != hipSuccess)
+	// every device write goes through the control stream: a plain hipMemset
+	// runs on the null stream, which a non-blocking stream does not order with
+	if (hipMemsetAsync(c->d_rx, 0, sizeof(fwd4_rx) * max_ifaces, c->ctl) != hipSuccess
+	    || hipMemsetAsync(c->d_adj, 0, sizeof(fwd4_adj) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess)
 		goto fail;
 	c->stage = FWD4_STAGE_LDS;
 	c->stats_on = 1;
@@ -277,9 +395,8 @@ extern "C" int gr_hip_fini(gr_hip_ctx_t *c) {
 		hipFree(v.d24);
 		hipFree(v.d8);
 	}
-	hipFree(c->d_ifaces);
-	hipFree(c->d_nh);
-	hipFree(c->d_fibs);
+	hipFree(c->d_rx);
+	hipFree(c->d_adj);
 	hipFree(c->d_reta);
 	hipFree(c->d_vlan_keys);
 	hipFree(c->d_vlan_vals);
@@ -309,7 +426,7 @@ extern "C" int gr_hip_edges_eth_type(gr_hip_ctx_t *c, uint16_t be_type, uint8_t 
 			E.eth_type_edge[i] = edge;
 			hipSetDevice(c->dev);
 			int r = quiesce(c);
-			return r ? r : upload_tables(c);
+			return r ? r : upload_tables(c); // only the table reads ether types
 		}
 	}
 	if (E.n_eth_types >= FWD4_MAX_ETH_TYPES)
@@ -330,6 +447,8 @@ extern "C" int gr_hip_edges_eth_type(gr_hip_ctx_t *c, uint16_t be_type, uint8_t 
 		c->edges.field[key] = edge;                                                        \
 		hipSetDevice(c->dev);                                                              \
 		int r = quiesce(c);                                                                \
+		if (r == 0)                                                                        \
+			r = upload_views(c, true, 0, 0, true);                                     \
 		return r ? r : upload_tables(c);                                                   \
 	}
 EDGE_SETTER(gr_hip_edges_iface_mode, mode, GR_HIP_IFACE_MODE_COUNT)
@@ -396,10 +515,8 @@ extern "C" int gr_hip_iface_set(gr_hip_ctx_t *c, const struct gr_hip_iface *ifs,
 		c->ifaces[ifs[i].id] = ifs[i];
 	}
 	int r = quiesce(c);
-	if (r == 0)
-		r = h2d(c, c->d_ifaces, c->ifaces.data(), sizeof(gr_hip_iface) * c->max_ifaces);
-	if (r == 0)
-		r = ctl_sync(c);
+	if (r == 0) // ifaces feed every RX view and every adjacency
+		r = upload_views(c, true, 0, 0, true);
 	if (r == 0 && (vlans || c->vlan_cap == 0))
 		r = upload_vlans(c);
 	return r;
@@ -414,9 +531,7 @@ extern "C" int gr_hip_iface_del(gr_hip_ctx_t *c, uint16_t id) {
 	c->ifaces[id] = gr_hip_iface {};
 	int r = quiesce(c);
 	if (r == 0)
-		r = h2d(c, c->d_ifaces + id, &c->ifaces[id], sizeof(gr_hip_iface));
-	if (r == 0)
-		r = ctl_sync(c);
+		r = upload_views(c, true, 0, 0, true);
 	if (r == 0 && vlan)
 		r = upload_vlans(c);
 	return r;
@@ -429,11 +544,11 @@ extern "C" int gr_hip_nh_set(gr_hip_ctx_t *c, uint32_t first, const struct gr_hi
 	std::lock_guard<std::mutex> l(c->mu);
 	hipSetDevice(c->dev);
 	memcpy(&c->nh[first], nh, (size_t)n * sizeof(*nh));
+	if (n && first + n - 1 > c->nh_hi)
+		c->nh_hi = first + n - 1;
 	int r = quiesce(c);
-	if (r == 0)
-		r = h2d(c, c->d_nh + first, &c->nh[first], (size_t)n * sizeof(*nh));
-	if (r == 0)
-		r = ctl_sync(c);
+	if (r == 0 && n)
+		r = upload_views(c, false, first, n, true);
 	return r;
 }
 
@@ -455,7 +570,7 @@ extern "C" int gr_hip_reta_set(gr_hip_ctx_t *c, uint32_t first, const uint32_t *
 		uint32_t *d = nullptr;
 		HCK(hipStreamSynchronize(c->ctl));
 		HCK(hipMalloc(&d, (size_t)cap * sizeof(uint32_t)));
-		HCK(hipMemset(d, 0, (size_t)cap * sizeof(uint32_t)));
+		HCK(hipMemsetAsync(d, 0, (size_t)cap * sizeof(uint32_t), c->ctl));
 		hipFree(c->d_reta);
 		c->d_reta = d;
 		c->d_reta_cap = cap;
@@ -490,8 +605,8 @@ extern "C" int gr_hip_fib4_create(gr_hip_ctx_t *c, uint16_t vrf, uint32_t max_ro
 	v.num_tbl8 = num_tbl8;
 	if (hipMalloc(&v.d24, sizeof(uint32_t) * GR_FIB4_TBL24_ENTRIES) != hipSuccess
 	    || hipMalloc(&v.d8, sizeof(uint32_t) * 256 * (size_t)num_tbl8) != hipSuccess
-	    || hipMemset(v.d24, 0, sizeof(uint32_t) * GR_FIB4_TBL24_ENTRIES) != hipSuccess
-	    || hipMemset(v.d8, 0, sizeof(uint32_t) * 256 * (size_t)num_tbl8) != hipSuccess) {
+	    || hipMemsetAsync(v.d24, 0, sizeof(uint32_t) * GR_FIB4_TBL24_ENTRIES, c->ctl) != hipSuccess
+	    || hipMemsetAsync(v.d8, 0, sizeof(uint32_t) * 256 * (size_t)num_tbl8, c->ctl) != hipSuccess) {
 		(void)hipGetLastError();
 		hipFree(v.d24);
 		hipFree(v.d8);
@@ -500,12 +615,9 @@ extern "C" int gr_hip_fib4_create(gr_hip_ctx_t *c, uint16_t vrf, uint32_t max_ro
 		return -ENOMEM;
 	}
 	gr_fib4_dirty_clear(v.rib);
-	c->fibs[vrf] = fwd4_fib {v.d24, v.d8};
 	int r = quiesce(c);
-	if (r == 0)
-		r = h2d(c, c->d_fibs + vrf, &c->fibs[vrf], sizeof(fwd4_fib));
-	if (r == 0)
-		r = ctl_sync(c);
+	if (r == 0) // the RX views of the VRF's ifaces now point at the FIB
+		r = upload_views(c, true, 0, 0, false);
 	return r;
 }
 
@@ -517,14 +629,16 @@ extern "C" int gr_hip_fib4_destroy(gr_hip_ctx_t *c, uint16_t vrf) {
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib == nullptr)
 		return -ENOENT;
-	c->fibs[vrf] = fwd4_fib {nullptr, nullptr};
+	gr_fib4 *rib = v.rib;
+	v.rib = nullptr; // make_rx() stops pointing at it
 	int r = quiesce(c);
 	if (r == 0)
-		r = h2d(c, c->d_fibs + vrf, &c->fibs[vrf], sizeof(fwd4_fib));
-	if (r == 0)
-		r = ctl_sync(c);
-	if (r != 0)
+		r = upload_views(c, true, 0, 0, false);
+	if (r != 0) {
+		v.rib = rib;
 		return r;
+	}
+	v.rib = rib;
 	hipFree(v.d24);
 	hipFree(v.d8);
 	gr_fib4_free(v.rib);
@@ -658,7 +772,7 @@ extern "C" int gr_hip_queue_create(gr_hip_ctx_t *c, void *stream, gr_hip_queue_t
 	}
 	hipEventCreateWithFlags(&q->quiesce, hipEventDisableTiming);
 	size_t sb = sizeof(gr_hip_iface_stats) * FWD4_STAT_SHARDS * c->max_ifaces;
-	if (hipMalloc(&q->d_stats, sb) != hipSuccess || hipMemset(q->d_stats, 0, sb) != hipSuccess) {
+	if (hipMalloc(&q->d_stats, sb) != hipSuccess || hipMemsetAsync(q->d_stats, 0, sb, q->s) != hipSuccess) {
 		(void)hipGetLastError();
 		q->d_stats = nullptr;
 	}
@@ -889,7 +1003,7 @@ extern "C" int gr_hip_queue_stats(gr_hip_queue_t *q, struct gr_hip_iface_stats *
 		}
 	}
 	if (reset)
-		HCK(hipMemset(q->d_stats, 0, all.size() * sizeof(gr_hip_iface_stats)));
+		HCK(hipMemsetAsync(q->d_stats, 0, all.size() * sizeof(gr_hip_iface_stats), q->s));
 	return 0;
 }
 

@@ -217,3 +217,23 @@ def test_kernel_variants(fastpath, staging, stats):
         compare(o, run_gpu(fastpath, tf, fr, me))
     finally:
         fastpath.tune("staging", 0)
+
+
+def test_mirror_updates_propagate(fastpath):
+    """Iface / nexthop changes after load reach the precomputed adjacencies."""
+    t, nh = SC.corpus_topology()
+    fr, me, lab = SC.corpus_arrays()
+    run_gpu(fastpath, t, fr, me)  # loads t
+    # p1 admin down (egress for most forwards), p2 MTU 1500, p0 loses its MAC,
+    # one nexthop becomes unresolved, another changes MAC
+    t.ifaces[SC.P1]["flags"] &= ~abi.IFACE_F_UP
+    t.ifaces[SC.P2]["mtu"] = 1500
+    t.ifaces[SC.BOND]["mac_ok"] = 0
+    t.nh[nh["fwd2"]]["state"] = abi.NH_S["STALE"]
+    t.nh[nh["fwd3"]]["mac"] = [2, 0, 0, 1, 0x33, 0x33]
+    fastpath.set_ifaces(t.ifaces)
+    fastpath.set_nexthops(t.nh[1:t.n_nh + 1], first=1)
+    try:
+        compare(oracle.Oracle(t).process(fr, me), run_gpu(fastpath, t, fr, me), lab)
+    finally:
+        fresh_fastpath_state(fastpath, T.config_single_route())
