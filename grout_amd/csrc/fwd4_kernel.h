@@ -31,6 +31,7 @@ struct fwd4_edges {
 #define FWD4_RX_MAC_OK 0x01 // iface_get_eth_addr() succeeds
 #define FWD4_RX_SNAT_DYN 0x02 // GR_IFACE_F_SNAT_DYNAMIC
 #define FWD4_RX_VLAN_DEMUX 0x04 // mode VRF: tagged packets look up a sub-iface
+#define FWD4_RX_FIB16 0x08 // the FIB uses 2-byte entries (bit15 = tbl8 group)
 struct fwd4_rx {
 	uint16_t id; // 0: no such iface
 	uint8_t e_in; // iface_input edge: ADMIN_DOWN, mode edge or CHAIN (eth_input)
@@ -98,9 +99,8 @@ struct fwd4_params {
 	uint32_t readable; // frame bytes present per packet (64 or in_stride)
 };
 
-// Kernel variants (gr_hip_tune "staging"): how header lines move between
-// HBM and registers.
-enum {
-	FWD4_STAGE_LDS = 0, // coalesced 16 B/lane loads -> LDS -> per-lane rows
-	FWD4_STAGE_DIRECT = 1, // each lane loads / stores its own 64 B line
-};
+// Kernel variants (bit mask, gr_hip_tune): counters, nontemporal loads and
+// stores of the streamed data.
+#define FWD4_V_STATS 0x1
+#define FWD4_V_NT_LOAD 0x2
+#define FWD4_V_NT_STORE 0x4

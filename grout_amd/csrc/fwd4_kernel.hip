@@ -116,7 +116,7 @@ struct stat_slot {
 };
 
 // One lane (the wave leader of a key) adds a wave's contribution.
-__device__ __noinline__ void slot_add(stat_slot *slots, const kctx &P, uint32_t key, uint32_t pkts, uint32_t bytes) {
+__device__ __forceinline__ void slot_add(stat_slot *slots, const kctx &P, uint32_t key, uint32_t pkts, uint32_t bytes) {
 	uint32_t h = (key * 0x9e3779b1u) >> 27; // 32 slots
 #pragma unroll 1
 	for (uint32_t i = 0; i < FWD4_STAT_SLOTS; i++) {
@@ -311,10 +311,18 @@ __device__ __forceinline__ result process(const kctx &P, uint32_t (&w)[16], cons
 	uint32_t slot = 0;
 	if (rx.tbl24 != nullptr) {
 		const uint32_t ip = __builtin_bswap32(dst);
-		uint32_t ent = rx.tbl24[ip >> 8];
-		if (ent & 0x80000000u)
-			ent = rx.tbl8[(size_t)(ent & 0x7fffffffu) * 256 + (ip & 0xff)];
-		slot = ent;
+		if (rx.flags & FWD4_RX_FIB16) { // 2-byte entries, bit15 = tbl8 group
+			const uint16_t *t24 = reinterpret_cast<const uint16_t *>(rx.tbl24);
+			uint32_t ent = t24[ip >> 8];
+			if (ent & 0x8000u)
+				ent = reinterpret_cast<const uint16_t *>(rx.tbl8)[(size_t)(ent & 0x7fffu) * 256 + (ip & 0xff)];
+			slot = ent;
+		} else {
+			uint32_t ent = rx.tbl24[ip >> 8];
+			if (ent & 0x80000000u)
+				ent = rx.tbl8[(size_t)(ent & 0x7fffffffu) * 256 + (ip & 0xff)];
+			slot = ent;
+		}
 	}
 	if (slot == 0 || slot > P.max_nh) {
 		r.edge = GR_HIP_E_IP_ERROR_DEST_UNREACH; // NO_ROUTE :150-153
@@ -391,9 +399,30 @@ __device__ __forceinline__ result process(const kctx &P, uint32_t (&w)[16], cons
 	return r;
 }
 
-template <int STAGE, bool STATS>
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ u4v ld16(const uint8_t *p) {
+	const u4v *q = reinterpret_cast<const u4v *>(p);
+	if (NT)
+		return __builtin_nontemporal_load(q);
+	return *q;
+}
+
+template <bool NT>
+__device__ __forceinline__ void st16(uint8_t *p, u4v v) {
+	u4v *q = reinterpret_cast<u4v *>(p);
+	if (NT)
+		__builtin_nontemporal_store(v, q);
+	else
+		*q = v;
+}
+
+// STATS: per-iface counters. NTL / NTS: nontemporal loads / stores of the
+// streamed lines, metadata and verdicts (keeps L2 for the FIB gathers).
+template <bool STATS, bool NTL, bool NTS>
 __global__ void __launch_bounds__(FWD4_BLOCK) gr_fwd4_kernel(const fwd4_params A) {
-	__shared__ __attribute__((aligned(16))) uint8_t lines[STAGE == FWD4_STAGE_LDS ? FWD4_BLOCK * FWD4_ROW : 16];
+	__shared__ __attribute__((aligned(16))) uint8_t lines[FWD4_BLOCK * FWD4_ROW];
 	__shared__ stat_slot slots[FWD4_STAT_SLOTS];
 	__shared__ fwd4_edges edges;
 	const uint32_t tid = threadIdx.x;
@@ -419,74 +448,60 @@ __global__ void __launch_bounds__(FWD4_BLOCK) gr_fwd4_kernel(const fwd4_params A
 	P.readable = A.readable;
 	P.edges = &edges;
 	P.stats = A.stats;
-	__syncthreads();
 
 	const uint32_t n_tiles = (A.n + FWD4_BLOCK - 1) / FWD4_BLOCK;
 	for (uint32_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
 		const uint32_t base = tile * FWD4_BLOCK;
 		const uint32_t cnt = min((uint32_t)FWD4_BLOCK, A.n - base);
 		const bool live = tid < cnt;
-		uint32_t w[16];
 		gr_hip_pkt_meta m = {0, 0, 0, 0};
-		if (live)
-			m = A.meta[base + tid];
+		if (live) {
+			uint2 mm;
+			if (NTL)
+				mm = make_uint2(__builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(A.meta + base + tid)),
+						__builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(A.meta + base + tid) + 1));
+			else
+				mm = *reinterpret_cast<const uint2 *>(A.meta + base + tid);
+			m.iface = mm.x & 0xffff;
+			m.vlan_ck = mm.x >> 16;
+			m.pkt_len = mm.y & 0xffff;
+			m.rss = mm.y >> 16;
+		}
+		// stage: 4 lanes per 64-byte line, 16 bytes each (coalesced)
+#pragma unroll
+		for (uint32_t k = 0; k < 4; k++) {
+			uint32_t c = k * FWD4_BLOCK + tid;
+			uint32_t p = c >> 2, part = c & 3;
+			if (p < cnt)
+				*reinterpret_cast<u4v *>(&lines[p * FWD4_ROW + part * 16]) =
+					ld16<NTL>(A.in + (size_t)(base + p) * A.in_stride + part * 16);
+		}
+		__syncthreads();
 
-		if (STAGE == FWD4_STAGE_LDS) {
-			// 4 lanes per 64-byte line, 16 bytes each (coalesced)
-#pragma unroll
-			for (uint32_t k = 0; k < 4; k++) {
-				uint32_t c = k * FWD4_BLOCK + tid;
-				uint32_t p = c >> 2, part = c & 3;
-				if (p < cnt) {
-					const uint4 *src = reinterpret_cast<const uint4 *>(
-						A.in + (size_t)(base + p) * A.in_stride + part * 16);
-					*reinterpret_cast<uint4 *>(&lines[p * FWD4_ROW + part * 16]) = *src;
-				}
-			}
-			__syncthreads();
-			if (live) {
-				const uint4 *row = reinterpret_cast<const uint4 *>(&lines[tid * FWD4_ROW]);
-#pragma unroll
-				for (int k = 0; k < 4; k++) {
-					uint4 x = row[k];
-					w[4 * k] = x.x;
-					w[4 * k + 1] = x.y;
-					w[4 * k + 2] = x.z;
-					w[4 * k + 3] = x.w;
-				}
-			}
-		} else if (live) {
-			const uint4 *src = reinterpret_cast<const uint4 *>(A.in + (size_t)(base + tid) * A.in_stride);
+		result r = {0, 0, 0, 0, 0, 0, 0, 0};
+		if (live) {
+			uint32_t w[16];
+			u4v *row = reinterpret_cast<u4v *>(&lines[tid * FWD4_ROW]);
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
-				uint4 x = src[k];
+				u4v x = row[k];
 				w[4 * k] = x.x;
 				w[4 * k + 1] = x.y;
 				w[4 * k + 2] = x.z;
 				w[4 * k + 3] = x.w;
 			}
-		}
-
-		result r = {0, 0, 0, 0, 0, 0, 0, 0};
-		if (live) {
 			const uint8_t *frame = A.in + (size_t)(base + tid) * A.in_stride;
 			r = process(P, w, m, frame);
-			gr_hip_verdict v;
-			v.edge = (uint8_t)r.edge;
-			v.domain = (uint8_t)r.domain;
-			v.iface = (uint16_t)r.iface;
-			v.nh = r.nh;
-			A.verdicts[base + tid] = v;
-			if (STAGE == FWD4_STAGE_DIRECT) {
-				uint4 *dst = reinterpret_cast<uint4 *>(A.out + (size_t)(base + tid) * A.out_stride);
 #pragma unroll
-				for (int k = 0; k < 4; k++)
-					dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+			for (int k = 0; k < 4; k++)
+				row[k] = u4v{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
+			uint32_t v0 = r.edge | (r.domain << 8) | (r.iface << 16);
+			uint32_t *vp = reinterpret_cast<uint32_t *>(A.verdicts + base + tid);
+			if (NTS) {
+				__builtin_nontemporal_store(v0, vp);
+				__builtin_nontemporal_store(r.nh, vp + 1);
 			} else {
-				uint4 *row = reinterpret_cast<uint4 *>(&lines[tid * FWD4_ROW]);
-#pragma unroll
-				for (int k = 0; k < 4; k++)
-					row[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+				*reinterpret_cast<uint2 *>(vp) = make_uint2(v0, r.nh);
 			}
 		}
 		if (STATS) { // every lane of the wave takes part in the ballots
@@ -496,20 +511,17 @@ __global__ void __launch_bounds__(FWD4_BLOCK) gr_fwd4_kernel(const fwd4_params A
 			wave_count(slots, P, r.tx_if ? (r.tx_if | 0x10000u) + 1 : 0, len);
 			wave_count(slots, P, r.tx_par ? (r.tx_par | 0x10000u) + 1 : 0, len);
 		}
-		if (STAGE == FWD4_STAGE_LDS) {
-			__syncthreads();
+		__syncthreads();
 #pragma unroll
-			for (uint32_t k = 0; k < 4; k++) {
-				uint32_t c = k * FWD4_BLOCK + tid;
-				uint32_t p = c >> 2, part = c & 3;
-				if (p < cnt) {
-					uint4 *dst = reinterpret_cast<uint4 *>(
-						A.out + (size_t)(base + p) * A.out_stride + part * 16);
-					*dst = *reinterpret_cast<const uint4 *>(&lines[p * FWD4_ROW + part * 16]);
-				}
-			}
-			__syncthreads();
+		for (uint32_t k = 0; k < 4; k++) {
+			uint32_t c = k * FWD4_BLOCK + tid;
+			uint32_t p = c >> 2, part = c & 3;
+			if (p < cnt)
+				st16<NTS>(A.out + (size_t)(base + p) * A.out_stride + part * 16,
+					  *reinterpret_cast<const u4v *>(&lines[p * FWD4_ROW + part * 16]));
 		}
+		if (tile + gridDim.x < n_tiles)
+			__syncthreads(); // the next tile reuses the LDS rows
 	}
 
 	if (STATS) {
@@ -527,33 +539,22 @@ __global__ void __launch_bounds__(FWD4_BLOCK) gr_fwd4_kernel(const fwd4_params A
 	}
 }
 
-template <int STAGE, bool STATS>
-static hipError_t launch_one(const fwd4_params *A, uint32_t grid, hipStream_t s) {
-	hipLaunchKernelGGL((gr_fwd4_kernel<STAGE, STATS>), dim3(grid), dim3(FWD4_BLOCK), 0, s, *A);
+typedef void (*fwd4_kfn)(const fwd4_params);
+#define KV(v) gr_fwd4_kernel<((v) & 1) != 0, ((v) & 2) != 0, ((v) & 4) != 0>
+static const fwd4_kfn kernels[8] = {KV(0), KV(1), KV(2), KV(3), KV(4), KV(5), KV(6), KV(7)};
+
+// variant: bit0 counters, bit1 nontemporal loads, bit2 nontemporal stores.
+extern "C" hipError_t gr_fwd4_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant) {
+	hipLaunchKernelGGL(kernels[variant & 7], dim3(grid), dim3(FWD4_BLOCK), 0, s, *A);
 	return hipGetLastError();
 }
 
-template <int STAGE, bool STATS>
-static int occ_one() {
+// Resident workgroups per CU of a variant.
+extern "C" int gr_fwd4_occupancy(int variant) {
 	int b = 0;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gr_fwd4_kernel<STAGE, STATS>, FWD4_BLOCK, 0) != hipSuccess) {
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernels[variant & 7], FWD4_BLOCK, 0) != hipSuccess) {
 		(void)hipGetLastError();
 		return 0;
 	}
 	return b;
-}
-
-// stage: FWD4_STAGE_*; stats: counters on/off (off only for measurements).
-extern "C" hipError_t gr_fwd4_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int stage, int stats) {
-	if (stage == FWD4_STAGE_DIRECT)
-		return stats ? launch_one<FWD4_STAGE_DIRECT, true>(A, grid, s)
-			     : launch_one<FWD4_STAGE_DIRECT, false>(A, grid, s);
-	return stats ? launch_one<FWD4_STAGE_LDS, true>(A, grid, s) : launch_one<FWD4_STAGE_LDS, false>(A, grid, s);
-}
-
-// Resident workgroups per CU of a variant (sizes the persistent grid).
-extern "C" int gr_fwd4_occupancy(int stage, int stats) {
-	if (stage == FWD4_STAGE_DIRECT)
-		return stats ? occ_one<FWD4_STAGE_DIRECT, true>() : occ_one<FWD4_STAGE_DIRECT, false>();
-	return stats ? occ_one<FWD4_STAGE_LDS, true>() : occ_one<FWD4_STAGE_LDS, false>();
 }

@@ -23,8 +23,8 @@
 #include <string.h>
 #include <vector>
 
-extern "C" hipError_t gr_fwd4_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int stage, int stats);
-extern "C" int gr_fwd4_occupancy(int stage, int stats);
+extern "C" hipError_t gr_fwd4_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant);
+extern "C" int gr_fwd4_occupancy(int variant);
 
 #define HCK(expr)                                                                                  \
 	do {                                                                                       \
@@ -43,10 +43,14 @@ constexpr uint32_t HOST_CHUNK = 1u << 18; // packets per host-mode chunk
 
 struct vrf_fib {
 	gr_fib4 *rib = nullptr;
-	uint32_t *d24 = nullptr;
+	uint32_t *d24 = nullptr; // 4-byte entries (fib4.h encoding)
 	uint32_t *d8 = nullptr;
+	uint16_t *d24_16 = nullptr; // 2-byte entries, used while every slot fits 15 bits
+	uint16_t *d8_16 = nullptr;
+	bool fmt16 = false; // format on the device
+	uint32_t max_slot = 0; // highest nexthop slot ever routed (never decreases)
 	uint32_t num_tbl8 = 0;
-	bool uploaded = false; // tbl24 uploaded at least once
+	bool uploaded = false; // tables uploaded at least once
 };
 
 struct host_slot {
@@ -93,10 +97,11 @@ struct gr_hip_ctx {
 	fwd4_tables *d_tables; // device copy of what every launch reads
 	std::vector<gr_hip_queue *> queues;
 	// tuning knobs (gr_hip_tune)
-	int stage; // FWD4_STAGE_*
+	int nt; // FWD4_V_NT_LOAD | FWD4_V_NT_STORE
 	int stats_on;
-	int wg_per_cu; // 0 = occupancy of the variant
-	int occ[2][2];
+	int wg_per_cu; // 0 = one tile per workgroup, N = persistent N per CU
+	int fib16; // allow the 2-byte FIB format
+	int occ[8];
 };
 
 // ---------------------------------------------------------------------------
@@ -147,9 +152,17 @@ static fwd4_rx make_rx(const gr_hip_ctx *c, uint32_t id) {
 		| (i->mode == GR_HIP_IFACE_MODE_VRF ? FWD4_RX_VLAN_DEMUX : 0);
 	memcpy(r.mac, i->mac, 6);
 	const gr_hip_iface *vrf = iface_get(c, i->vrf_id);
-	if (vrf != nullptr && vrf->type == GR_HIP_IFACE_TYPE_VRF && c->vrfs[i->vrf_id].rib != nullptr) {
-		r.tbl24 = c->vrfs[i->vrf_id].d24;
-		r.tbl8 = c->vrfs[i->vrf_id].d8;
+	if (vrf != nullptr && vrf->type == GR_HIP_IFACE_TYPE_VRF && c->vrfs[i->vrf_id].rib != nullptr
+	    && c->vrfs[i->vrf_id].uploaded) {
+		const vrf_fib &v = c->vrfs[i->vrf_id];
+		if (v.fmt16) {
+			r.tbl24 = reinterpret_cast<const uint32_t *>(v.d24_16);
+			r.tbl8 = reinterpret_cast<const uint32_t *>(v.d8_16);
+			r.flags |= FWD4_RX_FIB16;
+		} else {
+			r.tbl24 = v.d24;
+			r.tbl8 = v.d8;
+		}
 	}
 	return r;
 }
@@ -367,12 +380,12 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	if (hipMemsetAsync(c->d_rx, 0, sizeof(fwd4_rx) * max_ifaces, c->ctl) != hipSuccess
 	    || hipMemsetAsync(c->d_adj, 0, sizeof(fwd4_adj) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess)
 		goto fail;
-	c->stage = FWD4_STAGE_LDS;
+	c->nt = 0;
 	c->stats_on = 1;
 	c->wg_per_cu = 0;
-	for (int a = 0; a < 2; a++)
-		for (int b = 0; b < 2; b++)
-			c->occ[a][b] = gr_fwd4_occupancy(a, b);
+	c->fib16 = 1;
+	for (int v = 0; v < 8; v++)
+		c->occ[v] = gr_fwd4_occupancy(v);
 	ret = -EIO;
 	if (upload_tables(c) != 0)
 		goto fail;
@@ -394,6 +407,8 @@ extern "C" int gr_hip_fini(gr_hip_ctx_t *c) {
 		gr_fib4_free(v.rib);
 		hipFree(v.d24);
 		hipFree(v.d8);
+		hipFree(v.d24_16);
+		hipFree(v.d8_16);
 	}
 	hipFree(c->d_rx);
 	hipFree(c->d_adj);
@@ -603,22 +618,9 @@ extern "C" int gr_hip_fib4_create(gr_hip_ctx_t *c, uint16_t vrf, uint32_t max_ro
 	if (v.rib == nullptr)
 		return -ENOMEM;
 	v.num_tbl8 = num_tbl8;
-	if (hipMalloc(&v.d24, sizeof(uint32_t) * GR_FIB4_TBL24_ENTRIES) != hipSuccess
-	    || hipMalloc(&v.d8, sizeof(uint32_t) * 256 * (size_t)num_tbl8) != hipSuccess
-	    || hipMemsetAsync(v.d24, 0, sizeof(uint32_t) * GR_FIB4_TBL24_ENTRIES, c->ctl) != hipSuccess
-	    || hipMemsetAsync(v.d8, 0, sizeof(uint32_t) * 256 * (size_t)num_tbl8, c->ctl) != hipSuccess) {
-		(void)hipGetLastError();
-		hipFree(v.d24);
-		hipFree(v.d8);
-		gr_fib4_free(v.rib);
-		v = vrf_fib {};
-		return -ENOMEM;
-	}
+	// device tables are allocated by the first commit, in the format it picks
 	gr_fib4_dirty_clear(v.rib);
-	int r = quiesce(c);
-	if (r == 0) // the RX views of the VRF's ifaces now point at the FIB
-		r = upload_views(c, true, 0, 0, false);
-	return r;
+	return 0;
 }
 
 extern "C" int gr_hip_fib4_destroy(gr_hip_ctx_t *c, uint16_t vrf) {
@@ -641,6 +643,8 @@ extern "C" int gr_hip_fib4_destroy(gr_hip_ctx_t *c, uint16_t vrf) {
 	v.rib = rib;
 	hipFree(v.d24);
 	hipFree(v.d8);
+	hipFree(v.d24_16);
+	hipFree(v.d8_16);
 	gr_fib4_free(v.rib);
 	v = vrf_fib {};
 	return 0;
@@ -660,6 +664,8 @@ extern "C" int gr_hip_route4_add(gr_hip_ctx_t *c, const struct gr_hip_route4 *rt
 		int r = gr_fib4_add(v.rib, __builtin_bswap32(rt[i].ip), rt[i].prefixlen, rt[i].nh, replace);
 		if (r < 0)
 			return r;
+		if (rt[i].nh > v.max_slot)
+			v.max_slot = rt[i].nh;
 	}
 	return 0;
 }
@@ -674,6 +680,30 @@ extern "C" int gr_hip_route4_del(gr_hip_ctx_t *c, uint16_t vrf, uint32_t ip, uin
 	return gr_fib4_del(v.rib, __builtin_bswap32(ip), len);
 }
 
+// Upload runs of tbl8 groups (sorted) from a host table of `esz`-byte entries.
+template <typename E>
+static int upload_groups(gr_hip_ctx *c, E *dev, const E *host, std::vector<uint32_t> &gs) {
+	std::sort(gs.begin(), gs.end());
+	for (size_t i = 0; i < gs.size();) {
+		size_t j = i + 1;
+		while (j < gs.size() && gs[j] == gs[j - 1] + 1)
+			j++;
+		int r = h2d(c, dev + (size_t)gs[i] * 256, host + (size_t)gs[i] * 256, (j - i) * 256 * sizeof(E));
+		if (r)
+			return r;
+		i = j;
+	}
+	return 0;
+}
+
+static uint16_t to16(uint32_t e) { // fib4.h 4-byte entry -> 2-byte entry
+	return (uint16_t)((e & GR_FIB4_EXT) ? (0x8000u | (e & 0x7fffu)) : e);
+}
+
+// Stream-ordered FIB publication: quiesce the queues, upload what changed in
+// the format the tables fit (2-byte entries while every nexthop slot fits 15
+// bits and every tbl8 group index too, else 4-byte), then re-point the RX
+// views when the format or the first upload changed them.
 extern "C" int gr_hip_fib4_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
@@ -682,38 +712,68 @@ extern "C" int gr_hip_fib4_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib == nullptr)
 		return -ENONET;
+	const bool want16 = c->fib16 && v.max_slot <= 0x7fff && v.num_tbl8 <= 0x8000;
+	const bool full = !v.uploaded || want16 != v.fmt16;
 	uint32_t lo, hi;
 	gr_fib4_dirty_tbl24(v.rib, &lo, &hi);
-	std::vector<uint32_t> groups(v.num_tbl8);
-	int ng = gr_fib4_dirty_tbl8(v.rib, groups.data(), v.num_tbl8);
+	std::vector<uint32_t> gs(v.num_tbl8);
+	int ng = gr_fib4_dirty_tbl8(v.rib, gs.data(), v.num_tbl8);
+	if (full) {
+		lo = 0;
+		hi = GR_FIB4_TBL24_ENTRIES;
+		ng = -1;
+	}
+	if (ng >= 0)
+		gs.resize((size_t)ng);
+	else {
+		gs.resize(v.num_tbl8);
+		for (uint32_t g = 0; g < v.num_tbl8; g++)
+			gs[g] = g;
+	}
 	int r = quiesce(c);
 	if (r != 0)
 		return r;
 	const uint32_t *t24 = gr_fib4_tbl24(v.rib);
 	const uint32_t *t8 = gr_fib4_tbl8(v.rib);
-	if (lo < hi)
-		r = h2d(c, v.d24 + lo, t24 + lo, (size_t)(hi - lo) * sizeof(uint32_t));
-	if (r == 0 && ng < 0) {
-		r = h2d(c, v.d8, t8, sizeof(uint32_t) * 256 * (size_t)v.num_tbl8);
-	} else if (r == 0 && ng > 0) {
-		// coalesce runs of consecutive groups
-		std::vector<uint32_t> gs(groups.begin(), groups.begin() + ng);
-		std::sort(gs.begin(), gs.end());
-		for (size_t i = 0; i < gs.size() && r == 0;) {
-			size_t j = i + 1;
-			while (j < gs.size() && gs[j] == gs[j - 1] + 1)
-				j++;
-			r = h2d(c, v.d8 + (size_t)gs[i] * 256, t8 + (size_t)gs[i] * 256,
-				(j - i) * 256 * sizeof(uint32_t));
-			i = j;
+	if (want16) {
+		if (v.d24_16 == nullptr) {
+			HCK(hipStreamSynchronize(c->ctl));
+			HCK(hipMalloc(&v.d24_16, sizeof(uint16_t) * GR_FIB4_TBL24_ENTRIES));
+			HCK(hipMalloc(&v.d8_16, sizeof(uint16_t) * 256 * (size_t)v.num_tbl8));
 		}
+		std::vector<uint16_t> h24(hi > lo ? hi - lo : 0), h8((size_t)v.num_tbl8 * 256);
+		for (uint32_t i = lo; i < hi; i++)
+			h24[i - lo] = to16(t24[i]);
+		for (uint32_t g : gs)
+			for (uint32_t k = 0; k < 256; k++)
+				h8[(size_t)g * 256 + k] = to16(t8[(size_t)g * 256 + k]);
+		if (hi > lo)
+			r = h2d(c, v.d24_16 + lo, h24.data(), (size_t)(hi - lo) * sizeof(uint16_t));
+		if (r == 0)
+			r = upload_groups<uint16_t>(c, v.d8_16, h8.data(), gs);
+		if (r == 0)
+			r = ctl_sync(c); // the staging vectors go out of scope
+	} else {
+		if (v.d24 == nullptr) {
+			HCK(hipStreamSynchronize(c->ctl));
+			HCK(hipMalloc(&v.d24, sizeof(uint32_t) * GR_FIB4_TBL24_ENTRIES));
+			HCK(hipMalloc(&v.d8, sizeof(uint32_t) * 256 * (size_t)v.num_tbl8));
+		}
+		if (hi > lo)
+			r = h2d(c, v.d24 + lo, t24 + lo, (size_t)(hi - lo) * sizeof(uint32_t));
+		if (r == 0)
+			r = upload_groups<uint32_t>(c, v.d8, t8, gs);
+		if (r == 0)
+			r = ctl_sync(c);
 	}
-	if (r == 0)
-		r = ctl_sync(c);
-	if (r == 0) {
-		gr_fib4_dirty_clear(v.rib);
-		v.uploaded = true;
-	}
+	if (r != 0)
+		return r;
+	gr_fib4_dirty_clear(v.rib);
+	bool repoint = full;
+	v.fmt16 = want16;
+	v.uploaded = true;
+	if (repoint)
+		r = upload_views(c, true, 0, 0, false);
 	return r;
 }
 
@@ -740,7 +800,8 @@ extern "C" int gr_hip_fib4_info(gr_hip_ctx_t *c, uint16_t vrf, uint32_t *n_route
 	if (tbl8_used)
 		*tbl8_used = gr_fib4_tbl8_used(v.rib);
 	if (bytes)
-		*bytes = sizeof(uint32_t) * ((uint64_t)GR_FIB4_TBL24_ENTRIES + 256ull * v.num_tbl8);
+		*bytes = (v.fmt16 ? sizeof(uint16_t) : sizeof(uint32_t))
+			* ((uint64_t)GR_FIB4_TBL24_ENTRIES + 256ull * v.num_tbl8);
 	return 0;
 }
 
@@ -834,17 +895,15 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	A.out_stride = b->out_stride;
 	A.readable = (b->flags & GR_HIP_BATCH_F_LINES_ONLY) ? GR_HIP_LINE : b->in_stride;
 	int stats = c->stats_on && q->d_stats != nullptr;
-	uint32_t per_cu = c->wg_per_cu > 0 ? (uint32_t)c->wg_per_cu : (uint32_t)c->occ[c->stage][stats];
-	if (per_cu == 0)
-		per_cu = 4;
+	int variant = (stats ? FWD4_V_STATS : 0) | c->nt;
 	uint32_t tiles = (b->n + FWD4_BLOCK - 1) / FWD4_BLOCK;
-	uint32_t grid = (uint32_t)c->n_cu * per_cu;
+	uint32_t grid = c->wg_per_cu > 0 ? (uint32_t)c->n_cu * (uint32_t)c->wg_per_cu : tiles;
 	if (grid > tiles)
 		grid = tiles;
 	uint32_t slot = (uint32_t)(q->n_launch % N_TIMED);
 	if (timed)
 		HCK(hipEventRecord(q->ev0[slot], s));
-	HCK(gr_fwd4_launch(&A, grid, s, c->stage, stats));
+	HCK(gr_fwd4_launch(&A, grid, s, variant));
 	if (timed) {
 		HCK(hipEventRecord(q->ev1[slot], s));
 		q->n_launch++;
@@ -856,18 +915,20 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 	if (c == nullptr || key == nullptr)
 		return -EINVAL;
 	std::lock_guard<std::mutex> l(c->mu);
-	if (strcmp(key, "staging") == 0) {
-		if (value != FWD4_STAGE_LDS && value != FWD4_STAGE_DIRECT)
+	if (strcmp(key, "nt") == 0) {
+		if (value < 0 || value > 3)
 			return -EINVAL;
-		c->stage = value;
+		c->nt = (value & 1 ? FWD4_V_NT_LOAD : 0) | (value & 2 ? FWD4_V_NT_STORE : 0);
 	} else if (strcmp(key, "stats") == 0) {
 		c->stats_on = value != 0;
 	} else if (strcmp(key, "wg_per_cu") == 0) {
 		if (value < 0 || value > 32)
 			return -EINVAL;
 		c->wg_per_cu = value;
+	} else if (strcmp(key, "fib16") == 0) { // takes effect at the next commit
+		c->fib16 = value != 0;
 	} else if (strcmp(key, "occupancy") == 0) { // read-only: WGs/CU of the current variant
-		return c->occ[c->stage][c->stats_on];
+		return c->occ[(c->stats_on ? FWD4_V_STATS : 0) | c->nt];
 	} else {
 		return -ENOENT;
 	}

@@ -343,9 +343,12 @@ int gr_hip_queue_sync(gr_hip_queue_t *);
 int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *count);
 
 // Tuning knobs, for measurements (A/B in one process). Keys:
-//   "staging"   0 = LDS-staged coalesced lines (default), 1 = per-lane lines
 //   "stats"     1 = per-iface counters (default; grout always counts), 0 = off
-//   "wg_per_cu" persistent workgroups per CU, 0 = occupancy of the variant
+//   "nt"        nontemporal streamed data: bit0 loads, bit1 stores (default 0)
+//   "wg_per_cu" 0 = one 256-packet tile per workgroup (default),
+//               N = persistent grid of N workgroups per CU
+//   "fib16"     1 = 2-byte FIB entries when slots fit 15 bits (default),
+//               0 = always 4-byte; applies from the next gr_hip_fib4_commit
 //   "occupancy" (read) resident workgroups per CU of the current variant
 // Returns 0 (or the value read), -EINVAL, or -ENOENT for an unknown key.
 int gr_hip_tune(gr_hip_ctx_t *, const char *key, int value);

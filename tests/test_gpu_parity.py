@@ -191,32 +191,34 @@ def test_kernel_timing_api(fastpath):
     q.close()
 
 
-@pytest.mark.parametrize("staging,stats", [(1, 1), (1, 0), (0, 0)])
-def test_kernel_variants(fastpath, staging, stats):
+@pytest.mark.parametrize("nt,stats,wg,fib16", [(3, 1, 0, 1), (1, 0, 6, 1), (2, 1, 4, 0), (0, 1, 0, 0)])
+def test_kernel_variants(fastpath, nt, stats, wg, fib16):
     """Every tuning variant (gr_hip_tune) forwards bit-exact."""
     t, _ = SC.corpus_topology()
     fr, me, lab = SC.corpus_arrays()
-    o = oracle.Oracle(t).process(fr, me)
-    fastpath.tune("staging", staging)
-    fastpath.tune("stats", stats)
-    try:
-        g = run_gpu(fastpath, t, fr, me)
-    finally:
-        fastpath.tune("staging", 0)
-        fastpath.tune("stats", 1)
-    if stats:
-        compare(o, g, lab)
-    else:
-        compare((o[0], o[1], g[2]), g, lab)
-        assert not g[2]["rx_packets"].any()
     tf = _fullview()
-    fr, me = S.stream(1 << 20, 0xAB + staging, routes=tf.route_array())
-    o = oracle.Oracle(tf).process(fr, me)
-    fastpath.tune("staging", staging)
+    fr2, me2 = S.stream(1 << 20, 0xAB + nt, routes=tf.route_array())
+    o1 = oracle.Oracle(t).process(fr, me)
+    o2 = oracle.Oracle(tf).process(fr2, me2)
+    fastpath.tune("nt", nt)
+    fastpath.tune("stats", stats)
+    fastpath.tune("wg_per_cu", wg)
+    fastpath.tune("fib16", fib16)
     try:
-        compare(o, run_gpu(fastpath, tf, fr, me))
+        fresh_fastpath_state(fastpath, T.config_single_route())  # force a reload (commit)
+        g = run_gpu(fastpath, t, fr, me)
+        if stats:
+            compare(o1, g, lab)
+        else:
+            compare((o1[0], o1[1], g[2]), g, lab)
+            assert not g[2]["rx_packets"].any()
+        g2 = run_gpu(fastpath, tf, fr2, me2)
+        compare(o2 if stats else (o2[0], o2[1], g2[2]), g2)
+        assert fastpath.fib_info(1)["dev_bytes"] == (2 if fib16 else 4) * ((1 << 24) + 256 * max(256, 1_000_010 // 500))
     finally:
-        fastpath.tune("staging", 0)
+        for k, v in [("nt", 0), ("stats", 1), ("wg_per_cu", 0), ("fib16", 1)]:
+            fastpath.tune(k, v)
+        fresh_fastpath_state(fastpath, T.config_single_route())
 
 
 def test_mirror_updates_propagate(fastpath):
@@ -226,7 +228,7 @@ def test_mirror_updates_propagate(fastpath):
     run_gpu(fastpath, t, fr, me)  # loads t
     # p1 admin down (egress for most forwards), p2 MTU 1500, p0 loses its MAC,
     # one nexthop becomes unresolved, another changes MAC
-    t.ifaces[SC.P1]["flags"] &= ~abi.IFACE_F_UP
+    t.ifaces[SC.P1]["flags"] = int(t.ifaces[SC.P1]["flags"]) & ~abi.IFACE_F_UP & 0xFFFF
     t.ifaces[SC.P2]["mtu"] = 1500
     t.ifaces[SC.BOND]["mac_ok"] = 0
     t.nh[nh["fwd2"]]["state"] = abi.NH_S["STALE"]

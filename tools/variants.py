@@ -1,8 +1,10 @@
 # SPDX-License-Identifier: BSD-3-Clause
 """A/B the kernel variants in ONE process, interleaved rounds (methodology
-rule 24 of cdna_hip_programming.md): staging x stats x workgroups per CU on
-the headline workload. Prints one JSON line per variant (median / min ms)."""
+rule 24 of cdna_hip_programming.md) on a bench workload: counters on/off,
+nontemporal loads/stores, grid shape, FIB entry size. One JSON line per
+variant (median / min kernel ms from the library's HIP events)."""
 import argparse
+import itertools
 import json
 import os
 import sys
@@ -12,12 +14,20 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def ints(s):
+    return [int(x) for x in s.split(",")]
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--batch", type=int, default=1 << 24)
-    ap.add_argument("--wg", default="0,2,4")
+    ap.add_argument("--workload", default="fullview64", choices=["fullview64", "single64"])
+    ap.add_argument("--nt", default="0,1,2,3")
+    ap.add_argument("--wg", default="0,6")
+    ap.add_argument("--fib16", default="1,0")
+    ap.add_argument("--stats", default="1")
     args = ap.parse_args()
     import torch
 
@@ -26,40 +36,48 @@ def main():
     from grout_amd.fwd import FastPath
 
     dev = torch.device("cuda", 0)
-    topo = T.config_fullview()
+    if args.workload == "single64":
+        topo = T.config_single_route()
+        kw = dict(dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    else:
+        topo = T.config_fullview()
+        kw = dict(routes=topo.route_array())
     fp = FastPath(0)
     fp.load(topo)
     n = args.batch
-    frames, meta = S.stream(n, S.SEED_GPU_BASE, routes=topo.route_array())
+    frames, meta = S.stream(n, S.SEED_GPU_BASE, **kw)
     d_in = torch.from_numpy(frames.reshape(-1)).to(dev)
     d_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
     d_out = torch.empty_like(d_in)
     d_v = torch.empty(n * 8, dtype=torch.uint8, device=dev)
     q = fp.queue(torch.cuda.current_stream(dev).cuda_stream)
-    variants = []
-    for st in (0, 1):
-        for stats in (1, 0):
-            for wg in [int(x) for x in args.wg.split(",")]:
-                variants.append((st, stats, wg))
+    variants = list(itertools.product(ints(args.fib16), ints(args.stats), ints(args.nt), ints(args.wg)))
     times = {v: [] for v in variants}
-    occ = {}
+    ref = None
     for r in range(args.rounds):
         for v in variants:
-            fp.tune("staging", v[0])
-            fp.tune("stats", v[1])
-            fp.tune("wg_per_cu", v[2])
-            occ[v] = fp.tune("occupancy")
+            f16, st, nt, wg = v
+            fp.tune("fib16", f16)
+            fp.fib_commit(T.VRF_MAIN)  # re-uploads when the format changes
+            fp.tune("stats", st)
+            fp.tune("nt", nt)
+            fp.tune("wg_per_cu", wg)
             q.submit(d_in, d_out, d_meta, d_v, n)  # warm
             for _ in range(args.reps):
                 q.submit(d_in, d_out, d_meta, d_v, n)
             q.sync()
             ms, cnt = q.kernel_ms(args.reps)
             times[v].append(ms / cnt)
+            if r == 0:  # every variant must produce the same verdicts
+                h = int(torch.sum(d_v.view(torch.int32).to(torch.int64)).item())
+                ref = h if ref is None else ref
+                assert h == ref, ("verdicts differ", v)
     for v in variants:
         t = np.array(times[v])
-        print(json.dumps({"staging": ["lds", "direct"][v[0]], "stats": v[1], "wg_per_cu": v[2] or occ[v],
-                          "median_ms": round(float(np.median(t)), 4), "min_ms": round(float(t.min()), 4),
-                          "mpps": round(n / float(np.median(t)) / 1e3, 1)}), flush=True)
+        print(json.dumps({"workload": args.workload, "fib16": v[0], "stats": v[1], "nt": v[2],
+                          "wg_per_cu": v[3], "median_ms": round(float(np.median(t)), 4),
+                          "min_ms": round(float(t.min()), 4), "mpps": round(n / float(np.median(t)) / 1e3, 1)}),
+              flush=True)
     q.close()
     fp.close()
 
