@@ -8,7 +8,6 @@
 
 #include <stdint.h>
 
-#define FWD4_BLOCK 256 // packets per tile = threads per block (4 waves)
 #define FWD4_ROW 80 // LDS bytes per staged 64-byte line (+16: no bank conflicts)
 #define FWD4_STAT_SLOTS 32 // per-block iface counter slots (LDS)
 #define FWD4_STAT_SHARDS 64 // global counter shards (block % shards)
@@ -102,5 +101,5 @@ struct fwd4_params {
 // Kernel variants (bit mask, gr_hip_tune): counters, nontemporal loads and
 // stores of the streamed data.
 #define FWD4_V_STATS 0x1
-#define FWD4_V_NT_LOAD 0x2
-#define FWD4_V_NT_STORE 0x4
+#define FWD4_V_NT 0x2 // nontemporal loads and stores of the streamed data
+#define FWD4_V_TILE64 0x4 // one-wave workgroups, 64-packet tiles (else 256)

@@ -400,6 +400,7 @@ __device__ __forceinline__ result process(const kctx &P, uint32_t (&w)[16], cons
 }
 
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u2v __attribute__((ext_vector_type(2)));
 
 template <bool NT>
 __device__ __forceinline__ u4v ld16(const uint8_t *p) {
@@ -418,18 +419,19 @@ __device__ __forceinline__ void st16(uint8_t *p, u4v v) {
 		*q = v;
 }
 
-// STATS: per-iface counters. NTL / NTS: nontemporal loads / stores of the
-// streamed lines, metadata and verdicts (keeps L2 for the FIB gathers).
-template <bool STATS, bool NTL, bool NTS>
-__global__ void __launch_bounds__(FWD4_BLOCK) gr_fwd4_kernel(const fwd4_params A) {
-	__shared__ __attribute__((aligned(16))) uint8_t lines[FWD4_BLOCK * FWD4_ROW];
+// STATS: per-iface counters. NT: nontemporal loads and stores of the streamed
+// lines, metadata and verdicts (keeps L2 for the FIB gathers). TILE: packets
+// per workgroup = threads per workgroup (64: one wave, 256: four waves).
+template <bool STATS, bool NT, int TILE>
+__global__ void __launch_bounds__(TILE) gr_fwd4_kernel(const fwd4_params A) {
+	__shared__ __attribute__((aligned(16))) uint8_t lines[TILE * FWD4_ROW];
 	__shared__ stat_slot slots[FWD4_STAT_SLOTS];
 	__shared__ fwd4_edges edges;
 	const uint32_t tid = threadIdx.x;
 	const fwd4_tables *T = A.T;
 
-	if (tid < sizeof(fwd4_edges))
-		reinterpret_cast<uint8_t *>(&edges)[tid] = reinterpret_cast<const uint8_t *>(&T->edges)[tid];
+	for (uint32_t i = tid; i < sizeof(fwd4_edges); i += TILE)
+		reinterpret_cast<uint8_t *>(&edges)[i] = reinterpret_cast<const uint8_t *>(&T->edges)[i];
 	if (STATS && tid < FWD4_STAT_SLOTS) {
 		slots[tid].key = 0;
 		slots[tid].pkts = 0;
@@ -449,19 +451,19 @@ __global__ void __launch_bounds__(FWD4_BLOCK) gr_fwd4_kernel(const fwd4_params A
 	P.edges = &edges;
 	P.stats = A.stats;
 
-	const uint32_t n_tiles = (A.n + FWD4_BLOCK - 1) / FWD4_BLOCK;
+	const uint32_t n_tiles = (A.n + TILE - 1) / TILE;
 	for (uint32_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-		const uint32_t base = tile * FWD4_BLOCK;
-		const uint32_t cnt = min((uint32_t)FWD4_BLOCK, A.n - base);
+		const uint32_t base = tile * TILE;
+		const uint32_t cnt = min((uint32_t)TILE, A.n - base);
 		const bool live = tid < cnt;
 		gr_hip_pkt_meta m = {0, 0, 0, 0};
 		if (live) {
-			uint2 mm;
-			if (NTL)
-				mm = make_uint2(__builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(A.meta + base + tid)),
-						__builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(A.meta + base + tid) + 1));
+			u2v mm;
+			const u2v *mp = reinterpret_cast<const u2v *>(A.meta + base + tid);
+			if (NT)
+				mm = __builtin_nontemporal_load(mp);
 			else
-				mm = *reinterpret_cast<const uint2 *>(A.meta + base + tid);
+				mm = *mp;
 			m.iface = mm.x & 0xffff;
 			m.vlan_ck = mm.x >> 16;
 			m.pkt_len = mm.y & 0xffff;
@@ -470,11 +472,11 @@ __global__ void __launch_bounds__(FWD4_BLOCK) gr_fwd4_kernel(const fwd4_params A
 		// stage: 4 lanes per 64-byte line, 16 bytes each (coalesced)
 #pragma unroll
 		for (uint32_t k = 0; k < 4; k++) {
-			uint32_t c = k * FWD4_BLOCK + tid;
+			uint32_t c = k * TILE + tid;
 			uint32_t p = c >> 2, part = c & 3;
 			if (p < cnt)
 				*reinterpret_cast<u4v *>(&lines[p * FWD4_ROW + part * 16]) =
-					ld16<NTL>(A.in + (size_t)(base + p) * A.in_stride + part * 16);
+					ld16<NT>(A.in + (size_t)(base + p) * A.in_stride + part * 16);
 		}
 		__syncthreads();
 
@@ -495,14 +497,12 @@ __global__ void __launch_bounds__(FWD4_BLOCK) gr_fwd4_kernel(const fwd4_params A
 #pragma unroll
 			for (int k = 0; k < 4; k++)
 				row[k] = u4v{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
-			uint32_t v0 = r.edge | (r.domain << 8) | (r.iface << 16);
-			uint32_t *vp = reinterpret_cast<uint32_t *>(A.verdicts + base + tid);
-			if (NTS) {
-				__builtin_nontemporal_store(v0, vp);
-				__builtin_nontemporal_store(r.nh, vp + 1);
-			} else {
-				*reinterpret_cast<uint2 *>(vp) = make_uint2(v0, r.nh);
-			}
+			u2v vv = u2v{r.edge | (r.domain << 8) | (r.iface << 16), r.nh};
+			u2v *vp = reinterpret_cast<u2v *>(A.verdicts + base + tid);
+			if (NT)
+				__builtin_nontemporal_store(vv, vp);
+			else
+				*vp = vv;
 		}
 		if (STATS) { // every lane of the wave takes part in the ballots
 			uint32_t len = m.pkt_len;
@@ -514,11 +514,11 @@ __global__ void __launch_bounds__(FWD4_BLOCK) gr_fwd4_kernel(const fwd4_params A
 		__syncthreads();
 #pragma unroll
 		for (uint32_t k = 0; k < 4; k++) {
-			uint32_t c = k * FWD4_BLOCK + tid;
+			uint32_t c = k * TILE + tid;
 			uint32_t p = c >> 2, part = c & 3;
 			if (p < cnt)
-				st16<NTS>(A.out + (size_t)(base + p) * A.out_stride + part * 16,
-					  *reinterpret_cast<const u4v *>(&lines[p * FWD4_ROW + part * 16]));
+				st16<NT>(A.out + (size_t)(base + p) * A.out_stride + part * 16,
+					 *reinterpret_cast<const u4v *>(&lines[p * FWD4_ROW + part * 16]));
 		}
 		if (tile + gridDim.x < n_tiles)
 			__syncthreads(); // the next tile reuses the LDS rows
@@ -540,19 +540,27 @@ __global__ void __launch_bounds__(FWD4_BLOCK) gr_fwd4_kernel(const fwd4_params A
 }
 
 typedef void (*fwd4_kfn)(const fwd4_params);
-#define KV(v) gr_fwd4_kernel<((v) & 1) != 0, ((v) & 2) != 0, ((v) & 4) != 0>
+#define KV(v) gr_fwd4_kernel<((v) & 1) != 0, ((v) & 2) != 0, ((v) & 4) ? 64 : 256>
 static const fwd4_kfn kernels[8] = {KV(0), KV(1), KV(2), KV(3), KV(4), KV(5), KV(6), KV(7)};
 
-// variant: bit0 counters, bit1 nontemporal loads, bit2 nontemporal stores.
+static uint32_t tile_of(int variant) {
+	return (variant & FWD4_V_TILE64) ? 64 : 256;
+}
+
+// variant: FWD4_V_* bits (counters, nontemporal streams, 64-packet tiles).
 extern "C" hipError_t gr_fwd4_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant) {
-	hipLaunchKernelGGL(kernels[variant & 7], dim3(grid), dim3(FWD4_BLOCK), 0, s, *A);
+	hipLaunchKernelGGL(kernels[variant & 7], dim3(grid), dim3(tile_of(variant)), 0, s, *A);
 	return hipGetLastError();
+}
+
+extern "C" uint32_t gr_fwd4_tile(int variant) {
+	return tile_of(variant);
 }
 
 // Resident workgroups per CU of a variant.
 extern "C" int gr_fwd4_occupancy(int variant) {
 	int b = 0;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernels[variant & 7], FWD4_BLOCK, 0) != hipSuccess) {
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernels[variant & 7], (int)tile_of(variant), 0) != hipSuccess) {
 		(void)hipGetLastError();
 		return 0;
 	}

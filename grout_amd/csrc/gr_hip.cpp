@@ -25,6 +25,7 @@
 
 extern "C" hipError_t gr_fwd4_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant);
 extern "C" int gr_fwd4_occupancy(int variant);
+extern "C" uint32_t gr_fwd4_tile(int variant);
 
 #define HCK(expr)                                                                                  \
 	do {                                                                                       \
@@ -97,11 +98,12 @@ struct gr_hip_ctx {
 	fwd4_tables *d_tables; // device copy of what every launch reads
 	std::vector<gr_hip_queue *> queues;
 	// tuning knobs (gr_hip_tune)
-	int nt; // FWD4_V_NT_LOAD | FWD4_V_NT_STORE
+	int nt; // FWD4_V_NT
 	int stats_on;
 	int wg_per_cu; // 0 = one tile per workgroup, N = persistent N per CU
 	int fib16; // allow the 2-byte FIB format
 	int occ[8];
+	int tile64; // FWD4_V_TILE64
 };
 
 // ---------------------------------------------------------------------------
@@ -384,6 +386,7 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->stats_on = 1;
 	c->wg_per_cu = 0;
 	c->fib16 = 1;
+	c->tile64 = 0;
 	for (int v = 0; v < 8; v++)
 		c->occ[v] = gr_fwd4_occupancy(v);
 	ret = -EIO;
@@ -895,8 +898,9 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	A.out_stride = b->out_stride;
 	A.readable = (b->flags & GR_HIP_BATCH_F_LINES_ONLY) ? GR_HIP_LINE : b->in_stride;
 	int stats = c->stats_on && q->d_stats != nullptr;
-	int variant = (stats ? FWD4_V_STATS : 0) | c->nt;
-	uint32_t tiles = (b->n + FWD4_BLOCK - 1) / FWD4_BLOCK;
+	int variant = (stats ? FWD4_V_STATS : 0) | c->nt | c->tile64;
+	uint32_t tile = gr_fwd4_tile(variant);
+	uint32_t tiles = (b->n + tile - 1) / tile;
 	uint32_t grid = c->wg_per_cu > 0 ? (uint32_t)c->n_cu * (uint32_t)c->wg_per_cu : tiles;
 	if (grid > tiles)
 		grid = tiles;
@@ -916,11 +920,13 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		return -EINVAL;
 	std::lock_guard<std::mutex> l(c->mu);
 	if (strcmp(key, "nt") == 0) {
-		if (value < 0 || value > 3)
-			return -EINVAL;
-		c->nt = (value & 1 ? FWD4_V_NT_LOAD : 0) | (value & 2 ? FWD4_V_NT_STORE : 0);
+		c->nt = value ? FWD4_V_NT : 0;
 	} else if (strcmp(key, "stats") == 0) {
 		c->stats_on = value != 0;
+	} else if (strcmp(key, "tile") == 0) { // packets per workgroup: 256 (default) or 64
+		if (value != 64 && value != 256)
+			return -EINVAL;
+		c->tile64 = value == 64 ? FWD4_V_TILE64 : 0;
 	} else if (strcmp(key, "wg_per_cu") == 0) {
 		if (value < 0 || value > 32)
 			return -EINVAL;
@@ -928,7 +934,7 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 	} else if (strcmp(key, "fib16") == 0) { // takes effect at the next commit
 		c->fib16 = value != 0;
 	} else if (strcmp(key, "occupancy") == 0) { // read-only: WGs/CU of the current variant
-		return c->occ[(c->stats_on ? FWD4_V_STATS : 0) | c->nt];
+		return c->occ[(c->stats_on ? FWD4_V_STATS : 0) | c->nt | c->tile64];
 	} else {
 		return -ENOENT;
 	}

@@ -344,7 +344,8 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 
 // Tuning knobs, for measurements (A/B in one process). Keys:
 //   "stats"     1 = per-iface counters (default; grout always counts), 0 = off
-//   "nt"        nontemporal streamed data: bit0 loads, bit1 stores (default 0)
+//   "nt"        1 = nontemporal loads / stores of the streamed data
+//   "tile"      packets per workgroup: 256 (four waves) or 64 (one wave)
 //   "wg_per_cu" 0 = one 256-packet tile per workgroup (default),
 //               N = persistent grid of N workgroups per CU
 //   "fib16"     1 = 2-byte FIB entries when slots fit 15 bits (default),

@@ -191,8 +191,9 @@ def test_kernel_timing_api(fastpath):
     q.close()
 
 
-@pytest.mark.parametrize("nt,stats,wg,fib16", [(3, 1, 0, 1), (1, 0, 6, 1), (2, 1, 4, 0), (0, 1, 0, 0)])
-def test_kernel_variants(fastpath, nt, stats, wg, fib16):
+@pytest.mark.parametrize("nt,stats,wg,fib16,tile", [(1, 1, 0, 1, 64), (1, 0, 6, 1, 256), (0, 1, 4, 0, 64),
+                                                    (0, 1, 0, 0, 256), (1, 1, 8, 1, 64)])
+def test_kernel_variants(fastpath, nt, stats, wg, fib16, tile):
     """Every tuning variant (gr_hip_tune) forwards bit-exact."""
     t, _ = SC.corpus_topology()
     fr, me, lab = SC.corpus_arrays()
@@ -204,6 +205,7 @@ def test_kernel_variants(fastpath, nt, stats, wg, fib16):
     fastpath.tune("stats", stats)
     fastpath.tune("wg_per_cu", wg)
     fastpath.tune("fib16", fib16)
+    fastpath.tune("tile", tile)
     try:
         fresh_fastpath_state(fastpath, T.config_single_route())  # force a reload (commit)
         g = run_gpu(fastpath, t, fr, me)
@@ -216,7 +218,7 @@ def test_kernel_variants(fastpath, nt, stats, wg, fib16):
         compare(o2 if stats else (o2[0], o2[1], g2[2]), g2)
         assert fastpath.fib_info(1)["dev_bytes"] == (2 if fib16 else 4) * ((1 << 24) + 256 * max(256, 1_000_010 // 500))
     finally:
-        for k, v in [("nt", 0), ("stats", 1), ("wg_per_cu", 0), ("fib16", 1)]:
+        for k, v in [("nt", 0), ("stats", 1), ("wg_per_cu", 0), ("fib16", 1), ("tile", 256)]:
             fastpath.tune(k, v)
         fresh_fastpath_state(fastpath, T.config_single_route())
 

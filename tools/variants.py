@@ -24,10 +24,11 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--batch", type=int, default=1 << 24)
     ap.add_argument("--workload", default="fullview64", choices=["fullview64", "single64"])
-    ap.add_argument("--nt", default="0,1,2,3")
+    ap.add_argument("--nt", default="0,1")
     ap.add_argument("--wg", default="0,6")
     ap.add_argument("--fib16", default="1,0")
     ap.add_argument("--stats", default="1")
+    ap.add_argument("--tile", default="256")
     args = ap.parse_args()
     import torch
 
@@ -51,12 +52,14 @@ def main():
     d_out = torch.empty_like(d_in)
     d_v = torch.empty(n * 8, dtype=torch.uint8, device=dev)
     q = fp.queue(torch.cuda.current_stream(dev).cuda_stream)
-    variants = list(itertools.product(ints(args.fib16), ints(args.stats), ints(args.nt), ints(args.wg)))
+    variants = list(itertools.product(ints(args.fib16), ints(args.stats), ints(args.nt), ints(args.wg),
+                                      ints(args.tile)))
     times = {v: [] for v in variants}
     ref = None
     for r in range(args.rounds):
         for v in variants:
-            f16, st, nt, wg = v
+            f16, st, nt, wg, tile = v
+            fp.tune("tile", tile)
             fp.tune("fib16", f16)
             fp.fib_commit(T.VRF_MAIN)  # re-uploads when the format changes
             fp.tune("stats", st)
@@ -75,7 +78,7 @@ def main():
     for v in variants:
         t = np.array(times[v])
         print(json.dumps({"workload": args.workload, "fib16": v[0], "stats": v[1], "nt": v[2],
-                          "wg_per_cu": v[3], "median_ms": round(float(np.median(t)), 4),
+                          "wg_per_cu": v[3], "tile": v[4], "median_ms": round(float(np.median(t)), 4),
                           "min_ms": round(float(t.min()), 4), "mpps": round(n / float(np.median(t)) / 1e3, 1)}),
               flush=True)
     q.close()
