@@ -30,7 +30,9 @@ struct fwd4_edges {
 #define FWD4_RX_MAC_OK 0x01 // iface_get_eth_addr() succeeds
 #define FWD4_RX_SNAT_DYN 0x02 // GR_IFACE_F_SNAT_DYNAMIC
 #define FWD4_RX_VLAN_DEMUX 0x04 // mode VRF: tagged packets look up a sub-iface
-#define FWD4_RX_FIB16 0x08 // the FIB uses 2-byte entries (bit15 = tbl8 group)
+#define FWD4_RX_FIB16 0x08 // DIR-16-8-8 FIB: tbl24 points at top[65536] (u32,
+                           // bit31 = chunk) followed by 2-byte /24 chunks;
+                           // tbl8 has 2-byte entries (bit15 = tbl8 group)
 struct fwd4_rx {
 	uint16_t id; // 0: no such iface
 	uint8_t e_in; // iface_input edge: ADMIN_DOWN, mode edge or CHAIN (eth_input)

@@ -311,9 +311,12 @@ __device__ __forceinline__ result process(const kctx &P, uint32_t (&w)[16], cons
 	uint32_t slot = 0;
 	if (rx.tbl24 != nullptr) {
 		const uint32_t ip = __builtin_bswap32(dst);
-		if (rx.flags & FWD4_RX_FIB16) { // 2-byte entries, bit15 = tbl8 group
-			const uint16_t *t24 = reinterpret_cast<const uint16_t *>(rx.tbl24);
-			uint32_t ent = t24[ip >> 8];
+		if (rx.flags & FWD4_RX_FIB16) { // DIR-16-8-8, 2-byte entries, bit15 = tbl8 group
+			uint32_t ent = rx.tbl24[ip >> 16]; // top: bit31 = chunk of 256 /24 entries
+			if (ent & 0x80000000u) {
+				const uint16_t *chunks = reinterpret_cast<const uint16_t *>(rx.tbl24 + 65536);
+				ent = chunks[(size_t)(ent & 0x7fffffffu) * 256 + ((ip >> 8) & 0xff)];
+			}
 			if (ent & 0x8000u)
 				ent = reinterpret_cast<const uint16_t *>(rx.tbl8)[(size_t)(ent & 0x7fffu) * 256 + (ip & 0xff)];
 			slot = ent;

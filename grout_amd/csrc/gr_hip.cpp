@@ -46,8 +46,14 @@ struct vrf_fib {
 	gr_fib4 *rib = nullptr;
 	uint32_t *d24 = nullptr; // 4-byte entries (fib4.h encoding)
 	uint32_t *d8 = nullptr;
-	uint16_t *d24_16 = nullptr; // 2-byte entries, used while every slot fits 15 bits
+	// DIR-16-8-8 with 2-byte entries, used while every slot fits 15 bits:
+	// top[65536] (u32: bit31 = chunk index, else the /16's entry), then
+	// chunks of 256 2-byte /24 entries for the non-uniform /16s only.
+	uint32_t *d16 = nullptr; // top, followed by the chunks
 	uint16_t *d8_16 = nullptr;
+	std::vector<int32_t> chunk_of; // per /16: chunk index or -1
+	std::vector<uint32_t> chunk_free; // free chunk indexes (stack)
+	uint32_t n_chunks = 0; // chunks in use
 	bool fmt16 = false; // format on the device
 	uint32_t max_slot = 0; // highest nexthop slot ever routed (never decreases)
 	uint32_t num_tbl8 = 0;
@@ -158,7 +164,7 @@ static fwd4_rx make_rx(const gr_hip_ctx *c, uint32_t id) {
 	    && c->vrfs[i->vrf_id].uploaded) {
 		const vrf_fib &v = c->vrfs[i->vrf_id];
 		if (v.fmt16) {
-			r.tbl24 = reinterpret_cast<const uint32_t *>(v.d24_16);
+			r.tbl24 = v.d16;
 			r.tbl8 = reinterpret_cast<const uint32_t *>(v.d8_16);
 			r.flags |= FWD4_RX_FIB16;
 		} else {
@@ -410,7 +416,7 @@ extern "C" int gr_hip_fini(gr_hip_ctx_t *c) {
 		gr_fib4_free(v.rib);
 		hipFree(v.d24);
 		hipFree(v.d8);
-		hipFree(v.d24_16);
+		hipFree(v.d16);
 		hipFree(v.d8_16);
 	}
 	hipFree(c->d_rx);
@@ -646,7 +652,7 @@ extern "C" int gr_hip_fib4_destroy(gr_hip_ctx_t *c, uint16_t vrf) {
 	v.rib = rib;
 	hipFree(v.d24);
 	hipFree(v.d8);
-	hipFree(v.d24_16);
+	hipFree(v.d16);
 	hipFree(v.d8_16);
 	gr_fib4_free(v.rib);
 	v = vrf_fib {};
@@ -739,19 +745,64 @@ extern "C" int gr_hip_fib4_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 	const uint32_t *t24 = gr_fib4_tbl24(v.rib);
 	const uint32_t *t8 = gr_fib4_tbl8(v.rib);
 	if (want16) {
-		if (v.d24_16 == nullptr) {
+		const size_t top_n = 65536, chunk_n = 256;
+		if (v.d16 == nullptr) {
 			HCK(hipStreamSynchronize(c->ctl));
-			HCK(hipMalloc(&v.d24_16, sizeof(uint16_t) * GR_FIB4_TBL24_ENTRIES));
+			// top + the worst case of one chunk per /16
+			HCK(hipMalloc(&v.d16, sizeof(uint32_t) * top_n + sizeof(uint16_t) * chunk_n * top_n));
 			HCK(hipMalloc(&v.d8_16, sizeof(uint16_t) * 256 * (size_t)v.num_tbl8));
 		}
-		std::vector<uint16_t> h24(hi > lo ? hi - lo : 0), h8((size_t)v.num_tbl8 * 256);
-		for (uint32_t i = lo; i < hi; i++)
-			h24[i - lo] = to16(t24[i]);
+		if (full || v.chunk_of.empty()) {
+			v.chunk_of.assign(top_n, -1);
+			v.chunk_free.clear();
+			for (uint32_t k = 0; k < top_n; k++)
+				v.chunk_free.push_back((uint32_t)(top_n - 1 - k));
+			v.n_chunks = 0;
+		}
+		uint16_t *chunks_dev = reinterpret_cast<uint16_t *>(v.d16 + top_n);
+		// rebuild the dirty /16s
+		uint32_t k_lo = lo >> 8, k_hi = (hi + 255) >> 8;
+		std::vector<uint32_t> top(k_hi > k_lo ? k_hi - k_lo : 0);
+		std::vector<uint16_t> cbuf;
+		std::vector<uint32_t> cidx;
+		for (uint32_t k = k_lo; k < k_hi; k++) {
+			const uint32_t *e = t24 + (size_t)k * 256;
+			bool uniform = !(e[0] & GR_FIB4_EXT);
+			for (uint32_t j = 1; uniform && j < 256; j++)
+				uniform = e[j] == e[0];
+			if (uniform) {
+				top[k - k_lo] = to16(e[0]);
+				if (v.chunk_of[k] >= 0) {
+					v.chunk_free.push_back((uint32_t)v.chunk_of[k]);
+					v.chunk_of[k] = -1;
+					v.n_chunks--;
+				}
+				continue;
+			}
+			if (v.chunk_of[k] < 0) {
+				v.chunk_of[k] = (int32_t)v.chunk_free.back();
+				v.chunk_free.pop_back();
+				v.n_chunks++;
+			}
+			top[k - k_lo] = 0x80000000u | (uint32_t)v.chunk_of[k];
+			cidx.push_back((uint32_t)v.chunk_of[k]);
+			for (uint32_t j = 0; j < 256; j++)
+				cbuf.push_back(to16(e[j]));
+		}
+		std::vector<uint16_t> h8((size_t)v.num_tbl8 * 256);
 		for (uint32_t g : gs)
 			for (uint32_t k = 0; k < 256; k++)
 				h8[(size_t)g * 256 + k] = to16(t8[(size_t)g * 256 + k]);
-		if (hi > lo)
-			r = h2d(c, v.d24_16 + lo, h24.data(), (size_t)(hi - lo) * sizeof(uint16_t));
+		if (k_hi > k_lo)
+			r = h2d(c, v.d16 + k_lo, top.data(), top.size() * sizeof(uint32_t));
+		for (size_t i = 0; i < cidx.size() && r == 0;) { // runs of consecutive chunks
+			size_t j = i + 1;
+			while (j < cidx.size() && cidx[j] == cidx[j - 1] + 1)
+				j++;
+			r = h2d(c, chunks_dev + (size_t)cidx[i] * chunk_n, cbuf.data() + i * chunk_n,
+				(j - i) * chunk_n * sizeof(uint16_t));
+			i = j;
+		}
 		if (r == 0)
 			r = upload_groups<uint16_t>(c, v.d8_16, h8.data(), gs);
 		if (r == 0)
@@ -802,9 +853,9 @@ extern "C" int gr_hip_fib4_info(gr_hip_ctx_t *c, uint16_t vrf, uint32_t *n_route
 		*n_routes = gr_fib4_n_routes(v.rib);
 	if (tbl8_used)
 		*tbl8_used = gr_fib4_tbl8_used(v.rib);
-	if (bytes)
-		*bytes = (v.fmt16 ? sizeof(uint16_t) : sizeof(uint32_t))
-			* ((uint64_t)GR_FIB4_TBL24_ENTRIES + 256ull * v.num_tbl8);
+	if (bytes) // device bytes a lookup can touch
+		*bytes = v.fmt16 ? 4ull * 65536 + 512ull * v.n_chunks + 512ull * v.num_tbl8
+				 : 4ull * GR_FIB4_TBL24_ENTRIES + 1024ull * v.num_tbl8;
 	return 0;
 }
 
