@@ -115,44 +115,53 @@ struct stat_slot {
 	unsigned long long bytes;
 };
 
-// One lane (the wave leader of a key) adds a wave's contribution.
+// One lane (the wave leader of a key) adds a wave's contribution to the
+// workgroup's LDS slots: direct-mapped on (iface, kind), claimed once with a
+// compare-and-swap, then fire-and-forget LDS atomics. A slot already owned
+// by another key (two ifaces 32 apart) sends the update to the global shard.
 __device__ __forceinline__ void slot_add(stat_slot *slots, const kctx &P, uint32_t key, uint32_t pkts, uint32_t bytes) {
-	uint32_t h = (key * 0x9e3779b1u) >> 27; // 32 slots
-#pragma unroll 1
-	for (uint32_t i = 0; i < FWD4_STAT_SLOTS; i++) {
-		uint32_t s = (h + i) & (FWD4_STAT_SLOTS - 1);
-		uint32_t old = atomicCAS(&slots[s].key, 0u, key);
-		if (old == 0 || old == key) {
-			atomicAdd(&slots[s].pkts, pkts);
-			atomicAdd(&slots[s].bytes, (unsigned long long)bytes);
-			return;
-		}
+	const uint32_t kind = (key - 1) >> 16, iface = (key - 1) & 0xffff;
+	stat_slot *sl = &slots[(iface * 2 + kind) & (FWD4_STAT_SLOTS - 1)];
+	uint32_t cur = sl->key;
+	if (cur != key && cur == 0)
+		cur = atomicCAS(&sl->key, 0u, key) == 0 ? key : sl->key;
+	if (cur == key) {
+		atomicAdd(&sl->pkts, pkts);
+		atomicAdd(&sl->bytes, (unsigned long long)bytes);
+		return;
 	}
-	// table full: straight to the global shard
-	uint32_t kind = (key - 1) >> 16, iface = (key - 1) & 0xffff;
 	gr_hip_iface_stats *st = P.stats + (size_t)(blockIdx.x % FWD4_STAT_SHARDS) * P.max_ifaces + iface;
 	unsigned long long *c = reinterpret_cast<unsigned long long *>(kind ? &st->tx_packets : &st->rx_packets);
 	atomicAdd(c, (unsigned long long)pkts);
 	atomicAdd(c + 1, (unsigned long long)bytes);
 }
 
+// Sum of v over the wave with DPP (no LDS): quad, half-row and row steps,
+// then row broadcasts; lane 63 ends with the total.
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+	v += __builtin_amdgcn_update_dpp(0u, v, 0xb1, 0xf, 0xf, false); // quad_perm [1,0,3,2]
+	v += __builtin_amdgcn_update_dpp(0u, v, 0x4e, 0xf, 0xf, false); // quad_perm [2,3,0,1]
+	v += __builtin_amdgcn_update_dpp(0u, v, 0x141, 0xf, 0xf, false); // row_half_mirror
+	v += __builtin_amdgcn_update_dpp(0u, v, 0x140, 0xf, 0xf, false); // row_mirror
+	v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false); // row_bcast:15
+	v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false); // row_bcast:31
+	return __builtin_amdgcn_readlane(v, 63);
+}
+
 // Wave-aggregate one counter key per lane (0 = nothing) into the LDS slots.
+// Every lane of the wave must call it (converged).
 __device__ __forceinline__ void wave_count(stat_slot *slots, const kctx &P, uint32_t key, uint32_t len) {
-	const int lane = threadIdx.x & 63;
 	for (;;) {
 		unsigned long long act = __ballot(key != 0);
 		if (act == 0)
 			break;
-		int lead = __ffsll((long long)act) - 1;
-		uint32_t k = __shfl(key, lead, 64);
-		bool same = key == k;
-		unsigned long long sm = __ballot(same);
-		uint32_t b = same ? len : 0;
-#pragma unroll
-		for (int o = 32; o > 0; o >>= 1)
-			b += __shfl_xor(b, o, 64);
-		if (lane == lead)
-			slot_add(slots, P, k, (uint32_t)__popcll(sm), b);
+		const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1;
+		const uint32_t k = __builtin_amdgcn_readlane(key, lead);
+		const bool same = key == k;
+		const uint32_t cnt = (uint32_t)__popcll(__ballot(same));
+		const uint32_t b = wave_sum(same ? len : 0u);
+		if ((threadIdx.x & 63) == lead)
+			slot_add(slots, P, k, cnt, b);
 		if (same)
 			key = 0;
 	}
@@ -507,13 +516,9 @@ __global__ void __launch_bounds__(TILE) gr_fwd4_kernel(const fwd4_params A) {
 			else
 				*vp = vv;
 		}
-		if (STATS) { // every lane of the wave takes part in the ballots
-			uint32_t len = m.pkt_len;
-			wave_count(slots, P, r.rx_if ? r.rx_if + 1 : 0, len);
-			wave_count(slots, P, r.rx_par ? r.rx_par + 1 : 0, len);
-			wave_count(slots, P, r.tx_if ? (r.tx_if | 0x10000u) + 1 : 0, len);
-			wave_count(slots, P, r.tx_par ? (r.tx_par | 0x10000u) + 1 : 0, len);
-		}
+		// counter keys, packed: rx | rx_par << 16, tx | tx_par << 16
+		const uint32_t rxk = r.rx_if | (r.rx_par << 16), txk = r.tx_if | (r.tx_par << 16);
+		const uint32_t len = m.pkt_len;
 		__syncthreads();
 #pragma unroll
 		for (uint32_t k = 0; k < 4; k++) {
@@ -522,6 +527,12 @@ __global__ void __launch_bounds__(TILE) gr_fwd4_kernel(const fwd4_params A) {
 			if (p < cnt)
 				st16<NT>(A.out + (size_t)(base + p) * A.out_stride + part * 16,
 					 *reinterpret_cast<const u4v *>(&lines[p * FWD4_ROW + part * 16]));
+		}
+		if (STATS) { // every lane of the wave takes part in the ballots
+			wave_count(slots, P, (rxk & 0xffff) ? (rxk & 0xffff) + 1 : 0, len);
+			wave_count(slots, P, (rxk >> 16) ? (rxk >> 16) + 1 : 0, len);
+			wave_count(slots, P, (txk & 0xffff) ? ((txk & 0xffff) | 0x10000u) + 1 : 0, len);
+			wave_count(slots, P, (txk >> 16) ? ((txk >> 16) | 0x10000u) + 1 : 0, len);
 		}
 		if (tile + gridDim.x < n_tiles)
 			__syncthreads(); // the next tile reuses the LDS rows
