@@ -48,25 +48,18 @@ def log(*a):
 def main():
     args = parse()
     import torch
-    import torch.distributed as dist
 
     from grout_amd import abi
     from grout_amd import synth as S
     from grout_amd import topology as T
     from grout_amd.fwd import FastPath
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    from grout_amd.replicas import Replicas
+
+    rep = Replicas("nccl")
+    world, rank, local = rep.world, rep.rank, rep.local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
 
     # ---- control plane: topology + FIB replica on this GPU
     t0 = time.time()
@@ -86,7 +79,7 @@ def main():
 
     # ---- synthetic RX stream of this GPU (seed 0x67721000 + g)
     n = args.batch
-    seed = S.SEED_GPU_BASE + rank
+    seed = rep.seed()
     imix = args.workload == "imix"
     t0 = time.time()
     frames, meta = S.stream(n, seed, routes=routes, dst_range=dst_range, imix=imix, lines_only=imix)
@@ -105,24 +98,20 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    barrier()
+    rep.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    barrier()
+    rep.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms, kcount = q.kernel_ms(args.steps)
-    tmax = elapsed
-    if world > 1:
-        x = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(x, op=dist.ReduceOp.MAX)
-        tmax = float(x.item())
+    tmax = rep.max_over_ranks(elapsed)
 
     edges = torch.bincount(d_v.view(n, 8)[:, 0].long(), minlength=abi.E_COUNT).cpu().numpy()
     fwd_frac = float(edges[abi.EDGE["port_output"]]) / n
-    value = world * n * args.steps / tmax / 1e6
+    value = rep.aggregate_mpps(n, args.steps, tmax)
     avg_kernel_s = kern_ms / max(kcount, 1) / 1e3
     achieved = n * B_PKT / avg_kernel_s / 1e9
 
@@ -223,8 +212,7 @@ def main():
         print(json.dumps(result), flush=True)
     q.close()
     fp.close()
-    if world > 1:
-        dist.destroy_process_group()
+    rep.close()
 
 
 if __name__ == "__main__":
