@@ -1,0 +1,340 @@
+// SPDX-License-Identifier: BSD-3-Clause
+//
+// fwd4_chain.h -- the node chain split at its dependent loads, for kernels
+// that keep a tile's header lines in an LDS image (fwd4_pipe.hip,
+// fwd4_ring.hip): pipe_head (iface_input .. ip_input checks), pipe_fib
+// (fib4_lookup), pipe_tail (adjacency .. iface_output, rewriting the row).
+// Node citations as process() in fwd4_kernel.hip. Not a public header.
+//
+// LDS image of a 64-packet tile: row r (64 bytes) = packet r, its 16-byte
+// chunk j at slot j ^ ((r >> 2) & 3) -- conflict-free both for the
+// 4-lanes-per-row coalesced fill/drain and for one-row-per-lane reads.
+#pragma once
+
+#include "fwd4_dev.h"
+
+// Kernel-wide view of the tables (read once per wave from fwd4_tables).
+__device__ __forceinline__ kctx make_kctx(const fwd4_params &A, const fwd4_edges *edges) {
+	const fwd4_tables *T = A.T;
+	kctx P;
+	P.rx = T->rx;
+	P.adj = T->adj;
+	P.nhf = T->nhf;
+	P.reta = T->reta;
+	P.vlan_keys = T->vlan_keys;
+	P.vlan_vals = T->vlan_vals;
+	P.reta_cap = T->reta_cap;
+	P.vlan_mask = T->vlan_mask;
+	P.max_ifaces = T->max_ifaces;
+	P.max_nh = T->max_nh;
+	P.readable = A.readable;
+	P.edges = edges;
+	P.stats = A.stats;
+	P.ip4_edge = ip4_edge_of(*edges);
+	return P;
+}
+
+// Byte offset of 16-byte chunk j of row r in a wave's LDS image.
+__device__ __forceinline__ uint32_t row_off(uint32_t r, uint32_t j) {
+	return r * 64 + ((j ^ ((r >> 2) & 3)) << 4);
+}
+
+__device__ __forceinline__ u4v lds_get(const uint8_t *R, uint32_t r, uint32_t j) {
+	return *reinterpret_cast<const u4v *>(R + row_off(r, j));
+}
+
+__device__ __forceinline__ void lds_put(uint8_t *R, uint32_t r, uint32_t j, u4v v) {
+	*reinterpret_cast<u4v *>(R + row_off(r, j)) = v;
+}
+
+__device__ __forceinline__ void compiler_fence() {
+	asm volatile("" ::: "memory");
+}
+
+// RX view of a wave-uniform iface id through the scalar cache.
+__device__ __forceinline__ rxv load_rx_scalar(const kctx &P, uint32_t id) {
+	rxv r;
+	r.id = 0;
+	if (id == 0 || id >= P.max_ifaces)
+		return r;
+	typedef uint32_t u8s __attribute__((ext_vector_type(8)));
+	u8s v;
+	const fwd4_rx *p = P.rx + id;
+	asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+	return unpack_rx(uint4{v[0], v[1], v[2], v[3]}, uint4{v[4], v[5], v[6], v[7]});
+}
+
+// iface_input -> eth_input -> ip_input up to the FIB lookup, for the packet
+// in row `row` of R. Returns false when the packet left the chain (r.edge
+// set); otherwise dst (network order as stored) and data_len are set.
+__device__ __forceinline__ bool pipe_head(const kctx &P, const uint8_t *R, uint32_t row, const gr_hip_pkt_meta &m,
+					  rxv &rx, result &r, uint32_t &dst, uint32_t &data_len, const uint8_t *frame) {
+	// ---- iface_input (iface_input.c:52-112)
+	if (rx.id == 0)
+		return false; // PUNT
+	const uint32_t vlan = m.vlan_ck & 0xfff;
+	if (vlan != 0 && (rx.flags & FWD4_RX_VLAN_DEMUX)) { // :74-86
+		rxv v = load_rx(P, vlan_lookup(P, rx.id, vlan));
+		if (v.id == 0) {
+			r.edge = GR_HIP_E_IFACE_INPUT_UNKNOWN_VLAN;
+			return false;
+		}
+		rx = v;
+	}
+	r.iface = rx.id;
+	if (rx.e_in != CHAIN) { // admin down :88-91, or the mode edge :97
+		r.edge = rx.e_in;
+		if (rx.e_in != GR_HIP_E_IFACE_INPUT_ADMIN_DOWN) {
+			r.rx_if = rx.id;
+			r.rx_par = m.iface != rx.id ? m.iface : 0;
+		}
+		return false;
+	}
+	r.rx_if = rx.id; // IFACE_STATS_INC :93-95
+	r.rx_par = m.iface != rx.id ? m.iface : 0;
+
+	// ---- eth_input (eth_input.c:35-88)
+	const u4v c0 = lds_get(R, row, 0);
+	const uint32_t type_raw = lo16(c0.w);
+	const uint32_t type = bswap16(type_raw);
+	if (type < 1536 || type == 0x8870) { // snap.h:11-12
+		r.edge = GR_HIP_E_SNAP_INPUT;
+		return false;
+	}
+	if (!(rx.flags & FWD4_RX_MAC_OK)) {
+		r.edge = GR_HIP_E_ETH_INPUT_INVALID_IFACE;
+		return false;
+	}
+	if (c0.x & 1) {
+		bool bc = c0.x == 0xffffffffu && lo16(c0.y) == 0xffff;
+		r.domain = bc ? GR_HIP_ETH_DOMAIN_BROADCAST : GR_HIP_ETH_DOMAIN_MULTICAST;
+	} else if (c0.x == rx.mac_lo && lo16(c0.y) == rx.mac_hi) {
+		r.domain = GR_HIP_ETH_DOMAIN_LOCAL;
+	} else {
+		r.domain = GR_HIP_ETH_DOMAIN_OTHER;
+	}
+	data_len = m.pkt_len >= 14 ? m.pkt_len - 14u : m.pkt_len;
+	const uint32_t e = eth_type_edge(P, type_raw);
+	if (e != CHAIN) {
+		r.edge = e;
+		return false;
+	}
+
+	// ---- ip_input (ip_input.c:58-187)
+	const uint32_t vihl = (c0.w >> 16) & 0xff;
+	const uint32_t ihl = vihl & 0xf;
+	if (data_len < 20) { // (1)
+		r.edge = GR_HIP_E_IP_INPUT_BAD_LENGTH;
+		return false;
+	}
+	const u4v c1 = lds_get(R, row, 1);
+	const u4v c2 = lds_get(R, row, 2);
+	const uint32_t ck = (m.vlan_ck >> 12) & 3;
+	if (ck == GR_HIP_CKSUM_UNKNOWN) { // (2) rte_ipv4_cksum over ihl*4 bytes
+		const uint32_t hl = ihl * 4;
+		if (14 + hl > P.readable) {
+			r.edge = GR_HIP_E_PUNT;
+			r.rx_if = r.rx_par = 0;
+			r.domain = 0;
+			r.iface = m.iface;
+			return false;
+		}
+		uint32_t sum = 0;
+		if (ihl != 0) {
+			const u4v c3 = lds_get(R, row, 3);
+			const uint32_t w[12] = {c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+			sum = hi16(c0.w);
+#pragma unroll
+			for (uint32_t j = 4; j < 16; j++) {
+				uint32_t v = w[j - 4];
+				uint32_t full = lo16(v) + hi16(v);
+				sum += (j <= 2 + ihl) ? full : (j == 3 + ihl ? lo16(v) : 0u);
+			}
+			if (ihl > 12) { // options reach past the line: bytes 64..73
+				uint4 x = gld4(frame + 64);
+				uint32_t xw[3] = {x.x, x.y, x.z};
+#pragma unroll
+				for (uint32_t j = 16; j < 19; j++) {
+					uint32_t v = xw[j - 16];
+					uint32_t full = lo16(v) + hi16(v);
+					sum += (j <= 2 + ihl) ? full : (j == 3 + ihl ? lo16(v) : 0u);
+				}
+			}
+		}
+		sum = (sum & 0xffff) + (sum >> 16);
+		sum = (sum & 0xffff) + (sum >> 16);
+		if (sum != 0xffff) {
+			r.edge = GR_HIP_E_IP_INPUT_BAD_CHECKSUM;
+			return false;
+		}
+	} else if (ck == GR_HIP_CKSUM_BAD) {
+		r.edge = GR_HIP_E_IP_INPUT_BAD_CHECKSUM;
+		return false;
+	}
+	dst = hi16(c1.w) | (lo16(c2.x) << 16);
+	if (dst == 0) {
+		r.edge = GR_HIP_E_IP_INPUT_BAD_ADDRESS;
+		return false;
+	}
+	if ((vihl >> 4) != 4) { // (3)
+		r.edge = GR_HIP_E_IP_INPUT_BAD_VERSION;
+		return false;
+	}
+	if (ihl * 4 < 20) { // (4)
+		r.edge = GR_HIP_E_IP_INPUT_BAD_LENGTH;
+		return false;
+	}
+	if (bswap16(lo16(c1.x)) < 20) { // (5)
+		r.edge = GR_HIP_E_IP_INPUT_BAD_LENGTH;
+		return false;
+	}
+	if (r.domain != GR_HIP_ETH_DOMAIN_LOCAL) {
+		bool mc = r.domain == GR_HIP_ETH_DOMAIN_BROADCAST || r.domain == GR_HIP_ETH_DOMAIN_MULTICAST;
+		r.edge = mc ? GR_HIP_E_IP_INPUT_LOCAL : GR_HIP_E_IP_INPUT_OTHER_HOST;
+		return false;
+	}
+	const uint32_t d0 = dst & 0xff;
+	if (dst == 0xffffffffu || (d0 >= 224 && d0 <= 239)) {
+		r.edge = GR_HIP_E_IP_INPUT_LOCAL;
+		return false;
+	}
+	return true;
+}
+
+// fib4_lookup (route.c:147-167) in the iface's VRF table.
+__device__ __forceinline__ uint32_t pipe_fib(const rxv &rx, uint32_t dst) {
+	if (rx.tbl24 == nullptr)
+		return 0;
+	const uint32_t ip = __builtin_bswap32(dst);
+	if (rx.flags & FWD4_RX_FIB16) {
+		uint32_t ent = gld(rx.tbl24 + (ip >> 16));
+		if (ent & 0x80000000u) {
+			const uint16_t *chunks = reinterpret_cast<const uint16_t *>(rx.tbl24 + 65536);
+			ent = gld(chunks + (size_t)(ent & 0x7fffffffu) * 256 + ((ip >> 8) & 0xff));
+		}
+		if (ent & 0x8000u)
+			ent = gld(reinterpret_cast<const uint16_t *>(rx.tbl8) + (size_t)(ent & 0x7fffu) * 256 + (ip & 0xff));
+		return ent;
+	}
+	uint32_t ent = gld(rx.tbl24 + (ip >> 8));
+	if (ent & 0x80000000u)
+		ent = gld(rx.tbl8 + (size_t)(ent & 0x7fffffffu) * 256 + (ip & 0xff));
+	return ent;
+}
+
+// From the adjacency (its first 32 bytes in a, b) to the verdict:
+// group resolution, ip_input's nexthop checks, ip_forward, ip_output,
+// eth_output, iface_output. Rewrites row `row` of R.
+__device__ __forceinline__ void pipe_tail(const kctx &P, uint8_t *R, uint32_t row, const gr_hip_pkt_meta &m,
+					  uint32_t rx_flags, result &r, uint32_t dst, uint32_t data_len, uint32_t slot,
+					  uint4 a, uint4 b) {
+	adjv A = unpack_adj(a, b, uint4{0, 0, 0, 0});
+	if (A.type == GR_HIP_NH_T_GROUP) { // nexthop_group_get_nh, nexthop.h:89-96
+		const uint4 c = gld4(reinterpret_cast<const uint4 *>(P.adj + slot) + 2);
+		const uint32_t n_members = c.x & 0xffff, reta_size = c.x >> 16;
+		if (n_members == 1) {
+			slot = c.z;
+		} else if (n_members == 0) {
+			slot = 0;
+		} else {
+			uint32_t i = c.y + (m.rss & (reta_size - 1));
+			slot = i < P.reta_cap ? gld(P.reta + i) : 0;
+		}
+		if (slot == 0 || slot > P.max_nh) {
+			r.edge = GR_HIP_E_IP_ERROR_DEST_UNREACH;
+			return;
+		}
+		A = load_adj(P, slot);
+	}
+	r.nh = slot;
+	if (A.e_in != CHAIN) {
+		r.edge = A.e_in;
+		return;
+	}
+	if ((A.flags & FWD4_ADJ_LOCAL) && dst == A.ipv4) {
+		r.edge = (rx_flags & FWD4_RX_SNAT_DYN) ? GR_HIP_E_IP_INPUT_LOCAL_CT : GR_HIP_E_IP_INPUT_LOCAL;
+		return;
+	}
+
+	// ---- ip_forward (ip_forward.c:21-33)
+	u4v c1 = lds_get(R, row, 1); // bytes 16-31: w5 = c1.y (ttl), w6 = c1.z (cksum)
+	const uint32_t ttl = (c1.y >> 16) & 0xff;
+	if (ttl <= 1) {
+		r.edge = GR_HIP_E_IP_ERROR_TTL_EXCEEDED;
+		return;
+	}
+	c1.y = (c1.y & 0xff00ffffu) | ((ttl - 1) << 16);
+	uint32_t ck = lo16(c1.z) + 1;
+	ck += ck >= 0xffff;
+	c1.z = (c1.z & 0xffff0000u) | (ck & 0xffff);
+	lds_put(R, row, 1, c1);
+
+	// ---- ip_output (ip_output.c:135-213)
+	if (A.e_pre != CHAIN) {
+		r.edge = A.e_pre;
+		return;
+	}
+	r.iface = A.oif;
+	if (data_len > A.mtu) {
+		r.edge = (c1.y & 0x40) ? GR_HIP_E_IP_ERROR_FRAG_NEEDED : GR_HIP_E_IP_FRAGMENT;
+		return;
+	}
+	if (A.e_mid != CHAIN) {
+		r.edge = A.e_mid;
+		return;
+	}
+	if ((A.flags & FWD4_ADJ_LINK) && dst != A.ipv4) {
+		r.edge = GR_HIP_E_IP_HOLD;
+		return;
+	}
+
+	// ---- eth_output (eth_output.c:297-316) + iface_output (iface_output.c:213-246)
+	u4v c0 = lds_get(R, row, 0);
+	c0.x = A.dmac_lo;
+	c0.y = (c0.y & 0xffff0000u) | A.dmac_hi;
+	r.edge = A.e_post;
+	if (A.e_post != GR_HIP_E_ETH_OUTPUT_NO_MAC) {
+		c0.y = lo16(c0.y) | (A.smac_lo << 16);
+		c0.z = (A.smac_lo >> 16) | (A.smac_hi << 16);
+		c0.w = (c0.w & 0xffff0000u) | 0x0008u;
+		r.iface = A.post_iface;
+		r.tx_if = A.tx_if;
+		r.tx_par = A.tx_par;
+	}
+	lds_put(R, row, 0, c0);
+}
+
+
+// The plain forward of a fast adjacency f (fwd4_nhf as 4 words): the same
+// steps and results as pipe_tail for such a nexthop -- ip_forward
+// (ip_forward.c:21-33), the MTU/DF check (ip_output.c:159-166), eth_output
+// (eth_output.c:297-316) and iface_output to port_output.
+__device__ __forceinline__ void fast_tail(uint8_t *R, uint32_t row, result &r, uint32_t data_len, uint32_t slot,
+					  uint4 f) {
+	r.nh = slot;
+	u4v c1 = lds_get(R, row, 1);
+	const uint32_t ttl = (c1.y >> 16) & 0xff;
+	if (ttl <= 1) {
+		r.edge = GR_HIP_E_IP_ERROR_TTL_EXCEEDED;
+		return;
+	}
+	c1.y = (c1.y & 0xff00ffffu) | ((ttl - 1) << 16);
+	uint32_t ck = lo16(c1.z) + 1;
+	ck += ck >= 0xffff;
+	c1.z = (c1.z & 0xffff0000u) | (ck & 0xffff);
+	lds_put(R, row, 1, c1);
+	const uint32_t oif = f.y >> 16;
+	r.iface = oif;
+	if (data_len > (f.w >> 16)) {
+		r.edge = (c1.y & 0x40) ? GR_HIP_E_IP_ERROR_FRAG_NEEDED : GR_HIP_E_IP_FRAGMENT;
+		return;
+	}
+	u4v c0 = lds_get(R, row, 0);
+	c0.x = f.x;
+	c0.y = (f.y & 0xffff) | (f.z << 16);
+	c0.z = (f.z >> 16) | (f.w << 16);
+	c0.w = (c0.w & 0xffff0000u) | 0x0008u;
+	lds_put(R, row, 0, c0);
+	r.edge = GR_HIP_E_PORT_OUTPUT;
+	r.tx_if = oif;
+}

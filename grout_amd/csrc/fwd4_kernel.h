@@ -71,11 +71,23 @@ struct fwd4_adj {
 	uint32_t _pad[5];
 };
 
+// Fast adjacency, 16 bytes: a nexthop whose packets take the plain forward
+// (L3, no LOCAL/LINK flag, ip_output/eth_output/iface_output all chain to
+// port_output of a port oif: post_iface = tx iface = oif, no parent) needs
+// only its MACs, oif and MTU. mtu == 0: not plain, read the fwd4_adj.
+struct fwd4_nhf {
+	uint8_t dmac[6];
+	uint16_t oif;
+	uint8_t smac[6];
+	uint16_t mtu;
+};
+
 // Device-resident per-context tables (updated by the control plane under
 // quiesce, read by every launch through one pointer).
 struct fwd4_tables {
 	const struct fwd4_rx *rx; // [max_ifaces]
 	const struct fwd4_adj *adj; // [max_nh + 1]
+	const struct fwd4_nhf *nhf; // [max_nh + 1]
 	const uint32_t *reta;
 	const uint32_t *vlan_keys; // (parent << 16 | vlan_id) + 1, 0 = empty
 	const uint16_t *vlan_vals;
@@ -98,6 +110,7 @@ struct fwd4_params {
 	uint32_t in_stride;
 	uint32_t out_stride;
 	uint32_t readable; // frame bytes present per packet (64 or in_stride)
+	uint32_t nhf_lds; // fwd4_ring.hip: fast adjacencies 1..nhf_lds staged in LDS
 };
 
 // Kernel variants (bit mask, gr_hip_tune): counters, nontemporal loads and

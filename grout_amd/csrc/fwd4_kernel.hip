@@ -15,172 +15,7 @@
 // (ballot), per workgroup (LDS slot table) and flushed once per workgroup to
 // a sharded global table. The grid is persistent (<= 8 workgroups per CU) and
 // strides over tiles. No MFMA: this is HBM-bound integer work.
-#include <hip/hip_runtime.h>
-
-#include "fwd4_kernel.h"
-
-#define CHAIN GR_HIP_EDGE_CHAIN
-
-// What process() reads: table pointers (loaded once per workgroup from the
-// device-resident fwd4_tables) and the ether type table, copied into LDS.
-struct kctx {
-	const fwd4_rx *rx;
-	const fwd4_adj *adj;
-	const uint32_t *reta;
-	const uint32_t *vlan_keys;
-	const uint16_t *vlan_vals;
-	uint32_t reta_cap, vlan_mask, max_ifaces, max_nh, readable;
-	const fwd4_edges *edges; // LDS copy
-	gr_hip_iface_stats *stats;
-};
-
-struct rxv {
-	uint32_t id, e_in, flags, mac_lo, mac_hi;
-	const uint32_t *tbl24, *tbl8;
-};
-
-// The RX view of an iface (iface_from_id, iface.c:459-466 + get_fib).
-__device__ __forceinline__ rxv load_rx(const kctx &P, uint32_t id) {
-	rxv r;
-	r.id = 0;
-	if (id == 0 || id >= P.max_ifaces)
-		return r;
-	const uint4 *p = reinterpret_cast<const uint4 *>(P.rx + id);
-	uint4 a = p[0];
-	uint4 b = p[1];
-	r.id = a.x & 0xffff;
-	r.e_in = (a.x >> 16) & 0xff;
-	r.flags = a.x >> 24;
-	r.mac_lo = a.y;
-	r.mac_hi = a.z & 0xffff;
-	r.tbl24 = reinterpret_cast<const uint32_t *>(((uint64_t)b.y << 32) | b.x);
-	r.tbl8 = reinterpret_cast<const uint32_t *>(((uint64_t)b.w << 32) | b.z);
-	return r;
-}
-
-struct adjv {
-	uint32_t type, e_in, flags, e_pre, e_mid, e_post, oif, mtu, post_iface, ipv4, tx_if, tx_par;
-	uint32_t dmac_lo, dmac_hi, smac_lo, smac_hi; // bytes 0-3 / 4-5
-	uint32_t n_members, reta_size, reta_off, single;
-};
-
-__device__ __forceinline__ adjv load_adj(const kctx &P, uint32_t slot) {
-	const uint4 *p = reinterpret_cast<const uint4 *>(P.adj + slot);
-	uint4 a = p[0], b = p[1], c = p[2];
-	adjv r;
-	r.type = a.x & 0xff;
-	r.e_in = (a.x >> 8) & 0xff;
-	r.flags = (a.x >> 16) & 0xff;
-	r.e_pre = a.x >> 24;
-	r.e_mid = a.y & 0xff;
-	r.e_post = (a.y >> 8) & 0xff;
-	r.oif = a.y >> 16;
-	r.mtu = a.z & 0xffff;
-	r.post_iface = a.z >> 16;
-	r.ipv4 = a.w;
-	r.tx_if = b.x & 0xffff;
-	r.tx_par = b.x >> 16;
-	r.dmac_lo = b.y; // bytes 20-23
-	r.dmac_hi = b.z & 0xffff; // 24-25
-	r.smac_lo = (b.z >> 16) | (b.w << 16); // 26-29
-	r.smac_hi = b.w >> 16; // 30-31
-	r.n_members = c.x & 0xffff;
-	r.reta_size = c.x >> 16;
-	r.reta_off = c.y;
-	r.single = c.z;
-	return r;
-}
-
-// VLAN sub-interface demux, vlan_get_iface (vlan.c:27-34): open addressing
-// on (parent << 16 | vlan) + 1.
-__device__ __forceinline__ uint32_t vlan_lookup(const kctx &P, uint32_t parent, uint32_t vid) {
-	if (P.vlan_keys == nullptr)
-		return 0;
-	uint32_t key = ((parent << 16) | vid) + 1;
-	uint32_t h = (key * 0x9e3779b1u) & P.vlan_mask;
-	for (uint32_t i = 0; i <= P.vlan_mask; i++) {
-		uint32_t k = P.vlan_keys[h];
-		if (k == key)
-			return P.vlan_vals[h];
-		if (k == 0)
-			return 0;
-		h = (h + 1) & P.vlan_mask;
-	}
-	return 0;
-}
-
-struct stat_slot {
-	uint32_t key; // ((kind << 16) | iface) + 1, 0 = free
-	uint32_t pkts;
-	unsigned long long bytes;
-};
-
-// One lane (the wave leader of a key) adds a wave's contribution to the
-// workgroup's LDS slots: direct-mapped on (iface, kind), claimed once with a
-// compare-and-swap, then fire-and-forget LDS atomics. A slot already owned
-// by another key (two ifaces 32 apart) sends the update to the global shard.
-__device__ __forceinline__ void slot_add(stat_slot *slots, const kctx &P, uint32_t key, uint32_t pkts, uint32_t bytes) {
-	const uint32_t kind = (key - 1) >> 16, iface = (key - 1) & 0xffff;
-	stat_slot *sl = &slots[(iface * 2 + kind) & (FWD4_STAT_SLOTS - 1)];
-	uint32_t cur = sl->key;
-	if (cur != key && cur == 0)
-		cur = atomicCAS(&sl->key, 0u, key) == 0 ? key : sl->key;
-	if (cur == key) {
-		atomicAdd(&sl->pkts, pkts);
-		atomicAdd(&sl->bytes, (unsigned long long)bytes);
-		return;
-	}
-	gr_hip_iface_stats *st = P.stats + (size_t)(blockIdx.x % FWD4_STAT_SHARDS) * P.max_ifaces + iface;
-	unsigned long long *c = reinterpret_cast<unsigned long long *>(kind ? &st->tx_packets : &st->rx_packets);
-	atomicAdd(c, (unsigned long long)pkts);
-	atomicAdd(c + 1, (unsigned long long)bytes);
-}
-
-// Sum of v over the wave with DPP (no LDS): quad, half-row and row steps,
-// then row broadcasts; lane 63 ends with the total.
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-	v += __builtin_amdgcn_update_dpp(0u, v, 0xb1, 0xf, 0xf, false); // quad_perm [1,0,3,2]
-	v += __builtin_amdgcn_update_dpp(0u, v, 0x4e, 0xf, 0xf, false); // quad_perm [2,3,0,1]
-	v += __builtin_amdgcn_update_dpp(0u, v, 0x141, 0xf, 0xf, false); // row_half_mirror
-	v += __builtin_amdgcn_update_dpp(0u, v, 0x140, 0xf, 0xf, false); // row_mirror
-	v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false); // row_bcast:15
-	v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false); // row_bcast:31
-	return __builtin_amdgcn_readlane(v, 63);
-}
-
-// Wave-aggregate one counter key per lane (0 = nothing) into the LDS slots.
-// Every lane of the wave must call it (converged).
-__device__ __forceinline__ void wave_count(stat_slot *slots, const kctx &P, uint32_t key, uint32_t len) {
-	for (;;) {
-		unsigned long long act = __ballot(key != 0);
-		if (act == 0)
-			break;
-		const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1;
-		const uint32_t k = __builtin_amdgcn_readlane(key, lead);
-		const bool same = key == k;
-		const uint32_t cnt = (uint32_t)__popcll(__ballot(same));
-		const uint32_t b = wave_sum(same ? len : 0u);
-		if ((threadIdx.x & 63) == lead)
-			slot_add(slots, P, k, cnt, b);
-		if (same)
-			key = 0;
-	}
-}
-
-__device__ __forceinline__ uint32_t lo16(uint32_t x) {
-	return x & 0xffff;
-}
-__device__ __forceinline__ uint32_t hi16(uint32_t x) {
-	return x >> 16;
-}
-__device__ __forceinline__ uint32_t bswap16(uint32_t x) {
-	return ((x & 0xff) << 8) | ((x >> 8) & 0xff);
-}
-
-struct result {
-	uint32_t edge, domain, iface, nh;
-	uint32_t rx_if, rx_par, tx_if, tx_par; // counter keys (0 = none)
-};
+#include "fwd4_dev.h"
 
 // The node chain for one packet. w[] is the 64-byte line (little-endian
 // words: byte j is (w[j/4] >> 8*(j%4)) & 0xff), modified in place.
@@ -232,11 +67,7 @@ __device__ __forceinline__ result process(const kctx &P, uint32_t (&w)[16], cons
 		r.domain = GR_HIP_ETH_DOMAIN_OTHER;
 	}
 	const uint32_t data_len = m.pkt_len >= 14 ? m.pkt_len - 14u : m.pkt_len; // rte_pktmbuf_adj
-	uint32_t e = GR_HIP_E_ETH_INPUT_UNKNOWN_TYPE;
-	const fwd4_edges &E = *P.edges;
-	for (uint32_t i = 0; i < E.n_eth_types; i++) // l2l3_edges[ether_type]
-		if (E.eth_type_be[i] == type_raw)
-			e = E.eth_type_edge[i];
+	const uint32_t e = eth_type_edge(P, type_raw); // l2l3_edges[ether_type]
 	if (e != CHAIN) {
 		r.edge = e;
 		return r;
@@ -269,7 +100,7 @@ __device__ __forceinline__ result process(const kctx &P, uint32_t (&w)[16], cons
 				sum += (j <= 2 + ihl) ? full : (j == 3 + ihl ? lo16(w[j]) : 0u);
 			}
 			if (ihl > 12) { // options reach past the line: bytes 64..73
-				uint4 x = *reinterpret_cast<const uint4 *>(frame + 64);
+				uint4 x = gld4(frame + 64);
 				uint32_t xw[3] = {x.x, x.y, x.z};
 #pragma unroll
 				for (uint32_t j = 16; j < 19; j++) {
@@ -321,18 +152,18 @@ __device__ __forceinline__ result process(const kctx &P, uint32_t (&w)[16], cons
 	if (rx.tbl24 != nullptr) {
 		const uint32_t ip = __builtin_bswap32(dst);
 		if (rx.flags & FWD4_RX_FIB16) { // DIR-16-8-8, 2-byte entries, bit15 = tbl8 group
-			uint32_t ent = rx.tbl24[ip >> 16]; // top: bit31 = chunk of 256 /24 entries
+			uint32_t ent = gld(rx.tbl24 + (ip >> 16)); // top: bit31 = chunk of 256 /24 entries
 			if (ent & 0x80000000u) {
 				const uint16_t *chunks = reinterpret_cast<const uint16_t *>(rx.tbl24 + 65536);
-				ent = chunks[(size_t)(ent & 0x7fffffffu) * 256 + ((ip >> 8) & 0xff)];
+				ent = gld(chunks + (size_t)(ent & 0x7fffffffu) * 256 + ((ip >> 8) & 0xff));
 			}
 			if (ent & 0x8000u)
-				ent = reinterpret_cast<const uint16_t *>(rx.tbl8)[(size_t)(ent & 0x7fffu) * 256 + (ip & 0xff)];
+				ent = gld(reinterpret_cast<const uint16_t *>(rx.tbl8) + (size_t)(ent & 0x7fffu) * 256 + (ip & 0xff));
 			slot = ent;
 		} else {
-			uint32_t ent = rx.tbl24[ip >> 8];
+			uint32_t ent = gld(rx.tbl24 + (ip >> 8));
 			if (ent & 0x80000000u)
-				ent = rx.tbl8[(size_t)(ent & 0x7fffffffu) * 256 + (ip & 0xff)];
+				ent = gld(rx.tbl8 + (size_t)(ent & 0x7fffffffu) * 256 + (ip & 0xff));
 			slot = ent;
 		}
 	}
@@ -348,7 +179,7 @@ __device__ __forceinline__ result process(const kctx &P, uint32_t (&w)[16], cons
 			slot = 0;
 		} else {
 			uint32_t i = a.reta_off + (m.rss & (a.reta_size - 1));
-			slot = i < P.reta_cap ? P.reta[i] : 0;
+			slot = i < P.reta_cap ? gld(P.reta + i) : 0;
 		}
 		if (slot == 0 || slot > P.max_nh) {
 			r.edge = GR_HIP_E_IP_ERROR_DEST_UNREACH;
@@ -411,26 +242,6 @@ __device__ __forceinline__ result process(const kctx &P, uint32_t (&w)[16], cons
 	return r;
 }
 
-typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-typedef uint32_t u2v __attribute__((ext_vector_type(2)));
-
-template <bool NT>
-__device__ __forceinline__ u4v ld16(const uint8_t *p) {
-	const u4v *q = reinterpret_cast<const u4v *>(p);
-	if (NT)
-		return __builtin_nontemporal_load(q);
-	return *q;
-}
-
-template <bool NT>
-__device__ __forceinline__ void st16(uint8_t *p, u4v v) {
-	u4v *q = reinterpret_cast<u4v *>(p);
-	if (NT)
-		__builtin_nontemporal_store(v, q);
-	else
-		*q = v;
-}
-
 // STATS: per-iface counters. NT: nontemporal loads and stores of the streamed
 // lines, metadata and verdicts (keeps L2 for the FIB gathers). TILE: packets
 // per workgroup = threads per workgroup (64: one wave, 256: four waves).
@@ -462,6 +273,8 @@ __global__ void __launch_bounds__(TILE) gr_fwd4_kernel(const fwd4_params A) {
 	P.readable = A.readable;
 	P.edges = &edges;
 	P.stats = A.stats;
+	__syncthreads();
+	P.ip4_edge = ip4_edge_of(edges);
 
 	const uint32_t n_tiles = (A.n + TILE - 1) / TILE;
 	for (uint32_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
@@ -541,14 +354,8 @@ __global__ void __launch_bounds__(TILE) gr_fwd4_kernel(const fwd4_params A) {
 	if (STATS) {
 		__syncthreads();
 		if (tid < FWD4_STAT_SLOTS && slots[tid].key != 0) {
-			uint32_t key = slots[tid].key - 1;
-			uint32_t kind = key >> 16, iface = key & 0xffff;
-			gr_hip_iface_stats *st =
-				A.stats + (size_t)(blockIdx.x % FWD4_STAT_SHARDS) * P.max_ifaces + iface;
-			unsigned long long *c =
-				reinterpret_cast<unsigned long long *>(kind ? &st->tx_packets : &st->rx_packets);
-			atomicAdd(c, (unsigned long long)slots[tid].pkts);
-			atomicAdd(c + 1, slots[tid].bytes);
+			const uint32_t key = slots[tid].key - 1;
+			shard_add(A.stats, P.max_ifaces, key >> 16, key & 0xffff, slots[tid].pkts, slots[tid].bytes);
 		}
 	}
 }

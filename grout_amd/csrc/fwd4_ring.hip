@@ -1,0 +1,323 @@
+// SPDX-License-Identifier: BSD-3-Clause
+//
+// fwd4_ring.hip -- the warp-specialised forwarding kernel for gfx950.
+//
+// gfx9 retires a wave's vector loads, stores and LDS-DMA in issue order
+// from one counter (vmcnt), so a wave that streams header lines AND walks
+// the dependent lookups (RX view -> FIB -> adjacency) pays the HBM latency
+// of its streams at its first lookup. Here the two never share a wave:
+//
+//   wave 0      loader:  LDS-DMA (global_load_lds) of each 64-packet tile's
+//                        header lines and metadata into a ring slot,
+//                        RING_AHEAD tiles in flight, published behind a
+//                        counted vmcnt;
+//   waves 2..7  compute: the node chain of a tile out of its slot (only the
+//                        dependent lookups on their vmcnt), rewritten rows
+//                        and verdicts back into the slot;
+//   wave 1      storer:  drains finished slots to HBM (coalesced 16-byte
+//                        stores) and hands them back to the loader.
+//
+// The hand-offs are LDS words with tile sequence numbers: ready[s] (loader
+// -> compute), done[s] (compute -> storer), free[s] (storer -> loader).
+// Every wait is bounded (RING_SPIN_MAX polls); a wave that gives up sets
+// the workgroup's abort word and every role leaves its loop, so the grid
+// always drains. Tiles of a workgroup are b, b + G, b + 2G ... (G = grid).
+#include "fwd4_chain.h"
+
+#define RING_WAVES 8
+#define RING_COMPUTE (RING_WAVES - 2)
+#define RING_SLOTS 8
+#define RING_AHEAD 4 // tiles the loader keeps in flight before publishing
+#define RING_GLDS_PER_TILE 6 // 4 x 1 KiB of lines + 2 x 256 B of metadata
+#define RING_SPIN_MAX (1u << 24)
+#define RING_NHF_LDS_MAX 2304 // fast adjacencies staged in LDS (36 KiB: two workgroups per CU)
+// vmcnt that leaves RING_AHEAD - 1 tiles in flight (an asm literal)
+#define RING_VMCNT_AHEAD 18
+static_assert(RING_VMCNT_AHEAD == RING_GLDS_PER_TILE * (RING_AHEAD - 1), "ring vmcnt");
+
+struct ring_lds {
+	uint8_t lines[RING_SLOTS][64 * 64]; // the tile's header lines (fwd4_chain.h image)
+	u2v meta[RING_SLOTS][64]; // gr_hip_pkt_meta
+	u2v verdict[RING_SLOTS][64];
+	uint32_t ready[RING_SLOTS], done[RING_SLOTS], free_[RING_SLOTS];
+	uint32_t abort;
+};
+
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+	return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+// LDS-DMA: 16 (or 4) bytes per active lane from gsrc to lds_base + lane * 16 (or 4).
+template <bool NT>
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_base) {
+	uint32_t keep;
+	if (NT)
+		asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+			     : "=&s"(keep)
+			     : "v"(gsrc), "s"(lds_base)
+			     : "memory");
+	else
+		asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+			     : "=&s"(keep)
+			     : "v"(gsrc), "s"(lds_base)
+			     : "memory");
+}
+
+template <bool NT>
+__device__ __forceinline__ void glds4(const void *gsrc, uint32_t lds_base) {
+	uint32_t keep;
+	if (NT)
+		asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off nt\n\ts_mov_b32 m0, %0"
+			     : "=&s"(keep)
+			     : "v"(gsrc), "s"(lds_base)
+			     : "memory");
+	else
+		asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+			     : "=&s"(keep)
+			     : "v"(gsrc), "s"(lds_base)
+			     : "memory");
+}
+
+__device__ __forceinline__ uint32_t flag_get(const uint32_t *f) {
+	return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void flag_set(uint32_t *f, uint32_t v) {
+	compiler_fence();
+	__hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Wait until *f >= want. False when the wait gave up or another wave did.
+__device__ __forceinline__ bool flag_wait(ring_lds &L, const uint32_t *f, uint32_t want) {
+	for (uint32_t spin = 0;; spin++) {
+		if ((int32_t)(flag_get(f) - want) >= 0)
+			return true;
+		if (flag_get(&L.abort))
+			return false;
+		if (spin >= RING_SPIN_MAX) {
+			flag_set(&L.abort, 1);
+			return false;
+		}
+		__builtin_amdgcn_s_sleep(1);
+	}
+}
+
+template <bool NT>
+__device__ void ring_loader(const fwd4_params &A, ring_lds &L, uint32_t n_local, uint32_t lane) {
+	const uint32_t G = gridDim.x;
+	const uint32_t prow = lane >> 2;
+	const uint32_t pchunk = (lane & 3) ^ ((lane >> 4) & 3); // chunk this lane lands in slot lane & 3
+	uint32_t pub = 0;
+	bool ok = true;
+	for (uint32_t k = 0; k < n_local && ok; k++) {
+		const uint32_t s = k % RING_SLOTS;
+		if (k >= RING_SLOTS && (int32_t)(flag_get(&L.free_[s]) - (k - RING_SLOTS + 1)) < 0) {
+			// ring full: publish what is in flight, then wait for the storer
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			for (; pub < k; pub++)
+				flag_set(&L.ready[pub % RING_SLOTS], pub + 1);
+			ok = flag_wait(L, &L.free_[s], k - RING_SLOTS + 1);
+			if (!ok)
+				break;
+		}
+		const uint32_t t = blockIdx.x + k * G;
+		const uint32_t base = t * 64, cnt = min(64u, A.n - base);
+		const uint32_t lb = lds_addr(L.lines[s]);
+#pragma unroll
+		for (uint32_t j = 0; j < 4; j++) {
+			const uint32_t r = j * 16 + prow;
+			if (r < cnt)
+				glds16<NT>(A.in + (size_t)(base + r) * A.in_stride + pchunk * 16, lb + j * 1024);
+		}
+		const uint32_t mb = lds_addr(L.meta[s]);
+		const uint8_t *msrc = reinterpret_cast<const uint8_t *>(A.meta + base);
+#pragma unroll
+		for (uint32_t j = 0; j < 2; j++)
+			if (j * 32 + (lane >> 1) < cnt)
+				glds4<NT>(msrc + j * 256 + lane * 4, mb + j * 256);
+		if (k + 1 - pub == RING_AHEAD) {
+			asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); // RING_VMCNT_AHEAD
+			flag_set(&L.ready[pub % RING_SLOTS], pub + 1);
+			pub++;
+		}
+	}
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	if (ok)
+		for (; pub < n_local; pub++)
+			flag_set(&L.ready[pub % RING_SLOTS], pub + 1);
+}
+
+template <bool NT>
+__device__ void ring_storer(const fwd4_params &A, ring_lds &L, uint32_t n_local, uint32_t lane) {
+	const uint32_t G = gridDim.x;
+	const uint32_t prow = lane >> 2, part = lane & 3;
+	const uint32_t pslot = (part ^ ((lane >> 4) & 3)) << 4;
+	for (uint32_t k = 0; k < n_local; k++) {
+		const uint32_t s = k % RING_SLOTS;
+		if (!flag_wait(L, &L.done[s], k + 1))
+			break;
+		const uint32_t t = blockIdx.x + k * G;
+		const uint32_t base = t * 64, cnt = min(64u, A.n - base);
+		u4v o[4];
+#pragma unroll
+		for (uint32_t j = 0; j < 4; j++)
+			o[j] = *reinterpret_cast<const u4v *>(&L.lines[s][(j * 16 + prow) * 64 + pslot]);
+		const u2v v = L.verdict[s][lane];
+		// the registers hold the tile: hand the slot back before storing
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+		flag_set(&L.free_[s], k + 1);
+#pragma unroll
+		for (uint32_t j = 0; j < 4; j++) {
+			const uint32_t r = j * 16 + prow;
+			if (r < cnt)
+				st16<NT>(A.out + (size_t)(base + r) * A.out_stride + part * 16, o[j]);
+		}
+		if (lane < cnt) {
+			u2v *vp = reinterpret_cast<u2v *>(A.verdicts + base + lane);
+			if (NT)
+				__builtin_nontemporal_store(v, vp);
+			else
+				*vp = v;
+		}
+	}
+}
+
+template <bool STATS>
+__device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds &L, stat_slot *slots, const uint4 *nhf_lds,
+			     uint32_t n_local, uint32_t c, uint32_t lane) {
+	const uint32_t G = gridDim.x;
+	for (uint32_t k = c; k < n_local; k += RING_COMPUTE) {
+		const uint32_t s = k % RING_SLOTS;
+		if (!flag_wait(L, &L.ready[s], k + 1))
+			break;
+		const uint32_t t = blockIdx.x + k * G;
+		const uint32_t base = t * 64, cnt = min(64u, A.n - base);
+		const bool live = lane < cnt;
+		uint8_t *R = L.lines[s];
+		gr_hip_pkt_meta m = {0, 0, 0, 0};
+		if (live) {
+			const u2v pm = L.meta[s][lane];
+			m.iface = pm.x & 0xffff;
+			m.vlan_ck = pm.x >> 16;
+			m.pkt_len = pm.y & 0xffff;
+			m.rss = pm.y >> 16;
+		}
+		const uint32_t if0 = __builtin_amdgcn_readfirstlane(m.iface);
+		rxv rx;
+		if (__ballot(live && m.iface != if0) == 0)
+			rx = load_rx_scalar(P, if0);
+		else
+			rx = load_rx(P, m.iface);
+
+		result r = {GR_HIP_E_PUNT, 0, m.iface, 0, 0, 0, 0, 0};
+		if (live) {
+			uint32_t dst = 0, data_len = 0;
+			const uint8_t *frame = A.in + (size_t)(base + lane) * A.in_stride;
+			if (pipe_head(P, R, lane, m, rx, r, dst, data_len, frame)) {
+				const uint32_t slot = pipe_fib(rx, dst);
+				if (slot == 0 || slot > P.max_nh) {
+					r.edge = GR_HIP_E_IP_ERROR_DEST_UNREACH; // NO_ROUTE :150-153
+				} else {
+					// fast adjacency: from LDS for the first slots, else one 16-byte gather
+					const uint4 f = slot <= A.nhf_lds ? nhf_lds[slot - 1] : gld4(P.nhf + slot);
+					if (f.w >> 16) {
+						fast_tail(R, lane, r, data_len, slot, f);
+					} else {
+						const uint4 *ap = reinterpret_cast<const uint4 *>(P.adj + slot);
+						pipe_tail(P, R, lane, m, rx.flags, r, dst, data_len, slot, gld4(ap), gld4(ap + 1));
+					}
+				}
+			}
+		}
+		L.verdict[s][lane] = u2v{r.edge | (r.domain << 8) | (r.iface << 16), r.nh};
+		flag_set(&L.done[s], k + 1);
+		if (STATS) {
+			const uint32_t len = m.pkt_len;
+			wave_count(slots, P, r.rx_if ? r.rx_if + 1 : 0, len);
+			wave_count(slots, P, r.rx_par ? r.rx_par + 1 : 0, len);
+			wave_count(slots, P, r.tx_if ? (r.tx_if | 0x10000u) + 1 : 0, len);
+			wave_count(slots, P, r.tx_par ? (r.tx_par | 0x10000u) + 1 : 0, len);
+		}
+	}
+}
+
+template <bool STATS, bool NT>
+__global__ void __launch_bounds__(RING_WAVES * 64) gr_fwd4_ring(const fwd4_params A) {
+	__shared__ __attribute__((aligned(16))) ring_lds L;
+	__shared__ stat_slot slots[FWD4_STAT_SLOTS];
+	__shared__ fwd4_edges edges;
+	extern __shared__ __attribute__((aligned(16))) uint4 nhf_lds[]; // [A.nhf_lds]: slots 1..
+	const uint32_t tid = threadIdx.x, lane = tid & 63;
+	const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+	const fwd4_tables *T = A.T;
+
+	{
+		const uint4 *src = reinterpret_cast<const uint4 *>(T->nhf) + 1;
+		for (uint32_t i = tid; i < A.nhf_lds; i += RING_WAVES * 64)
+			nhf_lds[i] = gld4(src + i);
+	}
+
+	for (uint32_t i = tid; i < sizeof(fwd4_edges); i += RING_WAVES * 64)
+		reinterpret_cast<uint8_t *>(&edges)[i] = reinterpret_cast<const uint8_t *>(&T->edges)[i];
+	if (tid < RING_SLOTS) {
+		L.ready[tid] = 0;
+		L.done[tid] = 0;
+		L.free_[tid] = 0;
+	}
+	if (tid == 0)
+		L.abort = 0;
+	if (STATS && tid < FWD4_STAT_SLOTS) {
+		slots[tid].key = 0;
+		slots[tid].pkts = 0;
+		slots[tid].bytes = 0;
+	}
+	__syncthreads();
+
+	const uint32_t n_tiles = (A.n + 63) >> 6;
+	const uint32_t n_local = blockIdx.x < n_tiles ? (n_tiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+	if (wv == 0) {
+		ring_loader<NT>(A, L, n_local, lane);
+	} else if (wv == 1) {
+		ring_storer<NT>(A, L, n_local, lane);
+	} else {
+		kctx P = make_kctx(A, &edges);
+		ring_compute<STATS>(A, P, L, slots, nhf_lds, n_local, wv - 2, lane);
+	}
+
+	if (STATS) {
+		__syncthreads();
+		if (tid < FWD4_STAT_SLOTS && slots[tid].key != 0) {
+			const uint32_t key = slots[tid].key - 1;
+			shard_add(A.stats, T->max_ifaces, key >> 16, key & 0xffff, slots[tid].pkts, slots[tid].bytes);
+		}
+	}
+}
+
+typedef void (*fwd4_rfn)(const fwd4_params);
+static const fwd4_rfn ring_kernels[4] = {
+	gr_fwd4_ring<false, false>,
+	gr_fwd4_ring<true, false>,
+	gr_fwd4_ring<false, true>,
+	gr_fwd4_ring<true, true>,
+};
+
+// variant: FWD4_V_STATS | FWD4_V_NT; one workgroup walks tiles b, b + grid, ...
+// A->nhf_lds fast adjacencies are staged in dynamic LDS.
+extern "C" hipError_t gr_fwd4_ring_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant) {
+	hipLaunchKernelGGL(ring_kernels[variant & 3], dim3(grid), dim3(RING_WAVES * 64), A->nhf_lds * sizeof(fwd4_nhf), s, *A);
+	return hipGetLastError();
+}
+
+extern "C" uint32_t gr_fwd4_ring_nhf_max(void) {
+	return RING_NHF_LDS_MAX;
+}
+
+extern "C" int gr_fwd4_ring_occupancy(int variant, uint32_t nhf_lds) {
+	int b = 0;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, ring_kernels[variant & 3], RING_WAVES * 64,
+							 nhf_lds * sizeof(fwd4_nhf)) != hipSuccess) {
+		(void)hipGetLastError();
+		return 0;
+	}
+	return b;
+}

@@ -26,6 +26,16 @@
 extern "C" hipError_t gr_fwd4_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant);
 extern "C" int gr_fwd4_occupancy(int variant);
 extern "C" uint32_t gr_fwd4_tile(int variant);
+extern "C" hipError_t gr_fwd4_pipe_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant);
+extern "C" int gr_fwd4_pipe_occupancy(int variant);
+extern "C" hipError_t gr_fwd4_ring_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant);
+extern "C" int gr_fwd4_ring_occupancy(int variant, uint32_t nhf_lds);
+extern "C" uint32_t gr_fwd4_ring_nhf_max(void);
+#define RING_WG_PER_CU 2 // default workgroups per CU of the ring kernel (measured)
+#define PIPE_WG_PACKETS 256 // fwd4_pipe.hip: 4 waves x 64-packet tiles
+
+// Forwarding kernels (gr_hip_tune "kernel")
+enum { KERNEL_TILE = 0, KERNEL_PIPE = 1, KERNEL_RING = 2 };
 
 #define HCK(expr)                                                                                  \
 	do {                                                                                       \
@@ -95,6 +105,8 @@ struct gr_hip_ctx {
 	uint32_t nh_hi; // highest nexthop slot ever set
 	fwd4_rx *d_rx;
 	fwd4_adj *d_adj;
+	std::vector<fwd4_nhf> nhf; // fast adjacencies (host image)
+	fwd4_nhf *d_nhf;
 	uint32_t *d_reta;
 	uint32_t d_reta_cap;
 	uint32_t *d_vlan_keys;
@@ -110,6 +122,10 @@ struct gr_hip_ctx {
 	int fib16; // allow the 2-byte FIB format
 	int occ[8];
 	int tile64; // FWD4_V_TILE64
+	int kernel; // KERNEL_*
+	int occ_pipe[4];
+	int occ_ring[4]; // at occ_ring_nhf staged fast adjacencies
+	uint32_t occ_ring_nhf;
 };
 
 // ---------------------------------------------------------------------------
@@ -240,6 +256,22 @@ static fwd4_adj make_adj(const gr_hip_ctx *c, uint32_t slot) {
 	return a;
 }
 
+// Fast adjacency of a precomputed adjacency: filled only for the plain
+// forward to a port (see fwd4_nhf), mtu = 0 otherwise.
+static fwd4_nhf make_nhf(const fwd4_adj &a) {
+	fwd4_nhf f;
+	memset(&f, 0, sizeof(f));
+	if (a.type == GR_HIP_NH_T_L3 && a.e_in == GR_HIP_EDGE_CHAIN && a.flags == 0 && a.e_pre == GR_HIP_EDGE_CHAIN
+	    && a.e_mid == GR_HIP_EDGE_CHAIN && a.e_post == GR_HIP_E_PORT_OUTPUT && a.post_iface == a.oif
+	    && a.tx_if == a.oif && a.tx_par == 0 && a.mtu != 0) {
+		memcpy(f.dmac, a.dmac, 6);
+		memcpy(f.smac, a.smac, 6);
+		f.oif = a.oif;
+		f.mtu = a.mtu;
+	}
+	return f;
+}
+
 // Recompute and upload the RX views (all) and adjacencies [first, first+n)
 // (n == 0: every slot up to nh_hi). Caller holds c->mu and has quiesced.
 static int upload_views(gr_hip_ctx *c, bool rx, uint32_t first, uint32_t n, bool adj) {
@@ -253,10 +285,14 @@ static int upload_views(gr_hip_ctx *c, bool rx, uint32_t first, uint32_t n, bool
 			first = 1;
 			n = c->nh_hi;
 		}
-		for (uint32_t i = first; i < first + n; i++)
+		for (uint32_t i = first; i < first + n; i++) {
 			c->adj[i] = make_adj(c, i);
-		if (n)
+			c->nhf[i] = make_nhf(c->adj[i]);
+		}
+		if (n) {
 			HCK(hipMemcpyAsync(c->d_adj + first, &c->adj[first], sizeof(fwd4_adj) * n, hipMemcpyHostToDevice, c->ctl));
+			HCK(hipMemcpyAsync(c->d_nhf + first, &c->nhf[first], sizeof(fwd4_nhf) * n, hipMemcpyHostToDevice, c->ctl));
+		}
 	}
 	HCK(hipStreamSynchronize(c->ctl));
 	return 0;
@@ -269,6 +305,7 @@ static int upload_tables(gr_hip_ctx *c) {
 	memset(&t, 0, sizeof(t));
 	t.rx = c->d_rx;
 	t.adj = c->d_adj;
+	t.nhf = c->d_nhf;
 	t.reta = c->d_reta;
 	t.vlan_keys = c->d_vlan_keys;
 	t.vlan_vals = c->d_vlan_vals;
@@ -367,6 +404,7 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->vrfs.assign(max_ifaces, vrf_fib {});
 	c->rx.assign(max_ifaces, fwd4_rx {});
 	c->adj.assign((size_t)max_nexthops + 1, fwd4_adj {});
+	c->nhf.assign((size_t)max_nexthops + 1, fwd4_nhf {});
 	c->nh_hi = 0;
 	set_default_edges(&c->edges);
 	c->d_reta = nullptr;
@@ -379,6 +417,8 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 		goto fail;
 	if (hipMalloc(&c->d_rx, sizeof(fwd4_rx) * max_ifaces) != hipSuccess)
 		goto fail;
+	if (hipMalloc(&c->d_nhf, sizeof(fwd4_nhf) * ((size_t)max_nexthops + 1)) != hipSuccess)
+		goto fail;
 	if (hipMalloc(&c->d_adj, sizeof(fwd4_adj) * ((size_t)max_nexthops + 1)) != hipSuccess)
 		goto fail;
 	if (hipMalloc(&c->d_tables, sizeof(fwd4_tables)) != hipSuccess)
@@ -386,15 +426,22 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	// every device write goes through the control stream: a plain hipMemset
 	// runs on the null stream, which a non-blocking stream does not order with
 	if (hipMemsetAsync(c->d_rx, 0, sizeof(fwd4_rx) * max_ifaces, c->ctl) != hipSuccess
-	    || hipMemsetAsync(c->d_adj, 0, sizeof(fwd4_adj) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess)
+	    || hipMemsetAsync(c->d_adj, 0, sizeof(fwd4_adj) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess
+	    || hipMemsetAsync(c->d_nhf, 0, sizeof(fwd4_nhf) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess)
 		goto fail;
 	c->nt = 0;
 	c->stats_on = 1;
 	c->wg_per_cu = 0;
 	c->fib16 = 1;
 	c->tile64 = 0;
+	c->kernel = KERNEL_RING;
 	for (int v = 0; v < 8; v++)
 		c->occ[v] = gr_fwd4_occupancy(v);
+	for (int v = 0; v < 4; v++)
+		c->occ_pipe[v] = gr_fwd4_pipe_occupancy(v);
+	for (int v = 0; v < 4; v++)
+		c->occ_ring[v] = gr_fwd4_ring_occupancy(v, 0);
+	c->occ_ring_nhf = 0;
 	ret = -EIO;
 	if (upload_tables(c) != 0)
 		goto fail;
@@ -421,6 +468,7 @@ extern "C" int gr_hip_fini(gr_hip_ctx_t *c) {
 	}
 	hipFree(c->d_rx);
 	hipFree(c->d_adj);
+	hipFree(c->d_nhf);
 	hipFree(c->d_reta);
 	hipFree(c->d_vlan_keys);
 	hipFree(c->d_vlan_vals);
@@ -948,17 +996,50 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	A.in_stride = b->in_stride;
 	A.out_stride = b->out_stride;
 	A.readable = (b->flags & GR_HIP_BATCH_F_LINES_ONLY) ? GR_HIP_LINE : b->in_stride;
+	A.nhf_lds = 0;
 	int stats = c->stats_on && q->d_stats != nullptr;
-	int variant = (stats ? FWD4_V_STATS : 0) | c->nt | c->tile64;
-	uint32_t tile = gr_fwd4_tile(variant);
-	uint32_t tiles = (b->n + tile - 1) / tile;
-	uint32_t grid = c->wg_per_cu > 0 ? (uint32_t)c->n_cu * (uint32_t)c->wg_per_cu : tiles;
-	if (grid > tiles)
-		grid = tiles;
 	uint32_t slot = (uint32_t)(q->n_launch % N_TIMED);
-	if (timed)
-		HCK(hipEventRecord(q->ev0[slot], s));
-	HCK(gr_fwd4_launch(&A, grid, s, variant));
+	if (c->kernel == KERNEL_RING) {
+		// persistent: one resident round of workgroups, each walking 64-packet tiles
+		int variant = (stats ? FWD4_V_STATS : 0) | c->nt;
+		uint32_t tiles = (b->n + 63) / 64;
+		A.nhf_lds = c->nh_hi < gr_fwd4_ring_nhf_max() ? c->nh_hi : gr_fwd4_ring_nhf_max();
+		if (A.nhf_lds != c->occ_ring_nhf) {
+			for (int v = 0; v < 4; v++)
+				c->occ_ring[v] = gr_fwd4_ring_occupancy(v, A.nhf_lds);
+			c->occ_ring_nhf = A.nhf_lds;
+		}
+		uint32_t per_cu = c->wg_per_cu > 0 ? (uint32_t)c->wg_per_cu : RING_WG_PER_CU;
+		if (c->occ_ring[variant] > 0 && per_cu > (uint32_t)c->occ_ring[variant])
+			per_cu = (uint32_t)c->occ_ring[variant];
+		uint32_t grid = (uint32_t)c->n_cu * per_cu;
+		if (grid > tiles)
+			grid = tiles;
+		if (timed)
+			HCK(hipEventRecord(q->ev0[slot], s));
+		HCK(gr_fwd4_ring_launch(&A, grid, s, variant));
+	} else if (c->kernel == KERNEL_PIPE) {
+		// every wave strides over 64-packet tiles: one resident round of workgroups
+		int variant = (stats ? FWD4_V_STATS : 0) | c->nt;
+		uint32_t wgs = (b->n + PIPE_WG_PACKETS - 1) / PIPE_WG_PACKETS;
+		uint32_t per_cu = c->wg_per_cu > 0 ? (uint32_t)c->wg_per_cu : (uint32_t)(c->occ_pipe[variant] > 0 ? c->occ_pipe[variant] : 1);
+		uint32_t grid = (uint32_t)c->n_cu * per_cu;
+		if (grid > wgs)
+			grid = wgs;
+		if (timed)
+			HCK(hipEventRecord(q->ev0[slot], s));
+		HCK(gr_fwd4_pipe_launch(&A, grid, s, variant));
+	} else {
+		int variant = (stats ? FWD4_V_STATS : 0) | c->nt | c->tile64;
+		uint32_t tile = gr_fwd4_tile(variant);
+		uint32_t tiles = (b->n + tile - 1) / tile;
+		uint32_t grid = c->wg_per_cu > 0 ? (uint32_t)c->n_cu * (uint32_t)c->wg_per_cu : tiles;
+		if (grid > tiles)
+			grid = tiles;
+		if (timed)
+			HCK(hipEventRecord(q->ev0[slot], s));
+		HCK(gr_fwd4_launch(&A, grid, s, variant));
+	}
 	if (timed) {
 		HCK(hipEventRecord(q->ev1[slot], s));
 		q->n_launch++;
@@ -984,7 +1065,15 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		c->wg_per_cu = value;
 	} else if (strcmp(key, "fib16") == 0) { // takes effect at the next commit
 		c->fib16 = value != 0;
+	} else if (strcmp(key, "kernel") == 0) { // 0: fwd4_kernel.hip, 1: fwd4_pipe.hip, 2: fwd4_ring.hip
+		if (value < KERNEL_TILE || value > KERNEL_RING)
+			return -EINVAL;
+		c->kernel = value;
 	} else if (strcmp(key, "occupancy") == 0) { // read-only: WGs/CU of the current variant
+		if (c->kernel == KERNEL_RING)
+			return c->occ_ring[(c->stats_on ? FWD4_V_STATS : 0) | c->nt]; // as of the last launch
+		if (c->kernel == KERNEL_PIPE)
+			return c->occ_pipe[(c->stats_on ? FWD4_V_STATS : 0) | c->nt];
 		return c->occ[(c->stats_on ? FWD4_V_STATS : 0) | c->nt | c->tile64];
 	} else {
 		return -ENOENT;

@@ -191,16 +191,22 @@ def test_kernel_timing_api(fastpath):
     q.close()
 
 
-@pytest.mark.parametrize("nt,stats,wg,fib16,tile", [(1, 1, 0, 1, 64), (1, 0, 6, 1, 256), (0, 1, 4, 0, 64),
-                                                    (0, 1, 0, 0, 256), (1, 1, 8, 1, 64)])
-def test_kernel_variants(fastpath, nt, stats, wg, fib16, tile):
-    """Every tuning variant (gr_hip_tune) forwards bit-exact."""
+@pytest.mark.parametrize("kernel,nt,stats,wg,fib16,tile", [
+    (0, 1, 1, 0, 1, 64), (0, 1, 0, 6, 1, 256), (0, 0, 1, 4, 0, 64), (0, 0, 1, 0, 0, 256), (0, 1, 1, 8, 1, 64),
+    (1, 1, 1, 0, 1, 256), (1, 0, 0, 1, 1, 256), (1, 1, 0, 2, 0, 256), (1, 0, 1, 0, 0, 256),
+    (2, 1, 1, 0, 1, 256), (2, 0, 0, 1, 1, 256), (2, 1, 0, 2, 0, 256), (2, 0, 1, 0, 0, 256)])
+def test_kernel_variants(fastpath, kernel, nt, stats, wg, fib16, tile):
+    """Every tuning variant (gr_hip_tune) forwards bit-exact: the three
+    kernels (0: fwd4_kernel.hip, 1: fwd4_pipe.hip, 2: fwd4_ring.hip);
+    wg_per_cu 1-2 making every wave / workgroup walk many tiles (a deep
+    ring, wrap-around of every slot)."""
     t, _ = SC.corpus_topology()
     fr, me, lab = SC.corpus_arrays()
     tf = _fullview()
     fr2, me2 = S.stream(1 << 20, 0xAB + nt, routes=tf.route_array())
     o1 = oracle.Oracle(t).process(fr, me)
     o2 = oracle.Oracle(tf).process(fr2, me2)
+    fastpath.tune("kernel", kernel)
     fastpath.tune("nt", nt)
     fastpath.tune("stats", stats)
     fastpath.tune("wg_per_cu", wg)
@@ -223,7 +229,7 @@ def test_kernel_variants(fastpath, nt, stats, wg, fib16, tile):
         else:
             assert info["dev_bytes"] == 4 * (1 << 24) + 1024 * n8
     finally:
-        for k, v in [("nt", 0), ("stats", 1), ("wg_per_cu", 0), ("fib16", 1), ("tile", 256)]:
+        for k, v in [("kernel", 2), ("nt", 0), ("stats", 1), ("wg_per_cu", 0), ("fib16", 1), ("tile", 256)]:
             fastpath.tune(k, v)
         fresh_fastpath_state(fastpath, T.config_single_route())
 
@@ -246,3 +252,53 @@ def test_mirror_updates_propagate(fastpath):
         compare(oracle.Oracle(t).process(fr, me), run_gpu(fastpath, t, fr, me), lab)
     finally:
         fresh_fastpath_state(fastpath, T.config_single_route())
+
+
+def _many_nh_topology(n_nh=6000, n_routes=50_000):
+    """More nexthops than the ring kernel stages in LDS (2304), a mix of
+    plain forwards and nexthops that leave the fast adjacency: unresolved
+    (HOLD), on a VLAN, flagged LINK, and on an admin-down port."""
+    t = T.base_ports(max_routes=n_routes + 10)
+    t.add_vlan(40, T.PORT_IFACE[2], 77)
+    t.add_port(41, 3, "02:00:00:00:00:29", up=False)
+    first = t.n_nh + 1
+    for j in range(1, n_nh + 1):
+        slot = first + j - 1
+        kind = j % 11
+        ip = f"100.{64 + (j >> 16)}.{(j >> 8) & 255}.{j & 255}"
+        mac = "02:00:00:02:%02x:%02x" % ((j >> 8) & 255, j & 255)
+        if kind == 3:
+            t.add_nexthop(T.PORT_IFACE[1], ip, None, slot=slot)  # no MAC: HOLD
+        elif kind == 5:
+            t.add_nexthop(40, ip, mac, slot=slot)  # VLAN oif
+        elif kind == 7:
+            t.add_nexthop(T.PORT_IFACE[3], ip, mac, flags=abi.NH_F_LINK, slot=slot)
+        elif kind == 9:
+            t.add_nexthop(41, ip, mac, slot=slot)  # admin-down port
+        else:
+            t.add_nexthop(T.PORT_IFACE[1 + j % 3], ip, mac, slot=slot)
+    routes = np.zeros(n_routes, dtype=abi.ROUTE_DT)
+    abi.check("gr_synth_fullview_routes",
+              abi.host().gr_synth_fullview_routes(n_routes, T.VRF_MAIN, first, n_nh, routes.ctypes.data))
+    t.add_routes(routes)
+    t.add_address(T.PORT_IFACE[0], "172.16.0.1/24")
+    return t
+
+
+@pytest.mark.parametrize("kernel", [2, 0])
+def test_many_nexthops_fast_adjacency(fastpath, kernel):
+    """Nexthop slots past the LDS-staged range read the fast adjacency with a
+    gather; non-plain nexthops fall back to the full adjacency."""
+    t = _many_nh_topology()
+    fr, me = S.stream(1 << 18, 0x5EED + kernel, routes=t.route_array())
+    o = oracle.Oracle(t).process(fr, me)
+    fastpath.tune("kernel", kernel)
+    try:
+        g = run_gpu(fastpath, t, fr, me)
+        compare(o, g)
+        edges = np.bincount(g[1]["edge"], minlength=abi.E_COUNT)
+        assert edges[abi.EDGE["port_output"]] > len(me) // 2
+        assert edges[abi.EDGE["ip_hold"]] > 0
+        assert (g[1]["nh"] > 2304).sum() > len(me) // 4
+    finally:
+        fastpath.tune("kernel", 2)

@@ -19,7 +19,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 24)
-    ap.add_argument("--staging", type=int, default=None)
+    ap.add_argument("--workload", default="fullview64", choices=["fullview64", "single64"])
+    ap.add_argument("--kernel", type=int, default=None, help="gr_hip_tune kernel: 0 tile, 1 pipe, 2 ring")
+    ap.add_argument("--wg", type=int, default=None, help="gr_hip_tune wg_per_cu")
+    ap.add_argument("--stats", type=int, default=None)
+    ap.add_argument("--nt", type=int, default=None)
+    ap.add_argument("--no-calib", action="store_true")
     args = ap.parse_args()
     import torch
 
@@ -29,13 +34,20 @@ def main():
     from grout_amd.fwd import FastPath
 
     dev = torch.device("cuda", 0)
-    topo = T.config_fullview()
+    if args.workload == "single64":
+        topo = T.config_single_route()
+        kw = dict(dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    else:
+        topo = T.config_fullview()
+        kw = dict(routes=topo.route_array())
     fp = FastPath(0)
     fp.load(topo)
-    if args.staging is not None:
-        fp.tune("staging", args.staging)
+    for k in ("kernel", "wg", "stats", "nt"):
+        v = getattr(args, k)
+        if v is not None:
+            fp.tune("wg_per_cu" if k == "wg" else k, v)
     n = args.batch
-    frames, meta = S.stream(n, S.SEED_GPU_BASE, routes=topo.route_array())
+    frames, meta = S.stream(n, S.SEED_GPU_BASE, **kw)
     d_in = torch.from_numpy(frames.reshape(-1)).to(dev)
     d_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
     d_out = torch.empty_like(d_in)
@@ -44,6 +56,8 @@ def main():
     for _ in range(args.reps):
         q.submit(d_in, d_out, d_meta, d_v, n)
     torch.cuda.synchronize()
+    if args.no_calib:
+        return
     # calibration: 1 GiB read + 1 GiB written by a streaming copy kernel
     a = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
     b = torch.empty_like(a)

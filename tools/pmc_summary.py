@@ -22,7 +22,8 @@ def main():
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for row in csv.DictReader(open(f)):
                 k = row.get("Kernel_Name", "?")
-                k = "gr_fwd4_kernel" if "gr_fwd4_kernel" in k else ("copy" if "copy" in k.lower() or "elementwise" in k else k[:60])
+                fw = [x for x in ("gr_fwd4_ring", "gr_fwd4_pipe", "gr_fwd4_kernel") if x in k]
+                k = fw[0] if fw else ("copy" if "copy" in k.lower() or "elementwise" in k else k[:60])
                 acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
     out = {}
     for k, ctrs in acc.items():

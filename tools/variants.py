@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--fib16", default="1,0")
     ap.add_argument("--stats", default="1")
     ap.add_argument("--tile", default="256")
+    ap.add_argument("--kernel", default="2,0", help="0 tile, 1 pipe, 2 ring")
     args = ap.parse_args()
     import torch
 
@@ -53,12 +54,13 @@ def main():
     d_v = torch.empty(n * 8, dtype=torch.uint8, device=dev)
     q = fp.queue(torch.cuda.current_stream(dev).cuda_stream)
     variants = list(itertools.product(ints(args.fib16), ints(args.stats), ints(args.nt), ints(args.wg),
-                                      ints(args.tile)))
+                                      ints(args.tile), ints(args.kernel)))
     times = {v: [] for v in variants}
     ref = None
     for r in range(args.rounds):
         for v in variants:
-            f16, st, nt, wg, tile = v
+            f16, st, nt, wg, tile, kern = v
+            fp.tune("kernel", kern)
             fp.tune("tile", tile)
             fp.tune("fib16", f16)
             fp.fib_commit(T.VRF_MAIN)  # re-uploads when the format changes
@@ -71,14 +73,15 @@ def main():
             q.sync()
             ms, cnt = q.kernel_ms(args.reps)
             times[v].append(ms / cnt)
-            if r == 0:  # every variant must produce the same verdicts
-                h = int(torch.sum(d_v.view(torch.int32).to(torch.int64)).item())
+            if r == 0:  # every variant must produce the same verdicts and lines
+                h = (int(torch.sum(d_v.view(torch.int32).to(torch.int64)).item()),
+                     int(torch.sum(d_out.view(torch.int32).to(torch.int64)).item()))
                 ref = h if ref is None else ref
-                assert h == ref, ("verdicts differ", v)
+                assert h == ref, ("outputs differ", v, h, ref)
     for v in variants:
         t = np.array(times[v])
         print(json.dumps({"workload": args.workload, "fib16": v[0], "stats": v[1], "nt": v[2],
-                          "wg_per_cu": v[3], "tile": v[4], "median_ms": round(float(np.median(t)), 4),
+                          "wg_per_cu": v[3], "tile": v[4], "kernel": v[5], "median_ms": round(float(np.median(t)), 4),
                           "min_ms": round(float(t.min()), 4), "mpps": round(n / float(np.median(t)) / 1e3, 1)}),
               flush=True)
     q.close()
