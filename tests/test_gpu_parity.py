@@ -229,7 +229,7 @@ def test_kernel_variants(fastpath, kernel, nt, stats, wg, fib16, tile):
         else:
             assert info["dev_bytes"] == 4 * (1 << 24) + 1024 * n8
     finally:
-        for k, v in [("kernel", 2), ("nt", 0), ("stats", 1), ("wg_per_cu", 0), ("fib16", 1), ("tile", 256)]:
+        for k, v in [("kernel", 2), ("nt", 1), ("stats", 1), ("wg_per_cu", 0), ("fib16", 1), ("tile", 256)]:
             fastpath.tune(k, v)
         fresh_fastpath_state(fastpath, T.config_single_route())
 
