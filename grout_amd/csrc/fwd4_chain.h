@@ -1,9 +1,9 @@
 // SPDX-License-Identifier: BSD-3-Clause
 //
 // fwd4_chain.h -- the node chain split at its dependent loads, for kernels
-// that keep a tile's header lines in an LDS image (fwd4_pipe.hip,
-// fwd4_ring.hip): pipe_head (iface_input .. ip_input checks), pipe_fib
-// (fib4_lookup), pipe_tail (adjacency .. iface_output, rewriting the row).
+// that keep a tile's header lines in an LDS image (fwd4_ring.hip):
+// chain_head (iface_input .. ip_input checks), chain_fib
+// (fib4_lookup), chain_tail (adjacency .. iface_output, rewriting the row).
 // Node citations as process() in fwd4_kernel.hip. Not a public header.
 //
 // LDS image of a 64-packet tile: row r (64 bytes) = packet r, its 16-byte
@@ -67,7 +67,7 @@ __device__ __forceinline__ rxv load_rx_scalar(const kctx &P, uint32_t id) {
 // iface_input -> eth_input -> ip_input up to the FIB lookup, for the packet
 // in row `row` of R. Returns false when the packet left the chain (r.edge
 // set); otherwise dst (network order as stored) and data_len are set.
-__device__ __forceinline__ bool pipe_head(const kctx &P, const uint8_t *R, uint32_t row, const gr_hip_pkt_meta &m,
+__device__ __forceinline__ bool chain_head(const kctx &P, const uint8_t *R, uint32_t row, const gr_hip_pkt_meta &m,
 					  rxv &rx, result &r, uint32_t &dst, uint32_t &data_len, const uint8_t *frame) {
 	// ---- iface_input (iface_input.c:52-112)
 	if (rx.id == 0)
@@ -202,7 +202,7 @@ __device__ __forceinline__ bool pipe_head(const kctx &P, const uint8_t *R, uint3
 }
 
 // fib4_lookup (route.c:147-167) in the iface's VRF table.
-__device__ __forceinline__ uint32_t pipe_fib(const rxv &rx, uint32_t dst) {
+__device__ __forceinline__ uint32_t chain_fib(const rxv &rx, uint32_t dst) {
 	if (rx.tbl24 == nullptr)
 		return 0;
 	const uint32_t ip = __builtin_bswap32(dst);
@@ -225,7 +225,7 @@ __device__ __forceinline__ uint32_t pipe_fib(const rxv &rx, uint32_t dst) {
 // From the adjacency (its first 32 bytes in a, b) to the verdict:
 // group resolution, ip_input's nexthop checks, ip_forward, ip_output,
 // eth_output, iface_output. Rewrites row `row` of R.
-__device__ __forceinline__ void pipe_tail(const kctx &P, uint8_t *R, uint32_t row, const gr_hip_pkt_meta &m,
+__device__ __forceinline__ void chain_tail(const kctx &P, uint8_t *R, uint32_t row, const gr_hip_pkt_meta &m,
 					  uint32_t rx_flags, result &r, uint32_t dst, uint32_t data_len, uint32_t slot,
 					  uint4 a, uint4 b) {
 	adjv A = unpack_adj(a, b, uint4{0, 0, 0, 0});
@@ -306,7 +306,7 @@ __device__ __forceinline__ void pipe_tail(const kctx &P, uint8_t *R, uint32_t ro
 
 
 // The plain forward of a fast adjacency f (fwd4_nhf as 4 words): the same
-// steps and results as pipe_tail for such a nexthop -- ip_forward
+// steps and results as chain_tail for such a nexthop -- ip_forward
 // (ip_forward.c:21-33), the MTU/DF check (ip_output.c:159-166), eth_output
 // (eth_output.c:297-316) and iface_output to port_output.
 __device__ __forceinline__ void fast_tail(uint8_t *R, uint32_t row, result &r, uint32_t data_len, uint32_t slot,

@@ -1,7 +1,7 @@
 // SPDX-License-Identifier: BSD-3-Clause
 //
 // fwd4_dev.h -- device helpers shared by the forwarding kernels
-// (fwd4_kernel.hip, fwd4_pipe.hip): table views, counter aggregation,
+// (fwd4_kernel.hip, fwd4_ring.hip): table views, counter aggregation,
 // vector loads and stores. Not a public header.
 #pragma once
 

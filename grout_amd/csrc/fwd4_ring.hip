@@ -7,15 +7,17 @@
 // the dependent lookups (RX view -> FIB -> adjacency) pays the HBM latency
 // of its streams at its first lookup. Here the two never share a wave:
 //
-//   wave 0      loader:  LDS-DMA (global_load_lds) of each 64-packet tile's
-//                        header lines and metadata into a ring slot,
-//                        RING_AHEAD tiles in flight, published behind a
-//                        counted vmcnt;
-//   waves 2..7  compute: the node chain of a tile out of its slot (only the
-//                        dependent lookups on their vmcnt), rewritten rows
-//                        and verdicts back into the slot;
-//   wave 1      storer:  drains finished slots to HBM (coalesced 16-byte
-//                        stores) and hands them back to the loader.
+//   loader waves:  LDS-DMA (global_load_lds) of each 64-packet tile's
+//                  header lines and metadata into a ring slot, AHEAD tiles
+//                  in flight per loader, published behind a counted vmcnt;
+//   compute waves: the node chain of a tile out of its slot (only the
+//                  dependent lookups on their vmcnt), rewritten rows and
+//                  verdicts back into the slot;
+//   storer waves:  drain finished slots to HBM (coalesced 16-byte stores)
+//                  and hand them back to the loaders.
+// The geometry (waves, loaders, storers, slots, AHEAD) is a ring_cfg; tile
+// k of a workgroup goes to loader k % LOADERS, compute wave k % COMPUTE,
+// storer k % STORERS and slot k % SLOTS.
 //
 // The hand-offs are LDS words with tile sequence numbers: ready[s] (loader
 // -> compute), done[s] (compute -> storer), free[s] (storer -> loader).
@@ -24,24 +26,42 @@
 // always drains. Tiles of a workgroup are b, b + G, b + 2G ... (G = grid).
 #include "fwd4_chain.h"
 
-#define RING_WAVES 8
-#define RING_COMPUTE (RING_WAVES - 2)
-#define RING_SLOTS 8
-#define RING_AHEAD 4 // tiles the loader keeps in flight before publishing
 #define RING_GLDS_PER_TILE 6 // 4 x 1 KiB of lines + 2 x 256 B of metadata
 #define RING_SPIN_MAX (1u << 24)
-#define RING_NHF_LDS_MAX 2304 // fast adjacencies staged in LDS (36 KiB: two workgroups per CU)
-// vmcnt that leaves RING_AHEAD - 1 tiles in flight (an asm literal)
-#define RING_VMCNT_AHEAD 18
-static_assert(RING_VMCNT_AHEAD == RING_GLDS_PER_TILE * (RING_AHEAD - 1), "ring vmcnt");
+#define RING_NHF_LDS_MAX 2304 // fast adjacencies staged in LDS (36 KiB)
 
+template <int WAVES_, int LOADERS_, int STORERS_, int SLOTS_, int AHEAD_>
+struct ring_cfg {
+	static constexpr uint32_t WAVES = WAVES_, LOADERS = LOADERS_, STORERS = STORERS_;
+	static constexpr uint32_t COMPUTE = WAVES_ - LOADERS_ - STORERS_;
+	static constexpr uint32_t SLOTS = SLOTS_, AHEAD = AHEAD_;
+	// vmcnt that leaves AHEAD - 1 tiles of one loader in flight
+	static constexpr int VMCNT_AHEAD = RING_GLDS_PER_TILE * (AHEAD_ - 1);
+	static_assert(COMPUTE >= 1 && SLOTS_ >= LOADERS_ * AHEAD_ && VMCNT_AHEAD <= 63, "ring geometry");
+};
+
+// The measured geometries (gr_hip_tune "ring"); 0 is the default.
+typedef ring_cfg<8, 1, 1, 8, 4> ring_cfg0;
+typedef ring_cfg<8, 2, 1, 8, 3> ring_cfg1;
+typedef ring_cfg<16, 2, 2, 16, 4> ring_cfg2;
+typedef ring_cfg<12, 2, 1, 12, 4> ring_cfg3;
+typedef ring_cfg<8, 1, 1, 8, 6> ring_cfg4;
+typedef ring_cfg<16, 2, 2, 16, 6> ring_cfg5;
+#define RING_NCFG 6
+
+template <class C>
 struct ring_lds {
-	uint8_t lines[RING_SLOTS][64 * 64]; // the tile's header lines (fwd4_chain.h image)
-	u2v meta[RING_SLOTS][64]; // gr_hip_pkt_meta
-	u2v verdict[RING_SLOTS][64];
-	uint32_t ready[RING_SLOTS], done[RING_SLOTS], free_[RING_SLOTS];
+	uint8_t lines[C::SLOTS][64 * 64]; // the tile's header lines (fwd4_chain.h image)
+	u2v meta[C::SLOTS][64]; // gr_hip_pkt_meta
+	u2v verdict[C::SLOTS][64];
+	uint32_t ready[C::SLOTS], done[C::SLOTS], free_[C::SLOTS];
 	uint32_t abort;
 };
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+	asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
 	return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
@@ -88,7 +108,8 @@ __device__ __forceinline__ void flag_set(uint32_t *f, uint32_t v) {
 }
 
 // Wait until *f >= want. False when the wait gave up or another wave did.
-__device__ __forceinline__ bool flag_wait(ring_lds &L, const uint32_t *f, uint32_t want) {
+template <class L_t>
+__device__ __forceinline__ bool flag_wait(L_t &L, const uint32_t *f, uint32_t want) {
 	for (uint32_t spin = 0;; spin++) {
 		if ((int32_t)(flag_get(f) - want) >= 0)
 			return true;
@@ -102,21 +123,21 @@ __device__ __forceinline__ bool flag_wait(ring_lds &L, const uint32_t *f, uint32
 	}
 }
 
-template <bool NT>
-__device__ void ring_loader(const fwd4_params &A, ring_lds &L, uint32_t n_local, uint32_t lane) {
+template <class C, bool NT>
+__device__ void ring_loader(const fwd4_params &A, ring_lds<C> &L, uint32_t n_local, uint32_t j, uint32_t lane) {
 	const uint32_t G = gridDim.x;
 	const uint32_t prow = lane >> 2;
 	const uint32_t pchunk = (lane & 3) ^ ((lane >> 4) & 3); // chunk this lane lands in slot lane & 3
-	uint32_t pub = 0;
+	uint32_t pub = j; // oldest of this loader's tiles not yet published
 	bool ok = true;
-	for (uint32_t k = 0; k < n_local && ok; k++) {
-		const uint32_t s = k % RING_SLOTS;
-		if (k >= RING_SLOTS && (int32_t)(flag_get(&L.free_[s]) - (k - RING_SLOTS + 1)) < 0) {
+	for (uint32_t k = j; k < n_local && ok; k += C::LOADERS) {
+		const uint32_t s = k % C::SLOTS;
+		if (k >= C::SLOTS && (int32_t)(flag_get(&L.free_[s]) - (k - C::SLOTS + 1)) < 0) {
 			// ring full: publish what is in flight, then wait for the storer
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-			for (; pub < k; pub++)
-				flag_set(&L.ready[pub % RING_SLOTS], pub + 1);
-			ok = flag_wait(L, &L.free_[s], k - RING_SLOTS + 1);
+			wait_vmcnt<0>();
+			for (; pub < k; pub += C::LOADERS)
+				flag_set(&L.ready[pub % C::SLOTS], pub + 1);
+			ok = flag_wait(L, &L.free_[s], k - C::SLOTS + 1);
 			if (!ok)
 				break;
 		}
@@ -124,53 +145,53 @@ __device__ void ring_loader(const fwd4_params &A, ring_lds &L, uint32_t n_local,
 		const uint32_t base = t * 64, cnt = min(64u, A.n - base);
 		const uint32_t lb = lds_addr(L.lines[s]);
 #pragma unroll
-		for (uint32_t j = 0; j < 4; j++) {
-			const uint32_t r = j * 16 + prow;
+		for (uint32_t q = 0; q < 4; q++) {
+			const uint32_t r = q * 16 + prow;
 			if (r < cnt)
-				glds16<NT>(A.in + (size_t)(base + r) * A.in_stride + pchunk * 16, lb + j * 1024);
+				glds16<NT>(A.in + (size_t)(base + r) * A.in_stride + pchunk * 16, lb + q * 1024);
 		}
 		const uint32_t mb = lds_addr(L.meta[s]);
 		const uint8_t *msrc = reinterpret_cast<const uint8_t *>(A.meta + base);
 #pragma unroll
-		for (uint32_t j = 0; j < 2; j++)
-			if (j * 32 + (lane >> 1) < cnt)
-				glds4<NT>(msrc + j * 256 + lane * 4, mb + j * 256);
-		if (k + 1 - pub == RING_AHEAD) {
-			asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); // RING_VMCNT_AHEAD
-			flag_set(&L.ready[pub % RING_SLOTS], pub + 1);
-			pub++;
+		for (uint32_t q = 0; q < 2; q++)
+			if (q * 32 + (lane >> 1) < cnt)
+				glds4<NT>(msrc + q * 256 + lane * 4, mb + q * 256);
+		if (k - pub == (C::AHEAD - 1) * C::LOADERS) {
+			wait_vmcnt<C::VMCNT_AHEAD>();
+			flag_set(&L.ready[pub % C::SLOTS], pub + 1);
+			pub += C::LOADERS;
 		}
 	}
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	wait_vmcnt<0>();
 	if (ok)
-		for (; pub < n_local; pub++)
-			flag_set(&L.ready[pub % RING_SLOTS], pub + 1);
+		for (; pub < n_local; pub += C::LOADERS)
+			flag_set(&L.ready[pub % C::SLOTS], pub + 1);
 }
 
-template <bool NT>
-__device__ void ring_storer(const fwd4_params &A, ring_lds &L, uint32_t n_local, uint32_t lane) {
+template <class C, bool NT>
+__device__ void ring_storer(const fwd4_params &A, ring_lds<C> &L, uint32_t n_local, uint32_t j, uint32_t lane) {
 	const uint32_t G = gridDim.x;
 	const uint32_t prow = lane >> 2, part = lane & 3;
 	const uint32_t pslot = (part ^ ((lane >> 4) & 3)) << 4;
-	for (uint32_t k = 0; k < n_local; k++) {
-		const uint32_t s = k % RING_SLOTS;
+	for (uint32_t k = j; k < n_local; k += C::STORERS) {
+		const uint32_t s = k % C::SLOTS;
 		if (!flag_wait(L, &L.done[s], k + 1))
 			break;
 		const uint32_t t = blockIdx.x + k * G;
 		const uint32_t base = t * 64, cnt = min(64u, A.n - base);
 		u4v o[4];
 #pragma unroll
-		for (uint32_t j = 0; j < 4; j++)
-			o[j] = *reinterpret_cast<const u4v *>(&L.lines[s][(j * 16 + prow) * 64 + pslot]);
+		for (uint32_t q = 0; q < 4; q++)
+			o[q] = *reinterpret_cast<const u4v *>(&L.lines[s][(q * 16 + prow) * 64 + pslot]);
 		const u2v v = L.verdict[s][lane];
 		// the registers hold the tile: hand the slot back before storing
 		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 		flag_set(&L.free_[s], k + 1);
 #pragma unroll
-		for (uint32_t j = 0; j < 4; j++) {
-			const uint32_t r = j * 16 + prow;
+		for (uint32_t q = 0; q < 4; q++) {
+			const uint32_t r = q * 16 + prow;
 			if (r < cnt)
-				st16<NT>(A.out + (size_t)(base + r) * A.out_stride + part * 16, o[j]);
+				st16<NT>(A.out + (size_t)(base + r) * A.out_stride + part * 16, o[q]);
 		}
 		if (lane < cnt) {
 			u2v *vp = reinterpret_cast<u2v *>(A.verdicts + base + lane);
@@ -182,12 +203,12 @@ __device__ void ring_storer(const fwd4_params &A, ring_lds &L, uint32_t n_local,
 	}
 }
 
-template <bool STATS>
-__device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds &L, stat_slot *slots, const uint4 *nhf_lds,
-			     uint32_t n_local, uint32_t c, uint32_t lane) {
+template <class C, bool STATS>
+__device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds<C> &L, stat_slot *slots,
+			     const uint4 *nhf_lds, uint32_t n_local, uint32_t c, uint32_t lane) {
 	const uint32_t G = gridDim.x;
-	for (uint32_t k = c; k < n_local; k += RING_COMPUTE) {
-		const uint32_t s = k % RING_SLOTS;
+	for (uint32_t k = c; k < n_local; k += C::COMPUTE) {
+		const uint32_t s = k % C::SLOTS;
 		if (!flag_wait(L, &L.ready[s], k + 1))
 			break;
 		const uint32_t t = blockIdx.x + k * G;
@@ -213,8 +234,8 @@ __device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds &L, s
 		if (live) {
 			uint32_t dst = 0, data_len = 0;
 			const uint8_t *frame = A.in + (size_t)(base + lane) * A.in_stride;
-			if (pipe_head(P, R, lane, m, rx, r, dst, data_len, frame)) {
-				const uint32_t slot = pipe_fib(rx, dst);
+			if (chain_head(P, R, lane, m, rx, r, dst, data_len, frame)) {
+				const uint32_t slot = chain_fib(rx, dst);
 				if (slot == 0 || slot > P.max_nh) {
 					r.edge = GR_HIP_E_IP_ERROR_DEST_UNREACH; // NO_ROUTE :150-153
 				} else {
@@ -224,7 +245,7 @@ __device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds &L, s
 						fast_tail(R, lane, r, data_len, slot, f);
 					} else {
 						const uint4 *ap = reinterpret_cast<const uint4 *>(P.adj + slot);
-						pipe_tail(P, R, lane, m, rx.flags, r, dst, data_len, slot, gld4(ap), gld4(ap + 1));
+						chain_tail(P, R, lane, m, rx.flags, r, dst, data_len, slot, gld4(ap), gld4(ap + 1));
 					}
 				}
 			}
@@ -241,9 +262,9 @@ __device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds &L, s
 	}
 }
 
-template <bool STATS, bool NT>
-__global__ void __launch_bounds__(RING_WAVES * 64) gr_fwd4_ring(const fwd4_params A) {
-	__shared__ __attribute__((aligned(16))) ring_lds L;
+template <class C, bool STATS, bool NT>
+__global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params A) {
+	__shared__ __attribute__((aligned(16))) ring_lds<C> L;
 	__shared__ stat_slot slots[FWD4_STAT_SLOTS];
 	__shared__ fwd4_edges edges;
 	extern __shared__ __attribute__((aligned(16))) uint4 nhf_lds[]; // [A.nhf_lds]: slots 1..
@@ -253,13 +274,12 @@ __global__ void __launch_bounds__(RING_WAVES * 64) gr_fwd4_ring(const fwd4_param
 
 	{
 		const uint4 *src = reinterpret_cast<const uint4 *>(T->nhf) + 1;
-		for (uint32_t i = tid; i < A.nhf_lds; i += RING_WAVES * 64)
+		for (uint32_t i = tid; i < A.nhf_lds; i += C::WAVES * 64)
 			nhf_lds[i] = gld4(src + i);
 	}
-
-	for (uint32_t i = tid; i < sizeof(fwd4_edges); i += RING_WAVES * 64)
+	for (uint32_t i = tid; i < sizeof(fwd4_edges); i += C::WAVES * 64)
 		reinterpret_cast<uint8_t *>(&edges)[i] = reinterpret_cast<const uint8_t *>(&T->edges)[i];
-	if (tid < RING_SLOTS) {
+	if (tid < C::SLOTS) {
 		L.ready[tid] = 0;
 		L.done[tid] = 0;
 		L.free_[tid] = 0;
@@ -275,13 +295,13 @@ __global__ void __launch_bounds__(RING_WAVES * 64) gr_fwd4_ring(const fwd4_param
 
 	const uint32_t n_tiles = (A.n + 63) >> 6;
 	const uint32_t n_local = blockIdx.x < n_tiles ? (n_tiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
-	if (wv == 0) {
-		ring_loader<NT>(A, L, n_local, lane);
-	} else if (wv == 1) {
-		ring_storer<NT>(A, L, n_local, lane);
+	if (wv < C::LOADERS) {
+		ring_loader<C, NT>(A, L, n_local, wv, lane);
+	} else if (wv < C::LOADERS + C::STORERS) {
+		ring_storer<C, NT>(A, L, n_local, wv - C::LOADERS, lane);
 	} else {
 		kctx P = make_kctx(A, &edges);
-		ring_compute<STATS>(A, P, L, slots, nhf_lds, n_local, wv - 2, lane);
+		ring_compute<C, STATS>(A, P, L, slots, nhf_lds, n_local, wv - C::LOADERS - C::STORERS, lane);
 	}
 
 	if (STATS) {
@@ -294,17 +314,22 @@ __global__ void __launch_bounds__(RING_WAVES * 64) gr_fwd4_ring(const fwd4_param
 }
 
 typedef void (*fwd4_rfn)(const fwd4_params);
-static const fwd4_rfn ring_kernels[4] = {
-	gr_fwd4_ring<false, false>,
-	gr_fwd4_ring<true, false>,
-	gr_fwd4_ring<false, true>,
-	gr_fwd4_ring<true, true>,
+struct ring_entry {
+	fwd4_rfn fn[4]; // by FWD4_V_STATS | FWD4_V_NT
+	uint32_t threads;
+};
+#define RING_ENTRY(C) {{gr_fwd4_ring<C, false, false>, gr_fwd4_ring<C, true, false>, gr_fwd4_ring<C, false, true>, \
+			 gr_fwd4_ring<C, true, true>}, C::WAVES * 64}
+static const ring_entry ring_kernels[RING_NCFG] = {
+	RING_ENTRY(ring_cfg0), RING_ENTRY(ring_cfg1), RING_ENTRY(ring_cfg2),
+	RING_ENTRY(ring_cfg3), RING_ENTRY(ring_cfg4), RING_ENTRY(ring_cfg5),
 };
 
-// variant: FWD4_V_STATS | FWD4_V_NT; one workgroup walks tiles b, b + grid, ...
-// A->nhf_lds fast adjacencies are staged in dynamic LDS.
-extern "C" hipError_t gr_fwd4_ring_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant) {
-	hipLaunchKernelGGL(ring_kernels[variant & 3], dim3(grid), dim3(RING_WAVES * 64), A->nhf_lds * sizeof(fwd4_nhf), s, *A);
+// variant: FWD4_V_STATS | FWD4_V_NT; cfg: ring geometry. A->nhf_lds fast
+// adjacencies are staged in dynamic LDS.
+extern "C" hipError_t gr_fwd4_ring_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant, int cfg) {
+	const ring_entry &e = ring_kernels[(unsigned)cfg % RING_NCFG];
+	hipLaunchKernelGGL(e.fn[variant & 3], dim3(grid), dim3(e.threads), A->nhf_lds * sizeof(fwd4_nhf), s, *A);
 	return hipGetLastError();
 }
 
@@ -312,10 +337,15 @@ extern "C" uint32_t gr_fwd4_ring_nhf_max(void) {
 	return RING_NHF_LDS_MAX;
 }
 
-extern "C" int gr_fwd4_ring_occupancy(int variant, uint32_t nhf_lds) {
+extern "C" int gr_fwd4_ring_ncfg(void) {
+	return RING_NCFG;
+}
+
+extern "C" int gr_fwd4_ring_occupancy(int variant, int cfg, uint32_t nhf_lds) {
+	const ring_entry &e = ring_kernels[(unsigned)cfg % RING_NCFG];
 	int b = 0;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, ring_kernels[variant & 3], RING_WAVES * 64,
-							 nhf_lds * sizeof(fwd4_nhf)) != hipSuccess) {
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, e.fn[variant & 3], (int)e.threads, nhf_lds * sizeof(fwd4_nhf))
+	    != hipSuccess) {
 		(void)hipGetLastError();
 		return 0;
 	}

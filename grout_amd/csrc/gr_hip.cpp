@@ -26,16 +26,14 @@
 extern "C" hipError_t gr_fwd4_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant);
 extern "C" int gr_fwd4_occupancy(int variant);
 extern "C" uint32_t gr_fwd4_tile(int variant);
-extern "C" hipError_t gr_fwd4_pipe_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant);
-extern "C" int gr_fwd4_pipe_occupancy(int variant);
-extern "C" hipError_t gr_fwd4_ring_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant);
-extern "C" int gr_fwd4_ring_occupancy(int variant, uint32_t nhf_lds);
+extern "C" hipError_t gr_fwd4_ring_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant, int cfg);
+extern "C" int gr_fwd4_ring_occupancy(int variant, int cfg, uint32_t nhf_lds);
 extern "C" uint32_t gr_fwd4_ring_nhf_max(void);
+extern "C" int gr_fwd4_ring_ncfg(void);
 #define RING_WG_PER_CU 2 // default workgroups per CU of the ring kernel (measured)
-#define PIPE_WG_PACKETS 256 // fwd4_pipe.hip: 4 waves x 64-packet tiles
 
 // Forwarding kernels (gr_hip_tune "kernel")
-enum { KERNEL_TILE = 0, KERNEL_PIPE = 1, KERNEL_RING = 2 };
+enum { KERNEL_TILE = 0, KERNEL_RING = 2 }; // 1 was a software-pipelined kernel, retired
 
 #define HCK(expr)                                                                                  \
 	do {                                                                                       \
@@ -123,9 +121,10 @@ struct gr_hip_ctx {
 	int occ[8];
 	int tile64; // FWD4_V_TILE64
 	int kernel; // KERNEL_*
-	int occ_pipe[4];
-	int occ_ring[4]; // at occ_ring_nhf staged fast adjacencies
+	int ring_cfg; // ring geometry (fwd4_ring.hip ring_cfgN)
+	int occ_ring[4]; // at occ_ring_nhf staged fast adjacencies, geometry occ_ring_cfg
 	uint32_t occ_ring_nhf;
+	int occ_ring_cfg;
 };
 
 // ---------------------------------------------------------------------------
@@ -437,11 +436,11 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->kernel = KERNEL_RING;
 	for (int v = 0; v < 8; v++)
 		c->occ[v] = gr_fwd4_occupancy(v);
+	c->ring_cfg = 1; // 2 loaders, 1 storer, 5 compute waves, 8 slots
 	for (int v = 0; v < 4; v++)
-		c->occ_pipe[v] = gr_fwd4_pipe_occupancy(v);
-	for (int v = 0; v < 4; v++)
-		c->occ_ring[v] = gr_fwd4_ring_occupancy(v, 0);
+		c->occ_ring[v] = gr_fwd4_ring_occupancy(v, 0, 0);
 	c->occ_ring_nhf = 0;
+	c->occ_ring_cfg = 0;
 	ret = -EIO;
 	if (upload_tables(c) != 0)
 		goto fail;
@@ -1004,10 +1003,11 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 		int variant = (stats ? FWD4_V_STATS : 0) | c->nt;
 		uint32_t tiles = (b->n + 63) / 64;
 		A.nhf_lds = c->nh_hi < gr_fwd4_ring_nhf_max() ? c->nh_hi : gr_fwd4_ring_nhf_max();
-		if (A.nhf_lds != c->occ_ring_nhf) {
+		if (A.nhf_lds != c->occ_ring_nhf || c->ring_cfg != c->occ_ring_cfg) {
 			for (int v = 0; v < 4; v++)
-				c->occ_ring[v] = gr_fwd4_ring_occupancy(v, A.nhf_lds);
+				c->occ_ring[v] = gr_fwd4_ring_occupancy(v, c->ring_cfg, A.nhf_lds);
 			c->occ_ring_nhf = A.nhf_lds;
+			c->occ_ring_cfg = c->ring_cfg;
 		}
 		uint32_t per_cu = c->wg_per_cu > 0 ? (uint32_t)c->wg_per_cu : RING_WG_PER_CU;
 		if (c->occ_ring[variant] > 0 && per_cu > (uint32_t)c->occ_ring[variant])
@@ -1017,18 +1017,7 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 			grid = tiles;
 		if (timed)
 			HCK(hipEventRecord(q->ev0[slot], s));
-		HCK(gr_fwd4_ring_launch(&A, grid, s, variant));
-	} else if (c->kernel == KERNEL_PIPE) {
-		// every wave strides over 64-packet tiles: one resident round of workgroups
-		int variant = (stats ? FWD4_V_STATS : 0) | c->nt;
-		uint32_t wgs = (b->n + PIPE_WG_PACKETS - 1) / PIPE_WG_PACKETS;
-		uint32_t per_cu = c->wg_per_cu > 0 ? (uint32_t)c->wg_per_cu : (uint32_t)(c->occ_pipe[variant] > 0 ? c->occ_pipe[variant] : 1);
-		uint32_t grid = (uint32_t)c->n_cu * per_cu;
-		if (grid > wgs)
-			grid = wgs;
-		if (timed)
-			HCK(hipEventRecord(q->ev0[slot], s));
-		HCK(gr_fwd4_pipe_launch(&A, grid, s, variant));
+		HCK(gr_fwd4_ring_launch(&A, grid, s, variant, c->ring_cfg));
 	} else {
 		int variant = (stats ? FWD4_V_STATS : 0) | c->nt | c->tile64;
 		uint32_t tile = gr_fwd4_tile(variant);
@@ -1065,15 +1054,17 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		c->wg_per_cu = value;
 	} else if (strcmp(key, "fib16") == 0) { // takes effect at the next commit
 		c->fib16 = value != 0;
-	} else if (strcmp(key, "kernel") == 0) { // 0: fwd4_kernel.hip, 1: fwd4_pipe.hip, 2: fwd4_ring.hip
-		if (value < KERNEL_TILE || value > KERNEL_RING)
+	} else if (strcmp(key, "ring") == 0) { // ring geometry, fwd4_ring.hip ring_cfgN
+		if (value < 0 || value >= gr_fwd4_ring_ncfg())
+			return -EINVAL;
+		c->ring_cfg = value;
+	} else if (strcmp(key, "kernel") == 0) { // 0: fwd4_kernel.hip, 2: fwd4_ring.hip
+		if (value != KERNEL_TILE && value != KERNEL_RING)
 			return -EINVAL;
 		c->kernel = value;
 	} else if (strcmp(key, "occupancy") == 0) { // read-only: WGs/CU of the current variant
 		if (c->kernel == KERNEL_RING)
 			return c->occ_ring[(c->stats_on ? FWD4_V_STATS : 0) | c->nt]; // as of the last launch
-		if (c->kernel == KERNEL_PIPE)
-			return c->occ_pipe[(c->stats_on ? FWD4_V_STATS : 0) | c->nt];
 		return c->occ[(c->stats_on ? FWD4_V_STATS : 0) | c->nt | c->tile64];
 	} else {
 		return -ENOENT;

@@ -193,11 +193,10 @@ def test_kernel_timing_api(fastpath):
 
 @pytest.mark.parametrize("kernel,nt,stats,wg,fib16,tile", [
     (0, 1, 1, 0, 1, 64), (0, 1, 0, 6, 1, 256), (0, 0, 1, 4, 0, 64), (0, 0, 1, 0, 0, 256), (0, 1, 1, 8, 1, 64),
-    (1, 1, 1, 0, 1, 256), (1, 0, 0, 1, 1, 256), (1, 1, 0, 2, 0, 256), (1, 0, 1, 0, 0, 256),
     (2, 1, 1, 0, 1, 256), (2, 0, 0, 1, 1, 256), (2, 1, 0, 2, 0, 256), (2, 0, 1, 0, 0, 256)])
 def test_kernel_variants(fastpath, kernel, nt, stats, wg, fib16, tile):
-    """Every tuning variant (gr_hip_tune) forwards bit-exact: the three
-    kernels (0: fwd4_kernel.hip, 1: fwd4_pipe.hip, 2: fwd4_ring.hip);
+    """Every tuning variant (gr_hip_tune) forwards bit-exact: both kernels
+    (0: fwd4_kernel.hip, 2: fwd4_ring.hip);
     wg_per_cu 1-2 making every wave / workgroup walk many tiles (a deep
     ring, wrap-around of every slot)."""
     t, _ = SC.corpus_topology()
@@ -302,3 +301,27 @@ def test_many_nexthops_fast_adjacency(fastpath, kernel):
         assert (g[1]["nh"] > 2304).sum() > len(me) // 4
     finally:
         fastpath.tune("kernel", 2)
+
+
+@pytest.mark.parametrize("cfg", range(6))
+def test_ring_geometries(fastpath, cfg):
+    """Every ring geometry (loaders / storers / slots / tiles in flight) of
+    fwd4_ring.hip forwards bit-exact; wg_per_cu 1 makes each workgroup walk
+    its ring many times round."""
+    t, _ = SC.corpus_topology()
+    fr, me, lab = SC.corpus_arrays()
+    tf = _fullview()
+    fr2, me2 = S.stream(1 << 20, 0xC0F + cfg, routes=tf.route_array())
+    o1 = oracle.Oracle(t).process(fr, me)
+    o2 = oracle.Oracle(tf).process(fr2, me2)
+    fastpath.tune("kernel", 2)
+    fastpath.tune("ring", cfg)
+    fastpath.tune("wg_per_cu", 1)
+    try:
+        compare(o1, run_gpu(fastpath, t, fr, me), lab)
+        compare(o2, run_gpu(fastpath, tf, fr2, me2))
+        n = 64 * 1000 + 17  # ragged last tile; some workgroups get one tile more than others
+        compare(oracle.Oracle(tf).process(fr2[:n], me2[:n]), run_gpu(fastpath, tf, fr2[:n], me2[:n]))
+    finally:
+        fastpath.tune("ring", 1)
+        fastpath.tune("wg_per_cu", 0)

@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 24)
     ap.add_argument("--workload", default="fullview64", choices=["fullview64", "single64"])
-    ap.add_argument("--kernel", type=int, default=None, help="gr_hip_tune kernel: 0 tile, 1 pipe, 2 ring")
+    ap.add_argument("--kernel", type=int, default=None, help="gr_hip_tune kernel: 0 tile, 2 ring")
     ap.add_argument("--wg", type=int, default=None, help="gr_hip_tune wg_per_cu")
     ap.add_argument("--stats", type=int, default=None)
     ap.add_argument("--nt", type=int, default=None)
