@@ -24,11 +24,15 @@ $(BUILD)/gr_hip.o: $(CSRC)/gr_hip.cpp $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
+$(BUILD)/gr_node.o: $(CSRC)/gr_node.cpp include/grout_hip.h
+	@mkdir -p $(BUILD)
+	$(CXX) -O3 -march=x86-64-v3 -fPIC -Wall -Wextra -std=c++17 -c -o $@ $<
+
 $(BUILD)/fib4.o: $(CSRC)/fib4.c $(CSRC)/fib4.h
 	@mkdir -p $(BUILD)
 	$(CC) $(CFLAGS_HOST) -c -o $@ $<
 
-$(LIB_HIP): $(BUILD)/fwd4_kernel.o $(BUILD)/fwd4_ring.o $(BUILD)/gr_hip.o $(BUILD)/fib4.o
+$(LIB_HIP): $(BUILD)/fwd4_kernel.o $(BUILD)/fwd4_ring.o $(BUILD)/gr_hip.o $(BUILD)/gr_node.o $(BUILD)/fib4.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 $(LIB_HOST): $(CSRC)/fib4.c $(CSRC)/synth.c $(CSRC)/fib4.h $(CSRC)/synth.h include/grout_hip.h

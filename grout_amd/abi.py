@@ -76,6 +76,16 @@ STATS_DT = np.dtype([
 ])
 assert IFACE_DT.itemsize == 32 and NH_DT.itemsize == 32 and ROUTE_DT.itemsize == 12
 assert META_DT.itemsize == 8 and VERDICT_DT.itemsize == 8 and STATS_DT.itemsize == 32
+# struct gr_hip_mbuf: the node shim's view of an rte_mbuf + priv (grout_hip.h)
+MBUF_DT = np.dtype([("frame", "<u8"), ("pkt_len", "<u4"), ("data_len", "<u2"), ("data_off", "<u2"),
+                    ("packet_type", "<u4"), ("rss", "<u4"), ("iface", "<u2"), ("vlan_id", "<u2"),
+                    ("ck", "u1"), ("edge", "u1"), ("domain", "u1"), ("_pad", "u1"), ("nh", "<u4"),
+                    ("_pad1", "<u4")])
+assert MBUF_DT.itemsize == 40
+NODE_NAMES = ["iface_input", "eth_input", "ip_input", "ip_forward", "ip_output", "eth_output", "iface_output"]
+NODE_COUNT = len(NODE_NAMES)
+NODE_STATS_DT = np.dtype([("packets", "<u8", NODE_COUNT), ("calls", "<u8", NODE_COUNT)])
+PTYPE_L3_IPV4 = 0x1
 
 
 class Batch(ctypes.Structure):
@@ -138,6 +148,10 @@ HIP_API = {
     "gr_hip_dev_free": (_I, [_P, _P]),
     "gr_hip_memcpy_h2d": (_I, [_P, _P, _P, ctypes.c_size_t]),
     "gr_hip_memcpy_d2h": (_I, [_P, _P, _P, ctypes.c_size_t]),
+    "gr_hip_edge_node": (_I, [_U8, _U32]),
+    "gr_hip_node_stage": (_I, [_P, _U32, _P, _P]),
+    "gr_hip_node_apply": (_I, [_P, _U32, _P, _U32, _P, _P, _U32, _P, _U32, _U32, _P]),
+    "gr_hip_node_process": (_I, [_P, _P, _U32, _U32, _P]),
 }
 
 HOST_API = {

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <errno.h>
 #include <mutex>
+#include <shared_mutex>
 #include <new>
 #include <stdlib.h>
 #include <string.h>
@@ -86,13 +87,18 @@ struct gr_hip_queue {
 	hipEvent_t quiesce;
 	gr_hip_iface_stats *d_stats; // [FWD4_STAT_SHARDS][max_ifaces]
 	host_slot hs[HOST_SLOTS];
+	// gr_hip_node_process staging (pinned, grown on demand)
+	uint32_t node_cap;
+	uint8_t *node_lines, *node_out;
+	gr_hip_pkt_meta *node_meta;
+	gr_hip_verdict *node_v;
 };
 
 struct gr_hip_ctx {
 	int dev;
 	uint32_t max_ifaces, max_nh;
 	int n_cu;
-	std::mutex mu;
+	std::shared_mutex mu; // control-plane writers exclusive; node hand-back readers shared
 	hipStream_t ctl;
 	std::vector<gr_hip_iface> ifaces;
 	std::vector<gr_hip_nh> nh;
@@ -490,7 +496,7 @@ static bool edge_ok(uint8_t e) {
 extern "C" int gr_hip_edges_eth_type(gr_hip_ctx_t *c, uint16_t be_type, uint8_t edge) {
 	if (c == nullptr || !edge_ok(edge))
 		return -EINVAL;
-	std::lock_guard<std::mutex> l(c->mu);
+	std::lock_guard<std::shared_mutex> l(c->mu);
 	fwd4_edges &E = c->edges;
 	for (uint32_t i = 0; i < E.n_eth_types; i++) {
 		if (E.eth_type_be[i] == be_type) {
@@ -514,7 +520,7 @@ extern "C" int gr_hip_edges_eth_type(gr_hip_ctx_t *c, uint16_t be_type, uint8_t 
 	extern "C" int fn(gr_hip_ctx_t *c, uint8_t key, uint8_t edge) {                            \
 		if (c == nullptr || key >= (limit) || !edge_ok(edge))                              \
 			return -EINVAL;                                                            \
-		std::lock_guard<std::mutex> l(c->mu);                                              \
+		std::lock_guard<std::shared_mutex> l(c->mu);                                              \
 		c->edges.field[key] = edge;                                                        \
 		hipSetDevice(c->dev);                                                              \
 		int r = quiesce(c);                                                                \
@@ -577,7 +583,7 @@ extern "C" int gr_hip_iface_set(gr_hip_ctx_t *c, const struct gr_hip_iface *ifs,
 	for (uint32_t i = 0; i < n; i++)
 		if (ifs[i].id == 0 || ifs[i].id >= c->max_ifaces)
 			return -EINVAL;
-	std::lock_guard<std::mutex> l(c->mu);
+	std::lock_guard<std::shared_mutex> l(c->mu);
 	hipSetDevice(c->dev);
 	bool vlans = false;
 	for (uint32_t i = 0; i < n; i++) {
@@ -596,7 +602,7 @@ extern "C" int gr_hip_iface_set(gr_hip_ctx_t *c, const struct gr_hip_iface *ifs,
 extern "C" int gr_hip_iface_del(gr_hip_ctx_t *c, uint16_t id) {
 	if (c == nullptr || id == 0 || id >= c->max_ifaces)
 		return -EINVAL;
-	std::lock_guard<std::mutex> l(c->mu);
+	std::lock_guard<std::shared_mutex> l(c->mu);
 	hipSetDevice(c->dev);
 	bool vlan = c->ifaces[id].type == GR_HIP_IFACE_TYPE_VLAN;
 	c->ifaces[id] = gr_hip_iface {};
@@ -612,7 +618,7 @@ extern "C" int gr_hip_nh_set(gr_hip_ctx_t *c, uint32_t first, const struct gr_hi
 	if (c == nullptr || first == 0 || (nh == nullptr && n)
 	    || (uint64_t)first + n > (uint64_t)c->max_nh + 1)
 		return -EINVAL;
-	std::lock_guard<std::mutex> l(c->mu);
+	std::lock_guard<std::shared_mutex> l(c->mu);
 	hipSetDevice(c->dev);
 	memcpy(&c->nh[first], nh, (size_t)n * sizeof(*nh));
 	if (n && first + n - 1 > c->nh_hi)
@@ -626,7 +632,7 @@ extern "C" int gr_hip_nh_set(gr_hip_ctx_t *c, uint32_t first, const struct gr_hi
 extern "C" int gr_hip_reta_set(gr_hip_ctx_t *c, uint32_t first, const uint32_t *slots, uint32_t n) {
 	if (c == nullptr || (slots == nullptr && n) || (uint64_t)first + n > (1ull << 31))
 		return -EINVAL;
-	std::lock_guard<std::mutex> l(c->mu);
+	std::lock_guard<std::shared_mutex> l(c->mu);
 	hipSetDevice(c->dev);
 	if ((uint64_t)first + n > c->reta.size())
 		c->reta.resize((size_t)first + n, 0);
@@ -663,7 +669,7 @@ extern "C" int gr_hip_reta_set(gr_hip_ctx_t *c, uint32_t first, const uint32_t *
 extern "C" int gr_hip_fib4_create(gr_hip_ctx_t *c, uint16_t vrf, uint32_t max_routes, uint32_t num_tbl8) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
-	std::lock_guard<std::mutex> l(c->mu);
+	std::lock_guard<std::shared_mutex> l(c->mu);
 	hipSetDevice(c->dev);
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib != nullptr)
@@ -682,7 +688,7 @@ extern "C" int gr_hip_fib4_create(gr_hip_ctx_t *c, uint16_t vrf, uint32_t max_ro
 extern "C" int gr_hip_fib4_destroy(gr_hip_ctx_t *c, uint16_t vrf) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
-	std::lock_guard<std::mutex> l(c->mu);
+	std::lock_guard<std::shared_mutex> l(c->mu);
 	hipSetDevice(c->dev);
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib == nullptr)
@@ -709,7 +715,7 @@ extern "C" int gr_hip_fib4_destroy(gr_hip_ctx_t *c, uint16_t vrf) {
 extern "C" int gr_hip_route4_add(gr_hip_ctx_t *c, const struct gr_hip_route4 *rt, uint32_t n, int replace) {
 	if (c == nullptr || (rt == nullptr && n))
 		return -EINVAL;
-	std::lock_guard<std::mutex> l(c->mu);
+	std::lock_guard<std::shared_mutex> l(c->mu);
 	for (uint32_t i = 0; i < n; i++) {
 		if (rt[i].vrf_id == 0 || rt[i].vrf_id >= c->max_ifaces || rt[i].nh == 0
 		    || rt[i].nh > c->max_nh)
@@ -729,7 +735,7 @@ extern "C" int gr_hip_route4_add(gr_hip_ctx_t *c, const struct gr_hip_route4 *rt
 extern "C" int gr_hip_route4_del(gr_hip_ctx_t *c, uint16_t vrf, uint32_t ip, uint8_t len) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
-	std::lock_guard<std::mutex> l(c->mu);
+	std::lock_guard<std::shared_mutex> l(c->mu);
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib == nullptr)
 		return -ENONET;
@@ -763,7 +769,7 @@ static uint16_t to16(uint32_t e) { // fib4.h 4-byte entry -> 2-byte entry
 extern "C" int gr_hip_fib4_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
-	std::lock_guard<std::mutex> l(c->mu);
+	std::lock_guard<std::shared_mutex> l(c->mu);
 	hipSetDevice(c->dev);
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib == nullptr)
@@ -881,7 +887,7 @@ extern "C" int gr_hip_fib4_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 extern "C" int gr_hip_fib4_lookup_host(gr_hip_ctx_t *c, uint16_t vrf, uint32_t ip_be, uint32_t *nh) {
 	if (c == nullptr || nh == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
-	std::lock_guard<std::mutex> l(c->mu);
+	std::lock_guard<std::shared_mutex> l(c->mu);
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib == nullptr)
 		return -ENONET;
@@ -892,7 +898,7 @@ extern "C" int gr_hip_fib4_lookup_host(gr_hip_ctx_t *c, uint16_t vrf, uint32_t i
 extern "C" int gr_hip_fib4_info(gr_hip_ctx_t *c, uint16_t vrf, uint32_t *n_routes, uint32_t *tbl8_used, uint64_t *bytes) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
-	std::lock_guard<std::mutex> l(c->mu);
+	std::lock_guard<std::shared_mutex> l(c->mu);
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib == nullptr)
 		return -ENONET;
@@ -913,7 +919,7 @@ extern "C" int gr_hip_fib4_info(gr_hip_ctx_t *c, uint16_t vrf, uint32_t *n_route
 extern "C" int gr_hip_queue_create(gr_hip_ctx_t *c, void *stream, gr_hip_queue_t **out) {
 	if (c == nullptr || out == nullptr)
 		return -EINVAL;
-	std::lock_guard<std::mutex> l(c->mu);
+	std::lock_guard<std::shared_mutex> l(c->mu);
 	hipSetDevice(c->dev);
 	gr_hip_queue *q = new (std::nothrow) gr_hip_queue();
 	if (q == nullptr)
@@ -965,6 +971,10 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 	}
 	hipEventDestroy(q->quiesce);
 	hipFree(q->d_stats);
+	hipHostFree(q->node_lines);
+	hipHostFree(q->node_out);
+	hipHostFree(q->node_meta);
+	hipHostFree(q->node_v);
 	if (q->own_stream)
 		hipStreamDestroy(q->s);
 	(void)hipGetLastError();
@@ -1039,7 +1049,7 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 	if (c == nullptr || key == nullptr)
 		return -EINVAL;
-	std::lock_guard<std::mutex> l(c->mu);
+	std::lock_guard<std::shared_mutex> l(c->mu);
 	if (strcmp(key, "nt") == 0) {
 		c->nt = value ? FWD4_V_NT : 0;
 	} else if (strcmp(key, "stats") == 0) {
@@ -1174,6 +1184,43 @@ extern "C" int gr_hip_fwd4_host(
 		HCK(hipStreamSynchronize(h.s));
 	}
 	return 0;
+}
+
+// The node's walk (include/grout_hip.h, "rte_graph node shim"): stage the
+// mbufs' header lines into the queue's pinned buffers, forward them on the
+// GPU, hand them back with the context's iface / nexthop mirrors.
+extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst,
+				   struct gr_hip_node_stats *stats) {
+	if (q == nullptr || (n && m == nullptr))
+		return -EINVAL;
+	if (n == 0)
+		return 0;
+	gr_hip_ctx *c = q->ctx;
+	if (n > q->node_cap) {
+		hipSetDevice(c->dev);
+		hipHostFree(q->node_lines);
+		hipHostFree(q->node_out);
+		hipHostFree(q->node_meta);
+		hipHostFree(q->node_v);
+		q->node_lines = q->node_out = nullptr;
+		q->node_meta = nullptr;
+		q->node_v = nullptr;
+		q->node_cap = 0;
+		HCK(hipHostMalloc((void **)&q->node_lines, (size_t)n * GR_HIP_LINE, hipHostMallocDefault));
+		HCK(hipHostMalloc((void **)&q->node_out, (size_t)n * GR_HIP_LINE, hipHostMallocDefault));
+		HCK(hipHostMalloc((void **)&q->node_meta, (size_t)n * sizeof(gr_hip_pkt_meta), hipHostMallocDefault));
+		HCK(hipHostMalloc((void **)&q->node_v, (size_t)n * sizeof(gr_hip_verdict), hipHostMallocDefault));
+		q->node_cap = n;
+	}
+	int r = gr_hip_node_stage(m, n, q->node_lines, q->node_meta);
+	if (r < 0)
+		return r;
+	r = gr_hip_fwd4_host(q, q->node_lines, q->node_meta, n, q->node_out, q->node_v);
+	if (r < 0)
+		return r;
+	std::shared_lock<std::shared_mutex> l(c->mu);
+	return gr_hip_node_apply(m, n, q->node_out, GR_HIP_LINE, q->node_v, c->ifaces.data(), c->max_ifaces, c->nh.data(),
+				 (uint32_t)c->nh.size(), burst, stats);
 }
 
 extern "C" int gr_hip_queue_stats(gr_hip_queue_t *q, struct gr_hip_iface_stats *st, uint32_t max, int reset) {

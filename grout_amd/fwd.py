@@ -144,6 +144,15 @@ class Queue:
         check("gr_hip_fwd4_host", self.lib.gr_hip_fwd4_host(self._h, ptr(lines), ptr(meta), n, ptr(out_lines), ptr(verdicts)))
         return out_lines, verdicts
 
+    def node_process(self, mbufs, burst=64):
+        """The rte_graph node's walk over host mbuf views (abi.MBUF_DT, frame
+        pointers into host memory): stage, forward, hand back in place.
+        Returns the per-node counters of this call (abi.NODE_STATS_DT)."""
+        assert mbufs.dtype == abi.MBUF_DT and mbufs.flags["C_CONTIGUOUS"]
+        ns = np.zeros(1, dtype=abi.NODE_STATS_DT)
+        check("gr_hip_node_process", self.lib.gr_hip_node_process(self._h, ptr(mbufs), len(mbufs), burst, ptr(ns)))
+        return ns[0]
+
     def stats(self, reset=False):
         st = np.zeros(self.fp.max_ifaces, dtype=abi.STATS_DT)
         check("gr_hip_queue_stats", self.lib.gr_hip_queue_stats(self._h, ptr(st), len(st), 1 if reset else 0))

@@ -383,6 +383,90 @@ int gr_hip_dev_free(gr_hip_ctx_t *, void *dptr);
 int gr_hip_memcpy_h2d(gr_hip_ctx_t *, void *dst, const void *src, size_t bytes);
 int gr_hip_memcpy_d2h(gr_hip_ctx_t *, void *dst, const void *src, size_t bytes);
 
+// ---------------------------------------------------------------------------
+// rte_graph node shim: mbuf staging and hand-back
+// ---------------------------------------------------------------------------
+//
+// What the grout node that replaces iface_input copies
+// between each rte_mbuf (+ its 64-byte private area, mbuf.h:29-41) and the
+// fast path. After gr_hip_node_apply() the mbuf is exactly as grout's CPU
+// chain would have left it at `edge`: frame bytes (the L2 rewrite, TTL and
+// checksum), data_off / data_len / pkt_len (eth_input's adj(14), undone by
+// eth_output's prepend), packet_type (ip_output.c:145) and the private data
+// the next node reads (iface, vlan_id, eth_input domain, l3 nexthop).
+struct gr_hip_mbuf {
+	void *frame; // in: rte_pktmbuf_mtod(m) as port_rx delivered it
+	uint32_t pkt_len; // in/out
+	uint16_t data_len; // in/out
+	uint16_t data_off; // in/out
+	uint32_t packet_type; // in/out: RTE_PTYPE_L3_IPV4 (0x1) set by ip_output
+	uint32_t rss; // in: m->hash.rss
+	uint16_t iface; // in/out: iface_mbuf_data.iface (by id)
+	uint16_t vlan_id; // in/out: iface_mbuf_data.vlan_id
+	uint8_t ck; // in: GR_HIP_CKSUM_* from ol_flags
+	uint8_t edge; // out: enum gr_hip_edge, the next node
+	uint8_t domain; // out: eth_input_mbuf_data.domain
+	uint8_t _pad;
+	uint32_t nh; // out: l3_mbuf_data.nh as a nexthop slot (0 = NULL)
+};
+
+#define GR_HIP_PTYPE_L3_IPV4 0x1 // RTE_PTYPE_L3_IPV4
+
+// The nodes the fast path replaces, for per-node statistics.
+enum gr_hip_node {
+	GR_HIP_NODE_IFACE_INPUT = 0,
+	GR_HIP_NODE_ETH_INPUT,
+	GR_HIP_NODE_IP_INPUT,
+	GR_HIP_NODE_IP_FORWARD,
+	GR_HIP_NODE_IP_OUTPUT,
+	GR_HIP_NODE_ETH_OUTPUT,
+	GR_HIP_NODE_IFACE_OUTPUT,
+	GR_HIP_NODE_COUNT,
+};
+
+// rte_graph node counters as grout collects them (main_loop.c:39-64):
+// packets = sum of process() return values, calls = process() invocations,
+// one per node per graph walk that reaches it. Every node returns nb_objs
+// except ip_output, which returns only what it sent to eth_output
+// (ip_output.c:153,162).
+struct gr_hip_node_stats {
+	uint64_t packets[GR_HIP_NODE_COUNT];
+	uint64_t calls[GR_HIP_NODE_COUNT];
+};
+
+// The last node of the fast path a packet with this verdict went through
+// (-1 for GR_HIP_E_PUNT, which grout's CPU iface_input takes instead).
+int gr_hip_edge_node(uint8_t edge, uint32_t nh);
+
+// Stage n mbufs: the first 64 bytes of each frame (zero-filled past
+// data_len) into lines[i * 64], and their metadata.
+int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, void *lines, struct gr_hip_pkt_meta *meta);
+
+// Hand back: apply the fast path's verdicts and rewritten header lines
+// (line_stride apart) to the mbufs. ifaces[id] / nh[slot] are the mirrors
+// pushed with gr_hip_iface_set / gr_hip_nh_set (the egress VLAN tag and the
+// ingress VLAN demux are read from them). stats (optional) accumulates the
+// per-node counters, the packets taken as consecutive graph walks of
+// `burst` packets.
+int gr_hip_node_apply(
+	struct gr_hip_mbuf *m,
+	uint32_t n,
+	const void *lines,
+	uint32_t line_stride,
+	const struct gr_hip_verdict *verdicts,
+	const struct gr_hip_iface *ifaces,
+	uint32_t n_ifaces,
+	const struct gr_hip_nh *nh,
+	uint32_t n_nh,
+	uint32_t burst,
+	struct gr_hip_node_stats *stats
+);
+
+// The node's whole walk on a queue: stage, forward on the GPU
+// (gr_hip_fwd4_host), apply with the context's mirrors.
+int gr_hip_node_process(gr_hip_queue_t *, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst,
+			struct gr_hip_node_stats *stats);
+
 #ifdef __cplusplus
 }
 #endif

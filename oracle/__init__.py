@@ -37,6 +37,7 @@ API = {
     "or_lpm_dir24": (_U32, [_P, _U16, _U32]),
     "or_lpm_brute": (_U32, [_P, _U16, _U32]),
     "or_process": (_I, [_P, _P, _U32, _P, _U32, _P, _U32, _P, _P, _U32]),
+    "or_process_ex": (_I, [_P, _P, _U32, _P, _U32, _P, _U32, _P, _P, _U32, _P, _P]),
     "or_bench": (ctypes.c_double, [_P, _P, _U32, _P, _U32, _I, _U64, ctypes.POINTER(_U64)]),
 }
 
@@ -125,6 +126,25 @@ class Oracle:
                                             out.ctypes.data, abi.LINE, v.ctypes.data, st.ctypes.data,
                                             abi.BATCH_F_LINES_ONLY if lines_only else 0))
         return out, v, st
+
+    def process_mbufs(self, frames, meta, lines_only=False):
+        """-> (out_lines, verdicts, stats, mbufs, node_stats): process() plus
+        the mbuf state at each edge (abi.MBUF_DT, RX data_off 128) and the
+        per-node counters of the bursts of 64."""
+        frames = np.ascontiguousarray(frames)
+        meta = np.ascontiguousarray(meta, dtype=abi.META_DT)
+        n = len(meta)
+        stride = frames.shape[1] if frames.ndim == 2 else frames.itemsize
+        out = np.zeros((n, abi.LINE), dtype=np.uint8)
+        v = np.zeros(n, dtype=abi.VERDICT_DT)
+        st = np.zeros(self.max_ifaces, dtype=abi.STATS_DT)
+        mb = np.zeros(n, dtype=abi.MBUF_DT)
+        ns = np.zeros(1, dtype=abi.NODE_STATS_DT)
+        _ck("or_process_ex", self.L.or_process_ex(self.h, frames.ctypes.data, stride, meta.ctypes.data, n,
+                                                  out.ctypes.data, abi.LINE, v.ctypes.data, st.ctypes.data,
+                                                  abi.BATCH_F_LINES_ONLY if lines_only else 0, mb.ctypes.data,
+                                                  ns.ctypes.data))
+        return out, v, st, mb, ns[0]
 
     def bench(self, frames, meta, threads, pkts_per_thread):
         fwd = ctypes.c_uint64()

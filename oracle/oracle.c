@@ -151,7 +151,7 @@ void or_topo_free(or_topo_t *t) {
 
 #define EDGE_SETTER(fn, table, limit)                                                              \
 	int fn(or_topo_t *t, uint8_t key, uint8_t edge) {                                          \
-		if (key >= (limit))                                                                \
+		if ((unsigned)key + 1 > (unsigned)(limit))                                         \
 			return -EINVAL;                                                            \
 		t->table[key] = edge;                                                              \
 		return 0;                                                                          \
@@ -494,6 +494,7 @@ struct or_mbuf {
 	uint16_t eth_type; // BE
 	// result
 	uint8_t edge;
+	uint8_t visited; // bit per enum gr_hip_node this packet was handed to
 	uint8_t rx_counted, tx_counted;
 	uint16_t tx_iface, tx_parent;
 	uint16_t rx_iface, rx_parent;
@@ -839,22 +840,47 @@ static void node_iface_output(struct or_graph *g, struct or_mbuf **objs, uint16_
 	}
 }
 
+static void mark(struct or_mbuf **objs, uint16_t n, int node) {
+	for (uint16_t i = 0; i < n; i++)
+		objs[i]->visited |= (uint8_t)(1u << node);
+}
+
 // One graph walk over a burst (rte_graph_walk RTC order, main_loop.c:459).
 static void graph_walk(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
+	mark(objs, n, GR_HIP_NODE_IFACE_INPUT);
 	node_iface_input(g, objs, n);
-#define RUN(name)                                                                                  \
+#define RUN(name, node)                                                                            \
 	if (g->name.n) {                                                                           \
 		uint16_t k = g->name.n;                                                            \
 		g->name.n = 0;                                                                     \
+		mark(g->name.objs, k, node);                                                       \
 		node_##name(g, g->name.objs, k);                                                   \
 	}
-	RUN(eth_input)
-	RUN(ip_input)
-	RUN(ip_forward)
-	RUN(ip_output)
-	RUN(eth_output)
-	RUN(iface_output)
+	RUN(eth_input, GR_HIP_NODE_ETH_INPUT)
+	RUN(ip_input, GR_HIP_NODE_IP_INPUT)
+	RUN(ip_forward, GR_HIP_NODE_IP_FORWARD)
+	RUN(ip_output, GR_HIP_NODE_IP_OUTPUT)
+	RUN(eth_output, GR_HIP_NODE_ETH_OUTPUT)
+	RUN(iface_output, GR_HIP_NODE_IFACE_OUTPUT)
 #undef RUN
+}
+
+// Node counters of one walk as rte_graph keeps them (main_loop.c:39-64):
+// calls = process() invocations, packets = their return values; ip_output
+// returns only what it enqueued to eth_output (ip_output.c:153,162).
+// Punted packets restart on grout's CPU nodes, which count them there.
+static void walk_node_stats(struct or_mbuf *mb, uint16_t k, struct gr_hip_node_stats *ns) {
+	uint32_t cnt[GR_HIP_NODE_COUNT] = {0};
+	for (uint16_t i = 0; i < k; i++) {
+		if (mb[i].edge == GR_HIP_E_PUNT)
+			continue;
+		for (int j = 0; j < GR_HIP_NODE_COUNT; j++)
+			cnt[j] += (mb[i].visited >> j) & 1;
+	}
+	for (int j = 0; j < GR_HIP_NODE_COUNT; j++) {
+		ns->calls[j] += cnt[j] != 0;
+		ns->packets[j] += j == GR_HIP_NODE_IP_OUTPUT ? cnt[GR_HIP_NODE_ETH_OUTPUT] : cnt[j];
+	}
 }
 
 static void rx_fill(struct or_mbuf *m, const uint8_t *frame, uint32_t copy, const struct gr_hip_pkt_meta *md) {
@@ -872,6 +898,7 @@ static void rx_fill(struct or_mbuf *m, const uint8_t *frame, uint32_t copy, cons
 	m->e_nh = 0;
 	m->l3_nh = 0;
 	m->edge = 0;
+	m->visited = 0;
 	m->rx_counted = m->tx_counted = 0;
 }
 
@@ -911,6 +938,23 @@ int or_process(
 	struct gr_hip_verdict *v,
 	struct gr_hip_iface_stats *stats,
 	uint32_t flags
+) {
+	return or_process_ex(t, in_frames, in_stride, meta, n, out_lines, out_stride, v, stats, flags, NULL, NULL);
+}
+
+int or_process_ex(
+	or_topo_t *t,
+	const void *in_frames,
+	uint32_t in_stride,
+	const struct gr_hip_pkt_meta *meta,
+	uint32_t n,
+	void *out_lines,
+	uint32_t out_stride,
+	struct gr_hip_verdict *v,
+	struct gr_hip_iface_stats *stats,
+	uint32_t flags,
+	struct gr_hip_mbuf *mo,
+	struct gr_hip_node_stats *ns
 ) {
 	if (in_stride < GR_HIP_LINE || out_stride < GR_HIP_LINE)
 		return -EINVAL;
@@ -954,7 +998,26 @@ int or_process(
 				memcpy(out + (size_t)(base + i) * out_stride,
 				       in + (size_t)(base + i) * in_stride, GR_HIP_LINE);
 			count_stats(m, stats, t->max_ifaces);
+			if (mo != NULL) { // the mbuf as grout leaves it at the edge (untouched if punted)
+				struct gr_hip_mbuf *b = &mo[base + i];
+				const struct gr_hip_pkt_meta *md = &meta[base + i];
+				const bool punt = m->edge == GR_HIP_E_PUNT;
+				memset(b, 0, sizeof(*b));
+				b->pkt_len = punt ? md->pkt_len : m->pkt_len;
+				b->data_len = (uint16_t)(punt ? md->pkt_len : m->data_len);
+				b->data_off = (uint16_t)(punt ? OR_HEADROOM : m->data_off);
+				b->packet_type = punt ? 0 : m->packet_type;
+				b->rss = md->rss;
+				b->iface = punt ? md->iface : m->iface;
+				b->vlan_id = punt ? (md->vlan_ck & 0xfff) : m->vlan_id;
+				b->ck = (uint8_t)((md->vlan_ck >> 12) & 3);
+				b->edge = m->edge;
+				b->domain = punt ? 0 : m->domain;
+				b->nh = punt ? 0 : m->l3_nh;
+			}
 		}
+		if (ns != NULL)
+			walk_node_stats(mb, k, ns);
 	}
 	free(bufs);
 	return 0;

@@ -76,6 +76,25 @@ int or_process(
 	uint32_t flags
 );
 
+// or_process, plus the mbuf state grout leaves at each packet's edge (mo[n],
+// frame NULL, data_off relative to an RX data_off of 128; a punted packet's
+// mbuf is reported untouched) and the per-node counters of the walks (ns,
+// accumulated; punted packets are not counted).
+int or_process_ex(
+	or_topo_t *,
+	const void *in_frames,
+	uint32_t in_stride,
+	const struct gr_hip_pkt_meta *meta,
+	uint32_t n,
+	void *out_lines,
+	uint32_t out_stride,
+	struct gr_hip_verdict *verdicts,
+	struct gr_hip_iface_stats *stats,
+	uint32_t flags,
+	struct gr_hip_mbuf *mo,
+	struct gr_hip_node_stats *ns
+);
+
 // CPU baseline: `threads` pthreads, each walks its own copy of the packet
 // stream in bursts of 64 until it has processed `pkts_per_thread` packets.
 // Returns the aggregate Mpps (wall clock, CLOCK_MONOTONIC).

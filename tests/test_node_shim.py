@@ -1,0 +1,163 @@
+# SPDX-License-Identifier: BSD-3-Clause
+"""The rte_graph node shim (include/grout_hip.h):
+staging mbufs into header lines and handing verdicts back onto mbufs, and
+the per-node counters, against the oracle's mbuf-level restatement of the
+chain (oracle.c: data_off / data_len / pkt_len through eth_input's adj and
+eth_output's prepend, packet_type, vlan_id, priv iface / domain / nexthop).
+
+CPU tests feed the oracle's own lines and verdicts to gr_hip_node_apply (a
+pure host function of libgrout_hip.so); the GPU test runs the whole node
+walk (gr_hip_node_process: stage, forward on the GPU, apply)."""
+import numpy as np
+import pytest
+
+import oracle
+import scenarios as SC
+from grout_amd import abi
+from grout_amd import synth as S
+from grout_amd import topology as T
+
+RX_DATA_OFF = 128  # RTE_PKTMBUF_HEADROOM
+
+
+def mbufs_for(frames, meta, data_room=2048):
+    """Host 'mbufs': each frame copied into its own buffer, views at RX."""
+    n = len(meta)
+    stride = frames.shape[1]
+    bufs = np.zeros((n, max(stride, abi.LINE)), dtype=np.uint8)
+    bufs[:, :stride] = frames
+    m = np.zeros(n, dtype=abi.MBUF_DT)
+    m["frame"] = bufs.ctypes.data + np.arange(n, dtype=np.uint64) * bufs.shape[1]
+    m["pkt_len"] = meta["pkt_len"]
+    m["data_len"] = meta["pkt_len"]
+    m["data_off"] = RX_DATA_OFF
+    m["rss"] = meta["rss"]
+    m["iface"] = meta["iface"]
+    m["vlan_id"] = meta["vlan_ck"] & 0xfff
+    m["ck"] = (meta["vlan_ck"] >> 12) & 3
+    return bufs, m
+
+
+def apply(m, lines, v, topo, burst=64):
+    ns = np.zeros(1, dtype=abi.NODE_STATS_DT)
+    L = abi.hip()
+    ifaces = np.ascontiguousarray(topo.ifaces)
+    nh = np.ascontiguousarray(topo.nh)
+    abi.check("gr_hip_node_apply", L.gr_hip_node_apply(
+        m.ctypes.data, len(m), np.ascontiguousarray(lines).ctypes.data, abi.LINE, v.ctypes.data,
+        ifaces.ctypes.data, len(ifaces), nh.ctypes.data, len(nh), burst, ns.ctypes.data))
+    return ns[0]
+
+
+FIELDS = ["pkt_len", "data_len", "data_off", "packet_type", "iface", "vlan_id", "edge", "domain", "nh"]
+
+
+def compare_mbufs(got, want, frames_after, lines_want, labels=None):
+    for f in FIELDS:
+        bad = np.nonzero(got[f] != want[f])[0]
+        assert len(bad) == 0, (f, [((labels[i] if labels else i), int(got[f][i]), int(want[f][i]),
+                                    abi.EDGE_NAMES[want["edge"][i]]) for i in bad[:6]])
+    # the frame ends as the oracle's line: grout's rewrite at that edge
+    n = len(got)
+    bad = np.nonzero((frames_after[:, :abi.LINE] != lines_want).any(axis=1))[0]
+    assert len(bad) == 0, [(labels[i] if labels else i) for i in bad[:6]]
+    assert n == len(want)
+
+
+def test_edge_node_table():
+    """Every verdict edge maps to the node that chose it."""
+    L = abi.hip()
+    node_of = {e: L.gr_hip_edge_node(i, 0) for i, e in enumerate(abi.EDGE_NAMES)}
+    assert node_of["punt"] == -1
+    assert node_of["port_output"] == node_of["iface_output_admin_down"] == 6
+    assert node_of["ip_hold"] == node_of["ip_output_snat"] == 4
+    assert node_of["ip_error_ttl_exceeded"] == 3
+    assert node_of["ip_error_dest_unreach"] == node_of["ip_input_local"] == 2
+    assert node_of["snap_input"] == node_of["arp_input"] == 1
+    assert node_of["iface_input_admin_down"] == node_of["bridge_input"] == 0
+    assert L.gr_hip_edge_node(abi.EDGE["bridge_input"], 7) == 6  # iface_output BRIDGE type edge
+    assert all(v >= -1 for v in node_of.values())
+    assert L.gr_hip_edge_node(abi.E_COUNT, 0) < -1
+
+
+def test_stage_roundtrip():
+    fr, me, _ = SC.corpus_arrays()
+    bufs, m = mbufs_for(fr, me)
+    lines = np.zeros((len(me), abi.LINE), dtype=np.uint8)
+    meta = np.zeros(len(me), dtype=abi.META_DT)
+    abi.check("gr_hip_node_stage", abi.hip().gr_hip_node_stage(m.ctypes.data, len(m), lines.ctypes.data,
+                                                               meta.ctypes.data))
+    assert np.array_equal(meta, me)
+    for i in range(len(me)):
+        k = min(abi.LINE, int(me["pkt_len"][i]))
+        assert np.array_equal(lines[i, :k], fr[i, :k])
+        assert not lines[i, k:].any()
+
+
+def test_apply_corpus_matches_oracle_mbufs():
+    """Every edge of the exception corpus: the hand-back leaves each mbuf as
+    grout's chain does at that edge, and the node counters match."""
+    t, _ = SC.corpus_topology()
+    fr, me, lab = SC.corpus_arrays()
+    lines, v, _, want, ns_want = oracle.Oracle(t).process_mbufs(fr, me)
+    bufs, m = mbufs_for(fr, me)
+    ns = apply(m, lines, v, t)
+    compare_mbufs(m, want, bufs, lines, lab)
+    assert np.array_equal(ns["packets"], ns_want["packets"]), (ns, ns_want)
+    assert np.array_equal(ns["calls"], ns_want["calls"]), (ns, ns_want)
+    edges = set(abi.EDGE_NAMES[e] for e in v["edge"])
+    assert {"port_output", "ip_hold", "ip_error_ttl_exceeded", "eth_output_no_mac", "snap_input",
+            "iface_input_unknown_vlan", "ip_input_bad_checksum"} <= edges
+
+
+@pytest.mark.parametrize("burst", [1, 7, 64])
+def test_node_stats_bursts(burst):
+    """Per-node packets / calls follow grout's rule for any walk size: the
+    oracle walks bursts of 64, so compare at 64 and check the invariants
+    for other sizes."""
+    t, _ = SC.corpus_topology()
+    fr, me, _ = SC.corpus_arrays()
+    lines, v, _, _, ns64 = oracle.Oracle(t).process_mbufs(fr, me)
+    _, m = mbufs_for(fr, me)
+    ns = apply(m, lines, v, t, burst=burst)
+    assert np.array_equal(ns["packets"], ns64["packets"])  # packets do not depend on the walk size
+    n_walks = -(-len(me) // burst)
+    assert (ns["calls"] <= n_walks).all()
+    if burst == 64:
+        assert np.array_equal(ns["calls"], ns64["calls"])
+    # ip_output returns what it sent to eth_output
+    assert ns["packets"][4] == ns["packets"][5]
+
+
+def test_apply_fullview_stream():
+    tf = T.config_fullview(count=100_000)
+    fr, me = S.stream(1 << 16, 0xA11, routes=tf.route_array())
+    lines, v, _, want, ns_want = oracle.Oracle(tf).process_mbufs(fr, me)
+    bufs, m = mbufs_for(fr, me)
+    ns = apply(m, lines, v, tf)
+    compare_mbufs(m, want, bufs, lines)
+    assert np.array_equal(ns["packets"], ns_want["packets"]) and np.array_equal(ns["calls"], ns_want["calls"])
+    fwd = m["edge"] == abi.EDGE["port_output"]
+    assert fwd.mean() > 0.99
+    assert (m["data_off"][fwd] == RX_DATA_OFF).all() and (m["packet_type"][fwd] == abi.PTYPE_L3_IPV4).all()
+    assert (m["data_off"][~fwd] == RX_DATA_OFF + 14).all()  # no route: left after eth_input's adj
+
+
+@pytest.mark.gpu
+def test_node_process_gpu(fastpath):
+    """The whole node walk on the GPU (stage, fwd4_host, apply) against the
+    oracle's mbufs, corpus and a full-view stream."""
+    from golden_util import fresh_fastpath_state
+    for topo, fr, me, lab in [(SC.corpus_topology()[0],) + tuple(SC.corpus_arrays()),
+                              (T.config_single_route(),) + S.stream(100_003, 0xB0B, dst_range=(
+                                  T.ip4("16.1.0.0"), T.ip4("16.1.255.255"))) + (None,)]:
+        fresh_fastpath_state(fastpath, topo)
+        lines, v, st, want, ns_want = oracle.Oracle(topo).process_mbufs(fr, me)
+        bufs, m = mbufs_for(fr, me)
+        q = fastpath.queue()
+        ns = q.node_process(m, burst=64)
+        compare_mbufs(m, want, bufs, lines, lab)
+        assert np.array_equal(ns["packets"], ns_want["packets"])
+        assert np.array_equal(ns["calls"], ns_want["calls"])
+        assert np.array_equal(q.stats(), st)  # the iface counters of the same packets
+        q.close()
