@@ -47,7 +47,10 @@ typedef ring_cfg<16, 2, 2, 16, 4> ring_cfg2;
 typedef ring_cfg<12, 2, 1, 12, 4> ring_cfg3;
 typedef ring_cfg<8, 1, 1, 8, 6> ring_cfg4;
 typedef ring_cfg<16, 2, 2, 16, 6> ring_cfg5;
-#define RING_NCFG 6
+typedef ring_cfg<16, 3, 1, 20, 4> ring_cfg6;
+typedef ring_cfg<16, 4, 2, 24, 3> ring_cfg7;
+typedef ring_cfg<16, 2, 2, 16, 8> ring_cfg8;
+#define RING_NCFG 9
 
 template <class C>
 struct ring_lds {
@@ -323,6 +326,7 @@ struct ring_entry {
 static const ring_entry ring_kernels[RING_NCFG] = {
 	RING_ENTRY(ring_cfg0), RING_ENTRY(ring_cfg1), RING_ENTRY(ring_cfg2),
 	RING_ENTRY(ring_cfg3), RING_ENTRY(ring_cfg4), RING_ENTRY(ring_cfg5),
+	RING_ENTRY(ring_cfg6), RING_ENTRY(ring_cfg7), RING_ENTRY(ring_cfg8),
 };
 
 // variant: FWD4_V_STATS | FWD4_V_NT; cfg: ring geometry. A->nhf_lds fast

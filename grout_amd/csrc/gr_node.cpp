@@ -93,12 +93,13 @@ extern "C" int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, void *
 		return -EINVAL;
 	uint8_t *L = static_cast<uint8_t *>(lines);
 	for (uint32_t i = 0; i < n; i++) {
-		uint8_t *line = L + (size_t)i * GR_HIP_LINE;
-		const uint32_t len = m[i].data_len < GR_HIP_LINE ? m[i].data_len : GR_HIP_LINE;
-		if (len && m[i].frame == nullptr)
+		// 64 bytes whatever data_len says: grout's nodes read the Ethernet and
+		// IPv4 headers from the data room without a length check (eth_input.c
+		// reads 14 bytes of a shorter frame), and an mbuf's data room always
+		// holds 64 bytes past data_off (mempool.c:66-68)
+		if (m[i].frame == nullptr)
 			return -EINVAL;
-		memcpy(line, m[i].frame, len);
-		memset(line + len, 0, GR_HIP_LINE - len);
+		memcpy(L + (size_t)i * GR_HIP_LINE, m[i].frame, GR_HIP_LINE);
 		meta[i].iface = m[i].iface;
 		meta[i].vlan_ck = (uint16_t)((m[i].vlan_id & 0xfff) | ((m[i].ck & 3) << 12));
 		meta[i].pkt_len = (uint16_t)(m[i].pkt_len > 0xffff ? 0xffff : m[i].pkt_len);

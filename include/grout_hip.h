@@ -346,7 +346,7 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //   "kernel"    2 = warp-specialised LDS-DMA ring kernel (default),
 //               0 = tile kernel (one 256-packet tile per workgroup)
 //   "ring"      geometry of the ring kernel (loaders / storers / slots /
-//               tiles in flight), 0..5; default 1
+//               tiles in flight), 0..8; default 1
 //   "stats"     1 = per-iface counters (default; grout always counts), 0 = off
 //   "nt"        1 = nontemporal loads / stores of the streamed data (default)
 //   "tile"      tile kernel: packets per workgroup, 256 (four waves) or 64
@@ -395,7 +395,7 @@ int gr_hip_memcpy_d2h(gr_hip_ctx_t *, void *dst, const void *src, size_t bytes);
 // eth_output's prepend), packet_type (ip_output.c:145) and the private data
 // the next node reads (iface, vlan_id, eth_input domain, l3 nexthop).
 struct gr_hip_mbuf {
-	void *frame; // in: rte_pktmbuf_mtod(m) as port_rx delivered it
+	void *frame; // in: rte_pktmbuf_mtod(m) as port_rx delivered it (64 bytes readable)
 	uint32_t pkt_len; // in/out
 	uint16_t data_len; // in/out
 	uint16_t data_off; // in/out
@@ -438,8 +438,9 @@ struct gr_hip_node_stats {
 // (-1 for GR_HIP_E_PUNT, which grout's CPU iface_input takes instead).
 int gr_hip_edge_node(uint8_t edge, uint32_t nh);
 
-// Stage n mbufs: the first 64 bytes of each frame (zero-filled past
-// data_len) into lines[i * 64], and their metadata.
+// Stage n mbufs: the first 64 bytes at each frame (read whatever data_len
+// says, as grout's nodes do: an mbuf's data room always has them) into
+// lines[i * 64], and their metadata.
 int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, void *lines, struct gr_hip_pkt_meta *meta);
 
 // Hand back: apply the fast path's verdicts and rewritten header lines

@@ -303,7 +303,7 @@ def test_many_nexthops_fast_adjacency(fastpath, kernel):
         fastpath.tune("kernel", 2)
 
 
-@pytest.mark.parametrize("cfg", range(6))
+@pytest.mark.parametrize("cfg", range(9))
 def test_ring_geometries(fastpath, cfg):
     """Every ring geometry (loaders / storers / slots / tiles in flight) of
     fwd4_ring.hip forwards bit-exact; wg_per_cu 1 makes each workgroup walk

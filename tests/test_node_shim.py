@@ -88,10 +88,7 @@ def test_stage_roundtrip():
     abi.check("gr_hip_node_stage", abi.hip().gr_hip_node_stage(m.ctypes.data, len(m), lines.ctypes.data,
                                                                meta.ctypes.data))
     assert np.array_equal(meta, me)
-    for i in range(len(me)):
-        k = min(abi.LINE, int(me["pkt_len"][i]))
-        assert np.array_equal(lines[i, :k], fr[i, :k])
-        assert not lines[i, k:].any()
+    assert np.array_equal(lines, fr[:, :abi.LINE])  # 64 bytes whatever data_len says
 
 
 def test_apply_corpus_matches_oracle_mbufs():
@@ -146,13 +143,15 @@ def test_apply_fullview_stream():
 @pytest.mark.gpu
 def test_node_process_gpu(fastpath):
     """The whole node walk on the GPU (stage, fwd4_host, apply) against the
-    oracle's mbufs, corpus and a full-view stream."""
+    oracle's mbufs, corpus and a one-route stream. The node stages 64-byte
+    header lines, so the oracle runs lines-only: an IPv4 header that does not
+    fit is punted to grout's CPU nodes, mbuf untouched."""
     from golden_util import fresh_fastpath_state
     for topo, fr, me, lab in [(SC.corpus_topology()[0],) + tuple(SC.corpus_arrays()),
                               (T.config_single_route(),) + S.stream(100_003, 0xB0B, dst_range=(
                                   T.ip4("16.1.0.0"), T.ip4("16.1.255.255"))) + (None,)]:
         fresh_fastpath_state(fastpath, topo)
-        lines, v, st, want, ns_want = oracle.Oracle(topo).process_mbufs(fr, me)
+        lines, v, st, want, ns_want = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
         bufs, m = mbufs_for(fr, me)
         q = fastpath.queue()
         ns = q.node_process(m, burst=64)
