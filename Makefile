@@ -32,7 +32,7 @@ $(BUILD)/fib4.o: $(CSRC)/fib4.c $(CSRC)/fib4.h
 	@mkdir -p $(BUILD)
 	$(CC) $(CFLAGS_HOST) -c -o $@ $<
 
-$(LIB_HIP): $(BUILD)/fwd4_kernel.o $(BUILD)/fwd4_ring.o $(BUILD)/gr_hip.o $(BUILD)/gr_node.o $(BUILD)/fib4.o
+$(LIB_HIP): $(BUILD)/fwd4_ring.o $(BUILD)/gr_hip.o $(BUILD)/gr_node.o $(BUILD)/fib4.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 $(LIB_HOST): $(CSRC)/fib4.c $(CSRC)/synth.c $(CSRC)/fib4.h $(CSRC)/synth.h include/grout_hip.h

@@ -4,7 +4,7 @@
 // that keep a tile's header lines in an LDS image (fwd4_ring.hip):
 // chain_head (iface_input .. ip_input checks), chain_fib
 // (fib4_lookup), chain_tail (adjacency .. iface_output, rewriting the row).
-// Node citations as process() in fwd4_kernel.hip. Not a public header.
+// Not a public header.
 //
 // LDS image of a 64-packet tile: row r (64 bytes) = packet r, its 16-byte
 // chunk j at slot j ^ ((r >> 2) & 3) -- conflict-free both for the

@@ -1,7 +1,7 @@
 // SPDX-License-Identifier: BSD-3-Clause
 //
 // fwd4_dev.h -- device helpers shared by the forwarding kernels
-// (fwd4_kernel.hip, fwd4_ring.hip): table views, counter aggregation,
+// (fwd4_ring.hip): table views, counter aggregation,
 // vector loads and stores. Not a public header.
 #pragma once
 
@@ -28,7 +28,7 @@ __device__ __forceinline__ uint4 gld4(const void *p) {
 	return uint4{v.x, v.y, v.z, v.w};
 }
 
-// What process() reads: table pointers (loaded once per workgroup from the
+// What the chain reads: table pointers (loaded once per workgroup from the
 // device-resident fwd4_tables) and the ether type table, copied into LDS.
 struct kctx {
 	const fwd4_rx *rx;

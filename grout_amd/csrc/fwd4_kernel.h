@@ -1,14 +1,14 @@
 // SPDX-License-Identifier: BSD-3-Clause
 //
-// fwd4_kernel.h -- device-side layout shared by the kernel and the C-ABI
-// implementation (gr_hip.hip). Not a public header.
+// fwd4_kernel.h -- device-side layout shared by the forwarding kernel
+// (fwd4_ring.hip) and the C-ABI implementation (gr_hip.cpp). Not a public
+// header.
 #pragma once
 
 #include "../../include/grout_hip.h"
 
 #include <stdint.h>
 
-#define FWD4_ROW 80 // LDS bytes per staged 64-byte line (+16: no bank conflicts)
 #define FWD4_STAT_SLOTS 32 // per-block iface counter slots (LDS)
 #define FWD4_STAT_SHARDS 64 // global counter shards (block % shards)
 #define FWD4_MAX_ETH_TYPES 16
@@ -117,4 +117,3 @@ struct fwd4_params {
 // stores of the streamed data.
 #define FWD4_V_STATS 0x1
 #define FWD4_V_NT 0x2 // nontemporal loads and stores of the streamed data
-#define FWD4_V_TILE64 0x4 // one-wave workgroups, 64-packet tiles (else 256)

@@ -24,17 +24,12 @@
 #include <string.h>
 #include <vector>
 
-extern "C" hipError_t gr_fwd4_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant);
-extern "C" int gr_fwd4_occupancy(int variant);
-extern "C" uint32_t gr_fwd4_tile(int variant);
 extern "C" hipError_t gr_fwd4_ring_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant, int cfg);
 extern "C" int gr_fwd4_ring_occupancy(int variant, int cfg, uint32_t nhf_lds);
 extern "C" uint32_t gr_fwd4_ring_nhf_max(void);
 extern "C" int gr_fwd4_ring_ncfg(void);
 #define RING_WG_PER_CU 2 // default workgroups per CU of the ring kernel (measured)
 
-// Forwarding kernels (gr_hip_tune "kernel")
-enum { KERNEL_TILE = 0, KERNEL_RING = 2 }; // 1 was a software-pipelined kernel, retired
 
 #define HCK(expr)                                                                                  \
 	do {                                                                                       \
@@ -124,9 +119,6 @@ struct gr_hip_ctx {
 	int stats_on;
 	int wg_per_cu; // 0 = one tile per workgroup, N = persistent N per CU
 	int fib16; // allow the 2-byte FIB format
-	int occ[8];
-	int tile64; // FWD4_V_TILE64
-	int kernel; // KERNEL_*
 	int ring_cfg; // ring geometry (fwd4_ring.hip ring_cfgN)
 	int occ_ring[4]; // at occ_ring_nhf staged fast adjacencies, geometry occ_ring_cfg
 	uint32_t occ_ring_nhf;
@@ -438,10 +430,6 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->stats_on = 1;
 	c->wg_per_cu = 0;
 	c->fib16 = 1;
-	c->tile64 = 0;
-	c->kernel = KERNEL_RING;
-	for (int v = 0; v < 8; v++)
-		c->occ[v] = gr_fwd4_occupancy(v);
 	c->ring_cfg = 1; // 2 loaders, 1 storer, 5 compute waves, 8 slots
 	for (int v = 0; v < 4; v++)
 		c->occ_ring[v] = gr_fwd4_ring_occupancy(v, 0, 0);
@@ -1008,37 +996,25 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	A.nhf_lds = 0;
 	int stats = c->stats_on && q->d_stats != nullptr;
 	uint32_t slot = (uint32_t)(q->n_launch % N_TIMED);
-	if (c->kernel == KERNEL_RING) {
-		// persistent: one resident round of workgroups, each walking 64-packet tiles
-		int variant = (stats ? FWD4_V_STATS : 0) | c->nt;
-		uint32_t tiles = (b->n + 63) / 64;
-		A.nhf_lds = c->nh_hi < gr_fwd4_ring_nhf_max() ? c->nh_hi : gr_fwd4_ring_nhf_max();
-		if (A.nhf_lds != c->occ_ring_nhf || c->ring_cfg != c->occ_ring_cfg) {
-			for (int v = 0; v < 4; v++)
-				c->occ_ring[v] = gr_fwd4_ring_occupancy(v, c->ring_cfg, A.nhf_lds);
-			c->occ_ring_nhf = A.nhf_lds;
-			c->occ_ring_cfg = c->ring_cfg;
-		}
-		uint32_t per_cu = c->wg_per_cu > 0 ? (uint32_t)c->wg_per_cu : RING_WG_PER_CU;
-		if (c->occ_ring[variant] > 0 && per_cu > (uint32_t)c->occ_ring[variant])
-			per_cu = (uint32_t)c->occ_ring[variant];
-		uint32_t grid = (uint32_t)c->n_cu * per_cu;
-		if (grid > tiles)
-			grid = tiles;
-		if (timed)
-			HCK(hipEventRecord(q->ev0[slot], s));
-		HCK(gr_fwd4_ring_launch(&A, grid, s, variant, c->ring_cfg));
-	} else {
-		int variant = (stats ? FWD4_V_STATS : 0) | c->nt | c->tile64;
-		uint32_t tile = gr_fwd4_tile(variant);
-		uint32_t tiles = (b->n + tile - 1) / tile;
-		uint32_t grid = c->wg_per_cu > 0 ? (uint32_t)c->n_cu * (uint32_t)c->wg_per_cu : tiles;
-		if (grid > tiles)
-			grid = tiles;
-		if (timed)
-			HCK(hipEventRecord(q->ev0[slot], s));
-		HCK(gr_fwd4_launch(&A, grid, s, variant));
+	// persistent: one resident round of workgroups, each walking 64-packet tiles
+	int variant = (stats ? FWD4_V_STATS : 0) | c->nt;
+	uint32_t tiles = (b->n + 63) / 64;
+	A.nhf_lds = c->nh_hi < gr_fwd4_ring_nhf_max() ? c->nh_hi : gr_fwd4_ring_nhf_max();
+	if (A.nhf_lds != c->occ_ring_nhf || c->ring_cfg != c->occ_ring_cfg) {
+		for (int v = 0; v < 4; v++)
+			c->occ_ring[v] = gr_fwd4_ring_occupancy(v, c->ring_cfg, A.nhf_lds);
+		c->occ_ring_nhf = A.nhf_lds;
+		c->occ_ring_cfg = c->ring_cfg;
 	}
+	uint32_t per_cu = c->wg_per_cu > 0 ? (uint32_t)c->wg_per_cu : RING_WG_PER_CU;
+	if (c->occ_ring[variant] > 0 && per_cu > (uint32_t)c->occ_ring[variant])
+		per_cu = (uint32_t)c->occ_ring[variant];
+	uint32_t grid = (uint32_t)c->n_cu * per_cu;
+	if (grid > tiles)
+		grid = tiles;
+	if (timed)
+		HCK(hipEventRecord(q->ev0[slot], s));
+	HCK(gr_fwd4_ring_launch(&A, grid, s, variant, c->ring_cfg));
 	if (timed) {
 		HCK(hipEventRecord(q->ev1[slot], s));
 		q->n_launch++;
@@ -1054,10 +1030,6 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		c->nt = value ? FWD4_V_NT : 0;
 	} else if (strcmp(key, "stats") == 0) {
 		c->stats_on = value != 0;
-	} else if (strcmp(key, "tile") == 0) { // packets per workgroup: 256 (default) or 64
-		if (value != 64 && value != 256)
-			return -EINVAL;
-		c->tile64 = value == 64 ? FWD4_V_TILE64 : 0;
 	} else if (strcmp(key, "wg_per_cu") == 0) {
 		if (value < 0 || value > 32)
 			return -EINVAL;
@@ -1068,14 +1040,8 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < 0 || value >= gr_fwd4_ring_ncfg())
 			return -EINVAL;
 		c->ring_cfg = value;
-	} else if (strcmp(key, "kernel") == 0) { // 0: fwd4_kernel.hip, 2: fwd4_ring.hip
-		if (value != KERNEL_TILE && value != KERNEL_RING)
-			return -EINVAL;
-		c->kernel = value;
 	} else if (strcmp(key, "occupancy") == 0) { // read-only: WGs/CU of the current variant
-		if (c->kernel == KERNEL_RING)
-			return c->occ_ring[(c->stats_on ? FWD4_V_STATS : 0) | c->nt]; // as of the last launch
-		return c->occ[(c->stats_on ? FWD4_V_STATS : 0) | c->nt | c->tile64];
+		return c->occ_ring[(c->stats_on ? FWD4_V_STATS : 0) | c->nt]; // as of the last launch
 	} else {
 		return -ENOENT;
 	}

@@ -343,15 +343,12 @@ int gr_hip_queue_sync(gr_hip_queue_t *);
 int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *count);
 
 // Tuning knobs, for measurements (A/B in one process). Keys:
-//   "kernel"    2 = warp-specialised LDS-DMA ring kernel (default),
-//               0 = tile kernel (one 256-packet tile per workgroup)
 //   "ring"      geometry of the ring kernel (loaders / storers / slots /
 //               tiles in flight), 0..8; default 1
 //   "stats"     1 = per-iface counters (default; grout always counts), 0 = off
 //   "nt"        1 = nontemporal loads / stores of the streamed data (default)
-//   "tile"      tile kernel: packets per workgroup, 256 (four waves) or 64
-//   "wg_per_cu" 0 = the kernel's default grid (ring: 2 workgroups per CU;
-//               tile: one workgroup per tile), N = N workgroups per CU
+//   "wg_per_cu" 0 = default grid (2 workgroups per CU, fewer if LDS
+//               limits), N = N workgroups per CU
 //   "fib16"     1 = 2-byte FIB entries when slots fit 15 bits (default),
 //               0 = always 4-byte; applies from the next gr_hip_fib4_commit
 //   "occupancy" (read) resident workgroups per CU of the current variant

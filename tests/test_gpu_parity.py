@@ -191,26 +191,21 @@ def test_kernel_timing_api(fastpath):
     q.close()
 
 
-@pytest.mark.parametrize("kernel,nt,stats,wg,fib16,tile", [
-    (0, 1, 1, 0, 1, 64), (0, 1, 0, 6, 1, 256), (0, 0, 1, 4, 0, 64), (0, 0, 1, 0, 0, 256), (0, 1, 1, 8, 1, 64),
-    (2, 1, 1, 0, 1, 256), (2, 0, 0, 1, 1, 256), (2, 1, 0, 2, 0, 256), (2, 0, 1, 0, 0, 256)])
-def test_kernel_variants(fastpath, kernel, nt, stats, wg, fib16, tile):
-    """Every tuning variant (gr_hip_tune) forwards bit-exact: both kernels
-    (0: fwd4_kernel.hip, 2: fwd4_ring.hip);
-    wg_per_cu 1-2 making every wave / workgroup walk many tiles (a deep
-    ring, wrap-around of every slot)."""
+@pytest.mark.parametrize("nt,stats,wg,fib16", [(1, 1, 0, 1), (0, 0, 1, 1), (1, 0, 2, 0), (0, 1, 0, 0), (1, 1, 3, 0)])
+def test_kernel_variants(fastpath, nt, stats, wg, fib16):
+    """Every tuning variant (gr_hip_tune) forwards bit-exact: nontemporal
+    streams, counters, grid (wg_per_cu 1-3: every workgroup walks its ring
+    many times round), FIB entry size."""
     t, _ = SC.corpus_topology()
     fr, me, lab = SC.corpus_arrays()
     tf = _fullview()
     fr2, me2 = S.stream(1 << 20, 0xAB + nt, routes=tf.route_array())
     o1 = oracle.Oracle(t).process(fr, me)
     o2 = oracle.Oracle(tf).process(fr2, me2)
-    fastpath.tune("kernel", kernel)
     fastpath.tune("nt", nt)
     fastpath.tune("stats", stats)
     fastpath.tune("wg_per_cu", wg)
     fastpath.tune("fib16", fib16)
-    fastpath.tune("tile", tile)
     try:
         fresh_fastpath_state(fastpath, T.config_single_route())  # force a reload (commit)
         g = run_gpu(fastpath, t, fr, me)
@@ -228,7 +223,7 @@ def test_kernel_variants(fastpath, kernel, nt, stats, wg, fib16, tile):
         else:
             assert info["dev_bytes"] == 4 * (1 << 24) + 1024 * n8
     finally:
-        for k, v in [("kernel", 2), ("nt", 1), ("stats", 1), ("wg_per_cu", 0), ("fib16", 1), ("tile", 256)]:
+        for k, v in [("nt", 1), ("stats", 1), ("wg_per_cu", 0), ("fib16", 1)]:
             fastpath.tune(k, v)
         fresh_fastpath_state(fastpath, T.config_single_route())
 
@@ -284,23 +279,18 @@ def _many_nh_topology(n_nh=6000, n_routes=50_000):
     return t
 
 
-@pytest.mark.parametrize("kernel", [2, 0])
-def test_many_nexthops_fast_adjacency(fastpath, kernel):
+def test_many_nexthops_fast_adjacency(fastpath):
     """Nexthop slots past the LDS-staged range read the fast adjacency with a
     gather; non-plain nexthops fall back to the full adjacency."""
     t = _many_nh_topology()
-    fr, me = S.stream(1 << 18, 0x5EED + kernel, routes=t.route_array())
+    fr, me = S.stream(1 << 18, 0x5EED, routes=t.route_array())
     o = oracle.Oracle(t).process(fr, me)
-    fastpath.tune("kernel", kernel)
-    try:
-        g = run_gpu(fastpath, t, fr, me)
-        compare(o, g)
-        edges = np.bincount(g[1]["edge"], minlength=abi.E_COUNT)
-        assert edges[abi.EDGE["port_output"]] > len(me) // 2
-        assert edges[abi.EDGE["ip_hold"]] > 0
-        assert (g[1]["nh"] > 2304).sum() > len(me) // 4
-    finally:
-        fastpath.tune("kernel", 2)
+    g = run_gpu(fastpath, t, fr, me)
+    compare(o, g)
+    edges = np.bincount(g[1]["edge"], minlength=abi.E_COUNT)
+    assert edges[abi.EDGE["port_output"]] > len(me) // 2
+    assert edges[abi.EDGE["ip_hold"]] > 0
+    assert (g[1]["nh"] > 2304).sum() > len(me) // 4
 
 
 @pytest.mark.parametrize("cfg", range(9))
@@ -314,7 +304,6 @@ def test_ring_geometries(fastpath, cfg):
     fr2, me2 = S.stream(1 << 20, 0xC0F + cfg, routes=tf.route_array())
     o1 = oracle.Oracle(t).process(fr, me)
     o2 = oracle.Oracle(tf).process(fr2, me2)
-    fastpath.tune("kernel", 2)
     fastpath.tune("ring", cfg)
     fastpath.tune("wg_per_cu", 1)
     try:

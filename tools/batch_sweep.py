@@ -1,9 +1,8 @@
 # SPDX-License-Identifier: BSD-3-Clause
-"""Kernel time against batch size for both kernels (full view, 64 B),
-interleaved in one process: where the warp-specialised ring kernel's
-per-workgroup set-up (staging the fast adjacencies in LDS) stops paying.
-One JSON line per (batch, kernel): median kernel µs (HIP events) and the
-median wall µs of submit + sync (what one burst waits for)."""
+"""Kernel time against batch size (full view, 64 B) for ring geometries,
+interleaved in one process. One JSON line per (batch, geometry): median
+kernel µs (HIP events) and the median wall µs of submit + sync (what one
+burst waits for)."""
 import argparse
 import json
 import os
@@ -19,7 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--kernels", default="2,0")
+    ap.add_argument("--rings", default="1")
     ap.add_argument("--log2", default="10,12,14,16,18,20,22,24")
     args = ap.parse_args()
     import torch
@@ -33,7 +32,7 @@ def main():
     fp = FastPath(0)
     fp.load(topo)
     sizes = [1 << int(x) for x in args.log2.split(",")]
-    kernels = [int(x) for x in args.kernels.split(",")]
+    kernels = [int(x) for x in args.rings.split(",")]
     nmax = max(sizes)
     frames, meta = S.stream(nmax, S.SEED_GPU_BASE, routes=topo.route_array())
     d_in = torch.from_numpy(frames.reshape(-1)).to(dev)
@@ -46,7 +45,7 @@ def main():
     for _ in range(args.rounds):
         for n in sizes:
             for k in kernels:
-                fp.tune("kernel", k)
+                fp.tune("ring", k)
                 q.submit(d_in, d_out, d_meta, d_v, n)
                 q.sync()
                 walls = []
@@ -61,7 +60,7 @@ def main():
     for n in sizes:
         for k in kernels:
             kus = float(np.median(kt[(n, k)])) * 1e3
-            print(json.dumps({"batch": n, "kernel": k, "kernel_us": round(kus, 2),
+            print(json.dumps({"batch": n, "ring": k, "kernel_us": round(kus, 2),
                               "wall_us": round(float(np.median(wt[(n, k)])) * 1e6, 2),
                               "mpps": round(n / kus, 1)}), flush=True)
     q.close()

@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 24)
     ap.add_argument("--workload", default="fullview64", choices=["fullview64", "single64"])
-    ap.add_argument("--kernel", type=int, default=None, help="gr_hip_tune kernel: 0 tile, 2 ring")
+    ap.add_argument("--ring", type=int, default=None, help="gr_hip_tune ring geometry")
     ap.add_argument("--wg", type=int, default=None, help="gr_hip_tune wg_per_cu")
     ap.add_argument("--stats", type=int, default=None)
     ap.add_argument("--nt", type=int, default=None)
@@ -42,7 +42,7 @@ def main():
         kw = dict(routes=topo.route_array())
     fp = FastPath(0)
     fp.load(topo)
-    for k in ("kernel", "wg", "stats", "nt"):
+    for k in ("ring", "wg", "stats", "nt"):
         v = getattr(args, k)
         if v is not None:
             fp.tune("wg_per_cu" if k == "wg" else k, v)

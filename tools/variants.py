@@ -28,8 +28,6 @@ def main():
     ap.add_argument("--wg", default="0,6")
     ap.add_argument("--fib16", default="1,0")
     ap.add_argument("--stats", default="1")
-    ap.add_argument("--tile", default="256")
-    ap.add_argument("--kernel", default="2,0", help="0 tile, 2 ring")
     ap.add_argument("--ring", default="1", help="ring geometries (fwd4_ring.hip ring_cfgN)")
     args = ap.parse_args()
     import torch
@@ -55,15 +53,13 @@ def main():
     d_v = torch.empty(n * 8, dtype=torch.uint8, device=dev)
     q = fp.queue(torch.cuda.current_stream(dev).cuda_stream)
     variants = list(itertools.product(ints(args.fib16), ints(args.stats), ints(args.nt), ints(args.wg),
-                                      ints(args.tile), ints(args.kernel), ints(args.ring)))
+                                      ints(args.ring)))
     times = {v: [] for v in variants}
     ref = None
     for r in range(args.rounds):
         for v in variants:
-            f16, st, nt, wg, tile, kern, ring = v
-            fp.tune("kernel", kern)
+            f16, st, nt, wg, ring = v
             fp.tune("ring", ring)
-            fp.tune("tile", tile)
             fp.tune("fib16", f16)
             fp.fib_commit(T.VRF_MAIN)  # re-uploads when the format changes
             fp.tune("stats", st)
@@ -83,7 +79,7 @@ def main():
     for v in variants:
         t = np.array(times[v])
         print(json.dumps({"workload": args.workload, "fib16": v[0], "stats": v[1], "nt": v[2],
-                          "wg_per_cu": v[3], "tile": v[4], "kernel": v[5], "ring": v[6], "median_ms": round(float(np.median(t)), 4),
+                          "wg_per_cu": v[3], "ring": v[4], "median_ms": round(float(np.median(t)), 4),
                           "min_ms": round(float(t.min()), 4), "mpps": round(n / float(np.median(t)) / 1e3, 1)}),
               flush=True)
     q.close()
