@@ -12,7 +12,7 @@ BUILD = build
 LIB_HIP = grout_amd/libgrout_hip.so
 LIB_HOST = grout_amd/libgrout_host.so
 LIB_ORACLE = oracle/liboracle.so
-HDRS = include/grout_hip.h $(CSRC)/fwd4_kernel.h $(CSRC)/fwd4_dev.h $(CSRC)/fwd4_chain.h $(CSRC)/fib4.h
+HDRS = include/grout_hip.h $(CSRC)/fib6.h $(CSRC)/fwd4_kernel.h $(CSRC)/fwd4_dev.h $(CSRC)/fwd4_chain.h $(CSRC)/fib4.h
 
 all: $(LIB_HIP) $(LIB_HOST) $(LIB_ORACLE)
 
@@ -32,11 +32,15 @@ $(BUILD)/fib4.o: $(CSRC)/fib4.c $(CSRC)/fib4.h
 	@mkdir -p $(BUILD)
 	$(CC) $(CFLAGS_HOST) -c -o $@ $<
 
-$(LIB_HIP): $(BUILD)/fwd4_ring.o $(BUILD)/gr_hip.o $(BUILD)/gr_node.o $(BUILD)/fib4.o
+$(BUILD)/fib6.o: $(CSRC)/fib6.c $(CSRC)/fib6.h
+	@mkdir -p $(BUILD)
+	$(CC) $(CFLAGS_HOST) -c -o $@ $<
+
+$(LIB_HIP): $(BUILD)/fwd4_ring.o $(BUILD)/gr_hip.o $(BUILD)/gr_node.o $(BUILD)/fib4.o $(BUILD)/fib6.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
-$(LIB_HOST): $(CSRC)/fib4.c $(CSRC)/synth.c $(CSRC)/fib4.h $(CSRC)/synth.h include/grout_hip.h
-	$(CC) $(CFLAGS_HOST) -shared -o $@ $(CSRC)/fib4.c $(CSRC)/synth.c
+$(LIB_HOST): $(CSRC)/fib4.c $(CSRC)/fib6.c $(CSRC)/synth.c $(CSRC)/fib4.h $(CSRC)/fib6.h $(CSRC)/synth.h include/grout_hip.h
+	$(CC) $(CFLAGS_HOST) -shared -o $@ $(CSRC)/fib4.c $(CSRC)/fib6.c $(CSRC)/synth.c
 
 $(LIB_ORACLE): oracle/oracle.c oracle/oracle.h include/grout_hip.h
 	$(CC) $(CFLAGS_HOST) -pthread -shared -o $@ oracle/oracle.c

@@ -27,7 +27,9 @@ NH_T = dict(L3=1, SR6_OUTPUT=2, SR6_LOCAL=3, DNAT=4, BLACKHOLE=5, REJECT=6, GROU
 AF_UNSPEC, AF_IP4, AF_IP6 = 0, 1, 2
 DOMAIN = dict(UNKNOWN=0, LOOPBACK=1, LOCAL=2, BROADCAST=3, MULTICAST=4, OTHER=5)
 CKSUM_UNKNOWN, CKSUM_BAD, CKSUM_GOOD = 0, 1, 2
+ABI_VERSION = 2  # GR_HIP_ABI_VERSION
 EDGE_CHAIN = 0xFF
+EDGE_CHAIN6 = 0xFE  # eth_input type edge: continue into ip6_input on the GPU
 LINE = 64
 BATCH_F_LINES_ONLY = 0x1
 
@@ -47,6 +49,10 @@ EDGE_NAMES = [
     "eth_output_no_mac",
     "iface_output_inval_type", "iface_output_admin_down", "iface_output_vlan_no_parent",
     "bond_output", "vxlan_output", "port_output",
+    "ip6_input_local", "ip6_error_dest_unreach", "ip6_input_not_member", "ip6_input_other_host",
+    "ip6_input_bad_version", "ip6_input_bad_addr", "ip6_input_bad_length", "ip6_blackhole", "sr6_local",
+    "ip6_error_ttl_exceeded",
+    "ip6_hold", "ip6_output_error", "ip6_output_too_big",
 ]
 EDGE = {n: i for i, n in enumerate(EDGE_NAMES)}
 E_COUNT = len(EDGE_NAMES)
@@ -64,17 +70,21 @@ NH_DT = np.dtype([
     ("iface_id", "<u2"), ("vrf_id", "<u2"),
     ("ipv4", ">u4"),  # network byte order in memory
     ("mac", "u1", (6,)), ("reta_size", "<u2"), ("reta_off", "<u4"), ("single", "<u4"),
-    ("n_members", "<u2"), ("_pad0", "<u2"),
+    ("n_members", "<u2"), ("_pad0", "<u2"), ("ipv6", "u1", (16,)),
 ])
 ROUTE_DT = np.dtype([
     ("ip", ">u4"), ("prefixlen", "u1"), ("_pad0", "u1"), ("vrf_id", "<u2"), ("nh", "<u4"),
+])
+ROUTE6_DT = np.dtype([
+    ("ip", "u1", (16,)), ("prefixlen", "u1"), ("_pad0", "u1"), ("vrf_id", "<u2"), ("iface_id", "<u2"),
+    ("_pad1", "<u2"), ("nh", "<u4"),
 ])
 META_DT = np.dtype([("iface", "<u2"), ("vlan_ck", "<u2"), ("pkt_len", "<u2"), ("rss", "<u2")])
 VERDICT_DT = np.dtype([("edge", "u1"), ("domain", "u1"), ("iface", "<u2"), ("nh", "<u4")])
 STATS_DT = np.dtype([
     ("rx_packets", "<u8"), ("rx_bytes", "<u8"), ("tx_packets", "<u8"), ("tx_bytes", "<u8"),
 ])
-assert IFACE_DT.itemsize == 32 and NH_DT.itemsize == 32 and ROUTE_DT.itemsize == 12
+assert IFACE_DT.itemsize == 32 and NH_DT.itemsize == 48 and ROUTE_DT.itemsize == 12 and ROUTE6_DT.itemsize == 28
 assert META_DT.itemsize == 8 and VERDICT_DT.itemsize == 8 and STATS_DT.itemsize == 32
 # struct gr_hip_mbuf: the node shim's view of an rte_mbuf + priv (grout_hip.h)
 MBUF_DT = np.dtype([("frame", "<u8"), ("pkt_len", "<u4"), ("data_len", "<u2"), ("data_off", "<u2"),
@@ -82,10 +92,11 @@ MBUF_DT = np.dtype([("frame", "<u8"), ("pkt_len", "<u4"), ("data_len", "<u2"), (
                     ("ck", "u1"), ("edge", "u1"), ("domain", "u1"), ("_pad", "u1"), ("nh", "<u4"),
                     ("_pad1", "<u4")])
 assert MBUF_DT.itemsize == 40
-NODE_NAMES = ["iface_input", "eth_input", "ip_input", "ip_forward", "ip_output", "eth_output", "iface_output"]
+NODE_NAMES = ["iface_input", "eth_input", "ip_input", "ip_forward", "ip_output", "eth_output", "iface_output",
+              "ip6_input", "ip6_forward", "ip6_output"]
 NODE_COUNT = len(NODE_NAMES)
 NODE_STATS_DT = np.dtype([("packets", "<u8", NODE_COUNT), ("calls", "<u8", NODE_COUNT)])
-PTYPE_L3_IPV4 = 0x1
+PTYPE_L3_IPV4, PTYPE_L3_IPV6 = 0x1, 0x10
 
 
 class Batch(ctypes.Structure):
@@ -122,6 +133,9 @@ HIP_API = {
     "gr_hip_edges_ip_output_nh_type": (_I, [_P, _U8, _U8]),
     "gr_hip_edges_ip_output_iface_type": (_I, [_P, _U8, _U8]),
     "gr_hip_edges_iface_output_type": (_I, [_P, _U8, _U8]),
+    "gr_hip_edges_ip6_input_nh_type": (_I, [_P, _U8, _U8]),
+    "gr_hip_edges_ip6_output_nh_type": (_I, [_P, _U8, _U8]),
+    "gr_hip_edges_ip6_output_iface_type": (_I, [_P, _U8, _U8]),
     "gr_hip_iface_set": (_I, [_P, _P, _U32]),
     "gr_hip_iface_del": (_I, [_P, _U16]),
     "gr_hip_nh_set": (_I, [_P, _U32, _P, _U32]),
@@ -133,6 +147,13 @@ HIP_API = {
     "gr_hip_fib4_commit": (_I, [_P, _U16]),
     "gr_hip_fib4_lookup_host": (_I, [_P, _U16, _U32, ctypes.POINTER(_U32)]),
     "gr_hip_fib4_info": (_I, [_P, _U16, ctypes.POINTER(_U32), ctypes.POINTER(_U32), ctypes.POINTER(_U64)]),
+    "gr_hip_fib6_create": (_I, [_P, _U16, _U32, _U32]),
+    "gr_hip_fib6_destroy": (_I, [_P, _U16]),
+    "gr_hip_route6_add": (_I, [_P, _P, _U32, _I]),
+    "gr_hip_route6_del": (_I, [_P, _U16, _U16, _P, _U8]),
+    "gr_hip_fib6_commit": (_I, [_P, _U16]),
+    "gr_hip_fib6_lookup_host": (_I, [_P, _U16, _U16, _P, ctypes.POINTER(_U32)]),
+    "gr_hip_fib6_info": (_I, [_P, _U16, ctypes.POINTER(_U32), ctypes.POINTER(_U32), ctypes.POINTER(_U64)]),
     "gr_hip_queue_create": (_I, [_P, _P, PP]),
     "gr_hip_queue_destroy": (_I, [_P]),
     "gr_hip_queue_stream": (_P, [_P]),
@@ -148,7 +169,7 @@ HIP_API = {
     "gr_hip_dev_free": (_I, [_P, _P]),
     "gr_hip_memcpy_h2d": (_I, [_P, _P, _P, ctypes.c_size_t]),
     "gr_hip_memcpy_d2h": (_I, [_P, _P, _P, ctypes.c_size_t]),
-    "gr_hip_edge_node": (_I, [_U8, _U32]),
+    "gr_hip_edge_node": (_I, [_U8, _U32, _I]),
     "gr_hip_node_stage": (_I, [_P, _U32, _P, _P]),
     "gr_hip_node_apply": (_I, [_P, _U32, _P, _U32, _P, _P, _U32, _P, _U32, _U32, _P]),
     "gr_hip_node_process": (_I, [_P, _P, _U32, _U32, _P]),
@@ -170,6 +191,15 @@ HOST_API = {
     "gr_fib4_num_tbl8": (_U32, [_P]),
     "gr_fib4_tbl8_used": (_U32, [_P]),
     "gr_fib4_n_routes": (_U32, [_P]),
+    "gr_fib6_new": (_P, [_U32, _U32]),
+    "gr_fib6_free": (None, [_P]),
+    "gr_fib6_add": (_I, [_P, _P, _U8, _U32, _I]),
+    "gr_fib6_del": (_I, [_P, _P, _U8]),
+    "gr_fib6_build": (_I, [_P]),
+    "gr_fib6_lookup": (_U32, [_P, _P]),
+    "gr_fib6_lookup_rib": (_U32, [_P, _P]),
+    "gr_fib6_groups_used": (_U32, [_P]),
+    "gr_fib6_n_routes": (_U32, [_P]),
 }
 
 

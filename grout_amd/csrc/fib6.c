@@ -1,0 +1,288 @@
+// SPDX-License-Identifier: BSD-3-Clause
+//
+// fib6.c -- the IPv6 RIB of one VRF and the multibit trie the kernel walks
+// (see fib6.h). The RIB is an exact-prefix hash (rib6_insert_or_replace /
+// rib6_delete semantics of modules/ip6/control/route.c:230-345: one nexthop
+// per (prefix, length), replace on request). The trie is repainted from the
+// RIB on commit, routes in ascending prefix length so that a longer prefix
+// always overwrites a shorter one: a route ending in the first level paints
+// its 2^(16-len) entries; a longer route walks (creating groups, each
+// initialised with the entry it replaces, so shorter prefixes stay visible
+// below it) to the group of its last byte and paints 2^(8-k) entries there.
+#include "fib6.h"
+
+#include <errno.h>
+#include <stdbool.h>
+#include <stdlib.h>
+#include <string.h>
+
+struct rib6_ent {
+	uint8_t ip[16];
+	uint8_t len;
+	uint8_t used; // 0 free, 1 live, 2 deleted (tombstone)
+	uint8_t _pad[2];
+	uint32_t nh;
+};
+
+struct gr_fib6 {
+	struct rib6_ent *ht;
+	uint32_t cap; // power of two
+	uint32_t n_routes, n_tomb, max_routes;
+	uint32_t *top; // GR_FIB6_TOP
+	uint32_t *groups; // max_groups * GR_FIB6_GROUP
+	uint32_t max_groups, n_groups;
+	uint32_t max_slot;
+	bool dirty;
+	uint64_t generation;
+};
+
+static void mask6(uint8_t out[16], const uint8_t ip[16], uint8_t len) {
+	for (int i = 0; i < 16; i++) {
+		int bits = (int)len - 8 * i;
+		uint8_t m = bits >= 8 ? 0xff : bits <= 0 ? 0 : (uint8_t)(0xff << (8 - bits));
+		out[i] = ip[i] & m;
+	}
+}
+
+static uint32_t hash6(const uint8_t ip[16], uint8_t len) {
+	uint64_t a, b;
+	memcpy(&a, ip, 8);
+	memcpy(&b, ip + 8, 8);
+	uint64_t h = (a * 0x9e3779b97f4a7c15ull) ^ (b + 0x632be59bd9b4e019ull + len);
+	h ^= h >> 29;
+	h *= 0xbf58476d1ce4e5b9ull;
+	h ^= h >> 32;
+	return (uint32_t)h;
+}
+
+// Slot of (ip, len): live entry, or the first free/tombstone slot when absent.
+static struct rib6_ent *ht_find(const gr_fib6_t *f, const uint8_t ip[16], uint8_t len, bool *found) {
+	uint32_t m = f->cap - 1, i = hash6(ip, len) & m;
+	struct rib6_ent *first_free = NULL;
+	for (uint32_t probe = 0; probe < f->cap; probe++, i = (i + 1) & m) {
+		struct rib6_ent *e = &f->ht[i];
+		if (e->used == 0) {
+			*found = false;
+			return first_free ? first_free : e;
+		}
+		if (e->used == 2) {
+			if (!first_free)
+				first_free = e;
+			continue;
+		}
+		if (e->len == len && memcmp(e->ip, ip, 16) == 0) {
+			*found = true;
+			return e;
+		}
+	}
+	*found = false;
+	return first_free;
+}
+
+gr_fib6_t *gr_fib6_new(uint32_t max_routes, uint32_t max_groups) {
+	if (max_routes == 0 || max_routes > (1u << 28))
+		return NULL;
+	if (max_groups == 0)
+		max_groups = 1u << 16;
+	gr_fib6_t *f = calloc(1, sizeof(*f));
+	if (f == NULL)
+		return NULL;
+	uint32_t cap = 16;
+	while (cap < 2 * max_routes)
+		cap <<= 1;
+	f->cap = cap;
+	f->max_routes = max_routes;
+	f->max_groups = max_groups;
+	f->ht = calloc(cap, sizeof(*f->ht));
+	f->top = calloc(GR_FIB6_TOP, sizeof(uint32_t));
+	f->groups = malloc((size_t)max_groups * GR_FIB6_GROUP * sizeof(uint32_t));
+	if (!f->ht || !f->top || !f->groups) {
+		gr_fib6_free(f);
+		return NULL;
+	}
+	return f;
+}
+
+void gr_fib6_free(gr_fib6_t *f) {
+	if (f == NULL)
+		return;
+	free(f->ht);
+	free(f->top);
+	free(f->groups);
+	free(f);
+}
+
+static int ht_rehash(gr_fib6_t *f) { // drop tombstones
+	struct rib6_ent *old = f->ht;
+	f->ht = calloc(f->cap, sizeof(*f->ht));
+	if (f->ht == NULL) {
+		f->ht = old;
+		return -ENOMEM;
+	}
+	for (uint32_t i = 0; i < f->cap; i++) {
+		if (old[i].used != 1)
+			continue;
+		bool found;
+		struct rib6_ent *e = ht_find(f, old[i].ip, old[i].len, &found);
+		*e = old[i];
+	}
+	f->n_tomb = 0;
+	free(old);
+	return 0;
+}
+
+int gr_fib6_add(gr_fib6_t *f, const uint8_t ip[16], uint8_t len, uint32_t nh, int replace) {
+	if (f == NULL || ip == NULL || len > 128 || nh == 0 || nh >= GR_FIB6_EXT)
+		return -EINVAL;
+	uint8_t key[16];
+	mask6(key, ip, len);
+	bool found;
+	struct rib6_ent *e = ht_find(f, key, len, &found);
+	if (found) {
+		if (!replace)
+			return -EEXIST;
+		if (e->nh != nh) {
+			e->nh = nh;
+			f->dirty = true;
+		}
+	} else {
+		if (f->n_routes >= f->max_routes || e == NULL)
+			return -ENOSPC;
+		if (e->used == 2)
+			f->n_tomb--;
+		memcpy(e->ip, key, 16);
+		e->len = len;
+		e->nh = nh;
+		e->used = 1;
+		f->n_routes++;
+		f->dirty = true;
+	}
+	if (nh > f->max_slot)
+		f->max_slot = nh;
+	return 0;
+}
+
+int gr_fib6_del(gr_fib6_t *f, const uint8_t ip[16], uint8_t len) {
+	if (f == NULL || ip == NULL || len > 128)
+		return -EINVAL;
+	uint8_t key[16];
+	mask6(key, ip, len);
+	bool found;
+	struct rib6_ent *e = ht_find(f, key, len, &found);
+	if (!found)
+		return -ENOENT;
+	e->used = 2;
+	f->n_routes--;
+	f->n_tomb++;
+	f->dirty = true;
+	if (f->n_tomb > f->cap / 4)
+		(void)ht_rehash(f); // a failed rehash only costs probe length
+	return 0;
+}
+
+static int paint(gr_fib6_t *f, const struct rib6_ent *r) {
+	const uint8_t *ip = r->ip;
+	if (r->len <= 16) {
+		uint32_t base = ((uint32_t)ip[0] << 8) | ip[1];
+		uint32_t cnt = 1u << (16 - r->len);
+		for (uint32_t i = 0; i < cnt; i++)
+			f->top[base + i] = r->nh; // ascending order: never a group yet
+		return 0;
+	}
+	uint32_t *e = &f->top[((uint32_t)ip[0] << 8) | ip[1]];
+	unsigned consumed = 16, b = 2;
+	for (;;) {
+		if (!(*e & GR_FIB6_EXT)) {
+			if (f->n_groups >= f->max_groups)
+				return -ENOSPC;
+			uint32_t g = f->n_groups++;
+			uint32_t *grp = f->groups + (size_t)g * GR_FIB6_GROUP;
+			for (int i = 0; i < GR_FIB6_GROUP; i++)
+				grp[i] = *e;
+			*e = GR_FIB6_EXT | g;
+		}
+		uint32_t *grp = f->groups + (size_t)(*e & ~GR_FIB6_EXT) * GR_FIB6_GROUP;
+		if (r->len <= consumed + 8) {
+			unsigned nb = r->len - consumed;
+			uint32_t base = ip[b], cnt = 1u << (8 - nb);
+			for (uint32_t i = 0; i < cnt; i++)
+				grp[base + i] = r->nh;
+			return 0;
+		}
+		e = &grp[ip[b]];
+		b++;
+		consumed += 8;
+	}
+}
+
+int gr_fib6_build(gr_fib6_t *f) {
+	if (f == NULL)
+		return -EINVAL;
+	if (!f->dirty)
+		return 0;
+	// counting sort of the live routes by prefix length
+	uint32_t count[130] = {0};
+	for (uint32_t i = 0; i < f->cap; i++)
+		if (f->ht[i].used == 1)
+			count[f->ht[i].len + 1]++;
+	for (int l = 1; l < 130; l++)
+		count[l] += count[l - 1];
+	const struct rib6_ent **order = malloc((size_t)(f->n_routes ? f->n_routes : 1) * sizeof(*order));
+	if (order == NULL)
+		return -ENOMEM;
+	for (uint32_t i = 0; i < f->cap; i++)
+		if (f->ht[i].used == 1)
+			order[count[f->ht[i].len]++] = &f->ht[i];
+	memset(f->top, 0, GR_FIB6_TOP * sizeof(uint32_t));
+	f->n_groups = 0;
+	int ret = 0;
+	for (uint32_t i = 0; i < f->n_routes && ret == 0; i++)
+		ret = paint(f, order[i]);
+	free(order);
+	if (ret < 0)
+		return ret;
+	f->dirty = false;
+	f->generation++;
+	return 0;
+}
+
+uint32_t gr_fib6_lookup(const gr_fib6_t *f, const uint8_t ip[16]) {
+	uint32_t ent = f->top[((uint32_t)ip[0] << 8) | ip[1]];
+	for (int b = 2; b < 16 && (ent & GR_FIB6_EXT); b++)
+		ent = f->groups[(size_t)(ent & ~GR_FIB6_EXT) * GR_FIB6_GROUP + ip[b]];
+	return ent & GR_FIB6_EXT ? 0 : ent;
+}
+
+uint32_t gr_fib6_lookup_rib(const gr_fib6_t *f, const uint8_t ip[16]) {
+	for (int len = 128; len >= 0; len--) {
+		uint8_t key[16];
+		mask6(key, ip, (uint8_t)len);
+		bool found;
+		const struct rib6_ent *e = ht_find(f, key, (uint8_t)len, &found);
+		if (found)
+			return e->nh;
+	}
+	return 0;
+}
+
+const uint32_t *gr_fib6_top(const gr_fib6_t *f) {
+	return f->top;
+}
+const uint32_t *gr_fib6_groups(const gr_fib6_t *f) {
+	return f->groups;
+}
+uint32_t gr_fib6_groups_used(const gr_fib6_t *f) {
+	return f->n_groups;
+}
+uint32_t gr_fib6_max_groups(const gr_fib6_t *f) {
+	return f->max_groups;
+}
+uint32_t gr_fib6_n_routes(const gr_fib6_t *f) {
+	return f->n_routes;
+}
+uint32_t gr_fib6_max_slot(const gr_fib6_t *f) {
+	return f->max_slot;
+}
+uint64_t gr_fib6_generation(const gr_fib6_t *f) {
+	return f->generation;
+}

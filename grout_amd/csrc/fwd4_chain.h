@@ -30,7 +30,10 @@ __device__ __forceinline__ kctx make_kctx(const fwd4_params &A, const fwd4_edges
 	P.readable = A.readable;
 	P.edges = edges;
 	P.stats = A.stats;
-	P.ip4_edge = ip4_edge_of(*edges);
+	P.ip4_edge = type_edge_of(*edges, 0x0008u);
+	P.ip6_edge = type_edge_of(*edges, 0xdd86u);
+	P.rx6 = T->rx6;
+	P.adj6 = T->adj6;
 	return P;
 }
 
@@ -64,20 +67,24 @@ __device__ __forceinline__ rxv load_rx_scalar(const kctx &P, uint32_t id) {
 	return unpack_rx(uint4{v[0], v[1], v[2], v[3]}, uint4{v[4], v[5], v[6], v[7]});
 }
 
+#define HEAD_DONE 0 // the packet left the chain, r.edge set
+#define HEAD_IP4 4 // continue to the IPv4 FIB lookup: dst, data_len set
+#define HEAD_IP6 6 // continue into ip6_input (chain6): data_len set
+
 // iface_input -> eth_input -> ip_input up to the FIB lookup, for the packet
-// in row `row` of R. Returns false when the packet left the chain (r.edge
-// set); otherwise dst (network order as stored) and data_len are set.
-__device__ __forceinline__ bool chain_head(const kctx &P, const uint8_t *R, uint32_t row, const gr_hip_pkt_meta &m,
+// in row `row` of R. Returns HEAD_*; dst is the IPv4 destination in network
+// order as stored.
+__device__ __forceinline__ int chain_head(const kctx &P, const uint8_t *R, uint32_t row, const gr_hip_pkt_meta &m,
 					  rxv &rx, result &r, uint32_t &dst, uint32_t &data_len, const uint8_t *frame) {
 	// ---- iface_input (iface_input.c:52-112)
 	if (rx.id == 0)
-		return false; // PUNT
+		return HEAD_DONE; // PUNT
 	const uint32_t vlan = m.vlan_ck & 0xfff;
 	if (vlan != 0 && (rx.flags & FWD4_RX_VLAN_DEMUX)) { // :74-86
 		rxv v = load_rx(P, vlan_lookup(P, rx.id, vlan));
 		if (v.id == 0) {
 			r.edge = GR_HIP_E_IFACE_INPUT_UNKNOWN_VLAN;
-			return false;
+			return HEAD_DONE;
 		}
 		rx = v;
 	}
@@ -88,7 +95,7 @@ __device__ __forceinline__ bool chain_head(const kctx &P, const uint8_t *R, uint
 			r.rx_if = rx.id;
 			r.rx_par = m.iface != rx.id ? m.iface : 0;
 		}
-		return false;
+		return HEAD_DONE;
 	}
 	r.rx_if = rx.id; // IFACE_STATS_INC :93-95
 	r.rx_par = m.iface != rx.id ? m.iface : 0;
@@ -99,11 +106,11 @@ __device__ __forceinline__ bool chain_head(const kctx &P, const uint8_t *R, uint
 	const uint32_t type = bswap16(type_raw);
 	if (type < 1536 || type == 0x8870) { // snap.h:11-12
 		r.edge = GR_HIP_E_SNAP_INPUT;
-		return false;
+		return HEAD_DONE;
 	}
 	if (!(rx.flags & FWD4_RX_MAC_OK)) {
 		r.edge = GR_HIP_E_ETH_INPUT_INVALID_IFACE;
-		return false;
+		return HEAD_DONE;
 	}
 	if (c0.x & 1) {
 		bool bc = c0.x == 0xffffffffu && lo16(c0.y) == 0xffff;
@@ -115,9 +122,11 @@ __device__ __forceinline__ bool chain_head(const kctx &P, const uint8_t *R, uint
 	}
 	data_len = m.pkt_len >= 14 ? m.pkt_len - 14u : m.pkt_len;
 	const uint32_t e = eth_type_edge(P, type_raw);
+	if (e == GR_HIP_EDGE_CHAIN6)
+		return HEAD_IP6;
 	if (e != CHAIN) {
 		r.edge = e;
-		return false;
+		return HEAD_DONE;
 	}
 
 	// ---- ip_input (ip_input.c:58-187)
@@ -125,7 +134,7 @@ __device__ __forceinline__ bool chain_head(const kctx &P, const uint8_t *R, uint
 	const uint32_t ihl = vihl & 0xf;
 	if (data_len < 20) { // (1)
 		r.edge = GR_HIP_E_IP_INPUT_BAD_LENGTH;
-		return false;
+		return HEAD_DONE;
 	}
 	const u4v c1 = lds_get(R, row, 1);
 	const u4v c2 = lds_get(R, row, 2);
@@ -137,7 +146,7 @@ __device__ __forceinline__ bool chain_head(const kctx &P, const uint8_t *R, uint
 			r.rx_if = r.rx_par = 0;
 			r.domain = 0;
 			r.iface = m.iface;
-			return false;
+			return HEAD_DONE;
 		}
 		uint32_t sum = 0;
 		if (ihl != 0) {
@@ -165,40 +174,40 @@ __device__ __forceinline__ bool chain_head(const kctx &P, const uint8_t *R, uint
 		sum = (sum & 0xffff) + (sum >> 16);
 		if (sum != 0xffff) {
 			r.edge = GR_HIP_E_IP_INPUT_BAD_CHECKSUM;
-			return false;
+			return HEAD_DONE;
 		}
 	} else if (ck == GR_HIP_CKSUM_BAD) {
 		r.edge = GR_HIP_E_IP_INPUT_BAD_CHECKSUM;
-		return false;
+		return HEAD_DONE;
 	}
 	dst = hi16(c1.w) | (lo16(c2.x) << 16);
 	if (dst == 0) {
 		r.edge = GR_HIP_E_IP_INPUT_BAD_ADDRESS;
-		return false;
+		return HEAD_DONE;
 	}
 	if ((vihl >> 4) != 4) { // (3)
 		r.edge = GR_HIP_E_IP_INPUT_BAD_VERSION;
-		return false;
+		return HEAD_DONE;
 	}
 	if (ihl * 4 < 20) { // (4)
 		r.edge = GR_HIP_E_IP_INPUT_BAD_LENGTH;
-		return false;
+		return HEAD_DONE;
 	}
 	if (bswap16(lo16(c1.x)) < 20) { // (5)
 		r.edge = GR_HIP_E_IP_INPUT_BAD_LENGTH;
-		return false;
+		return HEAD_DONE;
 	}
 	if (r.domain != GR_HIP_ETH_DOMAIN_LOCAL) {
 		bool mc = r.domain == GR_HIP_ETH_DOMAIN_BROADCAST || r.domain == GR_HIP_ETH_DOMAIN_MULTICAST;
 		r.edge = mc ? GR_HIP_E_IP_INPUT_LOCAL : GR_HIP_E_IP_INPUT_OTHER_HOST;
-		return false;
+		return HEAD_DONE;
 	}
 	const uint32_t d0 = dst & 0xff;
 	if (dst == 0xffffffffu || (d0 >= 224 && d0 <= 239)) {
 		r.edge = GR_HIP_E_IP_INPUT_LOCAL;
-		return false;
+		return HEAD_DONE;
 	}
-	return true;
+	return HEAD_IP4;
 }
 
 // fib4_lookup (route.c:147-167) in the iface's VRF table.
@@ -337,4 +346,163 @@ __device__ __forceinline__ void fast_tail(uint8_t *R, uint32_t row, result &r, u
 	lds_put(R, row, 0, c0);
 	r.edge = GR_HIP_E_PORT_OUTPUT;
 	r.tx_if = oif;
+}
+
+// ---- IPv6: ip6_input -> ip6_forward -> ip6_output -> eth_output -> iface_output
+
+// 32-bit word of the header line at byte offset 4 * k + 2 (the IPv6
+// addresses start at 22 and 38): from the 16 little-endian line words.
+__device__ __forceinline__ uint32_t word_at2(const uint32_t (&w)[16], int k) {
+	return (w[k] >> 16) | (w[k + 1] << 16);
+}
+
+__device__ __forceinline__ uint32_t byte_of(const uint32_t (&a)[4], int i) {
+	return (a[i >> 2] >> (8 * (i & 3))) & 0xff;
+}
+
+// rte_fib6_lookup (route.c:151-173) in the fib6.h trie of the iface's VRF:
+// key = dst with link-local addresses scoped to the ingress iface
+// (addr6_linklocal_scope, ip6.h:23-36).
+__device__ __forceinline__ uint32_t chain_fib6(const fwd4_rx6 &v, const uint32_t (&dst)[4], uint32_t iface_id) {
+	if (v.top == nullptr)
+		return 0;
+	uint32_t key[4] = {dst[0], dst[1], dst[2], dst[3]};
+	if ((key[0] & 0xff) == 0xfe && (key[0] & 0xc000) == 0x8000)
+		key[0] = (key[0] & 0xffff) | ((iface_id >> 8) << 16) | ((iface_id & 0xff) << 24);
+	uint32_t ent = gld(v.top + ((byte_of(key, 0) << 8) | byte_of(key, 1)));
+	for (int b = 2; b < 16 && (ent & 0x80000000u); b++)
+		ent = gld(v.groups + (size_t)(ent & 0x7fffffffu) * 256 + byte_of(key, b));
+	return (ent & 0x80000000u) ? 0 : ent;
+}
+
+// From ip6_input (ip6_input.c:58-146) to iface_output for an IPv6 packet in
+// row `row` of R, eth_input done (domain in r, data_len = the mbuf's after
+// its adj). Rewrites the hop limit and the L2 header in R.
+__device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, const gr_hip_pkt_meta &m,
+				       const rxv &rx, result &r, uint32_t data_len) {
+	if (data_len < 40) { // :62-69
+		r.edge = GR_HIP_E_IP6_INPUT_BAD_LENGTH;
+		return;
+	}
+	uint32_t w[16];
+#pragma unroll
+	for (int k = 0; k < 4; k++) {
+		const u4v c = lds_get(R, row, k);
+		w[4 * k] = c.x;
+		w[4 * k + 1] = c.y;
+		w[4 * k + 2] = c.z;
+		w[4 * k + 3] = c.w;
+	}
+	// IPv6 header at byte 14: version 14, hop limit 21, src 22-37, dst 38-53
+	if ((((w[3] >> 16) & 0xff) & 0xf0) != 0x60) { // rte_ipv6_check_version, :71-74
+		r.edge = GR_HIP_E_IP6_INPUT_BAD_VERSION;
+		return;
+	}
+	const uint32_t dst[4] = {word_at2(w, 9), word_at2(w, 10), word_at2(w, 11), word_at2(w, 12)};
+	const uint32_t src0 = (w[5] >> 16) & 0xff;
+	if (src0 == 0xff || (dst[0] | dst[1] | dst[2] | dst[3]) == 0) { // mcast src, unspec dst :76-80
+		r.edge = GR_HIP_E_IP6_INPUT_BAD_ADDR;
+		return;
+	}
+	if ((dst[0] & 0xff) == 0xff) { // :82-101
+		const uint32_t scope = (dst[0] >> 8) & 0xf; // rte_ipv6_mc_scope
+		if (scope <= 1) { // RTE_IPV6_MC_SCOPE_NONE / _IFACELOCAL
+			r.edge = GR_HIP_E_IP6_INPUT_BAD_ADDR;
+		} else { // mcast6_get_member: group membership lives on the CPU
+			r.edge = GR_HIP_E_PUNT;
+			r.rx_if = r.rx_par = 0;
+			r.domain = 0;
+			r.iface = m.iface;
+		}
+		return;
+	}
+	if (r.domain != GR_HIP_ETH_DOMAIN_LOCAL) { // :104-118 (LOOPBACK never from a port)
+		const bool mc = r.domain == GR_HIP_ETH_DOMAIN_BROADCAST || r.domain == GR_HIP_ETH_DOMAIN_MULTICAST;
+		r.edge = mc ? GR_HIP_E_IP6_INPUT_LOCAL : GR_HIP_E_IP6_INPUT_OTHER_HOST;
+		return;
+	}
+	const fwd4_rx6 v = {gld(&P.rx6[rx.id].top), gld(&P.rx6[rx.id].groups)};
+	uint32_t slot = chain_fib6(v, dst, rx.id); // :122-128
+	if (slot == 0 || slot > P.max_nh) {
+		r.edge = GR_HIP_E_IP6_ERROR_DEST_UNREACH;
+		return;
+	}
+	const uint4 *ap = reinterpret_cast<const uint4 *>(P.adj6 + slot);
+	uint4 a = gld4(ap), b = gld4(ap + 1), c = gld4(ap + 2);
+	if ((a.x & 0xff) == GR_HIP_NH_T_GROUP) { // nexthop_group_get_nh, nexthop.h:89-96
+		const uint4 g = gld4(reinterpret_cast<const uint4 *>(P.adj + slot) + 2);
+		const uint32_t n_members = g.x & 0xffff, reta_size = g.x >> 16;
+		if (n_members == 1) {
+			slot = g.z;
+		} else if (n_members == 0) {
+			slot = 0;
+		} else {
+			const uint32_t i = g.y + (m.rss & (reta_size - 1));
+			slot = i < P.reta_cap ? gld(P.reta + i) : 0;
+		}
+		if (slot == 0 || slot > P.max_nh) {
+			r.edge = GR_HIP_E_IP6_ERROR_DEST_UNREACH;
+			return;
+		}
+		ap = reinterpret_cast<const uint4 *>(P.adj6 + slot);
+		a = gld4(ap);
+		b = gld4(ap + 1);
+		c = gld4(ap + 2);
+	}
+	r.nh = slot; // l3_mbuf_data(mbuf)->nh :151-153
+	const uint32_t e_in = (a.x >> 8) & 0xff, flags = (a.x >> 16) & 0xff;
+	if (e_in != CHAIN) { // nh_type_edges :130-132
+		r.edge = e_in;
+		return;
+	}
+	const bool is_nh = dst[0] == b.w && dst[1] == c.x && dst[2] == c.y && dst[3] == c.z;
+	if ((flags & FWD4_ADJ_LOCAL) && is_nh) { // :136-145
+		r.edge = GR_HIP_E_IP6_INPUT_LOCAL;
+		return;
+	}
+
+	// ---- ip6_forward (ip6_forward.c:25-30)
+	const uint32_t hop = (w[5] >> 8) & 0xff;
+	if (hop <= 1) {
+		r.edge = GR_HIP_E_IP6_ERROR_TTL_EXCEEDED;
+		return;
+	}
+	u4v c1 = lds_get(R, row, 1);
+	c1.y = (c1.y & 0xffff00ffu) | ((hop - 1) << 8);
+	lds_put(R, row, 1, c1);
+
+	// ---- ip6_output (ip6_output.c:70-123), adjacency resolved ahead of time
+	const uint32_t e_pre = a.x >> 24, e_mid = a.y & 0xff, e_post = (a.y >> 8) & 0xff;
+	if (e_pre != CHAIN) { // nh type edge :85-87, no iface :94-97
+		r.edge = e_pre;
+		return;
+	}
+	if (data_len > (a.z & 0xffff)) { // rte_pktmbuf_pkt_len > mtu :99-102
+		r.edge = GR_HIP_E_IP6_OUTPUT_TOO_BIG;
+		return;
+	}
+	r.iface = a.y >> 16; // mbuf_data(mbuf)->iface = iface :107
+	if (e_mid != CHAIN) { // iface type edge :106-109, state :113-119
+		r.edge = e_mid;
+		return;
+	}
+	if ((flags & FWD4_ADJ_LINK) && !is_nh) { // :113-119
+		r.edge = GR_HIP_E_IP6_HOLD;
+		return;
+	}
+
+	// ---- eth_output (eth_output.c:297-316) + iface_output (iface_output.c:213-246)
+	u4v c0 = lds_get(R, row, 0);
+	c0.x = b.x; // dst MAC 0-3
+	c0.y = (c0.y & 0xffff0000u) | (b.y & 0xffff); // dst MAC 4-5
+	r.edge = e_post;
+	if (e_post != GR_HIP_E_ETH_OUTPUT_NO_MAC) {
+		c0.y = b.y; // dst MAC 4-5, src MAC 0-1
+		c0.z = b.z; // src MAC 2-5
+		c0.w = (c0.w & 0xffff0000u) | 0xdd86u; // RTE_BE16(RTE_ETHER_TYPE_IPV6)
+		r.iface = a.z >> 16;
+		r.tx_if = a.w & 0xffff;
+		r.tx_par = a.w >> 16;
+	}
+	lds_put(R, row, 0, c0);
 }

@@ -39,7 +39,10 @@ struct kctx {
 	const uint16_t *vlan_vals;
 	uint32_t reta_cap, vlan_mask, max_ifaces, max_nh, readable;
 	const fwd4_edges *edges; // LDS copy
-	uint32_t ip4_edge; // eth_input edge of ether type IPv4 (wave-uniform)
+	uint32_t ip4_edge; // eth_input edges of ether types IPv4 / IPv6 (wave-uniform)
+	uint32_t ip6_edge;
+	const fwd4_rx6 *rx6;
+	const fwd4_adj6 *adj6;
 	gr_hip_iface_stats *stats;
 };
 
@@ -193,6 +196,8 @@ __device__ __forceinline__ void wave_count(stat_slot *slots, const kctx &P, uint
 __device__ __forceinline__ uint32_t eth_type_edge(const kctx &P, uint32_t type_raw) {
 	if (type_raw == 0x0008u) // RTE_BE16(RTE_ETHER_TYPE_IPV4)
 		return P.ip4_edge;
+	if (type_raw == 0xdd86u) // RTE_BE16(RTE_ETHER_TYPE_IPV6)
+		return P.ip6_edge;
 	uint32_t e = GR_HIP_E_ETH_INPUT_UNKNOWN_TYPE;
 	const fwd4_edges &E = *P.edges;
 	for (uint32_t i = 0; i < E.n_eth_types; i++)
@@ -201,11 +206,12 @@ __device__ __forceinline__ uint32_t eth_type_edge(const kctx &P, uint32_t type_r
 	return e;
 }
 
-// Edge of ether type IPv4, computed once per workgroup from the LDS table.
-__device__ __forceinline__ uint32_t ip4_edge_of(const fwd4_edges &E) {
+// Edge of one ether type (raw big-endian value), computed once per wave from
+// the LDS table.
+__device__ __forceinline__ uint32_t type_edge_of(const fwd4_edges &E, uint32_t type_raw) {
 	uint32_t e = GR_HIP_E_ETH_INPUT_UNKNOWN_TYPE;
 	for (uint32_t i = 0; i < E.n_eth_types; i++)
-		if (E.eth_type_be[i] == 0x0008u)
+		if (E.eth_type_be[i] == type_raw)
 			e = E.eth_type_edge[i];
 	return __builtin_amdgcn_readfirstlane(e);
 }

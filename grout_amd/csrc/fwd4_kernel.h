@@ -22,6 +22,9 @@ struct fwd4_edges {
 	uint8_t out_nh[8]; // ip_output nh type -> edge (CHAIN = eth_output)
 	uint8_t out_iface[8]; // ip_output iface type -> edge
 	uint8_t iout_type[8]; // iface_output iface type -> edge
+	uint8_t in6_nh[8]; // ip6_input nh type -> edge (CHAIN = ip6_forward)
+	uint8_t out6_nh[8]; // ip6_output nh type -> edge (CHAIN = eth_output)
+	uint8_t out6_iface[8]; // ip6_output iface type -> edge
 };
 
 // Per-iface RX view, 32 bytes: what iface_input and eth_input need from an
@@ -41,6 +44,13 @@ struct fwd4_rx {
 	uint8_t _pad[6];
 	const uint32_t *tbl24; // NULL: no FIB (no route)
 	const uint32_t *tbl8;
+};
+
+// Per-iface IPv6 view, 16 bytes: the FIB6 of the iface's VRF (get_fib6,
+// modules/ip6/control/route.c:51-64). NULL: no IPv6 FIB (no route).
+struct fwd4_rx6 {
+	const uint32_t *top; // [65536] (fib6.h encoding)
+	const uint32_t *groups; // [n][256]
 };
 
 // Per-nexthop adjacency, 64 bytes: the nexthop fields ip_input reads plus
@@ -71,6 +81,27 @@ struct fwd4_adj {
 	uint32_t _pad[5];
 };
 
+// Per-nexthop IPv6 adjacency, 64 bytes: fwd4_adj for the ip6_input /
+// ip6_output edge tables (ip6_input.c:130-145, ip6_output.c:70-123). e_pre
+// is the nh type edge or ERROR (before the MTU check, iface = ingress),
+// e_mid the iface type edge or HOLD by state (after it, iface = oif).
+struct fwd4_adj6 {
+	uint8_t type;
+	uint8_t e_in;
+	uint8_t flags; // FWD4_ADJ_LOCAL / FWD4_ADJ_LINK
+	uint8_t e_pre;
+	uint8_t e_mid;
+	uint8_t e_post;
+	uint16_t oif;
+	uint16_t mtu;
+	uint16_t post_iface;
+	uint16_t tx_if, tx_par;
+	uint8_t dmac[6];
+	uint8_t smac[6];
+	uint8_t ipv6[16];
+	uint32_t _pad[5];
+};
+
 // Fast adjacency, 16 bytes: a nexthop whose packets take the plain forward
 // (L3, no LOCAL/LINK flag, ip_output/eth_output/iface_output all chain to
 // port_output of a port oif: post_iface = tx iface = oif, no parent) needs
@@ -88,6 +119,8 @@ struct fwd4_tables {
 	const struct fwd4_rx *rx; // [max_ifaces]
 	const struct fwd4_adj *adj; // [max_nh + 1]
 	const struct fwd4_nhf *nhf; // [max_nh + 1]
+	const struct fwd4_rx6 *rx6; // [max_ifaces]
+	const struct fwd4_adj6 *adj6; // [max_nh + 1]
 	const uint32_t *reta;
 	const uint32_t *vlan_keys; // (parent << 16 | vlan_id) + 1, 0 = empty
 	const uint16_t *vlan_vals;

@@ -237,7 +237,8 @@ __device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds<C> &L
 		if (live) {
 			uint32_t dst = 0, data_len = 0;
 			const uint8_t *frame = A.in + (size_t)(base + lane) * A.in_stride;
-			if (chain_head(P, R, lane, m, rx, r, dst, data_len, frame)) {
+			const int head = chain_head(P, R, lane, m, rx, r, dst, data_len, frame);
+			if (head == HEAD_IP4) {
 				const uint32_t slot = chain_fib(rx, dst);
 				if (slot == 0 || slot > P.max_nh) {
 					r.edge = GR_HIP_E_IP_ERROR_DEST_UNREACH; // NO_ROUTE :150-153
@@ -251,6 +252,8 @@ __device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds<C> &L
 						chain_tail(P, R, lane, m, rx.flags, r, dst, data_len, slot, gld4(ap), gld4(ap + 1));
 					}
 				}
+			} else if (head == HEAD_IP6) {
+				chain6(P, R, lane, m, rx, r, data_len);
 			}
 		}
 		L.verdict[s][lane] = u2v{r.edge | (r.domain << 8) | (r.iface << 16), r.nh};

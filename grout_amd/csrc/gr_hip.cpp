@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include "fib4.h"
+#include "fib6.h"
 #include "fwd4_kernel.h"
 
 #include <algorithm>
@@ -62,6 +63,12 @@ struct vrf_fib {
 	uint32_t max_slot = 0; // highest nexthop slot ever routed (never decreases)
 	uint32_t num_tbl8 = 0;
 	bool uploaded = false; // tables uploaded at least once
+	// IPv6: fib6.h trie, on the device as top[65536] followed by the groups
+	gr_fib6_t *rib6 = nullptr;
+	uint32_t *d6 = nullptr;
+	uint32_t d6_groups = 0; // group capacity of d6
+	uint64_t gen6 = 0; // fib6 generation on the device
+	bool uploaded6 = false;
 };
 
 struct host_slot {
@@ -106,6 +113,10 @@ struct gr_hip_ctx {
 	fwd4_adj *d_adj;
 	std::vector<fwd4_nhf> nhf; // fast adjacencies (host image)
 	fwd4_nhf *d_nhf;
+	std::vector<fwd4_rx6> rx6; // IPv6 views and adjacencies (host images)
+	std::vector<fwd4_adj6> adj6;
+	fwd4_rx6 *d_rx6;
+	fwd4_adj6 *d_adj6;
 	uint32_t *d_reta;
 	uint32_t d_reta_cap;
 	uint32_t *d_vlan_keys;
@@ -188,6 +199,88 @@ static fwd4_rx make_rx(const gr_hip_ctx *c, uint32_t id) {
 	return r;
 }
 
+// IPv6 view of iface `id`: the FIB6 of its VRF (get_fib6, route.c:51-64).
+static fwd4_rx6 make_rx6(const gr_hip_ctx *c, uint32_t id) {
+	fwd4_rx6 r = {nullptr, nullptr};
+	const gr_hip_iface *i = iface_get(c, id);
+	if (i == nullptr)
+		return r;
+	const gr_hip_iface *vrf = iface_get(c, i->vrf_id);
+	if (vrf != nullptr && vrf->type == GR_HIP_IFACE_TYPE_VRF && c->vrfs[i->vrf_id].rib6 != nullptr
+	    && c->vrfs[i->vrf_id].uploaded6) {
+		const vrf_fib &v = c->vrfs[i->vrf_id];
+		r.top = v.d6;
+		r.groups = v.d6 + GR_FIB6_TOP;
+	}
+	return r;
+}
+
+// eth_output -> iface_output for a nexthop leaving through `oif`
+// (eth_output.c:297-316, iface_output.c:213-246), shared by both AFs.
+template <typename A>
+static void fill_post(const gr_hip_ctx *c, const gr_hip_nh &nh, const gr_hip_iface *oif, A &a) {
+	const fwd4_edges &E = c->edges;
+	memcpy(a.dmac, nh.mac, 6);
+	a.post_iface = oif->id;
+	if (!oif->mac_ok) {
+		a.e_post = GR_HIP_E_ETH_OUTPUT_NO_MAC;
+		return;
+	}
+	memcpy(a.smac, oif->mac, 6);
+	const gr_hip_iface *out = oif;
+	if (oif->type == GR_HIP_IFACE_TYPE_VLAN) {
+		out = iface_get(c, oif->parent_id);
+		if (out == nullptr) {
+			a.e_post = GR_HIP_E_IFACE_OUTPUT_VLAN_NO_PARENT;
+			return;
+		}
+	}
+	if (!(oif->flags & GR_HIP_IFACE_F_UP)) {
+		a.e_post = GR_HIP_E_IFACE_OUTPUT_ADMIN_DOWN;
+		return;
+	}
+	a.tx_if = oif->id;
+	a.tx_par = out != oif ? out->id : 0;
+	a.post_iface = out->id;
+	a.e_post = out->type < 8 ? E.iout_type[out->type] : GR_HIP_E_IFACE_OUTPUT_INVAL_TYPE;
+}
+
+// IPv6 adjacency of nexthop `slot`: ip6_input's view (ip6_input.c:130-145)
+// and ip6_output -> eth_output -> iface_output resolved for the nexthop
+// (ip6_output.c:70-123), leaving the MTU and LINK destination checks.
+static fwd4_adj6 make_adj6(const gr_hip_ctx *c, uint32_t slot) {
+	const fwd4_edges &E = c->edges;
+	const gr_hip_nh &nh = c->nh[slot];
+	fwd4_adj6 a;
+	memset(&a, 0, sizeof(a));
+	a.type = nh.type;
+	a.e_in = nh.type < 8 ? E.in6_nh[nh.type] : GR_HIP_EDGE_CHAIN;
+	a.flags = ((nh.type == GR_HIP_NH_T_L3 && (nh.flags & GR_HIP_NH_F_LOCAL)) ? FWD4_ADJ_LOCAL : 0)
+		| ((nh.flags & GR_HIP_NH_F_LINK) ? FWD4_ADJ_LINK : 0);
+	memcpy(a.ipv6, nh.ipv6, 16);
+	a.e_mid = a.e_post = GR_HIP_EDGE_CHAIN;
+	uint8_t e = nh.type < 8 ? E.out6_nh[nh.type] : GR_HIP_EDGE_CHAIN;
+	if (e != GR_HIP_EDGE_CHAIN) { // :85-87
+		a.e_pre = e;
+		return a;
+	}
+	const gr_hip_iface *oif = iface_get(c, nh.iface_id);
+	if (oif == nullptr) { // :94-97
+		a.e_pre = GR_HIP_E_IP6_OUTPUT_ERROR;
+		return a;
+	}
+	a.e_pre = GR_HIP_EDGE_CHAIN;
+	a.oif = oif->id;
+	a.mtu = oif->mtu;
+	e = oif->type < 8 ? E.out6_iface[oif->type] : GR_HIP_EDGE_CHAIN; // :106
+	if (e != GR_HIP_EDGE_CHAIN)
+		a.e_mid = e;
+	else if (nh.state != GR_HIP_NH_S_REACHABLE) // :113-119
+		a.e_mid = GR_HIP_E_IP6_HOLD;
+	fill_post(c, nh, oif, a);
+	return a;
+}
+
 // Adjacency of nexthop `slot`: the ip_input view (ip_input.c:156-187) and
 // ip_output -> eth_output -> iface_output resolved for that nexthop
 // (ip_output.c:147-213, eth_output.c:297-316, iface_output.c:213-246),
@@ -227,29 +320,7 @@ static fwd4_adj make_adj(const gr_hip_ctx *c, uint32_t slot) {
 		a.e_mid = e;
 	else if (nh.state != GR_HIP_NH_S_REACHABLE)
 		a.e_mid = GR_HIP_E_IP_HOLD;
-	memcpy(a.dmac, nh.mac, 6);
-	a.post_iface = oif->id;
-	if (!oif->mac_ok) {
-		a.e_post = GR_HIP_E_ETH_OUTPUT_NO_MAC;
-		return a;
-	}
-	memcpy(a.smac, oif->mac, 6);
-	const gr_hip_iface *out = oif;
-	if (oif->type == GR_HIP_IFACE_TYPE_VLAN) {
-		out = iface_get(c, oif->parent_id);
-		if (out == nullptr) {
-			a.e_post = GR_HIP_E_IFACE_OUTPUT_VLAN_NO_PARENT;
-			return a;
-		}
-	}
-	if (!(oif->flags & GR_HIP_IFACE_F_UP)) {
-		a.e_post = GR_HIP_E_IFACE_OUTPUT_ADMIN_DOWN;
-		return a;
-	}
-	a.tx_if = oif->id;
-	a.tx_par = out != oif ? out->id : 0;
-	a.post_iface = out->id;
-	a.e_post = out->type < 8 ? E.iout_type[out->type] : GR_HIP_E_IFACE_OUTPUT_INVAL_TYPE;
+	fill_post(c, nh, oif, a);
 	return a;
 }
 
@@ -273,9 +344,13 @@ static fwd4_nhf make_nhf(const fwd4_adj &a) {
 // (n == 0: every slot up to nh_hi). Caller holds c->mu and has quiesced.
 static int upload_views(gr_hip_ctx *c, bool rx, uint32_t first, uint32_t n, bool adj) {
 	if (rx) {
-		for (uint32_t i = 0; i < c->max_ifaces; i++)
+		for (uint32_t i = 0; i < c->max_ifaces; i++) {
 			c->rx[i] = make_rx(c, i);
+			c->rx6[i] = make_rx6(c, i);
+		}
 		HCK(hipMemcpyAsync(c->d_rx, c->rx.data(), sizeof(fwd4_rx) * c->max_ifaces, hipMemcpyHostToDevice, c->ctl));
+		HCK(hipMemcpyAsync(c->d_rx6, c->rx6.data(), sizeof(fwd4_rx6) * c->max_ifaces, hipMemcpyHostToDevice,
+				   c->ctl));
 	}
 	if (adj) {
 		if (n == 0) {
@@ -285,8 +360,11 @@ static int upload_views(gr_hip_ctx *c, bool rx, uint32_t first, uint32_t n, bool
 		for (uint32_t i = first; i < first + n; i++) {
 			c->adj[i] = make_adj(c, i);
 			c->nhf[i] = make_nhf(c->adj[i]);
+			c->adj6[i] = make_adj6(c, i);
 		}
 		if (n) {
+			HCK(hipMemcpyAsync(c->d_adj6 + first, &c->adj6[first], sizeof(fwd4_adj6) * n, hipMemcpyHostToDevice,
+					   c->ctl));
 			HCK(hipMemcpyAsync(c->d_adj + first, &c->adj[first], sizeof(fwd4_adj) * n, hipMemcpyHostToDevice, c->ctl));
 			HCK(hipMemcpyAsync(c->d_nhf + first, &c->nhf[first], sizeof(fwd4_nhf) * n, hipMemcpyHostToDevice, c->ctl));
 		}
@@ -303,6 +381,8 @@ static int upload_tables(gr_hip_ctx *c) {
 	t.rx = c->d_rx;
 	t.adj = c->d_adj;
 	t.nhf = c->d_nhf;
+	t.rx6 = c->d_rx6;
+	t.adj6 = c->d_adj6;
 	t.reta = c->d_reta;
 	t.vlan_keys = c->d_vlan_keys;
 	t.vlan_vals = c->d_vlan_vals;
@@ -330,7 +410,7 @@ static void set_default_edges(fwd4_edges *E) {
 	} types[] = {
 		{0x0800, GR_HIP_EDGE_CHAIN},
 		{0x0806, GR_HIP_E_ARP_INPUT},
-		{0x86dd, GR_HIP_E_IP6_INPUT},
+		{0x86dd, GR_HIP_EDGE_CHAIN6},
 		{0x8809, GR_HIP_E_LACP_INPUT},
 	};
 	for (auto &t : types) {
@@ -348,6 +428,16 @@ static void set_default_edges(fwd4_edges *E) {
 		E->out_iface[i] = GR_HIP_EDGE_CHAIN;
 		E->iout_type[i] = GR_HIP_E_IFACE_OUTPUT_INVAL_TYPE;
 	}
+	for (int i = 0; i < 8; i++) {
+		E->in6_nh[i] = GR_HIP_EDGE_CHAIN;
+		E->out6_nh[i] = GR_HIP_EDGE_CHAIN;
+		E->out6_iface[i] = GR_HIP_EDGE_CHAIN;
+	}
+	E->in6_nh[GR_HIP_NH_T_BLACKHOLE] = GR_HIP_E_IP6_BLACKHOLE; // ip6_input.c:163-164
+	E->in6_nh[GR_HIP_NH_T_REJECT] = GR_HIP_E_IP6_ERROR_DEST_UNREACH;
+	E->in6_nh[GR_HIP_NH_T_SR6_LOCAL] = GR_HIP_E_SR6_LOCAL; // srv6_local.c:481
+	E->out6_nh[GR_HIP_NH_T_SR6_OUTPUT] = GR_HIP_E_SR6_OUTPUT; // srv6_output.c:153
+	E->out6_iface[GR_HIP_IFACE_TYPE_VRF] = GR_HIP_E_XVRF; // xvrf.c:64
 	E->in_nh[GR_HIP_NH_T_BLACKHOLE] = GR_HIP_E_IP_BLACKHOLE;
 	E->in_nh[GR_HIP_NH_T_REJECT] = GR_HIP_E_IP_ERROR_DEST_UNREACH;
 	E->in_nh[GR_HIP_NH_T_DNAT] = GR_HIP_E_DNAT44_STATIC;
@@ -402,6 +492,8 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->rx.assign(max_ifaces, fwd4_rx {});
 	c->adj.assign((size_t)max_nexthops + 1, fwd4_adj {});
 	c->nhf.assign((size_t)max_nexthops + 1, fwd4_nhf {});
+	c->rx6.assign(max_ifaces, fwd4_rx6 {});
+	c->adj6.assign((size_t)max_nexthops + 1, fwd4_adj6 {});
 	c->nh_hi = 0;
 	set_default_edges(&c->edges);
 	c->d_reta = nullptr;
@@ -416,6 +508,10 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 		goto fail;
 	if (hipMalloc(&c->d_nhf, sizeof(fwd4_nhf) * ((size_t)max_nexthops + 1)) != hipSuccess)
 		goto fail;
+	if (hipMalloc(&c->d_rx6, sizeof(fwd4_rx6) * max_ifaces) != hipSuccess)
+		goto fail;
+	if (hipMalloc(&c->d_adj6, sizeof(fwd4_adj6) * ((size_t)max_nexthops + 1)) != hipSuccess)
+		goto fail;
 	if (hipMalloc(&c->d_adj, sizeof(fwd4_adj) * ((size_t)max_nexthops + 1)) != hipSuccess)
 		goto fail;
 	if (hipMalloc(&c->d_tables, sizeof(fwd4_tables)) != hipSuccess)
@@ -424,7 +520,9 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	// runs on the null stream, which a non-blocking stream does not order with
 	if (hipMemsetAsync(c->d_rx, 0, sizeof(fwd4_rx) * max_ifaces, c->ctl) != hipSuccess
 	    || hipMemsetAsync(c->d_adj, 0, sizeof(fwd4_adj) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess
-	    || hipMemsetAsync(c->d_nhf, 0, sizeof(fwd4_nhf) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess)
+	    || hipMemsetAsync(c->d_nhf, 0, sizeof(fwd4_nhf) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess
+	    || hipMemsetAsync(c->d_rx6, 0, sizeof(fwd4_rx6) * max_ifaces, c->ctl) != hipSuccess
+	    || hipMemsetAsync(c->d_adj6, 0, sizeof(fwd4_adj6) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess)
 		goto fail;
 	c->nt = FWD4_V_NT; // measured faster on every kernel
 	c->stats_on = 1;
@@ -458,8 +556,12 @@ extern "C" int gr_hip_fini(gr_hip_ctx_t *c) {
 		hipFree(v.d8);
 		hipFree(v.d16);
 		hipFree(v.d8_16);
+		gr_fib6_free(v.rib6);
+		hipFree(v.d6);
 	}
 	hipFree(c->d_rx);
+	hipFree(c->d_rx6);
+	hipFree(c->d_adj6);
 	hipFree(c->d_adj);
 	hipFree(c->d_nhf);
 	hipFree(c->d_reta);
@@ -482,7 +584,7 @@ static bool edge_ok(uint8_t e) {
 }
 
 extern "C" int gr_hip_edges_eth_type(gr_hip_ctx_t *c, uint16_t be_type, uint8_t edge) {
-	if (c == nullptr || !edge_ok(edge))
+	if (c == nullptr || !(edge_ok(edge) || edge == GR_HIP_EDGE_CHAIN6))
 		return -EINVAL;
 	std::lock_guard<std::shared_mutex> l(c->mu);
 	fwd4_edges &E = c->edges;
@@ -521,6 +623,9 @@ EDGE_SETTER(gr_hip_edges_ip_input_nh_type, in_nh, 8)
 EDGE_SETTER(gr_hip_edges_ip_output_nh_type, out_nh, 8)
 EDGE_SETTER(gr_hip_edges_ip_output_iface_type, out_iface, 8)
 EDGE_SETTER(gr_hip_edges_iface_output_type, iout_type, 8)
+EDGE_SETTER(gr_hip_edges_ip6_input_nh_type, in6_nh, 8)
+EDGE_SETTER(gr_hip_edges_ip6_output_nh_type, out6_nh, 8)
+EDGE_SETTER(gr_hip_edges_ip6_output_iface_type, out6_iface, 8)
 
 // ---------------------------------------------------------------------------
 // mirrors
@@ -897,6 +1002,160 @@ extern "C" int gr_hip_fib4_info(gr_hip_ctx_t *c, uint16_t vrf, uint32_t *n_route
 	if (bytes) // device bytes a lookup can touch
 		*bytes = v.fmt16 ? 4ull * 65536 + 512ull * v.n_chunks + 512ull * v.num_tbl8
 				 : 4ull * GR_FIB4_TBL24_ENTRIES + 1024ull * v.num_tbl8;
+	return 0;
+}
+
+// ---------------------------------------------------------------------------
+// FIB6
+// ---------------------------------------------------------------------------
+
+// addr6_linklocal_scope (modules/ip6/control/ip6.h:23-36): a link-local
+// address is keyed with the iface id in bytes 2-3.
+static void scope6(uint8_t out[16], const uint8_t ip[16], uint16_t iface_id) {
+	memcpy(out, ip, 16);
+	if (ip[0] == 0xfe && (ip[1] & 0xc0) == 0x80) {
+		out[2] = (uint8_t)(iface_id >> 8);
+		out[3] = (uint8_t)iface_id;
+	}
+}
+
+extern "C" int gr_hip_fib6_create(gr_hip_ctx_t *c, uint16_t vrf, uint32_t max_routes, uint32_t num_tbl8) {
+	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces || max_routes == 0)
+		return -EINVAL;
+	std::lock_guard<std::shared_mutex> l(c->mu);
+	vrf_fib &v = c->vrfs[vrf];
+	if (v.rib6 != nullptr)
+		return -EEXIST;
+	v.rib6 = gr_fib6_new(max_routes, num_tbl8);
+	return v.rib6 ? 0 : -ENOMEM;
+}
+
+extern "C" int gr_hip_fib6_destroy(gr_hip_ctx_t *c, uint16_t vrf) {
+	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
+		return -EINVAL;
+	std::lock_guard<std::shared_mutex> l(c->mu);
+	hipSetDevice(c->dev);
+	vrf_fib &v = c->vrfs[vrf];
+	if (v.rib6 == nullptr)
+		return -ENOENT;
+	bool was = v.uploaded6;
+	v.uploaded6 = false; // make_rx6() stops pointing at it
+	int r = quiesce(c);
+	if (r == 0)
+		r = upload_views(c, true, 0, 0, false);
+	if (r != 0) {
+		v.uploaded6 = was;
+		return r;
+	}
+	hipFree(v.d6);
+	gr_fib6_free(v.rib6);
+	v.rib6 = nullptr;
+	v.d6 = nullptr;
+	v.d6_groups = 0;
+	v.gen6 = 0;
+	return 0;
+}
+
+extern "C" int gr_hip_route6_add(gr_hip_ctx_t *c, const struct gr_hip_route6 *rt, uint32_t n, int replace) {
+	if (c == nullptr || (rt == nullptr && n))
+		return -EINVAL;
+	std::lock_guard<std::shared_mutex> l(c->mu);
+	for (uint32_t i = 0; i < n; i++) {
+		if (rt[i].vrf_id == 0 || rt[i].vrf_id >= c->max_ifaces || rt[i].nh == 0 || rt[i].nh > c->max_nh
+		    || rt[i].prefixlen > 128)
+			return -EINVAL;
+		vrf_fib &v = c->vrfs[rt[i].vrf_id];
+		if (v.rib6 == nullptr)
+			return -ENONET;
+		uint8_t key[16];
+		scope6(key, rt[i].ip, rt[i].iface_id);
+		int r = gr_fib6_add(v.rib6, key, rt[i].prefixlen, rt[i].nh, replace);
+		if (r < 0)
+			return r;
+	}
+	return 0;
+}
+
+extern "C" int gr_hip_route6_del(gr_hip_ctx_t *c, uint16_t vrf, uint16_t iface_id, const uint8_t ip[16], uint8_t len) {
+	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces || ip == nullptr || len > 128)
+		return -EINVAL;
+	std::lock_guard<std::shared_mutex> l(c->mu);
+	vrf_fib &v = c->vrfs[vrf];
+	if (v.rib6 == nullptr)
+		return -ENONET;
+	uint8_t key[16];
+	scope6(key, ip, iface_id);
+	return gr_fib6_del(v.rib6, key, len);
+}
+
+// Stream-ordered publication of a repainted trie (fib6.h): quiesce the
+// queues, upload the first level and the groups in use, point the IPv6
+// views at the table on its first upload.
+extern "C" int gr_hip_fib6_commit(gr_hip_ctx_t *c, uint16_t vrf) {
+	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
+		return -EINVAL;
+	std::lock_guard<std::shared_mutex> l(c->mu);
+	hipSetDevice(c->dev);
+	vrf_fib &v = c->vrfs[vrf];
+	if (v.rib6 == nullptr)
+		return -ENONET;
+	int r = gr_fib6_build(v.rib6);
+	if (r < 0)
+		return r;
+	if (v.uploaded6 && v.gen6 == gr_fib6_generation(v.rib6))
+		return 0;
+	r = quiesce(c);
+	if (r != 0)
+		return r;
+	const uint32_t groups = gr_fib6_groups_used(v.rib6);
+	if (v.d6 == nullptr) { // sized for the VRF's group capacity once
+		const uint32_t cap = gr_fib6_max_groups(v.rib6);
+		HCK(hipMalloc(&v.d6, ((size_t)GR_FIB6_TOP + (size_t)cap * GR_FIB6_GROUP) * sizeof(uint32_t)));
+		v.d6_groups = cap;
+	}
+	r = h2d(c, v.d6, gr_fib6_top(v.rib6), (size_t)GR_FIB6_TOP * sizeof(uint32_t));
+	if (r == 0 && groups)
+		r = h2d(c, v.d6 + GR_FIB6_TOP, gr_fib6_groups(v.rib6), (size_t)groups * GR_FIB6_GROUP * sizeof(uint32_t));
+	if (r == 0)
+		r = ctl_sync(c);
+	if (r != 0)
+		return r;
+	v.gen6 = gr_fib6_generation(v.rib6);
+	if (!v.uploaded6) {
+		v.uploaded6 = true;
+		r = upload_views(c, true, 0, 0, false);
+	}
+	return r;
+}
+
+extern "C" int gr_hip_fib6_lookup_host(gr_hip_ctx_t *c, uint16_t vrf, uint16_t iface_id, const uint8_t ip[16],
+				       uint32_t *nh) {
+	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces || ip == nullptr || nh == nullptr)
+		return -EINVAL;
+	std::shared_lock<std::shared_mutex> l(c->mu);
+	vrf_fib &v = c->vrfs[vrf];
+	if (v.rib6 == nullptr)
+		return -ENONET;
+	uint8_t key[16];
+	scope6(key, ip, iface_id);
+	*nh = gr_fib6_lookup(v.rib6, key);
+	return 0;
+}
+
+extern "C" int gr_hip_fib6_info(gr_hip_ctx_t *c, uint16_t vrf, uint32_t *n_routes, uint32_t *groups_used,
+				uint64_t *bytes) {
+	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
+		return -EINVAL;
+	std::shared_lock<std::shared_mutex> l(c->mu);
+	vrf_fib &v = c->vrfs[vrf];
+	if (v.rib6 == nullptr)
+		return -ENONET;
+	if (n_routes)
+		*n_routes = gr_fib6_n_routes(v.rib6);
+	if (groups_used)
+		*groups_used = gr_fib6_groups_used(v.rib6);
+	if (bytes) // device bytes a lookup can touch
+		*bytes = 4ull * GR_FIB6_TOP + 1024ull * gr_fib6_groups_used(v.rib6);
 	return 0;
 }
 

@@ -10,11 +10,15 @@
 //   node              data_off      packet_type  vlan_id                frame bytes
 //   iface_input       +0            -            0 if VLAN-demuxed      -
 //   eth_input         +0 / +14 (1)  -            0 if demuxed           -
-//   ip_input          +14           -            0 if demuxed           -
-//   ip_forward        +14           -            0 if demuxed           -
-//   ip_output         +14           L3_IPV4      0 if demuxed           TTL, checksum
-//   eth_output        +0 (2)        L3_IPV4      0                      + dst MAC
-//   iface_output      +0 (2)        L3_IPV4      egress VLAN tag or 0   bytes 0-13, TTL, checksum
+//   ip(6)_input       +14           -            0 if demuxed           -
+//   ip(6)_forward     +14           -            0 if demuxed           -
+//   ip(6)_output      +14           L3_IPV4/6    0 if demuxed           TTL + checksum / hop limit
+//   eth_output        +0 (2)        L3_IPV4/6    0                      + dst MAC
+//   iface_output      +0 (2)        L3_IPV4/6    egress VLAN tag or 0   + bytes 6-13
+//
+// An IPv4 packet walks iface_input, eth_input, ip_input, ip_forward,
+// ip_output, eth_output, iface_output; an IPv6 packet the ip6_* nodes in the
+// middle (ip6_input.c, ip6_forward.c, ip6_output.c).
 //
 // (1) snap_input and eth_input_invalid_iface leave eth_input before its
 //     rte_pktmbuf_adj(14) (eth_input.c:49-59 vs :80); adj is a no-op on a
@@ -34,7 +38,7 @@
 static_assert(sizeof(struct gr_hip_mbuf) == 40 && offsetof(struct gr_hip_mbuf, nh) == 32, "gr_hip_mbuf layout");
 static_assert(sizeof(struct gr_hip_node_stats) == 16 * GR_HIP_NODE_COUNT, "gr_hip_node_stats layout");
 
-extern "C" int gr_hip_edge_node(uint8_t edge, uint32_t nh) {
+extern "C" int gr_hip_edge_node(uint8_t edge, uint32_t nh, int ip6) {
 	switch (edge) {
 	case GR_HIP_E_PUNT:
 		return -1;
@@ -69,11 +73,28 @@ extern "C" int gr_hip_edge_node(uint8_t edge, uint32_t nh) {
 	case GR_HIP_E_IP_OUTPUT_ERROR:
 	case GR_HIP_E_IP_FRAGMENT:
 	case GR_HIP_E_IP_ERROR_FRAG_NEEDED:
-	case GR_HIP_E_SR6_OUTPUT:
-	case GR_HIP_E_XVRF:
 	case GR_HIP_E_IPIP_OUTPUT:
 	case GR_HIP_E_IP_OUTPUT_SNAT:
 		return GR_HIP_NODE_IP_OUTPUT;
+	case GR_HIP_E_SR6_OUTPUT: // nh type edge of both ip_output and ip6_output
+	case GR_HIP_E_XVRF: // iface type edge of both
+		return ip6 ? GR_HIP_NODE_IP6_OUTPUT : GR_HIP_NODE_IP_OUTPUT;
+	case GR_HIP_E_IP6_INPUT_LOCAL:
+	case GR_HIP_E_IP6_ERROR_DEST_UNREACH:
+	case GR_HIP_E_IP6_INPUT_NOT_MEMBER:
+	case GR_HIP_E_IP6_INPUT_OTHER_HOST:
+	case GR_HIP_E_IP6_INPUT_BAD_VERSION:
+	case GR_HIP_E_IP6_INPUT_BAD_ADDR:
+	case GR_HIP_E_IP6_INPUT_BAD_LENGTH:
+	case GR_HIP_E_IP6_BLACKHOLE:
+	case GR_HIP_E_SR6_LOCAL:
+		return GR_HIP_NODE_IP6_INPUT;
+	case GR_HIP_E_IP6_ERROR_TTL_EXCEEDED:
+		return GR_HIP_NODE_IP6_FORWARD;
+	case GR_HIP_E_IP6_HOLD:
+	case GR_HIP_E_IP6_OUTPUT_ERROR:
+	case GR_HIP_E_IP6_OUTPUT_TOO_BIG:
+		return GR_HIP_NODE_IP6_OUTPUT;
 	case GR_HIP_E_ETH_OUTPUT_NO_MAC:
 		return GR_HIP_NODE_ETH_OUTPUT;
 	case GR_HIP_E_IFACE_OUTPUT_INVAL_TYPE:
@@ -128,41 +149,61 @@ extern "C" int gr_hip_node_apply(
 	if (burst == 0)
 		burst = 64;
 	const uint8_t *L = static_cast<const uint8_t *>(lines);
+	// the nodes an IPv4 / IPv6 packet walks, in order
+	static const int path4[] = {GR_HIP_NODE_IFACE_INPUT, GR_HIP_NODE_ETH_INPUT, GR_HIP_NODE_IP_INPUT,
+				    GR_HIP_NODE_IP_FORWARD, GR_HIP_NODE_IP_OUTPUT, GR_HIP_NODE_ETH_OUTPUT,
+				    GR_HIP_NODE_IFACE_OUTPUT};
+	static const int path6[] = {GR_HIP_NODE_IFACE_INPUT, GR_HIP_NODE_ETH_INPUT, GR_HIP_NODE_IP6_INPUT,
+				    GR_HIP_NODE_IP6_FORWARD, GR_HIP_NODE_IP6_OUTPUT, GR_HIP_NODE_ETH_OUTPUT,
+				    GR_HIP_NODE_IFACE_OUTPUT};
 	uint32_t reach[GR_HIP_NODE_COUNT] = {};
+	uint32_t sent4 = 0, sent6 = 0; // what ip_output / ip6_output enqueued to eth_output
 	for (uint32_t i = 0; i < n; i++) {
 		struct gr_hip_mbuf &b = m[i];
 		const struct gr_hip_verdict &v = verdicts[i];
-		const int node = gr_hip_edge_node(v.edge, v.nh);
+		const uint8_t *line = L + (size_t)i * line_stride;
+		const bool ip6 = line[12] == 0x86 && line[13] == 0xdd; // RTE_ETHER_TYPE_IPV6
+		const int node = gr_hip_edge_node(v.edge, v.nh, ip6);
 		if (node < -1)
 			return -EINVAL;
 		b.edge = v.edge;
 		if (node >= 0) {
-			for (int k = 0; k <= node; k++)
-				reach[k]++;
+			const int *path = ip6 ? path6 : path4;
+			int depth = 0; // position of `node` on the packet's path
+			while (depth < 7 && path[depth] != node)
+				depth++;
+			if (depth == 7)
+				return -EINVAL;
+			for (int k = 0; k <= depth; k++)
+				reach[path[k]]++;
+			if (depth >= 5)
+				(ip6 ? sent6 : sent4)++;
 			// VLAN demux in iface_input: the tag was consumed
 			const bool demuxed = b.vlan_id != 0 && v.edge != GR_HIP_E_IFACE_INPUT_UNKNOWN_VLAN && b.iface < n_ifaces
 				&& ifaces != nullptr && ifaces[b.iface].id == b.iface
 				&& ifaces[b.iface].mode == GR_HIP_IFACE_MODE_VRF;
-			const bool adj = node >= GR_HIP_NODE_IP_INPUT
-				|| (node == GR_HIP_NODE_ETH_INPUT && v.edge != GR_HIP_E_SNAP_INPUT
-				    && v.edge != GR_HIP_E_ETH_INPUT_INVALID_IFACE);
-			if (adj && node < GR_HIP_NODE_ETH_OUTPUT && b.data_len >= 14) { // rte_pktmbuf_adj(14)
+			// depth: 0 iface_input, 1 eth_input, 2 ip(6)_input, 3 ip(6)_forward,
+			// 4 ip(6)_output, 5 eth_output, 6 iface_output
+			const bool adj = depth >= 2
+				|| (depth == 1 && v.edge != GR_HIP_E_SNAP_INPUT && v.edge != GR_HIP_E_ETH_INPUT_INVALID_IFACE);
+			if (adj && depth < 5 && b.data_len >= 14) { // rte_pktmbuf_adj(14)
 				b.data_off += 14;
 				b.data_len -= 14;
 				b.pkt_len -= 14;
 			}
-			if (node >= GR_HIP_NODE_IP_OUTPUT) {
-				b.packet_type = GR_HIP_PTYPE_L3_IPV4;
-				// the chain rewrote nothing past byte 25 (TTL 22, checksum 24-25, L2 0-13)
-				uint32_t len = b.data_len + (node < GR_HIP_NODE_ETH_OUTPUT ? 14u : 0u);
+			if (depth >= 4) {
+				b.packet_type = ip6 ? GR_HIP_PTYPE_L3_IPV6 : GR_HIP_PTYPE_L3_IPV4;
+				// the chain rewrote nothing past byte 25 (L2 0-13, TTL 22 and
+				// checksum 24-25, or the hop limit 21)
+				uint32_t len = b.data_len + (depth < 5 ? 14u : 0u);
 				if (len > 26)
 					len = 26;
-				memcpy(b.frame, L + (size_t)i * line_stride, len);
+				memcpy(b.frame, line, len);
 			}
-			if (node <= GR_HIP_NODE_IP_OUTPUT) {
+			if (depth <= 4) {
 				if (demuxed)
 					b.vlan_id = 0;
-			} else if (node == GR_HIP_NODE_ETH_OUTPUT) {
+			} else if (depth == 5) {
 				b.vlan_id = 0;
 			} else {
 				uint16_t vid = 0;
@@ -180,12 +221,17 @@ extern "C" int gr_hip_node_apply(
 		}
 		if (stats != nullptr && ((i + 1) % burst == 0 || i + 1 == n)) {
 			for (int k = 0; k < GR_HIP_NODE_COUNT; k++) {
-				// ip_output returns only what it sent to eth_output
-				const uint32_t ret = k == GR_HIP_NODE_IP_OUTPUT ? reach[GR_HIP_NODE_ETH_OUTPUT] : reach[k];
+				// ip_output / ip6_output return only what they sent to eth_output
+				uint32_t ret = reach[k];
+				if (k == GR_HIP_NODE_IP_OUTPUT)
+					ret = sent4;
+				else if (k == GR_HIP_NODE_IP6_OUTPUT)
+					ret = sent6;
 				stats->packets[k] += ret;
 				stats->calls[k] += reach[k] != 0;
 				reach[k] = 0;
 			}
+			sent4 = sent6 = 0;
 		}
 	}
 	return 0;

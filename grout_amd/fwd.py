@@ -72,6 +72,36 @@ class FastPath:
     def fib_commit(self, vrf_id):
         check("gr_hip_fib4_commit", self.lib.gr_hip_fib4_commit(self.h, vrf_id))
 
+    def fib6_create(self, vrf_id, max_routes=1 << 16, num_groups=0):
+        check("gr_hip_fib6_create", self.lib.gr_hip_fib6_create(self.h, vrf_id, max_routes, num_groups))
+
+    def fib6_destroy(self, vrf_id):
+        check("gr_hip_fib6_destroy", self.lib.gr_hip_fib6_destroy(self.h, vrf_id))
+
+    def route6_add(self, routes, replace=False):
+        a = np.ascontiguousarray(routes, dtype=abi.ROUTE6_DT)
+        check("gr_hip_route6_add", self.lib.gr_hip_route6_add(self.h, ptr(a), len(a), 1 if replace else 0))
+
+    def route6_del(self, vrf_id, ip16, prefixlen, iface_id=0):
+        a = np.frombuffer(bytes(ip16), np.uint8).copy()
+        check("gr_hip_route6_del", self.lib.gr_hip_route6_del(self.h, vrf_id, iface_id, ptr(a), prefixlen))
+
+    def fib6_commit(self, vrf_id):
+        check("gr_hip_fib6_commit", self.lib.gr_hip_fib6_commit(self.h, vrf_id))
+
+    def fib6_lookup(self, vrf_id, ip16, iface_id=0):
+        out = ctypes.c_uint32()
+        a = np.frombuffer(bytes(ip16), np.uint8).copy()
+        check("gr_hip_fib6_lookup_host", self.lib.gr_hip_fib6_lookup_host(self.h, vrf_id, iface_id, ptr(a),
+                                                                          ctypes.byref(out)))
+        return out.value
+
+    def fib6_info(self, vrf_id):
+        n, u, b = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint64()
+        check("gr_hip_fib6_info", self.lib.gr_hip_fib6_info(self.h, vrf_id, ctypes.byref(n), ctypes.byref(u),
+                                                            ctypes.byref(b)))
+        return dict(routes=n.value, groups_used=u.value, dev_bytes=b.value)
+
     def fib_lookup(self, vrf_id, ip_host):
         out = ctypes.c_uint32()
         be = int.from_bytes(ip_host.to_bytes(4, "big"), "little")
@@ -99,6 +129,13 @@ class FastPath:
             self.route_add(routes)
         for vrf_id in topo.fibs:
             self.fib_commit(vrf_id)
+        routes6 = topo.route6_array()
+        for vrf_id, (max_routes, num_groups) in topo.fibs6.items():
+            self.fib6_create(vrf_id, max_routes, num_groups)
+        if len(routes6):
+            self.route6_add(routes6)
+        for vrf_id in topo.fibs6:
+            self.fib6_commit(vrf_id)
 
     def queue(self, stream=None):
         q = Queue(self, stream)

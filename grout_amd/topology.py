@@ -14,6 +14,10 @@ routes exactly as grout's control plane would leave them for the datapath:
   (l3_nexthop.c:232-236).
 * add_group: GR_NH_T_GROUP with a power-of-two reta (nexthop.h:80-96).
 * add_route: gr_ip4_route_add_req (modules/ip/api/gr_ip4.h:47-56).
+* IPv6: every VRF also gets a FIB6 (route.c:100-122 of modules/ip6); an
+  IPv6 nexthop address makes an AF_IP6 nexthop; add_address6 mirrors
+  addr6_add (modules/ip6/control/address.c) and add_route6
+  gr_ip6_route_add_req, a link-local prefix scoped to its iface.
 
 The same arrays feed the HIP library (grout_amd.fwd) and the test oracle.
 """
@@ -27,6 +31,11 @@ from . import abi
 def ip4(s):
     """'a.b.c.d' -> host-order int."""
     return int(ipaddress.IPv4Address(s))
+
+
+def ip6(s):
+    """IPv6 text -> 16 bytes (network order)."""
+    return ipaddress.IPv6Address(s).packed
 
 
 def mac_bytes(m):
@@ -45,6 +54,8 @@ class Topology:
         self.reta = np.zeros(0, dtype=np.uint32)
         self.routes = []  # list of ROUTE_DT arrays
         self.fibs = {}  # vrf_id -> (max_routes, num_tbl8)
+        self.routes6 = []  # list of ROUTE6_DT arrays
+        self.fibs6 = {}  # vrf_id -> (max_routes, num_groups)
 
     # -- interfaces ---------------------------------------------------------
     def _iface(self, iface_id, itype, mode, flags, mtu, vrf_id, mac, **kw):
@@ -67,10 +78,11 @@ class Topology:
             r[k] = v
         return iface_id
 
-    def add_vrf(self, vrf_id=1, mac=None, max_routes=1 << 16, num_tbl8=0):
-        """A VRF iface and its IPv4 FIB (vrf.c, route.c:100-122)."""
+    def add_vrf(self, vrf_id=1, mac=None, max_routes=1 << 16, num_tbl8=0, max_routes6=1 << 16, num_groups6=0):
+        """A VRF iface and its IPv4 and IPv6 FIBs (vrf.c, route.c:100-122)."""
         self._iface(vrf_id, "VRF", "VRF", abi.IFACE_F_UP, 1500, vrf_id, mac)
         self.fibs[vrf_id] = (max_routes, num_tbl8)
+        self.fibs6[vrf_id] = (max_routes6, num_groups6)
         return vrf_id
 
     def add_port(self, iface_id, port_id, mac, vrf_id=1, mtu=1500, up=True, mode="VRF", flags=0):
@@ -113,6 +125,9 @@ class Topology:
             if ipv4 is None:
                 r["af"] = abi.AF_UNSPEC
                 flags |= abi.NH_F_LINK
+            elif isinstance(ipv4, str) and ":" in ipv4:  # an IPv6 nexthop
+                r["af"] = abi.AF_IP6
+                r["ipv6"] = np.frombuffer(ip6(ipv4), np.uint8)
             else:
                 r["af"] = abi.AF_IP4
                 r["ipv4"] = ip4(ipv4) if isinstance(ipv4, str) else ipv4
@@ -131,6 +146,16 @@ class Topology:
                                 flags=abi.NH_F_LOCAL | abi.NH_F_LINK,
                                 state=abi.NH_S["REACHABLE"])
         self.add_route(self.ifaces[iface_id]["vrf_id"], f"{net.ip}/{net.network.prefixlen}", slot)
+        return slot
+
+    def add_address6(self, iface_id, cidr):
+        """addr6_add: LOCAL|LINK nexthop + route on the address prefix."""
+        net = ipaddress.IPv6Interface(cidr)
+        slot = self.add_nexthop(iface_id, str(net.ip), self.iface_mac(iface_id),
+                                flags=abi.NH_F_LOCAL | abi.NH_F_LINK,
+                                state=abi.NH_S["REACHABLE"])
+        self.add_route6(self.ifaces[iface_id]["vrf_id"], f"{net.ip}/{net.network.prefixlen}", slot,
+                        iface_id=iface_id)
         return slot
 
     def add_group(self, members, reta_size=None, slot=None):
@@ -171,6 +196,24 @@ class Topology:
             return np.zeros(0, dtype=abi.ROUTE_DT)
         # np.concatenate normalises byte order: convert back to the C layout
         return np.concatenate(self.routes).astype(abi.ROUTE_DT)
+
+    def add_route6(self, vrf_id, cidr, nh_slot, iface_id=0):
+        net = ipaddress.IPv6Network(cidr, strict=False)
+        a = np.zeros(1, dtype=abi.ROUTE6_DT)
+        a["ip"] = np.frombuffer(net.network_address.packed, np.uint8)
+        a["prefixlen"] = net.prefixlen
+        a["vrf_id"] = vrf_id
+        a["iface_id"] = iface_id
+        a["nh"] = nh_slot
+        self.routes6.append(a)
+
+    def add_routes6(self, arr):
+        self.routes6.append(np.ascontiguousarray(arr, dtype=abi.ROUTE6_DT))
+
+    def route6_array(self):
+        if not self.routes6:
+            return np.zeros(0, dtype=abi.ROUTE6_DT)
+        return np.concatenate(self.routes6).astype(abi.ROUTE6_DT)
 
     def live_ifaces(self):
         return self.ifaces[self.ifaces["id"] != 0]
@@ -228,4 +271,60 @@ def config_fullview(count=1_000_000):
     t.add_routes(routes)
     t.add_address(PORT_IFACE[0], "172.16.0.1/24")
     del ctypes
+    return t
+
+
+# IPv6 view: the prefix-length mix of a global IPv6 table (most routes /48,
+# then /32, /44, /40, /36, /29 ...) drawn deterministically, over 512
+# REACHABLE IPv6 nexthops. No reference script generates one (fib_inject
+# is IPv4 only), so this is a synthetic stand-in with the
+# same LPM structure (nested prefixes, every trie level populated).
+N_FULLVIEW6_NH = 512
+SEED_FULLVIEW6 = 0x67720006
+V6_LEN_MIX = [(48, 0.46), (32, 0.12), (44, 0.10), (40, 0.07), (36, 0.05), (29, 0.04), (47, 0.03),
+              (46, 0.03), (45, 0.02), (56, 0.02), (64, 0.02), (24, 0.01), (28, 0.01), (128, 0.01),
+              (20, 0.004), (60, 0.006)]
+
+
+def fullview6_nexthops(t, n_nh=N_FULLVIEW6_NH):
+    """nh j -> {p(1+(j-1)%3), 2001:db8:ffff::j, 02:00:00:06:(j>>8):(j&255)}."""
+    first = t.n_nh + 1
+    for j in range(1, n_nh + 1):
+        port = 1 + (j - 1) % 3
+        t.add_nexthop(PORT_IFACE[port], f"2001:db8:ffff::{j:x}", "02:00:00:06:%02x:%02x" % (j >> 8, j & 255),
+                      slot=first + j - 1)
+    return first
+
+
+def fullview6_routes(count, vrf_id, first_nh, n_nh, seed=SEED_FULLVIEW6):
+    """`count` distinct prefixes in 2000::/3 with the V6_LEN_MIX lengths,
+    route i -> nexthop first_nh + i % n_nh."""
+    rng = np.random.default_rng(seed)
+    lens = np.array([l for l, _ in V6_LEN_MIX])
+    p = np.array([w for _, w in V6_LEN_MIX])
+    want = rng.choice(lens, size=count * 2, p=p / p.sum())
+    addr = rng.integers(0, 256, size=(count * 2, 16), dtype=np.uint8)
+    addr[:, 0] = 0x20 | (addr[:, 0] & 0x1F)  # 2000::/3
+    addr[:, 1] = addr[:, 1] & 0x0F  # a denser top level, like the real table
+    bits = np.arange(16)[None, :] * 8
+    mask = (0xFF00 >> np.clip(want[:, None] - bits, 0, 8)).astype(np.uint8)
+    addr &= mask
+    _, idx = np.unique(np.concatenate([addr, want[:, None].astype(np.uint8)], axis=1), axis=0,
+                       return_index=True)
+    idx = np.sort(idx)[:count]
+    r = np.zeros(len(idx), dtype=abi.ROUTE6_DT)
+    r["ip"] = addr[idx]
+    r["prefixlen"] = want[idx]
+    r["vrf_id"] = vrf_id
+    r["nh"] = first_nh + np.arange(len(idx)) % n_nh
+    return r
+
+
+def config_fullview6(count=100_000):
+    """An IPv6 view of `count` routes over 512 nexthops (the IPv6 workload)."""
+    t = base_ports(max_routes=1 << 10)
+    t.fibs6[VRF_MAIN] = (count + 10, max(1 << 16, 4 * count))  # ~3-4 trie groups per deep route
+    first = fullview6_nexthops(t)
+    t.add_routes6(fullview6_routes(count, VRF_MAIN, first, N_FULLVIEW6_NH))
+    t.add_address6(PORT_IFACE[0], "2001:db8::1/64")
     return t

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define GR_HIP_ABI_VERSION 1
+#define GR_HIP_ABI_VERSION 2
 
 // ---------------------------------------------------------------------------
 // Values mirrored from grout's public API (identical numbering).
@@ -176,12 +176,31 @@ enum gr_hip_edge {
 	GR_HIP_E_BOND_OUTPUT, // "bond_output"
 	GR_HIP_E_VXLAN_OUTPUT, // "vxlan_output"
 	GR_HIP_E_PORT_OUTPUT, // "port_output": the forwarded case
+	// ip6_input (ip6_input.c:19-29, nh type edges :33-41,163-164)
+	GR_HIP_E_IP6_INPUT_LOCAL, // "ip6_input_local"
+	GR_HIP_E_IP6_ERROR_DEST_UNREACH, // "ip6_error_dest_unreach"
+	GR_HIP_E_IP6_INPUT_NOT_MEMBER, // "ip6_input_not_member" (drop)
+	GR_HIP_E_IP6_INPUT_OTHER_HOST, // "ip6_input_other_host" (drop)
+	GR_HIP_E_IP6_INPUT_BAD_VERSION, // "ip6_input_bad_version" (drop)
+	GR_HIP_E_IP6_INPUT_BAD_ADDR, // "ip6_input_bad_addr" (drop)
+	GR_HIP_E_IP6_INPUT_BAD_LENGTH, // "ip6_input_bad_length" (drop)
+	GR_HIP_E_IP6_BLACKHOLE, // "ip6_blackhole" (drop)
+	GR_HIP_E_SR6_LOCAL, // "sr6_local" (srv6_local.c:481)
+	// ip6_forward (ip6_forward.c:7-11)
+	GR_HIP_E_IP6_ERROR_TTL_EXCEEDED, // "ip6_error_ttl_exceeded"
+	// ip6_output (ip6_output.c:19-26, type edges :28-50)
+	GR_HIP_E_IP6_HOLD, // "ip6_hold"
+	GR_HIP_E_IP6_OUTPUT_ERROR, // "ip6_output_error" (drop)
+	GR_HIP_E_IP6_OUTPUT_TOO_BIG, // "ip6_output_too_big" (drop)
 	GR_HIP_E_COUNT,
 };
 // Registration value meaning "the next node of the chain" (eth_input for an
 // iface mode, ip_input for an ether type, ip_forward for an ip_input nexthop
 // type, eth_output for an ip_output type): never appears in a verdict.
 #define GR_HIP_EDGE_CHAIN 0xff
+// eth_input type edge value: continue into ip6_input on the GPU (the default
+// for RTE_ETHER_TYPE_IPV6; GR_HIP_E_IP6_INPUT hands IPv6 to grout's CPU nodes)
+#define GR_HIP_EDGE_CHAIN6 0xfe
 
 // ---------------------------------------------------------------------------
 // Control-plane mirrors (host -> device).
@@ -223,6 +242,7 @@ struct gr_hip_nh {
 	uint32_t single; // GROUP: nhg->nh shortcut used when n_members == 1
 	uint16_t n_members; // GROUP
 	uint16_t _pad0;
+	uint8_t ipv6[16]; // L3, af GR_HIP_AF_IP6 (nexthop.h:49, gr_nexthop.h:100)
 };
 
 // One IPv4 route, as gr_ip4_route_add_req (modules/ip/api/gr_ip4.h:47-56).
@@ -231,6 +251,19 @@ struct gr_hip_route4 {
 	uint8_t prefixlen; // 0..32
 	uint8_t _pad0;
 	uint16_t vrf_id;
+	uint32_t nh; // nexthop slot (1..)
+};
+
+// One IPv6 route, as gr_ip6_route_add_req (modules/ip6/api/gr_ip6.h). A
+// link-local prefix (fe80::/10) is scoped to iface_id like
+// addr6_linklocal_scope (modules/ip6/control/ip6.h:23-36).
+struct gr_hip_route6 {
+	uint8_t ip[16]; // host bits are ignored (masked)
+	uint8_t prefixlen; // 0..128
+	uint8_t _pad0;
+	uint16_t vrf_id;
+	uint16_t iface_id; // scope of link-local prefixes, else ignored
+	uint16_t _pad1;
 	uint32_t nh; // nexthop slot (1..)
 };
 
@@ -308,6 +341,9 @@ int gr_hip_edges_ip_input_nh_type(gr_hip_ctx_t *, uint8_t nh_type, uint8_t edge)
 int gr_hip_edges_ip_output_nh_type(gr_hip_ctx_t *, uint8_t nh_type, uint8_t edge);
 int gr_hip_edges_ip_output_iface_type(gr_hip_ctx_t *, uint8_t iface_type, uint8_t edge);
 int gr_hip_edges_iface_output_type(gr_hip_ctx_t *, uint8_t iface_type, uint8_t edge);
+int gr_hip_edges_ip6_input_nh_type(gr_hip_ctx_t *, uint8_t nh_type, uint8_t edge); // ip6_input.c:33
+int gr_hip_edges_ip6_output_nh_type(gr_hip_ctx_t *, uint8_t nh_type, uint8_t edge); // ip6_output.c:40
+int gr_hip_edges_ip6_output_iface_type(gr_hip_ctx_t *, uint8_t iface_type, uint8_t edge); // ip6_output.c:29
 
 // Object mirrors. Changes become visible to submits issued after the call.
 int gr_hip_iface_set(gr_hip_ctx_t *, const struct gr_hip_iface *ifaces, uint32_t n);
@@ -327,6 +363,21 @@ int gr_hip_fib4_commit(gr_hip_ctx_t *, uint16_t vrf_id);
 int gr_hip_fib4_lookup_host(gr_hip_ctx_t *, uint16_t vrf_id, uint32_t ip_be, uint32_t *nh);
 // Device table geometry: tbl8 groups in use, bytes of device memory.
 int gr_hip_fib4_info(gr_hip_ctx_t *, uint16_t vrf_id, uint32_t *n_routes, uint32_t *tbl8_used, uint64_t *dev_bytes);
+
+// IPv6 FIB per VRF (create_fib6 / rib6_insert_or_replace / rib6_delete,
+// modules/ip6/control/route.c:66-98,230-345). A multibit trie: a 2^16-entry
+// first level indexed by the first two address bytes, then 256-entry groups
+// per further byte (num_tbl8 of them; 0 = 1 << 16). fib6_lookup
+// (route.c:151-173) walks it; link-local destinations are scoped to the
+// ingress iface first.
+int gr_hip_fib6_create(gr_hip_ctx_t *, uint16_t vrf_id, uint32_t max_routes, uint32_t num_tbl8);
+int gr_hip_fib6_destroy(gr_hip_ctx_t *, uint16_t vrf_id);
+int gr_hip_route6_add(gr_hip_ctx_t *, const struct gr_hip_route6 *routes, uint32_t n, int replace);
+int gr_hip_route6_del(gr_hip_ctx_t *, uint16_t vrf_id, uint16_t iface_id, const uint8_t ip[16], uint8_t prefixlen);
+int gr_hip_fib6_commit(gr_hip_ctx_t *, uint16_t vrf_id);
+// Host lookup in the committed tables (tests / control plane), scoped like fib6_lookup.
+int gr_hip_fib6_lookup_host(gr_hip_ctx_t *, uint16_t vrf_id, uint16_t iface_id, const uint8_t ip[16], uint32_t *nh);
+int gr_hip_fib6_info(gr_hip_ctx_t *, uint16_t vrf_id, uint32_t *n_routes, uint32_t *groups_used, uint64_t *dev_bytes);
 
 // Queues: one per RX queue / worker; each owns a HIP stream. stream == NULL
 // creates a private non-blocking stream, else the given hipStream_t is used.
@@ -396,7 +447,7 @@ struct gr_hip_mbuf {
 	uint32_t pkt_len; // in/out
 	uint16_t data_len; // in/out
 	uint16_t data_off; // in/out
-	uint32_t packet_type; // in/out: RTE_PTYPE_L3_IPV4 (0x1) set by ip_output
+	uint32_t packet_type; // in/out: RTE_PTYPE_L3_IPV4 / _IPV6 set by ip_output / ip6_output
 	uint32_t rss; // in: m->hash.rss
 	uint16_t iface; // in/out: iface_mbuf_data.iface (by id)
 	uint16_t vlan_id; // in/out: iface_mbuf_data.vlan_id
@@ -408,6 +459,7 @@ struct gr_hip_mbuf {
 };
 
 #define GR_HIP_PTYPE_L3_IPV4 0x1 // RTE_PTYPE_L3_IPV4
+#define GR_HIP_PTYPE_L3_IPV6 0x10 // RTE_PTYPE_L3_IPV6
 
 // The nodes the fast path replaces, for per-node statistics.
 enum gr_hip_node {
@@ -418,22 +470,26 @@ enum gr_hip_node {
 	GR_HIP_NODE_IP_OUTPUT,
 	GR_HIP_NODE_ETH_OUTPUT,
 	GR_HIP_NODE_IFACE_OUTPUT,
+	GR_HIP_NODE_IP6_INPUT,
+	GR_HIP_NODE_IP6_FORWARD,
+	GR_HIP_NODE_IP6_OUTPUT,
 	GR_HIP_NODE_COUNT,
 };
 
 // rte_graph node counters as grout collects them (main_loop.c:39-64):
 // packets = sum of process() return values, calls = process() invocations,
 // one per node per graph walk that reaches it. Every node returns nb_objs
-// except ip_output, which returns only what it sent to eth_output
-// (ip_output.c:153,162).
+// except ip_output and ip6_output, which return only what they sent to
+// eth_output (ip_output.c:153,162, ip6_output.c:146).
 struct gr_hip_node_stats {
 	uint64_t packets[GR_HIP_NODE_COUNT];
 	uint64_t calls[GR_HIP_NODE_COUNT];
 };
 
 // The last node of the fast path a packet with this verdict went through
-// (-1 for GR_HIP_E_PUNT, which grout's CPU iface_input takes instead).
-int gr_hip_edge_node(uint8_t edge, uint32_t nh);
+// (-1 for GR_HIP_E_PUNT, which grout's CPU iface_input takes instead); ip6:
+// the packet is IPv6 (the eth_output / iface_output edges are shared).
+int gr_hip_edge_node(uint8_t edge, uint32_t nh, int ip6);
 
 // Stage n mbufs: the first 64 bytes at each frame (read whatever data_len
 // says, as grout's nodes do: an mbuf's data room always has them) into

@@ -36,6 +36,14 @@ API = {
     "or_lpm_hash": (_U32, [_P, _U16, _U32]),
     "or_lpm_dir24": (_U32, [_P, _U16, _U32]),
     "or_lpm_brute": (_U32, [_P, _U16, _U32]),
+    "or_edge_ip6_input_nh_type": (_I, [_P, _U8, _U8]),
+    "or_edge_ip6_output_nh_type": (_I, [_P, _U8, _U8]),
+    "or_edge_ip6_output_iface_type": (_I, [_P, _U8, _U8]),
+    "or_fib6_create": (_I, [_P, _U16]),
+    "or_route6_add": (_I, [_P, _P, _U32, _I]),
+    "or_route6_del": (_I, [_P, _U16, _U16, _P, _U8]),
+    "or_lpm6": (_U32, [_P, _U16, _U16, _P]),
+    "or_lpm6_brute": (_U32, [_P, _U16, _U16, _P]),
     "or_process": (_I, [_P, _P, _U32, _P, _U32, _P, _U32, _P, _P, _U32]),
     "or_process_ex": (_I, [_P, _P, _U32, _P, _U32, _P, _U32, _P, _P, _U32, _P, _P]),
     "or_bench": (ctypes.c_double, [_P, _P, _U32, _P, _U32, _I, _U64, ctypes.POINTER(_U64)]),
@@ -87,6 +95,11 @@ class Oracle:
         routes = topo.route_array()
         if len(routes):
             _ck("or_route_add", L.or_route_add(self.h, routes.ctypes.data, len(routes), 0))
+        for vrf_id in getattr(topo, "fibs6", {}):
+            _ck("or_fib6_create", L.or_fib6_create(self.h, vrf_id))
+        routes6 = topo.route6_array() if hasattr(topo, "route6_array") else []
+        if len(routes6):
+            _ck("or_route6_add", L.or_route6_add(self.h, routes6.ctypes.data, len(routes6), 0))
         if build_dir24:
             for vrf_id in topo.fibs:
                 _ck("or_fib_build", L.or_fib_build(self.h, vrf_id))
@@ -107,11 +120,19 @@ class Oracle:
               "ip_input_nh_type": "or_edge_ip_input_nh_type",
               "ip_output_nh_type": "or_edge_ip_output_nh_type",
               "ip_output_iface_type": "or_edge_ip_output_iface_type",
-              "iface_output_type": "or_edge_iface_output_type"}[kind]
+              "iface_output_type": "or_edge_iface_output_type",
+              "ip6_input_nh_type": "or_edge_ip6_input_nh_type",
+              "ip6_output_nh_type": "or_edge_ip6_output_nh_type",
+              "ip6_output_iface_type": "or_edge_ip6_output_iface_type"}[kind]
         _ck(fn, getattr(self.L, fn)(self.h, key, edge))
 
     def lpm(self, vrf_id, ip_host, how="hash"):
         return getattr(self.L, "or_lpm_" + how)(self.h, vrf_id, ip_host)
+
+    def lpm6(self, vrf_id, ip16, iface_id=0, brute=False):
+        a = np.frombuffer(bytes(ip16), np.uint8).copy()
+        fn = self.L.or_lpm6_brute if brute else self.L.or_lpm6
+        return fn(self.h, vrf_id, iface_id, a.ctypes.data)
 
     def process(self, frames, meta, lines_only=False, stats=None):
         """-> (out_lines n x 64, verdicts)."""

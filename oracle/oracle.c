@@ -21,6 +21,7 @@
 #define OR_HEADROOM 128 // RTE_PKTMBUF_HEADROOM
 #define OR_DATAROOM 2048 // align32pow2(128+14+4+1800), mempool.c:66-68
 #define NEXT GR_HIP_EDGE_CHAIN
+#define NEXT6 GR_HIP_EDGE_CHAIN6 // eth_input: continue into ip6_input
 
 // ---------------------------------------------------------------------------
 // Topology (control-plane objects the nodes dereference)
@@ -44,6 +45,18 @@ struct or_fib {
 	bool built;
 };
 
+struct or_ht6 { // open addressing, key = masked 128-bit prefix
+	uint8_t (*keys)[16];
+	uint32_t *vals; // nh slot, 0 = empty
+	uint32_t cap;
+	uint32_t count;
+};
+
+struct or_fib6 { // RIB6: one exact-match table per prefix length
+	bool exists;
+	struct or_ht6 len[129];
+};
+
 struct or_topo {
 	uint32_t max_ifaces;
 	uint32_t max_nh;
@@ -52,12 +65,16 @@ struct or_topo {
 	uint32_t *reta;
 	uint32_t reta_cap;
 	struct or_fib *fibs; // indexed by vrf_id (an iface id)
+	struct or_fib6 *fibs6;
 	uint8_t eth_edges[65536]; // l2l3_edges indexed by BE ether type, eth_input.c:24
 	uint8_t mode_edges[GR_HIP_IFACE_MODE_COUNT]; // iface_input.c:20
 	uint8_t in_nh_edges[256]; // ip_input.c:34
 	uint8_t out_nh_edges[256]; // ip_output.c:104
 	uint8_t out_iface_edges[256]; // ip_output.c:92
 	uint8_t iout_type_edges[256]; // iface_output.c:161
+	uint8_t in6_nh_edges[256]; // ip6_input.c:31
+	uint8_t out6_nh_edges[256]; // ip6_output.c:38
+	uint8_t out6_iface_edges[256]; // ip6_output.c:27
 };
 
 static uint16_t be16(uint16_t host) {
@@ -73,7 +90,7 @@ static void or_default_edges(or_topo_t *t) {
 	memset(t->eth_edges, GR_HIP_E_ETH_INPUT_UNKNOWN_TYPE, sizeof(t->eth_edges));
 	t->eth_edges[be16(0x0800)] = NEXT;
 	t->eth_edges[be16(0x0806)] = GR_HIP_E_ARP_INPUT;
-	t->eth_edges[be16(0x86dd)] = GR_HIP_E_IP6_INPUT;
+	t->eth_edges[be16(0x86dd)] = NEXT6; // ip6_input.c:161
 	t->eth_edges[be16(0x8809)] = GR_HIP_E_LACP_INPUT;
 	for (int i = 0; i < GR_HIP_IFACE_MODE_COUNT; i++)
 		t->mode_edges[i] = GR_HIP_E_IFACE_MODE_UNKNOWN;
@@ -95,6 +112,14 @@ static void or_default_edges(or_topo_t *t) {
 	t->iout_type_edges[GR_HIP_IFACE_TYPE_BOND] = GR_HIP_E_BOND_OUTPUT;
 	t->iout_type_edges[GR_HIP_IFACE_TYPE_VXLAN] = GR_HIP_E_VXLAN_OUTPUT;
 	t->iout_type_edges[GR_HIP_IFACE_TYPE_BRIDGE] = GR_HIP_E_BRIDGE_INPUT;
+	memset(t->in6_nh_edges, NEXT, sizeof(t->in6_nh_edges));
+	t->in6_nh_edges[GR_HIP_NH_T_BLACKHOLE] = GR_HIP_E_IP6_BLACKHOLE; // ip6_input.c:163
+	t->in6_nh_edges[GR_HIP_NH_T_REJECT] = GR_HIP_E_IP6_ERROR_DEST_UNREACH; // :164
+	t->in6_nh_edges[GR_HIP_NH_T_SR6_LOCAL] = GR_HIP_E_SR6_LOCAL; // srv6_local.c:481
+	memset(t->out6_nh_edges, NEXT, sizeof(t->out6_nh_edges));
+	t->out6_nh_edges[GR_HIP_NH_T_SR6_OUTPUT] = GR_HIP_E_SR6_OUTPUT; // srv6_output.c:153
+	memset(t->out6_iface_edges, NEXT, sizeof(t->out6_iface_edges));
+	t->out6_iface_edges[GR_HIP_IFACE_TYPE_VRF] = GR_HIP_E_XVRF; // xvrf.c:64
 }
 
 or_topo_t *or_topo_new(uint32_t max_ifaces, uint32_t max_nexthops) {
@@ -109,7 +134,8 @@ or_topo_t *or_topo_new(uint32_t max_ifaces, uint32_t max_nexthops) {
 	t->ifaces = calloc(max_ifaces, sizeof(*t->ifaces));
 	t->nh = calloc((size_t)max_nexthops + 1, sizeof(*t->nh));
 	t->fibs = calloc(max_ifaces, sizeof(*t->fibs));
-	if (!t->ifaces || !t->nh || !t->fibs) {
+	t->fibs6 = calloc(max_ifaces, sizeof(*t->fibs6));
+	if (!t->ifaces || !t->nh || !t->fibs || !t->fibs6) {
 		or_topo_free(t);
 		return NULL;
 	}
@@ -143,6 +169,15 @@ void or_topo_free(or_topo_t *t) {
 		}
 	}
 	free(t->fibs);
+	if (t->fibs6) {
+		for (uint32_t v = 0; v < t->max_ifaces; v++) {
+			for (int l = 0; l <= 128; l++) {
+				free(t->fibs6[v].len[l].keys);
+				free(t->fibs6[v].len[l].vals);
+			}
+		}
+	}
+	free(t->fibs6);
 	free(t->ifaces);
 	free(t->nh);
 	free(t->reta);
@@ -161,6 +196,9 @@ EDGE_SETTER(or_edge_ip_input_nh_type, in_nh_edges, 256)
 EDGE_SETTER(or_edge_ip_output_nh_type, out_nh_edges, 256)
 EDGE_SETTER(or_edge_ip_output_iface_type, out_iface_edges, 256)
 EDGE_SETTER(or_edge_iface_output_type, iout_type_edges, 256)
+EDGE_SETTER(or_edge_ip6_input_nh_type, in6_nh_edges, 256)
+EDGE_SETTER(or_edge_ip6_output_nh_type, out6_nh_edges, 256)
+EDGE_SETTER(or_edge_ip6_output_iface_type, out6_iface_edges, 256)
 
 int or_edge_eth_type(or_topo_t *t, uint16_t be_type, uint8_t edge) {
 	t->eth_edges[be_type] = edge;
@@ -343,6 +381,156 @@ int or_route_del(or_topo_t *t, uint16_t vrf, uint32_t ip_be, uint8_t len) {
 	return 0;
 }
 
+// ---- IPv6 RIB: exact-prefix hash per length (rib6_insert_or_replace /
+// rib6_delete, modules/ip6/control/route.c:230-345)
+
+// addr6_linklocal_scope, modules/ip6/control/ip6.h:23-36.
+static void scope6(uint8_t out[16], const uint8_t ip[16], uint16_t iface_id) {
+	memcpy(out, ip, 16);
+	if (ip[0] == 0xfe && (ip[1] & 0xc0) == 0x80) { // rte_ipv6_addr_is_linklocal [DPDK]
+		out[2] = (uint8_t)(iface_id >> 8);
+		out[3] = (uint8_t)iface_id;
+	}
+}
+
+static void mask6(uint8_t out[16], const uint8_t ip[16], unsigned len) { // rte_ipv6_addr_mask [DPDK]
+	for (unsigned i = 0; i < 16; i++) {
+		int bits = (int)len - 8 * (int)i;
+		out[i] = ip[i] & (bits >= 8 ? 0xff : bits <= 0 ? 0 : (uint8_t)(0xff << (8 - bits)));
+	}
+}
+
+static uint32_t ht6_hash(const uint8_t k[16]) {
+	uint32_t h = 2166136261u; // FNV-1a
+	for (int i = 0; i < 16; i++)
+		h = (h ^ k[i]) * 16777619u;
+	return h;
+}
+
+static uint32_t *ht6_find(const struct or_ht6 *h, const uint8_t k[16]) {
+	if (h->cap == 0)
+		return NULL;
+	for (uint32_t j = ht6_hash(k) & (h->cap - 1);; j = (j + 1) & (h->cap - 1)) {
+		if (h->vals[j] == 0)
+			return NULL;
+		if (memcmp(h->keys[j], k, 16) == 0)
+			return &h->vals[j];
+	}
+}
+
+static int ht6_put(struct or_ht6 *h, const uint8_t k[16], uint32_t v) {
+	if ((h->count + 1) * 2 > h->cap) {
+		struct or_ht6 n = {0};
+		n.cap = h->cap ? h->cap * 2 : 16;
+		n.keys = calloc(n.cap, 16);
+		n.vals = calloc(n.cap, sizeof(uint32_t));
+		if (!n.keys || !n.vals) {
+			free(n.keys);
+			free(n.vals);
+			return -ENOMEM;
+		}
+		for (uint32_t i = 0; i < h->cap; i++)
+			if (h->vals[i])
+				ht6_put(&n, h->keys[i], h->vals[i]);
+		free(h->keys);
+		free(h->vals);
+		*h = n;
+	}
+	uint32_t j = ht6_hash(k) & (h->cap - 1);
+	while (h->vals[j] != 0)
+		j = (j + 1) & (h->cap - 1);
+	memcpy(h->keys[j], k, 16);
+	h->vals[j] = v;
+	h->count++;
+	return 0;
+}
+
+int or_fib6_create(or_topo_t *t, uint16_t vrf) {
+	if (vrf == 0 || vrf >= t->max_ifaces)
+		return -EINVAL;
+	t->fibs6[vrf].exists = true;
+	return 0;
+}
+
+int or_route6_add(or_topo_t *t, const struct gr_hip_route6 *r, uint32_t n, int replace) {
+	for (uint32_t i = 0; i < n; i++) {
+		if (r[i].vrf_id == 0 || r[i].vrf_id >= t->max_ifaces || r[i].prefixlen > 128 || r[i].nh == 0
+		    || r[i].nh > t->max_nh)
+			return -EINVAL;
+		struct or_fib6 *f = &t->fibs6[r[i].vrf_id];
+		if (!f->exists)
+			return -ENONET;
+		uint8_t sc[16], key[16];
+		scope6(sc, r[i].ip, r[i].iface_id);
+		mask6(key, sc, r[i].prefixlen);
+		uint32_t *v = ht6_find(&f->len[r[i].prefixlen], key);
+		if (v != NULL) {
+			if (!replace)
+				return -EEXIST;
+			*v = r[i].nh;
+			continue;
+		}
+		if (ht6_put(&f->len[r[i].prefixlen], key, r[i].nh) < 0)
+			return -ENOMEM;
+	}
+	return 0;
+}
+
+int or_route6_del(or_topo_t *t, uint16_t vrf, uint16_t iface_id, const uint8_t ip[16], uint8_t len) {
+	if (vrf == 0 || vrf >= t->max_ifaces || len > 128 || !t->fibs6[vrf].exists)
+		return -EINVAL;
+	struct or_ht6 *h = &t->fibs6[vrf].len[len];
+	uint8_t sc[16], key[16];
+	scope6(sc, ip, iface_id);
+	mask6(key, sc, len);
+	if (ht6_find(h, key) == NULL)
+		return -ENOENT;
+	struct or_ht6 n = {0};
+	for (uint32_t i = 0; i < h->cap; i++)
+		if (h->vals[i] && memcmp(h->keys[i], key, 16) != 0 && ht6_put(&n, h->keys[i], h->vals[i]) < 0)
+			return -ENOMEM;
+	free(h->keys);
+	free(h->vals);
+	*h = n;
+	return 0;
+}
+
+// fib6_lookup's LPM (route.c:151-173, rte_fib6_lookup_bulk): probe each
+// prefix length, longest first, on the scoped address.
+uint32_t or_lpm6(const or_topo_t *t, uint16_t vrf, uint16_t iface_id, const uint8_t ip[16]) {
+	if (vrf == 0 || vrf >= t->max_ifaces || !t->fibs6[vrf].exists)
+		return 0;
+	uint8_t sc[16], key[16];
+	scope6(sc, ip, iface_id);
+	for (int l = 128; l >= 0; l--) {
+		mask6(key, sc, (unsigned)l);
+		const uint32_t *v = ht6_find(&t->fibs6[vrf].len[l], key);
+		if (v != NULL)
+			return *v;
+	}
+	return 0;
+}
+
+// Brute force: every stored prefix, keep the longest covering one.
+uint32_t or_lpm6_brute(const or_topo_t *t, uint16_t vrf, uint16_t iface_id, const uint8_t ip[16]) {
+	if (vrf == 0 || vrf >= t->max_ifaces || !t->fibs6[vrf].exists)
+		return 0;
+	uint8_t sc[16], key[16];
+	scope6(sc, ip, iface_id);
+	int best = -1;
+	uint32_t nh = 0;
+	for (int l = 0; l <= 128; l++) {
+		const struct or_ht6 *h = &t->fibs6[vrf].len[l];
+		mask6(key, sc, (unsigned)l);
+		for (uint32_t i = 0; i < h->cap; i++)
+			if (h->vals[i] && memcmp(h->keys[i], key, 16) == 0 && l > best) {
+				best = l;
+				nh = h->vals[i];
+			}
+	}
+	return nh;
+}
+
 // Longest-prefix match by probing each prefix length, longest first.
 uint32_t or_lpm_hash(const or_topo_t *t, uint16_t vrf, uint32_t ip) {
 	if (vrf == 0 || vrf >= t->max_ifaces || !t->fibs[vrf].exists)
@@ -471,6 +659,28 @@ static uint32_t fib4_lookup(const or_topo_t *t, uint16_t vrf_id, uint32_t dst_be
 	return nh;
 }
 
+// fib6_lookup, modules/ip6/control/route.c:151-173: the VRF's FIB6, the
+// scoped destination, 0 = no route, GROUP resolved as for IPv4.
+static uint32_t fib6_lookup(const or_topo_t *t, uint16_t vrf_id, uint16_t iface_id, const uint8_t dst[16], uint16_t rss) {
+	const struct gr_hip_iface *vrf = iface_from_id(t, vrf_id);
+	if (vrf == NULL || vrf->type != GR_HIP_IFACE_TYPE_VRF)
+		return 0;
+	uint32_t nh = or_lpm6(t, vrf_id, iface_id, dst);
+	if (nh == 0 || nh > t->max_nh)
+		return 0;
+	const struct gr_hip_nh *n = &t->nh[nh];
+	if (n->type == GR_HIP_NH_T_GROUP) {
+		if (n->n_members == 1)
+			return n->single > t->max_nh ? 0 : n->single;
+		if (n->n_members == 0)
+			return 0;
+		uint32_t i = n->reta_off + (rss & (uint32_t)(n->reta_size - 1));
+		nh = i < t->reta_cap ? t->reta[i] : 0;
+		return nh > t->max_nh ? 0 : nh;
+	}
+	return nh;
+}
+
 // ---------------------------------------------------------------------------
 // mbuf stand-in and the nodes
 // ---------------------------------------------------------------------------
@@ -494,7 +704,7 @@ struct or_mbuf {
 	uint16_t eth_type; // BE
 	// result
 	uint8_t edge;
-	uint8_t visited; // bit per enum gr_hip_node this packet was handed to
+	uint16_t visited; // bit per enum gr_hip_node this packet was handed to
 	uint8_t rx_counted, tx_counted;
 	uint16_t tx_iface, tx_parent;
 	uint16_t rx_iface, rx_parent;
@@ -528,6 +738,7 @@ struct or_graph {
 	uint32_t flags;
 	uint32_t readable; // frame bytes present: 64 (lines only) or in_stride
 	struct or_stream eth_input, ip_input, ip_forward, ip_output, eth_output, iface_output;
+	struct or_stream ip6_input, ip6_forward, ip6_output;
 };
 
 static inline void enqueue(struct or_stream *s, struct or_mbuf *m) {
@@ -609,6 +820,8 @@ static void node_eth_input(struct or_graph *g, struct or_mbuf **objs, uint16_t n
 		uint8_t e = t->eth_edges[type_be];
 		if (e == NEXT)
 			enqueue(&g->ip_input, m);
+		else if (e == NEXT6)
+			enqueue(&g->ip6_input, m);
 		else
 			terminal(m, e);
 	}
@@ -791,6 +1004,133 @@ next:
 	}
 }
 
+// ip6_input_process, modules/ip6/datapath/ip6_input.c:44-158
+static void node_ip6_input(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
+	const or_topo_t *t = g->t;
+	for (uint16_t i = 0; i < n; i++) {
+		struct or_mbuf *m = objs[i];
+		const uint8_t *ip = MTOD(m); // struct rte_ipv6_hdr
+		const uint8_t *src = ip + 8, *dst = ip + 24;
+		const struct gr_hip_iface *iface = iface_from_id(t, m->iface);
+		uint32_t nh = 0;
+		uint8_t edge;
+		if (m->data_len < 40) { // :62-69
+			edge = GR_HIP_E_IP6_INPUT_BAD_LENGTH;
+			goto next;
+		}
+		if ((ip[0] & 0xf0) != 0x60) { // rte_ipv6_check_version [DPDK] :71-74
+			edge = GR_HIP_E_IP6_INPUT_BAD_VERSION;
+			goto next;
+		}
+		static const uint8_t zero[16];
+		if (src[0] == 0xff || memcmp(dst, zero, 16) == 0) { // mcast src, unspec dst :76-80
+			edge = GR_HIP_E_IP6_INPUT_BAD_ADDR;
+			goto next;
+		}
+		if (dst[0] == 0xff) { // :82-101
+			uint8_t scope = dst[1] & 0x0f; // rte_ipv6_mc_scope [DPDK]
+			if (scope == 0 || scope == 1) { // SCOPE_NONE, SCOPE_IFACELOCAL
+				edge = GR_HIP_E_IP6_INPUT_BAD_ADDR;
+				goto next;
+			}
+			// mcast6_get_member: multicast group state stays with grout's
+			// CPU nodes, the packet is handed back whole
+			terminal(m, GR_HIP_E_PUNT);
+			continue;
+		}
+		switch (m->domain) { // :103-118
+		case GR_HIP_ETH_DOMAIN_LOOPBACK:
+		case GR_HIP_ETH_DOMAIN_LOCAL:
+			break;
+		case GR_HIP_ETH_DOMAIN_BROADCAST:
+		case GR_HIP_ETH_DOMAIN_MULTICAST:
+			edge = GR_HIP_E_IP6_INPUT_LOCAL;
+			goto next;
+		default:
+			edge = GR_HIP_E_IP6_INPUT_OTHER_HOST;
+			goto next;
+		}
+		nh = m->e_nh ? m->e_nh : fib6_lookup(t, iface->vrf_id, iface->id, dst, m->rss); // :122-128
+		if (nh == 0) {
+			edge = GR_HIP_E_IP6_ERROR_DEST_UNREACH;
+			goto next;
+		}
+		const struct gr_hip_nh *h = &t->nh[nh];
+		edge = t->in6_nh_edges[h->type]; // :130-132
+		if (edge != NEXT)
+			goto next;
+		if (h->type == GR_HIP_NH_T_L3 && (h->flags & GR_HIP_NH_F_LOCAL)
+		    && memcmp(dst, h->ipv6, 16) == 0) { // :136-145
+			edge = GR_HIP_E_IP6_INPUT_LOCAL;
+			goto next;
+		}
+		m->l3_nh = nh; // :151-153
+		enqueue(&g->ip6_forward, m);
+		continue;
+next:
+		m->l3_nh = nh;
+		terminal(m, edge);
+	}
+}
+
+// ip6_forward_process, modules/ip6/datapath/ip6_forward.c:14-35
+static void node_ip6_forward(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
+	for (uint16_t i = 0; i < n; i++) {
+		struct or_mbuf *m = objs[i];
+		uint8_t *ip = MTOD(m);
+		if (ip[7] <= 1) { // hop_limits
+			terminal(m, GR_HIP_E_IP6_ERROR_TTL_EXCEEDED);
+			continue;
+		}
+		ip[7] -= 1;
+		enqueue(&g->ip6_output, m);
+	}
+}
+
+// ip6_output_process, modules/ip6/datapath/ip6_output.c:59-150
+static void node_ip6_output(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
+	const or_topo_t *t = g->t;
+	for (uint16_t i = 0; i < n; i++) {
+		struct or_mbuf *m = objs[i];
+		const uint8_t *ip = MTOD(m);
+		uint8_t edge;
+		if (m->l3_nh == 0) { // :77-81
+			edge = GR_HIP_E_IP6_ERROR_DEST_UNREACH;
+			goto next;
+		}
+		m->packet_type = 0x10; // RTE_PTYPE_L3_IPV6, :83
+		const struct gr_hip_nh *h = &t->nh[m->l3_nh];
+		edge = t->out6_nh_edges[h->type]; // :85-87
+		if (edge != NEXT)
+			goto next;
+		// a multicast destination never comes out of ip6_input here (:82-101)
+		const struct gr_hip_iface *iface = iface_from_id(t, h->iface_id);
+		if (iface == NULL) { // :94-97
+			edge = GR_HIP_E_IP6_OUTPUT_ERROR;
+			goto next;
+		}
+		if (m->pkt_len > iface->mtu) { // :99-102
+			edge = GR_HIP_E_IP6_OUTPUT_TOO_BIG;
+			goto next;
+		}
+		edge = t->out6_iface_edges[iface->type]; // :106
+		m->iface = iface->id; // :107
+		if (edge != NEXT)
+			goto next;
+		if (h->state != GR_HIP_NH_S_REACHABLE
+		    || ((h->flags & GR_HIP_NH_F_LINK) && memcmp(ip + 24, h->ipv6, 16) != 0)) { // :113-119
+			edge = GR_HIP_E_IP6_HOLD;
+			goto next;
+		}
+		memcpy(m->eth_dst, h->mac, 6); // :122-127
+		m->eth_type = be16(0x86dd);
+		enqueue(&g->eth_output, m);
+		continue;
+next:
+		terminal(m, edge);
+	}
+}
+
 // eth_output_process, modules/infra/datapath/eth_output.c:28-77
 static void node_eth_output(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
 	const or_topo_t *t = g->t;
@@ -842,7 +1182,7 @@ static void node_iface_output(struct or_graph *g, struct or_mbuf **objs, uint16_
 
 static void mark(struct or_mbuf **objs, uint16_t n, int node) {
 	for (uint16_t i = 0; i < n; i++)
-		objs[i]->visited |= (uint8_t)(1u << node);
+		objs[i]->visited |= (uint16_t)(1u << node);
 }
 
 // One graph walk over a burst (rte_graph_walk RTC order, main_loop.c:459).
@@ -860,6 +1200,9 @@ static void graph_walk(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
 	RUN(ip_input, GR_HIP_NODE_IP_INPUT)
 	RUN(ip_forward, GR_HIP_NODE_IP_FORWARD)
 	RUN(ip_output, GR_HIP_NODE_IP_OUTPUT)
+	RUN(ip6_input, GR_HIP_NODE_IP6_INPUT)
+	RUN(ip6_forward, GR_HIP_NODE_IP6_FORWARD)
+	RUN(ip6_output, GR_HIP_NODE_IP6_OUTPUT)
 	RUN(eth_output, GR_HIP_NODE_ETH_OUTPUT)
 	RUN(iface_output, GR_HIP_NODE_IFACE_OUTPUT)
 #undef RUN
@@ -870,16 +1213,20 @@ static void graph_walk(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
 // returns only what it enqueued to eth_output (ip_output.c:153,162).
 // Punted packets restart on grout's CPU nodes, which count them there.
 static void walk_node_stats(struct or_mbuf *mb, uint16_t k, struct gr_hip_node_stats *ns) {
-	uint32_t cnt[GR_HIP_NODE_COUNT] = {0};
+	uint32_t cnt[GR_HIP_NODE_COUNT] = {0}, sent4 = 0, sent6 = 0;
 	for (uint16_t i = 0; i < k; i++) {
 		if (mb[i].edge == GR_HIP_E_PUNT)
 			continue;
 		for (int j = 0; j < GR_HIP_NODE_COUNT; j++)
 			cnt[j] += (mb[i].visited >> j) & 1;
+		if (mb[i].visited & (1u << GR_HIP_NODE_ETH_OUTPUT)) { // ip(6)_output's return value
+			sent4 += (mb[i].visited >> GR_HIP_NODE_IP_OUTPUT) & 1;
+			sent6 += (mb[i].visited >> GR_HIP_NODE_IP6_OUTPUT) & 1;
+		}
 	}
 	for (int j = 0; j < GR_HIP_NODE_COUNT; j++) {
 		ns->calls[j] += cnt[j] != 0;
-		ns->packets[j] += j == GR_HIP_NODE_IP_OUTPUT ? cnt[GR_HIP_NODE_ETH_OUTPUT] : cnt[j];
+		ns->packets[j] += j == GR_HIP_NODE_IP_OUTPUT ? sent4 : j == GR_HIP_NODE_IP6_OUTPUT ? sent6 : cnt[j];
 	}
 }
 

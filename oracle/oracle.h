@@ -54,6 +54,18 @@ int or_route_del(or_topo_t *, uint16_t vrf_id, uint32_t ip_be, uint8_t prefixlen
 // Build the DIR24_8 restatement (DPDK lib/fib/dir24_8, 8-byte entries).
 int or_fib_build(or_topo_t *, uint16_t vrf_id);
 
+// IPv6 RIB (exact-prefix hash per length, link-local prefixes scoped to
+// iface_id as addr6_linklocal_scope, modules/ip6/control/ip6.h:23-36).
+int or_fib6_create(or_topo_t *, uint16_t vrf_id);
+int or_route6_add(or_topo_t *, const struct gr_hip_route6 *, uint32_t n, int replace);
+int or_route6_del(or_topo_t *, uint16_t vrf_id, uint16_t iface_id, const uint8_t ip[16], uint8_t prefixlen);
+// IPv6 LPM (scoped): hash-per-length probe and brute force.
+uint32_t or_lpm6(const or_topo_t *, uint16_t vrf_id, uint16_t iface_id, const uint8_t ip[16]);
+uint32_t or_lpm6_brute(const or_topo_t *, uint16_t vrf_id, uint16_t iface_id, const uint8_t ip[16]);
+int or_edge_ip6_input_nh_type(or_topo_t *, uint8_t nh_type, uint8_t edge);
+int or_edge_ip6_output_nh_type(or_topo_t *, uint8_t nh_type, uint8_t edge);
+int or_edge_ip6_output_iface_type(or_topo_t *, uint8_t iface_type, uint8_t edge);
+
 // LPM: hash-per-length probe (truth) and DIR24_8 restatement. ip host order.
 // Return the nexthop slot, 0 = no route.
 uint32_t or_lpm_hash(const or_topo_t *, uint16_t vrf_id, uint32_t ip);

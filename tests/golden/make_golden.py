@@ -10,6 +10,7 @@ reference's own ip_input known answers and hand-derived cases). Fixtures:
   single.npz     config 2 stream, 2048 x 64 B
   fullview.npz   config 3 stream over the 1M-route view, 4096 x 64 B
   imix.npz       config 4 stream (IMIX), 512 packets, header lines only
+  fullview6.npz  IPv6 stream over a 20k-route IPv6 view, 4096 x 64 B
 """
 import hashlib
 import os
@@ -33,6 +34,7 @@ def digest(t):
     h.update(t.nh[:t.n_nh + 1].tobytes())
     h.update(t.reta.tobytes())
     h.update(t.route_array().tobytes())
+    h.update(t.route6_array().tobytes())
     return h.hexdigest()
 
 
@@ -60,6 +62,10 @@ def main():
 
     fr, me = S.stream(512, S.SEED_IMIX, routes=t.route_array(), imix=True, lines_only=True)
     save("imix.npz", t, fr, me, lines_only=True)
+
+    t = T.config_fullview6(count=20_000)
+    fr, me = S.stream6(4096, S.SEED_FULLVIEW6, t.route6_array())
+    save("fullview6.npz", t, fr, me)
 
 
 if __name__ == "__main__":

@@ -21,11 +21,18 @@ def _fullview():
     return T.config_fullview()
 
 
+@functools.lru_cache(maxsize=None)
+def _fullview6():
+    return T.config_fullview6(count=20_000)
+
+
 def topo_for(name):
     if name == "corpus":
         return SC.corpus_topology()[0]
     if name == "single":
         return T.config_single_route()
+    if name == "fullview6":
+        return _fullview6()
     return _fullview()
 
 
@@ -41,11 +48,14 @@ def fresh_fastpath_state(fp, topo):
     # wipe previous state: FIBs, ifaces, nexthops
     for vrf in list(_loaded.get("fibs", [])):
         fp.fib_destroy(vrf)
+    for vrf in list(_loaded.get("fibs6", [])):
+        fp.fib6_destroy(vrf)
     for i in _loaded.get("ifaces", []):
         fp.del_iface(int(i))
     fp.set_nexthops(np.zeros(fp.max_nexthops, dtype=abi.NH_DT), first=1)
     fp.load(topo)
-    _loaded.update(key=key, fibs=list(topo.fibs), ifaces=list(topo.live_ifaces()["id"]), topo=topo)
+    _loaded.update(key=key, fibs=list(topo.fibs), fibs6=list(topo.fibs6), ifaces=list(topo.live_ifaces()["id"]),
+                   topo=topo)
 
 
 def run_gpu(fp, topo, frames, meta, lines_only=False, inplace=False, q=None):

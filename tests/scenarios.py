@@ -6,7 +6,11 @@ and the edge cases SURVEY.md §8d lists: bad checksum, TTL 0/1, dst 0,
 version 6, IHL 4, total_len 10, bcast/mcast dst MAC, other-host MAC, no
 route, 255.255.255.255, 224.0.0.5, local address, ARP/SNAP/unknown
 ethertype, > MTU with/without DF, VLAN, unresolved nexthop, admin-down
-ifaces, plus ECMP groups, tbl8 prefixes and the ip_forward checksum quirk.
+ifaces, plus ECMP groups, tbl8 prefixes and the ip_forward checksum quirk;
+and the same for IPv6 (ip6_input.c / ip6_forward.c / ip6_output.c): bad
+version / length / addresses, multicast scopes, hop limit 0/1/2, local
+addresses, link-local scoping, prefixes of every trie level, > MTU, hold,
+groups, VLAN / no-MAC / admin-down / xvrf egress.
 """
 import numpy as np
 
@@ -91,6 +95,39 @@ def corpus_topology():
     ]
     for cidr, k in routes:
         t.add_route(1, cidr, nh[k])
+
+    # IPv6
+    t.add_address6(P0, "2001:db8::1/64")
+    t.add_address6(P1, "2001:db8:1::1/64")
+    t.add_address6(P1, "fe80::1/64")  # link-local, scoped to p1
+    nh["fwd6"] = t.add_nexthop(P1, "2001:db8:1::2", "02:00:00:06:00:02")
+    nh["fwd6b"] = t.add_nexthop(P2, "2001:db8:2::3", "02:00:00:06:00:03")
+    nh["fwd6c"] = t.add_nexthop(P1, "2001:db8:1::4", "02:00:00:06:00:04")
+    nh["unres6"] = t.add_nexthop(P0, "2001:db8::2")
+    nh["ll6"] = t.add_nexthop(P1, "fe80::2", "02:00:00:06:00:05")
+    nh["mtu6"] = t.add_nexthop(P2, "2001:db8:2::6", "02:00:00:06:00:06")  # p2 MTU 1280
+    nh["vlan6"] = t.add_nexthop(VLAN200, "2001:db8:c8::2", "02:00:00:06:00:07")
+    nh["nomac6"] = t.add_nexthop(NOMAC, "2001:db8:7::2", "02:00:00:06:00:08")
+    nh["down6"] = t.add_nexthop(DOWN, "2001:db8:4::2", "02:00:00:06:00:09")
+    nh["xvrf6"] = t.add_nexthop(VRF2, "2001:db8:11::2", "02:00:00:06:00:0a")
+    nh["stale6"] = t.add_nexthop(P1, "2001:db8:1::33", "02:00:00:06:00:0b", state=abi.NH_S["STALE"])
+    nh["noif6"] = t.add_nexthop(999, "2001:db8:99::2", "02:00:00:06:00:0c", vrf_id=1)
+    g6a = t.add_nexthop(P1, "2001:db8:1::10", "02:00:00:06:01:0a")
+    g6b = t.add_nexthop(P2, "2001:db8:2::11", "02:00:00:06:01:0b")
+    nh["grp6"] = t.add_group([g6a, g6b], reta_size=8)
+    routes6 = [
+        ("2001:db8:100::/48", "fwd6"), ("2001:db8:100:1::/64", "fwd6b"), ("2001:db8:100:1::7/128", "fwd6c"),
+        ("2001:db8:100:2::/63", "fwd6c"), ("2001:db8:100:4:8000::/65", "fwd6b"),
+        ("2001:db8:101::/48", "unres6"), ("2001:db8:102::/48", "bh"), ("2001:db8:103::/48", "rej"),
+        ("2001:db8:104::/48", "grp6"), ("2001:db8:105::/48", "mtu6"), ("2001:db8:106::/48", "vlan6"),
+        ("2001:db8:107::/48", "nomac6"), ("2001:db8:108::/48", "down6"), ("2001:db8:109::/48", "xvrf6"),
+        ("2001:db8:10a::/48", "stale6"), ("2001:db8:10b::/48", "noif6"), ("2001:db8:10c::/48", "sr6"),
+        ("2001:db8::/32", "fwd6b"), ("2000::/3", "fwd6c"), ("3000::/12", "fwd6"), ("3000:8000::/17", "fwd6b"),
+        ("2001:db8:200::/40", "fwd6"), ("2001:db8:200:ff00::/56", "fwd6c"),
+    ]
+    for cidr, k in routes6:
+        t.add_route6(1, cidr, nh[k])
+    t.add_route6(1, "fe80::2/128", nh["ll6"], iface_id=P1)  # link-local host route on p1 only
     return t, nh
 
 
@@ -233,6 +270,62 @@ def corpus_frames(seed=0x5eed):
     del base
     for d in ["16.1.0.20", "16.1.0.21"]:
         add("ttl 255 " + d, fr(dst=d, ttl=255))
+    # ---- IPv6
+    f6 = S.frame6
+    for d in ["2001:db8:100::1", "2001:db8:100:1::1", "2001:db8:100:1::7", "2001:db8:100:1::8",
+              "2001:db8:100:3::1", "2001:db8:100:4:8000::9", "2001:db8:100:4:7fff::9", "2001:db8:5::1",
+              "2fff::1", "3000:1::1", "3000:8000::1", "3000:7fff::1", "2001:db8:200:ff00::1",
+              "2001:db8:200:fe00::1"]:
+        add("fwd6 " + d, f6(dst=d))
+    add("fwd6 hop 2", f6(dst="2001:db8:100::2", hop=2))
+    add("hop 1", f6(dst="2001:db8:100::2", hop=1))
+    add("hop 0", f6(dst="2001:db8:100::2", hop=0))
+    add("ip6 version 4", f6(dst="2001:db8:100::3", version=4))
+    add("ip6 version 7", f6(dst="2001:db8:100::3", version=7))
+    add("ip6 data_len 39", f6(dst="2001:db8:100::3"), pkt_len=53)
+    add("ip6 data_len 40", f6(dst="2001:db8:100::3"), pkt_len=54)
+    add("ip6 src mcast", f6(src="ff02::1", dst="2001:db8:100::3"))
+    add("ip6 dst unspec", f6(dst="::"))
+    add("ip6 mcast scope 0", f6(dst="ff00::1"))
+    add("ip6 mcast scope 1", f6(dst="ff01::1"))
+    add("ip6 mcast scope 2", f6(dst_mac="33:33:00:00:00:01", dst="ff02::1"))
+    add("ip6 mcast scope 5", f6(dst="ff05::1:3"))
+    add("ip6 bcast mac", f6(dst_mac="ff:ff:ff:ff:ff:ff", dst="2001:db8:100::4"))
+    add("ip6 mcast mac", f6(dst_mac="33:33:00:00:00:09", dst="2001:db8:100::4"))
+    add("ip6 other host mac", f6(dst_mac="02:00:00:aa:bb:cc", dst="2001:db8:100::4"))
+    add("ip6 no route", f6(dst="4000::1"))
+    add("ip6 local addr", f6(dst="2001:db8::1"))
+    add("ip6 local addr p1", f6(dst="2001:db8:1::1"))
+    add("ip6 connected hold", f6(dst="2001:db8:1::5"))
+    add("ip6 unresolved gw hold", f6(dst="2001:db8:101::1"))
+    add("ip6 stale hold", f6(dst="2001:db8:10a::1"))
+    add("ip6 blackhole", f6(dst="2001:db8:102::1"))
+    add("ip6 reject", f6(dst="2001:db8:103::1"))
+    add("ip6 sr6 output", f6(dst="2001:db8:10c::1"))
+    for r in range(6):
+        add("ip6 group rss %d" % r, f6(dst="2001:db8:104::%x" % (r + 1)), rss=int(rng.integers(0, 65536)))
+    add("ip6 mtu ok", f6(dst="2001:db8:105::1", payload_len=1240, length=100), pkt_len=1294)
+    add("ip6 too big", f6(dst="2001:db8:105::1", payload_len=1241, length=100), pkt_len=1295)
+    add("ip6 egress vlan", f6(dst="2001:db8:106::1"))
+    add("ip6 egress no mac", f6(dst="2001:db8:107::1"))
+    add("ip6 egress down", f6(dst="2001:db8:108::1"))
+    add("ip6 xvrf", f6(dst="2001:db8:109::1"))
+    add("ip6 nh iface missing", f6(dst="2001:db8:10b::1"))
+    add("ip6 link-local on p1", f6(dst_mac=PORT_MAC[1], dst="fe80::2"), iface=P1)
+    add("ip6 link-local on p0", f6(dst="fe80::2"))
+    add("ip6 link-local local p1", f6(dst_mac=PORT_MAC[1], dst="fe80::1"), iface=P1)
+    add("ip6 vlan 100 fwd", f6(dst="2001:db8:100::5"), vlan=100)
+    add("ip6 vlan 300 unknown", f6(dst="2001:db8:100::5"), vlan=300)
+    add("ip6 ingress down", f6(dst="2001:db8:100::6", dst_mac="02:00:00:00:00:04"), iface=DOWN)
+    add("ip6 vrf missing", f6(dst="2001:db8:100::6", dst_mac="02:00:00:00:00:12"), iface=VRF3_PORT)
+    for k in range(8):
+        b = bytearray(rng.integers(0, 256, 64, dtype=np.uint8).tobytes())
+        b[12:14] = b"\x86\xdd"
+        if k % 2:
+            b[0:6] = T.mac_bytes(PORT_MAC[0])
+        if k % 4 == 1:
+            b[14] = 0x60 | (b[14] & 0x0F)
+        add("random6 %d" % k, bytes(b))
     # random bytes frames
     for k in range(32):
         b = bytearray(rng.integers(0, 256, 64, dtype=np.uint8).tobytes())

@@ -5,6 +5,8 @@ Bit-exact on integer/byte work: verdict (edge, domain, iface, nexthop),
 the 64-byte header line each packet leaves with, and the per-iface rx/tx
 counters, on the same seeded inputs -- from the exception corpus up to the
 BASELINE full size (16M packets over the 1M-route view)."""
+import functools
+
 import numpy as np
 import pytest
 
@@ -314,3 +316,82 @@ def test_ring_geometries(fastpath, cfg):
     finally:
         fastpath.tune("ring", 1)
         fastpath.tune("wg_per_cu", 0)
+
+
+# ---- IPv6
+
+@functools.lru_cache(maxsize=None)
+def _fullview6_big():
+    return T.config_fullview6(count=100_000)
+
+
+def test_fullview6_stream(fastpath):
+    """IPv6 forwarding over a 100k-route IPv6 view, 2^20 packets."""
+    t = _fullview6_big()
+    fr, me = S.stream6(1 << 20, S.SEED_FULLVIEW6 + 1, t.route6_array())
+    o = oracle.Oracle(t).process(fr, me)
+    g = run_gpu(fastpath, t, fr, me)
+    compare(o, g)
+    assert (g[1]["edge"] == abi.EDGE["port_output"]).mean() > 0.99
+    info = fastpath.fib6_info(1)
+    assert info["routes"] == len(t.route6_array()) and info["groups_used"] > 100_000
+
+
+def test_mixed_v4_v6_stream(fastpath):
+    """IPv4 and IPv6 packets interleaved in every wave (divergent chains)."""
+    t, _ = SC.corpus_topology()
+    rng = np.random.default_rng(46)
+    f4, m4 = S.stream(1 << 16, 0x4646, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    r6 = t.route6_array()
+    f6, m6 = S.stream6(1 << 16, 0x6464, r6[r6["prefixlen"] < 128])
+    pick = rng.integers(0, 2, size=1 << 16).astype(bool)
+    fr = np.where(pick[:, None], f4, f6)
+    me = np.where(pick, m4, m6)
+    compare(oracle.Oracle(t).process(fr, me), run_gpu(fastpath, t, fr, me))
+
+
+def test_live_route6_updates(fastpath):
+    """route6 add / replace / delete after the first commit, then parity
+    (rib6_insert_or_replace / rib6_delete, modules/ip6/control/route.c)."""
+    t = T.config_fullview6(count=5_000)
+    r = t.route6_array()
+    fr, me = S.stream6(1 << 16, 0x1606, r[r["prefixlen"] < 128])
+    run_gpu(fastpath, t, fr, me)  # loads t
+    o = oracle.Oracle(t)
+    rng = np.random.default_rng(16)
+    idx = rng.permutation(len(r) - 1)  # leave the address route alone
+    for i in idx[:500]:
+        fastpath.route6_del(1, bytes(r["ip"][i]), int(r["prefixlen"][i]))
+        ip = np.ascontiguousarray(r["ip"][i])
+        assert o.L.or_route6_del(o.h, 1, 0, ip.ctypes.data, int(r["prefixlen"][i])) == 0
+    rep = r[idx[500:800]].copy()
+    rep["nh"] = np.roll(rep["nh"], 1)
+    fastpath.route6_add(rep, replace=True)
+    assert o.L.or_route6_add(o.h, rep.ctypes.data, len(rep), 1) == 0
+    new = r[idx[800:900]].copy()
+    new["prefixlen"] = np.minimum(new["prefixlen"].astype(np.int32) + 8, 128).astype(np.uint8)
+    new["ip"][:, 15] ^= 0x5A  # more-specifics under existing routes
+    uniq = {(bytes(x["ip"]), int(x["prefixlen"])) for x in r}
+    new = new[[(bytes(x["ip"]), int(x["prefixlen"])) not in uniq for x in new]]
+    fastpath.route6_add(new, replace=True)
+    assert o.L.or_route6_add(o.h, new.ctypes.data, len(new), 1) == 0
+    fastpath.fib6_commit(1)
+    compare(o.process(fr, me), run_gpu(fastpath, t, fr, me))
+    g = run_gpu(fastpath, t, fr, me)
+    assert (g[1]["edge"] == abi.EDGE["ip6_error_dest_unreach"]).sum() > 0
+    for x in list(r[idx[:20]]) + list(rep[:20]) + list(new[:20]):
+        assert fastpath.fib6_lookup(1, bytes(x["ip"])) == o.lpm6(1, bytes(x["ip"]))
+    fresh_fastpath_state(fastpath, T.config_single_route())  # drop the modified state
+
+
+def test_fib6_lookup_host_scoping(fastpath):
+    """The context's host lookup scopes link-local destinations like
+    fib6_lookup (addr6_linklocal_scope)."""
+    t, _ = SC.corpus_topology()
+    from golden_util import fresh_fastpath_state
+    fresh_fastpath_state(fastpath, t)
+    o = oracle.Oracle(t)
+    for dst in ["fe80::2", "fe80::1", "2001:db8:100:1::7", "3000:8000::1", "4000::1"]:
+        for iface in [T.PORT_IFACE[0], T.PORT_IFACE[1]]:
+            ip = T.ip6(dst)
+            assert fastpath.fib6_lookup(1, ip, iface) == o.lpm6(1, ip, iface), (dst, iface)

@@ -67,17 +67,25 @@ def compare_mbufs(got, want, frames_after, lines_want, labels=None):
 def test_edge_node_table():
     """Every verdict edge maps to the node that chose it."""
     L = abi.hip()
-    node_of = {e: L.gr_hip_edge_node(i, 0) for i, e in enumerate(abi.EDGE_NAMES)}
+    N = {n: i for i, n in enumerate(abi.NODE_NAMES)}
+    node_of = {e: L.gr_hip_edge_node(i, 0, 0) for i, e in enumerate(abi.EDGE_NAMES)}
     assert node_of["punt"] == -1
-    assert node_of["port_output"] == node_of["iface_output_admin_down"] == 6
-    assert node_of["ip_hold"] == node_of["ip_output_snat"] == 4
-    assert node_of["ip_error_ttl_exceeded"] == 3
-    assert node_of["ip_error_dest_unreach"] == node_of["ip_input_local"] == 2
-    assert node_of["snap_input"] == node_of["arp_input"] == 1
-    assert node_of["iface_input_admin_down"] == node_of["bridge_input"] == 0
-    assert L.gr_hip_edge_node(abi.EDGE["bridge_input"], 7) == 6  # iface_output BRIDGE type edge
+    assert node_of["port_output"] == node_of["iface_output_admin_down"] == N["iface_output"]
+    assert node_of["ip_hold"] == node_of["ip_output_snat"] == N["ip_output"]
+    assert node_of["ip_error_ttl_exceeded"] == N["ip_forward"]
+    assert node_of["ip_error_dest_unreach"] == node_of["ip_input_local"] == N["ip_input"]
+    assert node_of["snap_input"] == node_of["arp_input"] == node_of["ip6_input"] == N["eth_input"]
+    assert node_of["iface_input_admin_down"] == node_of["bridge_input"] == N["iface_input"]
+    assert node_of["ip6_input_bad_addr"] == node_of["ip6_error_dest_unreach"] == node_of["sr6_local"] == N["ip6_input"]
+    assert node_of["ip6_error_ttl_exceeded"] == N["ip6_forward"]
+    assert node_of["ip6_hold"] == node_of["ip6_output_too_big"] == N["ip6_output"]
+    # edges two nodes share: the nexthop / the address family tell them apart
+    assert L.gr_hip_edge_node(abi.EDGE["bridge_input"], 7, 0) == N["iface_output"]
+    assert L.gr_hip_edge_node(abi.EDGE["xvrf"], 7, 0) == N["ip_output"]
+    assert L.gr_hip_edge_node(abi.EDGE["xvrf"], 7, 1) == N["ip6_output"]
+    assert L.gr_hip_edge_node(abi.EDGE["sr6_output"], 7, 1) == N["ip6_output"]
     assert all(v >= -1 for v in node_of.values())
-    assert L.gr_hip_edge_node(abi.E_COUNT, 0) < -1
+    assert L.gr_hip_edge_node(abi.E_COUNT, 0, 0) < -1
 
 
 def test_stage_roundtrip():
@@ -104,7 +112,10 @@ def test_apply_corpus_matches_oracle_mbufs():
     assert np.array_equal(ns["calls"], ns_want["calls"]), (ns, ns_want)
     edges = set(abi.EDGE_NAMES[e] for e in v["edge"])
     assert {"port_output", "ip_hold", "ip_error_ttl_exceeded", "eth_output_no_mac", "snap_input",
-            "iface_input_unknown_vlan", "ip_input_bad_checksum"} <= edges
+            "iface_input_unknown_vlan", "ip_input_bad_checksum", "ip6_hold", "ip6_output_too_big",
+            "ip6_error_ttl_exceeded", "ip6_input_bad_addr", "xvrf"} <= edges
+    six = (m["packet_type"] == abi.PTYPE_L3_IPV6)
+    assert six.sum() > 10 and (m["packet_type"][six] == want["packet_type"][six]).all()
 
 
 @pytest.mark.parametrize("burst", [1, 7, 64])
@@ -122,8 +133,9 @@ def test_node_stats_bursts(burst):
     assert (ns["calls"] <= n_walks).all()
     if burst == 64:
         assert np.array_equal(ns["calls"], ns64["calls"])
-    # ip_output returns what it sent to eth_output
-    assert ns["packets"][4] == ns["packets"][5]
+    # ip_output / ip6_output return what they sent to eth_output
+    N = {n: i for i, n in enumerate(abi.NODE_NAMES)}
+    assert ns["packets"][N["ip_output"]] + ns["packets"][N["ip6_output"]] == ns["packets"][N["eth_output"]]
 
 
 def test_apply_fullview_stream():

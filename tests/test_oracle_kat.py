@@ -7,7 +7,12 @@
    here the same header follows an Ethernet header addressed to the RX port.
 2. ip_forward's incremental checksum (ip_forward.c:29-32), hand-derived.
 3. The longest-prefix match of both oracle LPMs against brute force.
+4. The five cases of ip6_input's unit test (ip6_input.c:245-318), the hop
+   limit of ip6_forward, and the IPv6 LPM (oracle hash, brute force and the
+   product's trie) against each other.
 """
+import ipaddress
+
 import numpy as np
 import pytest
 
@@ -120,3 +125,88 @@ def test_lpm_vs_brute_force():
         b = o.lpm(1, ip, "brute")
         assert o.lpm(1, ip, "hash") == b
         assert o.lpm(1, ip, "dir24") == b
+
+
+# ---- IPv6: the five cases of modules/ip6/datapath/ip6_input.c:245-318
+# (ipv6_init_default_mbuf :217-243: version 6, payload 0, next header NONE,
+# hop limit 64, src 0:3:0:3:1:9:8:8, dst 0:3:0:5:2:0:2:4, data_len 40,
+# domain OTHER), restated on frames to a MAC that is not the port's.
+OTHER_MAC = "02:00:00:aa:bb:cc"
+
+
+def kat6(**kw):
+    d = dict(dst_mac=OTHER_MAC, next_header=59, hop=64, src="0:3:0:3:1:9:8:8", dst="0:3:0:5:2:0:2:4",
+             payload_len=0, length=54)
+    d.update(kw)
+    return S.frame6(**d)
+
+
+def test_kat6_invalid_version():  # ip6_input.c:245-253
+    assert run(kat_topo(), [kat6(version=5)]) == ["ip6_input_bad_version"]
+
+
+def test_kat6_invalid_src_mcast_addr():  # ip6_input.c:255-266
+    assert run(kat_topo(), [kat6(src="ffff:ffff:ffff:ffff:ffff:ffff:ffff:ffff")]) == ["ip6_input_bad_addr"]
+
+
+def test_kat6_invalid_dst_unspec_addr():  # ip6_input.c:268-279
+    assert run(kat_topo(), [kat6(dst="::")]) == ["ip6_input_bad_addr"]
+
+
+def test_kat6_invalid_dst_mcast_addr():  # ip6_input.c:281-301: scope none, iface-local
+    assert run(kat_topo(), [kat6(dst="ff00::1"), kat6(dst="ff01::1")]) == ["ip6_input_bad_addr"] * 2
+
+
+def test_kat6_invalid_mbuf_len():  # ip6_input.c:303-311: data_len = 40 / 2
+    assert run(kat_topo(), [kat6()], pkt_lens=[14 + 20]) == ["ip6_input_bad_length"]
+
+
+def test_kat6_default_is_other_host():
+    # the default fake mbuf passes every check above and stops at the
+    # domain (ETH_DOMAIN_OTHER, ip6_input.c:114-118)
+    assert run(kat_topo(), [kat6()]) == ["ip6_input_other_host"]
+
+
+def test_kat6_hop_limit():  # ip6_forward.c:25-30: 1 -> error, 2 -> forwarded with 1
+    t = T.base_ports()
+    nh = t.add_nexthop(T.PORT_IFACE[1], "2001:db8:1::2", "02:00:00:06:00:02")
+    t.add_route6(1, "2001:db8:100::/48", nh)
+    f = [S.frame6(dst="2001:db8:100::1", hop=h) for h in (0, 1, 2)]
+    arr, meta = S.pack(f)
+    out, v, _ = oracle.Oracle(t).process(arr, meta)
+    assert [abi.EDGE_NAMES[e] for e in v["edge"]] == ["ip6_error_ttl_exceeded"] * 2 + ["port_output"]
+    assert out[2][21] == 1 and out[2][12] == 0x86 and out[2][13] == 0xdd
+    assert bytes(out[2][:6]) == T.mac_bytes("02:00:00:06:00:02")
+
+
+def test_lpm6_hash_matches_brute_force():
+    rng = np.random.default_rng(6)
+    t = T.base_ports()
+    nhs = [t.add_nexthop(T.PORT_IFACE[1], "2001:db8:1::%x" % (i + 2), "02:00:00:06:00:%02x" % i) for i in range(8)]
+    for i in range(300):
+        plen = int(rng.choice([0, 3, 8, 16, 17, 24, 31, 32, 40, 47, 48, 56, 64, 65, 96, 127, 128]))
+        a = bytearray(rng.integers(0, 256, 16, dtype=np.uint8).tobytes())
+        a[0] = 0x20 | (a[0] & 0x0F)
+        net = ipaddress.IPv6Network((bytes(a), plen), strict=False)
+        t.add_route6(1, str(net), nhs[i % 8])
+    # de-duplicate (later identical prefixes would be EEXIST)
+    r = t.route6_array()
+    _, keep = np.unique(np.concatenate([r["ip"], r["prefixlen"][:, None]], axis=1), axis=0, return_index=True)
+    t.routes6 = [r[np.sort(keep)]]
+    o = oracle.Oracle(t)
+    host = abi.host()
+    f = host.gr_fib6_new(1024, 4096)
+    for x in t.route6_array():
+        ip = np.ascontiguousarray(x["ip"])
+        assert host.gr_fib6_add(f, ip.ctypes.data, int(x["prefixlen"]), int(x["nh"]), 0) == 0
+    assert host.gr_fib6_build(f) == 0
+    for i in range(2000):
+        d = rng.integers(0, 256, 16, dtype=np.uint8)
+        if i % 2:  # under a route
+            x = t.route6_array()[i % len(t.route6_array())]
+            d[:x["prefixlen"] // 8] = x["ip"][:x["prefixlen"] // 8]
+        want = o.lpm6(1, bytes(d), brute=True)
+        assert o.lpm6(1, bytes(d)) == want
+        assert host.gr_fib6_lookup(f, d.ctypes.data) == want  # the product's trie
+        assert host.gr_fib6_lookup_rib(f, d.ctypes.data) == want
+    host.gr_fib6_free(f)
