@@ -63,6 +63,19 @@ struct vrf_fib {
 	uint32_t max_slot = 0; // highest nexthop slot ever routed (never decreases)
 	uint32_t num_tbl8 = 0;
 	bool uploaded = false; // tables uploaded at least once
+
+	void reset4() { // forget the IPv4 state only
+		rib = nullptr;
+		d24 = d8 = d16 = nullptr;
+		d8_16 = nullptr;
+		chunk_of.clear();
+		chunk_free.clear();
+		n_chunks = 0;
+		fmt16 = false;
+		max_slot = 0;
+		num_tbl8 = 0;
+		uploaded = false;
+	}
 	// IPv6: fib6.h trie, on the device as top[65536] followed by the groups
 	gr_fib6_t *rib6 = nullptr;
 	uint32_t *d6 = nullptr;
@@ -801,7 +814,7 @@ extern "C" int gr_hip_fib4_destroy(gr_hip_ctx_t *c, uint16_t vrf) {
 	hipFree(v.d16);
 	hipFree(v.d8_16);
 	gr_fib4_free(v.rib);
-	v = vrf_fib {};
+	v.reset4();
 	return 0;
 }
 

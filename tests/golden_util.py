@@ -45,12 +45,14 @@ def fresh_fastpath_state(fp, topo):
     if _loaded.get("key") == key:
         return
     _loaded.pop("topo", None)
-    # wipe previous state: FIBs, ifaces, nexthops
-    for vrf in list(_loaded.get("fibs", [])):
+    _loaded.pop("key", None)
+    # wipe previous state: FIBs, ifaces, nexthops (popped first, so that one
+    # failure does not cascade into every later test)
+    for vrf in _loaded.pop("fibs", []):
         fp.fib_destroy(vrf)
-    for vrf in list(_loaded.get("fibs6", [])):
+    for vrf in _loaded.pop("fibs6", []):
         fp.fib6_destroy(vrf)
-    for i in _loaded.get("ifaces", []):
+    for i in _loaded.pop("ifaces", []):
         fp.del_iface(int(i))
     fp.set_nexthops(np.zeros(fp.max_nexthops, dtype=abi.NH_DT), first=1)
     fp.load(topo)
