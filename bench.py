@@ -33,7 +33,7 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batch", type=int, default=1 << 24, help="packets per step per GPU")
-    p.add_argument("--workload", default="fullview64", choices=["fullview64", "single64", "imix"])
+    p.add_argument("--workload", default="fullview64", choices=["fullview64", "single64", "imix", "fullview6"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-path", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="wall time of the CPU baseline sample")
@@ -52,7 +52,7 @@ def main():
     from grout_amd import abi
     from grout_amd import synth as S
     from grout_amd import topology as T
-    from grout_amd.fwd import FastPath
+    from grout_amd.fwd import FastPath, shared_stream
 
     from grout_amd.replicas import Replicas
 
@@ -67,6 +67,10 @@ def main():
         topo = T.config_single_route()
         routes, dst_range = None, (T.ip4("16.1.0.0"), T.ip4("16.1.255.255"))
         workload = "config2: 64B synthetic burst, 1-route FIB"
+    elif args.workload == "fullview6":
+        topo = T.config_fullview6(200_000)
+        routes, dst_range = None, None
+        workload = "IPv6: 64B synthetic burst, 200k-route IPv6 view (2000::/3, /16../64 mix)"
     else:
         topo = T.config_fullview()
         routes, dst_range = topo.route_array(), None
@@ -74,7 +78,7 @@ def main():
                     else "config4: IMIX 64/570/1518 synthetic burst, full-view FIB, header lines staged")
     fp = FastPath(local)
     fp.load(topo)
-    info = fp.fib_info(T.VRF_MAIN)
+    info = fp.fib6_info(T.VRF_MAIN) if args.workload == "fullview6" else fp.fib_info(T.VRF_MAIN)
     log(f"[rank {rank}] topology + FIB loaded in {time.time() - t0:.1f}s: {info}")
 
     # ---- synthetic RX stream of this GPU (seed 0x67721000 + g)
@@ -82,7 +86,11 @@ def main():
     seed = rep.seed()
     imix = args.workload == "imix"
     t0 = time.time()
-    frames, meta = S.stream(n, seed, routes=routes, dst_range=dst_range, imix=imix, lines_only=imix)
+    if args.workload == "fullview6":
+        r6 = topo.route6_array()
+        frames, meta = S.stream6(n, seed, r6[r6["prefixlen"] < 128])
+    else:
+        frames, meta = S.stream(n, seed, routes=routes, dst_range=dst_range, imix=imix, lines_only=imix)
     d_in = torch.from_numpy(frames.reshape(-1)).to(dev)
     d_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
     d_out = torch.empty(n * abi.LINE, dtype=torch.uint8, device=dev)
@@ -90,7 +98,7 @@ def main():
     torch.cuda.synchronize()
     log(f"[rank {rank}] {n} packets generated and resident in {time.time() - t0:.1f}s")
 
-    q = fp.queue(torch.cuda.current_stream(dev).cuda_stream)
+    q = fp.queue(shared_stream(dev))
 
     def step():
         q.submit(d_in, d_out, d_meta, d_v, n, in_stride=abi.LINE, out_stride=abi.LINE, lines_only=imix)
@@ -142,7 +150,8 @@ def main():
             "workload": workload,
             "batch_pkts_per_gpu": n,
             "routes": int(info["routes"]),
-            "tbl8_groups_used": int(info["tbl8_used"]),
+            **({"trie_groups_used": int(info["groups_used"])} if "groups_used" in info
+               else {"tbl8_groups_used": int(info["tbl8_used"])}),
             "parallelism": f"replicas x{world} (one RX stream + FIB replica per GPU, no collective)",
             "forwarded_frac": round(fwd_frac, 6),
         },
@@ -157,7 +166,9 @@ def main():
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),
         },
     }
-    if args.workload != "fullview64":
+    if args.workload == "fullview6":
+        result["metric"] = "Mpps IPv6 forward, 64B pkts, 200k-route IPv6 view (device-resident) [non-headline]"
+    elif args.workload != "fullview64":
         result["metric"] = result["metric"] + f" [non-headline workload: {args.workload}]"
 
     # ---- host-memory path (PCIe-inclusive): reported, never `value`
@@ -202,8 +213,9 @@ def main():
             "cores": threads,
             "kind": "port",
             "single_core_mpps": round(m1, 2),
-            "sample": (f"oracle C restatement of grout's node chain (bursts of 64, DIR24_8 8-byte "
-                       f"entries), {threads} pinned threads x {per_thread} packets of the same "
+            "sample": (f"oracle C restatement of grout's node chain (bursts of 64, "
+                       f"{'per-length prefix hash LPM6' if args.workload == 'fullview6' else 'DIR24_8 8-byte entries'}), "
+                       f"{threads} pinned threads x {per_thread} packets of the same "
                        f"1M-packet prefix of this stream"),
         }
         o.close()

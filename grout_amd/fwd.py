@@ -143,10 +143,24 @@ class FastPath:
         return q
 
 
+def shared_stream(device):
+    """A created torch stream, made torch's current one on `device`, for a
+    queue that shares the stream with torch work (copies, reductions). The
+    null stream cannot be shared: gr_hip_queue_create(NULL) makes a private
+    non-blocking stream that does not order against it."""
+    import torch
+    s = torch.cuda.Stream(device)
+    torch.cuda.set_stream(s)
+    return s.cuda_stream
+
+
 class Queue:
     def __init__(self, fp, stream=None):
         self.fp = fp
         self.lib = fp.lib
+        if stream is not None and int(stream) == 0:
+            raise ValueError("the null stream cannot be shared with a queue (NULL = private stream); "
+                             "pass grout_amd.fwd.shared_stream(device)")
         h = ctypes.c_void_p()
         check("gr_hip_queue_create", self.lib.gr_hip_queue_create(fp.h, stream, ctypes.byref(h)))
         self._h = h

@@ -67,7 +67,8 @@ def run_gpu(fp, topo, frames, meta, lines_only=False, inplace=False, q=None):
     dev = torch.device("cuda")
     if q is None:
         if "q" not in _loaded:
-            _loaded["q"] = fp.queue(torch.cuda.current_stream().cuda_stream)
+            from grout_amd.fwd import shared_stream
+            _loaded["q"] = fp.queue(shared_stream(dev))
         q = _loaded["q"]
     n = len(meta)
     stride = frames.shape[1]

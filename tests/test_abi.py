@@ -1,6 +1,7 @@
 # SPDX-License-Identifier: BSD-3-Clause
 """The C-ABI library loads and exports every symbol include/grout_hip.h
 declares (no device calls: this runs without a GPU)."""
+import pytest
 import ctypes
 import os
 import re
@@ -60,3 +61,16 @@ def test_struct_sizes_match_header():
     text = open(os.path.join(ROOT, "include/grout_hip.h")).read()
     body = text[text.index("enum gr_hip_edge {"):text.index("GR_HIP_E_COUNT")]
     assert len(re.findall(r"\bGR_HIP_E_\w+", body)) == abi.E_COUNT
+
+
+def test_queue_refuses_null_stream():
+    """A queue never silently gets a private stream when the caller meant to
+    share torch's default (null) stream."""
+    from grout_amd.fwd import Queue
+
+    class _FP:
+        lib = None
+        h = None
+
+    with pytest.raises(ValueError):
+        Queue(_FP(), 0)

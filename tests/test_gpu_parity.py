@@ -61,6 +61,36 @@ def test_corpus_in_place(fastpath):
     compare(oracle.Oracle(t).process(fr, me), run_gpu(fastpath, t, fr, me, inplace=True), lab)
 
 
+def test_in_place_full_frames(fastpath):
+    """In place on full frames (grout rewrites mbufs in place): the first 64
+    bytes match the oracle, bytes 32 and up are untouched (nothing past the
+    IPv4 checksum / IPv6 hop limit is rewritten) and so is everything past
+    the 64-byte line. IPv4 and IPv6 corpus frames plus a stream, 128-byte stride."""
+    import torch
+    t, _ = SC.corpus_topology()
+    fr, me, lab = SC.corpus_arrays()
+    f2, m2 = S.stream(1 << 14, 0x3232, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")), stride=128)
+    fr = np.concatenate([np.pad(fr, ((0, 0), (0, 128 - fr.shape[1]))) if fr.shape[1] < 128 else fr[:, :128], f2])
+    me = np.concatenate([me, m2])
+    rng = np.random.default_rng(32)
+    fr[:, 64:] = rng.integers(0, 256, size=(len(fr), 64), dtype=np.uint8)  # sentinels past the line
+    fresh_fastpath_state(fastpath, t)
+    dev = torch.device("cuda")
+    buf = torch.from_numpy(fr.reshape(-1).copy()).to(dev)
+    dme = torch.from_numpy(me.view(np.uint8)).to(dev)
+    v = torch.zeros(len(me) * 8, dtype=torch.uint8, device=dev)
+    q = fastpath.queue()  # private stream: order the uploads first
+    torch.cuda.synchronize()
+    q.submit(buf, buf, dme, v, len(me), in_stride=128, out_stride=128)
+    q.sync()
+    q.close()
+    out = buf.cpu().numpy().reshape(len(me), 128)
+    o_lines, o_v, _ = oracle.Oracle(t).process(fr, me)
+    np.testing.assert_array_equal(out[:, :64], o_lines)
+    np.testing.assert_array_equal(out[:, 32:], fr[:, 32:])
+    np.testing.assert_array_equal(v.cpu().numpy().view(abi.VERDICT_DT), o_v)
+
+
 def test_single_route_stream(fastpath):
     t = T.config_single_route()
     fr, me = S.stream(1 << 20, S.SEED_SINGLE, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
@@ -157,6 +187,39 @@ def test_edge_registration(fastpath):
         assert L.gr_hip_edges_ip_input_nh_type(h, abi.NH_T["BLACKHOLE"], abi.EDGE["ip_blackhole"]) == 0
         assert L.gr_hip_edges_iface_mode(h, abi.IFACE_MODE["XC"], abi.EDGE["xconnect"]) == 0
         assert L.gr_hip_edges_iface_output_type(h, abi.IFACE_TYPE["BOND"], abi.EDGE["bond_output"]) == 0
+
+
+def test_edge_registration_ip6(fastpath):
+    """The IPv6 registration tables: ip6_input nh types (ip6_input.c:31),
+    ip6_output nh/iface types (ip6_output.c:27,38), and eth_input handing
+    0x86DD to the CPU instead of the device chain."""
+    t, _ = SC.corpus_topology()
+    fr, me, lab = SC.corpus_arrays()
+    run_gpu(fastpath, t, fr, me)
+    L, h = fastpath.lib, fastpath.h
+    o = oracle.Oracle(t)
+    sets = [("gr_hip_edges_ip6_input_nh_type", "ip6_input_nh_type", abi.NH_T["BLACKHOLE"], abi.EDGE_CHAIN),
+            ("gr_hip_edges_ip6_input_nh_type", "ip6_input_nh_type", abi.NH_T["REJECT"], abi.EDGE["ip6_blackhole"]),
+            ("gr_hip_edges_ip6_output_nh_type", "ip6_output_nh_type", abi.NH_T["SR6_OUTPUT"], abi.EDGE_CHAIN),
+            ("gr_hip_edges_ip6_output_iface_type", "ip6_output_iface_type", abi.IFACE_TYPE["VRF"],
+             abi.EDGE["port_output"])]
+    restore = [(fn, ofn, k, e) for (fn, ofn, k, _), e in zip(sets, [
+        abi.EDGE["ip6_blackhole"], abi.EDGE["ip6_error_dest_unreach"], abi.EDGE["sr6_output"], abi.EDGE["xvrf"]])]
+    try:
+        for fn, ofn, key, e in sets:
+            assert getattr(L, fn)(h, key, e) == 0
+            o.edge(ofn, key, e)
+        compare(o.process(fr, me), run_gpu(fastpath, t, fr, me), lab)
+        # IPv6 to the CPU from eth_input
+        assert L.gr_hip_edges_eth_type(h, 0xDD86, abi.EDGE["ip6_input"]) == 0
+        o.edge("eth_type", 0xDD86, abi.EDGE["ip6_input"])
+        g = run_gpu(fastpath, t, fr, me)
+        compare(o.process(fr, me), g, lab)
+        assert (g[1]["edge"] == abi.EDGE["ip6_input"]).sum() > 50
+    finally:
+        assert L.gr_hip_edges_eth_type(h, 0xDD86, abi.EDGE_CHAIN6) == 0
+        for fn, ofn, key, e in restore:
+            assert getattr(L, fn)(h, key, e) == 0
 
 
 def test_empty_and_ragged_batches(fastpath):

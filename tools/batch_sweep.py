@@ -25,7 +25,7 @@ def main():
 
     from grout_amd import synth as S
     from grout_amd import topology as T
-    from grout_amd.fwd import FastPath
+    from grout_amd.fwd import FastPath, shared_stream
 
     dev = torch.device("cuda", 0)
     topo = T.config_fullview()
@@ -39,7 +39,7 @@ def main():
     d_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
     d_out = torch.empty_like(d_in)
     d_v = torch.empty(nmax * 8, dtype=torch.uint8, device=dev)
-    q = fp.queue(torch.cuda.current_stream(dev).cuda_stream)
+    q = fp.queue(shared_stream(dev))
     kt = {(n, k): [] for n in sizes for k in kernels}
     wt = {(n, k): [] for n in sizes for k in kernels}
     for _ in range(args.rounds):

@@ -31,7 +31,7 @@ def main():
     from grout_amd import abi
     from grout_amd import synth as S
     from grout_amd import topology as T
-    from grout_amd.fwd import FastPath
+    from grout_amd.fwd import FastPath, shared_stream
 
     dev = torch.device("cuda", 0)
     if args.workload == "single64":
@@ -52,7 +52,7 @@ def main():
     d_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
     d_out = torch.empty_like(d_in)
     d_v = torch.empty(n * 8, dtype=torch.uint8, device=dev)
-    q = fp.queue(torch.cuda.current_stream(dev).cuda_stream)
+    q = fp.queue(shared_stream(dev))
     for _ in range(args.reps):
         q.submit(d_in, d_out, d_meta, d_v, n)
     torch.cuda.synchronize()
