@@ -99,12 +99,14 @@ def test_single_route_stream(fastpath):
     compare(o, run_gpu(fastpath, t, fr, me))
 
 
-def test_fullview_full_size(fastpath):
-    """BASELINE config 3 at full size: 16M x 64 B over the 1M-route FIB."""
+@pytest.mark.parametrize("inplace", [False, True])
+def test_fullview_full_size(fastpath, inplace):
+    """BASELINE config 3 at full size: 16M x 64 B over the 1M-route FIB,
+    into separate lines and in place (the bench's two placements)."""
     t = _fullview()
     fr, me = S.stream(1 << 24, S.SEED_FULLVIEW, routes=t.route_array())
     o = oracle.Oracle(t).process(fr, me)
-    g = run_gpu(fastpath, t, fr, me)
+    g = run_gpu(fastpath, t, fr, me, inplace=inplace)
     compare(o, g)
     assert (g[1]["edge"] == abi.EDGE["port_output"]).mean() > 0.99
 

@@ -16,7 +16,7 @@ stop_if_fatal() { # $1 = exit status, $2 = step
 	echo "$2 exit $s" | tee -a $OUT/steps.log
 }
 
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
 stop_if_fatal $? pytest_gpu
 tail -30 $OUT/pytest_gpu.log
 
