@@ -5,7 +5,7 @@ CC ?= gcc
 ARCH ?= gfx950
 # host code built here runs on the GPU box's host too: portable x86-64-v3
 CFLAGS_HOST = -O3 -march=x86-64-v3 -fPIC -Wall -Wextra -Wno-unused-parameter
-HIPFLAGS = -x hip --offload-arch=$(ARCH) -O3 -fPIC -Wall -Wno-unused-value -Wno-unused-result -std=c++17
+HIPFLAGS = -x hip --offload-arch=$(ARCH) -O3 -fPIC -Wall -Wno-unused-value -Wno-unused-result -std=c++17 $(EXTRA_HIPFLAGS)
 
 CSRC = grout_amd/csrc
 BUILD = build

@@ -541,7 +541,7 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->stats_on = 1;
 	c->wg_per_cu = 0;
 	c->fib16 = 1;
-	c->ring_cfg = 1; // 2 loaders, 1 storer, 5 compute waves, 8 slots
+	c->ring_cfg = 2; // 16 waves: 2 loaders, 2 storers, 12 compute, 16 slots
 	for (int v = 0; v < 4; v++)
 		c->occ_ring[v] = gr_fwd4_ring_occupancy(v, 0, 0);
 	c->occ_ring_nhf = 0;

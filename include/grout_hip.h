@@ -395,7 +395,7 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 
 // Tuning knobs, for measurements (A/B in one process). Keys:
 //   "ring"      geometry of the ring kernel (loaders / storers / slots /
-//               tiles in flight), 0..8; default 1
+//               tiles in flight), 0..8; default 2
 //   "stats"     1 = per-iface counters (default; grout always counts), 0 = off
 //   "nt"        1 = nontemporal loads / stores of the streamed data (default)
 //   "wg_per_cu" 0 = default grid (2 workgroups per CU, fewer if LDS

@@ -379,7 +379,7 @@ def test_ring_geometries(fastpath, cfg):
         n = 64 * 1000 + 17  # ragged last tile; some workgroups get one tile more than others
         compare(oracle.Oracle(tf).process(fr2[:n], me2[:n]), run_gpu(fastpath, tf, fr2[:n], me2[:n]))
     finally:
-        fastpath.tune("ring", 1)
+        fastpath.tune("ring", 2)  # the default geometry
         fastpath.tune("wg_per_cu", 0)
 
 

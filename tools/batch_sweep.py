@@ -18,7 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--rings", default="1")
+    ap.add_argument("--rings", default="2")
     ap.add_argument("--log2", default="10,12,14,16,18,20,22,24")
     args = ap.parse_args()
     import torch
