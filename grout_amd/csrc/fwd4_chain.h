@@ -215,6 +215,12 @@ __device__ __forceinline__ uint32_t chain_fib(const rxv &rx, uint32_t dst) {
 	if (rx.tbl24 == nullptr)
 		return 0;
 	const uint32_t ip = __builtin_bswap32(dst);
+	if (rx.flags & FWD4_RX_FIB24W2) {
+		uint32_t ent = gld(reinterpret_cast<const uint16_t *>(rx.tbl24) + (ip >> 8));
+		if (ent & 0x8000u)
+			ent = gld(reinterpret_cast<const uint16_t *>(rx.tbl8) + (size_t)(ent & 0x7fffu) * 256 + (ip & 0xff));
+		return ent;
+	}
 	if (rx.flags & FWD4_RX_FIB16) {
 		uint32_t ent = gld(rx.tbl24 + (ip >> 16));
 		if (ent & 0x80000000u) {

@@ -36,6 +36,8 @@ struct fwd4_edges {
 #define FWD4_RX_FIB16 0x08 // DIR-16-8-8 FIB: tbl24 points at top[65536] (u32,
                            // bit31 = chunk) followed by 2-byte /24 chunks;
                            // tbl8 has 2-byte entries (bit15 = tbl8 group)
+#define FWD4_RX_FIB24W2 0x10 // DIR24_8 with 2-byte entries: tbl24 points at
+                             // u16[2^24] (bit15 = tbl8 group), tbl8 as FIB16
 struct fwd4_rx {
 	uint16_t id; // 0: no such iface
 	uint8_t e_in; // iface_input edge: ADMIN_DOWN, mode edge or CHAIN (eth_input)

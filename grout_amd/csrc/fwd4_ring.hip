@@ -55,8 +55,7 @@ typedef ring_cfg<16, 2, 2, 16, 8> ring_cfg8;
 template <class C>
 struct ring_lds {
 	uint8_t lines[C::SLOTS][64 * 64]; // the tile's header lines (fwd4_chain.h image)
-	u2v meta[C::SLOTS][64]; // gr_hip_pkt_meta
-	u2v verdict[C::SLOTS][64];
+	u2v meta[C::SLOTS][64]; // gr_hip_pkt_meta in, then the lane's gr_hip_verdict out
 	uint32_t ready[C::SLOTS], done[C::SLOTS], free_[C::SLOTS];
 	uint32_t abort;
 };
@@ -186,7 +185,7 @@ __device__ void ring_storer(const fwd4_params &A, ring_lds<C> &L, uint32_t n_loc
 #pragma unroll
 		for (uint32_t q = 0; q < 4; q++)
 			o[q] = *reinterpret_cast<const u4v *>(&L.lines[s][(q * 16 + prow) * 64 + pslot]);
-		const u2v v = L.verdict[s][lane];
+		const u2v v = L.meta[s][lane];
 		// the registers hold the tile: hand the slot back before storing
 		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 		flag_set(&L.free_[s], k + 1);
@@ -256,7 +255,7 @@ __device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds<C> &L
 				chain6(P, R, lane, m, rx, r, data_len);
 			}
 		}
-		L.verdict[s][lane] = u2v{r.edge | (r.domain << 8) | (r.iface << 16), r.nh};
+		L.meta[s][lane] = u2v{r.edge | (r.domain << 8) | (r.iface << 16), r.nh};
 		flag_set(&L.done[s], k + 1);
 		if (STATS) {
 			const uint32_t len = m.pkt_len;

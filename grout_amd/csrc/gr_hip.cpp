@@ -47,6 +47,12 @@ constexpr uint32_t N_TIMED = 64;
 constexpr uint32_t HOST_SLOTS = 3;
 constexpr uint32_t HOST_CHUNK = 1u << 18; // packets per host-mode chunk
 
+// Device FIB formats (gr_hip_tune "fib_format"); the 2-byte ones apply while
+// every nexthop slot and tbl8 group index fits 15 bits, else FIB_FMT_24.
+#define FIB_FMT_24 0 // DIR24_8, 4-byte entries (fib4.h encoding)
+#define FIB_FMT_16_8_8 1 // DIR-16-8-8, 2-byte entries
+#define FIB_FMT_24_W2 2 // DIR24_8, 2-byte entries
+
 struct vrf_fib {
 	gr_fib4 *rib = nullptr;
 	uint32_t *d24 = nullptr; // 4-byte entries (fib4.h encoding)
@@ -56,10 +62,12 @@ struct vrf_fib {
 	// chunks of 256 2-byte /24 entries for the non-uniform /16s only.
 	uint32_t *d16 = nullptr; // top, followed by the chunks
 	uint16_t *d8_16 = nullptr;
+	// DIR24_8 with 2-byte entries (bit15 = tbl8 group), same condition
+	uint16_t *d24_16 = nullptr;
 	std::vector<int32_t> chunk_of; // per /16: chunk index or -1
 	std::vector<uint32_t> chunk_free; // free chunk indexes (stack)
 	uint32_t n_chunks = 0; // chunks in use
-	bool fmt16 = false; // format on the device
+	int fmt = FIB_FMT_24; // format on the device
 	uint32_t max_slot = 0; // highest nexthop slot ever routed (never decreases)
 	uint32_t num_tbl8 = 0;
 	bool uploaded = false; // tables uploaded at least once
@@ -67,11 +75,11 @@ struct vrf_fib {
 	void reset4() { // forget the IPv4 state only
 		rib = nullptr;
 		d24 = d8 = d16 = nullptr;
-		d8_16 = nullptr;
+		d8_16 = d24_16 = nullptr;
 		chunk_of.clear();
 		chunk_free.clear();
 		n_chunks = 0;
-		fmt16 = false;
+		fmt = FIB_FMT_24;
 		max_slot = 0;
 		num_tbl8 = 0;
 		uploaded = false;
@@ -142,7 +150,7 @@ struct gr_hip_ctx {
 	int nt; // FWD4_V_NT
 	int stats_on;
 	int wg_per_cu; // 0 = one tile per workgroup, N = persistent N per CU
-	int fib16; // allow the 2-byte FIB format
+	int fib_fmt; // FIB format when 2-byte entries fit (FIB_FMT_*)
 	int ring_cfg; // ring geometry (fwd4_ring.hip ring_cfgN)
 	int occ_ring[4]; // at occ_ring_nhf staged fast adjacencies, geometry occ_ring_cfg
 	uint32_t occ_ring_nhf;
@@ -200,10 +208,14 @@ static fwd4_rx make_rx(const gr_hip_ctx *c, uint32_t id) {
 	if (vrf != nullptr && vrf->type == GR_HIP_IFACE_TYPE_VRF && c->vrfs[i->vrf_id].rib != nullptr
 	    && c->vrfs[i->vrf_id].uploaded) {
 		const vrf_fib &v = c->vrfs[i->vrf_id];
-		if (v.fmt16) {
+		if (v.fmt == FIB_FMT_16_8_8) {
 			r.tbl24 = v.d16;
 			r.tbl8 = reinterpret_cast<const uint32_t *>(v.d8_16);
 			r.flags |= FWD4_RX_FIB16;
+		} else if (v.fmt == FIB_FMT_24_W2) {
+			r.tbl24 = reinterpret_cast<const uint32_t *>(v.d24_16);
+			r.tbl8 = reinterpret_cast<const uint32_t *>(v.d8_16);
+			r.flags |= FWD4_RX_FIB24W2;
 		} else {
 			r.tbl24 = v.d24;
 			r.tbl8 = v.d8;
@@ -540,7 +552,7 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->nt = FWD4_V_NT; // measured faster on every kernel
 	c->stats_on = 1;
 	c->wg_per_cu = 0;
-	c->fib16 = 1;
+	c->fib_fmt = FIB_FMT_24_W2;
 	c->ring_cfg = 2; // 16 waves: 2 loaders, 2 storers, 12 compute, 16 slots
 	for (int v = 0; v < 4; v++)
 		c->occ_ring[v] = gr_fwd4_ring_occupancy(v, 0, 0);
@@ -569,6 +581,7 @@ extern "C" int gr_hip_fini(gr_hip_ctx_t *c) {
 		hipFree(v.d8);
 		hipFree(v.d16);
 		hipFree(v.d8_16);
+		hipFree(v.d24_16);
 		gr_fib6_free(v.rib6);
 		hipFree(v.d6);
 	}
@@ -813,6 +826,7 @@ extern "C" int gr_hip_fib4_destroy(gr_hip_ctx_t *c, uint16_t vrf) {
 	hipFree(v.d8);
 	hipFree(v.d16);
 	hipFree(v.d8_16);
+	hipFree(v.d24_16);
 	gr_fib4_free(v.rib);
 	v.reset4();
 	return 0;
@@ -880,8 +894,9 @@ extern "C" int gr_hip_fib4_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib == nullptr)
 		return -ENONET;
-	const bool want16 = c->fib16 && v.max_slot <= 0x7fff && v.num_tbl8 <= 0x8000;
-	const bool full = !v.uploaded || want16 != v.fmt16;
+	const bool fits16 = v.max_slot <= 0x7fff && v.num_tbl8 <= 0x8000;
+	const int want = fits16 ? c->fib_fmt : FIB_FMT_24;
+	const bool full = !v.uploaded || want != v.fmt;
 	uint32_t lo, hi;
 	gr_fib4_dirty_tbl24(v.rib, &lo, &hi);
 	std::vector<uint32_t> gs(v.num_tbl8);
@@ -903,13 +918,34 @@ extern "C" int gr_hip_fib4_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 		return r;
 	const uint32_t *t24 = gr_fib4_tbl24(v.rib);
 	const uint32_t *t8 = gr_fib4_tbl8(v.rib);
-	if (want16) {
+	if (want != FIB_FMT_24 && v.d8_16 == nullptr) {
+		HCK(hipStreamSynchronize(c->ctl));
+		HCK(hipMalloc(&v.d8_16, sizeof(uint16_t) * 256 * (size_t)v.num_tbl8));
+	}
+	if (want == FIB_FMT_24_W2) {
+		if (v.d24_16 == nullptr) {
+			HCK(hipStreamSynchronize(c->ctl));
+			HCK(hipMalloc(&v.d24_16, sizeof(uint16_t) * GR_FIB4_TBL24_ENTRIES));
+		}
+		std::vector<uint16_t> h24(hi > lo ? hi - lo : 0);
+		for (uint32_t i = lo; i < hi; i++)
+			h24[i - lo] = to16(t24[i]);
+		std::vector<uint16_t> h8((size_t)v.num_tbl8 * 256);
+		for (uint32_t g : gs)
+			for (uint32_t k = 0; k < 256; k++)
+				h8[(size_t)g * 256 + k] = to16(t8[(size_t)g * 256 + k]);
+		if (hi > lo)
+			r = h2d(c, v.d24_16 + lo, h24.data(), h24.size() * sizeof(uint16_t));
+		if (r == 0)
+			r = upload_groups<uint16_t>(c, v.d8_16, h8.data(), gs);
+		if (r == 0)
+			r = ctl_sync(c); // the staging vectors go out of scope
+	} else if (want == FIB_FMT_16_8_8) {
 		const size_t top_n = 65536, chunk_n = 256;
 		if (v.d16 == nullptr) {
 			HCK(hipStreamSynchronize(c->ctl));
 			// top + the worst case of one chunk per /16
 			HCK(hipMalloc(&v.d16, sizeof(uint32_t) * top_n + sizeof(uint16_t) * chunk_n * top_n));
-			HCK(hipMalloc(&v.d8_16, sizeof(uint16_t) * 256 * (size_t)v.num_tbl8));
 		}
 		if (full || v.chunk_of.empty()) {
 			v.chunk_of.assign(top_n, -1);
@@ -983,7 +1019,7 @@ extern "C" int gr_hip_fib4_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 		return r;
 	gr_fib4_dirty_clear(v.rib);
 	bool repoint = full;
-	v.fmt16 = want16;
+	v.fmt = want;
 	v.uploaded = true;
 	if (repoint)
 		r = upload_views(c, true, 0, 0, false);
@@ -1013,8 +1049,9 @@ extern "C" int gr_hip_fib4_info(gr_hip_ctx_t *c, uint16_t vrf, uint32_t *n_route
 	if (tbl8_used)
 		*tbl8_used = gr_fib4_tbl8_used(v.rib);
 	if (bytes) // device bytes a lookup can touch
-		*bytes = v.fmt16 ? 4ull * 65536 + 512ull * v.n_chunks + 512ull * v.num_tbl8
-				 : 4ull * GR_FIB4_TBL24_ENTRIES + 1024ull * v.num_tbl8;
+		*bytes = v.fmt == FIB_FMT_16_8_8 ? 4ull * 65536 + 512ull * v.n_chunks + 512ull * v.num_tbl8
+			 : v.fmt == FIB_FMT_24_W2 ? 2ull * GR_FIB4_TBL24_ENTRIES + 512ull * v.num_tbl8
+						  : 4ull * GR_FIB4_TBL24_ENTRIES + 1024ull * v.num_tbl8;
 	return 0;
 }
 
@@ -1306,8 +1343,12 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < 0 || value > 32)
 			return -EINVAL;
 		c->wg_per_cu = value;
-	} else if (strcmp(key, "fib16") == 0) { // takes effect at the next commit
-		c->fib16 = value != 0;
+	} else if (strcmp(key, "fib_format") == 0) { // takes effect at the next commit
+		if (value < FIB_FMT_24 || value > FIB_FMT_24_W2)
+			return -EINVAL;
+		c->fib_fmt = value;
+	} else if (strcmp(key, "fib16") == 0) { // older key: 0 = 4-byte DIR24_8, else DIR-16-8-8
+		c->fib_fmt = value ? FIB_FMT_16_8_8 : FIB_FMT_24;
 	} else if (strcmp(key, "ring") == 0) { // ring geometry, fwd4_ring.hip ring_cfgN
 		if (value < 0 || value >= gr_fwd4_ring_ncfg())
 			return -EINVAL;

@@ -400,8 +400,11 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //   "nt"        1 = nontemporal loads / stores of the streamed data (default)
 //   "wg_per_cu" 0 = default grid (2 workgroups per CU, fewer if LDS
 //               limits), N = N workgroups per CU
-//   "fib16"     1 = 2-byte FIB entries when slots fit 15 bits (default),
-//               0 = always 4-byte; applies from the next gr_hip_fib4_commit
+//   "fib_format" device FIB layout while every nexthop slot and tbl8 group
+//               fits 15 bits: 2 = DIR24_8 with 2-byte entries (default),
+//               1 = DIR-16-8-8 with 2-byte entries, 0 = DIR24_8 with 4-byte
+//               entries (always used when 15 bits do not fit); applies from
+//               the next gr_hip_fib4_commit ("fib16": 1 -> 1, 0 -> 0)
 //   "occupancy" (read) resident workgroups per CU of the current variant
 // Returns 0 (or the value read), -EINVAL, or -ENOENT for an unknown key.
 int gr_hip_tune(gr_hip_ctx_t *, const char *key, int value);

@@ -139,10 +139,14 @@ def test_host_memory_path(fastpath):
     compare(o, (lines, v, st))
 
 
-def test_live_fib_updates(fastpath):
-    """Routes added / replaced / deleted after the first commit."""
+@pytest.mark.parametrize("fmt", [2, 1, 0])
+def test_live_fib_updates(fastpath, fmt):
+    """Routes added / replaced / deleted after the first commit, in every
+    device FIB format (incremental uploads of the dirty ranges)."""
     t, nh = SC.corpus_topology()
     fr, me, lab = SC.corpus_arrays()
+    fastpath.tune("fib_format", fmt)
+    fresh_fastpath_state(fastpath, T.config_single_route())  # force a reload in this format
     run_gpu(fastpath, t, fr, me)  # loads t
     changes = [("add", "200.1.0.0/16", nh["fwd"]), ("add", "16.1.0.0/17", nh["fwd2"]),
                ("del", "10.90.1.7/32", None), ("add", "10.66.1.0/24", nh["fwd"]),
@@ -165,6 +169,7 @@ def test_live_fib_updates(fastpath):
     # control-plane lookup agrees too
     for d in ["200.1.2.3", "16.1.0.1", "16.1.200.1", "10.90.1.7", "10.66.1.9", "1.2.3.4"]:
         assert fastpath.fib_lookup(1, T.ip4(d)) == o.lpm(1, T.ip4(d), "dir24")
+    fastpath.tune("fib_format", 2)
     fresh_fastpath_state(fastpath, T.config_single_route())  # drop the modified state
 
 
@@ -258,11 +263,13 @@ def test_kernel_timing_api(fastpath):
     q.close()
 
 
-@pytest.mark.parametrize("nt,stats,wg,fib16", [(1, 1, 0, 1), (0, 0, 1, 1), (1, 0, 2, 0), (0, 1, 0, 0), (1, 1, 3, 0)])
-def test_kernel_variants(fastpath, nt, stats, wg, fib16):
+@pytest.mark.parametrize("nt,stats,wg,fmt", [(1, 1, 0, 1), (0, 0, 1, 1), (1, 0, 2, 0), (0, 1, 0, 0), (1, 1, 3, 0),
+                                            (0, 1, 1, 2), (1, 0, 0, 2)])
+def test_kernel_variants(fastpath, nt, stats, wg, fmt):
     """Every tuning variant (gr_hip_tune) forwards bit-exact: nontemporal
     streams, counters, grid (wg_per_cu 1-3: every workgroup walks its ring
-    many times round), FIB entry size."""
+    many times round), FIB format (0 DIR24_8 4-byte, 1 DIR-16-8-8 2-byte,
+    2 DIR24_8 2-byte)."""
     t, _ = SC.corpus_topology()
     fr, me, lab = SC.corpus_arrays()
     tf = _fullview()
@@ -272,7 +279,7 @@ def test_kernel_variants(fastpath, nt, stats, wg, fib16):
     fastpath.tune("nt", nt)
     fastpath.tune("stats", stats)
     fastpath.tune("wg_per_cu", wg)
-    fastpath.tune("fib16", fib16)
+    fastpath.tune("fib_format", fmt)
     try:
         fresh_fastpath_state(fastpath, T.config_single_route())  # force a reload (commit)
         g = run_gpu(fastpath, t, fr, me)
@@ -285,12 +292,14 @@ def test_kernel_variants(fastpath, nt, stats, wg, fib16):
         compare(o2 if stats else (o2[0], o2[1], g2[2]), g2)
         info = fastpath.fib_info(1)
         n8 = max(256, 1_000_010 // 500)
-        if fib16:  # DIR-16-8-8: only the non-uniform /16s get a chunk
+        if fmt == 1:  # DIR-16-8-8: only the non-uniform /16s get a chunk
             assert info["dev_bytes"] < 4 * (1 << 20)
+        elif fmt == 2:
+            assert info["dev_bytes"] == 2 * (1 << 24) + 512 * n8
         else:
             assert info["dev_bytes"] == 4 * (1 << 24) + 1024 * n8
     finally:
-        for k, v in [("nt", 1), ("stats", 1), ("wg_per_cu", 0), ("fib16", 1)]:
+        for k, v in [("nt", 1), ("stats", 1), ("wg_per_cu", 0), ("fib_format", 2)]:
             fastpath.tune(k, v)
         fresh_fastpath_state(fastpath, T.config_single_route())
 

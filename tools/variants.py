@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--workload", default="fullview64", choices=["fullview64", "single64"])
     ap.add_argument("--nt", default="0,1")
     ap.add_argument("--wg", default="0,6")
-    ap.add_argument("--fib16", default="1,0")
+    ap.add_argument("--fib16", default="2,1,0", help="gr_hip_tune fib_format values")
     ap.add_argument("--stats", default="1")
     ap.add_argument("--ring", default="1", help="ring geometries (fwd4_ring.hip ring_cfgN)")
     ap.add_argument("--place", default="out", help="out = separate lines; in = in place")
@@ -62,7 +62,7 @@ def main():
         for v in variants:
             f16, st, nt, wg, ring, place = v
             fp.tune("ring", ring)
-            fp.tune("fib16", f16)
+            fp.tune("fib_format", f16)
             fp.fib_commit(T.VRF_MAIN)  # re-uploads when the format changes
             fp.tune("stats", st)
             fp.tune("nt", nt)
