@@ -23,7 +23,10 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-B_PKT = 64 + 8 + 4 + 64 + 8  # algorithmic HBM bytes per packet
+# algorithmic HBM bytes per packet: line in, metadata in, one
+# FIB entry (2 or 4 bytes by device format), line out, verdict out
+def b_pkt(fib_entry_bytes):
+    return 64 + 8 + fib_entry_bytes + 64 + 8
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
 
 
@@ -121,6 +124,11 @@ def main():
     fwd_frac = float(edges[abi.EDGE["port_output"]]) / n
     value = rep.aggregate_mpps(n, args.steps, tmax)
     avg_kernel_s = kern_ms / max(kcount, 1) / 1e3
+    if args.workload == "fullview6":
+        entry = 4  # fib6.h trie entries
+    else:
+        entry = 4 if fp.tune("fib_format_of", T.VRF_MAIN) == 0 else 2
+    B_PKT = b_pkt(entry)
     achieved = n * B_PKT / avg_kernel_s / 1e9
 
     traffic = None
@@ -128,7 +136,7 @@ def main():
     if os.path.exists(tf):
         try:
             pm = json.load(open(tf))
-            if pm.get("workload") == args.workload and pm.get("batch") == n:
+            if pm.get("workload") == args.workload and pm.get("batch") == n and pm.get("bytes_per_pkt") == B_PKT:
                 traffic = pm.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None

@@ -1347,6 +1347,11 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < FIB_FMT_24 || value > FIB_FMT_24_W2)
 			return -EINVAL;
 		c->fib_fmt = value;
+	} else if (strcmp(key, "fib_format_of") == 0) { // read: the format VRF `value` is on the device in
+		if (value <= 0 || (uint32_t)value >= c->max_ifaces || c->vrfs[value].rib == nullptr
+		    || !c->vrfs[value].uploaded)
+			return -ENONET;
+		return c->vrfs[value].fmt;
 	} else if (strcmp(key, "fib16") == 0) { // older key: 0 = 4-byte DIR24_8, else DIR-16-8-8
 		c->fib_fmt = value ? FIB_FMT_16_8_8 : FIB_FMT_24;
 	} else if (strcmp(key, "ring") == 0) { // ring geometry, fwd4_ring.hip ring_cfgN

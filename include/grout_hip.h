@@ -405,6 +405,7 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               1 = DIR-16-8-8 with 2-byte entries, 0 = DIR24_8 with 4-byte
 //               entries (always used when 15 bits do not fit); applies from
 //               the next gr_hip_fib4_commit ("fib16": 1 -> 1, 0 -> 0)
+//   "fib_format_of" (read) the format VRF `value`'s FIB is on the device in
 //   "occupancy" (read) resident workgroups per CU of the current variant
 // Returns 0 (or the value read), -EINVAL, or -ENOENT for an unknown key.
 int gr_hip_tune(gr_hip_ctx_t *, const char *key, int value);

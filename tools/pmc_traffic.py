@@ -5,7 +5,10 @@ summaries (tools/pmc_summary.py output), corrected as MI355X_MICROARCH.md
 reads half the bytes of a wide streaming read (x2, checked against the 1 GiB
 calibration copy when the summary holds one).
 
-    python tools/pmc_traffic.py SUMMARY.json KERNEL WORKLOAD BATCH > profiles/pmc_traffic.json
+    python tools/pmc_traffic.py SUMMARY.json KERNEL WORKLOAD BATCH [BYTES_PER_PKT] > profiles/pmc_traffic.json
+
+BYTES_PER_PKT is the algorithmic figure (bench.py b_pkt: 146 with the default
+2-byte FIB entries, 148 with 4-byte ones).
 """
 import json
 import sys
@@ -13,6 +16,7 @@ import sys
 
 def main():
     summ, kernel, workload, batch = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+    bpp = int(sys.argv[5]) if len(sys.argv) > 5 else 146
     d = json.load(open(summ))
     k = d[kernel]
     fetch = 2 * k["FETCH_SIZE"] * 1024
@@ -21,7 +25,8 @@ def main():
         "workload": workload, "batch": batch, "kernel": kernel,
         "hbm_bytes_per_launch": int(fetch + write),
         "read_bytes_per_launch": int(fetch), "write_bytes_per_launch": int(write),
-        "algorithmic_bytes_per_launch": 148 * batch,
+        "bytes_per_pkt": bpp,
+        "algorithmic_bytes_per_launch": bpp * batch,
         "correction": "read = 2 x FETCH_SIZE KiB (gfx950 wide-read tally), write = WRITE_SIZE KiB",
     }
     # check of the x2: the corrected reads against the bytes the kernel must read
