@@ -96,7 +96,7 @@ NODE_NAMES = ["iface_input", "eth_input", "ip_input", "ip_forward", "ip_output",
               "ip6_input", "ip6_forward", "ip6_output"]
 NODE_COUNT = len(NODE_NAMES)
 NODE_STATS_DT = np.dtype([("packets", "<u8", NODE_COUNT), ("calls", "<u8", NODE_COUNT)])
-PTYPE_L3_IPV4, PTYPE_L3_IPV6 = 0x1, 0x10
+PTYPE_L3_IPV4, PTYPE_L3_IPV6 = 0x10, 0x40  # DPDK rte_mbuf_ptype.h
 
 
 class Batch(ctypes.Structure):

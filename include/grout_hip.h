@@ -462,8 +462,8 @@ struct gr_hip_mbuf {
 	uint32_t nh; // out: l3_mbuf_data.nh as a nexthop slot (0 = NULL)
 };
 
-#define GR_HIP_PTYPE_L3_IPV4 0x1 // RTE_PTYPE_L3_IPV4
-#define GR_HIP_PTYPE_L3_IPV6 0x10 // RTE_PTYPE_L3_IPV6
+#define GR_HIP_PTYPE_L3_IPV4 0x10 // RTE_PTYPE_L3_IPV4 (rte_mbuf_ptype.h)
+#define GR_HIP_PTYPE_L3_IPV6 0x40 // RTE_PTYPE_L3_IPV6 (rte_mbuf_ptype.h)
 
 // The nodes the fast path replaces, for per-node statistics.
 enum gr_hip_node {

@@ -966,7 +966,7 @@ static void node_ip_output(struct or_graph *g, struct or_mbuf **objs, uint16_t n
 			edge = GR_HIP_E_IP_ERROR_DEST_UNREACH;
 			goto next;
 		}
-		m->packet_type = 0x1; // RTE_PTYPE_L3_IPV4, :145
+		m->packet_type = 0x10; // RTE_PTYPE_L3_IPV4 (DPDK rte_mbuf_ptype.h), :145
 		const struct gr_hip_nh *h = &t->nh[m->l3_nh];
 		edge = t->out_nh_edges[h->type]; // :147-149
 		if (edge != NEXT)
@@ -1098,7 +1098,7 @@ static void node_ip6_output(struct or_graph *g, struct or_mbuf **objs, uint16_t 
 			edge = GR_HIP_E_IP6_ERROR_DEST_UNREACH;
 			goto next;
 		}
-		m->packet_type = 0x10; // RTE_PTYPE_L3_IPV6, :83
+		m->packet_type = 0x40; // RTE_PTYPE_L3_IPV6 (DPDK rte_mbuf_ptype.h), :83
 		const struct gr_hip_nh *h = &t->nh[m->l3_nh];
 		edge = t->out6_nh_edges[h->type]; // :85-87
 		if (edge != NEXT)
