@@ -12,9 +12,14 @@ BUILD = build
 LIB_HIP = grout_amd/libgrout_hip.so
 LIB_HOST = grout_amd/libgrout_host.so
 LIB_ORACLE = oracle/liboracle.so
+LIB_GRAPH = grout_amd/libgrout_graph.so
+GRAPH = grout_amd/graph
+GRAPH_SRC = $(GRAPH)/rte_graph_min.c $(GRAPH)/gr_datapath_min.c $(GRAPH)/gpu_fwd4_node.c $(GRAPH)/walk_harness.c \
+	$(GRAPH)/graph_selftest.c
+GRAPH_HDRS = $(GRAPH)/rte_graph_min.h $(GRAPH)/gr_datapath_min.h $(GRAPH)/gpu_fwd4_node.h include/grout_hip.h
 HDRS = include/grout_hip.h $(CSRC)/fib6.h $(CSRC)/fwd4_kernel.h $(CSRC)/fwd4_dev.h $(CSRC)/fwd4_chain.h $(CSRC)/fib4.h
 
-all: $(LIB_HIP) $(LIB_HOST) $(LIB_ORACLE)
+all: $(LIB_HIP) $(LIB_HOST) $(LIB_ORACLE) $(LIB_GRAPH)
 
 $(BUILD)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(BUILD)
@@ -45,7 +50,12 @@ $(LIB_HOST): $(CSRC)/fib4.c $(CSRC)/fib6.c $(CSRC)/synth.c $(CSRC)/fib4.h $(CSRC
 $(LIB_ORACLE): oracle/oracle.c oracle/oracle.h include/grout_hip.h
 	$(CC) $(CFLAGS_HOST) -pthread -shared -o $@ oracle/oracle.c
 
+# The fast path's grout node (C) on the rte_graph / grout stand-ins, with the
+# test harness graph; links the HIP library (found next to it at run time).
+$(LIB_GRAPH): $(GRAPH_SRC) $(GRAPH_HDRS) $(LIB_HIP)
+	$(CC) -std=gnu11 $(CFLAGS_HOST) -Iinclude -shared -o $@ $(GRAPH_SRC) -Lgrout_amd -lgrout_hip '-Wl,-rpath,$$ORIGIN'
+
 clean:
-	rm -rf $(BUILD) $(LIB_HIP) $(LIB_HOST) $(LIB_ORACLE)
+	rm -rf $(BUILD) $(LIB_HIP) $(LIB_HOST) $(LIB_ORACLE) $(LIB_GRAPH)
 
 .PHONY: all clean

@@ -25,11 +25,25 @@ class FastPath:
         self.max_nexthops = max_nexthops
         self.queues = []
 
+    @classmethod
+    def borrow(cls, handle, max_ifaces=1024, max_nexthops=1 << 17):
+        """Wrap a context created elsewhere (e.g. by the grout node's module,
+        gpu_fwd4_hip_ctx()) without owning it: close() leaves it alive."""
+        self = cls.__new__(cls)
+        self.lib = abi.hip()
+        self.h = ctypes.c_void_p(handle)
+        self.max_ifaces = max_ifaces
+        self.max_nexthops = max_nexthops
+        self.queues = []
+        self._borrowed = True
+        return self
+
     def close(self):
         if self.h:
             for q in self.queues:
                 q._h = None
-            self.lib.gr_hip_fini(self.h)
+            if not getattr(self, "_borrowed", False):
+                self.lib.gr_hip_fini(self.h)
             self.h = None
 
     def __del__(self):

@@ -39,24 +39,26 @@ def topo_for(name):
 _loaded = {}
 
 
-def fresh_fastpath_state(fp, topo):
-    """(Re)load topo into the shared FastPath: clear the old objects first."""
+def fresh_fastpath_state(fp, topo, state=None):
+    """(Re)load topo into the shared FastPath (or into `fp` with its own
+    `state` dict): clear the old objects first."""
+    st = _loaded if state is None else state
     key = id(topo)
-    if _loaded.get("key") == key:
+    if st.get("key") == key:
         return
-    _loaded.pop("topo", None)
-    _loaded.pop("key", None)
+    st.pop("topo", None)
+    st.pop("key", None)
     # wipe previous state: FIBs, ifaces, nexthops (popped first, so that one
     # failure does not cascade into every later test)
-    for vrf in _loaded.pop("fibs", []):
+    for vrf in st.pop("fibs", []):
         fp.fib_destroy(vrf)
-    for vrf in _loaded.pop("fibs6", []):
+    for vrf in st.pop("fibs6", []):
         fp.fib6_destroy(vrf)
-    for i in _loaded.pop("ifaces", []):
+    for i in st.pop("ifaces", []):
         fp.del_iface(int(i))
     fp.set_nexthops(np.zeros(fp.max_nexthops, dtype=abi.NH_DT), first=1)
     fp.load(topo)
-    _loaded.update(key=key, fibs=list(topo.fibs), fibs6=list(topo.fibs6), ifaces=list(topo.live_ifaces()["id"]),
+    st.update(key=key, fibs=list(topo.fibs), fibs6=list(topo.fibs6), ifaces=list(topo.live_ifaces()["id"]),
                    topo=topo)
 
 
