@@ -203,7 +203,8 @@ def main():
             "pkts": hn,
             "h2d_bytes_per_pkt": abi.LINE + 8,
             "d2h_bytes_per_pkt": abi.LINE + 8,
-            "note": "header lines + metadata from pinned host memory, chunked H2D/kernel/D2H on 3 streams",
+            "note": ("header lines + metadata in pinned host memory; the kernel reads and writes them over "
+                     "PCIe itself (host_direct), H2D and D2H concurrent"),
         }
 
     # ---- CPU baseline: the oracle restatement on this host's cores

@@ -405,14 +405,20 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               1 = DIR-16-8-8 with 2-byte entries, 0 = DIR24_8 with 4-byte
 //               entries (always used when 15 bits do not fit); applies from
 //               the next gr_hip_fib4_commit ("fib16": 1 -> 1, 0 -> 0)
+//   "host_direct" 1 = gr_hip_fwd4_host on pinned (hipHostMalloc'd or
+//               registered) buffers runs the kernel on them directly, its
+//               loads and stores crossing PCIe (default); 0 = always staged
+//               chunk copies (pageable buffers always take that path)
 //   "fib_format_of" (read) the format VRF `value`'s FIB is on the device in
 //   "occupancy" (read) resident workgroups per CU of the current variant
 // Returns 0 (or the value read), -EINVAL, or -ENOENT for an unknown key.
 int gr_hip_tune(gr_hip_ctx_t *, const char *key, int value);
 
-// Host-memory path (header-only staging): copy `n` 64-byte header lines and
-// metadata from host memory, run the kernel, copy lines and verdicts back.
-// Pinned staging inside the queue, double-buffered; completes before return.
+// Host-memory path (header-only staging): `n` 64-byte header lines and
+// metadata in host memory in, lines and verdicts back to host memory. On
+// pinned buffers the kernel reads and writes them over PCIe itself
+// ("host_direct"); otherwise chunks are copied through the queue's device
+// staging on 3 streams. Completes before return.
 int gr_hip_fwd4_host(
 	gr_hip_queue_t *,
 	const void *lines,

@@ -139,6 +139,33 @@ def test_host_memory_path(fastpath):
     compare(o, (lines, v, st))
 
 
+@pytest.mark.parametrize("direct", [0, 1])
+def test_host_memory_path_pinned(fastpath, direct):
+    """gr_hip_fwd4_host on pinned buffers: staged copies (direct 0) or the
+    kernel reading and writing host memory over PCIe itself (direct 1)."""
+    import torch
+    t = _fullview()
+    fresh_fastpath_state(fastpath, t)
+    fr, me = S.stream(300_017, S.SEED_IMIX + 1, routes=t.route_array(), imix=True, lines_only=True)
+    o = oracle.Oracle(t).process(fr, me, lines_only=True)
+    n = len(me)
+    h_in = torch.from_numpy(np.ascontiguousarray(fr).reshape(-1)).pin_memory()
+    h_me = torch.from_numpy(me.view(np.uint8)).pin_memory()
+    h_out = torch.zeros(n * abi.LINE, dtype=torch.uint8).pin_memory()
+    h_v = torch.zeros(n * 8, dtype=torch.uint8).pin_memory()
+    fastpath.tune("host_direct", direct)
+    try:
+        q = fastpath.queue()
+        q.stats(reset=True)
+        abi.check("gr_hip_fwd4_host", fastpath.lib.gr_hip_fwd4_host(q._h, h_in.data_ptr(), h_me.data_ptr(), n,
+                                                                    h_out.data_ptr(), h_v.data_ptr()))
+        st = q.stats(reset=True)
+        q.close()
+    finally:
+        fastpath.tune("host_direct", 1)
+    compare(o, (h_out.numpy().reshape(n, abi.LINE), h_v.numpy().view(abi.VERDICT_DT), st))
+
+
 @pytest.mark.parametrize("fmt", [2, 1, 0])
 def test_live_fib_updates(fastpath, fmt):
     """Routes added / replaced / deleted after the first commit, in every
