@@ -97,6 +97,7 @@ NODE_NAMES = ["iface_input", "eth_input", "ip_input", "ip_forward", "ip_output",
 NODE_COUNT = len(NODE_NAMES)
 NODE_STATS_DT = np.dtype([("packets", "<u8", NODE_COUNT), ("calls", "<u8", NODE_COUNT)])
 PTYPE_L3_IPV4, PTYPE_L3_IPV6 = 0x10, 0x40  # DPDK rte_mbuf_ptype.h
+BATCH_F_FRAME_PTRS = 0x2
 
 
 class Batch(ctypes.Structure):
@@ -169,6 +170,9 @@ HIP_API = {
     "gr_hip_dev_free": (_I, [_P, _P]),
     "gr_hip_memcpy_h2d": (_I, [_P, _P, _P, ctypes.c_size_t]),
     "gr_hip_memcpy_d2h": (_I, [_P, _P, _P, ctypes.c_size_t]),
+    "gr_hip_host_register": (_I, [_P, _P, ctypes.c_size_t]),
+    "gr_hip_host_unregister": (_I, [_P, _P]),
+    "gr_hip_host_dev_addr": (_I, [_P, _P, _P]),
     "gr_hip_edge_node": (_I, [_U8, _U32, _I]),
     "gr_hip_node_stage": (_I, [_P, _U32, _P, _P]),
     "gr_hip_node_apply": (_I, [_P, _U32, _P, _U32, _P, _P, _U32, _P, _U32, _U32, _P]),
@@ -207,7 +211,12 @@ def _bind(path, api, what):
     if not os.path.exists(path):
         raise ImportError(f"{what} not built: {path} missing (run `make` or __graft_entry__.build())")
     lib = ctypes.CDLL(path)
+    # GR_HIP_AB_OLD=1: an older build under A/B (tools/ab_libs.sh) may lack
+    # the newest entry points; everything else binds every symbol or fails
+    lenient = os.environ.get("GR_HIP_AB_OLD") == "1"
     for name, (res, args) in api.items():
+        if lenient and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

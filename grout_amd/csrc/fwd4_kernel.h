@@ -152,3 +152,4 @@ struct fwd4_params {
 // stores of the streamed data.
 #define FWD4_V_STATS 0x1
 #define FWD4_V_NT 0x2 // nontemporal loads and stores of the streamed data
+#define FWD4_V_PTRS 0x4 // A.in is an array of frame addresses (GR_HIP_BATCH_F_FRAME_PTRS)

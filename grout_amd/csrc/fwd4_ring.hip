@@ -52,10 +52,11 @@ typedef ring_cfg<16, 4, 2, 24, 3> ring_cfg7;
 typedef ring_cfg<16, 2, 2, 16, 8> ring_cfg8;
 #define RING_NCFG 9
 
-template <class C>
+template <class C, bool PTRS>
 struct ring_lds {
 	uint8_t lines[C::SLOTS][64 * 64]; // the tile's header lines (fwd4_chain.h image)
 	u2v meta[C::SLOTS][64]; // gr_hip_pkt_meta in, then the lane's gr_hip_verdict out
+	uint64_t ptrs[PTRS ? C::SLOTS : 1][64]; // GR_HIP_BATCH_F_FRAME_PTRS: the tile's frames
 	uint32_t ready[C::SLOTS], done[C::SLOTS], free_[C::SLOTS];
 	uint32_t abort;
 };
@@ -125,13 +126,33 @@ __device__ __forceinline__ bool flag_wait(L_t &L, const uint32_t *f, uint32_t wa
 	}
 }
 
-template <class C, bool NT>
-__device__ void ring_loader(const fwd4_params &A, ring_lds<C> &L, uint32_t n_local, uint32_t j, uint32_t lane) {
+// Frame pointers of tile t, one per lane (rows past the batch repeat its last
+// packet, so that every tile issues the same number of loads).
+__device__ __forceinline__ uint64_t load_ptr(const fwd4_params &A, uint32_t t, uint32_t lane) {
+	const uint32_t i = min(t * 64 + lane, A.n - 1);
+	return gld(reinterpret_cast<const uint64_t *>(A.in) + i);
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+	const uint32_t lo = __shfl((uint32_t)v, (int)src, 64), hi = __shfl((uint32_t)(v >> 32), (int)src, 64);
+	return ((uint64_t)hi << 32) | lo;
+}
+
+// Every tile issues exactly RING_GLDS_PER_TILE LDS-DMA loads (rows and
+// metadata past a ragged last tile repeat its last packet into rows nobody
+// reads), so that the counted vmcnt waits below stay exact. In PTRS mode a
+// loader also loads the next tile's frame pointers ahead (one more load per
+// tile, issued before the tile's DMA, which only makes the waits longer).
+template <class C, bool NT, bool PTRS>
+__device__ void ring_loader(const fwd4_params &A, ring_lds<C, PTRS> &L, uint32_t n_local, uint32_t j, uint32_t lane) {
 	const uint32_t G = gridDim.x;
 	const uint32_t prow = lane >> 2;
 	const uint32_t pchunk = (lane & 3) ^ ((lane >> 4) & 3); // chunk this lane lands in slot lane & 3
 	uint32_t pub = j; // oldest of this loader's tiles not yet published
 	bool ok = true;
+	uint64_t pnext = 0;
+	if (PTRS && j < n_local)
+		pnext = load_ptr(A, blockIdx.x + j * G, lane);
 	for (uint32_t k = j; k < n_local && ok; k += C::LOADERS) {
 		const uint32_t s = k % C::SLOTS;
 		if (k >= C::SLOTS && (int32_t)(flag_get(&L.free_[s]) - (k - C::SLOTS + 1)) < 0) {
@@ -144,20 +165,34 @@ __device__ void ring_loader(const fwd4_params &A, ring_lds<C> &L, uint32_t n_loc
 				break;
 		}
 		const uint32_t t = blockIdx.x + k * G;
-		const uint32_t base = t * 64, cnt = min(64u, A.n - base);
+		const uint32_t base = t * 64, last = min(64u, A.n - base) - 1;
+		uint64_t pk = 0;
+		if (PTRS) {
+			pk = pnext;
+			if (k + C::LOADERS < n_local)
+				pnext = load_ptr(A, blockIdx.x + (k + C::LOADERS) * G, lane);
+			if (k == j)
+				wait_vmcnt<0>();
+			else
+				wait_vmcnt<RING_GLDS_PER_TILE>(); // pk's load is older than the last tile's DMA
+			L.ptrs[s][lane] = pk; // for the storer and the compute waves
+		}
 		const uint32_t lb = lds_addr(L.lines[s]);
 #pragma unroll
 		for (uint32_t q = 0; q < 4; q++) {
-			const uint32_t r = q * 16 + prow;
-			if (r < cnt)
-				glds16<NT>(A.in + (size_t)(base + r) * A.in_stride + pchunk * 16, lb + q * 1024);
+			const uint32_t r = min(q * 16 + prow, last);
+			const uint8_t *src = PTRS ? reinterpret_cast<const uint8_t *>(shfl64(pk, r))
+						  : A.in + (size_t)(base + r) * A.in_stride;
+			glds16<NT>(src + pchunk * 16, lb + q * 1024);
 		}
 		const uint32_t mb = lds_addr(L.meta[s]);
 		const uint8_t *msrc = reinterpret_cast<const uint8_t *>(A.meta + base);
 #pragma unroll
-		for (uint32_t q = 0; q < 2; q++)
-			if (q * 32 + (lane >> 1) < cnt)
-				glds4<NT>(msrc + q * 256 + lane * 4, mb + q * 256);
+		for (uint32_t q = 0; q < 2; q++) {
+			// 4 bytes per lane: packet q * 32 + lane / 2, half lane & 1
+			const uint32_t pkt = min(q * 32 + (lane >> 1), last);
+			glds4<NT>(msrc + pkt * 8 + (lane & 1) * 4, mb + q * 256);
+		}
 		if (k - pub == (C::AHEAD - 1) * C::LOADERS) {
 			wait_vmcnt<C::VMCNT_AHEAD>();
 			flag_set(&L.ready[pub % C::SLOTS], pub + 1);
@@ -170,8 +205,8 @@ __device__ void ring_loader(const fwd4_params &A, ring_lds<C> &L, uint32_t n_loc
 			flag_set(&L.ready[pub % C::SLOTS], pub + 1);
 }
 
-template <class C, bool NT>
-__device__ void ring_storer(const fwd4_params &A, ring_lds<C> &L, uint32_t n_local, uint32_t j, uint32_t lane) {
+template <class C, bool NT, bool PTRS>
+__device__ void ring_storer(const fwd4_params &A, ring_lds<C, PTRS> &L, uint32_t n_local, uint32_t j, uint32_t lane) {
 	const uint32_t G = gridDim.x;
 	const uint32_t prow = lane >> 2, part = lane & 3;
 	const uint32_t pslot = (part ^ ((lane >> 4) & 3)) << 4;
@@ -186,6 +221,14 @@ __device__ void ring_storer(const fwd4_params &A, ring_lds<C> &L, uint32_t n_loc
 		for (uint32_t q = 0; q < 4; q++)
 			o[q] = *reinterpret_cast<const u4v *>(&L.lines[s][(q * 16 + prow) * 64 + pslot]);
 		const u2v v = L.meta[s][lane];
+		uint8_t *dst[4];
+#pragma unroll
+		for (uint32_t q = 0; q < 4; q++) {
+			const uint32_t r = q * 16 + prow;
+			// in place at each frame (PTRS without out lines), else the lines
+			dst[q] = PTRS && A.out == nullptr ? reinterpret_cast<uint8_t *>(L.ptrs[s][r])
+							  : A.out + (size_t)(base + r) * A.out_stride;
+		}
 		// the registers hold the tile: hand the slot back before storing
 		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 		flag_set(&L.free_[s], k + 1);
@@ -193,7 +236,7 @@ __device__ void ring_storer(const fwd4_params &A, ring_lds<C> &L, uint32_t n_loc
 		for (uint32_t q = 0; q < 4; q++) {
 			const uint32_t r = q * 16 + prow;
 			if (r < cnt)
-				st16<NT>(A.out + (size_t)(base + r) * A.out_stride + part * 16, o[q]);
+				st16<NT>(dst[q] + part * 16, o[q]);
 		}
 		if (lane < cnt) {
 			u2v *vp = reinterpret_cast<u2v *>(A.verdicts + base + lane);
@@ -205,8 +248,8 @@ __device__ void ring_storer(const fwd4_params &A, ring_lds<C> &L, uint32_t n_loc
 	}
 }
 
-template <class C, bool STATS>
-__device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds<C> &L, stat_slot *slots,
+template <class C, bool STATS, bool PTRS>
+__device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds<C, PTRS> &L, stat_slot *slots,
 			     const uint4 *nhf_lds, uint32_t n_local, uint32_t c, uint32_t lane) {
 	const uint32_t G = gridDim.x;
 	for (uint32_t k = c; k < n_local; k += C::COMPUTE) {
@@ -235,7 +278,8 @@ __device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds<C> &L
 		result r = {GR_HIP_E_PUNT, 0, m.iface, 0, 0, 0, 0, 0};
 		if (live) {
 			uint32_t dst = 0, data_len = 0;
-			const uint8_t *frame = A.in + (size_t)(base + lane) * A.in_stride;
+			const uint8_t *frame = PTRS ? reinterpret_cast<const uint8_t *>(L.ptrs[s][lane])
+						    : A.in + (size_t)(base + lane) * A.in_stride;
 			const int head = chain_head(P, R, lane, m, rx, r, dst, data_len, frame);
 			if (head == HEAD_IP4) {
 				const uint32_t slot = chain_fib(rx, dst);
@@ -267,9 +311,9 @@ __device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds<C> &L
 	}
 }
 
-template <class C, bool STATS, bool NT>
+template <class C, bool STATS, bool NT, bool PTRS = false>
 __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params A) {
-	__shared__ __attribute__((aligned(16))) ring_lds<C> L;
+	__shared__ __attribute__((aligned(16))) ring_lds<C, PTRS> L;
 	__shared__ stat_slot slots[FWD4_STAT_SLOTS];
 	__shared__ fwd4_edges edges;
 	extern __shared__ __attribute__((aligned(16))) uint4 nhf_lds[]; // [A.nhf_lds]: slots 1..
@@ -301,12 +345,12 @@ __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params 
 	const uint32_t n_tiles = (A.n + 63) >> 6;
 	const uint32_t n_local = blockIdx.x < n_tiles ? (n_tiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
 	if (wv < C::LOADERS) {
-		ring_loader<C, NT>(A, L, n_local, wv, lane);
+		ring_loader<C, NT, PTRS>(A, L, n_local, wv, lane);
 	} else if (wv < C::LOADERS + C::STORERS) {
-		ring_storer<C, NT>(A, L, n_local, wv - C::LOADERS, lane);
+		ring_storer<C, NT, PTRS>(A, L, n_local, wv - C::LOADERS, lane);
 	} else {
 		kctx P = make_kctx(A, &edges);
-		ring_compute<C, STATS>(A, P, L, slots, nhf_lds, n_local, wv - C::LOADERS - C::STORERS, lane);
+		ring_compute<C, STATS, PTRS>(A, P, L, slots, nhf_lds, n_local, wv - C::LOADERS - C::STORERS, lane);
 	}
 
 	if (STATS) {
@@ -331,10 +375,20 @@ static const ring_entry ring_kernels[RING_NCFG] = {
 	RING_ENTRY(ring_cfg6), RING_ENTRY(ring_cfg7), RING_ENTRY(ring_cfg8),
 };
 
-// variant: FWD4_V_STATS | FWD4_V_NT; cfg: ring geometry. A->nhf_lds fast
-// adjacencies are staged in dynamic LDS.
+// Frame-pointer batches (GR_HIP_BATCH_F_FRAME_PTRS) run on geometry 2, the
+// default, only.
+#define RING_PTRS_CFG 2
+typedef ring_cfg2 ring_cfg_ptrs;
+static const ring_entry ring_ptrs_kernel = {
+	{gr_fwd4_ring<ring_cfg_ptrs, false, false, true>, gr_fwd4_ring<ring_cfg_ptrs, true, false, true>,
+	 gr_fwd4_ring<ring_cfg_ptrs, false, true, true>, gr_fwd4_ring<ring_cfg_ptrs, true, true, true>},
+	ring_cfg_ptrs::WAVES * 64};
+
+// variant: FWD4_V_STATS | FWD4_V_NT | FWD4_V_PTRS; cfg: ring geometry
+// (ignored for FWD4_V_PTRS). A->nhf_lds fast adjacencies are staged in
+// dynamic LDS.
 extern "C" hipError_t gr_fwd4_ring_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant, int cfg) {
-	const ring_entry &e = ring_kernels[(unsigned)cfg % RING_NCFG];
+	const ring_entry &e = (variant & FWD4_V_PTRS) ? ring_ptrs_kernel : ring_kernels[(unsigned)cfg % RING_NCFG];
 	hipLaunchKernelGGL(e.fn[variant & 3], dim3(grid), dim3(e.threads), A->nhf_lds * sizeof(fwd4_nhf), s, *A);
 	return hipGetLastError();
 }
@@ -348,7 +402,7 @@ extern "C" int gr_fwd4_ring_ncfg(void) {
 }
 
 extern "C" int gr_fwd4_ring_occupancy(int variant, int cfg, uint32_t nhf_lds) {
-	const ring_entry &e = ring_kernels[(unsigned)cfg % RING_NCFG];
+	const ring_entry &e = (variant & FWD4_V_PTRS) ? ring_ptrs_kernel : ring_kernels[(unsigned)cfg % RING_NCFG];
 	int b = 0;
 	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, e.fn[variant & 3], (int)e.threads, nhf_lds * sizeof(fwd4_nhf))
 	    != hipSuccess) {

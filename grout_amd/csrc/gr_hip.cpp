@@ -117,6 +117,12 @@ struct gr_hip_queue {
 	gr_hip_verdict *node_v;
 };
 
+struct host_range { // gr_hip_host_register
+	uintptr_t host, dev;
+	size_t len;
+	bool ours; // registered by us (hipHostUnregister on the way out)
+};
+
 struct gr_hip_ctx {
 	int dev;
 	uint32_t max_ifaces, max_nh;
@@ -153,7 +159,9 @@ struct gr_hip_ctx {
 	int fib_fmt; // FIB format when 2-byte entries fit (FIB_FMT_*)
 	int ring_cfg; // ring geometry (fwd4_ring.hip ring_cfgN)
 	int host_direct; // host path: the kernel reads / writes pinned host memory itself
-	int occ_ring[4]; // at occ_ring_nhf staged fast adjacencies, geometry occ_ring_cfg
+	int node_ptrs; // node path: frames in registered memory are handed over by address
+	std::vector<host_range> hregs; // registered host memory, by host address
+	int occ_ring[8]; // by variant, at occ_ring_nhf staged fast adjacencies, geometry occ_ring_cfg
 	uint32_t occ_ring_nhf;
 	int occ_ring_cfg;
 };
@@ -556,7 +564,8 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->fib_fmt = FIB_FMT_24_W2;
 	c->ring_cfg = 2; // 16 waves: 2 loaders, 2 storers, 12 compute, 16 slots
 	c->host_direct = 1; // measured 1.9x the staged copies
-	for (int v = 0; v < 4; v++)
+	c->node_ptrs = 1;
+	for (int v = 0; v < 8; v++)
 		c->occ_ring[v] = gr_fwd4_ring_occupancy(v, 0, 0);
 	c->occ_ring_nhf = 0;
 	c->occ_ring_cfg = 0;
@@ -577,6 +586,10 @@ extern "C" int gr_hip_fini(gr_hip_ctx_t *c) {
 	hipSetDevice(c->dev);
 	while (!c->queues.empty())
 		gr_hip_queue_destroy(c->queues.back());
+	for (const host_range &r : c->hregs)
+		if (r.ours)
+			hipHostUnregister(reinterpret_cast<void *>(r.host));
+	c->hregs.clear();
 	for (vrf_fib &v : c->vrfs) {
 		gr_fib4_free(v.rib);
 		hipFree(v.d24);
@@ -1317,16 +1330,18 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	A.n = b->n;
 	A.in_stride = b->in_stride;
 	A.out_stride = b->out_stride;
-	A.readable = (b->flags & GR_HIP_BATCH_F_LINES_ONLY) ? GR_HIP_LINE : b->in_stride;
+	A.readable = (b->flags & GR_HIP_BATCH_F_LINES_ONLY) ? GR_HIP_LINE
+		: (b->flags & GR_HIP_BATCH_F_FRAME_PTRS)    ? UINT32_MAX // whole frames
+							    : b->in_stride;
 	A.nhf_lds = 0;
 	int stats = c->stats_on && q->d_stats != nullptr;
 	uint32_t slot = (uint32_t)(q->n_launch % N_TIMED);
 	// persistent: one resident round of workgroups, each walking 64-packet tiles
-	int variant = (stats ? FWD4_V_STATS : 0) | c->nt;
+	int variant = (stats ? FWD4_V_STATS : 0) | c->nt | ((b->flags & GR_HIP_BATCH_F_FRAME_PTRS) ? FWD4_V_PTRS : 0);
 	uint32_t tiles = (b->n + 63) / 64;
 	A.nhf_lds = c->nh_hi < gr_fwd4_ring_nhf_max() ? c->nh_hi : gr_fwd4_ring_nhf_max();
 	if (A.nhf_lds != c->occ_ring_nhf || c->ring_cfg != c->occ_ring_cfg) {
-		for (int v = 0; v < 4; v++)
+		for (int v = 0; v < 8; v++)
 			c->occ_ring[v] = gr_fwd4_ring_occupancy(v, c->ring_cfg, A.nhf_lds);
 		c->occ_ring_nhf = A.nhf_lds;
 		c->occ_ring_cfg = c->ring_cfg;
@@ -1363,6 +1378,8 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < FIB_FMT_24 || value > FIB_FMT_24_W2)
 			return -EINVAL;
 		c->fib_fmt = value;
+	} else if (strcmp(key, "node_ptrs") == 0) {
+		c->node_ptrs = value != 0;
 	} else if (strcmp(key, "host_direct") == 0) {
 		c->host_direct = value != 0;
 	} else if (strcmp(key, "fib_format_of") == 0) { // read: the format VRF `value` is on the device in
@@ -1389,12 +1406,21 @@ static int batch_ok(const gr_hip_batch *b) {
 		return -EINVAL;
 	if (b->n == 0)
 		return 0;
-	if (!b->in_frames || !b->out_lines || !b->meta || !b->verdicts)
-		return -EINVAL;
-	if (b->in_stride < GR_HIP_LINE || b->out_stride < GR_HIP_LINE || (b->in_stride & 15)
-	    || (b->out_stride & 15) || ((uintptr_t)b->in_frames & 15) || ((uintptr_t)b->out_lines & 15)
-	    || ((uintptr_t)b->meta & 7) || ((uintptr_t)b->verdicts & 7))
-		return -EINVAL;
+	if (b->flags & GR_HIP_BATCH_F_FRAME_PTRS) {
+		// in_frames: n frame addresses; out_lines NULL = rewrite each frame in place
+		if (!b->in_frames || !b->meta || !b->verdicts || ((uintptr_t)b->in_frames & 7)
+		    || (b->out_lines && (b->out_stride < GR_HIP_LINE || (b->out_stride & 15)
+					 || ((uintptr_t)b->out_lines & 15)))
+		    || ((uintptr_t)b->meta & 7) || ((uintptr_t)b->verdicts & 7))
+			return -EINVAL;
+	} else {
+		if (!b->in_frames || !b->out_lines || !b->meta || !b->verdicts)
+			return -EINVAL;
+		if (b->in_stride < GR_HIP_LINE || b->out_stride < GR_HIP_LINE || (b->in_stride & 15)
+		    || (b->out_stride & 15) || ((uintptr_t)b->in_frames & 15) || ((uintptr_t)b->out_lines & 15)
+		    || ((uintptr_t)b->meta & 7) || ((uintptr_t)b->verdicts & 7))
+			return -EINVAL;
+	}
 	if (b->n > (1u << 31))
 		return -E2BIG;
 	return 1;
@@ -1504,6 +1530,87 @@ extern "C" int gr_hip_fwd4_host(
 	return 0;
 }
 
+// Registered host memory (gr_hip_host_register): host -> device address.
+static const host_range *hreg_find(const gr_hip_ctx *c, uintptr_t p) {
+	for (const host_range &r : c->hregs)
+		if (p - r.host < r.len)
+			return &r;
+	return nullptr;
+}
+
+// Every frame in registered memory and 16-byte aligned: their device
+// addresses into ptrs[n].
+static bool host_dev_ptr_ok(gr_hip_ctx *c, const gr_hip_mbuf *m, uint32_t n, uint64_t *ptrs) {
+	std::shared_lock<std::shared_mutex> l(c->mu);
+	if (c->hregs.empty())
+		return false;
+	const host_range *hit = &c->hregs[0];
+	for (uint32_t i = 0; i < n; i++) {
+		const uintptr_t p = reinterpret_cast<uintptr_t>(m[i].frame);
+		if ((p & 15) || (p - hit->host >= hit->len && (hit = hreg_find(c, p)) == nullptr))
+			return false;
+		ptrs[i] = hit->dev + (p - hit->host);
+	}
+	return true;
+}
+
+extern "C" int gr_hip_host_register(gr_hip_ctx_t *c, void *ptr, size_t bytes) {
+	if (c == nullptr || ptr == nullptr || bytes == 0)
+		return -EINVAL;
+	std::lock_guard<std::shared_mutex> l(c->mu);
+	hipSetDevice(c->dev);
+	const uintptr_t p = reinterpret_cast<uintptr_t>(ptr);
+	for (const host_range &r : c->hregs)
+		if (p < r.host + r.len && r.host < p + bytes)
+			return -EEXIST;
+	host_range r = {p, 0, bytes, false};
+	void *dp = nullptr;
+	if (host_dev_ptr(ptr, &dp)) { // already pinned (hipHostMalloc, torch pin_memory)
+		r.dev = reinterpret_cast<uintptr_t>(dp);
+	} else {
+		HCK(hipHostRegister(ptr, bytes, hipHostRegisterMapped));
+		if (hipHostGetDevicePointer(&dp, ptr, 0) != hipSuccess || dp == nullptr) {
+			(void)hipGetLastError();
+			hipHostUnregister(ptr);
+			return -EFAULT;
+		}
+		r.dev = reinterpret_cast<uintptr_t>(dp);
+		r.ours = true;
+	}
+	c->hregs.push_back(r);
+	return 0;
+}
+
+extern "C" int gr_hip_host_unregister(gr_hip_ctx_t *c, void *ptr) {
+	if (c == nullptr || ptr == nullptr)
+		return -EINVAL;
+	std::lock_guard<std::shared_mutex> l(c->mu);
+	hipSetDevice(c->dev);
+	for (size_t i = 0; i < c->hregs.size(); i++) {
+		if (c->hregs[i].host != reinterpret_cast<uintptr_t>(ptr))
+			continue;
+		int r = quiesce(c); // no kernel may still read it
+		if (r != 0)
+			return r;
+		if (c->hregs[i].ours)
+			HCK(hipHostUnregister(ptr));
+		c->hregs.erase(c->hregs.begin() + (long)i);
+		return 0;
+	}
+	return -ENOENT;
+}
+
+extern "C" int gr_hip_host_dev_addr(gr_hip_ctx_t *c, const void *ptr, uint64_t *dev) {
+	if (c == nullptr || dev == nullptr)
+		return -EINVAL;
+	std::shared_lock<std::shared_mutex> l(c->mu);
+	const host_range *r = hreg_find(c, reinterpret_cast<uintptr_t>(ptr));
+	if (r == nullptr)
+		return -ENOENT;
+	*dev = r->dev + (reinterpret_cast<uintptr_t>(ptr) - r->host);
+	return 0;
+}
+
 // The node's walk (include/grout_hip.h, "rte_graph node shim"): stage the
 // mbufs' header lines into the queue's pinned buffers, forward them on the
 // GPU, hand them back with the context's iface / nexthop mirrors.
@@ -1529,6 +1636,27 @@ extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uin
 		HCK(hipHostMalloc((void **)&q->node_meta, (size_t)n * sizeof(gr_hip_pkt_meta), hipHostMallocDefault));
 		HCK(hipHostMalloc((void **)&q->node_v, (size_t)n * sizeof(gr_hip_verdict), hipHostMallocDefault));
 		q->node_cap = n;
+	}
+	if (c->node_ptrs && host_dev_ptr_ok(c, m, n, reinterpret_cast<uint64_t *>(q->node_lines))) {
+		// the frames are device-accessible: hand them over by address, the
+		// kernel reads and rewrites them in place over PCIe
+		int r = gr_hip_node_stage(m, n, nullptr, q->node_meta);
+		if (r < 0)
+			return r;
+		void *d_ptrs, *d_meta, *d_v;
+		if (!host_dev_ptr(q->node_lines, &d_ptrs) || !host_dev_ptr(q->node_meta, &d_meta)
+		    || !host_dev_ptr(q->node_v, &d_v))
+			return -EFAULT;
+		gr_hip_batch b = {d_ptrs, nullptr, static_cast<const gr_hip_pkt_meta *>(d_meta),
+				  static_cast<gr_hip_verdict *>(d_v), n, 0, 0,
+				  GR_HIP_BATCH_F_LINES_ONLY | GR_HIP_BATCH_F_FRAME_PTRS};
+		// after everything already submitted on the queue, like gr_hip_fwd4_host
+		if ((r = launch(q, q->s, &b, true)) < 0)
+			return r;
+		HCK(hipStreamSynchronize(q->s));
+		std::shared_lock<std::shared_mutex> l(c->mu);
+		return gr_hip_node_apply(m, n, nullptr, 0, q->node_v, c->ifaces.data(), c->max_ifaces, c->nh.data(),
+					 (uint32_t)c->nh.size(), burst, stats);
 	}
 	int r = gr_hip_node_stage(m, n, q->node_lines, q->node_meta);
 	if (r < 0)

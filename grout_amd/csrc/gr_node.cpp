@@ -110,17 +110,23 @@ extern "C" int gr_hip_edge_node(uint8_t edge, uint32_t nh, int ip6) {
 }
 
 extern "C" int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, void *lines, struct gr_hip_pkt_meta *meta) {
-	if (n && (m == nullptr || lines == nullptr || meta == nullptr))
+	if (n && (m == nullptr || meta == nullptr))
 		return -EINVAL;
 	uint8_t *L = static_cast<uint8_t *>(lines);
+	constexpr uint32_t AHEAD = 16; // frames in flight: staging is bound by their cache misses
+	for (uint32_t i = 0; i < n && i < AHEAD && L != nullptr; i++)
+		__builtin_prefetch(m[i].frame, 0, 0);
 	for (uint32_t i = 0; i < n; i++) {
+		if (i + AHEAD < n && L != nullptr)
+			__builtin_prefetch(m[i + AHEAD].frame, 0, 0);
 		// 64 bytes whatever data_len says: grout's nodes read the Ethernet and
 		// IPv4 headers from the data room without a length check (eth_input.c
 		// reads 14 bytes of a shorter frame), and an mbuf's data room always
 		// holds 64 bytes past data_off (mempool.c:66-68)
 		if (m[i].frame == nullptr)
 			return -EINVAL;
-		memcpy(L + (size_t)i * GR_HIP_LINE, m[i].frame, GR_HIP_LINE);
+		if (L != nullptr) // NULL: metadata only (the GPU reads the frames itself)
+			memcpy(L + (size_t)i * GR_HIP_LINE, m[i].frame, GR_HIP_LINE);
 		meta[i].iface = m[i].iface;
 		meta[i].vlan_ck = (uint16_t)((m[i].vlan_id & 0xfff) | ((m[i].ck & 3) << 12));
 		meta[i].pkt_len = (uint16_t)(m[i].pkt_len > 0xffff ? 0xffff : m[i].pkt_len);
@@ -144,7 +150,7 @@ extern "C" int gr_hip_node_apply(
 ) {
 	if (n == 0)
 		return 0;
-	if (m == nullptr || lines == nullptr || verdicts == nullptr || line_stride < GR_HIP_LINE)
+	if (m == nullptr || verdicts == nullptr || (lines != nullptr && line_stride < GR_HIP_LINE))
 		return -EINVAL;
 	if (burst == 0)
 		burst = 64;
@@ -158,10 +164,18 @@ extern "C" int gr_hip_node_apply(
 				    GR_HIP_NODE_IFACE_OUTPUT};
 	uint32_t reach[GR_HIP_NODE_COUNT] = {};
 	uint32_t sent4 = 0, sent6 = 0; // what ip_output / ip6_output enqueued to eth_output
+	// frames read (the ether type) and written back: prefetch them, the loop
+	// is bound by their cache misses
+	constexpr uint32_t AHEAD = 16;
+	for (uint32_t i = 0; i < n && i < AHEAD; i++)
+		__builtin_prefetch(m[i].frame, 1, 0);
 	for (uint32_t i = 0; i < n; i++) {
+		if (i + AHEAD < n)
+			__builtin_prefetch(m[i + AHEAD].frame, 1, 0);
 		struct gr_hip_mbuf &b = m[i];
 		const struct gr_hip_verdict &v = verdicts[i];
-		const uint8_t *line = L + (size_t)i * line_stride;
+		// lines NULL: the GPU rewrote the frames in place already
+		const uint8_t *line = L != nullptr ? L + (size_t)i * line_stride : static_cast<const uint8_t *>(b.frame);
 		const bool ip6 = line[12] == 0x86 && line[13] == 0xdd; // RTE_ETHER_TYPE_IPV6
 		const int node = gr_hip_edge_node(v.edge, v.nh, ip6);
 		if (node < -1)
@@ -198,7 +212,8 @@ extern "C" int gr_hip_node_apply(
 				uint32_t len = b.data_len + (depth < 5 ? 14u : 0u);
 				if (len > 26)
 					len = 26;
-				memcpy(b.frame, line, len);
+				if (L != nullptr)
+					memcpy(b.frame, line, len);
 			}
 			if (depth <= 4) {
 				if (demuxed)

@@ -52,7 +52,21 @@ static struct {
 	struct rte_graph *graph;
 	char name[RTE_GRAPH_NAMESIZE];
 	int inited;
-} H = {.gid = RTE_GRAPH_ID_INVALID};
+	int pin; // register the mbuf memory with the fast path (frames by address)
+	void *pinned; // what is registered now
+} H = {.gid = RTE_GRAPH_ID_INVALID, .pin = 1};
+
+// Whether gh_load registers its mbuf memory with gr_hip_host_register (grout:
+// the mempools' memory), so that the node hands frames over by address.
+void gh_set_pin(int on) {
+	H.pin = on;
+}
+
+static void unpin(void) {
+	if (H.pinned != NULL && gpu_fwd4_hip_ctx() != NULL)
+		gr_hip_host_unregister(gpu_fwd4_hip_ctx(), H.pinned);
+	H.pinned = NULL;
+}
 
 static struct rte_mbuf *mbuf_at(uint32_t i) {
 	return (struct rte_mbuf *)(H.mem + (size_t)i * GH_MBUF_SZ);
@@ -215,6 +229,7 @@ int gh_graph_destroy(void) {
 int gh_load(const uint8_t *frames, uint32_t stride, const struct gr_hip_pkt_meta *meta, uint32_t n) {
 	if (stride > GH_ROOM - RTE_PKTMBUF_HEADROOM)
 		return -EINVAL;
+	unpin();
 	free(H.mem);
 	free(H.edge_of);
 	free(H.seq_of);
@@ -244,6 +259,12 @@ int gh_load(const uint8_t *frames, uint32_t stride, const struct gr_hip_pkt_meta
 	H.next_rx = 0;
 	H.recorded = 0;
 	H.meta_in = meta;
+	if (H.pin && n && gpu_fwd4_hip_ctx() != NULL) {
+		int r = gr_hip_host_register(gpu_fwd4_hip_ctx(), H.mem, (size_t)n * GH_MBUF_SZ);
+		if (r < 0)
+			return r;
+		H.pinned = H.mem;
+	}
 	return 0;
 }
 
@@ -321,6 +342,7 @@ int gh_rte_node_counters(const char *node, uint64_t out[3]) {
 }
 
 void gh_fini(void) {
+	unpin();
 	gh_graph_destroy();
 	gr_modules_fini(NULL);
 	free(H.mem);

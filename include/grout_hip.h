@@ -313,6 +313,12 @@ struct gr_hip_batch {
 // Only the first 64 bytes of each frame are present (header-only staging from
 // host mbufs): packets whose IPv4 header does not fit get GR_HIP_E_PUNT.
 #define GR_HIP_BATCH_F_LINES_ONLY 0x1
+// in_frames is an array of n frame addresses (uint64_t, device-accessible:
+// device memory, or host memory pinned with gr_hip_host_register, 16-byte
+// aligned frames), in_stride is ignored; out_lines NULL rewrites each frame's
+// first 64 bytes in place (the bytes grout's chain changes, and the others
+// as they were), else lines go to out_lines as usual.
+#define GR_HIP_BATCH_F_FRAME_PTRS 0x2
 
 // Per-iface counters of one queue (iface.h:105-119 subset the path touches).
 struct gr_hip_iface_stats {
@@ -409,6 +415,8 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               registered) buffers runs the kernel on them directly, its
 //               loads and stores crossing PCIe (default); 0 = always staged
 //               chunk copies (pageable buffers always take that path)
+//   "node_ptrs"  1 = gr_hip_node_process hands registered frames over by
+//               address (default), 0 = always stage header lines
 //   "fib_format_of" (read) the format VRF `value`'s FIB is on the device in
 //   "occupancy" (read) resident workgroups per CU of the current variant
 // Returns 0 (or the value read), -EINVAL, or -ENOENT for an unknown key.
@@ -440,6 +448,14 @@ int gr_hip_dev_alloc(gr_hip_ctx_t *, size_t bytes, void **dptr);
 int gr_hip_dev_free(gr_hip_ctx_t *, void *dptr);
 int gr_hip_memcpy_h2d(gr_hip_ctx_t *, void *dst, const void *src, size_t bytes);
 int gr_hip_memcpy_d2h(gr_hip_ctx_t *, void *dst, const void *src, size_t bytes);
+// Pin and map caller memory for the GPU (grout: the mbuf pools' memory), so
+// that frames in it can be handed over by address (GR_HIP_BATCH_F_FRAME_PTRS,
+// gr_hip_node_process). Memory already pinned is recorded as it is.
+// -EEXIST if the range overlaps a registered one.
+int gr_hip_host_register(gr_hip_ctx_t *, void *ptr, size_t bytes);
+int gr_hip_host_unregister(gr_hip_ctx_t *, void *ptr);
+// The device address of host address `ptr` in a registered range (-ENOENT).
+int gr_hip_host_dev_addr(gr_hip_ctx_t *, const void *ptr, uint64_t *dev);
 
 // ---------------------------------------------------------------------------
 // rte_graph node shim: mbuf staging and hand-back
@@ -503,11 +519,12 @@ int gr_hip_edge_node(uint8_t edge, uint32_t nh, int ip6);
 
 // Stage n mbufs: the first 64 bytes at each frame (read whatever data_len
 // says, as grout's nodes do: an mbuf's data room always has them) into
-// lines[i * 64], and their metadata.
+// lines[i * 64] (lines NULL: skipped), and their metadata.
 int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, void *lines, struct gr_hip_pkt_meta *meta);
 
 // Hand back: apply the fast path's verdicts and rewritten header lines
-// (line_stride apart) to the mbufs. ifaces[id] / nh[slot] are the mirrors
+// (line_stride apart; lines NULL: the frames were rewritten in place) to the
+// mbufs. ifaces[id] / nh[slot] are the mirrors
 // pushed with gr_hip_iface_set / gr_hip_nh_set (the egress VLAN tag and the
 // ingress VLAN demux are read from them). stats (optional) accumulates the
 // per-node counters, the packets taken as consecutive graph walks of
@@ -526,8 +543,12 @@ int gr_hip_node_apply(
 	struct gr_hip_node_stats *stats
 );
 
-// The node's whole walk on a queue: stage, forward on the GPU
-// (gr_hip_fwd4_host), apply with the context's mirrors.
+// The node's whole walk on a queue: stage, forward on the GPU, apply with the
+// context's mirrors. When every frame lies in memory registered with
+// gr_hip_host_register (and is 16-byte aligned), the GPU reads and rewrites
+// the frames in place over PCIe and only 8-byte frame addresses and metadata
+// are staged ("node_ptrs", default on); otherwise header lines are staged
+// through gr_hip_fwd4_host.
 int gr_hip_node_process(gr_hip_queue_t *, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst,
 			struct gr_hip_node_stats *stats);
 

@@ -5,6 +5,7 @@ Bit-exact on integer/byte work: verdict (edge, domain, iface, nexthop),
 the 64-byte header line each packet leaves with, and the per-iface rx/tx
 counters, on the same seeded inputs -- from the exception corpus up to the
 BASELINE full size (16M packets over the 1M-route view)."""
+import ctypes
 import functools
 
 import numpy as np
@@ -137,6 +138,44 @@ def test_host_memory_path(fastpath):
     st = q.stats(reset=True)
     q.close()
     compare(o, (lines, v, st))
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+def test_frame_pointer_batch(fastpath, inplace):
+    """GR_HIP_BATCH_F_FRAME_PTRS: frames scattered in device memory, handed
+    over by address (corpus + a full-view stream, ragged count), lines out of
+    place or each frame rewritten in place."""
+    import torch
+    t = _fullview()
+    fr2, me2 = S.stream(50_001, 0xF9, routes=t.route_array(), stride=128)
+    tc, _ = SC.corpus_topology()
+    frc, mec, lab = SC.corpus_arrays()
+    for topo, fr, me in [(tc, frc, mec), (t, fr2, me2)]:
+        fresh_fastpath_state(fastpath, topo)
+        n, stride = fr.shape
+        perm = np.random.default_rng(n).permutation(n)  # frame i lives in slot perm[i]
+        slots = np.zeros((n, stride), dtype=np.uint8)
+        slots[perm] = fr
+        dev = torch.device("cuda")
+        d_slots = torch.from_numpy(slots.reshape(-1)).to(dev)
+        ptrs = torch.from_numpy((d_slots.data_ptr() + perm.astype(np.uint64) * stride).view(np.int64)).to(dev)
+        d_me = torch.from_numpy(me.view(np.uint8)).to(dev)
+        d_out = torch.zeros(n * abi.LINE, dtype=torch.uint8, device=dev)
+        d_v = torch.zeros(n * 8, dtype=torch.uint8, device=dev)
+        q = fastpath.queue()
+        torch.cuda.synchronize()
+        q.stats(reset=True)
+        b = abi.Batch(ptrs.data_ptr(), None if inplace else d_out.data_ptr(), d_me.data_ptr(), d_v.data_ptr(), n, 0,
+                      abi.LINE, abi.BATCH_F_FRAME_PTRS)
+        abi.check("gr_hip_fwd4_submit", fastpath.lib.gr_hip_fwd4_submit(q._h, ctypes.byref(b)))
+        q.sync()
+        st = q.stats(reset=True)
+        q.close()
+        lines = (d_slots.cpu().numpy().reshape(n, stride)[perm, :abi.LINE] if inplace
+                 else d_out.cpu().numpy().reshape(n, abi.LINE))
+        compare(oracle.Oracle(topo).process(fr, me), (lines, d_v.cpu().numpy().view(abi.VERDICT_DT), st))
+        if inplace:  # nothing past the line moved
+            assert np.array_equal(d_slots.cpu().numpy().reshape(n, stride)[perm, abi.LINE:], fr[:, abi.LINE:])
 
 
 @pytest.mark.parametrize("direct", [0, 1])

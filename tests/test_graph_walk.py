@@ -192,13 +192,20 @@ def check_walk(topo, fr, me, labels=None):
 
 
 @pytest.mark.gpu
-def test_graph_walk_corpus():
+@pytest.mark.parametrize("pin", [1, 0])
+def test_graph_walk_corpus(pin):
+    """Every edge. pin 1: the mbuf memory is registered, frames go to the GPU
+    by address and come back rewritten in place; pin 0: header lines staged."""
+    lib().gh_set_pin(pin)
     t, _ = SC.corpus_topology()
     fr, me, lab = SC.corpus_arrays()
     # ol_flags has no value for the corpus's out-of-range status 3 ("ol 3")
     keep = ((me["vlan_ck"] >> 12) & 3) != 3
     fr, me, lab = fr[keep], me[keep], [x for x, k in zip(lab, keep) if k]
-    got = check_walk(t, fr, me, lab)
+    try:
+        got = check_walk(t, fr, me, lab)
+    finally:
+        lib().gh_set_pin(1)
     assert len(set(got["edge"])) > 20
 
 

@@ -172,3 +172,37 @@ def test_node_process_gpu(fastpath):
         assert np.array_equal(ns["calls"], ns_want["calls"])
         assert np.array_equal(q.stats(), st)  # the iface counters of the same packets
         q.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ptrs", [1, 0])
+def test_node_process_registered_frames(fastpath, ptrs):
+    """Frames in memory registered with gr_hip_host_register: the node hands
+    them to the GPU by address and the kernel rewrites them in place over
+    PCIe (node_ptrs 1); the same mbufs staged as lines (node_ptrs 0) must end
+    identical."""
+    import ctypes
+    from golden_util import fresh_fastpath_state
+    topo = T.config_fullview(count=100_000)
+    fr, me = S.stream(70_001, 0xB0E, routes=topo.route_array())
+    fresh_fastpath_state(fastpath, topo)
+    lines, v, st, want, ns_want = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
+    bufs, m = mbufs_for(fr, me)
+    L = fastpath.lib
+    abi.check("gr_hip_host_register", L.gr_hip_host_register(fastpath.h, bufs.ctypes.data, bufs.nbytes))
+    try:
+        dev = ctypes.c_uint64()
+        assert L.gr_hip_host_dev_addr(fastpath.h, bufs.ctypes.data + 64, ctypes.byref(dev)) == 0
+        assert L.gr_hip_host_register(fastpath.h, bufs.ctypes.data + 64, 64) == -17  # -EEXIST: overlaps
+        fastpath.tune("node_ptrs", ptrs)
+        q = fastpath.queue()
+        ns = q.node_process(m, burst=64)
+        compare_mbufs(m, want, bufs, lines)
+        assert np.array_equal(ns["packets"], ns_want["packets"]) and np.array_equal(ns["calls"], ns_want["calls"])
+        assert np.array_equal(q.stats(), st)
+        q.close()
+    finally:
+        fastpath.tune("node_ptrs", 1)
+        abi.check("gr_hip_host_unregister", L.gr_hip_host_unregister(fastpath.h, bufs.ctypes.data))
+    assert L.gr_hip_host_dev_addr(fastpath.h, bufs.ctypes.data, ctypes.byref(dev)) == -2  # -ENOENT
+

@@ -49,6 +49,36 @@ def main():
             print(json.dumps({"batch": n, "host_direct": direct, "us": round(dt * 1e6, 1),
                               "mpps": round(n / dt / 1e6, 1),
                               "GBps_per_dir": round(n * (abi.LINE + 8) / dt / 1e9, 1)}), flush=True)
+    # the rte_graph node's whole walk (gr_hip_node_process): stage the lines
+    # from the mbufs on the CPU, forward, hand back onto the mbufs
+    n = 1 << 21
+    bufs = np.zeros((n, 256), dtype=np.uint8)  # mbuf data rooms (frame at offset 0)
+    bufs[:, :64] = fr[:n]
+    mb = np.zeros(n, dtype=abi.MBUF_DT)
+    mb["frame"] = bufs.ctypes.data + np.arange(n, dtype=np.uint64) * 256
+    mb["pkt_len"] = me["pkt_len"][:n]
+    mb["data_len"] = me["pkt_len"][:n]
+    mb["data_off"] = 128
+    mb["rss"] = me["rss"][:n]
+    mb["iface"] = me["iface"][:n]
+    fp.tune("host_direct", 1)
+    abi.check("gr_hip_host_register", fp.lib.gr_hip_host_register(fp.h, bufs.ctypes.data, bufs.nbytes))
+    for mode in ("staged", "frame_ptrs"):
+        fp.tune("node_ptrs", 1 if mode == "frame_ptrs" else 0)
+        m = mb.copy()
+        q.node_process(m)
+        dt = []
+        for _ in range(4):
+            m[:] = mb
+            bufs[:, :64] = fr[:n]
+            t1 = time.perf_counter()
+            q.node_process(m)
+            dt.append(time.perf_counter() - t1)
+        d = float(np.median(dt))
+        print(json.dumps({"node_process_batch": n, "mode": mode, "us": round(d * 1e6, 1),
+                          "mpps": round(n / d / 1e6, 1), "cpu_threads": 1}), flush=True)
+    fp.tune("node_ptrs", 1)
+    abi.check("gr_hip_host_unregister", fp.lib.gr_hip_host_unregister(fp.h, bufs.ctypes.data))
     fp.tune("host_direct", 1)
     q.close()
     fp.close()
