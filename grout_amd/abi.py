@@ -203,6 +203,8 @@ HOST_API = {
     "gr_fib6_lookup": (_U32, [_P, _P]),
     "gr_fib6_lookup_rib": (_U32, [_P, _P]),
     "gr_fib6_groups_used": (_U32, [_P]),
+    "gr_fib6_skips_used": (_U32, [_P]),
+    "gr_fib6_groups_painted": (_U32, [_P]),
     "gr_fib6_n_routes": (_U32, [_P]),
 }
 

@@ -30,7 +30,11 @@ struct gr_fib6 {
 	uint32_t n_routes, n_tomb, max_routes;
 	uint32_t *top; // GR_FIB6_TOP
 	uint32_t *groups; // max_groups * GR_FIB6_GROUP
-	uint32_t max_groups, n_groups;
+	uint32_t max_groups, n_groups, n_painted;
+	struct gr_fib6_skip *skips; // max_groups: each replaces at least one group
+	uint32_t n_skips;
+	uint32_t *remap; // max_groups, compaction scratch
+	uint8_t *live; // max_groups
 	uint32_t max_slot;
 	bool dirty;
 	uint64_t generation;
@@ -96,7 +100,10 @@ gr_fib6_t *gr_fib6_new(uint32_t max_routes, uint32_t max_groups) {
 	f->ht = calloc(cap, sizeof(*f->ht));
 	f->top = calloc(GR_FIB6_TOP, sizeof(uint32_t));
 	f->groups = malloc((size_t)max_groups * GR_FIB6_GROUP * sizeof(uint32_t));
-	if (!f->ht || !f->top || !f->groups) {
+	f->skips = malloc((size_t)max_groups * sizeof(*f->skips));
+	f->remap = malloc((size_t)max_groups * sizeof(uint32_t));
+	f->live = malloc(max_groups);
+	if (!f->ht || !f->top || !f->groups || !f->skips || !f->remap || !f->live) {
 		gr_fib6_free(f);
 		return NULL;
 	}
@@ -109,6 +116,9 @@ void gr_fib6_free(gr_fib6_t *f) {
 	free(f->ht);
 	free(f->top);
 	free(f->groups);
+	free(f->skips);
+	free(f->remap);
+	free(f->live);
 	free(f);
 }
 
@@ -215,6 +225,95 @@ static int paint(gr_fib6_t *f, const struct rib6_ent *r) {
 	}
 }
 
+// Path compression (bottom-up): a group whose entries all hold one leaf D
+// but for one index x becomes a skip node {key x, child = entry x, miss D};
+// a skip whose child is a skip with the same miss and room in its key
+// absorbs it. Returns the entry that replaces `ent`.
+static uint32_t compress(gr_fib6_t *f, uint32_t ent) {
+	if (!(ent & GR_FIB6_EXT) || (ent & GR_FIB6_SKIP))
+		return ent;
+	uint32_t *grp = f->groups + (size_t)(ent & GR_FIB6_IDX) * GR_FIB6_GROUP;
+	for (int i = 0; i < GR_FIB6_GROUP; i++)
+		grp[i] = compress(f, grp[i]);
+	// the leaf most entries hold: one of the first three
+	uint32_t d = grp[0] == grp[1] || grp[0] == grp[2] ? grp[0] : grp[1];
+	if (d & GR_FIB6_EXT)
+		return ent;
+	int x = -1;
+	for (int i = 0; i < GR_FIB6_GROUP; i++) {
+		if (grp[i] == d)
+			continue;
+		if (x >= 0)
+			return ent; // two paths leave this group
+		x = i;
+	}
+	if (x < 0)
+		return d; // every entry the same leaf
+	const uint32_t child = grp[x];
+	if ((child & GR_FIB6_SKIP) && (child & GR_FIB6_EXT)) {
+		struct gr_fib6_skip *k = &f->skips[child & GR_FIB6_IDX];
+		if (k->miss == d && k->n < 7) { // prepend x to the child's key
+			memmove(k->key + 1, k->key, k->n);
+			k->key[0] = (uint8_t)x;
+			k->n++;
+			return child;
+		}
+	}
+	struct gr_fib6_skip *k = &f->skips[f->n_skips];
+	memset(k, 0, sizeof(*k));
+	k->key[0] = (uint8_t)x;
+	k->n = 1;
+	k->child = child;
+	k->miss = d;
+	return GR_FIB6_EXT | GR_FIB6_SKIP | f->n_skips++;
+}
+
+static void mark(gr_fib6_t *f, uint32_t ent) {
+	if (!(ent & GR_FIB6_EXT))
+		return;
+	if (ent & GR_FIB6_SKIP) {
+		mark(f, f->skips[ent & GR_FIB6_IDX].child);
+		return;
+	}
+	const uint32_t g = ent & GR_FIB6_IDX;
+	f->live[g] = 1;
+	for (int i = 0; i < GR_FIB6_GROUP; i++)
+		mark(f, f->groups[(size_t)g * GR_FIB6_GROUP + i]);
+}
+
+static uint32_t relink(const gr_fib6_t *f, uint32_t ent) {
+	if ((ent & GR_FIB6_EXT) && !(ent & GR_FIB6_SKIP))
+		return GR_FIB6_EXT | f->remap[ent & GR_FIB6_IDX];
+	return ent;
+}
+
+// Compress, then pack the groups still referenced to the front.
+static void compress_all(gr_fib6_t *f) {
+	f->n_painted = f->n_groups;
+	f->n_skips = 0;
+	for (uint32_t i = 0; i < GR_FIB6_TOP; i++)
+		f->top[i] = compress(f, f->top[i]);
+	memset(f->live, 0, f->n_groups);
+	for (uint32_t i = 0; i < GR_FIB6_TOP; i++)
+		mark(f, f->top[i]);
+	uint32_t n = 0;
+	for (uint32_t g = 0; g < f->n_groups; g++)
+		f->remap[g] = f->live[g] ? n++ : UINT32_MAX;
+	for (uint32_t i = 0; i < GR_FIB6_TOP; i++)
+		f->top[i] = relink(f, f->top[i]);
+	for (uint32_t k = 0; k < f->n_skips; k++)
+		f->skips[k].child = relink(f, f->skips[k].child);
+	for (uint32_t g = 0; g < f->n_groups; g++) {
+		if (!f->live[g])
+			continue;
+		uint32_t *src = f->groups + (size_t)g * GR_FIB6_GROUP;
+		uint32_t *dst = f->groups + (size_t)f->remap[g] * GR_FIB6_GROUP; // never above src
+		for (int i = 0; i < GR_FIB6_GROUP; i++)
+			dst[i] = relink(f, src[i]);
+	}
+	f->n_groups = n;
+}
+
 int gr_fib6_build(gr_fib6_t *f) {
 	if (f == NULL)
 		return -EINVAL;
@@ -241,6 +340,7 @@ int gr_fib6_build(gr_fib6_t *f) {
 	free(order);
 	if (ret < 0)
 		return ret;
+	compress_all(f);
 	f->dirty = false;
 	f->generation++;
 	return 0;
@@ -248,8 +348,17 @@ int gr_fib6_build(gr_fib6_t *f) {
 
 uint32_t gr_fib6_lookup(const gr_fib6_t *f, const uint8_t ip[16]) {
 	uint32_t ent = f->top[((uint32_t)ip[0] << 8) | ip[1]];
-	for (int b = 2; b < 16 && (ent & GR_FIB6_EXT); b++)
-		ent = f->groups[(size_t)(ent & ~GR_FIB6_EXT) * GR_FIB6_GROUP + ip[b]];
+	int b = 2;
+	while (b < 16 && (ent & GR_FIB6_EXT)) {
+		if (ent & GR_FIB6_SKIP) {
+			const struct gr_fib6_skip *k = &f->skips[ent & GR_FIB6_IDX];
+			const bool match = b + k->n <= 16 && memcmp(ip + b, k->key, k->n) == 0;
+			ent = match ? k->child : k->miss;
+			b += k->n;
+		} else {
+			ent = f->groups[(size_t)(ent & GR_FIB6_IDX) * GR_FIB6_GROUP + ip[b++]];
+		}
+	}
 	return ent & GR_FIB6_EXT ? 0 : ent;
 }
 
@@ -273,6 +382,15 @@ const uint32_t *gr_fib6_groups(const gr_fib6_t *f) {
 }
 uint32_t gr_fib6_groups_used(const gr_fib6_t *f) {
 	return f->n_groups;
+}
+const struct gr_fib6_skip *gr_fib6_skips(const gr_fib6_t *f) {
+	return f->skips;
+}
+uint32_t gr_fib6_skips_used(const gr_fib6_t *f) {
+	return f->n_skips;
+}
+uint32_t gr_fib6_groups_painted(const gr_fib6_t *f) {
+	return f->n_painted;
 }
 uint32_t gr_fib6_max_groups(const gr_fib6_t *f) {
 	return f->max_groups;

@@ -6,9 +6,13 @@
 // grout keeps IPv6 routes in rte_rib6 and looks them up in an rte_fib6 TRIE
 // (modules/ip6/control/route.c:66-98,151-173). The device table here is a
 // multibit trie: a first level of 2^16 entries indexed by address bytes 0-1,
-// then groups of 256 entries indexed by each further byte. Entry encoding
-// (u32): bit 31 set = group index in bits 0-30, else the nexthop slot of the
-// longest matching prefix (0 = no route, the FIB default_nh, route.c:80).
+// then groups of 256 entries indexed by each further byte, path-compressed:
+// a group whose 256 entries all hold one leaf but for one index becomes a
+// skip node ("bytes b..b+n-1 equal key: continue with child, else the leaf
+// miss"), and consecutive skips merge (up to 7 key bytes). Entry encoding
+// (u32): bit 31 clear = the nexthop slot of the longest matching prefix (0 =
+// no route, the FIB default_nh, route.c:80); bits 31 and 30 = skip node
+// index in bits 0-29; bit 31 alone = group index in bits 0-29.
 #pragma once
 
 #include <stdint.h>
@@ -18,6 +22,15 @@ extern "C" {
 #endif
 
 #define GR_FIB6_EXT 0x80000000u
+#define GR_FIB6_SKIP 0x40000000u
+#define GR_FIB6_IDX 0x3fffffffu
+
+struct gr_fib6_skip { // 16 bytes, as the kernel loads it
+	uint8_t key[7];
+	uint8_t n; // key bytes, 1..7
+	uint32_t child; // entry when they match (depth + n)
+	uint32_t miss; // leaf when they do not
+};
 #define GR_FIB6_TOP 65536
 #define GR_FIB6_GROUP 256
 
@@ -40,6 +53,10 @@ uint32_t gr_fib6_lookup_rib(const gr_fib6_t *, const uint8_t ip[16]);
 const uint32_t *gr_fib6_top(const gr_fib6_t *);
 const uint32_t *gr_fib6_groups(const gr_fib6_t *);
 uint32_t gr_fib6_groups_used(const gr_fib6_t *);
+const struct gr_fib6_skip *gr_fib6_skips(const gr_fib6_t *);
+uint32_t gr_fib6_skips_used(const gr_fib6_t *);
+// Groups the trie had before path compression (for the record).
+uint32_t gr_fib6_groups_painted(const gr_fib6_t *);
 uint32_t gr_fib6_max_groups(const gr_fib6_t *);
 uint32_t gr_fib6_n_routes(const gr_fib6_t *);
 uint32_t gr_fib6_max_slot(const gr_fib6_t *);

@@ -376,8 +376,21 @@ __device__ __forceinline__ uint32_t chain_fib6(const fwd4_rx6 &v, const uint32_t
 	if ((key[0] & 0xff) == 0xfe && (key[0] & 0xc000) == 0x8000)
 		key[0] = (key[0] & 0xffff) | ((iface_id >> 8) << 16) | ((iface_id & 0xff) << 24);
 	uint32_t ent = gld(v.top + ((byte_of(key, 0) << 8) | byte_of(key, 1)));
-	for (int b = 2; b < 16 && (ent & 0x80000000u); b++)
-		ent = gld(v.groups + (size_t)(ent & 0x7fffffffu) * 256 + byte_of(key, b));
+	int b = 2;
+	while (b < 16 && (ent & 0x80000000u)) {
+		if (ent & 0x40000000u) { // skip node: key bytes 0-6, n in byte 7
+			const uint4 k = gld4(v.skips + (ent & 0x3fffffffu));
+			const int n = k.y >> 24;
+			bool match = b + n <= 16;
+			for (int i = 0; i < n && match; i++)
+				match = byte_of(key, b + i) == ((i < 4 ? k.x >> (8 * i) : k.y >> (8 * (i - 4))) & 0xff);
+			ent = match ? k.z : k.w;
+			b += n;
+		} else {
+			ent = gld(v.groups + (size_t)(ent & 0x3fffffffu) * 256 + byte_of(key, b));
+			b++;
+		}
+	}
 	return (ent & 0x80000000u) ? 0 : ent;
 }
 
@@ -427,7 +440,7 @@ __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, 
 		r.edge = mc ? GR_HIP_E_IP6_INPUT_LOCAL : GR_HIP_E_IP6_INPUT_OTHER_HOST;
 		return;
 	}
-	const fwd4_rx6 v = {gld(&P.rx6[rx.id].top), gld(&P.rx6[rx.id].groups)};
+	const fwd4_rx6 v = {gld(&P.rx6[rx.id].top), gld(&P.rx6[rx.id].groups), gld(&P.rx6[rx.id].skips)};
 	uint32_t slot = chain_fib6(v, dst, rx.id); // :122-128
 	if (slot == 0 || slot > P.max_nh) {
 		r.edge = GR_HIP_E_IP6_ERROR_DEST_UNREACH;

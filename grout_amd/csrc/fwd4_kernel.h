@@ -53,6 +53,7 @@ struct fwd4_rx {
 struct fwd4_rx6 {
 	const uint32_t *top; // [65536] (fib6.h encoding)
 	const uint32_t *groups; // [n][256]
+	const uint4 *skips; // struct gr_fib6_skip [n]
 };
 
 // Per-nexthop adjacency, 64 bytes: the nexthop fields ip_input reads plus

@@ -235,7 +235,7 @@ static fwd4_rx make_rx(const gr_hip_ctx *c, uint32_t id) {
 
 // IPv6 view of iface `id`: the FIB6 of its VRF (get_fib6, route.c:51-64).
 static fwd4_rx6 make_rx6(const gr_hip_ctx *c, uint32_t id) {
-	fwd4_rx6 r = {nullptr, nullptr};
+	fwd4_rx6 r = {nullptr, nullptr, nullptr};
 	const gr_hip_iface *i = iface_get(c, id);
 	if (i == nullptr)
 		return r;
@@ -245,6 +245,7 @@ static fwd4_rx6 make_rx6(const gr_hip_ctx *c, uint32_t id) {
 		const vrf_fib &v = c->vrfs[i->vrf_id];
 		r.top = v.d6;
 		r.groups = v.d6 + GR_FIB6_TOP;
+		r.skips = reinterpret_cast<const uint4 *>(v.d6 + GR_FIB6_TOP + (size_t)v.d6_groups * GR_FIB6_GROUP);
 	}
 	return r;
 }
@@ -1172,15 +1173,19 @@ extern "C" int gr_hip_fib6_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 	r = quiesce(c);
 	if (r != 0)
 		return r;
-	const uint32_t groups = gr_fib6_groups_used(v.rib6);
-	if (v.d6 == nullptr) { // sized for the VRF's group capacity once
+	const uint32_t groups = gr_fib6_groups_used(v.rib6), skips = gr_fib6_skips_used(v.rib6);
+	if (v.d6 == nullptr) { // sized for the VRF's group capacity once: top, groups, skips
 		const uint32_t cap = gr_fib6_max_groups(v.rib6);
-		HCK(hipMalloc(&v.d6, ((size_t)GR_FIB6_TOP + (size_t)cap * GR_FIB6_GROUP) * sizeof(uint32_t)));
+		HCK(hipMalloc(&v.d6, ((size_t)GR_FIB6_TOP + (size_t)cap * GR_FIB6_GROUP) * sizeof(uint32_t)
+					     + (size_t)cap * sizeof(gr_fib6_skip)));
 		v.d6_groups = cap;
 	}
 	r = h2d(c, v.d6, gr_fib6_top(v.rib6), (size_t)GR_FIB6_TOP * sizeof(uint32_t));
 	if (r == 0 && groups)
 		r = h2d(c, v.d6 + GR_FIB6_TOP, gr_fib6_groups(v.rib6), (size_t)groups * GR_FIB6_GROUP * sizeof(uint32_t));
+	if (r == 0 && skips)
+		r = h2d(c, v.d6 + GR_FIB6_TOP + (size_t)v.d6_groups * GR_FIB6_GROUP, gr_fib6_skips(v.rib6),
+			(size_t)skips * sizeof(gr_fib6_skip));
 	if (r == 0)
 		r = ctl_sync(c);
 	if (r != 0)
@@ -1220,7 +1225,8 @@ extern "C" int gr_hip_fib6_info(gr_hip_ctx_t *c, uint16_t vrf, uint32_t *n_route
 	if (groups_used)
 		*groups_used = gr_fib6_groups_used(v.rib6);
 	if (bytes) // device bytes a lookup can touch
-		*bytes = 4ull * GR_FIB6_TOP + 1024ull * gr_fib6_groups_used(v.rib6);
+		*bytes = 4ull * GR_FIB6_TOP + 1024ull * gr_fib6_groups_used(v.rib6)
+			 + sizeof(gr_fib6_skip) * (uint64_t)gr_fib6_skips_used(v.rib6);
 	return 0;
 }
 

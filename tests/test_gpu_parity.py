@@ -474,7 +474,7 @@ def test_fullview6_stream(fastpath):
     compare(o, g)
     assert (g[1]["edge"] == abi.EDGE["port_output"]).mean() > 0.99
     info = fastpath.fib6_info(1)
-    assert info["routes"] == len(t.route6_array()) and info["groups_used"] > 100_000
+    assert info["routes"] == len(t.route6_array()) and info["groups_used"] > 20_000  # a deep, path-compressed trie
 
 
 def test_mixed_v4_v6_stream(fastpath):

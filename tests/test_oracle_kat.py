@@ -210,3 +210,42 @@ def test_lpm6_hash_matches_brute_force():
         assert host.gr_fib6_lookup(f, d.ctypes.data) == want  # the product's trie
         assert host.gr_fib6_lookup_rib(f, d.ctypes.data) == want
     host.gr_fib6_free(f)
+
+
+def test_fib6_path_compression_fullview6():
+    """The product's IPv6 trie is path-compressed (fib6.c): on the IPv6 view
+    most groups become skip nodes, and lookups under every route, next to
+    random ones, still equal the RIB's longest match, also after deletes and
+    a rebuild."""
+    host = abi.host()
+    t = T.config_fullview6(count=20_000)
+    r = t.route6_array()
+    f = host.gr_fib6_new(len(r) + 16, 4 * len(r))
+    for x in r:
+        ip = np.ascontiguousarray(x["ip"])
+        assert host.gr_fib6_add(f, ip.ctypes.data, int(x["prefixlen"]), int(x["nh"]), 0) == 0
+    assert host.gr_fib6_build(f) == 0
+    painted, kept, skips = host.gr_fib6_groups_painted(f), host.gr_fib6_groups_used(f), host.gr_fib6_skips_used(f)
+    assert kept < painted // 4 and skips > 0, (painted, kept, skips)
+    rng = np.random.default_rng(66)
+
+    def check(routes, n):
+        for i in range(n):
+            d = rng.integers(0, 256, 16, dtype=np.uint8)
+            if i % 4:  # under a route, random host bits
+                x = routes[rng.integers(len(routes))]
+                nb = int(x["prefixlen"])
+                full = nb // 8
+                d[:full] = x["ip"][:full]
+                if nb % 8:
+                    m = (0xFF00 >> (nb % 8)) & 0xFF
+                    d[full] = (int(x["ip"][full]) & m) | (int(d[full]) & (~m & 0xFF))
+            assert host.gr_fib6_lookup(f, d.ctypes.data) == host.gr_fib6_lookup_rib(f, d.ctypes.data)
+
+    check(r, 20_000)
+    for x in r[::3]:  # delete a third, repaint, compare again
+        ip = np.ascontiguousarray(x["ip"])
+        assert host.gr_fib6_del(f, ip.ctypes.data, int(x["prefixlen"])) == 0
+    assert host.gr_fib6_build(f) == 0
+    check(r, 20_000)
+    host.gr_fib6_free(f)
