@@ -35,8 +35,13 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=1 << 24, help="packets per step per GPU")
-    p.add_argument("--workload", default="fullview64", choices=["fullview64", "single64", "imix", "fullview6"])
+    p.add_argument("--batch", type=int, default=None,
+                   help="packets per step per GPU (default 2^24; 2^22 for imix_frames, 8 GiB of 2 KiB slots)")
+    p.add_argument("--workload", default="fullview64",
+                   choices=["fullview64", "single64", "imix", "imix_frames", "fullview6"])
+    p.add_argument("--slot", type=int, default=2240,
+                   help="imix_frames: bytes per frame slot (2240 = grout's mbuf object: 128 B rte_mbuf + "
+                        "64 B priv + 2048 B data room, mempool.c:57-100)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-path", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="wall time of the CPU baseline sample")
@@ -77,23 +82,27 @@ def main():
     else:
         topo = T.config_fullview()
         routes, dst_range = topo.route_array(), None
-        workload = ("config3: 64B synthetic burst, 1M-route full-view FIB (fib_inject)" if args.workload == "fullview64"
-                    else "config4: IMIX 64/570/1518 synthetic burst, full-view FIB, header lines staged")
+        workload = {"fullview64": "config3: 64B synthetic burst, 1M-route full-view FIB (fib_inject)",
+                    "imix": "config4: IMIX 64/570/1518 synthetic burst, full-view FIB, header lines staged",
+                    "imix_frames": ("config4: IMIX 64/570/1518 synthetic burst, full-view FIB, whole frames "
+                                    f"resident in {args.slot}-byte mbuf-like slots")}[args.workload]
     fp = FastPath(local)
     fp.load(topo)
     info = fp.fib6_info(T.VRF_MAIN) if args.workload == "fullview6" else fp.fib_info(T.VRF_MAIN)
     log(f"[rank {rank}] topology + FIB loaded in {time.time() - t0:.1f}s: {info}")
 
     # ---- synthetic RX stream of this GPU (seed 0x67721000 + g)
-    n = args.batch
+    n = args.batch or (1 << 22 if args.workload == "imix_frames" else 1 << 24)
     seed = rep.seed()
     imix = args.workload == "imix"
+    in_stride = args.slot if args.workload == "imix_frames" else abi.LINE
     t0 = time.time()
     if args.workload == "fullview6":
         r6 = topo.route6_array()
         frames, meta = S.stream6(n, seed, r6[r6["prefixlen"] < 128])
     else:
-        frames, meta = S.stream(n, seed, routes=routes, dst_range=dst_range, imix=imix, lines_only=imix)
+        frames, meta = S.stream(n, seed, routes=routes, dst_range=dst_range, imix=imix or in_stride > abi.LINE,
+                                lines_only=imix, stride=in_stride)
     d_in = torch.from_numpy(frames.reshape(-1)).to(dev)
     d_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
     d_out = torch.empty(n * abi.LINE, dtype=torch.uint8, device=dev)
@@ -104,7 +113,7 @@ def main():
     q = fp.queue(shared_stream(dev))
 
     def step():
-        q.submit(d_in, d_out, d_meta, d_v, n, in_stride=abi.LINE, out_stride=abi.LINE, lines_only=imix)
+        q.submit(d_in, d_out, d_meta, d_v, n, in_stride=in_stride, out_stride=abi.LINE, lines_only=imix)
 
     for _ in range(args.warmup):
         step()
@@ -182,7 +191,7 @@ def main():
     # ---- host-memory path (PCIe-inclusive): reported, never `value`
     if rank == 0 and world == 1 and not args.no_host_path:
         hn = min(n, 1 << 23)
-        lines = torch.from_numpy(frames[:hn].reshape(-1)[: hn * abi.LINE]).pin_memory()
+        lines = torch.from_numpy(np.ascontiguousarray(frames[:hn, :abi.LINE]).reshape(-1)).pin_memory()
         hmeta = torch.from_numpy(meta[:hn].view(np.uint8)).pin_memory()
         hout = torch.empty(hn * abi.LINE, dtype=torch.uint8).pin_memory()
         hv = torch.empty(hn * 8, dtype=torch.uint8).pin_memory()
