@@ -161,6 +161,7 @@ struct gr_hip_ctx {
 	int host_direct; // host path: the kernel reads / writes pinned host memory itself
 	int node_ptrs; // node path: frames in registered memory are handed over by address
 	std::vector<host_range> hregs; // registered host memory, by host address
+	std::mutex occ_mu; // the occupancy cache below (launches run concurrently)
 	int occ_ring[8]; // by variant, at occ_ring_nhf staged fast adjacencies, geometry occ_ring_cfg
 	uint32_t occ_ring_nhf;
 	int occ_ring_cfg;
@@ -1346,15 +1347,20 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	int variant = (stats ? FWD4_V_STATS : 0) | c->nt | ((b->flags & GR_HIP_BATCH_F_FRAME_PTRS) ? FWD4_V_PTRS : 0);
 	uint32_t tiles = (b->n + 63) / 64;
 	A.nhf_lds = c->nh_hi < gr_fwd4_ring_nhf_max() ? c->nh_hi : gr_fwd4_ring_nhf_max();
-	if (A.nhf_lds != c->occ_ring_nhf || c->ring_cfg != c->occ_ring_cfg) {
-		for (int v = 0; v < 8; v++)
-			c->occ_ring[v] = gr_fwd4_ring_occupancy(v, c->ring_cfg, A.nhf_lds);
-		c->occ_ring_nhf = A.nhf_lds;
-		c->occ_ring_cfg = c->ring_cfg;
+	int occ;
+	{
+		std::lock_guard<std::mutex> ol(c->occ_mu);
+		if (A.nhf_lds != c->occ_ring_nhf || c->ring_cfg != c->occ_ring_cfg) {
+			for (int v = 0; v < 8; v++)
+				c->occ_ring[v] = gr_fwd4_ring_occupancy(v, c->ring_cfg, A.nhf_lds);
+			c->occ_ring_nhf = A.nhf_lds;
+			c->occ_ring_cfg = c->ring_cfg;
+		}
+		occ = c->occ_ring[variant];
 	}
 	uint32_t per_cu = c->wg_per_cu > 0 ? (uint32_t)c->wg_per_cu : RING_WG_PER_CU;
-	if (c->occ_ring[variant] > 0 && per_cu > (uint32_t)c->occ_ring[variant])
-		per_cu = (uint32_t)c->occ_ring[variant];
+	if (occ > 0 && per_cu > (uint32_t)occ)
+		per_cu = (uint32_t)occ;
 	uint32_t grid = (uint32_t)c->n_cu * per_cu;
 	if (grid > tiles)
 		grid = tiles;
@@ -1438,6 +1444,9 @@ extern "C" int gr_hip_fwd4_submit(gr_hip_queue_t *q, const struct gr_hip_batch *
 	int ok = batch_ok(b);
 	if (ok <= 0)
 		return ok;
+	// enqueued entirely before a control-plane update's quiesce or entirely
+	// after its upload: the update holds the lock exclusively (RCU analogue)
+	std::shared_lock<std::shared_mutex> l(q->ctx->mu);
 	return launch(q, q->s, b, true);
 }
 
@@ -1484,6 +1493,7 @@ extern "C" int gr_hip_fwd4_host(
 		return -EINVAL;
 	gr_hip_ctx *c = q->ctx;
 	hipSetDevice(c->dev);
+	std::shared_lock<std::shared_mutex> l(c->mu); // see gr_hip_fwd4_submit
 	if (c->host_direct) {
 		// zero-copy: the kernel's loaders and storers move the lines over
 		// PCIe themselves, both directions at once, no staging copies
@@ -1547,7 +1557,7 @@ static const host_range *hreg_find(const gr_hip_ctx *c, uintptr_t p) {
 // Every frame in registered memory and 16-byte aligned: their device
 // addresses into ptrs[n].
 static bool host_dev_ptr_ok(gr_hip_ctx *c, const gr_hip_mbuf *m, uint32_t n, uint64_t *ptrs) {
-	std::shared_lock<std::shared_mutex> l(c->mu);
+	// the caller holds c->mu
 	if (c->hregs.empty())
 		return false;
 	const host_range *hit = &c->hregs[0];
@@ -1643,6 +1653,7 @@ extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uin
 		HCK(hipHostMalloc((void **)&q->node_v, (size_t)n * sizeof(gr_hip_verdict), hipHostMallocDefault));
 		q->node_cap = n;
 	}
+	std::shared_lock<std::shared_mutex> lk(c->mu); // see gr_hip_fwd4_submit
 	if (c->node_ptrs && host_dev_ptr_ok(c, m, n, reinterpret_cast<uint64_t *>(q->node_lines))) {
 		// the frames are device-accessible: hand them over by address, the
 		// kernel reads and rewrites them in place over PCIe
@@ -1660,10 +1671,10 @@ extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uin
 		if ((r = launch(q, q->s, &b, true)) < 0)
 			return r;
 		HCK(hipStreamSynchronize(q->s));
-		std::shared_lock<std::shared_mutex> l(c->mu);
 		return gr_hip_node_apply(m, n, nullptr, 0, q->node_v, c->ifaces.data(), c->max_ifaces, c->nh.data(),
 					 (uint32_t)c->nh.size(), burst, stats);
 	}
+	lk.unlock(); // gr_hip_fwd4_host takes it itself
 	int r = gr_hip_node_stage(m, n, q->node_lines, q->node_meta);
 	if (r < 0)
 		return r;

@@ -535,3 +535,79 @@ def test_fib6_lookup_host_scoping(fastpath):
         for iface in [T.PORT_IFACE[0], T.PORT_IFACE[1]]:
             ip = T.ip6(dst)
             assert fastpath.fib6_lookup(1, ip, iface) == o.lpm6(1, ip, iface), (dst, iface)
+
+
+def test_concurrent_queues_and_fib_updates(fastpath):
+    """Two worker queues forward full-view streams in their own threads
+    while the control thread adds and deletes routes (disjoint from the
+    streams' destinations) and switches the device FIB format back and forth
+    (full re-uploads, RX views re-pointed). Every batch must equal the
+    oracle: a kernel runs entirely before an update or entirely after it
+    (grout's RCU around FIB changes, route.c:740-771); the routes added last
+    take effect."""
+    import threading
+
+    import torch
+    t = T.config_fullview(count=100_000)
+    t.fibs[T.VRF_MAIN] = (100_200, 0)  # room for the routes added below
+    fresh_fastpath_state(fastpath, t)
+    dev = torch.device("cuda")
+    work = []
+    for w in range(2):
+        fr, me = S.stream(1 << 18, 0xC0C0 + w, routes=t.route_array())
+        lines, v, _ = oracle.Oracle(t).process(fr, me)
+        work.append(dict(
+            d_in=torch.from_numpy(fr.reshape(-1)).to(dev), d_me=torch.from_numpy(me.view(np.uint8)).to(dev),
+            want_l=torch.from_numpy(lines.reshape(-1)).to(dev), want_v=torch.from_numpy(v.view(np.uint8)).to(dev),
+            n=len(me), bad=0, iters=0))
+    torch.cuda.synchronize()
+    stop = threading.Event()
+    errors = []
+
+    def worker(wk):
+        try:
+            q = fastpath.queue()  # its own stream
+            d_out = torch.empty(wk["n"] * abi.LINE, dtype=torch.uint8, device=dev)
+            d_v = torch.empty(wk["n"] * 8, dtype=torch.uint8, device=dev)
+            while not stop.is_set() or wk["iters"] < 5:
+                d_out.zero_()
+                d_v.zero_()
+                torch.cuda.synchronize()
+                q.submit(wk["d_in"], d_out, wk["d_me"], d_v, wk["n"])
+                q.sync()
+                if not (torch.equal(d_out, wk["want_l"]) and torch.equal(d_v, wk["want_v"])):
+                    wk["bad"] += 1
+                wk["iters"] += 1
+            q.close()
+        except Exception as e:  # reported by the main thread
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(wk,)) for wk in work]
+    for th in threads:
+        th.start()
+    nh = int(t.route_array()["nh"][0])
+    try:
+        for i in range(24):
+            r = np.zeros(4, dtype=abi.ROUTE_DT)
+            for j, (ip, plen) in enumerate([("200.1.%d.0" % i, 24), ("201.%d.0.0" % i, 16),
+                                            ("202.0.%d.7" % i, 32), ("203.%d.0.0" % (i % 8), 13)]):
+                r[j]["ip"], r[j]["prefixlen"], r[j]["vrf_id"], r[j]["nh"] = T.ip4(ip), plen, 1, nh
+            fastpath.route_add(r, replace=True)
+            if i % 3 == 2:
+                fastpath.route_del(1, T.ip4("200.1.%d.0" % (i - 1)), 24)
+            if i % 6 == 5:
+                fastpath.tune("fib_format", 1 if (i // 6) % 2 == 0 else 2)
+            fastpath.fib_commit(1)
+    finally:
+        stop.set()
+        for th in threads:
+            th.join(timeout=120)
+        fastpath.tune("fib_format", 2)
+    assert not errors, errors
+    assert all(not th.is_alive() for th in threads)
+    assert all(wk["iters"] >= 5 for wk in work), [wk["iters"] for wk in work]
+    assert [wk["bad"] for wk in work] == [0, 0]
+    assert fastpath.fib_lookup(1, T.ip4("200.1.23.9")) == nh
+    assert fastpath.fib_lookup(1, T.ip4("200.1.22.9")) == 0  # deleted at i = 23
+    fastpath.fib_commit(1)
+    fresh_fastpath_state(fastpath, T.config_single_route())  # drop the modified state
