@@ -38,7 +38,7 @@
 static_assert(sizeof(struct gr_hip_mbuf) == 40 && offsetof(struct gr_hip_mbuf, nh) == 32, "gr_hip_mbuf layout");
 static_assert(sizeof(struct gr_hip_node_stats) == 16 * GR_HIP_NODE_COUNT, "gr_hip_node_stats layout");
 
-extern "C" int gr_hip_edge_node(uint8_t edge, uint32_t nh, int ip6) {
+static inline int edge_node(uint8_t edge, uint32_t nh, int ip6) {
 	switch (edge) {
 	case GR_HIP_E_PUNT:
 		return -1;
@@ -109,6 +109,10 @@ extern "C" int gr_hip_edge_node(uint8_t edge, uint32_t nh, int ip6) {
 	}
 }
 
+extern "C" int gr_hip_edge_node(uint8_t edge, uint32_t nh, int ip6) {
+	return edge_node(edge, nh, ip6);
+}
+
 extern "C" int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, void *lines, struct gr_hip_pkt_meta *meta) {
 	if (n && (m == nullptr || meta == nullptr))
 		return -EINVAL;
@@ -162,8 +166,15 @@ extern "C" int gr_hip_node_apply(
 	static const int path6[] = {GR_HIP_NODE_IFACE_INPUT, GR_HIP_NODE_ETH_INPUT, GR_HIP_NODE_IP6_INPUT,
 				    GR_HIP_NODE_IP6_FORWARD, GR_HIP_NODE_IP6_OUTPUT, GR_HIP_NODE_ETH_OUTPUT,
 				    GR_HIP_NODE_IFACE_OUTPUT};
+	// position of each node on a packet's path (-1: not on it), per family
+	static const int8_t depth_of[2][GR_HIP_NODE_COUNT] = {
+		{0, 1, 2, 3, 4, 5, 6, -1, -1, -1}, // IPv4: path4
+		{0, 1, -1, -1, -1, 5, 6, 2, 3, 4}, // IPv6: path6
+	};
+	static_assert(GR_HIP_NODE_COUNT == 10 && GR_HIP_NODE_IP6_INPUT == 7, "node order");
+	uint32_t ended[2][7] = {}; // packets of the walk that stopped at depth d, per family
 	uint32_t reach[GR_HIP_NODE_COUNT] = {};
-	uint32_t sent4 = 0, sent6 = 0; // what ip_output / ip6_output enqueued to eth_output
+	uint32_t left = burst; // packets left in the current graph walk
 	// frames read (the ether type) and written back: prefetch them, the loop
 	// is bound by their cache misses
 	constexpr uint32_t AHEAD = 16;
@@ -177,21 +188,15 @@ extern "C" int gr_hip_node_apply(
 		// lines NULL: the GPU rewrote the frames in place already
 		const uint8_t *line = L != nullptr ? L + (size_t)i * line_stride : static_cast<const uint8_t *>(b.frame);
 		const bool ip6 = line[12] == 0x86 && line[13] == 0xdd; // RTE_ETHER_TYPE_IPV6
-		const int node = gr_hip_edge_node(v.edge, v.nh, ip6);
+		const int node = edge_node(v.edge, v.nh, ip6);
 		if (node < -1)
 			return -EINVAL;
 		b.edge = v.edge;
 		if (node >= 0) {
-			const int *path = ip6 ? path6 : path4;
-			int depth = 0; // position of `node` on the packet's path
-			while (depth < 7 && path[depth] != node)
-				depth++;
-			if (depth == 7)
+			const int depth = depth_of[ip6][node]; // position of `node` on the packet's path
+			if (depth < 0)
 				return -EINVAL;
-			for (int k = 0; k <= depth; k++)
-				reach[path[k]]++;
-			if (depth >= 5)
-				(ip6 ? sent6 : sent4)++;
+			ended[ip6][depth]++;
 			// VLAN demux in iface_input: the tag was consumed
 			const bool demuxed = b.vlan_id != 0 && v.edge != GR_HIP_E_IFACE_INPUT_UNKNOWN_VLAN && b.iface < n_ifaces
 				&& ifaces != nullptr && ifaces[b.iface].id == b.iface
@@ -234,19 +239,34 @@ extern "C" int gr_hip_node_apply(
 			b.domain = v.domain;
 			b.nh = v.nh;
 		}
-		if (stats != nullptr && ((i + 1) % burst == 0 || i + 1 == n)) {
+		if (--left == 0 || i + 1 == n) { // a graph walk of `burst` packets ends here
+			left = burst;
+			if (stats == nullptr)
+				continue;
+			// a packet that stopped at depth d passed every node before it
+			uint32_t sent[2] = {0, 0}; // what ip_output / ip6_output enqueued to eth_output
+			for (int f = 0; f < 2; f++) {
+				const int *path = f ? path6 : path4;
+				uint32_t from = 0;
+				for (int d = 6; d >= 0; d--) {
+					from += ended[f][d];
+					reach[path[d]] += from;
+					if (d == 5)
+						sent[f] = from;
+					ended[f][d] = 0;
+				}
+			}
 			for (int k = 0; k < GR_HIP_NODE_COUNT; k++) {
 				// ip_output / ip6_output return only what they sent to eth_output
 				uint32_t ret = reach[k];
 				if (k == GR_HIP_NODE_IP_OUTPUT)
-					ret = sent4;
+					ret = sent[0];
 				else if (k == GR_HIP_NODE_IP6_OUTPUT)
-					ret = sent6;
+					ret = sent[1];
 				stats->packets[k] += ret;
 				stats->calls[k] += reach[k] != 0;
 				reach[k] = 0;
 			}
-			sent4 = sent6 = 0;
 		}
 	}
 	return 0;
