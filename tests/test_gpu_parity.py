@@ -435,6 +435,29 @@ def test_many_nexthops_fast_adjacency(fastpath):
     assert (g[1]["nh"] > 2304).sum() > len(me) // 4
 
 
+def test_high_slots_fall_back_to_4byte_fib(fastpath):
+    """Nexthop slots past 15 bits (up to the last of 2^17) cannot live in the
+    2-byte FIB formats: the commit falls back to 4-byte DIR24_8 entries by
+    itself, and forwarding stays bit-exact."""
+    t = T.base_ports(max_routes=20_010)
+    first = (1 << 17) - 400
+    for j in range(400):
+        t.add_nexthop(T.PORT_IFACE[1 + j % 3], f"100.66.{j >> 8}.{j & 255}", "02:00:00:03:%02x:%02x" % (j >> 8, j & 255),
+                      slot=first + j)
+    routes = np.zeros(20_000, dtype=abi.ROUTE_DT)
+    abi.check("gr_synth_fullview_routes",
+              abi.host().gr_synth_fullview_routes(20_000, T.VRF_MAIN, first, 400, routes.ctypes.data))
+    t.add_routes(routes)
+    t.add_address(T.PORT_IFACE[0], "172.16.0.1/24")
+    fr, me = S.stream(1 << 18, 0x7FFF, routes=t.route_array())
+    o = oracle.Oracle(t).process(fr, me)
+    g = run_gpu(fastpath, t, fr, me)
+    compare(o, g)
+    assert fastpath.tune("fib_format_of", 1) == 0  # 4-byte entries
+    assert (g[1]["edge"] == abi.EDGE["port_output"]).mean() > 0.99
+    assert g[1]["nh"].min() >= first and g[1]["nh"].max() > (1 << 15)
+
+
 @pytest.mark.parametrize("cfg", range(9))
 def test_ring_geometries(fastpath, cfg):
     """Every ring geometry (loaders / storers / slots / tiles in flight) of
