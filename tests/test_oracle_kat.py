@@ -249,3 +249,42 @@ def test_fib6_path_compression_fullview6():
     assert host.gr_fib6_build(f) == 0
     check(r, 20_000)
     host.gr_fib6_free(f)
+
+
+# ---- the same known answers through the GPU (the reference's expectations,
+# not the oracle's output, are the check)
+def _raw3():
+    f = bytearray(kat_header(version=3, cksum=0))
+    s = sum(int.from_bytes(f[14 + i:16 + i], "little") for i in range(0, 20, 2))
+    s = (s & 0xFFFF) + (s >> 16)
+    s = (s & 0xFFFF) + (s >> 16)
+    f[24:26] = s.to_bytes(2, "little")
+    return bytes(f)
+
+
+GPU_KATS = [  # (reference test, topology kwargs, frame, pkt_len or None, expected edge)
+    ("ip_input.c:302-312", {}, lambda: kat_header(), 14 + 10, "ip_input_bad_length"),
+    ("ip_input.c:314-323", {}, lambda: kat_header(cksum=0x666), None, "ip_input_bad_checksum"),
+    ("ip_input.c:325-335", {}, lambda: kat_header(version=5), None, "ip_input_bad_version"),
+    ("ip_input.c:337-349", {}, _raw3, None, "ip_input_bad_checksum"),
+    ("ip_input.c:351-361", {}, lambda: kat_header(total_len=10), None, "ip_input_bad_length"),
+    ("ip_input.c:363-383", dict(snat_dynamic=True, local_nh=True), lambda: kat_header(), None, "ip_input_local_ct"),
+    ("ip6_input.c:245-253", {}, lambda: kat6(version=5), None, "ip6_input_bad_version"),
+    ("ip6_input.c:255-266", {}, lambda: kat6(src="ffff:ffff:ffff:ffff:ffff:ffff:ffff:ffff"), None,
+     "ip6_input_bad_addr"),
+    ("ip6_input.c:268-279", {}, lambda: kat6(dst="::"), None, "ip6_input_bad_addr"),
+    ("ip6_input.c:281-301 scope none", {}, lambda: kat6(dst="ff00::1"), None, "ip6_input_bad_addr"),
+    ("ip6_input.c:281-301 iface-local", {}, lambda: kat6(dst="ff01::1"), None, "ip6_input_bad_addr"),
+    ("ip6_input.c:303-311", {}, lambda: kat6(), 14 + 20, "ip6_input_bad_length"),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ref,topo_kw,frame,pkt_len,expect", GPU_KATS, ids=[k[0] for k in GPU_KATS])
+def test_kat_gpu(fastpath, ref, topo_kw, frame, pkt_len, expect):
+    """grout's own unit-test cases (ip_input.c, ip6_input.c) on the GPU path."""
+    from golden_util import run_gpu
+    t = kat_topo(**topo_kw)
+    arr, meta = S.pack([frame()], pkt_lens=None if pkt_len is None else [pkt_len])
+    _, v, _ = run_gpu(fastpath, t, arr, meta)
+    assert abi.EDGE_NAMES[v["edge"][0]] == expect, ref
