@@ -4,7 +4,7 @@ its topology, HIP path against the oracle, bit-exact.
 
 The corpus (scenarios.py) places one packet on every edge. Each seed here
 perturbs it further. Frames get bit flips in the first 64 bytes, random
-destinations under random routes, random TTL / hop limits, ingress ifaces,
+destinations under random IPv4 and IPv6 routes, random TTL / hop limits, ingress ifaces,
 VLAN ids, checksum offload status, lengths and RSS hashes, and a recomputed
 header checksum for most of them, so that packets reach the deep nodes.
 The topology gets ifaces brought down, MTUs changed, and nexthop states,
@@ -80,6 +80,15 @@ def mutate_frames(fr, me, t, rng, n=N_PKTS):
     mask = ((np.uint64(0xFFFFFFFF) << (np.uint64(32) - plen)) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
     dst = (rt["ip"].astype(np.uint32) & mask) | (host & ~mask)
     fr[rows, 30:34] = dst.astype(">u4").view(np.uint8).reshape(-1, 4)
+    # IPv6 destinations under random routes: prefix bits kept, the rest random
+    routes6 = t.route6_array()
+    rows = np.nonzero(v6 & (rng.random(n) < 0.4))[0]
+    rt6 = routes6[rng.integers(len(routes6), size=len(rows))]
+    bits = np.arange(128)
+    keep = bits[None, :] < rt6["prefixlen"][:, None].astype(np.int64)  # per bit, MSB first
+    pfx = np.unpackbits(rt6["ip"], axis=1).astype(bool)
+    rnd = rng.random((len(rows), 128)) < 0.5
+    fr[rows, 38:54] = np.packbits(np.where(keep, pfx, rnd), axis=1)
     rows = np.nonzero(v4 & (rng.random(n) < 0.2))[0]
     fr[rows, 22] = rng.choice([0, 1, 2, 255], len(rows))
     rows = np.nonzero(v6 & (rng.random(n) < 0.2))[0]
