@@ -42,6 +42,10 @@ def parse():
     p.add_argument("--slot", type=int, default=2240,
                    help="imix_frames: bytes per frame slot (2240 = grout's mbuf object: 128 B rte_mbuf + "
                         "64 B priv + 2048 B data room, mempool.c:57-100)")
+    p.add_argument("--placement", default="calibrated", choices=["calibrated", "plain"],
+                   help="calibrated: batch buffers from gr_hip_batch_alloc, output lines re-placed by gr_hip_batch_place over "
+                        "--candidates allocations; plain: torch allocations")
+    p.add_argument("--candidates", type=int, default=6)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-path", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="wall time of the CPU baseline sample")
@@ -103,10 +107,25 @@ def main():
     else:
         frames, meta = S.stream(n, seed, routes=routes, dst_range=dst_range, imix=imix or in_stride > abi.LINE,
                                 lines_only=imix, stride=in_stride)
-    d_in = torch.from_numpy(frames.reshape(-1)).to(dev)
-    d_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
-    d_out = torch.empty(n * abi.LINE, dtype=torch.uint8, device=dev)
-    d_v = torch.empty(n * 8, dtype=torch.uint8, device=dev)
+    batch = None
+    if args.placement == "calibrated":
+        # gr_hip_batch_alloc + gr_hip_batch_place: the output lines' pages are
+        # picked among --candidates allocations by timing them over this batch
+        # 
+        batch = fp.batch_alloc(n, in_stride)
+        for dst, src in ((batch.in_frames, frames), (batch.meta, meta)):
+            src = np.ascontiguousarray(src)
+            abi.check("gr_hip_memcpy_h2d", fp.lib.gr_hip_memcpy_h2d(fp.h, dst, src.ctypes.data, src.nbytes))
+        if imix:
+            batch.flags = abi.BATCH_F_LINES_ONLY
+        fp.batch_place(batch, args.candidates)
+        batch.flags = 0
+        d_in, d_out, d_meta, d_v = batch.in_frames, batch.out_lines, batch.meta, batch.verdicts
+    else:
+        d_in = torch.from_numpy(frames.reshape(-1)).to(dev)
+        d_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
+        d_out = torch.empty(n * abi.LINE, dtype=torch.uint8, device=dev)
+        d_v = torch.empty(n * 8, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     log(f"[rank {rank}] {n} packets generated and resident in {time.time() - t0:.1f}s")
 
@@ -129,7 +148,13 @@ def main():
     kern_ms, kcount = q.kernel_ms(args.steps)
     tmax = rep.max_over_ranks(elapsed)
 
-    edges = torch.bincount(d_v.view(n, 8)[:, 0].long(), minlength=abi.E_COUNT).cpu().numpy()
+    if batch is not None:
+        vh = np.empty(n, dtype=abi.VERDICT_DT)
+        abi.check("gr_hip_memcpy_d2h", fp.lib.gr_hip_memcpy_d2h(fp.h, vh.ctypes.data, d_v, vh.nbytes))
+        edges = np.bincount(vh["edge"], minlength=abi.E_COUNT)
+        fp.batch_free(batch)
+    else:
+        edges = torch.bincount(d_v.view(n, 8)[:, 0].long(), minlength=abi.E_COUNT).cpu().numpy()
     fwd_frac = float(edges[abi.EDGE["port_output"]]) / n
     value = rep.aggregate_mpps(n, args.steps, tmax)
     avg_kernel_s = kern_ms / max(kcount, 1) / 1e3
@@ -171,6 +196,8 @@ def main():
                else {"tbl8_groups_used": int(info["tbl8_used"])}),
             "parallelism": f"replicas x{world} (one RX stream + FIB replica per GPU, no collective)",
             "forwarded_frac": round(fwd_frac, 6),
+            "placement": (f"calibrated: output lines = fastest of {args.candidates + 1} allocations, each timed "
+                          "over this batch (gr_hip_batch_place)" if batch is not None else "plain torch allocations"),
         },
         "roofline": {
             "bound": "hbm",

@@ -168,6 +168,9 @@ HIP_API = {
     "gr_hip_host_free": (_I, [_P, _P]),
     "gr_hip_dev_alloc": (_I, [_P, ctypes.c_size_t, PP]),
     "gr_hip_dev_free": (_I, [_P, _P]),
+    "gr_hip_batch_alloc": (_I, [_P, _U32, _U32, ctypes.POINTER(Batch)]),
+    "gr_hip_batch_place": (_I, [_P, ctypes.POINTER(Batch), _U32]),
+    "gr_hip_batch_free": (_I, [_P, ctypes.POINTER(Batch)]),
     "gr_hip_memcpy_h2d": (_I, [_P, _P, _P, ctypes.c_size_t]),
     "gr_hip_memcpy_d2h": (_I, [_P, _P, _P, ctypes.c_size_t]),
     "gr_hip_host_register": (_I, [_P, _P, ctypes.c_size_t]),

@@ -147,6 +147,10 @@ struct fwd4_params {
 	uint32_t out_stride;
 	uint32_t readable; // frame bytes present per packet (64 or in_stride)
 	uint32_t nhf_lds; // fwd4_ring.hip: fast adjacencies 1..nhf_lds staged in LDS
+	uint32_t chunk; // fwd4_ring.hip: 0 = workgroup b takes tiles b, b + G, ...;
+	                // else the contiguous tiles [b * chunk, (b + 1) * chunk)
+	uint32_t order; // 2: XCD x (= b % 8) takes region [x * chunk, (x + 1) * chunk),
+	                // its workgroups interleaved in it (grid % 8 == 0)
 };
 
 // Kernel variants (bit mask, gr_hip_tune): counters, nontemporal loads and

@@ -23,7 +23,8 @@
 // -> compute), done[s] (compute -> storer), free[s] (storer -> loader).
 // Every wait is bounded (RING_SPIN_MAX polls); a wave that gives up sets
 // the workgroup's abort word and every role leaves its loop, so the grid
-// always drains. Tiles of a workgroup are b, b + G, b + 2G ... (G = grid).
+// always drains. Tiles of a workgroup are b, b + G, b + 2G ... (G = grid),
+// or one contiguous run per workgroup (fwd4_params.chunk).
 #include "fwd4_chain.h"
 
 #define RING_GLDS_PER_TILE 6 // 4 x 1 KiB of lines + 2 x 256 B of metadata
@@ -126,6 +127,15 @@ __device__ __forceinline__ bool flag_wait(L_t &L, const uint32_t *f, uint32_t wa
 	}
 }
 
+// Tile k of this workgroup (see fwd4_params.chunk).
+__device__ __forceinline__ uint32_t tile_of(const fwd4_params &A, uint32_t k) {
+	if (A.order == 2) { // XCD x = b % 8 interleaves its workgroups over region x
+		const uint32_t x = blockIdx.x & 7, l = blockIdx.x >> 3, per = gridDim.x >> 3;
+		return x * A.chunk + l + k * per;
+	}
+	return A.chunk ? blockIdx.x * A.chunk + k : blockIdx.x + k * gridDim.x;
+}
+
 // Frame pointers of tile t, one per lane (rows past the batch repeat its last
 // packet, so that every tile issues the same number of loads).
 __device__ __forceinline__ uint64_t load_ptr(const fwd4_params &A, uint32_t t, uint32_t lane) {
@@ -145,14 +155,13 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
 // tile, issued before the tile's DMA, which only makes the waits longer).
 template <class C, bool NT, bool PTRS>
 __device__ void ring_loader(const fwd4_params &A, ring_lds<C, PTRS> &L, uint32_t n_local, uint32_t j, uint32_t lane) {
-	const uint32_t G = gridDim.x;
 	const uint32_t prow = lane >> 2;
 	const uint32_t pchunk = (lane & 3) ^ ((lane >> 4) & 3); // chunk this lane lands in slot lane & 3
 	uint32_t pub = j; // oldest of this loader's tiles not yet published
 	bool ok = true;
 	uint64_t pnext = 0;
 	if (PTRS && j < n_local)
-		pnext = load_ptr(A, blockIdx.x + j * G, lane);
+		pnext = load_ptr(A, tile_of(A, j), lane);
 	for (uint32_t k = j; k < n_local && ok; k += C::LOADERS) {
 		const uint32_t s = k % C::SLOTS;
 		if (k >= C::SLOTS && (int32_t)(flag_get(&L.free_[s]) - (k - C::SLOTS + 1)) < 0) {
@@ -164,13 +173,13 @@ __device__ void ring_loader(const fwd4_params &A, ring_lds<C, PTRS> &L, uint32_t
 			if (!ok)
 				break;
 		}
-		const uint32_t t = blockIdx.x + k * G;
+		const uint32_t t = tile_of(A, k);
 		const uint32_t base = t * 64, last = min(64u, A.n - base) - 1;
 		uint64_t pk = 0;
 		if (PTRS) {
 			pk = pnext;
 			if (k + C::LOADERS < n_local)
-				pnext = load_ptr(A, blockIdx.x + (k + C::LOADERS) * G, lane);
+				pnext = load_ptr(A, tile_of(A, k + C::LOADERS), lane);
 			if (k == j)
 				wait_vmcnt<0>();
 			else
@@ -207,14 +216,13 @@ __device__ void ring_loader(const fwd4_params &A, ring_lds<C, PTRS> &L, uint32_t
 
 template <class C, bool NT, bool PTRS>
 __device__ void ring_storer(const fwd4_params &A, ring_lds<C, PTRS> &L, uint32_t n_local, uint32_t j, uint32_t lane) {
-	const uint32_t G = gridDim.x;
 	const uint32_t prow = lane >> 2, part = lane & 3;
 	const uint32_t pslot = (part ^ ((lane >> 4) & 3)) << 4;
 	for (uint32_t k = j; k < n_local; k += C::STORERS) {
 		const uint32_t s = k % C::SLOTS;
 		if (!flag_wait(L, &L.done[s], k + 1))
 			break;
-		const uint32_t t = blockIdx.x + k * G;
+		const uint32_t t = tile_of(A, k);
 		const uint32_t base = t * 64, cnt = min(64u, A.n - base);
 		u4v o[4];
 #pragma unroll
@@ -251,12 +259,11 @@ __device__ void ring_storer(const fwd4_params &A, ring_lds<C, PTRS> &L, uint32_t
 template <class C, bool STATS, bool PTRS>
 __device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds<C, PTRS> &L, stat_slot *slots,
 			     const uint4 *nhf_lds, uint32_t n_local, uint32_t c, uint32_t lane) {
-	const uint32_t G = gridDim.x;
 	for (uint32_t k = c; k < n_local; k += C::COMPUTE) {
 		const uint32_t s = k % C::SLOTS;
 		if (!flag_wait(L, &L.ready[s], k + 1))
 			break;
-		const uint32_t t = blockIdx.x + k * G;
+		const uint32_t t = tile_of(A, k);
 		const uint32_t base = t * 64, cnt = min(64u, A.n - base);
 		const bool live = lane < cnt;
 		uint8_t *R = L.lines[s];
@@ -343,7 +350,15 @@ __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params 
 	__syncthreads();
 
 	const uint32_t n_tiles = (A.n + 63) >> 6;
-	const uint32_t n_local = blockIdx.x < n_tiles ? (n_tiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+	uint32_t n_local;
+	if (A.order == 2) {
+		const uint32_t x = blockIdx.x & 7, l = blockIdx.x >> 3, per = gridDim.x >> 3;
+		const uint32_t lo = x * A.chunk + l, hi = min((x + 1) * A.chunk, n_tiles);
+		n_local = lo < hi ? (hi - 1 - lo) / per + 1 : 0;
+	} else if (A.chunk)
+		n_local = blockIdx.x * A.chunk < n_tiles ? min(A.chunk, n_tiles - blockIdx.x * A.chunk) : 0;
+	else
+		n_local = blockIdx.x < n_tiles ? (n_tiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
 	if (wv < C::LOADERS) {
 		ring_loader<C, NT, PTRS>(A, L, n_local, wv, lane);
 	} else if (wv < C::LOADERS + C::STORERS) {

@@ -160,6 +160,7 @@ struct gr_hip_ctx {
 	int ring_cfg; // ring geometry (fwd4_ring.hip ring_cfgN)
 	int host_direct; // host path: the kernel reads / writes pinned host memory itself
 	int node_ptrs; // node path: frames in registered memory are handed over by address
+	int tile_order; // 0: workgroup b takes tiles b, b + G, ...; 1: one contiguous run each
 	std::vector<host_range> hregs; // registered host memory, by host address
 	std::mutex occ_mu; // the occupancy cache below (launches run concurrently)
 	int occ_ring[8]; // by variant, at occ_ring_nhf staged fast adjacencies, geometry occ_ring_cfg
@@ -567,6 +568,7 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->ring_cfg = 2; // 16 waves: 2 loaders, 2 storers, 12 compute, 16 slots
 	c->host_direct = 1; // measured 1.9x the staged copies
 	c->node_ptrs = 1;
+	c->tile_order = 0;
 	for (int v = 0; v < 8; v++)
 		c->occ_ring[v] = gr_fwd4_ring_occupancy(v, 0, 0);
 	c->occ_ring_nhf = 0;
@@ -1364,6 +1366,14 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	uint32_t grid = (uint32_t)c->n_cu * per_cu;
 	if (grid > tiles)
 		grid = tiles;
+	A.order = c->tile_order;
+	A.chunk = 0;
+	if (c->tile_order == 1)
+		A.chunk = (tiles + grid - 1) / grid;
+	if (c->tile_order == 2 && grid % 8 == 0)
+		A.chunk = (tiles + 7) / 8;
+	else if (c->tile_order == 2)
+		A.order = 0;
 	if (timed)
 		HCK(hipEventRecord(q->ev0[slot], s));
 	HCK(gr_fwd4_ring_launch(&A, grid, s, variant, c->ring_cfg));
@@ -1392,6 +1402,10 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		c->fib_fmt = value;
 	} else if (strcmp(key, "node_ptrs") == 0) {
 		c->node_ptrs = value != 0;
+	} else if (strcmp(key, "tile_order") == 0) {
+		if (value < 0 || value > 2)
+			return -EINVAL;
+		c->tile_order = value;
 	} else if (strcmp(key, "host_direct") == 0) {
 		c->host_direct = value != 0;
 	} else if (strcmp(key, "fib_format_of") == 0) { // read: the format VRF `value` is on the device in
@@ -1731,6 +1745,96 @@ extern "C" int gr_hip_dev_free(gr_hip_ctx_t *c, void *p) {
 	if (c == nullptr)
 		return -EINVAL;
 	HCK(hipFree(p));
+	return 0;
+}
+
+extern "C" int gr_hip_batch_alloc(gr_hip_ctx_t *c, uint32_t n, uint32_t in_stride, gr_hip_batch *b) {
+	if (c == nullptr || b == nullptr || n == 0 || n > (1u << 31) || in_stride < GR_HIP_LINE || (in_stride & 15))
+		return -EINVAL;
+	hipSetDevice(c->dev);
+	const size_t sizes[4] = {(size_t)n * in_stride, (size_t)n * GR_HIP_LINE, (size_t)n * 8, (size_t)n * 8};
+	void *p[4] = {nullptr, nullptr, nullptr, nullptr};
+	for (int k = 0; k < 4; k++)
+		if (hipMalloc(&p[k], sizes[k]) != hipSuccess || hipMemset(p[k], 0, sizes[k]) != hipSuccess) {
+			(void)hipGetLastError();
+			for (void *q : p)
+				if (q)
+					hipFree(q);
+			return -ENOMEM;
+		}
+	b->in_frames = p[0];
+	b->out_lines = p[1];
+	b->meta = static_cast<gr_hip_pkt_meta *>(p[2]);
+	b->verdicts = static_cast<gr_hip_verdict *>(p[3]);
+	b->n = n;
+	b->in_stride = in_stride;
+	b->out_stride = GR_HIP_LINE;
+	b->flags = 0;
+	return 0;
+}
+
+extern "C" int gr_hip_batch_place(gr_hip_ctx_t *c, gr_hip_batch *b, uint32_t candidates) {
+	if (c == nullptr || b == nullptr || b->out_lines == nullptr || b->out_stride != GR_HIP_LINE || candidates > 16
+	    || (b->flags & GR_HIP_BATCH_F_FRAME_PTRS))
+		return -EINVAL;
+	int r = batch_ok(b);
+	if (r <= 0)
+		return r ? r : -EINVAL;
+	hipSetDevice(c->dev);
+	const size_t out_b = (size_t)b->n * GR_HIP_LINE;
+	std::vector<void *> outs{b->out_lines};
+	for (uint32_t k = 0; k < candidates; k++) {
+		void *o = nullptr;
+		if (hipMalloc(&o, out_b) != hipSuccess) { // fewer candidates when memory runs short
+			(void)hipGetLastError();
+			break;
+		}
+		outs.push_back(o);
+	}
+	gr_hip_queue_t *q = nullptr;
+	r = outs.size() > 1 ? gr_hip_queue_create(c, nullptr, &q) : 0;
+	size_t pick = 0;
+	if (q != nullptr) {
+		// no counters on this queue: the probe launches run the counter-less
+		// kernel variant, so they neither count nor show up as the counted one
+		hipStreamSynchronize(q->s);
+		hipFree(q->d_stats);
+		q->d_stats = nullptr;
+		float best = 0;
+		for (size_t k = 0; k < outs.size() && r == 0; k++) {
+			gr_hip_batch t = *b;
+			t.out_lines = outs[k];
+			for (int i = 0; i < 6 && r == 0; i++) // 2 warm-up launches, 4 timed
+				r = gr_hip_fwd4_submit(q, &t);
+			float ms = 0;
+			uint32_t cnt = 0;
+			if (r == 0)
+				r = gr_hip_queue_kernel_ms(q, 4, &ms, &cnt);
+			if (r == 0 && (k == 0 || ms < best)) {
+				best = ms;
+				pick = k;
+			}
+		}
+		gr_hip_queue_destroy(q);
+	}
+	if (r)
+		pick = 0; // keep the batch as it was
+	for (size_t k = 0; k < outs.size(); k++)
+		if (k != pick)
+			hipFree(outs[k]);
+	b->out_lines = outs[pick];
+	return r;
+}
+
+extern "C" int gr_hip_batch_free(gr_hip_ctx_t *c, gr_hip_batch *b) {
+	if (c == nullptr || b == nullptr)
+		return -EINVAL;
+	hipSetDevice(c->dev);
+	for (const void *p : {b->in_frames, static_cast<const void *>(b->out_lines), static_cast<const void *>(b->meta),
+			      static_cast<const void *>(b->verdicts)})
+		if (p)
+			hipFree(const_cast<void *>(p));
+	memset(b, 0, sizeof(*b));
 	return 0;
 }
 

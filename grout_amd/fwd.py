@@ -151,6 +151,19 @@ class FastPath:
         for vrf_id in topo.fibs6:
             self.fib6_commit(vrf_id)
 
+    def batch_alloc(self, n, in_stride=64):
+        """Zeroed device buffers of an n-packet batch (gr_hip_batch_alloc); -> abi.Batch."""
+        b = abi.Batch()
+        check("gr_hip_batch_alloc", self.lib.gr_hip_batch_alloc(self.h, n, in_stride, ctypes.byref(b)))
+        return b
+
+    def batch_place(self, b, candidates=6):
+        """gr_hip_batch_place: re-place b's output lines by timing candidates."""
+        check("gr_hip_batch_place", self.lib.gr_hip_batch_place(self.h, ctypes.byref(b), candidates))
+
+    def batch_free(self, b):
+        check("gr_hip_batch_free", self.lib.gr_hip_batch_free(self.h, ctypes.byref(b)))
+
     def queue(self, stream=None):
         q = Queue(self, stream)
         self.queues.append(q)

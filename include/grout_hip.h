@@ -417,6 +417,8 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               chunk copies (pageable buffers always take that path)
 //   "node_ptrs"  1 = gr_hip_node_process hands registered frames over by
 //               address (default), 0 = always stage header lines
+//   "tile_order" 0 = workgroup b takes 64-packet tiles b, b + G, b + 2G ...
+//               (default), 1 = one contiguous run of tiles per workgroup
 //   "fib_format_of" (read) the format VRF `value`'s FIB is on the device in
 //   "occupancy" (read) resident workgroups per CU of the current variant
 // Returns 0 (or the value read), -EINVAL, or -ENOENT for an unknown key.
@@ -448,6 +450,20 @@ int gr_hip_dev_alloc(gr_hip_ctx_t *, size_t bytes, void **dptr);
 int gr_hip_dev_free(gr_hip_ctx_t *, void *dptr);
 int gr_hip_memcpy_h2d(gr_hip_ctx_t *, void *dst, const void *src, size_t bytes);
 int gr_hip_memcpy_d2h(gr_hip_ctx_t *, void *dst, const void *src, size_t bytes);
+// Device buffers of a batch of `n` packets for gr_hip_fwd4_submit: frames
+// (n * in_stride bytes), output lines (n * 64), metadata and verdicts, all
+// zeroed; fills *b (flags 0, out_stride 64). Free with gr_hip_batch_free.
+int gr_hip_batch_alloc(gr_hip_ctx_t *, uint32_t n, uint32_t in_stride, struct gr_hip_batch *b);
+// Where the output lines' HBM pages lie relative to the frames' changes the
+// kernel's time by up to ~20 % (concurrent reads and writes that collide in
+// the memory channels). With the batch's frames and metadata in
+// place, this allocates `candidates` more output-line buffers, times each
+// (and the current one) over the batch on a private queue without counters,
+// keeps the fastest and frees the rest. `b` must come from
+// gr_hip_batch_alloc; its output lines and verdicts are overwritten (with
+// the batch's results). On error the batch is left as it was.
+int gr_hip_batch_place(gr_hip_ctx_t *, struct gr_hip_batch *b, uint32_t candidates);
+int gr_hip_batch_free(gr_hip_ctx_t *, struct gr_hip_batch *b);
 // Pin and map caller memory for the GPU (grout: the mbuf pools' memory), so
 // that frames in it can be handed over by address (GR_HIP_BATCH_F_FRAME_PTRS,
 // gr_hip_node_process). Memory already pinned is recorded as it is.

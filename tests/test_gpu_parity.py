@@ -295,6 +295,56 @@ def test_edge_registration_ip6(fastpath):
             assert getattr(L, fn)(h, key, e) == 0
 
 
+def test_batch_alloc_and_place(fastpath):
+    """gr_hip_batch_alloc: zeroed buffers of the right sizes that a submit
+    can use; gr_hip_batch_place: the re-placed batch still forwards
+    bit-exact, the candidates it did not keep are freed, bad arguments are
+    refused and leave the batch as it was."""
+    t = T.config_single_route()
+    fresh_fastpath_state(fastpath, t)
+    n, stride = 100_003, 128
+    fr, me = S.stream(n, 0xBA7C, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")), stride=stride)
+    L = fastpath.lib
+    want = oracle.Oracle(t).process(fr, me)
+    free0 = torch_free_bytes()
+    b = fastpath.batch_alloc(n, stride)
+    assert b.n == n and b.in_stride == stride and b.out_stride == abi.LINE and b.flags == 0
+    z = np.ones(n, dtype=abi.VERDICT_DT)
+    abi.check("d2h", L.gr_hip_memcpy_d2h(fastpath.h, z.ctypes.data, b.verdicts, z.nbytes))
+    assert not z.view(np.uint8).any()
+    for dst, src in ((b.in_frames, fr), (b.meta, me)):
+        abi.check("h2d", L.gr_hip_memcpy_h2d(fastpath.h, dst, src.ctypes.data, src.nbytes))
+    q = fastpath.queue()
+    for cand in (0, 4):
+        if cand:
+            fastpath.batch_place(b, cand)
+        q.stats(reset=True)
+        abi.check("submit", L.gr_hip_fwd4_submit(q._h, ctypes.byref(b)))
+        q.sync()
+        lines = np.empty((n, abi.LINE), dtype=np.uint8)
+        v = np.empty(n, dtype=abi.VERDICT_DT)
+        abi.check("d2h", L.gr_hip_memcpy_d2h(fastpath.h, lines.ctypes.data, b.out_lines, lines.nbytes))
+        abi.check("d2h", L.gr_hip_memcpy_d2h(fastpath.h, v.ctypes.data, b.verdicts, v.nbytes))
+        compare(want, (lines, v, q.stats()))
+    q.close()
+    keep = b.out_lines
+    b.out_stride = 128
+    assert L.gr_hip_batch_place(fastpath.h, ctypes.byref(b), 2) == -22
+    b.out_stride = abi.LINE
+    assert L.gr_hip_batch_place(fastpath.h, ctypes.byref(b), 17) == -22 and b.out_lines == keep
+    fastpath.batch_free(b)
+    assert b.in_frames is None and b.n == 0
+    assert torch_free_bytes() >= free0 - (64 << 20)  # the candidates did not leak
+    bad = abi.Batch()
+    assert L.gr_hip_batch_alloc(fastpath.h, 0, 64, ctypes.byref(bad)) == -22
+    assert L.gr_hip_batch_alloc(fastpath.h, 64, 72, ctypes.byref(bad)) == -22
+
+
+def torch_free_bytes():
+    import torch
+    return torch.cuda.mem_get_info()[0]
+
+
 def test_empty_and_ragged_batches(fastpath):
     t = T.config_single_route()
     fresh_fastpath_state(fastpath, t)
