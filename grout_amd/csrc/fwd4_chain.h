@@ -62,7 +62,10 @@ __device__ __forceinline__ rxv load_rx_scalar(const kctx &P, uint32_t id) {
 		return r;
 	typedef uint32_t u8s __attribute__((ext_vector_type(8)));
 	u8s v;
-	const fwd4_rx *p = P.rx + id;
+	// the address is wave-uniform; say so, so that it is always in SGPRs
+	const uint64_t a = reinterpret_cast<uint64_t>(P.rx + id);
+	const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)), lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+	const uint64_t p = ((uint64_t)hi << 32) | lo;
 	asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
 	return unpack_rx(uint4{v[0], v[1], v[2], v[3]}, uint4{v[4], v[5], v[6], v[7]});
 }

@@ -318,8 +318,22 @@ __device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds<C, PT
 	}
 }
 
+#ifdef RING_TRACE
+#define RING_TRACE_MAX 4096
+__device__ uint64_t ring_trace[2 * RING_TRACE_MAX];
+extern "C" int gr_fwd4_ring_trace(uint64_t *out, uint32_t n) {
+	if (n > 2 * RING_TRACE_MAX)
+		n = 2 * RING_TRACE_MAX;
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(ring_trace), n * sizeof(uint64_t)) == hipSuccess ? 0 : -5;
+}
+#endif
+
 template <class C, bool STATS, bool NT, bool PTRS = false>
 __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params A) {
+#ifdef RING_TRACE
+	if (threadIdx.x == 0 && blockIdx.x < RING_TRACE_MAX)
+		ring_trace[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
 	__shared__ __attribute__((aligned(16))) ring_lds<C, PTRS> L;
 	__shared__ stat_slot slots[FWD4_STAT_SLOTS];
 	__shared__ fwd4_edges edges;
@@ -375,6 +389,13 @@ __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params 
 			shard_add(A.stats, T->max_ifaces, key >> 16, key & 0xffff, slots[tid].pkts, slots[tid].bytes);
 		}
 	}
+#ifdef RING_TRACE
+	// measurement builds: when each workgroup started and finished (s_memrealtime, 100 MHz)
+	__syncthreads();
+	if (tid == 0 && blockIdx.x < RING_TRACE_MAX) {
+		ring_trace[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+	}
+#endif
 }
 
 typedef void (*fwd4_rfn)(const fwd4_params);
