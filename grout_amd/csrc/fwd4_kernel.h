@@ -151,6 +151,8 @@ struct fwd4_params {
 	                // else the contiguous tiles [b * chunk, (b + 1) * chunk)
 	uint32_t order; // 2: XCD x (= b % 8) takes region [x * chunk, (x + 1) * chunk),
 	                // its workgroups interleaved in it (grid % 8 == 0)
+	uint32_t spin_max; // polls before a ring wait gives up (0 = RING_SPIN_MAX)
+	uint32_t *err; // set to 1 when a workgroup gave up (host-mapped; may be NULL)
 };
 
 // Kernel variants (bit mask, gr_hip_tune): counters, nontemporal loads and

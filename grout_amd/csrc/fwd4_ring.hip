@@ -23,8 +23,10 @@
 // -> compute), done[s] (compute -> storer), free[s] (storer -> loader).
 // Every wait is bounded (RING_SPIN_MAX polls); a wave that gives up sets
 // the workgroup's abort word and every role leaves its loop, so the grid
-// always drains. Tiles of a workgroup are b, b + G, b + 2G ... (G = grid),
-// or one contiguous run per workgroup (fwd4_params.chunk).
+// always drains; the workgroup then reports it in *A.err (the queue's error
+// word: the next sync returns -ETIMEDOUT). Tiles of a workgroup are b,
+// b + G, b + 2G ... (G = grid), or one contiguous run per workgroup
+// (fwd4_params.chunk).
 #include "fwd4_chain.h"
 
 #define RING_GLDS_PER_TILE 6 // 4 x 1 KiB of lines + 2 x 256 B of metadata
@@ -60,6 +62,7 @@ struct ring_lds {
 	uint64_t ptrs[PTRS ? C::SLOTS : 1][64]; // GR_HIP_BATCH_F_FRAME_PTRS: the tile's frames
 	uint32_t ready[C::SLOTS], done[C::SLOTS], free_[C::SLOTS];
 	uint32_t abort;
+	uint32_t spin_max;
 };
 
 template <int N>
@@ -114,12 +117,13 @@ __device__ __forceinline__ void flag_set(uint32_t *f, uint32_t v) {
 // Wait until *f >= want. False when the wait gave up or another wave did.
 template <class L_t>
 __device__ __forceinline__ bool flag_wait(L_t &L, const uint32_t *f, uint32_t want) {
+	const uint32_t lim = L.spin_max;
 	for (uint32_t spin = 0;; spin++) {
 		if ((int32_t)(flag_get(f) - want) >= 0)
 			return true;
 		if (flag_get(&L.abort))
 			return false;
-		if (spin >= RING_SPIN_MAX) {
+		if (spin >= lim) {
 			flag_set(&L.abort, 1);
 			return false;
 		}
@@ -354,8 +358,10 @@ __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params 
 		L.done[tid] = 0;
 		L.free_[tid] = 0;
 	}
-	if (tid == 0)
+	if (tid == 0) {
 		L.abort = 0;
+		L.spin_max = A.spin_max ? A.spin_max : RING_SPIN_MAX;
+	}
 	if (STATS && tid < FWD4_STAT_SLOTS) {
 		slots[tid].key = 0;
 		slots[tid].pkts = 0;
@@ -382,8 +388,10 @@ __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params 
 		ring_compute<C, STATS, PTRS>(A, P, L, slots, nhf_lds, n_local, wv - C::LOADERS - C::STORERS, lane);
 	}
 
+	__syncthreads(); // every role has left its loop (each wait is bounded)
+	if (tid == 0 && L.abort && A.err != nullptr)
+		__hip_atomic_store(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 	if (STATS) {
-		__syncthreads();
 		if (tid < FWD4_STAT_SLOTS && slots[tid].key != 0) {
 			const uint32_t key = slots[tid].key - 1;
 			shard_add(A.stats, T->max_ifaces, key >> 16, key & 0xffff, slots[tid].pkts, slots[tid].bytes);

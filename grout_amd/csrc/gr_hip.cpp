@@ -115,6 +115,7 @@ struct gr_hip_queue {
 	uint8_t *node_lines, *node_out;
 	gr_hip_pkt_meta *node_meta;
 	gr_hip_verdict *node_v;
+	uint32_t *h_err, *d_err; // kernel error word (pinned, mapped): a workgroup gave up
 };
 
 struct host_range { // gr_hip_host_register
@@ -161,6 +162,7 @@ struct gr_hip_ctx {
 	int host_direct; // host path: the kernel reads / writes pinned host memory itself
 	int node_ptrs; // node path: frames in registered memory are handed over by address
 	int tile_order; // 0: workgroup b takes tiles b, b + G, ...; 1: one contiguous run each
+	uint32_t spin_max; // ring waits: polls before giving up (0 = the kernel's default)
 	std::vector<host_range> hregs; // registered host memory, by host address
 	std::mutex occ_mu; // the occupancy cache below (launches run concurrently)
 	int occ_ring[8]; // by variant, at occ_ring_nhf staged fast adjacencies, geometry occ_ring_cfg
@@ -569,6 +571,7 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->host_direct = 1; // measured 1.9x the staged copies
 	c->node_ptrs = 1;
 	c->tile_order = 0;
+	c->spin_max = 0;
 	for (int v = 0; v < 8; v++)
 		c->occ_ring[v] = gr_fwd4_ring_occupancy(v, 0, 0);
 	c->occ_ring_nhf = 0;
@@ -1260,6 +1263,14 @@ extern "C" int gr_hip_queue_create(gr_hip_ctx_t *c, void *stream, gr_hip_queue_t
 		hipEventCreate(&q->ev1[i]);
 	}
 	hipEventCreateWithFlags(&q->quiesce, hipEventDisableTiming);
+	if (hipHostMalloc(reinterpret_cast<void **>(&q->h_err), sizeof(uint32_t), hipHostMallocMapped) == hipSuccess) {
+		*q->h_err = 0;
+		if (hipHostGetDevicePointer(reinterpret_cast<void **>(&q->d_err), q->h_err, 0) != hipSuccess) {
+			hipHostFree(q->h_err);
+			q->h_err = q->d_err = nullptr;
+		}
+	}
+	(void)hipGetLastError();
 	size_t sb = sizeof(gr_hip_iface_stats) * FWD4_STAT_SHARDS * c->max_ifaces;
 	if (hipMalloc(&q->d_stats, sb) != hipSuccess || hipMemsetAsync(q->d_stats, 0, sb, q->s) != hipSuccess) {
 		(void)hipGetLastError();
@@ -1292,6 +1303,7 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 	}
 	hipEventDestroy(q->quiesce);
 	hipFree(q->d_stats);
+	hipHostFree(q->h_err);
 	hipHostFree(q->node_lines);
 	hipHostFree(q->node_out);
 	hipHostFree(q->node_meta);
@@ -1366,6 +1378,8 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	uint32_t grid = (uint32_t)c->n_cu * per_cu;
 	if (grid > tiles)
 		grid = tiles;
+	A.err = q->d_err;
+	A.spin_max = c->spin_max;
 	A.order = c->tile_order;
 	A.chunk = 0;
 	if (c->tile_order == 1)
@@ -1402,6 +1416,10 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		c->fib_fmt = value;
 	} else if (strcmp(key, "node_ptrs") == 0) {
 		c->node_ptrs = value != 0;
+	} else if (strcmp(key, "spin_max") == 0) { // tests: make ring waits give up early
+		if (value < 0)
+			return -EINVAL;
+		c->spin_max = (uint32_t)value;
 	} else if (strcmp(key, "tile_order") == 0) {
 		if (value < 0 || value > 2)
 			return -EINVAL;
@@ -1464,11 +1482,21 @@ extern "C" int gr_hip_fwd4_submit(gr_hip_queue_t *q, const struct gr_hip_batch *
 	return launch(q, q->s, b, true);
 }
 
+// After a sync: did a workgroup of a kernel on this queue give up a ring
+// wait (its results are incomplete)? Reports it once.
+static int q_check(gr_hip_queue *q) {
+	if (q->h_err != nullptr && __atomic_load_n(q->h_err, __ATOMIC_ACQUIRE)) {
+		__atomic_store_n(q->h_err, 0, __ATOMIC_RELEASE);
+		return -ETIMEDOUT;
+	}
+	return 0;
+}
+
 extern "C" int gr_hip_queue_sync(gr_hip_queue_t *q) {
 	if (q == nullptr)
 		return -EINVAL;
 	HCK(hipStreamSynchronize(q->s));
-	return 0;
+	return q_check(q);
 }
 
 extern "C" int gr_hip_queue_kernel_ms(gr_hip_queue_t *q, uint32_t n, float *ms, uint32_t *count) {
@@ -1521,7 +1549,7 @@ extern "C" int gr_hip_fwd4_host(
 			if (r < 0)
 				return r;
 			HCK(hipStreamSynchronize(q->s));
-			return 0;
+			return q_check(q);
 		}
 	}
 	for (host_slot &h : q->hs) {
@@ -1557,7 +1585,7 @@ extern "C" int gr_hip_fwd4_host(
 	for (host_slot &h : q->hs) {
 		HCK(hipStreamSynchronize(h.s));
 	}
-	return 0;
+	return q_check(q);
 }
 
 // Registered host memory (gr_hip_host_register): host -> device address.
@@ -1685,6 +1713,8 @@ extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uin
 		if ((r = launch(q, q->s, &b, true)) < 0)
 			return r;
 		HCK(hipStreamSynchronize(q->s));
+		if ((r = q_check(q)) < 0)
+			return r;
 		return gr_hip_node_apply(m, n, nullptr, 0, q->node_v, c->ifaces.data(), c->max_ifaces, c->nh.data(),
 					 (uint32_t)c->nh.size(), burst, stats);
 	}
@@ -1815,6 +1845,8 @@ extern "C" int gr_hip_batch_place(gr_hip_ctx_t *c, gr_hip_batch *b, uint32_t can
 				pick = k;
 			}
 		}
+		if (r == 0)
+			r = gr_hip_queue_sync(q);
 		gr_hip_queue_destroy(q);
 	}
 	if (r)

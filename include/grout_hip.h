@@ -393,7 +393,9 @@ void *gr_hip_queue_stream(gr_hip_queue_t *);
 
 // Device-resident fast path: enqueue the fused kernel on the queue's stream.
 int gr_hip_fwd4_submit(gr_hip_queue_t *, const struct gr_hip_batch *);
-// Wait until everything submitted on the queue is done.
+// Wait until everything submitted on the queue is done. -ETIMEDOUT if a
+// kernel gave up a ring wait since the last sync (its workgroup stopped
+// early, so that batch's results are incomplete); the grid still drained.
 int gr_hip_queue_sync(gr_hip_queue_t *);
 // Device time in ms of the last `n` submits (HIP events around each launch,
 // ring of 64). Returns the sum; *count receives how many were measured.
@@ -417,6 +419,8 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               chunk copies (pageable buffers always take that path)
 //   "node_ptrs"  1 = gr_hip_node_process hands registered frames over by
 //               address (default), 0 = always stage header lines
+//   "spin_max"  polls before a ring wait gives up (0 = default, ~0.4 s):
+//               for tests of the give-up path
 //   "tile_order" 0 = workgroup b takes 64-packet tiles b, b + G, b + 2G ...
 //               (default), 1 = one contiguous run of tiles per workgroup
 //   "fib_format_of" (read) the format VRF `value`'s FIB is on the device in

@@ -340,6 +340,37 @@ def test_batch_alloc_and_place(fastpath):
     assert L.gr_hip_batch_alloc(fastpath.h, 64, 72, ctypes.byref(bad)) == -22
 
 
+def test_ring_give_up_is_reported(fastpath):
+    """A ring wait that gives up (forced with spin_max 1) ends the grid and
+    the next sync reports it (-ETIMEDOUT) once; the queue then works as before."""
+    t = T.config_single_route()
+    fresh_fastpath_state(fastpath, t)
+    n = 1 << 20
+    fr, me = S.stream(n, 0x5A1, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    L = fastpath.lib
+    b = fastpath.batch_alloc(n)
+    for dst, src in ((b.in_frames, fr), (b.meta, me)):
+        abi.check("h2d", L.gr_hip_memcpy_h2d(fastpath.h, dst, src.ctypes.data, src.nbytes))
+    q = fastpath.queue()
+    try:
+        assert fastpath.tune("spin_max", 1) == 0
+        abi.check("submit", L.gr_hip_fwd4_submit(q._h, ctypes.byref(b)))
+        assert L.gr_hip_queue_sync(q._h) == -110
+        assert L.gr_hip_queue_sync(q._h) == 0  # reported once
+    finally:
+        fastpath.tune("spin_max", 0)
+    q.stats(reset=True)
+    abi.check("submit", L.gr_hip_fwd4_submit(q._h, ctypes.byref(b)))
+    assert L.gr_hip_queue_sync(q._h) == 0
+    lines = np.empty((n, abi.LINE), dtype=np.uint8)
+    v = np.empty(n, dtype=abi.VERDICT_DT)
+    abi.check("d2h", L.gr_hip_memcpy_d2h(fastpath.h, lines.ctypes.data, b.out_lines, lines.nbytes))
+    abi.check("d2h", L.gr_hip_memcpy_d2h(fastpath.h, v.ctypes.data, b.verdicts, v.nbytes))
+    compare(oracle.Oracle(t).process(fr, me), (lines, v, q.stats()))
+    q.close()
+    fastpath.batch_free(b)
+
+
 def torch_free_bytes():
     import torch
     return torch.cuda.mem_get_info()[0]
