@@ -34,6 +34,9 @@ __device__ __forceinline__ kctx make_kctx(const fwd4_params &A, const fwd4_edges
 	P.ip6_edge = type_edge_of(*edges, 0xdd86u);
 	P.rx6 = T->rx6;
 	P.adj6 = T->adj6;
+	P.nhf6 = T->nhf6;
+	P.nhf6_lds = nullptr; // set by the kernel that stages them
+	P.nhf6_n = 0;
 	return P;
 }
 
@@ -448,6 +451,45 @@ __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, 
 	if (slot == 0 || slot > P.max_nh) {
 		r.edge = GR_HIP_E_IP6_ERROR_DEST_UNREACH;
 		return;
+	}
+	{
+		// fast adjacency (make_nhf6: L3, no LOCAL/LINK flag, every edge chains to
+		// port_output of a port): ip6_forward, ip6_output, eth_output and
+		// iface_output on its MACs, oif and MTU alone -- the same steps and
+		// results as below for such a nexthop
+		uint4 f;
+		if (slot <= P.nhf6_n) {
+			const u4v v = P.nhf6_lds[slot - 1];
+			f = uint4{v.x, v.y, v.z, v.w};
+		} else {
+			f = gld4(P.nhf6 + slot);
+		}
+		if (f.w >> 16) {
+			r.nh = slot;
+			const uint32_t hop = (w[5] >> 8) & 0xff;
+			if (hop <= 1) { // ip6_forward.c:25-30
+				r.edge = GR_HIP_E_IP6_ERROR_TTL_EXCEEDED;
+				return;
+			}
+			u4v c1 = lds_get(R, row, 1);
+			c1.y = (c1.y & 0xffff00ffu) | ((hop - 1) << 8);
+			lds_put(R, row, 1, c1);
+			if (data_len > (f.w >> 16)) { // ip6_output.c:99-102
+				r.edge = GR_HIP_E_IP6_OUTPUT_TOO_BIG;
+				return;
+			}
+			const uint32_t oif = f.y >> 16;
+			u4v c0 = lds_get(R, row, 0);
+			c0.x = f.x;
+			c0.y = (f.y & 0xffff) | (f.z << 16);
+			c0.z = (f.z >> 16) | (f.w << 16);
+			c0.w = (c0.w & 0xffff0000u) | 0xdd86u;
+			lds_put(R, row, 0, c0);
+			r.iface = oif;
+			r.edge = GR_HIP_E_PORT_OUTPUT;
+			r.tx_if = oif;
+			return;
+		}
 	}
 	const uint4 *ap = reinterpret_cast<const uint4 *>(P.adj6 + slot);
 	uint4 a = gld4(ap), b = gld4(ap + 1), c = gld4(ap + 2);

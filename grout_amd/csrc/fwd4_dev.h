@@ -44,6 +44,9 @@ struct kctx {
 	const fwd4_rx6 *rx6;
 	const fwd4_adj6 *adj6;
 	gr_hip_iface_stats *stats;
+	const fwd4_nhf *nhf6;
+	const __attribute__((address_space(3))) u4v *nhf6_lds; // slots 1..nhf6_n staged in LDS
+	uint32_t nhf6_n;
 };
 
 struct rxv {

@@ -108,7 +108,8 @@ struct fwd4_adj6 {
 // Fast adjacency, 16 bytes: a nexthop whose packets take the plain forward
 // (L3, no LOCAL/LINK flag, ip_output/eth_output/iface_output all chain to
 // port_output of a port oif: post_iface = tx iface = oif, no parent) needs
-// only its MACs, oif and MTU. mtu == 0: not plain, read the fwd4_adj.
+// only its MACs, oif and MTU. mtu == 0: not plain, read the fwd4_adj. The
+// IPv6 chain has its own table (nhf6, plain by fwd4_adj6's edges).
 struct fwd4_nhf {
 	uint8_t dmac[6];
 	uint16_t oif;
@@ -124,6 +125,7 @@ struct fwd4_tables {
 	const struct fwd4_nhf *nhf; // [max_nh + 1]
 	const struct fwd4_rx6 *rx6; // [max_ifaces]
 	const struct fwd4_adj6 *adj6; // [max_nh + 1]
+	const struct fwd4_nhf *nhf6; // [max_nh + 1] fast adjacencies of the IPv6 chain
 	const uint32_t *reta;
 	const uint32_t *vlan_keys; // (parent << 16 | vlan_id) + 1, 0 = empty
 	const uint16_t *vlan_vals;
@@ -147,6 +149,7 @@ struct fwd4_params {
 	uint32_t out_stride;
 	uint32_t readable; // frame bytes present per packet (64 or in_stride)
 	uint32_t nhf_lds; // fwd4_ring.hip: fast adjacencies 1..nhf_lds staged in LDS
+	uint32_t nhf6_lds; // and IPv6 fast adjacencies 1..nhf6_lds after them
 	uint32_t chunk; // fwd4_ring.hip: 0 = workgroup b takes tiles b, b + G, ...;
 	                // else the contiguous tiles [b * chunk, (b + 1) * chunk)
 	uint32_t order; // 2: XCD x (= b % 8) takes region [x * chunk, (x + 1) * chunk),

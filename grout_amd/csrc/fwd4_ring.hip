@@ -341,7 +341,7 @@ __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params 
 	__shared__ __attribute__((aligned(16))) ring_lds<C, PTRS> L;
 	__shared__ stat_slot slots[FWD4_STAT_SLOTS];
 	__shared__ fwd4_edges edges;
-	extern __shared__ __attribute__((aligned(16))) uint4 nhf_lds[]; // [A.nhf_lds]: slots 1..
+	extern __shared__ __attribute__((aligned(16))) uint4 nhf_lds[]; // [A.nhf_lds]: slots 1.., then [A.nhf6_lds]
 	const uint32_t tid = threadIdx.x, lane = tid & 63;
 	const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
 	const fwd4_tables *T = A.T;
@@ -350,6 +350,9 @@ __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params 
 		const uint4 *src = reinterpret_cast<const uint4 *>(T->nhf) + 1;
 		for (uint32_t i = tid; i < A.nhf_lds; i += C::WAVES * 64)
 			nhf_lds[i] = gld4(src + i);
+		const uint4 *src6 = reinterpret_cast<const uint4 *>(T->nhf6) + 1;
+		for (uint32_t i = tid; i < A.nhf6_lds; i += C::WAVES * 64)
+			nhf_lds[A.nhf_lds + i] = gld4(src6 + i);
 	}
 	for (uint32_t i = tid; i < sizeof(fwd4_edges); i += C::WAVES * 64)
 		reinterpret_cast<uint8_t *>(&edges)[i] = reinterpret_cast<const uint8_t *>(&T->edges)[i];
@@ -385,6 +388,8 @@ __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params 
 		ring_storer<C, NT, PTRS>(A, L, n_local, wv - C::LOADERS, lane);
 	} else {
 		kctx P = make_kctx(A, &edges);
+		P.nhf6_lds = (const __attribute__((address_space(3))) u4v *)(nhf_lds + A.nhf_lds);
+		P.nhf6_n = A.nhf6_lds;
 		ring_compute<C, STATS, PTRS>(A, P, L, slots, nhf_lds, n_local, wv - C::LOADERS - C::STORERS, lane);
 	}
 
@@ -433,7 +438,8 @@ static const ring_entry ring_ptrs_kernel = {
 // dynamic LDS.
 extern "C" hipError_t gr_fwd4_ring_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant, int cfg) {
 	const ring_entry &e = (variant & FWD4_V_PTRS) ? ring_ptrs_kernel : ring_kernels[(unsigned)cfg % RING_NCFG];
-	hipLaunchKernelGGL(e.fn[variant & 3], dim3(grid), dim3(e.threads), A->nhf_lds * sizeof(fwd4_nhf), s, *A);
+	hipLaunchKernelGGL(e.fn[variant & 3], dim3(grid), dim3(e.threads), (A->nhf_lds + A->nhf6_lds) * sizeof(fwd4_nhf), s,
+			   *A);
 	return hipGetLastError();
 }
 

@@ -141,6 +141,9 @@ struct gr_hip_ctx {
 	fwd4_adj *d_adj;
 	std::vector<fwd4_nhf> nhf; // fast adjacencies (host image)
 	fwd4_nhf *d_nhf;
+	std::vector<fwd4_nhf> nhf6; // the same for the IPv6 chain
+	fwd4_nhf *d_nhf6;
+	uint32_t v6_routes; // IPv6 routes on the device, all VRFs (stage nhf6 in LDS when > 0)
 	std::vector<fwd4_rx6> rx6; // IPv6 views and adjacencies (host images)
 	std::vector<fwd4_adj6> adj6;
 	fwd4_rx6 *d_rx6;
@@ -165,9 +168,13 @@ struct gr_hip_ctx {
 	uint32_t spin_max; // ring waits: polls before giving up (0 = the kernel's default)
 	std::vector<host_range> hregs; // registered host memory, by host address
 	std::mutex occ_mu; // the occupancy cache below (launches run concurrently)
-	int occ_ring[8]; // by variant, at occ_ring_nhf staged fast adjacencies, geometry occ_ring_cfg
-	uint32_t occ_ring_nhf;
-	int occ_ring_cfg;
+	int occ_ring[8]; // by variant, of the last launch's geometry and staging ("occupancy")
+	struct occ_entry {
+		uint32_t staged; // fast adjacencies staged in LDS (IPv4 + IPv6)
+		int cfg; // ring geometry
+		int occ[8]; // workgroups per CU by variant, 0 = does not fit
+	} occ_cache[4];
+	uint32_t occ_n; // entries filled (round robin past 4)
 };
 
 // ---------------------------------------------------------------------------
@@ -379,6 +386,22 @@ static fwd4_nhf make_nhf(const fwd4_adj &a) {
 	return f;
 }
 
+// The IPv6 chain's fast adjacency (chain6): the same plain forward by the
+// IPv6 edges (ip6_input / ip6_output registrations), mtu = 0 otherwise.
+static fwd4_nhf make_nhf6(const fwd4_adj6 &a) {
+	fwd4_nhf f;
+	memset(&f, 0, sizeof(f));
+	if (a.type == GR_HIP_NH_T_L3 && a.e_in == GR_HIP_EDGE_CHAIN && a.flags == 0 && a.e_pre == GR_HIP_EDGE_CHAIN
+	    && a.e_mid == GR_HIP_EDGE_CHAIN && a.e_post == GR_HIP_E_PORT_OUTPUT && a.post_iface == a.oif
+	    && a.tx_if == a.oif && a.tx_par == 0 && a.mtu != 0) {
+		memcpy(f.dmac, a.dmac, 6);
+		memcpy(f.smac, a.smac, 6);
+		f.oif = a.oif;
+		f.mtu = a.mtu;
+	}
+	return f;
+}
+
 // Recompute and upload the RX views (all) and adjacencies [first, first+n)
 // (n == 0: every slot up to nh_hi). Caller holds c->mu and has quiesced.
 static int upload_views(gr_hip_ctx *c, bool rx, uint32_t first, uint32_t n, bool adj) {
@@ -400,12 +423,15 @@ static int upload_views(gr_hip_ctx *c, bool rx, uint32_t first, uint32_t n, bool
 			c->adj[i] = make_adj(c, i);
 			c->nhf[i] = make_nhf(c->adj[i]);
 			c->adj6[i] = make_adj6(c, i);
+			c->nhf6[i] = make_nhf6(c->adj6[i]);
 		}
 		if (n) {
 			HCK(hipMemcpyAsync(c->d_adj6 + first, &c->adj6[first], sizeof(fwd4_adj6) * n, hipMemcpyHostToDevice,
 					   c->ctl));
 			HCK(hipMemcpyAsync(c->d_adj + first, &c->adj[first], sizeof(fwd4_adj) * n, hipMemcpyHostToDevice, c->ctl));
 			HCK(hipMemcpyAsync(c->d_nhf + first, &c->nhf[first], sizeof(fwd4_nhf) * n, hipMemcpyHostToDevice, c->ctl));
+			HCK(hipMemcpyAsync(c->d_nhf6 + first, &c->nhf6[first], sizeof(fwd4_nhf) * n, hipMemcpyHostToDevice,
+					   c->ctl));
 		}
 	}
 	HCK(hipStreamSynchronize(c->ctl));
@@ -420,6 +446,7 @@ static int upload_tables(gr_hip_ctx *c) {
 	t.rx = c->d_rx;
 	t.adj = c->d_adj;
 	t.nhf = c->d_nhf;
+	t.nhf6 = c->d_nhf6;
 	t.rx6 = c->d_rx6;
 	t.adj6 = c->d_adj6;
 	t.reta = c->d_reta;
@@ -531,6 +558,8 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->rx.assign(max_ifaces, fwd4_rx {});
 	c->adj.assign((size_t)max_nexthops + 1, fwd4_adj {});
 	c->nhf.assign((size_t)max_nexthops + 1, fwd4_nhf {});
+	c->nhf6.assign((size_t)max_nexthops + 1, fwd4_nhf {});
+	c->v6_routes = 0;
 	c->rx6.assign(max_ifaces, fwd4_rx6 {});
 	c->adj6.assign((size_t)max_nexthops + 1, fwd4_adj6 {});
 	c->nh_hi = 0;
@@ -547,6 +576,8 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 		goto fail;
 	if (hipMalloc(&c->d_nhf, sizeof(fwd4_nhf) * ((size_t)max_nexthops + 1)) != hipSuccess)
 		goto fail;
+	if (hipMalloc(&c->d_nhf6, sizeof(fwd4_nhf) * ((size_t)max_nexthops + 1)) != hipSuccess)
+		goto fail;
 	if (hipMalloc(&c->d_rx6, sizeof(fwd4_rx6) * max_ifaces) != hipSuccess)
 		goto fail;
 	if (hipMalloc(&c->d_adj6, sizeof(fwd4_adj6) * ((size_t)max_nexthops + 1)) != hipSuccess)
@@ -560,6 +591,7 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	if (hipMemsetAsync(c->d_rx, 0, sizeof(fwd4_rx) * max_ifaces, c->ctl) != hipSuccess
 	    || hipMemsetAsync(c->d_adj, 0, sizeof(fwd4_adj) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess
 	    || hipMemsetAsync(c->d_nhf, 0, sizeof(fwd4_nhf) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess
+	    || hipMemsetAsync(c->d_nhf6, 0, sizeof(fwd4_nhf) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess
 	    || hipMemsetAsync(c->d_rx6, 0, sizeof(fwd4_rx6) * max_ifaces, c->ctl) != hipSuccess
 	    || hipMemsetAsync(c->d_adj6, 0, sizeof(fwd4_adj6) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess)
 		goto fail;
@@ -574,8 +606,7 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->spin_max = 0;
 	for (int v = 0; v < 8; v++)
 		c->occ_ring[v] = gr_fwd4_ring_occupancy(v, 0, 0);
-	c->occ_ring_nhf = 0;
-	c->occ_ring_cfg = 0;
+	c->occ_n = 0;
 	ret = -EIO;
 	if (upload_tables(c) != 0)
 		goto fail;
@@ -612,6 +643,7 @@ extern "C" int gr_hip_fini(gr_hip_ctx_t *c) {
 	hipFree(c->d_adj6);
 	hipFree(c->d_adj);
 	hipFree(c->d_nhf);
+	hipFree(c->d_nhf6);
 	hipFree(c->d_reta);
 	hipFree(c->d_vlan_keys);
 	hipFree(c->d_vlan_vals);
@@ -1091,6 +1123,16 @@ static void scope6(uint8_t out[16], const uint8_t ip[16], uint16_t iface_id) {
 	}
 }
 
+// IPv6 routes on the device over all VRFs: the launches stage the IPv6
+// fast adjacencies in LDS only when there are some. Caller holds c->mu.
+static void count_v6(gr_hip_ctx *c) {
+	uint32_t n = 0;
+	for (const vrf_fib &v : c->vrfs)
+		if (v.rib6 != nullptr && v.uploaded6)
+			n += gr_fib6_n_routes(v.rib6);
+	c->v6_routes = n;
+}
+
 extern "C" int gr_hip_fib6_create(gr_hip_ctx_t *c, uint16_t vrf, uint32_t max_routes, uint32_t num_tbl8) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces || max_routes == 0)
 		return -EINVAL;
@@ -1124,6 +1166,7 @@ extern "C" int gr_hip_fib6_destroy(gr_hip_ctx_t *c, uint16_t vrf) {
 	v.rib6 = nullptr;
 	v.d6 = nullptr;
 	v.d6_groups = 0;
+	count_v6(c);
 	v.gen6 = 0;
 	return 0;
 }
@@ -1201,6 +1244,7 @@ extern "C" int gr_hip_fib6_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 		v.uploaded6 = true;
 		r = upload_views(c, true, 0, 0, false);
 	}
+	count_v6(c);
 	return r;
 }
 
@@ -1341,7 +1385,7 @@ static bool host_dev_ptr(const void *p, void **dp) {
 
 static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool timed) {
 	gr_hip_ctx *c = q->ctx;
-	fwd4_params A;
+	fwd4_params A{};
 	A.in = static_cast<const uint8_t *>(b->in_frames);
 	A.out = static_cast<uint8_t *>(b->out_lines);
 	A.meta = b->meta;
@@ -1360,18 +1404,40 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	// persistent: one resident round of workgroups, each walking 64-packet tiles
 	int variant = (stats ? FWD4_V_STATS : 0) | c->nt | ((b->flags & GR_HIP_BATCH_F_FRAME_PTRS) ? FWD4_V_PTRS : 0);
 	uint32_t tiles = (b->n + 63) / 64;
-	A.nhf_lds = c->nh_hi < gr_fwd4_ring_nhf_max() ? c->nh_hi : gr_fwd4_ring_nhf_max();
+	// fast adjacencies staged in LDS: IPv4, and IPv6 when IPv6 routes exist,
+	// as many as the geometry's LDS leaves room for (IPv6 given up first)
+	uint32_t n4 = c->nh_hi < gr_fwd4_ring_nhf_max() ? c->nh_hi : gr_fwd4_ring_nhf_max();
+	uint32_t n6 = c->v6_routes ? n4 : 0;
 	int occ;
 	{
 		std::lock_guard<std::mutex> ol(c->occ_mu);
-		if (A.nhf_lds != c->occ_ring_nhf || c->ring_cfg != c->occ_ring_cfg) {
+		const int cfg = c->ring_cfg;
+		auto occ_of = [&](uint32_t staged) -> const gr_hip_ctx::occ_entry & {
+			const uint32_t filled = c->occ_n < 4 ? c->occ_n : 4;
+			for (uint32_t i = 0; i < filled; i++)
+				if (c->occ_cache[i].staged == staged && c->occ_cache[i].cfg == cfg)
+					return c->occ_cache[i];
+			gr_hip_ctx::occ_entry &e = c->occ_cache[c->occ_n++ % 4];
+			e.staged = staged;
+			e.cfg = cfg;
 			for (int v = 0; v < 8; v++)
-				c->occ_ring[v] = gr_fwd4_ring_occupancy(v, c->ring_cfg, A.nhf_lds);
-			c->occ_ring_nhf = A.nhf_lds;
-			c->occ_ring_cfg = c->ring_cfg;
+				e.occ[v] = gr_fwd4_ring_occupancy(v, cfg, staged);
+			return e;
+		};
+		const gr_hip_ctx::occ_entry *e = &occ_of(n4 + n6);
+		if (e->occ[variant] <= 0 && n6) {
+			n6 = 0;
+			e = &occ_of(n4);
 		}
-		occ = c->occ_ring[variant];
+		if (e->occ[variant] <= 0 && n4) {
+			n4 = 0;
+			e = &occ_of(0);
+		}
+		occ = e->occ[variant];
+		memcpy(c->occ_ring, e->occ, sizeof(c->occ_ring));
 	}
+	A.nhf_lds = n4;
+	A.nhf6_lds = n6;
 	uint32_t per_cu = c->wg_per_cu > 0 ? (uint32_t)c->wg_per_cu : RING_WG_PER_CU;
 	if (occ > 0 && per_cu > (uint32_t)occ)
 		per_cu = (uint32_t)occ;
