@@ -74,3 +74,16 @@ def test_queue_refuses_null_stream():
 
     with pytest.raises(ValueError):
         Queue(_FP(), 0)
+
+
+def test_product_fails_loudly_without_the_hip_library(monkeypatch):
+    """No fallback: without libgrout_hip.so the package refuses to run (the
+    oracle is never a stand-in for the product path)."""
+    from grout_amd import abi as A
+    monkeypatch.setattr(A, "LIB_HIP", "/nonexistent/libgrout_hip.so")
+    monkeypatch.setattr(A, "_hip", None)
+    with pytest.raises(ImportError, match="not built"):
+        A.hip()
+    from grout_amd.fwd import FastPath
+    with pytest.raises(ImportError):
+        FastPath(0)
