@@ -562,6 +562,20 @@ def test_ring_geometries(fastpath, cfg):
         fastpath.tune("wg_per_cu", 0)
 
 
+@pytest.mark.parametrize("order", [1, 2])
+def test_tile_orders(fastpath, order):
+    """The other tile orders (one contiguous run per workgroup; one region per
+    XCD) cover every tile exactly once, ragged sizes included, bit-exact."""
+    tf = _fullview()
+    fr, me = S.stream(1 << 20, 0x7110 + order, routes=tf.route_array())
+    fastpath.tune("tile_order", order)
+    try:
+        for n in (1 << 20, 64 * 1000 + 17, 64 * 257 + 1, 63, 1):
+            compare(oracle.Oracle(tf).process(fr[:n], me[:n]), run_gpu(fastpath, tf, fr[:n], me[:n]))
+    finally:
+        fastpath.tune("tile_order", 0)
+
+
 # ---- IPv6
 
 @functools.lru_cache(maxsize=None)
