@@ -106,7 +106,8 @@ struct gr_hip_queue {
 	hipStream_t s;
 	bool own_stream;
 	hipEvent_t ev0[N_TIMED], ev1[N_TIMED];
-	uint64_t n_launch;
+	uint64_t n_launch; // timed launches
+	uint64_t n_submit; // submits that could be timed (time_every sampling)
 	hipEvent_t quiesce;
 	gr_hip_iface_stats *d_stats; // [FWD4_STAT_SHARDS][max_ifaces]
 	host_slot hs[HOST_SLOTS];
@@ -166,6 +167,8 @@ struct gr_hip_ctx {
 	int node_ptrs; // node path: frames in registered memory are handed over by address
 	int tile_order; // 0: workgroup b takes tiles b, b + G, ...; 1: one contiguous run each
 	uint32_t spin_max; // ring waits: polls before giving up (0 = the kernel's default)
+	int untimed; // measurements: no HIP events around launches (gr_hip_queue_kernel_ms sees none)
+	uint32_t time_every; // HIP events around every N-th submit of a queue only (0, 1 = every one)
 	std::vector<host_range> hregs; // registered host memory, by host address
 	std::mutex occ_mu; // the occupancy cache below (launches run concurrently)
 	int occ_ring[8]; // by variant, of the last launch's geometry and staging ("occupancy")
@@ -604,6 +607,8 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->node_ptrs = 1;
 	c->tile_order = 0;
 	c->spin_max = 0;
+	c->untimed = 0;
+	c->time_every = 1;
 	for (int v = 0; v < 8; v++)
 		c->occ_ring[v] = gr_fwd4_ring_occupancy(v, 0, 0);
 	c->occ_n = 0;
@@ -1454,6 +1459,8 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 		A.chunk = (tiles + 7) / 8;
 	else if (c->tile_order == 2)
 		A.order = 0;
+	// every `time_every`-th submit of the queue carries the event pair
+	timed = timed && !c->untimed && (c->time_every <= 1 || q->n_submit++ % c->time_every == 0);
 	if (timed)
 		HCK(hipEventRecord(q->ev0[slot], s));
 	HCK(gr_fwd4_ring_launch(&A, grid, s, variant, c->ring_cfg));
@@ -1482,6 +1489,12 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		c->fib_fmt = value;
 	} else if (strcmp(key, "node_ptrs") == 0) {
 		c->node_ptrs = value != 0;
+	} else if (strcmp(key, "untimed") == 0) {
+		c->untimed = value != 0;
+	} else if (strcmp(key, "time_every") == 0) { // sample the launch timing: less event overhead
+		if (value < 0 || value > 1024)
+			return -EINVAL;
+		c->time_every = (uint32_t)value;
 	} else if (strcmp(key, "spin_max") == 0) { // tests: make ring waits give up early
 		if (value < 0)
 			return -EINVAL;

@@ -397,8 +397,9 @@ int gr_hip_fwd4_submit(gr_hip_queue_t *, const struct gr_hip_batch *);
 // kernel gave up a ring wait since the last sync (its workgroup stopped
 // early, so that batch's results are incomplete); the grid still drained.
 int gr_hip_queue_sync(gr_hip_queue_t *);
-// Device time in ms of the last `n` submits (HIP events around each launch,
-// ring of 64). Returns the sum; *count receives how many were measured.
+// Device time in ms of the last `n` timed submits (HIP events around each
+// timed launch, ring of 64; see "time_every"). Returns the sum; *count
+// receives how many were measured.
 int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *count);
 
 // Tuning knobs, for measurements (A/B in one process). Keys:
@@ -419,6 +420,10 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               chunk copies (pageable buffers always take that path)
 //   "node_ptrs"  1 = gr_hip_node_process hands registered frames over by
 //               address (default), 0 = always stage header lines
+//   "time_every" N: only every N-th submit of a queue gets the HIP event
+//               pair that gr_hip_queue_kernel_ms reads (default 1: all);
+//               each pair costs ~7 us of stream time per launch
+//   "untimed"   1 = no events at all
 //   "spin_max"  polls before a ring wait gives up (0 = default, ~0.4 s):
 //               for tests of the give-up path
 //   "tile_order" 0 = workgroup b takes 64-packet tiles b, b + G, b + 2G ...

@@ -408,6 +408,18 @@ def test_kernel_timing_api(fastpath):
     ms, cnt = q.kernel_ms(3)
     assert cnt == 3 and ms > 0
     q.close()
+    # sampled: only submits 0, 3, 6 of a fresh queue carry events
+    q = fastpath.queue()
+    fastpath.tune("time_every", 3)
+    try:
+        for _ in range(7):
+            q.submit(fin, out, mt, v, len(me))
+        q.sync()
+        ms, cnt = q.kernel_ms(10)
+        assert cnt == 3 and ms > 0
+    finally:
+        fastpath.tune("time_every", 1)
+    q.close()
 
 
 @pytest.mark.parametrize("nt,stats,wg,fmt", [(1, 1, 0, 1), (0, 0, 1, 1), (1, 0, 2, 0), (0, 1, 0, 0), (1, 1, 3, 0),
