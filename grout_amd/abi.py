@@ -27,11 +27,13 @@ NH_T = dict(L3=1, SR6_OUTPUT=2, SR6_LOCAL=3, DNAT=4, BLACKHOLE=5, REJECT=6, GROU
 AF_UNSPEC, AF_IP4, AF_IP6 = 0, 1, 2
 DOMAIN = dict(UNKNOWN=0, LOOPBACK=1, LOCAL=2, BROADCAST=3, MULTICAST=4, OTHER=5)
 CKSUM_UNKNOWN, CKSUM_BAD, CKSUM_GOOD = 0, 1, 2
-ABI_VERSION = 2  # GR_HIP_ABI_VERSION
+ABI_VERSION = 3  # GR_HIP_ABI_VERSION
 EDGE_CHAIN = 0xFF
 EDGE_CHAIN6 = 0xFE  # eth_input type edge: continue into ip6_input on the GPU
 LINE = 64
 BATCH_F_LINES_ONLY = 0x1
+META_WALK = 0x4000  # gr_hip_pkt_meta.vlan_ck: this packet starts a graph walk
+MBUF_F_WALK = 0x01  # gr_hip_mbuf.flags: this mbuf starts a graph walk
 
 # enum gr_hip_edge, in order; names are the grout node each value stands for
 EDGE_NAMES = [
@@ -89,7 +91,7 @@ assert META_DT.itemsize == 8 and VERDICT_DT.itemsize == 8 and STATS_DT.itemsize 
 # struct gr_hip_mbuf: the node shim's view of an rte_mbuf + priv (grout_hip.h)
 MBUF_DT = np.dtype([("frame", "<u8"), ("pkt_len", "<u4"), ("data_len", "<u2"), ("data_off", "<u2"),
                     ("packet_type", "<u4"), ("rss", "<u4"), ("iface", "<u2"), ("vlan_id", "<u2"),
-                    ("ck", "u1"), ("edge", "u1"), ("domain", "u1"), ("_pad", "u1"), ("nh", "<u4"),
+                    ("ck", "u1"), ("edge", "u1"), ("domain", "u1"), ("flags", "u1"), ("nh", "<u4"),
                     ("_pad1", "<u4")])
 assert MBUF_DT.itemsize == 40
 NODE_NAMES = ["iface_input", "eth_input", "ip_input", "ip_forward", "ip_output", "eth_output", "iface_output",
@@ -177,8 +179,9 @@ HIP_API = {
     "gr_hip_host_unregister": (_I, [_P, _P]),
     "gr_hip_host_dev_addr": (_I, [_P, _P, _P]),
     "gr_hip_edge_node": (_I, [_U8, _U32, _I]),
-    "gr_hip_node_stage": (_I, [_P, _U32, _P, _P]),
-    "gr_hip_node_apply": (_I, [_P, _U32, _P, _U32, _P, _P, _U32, _P, _U32, _U32, _P]),
+    "gr_hip_node_layout": (_I, [_P, _U32, _U32, _P]),
+    "gr_hip_node_stage": (_I, [_P, _U32, _U32, _P, _P, _P]),
+    "gr_hip_node_apply": (_I, [_P, _U32, _U32, _P, _P, _U32, _P, _P, _U32, _P, _U32, _P]),
     "gr_hip_node_process": (_I, [_P, _P, _U32, _U32, _P]),
 }
 

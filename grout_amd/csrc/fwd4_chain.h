@@ -74,6 +74,7 @@ __device__ __forceinline__ rxv load_rx_scalar(const kctx &P, uint32_t id) {
 }
 
 #define HEAD_DONE 0 // the packet left the chain, r.edge set
+#define HEAD_IN4 1 // the packet left the chain in ip_input, r.edge set
 #define HEAD_IP4 4 // continue to the IPv4 FIB lookup: dst, data_len set
 #define HEAD_IP6 6 // continue into ip6_input (chain6): data_len set
 
@@ -140,7 +141,7 @@ __device__ __forceinline__ int chain_head(const kctx &P, const uint8_t *R, uint3
 	const uint32_t ihl = vihl & 0xf;
 	if (data_len < 20) { // (1)
 		r.edge = GR_HIP_E_IP_INPUT_BAD_LENGTH;
-		return HEAD_DONE;
+		return HEAD_IN4;
 	}
 	const u4v c1 = lds_get(R, row, 1);
 	const u4v c2 = lds_get(R, row, 2);
@@ -152,7 +153,7 @@ __device__ __forceinline__ int chain_head(const kctx &P, const uint8_t *R, uint3
 			r.rx_if = r.rx_par = 0;
 			r.domain = 0;
 			r.iface = m.iface;
-			return HEAD_DONE;
+			return HEAD_IN4;
 		}
 		uint32_t sum = 0;
 		if (ihl != 0) {
@@ -180,38 +181,38 @@ __device__ __forceinline__ int chain_head(const kctx &P, const uint8_t *R, uint3
 		sum = (sum & 0xffff) + (sum >> 16);
 		if (sum != 0xffff) {
 			r.edge = GR_HIP_E_IP_INPUT_BAD_CHECKSUM;
-			return HEAD_DONE;
+			return HEAD_IN4;
 		}
 	} else if (ck == GR_HIP_CKSUM_BAD) {
 		r.edge = GR_HIP_E_IP_INPUT_BAD_CHECKSUM;
-		return HEAD_DONE;
+		return HEAD_IN4;
 	}
 	dst = hi16(c1.w) | (lo16(c2.x) << 16);
 	if (dst == 0) {
 		r.edge = GR_HIP_E_IP_INPUT_BAD_ADDRESS;
-		return HEAD_DONE;
+		return HEAD_IN4;
 	}
 	if ((vihl >> 4) != 4) { // (3)
 		r.edge = GR_HIP_E_IP_INPUT_BAD_VERSION;
-		return HEAD_DONE;
+		return HEAD_IN4;
 	}
 	if (ihl * 4 < 20) { // (4)
 		r.edge = GR_HIP_E_IP_INPUT_BAD_LENGTH;
-		return HEAD_DONE;
+		return HEAD_IN4;
 	}
 	if (bswap16(lo16(c1.x)) < 20) { // (5)
 		r.edge = GR_HIP_E_IP_INPUT_BAD_LENGTH;
-		return HEAD_DONE;
+		return HEAD_IN4;
 	}
 	if (r.domain != GR_HIP_ETH_DOMAIN_LOCAL) {
 		bool mc = r.domain == GR_HIP_ETH_DOMAIN_BROADCAST || r.domain == GR_HIP_ETH_DOMAIN_MULTICAST;
 		r.edge = mc ? GR_HIP_E_IP_INPUT_LOCAL : GR_HIP_E_IP_INPUT_OTHER_HOST;
-		return HEAD_DONE;
+		return HEAD_IN4;
 	}
 	const uint32_t d0 = dst & 0xff;
 	if (dst == 0xffffffffu || (d0 >= 224 && d0 <= 239)) {
 		r.edge = GR_HIP_E_IP_INPUT_LOCAL;
-		return HEAD_DONE;
+		return HEAD_IN4;
 	}
 	return HEAD_IP4;
 }
@@ -569,4 +570,73 @@ __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, 
 		r.tx_par = a.w >> 16;
 	}
 	lds_put(R, row, 0, c0);
+}
+
+// ---- eth_output's per-walk source-MAC cache (eth_output.c:37-59)
+//
+// eth_output looks the source MAC up only when the packet's iface differs
+// from the last one it looked up in this graph walk (last_iface_id, which a
+// failed lookup leaves unchanged); a failed lookup (eth_output_no_mac)
+// zeroes the cached MAC. So a packet of the cached iface that follows a
+// no-MAC packet in the same walk leaves with source MAC 00:00:00:00:00:00.
+// Walks lie inside a 64-packet tile (GR_HIP_META_WALK): a wave resolves its
+// tile's walks after the chain, only when one of its packets is no-MAC.
+//
+// eth_output's stream in a walk is rte_graph's order: the IPv4 packets that
+// reached it (in RX order), then the IPv6 ones -- or the other way round when
+// ip6_input received a packet before ip_input did (the walk's pending queue
+// runs ip6_input -> ip6_forward -> ip6_output first).
+
+// The packet went through eth_output to an iface_output edge.
+__device__ __forceinline__ bool past_eth_output(uint32_t edge, uint32_t nh) {
+	return (edge >= GR_HIP_E_IFACE_OUTPUT_INVAL_TYPE && edge <= GR_HIP_E_PORT_OUTPUT)
+		|| (edge == GR_HIP_E_BRIDGE_INPUT && nh != 0);
+}
+
+// fam: 1 = the packet entered ip_input, 2 = ip6_input, 0 = neither.
+// Returns whether lane's row must get a zero source MAC. Wave-converged.
+__device__ bool eth_output_walks(const kctx &P, uint32_t lane, bool live, bool walk_bit, uint32_t fam, const result &r) {
+	static_assert(GR_HIP_E_PORT_OUTPUT - GR_HIP_E_IFACE_OUTPUT_INVAL_TYPE == 5, "iface_output edges");
+	const bool nomac = live && r.edge == GR_HIP_E_ETH_OUTPUT_NO_MAC;
+	const bool out = live && past_eth_output(r.edge, r.nh);
+	uint32_t eo = 0; // priv->iface at eth_output: the nexthop's iface (ip_output.c:91-97)
+	if (nomac)
+		eo = r.iface;
+	else if (out)
+		eo = fam == 2 ? gld(&P.adj6[r.nh].oif) : gld(&P.adj[r.nh].oif);
+	const uint64_t E = __ballot(nomac || out), N = __ballot(nomac);
+	const uint64_t F4 = __ballot(live && fam == 1), F6 = __ballot(live && fam == 2);
+	uint64_t starts = __ballot(live && walk_bit) | 1;
+	uint64_t zero = 0;
+	while (starts) {
+		const uint32_t b = (uint32_t)__builtin_ctzll(starts);
+		starts &= starts - 1;
+		const uint32_t e = starts ? (uint32_t)__builtin_ctzll(starts) : 64;
+		const uint64_t w = (e == 64 ? ~0ull : (1ull << e) - 1) & ~((1ull << b) - 1);
+		if ((E & N & w) == 0)
+			continue; // no failed lookup in this walk: every packet has its iface's MAC
+		const uint64_t f4 = F4 & w, f6 = F6 & w;
+		const bool six_first = f6 != 0 && (f4 == 0 || __builtin_ctzll(f6) < __builtin_ctzll(f4));
+		uint32_t last = GR_HIP_IFACE_ID_UNDEF;
+		bool cleared = false; // the cached source MAC was zeroed
+		for (int pass = 0; pass < 2; pass++) {
+			uint64_t s = E & ((pass == 0) == six_first ? f6 : f4);
+			while (s) {
+				const uint32_t i = (uint32_t)__builtin_ctzll(s);
+				s &= s - 1;
+				const uint32_t ifc = __builtin_amdgcn_readlane(eo, i);
+				if (ifc != last) {
+					if ((N >> i) & 1) { // iface_get_eth_addr failed: src_mac zeroed, last kept
+						cleared = true;
+						continue;
+					}
+					last = ifc;
+					cleared = false;
+				} else if (cleared) {
+					zero |= 1ull << i;
+				}
+			}
+		}
+	}
+	return (zero >> lane) & 1;
 }

@@ -287,11 +287,13 @@ __device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds<C, PT
 			rx = load_rx(P, m.iface);
 
 		result r = {GR_HIP_E_PUNT, 0, m.iface, 0, 0, 0, 0, 0};
+		uint32_t fam = 0; // the packet entered ip_input (1) / ip6_input (2)
 		if (live) {
 			uint32_t dst = 0, data_len = 0;
 			const uint8_t *frame = PTRS ? reinterpret_cast<const uint8_t *>(L.ptrs[s][lane])
 						    : A.in + (size_t)(base + lane) * A.in_stride;
 			const int head = chain_head(P, R, lane, m, rx, r, dst, data_len, frame);
+			fam = head == HEAD_IN4 || head == HEAD_IP4 ? 1 : head == HEAD_IP6 ? 2 : 0;
 			if (head == HEAD_IP4) {
 				const uint32_t slot = chain_fib(rx, dst);
 				if (slot == 0 || slot > P.max_nh) {
@@ -309,6 +311,13 @@ __device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds<C, PT
 			} else if (head == HEAD_IP6) {
 				chain6(P, R, lane, m, rx, r, data_len);
 			}
+		}
+		if (__ballot(r.edge == GR_HIP_E_ETH_OUTPUT_NO_MAC) != 0
+		    && eth_output_walks(P, lane, live, (m.vlan_ck & GR_HIP_META_WALK) != 0, fam, r)) {
+			u4v c0 = lds_get(R, lane, 0); // source MAC, bytes 6-11: zero
+			c0.y &= 0xffffu;
+			c0.z = 0;
+			lds_put(R, lane, 0, c0);
 		}
 		L.meta[s][lane] = u2v{r.edge | (r.domain << 8) | (r.iface << 16), r.nh};
 		flag_set(&L.done[s], k + 1);

@@ -116,6 +116,8 @@ struct gr_hip_queue {
 	uint8_t *node_lines, *node_out;
 	gr_hip_pkt_meta *node_meta;
 	gr_hip_verdict *node_v;
+	std::vector<uint32_t> node_pos; // where each mbuf is staged (gr_hip_node_layout)
+	uint8_t *d_pad; // the zeroed line pad slots of a frames-by-address batch point at
 	uint32_t *h_err, *d_err; // kernel error word (pinned, mapped): a workgroup gave up
 };
 
@@ -1357,6 +1359,7 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 	hipHostFree(q->node_out);
 	hipHostFree(q->node_meta);
 	hipHostFree(q->node_v);
+	hipFree(q->d_pad);
 	if (q->own_stream)
 		hipStreamDestroy(q->s);
 	(void)hipGetLastError();
@@ -1653,6 +1656,8 @@ extern "C" int gr_hip_fwd4_host(
 		HCK(hipMemcpyAsync(h.in, in + (size_t)off * GR_HIP_LINE, (size_t)cnt * GR_HIP_LINE,
 				   hipMemcpyHostToDevice, h.s));
 		HCK(hipMemcpyAsync(h.meta, meta + off, (size_t)cnt * sizeof(*meta), hipMemcpyHostToDevice, h.s));
+		// verdicts of packets a kernel that gave up never reached read back as 0xff
+		HCK(hipMemsetAsync(h.v, 0xff, (size_t)cnt * sizeof(*verdicts), h.s));
 		gr_hip_batch b = {h.in, h.out, h.meta, h.v, cnt, GR_HIP_LINE, GR_HIP_LINE, GR_HIP_BATCH_F_LINES_ONLY};
 		int r = launch(q, h.s, &b, false);
 		if (r < 0)
@@ -1676,8 +1681,8 @@ static const host_range *hreg_find(const gr_hip_ctx *c, uintptr_t p) {
 }
 
 // Every frame in registered memory and 16-byte aligned: their device
-// addresses into ptrs[n].
-static bool host_dev_ptr_ok(gr_hip_ctx *c, const gr_hip_mbuf *m, uint32_t n, uint64_t *ptrs) {
+// addresses into ptrs[pos[i]].
+static bool host_dev_ptr_ok(gr_hip_ctx *c, const gr_hip_mbuf *m, uint32_t n, uint64_t *ptrs, const uint32_t *pos) {
 	// the caller holds c->mu
 	if (c->hregs.empty())
 		return false;
@@ -1686,7 +1691,7 @@ static bool host_dev_ptr_ok(gr_hip_ctx *c, const gr_hip_mbuf *m, uint32_t n, uin
 		const uintptr_t p = reinterpret_cast<uintptr_t>(m[i].frame);
 		if ((p & 15) || (p - hit->host >= hit->len && (hit = hreg_find(c, p)) == nullptr))
 			return false;
-		ptrs[i] = hit->dev + (p - hit->host);
+		ptrs[pos[i]] = hit->dev + (p - hit->host);
 	}
 	return true;
 }
@@ -1748,9 +1753,28 @@ extern "C" int gr_hip_host_dev_addr(gr_hip_ctx_t *c, const void *ptr, uint64_t *
 	return 0;
 }
 
-// The node's walk (include/grout_hip.h, "rte_graph node shim"): stage the
-// mbufs' header lines into the queue's pinned buffers, forward them on the
-// GPU, hand them back with the context's iface / nexthop mirrors.
+// A kernel that gave up (-ETIMEDOUT) wrote each 64-packet tile's lines and
+// verdicts together or not at all (the storer stores a whole tile once it
+// took it): a verdict still holding the fill value was not processed, its
+// frame is untouched. Those packets go back to grout's CPU nodes (PUNT).
+#define NODE_V_FILL 0xff
+
+static uint32_t node_unfinished(const gr_hip_mbuf *m, uint32_t n, const uint32_t *pos, gr_hip_verdict *v) {
+	uint32_t k = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		gr_hip_verdict &x = v[pos[i]];
+		if (x.edge != NODE_V_FILL)
+			continue;
+		x = gr_hip_verdict{GR_HIP_E_PUNT, 0, m[i].iface, 0};
+		k++;
+	}
+	return k;
+}
+
+// The node's walk (include/grout_hip.h, "rte_graph node shim"): lay the
+// graph walks out on 64-packet tiles, stage the mbufs' header lines (or
+// frame addresses) into the queue's pinned buffers, forward them on the GPU,
+// hand them back with the context's iface / nexthop mirrors.
 extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst,
 				   struct gr_hip_node_stats *stats) {
 	if (q == nullptr || (n && m == nullptr))
@@ -1758,8 +1782,15 @@ extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uin
 	if (n == 0)
 		return 0;
 	gr_hip_ctx *c = q->ctx;
-	if (n > q->node_cap) {
-		hipSetDevice(c->dev);
+	if (q->node_pos.size() < n)
+		q->node_pos.resize(n);
+	uint32_t *pos = q->node_pos.data();
+	const int staged = gr_hip_node_layout(m, n, burst, pos);
+	if (staged < 0)
+		return staged;
+	const uint32_t ns = (uint32_t)staged;
+	hipSetDevice(c->dev);
+	if (ns > q->node_cap) {
 		hipHostFree(q->node_lines);
 		hipHostFree(q->node_out);
 		hipHostFree(q->node_meta);
@@ -1768,45 +1799,59 @@ extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uin
 		q->node_meta = nullptr;
 		q->node_v = nullptr;
 		q->node_cap = 0;
-		HCK(hipHostMalloc((void **)&q->node_lines, (size_t)n * GR_HIP_LINE, hipHostMallocDefault));
-		HCK(hipHostMalloc((void **)&q->node_out, (size_t)n * GR_HIP_LINE, hipHostMallocDefault));
-		HCK(hipHostMalloc((void **)&q->node_meta, (size_t)n * sizeof(gr_hip_pkt_meta), hipHostMallocDefault));
-		HCK(hipHostMalloc((void **)&q->node_v, (size_t)n * sizeof(gr_hip_verdict), hipHostMallocDefault));
-		q->node_cap = n;
+		HCK(hipHostMalloc((void **)&q->node_lines, (size_t)ns * GR_HIP_LINE, hipHostMallocDefault));
+		HCK(hipHostMalloc((void **)&q->node_out, (size_t)ns * GR_HIP_LINE, hipHostMallocDefault));
+		HCK(hipHostMalloc((void **)&q->node_meta, (size_t)ns * sizeof(gr_hip_pkt_meta), hipHostMallocDefault));
+		HCK(hipHostMalloc((void **)&q->node_v, (size_t)ns * sizeof(gr_hip_verdict), hipHostMallocDefault));
+		q->node_cap = ns;
 	}
+	if (q->d_pad == nullptr) { // the frame a pad slot points at (frames by address)
+		HCK(hipMalloc((void **)&q->d_pad, GR_HIP_LINE));
+		HCK(hipMemset(q->d_pad, 0, GR_HIP_LINE));
+	}
+	memset(q->node_v, NODE_V_FILL, (size_t)ns * sizeof(gr_hip_verdict));
 	std::shared_lock<std::shared_mutex> lk(c->mu); // see gr_hip_fwd4_submit
-	if (c->node_ptrs && host_dev_ptr_ok(c, m, n, reinterpret_cast<uint64_t *>(q->node_lines))) {
+	uint64_t *ptrs = reinterpret_cast<uint64_t *>(q->node_lines);
+	const bool by_addr = c->node_ptrs && host_dev_ptr_ok(c, m, n, ptrs, pos);
+	int r;
+	if (by_addr) {
 		// the frames are device-accessible: hand them over by address, the
 		// kernel reads and rewrites them in place over PCIe
-		int r = gr_hip_node_stage(m, n, nullptr, q->node_meta);
-		if (r < 0)
+		for (uint32_t i = 0, next = 0; i <= n; i++) { // pads point at a zeroed device line
+			const uint32_t at = i < n ? pos[i] : ns;
+			for (; next < at; next++)
+				ptrs[next] = reinterpret_cast<uint64_t>(q->d_pad);
+			next = at + 1;
+		}
+		if ((r = gr_hip_node_stage(m, n, burst, pos, nullptr, q->node_meta)) < 0)
 			return r;
 		void *d_ptrs, *d_meta, *d_v;
 		if (!host_dev_ptr(q->node_lines, &d_ptrs) || !host_dev_ptr(q->node_meta, &d_meta)
 		    || !host_dev_ptr(q->node_v, &d_v))
 			return -EFAULT;
 		gr_hip_batch b = {d_ptrs, nullptr, static_cast<const gr_hip_pkt_meta *>(d_meta),
-				  static_cast<gr_hip_verdict *>(d_v), n, 0, 0,
+				  static_cast<gr_hip_verdict *>(d_v), ns, 0, 0,
 				  GR_HIP_BATCH_F_LINES_ONLY | GR_HIP_BATCH_F_FRAME_PTRS};
 		// after everything already submitted on the queue, like gr_hip_fwd4_host
 		if ((r = launch(q, q->s, &b, true)) < 0)
 			return r;
 		HCK(hipStreamSynchronize(q->s));
-		if ((r = q_check(q)) < 0)
+		r = q_check(q);
+	} else {
+		lk.unlock(); // gr_hip_fwd4_host takes it itself
+		if ((r = gr_hip_node_stage(m, n, burst, pos, q->node_lines, q->node_meta)) < 0)
 			return r;
-		return gr_hip_node_apply(m, n, nullptr, 0, q->node_v, c->ifaces.data(), c->max_ifaces, c->nh.data(),
-					 (uint32_t)c->nh.size(), burst, stats);
+		r = gr_hip_fwd4_host(q, q->node_lines, q->node_meta, ns, q->node_out, q->node_v);
+		lk.lock();
 	}
-	lk.unlock(); // gr_hip_fwd4_host takes it itself
-	int r = gr_hip_node_stage(m, n, q->node_lines, q->node_meta);
-	if (r < 0)
+	uint32_t unfinished = 0;
+	if (r == -ETIMEDOUT) // hand back what the GPU finished, the rest to grout's CPU nodes
+		unfinished = node_unfinished(m, n, pos, q->node_v);
+	else if (r < 0)
 		return r;
-	r = gr_hip_fwd4_host(q, q->node_lines, q->node_meta, n, q->node_out, q->node_v);
-	if (r < 0)
-		return r;
-	std::shared_lock<std::shared_mutex> l(c->mu);
-	return gr_hip_node_apply(m, n, q->node_out, GR_HIP_LINE, q->node_v, c->ifaces.data(), c->max_ifaces, c->nh.data(),
-				 (uint32_t)c->nh.size(), burst, stats);
+	r = gr_hip_node_apply(m, n, burst, pos, by_addr ? nullptr : q->node_out, GR_HIP_LINE, q->node_v,
+			      c->ifaces.data(), c->max_ifaces, c->nh.data(), (uint32_t)c->nh.size(), stats);
+	return r < 0 ? r : (int)unfinished;
 }
 
 extern "C" int gr_hip_queue_stats(gr_hip_queue_t *q, struct gr_hip_iface_stats *st, uint32_t max, int reset) {

@@ -113,16 +113,59 @@ extern "C" int gr_hip_edge_node(uint8_t edge, uint32_t nh, int ip6) {
 	return edge_node(edge, nh, ip6);
 }
 
-extern "C" int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, void *lines, struct gr_hip_pkt_meta *meta) {
+// Walk boundaries of the node's mbufs (include/grout_hip.h,
+// gr_hip_node_layout): a walk starts at m[0], at GR_HIP_MBUF_F_WALK, and
+// `burst` mbufs after the previous start.
+static inline uint32_t walk_burst(uint32_t burst) {
+	return burst == 0 || burst > 64 ? 64 : burst;
+}
+
+static inline bool walk_start(const struct gr_hip_mbuf *m, uint32_t i, uint32_t start, uint32_t burst) {
+	return i == 0 || (m[i].flags & GR_HIP_MBUF_F_WALK) || i - start == burst;
+}
+
+extern "C" int gr_hip_node_layout(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, uint32_t *pos) {
+	if (n && (m == nullptr || pos == nullptr))
+		return -EINVAL;
+	burst = walk_burst(burst);
+	uint32_t p = 0;
+	for (uint32_t i = 0; i < n;) {
+		// this walk: [i, e)
+		uint32_t e = i + 1;
+		while (e < n && !walk_start(m, e, i, burst))
+			e++;
+		const uint32_t len = e - i;
+		if ((p & 63) + len > 64) // would straddle a tile: start it on the next one
+			p = (p + 63) & ~63u;
+		for (uint32_t k = i; k < e; k++)
+			pos[k] = p++;
+		i = e;
+	}
+	if (p > INT32_MAX)
+		return -E2BIG;
+	return (int)p;
+}
+
+extern "C" int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, const uint32_t *pos,
+				 void *lines, struct gr_hip_pkt_meta *meta) {
 	if (n && (m == nullptr || meta == nullptr))
 		return -EINVAL;
+	burst = walk_burst(burst);
 	uint8_t *L = static_cast<uint8_t *>(lines);
 	constexpr uint32_t AHEAD = 16; // frames in flight: staging is bound by their cache misses
 	for (uint32_t i = 0; i < n && i < AHEAD && L != nullptr; i++)
 		__builtin_prefetch(m[i].frame, 0, 0);
+	uint32_t start = 0, next = 0; // next: first slot not yet written
 	for (uint32_t i = 0; i < n; i++) {
 		if (i + AHEAD < n && L != nullptr)
 			__builtin_prefetch(m[i + AHEAD].frame, 0, 0);
+		const uint32_t at = pos != nullptr ? pos[i] : i;
+		for (; next < at; next++) { // a pad slot: punted by the kernel, counted nowhere
+			meta[next] = gr_hip_pkt_meta{0, 0, 0, 0};
+			if (L != nullptr)
+				memset(L + (size_t)next * GR_HIP_LINE, 0, GR_HIP_LINE);
+		}
+		next = at + 1;
 		// 64 bytes whatever data_len says: grout's nodes read the Ethernet and
 		// IPv4 headers from the data room without a length check (eth_input.c
 		// reads 14 bytes of a shorter frame), and an mbuf's data room always
@@ -130,11 +173,16 @@ extern "C" int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, void *
 		if (m[i].frame == nullptr)
 			return -EINVAL;
 		if (L != nullptr) // NULL: metadata only (the GPU reads the frames itself)
-			memcpy(L + (size_t)i * GR_HIP_LINE, m[i].frame, GR_HIP_LINE);
-		meta[i].iface = m[i].iface;
-		meta[i].vlan_ck = (uint16_t)((m[i].vlan_id & 0xfff) | ((m[i].ck & 3) << 12));
-		meta[i].pkt_len = (uint16_t)(m[i].pkt_len > 0xffff ? 0xffff : m[i].pkt_len);
-		meta[i].rss = (uint16_t)m[i].rss;
+			memcpy(L + (size_t)at * GR_HIP_LINE, m[i].frame, GR_HIP_LINE);
+		uint16_t vc = (uint16_t)((m[i].vlan_id & 0xfff) | ((m[i].ck & 3) << 12));
+		if (walk_start(m, i, start, burst)) {
+			start = i;
+			vc |= GR_HIP_META_WALK;
+		}
+		meta[at].iface = m[i].iface;
+		meta[at].vlan_ck = vc;
+		meta[at].pkt_len = (uint16_t)(m[i].pkt_len > 0xffff ? 0xffff : m[i].pkt_len);
+		meta[at].rss = (uint16_t)m[i].rss;
 	}
 	return 0;
 }
@@ -142,6 +190,8 @@ extern "C" int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, void *
 extern "C" int gr_hip_node_apply(
 	struct gr_hip_mbuf *m,
 	uint32_t n,
+	uint32_t burst,
+	const uint32_t *pos,
 	const void *lines,
 	uint32_t line_stride,
 	const struct gr_hip_verdict *verdicts,
@@ -149,15 +199,13 @@ extern "C" int gr_hip_node_apply(
 	uint32_t n_ifaces,
 	const struct gr_hip_nh *nh,
 	uint32_t n_nh,
-	uint32_t burst,
 	struct gr_hip_node_stats *stats
 ) {
 	if (n == 0)
 		return 0;
 	if (m == nullptr || verdicts == nullptr || (lines != nullptr && line_stride < GR_HIP_LINE))
 		return -EINVAL;
-	if (burst == 0)
-		burst = 64;
+	burst = walk_burst(burst);
 	const uint8_t *L = static_cast<const uint8_t *>(lines);
 	// the nodes an IPv4 / IPv6 packet walks, in order
 	static const int path4[] = {GR_HIP_NODE_IFACE_INPUT, GR_HIP_NODE_ETH_INPUT, GR_HIP_NODE_IP_INPUT,
@@ -174,7 +222,7 @@ extern "C" int gr_hip_node_apply(
 	static_assert(GR_HIP_NODE_COUNT == 10 && GR_HIP_NODE_IP6_INPUT == 7, "node order");
 	uint32_t ended[2][7] = {}; // packets of the walk that stopped at depth d, per family
 	uint32_t reach[GR_HIP_NODE_COUNT] = {};
-	uint32_t left = burst; // packets left in the current graph walk
+	uint32_t start = 0; // first mbuf of the current graph walk
 	// frames read (the ether type) and written back: prefetch them, the loop
 	// is bound by their cache misses
 	constexpr uint32_t AHEAD = 16;
@@ -184,9 +232,10 @@ extern "C" int gr_hip_node_apply(
 		if (i + AHEAD < n)
 			__builtin_prefetch(m[i + AHEAD].frame, 1, 0);
 		struct gr_hip_mbuf &b = m[i];
-		const struct gr_hip_verdict &v = verdicts[i];
+		const uint32_t at = pos != nullptr ? pos[i] : i;
+		const struct gr_hip_verdict &v = verdicts[at];
 		// lines NULL: the GPU rewrote the frames in place already
-		const uint8_t *line = L != nullptr ? L + (size_t)i * line_stride : static_cast<const uint8_t *>(b.frame);
+		const uint8_t *line = L != nullptr ? L + (size_t)at * line_stride : static_cast<const uint8_t *>(b.frame);
 		const bool ip6 = line[12] == 0x86 && line[13] == 0xdd; // RTE_ETHER_TYPE_IPV6
 		const int node = edge_node(v.edge, v.nh, ip6);
 		if (node < -1)
@@ -239,8 +288,8 @@ extern "C" int gr_hip_node_apply(
 			b.domain = v.domain;
 			b.nh = v.nh;
 		}
-		if (--left == 0 || i + 1 == n) { // a graph walk of `burst` packets ends here
-			left = burst;
+		if (i + 1 == n || walk_start(m, i + 1, start, burst)) { // this graph walk ends here
+			start = i + 1;
 			if (stats == nullptr)
 				continue;
 			// a packet that stopped at depth d passed every node before it

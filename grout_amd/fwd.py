@@ -228,7 +228,9 @@ class Queue:
         Returns the per-node counters of this call (abi.NODE_STATS_DT)."""
         assert mbufs.dtype == abi.MBUF_DT and mbufs.flags["C_CONTIGUOUS"]
         ns = np.zeros(1, dtype=abi.NODE_STATS_DT)
-        check("gr_hip_node_process", self.lib.gr_hip_node_process(self._h, ptr(mbufs), len(mbufs), burst, ptr(ns)))
+        r = check("gr_hip_node_process", self.lib.gr_hip_node_process(self._h, ptr(mbufs), len(mbufs), burst,
+                                                                     ptr(ns)))
+        self.unfinished = r  # mbufs handed back as PUNT because a kernel gave up
         return ns[0]
 
     def stats(self, reset=False):

@@ -151,12 +151,17 @@ static void hand_back(struct rte_mbuf *m, const struct gr_hip_mbuf *v) {
 static void flush(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
 	if (w->n == 0)
 		return;
-	if (gr_hip_node_process(w->q, w->v, w->n, conf.rx_burst, &w->stats) < 0) {
-		// the GPU could not take them: grout's CPU nodes do, unchanged
+	const int r = gr_hip_node_process(w->q, w->v, w->n, conf.rx_burst, &w->stats);
+	if (r < 0) {
+		// the GPU could not take them (mbufs untouched): grout's CPU nodes do
 		w->gpu_errors++;
 		for (uint32_t i = 0; i < w->n; i++)
 			rte_node_enqueue_x1(graph, node, GR_HIP_E_PUNT, w->mbufs[i]);
 	} else {
+		// r > 0: a kernel gave up; the packets it did not reach come back
+		// as PUNT with their frames untouched, the others forwarded as usual
+		if (r > 0)
+			w->gpu_errors++;
 		for (uint32_t i = 0; i < w->n; i++) {
 			if (w->v[i].edge != GR_HIP_E_PUNT)
 				hand_back(w->mbufs[i], &w->v[i]);
@@ -169,6 +174,7 @@ static void flush(struct rte_graph *graph, struct rte_node *node, struct gpu_wal
 
 static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node, void **objs, uint16_t nb_objs) {
 	struct gpu_walk *w = gpu_fwd4_ctx(node)->w;
+	uint8_t walk = GR_HIP_MBUF_F_WALK; // this call is one graph walk's iface_input stream
 	for (uint16_t i = 0; i < nb_objs; i++) {
 		struct rte_mbuf *m = objs[i];
 		if (m->nb_segs > 1 || gr_mbuf_is_traced(m)) { // grout's CPU nodes
@@ -189,7 +195,9 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 			.iface = d->iface != NULL ? d->iface->id : 0,
 			.vlan_id = d->vlan_id,
 			.ck = ck_status(m->ol_flags),
+			.flags = walk,
 		};
+		walk = 0;
 	}
 	if (w->n == 0)
 		return nb_objs;

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define GR_HIP_ABI_VERSION 2
+#define GR_HIP_ABI_VERSION 3
 
 // ---------------------------------------------------------------------------
 // Values mirrored from grout's public API (identical numbering).
@@ -277,10 +277,21 @@ struct gr_hip_route6 {
 struct gr_hip_pkt_meta {
 	uint16_t iface; // iface_mbuf_data.iface (RX port iface id)
 	uint16_t vlan_ck; // bits 0-11: iface_mbuf_data.vlan_id;
-	                  // bits 12-13: GR_HIP_CKSUM_* from ol_flags
+	                  // bits 12-13: GR_HIP_CKSUM_* from ol_flags;
+	                  // bit 14: GR_HIP_META_WALK
 	uint16_t pkt_len; // rte_pktmbuf_pkt_len == data_len (single segment)
 	uint16_t rss; // low 16 bits of m->hash.rss (reta_size <= 4096)
 };
+// Graph walks. grout runs the nodes of one rte_graph_walk over at most 64
+// packets (graph.c:88-91: vector_max 64, each RX queue's burst a share of
+// it), and eth_output keeps a per-walk cache of the last source MAC it
+// looked up (eth_output.c:37-59): after an eth_output_no_mac packet the next
+// packet of the cached iface in the same walk leaves with source MAC
+// 00:00:00:00:00:00. A batch is therefore cut into walks: one starts at
+// packet 0, at every multiple of 64 and at every packet whose metadata has
+// this bit. The rte_graph node (gr_hip_node_process) sets it at the start
+// of each walk and pads so that no walk straddles a multiple of 64.
+#define GR_HIP_META_WALK 0x4000
 
 // Output verdict, 8 bytes per packet.
 struct gr_hip_verdict {
@@ -437,7 +448,10 @@ int gr_hip_tune(gr_hip_ctx_t *, const char *key, int value);
 // metadata in host memory in, lines and verdicts back to host memory. On
 // pinned buffers the kernel reads and writes them over PCIe itself
 // ("host_direct"); otherwise chunks are copied through the queue's device
-// staging on 3 streams. Completes before return.
+// staging on 3 streams. Completes before return. On -ETIMEDOUT (a kernel
+// gave up, see gr_hip_queue_sync) every 64-packet tile was either processed
+// whole or not at all: the verdicts of the packets it did not reach are
+// left as they were (the staged path fills them with 0xff bytes).
 int gr_hip_fwd4_host(
 	gr_hip_queue_t *,
 	const void *lines,
@@ -505,9 +519,12 @@ struct gr_hip_mbuf {
 	uint8_t ck; // in: GR_HIP_CKSUM_* from ol_flags
 	uint8_t edge; // out: enum gr_hip_edge, the next node
 	uint8_t domain; // out: eth_input_mbuf_data.domain
-	uint8_t _pad;
+	uint8_t flags; // in: GR_HIP_MBUF_F_*
 	uint32_t nh; // out: l3_mbuf_data.nh as a nexthop slot (0 = NULL)
 };
+// This mbuf starts a graph walk: the node sets it on the first mbuf of each
+// process() call (one rte_graph_walk's iface_input stream).
+#define GR_HIP_MBUF_F_WALK 0x01
 
 #define GR_HIP_PTYPE_L3_IPV4 0x10 // RTE_PTYPE_L3_IPV4 (rte_mbuf_ptype.h)
 #define GR_HIP_PTYPE_L3_IPV6 0x40 // RTE_PTYPE_L3_IPV6 (rte_mbuf_ptype.h)
@@ -542,21 +559,34 @@ struct gr_hip_node_stats {
 // the packet is IPv6 (the eth_output / iface_output edges are shared).
 int gr_hip_edge_node(uint8_t edge, uint32_t nh, int ip6);
 
+// Graph walks of n mbufs: one starts at m[0], at every mbuf with
+// GR_HIP_MBUF_F_WALK, and `burst` (1..64; 0 = 64) mbufs after the previous
+// start. The staged layout puts mbuf i at pos[i], padding so that no walk
+// straddles a multiple of 64 packets (the kernel resolves eth_output's
+// per-walk cache inside a 64-packet tile, see GR_HIP_META_WALK). Returns
+// the number of staged slots (>= n), or -errno.
+int gr_hip_node_layout(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, uint32_t *pos);
+
 // Stage n mbufs: the first 64 bytes at each frame (read whatever data_len
 // says, as grout's nodes do: an mbuf's data room always has them) into
-// lines[i * 64] (lines NULL: skipped), and their metadata.
-int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, void *lines, struct gr_hip_pkt_meta *meta);
+// lines[pos[i] * 64] (lines NULL: skipped), and their metadata, with
+// GR_HIP_META_WALK at each walk start. pos NULL: pos[i] = i. Slots the
+// layout leaves free get metadata with iface 0 (the kernel punts them, they
+// count nowhere) and zeroed lines.
+int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, const uint32_t *pos, void *lines,
+		      struct gr_hip_pkt_meta *meta);
 
 // Hand back: apply the fast path's verdicts and rewritten header lines
-// (line_stride apart; lines NULL: the frames were rewritten in place) to the
-// mbufs. ifaces[id] / nh[slot] are the mirrors
-// pushed with gr_hip_iface_set / gr_hip_nh_set (the egress VLAN tag and the
-// ingress VLAN demux are read from them). stats (optional) accumulates the
-// per-node counters, the packets taken as consecutive graph walks of
-// `burst` packets.
+// (slot pos[i], line_stride apart; lines NULL: the frames were rewritten in
+// place) to the mbufs. ifaces[id] / nh[slot] are the mirrors pushed with
+// gr_hip_iface_set / gr_hip_nh_set (the egress VLAN tag and the ingress VLAN
+// demux are read from them). stats (optional) accumulates the per-node
+// counters of the graph walks (as gr_hip_node_layout cuts them).
 int gr_hip_node_apply(
 	struct gr_hip_mbuf *m,
 	uint32_t n,
+	uint32_t burst,
+	const uint32_t *pos,
 	const void *lines,
 	uint32_t line_stride,
 	const struct gr_hip_verdict *verdicts,
@@ -564,7 +594,6 @@ int gr_hip_node_apply(
 	uint32_t n_ifaces,
 	const struct gr_hip_nh *nh,
 	uint32_t n_nh,
-	uint32_t burst,
 	struct gr_hip_node_stats *stats
 );
 
@@ -573,7 +602,10 @@ int gr_hip_node_apply(
 // gr_hip_host_register (and is 16-byte aligned), the GPU reads and rewrites
 // the frames in place over PCIe and only 8-byte frame addresses and metadata
 // are staged ("node_ptrs", default on); otherwise header lines are staged
-// through gr_hip_fwd4_host.
+// through gr_hip_fwd4_host. Returns the number of mbufs handed back as
+// GR_HIP_E_PUNT, untouched, because a kernel gave up before reaching them
+// (0 normally; the others are handed back as usual), or -errno with every
+// mbuf untouched.
 int gr_hip_node_process(gr_hip_queue_t *, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst,
 			struct gr_hip_node_stats *stats);
 

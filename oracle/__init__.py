@@ -49,6 +49,8 @@ API = {
     "or_bench": (ctypes.c_double, [_P, _P, _U32, _P, _U32, _I, _U64, ctypes.POINTER(_U64)]),
 }
 
+OR_F_MBUF_WALKS = 0x80000000  # oracle.h
+
 _lib = None
 
 
@@ -151,7 +153,9 @@ class Oracle:
     def process_mbufs(self, frames, meta, lines_only=False):
         """-> (out_lines, verdicts, stats, mbufs, node_stats): process() plus
         the mbuf state at each edge (abi.MBUF_DT, RX data_off 128) and the
-        per-node counters of the bursts of 64."""
+        per-node counters. Graph walks as the rte_graph node cuts mbufs
+        (OR_F_MBUF_WALKS): at each abi.META_WALK mark and 64 packets after
+        the previous start."""
         frames = np.ascontiguousarray(frames)
         meta = np.ascontiguousarray(meta, dtype=abi.META_DT)
         n = len(meta)
@@ -163,7 +167,8 @@ class Oracle:
         ns = np.zeros(1, dtype=abi.NODE_STATS_DT)
         _ck("or_process_ex", self.L.or_process_ex(self.h, frames.ctypes.data, stride, meta.ctypes.data, n,
                                                   out.ctypes.data, abi.LINE, v.ctypes.data, st.ctypes.data,
-                                                  abi.BATCH_F_LINES_ONLY if lines_only else 0, mb.ctypes.data,
+                                                  (abi.BATCH_F_LINES_ONLY if lines_only else 0) | OR_F_MBUF_WALKS,
+                                                  mb.ctypes.data,
                                                   ns.ctypes.data))
         return out, v, st, mb, ns[0]
 

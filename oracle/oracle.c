@@ -733,15 +733,23 @@ struct or_stream {
 	uint16_t n;
 };
 
+// The nodes after iface_input, by enum gr_hip_node.
 struct or_graph {
 	const or_topo_t *t;
 	uint32_t flags;
 	uint32_t readable; // frame bytes present: 64 (lines only) or in_stride
-	struct or_stream eth_input, ip_input, ip_forward, ip_output, eth_output, iface_output;
-	struct or_stream ip6_input, ip6_forward, ip6_output;
+	struct or_stream st[GR_HIP_NODE_COUNT];
+	// rte_graph's pending queue [DPDK lib/graph rte_graph_walk]: a node
+	// joins its tail when its stream goes from empty to non-empty, the walk
+	// runs the queue head first (so a node may run again later in the walk)
+	uint8_t pend[4 * GR_HIP_NODE_COUNT];
+	uint32_t pend_head, pend_tail;
 };
 
-static inline void enqueue(struct or_stream *s, struct or_mbuf *m) {
+static inline void enqueue(struct or_graph *g, int node, struct or_mbuf *m) {
+	struct or_stream *s = &g->st[node];
+	if (s->n == 0)
+		g->pend[g->pend_tail++ % (4 * GR_HIP_NODE_COUNT)] = (uint8_t)node;
 	s->objs[s->n++] = m;
 }
 
@@ -781,7 +789,7 @@ static void node_iface_input(struct or_graph *g, struct or_mbuf **objs, uint16_t
 		if (iface->mode >= GR_HIP_IFACE_MODE_COUNT)
 			e = GR_HIP_E_IFACE_MODE_UNKNOWN;
 		if (e == NEXT)
-			enqueue(&g->eth_input, m);
+			enqueue(g, GR_HIP_NODE_ETH_INPUT, m);
 		else
 			terminal(m, e);
 	}
@@ -819,9 +827,9 @@ static void node_eth_input(struct or_graph *g, struct or_mbuf **objs, uint16_t n
 		mbuf_adj(m, 14);
 		uint8_t e = t->eth_edges[type_be];
 		if (e == NEXT)
-			enqueue(&g->ip_input, m);
+			enqueue(g, GR_HIP_NODE_IP_INPUT, m);
 		else if (e == NEXT6)
-			enqueue(&g->ip6_input, m);
+			enqueue(g, GR_HIP_NODE_IP6_INPUT, m);
 		else
 			terminal(m, e);
 	}
@@ -919,7 +927,7 @@ static void node_ip_input(struct or_graph *g, struct or_mbuf **objs, uint16_t n)
 		if (edge != NEXT)
 			goto next;
 		if (domain == GR_HIP_ETH_DOMAIN_LOOPBACK) { // :164-165 (not reachable from ports)
-			enqueue(&g->ip_output, m);
+			enqueue(g, GR_HIP_NODE_IP_OUTPUT, m);
 			continue;
 		} else if (h->type == GR_HIP_NH_T_L3) { // :166-187
 			if ((h->flags & GR_HIP_NH_F_LOCAL) && dst == h->ipv4) {
@@ -929,7 +937,7 @@ static void node_ip_input(struct or_graph *g, struct or_mbuf **objs, uint16_t n)
 				goto next;
 			}
 		}
-		enqueue(&g->ip_forward, m);
+		enqueue(g, GR_HIP_NODE_IP_FORWARD, m);
 		continue;
 next:
 		terminal(m, edge);
@@ -951,7 +959,7 @@ static void node_ip_forward(struct or_graph *g, struct or_mbuf **objs, uint16_t 
 		csum += csum >= 0xffff;
 		ip[10] = (uint8_t)csum;
 		ip[11] = (uint8_t)(csum >> 8);
-		enqueue(&g->ip_output, m);
+		enqueue(g, GR_HIP_NODE_IP_OUTPUT, m);
 	}
 }
 
@@ -997,7 +1005,7 @@ static void node_ip_output(struct or_graph *g, struct or_mbuf **objs, uint16_t n
 		}
 		memcpy(m->eth_dst, h->mac, 6); // :201-203
 		m->eth_type = be16(0x0800);
-		enqueue(&g->eth_output, m);
+		enqueue(g, GR_HIP_NODE_ETH_OUTPUT, m);
 		continue;
 next:
 		terminal(m, edge);
@@ -1065,7 +1073,7 @@ static void node_ip6_input(struct or_graph *g, struct or_mbuf **objs, uint16_t n
 			goto next;
 		}
 		m->l3_nh = nh; // :151-153
-		enqueue(&g->ip6_forward, m);
+		enqueue(g, GR_HIP_NODE_IP6_FORWARD, m);
 		continue;
 next:
 		m->l3_nh = nh;
@@ -1083,7 +1091,7 @@ static void node_ip6_forward(struct or_graph *g, struct or_mbuf **objs, uint16_t
 			continue;
 		}
 		ip[7] -= 1;
-		enqueue(&g->ip6_output, m);
+		enqueue(g, GR_HIP_NODE_IP6_OUTPUT, m);
 	}
 }
 
@@ -1124,31 +1132,43 @@ static void node_ip6_output(struct or_graph *g, struct or_mbuf **objs, uint16_t 
 		}
 		memcpy(m->eth_dst, h->mac, 6); // :122-127
 		m->eth_type = be16(0x86dd);
-		enqueue(&g->eth_output, m);
+		enqueue(g, GR_HIP_NODE_ETH_OUTPUT, m);
 		continue;
 next:
 		terminal(m, edge);
 	}
 }
 
-// eth_output_process, modules/infra/datapath/eth_output.c:28-77
+// eth_output_process, modules/infra/datapath/eth_output.c:27-77. The source
+// MAC is looked up only when the iface differs from last_iface_id, which a
+// failed lookup leaves as it was while zeroing the cached MAC (:51-58): in
+// one walk, after an eth_output_no_mac packet, the next packet of the cached
+// iface leaves with source MAC 00:00:00:00:00:00. gr_mbuf_prepend (:43-49,
+// mbuf.h:89-106) cannot fail here: eth_input's adj(14) left the headroom.
 static void node_eth_output(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
 	const or_topo_t *t = g->t;
+	uint16_t last_iface_id = GR_HIP_IFACE_ID_UNDEF;
+	uint8_t src_mac[6] = {0};
 	for (uint16_t i = 0; i < n; i++) {
 		struct or_mbuf *m = objs[i];
-		mbuf_prepend(m, 14); // gr_mbuf_prepend, mbuf.h:89-106
+		mbuf_prepend(m, 14);
 		uint8_t *eth = MTOD(m);
-		memcpy(eth, m->eth_dst, 6);
-		const struct gr_hip_iface *iface = iface_from_id(t, m->iface);
-		if (iface == NULL || !iface->mac_ok) {
-			terminal(m, GR_HIP_E_ETH_OUTPUT_NO_MAC);
-			m->vlan_id = 0;
-			continue;
+		memcpy(eth, m->eth_dst, 6); // :50
+		if (m->iface != last_iface_id) {
+			const struct gr_hip_iface *iface = iface_from_id(t, m->iface);
+			if (iface == NULL || !iface->mac_ok) { // iface_get_eth_addr() < 0
+				memset(src_mac, 0, 6);
+				terminal(m, GR_HIP_E_ETH_OUTPUT_NO_MAC);
+				m->vlan_id = 0; // :71
+				continue;
+			}
+			memcpy(src_mac, iface->mac, 6);
+			last_iface_id = m->iface;
 		}
-		memcpy(eth + 6, iface->mac, 6);
-		memcpy(eth + 12, &m->eth_type, 2);
-		m->vlan_id = 0; // :325
-		enqueue(&g->iface_output, m);
+		memcpy(eth + 6, src_mac, 6); // :59
+		memcpy(eth + 12, &m->eth_type, 2); // :60
+		m->vlan_id = 0; // :71
+		enqueue(g, GR_HIP_NODE_IFACE_OUTPUT, m);
 	}
 }
 
@@ -1185,27 +1205,50 @@ static void mark(struct or_mbuf **objs, uint16_t n, int node) {
 		objs[i]->visited |= (uint16_t)(1u << node);
 }
 
-// One graph walk over a burst (rte_graph_walk RTC order, main_loop.c:459).
+// One graph walk over a burst (rte_graph_walk from gr_datapath_loop,
+// main_loop.c): iface_input on the RX burst, then the pending queue in order.
 static void graph_walk(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
 	mark(objs, n, GR_HIP_NODE_IFACE_INPUT);
 	node_iface_input(g, objs, n);
-#define RUN(name, node)                                                                            \
-	if (g->name.n) {                                                                           \
-		uint16_t k = g->name.n;                                                            \
-		g->name.n = 0;                                                                     \
-		mark(g->name.objs, k, node);                                                       \
-		node_##name(g, g->name.objs, k);                                                   \
+	struct or_mbuf *batch[OR_BURST];
+	while (g->pend_head != g->pend_tail) {
+		const int node = g->pend[g->pend_head++ % (4 * GR_HIP_NODE_COUNT)];
+		struct or_stream *s = &g->st[node];
+		const uint16_t k = s->n;
+		memcpy(batch, s->objs, k * sizeof(batch[0]));
+		s->n = 0;
+		mark(batch, k, node);
+		switch (node) {
+		case GR_HIP_NODE_ETH_INPUT:
+			node_eth_input(g, batch, k);
+			break;
+		case GR_HIP_NODE_IP_INPUT:
+			node_ip_input(g, batch, k);
+			break;
+		case GR_HIP_NODE_IP_FORWARD:
+			node_ip_forward(g, batch, k);
+			break;
+		case GR_HIP_NODE_IP_OUTPUT:
+			node_ip_output(g, batch, k);
+			break;
+		case GR_HIP_NODE_IP6_INPUT:
+			node_ip6_input(g, batch, k);
+			break;
+		case GR_HIP_NODE_IP6_FORWARD:
+			node_ip6_forward(g, batch, k);
+			break;
+		case GR_HIP_NODE_IP6_OUTPUT:
+			node_ip6_output(g, batch, k);
+			break;
+		case GR_HIP_NODE_ETH_OUTPUT:
+			node_eth_output(g, batch, k);
+			break;
+		case GR_HIP_NODE_IFACE_OUTPUT:
+			node_iface_output(g, batch, k);
+			break;
+		}
 	}
-	RUN(eth_input, GR_HIP_NODE_ETH_INPUT)
-	RUN(ip_input, GR_HIP_NODE_IP_INPUT)
-	RUN(ip_forward, GR_HIP_NODE_IP_FORWARD)
-	RUN(ip_output, GR_HIP_NODE_IP_OUTPUT)
-	RUN(ip6_input, GR_HIP_NODE_IP6_INPUT)
-	RUN(ip6_forward, GR_HIP_NODE_IP6_FORWARD)
-	RUN(ip6_output, GR_HIP_NODE_IP6_OUTPUT)
-	RUN(eth_output, GR_HIP_NODE_ETH_OUTPUT)
-	RUN(iface_output, GR_HIP_NODE_IFACE_OUTPUT)
-#undef RUN
+	g->pend_head = g->pend_tail = 0;
 }
 
 // Node counters of one walk as rte_graph keeps them (main_loop.c:39-64):
@@ -1319,14 +1362,23 @@ int or_process_ex(
 		mb[i].buf = bufs + (size_t)i * OR_DATAROOM;
 	const uint8_t *in = in_frames;
 	uint8_t *out = out_lines;
-	for (uint32_t base = 0; base < n; base += OR_BURST) {
-		uint16_t k = (uint16_t)((n - base) < OR_BURST ? (n - base) : OR_BURST);
+	for (uint32_t base = 0, k; base < n; base += k) {
+		// this graph walk: up to the next GR_HIP_META_WALK mark, at most 64
+		// packets (graph.c:88-91) and, for a batch (not OR_F_MBUF_WALKS),
+		// never past a multiple of 64 (include/grout_hip.h)
+		uint32_t end = base + OR_BURST;
+		if (!(flags & OR_F_MBUF_WALKS))
+			end = (base / OR_BURST + 1) * OR_BURST;
+		if (end > n)
+			end = n;
+		for (k = 1; base + k < end && !(meta[base + k].vlan_ck & GR_HIP_META_WALK); k++)
+			;
 		for (uint16_t i = 0; i < k; i++) {
 			const struct gr_hip_pkt_meta *md = &meta[base + i];
 			rx_fill(&mb[i], in + (size_t)(base + i) * in_stride, readable, md);
 			objs[i] = &mb[i];
 		}
-		graph_walk(&g, objs, k);
+		graph_walk(&g, objs, (uint16_t)k);
 		for (uint16_t i = 0; i < k; i++) {
 			const struct or_mbuf *m = &mb[i];
 			struct gr_hip_verdict *o = &v[base + i];
@@ -1364,7 +1416,7 @@ int or_process_ex(
 			}
 		}
 		if (ns != NULL)
-			walk_node_stats(mb, k, ns);
+			walk_node_stats(mb, (uint16_t)k, ns);
 	}
 	free(bufs);
 	return 0;

@@ -75,6 +75,12 @@ uint32_t or_lpm_brute(const or_topo_t *, uint16_t vrf_id, uint32_t ip);
 
 // Run n packets through the node chain. Same buffer contract as
 // struct gr_hip_batch (grout_hip.h). stats: max_ifaces entries, accumulated.
+// Graph walks as a batch defines them (GR_HIP_META_WALK): one starts at
+// packet 0, at each multiple of 64 and at each marked packet.
+// OR_F_MBUF_WALKS (a flags bit): walks as the rte_graph node cuts its mbufs
+// instead (gr_hip_node_layout): at each marked packet and 64 packets after
+// the previous start, wherever that falls.
+#define OR_F_MBUF_WALKS 0x80000000u
 int or_process(
 	or_topo_t *,
 	const void *in_frames,

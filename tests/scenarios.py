@@ -355,3 +355,76 @@ def corpus_arrays(stride=STRIDE):
         meta[i]["rss"] = m["rss"]
         labels.append(lab)
     return frames, meta, labels
+
+
+# ---- eth_output's per-walk source-MAC cache (eth_output.c:37-59) ----------
+# Graph walks of packets from p0 in the corpus topology, each with the
+# positions (in the walk) that grout sends out with source MAC
+# 00:00:00:00:00:00, derived by hand from eth_output.c:37-59 and rte_graph's
+# pending-queue order (ip6_input before ip_input when it got a packet first).
+#   X  forward via p1 (nh "fwd")         Z  forward via p2 (nh "fwd2")
+#   Y  egress iface without a MAC        X6 IPv6 forward via p1 (nh "fwd6")
+#   Y6 IPv6 egress without a MAC         V  egress VLAN 200 (parent p1)
+#   D  egress iface admin down (eth_output runs, iface_output drops)
+#   T  ttl 1 (never reaches eth_output)
+ETH_OUTPUT_CACHE_WALKS = [
+    ("X Y X", {2}),
+    ("Y X", set()),
+    ("X Y Z X", set()),
+    ("X Y X X Z X", {2, 3}),
+    ("X6 X Y X X6", {3}),          # ip6_input first: [X6 X6 | X Y X]
+    ("X X6 Y X X6", {1, 3, 4}),    # ip_input first: [X Y X | X6 X6]
+    ("X Y6 X", set()),             # [X X | Y6]
+    ("X Y6 X6", {2}),              # [X | Y6 X6]
+    ("V Y V", {2}),
+    ("X Y T X", {3}),
+    ("D Y D", {2}),
+    ("X D Y X", set()),
+    ("X Y", set()),
+    ("X", set()),                  # a new walk: the cache starts empty
+    ("X Y " + "X " * 62, set(range(2, 64))),
+    ("Z Y Z Y Z X Y X", {2, 4, 7}),
+]
+
+
+def eth_output_cache_arrays(stride=STRIDE):
+    """frames, meta (abi.META_WALK at each walk start), labels, zero (bool:
+    grout sends the packet with a zero source MAC)."""
+    fr, f6 = S.frame, S.frame6
+    make = {
+        "X": lambda k: fr(dst="16.1.7.%d" % (k % 250 + 1)),
+        "Z": lambda k: fr(dst="10.90.1.%d" % (200 + k % 50)),
+        "Y": lambda k: fr(dst="10.76.0.%d" % (k % 250 + 1)),
+        "V": lambda k: fr(dst="10.74.0.%d" % (k % 250 + 1)),
+        "D": lambda k: fr(dst="10.73.0.%d" % (k % 250 + 1)),
+        "T": lambda k: fr(dst="16.1.7.%d" % (k % 250 + 1), ttl=1),
+        "X6": lambda k: f6(dst="2001:db8:100::%x" % (k + 1)),
+        "Y6": lambda k: f6(dst="2001:db8:107::%x" % (k + 1)),
+    }
+    rows, walk, zero, labels = [], [], [], []
+    k = 0
+    for w, (spec, z) in enumerate(ETH_OUTPUT_CACHE_WALKS):
+        syms = spec.split()
+        while len(rows) % 64 + len(syms) > 64:  # a batch walk never straddles a tile: pad
+            rows.append(None)
+            walk.append(True)
+            zero.append(False)
+            labels.append("pad")
+        for j, sym in enumerate(syms):
+            rows.append(make[sym](k))
+            walk.append(j == 0)
+            zero.append(j in z)
+            labels.append("walk %d %s[%d]" % (w, sym, j))
+            k += 1
+    n = len(rows)
+    frames = np.zeros((n, stride), dtype=np.uint8)
+    meta = np.zeros(n, dtype=abi.META_DT)
+    for i, f in enumerate(rows):
+        if f is None:  # iface 0: punted, counted nowhere, its own walk
+            meta[i]["vlan_ck"] = abi.META_WALK
+            continue
+        frames[i, :len(f)] = np.frombuffer(f[:stride], np.uint8)
+        meta[i]["iface"] = P0
+        meta[i]["vlan_ck"] = (abi.CKSUM_UNKNOWN << 12) | (abi.META_WALK if walk[i] else 0)
+        meta[i]["pkt_len"] = len(f)
+    return frames, meta, labels, np.array(zero)

@@ -36,7 +36,7 @@ def test_python_binding_covers_header():
 
 def test_library_loads_and_reports_abi():
     lib = abi.hip()
-    assert lib.gr_hip_abi_version() == abi.ABI_VERSION == 2
+    assert lib.gr_hip_abi_version() == abi.ABI_VERSION == 3
     assert isinstance(ctypes.CDLL(abi.LIB_HIP), ctypes.CDLL)
 
 

@@ -44,8 +44,8 @@ def apply(m, lines, v, topo, burst=64):
     ifaces = np.ascontiguousarray(topo.ifaces)
     nh = np.ascontiguousarray(topo.nh)
     abi.check("gr_hip_node_apply", L.gr_hip_node_apply(
-        m.ctypes.data, len(m), np.ascontiguousarray(lines).ctypes.data, abi.LINE, v.ctypes.data,
-        ifaces.ctypes.data, len(ifaces), nh.ctypes.data, len(nh), burst, ns.ctypes.data))
+        m.ctypes.data, len(m), burst, None, np.ascontiguousarray(lines).ctypes.data, abi.LINE, v.ctypes.data,
+        ifaces.ctypes.data, len(ifaces), nh.ctypes.data, len(nh), ns.ctypes.data))
     return ns[0]
 
 
@@ -93,8 +93,11 @@ def test_stage_roundtrip():
     bufs, m = mbufs_for(fr, me)
     lines = np.zeros((len(me), abi.LINE), dtype=np.uint8)
     meta = np.zeros(len(me), dtype=abi.META_DT)
-    abi.check("gr_hip_node_stage", abi.hip().gr_hip_node_stage(m.ctypes.data, len(m), lines.ctypes.data,
+    abi.check("gr_hip_node_stage", abi.hip().gr_hip_node_stage(m.ctypes.data, len(m), 64, None, lines.ctypes.data,
                                                                meta.ctypes.data))
+    walk = (meta["vlan_ck"] & abi.META_WALK) != 0
+    assert np.array_equal(np.nonzero(walk)[0], np.arange(0, len(me), 64))  # graph walks of 64
+    meta["vlan_ck"] &= 0xFFFF ^ abi.META_WALK
     assert np.array_equal(meta, me)
     assert np.array_equal(lines, fr[:, :abi.LINE])  # 64 bytes whatever data_len says
 
@@ -206,3 +209,41 @@ def test_node_process_registered_frames(fastpath, ptrs):
         abi.check("gr_hip_host_unregister", L.gr_hip_host_unregister(fastpath.h, bufs.ctypes.data))
     assert L.gr_hip_host_dev_addr(fastpath.h, bufs.ctypes.data, ctypes.byref(dev)) == -2  # -ENOENT
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ptrs", [1, 0])
+def test_node_give_up_hands_back(fastpath, ptrs):
+    """A kernel that gives up (spin_max 1) processed each 64-packet tile whole
+    or not at all: the node hands back the finished packets as usual and the
+    rest as PUNT with frames and mbufs untouched (grout's CPU nodes take
+    them), instead of punting frames it already rewrote."""
+    from golden_util import fresh_fastpath_state
+    topo = T.config_single_route()
+    n = 1 << 18
+    fr, me = S.stream(n, 0x61FE, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    fresh_fastpath_state(fastpath, topo)
+    lines, v, st, want, _ = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
+    bufs, m = mbufs_for(fr, me)
+    orig_bufs, orig_m = bufs.copy(), m.copy()
+    L = fastpath.lib
+    if ptrs:
+        abi.check("gr_hip_host_register", L.gr_hip_host_register(fastpath.h, bufs.ctypes.data, bufs.nbytes))
+    q = fastpath.queue()
+    try:
+        fastpath.tune("node_ptrs", ptrs)
+        assert fastpath.tune("spin_max", 1) == 0
+        q.node_process(m, burst=64)
+    finally:
+        fastpath.tune("spin_max", 0)
+        fastpath.tune("node_ptrs", 1)
+        if ptrs:
+            abi.check("gr_hip_host_unregister", L.gr_hip_host_unregister(fastpath.h, bufs.ctypes.data))
+    punt = m["edge"] == abi.EDGE["punt"]
+    assert q.unfinished == punt.sum() > 0  # (frames over PCIe: often every tile gives up)
+    assert np.array_equal(bufs[punt], orig_bufs[punt])
+    orig_m["edge"] = abi.EDGE["punt"]
+    assert np.array_equal(m[punt], orig_m[punt])
+    done = ~punt
+    compare_mbufs(m[done], want[done], bufs[done], lines[done])
+    q.close()
