@@ -55,7 +55,50 @@ $(LIB_ORACLE): oracle/oracle.c oracle/oracle.h include/grout_hip.h
 $(LIB_GRAPH): $(GRAPH_SRC) $(GRAPH_HDRS) $(LIB_HIP)
 	$(CC) -std=gnu11 $(CFLAGS_HOST) -Iinclude -shared -o $@ $(GRAPH_SRC) -Lgrout_amd -lgrout_hip '-Wl,-rpath,$$ORIGIN'
 
+# ---- AddressSanitizer + UBSan build of the host code (CPU only) ----------
+# Every host C/C++ source of the libraries and the oracle, built with the ROCm
+# LLVM toolchain (hipcc's clang) so that one sanitizer runtime serves them
+# all; the gfx950 kernel object is the normal one (no GPU sanitizer). The CPU
+# test suite runs on these libraries with `make asan-test`.
+LLVM = /opt/rocm/lib/llvm
+ASAN_DIR = $(BUILD)/asan
+ASAN_RT = $(firstword $(wildcard $(LLVM)/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so))
+SAN = -fsanitize=address,undefined -fno-sanitize-recover=undefined -shared-libsan -fno-omit-frame-pointer -g -O1
+SAN_C = $(LLVM)/bin/clang $(SAN) -fPIC -march=x86-64-v3 -Wall -Wno-unused-parameter
+SAN_CXX = $(LLVM)/bin/clang++ $(SAN) -fPIC -march=x86-64-v3 -std=c++17 -Wall
+SAN_HIP = $(HIPCC) -x hip --offload-arch=$(ARCH) -O1 -g -fPIC -std=c++17 -fno-omit-frame-pointer -Wno-unused-value \
+	-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -shared-libsan
+
+$(ASAN_DIR)/gr_hip.o: $(CSRC)/gr_hip.cpp $(HDRS)
+	@mkdir -p $(ASAN_DIR)
+	$(SAN_HIP) -c -o $@ $<
+
+$(ASAN_DIR)/libgrout_hip.so: $(BUILD)/fwd4_ring.o $(ASAN_DIR)/gr_hip.o $(CSRC)/gr_node.cpp $(CSRC)/fib4.c $(CSRC)/fib6.c $(HDRS)
+	$(SAN_C) -c -o $(ASAN_DIR)/fib4.o $(CSRC)/fib4.c
+	$(SAN_C) -c -o $(ASAN_DIR)/fib6.o $(CSRC)/fib6.c
+	$(SAN_CXX) -c -o $(ASAN_DIR)/gr_node.o $(CSRC)/gr_node.cpp
+	$(SAN_CXX) -shared -o $@ $(BUILD)/fwd4_ring.o $(ASAN_DIR)/gr_hip.o $(ASAN_DIR)/gr_node.o \
+		$(ASAN_DIR)/fib4.o $(ASAN_DIR)/fib6.o -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
+
+$(ASAN_DIR)/libgrout_host.so: $(CSRC)/fib4.c $(CSRC)/fib6.c $(CSRC)/synth.c $(CSRC)/fib4.h $(CSRC)/fib6.h $(CSRC)/synth.h
+	@mkdir -p $(ASAN_DIR)
+	$(SAN_C) -shared -o $@ $(CSRC)/fib4.c $(CSRC)/fib6.c $(CSRC)/synth.c
+
+$(ASAN_DIR)/liboracle.so: oracle/oracle.c oracle/oracle.h include/grout_hip.h
+	@mkdir -p $(ASAN_DIR)
+	$(SAN_C) -pthread -shared -o $@ oracle/oracle.c
+
+$(ASAN_DIR)/libgrout_graph.so: $(GRAPH_SRC) $(GRAPH_HDRS) $(ASAN_DIR)/libgrout_hip.so
+	$(SAN_C) -std=gnu11 -Iinclude -shared -o $@ $(GRAPH_SRC) -L$(ASAN_DIR) -lgrout_hip '-Wl,-rpath,$$ORIGIN'
+
+asan: $(ASAN_DIR)/libgrout_hip.so $(ASAN_DIR)/libgrout_host.so $(ASAN_DIR)/liboracle.so $(ASAN_DIR)/libgrout_graph.so
+
+# the CPU suite on the sanitized libraries (GR_LIBDIR: abi.py / oracle load from there)
+asan-test: asan
+	GR_LIBDIR=$(ASAN_DIR) LD_PRELOAD=$(ASAN_RT) ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 \
+		UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 python -m pytest tests -x -q -m "not gpu" -p no:cacheprovider
+
 clean:
 	rm -rf $(BUILD) $(LIB_HIP) $(LIB_HOST) $(LIB_ORACLE) $(LIB_GRAPH)
 
-.PHONY: all clean
+.PHONY: all clean asan asan-test

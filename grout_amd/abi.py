@@ -11,8 +11,10 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_HIP = os.path.join(HERE, "libgrout_hip.so")
-LIB_HOST = os.path.join(HERE, "libgrout_host.so")
+# GR_LIBDIR: load the libraries from another build (`make asan-test`)
+LIBDIR = os.environ.get("GR_LIBDIR") or HERE
+LIB_HIP = os.path.join(LIBDIR, "libgrout_hip.so")
+LIB_HOST = os.path.join(LIBDIR, "libgrout_host.so")
 
 # ---------------------------------------------------------------------------
 # constants (grout_hip.h)

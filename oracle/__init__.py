@@ -13,7 +13,7 @@ import numpy as np
 from grout_amd import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "liboracle.so")
+LIB = os.path.join(os.environ.get("GR_LIBDIR") or HERE, "liboracle.so")  # GR_LIBDIR: `make asan-test`
 
 _P, _U8, _U16, _U32, _U64, _I = (ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint16, ctypes.c_uint32,
                                  ctypes.c_uint64, ctypes.c_int)
