@@ -5,7 +5,7 @@
 //
 // Replaces DPDK rte_fib/rte_rib as created by grout's create_fib
 // (modules/ip/control/route.c:63-98) and updated by rte_fib_add /
-// rte_fib_delete in rib4_insert_or_replace / rib4_delete (route.c:212-330).
+// rte_fib_delete in rib4_insert_or_replace / rib4_delete (modules/ip/control/route.c:212-330).
 //
 // Table encoding (the layout the HIP kernel walks):
 //   tbl24[ip >> 8]:  0            no route

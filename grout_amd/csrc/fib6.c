@@ -2,7 +2,7 @@
 //
 // fib6.c -- the IPv6 RIB of one VRF and the multibit trie the kernel walks
 // (see fib6.h). The RIB is an exact-prefix hash (rib6_insert_or_replace /
-// rib6_delete semantics of modules/ip6/control/route.c:230-345: one nexthop
+// rib6_delete semantics of modules/ip6/control/route.c:229-345: one nexthop
 // per (prefix, length), replace on request). The trie is repainted from the
 // RIB on commit, routes in ascending prefix length so that a longer prefix
 // always overwrites a shorter one: a route ending in the first level paints

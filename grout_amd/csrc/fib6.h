@@ -11,7 +11,7 @@
 // skip node ("bytes b..b+n-1 equal key: continue with child, else the leaf
 // miss"), and consecutive skips merge (up to 7 key bytes). Entry encoding
 // (u32): bit 31 clear = the nexthop slot of the longest matching prefix (0 =
-// no route, the FIB default_nh, route.c:80); bits 31 and 30 = skip node
+// no route, the FIB default_nh, modules/ip6/control/route.c:68); bits 31 and 30 = skip node
 // index in bits 0-29; bit 31 alone = group index in bits 0-29.
 #pragma once
 

@@ -217,7 +217,7 @@ __device__ __forceinline__ int chain_head(const kctx &P, const uint8_t *R, uint3
 	return HEAD_IP4;
 }
 
-// fib4_lookup (route.c:147-167) in the iface's VRF table.
+// fib4_lookup (modules/ip/control/route.c:147-167) in the iface's VRF table.
 __device__ __forceinline__ uint32_t chain_fib(const rxv &rx, uint32_t dst) {
 	if (rx.tbl24 == nullptr)
 		return 0;
@@ -291,7 +291,7 @@ __device__ __forceinline__ void chain_tail(const kctx &P, uint8_t *R, uint32_t r
 	c1.z = (c1.z & 0xffff0000u) | (ck & 0xffff);
 	lds_put(R, row, 1, c1);
 
-	// ---- ip_output (ip_output.c:135-213)
+	// ---- ip_output (ip_output.c:79-138)
 	if (A.e_pre != CHAIN) {
 		r.edge = A.e_pre;
 		return;
@@ -310,7 +310,7 @@ __device__ __forceinline__ void chain_tail(const kctx &P, uint8_t *R, uint32_t r
 		return;
 	}
 
-	// ---- eth_output (eth_output.c:297-316) + iface_output (iface_output.c:213-246)
+	// ---- eth_output (eth_output.c:43-62) + iface_output (iface_output.c:75-108)
 	u4v c0 = lds_get(R, row, 0);
 	c0.x = A.dmac_lo;
 	c0.y = (c0.y & 0xffff0000u) | A.dmac_hi;
@@ -329,8 +329,8 @@ __device__ __forceinline__ void chain_tail(const kctx &P, uint8_t *R, uint32_t r
 
 // The plain forward of a fast adjacency f (fwd4_nhf as 4 words): the same
 // steps and results as chain_tail for such a nexthop -- ip_forward
-// (ip_forward.c:21-33), the MTU/DF check (ip_output.c:159-166), eth_output
-// (eth_output.c:297-316) and iface_output to port_output.
+// (ip_forward.c:21-33), the MTU/DF check (ip_output.c:99-106), eth_output
+// (eth_output.c:43-62) and iface_output to port_output.
 __device__ __forceinline__ void fast_tail(uint8_t *R, uint32_t row, result &r, uint32_t data_len, uint32_t slot,
 					  uint4 f) {
 	r.nh = slot;
@@ -373,7 +373,7 @@ __device__ __forceinline__ uint32_t byte_of(const uint32_t (&a)[4], int i) {
 	return (a[i >> 2] >> (8 * (i & 3))) & 0xff;
 }
 
-// rte_fib6_lookup (route.c:151-173) in the fib6.h trie of the iface's VRF:
+// rte_fib6_lookup (modules/ip6/control/route.c:150-173) in the fib6.h trie of the iface's VRF:
 // key = dst with link-local addresses scoped to the ingress iface
 // (addr6_linklocal_scope, ip6.h:23-36).
 __device__ __forceinline__ uint32_t chain_fib6(const fwd4_rx6 &v, const uint32_t (&dst)[4], uint32_t iface_id) {
@@ -401,12 +401,12 @@ __device__ __forceinline__ uint32_t chain_fib6(const fwd4_rx6 &v, const uint32_t
 	return (ent & 0x80000000u) ? 0 : ent;
 }
 
-// From ip6_input (ip6_input.c:58-146) to iface_output for an IPv6 packet in
+// From ip6_input (ip6_input.c:58-145) to iface_output for an IPv6 packet in
 // row `row` of R, eth_input done (domain in r, data_len = the mbuf's after
 // its adj). Rewrites the hop limit and the L2 header in R.
 __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, const gr_hip_pkt_meta &m,
 				       const rxv &rx, result &r, uint32_t data_len) {
-	if (data_len < 40) { // :62-69
+	if (data_len < 40) { // ip6_input.c:63-70
 		r.edge = GR_HIP_E_IP6_INPUT_BAD_LENGTH;
 		return;
 	}
@@ -420,17 +420,17 @@ __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, 
 		w[4 * k + 3] = c.w;
 	}
 	// IPv6 header at byte 14: version 14, hop limit 21, src 22-37, dst 38-53
-	if ((((w[3] >> 16) & 0xff) & 0xf0) != 0x60) { // rte_ipv6_check_version, :71-74
+	if ((((w[3] >> 16) & 0xff) & 0xf0) != 0x60) { // rte_ipv6_check_version, ip6_input.c:72-75
 		r.edge = GR_HIP_E_IP6_INPUT_BAD_VERSION;
 		return;
 	}
 	const uint32_t dst[4] = {word_at2(w, 9), word_at2(w, 10), word_at2(w, 11), word_at2(w, 12)};
 	const uint32_t src0 = (w[5] >> 16) & 0xff;
-	if (src0 == 0xff || (dst[0] | dst[1] | dst[2] | dst[3]) == 0) { // mcast src, unspec dst :76-80
+	if (src0 == 0xff || (dst[0] | dst[1] | dst[2] | dst[3]) == 0) { // mcast src, unspec dst, ip6_input.c:77-81
 		r.edge = GR_HIP_E_IP6_INPUT_BAD_ADDR;
 		return;
 	}
-	if ((dst[0] & 0xff) == 0xff) { // :82-101
+	if ((dst[0] & 0xff) == 0xff) { // ip6_input.c:83-103
 		const uint32_t scope = (dst[0] >> 8) & 0xf; // rte_ipv6_mc_scope
 		if (scope <= 1) { // RTE_IPV6_MC_SCOPE_NONE / _IFACELOCAL
 			r.edge = GR_HIP_E_IP6_INPUT_BAD_ADDR;
@@ -442,13 +442,13 @@ __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, 
 		}
 		return;
 	}
-	if (r.domain != GR_HIP_ETH_DOMAIN_LOCAL) { // :104-118 (LOOPBACK never from a port)
+	if (r.domain != GR_HIP_ETH_DOMAIN_LOCAL) { // ip6_input.c:105-120 (LOOPBACK never from a port)
 		const bool mc = r.domain == GR_HIP_ETH_DOMAIN_BROADCAST || r.domain == GR_HIP_ETH_DOMAIN_MULTICAST;
 		r.edge = mc ? GR_HIP_E_IP6_INPUT_LOCAL : GR_HIP_E_IP6_INPUT_OTHER_HOST;
 		return;
 	}
 	const fwd4_rx6 v = {gld(&P.rx6[rx.id].top), gld(&P.rx6[rx.id].groups), gld(&P.rx6[rx.id].skips)};
-	uint32_t slot = chain_fib6(v, dst, rx.id); // :122-128
+	uint32_t slot = chain_fib6(v, dst, rx.id); // ip6_input.c:124-131
 	if (slot == 0 || slot > P.max_nh) {
 		r.edge = GR_HIP_E_IP6_ERROR_DEST_UNREACH;
 		return;
@@ -475,7 +475,7 @@ __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, 
 			u4v c1 = lds_get(R, row, 1);
 			c1.y = (c1.y & 0xffff00ffu) | ((hop - 1) << 8);
 			lds_put(R, row, 1, c1);
-			if (data_len > (f.w >> 16)) { // ip6_output.c:99-102
+			if (data_len > (f.w >> 16)) { // ip6_output.c:97-100
 				r.edge = GR_HIP_E_IP6_OUTPUT_TOO_BIG;
 				return;
 			}
@@ -514,14 +514,14 @@ __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, 
 		b = gld4(ap + 1);
 		c = gld4(ap + 2);
 	}
-	r.nh = slot; // l3_mbuf_data(mbuf)->nh :151-153
+	r.nh = slot; // l3_mbuf_data(mbuf)->nh, ip6_input.c:151-153
 	const uint32_t e_in = (a.x >> 8) & 0xff, flags = (a.x >> 16) & 0xff;
-	if (e_in != CHAIN) { // nh_type_edges :130-132
+	if (e_in != CHAIN) { // nh_type_edges, ip6_input.c:133-135
 		r.edge = e_in;
 		return;
 	}
 	const bool is_nh = dst[0] == b.w && dst[1] == c.x && dst[2] == c.y && dst[3] == c.z;
-	if ((flags & FWD4_ADJ_LOCAL) && is_nh) { // :136-145
+	if ((flags & FWD4_ADJ_LOCAL) && is_nh) { // ip6_input.c:139-144
 		r.edge = GR_HIP_E_IP6_INPUT_LOCAL;
 		return;
 	}
@@ -536,27 +536,27 @@ __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, 
 	c1.y = (c1.y & 0xffff00ffu) | ((hop - 1) << 8);
 	lds_put(R, row, 1, c1);
 
-	// ---- ip6_output (ip6_output.c:70-123), adjacency resolved ahead of time
+	// ---- ip6_output (ip6_output.c:75-134), adjacency resolved ahead of time
 	const uint32_t e_pre = a.x >> 24, e_mid = a.y & 0xff, e_post = (a.y >> 8) & 0xff;
-	if (e_pre != CHAIN) { // nh type edge :85-87, no iface :94-97
+	if (e_pre != CHAIN) { // nh type edge ip6_output.c:83-85, no iface :92-95
 		r.edge = e_pre;
 		return;
 	}
-	if (data_len > (a.z & 0xffff)) { // rte_pktmbuf_pkt_len > mtu :99-102
+	if (data_len > (a.z & 0xffff)) { // rte_pktmbuf_pkt_len > mtu, ip6_output.c:97-100
 		r.edge = GR_HIP_E_IP6_OUTPUT_TOO_BIG;
 		return;
 	}
-	r.iface = a.y >> 16; // mbuf_data(mbuf)->iface = iface :107
-	if (e_mid != CHAIN) { // iface type edge :106-109, state :113-119
+	r.iface = a.y >> 16; // mbuf_data(mbuf)->iface = iface, ip6_output.c:105
+	if (e_mid != CHAIN) { // iface type edge ip6_output.c:104-107, state :111-117
 		r.edge = e_mid;
 		return;
 	}
-	if ((flags & FWD4_ADJ_LINK) && !is_nh) { // :113-119
+	if ((flags & FWD4_ADJ_LINK) && !is_nh) { // ip6_output.c:111-117
 		r.edge = GR_HIP_E_IP6_HOLD;
 		return;
 	}
 
-	// ---- eth_output (eth_output.c:297-316) + iface_output (iface_output.c:213-246)
+	// ---- eth_output (eth_output.c:43-62) + iface_output (iface_output.c:75-108)
 	u4v c0 = lds_get(R, row, 0);
 	c0.x = b.x; // dst MAC 0-3
 	c0.y = (c0.y & 0xffff0000u) | (b.y & 0xffff); // dst MAC 4-5

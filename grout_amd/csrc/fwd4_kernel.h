@@ -28,7 +28,7 @@ struct fwd4_edges {
 };
 
 // Per-iface RX view, 32 bytes: what iface_input and eth_input need from an
-// ingress iface, and the FIB of its VRF (get_fib, route.c:51-61), resolved
+// ingress iface, and the FIB of its VRF (get_fib, modules/ip/control/route.c:51-61), resolved
 // by the control plane when ifaces, VRFs or edge registrations change.
 #define FWD4_RX_MAC_OK 0x01 // iface_get_eth_addr() succeeds
 #define FWD4_RX_SNAT_DYN 0x02 // GR_IFACE_F_SNAT_DYNAMIC
@@ -49,7 +49,7 @@ struct fwd4_rx {
 };
 
 // Per-iface IPv6 view, 16 bytes: the FIB6 of the iface's VRF (get_fib6,
-// modules/ip6/control/route.c:51-64). NULL: no IPv6 FIB (no route).
+// modules/ip6/control/route.c:54-64). NULL: no IPv6 FIB (no route).
 struct fwd4_rx6 {
 	const uint32_t *top; // [65536] (fib6.h encoding)
 	const uint32_t *groups; // [n][256]
@@ -62,7 +62,7 @@ struct fwd4_rx6 {
 // MTU/DF and LINK destination checks). Recomputed on nexthop, iface and
 // edge-registration changes.
 #define FWD4_ADJ_LOCAL 0x01 // L3 nexthop flagged LOCAL (ip_input.c:166-168)
-#define FWD4_ADJ_LINK 0x02 // flagged LINK (ip_output.c:187)
+#define FWD4_ADJ_LINK 0x02 // flagged LINK (ip_output.c:126-127)
 struct fwd4_adj {
 	uint8_t type; // GR_HIP_NH_T_*
 	uint8_t e_in; // ip_input nh type edge (CHAIN = ip_forward)
@@ -85,7 +85,7 @@ struct fwd4_adj {
 };
 
 // Per-nexthop IPv6 adjacency, 64 bytes: fwd4_adj for the ip6_input /
-// ip6_output edge tables (ip6_input.c:130-145, ip6_output.c:70-123). e_pre
+// ip6_output edge tables (ip6_input.c:133-144, ip6_output.c:75-134). e_pre
 // is the nh type edge or ERROR (before the MTU check, iface = ingress),
 // e_mid the iface type edge or HOLD by state (after it, iface = oif).
 struct fwd4_adj6 {

@@ -9,7 +9,7 @@
 // every queue's submitted work, then copies, then the caller returns once the
 // copies are done. Submits issued after the call see the new state; in-flight
 // kernels never see a half-updated table. That is the role of the RCU QSBR
-// synchronisation grout performs around FIB changes (route.c:87-95,740-771).
+// synchronisation grout performs around FIB changes (modules/ip/control/route.c:86-95,740-771).
 #include <hip/hip_runtime.h>
 
 #include "fib4.h"
@@ -214,7 +214,7 @@ static const gr_hip_iface *iface_get(const gr_hip_ctx *c, uint32_t id) {
 }
 
 // RX view of iface `id`: iface_input's admin/mode edge (iface_input.c:88-97),
-// eth_input's MAC (eth_input.c:62-68) and the VRF FIB (route.c:51-61).
+// eth_input's MAC (eth_input.c:62-68) and the VRF FIB (modules/ip/control/route.c:51-61).
 static fwd4_rx make_rx(const gr_hip_ctx *c, uint32_t id) {
 	fwd4_rx r;
 	memset(&r, 0, sizeof(r));
@@ -249,7 +249,7 @@ static fwd4_rx make_rx(const gr_hip_ctx *c, uint32_t id) {
 	return r;
 }
 
-// IPv6 view of iface `id`: the FIB6 of its VRF (get_fib6, route.c:51-64).
+// IPv6 view of iface `id`: the FIB6 of its VRF (get_fib6, modules/ip6/control/route.c:54-64).
 static fwd4_rx6 make_rx6(const gr_hip_ctx *c, uint32_t id) {
 	fwd4_rx6 r = {nullptr, nullptr, nullptr};
 	const gr_hip_iface *i = iface_get(c, id);
@@ -267,7 +267,7 @@ static fwd4_rx6 make_rx6(const gr_hip_ctx *c, uint32_t id) {
 }
 
 // eth_output -> iface_output for a nexthop leaving through `oif`
-// (eth_output.c:297-316, iface_output.c:213-246), shared by both AFs.
+// (eth_output.c:43-62, iface_output.c:75-108), shared by both AFs.
 template <typename A>
 static void fill_post(const gr_hip_ctx *c, const gr_hip_nh &nh, const gr_hip_iface *oif, A &a) {
 	const fwd4_edges &E = c->edges;
@@ -296,9 +296,9 @@ static void fill_post(const gr_hip_ctx *c, const gr_hip_nh &nh, const gr_hip_ifa
 	a.e_post = out->type < 8 ? E.iout_type[out->type] : GR_HIP_E_IFACE_OUTPUT_INVAL_TYPE;
 }
 
-// IPv6 adjacency of nexthop `slot`: ip6_input's view (ip6_input.c:130-145)
+// IPv6 adjacency of nexthop `slot`: ip6_input's view (ip6_input.c:133-144)
 // and ip6_output -> eth_output -> iface_output resolved for the nexthop
-// (ip6_output.c:70-123), leaving the MTU and LINK destination checks.
+// (ip6_output.c:75-134), leaving the MTU and LINK destination checks.
 static fwd4_adj6 make_adj6(const gr_hip_ctx *c, uint32_t slot) {
 	const fwd4_edges &E = c->edges;
 	const gr_hip_nh &nh = c->nh[slot];
@@ -334,7 +334,7 @@ static fwd4_adj6 make_adj6(const gr_hip_ctx *c, uint32_t slot) {
 
 // Adjacency of nexthop `slot`: the ip_input view (ip_input.c:156-187) and
 // ip_output -> eth_output -> iface_output resolved for that nexthop
-// (ip_output.c:147-213, eth_output.c:297-316, iface_output.c:213-246),
+// (ip_output.c:87-152, eth_output.c:43-62, iface_output.c:75-108),
 // leaving the packet-dependent MTU/DF and LINK destination checks.
 static fwd4_adj make_adj(const gr_hip_ctx *c, uint32_t slot) {
 	const fwd4_edges &E = c->edges;
@@ -854,7 +854,7 @@ extern "C" int gr_hip_fib4_create(gr_hip_ctx_t *c, uint16_t vrf, uint32_t max_ro
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib != nullptr)
 		return -EEXIST;
-	if (num_tbl8 == 0) // fib4_auto_tbl8, route.c:38-41
+	if (num_tbl8 == 0) // fib4_auto_tbl8, modules/ip/control/route.c:38-41
 		num_tbl8 = max_routes / 500 < 256 ? 256 : max_routes / 500;
 	v.rib = gr_fib4_new(max_routes, num_tbl8);
 	if (v.rib == nullptr)

@@ -21,14 +21,14 @@
 // middle (ip6_input.c, ip6_forward.c, ip6_output.c).
 //
 // (1) snap_input and eth_input_invalid_iface leave eth_input before its
-//     rte_pktmbuf_adj(14) (eth_input.c:49-59 vs :80); adj is a no-op on a
+//     rte_pktmbuf_adj(14) (eth_input.c:55-66 vs :80); adj is a no-op on a
 //     frame shorter than 14 bytes (DPDK rte_pktmbuf_adj).
-// (2) eth_output's gr_mbuf_prepend(14) (eth_output.c:305, mbuf.h:89-106)
+// (2) eth_output's gr_mbuf_prepend(14) (eth_output.c:43, mbuf.h:89-106)
 //     undoes the adj: net data_off unchanged vs RX.
 // vlan_id: iface_input clears it when it demuxes a tagged packet to a VLAN
 // sub-interface (iface_input.c:74-86), eth_output clears it
-// (eth_output.c:325), iface_output sets the egress VLAN's id
-// (iface_output.c:219-224).
+// (eth_output.c:71), iface_output sets the egress VLAN's id
+// (iface_output.c:81-86).
 #include "../../include/grout_hip.h"
 
 #include <errno.h>

@@ -15,7 +15,7 @@ extern "C" {
 
 uint64_t gr_synth_splitmix64(uint64_t *state);
 
-// fib_inject -4 -n count (smoke/fib_inject.c:24-35,53-79,107-134): prefix
+// fib_inject -4 -n count (smoke/fib_inject.c:23-34,53-79,107-134): prefix
 // length picked round-robin from the BGP distribution by route index % 1000,
 // ip = (per-length seq + 1) << (32 - len), nexthop = (i % n_nh) + 1, here
 // mapped to slot nh_base + (i % n_nh).

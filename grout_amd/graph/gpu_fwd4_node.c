@@ -110,7 +110,7 @@ static uint8_t ck_status(uint64_t ol_flags) {
 		return GR_HIP_CKSUM_GOOD;
 	case RTE_MBUF_F_RX_IP_CKSUM_BAD:
 		return GR_HIP_CKSUM_BAD;
-	default: // UNKNOWN or NONE: ip_input verifies in software (ip_input.c:78-88)
+	default: // UNKNOWN or NONE: ip_input verifies in software (ip_input.c:80-92)
 		return GR_HIP_CKSUM_UNKNOWN;
 	}
 }
@@ -118,8 +118,8 @@ static uint8_t ck_status(uint64_t ol_flags) {
 // The private data grout's chain leaves for the node behind `edge`: the iface
 // everywhere; iface_input's vlan_id before eth_input; eth_input's domain and
 // pre-resolved nexthop (NULL), then ip_input's / ip6_input's l3 nexthop over
-// them (l3.h:9 shares the bytes, ip_input.c:158); iface_output's vlan_id for
-// port_output / port_tx (iface_output.c:213-246, port_tx.c:84-118).
+// them (l3.h:9 shares the bytes, ip_input.c:156); iface_output's vlan_id for
+// port_output / port_tx (iface_output.c:81-86, port_tx.c:84-118).
 static void hand_back(struct rte_mbuf *m, const struct gr_hip_mbuf *v) {
 	m->data_off = v->data_off; // frame bytes were rewritten in place
 	m->data_len = v->data_len;

@@ -5,7 +5,7 @@
 //
 //   mbuf private data       modules/infra/datapath/mbuf.h:27-41 (layout:
 //                           trace head, iface, then the node's fields),
-//                           rxtx.h:45-48, eth.h:14-30, l3.h:9
+//                           rxtx.h:45-48, eth.h:14-36, l3.h:9
 //   node registration       modules/infra/control/graph.h:31-85
 //                           (GR_NODE_CTX_TYPE, gr_node_info, GR_NODE_REGISTER,
 //                           GR_DROP_REGISTER), gr_node_attach_parent

@@ -11,10 +11,10 @@ routes exactly as grout's control plane would leave them for the datapath:
   on the address prefix (host bits masked by the FIB).
 * add_nexthop: a gr_nexthop_info_l3 (gr_nexthop.h:93-105); a MAC makes it
   REACHABLE (l3_nexthop.c:244-250), no address makes it a LINK nexthop
-  (l3_nexthop.c:232-236).
+  (l3_nexthop.c:233-238).
 * add_group: GR_NH_T_GROUP with a power-of-two reta (nexthop.h:80-96).
 * add_route: gr_ip4_route_add_req (modules/ip/api/gr_ip4.h:47-56).
-* IPv6: every VRF also gets a FIB6 (route.c:100-122 of modules/ip6); an
+* IPv6: every VRF also gets a FIB6 (modules/ip6/control/route.c:103-125); an
   IPv6 nexthop address makes an AF_IP6 nexthop; add_address6 mirrors
   addr6_add (modules/ip6/control/address.c) and add_route6
   gr_ip6_route_add_req, a link-local prefix scoped to its iface.
@@ -79,7 +79,7 @@ class Topology:
         return iface_id
 
     def add_vrf(self, vrf_id=1, mac=None, max_routes=1 << 16, num_tbl8=0, max_routes6=1 << 16, num_groups6=0):
-        """A VRF iface and its IPv4 and IPv6 FIBs (vrf.c, route.c:100-122)."""
+        """A VRF iface and its IPv4 and IPv6 FIBs (fib4_init, modules/ip/control/route.c:100-122)."""
         self._iface(vrf_id, "VRF", "VRF", abi.IFACE_F_UP, 1500, vrf_id, mac)
         self.fibs[vrf_id] = (max_routes, num_tbl8)
         self.fibs6[vrf_id] = (max_routes6, num_groups6)
@@ -90,7 +90,7 @@ class Topology:
         return self._iface(iface_id, "PORT", mode, f, mtu, vrf_id, mac, port_id=port_id)
 
     def add_vlan(self, iface_id, parent_id, vlan_id, mac=None, vrf_id=1, mtu=1500, up=True, flags=0):
-        if mac is None:  # iface_vlan_get_eth_addr falls back to the parent (vlan.c:174-190)
+        if mac is None:  # a VLAN set without a MAC takes its parent's (iface_vlan_set_eth_addr, modules/infra/control/vlan.c:180-192)
             p = self.ifaces[parent_id]
             mac = bytes(p["mac"]) if p["mac_ok"] else None
         f = (abi.IFACE_F_UP if up else 0) | flags

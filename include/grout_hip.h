@@ -13,17 +13,18 @@
 //     (modules/infra/datapath/iface_input.c:52-112, eth_input.c:35-88,
 //      modules/ip/datapath/ip_input.c:47-197, modules/ip/control/route.c:147-167,
 //      modules/ip/datapath/ip_forward.c:14-41, ip_output.c:63-163,
-//      modules/infra/datapath/eth_output.c:28-77, iface_output.c:60-117)
+//      modules/infra/datapath/eth_output.c:27-77, iface_output.c:60-117)
 //     is gr_hip_fwd4_submit(): one fused HIP kernel, one lane per packet.
-//   * the DIR24_8 FIB that route.c:63-98 creates through DPDK rte_fib, and the
-//     rte_fib_add() calls of rib4_insert_or_replace (route.c:212-275), are the
+//   * the DIR24_8 FIB that modules/ip/control/route.c:63-98 creates through
+//     DPDK rte_fib, and the rte_fib_add() calls of rib4_insert_or_replace
+//     (modules/ip/control/route.c:212-275), are the
 //     gr_hip_route4_* / gr_hip_fib4_commit entry points (device-resident tables).
 //   * the nexthop / iface objects the nodes dereference (nexthop.h:22-54,
 //     iface.h:20-35) are mirrored with gr_hip_nh_set / gr_hip_iface_set
-//     (hook: GR_EVENT_NEXTHOP_UPDATE, modules/infra/control/nexthop.c:385).
+//     (hook: GR_EVENT_NEXTHOP_UPDATE, modules/infra/control/nexthop.c:386).
 //   * the dynamic edge registrations (gr_eth_input_add_type eth_input.c:26,
 //     ip_input_register_nexthop_type ip_input.c:36, ip_output_register_*
-//     ip_output.c:94,106, iface_input_mode_register iface_input.c:22,
+//     ip_output.c:34,46, iface_input_mode_register iface_input.c:22,
 //     iface_output_type_register iface_output.c:25) are gr_hip_edges_*.
 //
 // Every per-packet output ("verdict") names the grout node the packet must be
@@ -97,7 +98,7 @@ enum {
 	GR_HIP_NH_T_COUNT,
 };
 
-// eth_domain_t, modules/infra/datapath/eth.h:13-20
+// eth_domain_t, modules/infra/datapath/eth.h:14-21
 enum {
 	GR_HIP_ETH_DOMAIN_UNKNOWN = 0,
 	GR_HIP_ETH_DOMAIN_LOOPBACK,
@@ -117,8 +118,8 @@ enum {
 #define GR_HIP_CKSUM_BAD 1
 #define GR_HIP_CKSUM_GOOD 2
 
-#define GR_HIP_IFACE_ID_UNDEF 0 // gr_infra.h:45
-#define GR_HIP_MAX_IFACES 1024 // default GROUT_MAX_IFACES, main/config.c:276
+#define GR_HIP_IFACE_ID_UNDEF 0 // gr_infra.h:48
+#define GR_HIP_MAX_IFACES 1024 // default GROUT_MAX_IFACES, main/config.c:277
 #define GR_HIP_MAX_NEXTHOPS ((1u << 24) - 1) // nh slot must fit 24 bits
 #define GR_HIP_MAX_NH_GROUP_RETA 4096 // MAX_NH_GROUP_RETA_SIZE, nexthop.h:80
 
@@ -156,7 +157,7 @@ enum gr_hip_edge {
 	GR_HIP_E_DNAT44_STATIC, // "dnat44_static"
 	// ip_forward (ip_forward.c:7-11)
 	GR_HIP_E_IP_ERROR_TTL_EXCEEDED, // "ip_error_ttl_exceeded"
-	// ip_output (ip_output.c:81-90, type edges :92-114)
+	// ip_output (ip_output.c:21-30, type edges :32-54)
 	GR_HIP_E_IP_HOLD, // "ip_hold"
 	GR_HIP_E_IP_OUTPUT_ERROR, // "ip_output_error" (drop)
 	GR_HIP_E_IP_FRAGMENT, // "ip_fragment"
@@ -176,7 +177,7 @@ enum gr_hip_edge {
 	GR_HIP_E_BOND_OUTPUT, // "bond_output"
 	GR_HIP_E_VXLAN_OUTPUT, // "vxlan_output"
 	GR_HIP_E_PORT_OUTPUT, // "port_output": the forwarded case
-	// ip6_input (ip6_input.c:19-29, nh type edges :33-41,163-164)
+	// ip6_input (ip6_input.c:19-29, nh type edges :32-42,163-164)
 	GR_HIP_E_IP6_INPUT_LOCAL, // "ip6_input_local"
 	GR_HIP_E_IP6_ERROR_DEST_UNREACH, // "ip6_error_dest_unreach"
 	GR_HIP_E_IP6_INPUT_NOT_MEMBER, // "ip6_input_not_member" (drop)
@@ -227,7 +228,7 @@ struct gr_hip_iface {
 // Device mirror of struct nexthop (nexthop.h:22-31) with the L3 info
 // (nexthop.h:41-54, gr_nexthop.h:93-105) or the group info (nexthop.h:80-96).
 // 32 bytes. A nexthop is identified by its slot index (1..); slot 0 is "no
-// nexthop" (NULL), like the FIB value 0 in route.c:65,156.
+// nexthop" (NULL), like the FIB value 0 in modules/ip/control/route.c:65,156.
 struct gr_hip_nh {
 	uint8_t type; // GR_HIP_NH_T_*
 	uint8_t state; // GR_HIP_NH_S_* (L3)
@@ -242,7 +243,7 @@ struct gr_hip_nh {
 	uint32_t single; // GROUP: nhg->nh shortcut used when n_members == 1
 	uint16_t n_members; // GROUP
 	uint16_t _pad0;
-	uint8_t ipv6[16]; // L3, af GR_HIP_AF_IP6 (nexthop.h:49, gr_nexthop.h:100)
+	uint8_t ipv6[16]; // L3, af GR_HIP_AF_IP6 (gr_nexthop.h:98-102)
 };
 
 // One IPv4 route, as gr_ip4_route_add_req (modules/ip/api/gr_ip4.h:47-56).
@@ -272,7 +273,7 @@ struct gr_hip_route6 {
 // ---------------------------------------------------------------------------
 
 // Input metadata, 8 bytes per packet: what port_rx leaves in the mbuf and its
-// private data (port_rx.c:281-316, rxtx.h:154-157) and what ip_input reads
+// private data (port_rx.c:281-316, rxtx.h:45-48) and what ip_input reads
 // from rte_mbuf (ip_input.c:70-92,147).
 struct gr_hip_pkt_meta {
 	uint16_t iface; // iface_mbuf_data.iface (RX port iface id)
@@ -358,9 +359,9 @@ int gr_hip_edges_ip_input_nh_type(gr_hip_ctx_t *, uint8_t nh_type, uint8_t edge)
 int gr_hip_edges_ip_output_nh_type(gr_hip_ctx_t *, uint8_t nh_type, uint8_t edge);
 int gr_hip_edges_ip_output_iface_type(gr_hip_ctx_t *, uint8_t iface_type, uint8_t edge);
 int gr_hip_edges_iface_output_type(gr_hip_ctx_t *, uint8_t iface_type, uint8_t edge);
-int gr_hip_edges_ip6_input_nh_type(gr_hip_ctx_t *, uint8_t nh_type, uint8_t edge); // ip6_input.c:33
-int gr_hip_edges_ip6_output_nh_type(gr_hip_ctx_t *, uint8_t nh_type, uint8_t edge); // ip6_output.c:40
-int gr_hip_edges_ip6_output_iface_type(gr_hip_ctx_t *, uint8_t iface_type, uint8_t edge); // ip6_output.c:29
+int gr_hip_edges_ip6_input_nh_type(gr_hip_ctx_t *, uint8_t nh_type, uint8_t edge); // ip6_input.c:34
+int gr_hip_edges_ip6_output_nh_type(gr_hip_ctx_t *, uint8_t nh_type, uint8_t edge); // ip6_output.c:42
+int gr_hip_edges_ip6_output_iface_type(gr_hip_ctx_t *, uint8_t iface_type, uint8_t edge); // ip6_output.c:30
 
 // Object mirrors. Changes become visible to submits issued after the call.
 int gr_hip_iface_set(gr_hip_ctx_t *, const struct gr_hip_iface *ifaces, uint32_t n);
@@ -370,13 +371,13 @@ int gr_hip_reta_set(gr_hip_ctx_t *, uint32_t first, const uint32_t *slots, uint3
 
 // RIB + device FIB (DIR24_8-equivalent, 4-byte entries). Routes are staged in
 // the host RIB; gr_hip_fib4_commit() makes them visible to later submits
-// (stream-ordered swap, the rte_rcu_qsbr_synchronize analogue of route.c:764).
+// (stream-ordered swap, the rte_rcu_qsbr_synchronize analogue of modules/ip/control/route.c:764).
 int gr_hip_fib4_create(gr_hip_ctx_t *, uint16_t vrf_id, uint32_t max_routes, uint32_t num_tbl8);
 int gr_hip_fib4_destroy(gr_hip_ctx_t *, uint16_t vrf_id);
 int gr_hip_route4_add(gr_hip_ctx_t *, const struct gr_hip_route4 *routes, uint32_t n, int replace);
 int gr_hip_route4_del(gr_hip_ctx_t *, uint16_t vrf_id, uint32_t ip, uint8_t prefixlen);
 int gr_hip_fib4_commit(gr_hip_ctx_t *, uint16_t vrf_id);
-// Host-side lookup in the committed tables (control-plane helper, route.c:183).
+// Host-side lookup in the committed tables (control-plane helper, modules/ip/control/route.c:169-185).
 int gr_hip_fib4_lookup_host(gr_hip_ctx_t *, uint16_t vrf_id, uint32_t ip_be, uint32_t *nh);
 // Device table geometry: tbl8 groups in use, bytes of device memory.
 int gr_hip_fib4_info(gr_hip_ctx_t *, uint16_t vrf_id, uint32_t *n_routes, uint32_t *tbl8_used, uint64_t *dev_bytes);
@@ -385,7 +386,7 @@ int gr_hip_fib4_info(gr_hip_ctx_t *, uint16_t vrf_id, uint32_t *n_routes, uint32
 // modules/ip6/control/route.c:66-98,230-345). A multibit trie: a 2^16-entry
 // first level indexed by the first two address bytes, then 256-entry groups
 // per further byte (num_tbl8 of them; 0 = 1 << 16). fib6_lookup
-// (route.c:151-173) walks it; link-local destinations are scoped to the
+// (modules/ip6/control/route.c:151-173) walks it; link-local destinations are scoped to the
 // ingress iface first.
 int gr_hip_fib6_create(gr_hip_ctx_t *, uint16_t vrf_id, uint32_t max_routes, uint32_t num_tbl8);
 int gr_hip_fib6_destroy(gr_hip_ctx_t *, uint16_t vrf_id);
@@ -505,7 +506,7 @@ int gr_hip_host_dev_addr(gr_hip_ctx_t *, const void *ptr, uint64_t *dev);
 // fast path. After gr_hip_node_apply() the mbuf is exactly as grout's CPU
 // chain would have left it at `edge`: frame bytes (the L2 rewrite, TTL and
 // checksum), data_off / data_len / pkt_len (eth_input's adj(14), undone by
-// eth_output's prepend), packet_type (ip_output.c:145) and the private data
+// eth_output's prepend), packet_type (ip_output.c:85) and the private data
 // the next node reads (iface, vlan_id, eth_input domain, l3 nexthop).
 struct gr_hip_mbuf {
 	void *frame; // in: rte_pktmbuf_mtod(m) as port_rx delivered it (64 bytes readable)
@@ -544,11 +545,11 @@ enum gr_hip_node {
 	GR_HIP_NODE_COUNT,
 };
 
-// rte_graph node counters as grout collects them (main_loop.c:39-64):
+// rte_graph node counters as grout collects them (main_loop.c:40-66):
 // packets = sum of process() return values, calls = process() invocations,
 // one per node per graph walk that reaches it. Every node returns nb_objs
 // except ip_output and ip6_output, which return only what they sent to
-// eth_output (ip_output.c:153,162, ip6_output.c:146).
+// eth_output (ip_output.c:153,162, ip6_output.c:144).
 struct gr_hip_node_stats {
 	uint64_t packets[GR_HIP_NODE_COUNT];
 	uint64_t calls[GR_HIP_NODE_COUNT];

@@ -38,7 +38,7 @@ struct or_fib {
 	bool exists;
 	uint32_t num_tbl8;
 	struct or_ht len[33]; // RIB: one exact-match table per prefix length
-	// DIR24_8 restatement [DPDK lib/fib/dir24_8.c, nh_sz = 8B, route.c:69-74]
+	// DIR24_8 restatement [DPDK lib/fib/dir24_8.c], nh_sz = 8B (modules/ip/control/route.c:72-74)
 	uint64_t *tbl24; // 1<<24 entries: (nh << 1) | ext
 	uint64_t *tbl8; // num_tbl8 * 256
 	uint32_t tbl8_used;
@@ -69,12 +69,12 @@ struct or_topo {
 	uint8_t eth_edges[65536]; // l2l3_edges indexed by BE ether type, eth_input.c:24
 	uint8_t mode_edges[GR_HIP_IFACE_MODE_COUNT]; // iface_input.c:20
 	uint8_t in_nh_edges[256]; // ip_input.c:34
-	uint8_t out_nh_edges[256]; // ip_output.c:104
-	uint8_t out_iface_edges[256]; // ip_output.c:92
-	uint8_t iout_type_edges[256]; // iface_output.c:161
-	uint8_t in6_nh_edges[256]; // ip6_input.c:31
-	uint8_t out6_nh_edges[256]; // ip6_output.c:38
-	uint8_t out6_iface_edges[256]; // ip6_output.c:27
+	uint8_t out_nh_edges[256]; // ip_output.c:44
+	uint8_t out_iface_edges[256]; // ip_output.c:32
+	uint8_t iout_type_edges[256]; // iface_output.c:23
+	uint8_t in6_nh_edges[256]; // ip6_input.c:32
+	uint8_t out6_nh_edges[256]; // ip6_output.c:40
+	uint8_t out6_iface_edges[256]; // ip6_output.c:28
 };
 
 static uint16_t be16(uint16_t host) {
@@ -632,9 +632,10 @@ uint32_t or_lpm_dir24(const or_topo_t *t, uint16_t vrf, uint32_t ip) {
 	return dir24_lookup(&t->fibs[vrf], ip);
 }
 
-// fib4_lookup, modules/ip/control/route.c:147-167: get_fib() needs the VRF
-// iface (vrf.c:51-57) and its FIB; value 0 is no route; a GROUP nexthop is
-// resolved through nexthop_group_get_nh (nexthop.h:89-96).
+// fib4_lookup, modules/ip/control/route.c:147-167: get_fib() (:51-61) needs
+// the VRF iface (get_vrf_iface, modules/infra/control/vrf.c:51-57) and its
+// FIB; value 0 is no route (.default_nh = 0, :65); a GROUP nexthop is
+// resolved through nexthop_group_get_nh (modules/infra/control/nexthop.h:89-96).
 static uint32_t fib4_lookup(const or_topo_t *t, uint16_t vrf_id, uint32_t dst_be, uint16_t rss) {
 	const struct gr_hip_iface *vrf = iface_from_id(t, vrf_id);
 	if (vrf == NULL || vrf->type != GR_HIP_IFACE_TYPE_VRF)
@@ -693,8 +694,9 @@ struct or_mbuf {
 	uint8_t ck; // GR_HIP_CKSUM_*
 	uint16_t rss;
 	uint32_t packet_type;
-	// private area, mbuf.h:29-38 and the per-node views (rxtx.h:154-157,
-	// eth.h:151-164, l3.h:9)
+	// private area: modules/infra/datapath/mbuf.h:29-38 (traces, iface) and
+	// the per-node views iface_mbuf_data (rxtx.h:45-48), eth_input_mbuf_data
+	// and eth_output_mbuf_data (eth.h:23-36), l3_mbuf_data (l3.h:9)
 	uint16_t iface;
 	uint16_t vlan_id;
 	uint8_t domain;
@@ -911,7 +913,7 @@ static void node_ip_input(struct or_graph *g, struct or_mbuf **objs, uint16_t n)
 			edge = GR_HIP_E_IP_INPUT_OTHER_HOST;
 			goto next;
 		}
-		// IPV4_ADDR_BCAST / ip4_addr_is_mcast, api/gr_net_types.h:97-106
+		// IPV4_ADDR_BCAST / ip4_addr_is_mcast (api/gr_net_types.h:97-106)
 		if (dst == 0xffffffffu || (ip[16] >= 224 && ip[16] <= 239)) { // :139-142
 			edge = GR_HIP_E_IP_INPUT_LOCAL;
 			goto next;
@@ -963,47 +965,47 @@ static void node_ip_forward(struct or_graph *g, struct or_mbuf **objs, uint16_t 
 	}
 }
 
-// ip_output_process, modules/ip/datapath/ip_output.c:122-223
+// ip_output_process, modules/ip/datapath/ip_output.c:62-163
 static void node_ip_output(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
 	const or_topo_t *t = g->t;
 	for (uint16_t i = 0; i < n; i++) {
 		struct or_mbuf *m = objs[i];
 		const uint8_t *ip = MTOD(m);
 		uint8_t edge;
-		if (m->l3_nh == 0) { // :139-143
+		if (m->l3_nh == 0) { // :79-83
 			edge = GR_HIP_E_IP_ERROR_DEST_UNREACH;
 			goto next;
 		}
-		m->packet_type = 0x10; // RTE_PTYPE_L3_IPV4 (DPDK rte_mbuf_ptype.h), :145
+		m->packet_type = 0x10; // :85, RTE_PTYPE_L3_IPV4 [DPDK rte_mbuf_ptype.h]
 		const struct gr_hip_nh *h = &t->nh[m->l3_nh];
-		edge = t->out_nh_edges[h->type]; // :147-149
+		edge = t->out_nh_edges[h->type]; // :87-89
 		if (edge != NEXT)
 			goto next;
 		const struct gr_hip_iface *iface = iface_from_id(t, h->iface_id);
-		if (iface == NULL) { // :151-155
+		if (iface == NULL) { // :91-95
 			edge = GR_HIP_E_IP_OUTPUT_ERROR;
 			goto next;
 		}
-		m->iface = iface->id; // :157
-		if (m->pkt_len > iface->mtu) { // :159-166, DF = BE 0x4000
+		m->iface = iface->id; // :97
+		if (m->pkt_len > iface->mtu) { // :99-106, DF = BE 0x4000
 			edge = (ip[6] & 0x40) ? GR_HIP_E_IP_ERROR_FRAG_NEEDED : GR_HIP_E_IP_FRAGMENT;
 			goto next;
 		}
-		edge = t->out_iface_edges[iface->type]; // :170
+		edge = t->out_iface_edges[iface->type]; // :110
 		if (iface->flags & (GR_HIP_IFACE_F_SNAT_STATIC | GR_HIP_IFACE_F_SNAT_DYNAMIC)) {
-			edge = GR_HIP_E_IP_OUTPUT_SNAT; // snat44_process :172-179 needs conntrack
+			edge = GR_HIP_E_IP_OUTPUT_SNAT; // snat44_process :112-119 needs the NAT tables
 			goto next;
 		}
-		if (edge != NEXT)
+		if (edge != NEXT) // :121-122
 			goto next;
 		uint32_t dst;
 		memcpy(&dst, ip + 16, 4);
 		if (h->state != GR_HIP_NH_S_REACHABLE
-		    || ((h->flags & GR_HIP_NH_F_LINK) && dst != h->ipv4)) { // :186-198
+		    || ((h->flags & GR_HIP_NH_F_LINK) && dst != h->ipv4)) { // :124-138
 			edge = GR_HIP_E_IP_HOLD;
 			goto next;
 		}
-		memcpy(m->eth_dst, h->mac, 6); // :201-203
+		memcpy(m->eth_dst, h->mac, 6); // :140-152 (vtep: not on the forward path)
 		m->eth_type = be16(0x0800);
 		enqueue(g, GR_HIP_NODE_ETH_OUTPUT, m);
 		continue;
@@ -1022,20 +1024,20 @@ static void node_ip6_input(struct or_graph *g, struct or_mbuf **objs, uint16_t n
 		const struct gr_hip_iface *iface = iface_from_id(t, m->iface);
 		uint32_t nh = 0;
 		uint8_t edge;
-		if (m->data_len < 40) { // :62-69
+		if (m->data_len < 40) { // :63-70
 			edge = GR_HIP_E_IP6_INPUT_BAD_LENGTH;
 			goto next;
 		}
-		if ((ip[0] & 0xf0) != 0x60) { // rte_ipv6_check_version [DPDK] :71-74
+		if ((ip[0] & 0xf0) != 0x60) { // :72-75, rte_ipv6_check_version [DPDK]
 			edge = GR_HIP_E_IP6_INPUT_BAD_VERSION;
 			goto next;
 		}
 		static const uint8_t zero[16];
-		if (src[0] == 0xff || memcmp(dst, zero, 16) == 0) { // mcast src, unspec dst :76-80
+		if (src[0] == 0xff || memcmp(dst, zero, 16) == 0) { // mcast src, unspec dst :77-81
 			edge = GR_HIP_E_IP6_INPUT_BAD_ADDR;
 			goto next;
 		}
-		if (dst[0] == 0xff) { // :82-101
+		if (dst[0] == 0xff) { // :83-103
 			uint8_t scope = dst[1] & 0x0f; // rte_ipv6_mc_scope [DPDK]
 			if (scope == 0 || scope == 1) { // SCOPE_NONE, SCOPE_IFACELOCAL
 				edge = GR_HIP_E_IP6_INPUT_BAD_ADDR;
@@ -1046,7 +1048,7 @@ static void node_ip6_input(struct or_graph *g, struct or_mbuf **objs, uint16_t n
 			terminal(m, GR_HIP_E_PUNT);
 			continue;
 		}
-		switch (m->domain) { // :103-118
+		switch (m->domain) { // :105-120
 		case GR_HIP_ETH_DOMAIN_LOOPBACK:
 		case GR_HIP_ETH_DOMAIN_LOCAL:
 			break;
@@ -1058,21 +1060,21 @@ static void node_ip6_input(struct or_graph *g, struct or_mbuf **objs, uint16_t n
 			edge = GR_HIP_E_IP6_INPUT_OTHER_HOST;
 			goto next;
 		}
-		nh = m->e_nh ? m->e_nh : fib6_lookup(t, iface->vrf_id, iface->id, dst, m->rss); // :122-128
+		nh = m->e_nh ? m->e_nh : fib6_lookup(t, iface->vrf_id, iface->id, dst, m->rss); // :124-131
 		if (nh == 0) {
 			edge = GR_HIP_E_IP6_ERROR_DEST_UNREACH;
 			goto next;
 		}
 		const struct gr_hip_nh *h = &t->nh[nh];
-		edge = t->in6_nh_edges[h->type]; // :130-132
+		edge = t->in6_nh_edges[h->type]; // :133-135
 		if (edge != NEXT)
 			goto next;
 		if (h->type == GR_HIP_NH_T_L3 && (h->flags & GR_HIP_NH_F_LOCAL)
-		    && memcmp(dst, h->ipv6, 16) == 0) { // :136-145
+		    && memcmp(dst, h->ipv6, 16) == 0) { // :137-145
 			edge = GR_HIP_E_IP6_INPUT_LOCAL;
 			goto next;
 		}
-		m->l3_nh = nh; // :151-153
+		m->l3_nh = nh; // :151-153 (every edge: l3_mbuf_data nh)
 		enqueue(g, GR_HIP_NODE_IP6_FORWARD, m);
 		continue;
 next:
@@ -1081,7 +1083,7 @@ next:
 	}
 }
 
-// ip6_forward_process, modules/ip6/datapath/ip6_forward.c:14-35
+// ip6_forward_process, modules/ip6/datapath/ip6_forward.c:13-34
 static void node_ip6_forward(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
 	for (uint16_t i = 0; i < n; i++) {
 		struct or_mbuf *m = objs[i];
@@ -1095,42 +1097,42 @@ static void node_ip6_forward(struct or_graph *g, struct or_mbuf **objs, uint16_t
 	}
 }
 
-// ip6_output_process, modules/ip6/datapath/ip6_output.c:59-150
+// ip6_output_process, modules/ip6/datapath/ip6_output.c:58-145
 static void node_ip6_output(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
 	const or_topo_t *t = g->t;
 	for (uint16_t i = 0; i < n; i++) {
 		struct or_mbuf *m = objs[i];
 		const uint8_t *ip = MTOD(m);
 		uint8_t edge;
-		if (m->l3_nh == 0) { // :77-81
+		if (m->l3_nh == 0) { // :75-79
 			edge = GR_HIP_E_IP6_ERROR_DEST_UNREACH;
 			goto next;
 		}
-		m->packet_type = 0x40; // RTE_PTYPE_L3_IPV6 (DPDK rte_mbuf_ptype.h), :83
+		m->packet_type = 0x40; // :81, RTE_PTYPE_L3_IPV6 [DPDK rte_mbuf_ptype.h]
 		const struct gr_hip_nh *h = &t->nh[m->l3_nh];
-		edge = t->out6_nh_edges[h->type]; // :85-87
+		edge = t->out6_nh_edges[h->type]; // :83-85
 		if (edge != NEXT)
 			goto next;
-		// a multicast destination never comes out of ip6_input here (:82-101)
+		// no multicast destination comes out of ip6_input here (:87-91)
 		const struct gr_hip_iface *iface = iface_from_id(t, h->iface_id);
-		if (iface == NULL) { // :94-97
+		if (iface == NULL) { // :92-95
 			edge = GR_HIP_E_IP6_OUTPUT_ERROR;
 			goto next;
 		}
-		if (m->pkt_len > iface->mtu) { // :99-102
+		if (m->pkt_len > iface->mtu) { // :97-100
 			edge = GR_HIP_E_IP6_OUTPUT_TOO_BIG;
 			goto next;
 		}
-		edge = t->out6_iface_edges[iface->type]; // :106
-		m->iface = iface->id; // :107
+		edge = t->out6_iface_edges[iface->type]; // :104
+		m->iface = iface->id; // :105
 		if (edge != NEXT)
 			goto next;
 		if (h->state != GR_HIP_NH_S_REACHABLE
-		    || ((h->flags & GR_HIP_NH_F_LINK) && memcmp(ip + 24, h->ipv6, 16) != 0)) { // :113-119
+		    || ((h->flags & GR_HIP_NH_F_LINK) && memcmp(ip + 24, h->ipv6, 16) != 0)) { // :111-117
 			edge = GR_HIP_E_IP6_HOLD;
 			goto next;
 		}
-		memcpy(m->eth_dst, h->mac, 6); // :122-127
+		memcpy(m->eth_dst, h->mac, 6); // :119-134
 		m->eth_type = be16(0x86dd);
 		enqueue(g, GR_HIP_NODE_ETH_OUTPUT, m);
 		continue;
@@ -1143,8 +1145,9 @@ next:
 // MAC is looked up only when the iface differs from last_iface_id, which a
 // failed lookup leaves as it was while zeroing the cached MAC (:51-58): in
 // one walk, after an eth_output_no_mac packet, the next packet of the cached
-// iface leaves with source MAC 00:00:00:00:00:00. gr_mbuf_prepend (:43-49,
-// mbuf.h:89-106) cannot fail here: eth_input's adj(14) left the headroom.
+// iface leaves with source MAC 00:00:00:00:00:00. The prepend cannot fail
+// here (NO_HEADROOM, :43-49): eth_input's adj(14) left the headroom
+// (gr_mbuf_prepend: modules/infra/datapath/mbuf.h:89-106).
 static void node_eth_output(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
 	const or_topo_t *t = g->t;
 	uint16_t last_iface_id = GR_HIP_IFACE_ID_UNDEF;
@@ -1153,7 +1156,7 @@ static void node_eth_output(struct or_graph *g, struct or_mbuf **objs, uint16_t 
 		struct or_mbuf *m = objs[i];
 		mbuf_prepend(m, 14);
 		uint8_t *eth = MTOD(m);
-		memcpy(eth, m->eth_dst, 6); // :50
+		memcpy(eth, m->eth_dst, 6); // eth_output.c:50
 		if (m->iface != last_iface_id) {
 			const struct gr_hip_iface *iface = iface_from_id(t, m->iface);
 			if (iface == NULL || !iface->mac_ok) { // iface_get_eth_addr() < 0
@@ -1172,31 +1175,31 @@ static void node_eth_output(struct or_graph *g, struct or_mbuf **objs, uint16_t 
 	}
 }
 
-// iface_output_process, modules/infra/datapath/iface_output.c:198-255
+// iface_output_process, modules/infra/datapath/iface_output.c:60-117
 static void node_iface_output(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
 	const or_topo_t *t = g->t;
 	for (uint16_t i = 0; i < n; i++) {
 		struct or_mbuf *m = objs[i];
 		const struct gr_hip_iface *d_iface = iface_from_id(t, m->iface);
 		const struct gr_hip_iface *iface = d_iface, *parent = NULL;
-		if (d_iface->type == GR_HIP_IFACE_TYPE_VLAN) { // :219-224
+		if (d_iface->type == GR_HIP_IFACE_TYPE_VLAN) { // :81-86
 			m->vlan_id = d_iface->vlan_id;
 			iface = iface_from_id(t, d_iface->parent_id);
 			parent = iface;
 		}
-		if (iface == NULL) {
+		if (iface == NULL) { // :94-97
 			terminal(m, GR_HIP_E_IFACE_OUTPUT_VLAN_NO_PARENT);
 			continue;
 		}
-		if (!(d_iface->flags & GR_HIP_IFACE_F_UP)) {
+		if (!(d_iface->flags & GR_HIP_IFACE_F_UP)) { // :98-101
 			terminal(m, GR_HIP_E_IFACE_OUTPUT_ADMIN_DOWN);
 			continue;
 		}
-		m->tx_counted = 1; // :241-243
+		m->tx_counted = 1; // IFACE_STATS_INC :103-105
 		m->tx_iface = d_iface->id;
 		m->tx_parent = parent ? parent->id : 0;
 		m->iface = iface->id;
-		terminal(m, t->iout_type_edges[iface->type]);
+		terminal(m, t->iout_type_edges[iface->type]); // :107-108
 	}
 }
 
@@ -1206,7 +1209,8 @@ static void mark(struct or_mbuf **objs, uint16_t n, int node) {
 }
 
 // One graph walk over a burst (rte_graph_walk from gr_datapath_loop,
-// main_loop.c): iface_input on the RX burst, then the pending queue in order.
+// modules/infra/datapath/main_loop.c:459): iface_input on the RX burst, then
+// the pending queue in order.
 static void graph_walk(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
 	mark(objs, n, GR_HIP_NODE_IFACE_INPUT);
 	node_iface_input(g, objs, n);
@@ -1251,7 +1255,8 @@ static void graph_walk(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
 	g->pend_head = g->pend_tail = 0;
 }
 
-// Node counters of one walk as rte_graph keeps them (main_loop.c:39-64):
+// Node counters of one walk as grout collects them (node_stats_callback,
+// modules/infra/datapath/main_loop.c:40-66, over DPDK's per-node totals):
 // calls = process() invocations, packets = their return values; ip_output
 // returns only what it enqueued to eth_output (ip_output.c:153,162).
 // Punted packets restart on grout's CPU nodes, which count them there.

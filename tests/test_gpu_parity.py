@@ -263,8 +263,8 @@ def test_edge_registration(fastpath):
 
 
 def test_edge_registration_ip6(fastpath):
-    """The IPv6 registration tables: ip6_input nh types (ip6_input.c:31),
-    ip6_output nh/iface types (ip6_output.c:27,38), and eth_input handing
+    """The IPv6 registration tables: ip6_input nh types (ip6_input.c:32),
+    ip6_output nh/iface types (ip6_output.c:28,40), and eth_input handing
     0x86DD to the CPU instead of the device chain."""
     t, _ = SC.corpus_topology()
     fr, me, lab = SC.corpus_arrays()
@@ -673,7 +673,7 @@ def test_concurrent_queues_and_fib_updates(fastpath):
     streams' destinations) and switches the device FIB format back and forth
     (full re-uploads, RX views re-pointed). Every batch must equal the
     oracle: a kernel runs entirely before an update or entirely after it
-    (grout's RCU around FIB changes, route.c:740-771); the routes added last
+    (grout's RCU around FIB changes, modules/ip/control/route.c:740-771); the routes added last
     take effect."""
     import threading
 

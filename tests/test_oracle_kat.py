@@ -163,7 +163,7 @@ def test_kat6_invalid_mbuf_len():  # ip6_input.c:303-311: data_len = 40 / 2
 
 def test_kat6_default_is_other_host():
     # the default fake mbuf passes every check above and stops at the
-    # domain (ETH_DOMAIN_OTHER, ip6_input.c:114-118)
+    # domain (ETH_DOMAIN_OTHER, ip6_input.c:115-119)
     assert run(kat_topo(), [kat6()]) == ["ip6_input_other_host"]
 
 

@@ -4,9 +4,9 @@
 reference (/root/reference) and against the repo's own files.
 
 A citation is `name.c:RANGES` / `name.h:RANGES` (optionally with a path
-prefix), RANGES = N, N-M, comma separated. A bare `:RANGES` right after a
-citation on the same line, or in a comment whose last explicit file is
-within the preceding 40 lines, continues that file.
+prefix), RANGES = N, N-M, comma separated. A bare `:RANGES` continues the
+file cited last on its line, else the last main citation (not inside
+parentheses) of the 40 lines above.
 
 Prints one line per citation whose line range does not exist in the file it
 names (or, with --show, every citation with the first cited line's text, for
@@ -29,7 +29,7 @@ SCAN = [
 EXT = (".c", ".h", ".cpp", ".hip", ".py", ".md")
 
 EXPLICIT = re.compile(r"((?:[\w.-]+/)*[\w-]+(?:\.[\w-]+)*\.(?:c|h|cpp|hip)):(\d+(?:-\d+)?(?:,\s?\d+(?:-\d+)?)*)")
-BARE = re.compile(r"(?:^|[\s(\[,;])(?<![\w.]):(\d+(?:-\d+)?(?:,\s?\d+(?:-\d+)?)*)")
+BARE = re.compile(r"(?:^|[\s(,;])(?<![\w.]):(\d+(?:-\d+)?(?:,\s?\d+(?:-\d+)?)*)")
 
 
 def index_files(top, skip=()):
@@ -84,14 +84,23 @@ def scan_file(path):
         for m in BARE.finditer(text):
             spans.append((m.start(1) - 1, None, m.group(1)))
         spans.sort()
+        here = None  # the last explicit citation on this line
         for pos, name, spec in spans:
             if name is None:
-                # a bare range: the file cited last, nearby
-                if last is None or no - last[1] > 40:
+                # a bare range: the file cited just before it on this line,
+                # else the main citation of the lines above, nearby
+                if here is not None:
+                    name = here
+                elif last is None or no - last[1] > 40:
                     continue
-                name = last[0]
-            else:
-                # an explicit citation also swallows ":N" directly after it
+                else:
+                    name = last[0]
+                yield rel, no, name, spec
+                continue
+            here = name
+            if text[:pos].count("(") <= text[:pos].count(")"):
+                # a main citation: bare ranges after it continue it (one in
+                # parentheses is a side note and does not)
                 last = (name, no)
             yield rel, no, name, spec
 
