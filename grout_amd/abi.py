@@ -141,6 +141,9 @@ HIP_API = {
     "gr_hip_edges_ip6_input_nh_type": (_I, [_P, _U8, _U8]),
     "gr_hip_edges_ip6_output_nh_type": (_I, [_P, _U8, _U8]),
     "gr_hip_edges_ip6_output_iface_type": (_I, [_P, _U8, _U8]),
+    "gr_hip_edges_get": (_I, [_P, _I, _U16]),
+    "gr_hip_device_count": (_I, []),
+    "gr_hip_device_numa_node": (_I, [_I]),
     "gr_hip_iface_set": (_I, [_P, _P, _U32]),
     "gr_hip_iface_del": (_I, [_P, _U16]),
     "gr_hip_nh_set": (_I, [_P, _U32, _P, _U32]),

@@ -21,6 +21,7 @@
 #include <mutex>
 #include <shared_mutex>
 #include <new>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <vector>
@@ -713,6 +714,87 @@ EDGE_SETTER(gr_hip_edges_iface_output_type, iout_type, 8)
 EDGE_SETTER(gr_hip_edges_ip6_input_nh_type, in6_nh, 8)
 EDGE_SETTER(gr_hip_edges_ip6_output_nh_type, out6_nh, 8)
 EDGE_SETTER(gr_hip_edges_ip6_output_iface_type, out6_iface, 8)
+
+extern "C" int gr_hip_edges_get(gr_hip_ctx_t *c, int table, uint16_t key) {
+	if (c == nullptr)
+		return -EINVAL;
+	std::shared_lock<std::shared_mutex> l(c->mu);
+	const fwd4_edges &E = c->edges;
+	const uint8_t *t = nullptr;
+	uint32_t lim = 8;
+	switch (table) {
+	case GR_HIP_EDGES_ETH_TYPE: {
+		int e = GR_HIP_E_ETH_INPUT_UNKNOWN_TYPE; // l2l3_edges default (eth_input.c:24)
+		for (uint32_t i = 0; i < E.n_eth_types; i++)
+			if (E.eth_type_be[i] == key)
+				e = E.eth_type_edge[i];
+		return e;
+	}
+	case GR_HIP_EDGES_IFACE_MODE:
+		t = E.mode;
+		lim = GR_HIP_IFACE_MODE_COUNT;
+		break;
+	case GR_HIP_EDGES_IP_INPUT_NH_TYPE:
+		t = E.in_nh;
+		break;
+	case GR_HIP_EDGES_IP_OUTPUT_NH_TYPE:
+		t = E.out_nh;
+		break;
+	case GR_HIP_EDGES_IP_OUTPUT_IFACE_TYPE:
+		t = E.out_iface;
+		break;
+	case GR_HIP_EDGES_IFACE_OUTPUT_TYPE:
+		t = E.iout_type;
+		break;
+	case GR_HIP_EDGES_IP6_INPUT_NH_TYPE:
+		t = E.in6_nh;
+		break;
+	case GR_HIP_EDGES_IP6_OUTPUT_NH_TYPE:
+		t = E.out6_nh;
+		break;
+	case GR_HIP_EDGES_IP6_OUTPUT_IFACE_TYPE:
+		t = E.out6_iface;
+		break;
+	default:
+		return -EINVAL;
+	}
+	return key < lim ? t[key] : -EINVAL;
+}
+
+// ---------------------------------------------------------------------------
+// devices
+// ---------------------------------------------------------------------------
+
+extern "C" int gr_hip_device_count(void) {
+	int n = 0;
+	if (hipGetDeviceCount(&n) != hipSuccess) {
+		(void)hipGetLastError();
+		return -ENODEV;
+	}
+	return n;
+}
+
+extern "C" int gr_hip_device_numa_node(int dev) {
+	char bus[64];
+	if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) {
+		(void)hipGetLastError();
+		return -ENODEV;
+	}
+	for (char *p = bus; *p; p++) // sysfs names are lower case
+		if (*p >= 'A' && *p <= 'F')
+			*p = (char)(*p - 'A' + 'a');
+	char path[160];
+	snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
+	FILE *f = fopen(path, "r");
+	if (f == nullptr)
+		return -ENOENT;
+	int node = -1;
+	const int got = fscanf(f, "%d", &node);
+	fclose(f);
+	if (got != 1)
+		return -EIO;
+	return node < 0 ? 0 : node; // -1: no NUMA information (one node)
+}
 
 // ---------------------------------------------------------------------------
 // mirrors

@@ -8,6 +8,11 @@
 // enum order. grout's stock iface_input stays registered as
 // "iface_input_cpu", the PUNT target.
 //
+// The module opens one fast-path context per configured GPU (all visible
+// ones by default). Each worker graph binds to one of them at creation,
+// NUMA-aware (pick_gpu); the control plane applies every change to all of
+// them (gpu_fwd4_iface_set ... below, FANOUT).
+//
 // Per graph (one per worker, worker.c) the node keeps a walk: the mbufs of
 // successive RX bursts accumulate until a batch is full, an RX burst comes
 // back short (the queue drained: latency matters more than batching) or the
@@ -27,41 +32,82 @@
 
 #include <errno.h>
 #include <stdlib.h>
+#include <string.h>
 #include <time.h>
 
 static struct gpu_fwd4_conf conf = {
-	.dev = 0,
+	.n_devs = 0, // every visible device
 	.max_ifaces = 1024,
 	.max_nexthops = 1u << 17,
 	.batch = 1u << 16,
 	.rx_burst = 64,
 	.max_delay_ns = 50000,
 };
-static gr_hip_ctx_t *hip_ctx;
+
+// One fast-path context per GPU; the worker graphs are spread over them.
+static struct {
+	gr_hip_ctx_t *ctx;
+	int dev;
+	int numa; // the device's NUMA node
+	uint32_t graphs; // worker graphs bound to it
+} gpus[GPU_FWD4_MAX_DEVS];
+static uint32_t n_gpus;
 
 int gpu_fwd4_configure(const struct gpu_fwd4_conf *c) {
-	if (c == NULL || c->batch == 0 || c->rx_burst == 0 || hip_ctx != NULL)
+	if (c == NULL || c->batch == 0 || c->rx_burst == 0 || c->n_devs > GPU_FWD4_MAX_DEVS || n_gpus != 0)
 		return -EINVAL;
 	conf = *c;
 	return 0;
 }
 
 gr_hip_ctx_t *gpu_fwd4_hip_ctx(void) {
-	return hip_ctx;
+	return n_gpus ? gpus[0].ctx : NULL;
 }
 
-// ---- module: one fast-path context per process (one GPU) -------------------
+uint32_t gpu_fwd4_n_ctx(void) {
+	return n_gpus;
+}
+
+gr_hip_ctx_t *gpu_fwd4_ctx_at(uint32_t i) {
+	return i < n_gpus ? gpus[i].ctx : NULL;
+}
+
+// ---- module: one fast-path context per configured device -------------------
+static void gpu_fini(struct event_base *ev);
+
 static void gpu_init(struct event_base *ev) {
 	(void)ev;
-	if (gr_hip_init(conf.dev, conf.max_ifaces, conf.max_nexthops, &hip_ctx) < 0)
-		hip_ctx = NULL; // the node's init fails, so does graph creation
+	int devs[GPU_FWD4_MAX_DEVS];
+	uint32_t n = conf.n_devs;
+	if (n == 0) { // every visible device
+		const int count = gr_hip_device_count();
+		n = count > 0 ? (uint32_t)count : 0;
+		if (n > GPU_FWD4_MAX_DEVS)
+			n = GPU_FWD4_MAX_DEVS;
+		for (uint32_t i = 0; i < n; i++)
+			devs[i] = (int)i;
+	} else {
+		memcpy(devs, conf.devs, n * sizeof(devs[0]));
+	}
+	for (uint32_t i = 0; i < n; i++) {
+		gr_hip_ctx_t *c = NULL;
+		if (gr_hip_init(devs[i], conf.max_ifaces, conf.max_nexthops, &c) < 0) {
+			gpu_fini(NULL); // all or nothing: the nodes' init then fails
+			return;
+		}
+		const int numa = gr_hip_device_numa_node(devs[i]);
+		gpus[n_gpus].ctx = c;
+		gpus[n_gpus].dev = devs[i];
+		gpus[n_gpus].numa = numa < 0 ? 0 : numa;
+		gpus[n_gpus].graphs = 0;
+		n_gpus++;
+	}
 }
 
 static void gpu_fini(struct event_base *ev) {
 	(void)ev;
-	if (hip_ctx != NULL)
-		gr_hip_fini(hip_ctx);
-	hip_ctx = NULL;
+	while (n_gpus > 0)
+		gr_hip_fini(gpus[--n_gpus].ctx);
 }
 
 static struct module gpu_module = {
@@ -74,9 +120,27 @@ RTE_INIT(gpu_module_init) {
 	module_register(&gpu_module);
 }
 
+// The GPU a worker graph runs on: one on the graph's NUMA socket (any GPU if
+// none is), the one with the fewest graphs, lowest first -- the policy of
+// grout's RX queue distribution over workers (worker.c:424-481): round robin
+// over the CPUs of the port's socket.
+static int pick_gpu(const struct rte_graph *graph) {
+	int best = -1;
+	for (int pass = 0; pass < 2 && best < 0; pass++) {
+		for (uint32_t i = 0; i < n_gpus; i++) {
+			if (pass == 0 && gpus[i].numa != graph->socket)
+				continue;
+			if (best < 0 || gpus[i].graphs < gpus[best].graphs)
+				best = (int)i;
+		}
+	}
+	return best;
+}
+
 // ---- per-graph walk state ----------------------------------------------------
 struct gpu_walk {
 	const struct rte_graph *graph;
+	int gpu; // index in gpus[]
 	gr_hip_queue_t *q;
 	uint32_t n, cap;
 	uint64_t first_ns; // arrival of the oldest held packet, 0 = none
@@ -210,7 +274,7 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 }
 
 static int gpu_fwd4_init(const struct rte_graph *graph, struct rte_node *node) {
-	if (hip_ctx == NULL)
+	if (n_gpus == 0)
 		return -ENODEV;
 	int slot = 0;
 	while (slot < MAX_WALKS && walks[slot] != NULL)
@@ -221,16 +285,18 @@ static int gpu_fwd4_init(const struct rte_graph *graph, struct rte_node *node) {
 	if (w == NULL)
 		return -ENOMEM;
 	w->graph = graph;
+	w->gpu = pick_gpu(graph);
 	w->cap = conf.batch + RTE_GRAPH_BURST_SIZE;
 	w->mbufs = calloc(w->cap, sizeof(*w->mbufs));
 	w->v = calloc(w->cap, sizeof(*w->v));
-	int r = (w->mbufs == NULL || w->v == NULL) ? -ENOMEM : gr_hip_queue_create(hip_ctx, NULL, &w->q);
+	int r = (w->mbufs == NULL || w->v == NULL) ? -ENOMEM : gr_hip_queue_create(gpus[w->gpu].ctx, NULL, &w->q);
 	if (r < 0) {
 		free(w->mbufs);
 		free(w->v);
 		free(w);
 		return r;
 	}
+	gpus[w->gpu].graphs++;
 	walks[slot] = w;
 	gpu_fwd4_ctx(node)->w = w;
 	return 0;
@@ -243,66 +309,14 @@ static void gpu_fwd4_fini(const struct rte_graph *graph, struct rte_node *node) 
 		if (w == NULL || w->graph != graph)
 			continue;
 		gr_hip_queue_destroy(w->q);
+		if ((uint32_t)w->gpu < n_gpus && gpus[w->gpu].graphs > 0)
+			gpus[w->gpu].graphs--;
 		free(w->mbufs);
 		free(w->v);
 		free(w);
 		walks[i] = NULL;
 	}
 }
-
-// next_nodes in enum gr_hip_edge order (include/grout_hip.h)
-#define GPU_FWD4_EDGES                                                                             \
-	[GR_HIP_E_PUNT] = "iface_input_cpu",                                                       \
-	[GR_HIP_E_IFACE_MODE_UNKNOWN] = "iface_mode_unknown",                                      \
-	[GR_HIP_E_IFACE_INPUT_ADMIN_DOWN] = "iface_input_admin_down",                              \
-	[GR_HIP_E_IFACE_INPUT_UNKNOWN_VLAN] = "iface_input_unknown_vlan",                          \
-	[GR_HIP_E_XCONNECT] = "xconnect",                                                          \
-	[GR_HIP_E_BRIDGE_INPUT] = "bridge_input",                                                  \
-	[GR_HIP_E_ETH_INPUT_UNKNOWN_TYPE] = "eth_input_unknown_type",                              \
-	[GR_HIP_E_ETH_INPUT_INVALID_IFACE] = "eth_input_invalid_iface",                            \
-	[GR_HIP_E_SNAP_INPUT] = "snap_input",                                                      \
-	[GR_HIP_E_ARP_INPUT] = "arp_input",                                                        \
-	[GR_HIP_E_IP6_INPUT] = "ip6_input",                                                        \
-	[GR_HIP_E_LACP_INPUT] = "lacp_input",                                                      \
-	[GR_HIP_E_IP_INPUT_LOCAL] = "ip_input_local",                                              \
-	[GR_HIP_E_IP_INPUT_LOCAL_CT] = "ip_input_local_ct",                                        \
-	[GR_HIP_E_IP_ERROR_DEST_UNREACH] = "ip_error_dest_unreach",                                \
-	[GR_HIP_E_IP_INPUT_BAD_CHECKSUM] = "ip_input_bad_checksum",                                \
-	[GR_HIP_E_IP_INPUT_BAD_ADDRESS] = "ip_input_bad_address",                                  \
-	[GR_HIP_E_IP_INPUT_BAD_LENGTH] = "ip_input_bad_length",                                    \
-	[GR_HIP_E_IP_INPUT_BAD_VERSION] = "ip_input_bad_version",                                  \
-	[GR_HIP_E_IP_INPUT_OTHER_HOST] = "ip_input_other_host",                                    \
-	[GR_HIP_E_IP_BLACKHOLE] = "ip_blackhole",                                                  \
-	[GR_HIP_E_DNAT44_STATIC] = "dnat44_static",                                                \
-	[GR_HIP_E_IP_ERROR_TTL_EXCEEDED] = "ip_error_ttl_exceeded",                                \
-	[GR_HIP_E_IP_HOLD] = "ip_hold",                                                            \
-	[GR_HIP_E_IP_OUTPUT_ERROR] = "ip_output_error",                                            \
-	[GR_HIP_E_IP_FRAGMENT] = "ip_fragment",                                                    \
-	[GR_HIP_E_IP_ERROR_FRAG_NEEDED] = "ip_error_frag_needed",                                  \
-	[GR_HIP_E_SR6_OUTPUT] = "sr6_output",                                                      \
-	[GR_HIP_E_XVRF] = "xvrf",                                                                  \
-	[GR_HIP_E_IPIP_OUTPUT] = "ipip_output",                                                    \
-	[GR_HIP_E_IP_OUTPUT_SNAT] = "ip_output_snat",                                              \
-	[GR_HIP_E_ETH_OUTPUT_NO_MAC] = "eth_output_no_mac",                                        \
-	[GR_HIP_E_IFACE_OUTPUT_INVAL_TYPE] = "iface_output_inval_type",                            \
-	[GR_HIP_E_IFACE_OUTPUT_ADMIN_DOWN] = "iface_output_admin_down",                            \
-	[GR_HIP_E_IFACE_OUTPUT_VLAN_NO_PARENT] = "iface_output_vlan_no_parent",                    \
-	[GR_HIP_E_BOND_OUTPUT] = "bond_output",                                                    \
-	[GR_HIP_E_VXLAN_OUTPUT] = "vxlan_output",                                                  \
-	[GR_HIP_E_PORT_OUTPUT] = "port_output",                                                    \
-	[GR_HIP_E_IP6_INPUT_LOCAL] = "ip6_input_local",                                            \
-	[GR_HIP_E_IP6_ERROR_DEST_UNREACH] = "ip6_error_dest_unreach",                              \
-	[GR_HIP_E_IP6_INPUT_NOT_MEMBER] = "ip6_input_not_member",                                  \
-	[GR_HIP_E_IP6_INPUT_OTHER_HOST] = "ip6_input_other_host",                                  \
-	[GR_HIP_E_IP6_INPUT_BAD_VERSION] = "ip6_input_bad_version",                                \
-	[GR_HIP_E_IP6_INPUT_BAD_ADDR] = "ip6_input_bad_addr",                                      \
-	[GR_HIP_E_IP6_INPUT_BAD_LENGTH] = "ip6_input_bad_length",                                  \
-	[GR_HIP_E_IP6_BLACKHOLE] = "ip6_blackhole",                                                \
-	[GR_HIP_E_SR6_LOCAL] = "sr6_local",                                                        \
-	[GR_HIP_E_IP6_ERROR_TTL_EXCEEDED] = "ip6_error_ttl_exceeded",                              \
-	[GR_HIP_E_IP6_HOLD] = "ip6_hold",                                                          \
-	[GR_HIP_E_IP6_OUTPUT_ERROR] = "ip6_output_error",                                          \
-	[GR_HIP_E_IP6_OUTPUT_TOO_BIG] = "ip6_output_too_big",
 
 static struct rte_node_register gpu_fwd4_node = {
 	.name = "iface_input",
@@ -369,4 +383,102 @@ int gpu_fwd4_queue_stats(const struct rte_graph *graph, struct gr_hip_iface_stat
 	if (w == NULL)
 		return -ENOENT;
 	return gr_hip_queue_stats(w->q, stats, max_ifaces, reset);
+}
+
+int gpu_fwd4_graph_gpu(const struct rte_graph *graph) {
+	struct gpu_walk *w = walk_of(graph);
+	return w == NULL ? -ENOENT : w->gpu;
+}
+
+// ---- control plane: every change goes to every GPU's context ---------------
+// (grout's control thread calls these from its event handlers, INTEGRATION.md
+// §3; each context is updated under its own quiesce, so a GPU's in-flight
+// walks see the old or the new state, never a mix.) The first error is
+// returned; the other contexts still get the change.
+#define FANOUT(call)                                                                               \
+	do {                                                                                       \
+		int ret__ = n_gpus ? 0 : -ENODEV;                                                  \
+		for (uint32_t i = 0; i < n_gpus; i++) {                                            \
+			gr_hip_ctx_t *ctx = gpus[i].ctx;                                           \
+			const int r__ = (call);                                                    \
+			if (r__ < 0 && ret__ == 0)                                                 \
+				ret__ = r__;                                                       \
+		}                                                                                  \
+		return ret__;                                                                      \
+	} while (0)
+
+int gpu_fwd4_iface_set(const struct gr_hip_iface *ifaces, uint32_t n) {
+	FANOUT(gr_hip_iface_set(ctx, ifaces, n));
+}
+int gpu_fwd4_iface_del(uint16_t iface_id) {
+	FANOUT(gr_hip_iface_del(ctx, iface_id));
+}
+int gpu_fwd4_nh_set(uint32_t first_slot, const struct gr_hip_nh *nh, uint32_t n) {
+	FANOUT(gr_hip_nh_set(ctx, first_slot, nh, n));
+}
+int gpu_fwd4_reta_set(uint32_t first, const uint32_t *slots, uint32_t n) {
+	FANOUT(gr_hip_reta_set(ctx, first, slots, n));
+}
+int gpu_fwd4_fib4_create(uint16_t vrf_id, uint32_t max_routes, uint32_t num_tbl8) {
+	FANOUT(gr_hip_fib4_create(ctx, vrf_id, max_routes, num_tbl8));
+}
+int gpu_fwd4_fib4_destroy(uint16_t vrf_id) {
+	FANOUT(gr_hip_fib4_destroy(ctx, vrf_id));
+}
+int gpu_fwd4_route4_add(const struct gr_hip_route4 *routes, uint32_t n, int replace) {
+	FANOUT(gr_hip_route4_add(ctx, routes, n, replace));
+}
+int gpu_fwd4_route4_del(uint16_t vrf_id, uint32_t ip, uint8_t prefixlen) {
+	FANOUT(gr_hip_route4_del(ctx, vrf_id, ip, prefixlen));
+}
+int gpu_fwd4_fib4_commit(uint16_t vrf_id) {
+	FANOUT(gr_hip_fib4_commit(ctx, vrf_id));
+}
+int gpu_fwd4_fib6_create(uint16_t vrf_id, uint32_t max_routes, uint32_t num_tbl8) {
+	FANOUT(gr_hip_fib6_create(ctx, vrf_id, max_routes, num_tbl8));
+}
+int gpu_fwd4_fib6_destroy(uint16_t vrf_id) {
+	FANOUT(gr_hip_fib6_destroy(ctx, vrf_id));
+}
+int gpu_fwd4_route6_add(const struct gr_hip_route6 *routes, uint32_t n, int replace) {
+	FANOUT(gr_hip_route6_add(ctx, routes, n, replace));
+}
+int gpu_fwd4_route6_del(uint16_t vrf_id, uint16_t iface_id, const uint8_t ip[16], uint8_t prefixlen) {
+	FANOUT(gr_hip_route6_del(ctx, vrf_id, iface_id, ip, prefixlen));
+}
+int gpu_fwd4_fib6_commit(uint16_t vrf_id) {
+	FANOUT(gr_hip_fib6_commit(ctx, vrf_id));
+}
+int gpu_fwd4_edges_set(int table, uint16_t key, uint8_t edge) {
+	switch (table) {
+	case GR_HIP_EDGES_ETH_TYPE:
+		FANOUT(gr_hip_edges_eth_type(ctx, key, edge));
+	case GR_HIP_EDGES_IFACE_MODE:
+		FANOUT(gr_hip_edges_iface_mode(ctx, (uint8_t)key, edge));
+	case GR_HIP_EDGES_IP_INPUT_NH_TYPE:
+		FANOUT(gr_hip_edges_ip_input_nh_type(ctx, (uint8_t)key, edge));
+	case GR_HIP_EDGES_IP_OUTPUT_NH_TYPE:
+		FANOUT(gr_hip_edges_ip_output_nh_type(ctx, (uint8_t)key, edge));
+	case GR_HIP_EDGES_IP_OUTPUT_IFACE_TYPE:
+		FANOUT(gr_hip_edges_ip_output_iface_type(ctx, (uint8_t)key, edge));
+	case GR_HIP_EDGES_IFACE_OUTPUT_TYPE:
+		FANOUT(gr_hip_edges_iface_output_type(ctx, (uint8_t)key, edge));
+	case GR_HIP_EDGES_IP6_INPUT_NH_TYPE:
+		FANOUT(gr_hip_edges_ip6_input_nh_type(ctx, (uint8_t)key, edge));
+	case GR_HIP_EDGES_IP6_OUTPUT_NH_TYPE:
+		FANOUT(gr_hip_edges_ip6_output_nh_type(ctx, (uint8_t)key, edge));
+	case GR_HIP_EDGES_IP6_OUTPUT_IFACE_TYPE:
+		FANOUT(gr_hip_edges_ip6_output_iface_type(ctx, (uint8_t)key, edge));
+	default:
+		return -EINVAL;
+	}
+}
+int gpu_fwd4_tune(const char *key, int value) {
+	FANOUT(gr_hip_tune(ctx, key, value));
+}
+int gpu_fwd4_host_register(void *ptr, size_t bytes) {
+	FANOUT(gr_hip_host_register(ctx, ptr, bytes));
+}
+int gpu_fwd4_host_unregister(void *ptr) {
+	FANOUT(gr_hip_host_unregister(ctx, ptr));
 }

@@ -137,3 +137,127 @@ void gr_modules_fini(struct event_base *ev) {
 			m->fini(ev);
 	}
 }
+
+// ---- conntrack / NAT stand-ins (tests) -------------------------------------
+#define MAX_CONNS 64
+#define MAX_SNAT 64
+
+static struct conn conns[MAX_CONNS];
+static uint32_t n_conns;
+static struct {
+	uint16_t iface_id;
+	ip4_addr_t from, to;
+} snat_rules[MAX_SNAT];
+static uint32_t n_snat;
+
+void gr_test_policy_clear(void) {
+	n_conns = 0;
+	n_snat = 0;
+}
+
+int gr_test_conn_add(const struct conn_key *fwd, const struct conn_key *rev, struct conn **out) {
+	if (n_conns == MAX_CONNS)
+		return -ENOSPC;
+	struct conn *c = &conns[n_conns++];
+	c->fwd_key = *fwd;
+	c->rev_key = *rev;
+	if (out != NULL)
+		*out = c;
+	return 0;
+}
+
+int gr_test_snat44_static_add(uint16_t iface_id, ip4_addr_t from, ip4_addr_t to) {
+	if (n_snat == MAX_SNAT)
+		return -ENOSPC;
+	snat_rules[n_snat].iface_id = iface_id;
+	snat_rules[n_snat].from = from;
+	snat_rules[n_snat].to = to;
+	n_snat++;
+	return 0;
+}
+
+// The key of an IPv4 packet's first fragment: iface, protocol, addresses
+// and UDP ports (grout's gr_conn_parse_key also reads TCP ports and ICMP ids).
+bool gr_conn_parse_key(const struct iface *iface, const addr_family_t af, const struct rte_mbuf *m,
+		       struct conn_key *key) {
+	const struct rte_ipv4_hdr *ip = rte_pktmbuf_mtod(m, const struct rte_ipv4_hdr *);
+	if (af != GR_AF_IP4 || (rte_be_to_cpu_16(ip->fragment_offset) & RTE_IPV4_HDR_OFFSET_MASK) != 0)
+		return false;
+	memset(key, 0, sizeof(*key));
+	key->iface_id = iface->id;
+	key->af = af;
+	key->proto = ip->next_proto_id;
+	key->src = ip->src_addr;
+	key->dst = ip->dst_addr;
+	if (ip->next_proto_id == 17) { // IPPROTO_UDP
+		const struct rte_udp_hdr *udp = rte_pktmbuf_mtod_offset(m, const struct rte_udp_hdr *,
+									  rte_ipv4_hdr_len(ip));
+		key->src_id = udp->src_port;
+		key->dst_id = udp->dst_port;
+	}
+	return true;
+}
+
+static bool key_eq(const struct conn_key *a, const struct conn_key *b) {
+	return a->iface_id == b->iface_id && a->af == b->af && a->proto == b->proto && a->src == b->src
+		&& a->dst == b->dst && a->src_id == b->src_id && a->dst_id == b->dst_id;
+}
+
+struct conn *gr_conn_lookup(const struct conn_key *key, conn_flow_t *flow) {
+	for (uint32_t i = 0; i < n_conns; i++) {
+		if (key_eq(&conns[i].fwd_key, key)) {
+			*flow = CONN_FLOW_FWD;
+			return &conns[i];
+		}
+		if (key_eq(&conns[i].rev_key, key)) {
+			*flow = CONN_FLOW_REV;
+			return &conns[i];
+		}
+	}
+	return NULL;
+}
+
+// One's-complement update of a checksum for a changed 32-bit field (RFC 1624
+// eqn. 3, what grout's fixup_checksum_32 computes).
+static rte_be16_t cksum_update32(rte_be16_t cksum, uint32_t from, uint32_t to) {
+	uint32_t sum = (uint16_t)~cksum;
+	sum += (uint16_t)~from + (uint16_t)~(from >> 16);
+	sum += (to & 0xffff) + (to >> 16);
+	sum = (sum & 0xffff) + (sum >> 16);
+	sum = (sum & 0xffff) + (sum >> 16);
+	return (rte_be16_t)~sum;
+}
+
+// snat44_process with static rules only: a packet whose source has a rule
+// on the egress iface gets the translated source, its IPv4 checksum and a
+// non-zero UDP checksum updated (FINAL); anything else CONTINUEs.
+nat_verdict_t snat44_process(const struct iface *iface, struct rte_mbuf *m) {
+	if (!(iface->flags & GR_IFACE_F_SNAT_STATIC))
+		return NAT_VERDICT_CONTINUE;
+	struct rte_ipv4_hdr *ip = rte_pktmbuf_mtod(m, struct rte_ipv4_hdr *);
+	for (uint32_t i = 0; i < n_snat; i++) {
+		if (snat_rules[i].iface_id != iface->id || snat_rules[i].from != ip->src_addr)
+			continue;
+		const ip4_addr_t to = snat_rules[i].to;
+		ip->hdr_checksum = cksum_update32(ip->hdr_checksum, ip->src_addr, to);
+		if ((rte_be_to_cpu_16(ip->fragment_offset) & RTE_IPV4_HDR_OFFSET_MASK) == 0 && ip->next_proto_id == 17) {
+			struct rte_udp_hdr *udp = rte_pktmbuf_mtod_offset(m, struct rte_udp_hdr *, rte_ipv4_hdr_len(ip));
+			if (udp->dgram_cksum != 0) {
+				udp->dgram_cksum = cksum_update32(udp->dgram_cksum, ip->src_addr, to);
+				if (udp->dgram_cksum == 0)
+					udp->dgram_cksum = 0xffff;
+			}
+		}
+		ip->src_addr = to;
+		return NAT_VERDICT_FINAL;
+	}
+	return NAT_VERDICT_CONTINUE;
+}
+
+// A connection's table index + 1 (0: not one of the stand-in's connections),
+// for the harness to decode conn_mbuf_data without dereferencing it.
+uint32_t gr_test_conn_index(const struct conn *c) {
+	if (c < conns || c >= conns + n_conns)
+		return 0;
+	return (uint32_t)(c - conns) + 1;
+}

@@ -11,7 +11,7 @@
 //                           GR_DROP_REGISTER), gr_node_attach_parent
 //                           (graph.c:35-63), the registration walk of
 //                           graph_init (graph.c:652-688)
-//   modules                 main/module.h:45-53 (struct module, module_register)
+//   modules                 main/module.h:43-49 (struct module, module_register)
 //
 // The objects grout's nodes dereference (struct iface, struct nexthop) are
 // reduced to what the GPU node needs to hand packets back: an id and a
@@ -21,6 +21,7 @@
 
 #include "rte_graph_min.h"
 
+#include <grout_hip.h>
 #include <stdbool.h>
 #include <sys/queue.h>
 
@@ -29,14 +30,63 @@ extern "C" {
 #endif
 
 // ---- objects ---------------------------------------------------------------
+// gr_iface_type_t / gr_iface_flags_t (gr_infra.h:18-37), gr_nh_* and
+// addr_family_t (gr_nexthop.h:12-40, gr_net_types.h): grout's values.
+typedef uint8_t gr_iface_type_t; // grout: enum : uint8_t (C23)
+enum {
+	GR_IFACE_TYPE_UNDEF = 0,
+	GR_IFACE_TYPE_VRF,
+	GR_IFACE_TYPE_PORT,
+	GR_IFACE_TYPE_VLAN,
+	GR_IFACE_TYPE_IPIP,
+	GR_IFACE_TYPE_BOND,
+	GR_IFACE_TYPE_BRIDGE,
+	GR_IFACE_TYPE_VXLAN,
+};
+#define GR_IFACE_F_UP GR_HIP_IFACE_F_UP
+#define GR_IFACE_F_SNAT_STATIC GR_HIP_IFACE_F_SNAT_STATIC
+#define GR_IFACE_F_SNAT_DYNAMIC GR_HIP_IFACE_F_SNAT_DYNAMIC
+typedef uint8_t addr_family_t;
+#define GR_AF_UNSPEC GR_HIP_AF_UNSPEC
+#define GR_AF_IP4 GR_HIP_AF_IP4
+#define GR_AF_IP6 GR_HIP_AF_IP6
+typedef uint8_t gr_nh_type_t;
+#define GR_NH_T_L3 GR_HIP_NH_T_L3
+#define GR_NH_S_REACHABLE GR_HIP_NH_S_REACHABLE
+#define GR_NH_F_LOCAL GR_HIP_NH_F_LOCAL
+#define GR_NH_F_LINK GR_HIP_NH_F_LINK
+typedef uint32_t ip4_addr_t; // network order
+
 struct iface {
 	uint16_t id;
+	gr_iface_type_t type;
+	uint8_t mode;
+	uint16_t flags;
+	uint16_t mtu;
 	uint16_t vrf_id;
+};
+
+// nexthop_info_l3 (nexthop.h:41-54 over gr_nexthop.h:93-105)
+struct nexthop_info_l3 {
+	uint8_t state;
+	uint8_t flags;
+	addr_family_t af;
+	ip4_addr_t ipv4;
+	uint8_t ipv6[16];
+	struct rte_ether_addr mac;
 };
 
 struct nexthop {
 	uint32_t slot; // the dense index the device FIB holds
+	gr_nh_type_t type;
+	uint16_t iface_id;
+	uint16_t vrf_id;
+	struct nexthop_info_l3 l3;
 };
+
+static inline const struct nexthop_info_l3 *nexthop_info_l3(const struct nexthop *nh) {
+	return &nh->l3;
+}
 
 // Registries the control plane fills (grout: iface.c / nexthop.c pools).
 const struct iface *iface_from_id(uint16_t id);
@@ -71,8 +121,11 @@ typedef enum {
 } eth_domain_t;
 
 struct l3_addr { // gr_net_types.h: an address family and an IPv4/IPv6 address
-	uint8_t family;
-	uint8_t addr[16];
+	addr_family_t af;
+	union {
+		ip4_addr_t ipv4;
+		uint8_t ipv6[16];
+	};
 };
 
 GR_MBUF_PRIV_DATA_TYPE(mbuf_data, {});
@@ -85,6 +138,56 @@ GR_MBUF_PRIV_DATA_TYPE(eth_input_mbuf_data, {
 	const struct nexthop *nh;
 });
 GR_MBUF_PRIV_DATA_TYPE(l3_mbuf_data, { const struct nexthop *nh; });
+GR_MBUF_PRIV_DATA_TYPE(eth_output_mbuf_data, {
+	struct rte_ether_addr dst;
+	rte_be16_t ether_type;
+	struct l3_addr vtep;
+});
+
+// ---- conntrack and NAT (modules/policy: conntrack.h:24-67,
+// nat_datapath.h:48-67). Stand-ins for the tests: a connection table and a
+// static SNAT table filled by the harness (walk_harness.c), with grout's
+// signatures and private data; in grout the nodes use the real ones.
+typedef enum {
+	CONN_FLOW_FWD = 0,
+	CONN_FLOW_REV,
+} conn_flow_t;
+
+struct conn_key {
+	uint16_t iface_id;
+	addr_family_t af;
+	uint8_t proto;
+	ip4_addr_t src;
+	ip4_addr_t dst;
+	rte_be16_t src_id;
+	rte_be16_t dst_id;
+};
+
+struct conn {
+	struct conn_key fwd_key;
+	struct conn_key rev_key;
+};
+
+GR_MBUF_PRIV_DATA_TYPE(conn_mbuf_data, {
+	struct conn *conn;
+	conn_flow_t flow;
+});
+
+bool gr_conn_parse_key(const struct iface *, const addr_family_t, const struct rte_mbuf *, struct conn_key *);
+struct conn *gr_conn_lookup(const struct conn_key *, conn_flow_t *);
+
+typedef enum {
+	NAT_VERDICT_CONTINUE,
+	NAT_VERDICT_FINAL,
+	NAT_VERDICT_DROP,
+} nat_verdict_t;
+
+nat_verdict_t snat44_process(const struct iface *, struct rte_mbuf *);
+
+// Test tables behind the stand-ins (0 or -ENOSPC).
+int gr_test_conn_add(const struct conn_key *fwd, const struct conn_key *rev, struct conn **out);
+int gr_test_snat44_static_add(uint16_t iface_id, ip4_addr_t from, ip4_addr_t to);
+void gr_test_policy_clear(void);
 
 static inline bool gr_mbuf_is_traced(struct rte_mbuf *m) {
 	return !STAILQ_EMPTY(&mbuf_data(m)->traces);

@@ -26,9 +26,7 @@ struct node_def {
 static struct node_def defs[MAX_NODES];
 static rte_node_t n_defs;
 
-struct rte_graph {
-	char name[RTE_GRAPH_NAMESIZE];
-	rte_graph_t id;
+struct rte_graph_priv {
 	uint32_t n_nodes;
 	struct rte_node **nodes; // instances, by position
 	int32_t *inst_of; // [MAX_NODES]: node id -> position, -1 if absent
@@ -118,28 +116,29 @@ rte_edge_t rte_node_edge_get(rte_node_t id, char *next_nodes[]) {
 static void graph_free(struct rte_graph *g) {
 	if (g == NULL)
 		return;
-	for (uint32_t i = 0; i < g->n_nodes; i++) {
-		struct rte_node *n = g->nodes[i];
+	for (uint32_t i = 0; i < g->priv->n_nodes; i++) {
+		struct rte_node *n = g->priv->nodes[i];
 		if (n == NULL)
 			continue;
 		free(n->objs);
 		free(n->nodes);
 		free(n);
 	}
-	free(g->nodes);
-	free(g->inst_of);
-	free(g->pending);
+	free(g->priv->nodes);
+	free(g->priv->inst_of);
+	free(g->priv->pending);
+	free(g->priv);
 	free(g);
 }
 
 static int add_node(struct rte_graph *g, rte_node_t id) {
-	if (g->inst_of[id] >= 0)
+	if (g->priv->inst_of[id] >= 0)
 		return 0;
 	struct rte_node *n = calloc(1, sizeof(*n));
 	if (n == NULL)
 		return -ENOMEM;
-	g->inst_of[id] = (int32_t)g->n_nodes;
-	g->nodes[g->n_nodes++] = n;
+	g->priv->inst_of[id] = (int32_t)g->priv->n_nodes;
+	g->priv->nodes[g->priv->n_nodes++] = n;
 	const struct node_def *d = &defs[id];
 	snprintf(n->name, sizeof(n->name), "%s", d->name);
 	n->id = id;
@@ -170,16 +169,21 @@ rte_graph_t rte_graph_create(const char *name, struct rte_graph_param *prm) {
 	struct rte_graph *g = calloc(1, sizeof(*g));
 	if (g == NULL)
 		return RTE_GRAPH_ID_INVALID;
+	if ((g->priv = calloc(1, sizeof(*g->priv))) == NULL) {
+		free(g);
+		return RTE_GRAPH_ID_INVALID;
+	}
 	snprintf(g->name, sizeof(g->name), "%s", name);
 	g->id = id;
-	g->nodes = calloc(MAX_NODES, sizeof(*g->nodes));
-	g->inst_of = malloc(MAX_NODES * sizeof(*g->inst_of));
-	g->pend_cap = MAX_NODES + 1;
-	g->pending = calloc(g->pend_cap, sizeof(*g->pending));
-	if (g->nodes == NULL || g->inst_of == NULL || g->pending == NULL)
+	g->socket = prm->socket_id;
+	g->priv->nodes = calloc(MAX_NODES, sizeof(*g->priv->nodes));
+	g->priv->inst_of = malloc(MAX_NODES * sizeof(*g->priv->inst_of));
+	g->priv->pend_cap = MAX_NODES + 1;
+	g->priv->pending = calloc(g->priv->pend_cap, sizeof(*g->priv->pending));
+	if (g->priv->nodes == NULL || g->priv->inst_of == NULL || g->priv->pending == NULL)
 		goto fail;
 	for (uint32_t i = 0; i < MAX_NODES; i++)
-		g->inst_of[i] = -1;
+		g->priv->inst_of[i] = -1;
 	for (uint16_t p = 0; p < prm->nb_node_patterns; p++) {
 		int matched = 0;
 		for (rte_node_t i = 0; i < n_defs; i++) {
@@ -193,18 +197,18 @@ rte_graph_t rte_graph_create(const char *name, struct rte_graph_param *prm) {
 			goto fail; // DPDK: a pattern must select at least one node
 	}
 	// resolve edges to instances, then init
-	for (uint32_t i = 0; i < g->n_nodes; i++) {
-		struct rte_node *n = g->nodes[i];
+	for (uint32_t i = 0; i < g->priv->n_nodes; i++) {
+		struct rte_node *n = g->priv->nodes[i];
 		const struct node_def *d = &defs[n->id];
 		n->nb_edges = d->nb_edges;
 		n->nodes = calloc(d->nb_edges ? d->nb_edges : 1, sizeof(*n->nodes));
 		if (n->nodes == NULL)
 			goto fail;
 		for (rte_edge_t e = 0; e < d->nb_edges; e++)
-			n->nodes[e] = g->nodes[g->inst_of[rte_node_from_name(d->edges[e])]];
+			n->nodes[e] = g->priv->nodes[g->priv->inst_of[rte_node_from_name(d->edges[e])]];
 	}
-	for (uint32_t i = 0; i < g->n_nodes; i++) {
-		struct rte_node *n = g->nodes[i];
+	for (uint32_t i = 0; i < g->priv->n_nodes; i++) {
+		struct rte_node *n = g->priv->nodes[i];
 		if (defs[n->id].init != NULL && defs[n->id].init(g, n) < 0)
 			goto fail;
 	}
@@ -219,9 +223,9 @@ int rte_graph_destroy(rte_graph_t id) {
 	if (id >= MAX_GRAPHS || graphs[id] == NULL)
 		return -ENOENT;
 	struct rte_graph *g = graphs[id];
-	for (uint32_t i = 0; i < g->n_nodes; i++)
-		if (defs[g->nodes[i]->id].fini != NULL)
-			defs[g->nodes[i]->id].fini(g, g->nodes[i]);
+	for (uint32_t i = 0; i < g->priv->n_nodes; i++)
+		if (defs[g->priv->nodes[i]->id].fini != NULL)
+			defs[g->priv->nodes[i]->id].fini(g, g->priv->nodes[i]);
 	graphs[id] = NULL;
 	graph_free(g);
 	return 0;
@@ -237,17 +241,17 @@ struct rte_graph *rte_graph_lookup(const char *name) {
 struct rte_node *rte_graph_node_get_by_name(const char *graph, const char *name) {
 	struct rte_graph *g = rte_graph_lookup(graph);
 	rte_node_t id = rte_node_from_name(name);
-	if (g == NULL || id == RTE_NODE_ID_INVALID || g->inst_of[id] < 0)
+	if (g == NULL || id == RTE_NODE_ID_INVALID || g->priv->inst_of[id] < 0)
 		return NULL;
-	return g->nodes[g->inst_of[id]];
+	return g->priv->nodes[g->priv->inst_of[id]];
 }
 
 static void make_pending(struct rte_graph *g, struct rte_node *n) {
 	if (n->pending)
 		return;
 	n->pending = 1;
-	g->pending[g->pend_tail] = n;
-	g->pend_tail = (g->pend_tail + 1) % g->pend_cap;
+	g->priv->pending[g->priv->pend_tail] = n;
+	g->priv->pend_tail = (g->priv->pend_tail + 1) % g->priv->pend_cap;
 }
 
 static int grow(struct rte_node *n, uint32_t need) {
@@ -310,17 +314,17 @@ static void run(struct rte_graph *g, struct rte_node *n) {
 }
 
 void rte_graph_walk(struct rte_graph *g) {
-	for (uint32_t i = 0; i < g->n_nodes; i++) { // sources first
-		struct rte_node *n = g->nodes[i];
+	for (uint32_t i = 0; i < g->priv->n_nodes; i++) { // sources first
+		struct rte_node *n = g->priv->nodes[i];
 		if (defs[n->id].flags & RTE_NODE_SOURCE_F) {
 			uint16_t ret = n->process(g, n, NULL, 0);
 			n->total_calls++;
 			n->total_packets += ret;
 		}
 	}
-	while (g->pend_head != g->pend_tail) {
-		struct rte_node *n = g->pending[g->pend_head];
-		g->pend_head = (g->pend_head + 1) % g->pend_cap;
+	while (g->priv->pend_head != g->priv->pend_tail) {
+		struct rte_node *n = g->priv->pending[g->priv->pend_head];
+		g->priv->pend_head = (g->priv->pend_head + 1) % g->priv->pend_cap;
 		n->pending = 0;
 		if (n->idx)
 			run(g, n);

@@ -79,6 +79,45 @@ _Static_assert(sizeof(struct rte_mbuf) == 128, "rte_mbuf is two cache lines");
 static inline void *rte_mbuf_to_priv(struct rte_mbuf *m) {
 	return (char *)m + sizeof(struct rte_mbuf);
 }
+#define rte_pktmbuf_mtod_offset(m, t, o) ((t)((char *)(m)->buf_addr + (m)->data_off + (o)))
+
+// ---- lib/net (the headers the CPU continuation nodes read) -----------------
+typedef uint16_t rte_be16_t;
+typedef uint32_t rte_be32_t;
+#define RTE_BE16(v) ((rte_be16_t)((((v) & 0xffu) << 8) | (((v) >> 8) & 0xffu)))
+#define rte_be_to_cpu_16(v) RTE_BE16(v)
+#define rte_cpu_to_be_16(v) RTE_BE16(v)
+#define RTE_ETHER_TYPE_IPV4 0x0800
+#define RTE_IPV4_HDR_DF_FLAG (1 << 14)
+#define RTE_IPV4_HDR_OFFSET_MASK 0x1fff
+
+struct rte_ether_addr {
+	uint8_t addr_bytes[6];
+} __attribute__((aligned(2)));
+
+struct rte_ipv4_hdr {
+	uint8_t version_ihl;
+	uint8_t type_of_service;
+	rte_be16_t total_length;
+	rte_be16_t packet_id;
+	rte_be16_t fragment_offset;
+	uint8_t time_to_live;
+	uint8_t next_proto_id;
+	rte_be16_t hdr_checksum;
+	rte_be32_t src_addr;
+	rte_be32_t dst_addr;
+} __attribute__((packed));
+
+struct rte_udp_hdr {
+	rte_be16_t src_port;
+	rte_be16_t dst_port;
+	rte_be16_t dgram_len;
+	rte_be16_t dgram_cksum;
+} __attribute__((packed));
+
+static inline uint8_t rte_ipv4_hdr_len(const struct rte_ipv4_hdr *ip) {
+	return (uint8_t)((ip->version_ihl & 0xf) * 4);
+}
 
 // ---- rte_graph --------------------------------------------------------------
 #define RTE_GRAPH_BURST_SIZE 256
@@ -134,6 +173,17 @@ struct rte_graph_param {
 	int socket_id;
 	uint16_t nb_node_patterns;
 	const char **node_patterns;
+};
+
+// The fields of DPDK's struct rte_graph a node's init may read (the graph
+// of a grout worker is named "gr-%04x" after (cpu_id << 1) | index,
+// graph.c:118-119, and created on the worker's NUMA socket, :134-135).
+struct rte_graph_priv;
+struct rte_graph {
+	char name[RTE_GRAPH_NAMESIZE];
+	rte_graph_t id;
+	int socket;
+	struct rte_graph_priv *priv; // the stand-in runtime's own state
 };
 
 rte_node_t __rte_node_register(const struct rte_node_register *reg);

@@ -1,15 +1,20 @@
 // SPDX-License-Identifier: BSD-3-Clause
 //
-// walk_harness.c -- test harness (not the product): a graph around the fast
-// path's grout node, for tests/test_graph_walk.py.
+// walk_harness.c -- test harness (not the product): worker graphs around the
+// fast path's grout node, for tests/test_graph_walk.py.
 //
 //   port_rx (source, stand-in for port_rx.c:281-316: bursts of rx_burst
 //   mbufs from an injected array, iface / vlan_id in the private data)
-//     -> iface_input (gpu_fwd4_node.c) -> one recorder node per verdict edge
-//   gpu_fwd4_flush (source) -> the same recorder nodes
+//     -> iface_input (gpu_fwd4_node.c) -> grout's next nodes
+//   gpu_fwd4_flush (source) -> the same next nodes
 //
-// Recorder nodes stand in for grout's next nodes (ip_hold, port_output, the
-// drop nodes ...): they note which edge each mbuf arrived on, in order.
+// Every node of the graph carries a grout node name: the fast path's two
+// nodes, the two CPU continuation nodes (gpu_fwd4_cpu_nodes.c:
+// ip_input_local_ct, ip_output_snat), and recorders standing in for the rest
+// of grout's nodes under their own names (ip_hold, port_output, eth_output,
+// dnat44_dynamic, the drop nodes ... and iface_input_cpu, grout's iface_input
+// renamed by integration/grout-iface_input_cpu.patch). A recorder notes
+// which node each mbuf reached, in order, and keeps the mbuf.
 // mbufs are built like grout's pool (mempool.c:57-100): 128-byte rte_mbuf,
 // 64-byte private area, 2048-byte data room, frame at headroom 128.
 #include "gpu_fwd4_node.h"
@@ -22,6 +27,8 @@
 #define GH_PRIV 64
 #define GH_ROOM 2048
 #define GH_MBUF_SZ (sizeof(struct rte_mbuf) + GH_PRIV + GH_ROOM)
+#define GH_MAX_GRAPHS 8
+#define GH_MAX_RECORDERS 128
 
 struct gh_mbuf_out { // per injected mbuf, in injection order
 	uint32_t pkt_len;
@@ -30,12 +37,17 @@ struct gh_mbuf_out { // per injected mbuf, in injection order
 	uint32_t packet_type;
 	uint16_t iface; // mbuf_data(m)->iface->id (0 = NULL)
 	uint16_t vlan_id; // iface_mbuf_data(m)->vlan_id
-	uint8_t edge; // the recorder node it reached (edge index of iface_input), 0xff = none
+	uint8_t edge; // the recorder it reached (gh_recorder_name), 0xff = none
 	uint8_t domain; // eth_input_mbuf_data(m)->domain (low byte)
-	uint16_t _pad;
+	uint16_t conn; // conn_mbuf_data(m)->conn as a table index + 1 (0 = none)
 	uint32_t nh; // l3_mbuf_data(m)->nh->slot (0 = NULL)
 	uint32_t seq; // arrival order over all recorders
 	uint32_t eth_nh; // eth_input_mbuf_data(m)->nh->slot (0 = NULL)
+	uint8_t eth_dst[6]; // eth_output_mbuf_data(m)->dst
+	uint16_t eth_type; // eth_output_mbuf_data(m)->ether_type (as stored)
+	uint8_t vtep_af; // eth_output_mbuf_data(m)->vtep.af
+	uint8_t flow; // conn_mbuf_data(m)->flow
+	uint16_t _pad;
 };
 
 static struct {
@@ -48,13 +60,18 @@ static struct {
 	struct iface *ifaces;
 	struct nexthop *nhs;
 	uint32_t max_ifaces, max_nh;
-	rte_graph_t gid;
-	struct rte_graph *graph;
-	char name[RTE_GRAPH_NAMESIZE];
+	struct {
+		rte_graph_t gid;
+		struct rte_graph *graph;
+		char name[RTE_GRAPH_NAMESIZE];
+	} graphs[GH_MAX_GRAPHS];
+	int cur; // the graph gh_run / gh_results / stats use
+	char *recorders[GH_MAX_RECORDERS]; // recorder id -> node name
+	uint32_t n_recorders;
 	int inited;
 	int pin; // register the mbuf memory with the fast path (frames by address)
 	void *pinned; // what is registered now
-} H = {.gid = RTE_GRAPH_ID_INVALID, .pin = 1};
+} H = {.cur = -1, .pin = 1};
 
 // Whether gh_load registers its mbuf memory with gr_hip_host_register (grout:
 // the mempools' memory), so that the node hands frames over by address.
@@ -63,8 +80,8 @@ void gh_set_pin(int on) {
 }
 
 static void unpin(void) {
-	if (H.pinned != NULL && gpu_fwd4_hip_ctx() != NULL)
-		gr_hip_host_unregister(gpu_fwd4_hip_ctx(), H.pinned);
+	if (H.pinned != NULL && gpu_fwd4_n_ctx() != 0)
+		gpu_fwd4_host_unregister(H.pinned);
 	H.pinned = NULL;
 }
 
@@ -98,15 +115,15 @@ static struct rte_node_register port_rx_node = {
 	.next_nodes = {"iface_input"},
 };
 
-// a recorder's ctx holds the edge index it stands for
+// a recorder's ctx holds its recorder id
 static uint16_t recorder_process(struct rte_graph *graph, struct rte_node *node, void **objs, uint16_t nb) {
 	(void)graph;
-	const uint8_t edge = node->ctx[0];
+	const uint8_t id = node->ctx[0];
 	for (uint16_t k = 0; k < nb; k++) {
 		const size_t off = (uint8_t *)objs[k] - H.mem;
 		const uint32_t i = (uint32_t)(off / GH_MBUF_SZ);
 		if (i < H.n) {
-			H.edge_of[i] = edge;
+			H.edge_of[i] = id;
 			H.seq_of[i] = H.recorded++;
 		}
 	}
@@ -115,43 +132,59 @@ static uint16_t recorder_process(struct rte_graph *graph, struct rte_node *node,
 
 static int recorder_init(const struct rte_graph *graph, struct rte_node *node) {
 	(void)graph;
-	// the recorder for edge e is named after edge e of iface_input
-	rte_node_t fwd = rte_node_from_name("iface_input");
-	rte_edge_t n = rte_node_edge_count(fwd);
-	char **names = calloc(n, sizeof(char *));
-	if (names == NULL)
-		return -ENOMEM;
-	rte_node_edge_get(fwd, names);
 	node->ctx[0] = 0xff;
-	for (rte_edge_t e = 0; e < n; e++)
-		if (strcmp(names[e], node->name) == 0)
-			node->ctx[0] = (uint8_t)e;
-	free(names);
+	for (uint32_t r = 0; r < H.n_recorders; r++)
+		if (strcmp(H.recorders[r], node->name) == 0)
+			node->ctx[0] = (uint8_t)r;
 	return 0;
 }
 
-static int register_recorders(void) {
-	rte_node_t fwd = rte_node_from_name("iface_input");
-	if (fwd == RTE_NODE_ID_INVALID)
-		return -ENOENT;
-	rte_edge_t n = rte_node_edge_count(fwd);
-	char **names = calloc(n, sizeof(char *));
-	if (names == NULL)
+static int add_recorder(const char *name) {
+	if (rte_node_from_name(name) != RTE_NODE_ID_INVALID)
+		return 0;
+	if (H.n_recorders == GH_MAX_RECORDERS)
+		return -ENOSPC;
+	struct rte_node_register *r = calloc(1, sizeof(*r));
+	if (r == NULL)
 		return -ENOMEM;
-	rte_node_edge_get(fwd, names);
-	for (rte_edge_t e = 0; e < n; e++) {
-		if (rte_node_from_name(names[e]) != RTE_NODE_ID_INVALID)
-			continue;
-		struct rte_node_register *r = calloc(1, sizeof(*r));
-		if (r == NULL)
-			break;
-		snprintf(r->name, sizeof(r->name), "%s", names[e]);
-		r->process = recorder_process;
-		r->init = recorder_init;
-		if (__rte_node_register(r) == RTE_NODE_ID_INVALID)
-			break;
+	snprintf(r->name, sizeof(r->name), "%s", name);
+	r->process = recorder_process;
+	r->init = recorder_init;
+	if (__rte_node_register(r) == RTE_NODE_ID_INVALID)
+		return -EINVAL;
+	H.recorders[H.n_recorders++] = strdup(name);
+	return 0;
+}
+
+// Recorders for every next node no registered node provides, reachable from
+// the fast path's node: the ones named after its edges first (recorder id ==
+// edge), then those behind the CPU continuation nodes.
+static int register_recorders(void) {
+	const char *roots[] = {"iface_input", "ip_input_local_ct", "ip_output_snat"};
+	for (unsigned k = 0; k < sizeof(roots) / sizeof(roots[0]); k++) {
+		rte_node_t id = rte_node_from_name(roots[k]);
+		if (id == RTE_NODE_ID_INVALID)
+			return -ENOENT;
+		rte_edge_t n = rte_node_edge_count(id);
+		char **names = calloc(n, sizeof(char *));
+		if (names == NULL)
+			return -ENOMEM;
+		rte_node_edge_get(id, names);
+		for (rte_edge_t e = 0; e < n; e++) {
+			if (k == 0 && rte_node_from_name(names[e]) != RTE_NODE_ID_INVALID && H.n_recorders == e) {
+				// a real node at this edge (the CPU continuation nodes): keep
+				// recorder ids equal to edge ids with a placeholder
+				H.recorders[H.n_recorders++] = strdup(names[e]);
+				continue;
+			}
+			int r = add_recorder(names[e]);
+			if (r < 0) {
+				free(names);
+				return r;
+			}
+		}
+		free(names);
 	}
-	free(names);
 	return 0;
 }
 
@@ -170,11 +203,21 @@ int gh_register(void) {
 	return 0;
 }
 
-int gh_init(int dev, uint32_t max_ifaces, uint32_t max_nh, uint32_t batch, uint32_t rx_burst,
-	    uint64_t max_delay_ns) {
+const char *gh_recorder_name(uint32_t id) {
+	return id < H.n_recorders ? H.recorders[id] : NULL;
+}
+
+// devs[n_devs]: the GPUs the module opens (n_devs 0: all).
+int gh_init(const int *devs, uint32_t n_devs, uint32_t max_ifaces, uint32_t max_nh, uint32_t batch,
+	    uint32_t rx_burst, uint64_t max_delay_ns) {
 	if (H.inited)
 		return -EALREADY;
-	struct gpu_fwd4_conf c = {dev, max_ifaces, max_nh, batch, rx_burst, max_delay_ns};
+	struct gpu_fwd4_conf c = {.n_devs = n_devs, .max_ifaces = max_ifaces, .max_nexthops = max_nh,
+				  .batch = batch, .rx_burst = rx_burst, .max_delay_ns = max_delay_ns};
+	if (n_devs > GPU_FWD4_MAX_DEVS)
+		return -EINVAL;
+	for (uint32_t i = 0; i < n_devs; i++)
+		c.devs[i] = devs[i];
 	int r = gpu_fwd4_configure(&c);
 	if (r < 0)
 		return r;
@@ -198,31 +241,115 @@ int gh_init(int dev, uint32_t max_ifaces, uint32_t max_nh, uint32_t batch, uint3
 	if ((r = gr_modules_init(NULL)) < 0)
 		return r;
 	H.inited = 1;
-	return gpu_fwd4_hip_ctx() != NULL ? 0 : -ENODEV;
+	return gpu_fwd4_n_ctx() != 0 ? 0 : -ENODEV;
 }
 
 void *gh_hip_ctx(void) {
 	return gpu_fwd4_hip_ctx();
 }
 
-// The graph of one worker: what worker_graph_new would select.
-int gh_graph_create(const char *name) {
-	const char *patterns[] = {"port_rx", "gpu_fwd4_flush"};
-	struct rte_graph_param prm = {.socket_id = 0, .nb_node_patterns = 2, .node_patterns = patterns};
-	H.gid = rte_graph_create(name, &prm);
-	if (H.gid == RTE_GRAPH_ID_INVALID)
-		return -EINVAL;
-	H.graph = rte_graph_lookup(name);
-	snprintf(H.name, sizeof(H.name), "%s", name);
+void *gh_ctx_at(uint32_t i) {
+	return gpu_fwd4_ctx_at(i);
+}
+
+uint32_t gh_n_ctx(void) {
+	return gpu_fwd4_n_ctx();
+}
+
+// grout's control plane objects the CPU continuation nodes read (the type,
+// flags and L3 nexthop info the GPU mirrors hold as well).
+int gh_set_objects(const struct gr_hip_iface *ifs, uint32_t n_if, const struct gr_hip_nh *nhs, uint32_t first,
+		   uint32_t n_nh) {
+	if (H.ifaces == NULL)
+		return -ENODEV;
+	for (uint32_t k = 0; k < n_if; k++) {
+		const struct gr_hip_iface *s = &ifs[k];
+		if (s->id == 0 || s->id >= H.max_ifaces)
+			return -EINVAL;
+		struct iface *d = &H.ifaces[s->id];
+		d->type = s->type;
+		d->mode = s->mode;
+		d->flags = s->flags;
+		d->mtu = s->mtu;
+		d->vrf_id = s->vrf_id;
+	}
+	for (uint32_t k = 0; k < n_nh; k++) {
+		const uint32_t slot = first + k;
+		if (slot == 0 || slot > H.max_nh)
+			return -EINVAL;
+		const struct gr_hip_nh *s = &nhs[k];
+		struct nexthop *d = &H.nhs[slot];
+		d->type = s->type;
+		d->iface_id = s->iface_id;
+		d->vrf_id = s->vrf_id;
+		d->l3.state = s->state;
+		d->l3.flags = s->flags;
+		d->l3.af = s->af;
+		d->l3.ipv4 = s->ipv4;
+		memcpy(d->l3.ipv6, s->ipv6, 16);
+		memcpy(d->l3.mac.addr_bytes, s->mac, 6);
+	}
 	return 0;
 }
 
-int gh_graph_destroy(void) {
-	if (H.gid == RTE_GRAPH_ID_INVALID)
+// The conntrack / SNAT stand-ins' tables (gr_datapath_min.h).
+int gh_conn_add(const struct conn_key *fwd, const struct conn_key *rev) {
+	return gr_test_conn_add(fwd, rev, NULL);
+}
+
+int gh_snat44_static_add(uint16_t iface_id, uint32_t from, uint32_t to) {
+	return gr_test_snat44_static_add(iface_id, from, to);
+}
+
+void gh_policy_clear(void) {
+	gr_test_policy_clear();
+}
+
+// One worker's graph: what worker_graph_new selects (graph.c:93-145), named
+// after the worker's CPU like grout's ("gr-%04x", (cpu << 1) | index) and
+// created on `socket`. It becomes the current graph.
+int gh_graph_create(unsigned cpu, int socket) {
+	int k = 0;
+	while (k < GH_MAX_GRAPHS && H.graphs[k].graph != NULL)
+		k++;
+	if (k == GH_MAX_GRAPHS)
+		return -ENOSPC;
+	char name[RTE_GRAPH_NAMESIZE];
+	snprintf(name, sizeof(name), "gr-%04x", (cpu << 1) & 0xffff);
+	const char *patterns[] = {"port_rx", "gpu_fwd4_flush"};
+	struct rte_graph_param prm = {.socket_id = socket, .nb_node_patterns = 2, .node_patterns = patterns};
+	rte_graph_t gid = rte_graph_create(name, &prm);
+	if (gid == RTE_GRAPH_ID_INVALID)
+		return -EINVAL;
+	H.graphs[k].gid = gid;
+	H.graphs[k].graph = rte_graph_lookup(name);
+	snprintf(H.graphs[k].name, sizeof(H.graphs[k].name), "%s", name);
+	H.cur = k;
+	return k;
+}
+
+int gh_graph_use(int k) {
+	if (k < 0 || k >= GH_MAX_GRAPHS || H.graphs[k].graph == NULL)
 		return -ENOENT;
-	int r = rte_graph_destroy(H.gid);
-	H.gid = RTE_GRAPH_ID_INVALID;
-	H.graph = NULL;
+	H.cur = k;
+	return 0;
+}
+
+// The GPU context index the current graph's node runs on.
+int gh_graph_gpu(void) {
+	return H.cur >= 0 ? gpu_fwd4_graph_gpu(H.graphs[H.cur].graph) : -ENOENT;
+}
+
+static struct rte_graph *cur_graph(void) {
+	return H.cur >= 0 ? H.graphs[H.cur].graph : NULL;
+}
+
+int gh_graph_destroy(void) {
+	if (H.cur < 0 || H.graphs[H.cur].graph == NULL)
+		return -ENOENT;
+	int r = rte_graph_destroy(H.graphs[H.cur].gid);
+	H.graphs[H.cur].graph = NULL;
+	H.cur = -1;
 	return r;
 }
 
@@ -259,8 +386,8 @@ int gh_load(const uint8_t *frames, uint32_t stride, const struct gr_hip_pkt_meta
 	H.next_rx = 0;
 	H.recorded = 0;
 	H.meta_in = meta;
-	if (H.pin && n && gpu_fwd4_hip_ctx() != NULL) {
-		int r = gr_hip_host_register(gpu_fwd4_hip_ctx(), H.mem, (size_t)n * GH_MBUF_SZ);
+	if (H.pin && n && gpu_fwd4_n_ctx() != 0) {
+		int r = gpu_fwd4_host_register(H.mem, (size_t)n * GH_MBUF_SZ);
 		if (r < 0)
 			return r;
 		H.pinned = H.mem;
@@ -268,13 +395,14 @@ int gh_load(const uint8_t *frames, uint32_t stride, const struct gr_hip_pkt_meta
 	return 0;
 }
 
-// Walk until every injected mbuf reached a recorder, at most max_walks
-// times. Returns the number of walks, or -ETIMEDOUT.
+// Walk the current graph until every injected mbuf reached a recorder, at
+// most max_walks times. Returns the number of walks, or -ETIMEDOUT.
 int gh_run(uint32_t max_walks) {
-	if (H.graph == NULL)
+	struct rte_graph *g = cur_graph();
+	if (g == NULL)
 		return -ENOENT;
 	for (uint32_t w = 1; w <= max_walks; w++) {
-		rte_graph_walk(H.graph);
+		rte_graph_walk(g);
 		if (H.recorded == H.n && H.next_rx == H.n)
 			return (int)w;
 	}
@@ -300,6 +428,8 @@ static uint32_t iface_id_of(const struct iface *i) {
 	return (uint32_t)(i - H.ifaces);
 }
 
+uint32_t gr_test_conn_index(const struct conn *c); // gr_datapath_min.c
+
 int gh_results(struct gh_mbuf_out *out, uint8_t *lines) {
 	for (uint32_t i = 0; i < H.n; i++) {
 		struct rte_mbuf *m = mbuf_at(i);
@@ -316,6 +446,13 @@ int gh_results(struct gh_mbuf_out *out, uint8_t *lines) {
 		o->nh = slot_of(l3_mbuf_data(m)->nh);
 		o->eth_nh = slot_of(eth_input_mbuf_data(m)->nh);
 		o->seq = H.seq_of[i];
+		const struct eth_output_mbuf_data *e = eth_output_mbuf_data(m);
+		memcpy(o->eth_dst, e->dst.addr_bytes, 6);
+		o->eth_type = e->ether_type;
+		o->vtep_af = e->vtep.af;
+		const struct conn_mbuf_data *cd = conn_mbuf_data(m);
+		o->conn = (uint16_t)gr_test_conn_index(cd->conn);
+		o->flow = (uint8_t)cd->flow;
 		// the frame as port_rx delivered it: header line at the RX position
 		memcpy(lines + (size_t)i * GR_HIP_LINE, (uint8_t *)m->buf_addr + RTE_PKTMBUF_HEADROOM, GR_HIP_LINE);
 	}
@@ -323,16 +460,18 @@ int gh_results(struct gh_mbuf_out *out, uint8_t *lines) {
 }
 
 int gh_node_stats(struct gr_hip_node_stats *stats, uint64_t *gpu_errors) {
-	return H.graph ? gpu_fwd4_node_stats(H.graph, stats, gpu_errors) : -ENOENT;
+	struct rte_graph *g = cur_graph();
+	return g ? gpu_fwd4_node_stats(g, stats, gpu_errors) : -ENOENT;
 }
 
 int gh_queue_stats(struct gr_hip_iface_stats *stats, uint32_t max_ifaces, int reset) {
-	return H.graph ? gpu_fwd4_queue_stats(H.graph, stats, max_ifaces, reset) : -ENOENT;
+	struct rte_graph *g = cur_graph();
+	return g ? gpu_fwd4_queue_stats(g, stats, max_ifaces, reset) : -ENOENT;
 }
 
-// rte_graph's own counters of a node of the graph (objs, calls, packets).
+// rte_graph's own counters of a node of the current graph (objs, calls, packets).
 int gh_rte_node_counters(const char *node, uint64_t out[3]) {
-	struct rte_node *n = H.graph ? rte_graph_node_get_by_name(H.name, node) : NULL;
+	struct rte_node *n = H.cur >= 0 ? rte_graph_node_get_by_name(H.graphs[H.cur].name, node) : NULL;
 	if (n == NULL)
 		return -ENOENT;
 	out[0] = n->total_objs;
@@ -343,7 +482,13 @@ int gh_rte_node_counters(const char *node, uint64_t out[3]) {
 
 void gh_fini(void) {
 	unpin();
-	gh_graph_destroy();
+	for (int k = 0; k < GH_MAX_GRAPHS; k++) {
+		if (H.graphs[k].graph != NULL) {
+			rte_graph_destroy(H.graphs[k].gid);
+			H.graphs[k].graph = NULL;
+		}
+	}
+	H.cur = -1;
 	gr_modules_fini(NULL);
 	free(H.mem);
 	free(H.edge_of);

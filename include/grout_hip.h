@@ -348,6 +348,12 @@ typedef struct gr_hip_queue gr_hip_queue_t;
 
 // Library / device lifetime. dev = HIP device ordinal.
 int gr_hip_abi_version(void);
+// Visible HIP devices (-ENODEV without a GPU), and the NUMA node of a device
+// (from its PCI function in sysfs; 0 when the host reports none): the
+// grout node maps worker graphs to devices on their socket, as grout maps
+// RX queues to workers (modules/infra/control/worker.c:424-481).
+int gr_hip_device_count(void);
+int gr_hip_device_numa_node(int dev);
 int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, gr_hip_ctx_t **out);
 int gr_hip_fini(gr_hip_ctx_t *ctx);
 const char *gr_hip_strerror(int err);
@@ -362,6 +368,21 @@ int gr_hip_edges_iface_output_type(gr_hip_ctx_t *, uint8_t iface_type, uint8_t e
 int gr_hip_edges_ip6_input_nh_type(gr_hip_ctx_t *, uint8_t nh_type, uint8_t edge); // ip6_input.c:34
 int gr_hip_edges_ip6_output_nh_type(gr_hip_ctx_t *, uint8_t nh_type, uint8_t edge); // ip6_output.c:42
 int gr_hip_edges_ip6_output_iface_type(gr_hip_ctx_t *, uint8_t iface_type, uint8_t edge); // ip6_output.c:30
+// The edge registered for `key` in one of the tables above (a grout node
+// that continues a replaced node's work reads it, e.g. ip_output_snat):
+// an enum gr_hip_edge value, GR_HIP_EDGE_CHAIN or GR_HIP_EDGE_CHAIN6.
+enum {
+	GR_HIP_EDGES_ETH_TYPE = 0, // key: raw big-endian ether type
+	GR_HIP_EDGES_IFACE_MODE,
+	GR_HIP_EDGES_IP_INPUT_NH_TYPE,
+	GR_HIP_EDGES_IP_OUTPUT_NH_TYPE,
+	GR_HIP_EDGES_IP_OUTPUT_IFACE_TYPE,
+	GR_HIP_EDGES_IFACE_OUTPUT_TYPE,
+	GR_HIP_EDGES_IP6_INPUT_NH_TYPE,
+	GR_HIP_EDGES_IP6_OUTPUT_NH_TYPE,
+	GR_HIP_EDGES_IP6_OUTPUT_IFACE_TYPE,
+};
+int gr_hip_edges_get(gr_hip_ctx_t *, int table, uint16_t key);
 
 // Object mirrors. Changes become visible to submits issued after the call.
 int gr_hip_iface_set(gr_hip_ctx_t *, const struct gr_hip_iface *ifaces, uint32_t n);

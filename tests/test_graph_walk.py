@@ -28,9 +28,13 @@ from grout_amd import topology as T
 LIB = os.path.join(os.path.dirname(abi.LIB_HIP), "libgrout_graph.so")
 
 OUT_DT = np.dtype([("pkt_len", "<u4"), ("data_len", "<u2"), ("data_off", "<u2"), ("packet_type", "<u4"),
-                   ("iface", "<u2"), ("vlan_id", "<u2"), ("edge", "u1"), ("domain", "u1"), ("_pad", "<u2"),
-                   ("nh", "<u4"), ("seq", "<u4"), ("eth_nh", "<u4")])
-assert OUT_DT.itemsize == 32
+                   ("iface", "<u2"), ("vlan_id", "<u2"), ("edge", "u1"), ("domain", "u1"), ("conn", "<u2"),
+                   ("nh", "<u4"), ("seq", "<u4"), ("eth_nh", "<u4"), ("eth_dst", "u1", (6,)), ("eth_type", "<u2"),
+                   ("vtep_af", "u1"), ("flow", "u1"), ("_pad", "<u2")])
+assert OUT_DT.itemsize == 44
+CONN_KEY_DT = np.dtype([("iface_id", "<u2"), ("af", "u1"), ("proto", "u1"), ("src", ">u4"), ("dst", ">u4"),
+                        ("src_id", ">u2"), ("dst_id", ">u2")])
+assert CONN_KEY_DT.itemsize == 16
 
 _lib = None
 
@@ -40,22 +44,39 @@ def lib():
     if _lib is None:
         abi.hip()  # libgrout_hip.so first (torch's HIP runtime, abi.py)
         _lib = ctypes.CDLL(LIB)
-        _lib.gh_hip_ctx.restype = ctypes.c_void_p
-        _lib.gh_init.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
-                                 ctypes.c_uint64]
-        _lib.gh_graph_create.argtypes = [ctypes.c_char_p]
+        P, U32, U16 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint16
+        _lib.gh_hip_ctx.restype = P
+        _lib.gh_ctx_at.restype = P
+        _lib.gh_ctx_at.argtypes = [U32]
+        _lib.gh_n_ctx.restype = U32
+        _lib.gh_init.argtypes = [P, U32, U32, U32, U32, U32, ctypes.c_uint64]
+        _lib.gh_graph_create.argtypes = [ctypes.c_uint, ctypes.c_int]
+        _lib.gh_graph_use.argtypes = [ctypes.c_int]
+        _lib.gh_recorder_name.restype = ctypes.c_char_p
+        _lib.gh_recorder_name.argtypes = [U32]
         _lib.rte_node_from_name.argtypes = [ctypes.c_char_p]
-        _lib.rte_node_from_name.restype = ctypes.c_uint32
+        _lib.rte_node_from_name.restype = U32
+        _lib.rte_node_id_to_name.restype = ctypes.c_char_p
+        _lib.rte_node_id_to_name.argtypes = [U32]
+        _lib.rte_node_max_count.restype = U32
         _lib.rte_node_edge_count.restype = ctypes.c_uint16
         _lib.rte_node_edge_get.restype = ctypes.c_uint16
-        _lib.gh_rte_node_counters.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+        _lib.gh_rte_node_counters.argtypes = [ctypes.c_char_p, P]
         # pointers as c_void_p (a bare Python int would be passed as a C int)
-        _lib.gh_load.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
-        _lib.gh_run.argtypes = [ctypes.c_uint32]
-        _lib.gh_results.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-        _lib.gh_node_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-        _lib.gh_queue_stats.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int]
+        _lib.gh_load.argtypes = [P, U32, P, U32]
+        _lib.gh_run.argtypes = [U32]
+        _lib.gh_results.argtypes = [P, P]
+        _lib.gh_node_stats.argtypes = [P, P]
+        _lib.gh_queue_stats.argtypes = [P, U32, ctypes.c_int]
+        _lib.gh_set_objects.argtypes = [P, U32, P, U32, U32]
+        _lib.gh_conn_add.argtypes = [P, P]
+        _lib.gh_snat44_static_add.argtypes = [U16, U32, U32]
     return _lib
+
+
+def rec_name(i):
+    n = lib().gh_recorder_name(int(i))
+    return n.decode() if n else None
 
 
 def edges_of(name):
@@ -77,10 +98,51 @@ def test_runtime_semantics():
 def test_node_registration():
     L = lib()
     assert L.gh_register() == 0
-    want = ["iface_input_cpu"] + abi.EDGE_NAMES[1:]  # PUNT: grout's stock iface_input
+    want = ["iface_input_cpu"] + abi.EDGE_NAMES[1:]  # PUNT: grout's stock iface_input, renamed
     assert edges_of("iface_input") == want
     assert edges_of("gpu_fwd4_flush") == want
     assert edges_of("port_rx") == ["iface_input"]
+    # the CPU continuation nodes and where they go (ip_input.c:20-32, ip_output.c:21-30)
+    assert edges_of("ip_input_local_ct") == ["ip_input_local", "dnat44_dynamic"]
+    snat = edges_of("ip_output_snat")
+    assert snat[:abi.E_COUNT] == want and snat[abi.E_COUNT:] == ["eth_output", "ip_output_drop"]
+    # recorder ids of the fast path's edges are the edge values
+    assert [rec_name(e) for e in range(abi.E_COUNT)] == want
+
+
+def _reference_node_names():
+    import re
+    names = set()
+    for root, _, files in os.walk("/root/reference/modules"):
+        for f in files:
+            if f.endswith(".c"):
+                t = open(os.path.join(root, f), encoding="utf-8", errors="replace").read()
+                names |= set(re.findall(r'\.name = "([a-z0-9_]+)"', t))
+                names |= set(re.findall(r"GR_DROP_REGISTER\((\w+)\)", t))
+    names |= {"port_rx", "port_tx"}  # .name = RX_NODE_BASE / TX_NODE_BASE (rxtx.h:20-23)
+    return names
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/modules"), reason="reference not mounted")
+def test_graph_nodes_are_grouts():
+    """Every node the worker graph can hold is one of grout's, by name, or one
+    of the four this integration adds: the fast path's node (taking grout's
+    own "iface_input" name), its flush source, the two CPU continuation nodes
+    -- and "iface_input_cpu", grout's iface_input under the name
+    integration/grout-iface_input_cpu.patch gives it."""
+    L = lib()
+    assert L.gh_register() == 0
+    ours = {"gpu_fwd4_flush", "ip_input_local_ct", "ip_output_snat", "iface_input_cpu"}
+    ref = _reference_node_names()
+    names, todo = set(), ["port_rx", "gpu_fwd4_flush"]  # what a worker graph holds: reachable nodes
+    while todo:
+        n = todo.pop()
+        if n not in names:
+            names.add(n)
+            todo += edges_of(n)
+    assert "iface_input" in ref and "iface_input" in names
+    assert names - ref <= ours, sorted(names - ref - ours)
+    assert ours <= names
 
 
 def test_graph_refused_without_gpu_module():
@@ -90,7 +152,7 @@ def test_graph_refused_without_gpu_module():
     assert L.gh_register() == 0
     if L.gh_hip_ctx():
         pytest.skip("module already initialised in this process")
-    assert L.gh_graph_create(b"no_gpu") < 0
+    assert L.gh_graph_create(0, 0) < 0
 
 
 # ---------------------------------------------------------------------------
@@ -100,21 +162,60 @@ BATCH, BURST, DELAY_NS = 4096, 64, 2_000_000
 _gh = {}
 
 
-def graph_ctx():
-    """One node module (fast-path context) and one worker graph per process."""
-    from grout_amd.fwd import FastPath
+class _FanOut:
+    """libgrout_hip's gr_hip_* control calls, routed to the node module's
+    gpu_fwd4_* fan-out (every context), so FastPath.load drives them."""
+
+    def __init__(self, L):
+        self._L = L
+
+    def __getattr__(self, name):
+        fn = getattr(self._L, name.replace("gr_hip_", "gpu_fwd4_", 1))
+        res, args = abi.HIP_API[name]
+        fn.restype, fn.argtypes = res, args[1:]  # the same call without the context
+        return lambda _h, *a: fn(*a)
+
+
+class FanOutPath:
+    """A FastPath-shaped handle on all of the node module's contexts."""
+
+    def __init__(self, L, max_ifaces=1024, max_nexthops=1 << 17):
+        from grout_amd.fwd import FastPath
+        self.lib = _FanOut(L)
+        self.h = None
+        self.max_ifaces = max_ifaces
+        self.max_nexthops = max_nexthops
+        for k in ("set_ifaces", "del_iface", "set_nexthops", "set_reta", "fib_create", "fib_destroy", "route_add",
+                  "route_del", "fib_commit", "fib6_create", "fib6_destroy", "route6_add", "route6_del",
+                  "fib6_commit", "load", "tune"):
+            setattr(self, k, getattr(FastPath, k).__get__(self))
+
+
+DEVS = (0, 0)  # two fast-path contexts on the one GPU of the box: two "GPUs"
+
+
+def graph_ctx(devs=DEVS):
+    """One node module (one fast-path context per entry of devs) and one
+    worker graph (cpu 0, socket 0) per process; graph 0 is the current one."""
     L = lib()
-    if "fp" not in _gh:
-        r = L.gh_init(0, 1024, 1 << 17, BATCH, BURST, DELAY_NS)
+    if "fp" in _gh:
+        assert L.gh_graph_use(0) == 0
+    else:
+        d = (ctypes.c_int * len(devs))(*devs)
+        r = L.gh_init(ctypes.cast(d, ctypes.c_void_p), len(devs), 1024, 1 << 17, BATCH, BURST, DELAY_NS)
         assert r == 0, r
-        assert L.gh_graph_create(b"gh") == 0
-        _gh["fp"] = FastPath.borrow(L.gh_hip_ctx())
+        assert L.gh_graph_create(0, 0) == 0
+        _gh["fp"] = FanOutPath(L)
     return _gh["fp"]
 
 
 def load(fp, topo):
     from golden_util import fresh_fastpath_state
     fresh_fastpath_state(fp, topo, _gh.setdefault("state", {}))
+    L = lib()
+    ifs = np.ascontiguousarray(topo.ifaces[topo.ifaces["id"] != 0])
+    nh = np.ascontiguousarray(topo.nh[1:topo.n_nh + 1])
+    assert L.gh_set_objects(ifs.ctypes.data, len(ifs), nh.ctypes.data, 1, len(nh)) == 0
 
 
 def walk(frames, meta):
@@ -150,11 +251,18 @@ def check_walk(topo, fr, me, labels=None):
     o_lines, o_v, o_st, want, ns_want = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
     got, lines, ns, _ = walk(fr, me)
     lab = (lambda i: labels[i]) if labels else (lambda i: i)
+    # packets handed to a CPU continuation node (conntrack, SNAT) end further
+    # on: checked by test_graph_walk_cpu_continuations
+    cont = np.isin(want["edge"], [abi.EDGE["ip_input_local_ct"], abi.EDGE["ip_output_snat"]])
+    direct = ~cont
     for f in ["edge", "pkt_len", "data_len", "data_off", "packet_type", "iface"]:
-        bad = np.nonzero(got[f] != want[f])[0]
+        bad = np.nonzero((got[f] != want[f]) & direct)[0]
         assert len(bad) == 0, (f, [(lab(i), int(got[f][i]), int(want[f][i])) for i in bad[:6]])
-    bad = np.nonzero((lines != o_lines).any(axis=1))[0]
+    bad = np.nonzero((lines != o_lines).any(axis=1) & direct)[0]
     assert len(bad) == 0, [lab(i) for i in bad[:6]]
+    got, want, lines, o_lines, fr = got[direct], want[direct], lines[direct], o_lines[direct], fr[direct]
+    if labels:
+        labels = [x for x, d in zip(labels, direct) if d]
     # private data, as the node behind each edge reads it
     ip6 = (fr[:, 12] == 0x86) & (fr[:, 13] == 0xDD)
     st = stage_of(want["edge"], want["nh"], ip6)
@@ -185,8 +293,7 @@ def check_walk(topo, fr, me, labels=None):
     # every packet reached the recorder of its edge, counted by rte_graph
     for e in np.unique(got["edge"]):
         c = np.zeros(3, dtype=np.uint64)
-        name = "iface_input_cpu" if e == 0 else abi.EDGE_NAMES[e]
-        assert L.gh_rte_node_counters(name.encode(), c.ctypes.data) == 0
+        assert L.gh_rte_node_counters(rec_name(e).encode(), c.ctypes.data) == 0
         assert c[0] >= (got["edge"] == e).sum()
     return got
 
@@ -230,3 +337,104 @@ def test_graph_walk_flush_node():
     c = np.zeros(3, dtype=np.uint64)
     assert lib().gh_rte_node_counters(b"gpu_fwd4_flush", c.ctypes.data) == 0
     assert c[2] >= 2 * BURST  # the flush node handed those packets on
+
+
+@pytest.mark.gpu
+def test_graph_walk_two_gpus():
+    """grout's multi-worker, multi-GPU shape: the module opens one context
+    per configured GPU (here two on the box's one device), worker graphs bind
+    to them least-loaded on their NUMA socket, every control-plane change is
+    applied to all of them (gpu_fwd4_* fan-out), and each worker graph
+    forwards bit-exact on its own GPU."""
+    L = lib()
+    fp = graph_ctx()
+    assert L.gh_n_ctx() == len(DEVS)
+    assert L.gh_graph_use(0) == 0 and L.gh_graph_gpu() == 0
+    k = L.gh_graph_create(1, 0)  # a second worker, cpu 1
+    assert k == 1 and L.gh_graph_gpu() == 1
+    try:
+        t = T.config_fullview(count=50_000)
+        fr, me = S.stream(20_000, 0xB1E, routes=t.route_array())
+        for g in (0, 1):
+            assert L.gh_graph_use(g) == 0
+            got = check_walk(t, fr, me)
+            assert (got["edge"] == abi.EDGE["port_output"]).mean() > 0.99
+        # a route change reaches both contexts: a /32 of the stream moves
+        # to another nexthop, both workers forward it there
+        from grout_amd.fwd import FastPath
+        dst = int.from_bytes(bytes(fr[0, 30:34]), "big")
+        nh_new = int(t.route_array()["nh"][1])
+        r = np.zeros(1, dtype=abi.ROUTE_DT)
+        r[0] = (dst, 32, 0, 1, nh_new)
+        fp.route_add(r, replace=True)
+        fp.fib_commit(1)
+        for i in range(L.gh_n_ctx()):
+            h = FastPath.borrow(L.gh_ctx_at(i))
+            assert h.fib_lookup(1, dst) == nh_new
+        _gh["state"]["key"] = None  # the topology changed under fresh_fastpath_state: reload
+    finally:
+        assert L.gh_graph_use(1) == 0
+        assert L.gh_graph_destroy() == 0
+        L.gh_graph_use(0)
+
+
+@pytest.mark.gpu
+def test_graph_walk_cpu_continuations():
+    """The verdicts that stop at grout's conntrack / NAT hooks continue in
+    the CPU nodes ip_input_local_ct (ip_input.c:166-187) and ip_output_snat
+    (ip_output.c:108-153), in the graph, with grout's private data:
+    a conntrack hit reaches dnat44_dynamic with its connection, a miss
+    ip_input_local; a static SNAT rule rewrites the source (RFC 1624 checksum
+    update) and the packet reaches eth_output with eth_output_mbuf_data set."""
+    L = lib()
+    fp = graph_ctx()
+    t, nh = SC.corpus_topology()
+    load(fp, t)
+    fr, me, lab = SC.corpus_arrays()
+    pick = [lab.index(x) for x in ("snat dyn local", "snat egress", "fwd 16.1.0.1")]
+    fr, me = np.ascontiguousarray(fr[pick * 3]), np.ascontiguousarray(me[pick * 3])
+    L.gh_policy_clear()
+    # the local packet's flow, seen from the NATed side: a conntrack REV hit
+    f = fr[0]
+    ihl = (f[14] & 0xF) * 4
+    key = np.zeros(2, dtype=CONN_KEY_DT)
+    key[1] = (SC.SNATDYN, abi.AF_IP4, f[23], int.from_bytes(bytes(f[26:30]), "big"),
+              int.from_bytes(bytes(f[30:34]), "big"), int.from_bytes(bytes(f[14 + ihl:16 + ihl]), "big"),
+              int.from_bytes(bytes(f[16 + ihl:18 + ihl]), "big"))
+    key[0] = key[1]
+    key[0]["src"], key[0]["dst"] = key[1]["dst"], key[1]["src"]
+    assert L.gh_conn_add(key[0:1].ctypes.data, key[1:2].ctypes.data) == 0
+    src_be = bytes(fr[1, 26:30])
+    to = bytes([100, 64, 99, 1])
+    assert L.gh_snat44_static_add(SC.P3, int.from_bytes(src_be, "little"), int.from_bytes(to, "little")) == 0
+    o_lines, o_v, _, want, _ = oracle.Oracle(t).process_mbufs(fr, me, lines_only=True)
+    got, lines, _, _ = walk(fr, me)
+    names = [rec_name(e) for e in got["edge"]]
+    assert names == ["dnat44_dynamic", "eth_output", "port_output"] * 3
+    # conntrack hit: the connection and its direction in conn_mbuf_data
+    assert (got["conn"][0::3] == 1).all() and (got["flow"][0::3] == 1).all()  # CONN_FLOW_REV
+    assert (got["data_off"][0::3] == want["data_off"][0::3]).all()  # after eth_input's adj
+    # SNAT: the source rewritten, the header checksum still verifies, the rest
+    # of the header as the GPU left it (TTL, the fast path's checksum update)
+    s = lines[1::3]
+    o = o_lines[1::3]
+    assert (s[:, 26:30] == np.frombuffer(to, np.uint8)).all()
+    for row in s:
+        hdr = bytes(row[14:34])
+        tot = sum(int.from_bytes(hdr[i:i + 2], "big") for i in range(0, 20, 2))
+        while tot >> 16:
+            tot = (tot & 0xFFFF) + (tot >> 16)
+        assert tot == 0xFFFF
+    assert (s[:, :24] == o[:, :24]).all() and (s[:, 30:] == o[:, 30:]).all()
+    # eth_output_mbuf_data: the nexthop's MAC, IPv4, no vtep
+    assert (got["eth_dst"][1::3] == np.frombuffer(T.mac_bytes("02:00:00:01:00:15"), np.uint8)).all()
+    assert (got["eth_type"][1::3] == 0x0008).all() and (got["vtep_af"][1::3] == 0).all()
+    assert (got["iface"][1::3] == SC.P3).all() and (got["packet_type"][1::3] == abi.PTYPE_L3_IPV4).all()
+    # ip_output's return rule: the SNAT node counted what it sent to eth_output
+    c = np.zeros(3, dtype=np.uint64)
+    assert L.gh_rte_node_counters(b"ip_output_snat", c.ctypes.data) == 0 and c[2] >= 3
+    # no conntrack entry, no rule: ip_input_local, eth_output with the source kept
+    L.gh_policy_clear()
+    got, lines, _, _ = walk(fr, me)
+    assert [rec_name(e) for e in got["edge"]] == ["ip_input_local", "eth_output", "port_output"] * 3
+    assert (lines[1::3] == o_lines[1::3]).all()
