@@ -46,6 +46,8 @@ def parse():
                    help="calibrated: batch buffers from gr_hip_batch_alloc, output lines re-placed by gr_hip_batch_place over "
                         "--candidates allocations; plain: torch allocations")
     p.add_argument("--candidates", type=int, default=6)
+    p.add_argument("--no-plain", action="store_true",
+                   help="skip the same measurement on plain torch allocations (value_plain_placement)")
     p.add_argument("--time-every", type=int, default=4,
                    help="HIP events around every N-th launch only (the kernel time is their average; "
                         "each event pair costs ~7 us of stream time)")
@@ -83,9 +85,10 @@ def main():
         routes, dst_range = None, (T.ip4("16.1.0.0"), T.ip4("16.1.255.255"))
         workload = "config2: 64B synthetic burst, 1-route FIB"
     elif args.workload == "fullview6":
-        topo = T.config_fullview6(200_000)
+        topo = T.config_fullview6()
         routes, dst_range = None, None
-        workload = "IPv6: 64B synthetic burst, 200k-route IPv6 view (2000::/3, /16../64 mix)"
+        workload = ("IPv6: 64B synthetic burst, 200k-route IPv6 full view (fib_inject -6, "
+                    "smoke/fib6_fullview_manualtest.sh sizing)")
     else:
         topo = T.config_fullview()
         routes, dst_range = topo.route_array(), None
@@ -104,25 +107,36 @@ def main():
     imix = args.workload == "imix"
     in_stride = args.slot if args.workload == "imix_frames" else abi.LINE
     t0 = time.time()
-    if args.workload == "fullview6":
-        r6 = topo.route6_array()
-        frames, meta = S.stream6(n, seed, r6[r6["prefixlen"] < 128])
-    else:
-        frames, meta = S.stream(n, seed, routes=routes, dst_range=dst_range, imix=imix or in_stride > abi.LINE,
-                                lines_only=imix, stride=in_stride)
+
+    def make_stream(s):
+        if args.workload == "fullview6":
+            r6 = topo.route6_array()
+            return S.stream6(n, s, r6[r6["prefixlen"] < 128])
+        return S.stream(n, s, routes=routes, dst_range=dst_range, imix=imix or in_stride > abi.LINE,
+                        lines_only=imix, stride=in_stride)
+
+    def h2d(dst, src):
+        src = np.ascontiguousarray(src)
+        abi.check("gr_hip_memcpy_h2d", fp.lib.gr_hip_memcpy_h2d(fp.h, dst, src.ctypes.data, src.nbytes))
+
+    frames, meta = make_stream(seed)
     batch = None
     if args.placement == "calibrated":
         # gr_hip_batch_alloc + gr_hip_batch_place: the output lines' pages are
-        # picked among --candidates allocations by timing them over this batch
-        # 
+        # picked among --candidates allocations by timing them over a batch of
+        # the same workload drawn with ANOTHER seed; the
+        # measured stream is then loaded into the placed buffers
         batch = fp.batch_alloc(n, in_stride)
-        for dst, src in ((batch.in_frames, frames), (batch.meta, meta)):
-            src = np.ascontiguousarray(src)
-            abi.check("gr_hip_memcpy_h2d", fp.lib.gr_hip_memcpy_h2d(fp.h, dst, src.ctypes.data, src.nbytes))
+        cf, cm = make_stream(seed ^ 0xCA11B)
+        h2d(batch.in_frames, cf)
+        h2d(batch.meta, cm)
+        del cf, cm
         if imix:
             batch.flags = abi.BATCH_F_LINES_ONLY
         fp.batch_place(batch, args.candidates)
         batch.flags = 0
+        h2d(batch.in_frames, frames)
+        h2d(batch.meta, meta)
         d_in, d_out, d_meta, d_v = batch.in_frames, batch.out_lines, batch.meta, batch.verdicts
     else:
         d_in = torch.from_numpy(frames.reshape(-1)).to(dev)
@@ -134,26 +148,37 @@ def main():
 
     q = fp.queue(shared_stream(dev))
     every = max(1, min(args.time_every, args.steps))
-    fp.tune("time_every", every)  # the queue's submits 0, every, 2 * every ... carry events
 
-    def step():
-        q.submit(d_in, d_out, d_meta, d_v, n, in_stride=in_stride, out_stride=abi.LINE, lines_only=imix)
+    def measure(bufs, steps, warmup):
+        """warmup + steps launches on `bufs`; -> (max-over-ranks seconds of the
+        timed steps, kernel ms summed over the timed launches, their count)."""
+        d_in_, d_out_, d_meta_, d_v_ = bufs
+        fp.tune("time_every", every)  # every `every`-th submit of the queue carries events
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    rep.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    rep.barrier()
-    elapsed = time.perf_counter() - t0
-    n_timed = sum(1 for i in range(args.warmup, args.warmup + args.steps) if i % every == 0)
-    kern_ms, kcount = q.kernel_ms(n_timed)
-    fp.tune("time_every", 1)
-    tmax = rep.max_over_ranks(elapsed)
+        def step():
+            q.submit(d_in_, d_out_, d_meta_, d_v_, n, in_stride=in_stride, out_stride=abi.LINE, lines_only=imix)
+
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        q.sync()  # raises if a kernel gave up a ring wait (-ETIMEDOUT)
+        rep.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        rep.barrier()
+        el = time.perf_counter() - t0
+        q.sync()
+        # setting time_every restarted the queue's count: submits 0, every,
+        # 2 * every ... of warmup + steps carried events
+        timed = sum(1 for i in range(warmup, warmup + steps) if i % every == 0)
+        ms, cnt = q.kernel_ms(timed)
+        fp.tune("time_every", 1)
+        return rep.max_over_ranks(el), ms, cnt
+
+    tmax, kern_ms, kcount = measure((d_in, d_out, d_meta, d_v), args.steps, args.warmup)
 
     if batch is not None:
         vh = np.empty(n, dtype=abi.VERDICT_DT)
@@ -172,15 +197,35 @@ def main():
     B_PKT = b_pkt(entry)
     achieved = n * B_PKT / avg_kernel_s / 1e9
 
-    traffic = None
+    # HBM bytes per launch from PMC counters cannot be read from inside this
+    # process: they come from separate rocprofv3 --pmc passes of the same
+    # workload (tools/pmc_traffic.py), named with the file and run they came from
+    traffic, traffic_src = None, None
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
         try:
             pm = json.load(open(tf))
-            if pm.get("workload") == args.workload and pm.get("batch") == n and pm.get("bytes_per_pkt") == B_PKT:
-                traffic = pm.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+            for e in pm if isinstance(pm, list) else [pm]:
+                if e.get("workload") == args.workload and e.get("batch") == n and e.get("bytes_per_pkt") == B_PKT:
+                    traffic = e.get("hbm_bytes_per_launch")
+                    traffic_src = f"profiles/pmc_traffic.json <- {e.get('source', '?')}"
+        except (OSError, ValueError, AttributeError):
+            traffic, traffic_src = None, None
+
+    # the same measurement on plain torch allocations of the same stream:
+    # the placement's share of `value`, in the same run
+    plain = None
+    if batch is not None and not args.no_plain:
+        p_in = torch.from_numpy(frames.reshape(-1)).to(dev)
+        p_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
+        p_out = torch.empty(n * abi.LINE, dtype=torch.uint8, device=dev)
+        p_v = torch.empty(n * 8, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        pt, pms, pcnt = measure((p_in, p_out, p_meta, p_v), args.steps, args.warmup)
+        plain = {"value": round(rep.aggregate_mpps(n, args.steps, pt), 1),
+                 "ms_per_step": round(pt / args.steps * 1e3, 4),
+                 "kernel_ms_avg": round(pms / max(pcnt, 1), 4)}
+        del p_in, p_meta, p_out, p_v
 
     result = {
         "metric": "Mpps IPv4 forward, 64B pkts, ~1M-route FIB (device-resident), 1/8 GPU",
@@ -213,11 +258,15 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "bytes_per_pkt": B_PKT,
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),
             "kernel_launches_timed": kcount,
         },
     }
+    if plain is not None:
+        result["value_plain_placement"] = plain["value"]
+        result["plain_placement"] = plain
     if args.workload == "fullview6":
         result["metric"] = "Mpps IPv6 forward, 64B pkts, 200k-route IPv6 view (device-resident) [non-headline]"
     elif args.workload != "fullview64":

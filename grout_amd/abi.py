@@ -193,6 +193,7 @@ HIP_API = {
 HOST_API = {
     "gr_synth_splitmix64": (_U64, [ctypes.POINTER(_U64)]),
     "gr_synth_fullview_routes": (_I, [_U32, _U16, _U32, _U32, _P]),
+    "gr_synth_fullview6_routes": (_I, [_U32, _U16, _U32, _U32, _P]),
     "gr_synth_packets": (_I, [ctypes.POINTER(SynthStream), _U32, _U32, _I, _P, _P]),
     "gr_synth_ip4_cksum": (_U16, [_P, _U32]),
     "gr_fib4_new": (_P, [_U32, _U32]),

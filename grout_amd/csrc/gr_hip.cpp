@@ -109,6 +109,7 @@ struct gr_hip_queue {
 	hipEvent_t ev0[N_TIMED], ev1[N_TIMED];
 	uint64_t n_launch; // timed launches
 	uint64_t n_submit; // submits that could be timed (time_every sampling)
+	bool always_timed; // every launch carries events, whatever the knobs (gr_hip_batch_place's probes)
 	hipEvent_t quiesce;
 	gr_hip_iface_stats *d_stats; // [FWD4_STAT_SHARDS][max_ifaces]
 	host_slot hs[HOST_SLOTS];
@@ -1545,7 +1546,11 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	else if (c->tile_order == 2)
 		A.order = 0;
 	// every `time_every`-th submit of the queue carries the event pair
-	timed = timed && !c->untimed && (c->time_every <= 1 || q->n_submit++ % c->time_every == 0);
+	// (counted over every submit that could be timed, whatever the knobs)
+	if (timed && !q->always_timed) {
+		const uint64_t k = q->n_submit++;
+		timed = !c->untimed && (c->time_every <= 1 || k % c->time_every == 0);
+	}
 	if (timed)
 		HCK(hipEventRecord(q->ev0[slot], s));
 	HCK(gr_fwd4_ring_launch(&A, grid, s, variant, c->ring_cfg));
@@ -1580,6 +1585,8 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < 0 || value > 1024)
 			return -EINVAL;
 		c->time_every = (uint32_t)value;
+		for (gr_hip_queue *q : c->queues) // the sampling restarts: submits 0, N, 2N ... from now
+			q->n_submit = 0;
 	} else if (strcmp(key, "spin_max") == 0) { // tests: make ring waits give up early
 		if (value < 0)
 			return -EINVAL;
@@ -2036,6 +2043,7 @@ extern "C" int gr_hip_batch_place(gr_hip_ctx_t *c, gr_hip_batch *b, uint32_t can
 		hipStreamSynchronize(q->s);
 		hipFree(q->d_stats);
 		q->d_stats = nullptr;
+		q->always_timed = true; // "untimed" / "time_every" do not apply to the probes
 		float best = 0;
 		for (size_t k = 0; k < outs.size() && r == 0; k++) {
 			gr_hip_batch t = *b;
@@ -2046,6 +2054,8 @@ extern "C" int gr_hip_batch_place(gr_hip_ctx_t *c, gr_hip_batch *b, uint32_t can
 			uint32_t cnt = 0;
 			if (r == 0)
 				r = gr_hip_queue_kernel_ms(q, 4, &ms, &cnt);
+			if (r == 0 && cnt != 4)
+				r = -EIO; // the probes must all be timed
 			if (r == 0 && (k == 0 || ms < best)) {
 				best = ms;
 				pick = k;

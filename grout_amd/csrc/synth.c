@@ -56,6 +56,60 @@ int gr_synth_fullview_routes(
 	return 0;
 }
 
+// ipv6_dist, smoke/fib_inject.c:38-47 (parts per thousand, in table order:
+// the bucket index also picks the route's /8 base)
+static const struct {
+	uint8_t len;
+	uint16_t weight;
+} dist6[] = {
+	{32, 130}, {36, 40}, {40, 95}, {44, 105}, {48, 500}, {128, 10}, {46, 50}, {42, 40}, {38, 30},
+};
+#define N_DIST6 (sizeof(dist6) / sizeof(dist6[0]))
+
+// fib_inject -6 -n count (inject_ipv6, fib_inject.c:136-179): route i takes
+// the bucket pick_prefix gives index i (round robin over i % 1000), the /8
+// base 0x20 + bucket, and its per-bucket sequence number + 1 placed after
+// the /8 as the reference computes it.
+int gr_synth_fullview6_routes(
+	uint32_t count,
+	uint16_t vrf_id,
+	uint32_t nh_base,
+	uint32_t n_nh,
+	struct gr_hip_route6 *out
+) {
+	if (n_nh == 0 || nh_base == 0)
+		return -EINVAL;
+	uint32_t seq[N_DIST6] = {0};
+	for (uint32_t i = 0; i < count; i++) {
+		uint32_t slot = i % 1000, cum = 0; // pick_prefix, fib_inject.c:53-79
+		unsigned b = N_DIST6 - 1;
+		for (unsigned k = 0; k < N_DIST6; k++) {
+			cum += dist6[k].weight;
+			if (slot < cum) {
+				b = k;
+				break;
+			}
+		}
+		const uint8_t len = dist6[b].len;
+		const uint32_t v = seq[b]++ + 1; // fib_inject.c:145,159
+		struct gr_hip_route6 *r = &out[i];
+		memset(r, 0, sizeof(*r));
+		r->ip[0] = (uint8_t)(0x20 + b); // :152-153
+		const unsigned net_bits = len > 8 ? len - 8u : 1u; // :160
+		const unsigned bit_offset = net_bits > 32 ? net_bits - 32 : 0; // :163
+		const uint32_t shifted = v << (32 - net_bits + bit_offset); // :164
+		const unsigned start = bit_offset / 8; // :165
+		r->ip[1 + start] = (uint8_t)(shifted >> 24); // :166-169
+		r->ip[2 + start] = (uint8_t)(shifted >> 16);
+		r->ip[3 + start] = (uint8_t)(shifted >> 8);
+		r->ip[4 + start] = (uint8_t)shifted;
+		r->prefixlen = len;
+		r->vrf_id = vrf_id;
+		r->nh = nh_base + (i % n_nh); // :170
+	}
+	return 0;
+}
+
 uint16_t gr_synth_ip4_cksum(const uint8_t *ip, uint32_t hl) {
 	uint32_t sum = 0;
 	for (uint32_t i = 0; i < hl; i += 2) {

@@ -27,6 +27,17 @@ int gr_synth_fullview_routes(
 	struct gr_hip_route4 *out
 );
 
+// fib_inject -6 -n count (smoke/fib_inject.c:38-47,53-79,136-179): the IPv6
+// full view of smoke/fib6_fullview_manualtest.sh (200,000 routes), route i
+// -> nexthop nh_base + i % n_nh.
+int gr_synth_fullview6_routes(
+	uint32_t count,
+	uint16_t vrf_id,
+	uint32_t nh_base,
+	uint32_t n_nh,
+	struct gr_hip_route6 *out
+);
+
 enum {
 	GR_SYNTH_DST_RANGE = 0, // dst uniform in [dst_lo, dst_hi] (host order)
 	GR_SYNTH_DST_ROUTES = 1, // pick a route uniformly, random host bits

@@ -18,6 +18,8 @@ routes exactly as grout's control plane would leave them for the datapath:
   IPv6 nexthop address makes an AF_IP6 nexthop; add_address6 mirrors
   addr6_add (modules/ip6/control/address.c) and add_route6
   gr_ip6_route_add_req, a link-local prefix scoped to its iface.
+* config_fullview / config_fullview6: fib_inject -4 / -6's route sets
+  (smoke/fib_inject.c), ported in csrc/synth.c.
 
 The same arrays feed the HIP library (grout_amd.fwd) and the test oracle.
 """
@@ -274,16 +276,12 @@ def config_fullview(count=1_000_000):
     return t
 
 
-# IPv6 view: the prefix-length mix of a global IPv6 table (most routes /48,
-# then /32, /44, /40, /36, /29 ...) drawn deterministically, over 512
-# REACHABLE IPv6 nexthops. No reference script generates one (fib_inject
-# is IPv4 only), so this is a synthetic stand-in with the
-# same LPM structure (nested prefixes, every trie level populated).
-N_FULLVIEW6_NH = 512
-SEED_FULLVIEW6 = 0x67720006
-V6_LEN_MIX = [(48, 0.46), (32, 0.12), (44, 0.10), (40, 0.07), (36, 0.05), (29, 0.04), (47, 0.03),
-              (46, 0.03), (45, 0.02), (56, 0.02), (64, 0.02), (24, 0.01), (28, 0.01), (128, 0.01),
-              (20, 0.004), (60, 0.006)]
+# IPv6 full view: exactly fib_inject -6's route set (smoke/fib_inject.c:
+# 38-47,136-179; smoke/fib6_fullview_manualtest.sh injects 200,000), over
+# the same 2048 nexthops as the IPv4 view, made REACHABLE IPv6 nexthops
+# instead of fib_inject's blackholes so that packets forward.
+N_FULLVIEW6_NH = 2048
+FULLVIEW6_ROUTES = 200_000
 
 
 def fullview6_nexthops(t, n_nh=N_FULLVIEW6_NH):
@@ -296,32 +294,16 @@ def fullview6_nexthops(t, n_nh=N_FULLVIEW6_NH):
     return first
 
 
-def fullview6_routes(count, vrf_id, first_nh, n_nh, seed=SEED_FULLVIEW6):
-    """`count` distinct prefixes in 2000::/3 with the V6_LEN_MIX lengths,
-    route i -> nexthop first_nh + i % n_nh."""
-    rng = np.random.default_rng(seed)
-    lens = np.array([l for l, _ in V6_LEN_MIX])
-    p = np.array([w for _, w in V6_LEN_MIX])
-    want = rng.choice(lens, size=count * 2, p=p / p.sum())
-    addr = rng.integers(0, 256, size=(count * 2, 16), dtype=np.uint8)
-    addr[:, 0] = 0x20 | (addr[:, 0] & 0x1F)  # 2000::/3
-    addr[:, 1] = addr[:, 1] & 0x0F  # a denser top level, like the real table
-    bits = np.arange(16)[None, :] * 8
-    mask = (0xFF00 >> np.clip(want[:, None] - bits, 0, 8)).astype(np.uint8)
-    addr &= mask
-    _, idx = np.unique(np.concatenate([addr, want[:, None].astype(np.uint8)], axis=1), axis=0,
-                       return_index=True)
-    idx = np.sort(idx)[:count]
-    r = np.zeros(len(idx), dtype=abi.ROUTE6_DT)
-    r["ip"] = addr[idx]
-    r["prefixlen"] = want[idx]
-    r["vrf_id"] = vrf_id
-    r["nh"] = first_nh + np.arange(len(idx)) % n_nh
+def fullview6_routes(count, vrf_id, first_nh, n_nh):
+    """fib_inject -6 -n count: route i -> nexthop first_nh + i % n_nh."""
+    r = np.zeros(count, dtype=abi.ROUTE6_DT)
+    abi.check("gr_synth_fullview6_routes",
+              abi.host().gr_synth_fullview6_routes(count, vrf_id, first_nh, n_nh, r.ctypes.data))
     return r
 
 
-def config_fullview6(count=100_000):
-    """An IPv6 view of `count` routes over 512 nexthops (the IPv6 workload)."""
+def config_fullview6(count=FULLVIEW6_ROUTES):
+    """fib_inject -6 -n count over 2048 REACHABLE IPv6 nexthops (the IPv6 workload)."""
     t = base_ports(max_routes=1 << 10)
     t.fibs6[VRF_MAIN] = (count + 10, max(1 << 16, 4 * count))  # ~3-4 trie groups per deep route
     first = fullview6_nexthops(t)

@@ -455,7 +455,9 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               address (default), 0 = always stage header lines
 //   "time_every" N: only every N-th submit of a queue gets the HIP event
 //               pair that gr_hip_queue_kernel_ms reads (default 1: all);
-//               each pair costs ~7 us of stream time per launch
+//               each pair costs ~7 us of stream time per launch. Setting
+//               it restarts every queue's count: its submits 0, N, 2N ...
+//               from then on are timed
 //   "untimed"   1 = no events at all
 //   "spin_max"  polls before a ring wait gives up (0 = default, ~0.4 s):
 //               for tests of the give-up path

@@ -10,7 +10,8 @@ reference's own ip_input known answers and hand-derived cases). Fixtures:
   single.npz     config 2 stream, 2048 x 64 B
   fullview.npz   config 3 stream over the 1M-route view, 4096 x 64 B
   imix.npz       config 4 stream (IMIX), 512 packets, header lines only
-  fullview6.npz  IPv6 stream over a 20k-route IPv6 view, 4096 x 64 B
+  fullview6.npz  IPv6 stream over fib_inject -6's 200k-route view, 4096 x 64 B
+  eth_cache.npz  graph walks through eth_output's source-MAC cache (corpus topology)
 """
 import hashlib
 import os
@@ -63,9 +64,13 @@ def main():
     fr, me = S.stream(512, S.SEED_IMIX, routes=t.route_array(), imix=True, lines_only=True)
     save("imix.npz", t, fr, me, lines_only=True)
 
-    t = T.config_fullview6(count=20_000)
+    t = T.config_fullview6()
     fr, me = S.stream6(4096, S.SEED_FULLVIEW6, t.route6_array())
     save("fullview6.npz", t, fr, me)
+
+    t, _ = SC.corpus_topology()
+    frames, meta, labels, _ = SC.eth_output_cache_arrays()
+    save("eth_cache.npz", t, frames, meta, labels)
 
 
 if __name__ == "__main__":

@@ -23,11 +23,11 @@ def _fullview():
 
 @functools.lru_cache(maxsize=None)
 def _fullview6():
-    return T.config_fullview6(count=20_000)
+    return T.config_fullview6()
 
 
 def topo_for(name):
-    if name == "corpus":
+    if name in ("corpus", "eth_cache"):
         return SC.corpus_topology()[0]
     if name == "single":
         return T.config_single_route()

@@ -14,13 +14,13 @@ from golden_util import GOLDEN, topo_for, load, run_gpu
 from golden.make_golden import digest
 
 
-@pytest.mark.parametrize("name", ["corpus", "single", "fullview", "imix", "fullview6"])
+@pytest.mark.parametrize("name", ["corpus", "single", "fullview", "imix", "fullview6", "eth_cache"])
 def test_topology_unchanged(name):
     g = load(name)
     assert digest(topo_for(name)) == str(g["topo_sha256"])
 
 
-@pytest.mark.parametrize("name", ["corpus", "single", "fullview", "imix", "fullview6"])
+@pytest.mark.parametrize("name", ["corpus", "single", "fullview", "imix", "fullview6", "eth_cache"])
 def test_oracle_reproduces_golden(name):
     g = load(name)
     out, v, st = oracle.Oracle(topo_for(name)).process(g["frames"], g["meta"], lines_only=bool(g["lines_only"]))
@@ -30,7 +30,7 @@ def test_oracle_reproduces_golden(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["corpus", "single", "fullview", "imix", "fullview6"])
+@pytest.mark.parametrize("name", ["corpus", "single", "fullview", "imix", "fullview6", "eth_cache"])
 def test_gpu_matches_golden(fastpath, name):
     g = load(name)
     out, v, st = run_gpu(fastpath, topo_for(name), g["frames"], g["meta"], lines_only=bool(g["lines_only"]))

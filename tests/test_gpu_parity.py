@@ -741,3 +741,36 @@ def test_concurrent_queues_and_fib_updates(fastpath):
     assert fastpath.fib_lookup(1, T.ip4("200.1.22.9")) == 0  # deleted at i = 23
     fastpath.fib_commit(1)
     fresh_fastpath_state(fastpath, T.config_single_route())  # drop the modified state
+
+
+def test_batch_place_under_timing_knobs(fastpath):
+    """gr_hip_batch_place times its probe launches whatever "time_every" /
+    "untimed" say (a private always-timed queue), and the placed batch
+    forwards bit-exact."""
+    t = T.config_single_route()
+    fresh_fastpath_state(fastpath, t)
+    n = 1 << 18
+    fr, me = S.stream(n, 0x91AC, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    L = fastpath.lib
+    b = fastpath.batch_alloc(n)
+    try:
+        for dst, src in ((b.in_frames, fr), (b.meta, me)):
+            abi.check("h2d", L.gr_hip_memcpy_h2d(fastpath.h, dst, src.ctypes.data, src.nbytes))
+        for key, val in (("time_every", 4), ("untimed", 1)):
+            fastpath.tune(key, val)
+            try:
+                fastpath.batch_place(b, 3)
+            finally:
+                fastpath.tune(key, 1 if key == "time_every" else 0)
+        q = fastpath.queue()
+        q.stats(reset=True)
+        abi.check("submit", L.gr_hip_fwd4_submit(q._h, ctypes.byref(b)))
+        q.sync()
+        lines = np.empty((n, abi.LINE), dtype=np.uint8)
+        v = np.empty(n, dtype=abi.VERDICT_DT)
+        abi.check("d2h", L.gr_hip_memcpy_d2h(fastpath.h, lines.ctypes.data, b.out_lines, lines.nbytes))
+        abi.check("d2h", L.gr_hip_memcpy_d2h(fastpath.h, v.ctypes.data, b.verdicts, v.nbytes))
+        compare(oracle.Oracle(t).process(fr, me), (lines, v, q.stats()))
+        q.close()
+    finally:
+        fastpath.batch_free(b)

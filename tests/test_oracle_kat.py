@@ -212,42 +212,70 @@ def test_lpm6_hash_matches_brute_force():
     host.gr_fib6_free(f)
 
 
-def test_fib6_path_compression_fullview6():
-    """The product's IPv6 trie is path-compressed (fib6.c): on the IPv6 view
-    most groups become skip nodes, and lookups under every route, next to
-    random ones, still equal the RIB's longest match, also after deletes and
-    a rebuild."""
-    host = abi.host()
-    t = T.config_fullview6(count=20_000)
-    r = t.route6_array()
-    f = host.gr_fib6_new(len(r) + 16, 4 * len(r))
+def _fib6_check(host, f, routes, rng, n):
+    """Lookups under random routes (random host bits) and at random
+    addresses equal the RIB's longest match."""
+    for i in range(n):
+        d = rng.integers(0, 256, 16, dtype=np.uint8)
+        if i % 4:  # under a route, random host bits
+            x = routes[rng.integers(len(routes))]
+            nb = int(x["prefixlen"])
+            full = nb // 8
+            d[:full] = x["ip"][:full]
+            if nb % 8:
+                m = (0xFF00 >> (nb % 8)) & 0xFF
+                d[full] = (int(x["ip"][full]) & m) | (int(d[full]) & (~m & 0xFF))
+        assert host.gr_fib6_lookup(f, d.ctypes.data) == host.gr_fib6_lookup_rib(f, d.ctypes.data)
+
+
+def _fib6_of(host, r):
+    f = host.gr_fib6_new(len(r) + 16, max(1 << 16, 4 * len(r)))
     for x in r:
         ip = np.ascontiguousarray(x["ip"])
         assert host.gr_fib6_add(f, ip.ctypes.data, int(x["prefixlen"]), int(x["nh"]), 0) == 0
     assert host.gr_fib6_build(f) == 0
-    painted, kept, skips = host.gr_fib6_groups_painted(f), host.gr_fib6_groups_used(f), host.gr_fib6_skips_used(f)
-    assert kept < painted // 4 and skips > 0, (painted, kept, skips)
+    return f
+
+
+def test_fib6_fullview6_trie():
+    """The product's IPv6 trie (fib6.c) on fib_inject -6's full view: lookups
+    under every route, next to random ones, equal the RIB's longest match,
+    also after deletes and a rebuild."""
+    host = abi.host()
+    r = T.config_fullview6().route6_array()
+    assert len(r) == 200_001  # + the address route of p0
+    f = _fib6_of(host, r)
     rng = np.random.default_rng(66)
-
-    def check(routes, n):
-        for i in range(n):
-            d = rng.integers(0, 256, 16, dtype=np.uint8)
-            if i % 4:  # under a route, random host bits
-                x = routes[rng.integers(len(routes))]
-                nb = int(x["prefixlen"])
-                full = nb // 8
-                d[:full] = x["ip"][:full]
-                if nb % 8:
-                    m = (0xFF00 >> (nb % 8)) & 0xFF
-                    d[full] = (int(x["ip"][full]) & m) | (int(d[full]) & (~m & 0xFF))
-            assert host.gr_fib6_lookup(f, d.ctypes.data) == host.gr_fib6_lookup_rib(f, d.ctypes.data)
-
-    check(r, 20_000)
+    _fib6_check(host, f, r, rng, 20_000)
     for x in r[::3]:  # delete a third, repaint, compare again
         ip = np.ascontiguousarray(x["ip"])
         assert host.gr_fib6_del(f, ip.ctypes.data, int(x["prefixlen"])) == 0
     assert host.gr_fib6_build(f) == 0
-    check(r, 20_000)
+    _fib6_check(host, f, r, rng, 20_000)
+    host.gr_fib6_free(f)
+
+
+def test_fib6_path_compression():
+    """Sparse deep prefixes (random /56 .. /128 under 2000::/3): most of the
+    painted groups hold one exception and become skip nodes."""
+    host = abi.host()
+    rng = np.random.default_rng(67)
+    n = 5000
+    r = np.zeros(n, dtype=abi.ROUTE6_DT)
+    r["ip"] = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
+    r["ip"][:, 0] = 0x20 | (r["ip"][:, 0] & 0x1F)
+    r["prefixlen"] = rng.choice([56, 64, 96, 128], size=n)
+    for i in range(n):  # host bits clear
+        nb = int(r["prefixlen"][i])
+        for b in range(16):
+            keep = min(8, max(0, nb - 8 * b))
+            r["ip"][i, b] &= (0xFF00 >> keep) & 0xFF
+    r["vrf_id"] = 1
+    r["nh"] = 1 + np.arange(n) % 64
+    f = _fib6_of(host, r)
+    painted, kept, skips = host.gr_fib6_groups_painted(f), host.gr_fib6_groups_used(f), host.gr_fib6_skips_used(f)
+    assert kept < painted // 4 and skips > 0, (painted, kept, skips)
+    _fib6_check(host, f, r, rng, 20_000)
     host.gr_fib6_free(f)
 
 

@@ -19,7 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 24)
-    ap.add_argument("--workload", default="fullview64", choices=["fullview64", "single64"])
+    ap.add_argument("--workload", default="fullview64", choices=["fullview64", "single64", "fullview6"])
     ap.add_argument("--ring", type=int, default=None, help="gr_hip_tune ring geometry")
     ap.add_argument("--wg", type=int, default=None, help="gr_hip_tune wg_per_cu")
     ap.add_argument("--stats", type=int, default=None)
@@ -37,6 +37,9 @@ def main():
     if args.workload == "single64":
         topo = T.config_single_route()
         kw = dict(dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    elif args.workload == "fullview6":
+        topo = T.config_fullview6()
+        kw = None
     else:
         topo = T.config_fullview()
         kw = dict(routes=topo.route_array())
@@ -47,7 +50,11 @@ def main():
         if v is not None:
             fp.tune("wg_per_cu" if k == "wg" else k, v)
     n = args.batch
-    frames, meta = S.stream(n, S.SEED_GPU_BASE, **kw)
+    if kw is None:
+        r6 = topo.route6_array()
+        frames, meta = S.stream6(n, S.SEED_GPU_BASE, r6[r6["prefixlen"] < 128])
+    else:
+        frames, meta = S.stream(n, S.SEED_GPU_BASE, **kw)
     d_in = torch.from_numpy(frames.reshape(-1)).to(dev)
     d_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
     d_out = torch.empty_like(d_in)

@@ -5,18 +5,24 @@ summaries (tools/pmc_summary.py output), corrected as MI355X_MICROARCH.md
 reads half the bytes of a wide streaming read (x2, checked against the 1 GiB
 calibration copy when the summary holds one).
 
-    python tools/pmc_traffic.py SUMMARY.json KERNEL WORKLOAD BATCH [BYTES_PER_PKT] > profiles/pmc_traffic.json
+    python tools/pmc_traffic.py SUMMARY.json KERNEL WORKLOAD BATCH BYTES_PER_PKT SOURCE
 
-BYTES_PER_PKT is the algorithmic figure (bench.py b_pkt: 146 with the default
-2-byte FIB entries, 148 with 4-byte ones).
+merges the entry of WORKLOAD into profiles/pmc_traffic.json (a list, one
+entry per workload; bench.py reports the matching entry as roofline.traffic
+with its SOURCE). BYTES_PER_PKT is the algorithmic figure (bench.py b_pkt:
+146 with the default 2-byte FIB entries, 148 with 4-byte ones and IPv6).
 """
 import json
+import os
 import sys
+
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
 
 
 def main():
     summ, kernel, workload, batch = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
-    bpp = int(sys.argv[5]) if len(sys.argv) > 5 else 146
+    bpp = int(sys.argv[5])
+    source = sys.argv[6]
     d = json.load(open(summ))
     k = d[kernel]
     fetch = 2 * k["FETCH_SIZE"] * 1024
@@ -28,10 +34,19 @@ def main():
         "bytes_per_pkt": bpp,
         "algorithmic_bytes_per_launch": bpp * batch,
         "correction": "read = 2 x FETCH_SIZE KiB (gfx950 wide-read tally), write = WRITE_SIZE KiB",
+        "source": source,
     }
     # check of the x2: the corrected reads against the bytes the kernel must read
     # (64 B line + 8 B metadata per packet; FIB gathers are on-chip hits)
     out["read_vs_streamed"] = round(fetch / (72 * batch), 4)
+    old = []
+    if os.path.exists(OUT):
+        old = json.load(open(OUT))
+        old = old if isinstance(old, list) else [old]
+    entries = [e for e in old if e.get("workload") != workload] + [out]
+    with open(OUT, "w") as f:
+        json.dump(entries, f, indent=1)
+        f.write("\n")
     json.dump(out, sys.stdout, indent=1)
     print()
 
