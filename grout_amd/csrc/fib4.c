@@ -17,6 +17,7 @@
 
 #define NIL 0u // child == 0: no child (node 0 is the root, never a child)
 #define NONE UINT32_MAX // "no node" for the painters, which may start at the root
+#define DIRTY_CAP 4096 // tbl24 ranges tracked before the closest ones are merged
 
 struct node {
 	uint32_t child[2];
@@ -35,7 +36,8 @@ struct gr_fib4 {
 	uint32_t *tbl8; // num_tbl8 * 256
 	uint32_t *tbl8_free; // stack of free group indexes
 	uint32_t tbl8_nfree;
-	uint32_t dirty_lo, dirty_hi;
+	struct gr_fib4_range *dirty; // tbl24 index ranges touched, DIRTY_CAP at most
+	uint32_t n_dirty;
 	uint8_t *tbl8_dirty; // per group
 	uint32_t *dirty_groups;
 	uint32_t n_dirty_groups;
@@ -83,7 +85,8 @@ struct gr_fib4 *gr_fib4_new(uint32_t max_routes, uint32_t num_tbl8) {
 	f->tbl8_free = malloc((size_t)num_tbl8 * sizeof(uint32_t));
 	f->tbl8_dirty = calloc(num_tbl8, 1);
 	f->dirty_groups = malloc((size_t)num_tbl8 * sizeof(uint32_t));
-	if (!f->tbl24 || !f->tbl8 || !f->tbl8_free || !f->tbl8_dirty || !f->dirty_groups
+	f->dirty = malloc(DIRTY_CAP * sizeof(*f->dirty));
+	if (!f->tbl24 || !f->tbl8 || !f->tbl8_free || !f->tbl8_dirty || !f->dirty_groups || !f->dirty
 	    || node_alloc(f) != 0) {
 		gr_fib4_free(f);
 		return NULL;
@@ -91,8 +94,6 @@ struct gr_fib4 *gr_fib4_new(uint32_t max_routes, uint32_t num_tbl8) {
 	for (uint32_t g = 0; g < num_tbl8; g++) // pop lowest indexes first
 		f->tbl8_free[g] = num_tbl8 - 1 - g;
 	f->tbl8_nfree = num_tbl8;
-	f->dirty_lo = GR_FIB4_TBL24_ENTRIES;
-	f->dirty_hi = 0;
 	return f;
 }
 
@@ -106,6 +107,7 @@ void gr_fib4_free(struct gr_fib4 *f) {
 	free(f->tbl8_free);
 	free(f->tbl8_dirty);
 	free(f->dirty_groups);
+	free(f->dirty);
 	free(f);
 }
 
@@ -113,11 +115,55 @@ static uint32_t mask_of(uint8_t len) {
 	return len == 0 ? 0 : ~0u << (32 - len);
 }
 
+static int range_cmp(const void *a, const void *b) {
+	const struct gr_fib4_range *x = a, *y = b;
+	return x->lo < y->lo ? -1 : x->lo > y->lo;
+}
+
+// Sort the dirty ranges and merge those less than `gap` entries apart
+// (gap 0: overlapping or adjacent ones only).
+static void dirty_merge(struct gr_fib4 *f, uint32_t gap) {
+	if (f->n_dirty < 2)
+		return;
+	qsort(f->dirty, f->n_dirty, sizeof(*f->dirty), range_cmp);
+	uint32_t n = 0;
+	for (uint32_t i = 1; i < f->n_dirty; i++) {
+		struct gr_fib4_range *r = &f->dirty[n];
+		if ((uint64_t)f->dirty[i].lo <= (uint64_t)r->hi + gap) {
+			if (f->dirty[i].hi > r->hi)
+				r->hi = f->dirty[i].hi;
+		} else {
+			f->dirty[++n] = f->dirty[i];
+		}
+	}
+	f->n_dirty = n + 1;
+}
+
+// A painter wrote tbl24[lo, hi). Painting walks addresses upwards, so a
+// range usually extends the last one; a full list is merged, exactly first,
+// then over gaps 4x wider each pass until half of it is free again.
 static void mark_tbl24(struct gr_fib4 *f, uint32_t lo, uint32_t hi) {
-	if (lo < f->dirty_lo)
-		f->dirty_lo = lo;
-	if (hi > f->dirty_hi)
-		f->dirty_hi = hi;
+	if (f->n_dirty) {
+		struct gr_fib4_range *r = &f->dirty[f->n_dirty - 1];
+		if (lo <= r->hi && hi >= r->lo) {
+			if (lo < r->lo)
+				r->lo = lo;
+			if (hi > r->hi)
+				r->hi = hi;
+			return;
+		}
+	}
+	if (f->n_dirty == DIRTY_CAP) {
+		uint32_t gap = 0;
+		dirty_merge(f, gap);
+		while (f->n_dirty > DIRTY_CAP / 2) {
+			gap = gap ? gap * 4 : 16;
+			dirty_merge(f, gap);
+		}
+	}
+	f->dirty[f->n_dirty].lo = lo;
+	f->dirty[f->n_dirty].hi = hi;
+	f->n_dirty++;
 }
 
 static void mark_group(struct gr_fib4 *f, uint32_t g) {
@@ -337,9 +383,12 @@ uint32_t gr_fib4_n_routes(const struct gr_fib4 *f) {
 	return f->n_routes;
 }
 
-void gr_fib4_dirty_tbl24(struct gr_fib4 *f, uint32_t *lo, uint32_t *hi) {
-	*lo = f->dirty_lo;
-	*hi = f->dirty_hi;
+int gr_fib4_dirty_tbl24(struct gr_fib4 *f, struct gr_fib4_range *ranges, uint32_t max) {
+	dirty_merge(f, 0);
+	if (f->n_dirty > max)
+		return -1;
+	memcpy(ranges, f->dirty, (size_t)f->n_dirty * sizeof(*ranges));
+	return (int)f->n_dirty;
 }
 
 int gr_fib4_dirty_tbl8(struct gr_fib4 *f, uint32_t *groups, uint32_t max) {
@@ -353,6 +402,5 @@ void gr_fib4_dirty_clear(struct gr_fib4 *f) {
 	for (uint32_t i = 0; i < f->n_dirty_groups; i++)
 		f->tbl8_dirty[f->dirty_groups[i]] = 0;
 	f->n_dirty_groups = 0;
-	f->dirty_lo = GR_FIB4_TBL24_ENTRIES;
-	f->dirty_hi = 0;
+	f->n_dirty = 0;
 }

@@ -42,10 +42,15 @@ uint32_t gr_fib4_num_tbl8(const struct gr_fib4 *);
 uint32_t gr_fib4_tbl8_used(const struct gr_fib4 *);
 uint32_t gr_fib4_n_routes(const struct gr_fib4 *);
 
-// Dirty tracking for the device upload: tbl24 entries [*lo, *hi) and the
-// tbl8 groups touched since the last call; returns the number of dirty tbl8
-// groups written to `groups` (at most `max`; -1 if more, then upload all).
-void gr_fib4_dirty_tbl24(struct gr_fib4 *, uint32_t *lo, uint32_t *hi);
+// Dirty tracking for the device upload, since the last gr_fib4_dirty_clear:
+// the tbl24 index ranges [lo, hi) painted, sorted and disjoint (at most 4096
+// are kept: past that the closest ones are merged, so a range may cover
+// unchanged entries), and the tbl8 groups painted. Each returns the number
+// written (at most `max`; -1 if more: upload everything).
+struct gr_fib4_range {
+	uint32_t lo, hi;
+};
+int gr_fib4_dirty_tbl24(struct gr_fib4 *, struct gr_fib4_range *ranges, uint32_t max);
 int gr_fib4_dirty_tbl8(struct gr_fib4 *, uint32_t *groups, uint32_t max);
 void gr_fib4_dirty_clear(struct gr_fib4 *);
 

@@ -54,8 +54,10 @@ constexpr uint32_t HOST_CHUNK = 1u << 18; // packets per host-mode chunk
 #define FIB_FMT_16_8_8 1 // DIR-16-8-8, 2-byte entries
 #define FIB_FMT_24_W2 2 // DIR24_8, 2-byte entries
 
-struct vrf_fib {
-	gr_fib4 *rib = nullptr;
+// One of a VRF's two device copies of its IPv4 FIB (FIB publication is
+// double-buffered: launches read the published copy while a commit writes
+// the other, see gr_hip_fib4_commit).
+struct fib4_buf {
 	uint32_t *d24 = nullptr; // 4-byte entries (fib4.h encoding)
 	uint32_t *d8 = nullptr;
 	// DIR-16-8-8 with 2-byte entries, used while every slot fits 15 bits:
@@ -65,32 +67,80 @@ struct vrf_fib {
 	uint16_t *d8_16 = nullptr;
 	// DIR24_8 with 2-byte entries (bit15 = tbl8 group), same condition
 	uint16_t *d24_16 = nullptr;
+	int fmt = FIB_FMT_24; // format of the table it holds
+	bool up = false; // holds a complete table in `fmt`
+
+	void free_all() {
+		hipFree(d24);
+		hipFree(d8);
+		hipFree(d16);
+		hipFree(d8_16);
+		hipFree(d24_16);
+		*this = fib4_buf();
+	}
+};
+
+// The same for the IPv6 trie: top[65536], groups, skips (fib6.h).
+struct fib6_buf {
+	uint32_t *d6 = nullptr;
+	uint32_t groups = 0; // group capacity
+	uint64_t gen = 0; // fib6 generation it holds
+	bool up = false;
+
+	void free_all() {
+		hipFree(d6);
+		*this = fib6_buf();
+	}
+};
+
+struct vrf_fib {
+	gr_fib4 *rib = nullptr;
+	fib4_buf b4[2];
+	int pub4 = 1; // the copy the current generation's views point at (the other is written)
+	uint8_t sel4[2] = {1, 1}; // the copy each view generation points at
+	// what b4[pub4 ^ 1] misses of the published table: tbl24 index ranges
+	// (sorted, disjoint) and tbl8 groups (sorted), or everything
+	std::vector<gr_fib4_range> pend24;
+	std::vector<uint32_t> pend8;
+	bool pend_all = true;
+	// DIR-16-8-8 chunk assignment, shared by both copies (each dirty /16 is
+	// rewritten into a copy before that copy is published)
 	std::vector<int32_t> chunk_of; // per /16: chunk index or -1
 	std::vector<uint32_t> chunk_free; // free chunk indexes (stack)
 	uint32_t n_chunks = 0; // chunks in use
-	int fmt = FIB_FMT_24; // format on the device
 	uint32_t max_slot = 0; // highest nexthop slot ever routed (never decreases)
 	uint32_t num_tbl8 = 0;
-	bool uploaded = false; // tables uploaded at least once
 
-	void reset4() { // forget the IPv4 state only
+	const fib4_buf &pub() const {
+		return b4[pub4];
+	}
+	bool uploaded() const {
+		return b4[pub4].up;
+	}
+	void reset4() { // forget the IPv4 state only (device copies freed by the caller)
 		rib = nullptr;
-		d24 = d8 = d16 = nullptr;
-		d8_16 = d24_16 = nullptr;
+		b4[0] = fib4_buf();
+		b4[1] = fib4_buf();
+		pub4 = 1;
+		sel4[0] = sel4[1] = 1;
+		pend24.clear();
+		pend8.clear();
+		pend_all = true;
 		chunk_of.clear();
 		chunk_free.clear();
 		n_chunks = 0;
-		fmt = FIB_FMT_24;
 		max_slot = 0;
 		num_tbl8 = 0;
-		uploaded = false;
 	}
-	// IPv6: fib6.h trie, on the device as top[65536] followed by the groups
+	// IPv6: fib6.h trie, double-buffered the same way (whole-trie uploads)
 	gr_fib6_t *rib6 = nullptr;
-	uint32_t *d6 = nullptr;
-	uint32_t d6_groups = 0; // group capacity of d6
-	uint64_t gen6 = 0; // fib6 generation on the device
-	bool uploaded6 = false;
+	fib6_buf b6[2];
+	int pub6 = 1;
+	uint8_t sel6[2] = {1, 1};
+
+	bool uploaded6() const {
+		return b6[pub6].up;
+	}
 };
 
 struct host_slot {
@@ -111,6 +161,7 @@ struct gr_hip_queue {
 	uint64_t n_submit; // submits that could be timed (time_every sampling)
 	bool always_timed; // every launch carries events, whatever the knobs (gr_hip_batch_place's probes)
 	hipEvent_t quiesce;
+	hipEvent_t retire; // recorded at every FIB publication: the launches that may read the unpublished copies
 	gr_hip_iface_stats *d_stats; // [FWD4_STAT_SHARDS][max_ifaces]
 	host_slot hs[HOST_SLOTS];
 	// gr_hip_node_process staging (pinned, grown on demand)
@@ -133,25 +184,29 @@ struct gr_hip_ctx {
 	int dev;
 	uint32_t max_ifaces, max_nh;
 	int n_cu;
-	std::shared_mutex mu; // control-plane writers exclusive; node hand-back readers shared
+	std::shared_mutex mu; // control-plane writers exclusive; submitters shared
+	std::mutex fib_mu; // FIB writers (routes, commits), taken before mu
 	hipStream_t ctl;
 	std::vector<gr_hip_iface> ifaces;
 	std::vector<gr_hip_nh> nh;
 	std::vector<uint32_t> reta;
 	std::vector<vrf_fib> vrfs;
-	std::vector<fwd4_rx> rx; // host images of the device views
+	// Two generations of the RX views and of the table block a launch reads
+	// (double-buffered FIB publication): a submit takes generation `gen`.
+	uint32_t gen;
+	std::vector<fwd4_rx> rx[2]; // host images of the device views
 	std::vector<fwd4_adj> adj;
 	uint32_t nh_hi; // highest nexthop slot ever set
-	fwd4_rx *d_rx;
+	fwd4_rx *d_rx[2];
 	fwd4_adj *d_adj;
 	std::vector<fwd4_nhf> nhf; // fast adjacencies (host image)
 	fwd4_nhf *d_nhf;
 	std::vector<fwd4_nhf> nhf6; // the same for the IPv6 chain
 	fwd4_nhf *d_nhf6;
 	uint32_t v6_routes; // IPv6 routes on the device, all VRFs (stage nhf6 in LDS when > 0)
-	std::vector<fwd4_rx6> rx6; // IPv6 views and adjacencies (host images)
+	std::vector<fwd4_rx6> rx6[2]; // IPv6 views and adjacencies (host images)
 	std::vector<fwd4_adj6> adj6;
-	fwd4_rx6 *d_rx6;
+	fwd4_rx6 *d_rx6[2];
 	fwd4_adj6 *d_adj6;
 	uint32_t *d_reta;
 	uint32_t d_reta_cap;
@@ -159,7 +214,7 @@ struct gr_hip_ctx {
 	uint16_t *d_vlan_vals;
 	uint32_t vlan_cap;
 	fwd4_edges edges;
-	fwd4_tables *d_tables; // device copy of what every launch reads
+	fwd4_tables *d_tables[2]; // device copy of what every launch reads, by generation
 	std::vector<gr_hip_queue *> queues;
 	// tuning knobs (gr_hip_tune)
 	int nt; // FWD4_V_NT
@@ -174,6 +229,8 @@ struct gr_hip_ctx {
 	int untimed; // measurements: no HIP events around launches (gr_hip_queue_kernel_ms sees none)
 	uint32_t time_every; // HIP events around every N-th submit of a queue only (0, 1 = every one)
 	std::vector<host_range> hregs; // registered host memory, by host address
+	uint8_t *stage; // pinned staging of the FIB commits (fib_mu)
+	size_t stage_cap;
 	std::mutex occ_mu; // the occupancy cache below (launches run concurrently)
 	int occ_ring[8]; // by variant, of the last launch's geometry and staging ("occupancy")
 	struct occ_entry {
@@ -215,9 +272,10 @@ static const gr_hip_iface *iface_get(const gr_hip_ctx *c, uint32_t id) {
 	return &c->ifaces[id];
 }
 
-// RX view of iface `id`: iface_input's admin/mode edge (iface_input.c:88-97),
-// eth_input's MAC (eth_input.c:62-68) and the VRF FIB (modules/ip/control/route.c:51-61).
-static fwd4_rx make_rx(const gr_hip_ctx *c, uint32_t id) {
+// RX view of iface `id` in view generation `g`: iface_input's admin/mode
+// edge (iface_input.c:88-97), eth_input's MAC (eth_input.c:62-68) and the
+// copy of the VRF FIB that generation points at (modules/ip/control/route.c:51-61).
+static fwd4_rx make_rx(const gr_hip_ctx *c, uint32_t id, uint32_t g) {
 	fwd4_rx r;
 	memset(&r, 0, sizeof(r));
 	const gr_hip_iface *i = iface_get(c, id);
@@ -233,37 +291,38 @@ static fwd4_rx make_rx(const gr_hip_ctx *c, uint32_t id) {
 	memcpy(r.mac, i->mac, 6);
 	const gr_hip_iface *vrf = iface_get(c, i->vrf_id);
 	if (vrf != nullptr && vrf->type == GR_HIP_IFACE_TYPE_VRF && c->vrfs[i->vrf_id].rib != nullptr
-	    && c->vrfs[i->vrf_id].uploaded) {
-		const vrf_fib &v = c->vrfs[i->vrf_id];
-		if (v.fmt == FIB_FMT_16_8_8) {
-			r.tbl24 = v.d16;
-			r.tbl8 = reinterpret_cast<const uint32_t *>(v.d8_16);
+	    && c->vrfs[i->vrf_id].b4[c->vrfs[i->vrf_id].sel4[g]].up) {
+		const fib4_buf &b = c->vrfs[i->vrf_id].b4[c->vrfs[i->vrf_id].sel4[g]];
+		if (b.fmt == FIB_FMT_16_8_8) {
+			r.tbl24 = b.d16;
+			r.tbl8 = reinterpret_cast<const uint32_t *>(b.d8_16);
 			r.flags |= FWD4_RX_FIB16;
-		} else if (v.fmt == FIB_FMT_24_W2) {
-			r.tbl24 = reinterpret_cast<const uint32_t *>(v.d24_16);
-			r.tbl8 = reinterpret_cast<const uint32_t *>(v.d8_16);
+		} else if (b.fmt == FIB_FMT_24_W2) {
+			r.tbl24 = reinterpret_cast<const uint32_t *>(b.d24_16);
+			r.tbl8 = reinterpret_cast<const uint32_t *>(b.d8_16);
 			r.flags |= FWD4_RX_FIB24W2;
 		} else {
-			r.tbl24 = v.d24;
-			r.tbl8 = v.d8;
+			r.tbl24 = b.d24;
+			r.tbl8 = b.d8;
 		}
 	}
 	return r;
 }
 
-// IPv6 view of iface `id`: the FIB6 of its VRF (get_fib6, modules/ip6/control/route.c:54-64).
-static fwd4_rx6 make_rx6(const gr_hip_ctx *c, uint32_t id) {
+// IPv6 view of iface `id` in view generation `g`: the FIB6 of its VRF
+// (get_fib6, modules/ip6/control/route.c:54-64).
+static fwd4_rx6 make_rx6(const gr_hip_ctx *c, uint32_t id, uint32_t g) {
 	fwd4_rx6 r = {nullptr, nullptr, nullptr};
 	const gr_hip_iface *i = iface_get(c, id);
 	if (i == nullptr)
 		return r;
 	const gr_hip_iface *vrf = iface_get(c, i->vrf_id);
 	if (vrf != nullptr && vrf->type == GR_HIP_IFACE_TYPE_VRF && c->vrfs[i->vrf_id].rib6 != nullptr
-	    && c->vrfs[i->vrf_id].uploaded6) {
-		const vrf_fib &v = c->vrfs[i->vrf_id];
-		r.top = v.d6;
-		r.groups = v.d6 + GR_FIB6_TOP;
-		r.skips = reinterpret_cast<const uint4 *>(v.d6 + GR_FIB6_TOP + (size_t)v.d6_groups * GR_FIB6_GROUP);
+	    && c->vrfs[i->vrf_id].b6[c->vrfs[i->vrf_id].sel6[g]].up) {
+		const fib6_buf &b = c->vrfs[i->vrf_id].b6[c->vrfs[i->vrf_id].sel6[g]];
+		r.top = b.d6;
+		r.groups = b.d6 + GR_FIB6_TOP;
+		r.skips = reinterpret_cast<const uint4 *>(b.d6 + GR_FIB6_TOP + (size_t)b.groups * GR_FIB6_GROUP);
 	}
 	return r;
 }
@@ -409,17 +468,29 @@ static fwd4_nhf make_nhf6(const fwd4_adj6 &a) {
 	return f;
 }
 
-// Recompute and upload the RX views (all) and adjacencies [first, first+n)
-// (n == 0: every slot up to nh_hi). Caller holds c->mu and has quiesced.
+// Recompute and upload the RX views of generation g (IPv4 and IPv6, every
+// iface) on the control stream; does not wait.
+static int upload_rx(gr_hip_ctx *c, uint32_t g) {
+	for (uint32_t i = 0; i < c->max_ifaces; i++) {
+		c->rx[g][i] = make_rx(c, i, g);
+		c->rx6[g][i] = make_rx6(c, i, g);
+	}
+	HCK(hipMemcpyAsync(c->d_rx[g], c->rx[g].data(), sizeof(fwd4_rx) * c->max_ifaces, hipMemcpyHostToDevice, c->ctl));
+	HCK(hipMemcpyAsync(c->d_rx6[g], c->rx6[g].data(), sizeof(fwd4_rx6) * c->max_ifaces, hipMemcpyHostToDevice,
+			   c->ctl));
+	return 0;
+}
+
+// Recompute and upload the RX views (both generations, all ifaces) and
+// adjacencies [first, first+n) (n == 0: every slot up to nh_hi). Caller
+// holds c->mu exclusively and has quiesced.
 static int upload_views(gr_hip_ctx *c, bool rx, uint32_t first, uint32_t n, bool adj) {
 	if (rx) {
-		for (uint32_t i = 0; i < c->max_ifaces; i++) {
-			c->rx[i] = make_rx(c, i);
-			c->rx6[i] = make_rx6(c, i);
+		for (uint32_t g = 0; g < 2; g++) {
+			int r = upload_rx(c, g);
+			if (r)
+				return r;
 		}
-		HCK(hipMemcpyAsync(c->d_rx, c->rx.data(), sizeof(fwd4_rx) * c->max_ifaces, hipMemcpyHostToDevice, c->ctl));
-		HCK(hipMemcpyAsync(c->d_rx6, c->rx6.data(), sizeof(fwd4_rx6) * c->max_ifaces, hipMemcpyHostToDevice,
-				   c->ctl));
 	}
 	if (adj) {
 		if (n == 0) {
@@ -448,23 +519,25 @@ static int upload_views(gr_hip_ctx *c, bool rx, uint32_t first, uint32_t n, bool
 // Refresh the device-resident fwd4_tables (caller holds c->mu and has
 // quiesced the queues); completes before returning.
 static int upload_tables(gr_hip_ctx *c) {
-	fwd4_tables t;
-	memset(&t, 0, sizeof(t));
-	t.rx = c->d_rx;
-	t.adj = c->d_adj;
-	t.nhf = c->d_nhf;
-	t.nhf6 = c->d_nhf6;
-	t.rx6 = c->d_rx6;
-	t.adj6 = c->d_adj6;
-	t.reta = c->d_reta;
-	t.vlan_keys = c->d_vlan_keys;
-	t.vlan_vals = c->d_vlan_vals;
-	t.reta_cap = c->d_reta ? (uint32_t)c->reta.size() : 0;
-	t.vlan_mask = c->vlan_cap ? c->vlan_cap - 1 : 0;
-	t.max_ifaces = c->max_ifaces;
-	t.max_nh = c->max_nh;
-	t.edges = c->edges;
-	HCK(hipMemcpyAsync(c->d_tables, &t, sizeof(t), hipMemcpyHostToDevice, c->ctl));
+	fwd4_tables t[2];
+	memset(t, 0, sizeof(t));
+	for (uint32_t g = 0; g < 2; g++) {
+		t[g].rx = c->d_rx[g];
+		t[g].adj = c->d_adj;
+		t[g].nhf = c->d_nhf;
+		t[g].nhf6 = c->d_nhf6;
+		t[g].rx6 = c->d_rx6[g];
+		t[g].adj6 = c->d_adj6;
+		t[g].reta = c->d_reta;
+		t[g].vlan_keys = c->d_vlan_keys;
+		t[g].vlan_vals = c->d_vlan_vals;
+		t[g].reta_cap = c->d_reta ? (uint32_t)c->reta.size() : 0;
+		t[g].vlan_mask = c->vlan_cap ? c->vlan_cap - 1 : 0;
+		t[g].max_ifaces = c->max_ifaces;
+		t[g].max_nh = c->max_nh;
+		t[g].edges = c->edges;
+		HCK(hipMemcpyAsync(c->d_tables[g], &t[g], sizeof(t[g]), hipMemcpyHostToDevice, c->ctl));
+	}
 	HCK(hipStreamSynchronize(c->ctl));
 	return 0;
 }
@@ -562,12 +635,15 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->ifaces.assign(max_ifaces, gr_hip_iface {});
 	c->nh.assign((size_t)max_nexthops + 1, gr_hip_nh {});
 	c->vrfs.assign(max_ifaces, vrf_fib {});
-	c->rx.assign(max_ifaces, fwd4_rx {});
+	c->gen = 0;
+	for (uint32_t g = 0; g < 2; g++) {
+		c->rx[g].assign(max_ifaces, fwd4_rx {});
+		c->rx6[g].assign(max_ifaces, fwd4_rx6 {});
+	}
 	c->adj.assign((size_t)max_nexthops + 1, fwd4_adj {});
 	c->nhf.assign((size_t)max_nexthops + 1, fwd4_nhf {});
 	c->nhf6.assign((size_t)max_nexthops + 1, fwd4_nhf {});
 	c->v6_routes = 0;
-	c->rx6.assign(max_ifaces, fwd4_rx6 {});
 	c->adj6.assign((size_t)max_nexthops + 1, fwd4_adj6 {});
 	c->nh_hi = 0;
 	set_default_edges(&c->edges);
@@ -579,27 +655,28 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	int ret = -ENOMEM;
 	if (hipStreamCreateWithFlags(&c->ctl, hipStreamNonBlocking) != hipSuccess)
 		goto fail;
-	if (hipMalloc(&c->d_rx, sizeof(fwd4_rx) * max_ifaces) != hipSuccess)
-		goto fail;
+	for (uint32_t g = 0; g < 2; g++) {
+		if (hipMalloc(&c->d_rx[g], sizeof(fwd4_rx) * max_ifaces) != hipSuccess
+		    || hipMalloc(&c->d_rx6[g], sizeof(fwd4_rx6) * max_ifaces) != hipSuccess
+		    || hipMalloc(&c->d_tables[g], sizeof(fwd4_tables)) != hipSuccess)
+			goto fail;
+		if (hipMemsetAsync(c->d_rx[g], 0, sizeof(fwd4_rx) * max_ifaces, c->ctl) != hipSuccess
+		    || hipMemsetAsync(c->d_rx6[g], 0, sizeof(fwd4_rx6) * max_ifaces, c->ctl) != hipSuccess)
+			goto fail;
+	}
 	if (hipMalloc(&c->d_nhf, sizeof(fwd4_nhf) * ((size_t)max_nexthops + 1)) != hipSuccess)
 		goto fail;
 	if (hipMalloc(&c->d_nhf6, sizeof(fwd4_nhf) * ((size_t)max_nexthops + 1)) != hipSuccess)
-		goto fail;
-	if (hipMalloc(&c->d_rx6, sizeof(fwd4_rx6) * max_ifaces) != hipSuccess)
 		goto fail;
 	if (hipMalloc(&c->d_adj6, sizeof(fwd4_adj6) * ((size_t)max_nexthops + 1)) != hipSuccess)
 		goto fail;
 	if (hipMalloc(&c->d_adj, sizeof(fwd4_adj) * ((size_t)max_nexthops + 1)) != hipSuccess)
 		goto fail;
-	if (hipMalloc(&c->d_tables, sizeof(fwd4_tables)) != hipSuccess)
-		goto fail;
 	// every device write goes through the control stream: a plain hipMemset
 	// runs on the null stream, which a non-blocking stream does not order with
-	if (hipMemsetAsync(c->d_rx, 0, sizeof(fwd4_rx) * max_ifaces, c->ctl) != hipSuccess
-	    || hipMemsetAsync(c->d_adj, 0, sizeof(fwd4_adj) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess
+	if (hipMemsetAsync(c->d_adj, 0, sizeof(fwd4_adj) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess
 	    || hipMemsetAsync(c->d_nhf, 0, sizeof(fwd4_nhf) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess
 	    || hipMemsetAsync(c->d_nhf6, 0, sizeof(fwd4_nhf) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess
-	    || hipMemsetAsync(c->d_rx6, 0, sizeof(fwd4_rx6) * max_ifaces, c->ctl) != hipSuccess
 	    || hipMemsetAsync(c->d_adj6, 0, sizeof(fwd4_adj6) * ((size_t)max_nexthops + 1), c->ctl) != hipSuccess)
 		goto fail;
 	c->nt = FWD4_V_NT; // measured faster on every kernel
@@ -639,16 +716,17 @@ extern "C" int gr_hip_fini(gr_hip_ctx_t *c) {
 	c->hregs.clear();
 	for (vrf_fib &v : c->vrfs) {
 		gr_fib4_free(v.rib);
-		hipFree(v.d24);
-		hipFree(v.d8);
-		hipFree(v.d16);
-		hipFree(v.d8_16);
-		hipFree(v.d24_16);
 		gr_fib6_free(v.rib6);
-		hipFree(v.d6);
+		for (int k = 0; k < 2; k++) {
+			v.b4[k].free_all();
+			v.b6[k].free_all();
+		}
 	}
-	hipFree(c->d_rx);
-	hipFree(c->d_rx6);
+	for (uint32_t g = 0; g < 2; g++) {
+		hipFree(c->d_rx[g]);
+		hipFree(c->d_rx6[g]);
+		hipFree(c->d_tables[g]);
+	}
 	hipFree(c->d_adj6);
 	hipFree(c->d_adj);
 	hipFree(c->d_nhf);
@@ -656,7 +734,7 @@ extern "C" int gr_hip_fini(gr_hip_ctx_t *c) {
 	hipFree(c->d_reta);
 	hipFree(c->d_vlan_keys);
 	hipFree(c->d_vlan_vals);
-	hipFree(c->d_tables);
+	hipHostFree(c->stage);
 	if (c->ctl)
 		hipStreamDestroy(c->ctl);
 	(void)hipGetLastError();
@@ -929,9 +1007,96 @@ extern "C" int gr_hip_reta_set(gr_hip_ctx_t *c, uint32_t first, const uint32_t *
 // FIB
 // ---------------------------------------------------------------------------
 
+// FIB publication is double-buffered, the MI355X analogue of grout's RCU
+// (rte_fib with an RCU QSBR variable, modules/ip/control/route.c:87-95, and
+// rte_rcu_qsbr_synchronize before a FIB is freed, :766): every VRF keeps two
+// device copies of its tables, and the context two generations of the RX
+// views and table block a launch reads. A submit takes the current
+// generation (under the shared lock, for microseconds), so each launch sees
+// one table from its first packet to its last. A commit
+//   1. makes the control stream wait for the launches submitted before the
+//      previous publication (the only ones that can still read the copy it
+//      is about to write: `retire` events), writes the unpublished copy and
+//      the other generation's views, with c->mu held shared (submitters keep
+//      going);
+//   2. publishes: flips the generation and records `retire` on every queue,
+//      with c->mu held exclusively for a few microseconds.
+// Route adds and deletes only touch the host RIB (fib_mu).
+
+// Wait, on the control stream, for every launch submitted before the last
+// publication.
+static int retire_wait(gr_hip_ctx *c) {
+	for (gr_hip_queue *q : c->queues)
+		HCK(hipStreamWaitEvent(c->ctl, q->retire, 0));
+	return 0;
+}
+
+// Point generation g at every VRF's published copies (the caller then points
+// it at the copy it writes).
+static void views_follow_published(gr_hip_ctx *c, uint32_t g) {
+	for (vrf_fib &v : c->vrfs) {
+		v.sel4[g] = (uint8_t)v.pub4;
+		v.sel6[g] = (uint8_t)v.pub6;
+	}
+}
+
+static void count_v6(gr_hip_ctx *c);
+
+// Step 2: flip to generation g, which the caller has written. Takes c->mu
+// exclusively; `then` runs under it (the per-VRF published index).
+template <typename F>
+static int publish(gr_hip_ctx *c, uint32_t g, F then) {
+	std::lock_guard<std::shared_mutex> l(c->mu);
+	c->gen = g;
+	then();
+	count_v6(c);
+	for (gr_hip_queue *q : c->queues)
+		HCK(hipEventRecord(q->retire, q->s));
+	return 0;
+}
+
+// Host staging for one commit's uploads: the bytes of every (destination,
+// length) write packed into one pinned buffer, then one DMA per write.
+struct stager {
+	gr_hip_ctx *c;
+	std::vector<uint8_t> buf;
+	struct op {
+		void *dst;
+		size_t off, n;
+	};
+	std::vector<op> ops;
+
+	explicit stager(gr_hip_ctx *c_) : c(c_) {}
+	// room for n bytes going to dst; valid until the next add
+	template <typename E>
+	E *add(E *dst, size_t count) {
+		const size_t off = (buf.size() + 15) & ~(size_t)15;
+		buf.resize(off + count * sizeof(E));
+		ops.push_back({dst, off, count * sizeof(E)});
+		return reinterpret_cast<E *>(buf.data() + off);
+	}
+	int flush() { // enqueue on the control stream (the caller syncs it)
+		if (buf.empty())
+			return 0;
+		if (buf.size() > c->stage_cap) {
+			HCK(hipStreamSynchronize(c->ctl));
+			hipHostFree(c->stage);
+			c->stage = nullptr;
+			c->stage_cap = 0;
+			HCK(hipHostMalloc(reinterpret_cast<void **>(&c->stage), buf.size(), hipHostMallocDefault));
+			c->stage_cap = buf.size();
+		}
+		memcpy(c->stage, buf.data(), buf.size());
+		for (const op &o : ops)
+			HCK(hipMemcpyAsync(o.dst, c->stage + o.off, o.n, hipMemcpyHostToDevice, c->ctl));
+		return 0;
+	}
+};
+
 extern "C" int gr_hip_fib4_create(gr_hip_ctx_t *c, uint16_t vrf, uint32_t max_routes, uint32_t num_tbl8) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
+	std::lock_guard<std::mutex> f(c->fib_mu);
 	std::lock_guard<std::shared_mutex> l(c->mu);
 	hipSetDevice(c->dev);
 	vrf_fib &v = c->vrfs[vrf];
@@ -943,7 +1108,7 @@ extern "C" int gr_hip_fib4_create(gr_hip_ctx_t *c, uint16_t vrf, uint32_t max_ro
 	if (v.rib == nullptr)
 		return -ENOMEM;
 	v.num_tbl8 = num_tbl8;
-	// device tables are allocated by the first commit, in the format it picks
+	// device copies are allocated by the commits, in the format they pick
 	gr_fib4_dirty_clear(v.rib);
 	return 0;
 }
@@ -951,6 +1116,7 @@ extern "C" int gr_hip_fib4_create(gr_hip_ctx_t *c, uint16_t vrf, uint32_t max_ro
 extern "C" int gr_hip_fib4_destroy(gr_hip_ctx_t *c, uint16_t vrf) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
+	std::lock_guard<std::mutex> f(c->fib_mu);
 	std::lock_guard<std::shared_mutex> l(c->mu);
 	hipSetDevice(c->dev);
 	vrf_fib &v = c->vrfs[vrf];
@@ -965,13 +1131,9 @@ extern "C" int gr_hip_fib4_destroy(gr_hip_ctx_t *c, uint16_t vrf) {
 		v.rib = rib;
 		return r;
 	}
-	v.rib = rib;
-	hipFree(v.d24);
-	hipFree(v.d8);
-	hipFree(v.d16);
-	hipFree(v.d8_16);
-	hipFree(v.d24_16);
-	gr_fib4_free(v.rib);
+	v.b4[0].free_all();
+	v.b4[1].free_all();
+	gr_fib4_free(rib);
 	v.reset4();
 	return 0;
 }
@@ -979,7 +1141,7 @@ extern "C" int gr_hip_fib4_destroy(gr_hip_ctx_t *c, uint16_t vrf) {
 extern "C" int gr_hip_route4_add(gr_hip_ctx_t *c, const struct gr_hip_route4 *rt, uint32_t n, int replace) {
 	if (c == nullptr || (rt == nullptr && n))
 		return -EINVAL;
-	std::lock_guard<std::shared_mutex> l(c->mu);
+	std::lock_guard<std::mutex> f(c->fib_mu); // the host RIB only: launches go on
 	for (uint32_t i = 0; i < n; i++) {
 		if (rt[i].vrf_id == 0 || rt[i].vrf_id >= c->max_ifaces || rt[i].nh == 0
 		    || rt[i].nh > c->max_nh)
@@ -999,181 +1161,233 @@ extern "C" int gr_hip_route4_add(gr_hip_ctx_t *c, const struct gr_hip_route4 *rt
 extern "C" int gr_hip_route4_del(gr_hip_ctx_t *c, uint16_t vrf, uint32_t ip, uint8_t len) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
-	std::lock_guard<std::shared_mutex> l(c->mu);
+	std::lock_guard<std::mutex> f(c->fib_mu);
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib == nullptr)
 		return -ENONET;
 	return gr_fib4_del(v.rib, __builtin_bswap32(ip), len);
 }
 
-// Upload runs of tbl8 groups (sorted) from a host table of `esz`-byte entries.
-template <typename E>
-static int upload_groups(gr_hip_ctx *c, E *dev, const E *host, std::vector<uint32_t> &gs) {
-	std::sort(gs.begin(), gs.end());
-	for (size_t i = 0; i < gs.size();) {
-		size_t j = i + 1;
-		while (j < gs.size() && gs[j] == gs[j - 1] + 1)
-			j++;
-		int r = h2d(c, dev + (size_t)gs[i] * 256, host + (size_t)gs[i] * 256, (j - i) * 256 * sizeof(E));
-		if (r)
-			return r;
-		i = j;
-	}
-	return 0;
-}
-
 static uint16_t to16(uint32_t e) { // fib4.h 4-byte entry -> 2-byte entry
 	return (uint16_t)((e & GR_FIB4_EXT) ? (0x8000u | (e & 0x7fffu)) : e);
 }
 
-// Stream-ordered FIB publication: quiesce the queues, upload what changed in
-// the format the tables fit (2-byte entries while every nexthop slot fits 15
-// bits and every tbl8 group index too, else 4-byte), then re-point the RX
-// views when the format or the first upload changed them.
+// Sorted, disjoint union of sorted range lists; ranges less than `gap`
+// entries apart are merged too (re-writing unchanged entries in between
+// costs less than one more DMA).
+static std::vector<gr_fib4_range> range_union(const std::vector<gr_fib4_range> &a,
+					      const std::vector<gr_fib4_range> &b, uint32_t gap) {
+	std::vector<gr_fib4_range> all(a);
+	all.insert(all.end(), b.begin(), b.end());
+	std::sort(all.begin(), all.end(), [](const gr_fib4_range &x, const gr_fib4_range &y) { return x.lo < y.lo; });
+	std::vector<gr_fib4_range> out;
+	for (const gr_fib4_range &r : all) {
+		if (!out.empty() && (uint64_t)r.lo <= (uint64_t)out.back().hi + gap)
+			out.back().hi = std::max(out.back().hi, r.hi);
+		else
+			out.push_back(r);
+	}
+	return out;
+}
+
+static std::vector<uint32_t> group_union(const std::vector<uint32_t> &a, const std::vector<uint32_t> &b) {
+	std::vector<uint32_t> all(a);
+	all.insert(all.end(), b.begin(), b.end());
+	std::sort(all.begin(), all.end());
+	all.erase(std::unique(all.begin(), all.end()), all.end());
+	return all;
+}
+
+// Stage runs of tbl8 groups (sorted) of a host table converted entry by entry.
+template <typename E, typename Conv>
+static void stage_groups(stager &st, E *dev, const uint32_t *t8, const std::vector<uint32_t> &gs, Conv conv) {
+	for (size_t i = 0; i < gs.size();) {
+		size_t j = i + 1;
+		while (j < gs.size() && gs[j] == gs[j - 1] + 1)
+			j++;
+		E *h = st.add(dev + (size_t)gs[i] * 256, (j - i) * 256);
+		const uint32_t *src = t8 + (size_t)gs[i] * 256;
+		for (size_t k = 0; k < (j - i) * 256; k++)
+			h[k] = conv(src[k]);
+		i = j;
+	}
+}
+
+// Allocate the device arrays copy `b` needs in format `fmt`.
+static int fib4_buf_alloc(gr_hip_ctx *c, fib4_buf &b, int fmt, uint32_t num_tbl8) {
+	if (fmt != FIB_FMT_24 && b.d8_16 == nullptr)
+		HCK(hipMalloc(&b.d8_16, sizeof(uint16_t) * 256 * (size_t)num_tbl8));
+	if (fmt == FIB_FMT_24_W2 && b.d24_16 == nullptr)
+		HCK(hipMalloc(&b.d24_16, sizeof(uint16_t) * GR_FIB4_TBL24_ENTRIES));
+	if (fmt == FIB_FMT_16_8_8 && b.d16 == nullptr) // top + the worst case of one chunk per /16
+		HCK(hipMalloc(&b.d16, sizeof(uint32_t) * 65536 + sizeof(uint16_t) * 256 * 65536));
+	if (fmt == FIB_FMT_24 && b.d24 == nullptr) {
+		HCK(hipMalloc(&b.d24, sizeof(uint32_t) * GR_FIB4_TBL24_ENTRIES));
+		HCK(hipMalloc(&b.d8, sizeof(uint32_t) * 256 * (size_t)num_tbl8));
+	}
+	(void)c;
+	return 0;
+}
+
+// Stage the tbl24 ranges `rs` and tbl8 groups `gs` of the host table into
+// copy `b` in format `fmt` (DIR-16-8-8: the /16s the ranges touch, chunk
+// assignments updated on the way).
+static void fib4_stage(stager &st, vrf_fib &v, fib4_buf &b, int fmt, const std::vector<gr_fib4_range> &rs,
+		       const std::vector<uint32_t> &gs) {
+	const uint32_t *t24 = gr_fib4_tbl24(v.rib);
+	const uint32_t *t8 = gr_fib4_tbl8(v.rib);
+	if (fmt == FIB_FMT_24_W2) {
+		for (const gr_fib4_range &r : rs) {
+			uint16_t *h = st.add(b.d24_16 + r.lo, r.hi - r.lo);
+			for (uint32_t i = r.lo; i < r.hi; i++)
+				h[i - r.lo] = to16(t24[i]);
+		}
+		stage_groups(st, b.d8_16, t8, gs, to16);
+	} else if (fmt == FIB_FMT_16_8_8) {
+		const size_t top_n = 65536, chunk_n = 256;
+		uint16_t *chunks_dev = reinterpret_cast<uint16_t *>(b.d16 + top_n);
+		// the /16s the ranges touch, as sorted disjoint runs
+		std::vector<gr_fib4_range> ks;
+		for (const gr_fib4_range &r : rs) {
+			const uint32_t k_lo = r.lo >> 8, k_hi = (r.hi + 255) >> 8;
+			if (!ks.empty() && k_lo <= ks.back().hi)
+				ks.back().hi = std::max(ks.back().hi, k_hi);
+			else
+				ks.push_back({k_lo, k_hi});
+		}
+		std::vector<std::pair<uint32_t, uint32_t>> chunks; // (chunk, /16) rewritten
+		for (const gr_fib4_range &kr : ks) {
+			uint32_t *top = st.add(b.d16 + kr.lo, kr.hi - kr.lo);
+			for (uint32_t k = kr.lo; k < kr.hi; k++) {
+				const uint32_t *e = t24 + (size_t)k * 256;
+				bool uniform = !(e[0] & GR_FIB4_EXT);
+				for (uint32_t j = 1; uniform && j < 256; j++)
+					uniform = e[j] == e[0];
+				if (uniform) {
+					top[k - kr.lo] = to16(e[0]);
+					if (v.chunk_of[k] >= 0) {
+						v.chunk_free.push_back((uint32_t)v.chunk_of[k]);
+						v.chunk_of[k] = -1;
+						v.n_chunks--;
+					}
+					continue;
+				}
+				if (v.chunk_of[k] < 0) {
+					v.chunk_of[k] = (int32_t)v.chunk_free.back();
+					v.chunk_free.pop_back();
+					v.n_chunks++;
+				}
+				top[k - kr.lo] = 0x80000000u | (uint32_t)v.chunk_of[k];
+				chunks.push_back({(uint32_t)v.chunk_of[k], k});
+			}
+		}
+		std::sort(chunks.begin(), chunks.end());
+		for (size_t i = 0; i < chunks.size();) { // runs of consecutive chunks
+			size_t j = i + 1;
+			while (j < chunks.size() && chunks[j].first == chunks[j - 1].first + 1)
+				j++;
+			uint16_t *h = st.add(chunks_dev + (size_t)chunks[i].first * chunk_n, (j - i) * chunk_n);
+			for (size_t m = i; m < j; m++)
+				for (uint32_t e = 0; e < chunk_n; e++)
+					h[(m - i) * chunk_n + e] = to16(t24[(size_t)chunks[m].second * 256 + e]);
+			i = j;
+		}
+		stage_groups(st, b.d8_16, t8, gs, to16);
+	} else {
+		for (const gr_fib4_range &r : rs)
+			memcpy(st.add(b.d24 + r.lo, r.hi - r.lo), t24 + r.lo, (size_t)(r.hi - r.lo) * sizeof(uint32_t));
+		stage_groups(st, b.d8, t8, gs, [](uint32_t e) { return e; });
+	}
+}
+
+// Publish the VRF's IPv4 FIB as the host RIB holds it now: write the
+// unpublished copy (what changed since it was last written: its pending
+// list and this commit's dirty ranges, in the format the tables fit —
+// 2-byte entries while every nexthop slot and tbl8 group index fits 15
+// bits, else 4-byte), then flip (see the comment above retire_wait).
 extern "C" int gr_hip_fib4_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
-	std::lock_guard<std::shared_mutex> l(c->mu);
+	std::lock_guard<std::mutex> f(c->fib_mu);
 	hipSetDevice(c->dev);
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib == nullptr)
 		return -ENONET;
 	const bool fits16 = v.max_slot <= 0x7fff && v.num_tbl8 <= 0x8000;
 	const int want = fits16 ? c->fib_fmt : FIB_FMT_24;
-	const bool full = !v.uploaded || want != v.fmt;
-	uint32_t lo, hi;
-	gr_fib4_dirty_tbl24(v.rib, &lo, &hi);
-	std::vector<uint32_t> gs(v.num_tbl8);
-	int ng = gr_fib4_dirty_tbl8(v.rib, gs.data(), v.num_tbl8);
+	const int w = v.pub4 ^ 1;
+	fib4_buf &b = v.b4[w];
+	// this commit's changes
+	std::vector<gr_fib4_range> d24(4096);
+	std::vector<uint32_t> d8(v.num_tbl8);
+	int n24 = gr_fib4_dirty_tbl24(v.rib, d24.data(), (uint32_t)d24.size());
+	int n8 = gr_fib4_dirty_tbl8(v.rib, d8.data(), v.num_tbl8);
+	const bool d_all = n24 < 0 || n8 < 0;
+	d24.resize(n24 < 0 ? 0 : (size_t)n24);
+	d8.resize(n8 < 0 ? 0 : (size_t)n8);
+	if (!d_all && d24.empty() && d8.empty() && v.uploaded() && v.pub().fmt == want)
+		return 0; // nothing to publish
+	const bool full = d_all || v.pend_all || !b.up || b.fmt != want;
+	std::vector<gr_fib4_range> rs;
+	std::vector<uint32_t> gs;
 	if (full) {
-		lo = 0;
-		hi = GR_FIB4_TBL24_ENTRIES;
-		ng = -1;
-	}
-	if (ng >= 0)
-		gs.resize((size_t)ng);
-	else {
+		rs.push_back({0, GR_FIB4_TBL24_ENTRIES});
 		gs.resize(v.num_tbl8);
 		for (uint32_t g = 0; g < v.num_tbl8; g++)
 			gs[g] = g;
+	} else {
+		rs = range_union(v.pend24, d24, 2048);
+		gs = group_union(v.pend8, d8);
 	}
-	int r = quiesce(c);
-	if (r != 0)
-		return r;
-	const uint32_t *t24 = gr_fib4_tbl24(v.rib);
-	const uint32_t *t8 = gr_fib4_tbl8(v.rib);
-	if (want != FIB_FMT_24 && v.d8_16 == nullptr) {
-		HCK(hipStreamSynchronize(c->ctl));
-		HCK(hipMalloc(&v.d8_16, sizeof(uint16_t) * 256 * (size_t)v.num_tbl8));
-	}
-	if (want == FIB_FMT_24_W2) {
-		if (v.d24_16 == nullptr) {
-			HCK(hipStreamSynchronize(c->ctl));
-			HCK(hipMalloc(&v.d24_16, sizeof(uint16_t) * GR_FIB4_TBL24_ENTRIES));
-		}
-		std::vector<uint16_t> h24(hi > lo ? hi - lo : 0);
-		for (uint32_t i = lo; i < hi; i++)
-			h24[i - lo] = to16(t24[i]);
-		std::vector<uint16_t> h8((size_t)v.num_tbl8 * 256);
-		for (uint32_t g : gs)
-			for (uint32_t k = 0; k < 256; k++)
-				h8[(size_t)g * 256 + k] = to16(t8[(size_t)g * 256 + k]);
-		if (hi > lo)
-			r = h2d(c, v.d24_16 + lo, h24.data(), h24.size() * sizeof(uint16_t));
-		if (r == 0)
-			r = upload_groups<uint16_t>(c, v.d8_16, h8.data(), gs);
-		if (r == 0)
-			r = ctl_sync(c); // the staging vectors go out of scope
-	} else if (want == FIB_FMT_16_8_8) {
-		const size_t top_n = 65536, chunk_n = 256;
-		if (v.d16 == nullptr) {
-			HCK(hipStreamSynchronize(c->ctl));
-			// top + the worst case of one chunk per /16
-			HCK(hipMalloc(&v.d16, sizeof(uint32_t) * top_n + sizeof(uint16_t) * chunk_n * top_n));
-		}
-		if (full || v.chunk_of.empty()) {
-			v.chunk_of.assign(top_n, -1);
+	const uint32_t B = c->gen ^ 1; // the generation this commit writes
+	int r;
+	{
+		std::shared_lock<std::shared_mutex> l(c->mu); // submitters go on
+		r = fib4_buf_alloc(c, b, want, v.num_tbl8);
+		if (r != 0)
+			return r;
+		if (want == FIB_FMT_16_8_8 && (v.chunk_of.empty() || (full && !(v.pub().up && v.pub().fmt == FIB_FMT_16_8_8)))) {
+			// no copy uses the chunk assignment: start afresh
+			v.chunk_of.assign(65536, -1);
 			v.chunk_free.clear();
-			for (uint32_t k = 0; k < top_n; k++)
-				v.chunk_free.push_back((uint32_t)(top_n - 1 - k));
+			for (uint32_t k = 0; k < 65536; k++)
+				v.chunk_free.push_back(65535 - k);
 			v.n_chunks = 0;
 		}
-		uint16_t *chunks_dev = reinterpret_cast<uint16_t *>(v.d16 + top_n);
-		// rebuild the dirty /16s
-		uint32_t k_lo = lo >> 8, k_hi = (hi + 255) >> 8;
-		std::vector<uint32_t> top(k_hi > k_lo ? k_hi - k_lo : 0);
-		std::vector<uint16_t> cbuf;
-		std::vector<uint32_t> cidx;
-		for (uint32_t k = k_lo; k < k_hi; k++) {
-			const uint32_t *e = t24 + (size_t)k * 256;
-			bool uniform = !(e[0] & GR_FIB4_EXT);
-			for (uint32_t j = 1; uniform && j < 256; j++)
-				uniform = e[j] == e[0];
-			if (uniform) {
-				top[k - k_lo] = to16(e[0]);
-				if (v.chunk_of[k] >= 0) {
-					v.chunk_free.push_back((uint32_t)v.chunk_of[k]);
-					v.chunk_of[k] = -1;
-					v.n_chunks--;
-				}
-				continue;
-			}
-			if (v.chunk_of[k] < 0) {
-				v.chunk_of[k] = (int32_t)v.chunk_free.back();
-				v.chunk_free.pop_back();
-				v.n_chunks++;
-			}
-			top[k - k_lo] = 0x80000000u | (uint32_t)v.chunk_of[k];
-			cidx.push_back((uint32_t)v.chunk_of[k]);
-			for (uint32_t j = 0; j < 256; j++)
-				cbuf.push_back(to16(e[j]));
+		stager st(c);
+		fib4_stage(st, v, b, want, rs, gs);
+		b.fmt = want;
+		b.up = true;
+		views_follow_published(c, B);
+		v.sel4[B] = (uint8_t)w;
+		r = retire_wait(c); // no launch may still read copy w or generation B's views
+		if (r == 0)
+			r = st.flush();
+		if (r == 0)
+			r = upload_rx(c, B);
+		if (r == 0)
+			r = ctl_sync(c); // the generation is complete before anyone takes it
+		if (r != 0) {
+			b.up = false; // half written: rewritten in full next time
+			views_follow_published(c, B);
+			return r;
 		}
-		std::vector<uint16_t> h8((size_t)v.num_tbl8 * 256);
-		for (uint32_t g : gs)
-			for (uint32_t k = 0; k < 256; k++)
-				h8[(size_t)g * 256 + k] = to16(t8[(size_t)g * 256 + k]);
-		if (k_hi > k_lo)
-			r = h2d(c, v.d16 + k_lo, top.data(), top.size() * sizeof(uint32_t));
-		for (size_t i = 0; i < cidx.size() && r == 0;) { // runs of consecutive chunks
-			size_t j = i + 1;
-			while (j < cidx.size() && cidx[j] == cidx[j - 1] + 1)
-				j++;
-			r = h2d(c, chunks_dev + (size_t)cidx[i] * chunk_n, cbuf.data() + i * chunk_n,
-				(j - i) * chunk_n * sizeof(uint16_t));
-			i = j;
-		}
-		if (r == 0)
-			r = upload_groups<uint16_t>(c, v.d8_16, h8.data(), gs);
-		if (r == 0)
-			r = ctl_sync(c); // the staging vectors go out of scope
-	} else {
-		if (v.d24 == nullptr) {
-			HCK(hipStreamSynchronize(c->ctl));
-			HCK(hipMalloc(&v.d24, sizeof(uint32_t) * GR_FIB4_TBL24_ENTRIES));
-			HCK(hipMalloc(&v.d8, sizeof(uint32_t) * 256 * (size_t)v.num_tbl8));
-		}
-		if (hi > lo)
-			r = h2d(c, v.d24 + lo, t24 + lo, (size_t)(hi - lo) * sizeof(uint32_t));
-		if (r == 0)
-			r = upload_groups<uint32_t>(c, v.d8, t8, gs);
-		if (r == 0)
-			r = ctl_sync(c);
 	}
-	if (r != 0)
-		return r;
 	gr_fib4_dirty_clear(v.rib);
-	bool repoint = full;
-	v.fmt = want;
-	v.uploaded = true;
-	if (repoint)
-		r = upload_views(c, true, 0, 0, false);
-	return r;
+	return publish(c, B, [&] {
+		const bool old_up = v.pub().up;
+		v.pub4 = w;
+		// the copy just unpublished misses this commit's changes
+		v.pend_all = d_all || !old_up;
+		v.pend24 = std::move(d24);
+		v.pend8 = std::move(d8);
+	});
 }
 
 extern "C" int gr_hip_fib4_lookup_host(gr_hip_ctx_t *c, uint16_t vrf, uint32_t ip_be, uint32_t *nh) {
 	if (c == nullptr || nh == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
-	std::lock_guard<std::shared_mutex> l(c->mu);
+	std::lock_guard<std::mutex> f(c->fib_mu);
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib == nullptr)
 		return -ENONET;
@@ -1184,7 +1398,7 @@ extern "C" int gr_hip_fib4_lookup_host(gr_hip_ctx_t *c, uint16_t vrf, uint32_t i
 extern "C" int gr_hip_fib4_info(gr_hip_ctx_t *c, uint16_t vrf, uint32_t *n_routes, uint32_t *tbl8_used, uint64_t *bytes) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
-	std::lock_guard<std::shared_mutex> l(c->mu);
+	std::lock_guard<std::mutex> f(c->fib_mu);
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib == nullptr)
 		return -ENONET;
@@ -1192,10 +1406,11 @@ extern "C" int gr_hip_fib4_info(gr_hip_ctx_t *c, uint16_t vrf, uint32_t *n_route
 		*n_routes = gr_fib4_n_routes(v.rib);
 	if (tbl8_used)
 		*tbl8_used = gr_fib4_tbl8_used(v.rib);
-	if (bytes) // device bytes a lookup can touch
-		*bytes = v.fmt == FIB_FMT_16_8_8 ? 4ull * 65536 + 512ull * v.n_chunks + 512ull * v.num_tbl8
-			 : v.fmt == FIB_FMT_24_W2 ? 2ull * GR_FIB4_TBL24_ENTRIES + 512ull * v.num_tbl8
-						  : 4ull * GR_FIB4_TBL24_ENTRIES + 1024ull * v.num_tbl8;
+	const int fmt = v.pub().fmt;
+	if (bytes) // device bytes a lookup can touch (the published copy)
+		*bytes = fmt == FIB_FMT_16_8_8 ? 4ull * 65536 + 512ull * v.n_chunks + 512ull * v.num_tbl8
+			 : fmt == FIB_FMT_24_W2 ? 2ull * GR_FIB4_TBL24_ENTRIES + 512ull * v.num_tbl8
+						: 4ull * GR_FIB4_TBL24_ENTRIES + 1024ull * v.num_tbl8;
 	return 0;
 }
 
@@ -1213,12 +1428,12 @@ static void scope6(uint8_t out[16], const uint8_t ip[16], uint16_t iface_id) {
 	}
 }
 
-// IPv6 routes on the device over all VRFs: the launches stage the IPv6
-// fast adjacencies in LDS only when there are some. Caller holds c->mu.
+// IPv6 routes published, all VRFs: the launches stage the IPv6 fast
+// adjacencies in LDS only when there are some. Caller holds c->mu exclusively.
 static void count_v6(gr_hip_ctx *c) {
 	uint32_t n = 0;
 	for (const vrf_fib &v : c->vrfs)
-		if (v.rib6 != nullptr && v.uploaded6)
+		if (v.rib6 != nullptr && v.uploaded6())
 			n += gr_fib6_n_routes(v.rib6);
 	c->v6_routes = n;
 }
@@ -1226,6 +1441,7 @@ static void count_v6(gr_hip_ctx *c) {
 extern "C" int gr_hip_fib6_create(gr_hip_ctx_t *c, uint16_t vrf, uint32_t max_routes, uint32_t num_tbl8) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces || max_routes == 0)
 		return -EINVAL;
+	std::lock_guard<std::mutex> f(c->fib_mu);
 	std::lock_guard<std::shared_mutex> l(c->mu);
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib6 != nullptr)
@@ -1237,34 +1453,34 @@ extern "C" int gr_hip_fib6_create(gr_hip_ctx_t *c, uint16_t vrf, uint32_t max_ro
 extern "C" int gr_hip_fib6_destroy(gr_hip_ctx_t *c, uint16_t vrf) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
+	std::lock_guard<std::mutex> f(c->fib_mu);
 	std::lock_guard<std::shared_mutex> l(c->mu);
 	hipSetDevice(c->dev);
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib6 == nullptr)
 		return -ENOENT;
-	bool was = v.uploaded6;
-	v.uploaded6 = false; // make_rx6() stops pointing at it
+	gr_fib6_t *rib6 = v.rib6;
+	v.rib6 = nullptr; // make_rx6() stops pointing at it
 	int r = quiesce(c);
 	if (r == 0)
 		r = upload_views(c, true, 0, 0, false);
 	if (r != 0) {
-		v.uploaded6 = was;
+		v.rib6 = rib6;
 		return r;
 	}
-	hipFree(v.d6);
-	gr_fib6_free(v.rib6);
-	v.rib6 = nullptr;
-	v.d6 = nullptr;
-	v.d6_groups = 0;
+	v.b6[0].free_all();
+	v.b6[1].free_all();
+	v.pub6 = 1;
+	v.sel6[0] = v.sel6[1] = 1;
+	gr_fib6_free(rib6);
 	count_v6(c);
-	v.gen6 = 0;
 	return 0;
 }
 
 extern "C" int gr_hip_route6_add(gr_hip_ctx_t *c, const struct gr_hip_route6 *rt, uint32_t n, int replace) {
 	if (c == nullptr || (rt == nullptr && n))
 		return -EINVAL;
-	std::lock_guard<std::shared_mutex> l(c->mu);
+	std::lock_guard<std::mutex> f(c->fib_mu); // the host RIB only
 	for (uint32_t i = 0; i < n; i++) {
 		if (rt[i].vrf_id == 0 || rt[i].vrf_id >= c->max_ifaces || rt[i].nh == 0 || rt[i].nh > c->max_nh
 		    || rt[i].prefixlen > 128)
@@ -1284,7 +1500,7 @@ extern "C" int gr_hip_route6_add(gr_hip_ctx_t *c, const struct gr_hip_route6 *rt
 extern "C" int gr_hip_route6_del(gr_hip_ctx_t *c, uint16_t vrf, uint16_t iface_id, const uint8_t ip[16], uint8_t len) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces || ip == nullptr || len > 128)
 		return -EINVAL;
-	std::lock_guard<std::shared_mutex> l(c->mu);
+	std::lock_guard<std::mutex> f(c->fib_mu);
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib6 == nullptr)
 		return -ENONET;
@@ -1293,13 +1509,13 @@ extern "C" int gr_hip_route6_del(gr_hip_ctx_t *c, uint16_t vrf, uint16_t iface_i
 	return gr_fib6_del(v.rib6, key, len);
 }
 
-// Stream-ordered publication of a repainted trie (fib6.h): quiesce the
-// queues, upload the first level and the groups in use, point the IPv6
-// views at the table on its first upload.
+// Publish a repainted trie (fib6.h): the first level and the groups and
+// skips in use, written whole into the unpublished copy, then the same flip
+// as gr_hip_fib4_commit.
 extern "C" int gr_hip_fib6_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
-	std::lock_guard<std::shared_mutex> l(c->mu);
+	std::lock_guard<std::mutex> f(c->fib_mu);
 	hipSetDevice(c->dev);
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib6 == nullptr)
@@ -1307,42 +1523,55 @@ extern "C" int gr_hip_fib6_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 	int r = gr_fib6_build(v.rib6);
 	if (r < 0)
 		return r;
-	if (v.uploaded6 && v.gen6 == gr_fib6_generation(v.rib6))
+	const uint64_t gen = gr_fib6_generation(v.rib6);
+	if (v.uploaded6() && v.b6[v.pub6].gen == gen)
 		return 0;
-	r = quiesce(c);
-	if (r != 0)
-		return r;
-	const uint32_t groups = gr_fib6_groups_used(v.rib6), skips = gr_fib6_skips_used(v.rib6);
-	if (v.d6 == nullptr) { // sized for the VRF's group capacity once: top, groups, skips
-		const uint32_t cap = gr_fib6_max_groups(v.rib6);
-		HCK(hipMalloc(&v.d6, ((size_t)GR_FIB6_TOP + (size_t)cap * GR_FIB6_GROUP) * sizeof(uint32_t)
-					     + (size_t)cap * sizeof(gr_fib6_skip)));
-		v.d6_groups = cap;
+	const int w = v.pub6 ^ 1;
+	fib6_buf &b = v.b6[w];
+	const uint32_t B = c->gen ^ 1;
+	{
+		std::shared_lock<std::shared_mutex> l(c->mu); // submitters go on
+		const uint32_t groups = gr_fib6_groups_used(v.rib6), skips = gr_fib6_skips_used(v.rib6);
+		if (b.d6 == nullptr) { // sized for the VRF's group capacity once: top, groups, skips
+			const uint32_t cap = gr_fib6_max_groups(v.rib6);
+			HCK(hipMalloc(&b.d6, ((size_t)GR_FIB6_TOP + (size_t)cap * GR_FIB6_GROUP) * sizeof(uint32_t)
+						     + (size_t)cap * sizeof(gr_fib6_skip)));
+			b.groups = cap;
+		}
+		stager st(c);
+		memcpy(st.add(b.d6, GR_FIB6_TOP), gr_fib6_top(v.rib6), (size_t)GR_FIB6_TOP * sizeof(uint32_t));
+		if (groups)
+			memcpy(st.add(b.d6 + GR_FIB6_TOP, (size_t)groups * GR_FIB6_GROUP), gr_fib6_groups(v.rib6),
+			       (size_t)groups * GR_FIB6_GROUP * sizeof(uint32_t));
+		if (skips)
+			memcpy(st.add(reinterpret_cast<gr_fib6_skip *>(b.d6 + GR_FIB6_TOP + (size_t)b.groups * GR_FIB6_GROUP),
+				      skips),
+			       gr_fib6_skips(v.rib6), (size_t)skips * sizeof(gr_fib6_skip));
+		b.gen = gen;
+		b.up = true;
+		views_follow_published(c, B);
+		v.sel6[B] = (uint8_t)w;
+		r = retire_wait(c);
+		if (r == 0)
+			r = st.flush();
+		if (r == 0)
+			r = upload_rx(c, B);
+		if (r == 0)
+			r = ctl_sync(c);
+		if (r != 0) {
+			b.up = false;
+			views_follow_published(c, B);
+			return r;
+		}
 	}
-	r = h2d(c, v.d6, gr_fib6_top(v.rib6), (size_t)GR_FIB6_TOP * sizeof(uint32_t));
-	if (r == 0 && groups)
-		r = h2d(c, v.d6 + GR_FIB6_TOP, gr_fib6_groups(v.rib6), (size_t)groups * GR_FIB6_GROUP * sizeof(uint32_t));
-	if (r == 0 && skips)
-		r = h2d(c, v.d6 + GR_FIB6_TOP + (size_t)v.d6_groups * GR_FIB6_GROUP, gr_fib6_skips(v.rib6),
-			(size_t)skips * sizeof(gr_fib6_skip));
-	if (r == 0)
-		r = ctl_sync(c);
-	if (r != 0)
-		return r;
-	v.gen6 = gr_fib6_generation(v.rib6);
-	if (!v.uploaded6) {
-		v.uploaded6 = true;
-		r = upload_views(c, true, 0, 0, false);
-	}
-	count_v6(c);
-	return r;
+	return publish(c, B, [&] { v.pub6 = w; });
 }
 
 extern "C" int gr_hip_fib6_lookup_host(gr_hip_ctx_t *c, uint16_t vrf, uint16_t iface_id, const uint8_t ip[16],
 				       uint32_t *nh) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces || ip == nullptr || nh == nullptr)
 		return -EINVAL;
-	std::shared_lock<std::shared_mutex> l(c->mu);
+	std::lock_guard<std::mutex> f(c->fib_mu);
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib6 == nullptr)
 		return -ENONET;
@@ -1356,7 +1585,7 @@ extern "C" int gr_hip_fib6_info(gr_hip_ctx_t *c, uint16_t vrf, uint32_t *n_route
 				uint64_t *bytes) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
-	std::shared_lock<std::shared_mutex> l(c->mu);
+	std::lock_guard<std::mutex> f(c->fib_mu);
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib6 == nullptr)
 		return -ENONET;
@@ -1397,6 +1626,8 @@ extern "C" int gr_hip_queue_create(gr_hip_ctx_t *c, void *stream, gr_hip_queue_t
 		hipEventCreate(&q->ev1[i]);
 	}
 	hipEventCreateWithFlags(&q->quiesce, hipEventDisableTiming);
+	hipEventCreateWithFlags(&q->retire, hipEventDisableTiming);
+	hipEventRecord(q->retire, q->s); // nothing submitted yet
 	if (hipHostMalloc(reinterpret_cast<void **>(&q->h_err), sizeof(uint32_t), hipHostMallocMapped) == hipSuccess) {
 		*q->h_err = 0;
 		if (hipHostGetDevicePointer(reinterpret_cast<void **>(&q->d_err), q->h_err, 0) != hipSuccess) {
@@ -1436,6 +1667,7 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 		hipEventDestroy(q->ev1[i]);
 	}
 	hipEventDestroy(q->quiesce);
+	hipEventDestroy(q->retire);
 	hipFree(q->d_stats);
 	hipHostFree(q->h_err);
 	hipHostFree(q->node_lines);
@@ -1446,10 +1678,13 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 	if (q->own_stream)
 		hipStreamDestroy(q->s);
 	(void)hipGetLastError();
-	for (size_t i = 0; i < c->queues.size(); i++) {
-		if (c->queues[i] == q) {
-			c->queues.erase(c->queues.begin() + (long)i);
-			break;
+	{
+		std::lock_guard<std::shared_mutex> l(c->mu); // quiesce() and publish() walk the list
+		for (size_t i = 0; i < c->queues.size(); i++) {
+			if (c->queues[i] == q) {
+				c->queues.erase(c->queues.begin() + (long)i);
+				break;
+			}
 		}
 	}
 	delete q;
@@ -1482,7 +1717,7 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	A.meta = b->meta;
 	A.verdicts = b->verdicts;
 	A.stats = q->d_stats;
-	A.T = c->d_tables;
+	A.T = c->d_tables[c->gen]; // the generation published when this launch is enqueued
 	A.n = b->n;
 	A.in_stride = b->in_stride;
 	A.out_stride = b->out_stride;
@@ -1599,9 +1834,9 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		c->host_direct = value != 0;
 	} else if (strcmp(key, "fib_format_of") == 0) { // read: the format VRF `value` is on the device in
 		if (value <= 0 || (uint32_t)value >= c->max_ifaces || c->vrfs[value].rib == nullptr
-		    || !c->vrfs[value].uploaded)
+		    || !c->vrfs[value].uploaded())
 			return -ENONET;
-		return c->vrfs[value].fmt;
+		return c->vrfs[value].pub().fmt;
 	} else if (strcmp(key, "fib16") == 0) { // older key: 0 = 4-byte DIR24_8, else DIR-16-8-8
 		c->fib_fmt = value ? FIB_FMT_16_8_8 : FIB_FMT_24;
 	} else if (strcmp(key, "ring") == 0) { // ring geometry, fwd4_ring.hip ring_cfgN

@@ -1,0 +1,168 @@
+# SPDX-License-Identifier: BSD-3-Clause
+"""Double-buffered FIB publication (gr_hip_fib4_commit).
+
+Each VRF has two device copies of its tables; a commit writes the
+unpublished one (its pending list of what it missed, plus the new dirty
+ranges) and flips the view generation new launches take. grout's datapath
+never waits for a route change either (rte_fib under RCU,
+modules/ip/control/route.c:87-95); here a launch sees one table from its
+first packet to its last.
+
+  * a run of commits, each checked against the oracle, so the copies
+    alternate and the pending lists are exercised, in every device format;
+  * launches submitted from another thread while the FIB toggles between
+    two states: every launch's verdicts equal the oracle's for one state or
+    the other, whole (no launch reads a half-written copy)."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import oracle
+import scenarios as SC
+from golden_util import fresh_fastpath_state, run_gpu
+from grout_amd import abi
+from grout_amd import topology as T
+
+pytestmark = pytest.mark.gpu
+
+
+def _route(cidr, slot):
+    net = T.ipaddress.IPv4Network(cidr)
+    r = np.zeros(1, dtype=abi.ROUTE_DT)
+    r["ip"], r["prefixlen"], r["vrf_id"], r["nh"] = int(net.network_address), net.prefixlen, 1, slot
+    return r
+
+
+def _apply(fp, o, ops, nh):
+    for op in ops:
+        net = T.ipaddress.IPv4Network(op[1])
+        if op[0] in ("add", "rep"):
+            r = _route(op[1], nh[op[2]])
+            fp.route_add(r, replace=op[0] == "rep")
+            assert o.L.or_route_add(o.h, r.ctypes.data, 1, 1 if op[0] == "rep" else 0) == 0
+        else:
+            fp.route_del(1, int(net.network_address), net.prefixlen)
+            be = int.from_bytes(int(net.network_address).to_bytes(4, "big"), "little")
+            assert o.L.or_route_del(o.h, 1, be, net.prefixlen) == 0
+
+
+# each step is committed and checked; together they make /16s go from
+# uniform to chunked and back (DIR-16-8-8), tbl8 groups get freed and
+# reused, and one commit has nothing to publish
+STEPS = [
+    [("add", "200.1.0.0/16", "fwd")],
+    [("add", "16.1.0.0/17", "fwd2"), ("del", "10.90.1.7/32")],
+    [("add", "10.66.1.0/24", "fwd"), ("rep", "16.1.0.0/17", "fwd3")],
+    [("add", "16.1.5.5/32", "fwd2")],
+    [("del", "16.1.5.5/32"), ("add", "16.1.9.9/32", "fwd3")],
+    [("add", "0.0.0.0/0", "fwd3"), ("del", "10.66.1.0/24")],
+    [],
+    [("del", "10.70.0.0/16"), ("del", "200.1.0.0/16"), ("del", "16.1.9.9/32")],
+    [("del", "0.0.0.0/0"), ("del", "16.1.0.0/17")],
+]
+
+
+@pytest.mark.parametrize("fmt", [2, 1, 0])
+def test_commit_sequence(fastpath, fmt):
+    t, nh = SC.corpus_topology()
+    fr, me, lab = SC.corpus_arrays()
+    fastpath.tune("fib_format", fmt)
+    fresh_fastpath_state(fastpath, T.config_single_route())  # force a reload in this format
+    try:
+        run_gpu(fastpath, t, fr, me)  # loads t: first commit
+        o = oracle.Oracle(t, build_dir24=False)
+        for i, ops in enumerate(STEPS):
+            _apply(fastpath, o, ops, nh)
+            fastpath.fib_commit(1)
+            o.L.or_fib_build(o.h, 1)
+            g = run_gpu(fastpath, t, fr, me)
+            ref = o.process(fr, me)
+            bad = np.nonzero(ref[1] != g[1])[0]
+            assert len(bad) == 0, (i, [(lab[k], ref[1][k], g[1][k]) for k in bad[:6]])
+            assert np.array_equal(ref[0], g[0]), i
+        assert fastpath.tune("fib_format_of", 1) == fmt
+    finally:
+        fastpath.tune("fib_format", 2)
+        fresh_fastpath_state(fastpath, T.config_single_route())  # drop the modified state
+
+
+TOGGLE_B = [("rep", "16.1.0.0/16", "fwd2"), ("rep", "10.70.0.0/16", "fwd"), ("add", "16.1.7.0/25", "fwd3")]
+TOGGLE_A = [("rep", "16.1.0.0/16", "fwd"), ("rep", "10.70.0.0/16", "grp"), ("del", "16.1.7.0/25")]
+
+
+@pytest.mark.parametrize("fmt", [2, 1])
+def test_snapshot_under_churn(fastpath, fmt):
+    import torch
+
+    from grout_amd.fwd import shared_stream
+
+    t, nh = SC.corpus_topology()
+    fr, me, _ = SC.corpus_arrays()
+    fastpath.tune("fib_format", fmt)
+    fresh_fastpath_state(fastpath, T.config_single_route())
+    try:
+        run_gpu(fastpath, t, fr, me)
+        # the expected verdicts of each state, on the corpus
+        oa = oracle.Oracle(t, build_dir24=False)
+        va = oa.process(fr, me)[1].view("<u8")
+        ob = oracle.Oracle(t, build_dir24=False)
+        for op in TOGGLE_B:  # oracle only
+            r = _route(op[1], nh[op[2]])
+            assert ob.L.or_route_add(ob.h, r.ctypes.data, 1, 1 if op[0] == "rep" else 0) == 0
+        ob.L.or_fib_build(ob.h, 1)
+        vb = ob.process(fr, me)[1].view("<u8")
+        assert (va != vb).sum() > 4  # the two states tell apart
+        # a batch of the corpus tiled, launched K times into K verdict buffers
+        reps, K = 2048, 40
+        n = len(me) * reps
+        dev = torch.device("cuda")
+        fin = torch.from_numpy(np.ascontiguousarray(np.tile(fr, (reps, 1))).reshape(-1)).to(dev)
+        mt = torch.from_numpy(np.tile(me, reps).view(np.uint8)).to(dev)
+        outs = [torch.empty(n * abi.LINE, dtype=torch.uint8, device=dev) for _ in range(2)]
+        vs = [torch.zeros(n * 8, dtype=torch.uint8, device=dev) for _ in range(K)]
+        q = fastpath.queue(shared_stream(dev))
+        stop = threading.Event()
+        err = []
+
+        def submitter():
+            try:
+                for k in range(K):
+                    q.submit(fin, outs[k & 1], mt, vs[k], n, in_stride=fr.shape[1])
+                    time.sleep(0.002)
+            except Exception as e:  # pragma: no cover - reported below
+                err.append(e)
+            finally:
+                stop.set()
+
+        th = threading.Thread(target=submitter)
+        dummy = oracle.Oracle(t, build_dir24=False)  # absorbs _apply's oracle half
+        commits, state = 0, "A"
+        th.start()
+        while not stop.is_set():
+            _apply(fastpath, dummy, TOGGLE_B if state == "A" else TOGGLE_A, nh)
+            fastpath.fib_commit(1)
+            state = "B" if state == "A" else "A"
+            commits += 1
+        th.join()
+        q.sync()
+        assert not err, err
+        seen = []
+        for k in range(K):
+            got = vs[k].cpu().numpy().view("<u8").reshape(reps, len(me))
+            if (got == va).all():
+                seen.append("A")
+            elif (got == vb).all():
+                seen.append("B")
+            else:
+                rows = np.nonzero((got != va).any(axis=1) & (got != vb).any(axis=1))[0]
+                pytest.fail(f"launch {k}: {len(rows)} tiles match neither state (commits {commits})")
+        assert commits >= 4 and {"A", "B"} <= set(seen), (commits, seen)
+        q.close()
+        if state == "B":  # leave state A
+            _apply(fastpath, dummy, TOGGLE_A, nh)
+            fastpath.fib_commit(1)
+    finally:
+        fastpath.tune("fib_format", 2)
+        fresh_fastpath_state(fastpath, T.config_single_route())
