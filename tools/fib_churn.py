@@ -1,0 +1,178 @@
+# SPDX-License-Identifier: BSD-3-Clause
+"""FIB load rate and forwarding under route churn.
+
+1. Load: the 1M-route fib_inject -4 view (smoke/fib_inject.c:245-254 times
+   the injection and prints routes/s) into an empty VRF, one route per
+   gr_hip_route4_add call like fib_inject's one request per route, then one
+   commit; and again in one batched call. routes/s = routes / (adds + commit).
+2. Churn: the headline batch (2^24 packets over that view) submitted back to
+   back for --seconds, without and then with a control thread applying
+   --rate route changes per second (nexthop replacements, deletes and
+   re-adds of random full-view routes, in --period-ms batches, one commit
+   per batch). Mpps by wall clock over each window, and the commit latency.
+
+    python tools/fib_churn.py [--seconds 3] [--rate 10000] [--period-ms 10] > out.json
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=3.0)
+    ap.add_argument("--rate", type=int, default=10_000, help="route changes per second")
+    ap.add_argument("--period-ms", type=float, default=10.0, help="one commit per period")
+    ap.add_argument("--batch", type=int, default=1 << 24)
+    ap.add_argument("--no-per-route", action="store_true")
+    args = ap.parse_args()
+    import torch
+
+    from grout_amd import abi
+    from grout_amd import synth as S
+    from grout_amd import topology as T
+    from grout_amd.fwd import FastPath, shared_stream
+
+    out = {"tool": "fib_churn"}
+    topo = T.config_fullview()
+    routes = topo.route_array()
+    count = 1_000_000
+    view = routes[:count]
+    vrf = int(view["vrf_id"][0])
+
+    def fresh():
+        fp = FastPath(0)
+        fp.set_ifaces(topo.ifaces)
+        fp.set_nexthops(topo.nh[1:topo.n_nh + 1], first=1)
+        fp.set_reta(topo.reta)
+        for v, (mr, nt) in topo.fibs.items():
+            fp.fib_create(v, mr, nt)
+        return fp
+
+    # 1. load rates
+    if not args.no_per_route:
+        fp = fresh()
+        L, h = fp.lib, fp.h
+        base = view.ctypes.data
+        t0 = time.perf_counter()
+        for i in range(count):
+            r = L.gr_hip_route4_add(h, ctypes.c_void_p(base + 12 * i), 1, 0)
+            if r:
+                abi.check("gr_hip_route4_add", r)
+        t1 = time.perf_counter()
+        fp.fib_commit(vrf)
+        t2 = time.perf_counter()
+        out["load_per_route"] = {"routes": count, "add_s": round(t1 - t0, 3), "commit_s": round(t2 - t1, 4),
+                                 "routes_per_s": round(count / (t2 - t0)),
+                                 "note": "one gr_hip_route4_add per route from Python ctypes, then one commit"}
+        print(json.dumps(out["load_per_route"]), file=sys.stderr, flush=True)
+        fp.close()
+    fp = fresh()
+    t0 = time.perf_counter()
+    fp.route_add(view)
+    t1 = time.perf_counter()
+    fp.fib_commit(vrf)
+    t2 = time.perf_counter()
+    fp.route_add(routes[count:])  # the address route: the bench topology exactly
+    fp.fib_commit(vrf)
+    t3 = time.perf_counter()
+    out["load_batched"] = {"routes": count, "add_s": round(t1 - t0, 3), "commit_s": round(t2 - t1, 4),
+                           "routes_per_s": round(count / (t2 - t0)),
+                           "second_commit_s": round(t3 - t2, 4),
+                           "note": "one gr_hip_route4_add of all routes, then one commit (the first writes one "
+                                   "copy whole; the second commit writes the other copy whole)"}
+    print(json.dumps(out["load_batched"]), file=sys.stderr, flush=True)
+
+    # 2. churn
+    dev = torch.device("cuda", 0)
+    n = args.batch
+    frames, meta = S.stream(n, S.SEED_GPU_BASE, routes=routes)
+    fin = torch.from_numpy(frames.reshape(-1)).to(dev)
+    me = torch.from_numpy(meta.view(np.uint8)).to(dev)
+    fo = torch.empty(n * abi.LINE, dtype=torch.uint8, device=dev)
+    vo = torch.empty(n * 8, dtype=torch.uint8, device=dev)
+    del frames
+    q = fp.queue(shared_stream(dev))
+    fp.tune("untimed", 1)
+
+    def forward(seconds):
+        launches = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            for _ in range(4):
+                q.submit(fin, fo, me, vo, n)
+            q.sync()
+            launches += 4
+        dt = time.perf_counter() - t0
+        return {"launches": launches, "s": round(dt, 3), "mpps": round(launches * n / dt / 1e6, 1)}
+
+    forward(0.5)  # warm-up
+    base = forward(args.seconds)
+    print(json.dumps({"base": base}), file=sys.stderr, flush=True)
+
+    nh_slots = np.unique(view["nh"])
+    rng = np.random.default_rng(0xC4A9)
+    per_commit = max(1, int(round(args.rate * args.period_ms / 1000)))
+    stop = threading.Event()
+    lat, applied = [], [0]
+    deleted = []
+    live = np.ones(count, dtype=bool)
+
+    def control():
+        period = args.period_ms / 1000
+        nxt = time.perf_counter()
+        while not stop.is_set():
+            k_rep = per_commit // 2
+            k_del = (per_commit - k_rep) // 2
+            k_add = per_commit - k_rep - k_del
+            idx = rng.choice(np.nonzero(live)[0], size=k_rep + k_del, replace=False)
+            rep = view[idx[:k_rep]].copy()
+            rep["nh"] = rng.choice(nh_slots, size=k_rep)
+            t0 = time.perf_counter()
+            fp.route_add(rep, replace=True)
+            for i in idx[k_rep:]:
+                fp.route_del(vrf, int(view["ip"][i]), int(view["prefixlen"][i]))
+                live[i] = False
+                deleted.append(i)
+            back = [deleted.pop(0) for _ in range(min(k_add, len(deleted) - k_del))] if len(deleted) > k_del else []
+            if back:
+                fp.route_add(view[np.array(back)])
+                live[np.array(back)] = True
+            fp.fib_commit(vrf)
+            lat.append(time.perf_counter() - t0)
+            applied[0] += k_rep + k_del + len(back)
+            nxt += period
+            d = nxt - time.perf_counter()
+            if d > 0:
+                time.sleep(d)
+
+    th = threading.Thread(target=control)
+    t0 = time.perf_counter()
+    th.start()
+    churn = forward(args.seconds)
+    stop.set()
+    th.join()
+    dt = time.perf_counter() - t0
+    la = np.array(lat) * 1e3
+    churn.update({"route_changes": applied[0], "changes_per_s": round(applied[0] / dt),
+                  "commits": len(lat), "commit_ms_p50": round(float(np.percentile(la, 50)), 3),
+                  "commit_ms_p99": round(float(np.percentile(la, 99)), 3), "commit_ms_max": round(float(la.max()), 3),
+                  "changes_per_commit": per_commit})
+    out.update({"batch": n, "base": base, "churn": churn, "mpps_ratio": round(churn["mpps"] / base["mpps"], 4),
+                "note": "wall-clock Mpps, submits of 4 launches then a sync, untimed launches; commit latency = "
+                        "route adds/deletes + gr_hip_fib4_commit"})
+    print(json.dumps(out), flush=True)
+    q.close()
+    fp.close()
+
+
+if __name__ == "__main__":
+    main()
