@@ -53,7 +53,11 @@ typedef ring_cfg<16, 2, 2, 16, 6> ring_cfg5;
 typedef ring_cfg<16, 3, 1, 20, 4> ring_cfg6;
 typedef ring_cfg<16, 4, 2, 24, 3> ring_cfg7;
 typedef ring_cfg<16, 2, 2, 16, 8> ring_cfg8;
-#define RING_NCFG 9
+// two workgroups per CU (8 slots each): more compute waves per CU
+typedef ring_cfg<14, 1, 1, 8, 8> ring_cfg9;
+typedef ring_cfg<14, 2, 2, 8, 4> ring_cfg10;
+typedef ring_cfg<12, 1, 1, 8, 8> ring_cfg11;
+#define RING_NCFG 12
 
 template <class C, bool PTRS>
 struct ring_lds {
@@ -431,6 +435,7 @@ static const ring_entry ring_kernels[RING_NCFG] = {
 	RING_ENTRY(ring_cfg0), RING_ENTRY(ring_cfg1), RING_ENTRY(ring_cfg2),
 	RING_ENTRY(ring_cfg3), RING_ENTRY(ring_cfg4), RING_ENTRY(ring_cfg5),
 	RING_ENTRY(ring_cfg6), RING_ENTRY(ring_cfg7), RING_ENTRY(ring_cfg8),
+	RING_ENTRY(ring_cfg9), RING_ENTRY(ring_cfg10), RING_ENTRY(ring_cfg11),
 };
 
 // Frame-pointer batches (GR_HIP_BATCH_F_FRAME_PTRS) run on geometry 2, the

@@ -551,7 +551,7 @@ def test_high_slots_fall_back_to_4byte_fib(fastpath):
     assert g[1]["nh"].min() >= first and g[1]["nh"].max() > (1 << 15)
 
 
-@pytest.mark.parametrize("cfg", range(9))
+@pytest.mark.parametrize("cfg", range(12))
 def test_ring_geometries(fastpath, cfg):
     """Every ring geometry (loaders / storers / slots / tiles in flight) of
     fwd4_ring.hip forwards bit-exact; wg_per_cu 1 makes each workgroup walk
