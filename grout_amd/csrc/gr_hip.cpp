@@ -22,6 +22,7 @@
 #include <shared_mutex>
 #include <new>
 #include <stdio.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 #include <vector>
@@ -162,6 +163,8 @@ struct gr_hip_queue {
 	bool always_timed; // every launch carries events, whatever the knobs (gr_hip_batch_place's probes)
 	hipEvent_t quiesce;
 	hipEvent_t retire; // recorded at every FIB publication: the launches that may read the unpublished copies
+	uint64_t seen_serial; // the publication this queue's stream last waited for (ready_ev)
+	hipEvent_t sync_ev; // host waits on the queue's streams (host_wait)
 	gr_hip_iface_stats *d_stats; // [FWD4_STAT_SHARDS][max_ifaces]
 	host_slot hs[HOST_SLOTS];
 	// gr_hip_node_process staging (pinned, grown on demand)
@@ -229,8 +232,16 @@ struct gr_hip_ctx {
 	int untimed; // measurements: no HIP events around launches (gr_hip_queue_kernel_ms sees none)
 	uint32_t time_every; // HIP events around every N-th submit of a queue only (0, 1 = every one)
 	std::vector<host_range> hregs; // registered host memory, by host address
-	uint8_t *stage; // pinned staging of the FIB commits (fib_mu)
-	size_t stage_cap;
+	// FIB publication (see retire_wait): two pinned staging buffers used in
+	// turn by the commits (fib_mu), each with the event of its last upload,
+	// and per generation the event of the upload that made it complete
+	uint8_t *stage[2];
+	size_t stage_cap[2];
+	hipEvent_t stage_ev[2];
+	uint32_t stage_i;
+	hipEvent_t ready_ev[2];
+	uint64_t serial; // publications so far
+	uint32_t commit_us[3]; // the last commit: staging (host), enqueue (shared lock), publish (exclusive lock)
 	std::mutex occ_mu; // the occupancy cache below (launches run concurrently)
 	int occ_ring[8]; // by variant, of the last launch's geometry and staging ("occupancy")
 	struct occ_entry {
@@ -263,6 +274,17 @@ static int h2d(gr_hip_ctx *c, void *dst, const void *src, size_t n) {
 
 static int ctl_sync(gr_hip_ctx *c) {
 	HCK(hipStreamSynchronize(c->ctl));
+	return 0;
+}
+
+// The host waits for what queue q enqueued on stream s, through an event:
+// hipStreamSynchronize holds the stream for as long as it waits, which would
+// hold up the FIB publication recording its retire event there from the
+// control thread (measured: the publish step then took as long as the
+// rest of the queue's work, 1-1.6 ms).
+static int host_wait(gr_hip_queue *q, hipStream_t s) {
+	HCK(hipEventRecord(q->sync_ev, s));
+	HCK(hipEventSynchronize(q->sync_ev));
 	return 0;
 }
 
@@ -656,6 +678,11 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	if (hipStreamCreateWithFlags(&c->ctl, hipStreamNonBlocking) != hipSuccess)
 		goto fail;
 	for (uint32_t g = 0; g < 2; g++) {
+		if (hipEventCreateWithFlags(&c->ready_ev[g], hipEventDisableTiming) != hipSuccess
+		    || hipEventCreateWithFlags(&c->stage_ev[g], hipEventDisableTiming) != hipSuccess
+		    || hipEventRecord(c->ready_ev[g], c->ctl) != hipSuccess // nothing to wait for yet
+		    || hipEventRecord(c->stage_ev[g], c->ctl) != hipSuccess)
+			goto fail;
 		if (hipMalloc(&c->d_rx[g], sizeof(fwd4_rx) * max_ifaces) != hipSuccess
 		    || hipMalloc(&c->d_rx6[g], sizeof(fwd4_rx6) * max_ifaces) != hipSuccess
 		    || hipMalloc(&c->d_tables[g], sizeof(fwd4_tables)) != hipSuccess)
@@ -710,6 +737,8 @@ extern "C" int gr_hip_fini(gr_hip_ctx_t *c) {
 	hipSetDevice(c->dev);
 	while (!c->queues.empty())
 		gr_hip_queue_destroy(c->queues.back());
+	if (c->ctl)
+		hipStreamSynchronize(c->ctl); // the last commits' uploads
 	for (const host_range &r : c->hregs)
 		if (r.ours)
 			hipHostUnregister(reinterpret_cast<void *>(r.host));
@@ -734,7 +763,13 @@ extern "C" int gr_hip_fini(gr_hip_ctx_t *c) {
 	hipFree(c->d_reta);
 	hipFree(c->d_vlan_keys);
 	hipFree(c->d_vlan_vals);
-	hipHostFree(c->stage);
+	for (int i = 0; i < 2; i++) {
+		hipHostFree(c->stage[i]);
+		if (c->stage_ev[i])
+			hipEventDestroy(c->stage_ev[i]);
+		if (c->ready_ev[i])
+			hipEventDestroy(c->ready_ev[i]);
+	}
 	if (c->ctl)
 		hipStreamDestroy(c->ctl);
 	(void)hipGetLastError();
@@ -1014,14 +1049,25 @@ extern "C" int gr_hip_reta_set(gr_hip_ctx_t *c, uint32_t first, const uint32_t *
 // views and table block a launch reads. A submit takes the current
 // generation (under the shared lock, for microseconds), so each launch sees
 // one table from its first packet to its last. A commit
-//   1. makes the control stream wait for the launches submitted before the
-//      previous publication (the only ones that can still read the copy it
-//      is about to write: `retire` events), writes the unpublished copy and
-//      the other generation's views, with c->mu held shared (submitters keep
-//      going);
+//   1. with c->mu held shared (submitters keep going), stages what the
+//      unpublished copy misses and the other generation's views in pinned
+//      memory, and enqueues on the control stream: a wait for the launches
+//      submitted before the previous publication (the only ones that can
+//      still read that copy: `retire` events), the uploads, and the
+//      generation's `ready_ev`;
 //   2. publishes: flips the generation and records `retire` on every queue,
 //      with c->mu held exclusively for a few microseconds.
-// Route adds and deletes only touch the host RIB (fib_mu).
+// Nothing waits on the host: the first launch of each queue after a
+// publication makes its stream wait for `ready_ev` (launch()), so the
+// datapath sees the new table as soon as it is uploaded and the commit
+// returns once the work is enqueued. Route adds and deletes only touch the
+// host RIB (fib_mu).
+
+static uint64_t now_us() {
+	struct timespec t;
+	clock_gettime(CLOCK_MONOTONIC, &t);
+	return (uint64_t)t.tv_sec * 1000000u + (uint64_t)t.tv_nsec / 1000u;
+}
 
 // Wait, on the control stream, for every launch submitted before the last
 // publication.
@@ -1048,6 +1094,7 @@ template <typename F>
 static int publish(gr_hip_ctx *c, uint32_t g, F then) {
 	std::lock_guard<std::shared_mutex> l(c->mu);
 	c->gen = g;
+	c->serial++;
 	then();
 	count_v6(c);
 	for (gr_hip_queue *q : c->queues)
@@ -1056,7 +1103,10 @@ static int publish(gr_hip_ctx *c, uint32_t g, F then) {
 }
 
 // Host staging for one commit's uploads: the bytes of every (destination,
-// length) write packed into one pinned buffer, then one DMA per write.
+// length) write packed into a pinned buffer, then one DMA per write on the
+// control stream. Nothing is synchronised: the two staging buffers are used
+// in turn, and a commit waits only until the one it takes is free again
+// (the commit before last has uploaded).
 struct stager {
 	gr_hip_ctx *c;
 	std::vector<uint8_t> buf;
@@ -1067,7 +1117,7 @@ struct stager {
 	std::vector<op> ops;
 
 	explicit stager(gr_hip_ctx *c_) : c(c_) {}
-	// room for n bytes going to dst; valid until the next add
+	// room for `count` entries going to dst; valid until the next add
 	template <typename E>
 	E *add(E *dst, size_t count) {
 		const size_t off = (buf.size() + 15) & ~(size_t)15;
@@ -1075,23 +1125,35 @@ struct stager {
 		ops.push_back({dst, off, count * sizeof(E)});
 		return reinterpret_cast<E *>(buf.data() + off);
 	}
-	int flush() { // enqueue on the control stream (the caller syncs it)
+	int flush() { // enqueue on the control stream
 		if (buf.empty())
 			return 0;
-		if (buf.size() > c->stage_cap) {
-			HCK(hipStreamSynchronize(c->ctl));
-			hipHostFree(c->stage);
-			c->stage = nullptr;
-			c->stage_cap = 0;
-			HCK(hipHostMalloc(reinterpret_cast<void **>(&c->stage), buf.size(), hipHostMallocDefault));
-			c->stage_cap = buf.size();
+		const uint32_t i = c->stage_i ^= 1;
+		HCK(hipEventSynchronize(c->stage_ev[i]));
+		if (buf.size() > c->stage_cap[i]) {
+			hipHostFree(c->stage[i]);
+			c->stage[i] = nullptr;
+			c->stage_cap[i] = 0;
+			HCK(hipHostMalloc(reinterpret_cast<void **>(&c->stage[i]), buf.size(), hipHostMallocDefault));
+			c->stage_cap[i] = buf.size();
 		}
-		memcpy(c->stage, buf.data(), buf.size());
+		memcpy(c->stage[i], buf.data(), buf.size());
 		for (const op &o : ops)
-			HCK(hipMemcpyAsync(o.dst, c->stage + o.off, o.n, hipMemcpyHostToDevice, c->ctl));
+			HCK(hipMemcpyAsync(o.dst, c->stage[i] + o.off, o.n, hipMemcpyHostToDevice, c->ctl));
+		HCK(hipEventRecord(c->stage_ev[i], c->ctl));
 		return 0;
 	}
 };
+
+// Stage generation g's RX views (IPv4 and IPv6, every iface).
+static void stage_rx(stager &st, gr_hip_ctx *c, uint32_t g) {
+	for (uint32_t i = 0; i < c->max_ifaces; i++) {
+		c->rx[g][i] = make_rx(c, i, g);
+		c->rx6[g][i] = make_rx6(c, i, g);
+	}
+	memcpy(st.add(c->d_rx[g], c->max_ifaces), c->rx[g].data(), sizeof(fwd4_rx) * c->max_ifaces);
+	memcpy(st.add(c->d_rx6[g], c->max_ifaces), c->rx6[g].data(), sizeof(fwd4_rx6) * c->max_ifaces);
+}
 
 extern "C" int gr_hip_fib4_create(gr_hip_ctx_t *c, uint16_t vrf, uint32_t max_routes, uint32_t num_tbl8) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
@@ -1313,6 +1375,7 @@ extern "C" int gr_hip_fib4_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib == nullptr)
 		return -ENONET;
+	const uint64_t t0 = now_us();
 	const bool fits16 = v.max_slot <= 0x7fff && v.num_tbl8 <= 0x8000;
 	const int want = fits16 ? c->fib_fmt : FIB_FMT_24;
 	const int w = v.pub4 ^ 1;
@@ -1341,6 +1404,7 @@ extern "C" int gr_hip_fib4_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 	}
 	const uint32_t B = c->gen ^ 1; // the generation this commit writes
 	int r;
+	uint64_t t1 = t0;
 	{
 		std::shared_lock<std::shared_mutex> l(c->mu); // submitters go on
 		r = fib4_buf_alloc(c, b, want, v.num_tbl8);
@@ -1360,13 +1424,13 @@ extern "C" int gr_hip_fib4_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 		b.up = true;
 		views_follow_published(c, B);
 		v.sel4[B] = (uint8_t)w;
+		stage_rx(st, c, B);
+		t1 = now_us();
 		r = retire_wait(c); // no launch may still read copy w or generation B's views
 		if (r == 0)
 			r = st.flush();
-		if (r == 0)
-			r = upload_rx(c, B);
-		if (r == 0)
-			r = ctl_sync(c); // the generation is complete before anyone takes it
+		if (r == 0 && hipEventRecord(c->ready_ev[B], c->ctl) != hipSuccess) // launches of B wait for it
+			r = -EIO;
 		if (r != 0) {
 			b.up = false; // half written: rewritten in full next time
 			views_follow_published(c, B);
@@ -1374,7 +1438,8 @@ extern "C" int gr_hip_fib4_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 		}
 	}
 	gr_fib4_dirty_clear(v.rib);
-	return publish(c, B, [&] {
+	const uint64_t t2 = now_us();
+	r = publish(c, B, [&] {
 		const bool old_up = v.pub().up;
 		v.pub4 = w;
 		// the copy just unpublished misses this commit's changes
@@ -1382,6 +1447,11 @@ extern "C" int gr_hip_fib4_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 		v.pend24 = std::move(d24);
 		v.pend8 = std::move(d8);
 	});
+	const uint64_t t3 = now_us();
+	c->commit_us[0] = (uint32_t)(t1 - t0);
+	c->commit_us[1] = (uint32_t)(t2 - t1);
+	c->commit_us[2] = (uint32_t)(t3 - t2);
+	return r;
 }
 
 extern "C" int gr_hip_fib4_lookup_host(gr_hip_ctx_t *c, uint16_t vrf, uint32_t ip_be, uint32_t *nh) {
@@ -1551,13 +1621,12 @@ extern "C" int gr_hip_fib6_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 		b.up = true;
 		views_follow_published(c, B);
 		v.sel6[B] = (uint8_t)w;
+		stage_rx(st, c, B);
 		r = retire_wait(c);
 		if (r == 0)
 			r = st.flush();
-		if (r == 0)
-			r = upload_rx(c, B);
-		if (r == 0)
-			r = ctl_sync(c);
+		if (r == 0 && hipEventRecord(c->ready_ev[B], c->ctl) != hipSuccess)
+			r = -EIO;
 		if (r != 0) {
 			b.up = false;
 			views_follow_published(c, B);
@@ -1627,6 +1696,7 @@ extern "C" int gr_hip_queue_create(gr_hip_ctx_t *c, void *stream, gr_hip_queue_t
 	}
 	hipEventCreateWithFlags(&q->quiesce, hipEventDisableTiming);
 	hipEventCreateWithFlags(&q->retire, hipEventDisableTiming);
+	hipEventCreateWithFlags(&q->sync_ev, hipEventDisableTiming);
 	hipEventRecord(q->retire, q->s); // nothing submitted yet
 	if (hipHostMalloc(reinterpret_cast<void **>(&q->h_err), sizeof(uint32_t), hipHostMallocMapped) == hipSuccess) {
 		*q->h_err = 0;
@@ -1668,6 +1738,7 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 	}
 	hipEventDestroy(q->quiesce);
 	hipEventDestroy(q->retire);
+	hipEventDestroy(q->sync_ev);
 	hipFree(q->d_stats);
 	hipHostFree(q->h_err);
 	hipHostFree(q->node_lines);
@@ -1718,6 +1789,13 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	A.verdicts = b->verdicts;
 	A.stats = q->d_stats;
 	A.T = c->d_tables[c->gen]; // the generation published when this launch is enqueued
+	// ... whose upload the stream waits for, once per publication (the
+	// host's own streams of gr_hip_fwd4_host at every launch)
+	if (s != q->s || q->seen_serial != c->serial) {
+		HCK(hipStreamWaitEvent(s, c->ready_ev[c->gen], 0));
+		if (s == q->s)
+			q->seen_serial = c->serial;
+	}
 	A.n = b->n;
 	A.in_stride = b->in_stride;
 	A.out_stride = b->out_stride;
@@ -1843,6 +1921,12 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < 0 || value >= gr_fwd4_ring_ncfg())
 			return -EINVAL;
 		c->ring_cfg = value;
+	} else if (strncmp(key, "commit_us_", 10) == 0) { // read-only: the last IPv4 commit's phases
+		const char *k = key + 10;
+		const int i = strcmp(k, "stage") == 0 ? 0 : strcmp(k, "enqueue") == 0 ? 1 : strcmp(k, "publish") == 0 ? 2 : -1;
+		if (i < 0)
+			return -ENOENT;
+		return (int)(c->commit_us[i] > 0x7fffffffu ? 0x7fffffffu : c->commit_us[i]);
 	} else if (strcmp(key, "occupancy") == 0) { // read-only: WGs/CU of the current variant
 		return c->occ_ring[(c->stats_on ? FWD4_V_STATS : 0) | c->nt]; // as of the last launch
 	} else {
@@ -1901,7 +1985,8 @@ static int q_check(gr_hip_queue *q) {
 extern "C" int gr_hip_queue_sync(gr_hip_queue_t *q) {
 	if (q == nullptr)
 		return -EINVAL;
-	HCK(hipStreamSynchronize(q->s));
+	if (const int e_ = host_wait(q, q->s))
+		return e_;
 	return q_check(q);
 }
 
@@ -1954,7 +2039,8 @@ extern "C" int gr_hip_fwd4_host(
 			int r = launch(q, q->s, &b, true);
 			if (r < 0)
 				return r;
-			HCK(hipStreamSynchronize(q->s));
+			if (const int e_ = host_wait(q, q->s))
+				return e_;
 			return q_check(q);
 		}
 	}
@@ -1991,7 +2077,8 @@ extern "C" int gr_hip_fwd4_host(
 		HCK(hipMemcpyAsync(verdicts + off, h.v, (size_t)cnt * sizeof(*verdicts), hipMemcpyDeviceToHost, h.s));
 	}
 	for (host_slot &h : q->hs) {
-		HCK(hipStreamSynchronize(h.s));
+		if (const int e_ = host_wait(q, h.s))
+			return e_;
 	}
 	return q_check(q);
 }
@@ -2159,7 +2246,8 @@ extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uin
 		// after everything already submitted on the queue, like gr_hip_fwd4_host
 		if ((r = launch(q, q->s, &b, true)) < 0)
 			return r;
-		HCK(hipStreamSynchronize(q->s));
+		if (const int e_ = host_wait(q, q->s))
+			return e_;
 		r = q_check(q);
 	} else {
 		lk.unlock(); // gr_hip_fwd4_host takes it itself
@@ -2186,10 +2274,12 @@ extern "C" int gr_hip_queue_stats(gr_hip_queue_t *q, struct gr_hip_iface_stats *
 		return -ENOMEM;
 	hipSetDevice(c->dev);
 	std::vector<gr_hip_iface_stats> all((size_t)FWD4_STAT_SHARDS * c->max_ifaces);
-	HCK(hipStreamSynchronize(q->s));
+	if (const int e_ = host_wait(q, q->s))
+		return e_;
 	for (host_slot &h : q->hs)
 		if (h.s)
-			HCK(hipStreamSynchronize(h.s));
+			if (const int e_ = host_wait(q, h.s))
+				return e_;
 	HCK(hipMemcpy(all.data(), q->d_stats, all.size() * sizeof(gr_hip_iface_stats), hipMemcpyDeviceToHost));
 	uint32_t m = max < c->max_ifaces ? max : c->max_ifaces;
 	memset(st, 0, (size_t)max * sizeof(*st));

@@ -465,6 +465,9 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               (default), 1 = one contiguous run of tiles per workgroup
 //   "fib_format_of" (read) the format VRF `value`'s FIB is on the device in
 //   "occupancy" (read) resident workgroups per CU of the current variant
+//   "commit_us_stage" / "commit_us_enqueue" / "commit_us_publish" (read) the last
+//       gr_hip_fib4_commit's phases in microseconds: host staging, the
+//       enqueue under the shared lock, the flip under the exclusive lock
 // Returns 0 (or the value read), -EINVAL, or -ENOENT for an unknown key.
 int gr_hip_tune(gr_hip_ctx_t *, const char *key, int value);
 

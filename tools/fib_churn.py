@@ -122,7 +122,7 @@ def main():
     rng = np.random.default_rng(0xC4A9)
     per_commit = max(1, int(round(args.rate * args.period_ms / 1000)))
     stop = threading.Event()
-    lat, applied = [], [0]
+    lat, clat, phases, applied = [], [], [], [0]
     deleted = []
     live = np.ones(count, dtype=bool)
 
@@ -146,8 +146,12 @@ def main():
             if back:
                 fp.route_add(view[np.array(back)])
                 live[np.array(back)] = True
+            tc = time.perf_counter()
             fp.fib_commit(vrf)
-            lat.append(time.perf_counter() - t0)
+            t1 = time.perf_counter()
+            lat.append(t1 - t0)
+            clat.append(t1 - tc)
+            phases.append([fp.tune(k) for k in ("commit_us_stage", "commit_us_enqueue", "commit_us_publish")])
             applied[0] += k_rep + k_del + len(back)
             nxt += period
             d = nxt - time.perf_counter()
@@ -165,7 +169,10 @@ def main():
     churn.update({"route_changes": applied[0], "changes_per_s": round(applied[0] / dt),
                   "commits": len(lat), "commit_ms_p50": round(float(np.percentile(la, 50)), 3),
                   "commit_ms_p99": round(float(np.percentile(la, 99)), 3), "commit_ms_max": round(float(la.max()), 3),
-                  "changes_per_commit": per_commit})
+                  "changes_per_commit": per_commit,
+                  "commit_call_ms_p50": round(float(np.percentile(np.array(clat) * 1e3, 50)), 3),
+                  "commit_phase_us_p50": dict(zip(("stage", "enqueue", "publish"),
+                                                  np.percentile(np.array(phases), 50, axis=0).round(1).tolist()))})
     out.update({"batch": n, "base": base, "churn": churn, "mpps_ratio": round(churn["mpps"] / base["mpps"], 4),
                 "note": "wall-clock Mpps, submits of 4 launches then a sync, untimed launches; commit latency = "
                         "route adds/deletes + gr_hip_fib4_commit"})
