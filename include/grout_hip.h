@@ -390,9 +390,16 @@ int gr_hip_iface_del(gr_hip_ctx_t *, uint16_t iface_id);
 int gr_hip_nh_set(gr_hip_ctx_t *, uint32_t first_slot, const struct gr_hip_nh *nh, uint32_t n);
 int gr_hip_reta_set(gr_hip_ctx_t *, uint32_t first, const uint32_t *slots, uint32_t n);
 
-// RIB + device FIB (DIR24_8-equivalent, 4-byte entries). Routes are staged in
-// the host RIB; gr_hip_fib4_commit() makes them visible to later submits
-// (stream-ordered swap, the rte_rcu_qsbr_synchronize analogue of modules/ip/control/route.c:764).
+// RIB + device FIB (DIR24_8-equivalent; 2-byte entries while slots fit 15
+// bits). Routes are staged in the host RIB (adds and deletes never touch the
+// device or hold submitters). gr_hip_fib4_commit() publishes them: it writes
+// the VRF's unpublished device copy and flips the view generation, the
+// analogue of grout's RCU-protected rte_fib (modules/ip/control/route.c:87-95,
+// 764). It never waits for submitted launches and returns once the upload is
+// enqueued: launches already submitted finish on the old table, every submit
+// after the call runs on the new one (its stream waits for the upload), and
+// each launch reads one table from first packet to last. Thread-safe against
+// concurrent submits on any queue.
 int gr_hip_fib4_create(gr_hip_ctx_t *, uint16_t vrf_id, uint32_t max_routes, uint32_t num_tbl8);
 int gr_hip_fib4_destroy(gr_hip_ctx_t *, uint16_t vrf_id);
 int gr_hip_route4_add(gr_hip_ctx_t *, const struct gr_hip_route4 *routes, uint32_t n, int replace);
@@ -413,6 +420,8 @@ int gr_hip_fib6_create(gr_hip_ctx_t *, uint16_t vrf_id, uint32_t max_routes, uin
 int gr_hip_fib6_destroy(gr_hip_ctx_t *, uint16_t vrf_id);
 int gr_hip_route6_add(gr_hip_ctx_t *, const struct gr_hip_route6 *routes, uint32_t n, int replace);
 int gr_hip_route6_del(gr_hip_ctx_t *, uint16_t vrf_id, uint16_t iface_id, const uint8_t ip[16], uint8_t prefixlen);
+// Publishes like gr_hip_fib4_commit (the repainted trie, whole, into the
+// unpublished copy).
 int gr_hip_fib6_commit(gr_hip_ctx_t *, uint16_t vrf_id);
 // Host lookup in the committed tables (tests / control plane), scoped like fib6_lookup.
 int gr_hip_fib6_lookup_host(gr_hip_ctx_t *, uint16_t vrf_id, uint16_t iface_id, const uint8_t ip[16], uint32_t *nh);
@@ -437,7 +446,7 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 
 // Tuning knobs, for measurements (A/B in one process). Keys:
 //   "ring"      geometry of the ring kernel (loaders / storers / slots /
-//               tiles in flight), 0..8; default 2
+//               tiles in flight), 0..11; default 2
 //   "stats"     1 = per-iface counters (default; grout always counts), 0 = off
 //   "nt"        1 = nontemporal loads / stores of the streamed data (default)
 //   "wg_per_cu" 0 = default grid (2 workgroups per CU, fewer if LDS
