@@ -712,7 +712,7 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->fib_fmt = FIB_FMT_24_W2;
 	c->ring_cfg = 2; // 16 waves: 2 loaders, 2 storers, 12 compute, 16 slots
 	c->host_direct = 1; // measured 1.9x the staged copies
-	c->node_ptrs = 1;
+	c->node_ptrs = 0; // staged lines: faster than frames by address, more so with several workers
 	c->tile_order = 0;
 	c->spin_max = 0;
 	c->untimed = 0;
@@ -2039,6 +2039,7 @@ extern "C" int gr_hip_fwd4_host(
 			int r = launch(q, q->s, &b, true);
 			if (r < 0)
 				return r;
+			l.unlock(); // enqueued: the wait needs no lock (see gr_hip_node_process)
 			if (const int e_ = host_wait(q, q->s))
 				return e_;
 			return q_check(q);
@@ -2246,9 +2247,13 @@ extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uin
 		// after everything already submitted on the queue, like gr_hip_fwd4_host
 		if ((r = launch(q, q->s, &b, true)) < 0)
 			return r;
+		// the lock covers the enqueue, not the wait: control-plane writers
+		// (FIB publication) are not held behind the walk's GPU time
+		lk.unlock();
 		if (const int e_ = host_wait(q, q->s))
 			return e_;
 		r = q_check(q);
+		lk.lock(); // the hand-back reads the iface and nexthop mirrors
 	} else {
 		lk.unlock(); // gr_hip_fwd4_host takes it itself
 		if ((r = gr_hip_node_stage(m, n, burst, pos, q->node_lines, q->node_meta)) < 0)

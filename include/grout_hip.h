@@ -461,7 +461,8 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               loads and stores crossing PCIe (default); 0 = always staged
 //               chunk copies (pageable buffers always take that path)
 //   "node_ptrs"  1 = gr_hip_node_process hands registered frames over by
-//               address (default), 0 = always stage header lines
+//               address, 0 = stage header lines (default: faster from one
+//               worker thread up, and much faster with several)
 //   "time_every" N: only every N-th submit of a queue gets the HIP event
 //               pair that gr_hip_queue_kernel_ms reads (default 1: all);
 //               each pair costs ~7 us of stream time per launch. Setting
@@ -637,8 +638,8 @@ int gr_hip_node_apply(
 // context's mirrors. When every frame lies in memory registered with
 // gr_hip_host_register (and is 16-byte aligned), the GPU reads and rewrites
 // the frames in place over PCIe and only 8-byte frame addresses and metadata
-// are staged ("node_ptrs", default on); otherwise header lines are staged
-// through gr_hip_fwd4_host. Returns the number of mbufs handed back as
+// are staged when "node_ptrs" is on (default off); otherwise header lines are
+// staged through gr_hip_fwd4_host. Returns the number of mbufs handed back as
 // GR_HIP_E_PUNT, untouched, because a kernel gave up before reaching them
 // (0 normally; the others are handed back as usual), or -errno with every
 // mbuf untouched.

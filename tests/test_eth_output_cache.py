@@ -131,6 +131,6 @@ def test_gpu_node_walks_eth_output_cache(fastpath, ptrs):
         assert (bufs[zero, 6:12] == 0).all()
         q.close()
     finally:
-        fastpath.tune("node_ptrs", 1)
+        fastpath.tune("node_ptrs", 0)  # the default
         if ptrs:
             abi.check("gr_hip_host_unregister", L.gr_hip_host_unregister(fastpath.h, bufs.ctypes.data))

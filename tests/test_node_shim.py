@@ -205,7 +205,7 @@ def test_node_process_registered_frames(fastpath, ptrs):
         assert np.array_equal(q.stats(), st)
         q.close()
     finally:
-        fastpath.tune("node_ptrs", 1)
+        fastpath.tune("node_ptrs", 0)  # the default
         abi.check("gr_hip_host_unregister", L.gr_hip_host_unregister(fastpath.h, bufs.ctypes.data))
     assert L.gr_hip_host_dev_addr(fastpath.h, bufs.ctypes.data, ctypes.byref(dev)) == -2  # -ENOENT
 
@@ -236,7 +236,7 @@ def test_node_give_up_hands_back(fastpath, ptrs):
         q.node_process(m, burst=64)
     finally:
         fastpath.tune("spin_max", 0)
-        fastpath.tune("node_ptrs", 1)
+        fastpath.tune("node_ptrs", 0)  # the default
         if ptrs:
             abi.check("gr_hip_host_unregister", L.gr_hip_host_unregister(fastpath.h, bufs.ctypes.data))
     punt = m["edge"] == abi.EDGE["punt"]
