@@ -25,8 +25,8 @@ sys.path.insert(0, ROOT)
 
 # algorithmic HBM bytes per packet: line in, metadata in, one
 # FIB entry (2 or 4 bytes by device format), line out, verdict out
-def b_pkt(fib_entry_bytes):
-    return 64 + 8 + fib_entry_bytes + 64 + 8
+def b_pkt(fib_entry_bytes, out_bytes=64):
+    return 64 + 8 + fib_entry_bytes + out_bytes + 8
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
 
 
@@ -51,6 +51,11 @@ def parse():
     p.add_argument("--time-every", type=int, default=4,
                    help="HIP events around every N-th launch only (the kernel time is their average; "
                         "each event pair costs ~7 us of stream time)")
+    p.add_argument("--output", default="line", choices=["line", "prefix32"],
+                   help="line: each packet's whole 64-byte header line written back (BASELINE.md's 148 B); prefix32: "
+                        "packed 32-byte prefixes, every byte the path changes (GR_HIP_BATCH_F_PREFIX32)")
+    p.add_argument("--no-prefix-leg", action="store_true",
+                   help="skip the same measurement with packed 32-byte output prefixes (prefix32 in the line)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-path", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="wall time of the CPU baseline sample")
@@ -105,6 +110,8 @@ def main():
     n = args.batch or (1 << 22 if args.workload == "imix_frames" else 1 << 24)
     seed = rep.seed()
     imix = args.workload == "imix"
+    prefix32 = args.output == "prefix32"
+    out_bytes = abi.PREFIX if prefix32 else abi.LINE
     in_stride = args.slot if args.workload == "imix_frames" else abi.LINE
     t0 = time.time()
 
@@ -133,6 +140,9 @@ def main():
         del cf, cm
         if imix:
             batch.flags = abi.BATCH_F_LINES_ONLY
+        if prefix32:
+            batch.flags |= abi.BATCH_F_PREFIX32
+            batch.out_stride = abi.PREFIX
         fp.batch_place(batch, args.candidates)
         batch.flags = 0
         h2d(batch.in_frames, frames)
@@ -141,7 +151,7 @@ def main():
     else:
         d_in = torch.from_numpy(frames.reshape(-1)).to(dev)
         d_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
-        d_out = torch.empty(n * abi.LINE, dtype=torch.uint8, device=dev)
+        d_out = torch.empty(n * out_bytes, dtype=torch.uint8, device=dev)
         d_v = torch.empty(n * 8, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     log(f"[rank {rank}] {n} packets generated and resident in {time.time() - t0:.1f}s")
@@ -149,14 +159,16 @@ def main():
     q = fp.queue(shared_stream(dev))
     every = max(1, min(args.time_every, args.steps))
 
-    def measure(bufs, steps, warmup):
+    def measure(bufs, steps, warmup, prefix=None):
         """warmup + steps launches on `bufs`; -> (max-over-ranks seconds of the
         timed steps, kernel ms summed over the timed launches, their count)."""
         d_in_, d_out_, d_meta_, d_v_ = bufs
+        pfx = prefix32 if prefix is None else prefix
         fp.tune("time_every", every)  # every `every`-th submit of the queue carries events
 
         def step():
-            q.submit(d_in_, d_out_, d_meta_, d_v_, n, in_stride=in_stride, out_stride=abi.LINE, lines_only=imix)
+            q.submit(d_in_, d_out_, d_meta_, d_v_, n, in_stride=in_stride, out_stride=abi.LINE, lines_only=imix,
+                     prefix32=pfx)
 
         for _ in range(warmup):
             step()
@@ -194,7 +206,7 @@ def main():
         entry = 4  # fib6.h trie entries
     else:
         entry = 4 if fp.tune("fib_format_of", T.VRF_MAIN) == 0 else 2
-    B_PKT = b_pkt(entry)
+    B_PKT = b_pkt(entry, out_bytes)
     achieved = n * B_PKT / avg_kernel_s / 1e9
 
     # HBM bytes per launch from PMC counters cannot be read from inside this
@@ -218,7 +230,7 @@ def main():
     if batch is not None and not args.no_plain:
         p_in = torch.from_numpy(frames.reshape(-1)).to(dev)
         p_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
-        p_out = torch.empty(n * abi.LINE, dtype=torch.uint8, device=dev)
+        p_out = torch.empty(n * out_bytes, dtype=torch.uint8, device=dev)
         p_v = torch.empty(n * 8, dtype=torch.uint8, device=dev)
         torch.cuda.synchronize()
         pt, pms, pcnt = measure((p_in, p_out, p_meta, p_v), args.steps, args.warmup)
@@ -226,6 +238,28 @@ def main():
                  "ms_per_step": round(pt / args.steps * 1e3, 4),
                  "kernel_ms_avg": round(pms / max(pcnt, 1), 4)}
         del p_in, p_meta, p_out, p_v
+
+    # the same stream with packed 32-byte output prefixes (GR_HIP_BATCH_F_PREFIX32:
+    # every byte the path changes; bytes 32-63 of a frame never change), on
+    # plain allocations: what a deployment that writes back only the changed
+    # bytes gets. Reported beside `value`, which keeps whole lines
+    pfx_leg = None
+    if not prefix32 and not args.no_prefix_leg and not imix:
+        x_in = torch.from_numpy(frames.reshape(-1)).to(dev)
+        x_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
+        x_out = torch.empty(n * abi.PREFIX, dtype=torch.uint8, device=dev)
+        x_v = torch.empty(n * 8, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        xt, xms, xcnt = measure((x_in, x_out, x_meta, x_v), args.steps, args.warmup, prefix=True)
+        xb = b_pkt(entry, abi.PREFIX)
+        xk = xms / max(xcnt, 1)
+        pfx_leg = {"value": round(rep.aggregate_mpps(n, args.steps, xt), 1),
+                   "ms_per_step": round(xt / args.steps * 1e3, 4), "kernel_ms_avg": round(xk, 4),
+                   "bytes_per_pkt": xb, "frac": round(n * xb / (xk / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if xk else None,
+                   "placement": "plain torch allocations",
+                   "note": "out_lines = packed 32-byte prefixes (GR_HIP_BATCH_F_PREFIX32), same verdicts and "
+                           "changed bytes as whole lines"}
+        del x_in, x_meta, x_out, x_v
 
     result = {
         "metric": "Mpps IPv4 forward, 64B pkts, ~1M-route FIB (device-resident), 1/8 GPU",
@@ -249,7 +283,10 @@ def main():
             "parallelism": f"replicas x{world} (one RX stream + FIB replica per GPU, no collective)",
             "forwarded_frac": round(fwd_frac, 6),
             "placement": (f"calibrated: output lines = fastest of {args.candidates + 1} allocations, each timed "
-                          "over this batch (gr_hip_batch_place)" if batch is not None else "plain torch allocations"),
+                          "over a batch of this workload drawn with another seed (gr_hip_batch_place)"
+                          if batch is not None else "plain torch allocations"),
+            "output": ("packed 32-byte header prefixes (every byte the path changes; GR_HIP_BATCH_F_PREFIX32)"
+                       if prefix32 else "whole 64-byte header lines"),
         },
         "roofline": {
             "bound": "hbm",
@@ -267,6 +304,8 @@ def main():
     if plain is not None:
         result["value_plain_placement"] = plain["value"]
         result["plain_placement"] = plain
+    if pfx_leg is not None:
+        result["prefix32"] = pfx_leg
     if args.workload == "fullview6":
         result["metric"] = "Mpps IPv6 forward, 64B pkts, 200k-route IPv6 view (device-resident) [non-headline]"
     elif args.workload != "fullview64":
@@ -289,6 +328,15 @@ def main():
             r = fn(hq._h, lines.data_ptr(), hmeta.data_ptr(), hn, hout.data_ptr(), hv.data_ptr())
             abi.check("gr_hip_fwd4_host", r)
         ht = (time.perf_counter() - t0) / reps
+        # packed 32-byte prefixes back (gr_hip_fwd4_host_ex): 40 B per packet D2H
+        fx = fp.lib.gr_hip_fwd4_host_ex
+        abi.check("gr_hip_fwd4_host_ex", fx(hq._h, lines.data_ptr(), hmeta.data_ptr(), hn, hout.data_ptr(),
+                                            abi.PREFIX, hv.data_ptr()))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            abi.check("gr_hip_fwd4_host_ex", fx(hq._h, lines.data_ptr(), hmeta.data_ptr(), hn, hout.data_ptr(),
+                                                abi.PREFIX, hv.data_ptr()))
+        hx = (time.perf_counter() - t0) / reps
         hq.close()
         del ctypes
         result["host_path"] = {
@@ -296,8 +344,10 @@ def main():
             "pkts": hn,
             "h2d_bytes_per_pkt": abi.LINE + 8,
             "d2h_bytes_per_pkt": abi.LINE + 8,
+            "mpps_prefix32": round(hn / hx / 1e6, 1),
             "note": ("header lines + metadata in pinned host memory; the kernel reads and writes them over "
-                     "PCIe itself (host_direct), H2D and D2H concurrent"),
+                     "PCIe itself (host_direct), H2D and D2H concurrent; mpps_prefix32: 32-byte prefixes back "
+                     "(gr_hip_fwd4_host_ex), 40 B per packet D2H"),
         }
 
     # ---- CPU baseline: the oracle restatement on this host's cores

@@ -102,6 +102,8 @@ NODE_COUNT = len(NODE_NAMES)
 NODE_STATS_DT = np.dtype([("packets", "<u8", NODE_COUNT), ("calls", "<u8", NODE_COUNT)])
 PTYPE_L3_IPV4, PTYPE_L3_IPV6 = 0x10, 0x40  # DPDK rte_mbuf_ptype.h
 BATCH_F_FRAME_PTRS = 0x2
+BATCH_F_PREFIX32 = 0x4  # out_lines: packed 32-byte prefixes (every byte the path changes)
+PREFIX = 32
 
 
 class Batch(ctypes.Structure):
@@ -170,6 +172,7 @@ HIP_API = {
     "gr_hip_queue_kernel_ms": (_I, [_P, _U32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(_U32)]),
     "gr_hip_tune": (_I, [_P, ctypes.c_char_p, _I]),
     "gr_hip_fwd4_host": (_I, [_P, _P, _P, _U32, _P, _P]),
+    "gr_hip_fwd4_host_ex": (_I, [_P, _P, _P, _U32, _P, _U32, _P]),
     "gr_hip_queue_stats": (_I, [_P, _P, _U32, _I]),
     "gr_hip_host_alloc": (_I, [_P, ctypes.c_size_t, PP]),
     "gr_hip_host_free": (_I, [_P, _P]),

@@ -226,6 +226,7 @@ template <class C, bool NT, bool PTRS>
 __device__ void ring_storer(const fwd4_params &A, ring_lds<C, PTRS> &L, uint32_t n_local, uint32_t j, uint32_t lane) {
 	const uint32_t prow = lane >> 2, part = lane & 3;
 	const uint32_t pslot = (part ^ ((lane >> 4) & 3)) << 4;
+	const bool prefix = A.out_stride == GR_HIP_PREFIX; // packed 32-byte prefixes (whole lines are >= 64)
 	for (uint32_t k = j; k < n_local; k += C::STORERS) {
 		const uint32_t s = k % C::SLOTS;
 		if (!flag_wait(L, &L.done[s], k + 1))
@@ -251,7 +252,7 @@ __device__ void ring_storer(const fwd4_params &A, ring_lds<C, PTRS> &L, uint32_t
 #pragma unroll
 		for (uint32_t q = 0; q < 4; q++) {
 			const uint32_t r = q * 16 + prow;
-			if (r < cnt)
+			if (r < cnt && (!prefix || part < 2)) // GR_HIP_BATCH_F_PREFIX32: bytes 0-31 only
 				st16<NT>(dst[q] + part * 16, o[q]);
 		}
 		if (lane < cnt) {

@@ -1940,6 +1940,14 @@ static int batch_ok(const gr_hip_batch *b) {
 		return -EINVAL;
 	if (b->n == 0)
 		return 0;
+	if (b->flags & GR_HIP_BATCH_F_PREFIX32) { // 32-byte output prefixes, packed
+		if (!b->out_lines || b->out_stride != GR_HIP_PREFIX || ((uintptr_t)b->out_lines & 15))
+			return -EINVAL;
+		gr_hip_batch full = *b;
+		full.flags &= ~GR_HIP_BATCH_F_PREFIX32;
+		full.out_stride = GR_HIP_LINE; // the other checks as for whole lines
+		return batch_ok(&full);
+	}
 	if (b->flags & GR_HIP_BATCH_F_FRAME_PTRS) {
 		// in_frames: n frame addresses; out_lines NULL = rewrite each frame in place
 		if (!b->in_frames || !b->meta || !b->verdicts || ((uintptr_t)b->in_frames & 7)
@@ -2010,20 +2018,22 @@ extern "C" int gr_hip_queue_kernel_ms(gr_hip_queue_t *q, uint32_t n, float *ms, 
 	return 0;
 }
 
-extern "C" int gr_hip_fwd4_host(
+extern "C" int gr_hip_fwd4_host_ex(
 	gr_hip_queue_t *q,
 	const void *lines,
 	const struct gr_hip_pkt_meta *meta,
 	uint32_t n,
 	void *out_lines,
+	uint32_t out_stride,
 	struct gr_hip_verdict *verdicts
 ) {
 	if (q == nullptr)
 		return -EINVAL;
 	if (n == 0)
 		return 0;
-	if (!lines || !meta || !out_lines || !verdicts)
+	if (!lines || !meta || !out_lines || !verdicts || (out_stride != GR_HIP_LINE && out_stride != GR_HIP_PREFIX))
 		return -EINVAL;
+	const uint32_t oflags = out_stride == GR_HIP_PREFIX ? GR_HIP_BATCH_F_PREFIX32 : 0;
 	gr_hip_ctx *c = q->ctx;
 	hipSetDevice(c->dev);
 	std::shared_lock<std::shared_mutex> l(c->mu); // see gr_hip_fwd4_submit
@@ -2034,8 +2044,8 @@ extern "C" int gr_hip_fwd4_host(
 		if (host_dev_ptr(lines, &d_in) && host_dev_ptr(meta, &d_meta) && host_dev_ptr(out_lines, &d_out)
 		    && host_dev_ptr(verdicts, &d_v)) {
 			gr_hip_batch b = {d_in, d_out, static_cast<const gr_hip_pkt_meta *>(d_meta),
-					  static_cast<gr_hip_verdict *>(d_v), n, GR_HIP_LINE, GR_HIP_LINE,
-					  GR_HIP_BATCH_F_LINES_ONLY};
+					  static_cast<gr_hip_verdict *>(d_v), n, GR_HIP_LINE, out_stride,
+					  GR_HIP_BATCH_F_LINES_ONLY | oflags};
 			int r = launch(q, q->s, &b, true);
 			if (r < 0)
 				return r;
@@ -2069,11 +2079,11 @@ extern "C" int gr_hip_fwd4_host(
 		HCK(hipMemcpyAsync(h.meta, meta + off, (size_t)cnt * sizeof(*meta), hipMemcpyHostToDevice, h.s));
 		// verdicts of packets a kernel that gave up never reached read back as 0xff
 		HCK(hipMemsetAsync(h.v, 0xff, (size_t)cnt * sizeof(*verdicts), h.s));
-		gr_hip_batch b = {h.in, h.out, h.meta, h.v, cnt, GR_HIP_LINE, GR_HIP_LINE, GR_HIP_BATCH_F_LINES_ONLY};
+		gr_hip_batch b = {h.in, h.out, h.meta, h.v, cnt, GR_HIP_LINE, out_stride, GR_HIP_BATCH_F_LINES_ONLY | oflags};
 		int r = launch(q, h.s, &b, false);
 		if (r < 0)
 			return r;
-		HCK(hipMemcpyAsync(out + (size_t)off * GR_HIP_LINE, h.out, (size_t)cnt * GR_HIP_LINE,
+		HCK(hipMemcpyAsync(out + (size_t)off * out_stride, h.out, (size_t)cnt * out_stride,
 				   hipMemcpyDeviceToHost, h.s));
 		HCK(hipMemcpyAsync(verdicts + off, h.v, (size_t)cnt * sizeof(*verdicts), hipMemcpyDeviceToHost, h.s));
 	}
@@ -2082,6 +2092,11 @@ extern "C" int gr_hip_fwd4_host(
 			return e_;
 	}
 	return q_check(q);
+}
+
+extern "C" int gr_hip_fwd4_host(gr_hip_queue_t *q, const void *lines, const struct gr_hip_pkt_meta *meta, uint32_t n,
+				void *out_lines, struct gr_hip_verdict *verdicts) {
+	return gr_hip_fwd4_host_ex(q, lines, meta, n, out_lines, GR_HIP_LINE, verdicts);
 }
 
 // Registered host memory (gr_hip_host_register): host -> device address.
@@ -2212,7 +2227,7 @@ extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uin
 		q->node_v = nullptr;
 		q->node_cap = 0;
 		HCK(hipHostMalloc((void **)&q->node_lines, (size_t)ns * GR_HIP_LINE, hipHostMallocDefault));
-		HCK(hipHostMalloc((void **)&q->node_out, (size_t)ns * GR_HIP_LINE, hipHostMallocDefault));
+		HCK(hipHostMalloc((void **)&q->node_out, (size_t)ns * GR_HIP_PREFIX, hipHostMallocDefault));
 		HCK(hipHostMalloc((void **)&q->node_meta, (size_t)ns * sizeof(gr_hip_pkt_meta), hipHostMallocDefault));
 		HCK(hipHostMalloc((void **)&q->node_v, (size_t)ns * sizeof(gr_hip_verdict), hipHostMallocDefault));
 		q->node_cap = ns;
@@ -2258,7 +2273,9 @@ extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uin
 		lk.unlock(); // gr_hip_fwd4_host takes it itself
 		if ((r = gr_hip_node_stage(m, n, burst, pos, q->node_lines, q->node_meta)) < 0)
 			return r;
-		r = gr_hip_fwd4_host(q, q->node_lines, q->node_meta, ns, q->node_out, q->node_v);
+		// the hand-back writes back at most the first 26 bytes: packed
+		// 32-byte prefixes come back, not whole lines
+		r = gr_hip_fwd4_host_ex(q, q->node_lines, q->node_meta, ns, q->node_out, GR_HIP_PREFIX, q->node_v);
 		lk.lock();
 	}
 	uint32_t unfinished = 0;
@@ -2266,7 +2283,7 @@ extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uin
 		unfinished = node_unfinished(m, n, pos, q->node_v);
 	else if (r < 0)
 		return r;
-	r = gr_hip_node_apply(m, n, burst, pos, by_addr ? nullptr : q->node_out, GR_HIP_LINE, q->node_v,
+	r = gr_hip_node_apply(m, n, burst, pos, by_addr ? nullptr : q->node_out, GR_HIP_PREFIX, q->node_v,
 			      c->ifaces.data(), c->max_ifaces, c->nh.data(), (uint32_t)c->nh.size(), stats);
 	return r < 0 ? r : (int)unfinished;
 }
@@ -2347,14 +2364,16 @@ extern "C" int gr_hip_batch_alloc(gr_hip_ctx_t *c, uint32_t n, uint32_t in_strid
 }
 
 extern "C" int gr_hip_batch_place(gr_hip_ctx_t *c, gr_hip_batch *b, uint32_t candidates) {
-	if (c == nullptr || b == nullptr || b->out_lines == nullptr || b->out_stride != GR_HIP_LINE || candidates > 16
+	const bool prefix = b != nullptr && (b->flags & GR_HIP_BATCH_F_PREFIX32);
+	if (c == nullptr || b == nullptr || b->out_lines == nullptr
+	    || b->out_stride != (prefix ? (uint32_t)GR_HIP_PREFIX : (uint32_t)GR_HIP_LINE) || candidates > 16
 	    || (b->flags & GR_HIP_BATCH_F_FRAME_PTRS))
 		return -EINVAL;
 	int r = batch_ok(b);
 	if (r <= 0)
 		return r ? r : -EINVAL;
 	hipSetDevice(c->dev);
-	const size_t out_b = (size_t)b->n * GR_HIP_LINE;
+	const size_t out_b = (size_t)b->n * b->out_stride;
 	std::vector<void *> outs{b->out_lines};
 	for (uint32_t k = 0; k < candidates; k++) {
 		void *o = nullptr;

@@ -203,7 +203,7 @@ extern "C" int gr_hip_node_apply(
 ) {
 	if (n == 0)
 		return 0;
-	if (m == nullptr || verdicts == nullptr || (lines != nullptr && line_stride < GR_HIP_LINE))
+	if (m == nullptr || verdicts == nullptr || (lines != nullptr && line_stride < GR_HIP_PREFIX))
 		return -EINVAL;
 	burst = walk_burst(burst);
 	const uint8_t *L = static_cast<const uint8_t *>(lines);

@@ -196,10 +196,13 @@ class Queue:
     def stream(self):
         return self.lib.gr_hip_queue_stream(self._h)
 
-    def submit(self, in_frames, out_lines, meta, verdicts, n, in_stride=64, out_stride=64, lines_only=False):
-        """Enqueue the fused kernel on device buffers (torch tensors / pointers)."""
+    def submit(self, in_frames, out_lines, meta, verdicts, n, in_stride=64, out_stride=64, lines_only=False,
+               prefix32=False):
+        """Enqueue the fused kernel on device buffers (torch tensors / pointers).
+        prefix32: out_lines gets packed 32-byte prefixes (GR_HIP_BATCH_F_PREFIX32)."""
+        flags = (abi.BATCH_F_LINES_ONLY if lines_only else 0) | (abi.BATCH_F_PREFIX32 if prefix32 else 0)
         b = abi.Batch(ptr(in_frames), ptr(out_lines), ptr(meta), ptr(verdicts), n, in_stride,
-                      out_stride, abi.BATCH_F_LINES_ONLY if lines_only else 0)
+                      abi.PREFIX if prefix32 else out_stride, flags)
         check("gr_hip_fwd4_submit", self.lib.gr_hip_fwd4_submit(self._h, ctypes.byref(b)))
 
     def sync(self):

@@ -331,6 +331,12 @@ struct gr_hip_batch {
 // first 64 bytes in place (the bytes grout's chain changes, and the others
 // as they were), else lines go to out_lines as usual.
 #define GR_HIP_BATCH_F_FRAME_PTRS 0x2
+// out_lines receives only the first 32 bytes of each output line, out_stride
+// 32: every byte the path can change lies there (Ethernet header 0-13, IPv4
+// TTL 22 and checksum 24-25, IPv6 hop limit 21); bytes 32-63 of every frame
+// leave as they came. Not with in-place rewrite (out_lines NULL).
+#define GR_HIP_BATCH_F_PREFIX32 0x4
+#define GR_HIP_PREFIX 32
 
 // Per-iface counters of one queue (iface.h:105-119 subset the path touches).
 struct gr_hip_iface_stats {
@@ -497,6 +503,18 @@ int gr_hip_fwd4_host(
 	void *out_lines,
 	struct gr_hip_verdict *verdicts
 );
+// The same with the output stride chosen: GR_HIP_LINE (64, whole lines, as
+// gr_hip_fwd4_host) or GR_HIP_PREFIX (32: packed prefixes holding every byte
+// the path changes, GR_HIP_BATCH_F_PREFIX32; less PCIe traffic back).
+int gr_hip_fwd4_host_ex(
+	gr_hip_queue_t *,
+	const void *lines,
+	const struct gr_hip_pkt_meta *meta,
+	uint32_t n,
+	void *out_lines,
+	uint32_t out_stride,
+	struct gr_hip_verdict *verdicts
+);
 
 // Per-iface counters accumulated by the queue's kernels (rx in iface_input,
 // tx in iface_output). `stats` receives max_ifaces entries.
@@ -614,8 +632,9 @@ int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, c
 		      struct gr_hip_pkt_meta *meta);
 
 // Hand back: apply the fast path's verdicts and rewritten header lines
-// (slot pos[i], line_stride apart; lines NULL: the frames were rewritten in
-// place) to the mbufs. ifaces[id] / nh[slot] are the mirrors pushed with
+// (slot pos[i], line_stride apart, >= 32: only the first 26 bytes of a line
+// are written back, so packed 32-byte prefixes do; lines NULL: the frames
+// were rewritten in place) to the mbufs. ifaces[id] / nh[slot] are the mirrors pushed with
 // gr_hip_iface_set / gr_hip_nh_set (the egress VLAN tag and the ingress VLAN
 // demux are read from them). stats (optional) accumulates the per-node
 // counters of the graph walks (as gr_hip_node_layout cuts them).
