@@ -88,6 +88,8 @@ gr_fib6_t *gr_fib6_new(uint32_t max_routes, uint32_t max_groups) {
 		return NULL;
 	if (max_groups == 0)
 		max_groups = 1u << 16;
+	if (max_groups > GR_FIB6_IDX)
+		return NULL;
 	gr_fib6_t *f = calloc(1, sizeof(*f));
 	if (f == NULL)
 		return NULL;
@@ -275,24 +277,66 @@ static void mark(gr_fib6_t *f, uint32_t ent) {
 		mark(f, f->skips[ent & GR_FIB6_IDX].child);
 		return;
 	}
-	const uint32_t g = ent & GR_FIB6_IDX;
-	f->live[g] = 1;
-	for (int i = 0; i < GR_FIB6_GROUP; i++)
+	const uint32_t g = ent & GR_FIB6_IDX, slots = (ent & GR_FIB6_WIDE) ? GR_FIB6_GROUP : 1;
+	for (uint32_t s = 0; s < slots; s++)
+		f->live[g + s] = 1;
+	for (uint32_t i = 0; i < slots * GR_FIB6_GROUP; i++)
 		mark(f, f->groups[(size_t)g * GR_FIB6_GROUP + i]);
 }
 
 static uint32_t relink(const gr_fib6_t *f, uint32_t ent) {
+	// a wide group's slots stay consecutive: all live, packed in order
 	if ((ent & GR_FIB6_EXT) && !(ent & GR_FIB6_SKIP))
-		return GR_FIB6_EXT | f->remap[ent & GR_FIB6_IDX];
+		return (ent & (GR_FIB6_EXT | GR_FIB6_WIDE)) | f->remap[ent & GR_FIB6_IDX];
 	return ent;
 }
 
-// Compress, then pack the groups still referenced to the front.
-static void compress_all(gr_fib6_t *f) {
-	f->n_painted = f->n_groups;
-	f->n_skips = 0;
-	for (uint32_t i = 0; i < GR_FIB6_TOP; i++)
-		f->top[i] = compress(f, f->top[i]);
+// Level compression (top-down, entries at byte b): a group whose entries
+// hold at least GR_FIB6_WIDE_MIN child groups and no skip node, at b <= 14,
+// becomes a wide group: entry (x, y) = entry y of child x, or the group's
+// own leaf at x repeated. Stops quietly when the group capacity runs out.
+static uint32_t widen(gr_fib6_t *f, uint32_t ent, unsigned b) {
+	if (!(ent & GR_FIB6_EXT) || b >= 16)
+		return ent;
+	if (ent & GR_FIB6_SKIP) {
+		struct gr_fib6_skip *k = &f->skips[ent & GR_FIB6_IDX];
+		k->child = widen(f, k->child, b + k->n);
+		return ent;
+	}
+	const uint32_t g = ent & GR_FIB6_IDX;
+	uint32_t n_grp = 0, n_skip = 0;
+	for (int i = 0; i < GR_FIB6_GROUP; i++) {
+		const uint32_t e = f->groups[(size_t)g * GR_FIB6_GROUP + i];
+		if (e & GR_FIB6_EXT)
+			*((e & GR_FIB6_SKIP) ? &n_skip : &n_grp) += 1;
+	}
+	if (b <= 14 && n_skip == 0 && n_grp >= GR_FIB6_WIDE_MIN && f->n_groups + GR_FIB6_GROUP <= f->max_groups) {
+		const uint32_t w = f->n_groups;
+		f->n_groups += GR_FIB6_GROUP;
+		const uint32_t *grp = f->groups + (size_t)g * GR_FIB6_GROUP;
+		uint32_t *W = f->groups + (size_t)w * GR_FIB6_GROUP;
+		for (int x = 0; x < GR_FIB6_GROUP; x++) {
+			uint32_t *row = W + (size_t)x * GR_FIB6_GROUP;
+			if (grp[x] & GR_FIB6_EXT)
+				memcpy(row, f->groups + (size_t)(grp[x] & GR_FIB6_IDX) * GR_FIB6_GROUP,
+				       GR_FIB6_GROUP * sizeof(uint32_t));
+			else
+				for (int y = 0; y < GR_FIB6_GROUP; y++)
+					row[y] = grp[x];
+		}
+		for (uint32_t i = 0; i < GR_FIB6_GROUP * GR_FIB6_GROUP; i++)
+			W[i] = widen(f, W[i], b + 2);
+		return GR_FIB6_EXT | GR_FIB6_WIDE | w;
+	}
+	for (int i = 0; i < GR_FIB6_GROUP; i++) {
+		uint32_t *e = &f->groups[(size_t)g * GR_FIB6_GROUP + i];
+		*e = widen(f, *e, b + 1);
+	}
+	return ent;
+}
+
+// Pack the groups still referenced to the front.
+static void pack(gr_fib6_t *f) {
 	memset(f->live, 0, f->n_groups);
 	for (uint32_t i = 0; i < GR_FIB6_TOP; i++)
 		mark(f, f->top[i]);
@@ -312,6 +356,18 @@ static void compress_all(gr_fib6_t *f) {
 			dst[i] = relink(f, src[i]);
 	}
 	f->n_groups = n;
+}
+
+// Path-compress, pack, level-compress, pack again.
+static void compress_all(gr_fib6_t *f) {
+	f->n_painted = f->n_groups;
+	f->n_skips = 0;
+	for (uint32_t i = 0; i < GR_FIB6_TOP; i++)
+		f->top[i] = compress(f, f->top[i]);
+	pack(f);
+	for (uint32_t i = 0; i < GR_FIB6_TOP; i++)
+		f->top[i] = widen(f, f->top[i], 2);
+	pack(f);
 }
 
 int gr_fib6_build(gr_fib6_t *f) {
@@ -355,6 +411,9 @@ uint32_t gr_fib6_lookup(const gr_fib6_t *f, const uint8_t ip[16]) {
 			const bool match = b + k->n <= 16 && memcmp(ip + b, k->key, k->n) == 0;
 			ent = match ? k->child : k->miss;
 			b += k->n;
+		} else if (ent & GR_FIB6_WIDE) {
+			ent = f->groups[(size_t)(ent & GR_FIB6_IDX) * GR_FIB6_GROUP + ((uint32_t)ip[b] << 8) + ip[b + 1]];
+			b += 2;
 		} else {
 			ent = f->groups[(size_t)(ent & GR_FIB6_IDX) * GR_FIB6_GROUP + ip[b++]];
 		}

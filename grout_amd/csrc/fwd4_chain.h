@@ -11,6 +11,7 @@
 // 4-lanes-per-row coalesced fill/drain and for one-row-per-lane reads.
 #pragma once
 
+#include "fib6.h" // the trie entry encoding chain_fib6 walks
 #include "fwd4_dev.h"
 
 // Kernel-wide view of the tables (read once per wave from fwd4_tables).
@@ -385,16 +386,19 @@ __device__ __forceinline__ uint32_t chain_fib6(const fwd4_rx6 &v, const uint32_t
 	uint32_t ent = gld(v.top + ((byte_of(key, 0) << 8) | byte_of(key, 1)));
 	int b = 2;
 	while (b < 16 && (ent & 0x80000000u)) {
-		if (ent & 0x40000000u) { // skip node: key bytes 0-6, n in byte 7
-			const uint4 k = gld4(v.skips + (ent & 0x3fffffffu));
+		if (ent & GR_FIB6_SKIP) { // skip node: key bytes 0-6, n in byte 7
+			const uint4 k = gld4(v.skips + (ent & GR_FIB6_IDX));
 			const int n = k.y >> 24;
 			bool match = b + n <= 16;
 			for (int i = 0; i < n && match; i++)
 				match = byte_of(key, b + i) == ((i < 4 ? k.x >> (8 * i) : k.y >> (8 * (i - 4))) & 0xff);
 			ent = match ? k.z : k.w;
 			b += n;
+		} else if (ent & GR_FIB6_WIDE) { // wide group: bytes b and b + 1 (b <= 14)
+			ent = gld(v.groups + (size_t)(ent & GR_FIB6_IDX) * 256 + (byte_of(key, b) << 8) + byte_of(key, b + 1));
+			b += 2;
 		} else {
-			ent = gld(v.groups + (size_t)(ent & 0x3fffffffu) * 256 + byte_of(key, b));
+			ent = gld(v.groups + (size_t)(ent & GR_FIB6_IDX) * 256 + byte_of(key, b));
 			b++;
 		}
 	}

@@ -316,3 +316,46 @@ def test_kat_gpu(fastpath, ref, topo_kw, frame, pkt_len, expect):
     arr, meta = S.pack([frame()], pkt_lens=None if pkt_len is None else [pkt_len])
     _, v, _ = run_gpu(fastpath, t, arr, meta)
     assert abi.EDGE_NAMES[v["edge"][0]] == expect, ref
+
+
+def _wide_entries(host, f):
+    """Wide-group references (GR_FIB6_WIDE) in the painted trie: first
+    level, groups and skip-node children."""
+    import ctypes
+    for fn in ("gr_fib6_top", "gr_fib6_groups", "gr_fib6_skips"):
+        getattr(host, fn).restype = ctypes.c_void_p
+        getattr(host, fn).argtypes = [ctypes.c_void_p]
+    ng, ns = host.gr_fib6_groups_used(f), host.gr_fib6_skips_used(f)
+    top = np.ctypeslib.as_array(ctypes.cast(host.gr_fib6_top(f), ctypes.POINTER(ctypes.c_uint32)), shape=(65536,))
+    grp = np.ctypeslib.as_array(ctypes.cast(host.gr_fib6_groups(f), ctypes.POINTER(ctypes.c_uint32)),
+                                shape=(max(ng, 1) * 256,))
+    sk = np.ctypeslib.as_array(ctypes.cast(host.gr_fib6_skips(f), ctypes.POINTER(ctypes.c_uint32)),
+                               shape=(max(ns, 1) * 4,)).reshape(-1, 4)
+    allv = np.concatenate([top, grp[:ng * 256], sk[:ns, 2]])  # struct gr_fib6_skip: child at byte 8
+    return int(((allv & 0xE0000000) == 0xA0000000).sum())
+
+
+@pytest.mark.parametrize("max_groups", [1 << 16, 300])
+def test_fib6_level_compression(max_groups):
+    """Dense /48s (fib_inject -6's largest bucket shape: 2400:0:vvvv:vvvv::/48)
+    make wide groups (two bytes per gather) when the group capacity allows,
+    and the trie stays exact either way (300 groups: no room to widen)."""
+    host = abi.host()
+    n = 40_000
+    r = np.zeros(n, dtype=abi.ROUTE6_DT)
+    v = np.arange(1, n + 1, dtype=np.uint32)
+    r["ip"][:, 0] = 0x24
+    for k in range(4):
+        r["ip"][:, 2 + k] = (v >> (24 - 8 * k)) & 0xFF
+    r["prefixlen"] = 48
+    r["vrf_id"] = 1
+    r["nh"] = 1 + v % 2048
+    f = host.gr_fib6_new(n + 16, max_groups)
+    for x in r:
+        ip = np.ascontiguousarray(x["ip"])
+        assert host.gr_fib6_add(f, ip.ctypes.data, 48, int(x["nh"]), 0) == 0
+    assert host.gr_fib6_build(f) == 0
+    wide = _wide_entries(host, f)
+    assert (wide > 0) == (max_groups == 1 << 16), wide
+    _fib6_check(host, f, r, np.random.default_rng(68), 20_000)
+    host.gr_fib6_free(f)
