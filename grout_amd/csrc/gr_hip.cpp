@@ -17,6 +17,7 @@
 #include "fwd4_kernel.h"
 
 #include <algorithm>
+#include <atomic>
 #include <errno.h>
 #include <mutex>
 #include <shared_mutex>
@@ -241,7 +242,7 @@ struct gr_hip_ctx {
 	uint32_t stage_i;
 	hipEvent_t ready_ev[2];
 	uint64_t serial; // publications so far
-	uint32_t commit_us[3]; // the last commit: staging (host), enqueue (shared lock), publish (exclusive lock)
+	std::atomic<uint32_t> commit_us[3]; // the last commit: staging (host), enqueue (shared lock), publish (exclusive lock)
 	std::mutex occ_mu; // the occupancy cache below (launches run concurrently)
 	int occ_ring[8]; // by variant, of the last launch's geometry and staging ("occupancy")
 	struct occ_entry {
@@ -1448,9 +1449,9 @@ extern "C" int gr_hip_fib4_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 		v.pend8 = std::move(d8);
 	});
 	const uint64_t t3 = now_us();
-	c->commit_us[0] = (uint32_t)(t1 - t0);
-	c->commit_us[1] = (uint32_t)(t2 - t1);
-	c->commit_us[2] = (uint32_t)(t3 - t2);
+	c->commit_us[0].store((uint32_t)(t1 - t0), std::memory_order_relaxed);
+	c->commit_us[1].store((uint32_t)(t2 - t1), std::memory_order_relaxed);
+	c->commit_us[2].store((uint32_t)(t3 - t2), std::memory_order_relaxed);
 	return r;
 }
 
@@ -1926,7 +1927,8 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		const int i = strcmp(k, "stage") == 0 ? 0 : strcmp(k, "enqueue") == 0 ? 1 : strcmp(k, "publish") == 0 ? 2 : -1;
 		if (i < 0)
 			return -ENOENT;
-		return (int)(c->commit_us[i] > 0x7fffffffu ? 0x7fffffffu : c->commit_us[i]);
+		const uint32_t us = c->commit_us[i].load(std::memory_order_relaxed);
+		return (int)(us > 0x7fffffffu ? 0x7fffffffu : us);
 	} else if (strcmp(key, "occupancy") == 0) { // read-only: WGs/CU of the current variant
 		return c->occ_ring[(c->stats_on ? FWD4_V_STATS : 0) | c->nt]; // as of the last launch
 	} else {

@@ -124,3 +124,29 @@ def test_prefix32_rejects_bad_batches(fastpath):
             assert fastpath.lib.gr_hip_fwd4_submit(q._h, ctypes.byref(b)) == -22, (out - p if out else 0, stride)
     finally:
         q.close()
+
+
+@pytest.mark.gpu
+def test_prefix32_host_path(fastpath):
+    """gr_hip_fwd4_host_ex with 32-byte prefixes back, on pinned host memory
+    (the kernel's own PCIe loads and stores) and on pageable memory (staged
+    chunk copies): the same prefixes and verdicts as the oracle."""
+    import torch
+    tf = topo_for("fullview")
+    fresh_fastpath_state(fastpath, tf)
+    n = (1 << 19) + 5  # two chunks of the staged path and a ragged end
+    fr, me = S.stream(n, 0x32F3, routes=tf.route_array())
+    o = oracle.Oracle(tf).process(fr, me, lines_only=True)
+    q = fastpath.queue()
+    try:
+        for pinned in (True, False):
+            mk = (lambda a: torch.from_numpy(a).pin_memory()) if pinned else torch.from_numpy
+            h_in, h_me = mk(np.ascontiguousarray(fr)), mk(me.view(np.uint8).copy())
+            h_out = mk(np.zeros(n * abi.PREFIX, dtype=np.uint8))
+            h_v = mk(np.zeros(n * 8, dtype=np.uint8))
+            abi.check("gr_hip_fwd4_host_ex", fastpath.lib.gr_hip_fwd4_host_ex(
+                q._h, h_in.data_ptr(), h_me.data_ptr(), n, h_out.data_ptr(), abi.PREFIX, h_v.data_ptr()))
+            assert np.array_equal(o[1], h_v.numpy().view(abi.VERDICT_DT)), pinned
+            assert np.array_equal(o[0][:, :32], h_out.numpy().reshape(n, abi.PREFIX)), pinned
+    finally:
+        q.close()
