@@ -2365,6 +2365,33 @@ extern "C" int gr_hip_batch_alloc(gr_hip_ctx_t *c, uint32_t n, uint32_t in_strid
 	return 0;
 }
 
+// Kernel time of batch t on the probe queue q: 2 warm-up launches, 4 timed.
+static int place_time(gr_hip_queue *q, const gr_hip_batch &t, float *ms) {
+	for (int i = 0; i < 6; i++) {
+		const int r = gr_hip_fwd4_submit(q, &t);
+		if (r)
+			return r;
+	}
+	uint32_t cnt = 0;
+	const int r = gr_hip_queue_kernel_ms(q, 4, ms, &cnt);
+	return r ? r : cnt == 4 ? 0 : -EIO; // the probes must all be timed
+}
+
+// Up to `candidates` more device buffers of `bytes` each (fewer when memory
+// runs short), after `cur`.
+static std::vector<void *> place_alloc(void *cur, size_t bytes, uint32_t candidates) {
+	std::vector<void *> v{cur};
+	for (uint32_t k = 0; k < candidates; k++) {
+		void *o = nullptr;
+		if (hipMalloc(&o, bytes) != hipSuccess) {
+			(void)hipGetLastError();
+			break;
+		}
+		v.push_back(o);
+	}
+	return v;
+}
+
 extern "C" int gr_hip_batch_place(gr_hip_ctx_t *c, gr_hip_batch *b, uint32_t candidates) {
 	const bool prefix = b != nullptr && (b->flags & GR_HIP_BATCH_F_PREFIX32);
 	if (c == nullptr || b == nullptr || b->out_lines == nullptr
@@ -2375,53 +2402,66 @@ extern "C" int gr_hip_batch_place(gr_hip_ctx_t *c, gr_hip_batch *b, uint32_t can
 	if (r <= 0)
 		return r ? r : -EINVAL;
 	hipSetDevice(c->dev);
-	const size_t out_b = (size_t)b->n * b->out_stride;
-	std::vector<void *> outs{b->out_lines};
-	for (uint32_t k = 0; k < candidates; k++) {
-		void *o = nullptr;
-		if (hipMalloc(&o, out_b) != hipSuccess) { // fewer candidates when memory runs short
-			(void)hipGetLastError();
-			break;
-		}
-		outs.push_back(o);
-	}
+	if (candidates == 0)
+		return 0;
 	gr_hip_queue_t *q = nullptr;
-	r = outs.size() > 1 ? gr_hip_queue_create(c, nullptr, &q) : 0;
+	if ((r = gr_hip_queue_create(c, nullptr, &q)) != 0)
+		return r;
+	// no counters on this queue: the probe launches run the counter-less
+	// kernel variant, so they neither count nor show up as the counted one
+	hipStreamSynchronize(q->s);
+	hipFree(q->d_stats);
+	q->d_stats = nullptr;
+	q->always_timed = true; // "untimed" / "time_every" do not apply to the probes
+	// 1. the output lines: candidates against the current buffer
+	std::vector<void *> outs = place_alloc(b->out_lines, (size_t)b->n * b->out_stride, candidates);
 	size_t pick = 0;
-	if (q != nullptr) {
-		// no counters on this queue: the probe launches run the counter-less
-		// kernel variant, so they neither count nor show up as the counted one
-		hipStreamSynchronize(q->s);
-		hipFree(q->d_stats);
-		q->d_stats = nullptr;
-		q->always_timed = true; // "untimed" / "time_every" do not apply to the probes
-		float best = 0;
-		for (size_t k = 0; k < outs.size() && r == 0; k++) {
+	float best = 0;
+	for (size_t k = 0; k < outs.size() && r == 0; k++) {
+		gr_hip_batch t = *b;
+		t.out_lines = outs[k];
+		float ms = 0;
+		if ((r = place_time(q, t, &ms)) == 0 && (k == 0 || ms < best)) {
+			best = ms;
+			pick = k;
+		}
+	}
+	// 2. the frames, against the lines just kept: each candidate gets a
+	// copy of the batch's frames (the pair decides)
+	const size_t in_b = (size_t)b->n * b->in_stride;
+	std::vector<void *> ins{const_cast<void *>(b->in_frames)};
+	size_t pick_in = 0;
+	if (r == 0) {
+		ins = place_alloc(const_cast<void *>(b->in_frames), in_b, candidates);
+		for (size_t k = 1; k < ins.size() && r == 0; k++) {
+			if (hipMemcpyAsync(ins[k], b->in_frames, in_b, hipMemcpyDeviceToDevice, q->s) != hipSuccess) {
+				(void)hipGetLastError();
+				r = -EIO;
+				break;
+			}
 			gr_hip_batch t = *b;
-			t.out_lines = outs[k];
-			for (int i = 0; i < 6 && r == 0; i++) // 2 warm-up launches, 4 timed
-				r = gr_hip_fwd4_submit(q, &t);
+			t.in_frames = ins[k];
+			t.out_lines = outs[pick];
 			float ms = 0;
-			uint32_t cnt = 0;
-			if (r == 0)
-				r = gr_hip_queue_kernel_ms(q, 4, &ms, &cnt);
-			if (r == 0 && cnt != 4)
-				r = -EIO; // the probes must all be timed
-			if (r == 0 && (k == 0 || ms < best)) {
+			if ((r = place_time(q, t, &ms)) == 0 && ms < best) {
 				best = ms;
-				pick = k;
+				pick_in = k;
 			}
 		}
-		if (r == 0)
-			r = gr_hip_queue_sync(q);
-		gr_hip_queue_destroy(q);
 	}
+	if (r == 0)
+		r = gr_hip_queue_sync(q);
+	gr_hip_queue_destroy(q);
 	if (r)
-		pick = 0; // keep the batch as it was
+		pick = pick_in = 0; // keep the batch as it was
 	for (size_t k = 0; k < outs.size(); k++)
 		if (k != pick)
 			hipFree(outs[k]);
+	for (size_t k = 0; k < ins.size(); k++)
+		if (k != pick_in)
+			hipFree(ins[k]);
 	b->out_lines = outs[pick];
+	b->in_frames = ins[pick_in];
 	return r;
 }
 

@@ -536,10 +536,13 @@ int gr_hip_batch_alloc(gr_hip_ctx_t *, uint32_t n, uint32_t in_stride, struct gr
 // kernel's time by up to ~20 % (concurrent reads and writes that collide in
 // the memory channels). With the batch's frames and metadata in
 // place, this allocates `candidates` more output-line buffers, times each
-// (and the current one) over the batch on a private queue without counters,
-// keeps the fastest and frees the rest. `b` must come from
-// gr_hip_batch_alloc; its output lines and verdicts are overwritten (with
-// the batch's results). On error the batch is left as it was.
+// (and the current one) over the batch on a private queue without counters
+// and keeps the fastest; then `candidates` more frame buffers, each holding a
+// copy of the frames, timed against the lines kept, and keeps the fastest
+// of those and the current one. The rest are freed. `b` must come from
+// gr_hip_batch_alloc; in_frames and out_lines may change (the frames keep
+// their content), output lines and verdicts are overwritten (with the
+// batch's results). On error the batch is left as it was.
 int gr_hip_batch_place(gr_hip_ctx_t *, struct gr_hip_batch *b, uint32_t candidates);
 int gr_hip_batch_free(gr_hip_ctx_t *, struct gr_hip_batch *b);
 // Pin and map caller memory for the GPU (grout: the mbuf pools' memory), so
