@@ -282,8 +282,8 @@ def main():
                else {"tbl8_groups_used": int(info["tbl8_used"])}),
             "parallelism": f"replicas x{world} (one RX stream + FIB replica per GPU, no collective)",
             "forwarded_frac": round(fwd_frac, 6),
-            "placement": (f"calibrated: output lines = fastest of {args.candidates + 1} allocations, each timed "
-                          "over a batch of this workload drawn with another seed (gr_hip_batch_place)"
+            "placement": (f"calibrated: output lines, then frames = fastest of {args.candidates + 1} allocations each, "
+                          "timed over a batch of this workload drawn with another seed (gr_hip_batch_place)"
                           if batch is not None else "plain torch allocations"),
             "output": ("packed 32-byte header prefixes (every byte the path changes; GR_HIP_BATCH_F_PREFIX32)"
                        if prefix32 else "whole 64-byte header lines"),
