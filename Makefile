@@ -89,8 +89,10 @@ $(ASAN_DIR)/liboracle.so: oracle/oracle.c oracle/oracle.h include/grout_hip.h
 	@mkdir -p $(ASAN_DIR)
 	$(SAN_C) -pthread -shared -o $@ oracle/oracle.c
 
+# globals not instrumented here: the identical edge-name literals of the node
+# sources end up registered twice at one merged address (a false ODR report)
 $(ASAN_DIR)/libgrout_graph.so: $(GRAPH_SRC) $(GRAPH_HDRS) $(ASAN_DIR)/libgrout_hip.so
-	$(SAN_C) -std=gnu11 -Iinclude -shared -o $@ $(GRAPH_SRC) -L$(ASAN_DIR) -lgrout_hip '-Wl,-rpath,$$ORIGIN'
+	$(SAN_C) -mllvm -asan-globals=0 -std=gnu11 -Iinclude -shared -o $@ $(GRAPH_SRC) -L$(ASAN_DIR) -lgrout_hip '-Wl,-rpath,$$ORIGIN'
 
 asan: $(ASAN_DIR)/libgrout_hip.so $(ASAN_DIR)/libgrout_host.so $(ASAN_DIR)/liboracle.so $(ASAN_DIR)/libgrout_graph.so
 
