@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--batch", type=int, default=1 << 24)
-    ap.add_argument("--workload", default="fullview64", choices=["fullview64", "single64"])
+    ap.add_argument("--workload", default="fullview64", choices=["fullview64", "single64", "fullview6"])
     ap.add_argument("--nt", default="0,1")
     ap.add_argument("--wg", default="0,6")
     ap.add_argument("--fib16", default="2,1,0", help="gr_hip_tune fib_format values")
@@ -41,13 +41,19 @@ def main():
     if args.workload == "single64":
         topo = T.config_single_route()
         kw = dict(dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    elif args.workload == "fullview6":
+        topo = T.config_fullview6()
     else:
         topo = T.config_fullview()
         kw = dict(routes=topo.route_array())
     fp = FastPath(0)
     fp.load(topo)
     n = args.batch
-    frames, meta = S.stream(n, S.SEED_GPU_BASE, **kw)
+    if args.workload == "fullview6":
+        r6 = topo.route6_array()
+        frames, meta = S.stream6(n, S.SEED_GPU_BASE, r6[r6["prefixlen"] < 128])
+    else:
+        frames, meta = S.stream(n, S.SEED_GPU_BASE, **kw)
     d_src = torch.from_numpy(frames.reshape(-1)).to(dev)
     bufs = [torch.empty_like(d_src) for _ in range(args.reps + 1)]
     d_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
@@ -62,8 +68,9 @@ def main():
         for v in variants:
             f16, st, nt, wg, ring, place = v
             fp.tune("ring", ring)
-            fp.tune("fib_format", f16)
-            fp.fib_commit(T.VRF_MAIN)  # re-uploads when the format changes
+            if args.workload != "fullview6":
+                fp.tune("fib_format", f16)
+                fp.fib_commit(T.VRF_MAIN)  # re-uploads when the format changes
             fp.tune("stats", st)
             fp.tune("nt", nt)
             fp.tune("wg_per_cu", wg)
