@@ -166,3 +166,63 @@ def test_snapshot_under_churn(fastpath, fmt):
     finally:
         fastpath.tune("fib_format", 2)
         fresh_fastpath_state(fastpath, T.config_single_route())
+
+
+def _two_vrf_topology():
+    t = T.Topology(max_ifaces=64, max_nexthops=64)
+    t.add_vrf(1)
+    t.add_vrf(20)
+    t.add_port(2, 0, "02:00:00:00:00:02", vrf_id=1)
+    t.add_port(3, 1, "02:00:00:00:00:03", vrf_id=1)
+    t.add_port(4, 2, "02:00:00:00:00:04", vrf_id=20)
+    t.add_port(5, 3, "02:00:00:00:00:05", vrf_id=20)
+    nh = {"a": t.add_nexthop(3, "172.16.3.2", "02:00:00:01:00:0a"),
+          "b": t.add_nexthop(3, "172.16.3.3", "02:00:00:01:00:0b"),
+          "c": t.add_nexthop(5, "172.16.5.2", "02:00:00:01:00:0c"),
+          "d": t.add_nexthop(5, "172.16.5.3", "02:00:00:01:00:0d")}
+    t.add_route(1, "10.0.0.0/8", nh["a"])
+    t.add_route(20, "10.0.0.0/8", nh["c"])
+    t.add_route(20, "10.1.0.0/16", nh["d"])
+    return t, nh
+
+
+@pytest.mark.parametrize("fmt", [2, 1])
+def test_commits_interleaved_across_vrfs(fastpath, fmt):
+    """Commits of two VRFs interleaved: each publication flips the context's
+    view generation, and the other VRF must keep its published copy (not
+    the copy it last wrote). Streams enter both VRFs at once."""
+    from grout_amd import synth as S
+    t, nh = _two_vrf_topology()
+    n = 1 << 14
+    streams = [S.stream(n, 0x2F0 + k, dst_range=(T.ip4("10.0.0.0"), T.ip4("10.3.255.255")),
+                        in_iface=port, dst_mac=mac)
+               for k, (port, mac) in enumerate([(2, "02:00:00:00:00:02"), (4, "02:00:00:00:00:04")])]
+    fr = np.concatenate([streams[0][0], streams[1][0]])
+    me = np.concatenate([streams[0][1], streams[1][1]])
+    fastpath.tune("fib_format", fmt)
+    try:
+        run_gpu(fastpath, t, fr, me)  # loads t: both VRFs committed
+        o = oracle.Oracle(t, build_dir24=False)
+        steps = [(1, [("add", "10.2.0.0/16", "b")]), (20, [("rep", "10.1.0.0/16", "c")]),
+                 (20, [("add", "10.2.3.0/24", "d")]), (1, [("rep", "10.0.0.0/8", "b"), ("del", "10.2.0.0/16")]),
+                 (1, []), (20, [("del", "10.1.0.0/16")]), (1, [("add", "10.3.0.0/17", "a")])]
+        for vrf, ops in steps:
+            for op in ops:
+                r = _route(op[1], nh[op[2]]) if op[0] != "del" else None
+                if r is not None:
+                    r["vrf_id"] = vrf
+                    fastpath.route_add(r, replace=op[0] == "rep")
+                    assert o.L.or_route_add(o.h, r.ctypes.data, 1, 1 if op[0] == "rep" else 0) == 0
+                else:
+                    net = T.ipaddress.IPv4Network(op[1])
+                    fastpath.route_del(vrf, int(net.network_address), net.prefixlen)
+                    be = int.from_bytes(int(net.network_address).to_bytes(4, "big"), "little")
+                    assert o.L.or_route_del(o.h, vrf, be, net.prefixlen) == 0
+            fastpath.fib_commit(vrf)
+            o.L.or_fib_build(o.h, vrf)
+            ref, g = o.process(fr, me), run_gpu(fastpath, t, fr, me)
+            assert np.array_equal(ref[1], g[1]), (vrf, ops)
+            assert np.array_equal(ref[0], g[0]), (vrf, ops)
+    finally:
+        fastpath.tune("fib_format", 2)
+        fresh_fastpath_state(fastpath, T.config_single_route())
