@@ -622,22 +622,31 @@ def test_mixed_v4_v6_stream(fastpath):
 
 def test_live_route6_updates(fastpath):
     """route6 add / replace / delete after the first commit, then parity
-    (rib6_insert_or_replace / rib6_delete, modules/ip6/control/route.c)."""
-    t = T.config_fullview6(count=5_000)
+    (rib6_insert_or_replace / rib6_delete, modules/ip6/control/route.c), one
+    commit per kind of change so that the trie's two device copies alternate;
+    40k routes, so that the /48 bucket gets wide groups (fib6.h)."""
+    t = T.config_fullview6(count=40_000)
     r = t.route6_array()
     fr, me = S.stream6(1 << 16, 0x1606, r[r["prefixlen"] < 128])
     run_gpu(fastpath, t, fr, me)  # loads t
     o = oracle.Oracle(t)
     rng = np.random.default_rng(16)
     idx = rng.permutation(len(r) - 1)  # leave the address route alone
+
+    def commit_and_compare():
+        fastpath.fib6_commit(1)
+        compare(o.process(fr, me), run_gpu(fastpath, t, fr, me))
+
     for i in idx[:500]:
         fastpath.route6_del(1, bytes(r["ip"][i]), int(r["prefixlen"][i]))
         ip = np.ascontiguousarray(r["ip"][i])
         assert o.L.or_route6_del(o.h, 1, 0, ip.ctypes.data, int(r["prefixlen"][i])) == 0
+    commit_and_compare()
     rep = r[idx[500:800]].copy()
     rep["nh"] = np.roll(rep["nh"], 1)
     fastpath.route6_add(rep, replace=True)
     assert o.L.or_route6_add(o.h, rep.ctypes.data, len(rep), 1) == 0
+    commit_and_compare()
     new = r[idx[800:900]].copy()
     new["prefixlen"] = np.minimum(new["prefixlen"].astype(np.int32) + 8, 128).astype(np.uint8)
     new["ip"][:, 15] ^= 0x5A  # more-specifics under existing routes
@@ -645,8 +654,7 @@ def test_live_route6_updates(fastpath):
     new = new[[(bytes(x["ip"]), int(x["prefixlen"])) not in uniq for x in new]]
     fastpath.route6_add(new, replace=True)
     assert o.L.or_route6_add(o.h, new.ctypes.data, len(new), 1) == 0
-    fastpath.fib6_commit(1)
-    compare(o.process(fr, me), run_gpu(fastpath, t, fr, me))
+    commit_and_compare()
     g = run_gpu(fastpath, t, fr, me)
     assert (g[1]["edge"] == abi.EDGE["ip6_error_dest_unreach"]).sum() > 0
     for x in list(r[idx[:20]]) + list(rep[:20]) + list(new[:20]):
