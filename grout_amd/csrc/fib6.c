@@ -291,15 +291,48 @@ static uint32_t relink(const gr_fib6_t *f, uint32_t ent) {
 	return ent;
 }
 
+// Group slots in the subtree of `ent`, counting stops at `cap`.
+static uint32_t subtree_groups(const gr_fib6_t *f, uint32_t ent, uint32_t cap) {
+	if (!(ent & GR_FIB6_EXT))
+		return 0;
+	if (ent & GR_FIB6_SKIP)
+		return subtree_groups(f, f->skips[ent & GR_FIB6_IDX].child, cap);
+	const uint32_t slots = (ent & GR_FIB6_WIDE) ? GR_FIB6_GROUP : 1;
+	uint32_t n = slots;
+	const uint32_t *e = f->groups + (size_t)(ent & GR_FIB6_IDX) * GR_FIB6_GROUP;
+	for (uint32_t i = 0; i < slots * GR_FIB6_GROUP && n < cap; i++)
+		n += subtree_groups(f, e[i], cap - n);
+	return n;
+}
+
 // Level compression (top-down, entries at byte b): a group whose entries
 // hold at least GR_FIB6_WIDE_MIN child groups and no skip node, at b <= 14,
 // becomes a wide group: entry (x, y) = entry y of child x, or the group's
-// own leaf at x repeated. Stops quietly when the group capacity runs out.
+// own leaf at x repeated; so does a one-byte skip whose child group heads at
+// least GR_FIB6_SKIP_WIDE_MIN groups. Stops quietly when the group capacity
+// runs out.
 static uint32_t widen(gr_fib6_t *f, uint32_t ent, unsigned b) {
 	if (!(ent & GR_FIB6_EXT) || b >= 16)
 		return ent;
 	if (ent & GR_FIB6_SKIP) {
 		struct gr_fib6_skip *k = &f->skips[ent & GR_FIB6_IDX];
+		// a one-byte skip over a heavy subtree becomes a wide group: row
+		// key = the child group, every other row the miss leaf (the skip's
+		// test and the child's gather in one gather)
+		if (k->n == 1 && b <= 14 && (k->child & GR_FIB6_EXT) && !(k->child & (GR_FIB6_SKIP | GR_FIB6_WIDE))
+		    && f->n_groups + GR_FIB6_GROUP <= f->max_groups
+		    && subtree_groups(f, k->child, GR_FIB6_SKIP_WIDE_MIN) >= GR_FIB6_SKIP_WIDE_MIN) {
+			const uint32_t w = f->n_groups;
+			f->n_groups += GR_FIB6_GROUP;
+			uint32_t *W = f->groups + (size_t)w * GR_FIB6_GROUP;
+			for (uint32_t i = 0; i < GR_FIB6_GROUP * GR_FIB6_GROUP; i++)
+				W[i] = k->miss;
+			uint32_t *row = W + (size_t)k->key[0] * GR_FIB6_GROUP;
+			memcpy(row, f->groups + (size_t)(k->child & GR_FIB6_IDX) * GR_FIB6_GROUP, GR_FIB6_GROUP * sizeof(uint32_t));
+			for (uint32_t i = 0; i < GR_FIB6_GROUP; i++)
+				row[i] = widen(f, row[i], b + 2);
+			return GR_FIB6_EXT | GR_FIB6_WIDE | w;
+		}
 		k->child = widen(f, k->child, b + k->n);
 		return ent;
 	}

@@ -10,9 +10,10 @@
 // a group whose 256 entries all hold one leaf but for one index becomes a
 // skip node ("bytes b..b+n-1 equal key: continue with child, else the leaf
 // miss"), and consecutive skips merge (up to 7 key bytes); level-compressed:
-// a group whose entries are mostly child groups (and no skip) becomes one
-// wide group of 65536 entries indexed by two bytes, 256 consecutive group
-// slots, one dependent gather instead of two on its paths. Entry encoding
+// a group whose entries are mostly child groups (and no skip), or a one-byte
+// skip over a heavy subtree with its child group, becomes one wide group of
+// 65536 entries indexed by two bytes, 256 consecutive group slots, one
+// dependent gather instead of two on its paths. Entry encoding
 // (u32): bit 31 clear = the nexthop slot of the longest matching prefix (0 =
 // no route, the FIB default_nh, modules/ip6/control/route.c:68); bits 31 and 30 = skip node
 // index in bits 0-28; bits 31 and 29 = wide group (its first slot in bits
@@ -30,6 +31,7 @@ extern "C" {
 #define GR_FIB6_WIDE 0x20000000u
 #define GR_FIB6_IDX 0x1fffffffu
 #define GR_FIB6_WIDE_MIN 64 // child groups (of 256 entries) that make a group wide
+#define GR_FIB6_SKIP_WIDE_MIN 16 // groups under a one-byte skip's child that make the pair wide
 
 struct gr_fib6_skip { // 16 bytes, as the kernel loads it
 	uint8_t key[7];

@@ -359,3 +359,34 @@ def test_fib6_level_compression(max_groups):
     assert (wide > 0) == (max_groups == 1 << 16), wide
     _fib6_check(host, f, r, np.random.default_rng(68), 20_000)
     host.gr_fib6_free(f)
+
+
+@pytest.mark.parametrize("fanout,wide", [(32, True), (4, False)])
+def test_fib6_skip_widening(fanout, wide):
+    """A one-byte skip (2400:05xx::/24 is the only branch under 2400::/16)
+    over a heavy subtree (byte 3 fans out to `fanout` groups, below
+    GR_FIB6_WIDE_MIN) becomes a wide group with its child: 32 groups under it
+    qualify, 4 do not (GR_FIB6_SKIP_WIDE_MIN = 16); lookups exact either way."""
+    host = abi.host()
+    rows = []
+    for b3 in range(fanout):
+        for b4 in range(0, 256, 3):
+            rows.append((b3, b4))
+    r = np.zeros(len(rows), dtype=abi.ROUTE6_DT)
+    r["ip"][:, 0] = 0x24
+    r["ip"][:, 2] = 0x05
+    r["ip"][:, 3] = [a for a, _ in rows]
+    r["ip"][:, 4] = [b for _, b in rows]
+    r["prefixlen"] = 40
+    r["vrf_id"] = 1
+    r["nh"] = 1 + np.arange(len(rows)) % 1000
+    f = _fib6_of(host, r)
+    _wide_entries(host, f)  # sets the accessor signatures
+    import ctypes
+    top = np.ctypeslib.as_array(ctypes.cast(host.gr_fib6_top(f), ctypes.POINTER(ctypes.c_uint32)), shape=(65536,))
+    ent = int(top[0x2400])
+    assert ((ent & 0xE0000000) == 0xA0000000) == wide, hex(ent)
+    if not wide:
+        assert ent & 0x40000000, hex(ent)  # still the skip node
+    _fib6_check(host, f, r, np.random.default_rng(69 + fanout), 10_000)
+    host.gr_fib6_free(f)
