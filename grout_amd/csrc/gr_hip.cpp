@@ -1276,12 +1276,18 @@ static void stage_groups(stager &st, E *dev, const uint32_t *t8, const std::vect
 	}
 }
 
+#ifdef FIB_ALLOC_FLAGS // measurement builds: FIB arrays from hipExtMallocWithFlags
+#define fib_malloc(p, sz) hipExtMallocWithFlags((void **)(p), (sz), FIB_ALLOC_FLAGS)
+#else
+#define fib_malloc(p, sz) hipMalloc((p), (sz))
+#endif
+
 // Allocate the device arrays copy `b` needs in format `fmt`.
 static int fib4_buf_alloc(gr_hip_ctx *c, fib4_buf &b, int fmt, uint32_t num_tbl8) {
 	if (fmt != FIB_FMT_24 && b.d8_16 == nullptr)
-		HCK(hipMalloc(&b.d8_16, sizeof(uint16_t) * 256 * (size_t)num_tbl8));
+		HCK(fib_malloc(&b.d8_16, sizeof(uint16_t) * 256 * (size_t)num_tbl8));
 	if (fmt == FIB_FMT_24_W2 && b.d24_16 == nullptr)
-		HCK(hipMalloc(&b.d24_16, sizeof(uint16_t) * GR_FIB4_TBL24_ENTRIES));
+		HCK(fib_malloc(&b.d24_16, sizeof(uint16_t) * GR_FIB4_TBL24_ENTRIES));
 	if (fmt == FIB_FMT_16_8_8 && b.d16 == nullptr) // top + the worst case of one chunk per /16
 		HCK(hipMalloc(&b.d16, sizeof(uint32_t) * 65536 + sizeof(uint16_t) * 256 * 65536));
 	if (fmt == FIB_FMT_24 && b.d24 == nullptr) {
