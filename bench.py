@@ -78,8 +78,13 @@ def main():
 
     from grout_amd.replicas import Replicas
 
-    rep = Replicas("nccl")
-    world, rank, local = rep.world, rep.rank, rep.local
+    # GR_BENCH_SHARE_GPU=1: a rehearsal of the N>1 path on a one-GPU box,
+    # every rank on device 0 and gloo for the barrier and the clock (RCCL
+    # refuses two ranks on one GPU); the driver's runs never set it
+    share = os.environ.get("GR_BENCH_SHARE_GPU") == "1"
+    rep = Replicas("gloo" if share else "nccl")
+    world, rank = rep.world, rep.rank
+    local = 0 if share else rep.local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -280,7 +285,8 @@ def main():
             "routes": int(info["routes"]),
             **({"trie_groups_used": int(info["groups_used"])} if "groups_used" in info
                else {"tbl8_groups_used": int(info["tbl8_used"])}),
-            "parallelism": f"replicas x{world} (one RX stream + FIB replica per GPU, no collective)",
+            "parallelism": f"replicas x{world} (one RX stream + FIB replica per GPU, no collective)"
+            + (" [rehearsal: all ranks on one GPU]" if share else ""),
             "forwarded_frac": round(fwd_frac, 6),
             "placement": (f"calibrated: output lines, then frames = fastest of {args.candidates + 1} allocations each, "
                           "timed over a batch of this workload drawn with another seed (gr_hip_batch_place)"
