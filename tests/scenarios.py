@@ -428,3 +428,37 @@ def eth_output_cache_arrays(stride=STRIDE):
         meta[i]["vlan_ck"] = (abi.CKSUM_UNKNOWN << 12) | (abi.META_WALK if walk[i] else 0)
         meta[i]["pkt_len"] = len(f)
     return frames, meta, labels, np.array(zero)
+
+
+def clustered_routes6(seed):
+    """IPv6 prefixes in six clusters shaped to trigger the trie's level
+    compressions (fib6.c widen: dense fan-outs of /40-/64 under one-byte
+    skips, at bytes 2-5), each with a covering prefix, plus 200 sparse deep
+    routes; unique, masked, nh and vrf left to the caller."""
+    rng = np.random.default_rng(0x6C0 + seed)
+    rows = []
+    for c in range(6):
+        base = rng.integers(0, 256, 16, dtype=np.uint8)
+        base[0] = 0x20 + c
+        depth = int(rng.integers(2, 6))  # the byte the cluster fans out at
+        fan = int(rng.choice([4, 24, 96]))
+        for a in rng.choice(256, size=fan, replace=False):
+            for b in rng.choice(256, size=int(rng.integers(2, 40)), replace=False):
+                ip = base.copy()
+                ip[depth], ip[depth + 1] = a, b
+                rows.append((ip, 8 * (depth + 2)))
+        rows.append((base, 8 * depth - int(rng.integers(0, 5))))  # a covering prefix
+    for _ in range(200):  # sparse deep routes
+        ip = rng.integers(0, 256, 16, dtype=np.uint8)
+        ip[0] = 0x20 + int(rng.integers(0, 16))
+        rows.append((ip, int(rng.integers(17, 129))))
+    r = np.zeros(len(rows), dtype=abi.ROUTE6_DT)
+    for i, (ip, ln) in enumerate(rows):
+        m = np.zeros(16, dtype=np.uint8)
+        full = ln // 8
+        m[:full] = ip[:full]
+        if ln % 8:
+            m[full] = ip[full] & ((0xFF00 >> (ln % 8)) & 0xFF)
+        r[i]["ip"], r[i]["prefixlen"] = m, ln
+    _, keep = np.unique(np.concatenate([r["ip"], r["prefixlen"][:, None]], axis=1), axis=0, return_index=True)
+    return r[np.sort(keep)]

@@ -607,6 +607,25 @@ def test_fullview6_stream(fastpath):
     assert info["routes"] == len(t.route6_array()) and info["groups_used"] > 20_000  # a deep, path-compressed trie
 
 
+@pytest.mark.parametrize("seed", [1, 2])
+def test_clustered_routes6_stream(fastpath, seed):
+    """IPv6 forwarding over clustered tables whose tries widen at bytes 2-5
+    (scenarios.clustered_routes6: wide groups and widened one-byte skips
+    below the first level, the kernel's WIDE branch at several depths)."""
+    t = T.base_ports(max_routes=1 << 10)
+    r = SC.clustered_routes6(seed)
+    t.fibs6[T.VRF_MAIN] = (len(r) + 10, 1 << 16)
+    first = T.fullview6_nexthops(t)
+    r["vrf_id"] = T.VRF_MAIN
+    r["nh"] = first + np.arange(len(r)) % T.N_FULLVIEW6_NH
+    t.add_routes6(r)
+    fr, me = S.stream6(1 << 18, 0x6C10 + seed, r)
+    o = oracle.Oracle(t).process(fr, me)
+    g = run_gpu(fastpath, t, fr, me)
+    compare(o, g)
+    assert (g[1]["edge"] == abi.EDGE["port_output"]).mean() > 0.9
+
+
 def test_mixed_v4_v6_stream(fastpath):
     """IPv4 and IPv6 packets interleaved in every wave (divergent chains)."""
     t, _ = SC.corpus_topology()
