@@ -3,8 +3,8 @@
 
 The script builds two ports with connected /24s, `16.0.0.0/16 via
 172.16.0.2`, nexthop 45 on p1 and `16.1.0.0/16 via id 45` (:7-13), puts a
-Linux namespace behind each port (:15-26) and checks reachability with ping
-and TTL expiry with traceroute (:28-37). DPDK and network namespaces are not
+Linux namespace behind each port (:15-27) and checks reachability with ping
+and TTL expiry with traceroute (:29-38). DPDK and network namespaces are not
 available here, so each ping / traceroute becomes the frame it would put on
 the wire, and the check is the edge and rewrite grout's chain gives it:
 before the namespaces' addresses are resolved (ARP on the CPU: ip_hold) and
@@ -29,9 +29,12 @@ def smoke_topology(resolved):
     t.add_address(P1, "172.16.1.1/24")  # :10
     gw = t.add_nexthop(P0, "172.16.0.2", N0_MAC if resolved else None)
     t.add_route(T.VRF_MAIN, "16.0.0.0/16", gw)  # :11
-    nh45 = t.add_nexthop(P1, "172.16.1.2", N1_MAC if resolved else None, slot=45)  # :12
+    # :12 "nexthop add l3 iface p1 id 45": no address, so GR_AF_UNSPEC + GR_NH_F_LINK
+    # (l3_nexthop.c:233-239), like a connected route: every destination is held and learned
+    nh45 = t.add_nexthop(P1, None, slot=45)
     t.add_route(T.VRF_MAIN, "16.1.0.0/16", nh45)  # :13
-    if resolved:  # the /32 routes grout adds for neighbours it resolved (ARP)
+    if resolved:  # the /32 routes grout adds for neighbours it resolved (ARP, nexthop.c:62-90)
+        t.add_route(T.VRF_MAIN, "16.1.0.1/32", t.add_nexthop(P1, "16.1.0.1", N1_MAC))  # n1's x-p1 (:24)
         t.add_route(T.VRF_MAIN, "172.16.0.2/32", t.add_nexthop(P0, "172.16.0.2", N0_MAC))
         t.add_route(T.VRF_MAIN, "172.16.1.2/32", t.add_nexthop(P1, "172.16.1.2", N1_MAC))
     return t
@@ -39,17 +42,17 @@ def smoke_topology(resolved):
 
 # (script line, ingress iface, src MAC, src, dst, ttl, edge before / after resolution, egress iface)
 PINGS = [
-    (28, P0, N0_MAC, "172.16.0.2", "16.1.0.1", 64, "ip_hold", "port_output", P1),
-    (29, P1, N1_MAC, "16.1.0.1", "16.0.0.1", 64, "ip_hold", "port_output", P0),
-    (30, P0, N0_MAC, "172.16.0.2", "172.16.1.2", 64, "ip_hold", "port_output", P1),
-    (31, P1, N1_MAC, "172.16.1.2", "172.16.0.2", 64, "ip_hold", "port_output", P0),
-    (32, P0, N0_MAC, "172.16.0.2", "172.16.0.1", 64, "ip_input_local", "ip_input_local", None),
-    (33, P1, N1_MAC, "172.16.1.2", "172.16.1.1", 64, "ip_input_local", "ip_input_local", None),
+    (29, P0, N0_MAC, "172.16.0.2", "16.1.0.1", 64, "ip_hold", "port_output", P1),
+    (30, P1, N1_MAC, "16.1.0.1", "16.0.0.1", 64, "ip_hold", "port_output", P0),
+    (31, P0, N0_MAC, "172.16.0.2", "172.16.1.2", 64, "ip_hold", "port_output", P1),
+    (32, P1, N1_MAC, "172.16.1.2", "172.16.0.2", 64, "ip_hold", "port_output", P0),
+    (33, P0, N0_MAC, "172.16.0.2", "172.16.0.1", 64, "ip_input_local", "ip_input_local", None),
+    (34, P1, N1_MAC, "172.16.1.2", "172.16.1.1", 64, "ip_input_local", "ip_input_local", None),
     # traceroute -N1: the first probe carries TTL 1 and dies at grout
-    (34, P0, N0_MAC, "172.16.0.2", "16.1.0.1", 1, "ip_error_ttl_exceeded", "ip_error_ttl_exceeded", None),
-    (35, P1, N1_MAC, "16.1.0.1", "16.0.0.1", 1, "ip_error_ttl_exceeded", "ip_error_ttl_exceeded", None),
-    (36, P0, N0_MAC, "172.16.0.2", "172.16.1.2", 1, "ip_error_ttl_exceeded", "ip_error_ttl_exceeded", None),
-    (37, P1, N1_MAC, "172.16.1.2", "172.16.0.2", 1, "ip_error_ttl_exceeded", "ip_error_ttl_exceeded", None),
+    (35, P0, N0_MAC, "172.16.0.2", "16.1.0.1", 1, "ip_error_ttl_exceeded", "ip_error_ttl_exceeded", None),
+    (36, P1, N1_MAC, "16.1.0.1", "16.0.0.1", 1, "ip_error_ttl_exceeded", "ip_error_ttl_exceeded", None),
+    (37, P0, N0_MAC, "172.16.0.2", "172.16.1.2", 1, "ip_error_ttl_exceeded", "ip_error_ttl_exceeded", None),
+    (38, P1, N1_MAC, "172.16.1.2", "172.16.0.2", 1, "ip_error_ttl_exceeded", "ip_error_ttl_exceeded", None),
 ]
 
 
@@ -69,8 +72,8 @@ def check(out, v, resolved):
             continue
         assert v["iface"][i] == egress  # the port behind iface_output
         peer = {P0: N0_MAC, P1: N1_MAC}[egress]
-        if line == 28:
-            peer = N1_MAC  # 16.1.0.0/16 via nexthop 45, resolved to n1
+        if line == 29:
+            peer = N1_MAC  # 16.1.0.1 learned behind nexthop 45: n1
         assert bytes(out[i][0:6]) == T.mac_bytes(peer)
         assert bytes(out[i][6:12]) == T.mac_bytes(T.PORT_MAC[0] if egress == P0 else T.PORT_MAC[1])
         assert out[i][22] == ttl - 1

@@ -1,0 +1,384 @@
+# SPDX-License-Identifier: BSD-3-Clause
+"""grout's forwarding smoke scripts restated as packets, on the CPU oracle and
+through the rte_graph node walk on the GPU.
+
+Each script builds a topology with grcli, puts Linux namespaces behind the
+ports and checks reachability with ping / ping6 / traceroute. DPDK and
+network namespaces are not available here, so every probe becomes the frame
+it would put on the wire, entering the port it would enter, and the check
+is what grout's chain does with it: the next node (edge), the egress port and
+VLAN tag, the rewritten Ethernet header, TTL / hop limit and checksum. Each
+script runs twice: before the namespaces' neighbours are resolved (ARP / NDP
+on the CPU: ip_hold / ip6_hold) and after (the host routes grout installs for
+the neighbours it learned, modules/ip/control/nexthop.c:62-90 and
+modules/ip6/control/nexthop.c:65-90: packets are forwarded).
+
+The expectations below are written from the scripts and grout's node code,
+not taken from the oracle. The CPU test checks the oracle against them; the
+GPU test checks the HIP node walk against them and against the oracle, mbuf
+for mbuf.
+
+Scripts (under smoke/ in the reference):
+  ip6_forward_test.sh       IPv6 gateway and link nexthops, link-local, NDP
+  vlan_forward_test.sh      VLAN sub-interfaces on both sides
+  vrf_forward_test.sh       two VRFs holding the same addresses and routes
+  cross_vrf_forward_test.sh a route whose nexthop is another VRF (xvrf)
+  ip_forward_ip6nh_test.sh  IPv4 routes via IPv6 link-local nexthops
+  ip_loadbalance_test.sh    an ECMP group of two nexthops
+"""
+import ipaddress
+
+import numpy as np
+import pytest
+
+import oracle
+from grout_amd import abi
+from grout_amd import synth as S
+from grout_amd import topology as T
+from test_node_shim import RX_DATA_OFF, compare_mbufs, mbufs_for
+
+GR_MAC = ["02:00:00:00:00:%02x" % p for p in range(4)]  # grout's ports p0..p3
+NS_MAC = ["02:00:00:0a:00:%02x" % n for n in range(4)]  # the namespaces' ends x-p0..x-p3
+PORT = [10, 11, 12, 13]  # iface ids of p0..p3 (1 and 2 are left to the VRF ifaces)
+
+
+def eui64_ll(mac):
+    """fe80::/64 + modified EUI-64 of a MAC (rte_ipv6_llocal_from_ethernet),
+    the link-local address grout and Linux give a port."""
+    b = bytearray(T.mac_bytes(mac))
+    iid = bytes([b[0] ^ 0x02, b[1], b[2], 0xFF, 0xFE, b[3], b[4], b[5]])
+    return str(ipaddress.IPv6Address(b"\xfe\x80" + bytes(6) + iid))
+
+
+def ports(t, n, vrf=None):
+    for p in range(n):
+        v = vrf[p] if vrf else T.VRF_MAIN
+        t.add_port(PORT[p], p, GR_MAC[p], vrf_id=v)
+        t.add_address6(PORT[p], eui64_ll(GR_MAC[p]) + "/64")  # the link-local address every port gets
+
+
+def neighbour(t, vrf, iface, addr, mac):
+    """A neighbour grout learned: nexthop + host route (nexthop.c: rib4_insert /32, rib6 /128)."""
+    nh = t.add_nexthop(iface, addr, mac)
+    if ":" in addr:
+        t.add_route6(vrf, addr + "/128", nh, iface_id=iface if addr.startswith("fe80") else 0)
+    else:
+        t.add_route(vrf, addr + "/32", nh)
+    return nh
+
+
+class Probe:
+    """One frame on the wire and what grout does with it.
+
+    before / after: the edge before and after neighbour resolution; `out`:
+    (egress port index, VLAN tag, destination MAC) when it is port_output."""
+
+    def __init__(self, script, line, port, frame, before, after=None, out=None, vlan=0, out_any=None, rss=0):
+        self.script, self.line, self.port, self.frame = script, line, port, frame
+        self.before, self.after = before, after if after is not None else before
+        self.out, self.out_any, self.vlan, self.rss = out, out_any, vlan, rss
+
+    @property
+    def label(self):
+        return f"{self.script}:{self.line}"
+
+
+def v4(port, src, dst, ttl=64, proto=1, vlan=0, dst_mac=None):
+    # ping: ICMP echo with the default 56-byte payload (98-byte IP packet); traceroute: UDP probe
+    length = 14 + 84 if proto == 1 else 14 + 60
+    return S.frame(dst_mac=dst_mac or GR_MAC[port], src_mac=NS_MAC[port], src=src, dst=dst, ttl=ttl,
+                   proto=proto, length=length)
+
+
+def v6(port, src, dst, hop=64, nh=58, dst_mac=None):
+    length = 14 + 40 + 64 if nh == 58 else 14 + 40 + 32
+    return S.frame6(dst_mac=dst_mac or GR_MAC[port], src_mac=NS_MAC[port], src=src, dst=dst, hop=hop,
+                    next_header=nh, length=length)
+
+
+# ---------------------------------------------------------------------------
+# the scripts
+# ---------------------------------------------------------------------------
+def ip6_forward(resolved):
+    """smoke/ip6_forward_test.sh: ports p1, p2 (here p0, p1 of this file's
+    numbering: n1 behind p0, n2 behind p1)."""
+    s = "ip6_forward_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 2)
+    P1, P2 = PORT[0], PORT[1]
+    t.add_address6(P1, "fd00:ba4:1::1/64")  # :9
+    t.add_address6(P2, "fd00:ba4:2::1/64")  # :10
+    gw = t.add_nexthop(P1, "fd00:ba4:1::2", NS_MAC[0] if resolved else None)  # :11 (via fd00:ba4:1::2)
+    t.add_route6(T.VRF_MAIN, "fd00:f00:1::/64", gw)
+    nh45 = t.add_nexthop(P2, None, slot=45)  # :12 no address: GR_AF_UNSPEC + GR_NH_F_LINK (l3_nexthop.c:233-239)
+    t.add_route6(T.VRF_MAIN, "fd00:f00:2::/64", nh45)  # :13
+    if resolved:
+        neighbour(t, T.VRF_MAIN, P1, "fd00:ba4:1::2", NS_MAC[0])
+        neighbour(t, T.VRF_MAIN, P2, "fd00:ba4:2::2", NS_MAC[1])
+        neighbour(t, T.VRF_MAIN, P2, "fd00:f00:2::2", NS_MAC[1])  # on n2's x-p2 (:24): learned through nh45
+        neighbour(t, T.VRF_MAIN, P1, eui64_ll(NS_MAC[0]), NS_MAC[0])
+        neighbour(t, T.VRF_MAIN, P2, eui64_ll(NS_MAC[1]), NS_MAC[1])
+    n1_ll, n2_ll = eui64_ll(NS_MAC[0]), eui64_ll(NS_MAC[1])
+    pr = [
+        # ping6 to grout's link-local addresses (:29-30)
+        Probe(s, 29, 0, v6(0, n1_ll, eui64_ll(GR_MAC[0])), "ip6_input_local"),
+        Probe(s, 30, 1, v6(1, n2_ll, eui64_ll(GR_MAC[1])), "ip6_input_local"),
+        # n1 -> fd00:f00:2::2 via id 45 (a link nexthop: the neighbour is learned, :31)
+        Probe(s, 31, 0, v6(0, "fd00:ba4:1::2", "fd00:f00:2::2"), "ip6_hold", "port_output", (1, 0, NS_MAC[1])),
+        # n2 -> fd00:f00:1::2 via the gateway fd00:ba4:1::2 (:32)
+        Probe(s, 32, 1, v6(1, "fd00:f00:2::2", "fd00:f00:1::2"), "ip6_hold", "port_output", (0, 0, NS_MAC[0])),
+        # the connected /64s (:33-34)
+        Probe(s, 33, 0, v6(0, "fd00:ba4:1::2", "fd00:ba4:2::2"), "ip6_hold", "port_output", (1, 0, NS_MAC[1])),
+        Probe(s, 34, 1, v6(1, "fd00:ba4:2::2", "fd00:ba4:1::2"), "ip6_hold", "port_output", (0, 0, NS_MAC[0])),
+        # the neighbour solicitation for grout's address after the flush (:39-40): to the
+        # solicited-node group, whose membership lives on the CPU (mcast6_get_member)
+        Probe(s, 40, 0, v6(0, n1_ll, "ff02::1:ff00:1", hop=255, dst_mac="33:33:ff:00:00:01"), "punt"),
+        Probe(s, 40, 0, v6(0, "fd00:ba4:1::2", "fd00:ba4:1::1"), "ip6_input_local"),
+        Probe(s, 40, 1, v6(1, "fd00:ba4:2::2", "fd00:ba4:2::1"), "ip6_input_local"),
+        # traceroute -N1: the first probe carries hop limit 1 (:46-49)
+        Probe(s, 46, 0, v6(0, "fd00:ba4:1::2", "fd00:ba4:2::2", hop=1, nh=17), "ip6_error_ttl_exceeded"),
+        Probe(s, 47, 1, v6(1, "fd00:ba4:2::2", "fd00:ba4:1::2", hop=1, nh=17), "ip6_error_ttl_exceeded"),
+        Probe(s, 48, 0, v6(0, "fd00:ba4:1::2", "fd00:f00:2::2", hop=1, nh=17), "ip6_error_ttl_exceeded"),
+        Probe(s, 49, 1, v6(1, "fd00:f00:2::2", "fd00:f00:1::2", hop=1, nh=17), "ip6_error_ttl_exceeded"),
+        # a second hop: the probe with hop limit 2 leaves with 1
+        Probe(s, 48, 0, v6(0, "fd00:ba4:1::2", "fd00:f00:2::2", hop=2, nh=17), "ip6_hold", "port_output",
+              (1, 0, NS_MAC[1])),
+    ]
+    return t, pr
+
+
+def vlan_forward(resolved):
+    """smoke/vlan_forward_test.sh: p0.42 and p1.43 over ports p0, p1; the
+    namespaces tag their frames (port_rx strips the tag into vlan_id,
+    port_rx.c:225-231, iface_input demuxes it, iface_input.c:64-76)."""
+    s = "vlan_forward_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 2)
+    V0, V1 = 20, 21
+    t.add_vlan(V0, PORT[0], 42)  # :9
+    t.add_vlan(V1, PORT[1], 43)  # :10
+    t.add_address(V0, "172.16.0.1/24")  # :11
+    t.add_address(V1, "172.16.1.1/24")  # :12
+    if resolved:
+        neighbour(t, T.VRF_MAIN, V0, "172.16.0.2", NS_MAC[0])
+        neighbour(t, T.VRF_MAIN, V1, "172.16.1.2", NS_MAC[1])
+    pr = [
+        Probe(s, 27, 0, v4(0, "172.16.0.2", "172.16.1.2"), "ip_hold", "port_output", (1, 43, NS_MAC[1]), vlan=42),
+        Probe(s, 28, 1, v4(1, "172.16.1.2", "172.16.0.2"), "ip_hold", "port_output", (0, 42, NS_MAC[0]), vlan=43),
+        # the namespaces' ARP requests for their gateway, tagged
+        Probe(s, 27, 0, S.frame(dst_mac="ff:ff:ff:ff:ff:ff", src_mac=NS_MAC[0], ethertype=0x0806), "arp_input",
+              vlan=42),
+        # ping the gateway itself
+        Probe(s, 27, 0, v4(0, "172.16.0.2", "172.16.0.1"), "ip_input_local", vlan=42),
+        # an untagged frame stays on p0 itself, in the same VRF: routed all the same
+        Probe(s, 27, 0, v4(0, "172.16.0.2", "172.16.1.2"), "ip_hold", "port_output", (1, 43, NS_MAC[1])),
+        # a tag with no VLAN interface (iface_input.c:70-73)
+        Probe(s, 27, 0, v4(0, "172.16.0.2", "172.16.1.2"), "iface_input_unknown_vlan", vlan=44),
+    ]
+    return t, pr
+
+
+def vrf_forward(resolved):
+    """smoke/vrf_forward_test.sh: p0, p1 in gr-vrf1 and p2, p3 in gr-vrf2 with
+    the same addresses and routes; n0..n3 behind them, n1 and n3 holding the
+    same addresses (only their MACs tell them apart)."""
+    s = "vrf_forward_test.sh"
+    t = T.Topology()
+    t.add_vrf(1)  # gr-vrf1 (:7)
+    t.add_vrf(2)  # gr-vrf2 (:8)
+    ports(t, 4, vrf=[1, 1, 2, 2])  # :9-12
+    for vrf, a, b in ((1, PORT[0], PORT[1]), (2, PORT[2], PORT[3])):
+        t.add_address(a, "172.16.0.1/24")  # :13, :17
+        t.add_address(b, "172.16.1.1/24")  # :14, :18
+        k = 0 if vrf == 1 else 2
+        g0 = t.add_nexthop(a, "172.16.0.2", NS_MAC[k] if resolved else None)
+        g1 = t.add_nexthop(b, "172.16.1.2", NS_MAC[k + 1] if resolved else None)
+        t.add_route(vrf, "16.0.0.0/16", g0)  # :15, :19
+        t.add_route(vrf, "16.1.0.0/16", g1)  # :16, :20
+        if resolved:
+            neighbour(t, vrf, a, "172.16.0.2", NS_MAC[k])
+            neighbour(t, vrf, b, "172.16.1.2", NS_MAC[k + 1])
+    pr = [
+        Probe(s, 31, 0, v4(0, "172.16.0.2", "172.16.1.2"), "ip_hold", "port_output", (1, 0, NS_MAC[1])),
+        Probe(s, 32, 0, v4(0, "172.16.0.2", "16.1.0.1"), "ip_hold", "port_output", (1, 0, NS_MAC[1])),
+        Probe(s, 32, 1, v4(1, "16.1.0.1", "172.16.0.2"), "ip_hold", "port_output", (0, 0, NS_MAC[0])),
+        Probe(s, 43, 2, v4(2, "172.16.0.2", "172.16.1.2"), "ip_hold", "port_output", (3, 0, NS_MAC[3])),
+        Probe(s, 44, 2, v4(2, "172.16.0.2", "16.1.0.1"), "ip_hold", "port_output", (3, 0, NS_MAC[3])),
+        Probe(s, 44, 3, v4(3, "16.1.0.1", "172.16.0.2"), "ip_hold", "port_output", (2, 0, NS_MAC[2])),
+        # each VRF's own gateway address
+        Probe(s, 31, 0, v4(0, "172.16.0.2", "172.16.0.1"), "ip_input_local"),
+        Probe(s, 43, 2, v4(2, "172.16.0.2", "172.16.0.1"), "ip_input_local"),
+        # 16.0.0.0/16 has no route in either VRF's view from the far side except via the gateway
+        Probe(s, 44, 3, v4(3, "16.1.0.1", "10.9.9.9"), "ip_error_dest_unreach"),
+    ]
+    return t, pr
+
+
+def cross_vrf_forward(resolved):
+    """smoke/cross_vrf_forward_test.sh: p0 in gr-vrf1, p1 in gr-vrf2. From
+    16.0.0.1 to 16.1.0.1 one lookup in gr-vrf1 leaves by p1 (nexthop id 2
+    lives in gr-vrf2); the way back looks up gr-vrf2 first, whose nexthop is
+    the gr-vrf1 interface: ip_output hands it to xvrf (xvrf.c:61-64), which
+    re-enters ip_input in gr-vrf1 on the CPU."""
+    s = "cross_vrf_forward_test.sh"
+    t = T.Topology()
+    t.add_vrf(1)  # :7
+    t.add_vrf(2)  # :8
+    ports(t, 2, vrf=[1, 2])  # :9-10
+    t.add_address(PORT[0], "172.16.0.1/24")  # :11
+    t.add_address(PORT[1], "172.16.1.1/24")  # :12
+    nh2 = t.add_nexthop(PORT[1], "172.16.1.2", NS_MAC[1] if resolved else None, slot=2)  # :15
+    t.add_route(1, "16.1.0.0/16", nh2)  # :16
+    t.add_route(2, "16.1.0.0/16", nh2)  # :17
+    nh1 = t.add_nexthop(1, None, slot=1)  # :20 l3 iface gr-vrf1 (no address: LINK)
+    t.add_route(2, "16.0.0.0/16", nh1)  # :21
+    gw = t.add_nexthop(PORT[0], "172.16.0.2", NS_MAC[0] if resolved else None)
+    t.add_route(1, "16.0.0.0/16", gw)  # :22
+    pr = [
+        Probe(s, 34, 0, v4(0, "16.0.0.1", "16.1.0.1"), "ip_hold", "port_output", (1, 0, NS_MAC[1])),
+        Probe(s, 35, 1, v4(1, "16.1.0.1", "16.0.0.1"), "xvrf"),
+        Probe(s, 35, 1, v4(1, "16.1.0.1", "16.0.0.1", ttl=1), "ip_error_ttl_exceeded"),
+        # gr-vrf2 holds no route to 172.16.0.0/24
+        Probe(s, 35, 1, v4(1, "16.1.0.1", "172.16.0.2"), "ip_error_dest_unreach"),
+    ]
+    return t, pr
+
+
+def ip_forward_ip6nh(resolved):
+    """smoke/ip_forward_ip6nh_test.sh: 16.n.0.0/16 via nexthop 42+n, an L3
+    nexthop on p_n whose address is n's IPv6 link-local address (:18-20). The
+    nexthop is IPv6, the packets IPv4: ip_output only needs it reachable
+    (ip_output.c:126-138), and eth_output writes the IPv4 ether type."""
+    s = "ip_forward_ip6nh_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 2)
+    for n in (0, 1):
+        nh = t.add_nexthop(PORT[n], eui64_ll(NS_MAC[n]), NS_MAC[n] if resolved else None, slot=42 + n)  # :19
+        t.add_route(T.VRF_MAIN, f"16.{n}.0.0/16", nh)  # :20
+    pr = [
+        # n routes 16.(n^1).0.0/16 via grout's link-local: frames to p_n's MAC (:16, :25)
+        Probe(s, 25, 0, v4(0, "16.0.0.1", "16.1.0.1"), "ip_hold", "port_output", (1, 0, NS_MAC[1])),
+        Probe(s, 25, 1, v4(1, "16.1.0.1", "16.0.0.1"), "ip_hold", "port_output", (0, 0, NS_MAC[0])),
+        Probe(s, 25, 0, v4(0, "16.0.0.1", "16.1.0.1", ttl=1, proto=17), "ip_error_ttl_exceeded"),
+    ]
+    return t, pr
+
+
+def ip_loadbalance(resolved):
+    """smoke/ip_loadbalance_test.sh: 192.200.0.0/24 via group 10 = {100 on p0,
+    101 on p1} (:37-40). The script's own probes are grout-originated pings
+    (:43-44, they enter at ip_output, off this path) whose replies come back
+    to grout's addresses; transit frames from n1 behind p2 take the group,
+    one member per RSS hash (nexthop.h:89-96)."""
+    s = "ip_loadbalance_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 3)
+    for p in range(3):
+        t.add_address(PORT[p], f"172.16.{p}.1/24")  # :32-34
+    m100 = t.add_nexthop(PORT[0], "172.16.0.2", NS_MAC[0] if resolved else None, slot=100)  # :37
+    m101 = t.add_nexthop(PORT[1], "172.16.1.2", NS_MAC[1] if resolved else None, slot=101)  # :38
+    g = t.add_group([m100, m101], slot=10)  # :39
+    t.add_route(T.VRF_MAIN, "192.200.0.0/24", g)  # :40
+    pr = [
+        # the echo replies to grout's pings, one through each member
+        Probe(s, 43, 0, v4(0, "192.200.0.2", "172.16.0.1"), "ip_input_local"),
+        Probe(s, 44, 1, v4(1, "192.200.0.2", "172.16.1.1"), "ip_input_local"),
+    ]
+    for rss in range(8):  # n1 -> 192.200.0.2, every reta slot of the group
+        pr.append(Probe(s, 40, 2, v4(2, "172.16.2.2", "192.200.0.2"), "ip_hold", "port_output",
+                        out_any=[(0, 0, NS_MAC[0]), (1, 0, NS_MAC[1])], rss=rss))
+    return t, pr
+
+
+SCRIPTS = {f.__name__: f for f in (ip6_forward, vlan_forward, vrf_forward, cross_vrf_forward, ip_forward_ip6nh,
+                                   ip_loadbalance)}
+
+
+# ---------------------------------------------------------------------------
+# checks
+# ---------------------------------------------------------------------------
+def _pack(probes):
+    fr = [p.frame for p in probes]
+    arr, meta = S.pack(fr, stride=128, iface=[PORT[p.port] for p in probes], vlan=[p.vlan for p in probes])
+    meta["rss"] = [p.rss for p in probes]
+    return arr, meta
+
+
+def check(probes, frames_in, lines, m, resolved):
+    """lines: the first 64 bytes of each frame after the walk; m: the mbufs."""
+    used = set()
+    for i, p in enumerate(probes):
+        want = p.after if resolved else p.before
+        got = abi.EDGE_NAMES[m["edge"][i]]
+        assert got == want, (p.label, i, got, want)
+        if want != "port_output":
+            continue
+        outs = [p.out] if p.out else p.out_any
+        eg = [o for o in outs if PORT[o[0]] == m["iface"][i]]
+        assert len(eg) == 1, (p.label, i, int(m["iface"][i]))
+        port, tag, dmac = eg[0]
+        used.add((p.label, port))
+        assert m["vlan_id"][i] == tag, (p.label, i, int(m["vlan_id"][i]), tag)
+        assert m["data_off"][i] == RX_DATA_OFF  # eth_output prepended the header again
+        ln, fi = lines[i], frames_in[i]
+        assert bytes(ln[0:6]) == T.mac_bytes(dmac), p.label
+        assert bytes(ln[6:12]) == T.mac_bytes(GR_MAC[port]), p.label  # a VLAN iface takes its parent's MAC
+        six = fi[12] == 0x86
+        assert bytes(ln[12:14]) == (b"\x86\xdd" if six else b"\x08\x00")
+        if six:
+            assert ln[21] == fi[21] - 1  # ip6_forward.c:25-30
+            assert m["packet_type"][i] == abi.PTYPE_L3_IPV6
+        else:
+            assert ln[22] == fi[22] - 1  # ip_forward.c:25-32
+            hdr = bytes(ln[14:34])
+            s = sum(int.from_bytes(hdr[k:k + 2], "big") for k in range(0, 20, 2))
+            s = (s & 0xFFFF) + (s >> 16)
+            assert (s + (s >> 16)) & 0xFFFF == 0xFFFF, p.label
+            assert m["packet_type"][i] == abi.PTYPE_L3_IPV4
+        # the rest of the line is untouched
+        assert bytes(ln[14:21]) == bytes(fi[14:21]) and bytes(ln[26:64]) == bytes(fi[26:64]), p.label
+    return used
+
+
+def expect_both_members(used, resolved):
+    if resolved:
+        lb = {port for label, port in used if label.startswith("ip_loadbalance")}
+        assert lb == {0, 1}, lb  # the group spreads over both members
+
+
+PARAMS = [(name, r) for name in SCRIPTS for r in (False, True)]
+
+
+@pytest.mark.parametrize("script,resolved", PARAMS)
+def test_smoke_script_oracle(script, resolved):
+    t, probes = SCRIPTS[script](resolved)
+    fr, me = _pack(probes)
+    lines, v, _, m, _ = oracle.Oracle(t).process_mbufs(fr, me)
+    used = check(probes, fr, lines, m, resolved)
+    if script == "ip_loadbalance":
+        expect_both_members(used, resolved)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("script,resolved", PARAMS)
+def test_smoke_script_gpu(fastpath, script, resolved):
+    """The rte_graph node walk (stage, GPU, hand back onto the mbufs)."""
+    from golden_util import fresh_fastpath_state
+    t, probes = SCRIPTS[script](resolved)
+    fr, me = _pack(probes)
+    fresh_fastpath_state(fastpath, t)
+    bufs, m = mbufs_for(fr, me)
+    q = fastpath.queue()
+    try:
+        q.node_process(m, burst=64)
+    finally:
+        q.close()
+    used = check(probes, fr, bufs[:, :abi.LINE], m, resolved)
+    if script == "ip_loadbalance":
+        expect_both_members(used, resolved)
+    lines_o, _, _, want, _ = oracle.Oracle(t).process_mbufs(fr, me, lines_only=True)
+    compare_mbufs(m, want, bufs, lines_o, [p.label for p in probes])
