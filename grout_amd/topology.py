@@ -12,7 +12,7 @@ routes exactly as grout's control plane would leave them for the datapath:
 * add_nexthop: a gr_nexthop_info_l3 (gr_nexthop.h:93-105); a MAC makes it
   REACHABLE (l3_nexthop.c:244-250), no address makes it a LINK nexthop
   (l3_nexthop.c:233-238).
-* add_group: GR_NH_T_GROUP with a power-of-two reta (nexthop.h:80-96).
+* add_group: GR_NH_T_GROUP with grout's weighted reta (group_nexthop.c:27-56,101-166).
 * add_route: gr_ip4_route_add_req (modules/ip/api/gr_ip4.h:47-56).
 * IPv6: every VRF also gets a FIB6 (modules/ip6/control/route.c:103-125); an
   IPv6 nexthop address makes an AF_IP6 nexthop; add_address6 mirrors
@@ -160,24 +160,41 @@ class Topology:
                         iface_id=iface_id)
         return slot
 
-    def add_group(self, members, reta_size=None, slot=None):
-        """GR_NH_T_GROUP: members spread round-robin over a power-of-two reta."""
+    def add_group(self, members, reta_size=None, slot=None, weights=None):
+        """GR_NH_T_GROUP with the reta grout builds for it (group_import_info,
+        modules/infra/control/group_nexthop.c:101-166): members ordered by
+        weight, descending (:137-140; glibc's qsort keeps equal weights in
+        order), reta_size = align32pow2(max/min weight x n_members) capped at
+        MAX_NH_GROUP_RETA_SIZE 4096 (:142-154, nexthop.h:80), filled by
+        group_reta_distribute (:27-56). `reta_size` overrides the size (the
+        fill stays grout's); one member needs no reta (:131-135)."""
         slot = self._slot(slot)
         r = self.nh[slot]
         r["type"] = abi.NH_T["GROUP"]
         r["n_members"] = len(members)
         r["single"] = members[0] if len(members) == 1 else 0
+        w = [max(1, x) for x in weights] if weights is not None else [1] * len(members)  # weight ?: 1 (:125)
+        order = sorted(range(len(members)), key=lambda i: -w[i])
+        mem, w = [members[i] for i in order], [w[i] for i in order]
         if reta_size is None:
-            reta_size = 1
-            while reta_size < 4 * max(1, len(members)):
-                reta_size *= 2
+            reta_size = min((w[0] // w[-1]) * len(mem), 4096) if mem else 1
+            p = 1
+            while p < reta_size:
+                p *= 2
+            reta_size = p
         if reta_size & (reta_size - 1):
             raise ValueError("reta size must be a power of two")
         r["reta_size"] = reta_size
         r["reta_off"] = len(self.reta)
-        fill = np.array([members[i % len(members)] for i in range(reta_size)] if members else
-                        [0] * reta_size, dtype=np.uint32)
-        self.reta = np.concatenate([self.reta, fill])
+        fill = []
+        total = sum(w)
+        for m, x in zip(mem, w):  # group_reta_distribute
+            e = max((x * reta_size + total // 2) // total, 1)
+            fill += [m] * min(e, reta_size - len(fill))
+            if len(fill) >= reta_size:
+                break
+        fill += [mem[0] if mem else 0] * (reta_size - len(fill))
+        self.reta = np.concatenate([self.reta, np.array(fill, dtype=np.uint32)])
         return slot
 
     # -- routes ---------------------------------------------------------------

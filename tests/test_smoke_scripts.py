@@ -382,3 +382,24 @@ def test_smoke_script_gpu(fastpath, script, resolved):
         expect_both_members(used, resolved)
     lines_o, _, _, want, _ = oracle.Oracle(t).process_mbufs(fr, me, lines_only=True)
     compare_mbufs(m, want, bufs, lines_o, [p.label for p in probes])
+
+
+def test_group_reta_is_grouts():
+    """The test topologies' group reta follows group_import_info /
+    group_reta_distribute (group_nexthop.c:27-56,137-154), written out by hand."""
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 3)
+    a, b, c = (t.add_nexthop(PORT[p], f"172.16.{p}.2", NS_MAC[p]) for p in range(3))
+    cases = [
+        (dict(members=[a, b]), [a, b]),  # 2 x 1 -> 2 entries
+        (dict(members=[a, b, c]), [a, b, c, a]),  # 3 -> 4, one entry each, then the first member
+        (dict(members=[a, b], weights=[1, 3]), [b] * 6 + [a] * 2),  # ordered by weight: 3/1 x 2 = 6 -> 8
+        (dict(members=[a, b, c], reta_size=16), [a] * 5 + [b] * 5 + [c] * 5 + [a]),
+        (dict(members=[a, b], weights=[0, 0]), [a, b]),  # weight 0 counts as 1
+    ]
+    for kw, want in cases:
+        g = t.add_group(**kw)
+        r = t.nh[g]
+        got = t.reta[r["reta_off"]:r["reta_off"] + r["reta_size"]]
+        assert list(got) == want, (kw, list(got), want)
