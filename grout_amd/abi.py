@@ -191,6 +191,9 @@ HIP_API = {
     "gr_hip_node_stage": (_I, [_P, _U32, _U32, _P, _P, _P]),
     "gr_hip_node_apply": (_I, [_P, _U32, _U32, _P, _P, _U32, _P, _P, _U32, _P, _U32, _P]),
     "gr_hip_node_process": (_I, [_P, _P, _U32, _U32, _P]),
+    "gr_hip_node_start": (_I, [_P, _P, _U32, _U32]),
+    "gr_hip_node_finish": (_I, [_P, _P, _P, _P]),
+    "gr_hip_node_pending": (_I, [_P, _P]),
 }
 
 HOST_API = {

@@ -152,6 +152,22 @@ struct host_slot {
 	gr_hip_verdict *v = nullptr;
 };
 
+// One rte_graph node walk (gr_hip_node_start .. gr_hip_node_finish): its
+// pinned staging, grown on demand, and the walk in flight.
+struct node_slot {
+	uint32_t cap = 0;
+	uint8_t *lines = nullptr, *out = nullptr;
+	gr_hip_pkt_meta *meta = nullptr;
+	gr_hip_verdict *v = nullptr;
+	std::vector<uint32_t> pos; // where each mbuf is staged (gr_hip_node_layout)
+	hipEvent_t done = nullptr; // recorded behind the walk's GPU work
+	gr_hip_mbuf *m = nullptr;
+	uint32_t n = 0, ns = 0, burst = 0;
+	bool by_addr = false;
+	bool sync = false; // finished at start already (staged copies, or nothing to send)
+	int r = 0; // the GPU call's result when sync
+};
+
 } // namespace
 
 struct gr_hip_queue {
@@ -168,12 +184,9 @@ struct gr_hip_queue {
 	hipEvent_t sync_ev; // host waits on the queue's streams (host_wait)
 	gr_hip_iface_stats *d_stats; // [FWD4_STAT_SHARDS][max_ifaces]
 	host_slot hs[HOST_SLOTS];
-	// gr_hip_node_process staging (pinned, grown on demand)
-	uint32_t node_cap;
-	uint8_t *node_lines, *node_out;
-	gr_hip_pkt_meta *node_meta;
-	gr_hip_verdict *node_v;
-	std::vector<uint32_t> node_pos; // where each mbuf is staged (gr_hip_node_layout)
+	// node walks in flight (gr_hip_node_start / _finish), a ring of GR_HIP_NODE_DEPTH
+	node_slot nw[GR_HIP_NODE_DEPTH];
+	uint32_t nw_head, nw_count;
 	uint8_t *d_pad; // the zeroed line pad slots of a frames-by-address batch point at
 	uint32_t *h_err, *d_err; // kernel error word (pinned, mapped): a workgroup gave up
 };
@@ -1704,6 +1717,8 @@ extern "C" int gr_hip_queue_create(gr_hip_ctx_t *c, void *stream, gr_hip_queue_t
 	hipEventCreateWithFlags(&q->quiesce, hipEventDisableTiming);
 	hipEventCreateWithFlags(&q->retire, hipEventDisableTiming);
 	hipEventCreateWithFlags(&q->sync_ev, hipEventDisableTiming);
+	for (node_slot &w : q->nw)
+		hipEventCreateWithFlags(&w.done, hipEventDisableTiming);
 	hipEventRecord(q->retire, q->s); // nothing submitted yet
 	if (hipHostMalloc(reinterpret_cast<void **>(&q->h_err), sizeof(uint32_t), hipHostMallocMapped) == hipSuccess) {
 		*q->h_err = 0;
@@ -1748,10 +1763,13 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 	hipEventDestroy(q->sync_ev);
 	hipFree(q->d_stats);
 	hipHostFree(q->h_err);
-	hipHostFree(q->node_lines);
-	hipHostFree(q->node_out);
-	hipHostFree(q->node_meta);
-	hipHostFree(q->node_v);
+	for (node_slot &w : q->nw) {
+		hipEventDestroy(w.done);
+		hipHostFree(w.lines);
+		hipHostFree(w.out);
+		hipHostFree(w.meta);
+		hipHostFree(w.v);
+	}
 	hipFree(q->d_pad);
 	if (q->own_stream)
 		hipStreamDestroy(q->s);
@@ -2026,6 +2044,28 @@ extern "C" int gr_hip_queue_kernel_ms(gr_hip_queue_t *q, uint32_t n, float *ms, 
 	return 0;
 }
 
+// Zero-copy host batch (the context's "host_direct"): the kernel's loaders
+// and storers move the lines over PCIe themselves, both directions at once,
+// no staging copies. Enqueues the launch on the queue's stream and sets
+// *direct, or leaves it false when the buffers are not device-accessible
+// pinned memory (the caller stages them). The caller holds c->mu shared.
+static int host_direct_launch(gr_hip_queue *q, const void *lines, const gr_hip_pkt_meta *meta, uint32_t n,
+			      void *out_lines, uint32_t out_stride, gr_hip_verdict *verdicts, bool *direct) {
+	*direct = false;
+	if (!q->ctx->host_direct)
+		return 0;
+	void *d_in, *d_meta, *d_out, *d_v;
+	if (!host_dev_ptr(lines, &d_in) || !host_dev_ptr(meta, &d_meta) || !host_dev_ptr(out_lines, &d_out)
+	    || !host_dev_ptr(verdicts, &d_v))
+		return 0;
+	const uint32_t oflags = out_stride == GR_HIP_PREFIX ? GR_HIP_BATCH_F_PREFIX32 : 0;
+	gr_hip_batch b = {d_in, d_out, static_cast<const gr_hip_pkt_meta *>(d_meta), static_cast<gr_hip_verdict *>(d_v),
+			  n, GR_HIP_LINE, out_stride, GR_HIP_BATCH_F_LINES_ONLY | oflags};
+	const int r = launch(q, q->s, &b, true);
+	*direct = r == 0;
+	return r;
+}
+
 extern "C" int gr_hip_fwd4_host_ex(
 	gr_hip_queue_t *q,
 	const void *lines,
@@ -2045,23 +2085,14 @@ extern "C" int gr_hip_fwd4_host_ex(
 	gr_hip_ctx *c = q->ctx;
 	hipSetDevice(c->dev);
 	std::shared_lock<std::shared_mutex> l(c->mu); // see gr_hip_fwd4_submit
-	if (c->host_direct) {
-		// zero-copy: the kernel's loaders and storers move the lines over
-		// PCIe themselves, both directions at once, no staging copies
-		void *d_in, *d_meta, *d_out, *d_v;
-		if (host_dev_ptr(lines, &d_in) && host_dev_ptr(meta, &d_meta) && host_dev_ptr(out_lines, &d_out)
-		    && host_dev_ptr(verdicts, &d_v)) {
-			gr_hip_batch b = {d_in, d_out, static_cast<const gr_hip_pkt_meta *>(d_meta),
-					  static_cast<gr_hip_verdict *>(d_v), n, GR_HIP_LINE, out_stride,
-					  GR_HIP_BATCH_F_LINES_ONLY | oflags};
-			int r = launch(q, q->s, &b, true);
-			if (r < 0)
-				return r;
-			l.unlock(); // enqueued: the wait needs no lock (see gr_hip_node_process)
-			if (const int e_ = host_wait(q, q->s))
-				return e_;
-			return q_check(q);
-		}
+	bool direct = false;
+	if (const int r = host_direct_launch(q, lines, meta, n, out_lines, out_stride, verdicts, &direct); r < 0)
+		return r;
+	if (direct) {
+		l.unlock(); // enqueued: the wait needs no lock (see gr_hip_node_start)
+		if (const int e_ = host_wait(q, q->s))
+			return e_;
+		return q_check(q);
 	}
 	for (host_slot &h : q->hs) {
 		if (h.s != nullptr)
@@ -2208,48 +2239,62 @@ static uint32_t node_unfinished(const gr_hip_mbuf *m, uint32_t n, const uint32_t
 
 // The node's walk (include/grout_hip.h, "rte_graph node shim"): lay the
 // graph walks out on 64-packet tiles, stage the mbufs' header lines (or
-// frame addresses) into the queue's pinned buffers, forward them on the GPU,
-// hand them back with the context's iface / nexthop mirrors.
-extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst,
-				   struct gr_hip_node_stats *stats) {
+// frame addresses) into one of the queue's pinned walk slots and enqueue the
+// GPU work (gr_hip_node_start); wait for it and hand the walk back with the
+// context's iface / nexthop mirrors (gr_hip_node_finish). With two slots the
+// GPU forwards one walk while the CPU stages the next.
+extern "C" int gr_hip_node_start(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst) {
 	if (q == nullptr || (n && m == nullptr))
 		return -EINVAL;
-	if (n == 0)
-		return 0;
+	if (q->nw_count == GR_HIP_NODE_DEPTH)
+		return -EBUSY;
 	gr_hip_ctx *c = q->ctx;
-	if (q->node_pos.size() < n)
-		q->node_pos.resize(n);
-	uint32_t *pos = q->node_pos.data();
+	node_slot &w = q->nw[(q->nw_head + q->nw_count) % GR_HIP_NODE_DEPTH];
+	if (w.pos.size() < n)
+		w.pos.resize(n);
+	uint32_t *pos = w.pos.data();
 	const int staged = gr_hip_node_layout(m, n, burst, pos);
 	if (staged < 0)
 		return staged;
 	const uint32_t ns = (uint32_t)staged;
+	w.m = m;
+	w.n = n;
+	w.ns = ns;
+	w.burst = burst;
+	w.by_addr = false;
+	w.sync = true;
+	w.r = 0;
+	if (n == 0) { // nothing to send: finishes at once
+		q->nw_count++;
+		return 0;
+	}
 	hipSetDevice(c->dev);
-	if (ns > q->node_cap) {
-		hipHostFree(q->node_lines);
-		hipHostFree(q->node_out);
-		hipHostFree(q->node_meta);
-		hipHostFree(q->node_v);
-		q->node_lines = q->node_out = nullptr;
-		q->node_meta = nullptr;
-		q->node_v = nullptr;
-		q->node_cap = 0;
-		HCK(hipHostMalloc((void **)&q->node_lines, (size_t)ns * GR_HIP_LINE, hipHostMallocDefault));
-		HCK(hipHostMalloc((void **)&q->node_out, (size_t)ns * GR_HIP_PREFIX, hipHostMallocDefault));
-		HCK(hipHostMalloc((void **)&q->node_meta, (size_t)ns * sizeof(gr_hip_pkt_meta), hipHostMallocDefault));
-		HCK(hipHostMalloc((void **)&q->node_v, (size_t)ns * sizeof(gr_hip_verdict), hipHostMallocDefault));
-		q->node_cap = ns;
+	if (ns > w.cap) {
+		hipHostFree(w.lines);
+		hipHostFree(w.out);
+		hipHostFree(w.meta);
+		hipHostFree(w.v);
+		w.lines = w.out = nullptr;
+		w.meta = nullptr;
+		w.v = nullptr;
+		w.cap = 0;
+		HCK(hipHostMalloc((void **)&w.lines, (size_t)ns * GR_HIP_LINE, hipHostMallocDefault));
+		HCK(hipHostMalloc((void **)&w.out, (size_t)ns * GR_HIP_PREFIX, hipHostMallocDefault));
+		HCK(hipHostMalloc((void **)&w.meta, (size_t)ns * sizeof(gr_hip_pkt_meta), hipHostMallocDefault));
+		HCK(hipHostMalloc((void **)&w.v, (size_t)ns * sizeof(gr_hip_verdict), hipHostMallocDefault));
+		w.cap = ns;
 	}
 	if (q->d_pad == nullptr) { // the frame a pad slot points at (frames by address)
 		HCK(hipMalloc((void **)&q->d_pad, GR_HIP_LINE));
 		HCK(hipMemset(q->d_pad, 0, GR_HIP_LINE));
 	}
-	memset(q->node_v, NODE_V_FILL, (size_t)ns * sizeof(gr_hip_verdict));
+	memset(w.v, NODE_V_FILL, (size_t)ns * sizeof(gr_hip_verdict));
 	std::shared_lock<std::shared_mutex> lk(c->mu); // see gr_hip_fwd4_submit
-	uint64_t *ptrs = reinterpret_cast<uint64_t *>(q->node_lines);
-	const bool by_addr = c->node_ptrs && host_dev_ptr_ok(c, m, n, ptrs, pos);
+	uint64_t *ptrs = reinterpret_cast<uint64_t *>(w.lines);
+	w.by_addr = c->node_ptrs && host_dev_ptr_ok(c, m, n, ptrs, pos);
 	int r;
-	if (by_addr) {
+	bool enqueued = false;
+	if (w.by_addr) {
 		// the frames are device-accessible: hand them over by address, the
 		// kernel reads and rewrites them in place over PCIe
 		for (uint32_t i = 0, next = 0; i <= n; i++) { // pads point at a zeroed device line
@@ -2258,11 +2303,10 @@ extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uin
 				ptrs[next] = reinterpret_cast<uint64_t>(q->d_pad);
 			next = at + 1;
 		}
-		if ((r = gr_hip_node_stage(m, n, burst, pos, nullptr, q->node_meta)) < 0)
+		if ((r = gr_hip_node_stage(m, n, burst, pos, nullptr, w.meta)) < 0)
 			return r;
 		void *d_ptrs, *d_meta, *d_v;
-		if (!host_dev_ptr(q->node_lines, &d_ptrs) || !host_dev_ptr(q->node_meta, &d_meta)
-		    || !host_dev_ptr(q->node_v, &d_v))
+		if (!host_dev_ptr(w.lines, &d_ptrs) || !host_dev_ptr(w.meta, &d_meta) || !host_dev_ptr(w.v, &d_v))
 			return -EFAULT;
 		gr_hip_batch b = {d_ptrs, nullptr, static_cast<const gr_hip_pkt_meta *>(d_meta),
 				  static_cast<gr_hip_verdict *>(d_v), ns, 0, 0,
@@ -2270,30 +2314,99 @@ extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uin
 		// after everything already submitted on the queue, like gr_hip_fwd4_host
 		if ((r = launch(q, q->s, &b, true)) < 0)
 			return r;
-		// the lock covers the enqueue, not the wait: control-plane writers
-		// (FIB publication) are not held behind the walk's GPU time
-		lk.unlock();
-		if (const int e_ = host_wait(q, q->s))
-			return e_;
-		r = q_check(q);
-		lk.lock(); // the hand-back reads the iface and nexthop mirrors
+		enqueued = true;
 	} else {
-		lk.unlock(); // gr_hip_fwd4_host takes it itself
-		if ((r = gr_hip_node_stage(m, n, burst, pos, q->node_lines, q->node_meta)) < 0)
+		if ((r = gr_hip_node_stage(m, n, burst, pos, w.lines, w.meta)) < 0)
 			return r;
 		// the hand-back writes back at most the first 26 bytes: packed
 		// 32-byte prefixes come back, not whole lines
-		r = gr_hip_fwd4_host_ex(q, q->node_lines, q->node_meta, ns, q->node_out, GR_HIP_PREFIX, q->node_v);
-		lk.lock();
+		if ((r = host_direct_launch(q, w.lines, w.meta, ns, w.out, GR_HIP_PREFIX, w.v, &enqueued)) < 0)
+			return r;
+		if (!enqueued) { // not device-accessible: staged copies, waited for here
+			lk.unlock(); // gr_hip_fwd4_host takes it itself
+			w.r = gr_hip_fwd4_host_ex(q, w.lines, w.meta, ns, w.out, GR_HIP_PREFIX, w.v);
+		}
 	}
-	uint32_t unfinished = 0;
-	if (r == -ETIMEDOUT) // hand back what the GPU finished, the rest to grout's CPU nodes
-		unfinished = node_unfinished(m, n, pos, q->node_v);
-	else if (r < 0)
+	if (enqueued) {
+		HCK(hipEventRecord(w.done, q->s));
+		w.sync = false;
+	}
+	// the lock covers the enqueue, not the wait: control-plane writers
+	// (FIB publication) are not held behind the walk's GPU time
+	q->nw_count++;
+	return 0;
+}
+
+extern "C" int gr_hip_node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np,
+				  struct gr_hip_node_stats *stats) {
+	if (q == nullptr)
+		return -EINVAL;
+	if (q->nw_count == 0)
+		return -ENOENT;
+	gr_hip_ctx *c = q->ctx;
+	node_slot &w = q->nw[q->nw_head];
+	q->nw_head = (q->nw_head + 1) % GR_HIP_NODE_DEPTH;
+	q->nw_count--;
+	if (mp != nullptr)
+		*mp = w.m;
+	if (np != nullptr)
+		*np = w.n;
+	if (w.n == 0)
+		return 0;
+	int r = w.r;
+	if (!w.sync) {
+		hipSetDevice(c->dev);
+		HCK(hipEventSynchronize(w.done));
+		// the queue's error word covers every kernel in flight on it: which
+		// walk a give-up hit is read from the verdicts below
+		r = q_check(q);
+	}
+	if (r < 0 && r != -ETIMEDOUT)
 		return r;
-	r = gr_hip_node_apply(m, n, burst, pos, by_addr ? nullptr : q->node_out, GR_HIP_PREFIX, q->node_v,
+	// packets a kernel that gave up never reached go back to grout's CPU
+	// nodes, the others are handed back as usual
+	const uint32_t unfinished = node_unfinished(w.m, w.n, w.pos.data(), w.v);
+	std::shared_lock<std::shared_mutex> lk(c->mu); // the hand-back reads the iface and nexthop mirrors
+	r = gr_hip_node_apply(w.m, w.n, w.burst, w.pos.data(), w.by_addr ? nullptr : w.out, GR_HIP_PREFIX, w.v,
 			      c->ifaces.data(), c->max_ifaces, c->nh.data(), (uint32_t)c->nh.size(), stats);
 	return r < 0 ? r : (int)unfinished;
+}
+
+extern "C" int gr_hip_node_pending(gr_hip_queue_t *q, int *ready) {
+	if (q == nullptr)
+		return -EINVAL;
+	if (ready != nullptr) {
+		*ready = 0;
+		if (q->nw_count) {
+			const node_slot &w = q->nw[q->nw_head];
+			if (w.sync) {
+				*ready = 1;
+			} else {
+				hipSetDevice(q->ctx->dev);
+				const hipError_t e = hipEventQuery(w.done);
+				if (e == hipSuccess)
+					*ready = 1;
+				else if (e != hipErrorNotReady)
+					return -EIO;
+				(void)hipGetLastError();
+			}
+		}
+	}
+	return (int)q->nw_count;
+}
+
+extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst,
+				   struct gr_hip_node_stats *stats) {
+	if (q == nullptr || (n && m == nullptr))
+		return -EINVAL;
+	if (n == 0)
+		return 0;
+	if (q->nw_count)
+		return -EBUSY; // finish the pipelined walks first
+	const int r = gr_hip_node_start(q, m, n, burst);
+	if (r < 0)
+		return r;
+	return gr_hip_node_finish(q, nullptr, nullptr, stats);
 }
 
 extern "C" int gr_hip_queue_stats(gr_hip_queue_t *q, struct gr_hip_iface_stats *st, uint32_t max, int reset) {

@@ -191,6 +191,7 @@ class Queue:
         h = ctypes.c_void_p()
         check("gr_hip_queue_create", self.lib.gr_hip_queue_create(fp.h, stream, ctypes.byref(h)))
         self._h = h
+        self._walks = []  # mbuf arrays of the node walks in flight (node_start .. node_finish)
 
     @property
     def stream(self):
@@ -235,6 +236,31 @@ class Queue:
                                                                      ptr(ns)))
         self.unfinished = r  # mbufs handed back as PUNT because a kernel gave up
         return ns[0]
+
+    def node_start(self, mbufs, burst=64):
+        """First half of node_process: stage and enqueue without waiting.
+        The mbufs belong to the queue until the matching node_finish()."""
+        assert mbufs.dtype == abi.MBUF_DT and mbufs.flags["C_CONTIGUOUS"]
+        check("gr_hip_node_start", self.lib.gr_hip_node_start(self._h, ptr(mbufs), len(mbufs), burst))
+        self._walks.append(mbufs)  # keeps the views alive while the GPU works on them
+
+    def node_finish(self):
+        """Wait for the oldest started walk and hand it back; returns (the
+        mbuf array it was started with, per-node counters)."""
+        ns = np.zeros(1, dtype=abi.NODE_STATS_DT)
+        pm, pn = ctypes.c_void_p(), ctypes.c_uint32()
+        r = check("gr_hip_node_finish", self.lib.gr_hip_node_finish(self._h, ctypes.byref(pm), ctypes.byref(pn),
+                                                                   ptr(ns)))
+        m = self._walks.pop(0)
+        assert pn.value == len(m) and (len(m) == 0 or pm.value == m.ctypes.data)
+        self.unfinished = r
+        return m, ns[0]
+
+    def node_pending(self):
+        """(walks in flight, whether the oldest one's GPU work is done)."""
+        ready = ctypes.c_int()
+        n = check("gr_hip_node_pending", self.lib.gr_hip_node_pending(self._h, ctypes.byref(ready)))
+        return n, bool(ready.value)
 
     def stats(self, reset=False):
         st = np.zeros(self.fp.max_ifaces, dtype=abi.STATS_DT)

@@ -16,12 +16,17 @@
 // Per graph (one per worker, worker.c) the node keeps a walk: the mbufs of
 // successive RX bursts accumulate until a batch is full, an RX burst comes
 // back short (the queue drained: latency matters more than batching) or the
-// oldest packet has waited max_delay; then gr_hip_node_process() stages
-// their header lines, forwards them on the GPU and hands them back, and each
-// mbuf is enqueued on its verdict's edge with grout's private data for that
-// edge. A source node, "gpu_fwd4_flush", flushes a walk whose packets have
-// waited max_delay when no new burst arrives (rte_graph calls a node only
-// when it holds objects).
+// oldest packet has waited max_delay; then the batch's header lines are
+// staged and sent to the GPU (gr_hip_node_start), and once the GPU is done
+// the batch is handed back (gr_hip_node_finish): each mbuf is enqueued on
+// its verdict's edge with grout's private data for that edge. Batches are
+// pipelined two deep ("depth" 2, the default): while the GPU forwards one,
+// the worker accumulates and stages the next, and hands the one before back
+// as soon as it is done. Batches leave in the order they arrived. A source
+// node, "gpu_fwd4_flush", runs every graph walk: it hands back a batch whose
+// GPU work has completed, and flushes a batch whose packets have waited
+// max_delay when no new burst arrives (rte_graph calls a node only when it
+// holds objects).
 //
 // Built here against the rte_graph / grout stand-ins (rte_graph_min.h,
 // gr_datapath_min.h); in grout it includes <gr_graph.h>, <gr_mbuf.h>,
@@ -42,6 +47,7 @@ static struct gpu_fwd4_conf conf = {
 	.batch = 1u << 16,
 	.rx_burst = 64,
 	.max_delay_ns = 50000,
+	.depth = 2,
 };
 
 // One fast-path context per GPU; the worker graphs are spread over them.
@@ -54,9 +60,19 @@ static struct {
 static uint32_t n_gpus;
 
 int gpu_fwd4_configure(const struct gpu_fwd4_conf *c) {
-	if (c == NULL || c->batch == 0 || c->rx_burst == 0 || c->n_devs > GPU_FWD4_MAX_DEVS || n_gpus != 0)
+	if (c == NULL || c->batch == 0 || c->rx_burst == 0 || c->n_devs > GPU_FWD4_MAX_DEVS || n_gpus != 0
+	    || c->depth > GR_HIP_NODE_DEPTH)
 		return -EINVAL;
 	conf = *c;
+	if (conf.depth == 0)
+		conf.depth = GR_HIP_NODE_DEPTH;
+	return 0;
+}
+
+int gpu_fwd4_set_depth(uint32_t depth) {
+	if (depth == 0 || depth > GR_HIP_NODE_DEPTH)
+		return -EINVAL;
+	conf.depth = depth; // a graph's next flush switches (finishing what is in flight first)
 	return 0;
 }
 
@@ -142,10 +158,14 @@ struct gpu_walk {
 	const struct rte_graph *graph;
 	int gpu; // index in gpus[]
 	gr_hip_queue_t *q;
-	uint32_t n, cap;
+	uint32_t n, cap; // the batch accumulating, in buffer `cur`
 	uint64_t first_ns; // arrival of the oldest held packet, 0 = none
-	struct rte_mbuf **mbufs;
-	struct gr_hip_mbuf *v;
+	uint32_t cur;
+	struct rte_mbuf **mbufs[2];
+	struct gr_hip_mbuf *v[2];
+	int pending; // the other buffer's batch is on the GPU (gr_hip_node_start'ed)
+	uint32_t pend_n; // its size
+	uint64_t pend_ns; // when it was sent
 	struct gr_hip_node_stats stats;
 	uint64_t gpu_errors; // batches punted because the GPU call failed
 };
@@ -212,28 +232,76 @@ static void hand_back(struct rte_mbuf *m, const struct gr_hip_mbuf *v) {
 	}
 }
 
-static void flush(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
-	if (w->n == 0)
-		return;
-	const int r = gr_hip_node_process(w->q, w->v, w->n, conf.rx_burst, &w->stats);
-	if (r < 0) {
-		// the GPU could not take them (mbufs untouched): grout's CPU nodes do
+// Enqueue batch buffer k (n mbufs) on the verdict edges; r: what the GPU call
+// returned (< 0: the GPU could not take them, mbufs untouched: grout's CPU
+// nodes do; > 0: a kernel gave up, the packets it did not reach come back as
+// PUNT with their frames untouched, the others are forwarded as usual).
+static void deliver(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w, uint32_t k, uint32_t n,
+		    int r) {
+	struct rte_mbuf **mb = w->mbufs[k];
+	const struct gr_hip_mbuf *v = w->v[k];
+	if (r != 0)
 		w->gpu_errors++;
-		for (uint32_t i = 0; i < w->n; i++)
-			rte_node_enqueue_x1(graph, node, GR_HIP_E_PUNT, w->mbufs[i]);
-	} else {
-		// r > 0: a kernel gave up; the packets it did not reach come back
-		// as PUNT with their frames untouched, the others forwarded as usual
-		if (r > 0)
-			w->gpu_errors++;
-		for (uint32_t i = 0; i < w->n; i++) {
-			if (w->v[i].edge != GR_HIP_E_PUNT)
-				hand_back(w->mbufs[i], &w->v[i]);
-			rte_node_enqueue_x1(graph, node, w->v[i].edge, w->mbufs[i]);
-		}
+	if (r < 0) {
+		for (uint32_t i = 0; i < n; i++)
+			rte_node_enqueue_x1(graph, node, GR_HIP_E_PUNT, mb[i]);
+		return;
 	}
+	for (uint32_t i = 0; i < n; i++) {
+		if (v[i].edge != GR_HIP_E_PUNT)
+			hand_back(mb[i], &v[i]);
+		rte_node_enqueue_x1(graph, node, v[i].edge, mb[i]);
+	}
+}
+
+// Wait for the batch on the GPU and hand it back. Returns its size.
+static uint32_t finish_pending(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
+	if (!w->pending)
+		return 0;
+	struct gr_hip_mbuf *vm = NULL;
+	uint32_t n = 0;
+	const int r = gr_hip_node_finish(w->q, &vm, &n, &w->stats);
+	const uint32_t k = w->cur ^ 1;
+	w->pending = 0;
+	if (vm != w->v[k]) // cannot happen: one walk in flight per graph, started here
+		return 0;
+	deliver(graph, node, w, k, n, r);
+	return n;
+}
+
+// Send the accumulated batch; returns the mbufs handed back meanwhile.
+static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
+	if (w->n == 0)
+		return 0;
+	const uint32_t k = w->cur, n = w->n;
 	w->n = 0;
 	w->first_ns = 0;
+	if (conf.depth < 2) { // synchronous: finish what an earlier depth left, then this batch
+		const uint32_t d = finish_pending(graph, node, w);
+		deliver(graph, node, w, k, n, gr_hip_node_process(w->q, w->v[k], n, conf.rx_burst, &w->stats));
+		return d + n;
+	}
+	// stage and send this batch while the previous one may still be on the
+	// GPU, then hand the previous one back: batches leave in arrival order
+	const int r = gr_hip_node_start(w->q, w->v[k], n, conf.rx_burst);
+	uint32_t delivered = finish_pending(graph, node, w);
+	if (r < 0) {
+		deliver(graph, node, w, k, n, r);
+		return delivered + n;
+	}
+	w->pending = 1;
+	w->pend_n = n;
+	w->pend_ns = now_ns();
+	w->cur = k ^ 1;
+	return delivered;
+}
+
+// The batch on the GPU is done: hand it back now (a poll, no wait).
+static uint32_t reap(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
+	int ready = 0;
+	if (!w->pending || gr_hip_node_pending(w->q, &ready) < 0 || !ready)
+		return 0;
+	return finish_pending(graph, node, w);
 }
 
 static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node, void **objs, uint16_t nb_objs) {
@@ -248,8 +316,8 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 		if (w->n == w->cap)
 			flush(graph, node, w);
 		const struct iface_mbuf_data *d = iface_mbuf_data(m);
-		w->mbufs[w->n] = m;
-		w->v[w->n++] = (struct gr_hip_mbuf) {
+		w->mbufs[w->cur][w->n] = m;
+		w->v[w->cur][w->n++] = (struct gr_hip_mbuf) {
 			.frame = rte_pktmbuf_mtod(m, void *),
 			.pkt_len = rte_pktmbuf_pkt_len(m),
 			.data_len = m->data_len,
@@ -263,13 +331,17 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 		};
 		walk = 0;
 	}
-	if (w->n == 0)
+	if (w->n == 0) {
+		reap(graph, node, w);
 		return nb_objs;
+	}
 	const uint64_t t = now_ns();
 	if (w->first_ns == 0)
 		w->first_ns = t;
 	if (w->n >= conf.batch || nb_objs < conf.rx_burst || t - w->first_ns >= conf.max_delay_ns)
 		flush(graph, node, w);
+	else
+		reap(graph, node, w);
 	return nb_objs;
 }
 
@@ -287,12 +359,20 @@ static int gpu_fwd4_init(const struct rte_graph *graph, struct rte_node *node) {
 	w->graph = graph;
 	w->gpu = pick_gpu(graph);
 	w->cap = conf.batch + RTE_GRAPH_BURST_SIZE;
-	w->mbufs = calloc(w->cap, sizeof(*w->mbufs));
-	w->v = calloc(w->cap, sizeof(*w->v));
-	int r = (w->mbufs == NULL || w->v == NULL) ? -ENOMEM : gr_hip_queue_create(gpus[w->gpu].ctx, NULL, &w->q);
+	int r = 0;
+	for (int k = 0; k < 2; k++) {
+		w->mbufs[k] = calloc(w->cap, sizeof(*w->mbufs[k]));
+		w->v[k] = calloc(w->cap, sizeof(*w->v[k]));
+		if (w->mbufs[k] == NULL || w->v[k] == NULL)
+			r = -ENOMEM;
+	}
+	if (r == 0)
+		r = gr_hip_queue_create(gpus[w->gpu].ctx, NULL, &w->q);
 	if (r < 0) {
-		free(w->mbufs);
-		free(w->v);
+		for (int k = 0; k < 2; k++) {
+			free(w->mbufs[k]);
+			free(w->v[k]);
+		}
 		free(w);
 		return r;
 	}
@@ -308,11 +388,18 @@ static void gpu_fwd4_fini(const struct rte_graph *graph, struct rte_node *node) 
 		struct gpu_walk *w = walks[i];
 		if (w == NULL || w->graph != graph)
 			continue;
+		if (w->pending) // the GPU must be done with its buffers; the mbufs go back to their pool
+			gr_hip_node_finish(w->q, NULL, NULL, NULL);
+		if (w->pending)
+			for (uint32_t i = 0; i < w->pend_n; i++)
+				rte_pktmbuf_free(w->mbufs[w->cur ^ 1][i]);
 		gr_hip_queue_destroy(w->q);
 		if ((uint32_t)w->gpu < n_gpus && gpus[w->gpu].graphs > 0)
 			gpus[w->gpu].graphs--;
-		free(w->mbufs);
-		free(w->v);
+		for (int k = 0; k < 2; k++) {
+			free(w->mbufs[k]);
+			free(w->v[k]);
+		}
 		free(w);
 		walks[i] = NULL;
 	}
@@ -344,10 +431,13 @@ static uint16_t gpu_flush_process(struct rte_graph *graph, struct rte_node *node
 	if (c->w == NULL && (c->w = walk_of(graph)) == NULL)
 		return 0;
 	struct gpu_walk *w = c->w;
-	if (w->n == 0 || now_ns() - w->first_ns < conf.max_delay_ns)
-		return 0;
-	const uint32_t n = w->n;
-	flush(graph, node, w); // same edges as iface_input, same order
+	// same edges as iface_input, same order
+	uint32_t n = reap(graph, node, w);
+	const uint64_t t = now_ns();
+	if (w->pending && t - w->pend_ns >= conf.max_delay_ns)
+		n += finish_pending(graph, node, w); // waited long enough: wait for the GPU
+	if (w->n != 0 && t - w->first_ns >= conf.max_delay_ns)
+		n += flush(graph, node, w); // pipelined: a later walk of the graph hands it back
 	return (uint16_t)(n > UINT16_MAX ? UINT16_MAX : n);
 }
 

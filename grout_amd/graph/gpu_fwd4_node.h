@@ -79,10 +79,13 @@ struct gpu_fwd4_conf {
 	uint32_t batch; // packets accumulated before a GPU walk
 	uint32_t rx_burst; // port_rx burst size: a shorter burst flushes
 	uint64_t max_delay_ns; // a held packet never waits longer (flush node)
+	uint32_t depth; // batches in flight per graph: 1 = each waited for, 2 = pipelined (0: 2)
 };
 
 // Before module init (grout: from its configuration). 0 or -EINVAL.
 int gpu_fwd4_configure(const struct gpu_fwd4_conf *);
+// Batches in flight per graph (1 or 2), at any time. 0 or -EINVAL.
+int gpu_fwd4_set_depth(uint32_t depth);
 // The module's fast-path contexts, one per GPU (NULL before init or on
 // failure); gpu_fwd4_hip_ctx() is the first.
 gr_hip_ctx_t *gpu_fwd4_hip_ctx(void);

@@ -668,6 +668,22 @@ int gr_hip_node_apply(
 int gr_hip_node_process(gr_hip_queue_t *, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst,
 			struct gr_hip_node_stats *stats);
 
+// The same walk in two halves, so that the GPU forwards one walk while the
+// CPU stages the next (and the node hands back the one before): start lays
+// out and stages the mbufs and enqueues the GPU work without waiting; finish
+// waits for the OLDEST walk started on the queue and hands it back, with the
+// return value of gr_hip_node_process. Up to GR_HIP_NODE_DEPTH walks per
+// queue are in flight (start returns -EBUSY beyond); their mbufs belong to
+// the queue until their finish, which reports them in *m / *n. Walks finish
+// in start order. gr_hip_node_process is start + finish and returns -EBUSY
+// while walks are in flight.
+#define GR_HIP_NODE_DEPTH 2
+int gr_hip_node_start(gr_hip_queue_t *, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst);
+int gr_hip_node_finish(gr_hip_queue_t *, struct gr_hip_mbuf **m, uint32_t *n, struct gr_hip_node_stats *stats);
+// Walks in flight on the queue; *ready (optional) = 1 when the oldest one's
+// GPU work has completed (its finish will not wait).
+int gr_hip_node_pending(gr_hip_queue_t *, int *ready);
+
 #ifdef __cplusplus
 }
 #endif

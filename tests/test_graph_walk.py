@@ -69,6 +69,7 @@ def lib():
         _lib.gh_node_stats.argtypes = [P, P]
         _lib.gh_queue_stats.argtypes = [P, U32, ctypes.c_int]
         _lib.gh_set_objects.argtypes = [P, U32, P, U32, U32]
+        _lib.gpu_fwd4_set_depth.argtypes = [U32]
         _lib.gh_conn_add.argtypes = [P, P]
         _lib.gh_snat44_static_add.argtypes = [U16, U32, U32]
     return _lib
@@ -316,10 +317,20 @@ def test_graph_walk_corpus(pin):
     assert len(set(got["edge"])) > 20
 
 
+@pytest.fixture(params=[2, 1], ids=["pipelined", "depth1"])
+def depth(request):
+    """Batches in flight per graph: 2 (the default) or 1 (each waited for)."""
+    graph_ctx()
+    assert lib().gpu_fwd4_set_depth(request.param) == 0
+    yield request.param
+    lib().gpu_fwd4_set_depth(2)
+
+
 @pytest.mark.gpu
-def test_graph_walk_stream_batches():
+def test_graph_walk_stream_batches(depth):
     """A one-route stream over many batches: 4096-packet batches fill, the
-    last RX burst is short and flushes the rest."""
+    last RX burst is short and flushes the rest. Pipelined, batch i+1 is
+    staged while batch i is on the GPU; they still leave in RX order."""
     t = T.config_single_route()
     fr, me = S.stream(100_003, 0xB0C, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
     got = check_walk(t, fr, me)
@@ -327,16 +338,19 @@ def test_graph_walk_stream_batches():
 
 
 @pytest.mark.gpu
-def test_graph_walk_flush_node():
+def test_graph_walk_flush_node(depth):
     """Full bursts only: the packets behind the last full batch wait for the
-    flush source node (max_delay), then leave in order."""
+    flush source node (max_delay), then leave in order. Pipelined, the source
+    node also hands back the last batch the GPU finished."""
     t = T.config_single_route()
     n = BATCH + 2 * BURST
     fr, me = S.stream(n, 0xB0D, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    c0 = np.zeros(3, dtype=np.uint64)
+    assert lib().gh_rte_node_counters(b"gpu_fwd4_flush", c0.ctypes.data) == 0
     check_walk(t, fr, me)
     c = np.zeros(3, dtype=np.uint64)
     assert lib().gh_rte_node_counters(b"gpu_fwd4_flush", c.ctypes.data) == 0
-    assert c[2] >= 2 * BURST  # the flush node handed those packets on
+    assert c[2] - c0[2] >= 2 * BURST  # the flush node handed those packets on
 
 
 @pytest.mark.gpu

@@ -247,3 +247,59 @@ def test_node_give_up_hands_back(fastpath, ptrs):
     done = ~punt
     compare_mbufs(m[done], want[done], bufs[done], lines[done])
     q.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ptrs", [0, 1])
+def test_node_pipelined_walks(fastpath, ptrs):
+    """gr_hip_node_start / _finish: walk i+1 is staged and sent while walk i
+    is on the GPU, and walks finish in start order; every walk ends exactly
+    as gr_hip_node_process leaves it (the oracle's mbufs), counters included.
+    A third walk in flight is refused (-EBUSY), and so is node_process while
+    walks are in flight; finishing with none in flight is -ENOENT."""
+    from golden_util import fresh_fastpath_state
+    topo = T.config_fullview(count=100_000)
+    fr, me = S.stream(50_000, 0xB1F, routes=topo.route_array())
+    fresh_fastpath_state(fastpath, topo)
+    lines, v, st, want, ns_want = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
+    bufs, m = mbufs_for(fr, me)
+    L = fastpath.lib
+    if ptrs:
+        abi.check("gr_hip_host_register", L.gr_hip_host_register(fastpath.h, bufs.ctypes.data, bufs.nbytes))
+    q = fastpath.queue()
+    try:
+        fastpath.tune("node_ptrs", ptrs)
+        # walk boundaries on multiples of 64: the oracle's graph walks of 64 stay whole
+        cuts = [0, 64 * 100, 64 * 101, 64 * 400, 64 * 401 + 64, len(m)]
+        parts = [m[a:b] for a, b in zip(cuts, cuts[1:])]
+        total = np.zeros(1, dtype=abi.NODE_STATS_DT)[0]
+        q.node_start(parts[0])
+        assert q.node_pending()[0] == 1
+        for k in range(1, len(parts)):
+            q.node_start(parts[k])
+            assert q.node_pending()[0] == 2
+            assert L.gr_hip_node_start(q._h, parts[k].ctypes.data, len(parts[k]), 64) == -16  # -EBUSY
+            assert L.gr_hip_node_process(q._h, parts[k].ctypes.data, len(parts[k]), 64, None) == -16
+            got, ns = q.node_finish()
+            assert got is parts[k - 1] and q.unfinished == 0
+            total["packets"] += ns["packets"]
+            total["calls"] += ns["calls"]
+        got, ns = q.node_finish()
+        assert got is parts[-1]
+        total["packets"] += ns["packets"]
+        total["calls"] += ns["calls"]
+        assert q.node_pending() == (0, False)
+        assert L.gr_hip_node_finish(q._h, None, None, None) == -2  # -ENOENT
+        compare_mbufs(m, want, bufs, lines)
+        assert np.array_equal(total["packets"], ns_want["packets"])
+        assert np.array_equal(total["calls"], ns_want["calls"])
+        assert np.array_equal(q.stats(), st)
+        # an empty walk passes through the pipeline too
+        q.node_start(m[:0])
+        got, ns = q.node_finish()
+        assert len(got) == 0 and ns["packets"].sum() == 0
+    finally:
+        fastpath.tune("node_ptrs", 0)
+        if ptrs:
+            abi.check("gr_hip_host_unregister", L.gr_hip_host_unregister(fastpath.h, bufs.ctypes.data))
+        q.close()

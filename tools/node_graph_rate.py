@@ -1,0 +1,68 @@
+# SPDX-License-Identifier: BSD-3-Clause
+"""Forwarding rate of the grout node itself (gpu_fwd4_node.c) inside a whole
+rte_graph walk, driven from C: the walk harness's port_rx stand-in feeds
+full 64-packet bursts of the full-view stream, the node accumulates them into
+batches of --batch packets, the GPU forwards them and the node hands every
+mbuf to the recorder node of its edge (walk_harness.c). One worker thread,
+one graph; depth 1 (each batch waited for) against depth 2 (pipelined,
+the default), alternating, --reps times each. Mpps = mbufs / wall time of
+gh_run (one C call: no Python in the loop).
+
+    python tools/node_graph_rate.py --batch 16384 > out.jsonl
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=16384)
+    ap.add_argument("--mbufs", type=int, default=1 << 20)
+    ap.add_argument("--reps", type=int, default=4)
+    ap.add_argument("--pin", type=int, default=0, help="1: frames by address (node_ptrs)")
+    args = ap.parse_args()
+
+    import test_graph_walk as G  # the harness bindings and the fan-out control plane
+    from grout_amd import synth as S
+    from grout_amd import topology as T
+
+    L = G.lib()
+    devs = (ctypes.c_int * 1)(0)
+    r = L.gh_init(ctypes.cast(devs, ctypes.c_void_p), 1, 1024, 1 << 17, args.batch, 64, 50_000)
+    assert r == 0, r
+    assert L.gh_graph_create(0, 0) == 0
+    G._gh["fp"] = fp = G.FanOutPath(L)
+    topo = T.config_fullview()
+    G.load(fp, topo)
+    fp.tune("node_ptrs", args.pin)
+    L.gh_set_pin(args.pin)
+    fr, me = S.stream(args.mbufs, S.SEED_GPU_BASE, routes=topo.route_array())
+    fr = np.ascontiguousarray(fr)
+    me = np.ascontiguousarray(me)
+    for rep in range(args.reps + 1):
+        for depth in (1, 2):
+            assert L.gpu_fwd4_set_depth(depth) == 0
+            assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, len(me)) == 0
+            t0 = time.perf_counter()
+            walks = L.gh_run(1 << 24)
+            dt = time.perf_counter() - t0
+            assert walks > 0, walks
+            if rep == 0:
+                continue  # warm-up: staging buffers grown, pages touched
+            print(json.dumps({"batch": args.batch, "depth": depth, "mbufs": len(me), "graph_walks": walks,
+                              "ms": round(dt * 1e3, 2), "mpps": round(len(me) / dt / 1e6, 1),
+                              "mode": "frames by address" if args.pin else "staged lines"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,120 @@
+# SPDX-License-Identifier: BSD-3-Clause
+"""The rte_graph node's walk done in flushes of F packets, one flush waited
+for at a time (depth 1: gr_hip_node_process) or pipelined two deep (depth 2:
+gr_hip_node_start of flush i, then gr_hip_node_finish of flush i-1, as the
+grout node does, gpu_fwd4_node.c). K worker threads at once, each with its
+own queue and 2^20 mbufs of the full-view stream (staged header lines, the
+node's default). Per round every thread resets its mbufs, a barrier, walks
+them all, a barrier; aggregate Mpps = K x mbufs / the median round.
+
+    python tools/node_pipeline.py [--threads 1,4,8] [--flush 4096,16384,65536] > out.jsonl
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def walk(q, m, flush, depth):
+    n = len(m)
+    if depth == 1:
+        for o in range(0, n, flush):
+            q.node_process(m[o:o + flush])
+        return
+    for o in range(0, n, flush):
+        q.node_start(m[o:o + flush])
+        if o:
+            q.node_finish()
+    q.node_finish()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--threads", default="1,4,8")
+    ap.add_argument("--flush", default="4096,16384,65536")
+    ap.add_argument("--mbufs", type=int, default=1 << 20)
+    ap.add_argument("--rounds", type=int, default=5)
+    args = ap.parse_args()
+
+    from grout_amd import abi
+    from grout_amd import synth as S
+    from grout_amd import topology as T
+    from grout_amd.fwd import FastPath
+
+    topo = T.config_fullview()
+    fp = FastPath(0)
+    fp.load(topo)
+    n = args.mbufs
+    threads = [int(x) for x in args.threads.split(",")]
+    workers = []
+    for w in range(max(threads)):
+        fr, me = S.stream(n, S.SEED_GPU_BASE + w, routes=topo.route_array())
+        bufs = np.zeros((n, 256), dtype=np.uint8)  # mbuf data rooms (frame at offset 0)
+        bufs[:, :64] = fr
+        mb = np.zeros(n, dtype=abi.MBUF_DT)
+        mb["frame"] = bufs.ctypes.data + np.arange(n, dtype=np.uint64) * 256
+        mb["pkt_len"] = me["pkt_len"]
+        mb["data_len"] = me["pkt_len"]
+        mb["data_off"] = 128
+        mb["rss"] = me["rss"]
+        mb["iface"] = me["iface"]
+        wk = {"fr": fr, "bufs": bufs, "mb": mb, "m": mb.copy(), "q": fp.queue()}
+        walk(wk["q"], wk["m"], 1 << 16, 2)  # warm-up: both staging slots grown
+        workers.append(wk)
+    check = None
+    for flush in (int(x) for x in args.flush.split(",")):
+        for k in threads:
+            for depth in (1, 2):
+                bar = threading.Barrier(k + 1)
+                err = []
+
+                def run(wk):
+                    try:
+                        for _ in range(args.rounds):
+                            wk["m"][:] = wk["mb"]
+                            wk["bufs"][:, :64] = wk["fr"]
+                            bar.wait()
+                            walk(wk["q"], wk["m"], flush, depth)
+                            bar.wait()
+                    except Exception as e:  # reported below
+                        err.append(e)
+                        bar.abort()
+
+                ths = [threading.Thread(target=run, args=(workers[i],)) for i in range(k)]
+                for t in ths:
+                    t.start()
+                times = []
+                try:
+                    for _ in range(args.rounds):
+                        bar.wait()
+                        t0 = time.perf_counter()
+                        bar.wait()
+                        times.append(time.perf_counter() - t0)
+                except threading.BrokenBarrierError:
+                    pass
+                for t in ths:
+                    t.join()
+                if err:
+                    raise err[0]
+                # both depths leave the same mbufs: edges and rewritten frames
+                got = (workers[0]["m"]["edge"].copy(), workers[0]["bufs"][:, :32].copy())
+                if check is None:
+                    check = got
+                same = bool(np.array_equal(got[0], check[0]) and np.array_equal(got[1], check[1]))
+                d = float(np.median(times))
+                print(json.dumps({"flush_pkts": flush, "threads": k, "depth": depth, "mbufs_per_thread": n,
+                                  "ms_per_round": round(d * 1e3, 2), "mpps_aggregate": round(k * n / d / 1e6, 1),
+                                  "mpps_per_thread": round(n / d / 1e6, 1), "same_results": same}), flush=True)
+    for wk in workers:
+        wk["q"].close()
+    fp.close()
+
+
+if __name__ == "__main__":
+    main()
