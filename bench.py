@@ -56,6 +56,10 @@ def parse():
                         "packed 32-byte prefixes, every byte the path changes (GR_HIP_BATCH_F_PREFIX32)")
     p.add_argument("--no-prefix-leg", action="store_true",
                    help="skip the same measurement with packed 32-byte output prefixes (prefix32 in the line)")
+    p.add_argument("--settle-ms", type=float, default=60.0,
+                   help="before the --warmup steps of each leg, run the same step untimed for this long: after the "
+                        "idle gap of the stream upload the GPU takes ~20-40 launches to reach its steady clock "
+                        "(tools/clock_probe.py); the forwarding plane's throughput is its steady-state rate")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-path", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="wall time of the CPU baseline sample")
@@ -163,17 +167,30 @@ def main():
 
     q = fp.queue(shared_stream(dev))
     every = max(1, min(args.time_every, args.steps))
+    settle_launches = []  # per leg
 
     def measure(bufs, steps, warmup, prefix=None):
         """warmup + steps launches on `bufs`; -> (max-over-ranks seconds of the
         timed steps, kernel ms summed over the timed launches, their count)."""
         d_in_, d_out_, d_meta_, d_v_ = bufs
         pfx = prefix32 if prefix is None else prefix
-        fp.tune("time_every", every)  # every `every`-th submit of the queue carries events
 
         def step():
             q.submit(d_in_, d_out_, d_meta_, d_v_, n, in_stride=in_stride, out_stride=abi.LINE, lines_only=imix,
                      prefix32=pfx)
+
+        # settle: the same step, untimed, until the GPU has been busy for
+        # --settle-ms (its clock ramps up over the first tens of ms after idle)
+        fp.tune("untimed", 1)
+        t_settle, settled = time.perf_counter(), 0
+        while time.perf_counter() - t_settle < args.settle_ms / 1e3:
+            for _ in range(8):
+                step()
+            settled += 8
+            torch.cuda.synchronize()
+        fp.tune("untimed", 0)
+        settle_launches.append(settled)
+        fp.tune("time_every", every)  # every `every`-th submit of the queue carries events (count restarts)
 
         for _ in range(warmup):
             step()
@@ -273,6 +290,9 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "settle": {"ms": args.settle_ms, "launches": settle_launches[0] if settle_launches else 0,
+                   "note": "untimed launches of the same step before the warmup steps of each leg: the GPU's "
+                           "steady clock after the stream upload's idle gap"},
         "ms_per_step": round(tmax / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
