@@ -10,6 +10,7 @@ import socket
 import time
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -72,3 +73,30 @@ def test_two_replicas_gloo():
     assert all(r["fwd"] == r["n"] for r in res)
     # whole-job rate = all ranks' packets over the slowest clock
     assert abs(res[0]["mpps"] - 2 * 4096 / res[0]["tmax"] / 1e6) < 1e-9
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_the_gpu():
+    """The driver's N>1 command, on the box's one GPU: torch.distributed.run
+    starts two bench.py ranks, each forwards its own stream on its own FIB
+    replica through libgrout_hip.so (GR_BENCH_SHARE_GPU=1: both on device 0,
+    gloo for the barrier and the clock, since RCCL refuses two ranks on one
+    GPU), and rank 0 alone prints the whole-job line."""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ, GR_BENCH_SHARE_GPU="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--steps", "4", "--warmup", "2", "--workload", "single64", "--batch", str(1 << 20), "--placement", "plain",
+           "--settle-ms", "5", "--no-plain", "--no-prefix-leg", "--no-cpu-baseline", "--no-host-path"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 4 and d["warmup"] == 2 and d["scaling"] == "weak"
+    assert d["config"]["batch_pkts_per_gpu"] == 1 << 20
+    assert d["config"]["forwarded_frac"] == 1.0  # every packet of rank 0's stream left by port_output
+    # whole-job rate: both ranks' packets over the slowest rank's clock
+    assert abs(d["value"] - 2 * (1 << 20) * 4 / (d["ms_per_step"] * 4 / 1e3) / 1e6) < 0.01 * d["value"]
