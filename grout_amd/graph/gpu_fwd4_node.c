@@ -170,6 +170,32 @@ struct gpu_walk {
 	uint64_t gpu_errors; // batches punted because the GPU call failed
 };
 
+static uint64_t now_ns(void) {
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+// Where a worker's time goes (gpu_fwd4_prof): accumulated only while on.
+static struct {
+	int on;
+	uint64_t ns[GPU_FWD4_PROF_COUNT];
+} prof;
+
+void gpu_fwd4_prof(int on, uint64_t *out) {
+	if (out != NULL)
+		memcpy(out, prof.ns, sizeof(prof.ns));
+	memset(prof.ns, 0, sizeof(prof.ns));
+	prof.on = on;
+}
+
+#define PROF_T0() const uint64_t prof_t0__ = prof.on ? now_ns() : 0
+#define PROF_ADD(k)                                                                                \
+	do {                                                                                       \
+		if (prof.on)                                                                       \
+			prof.ns[k] += now_ns() - prof_t0__;                                        \
+	} while (0)
+
 #define MAX_WALKS 64
 static struct gpu_walk *walks[MAX_WALKS];
 
@@ -182,11 +208,6 @@ static struct gpu_walk *walk_of(const struct rte_graph *g) {
 
 GR_NODE_CTX_TYPE(gpu_fwd4_ctx, { struct gpu_walk *w; });
 
-static uint64_t now_ns(void) {
-	struct timespec ts;
-	clock_gettime(CLOCK_MONOTONIC, &ts);
-	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
-}
 
 static uint8_t ck_status(uint64_t ol_flags) {
 	switch (ol_flags & RTE_MBUF_F_RX_IP_CKSUM_MASK) {
@@ -238,6 +259,7 @@ static void hand_back(struct rte_mbuf *m, const struct gr_hip_mbuf *v) {
 // PUNT with their frames untouched, the others are forwarded as usual).
 static void deliver(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w, uint32_t k, uint32_t n,
 		    int r) {
+	PROF_T0();
 	struct rte_mbuf **mb = w->mbufs[k];
 	const struct gr_hip_mbuf *v = w->v[k];
 	if (r != 0)
@@ -252,6 +274,7 @@ static void deliver(struct rte_graph *graph, struct rte_node *node, struct gpu_w
 			hand_back(mb[i], &v[i]);
 		rte_node_enqueue_x1(graph, node, v[i].edge, mb[i]);
 	}
+	PROF_ADD(GPU_FWD4_PROF_DELIVER);
 }
 
 // Wait for the batch on the GPU and hand it back. Returns its size.
@@ -260,7 +283,9 @@ static uint32_t finish_pending(struct rte_graph *graph, struct rte_node *node, s
 		return 0;
 	struct gr_hip_mbuf *vm = NULL;
 	uint32_t n = 0;
+	PROF_T0();
 	const int r = gr_hip_node_finish(w->q, &vm, &n, &w->stats);
+	PROF_ADD(GPU_FWD4_PROF_FINISH);
 	const uint32_t k = w->cur ^ 1;
 	w->pending = 0;
 	if (vm != w->v[k]) // cannot happen: one walk in flight per graph, started here
@@ -283,7 +308,9 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 	}
 	// stage and send this batch while the previous one may still be on the
 	// GPU, then hand the previous one back: batches leave in arrival order
+	PROF_T0();
 	const int r = gr_hip_node_start(w->q, w->v[k], n, conf.rx_burst);
+	PROF_ADD(GPU_FWD4_PROF_START);
 	uint32_t delivered = finish_pending(graph, node, w);
 	if (r < 0) {
 		deliver(graph, node, w, k, n, r);
@@ -306,6 +333,7 @@ static uint32_t reap(struct rte_graph *graph, struct rte_node *node, struct gpu_
 
 static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node, void **objs, uint16_t nb_objs) {
 	struct gpu_walk *w = gpu_fwd4_ctx(node)->w;
+	PROF_T0();
 	uint8_t walk = GR_HIP_MBUF_F_WALK; // this call is one graph walk's iface_input stream
 	for (uint16_t i = 0; i < nb_objs; i++) {
 		struct rte_mbuf *m = objs[i];
@@ -331,6 +359,7 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 		};
 		walk = 0;
 	}
+	PROF_ADD(GPU_FWD4_PROF_ACCUMULATE);
 	if (w->n == 0) {
 		reap(graph, node, w);
 		return nb_objs;

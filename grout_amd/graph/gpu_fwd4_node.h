@@ -86,6 +86,16 @@ struct gpu_fwd4_conf {
 int gpu_fwd4_configure(const struct gpu_fwd4_conf *);
 // Batches in flight per graph (1 or 2), at any time. 0 or -EINVAL.
 int gpu_fwd4_set_depth(uint32_t depth);
+// Measurement: nanoseconds the node spent, per phase, since the last call
+// (then reset); on = 0 stops accumulating. out: GPU_FWD4_PROF_COUNT values.
+enum {
+	GPU_FWD4_PROF_ACCUMULATE, // process(): mbufs into the batch's gr_hip_mbuf views
+	GPU_FWD4_PROF_START, // gr_hip_node_start: layout, staging, launch
+	GPU_FWD4_PROF_FINISH, // gr_hip_node_finish: wait for the GPU, hand-back onto the views
+	GPU_FWD4_PROF_DELIVER, // the views onto the rte_mbufs + private data, enqueues
+	GPU_FWD4_PROF_COUNT,
+};
+void gpu_fwd4_prof(int on, uint64_t *out);
 // The module's fast-path contexts, one per GPU (NULL before init or on
 // failure); gpu_fwd4_hip_ctx() is the first.
 gr_hip_ctx_t *gpu_fwd4_hip_ctx(void);

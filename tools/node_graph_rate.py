@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--mbufs", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--pin", type=int, default=0, help="1: frames by address (node_ptrs)")
+    ap.add_argument("--depths", default="1,2")
     args = ap.parse_args()
 
     import test_graph_walk as G  # the harness bindings and the fan-out control plane
@@ -37,6 +38,8 @@ def main():
     from grout_amd import topology as T
 
     L = G.lib()
+    L.gpu_fwd4_prof.argtypes = [ctypes.c_int, ctypes.c_void_p]
+    L.gpu_fwd4_prof.restype = None
     devs = (ctypes.c_int * 1)(0)
     r = L.gh_init(ctypes.cast(devs, ctypes.c_void_p), 1, 1024, 1 << 17, args.batch, 64, 50_000)
     assert r == 0, r
@@ -50,17 +53,26 @@ def main():
     fr = np.ascontiguousarray(fr)
     me = np.ascontiguousarray(me)
     for rep in range(args.reps + 1):
-        for depth in (1, 2):
+        for depth in (int(d) for d in args.depths.split(",")):
             assert L.gpu_fwd4_set_depth(depth) == 0
             assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, len(me)) == 0
+            L.gpu_fwd4_prof(1, None)
             t0 = time.perf_counter()
             walks = L.gh_run(1 << 24)
             dt = time.perf_counter() - t0
+            ph = np.zeros(4, dtype=np.uint64)
+            L.gpu_fwd4_prof(0, ph.ctypes.data)
             assert walks > 0, walks
             if rep == 0:
                 continue  # warm-up: staging buffers grown, pages touched
+            # ns per packet in each phase of the node (depth 2: start and finish
+            # are the library's halves; depth 1 runs gr_hip_node_process, not split)
+            names = ["accumulate", "start", "finish", "deliver"]
+            per = {k: round(float(v) / len(me), 2) for k, v in zip(names, ph)}
+            per["rest_of_walk"] = round(dt * 1e9 / len(me) - sum(per.values()), 2)
             print(json.dumps({"batch": args.batch, "depth": depth, "mbufs": len(me), "graph_walks": walks,
                               "ms": round(dt * 1e3, 2), "mpps": round(len(me) / dt / 1e6, 1),
+                              "ns_per_pkt": per,
                               "mode": "frames by address" if args.pin else "staged lines"}), flush=True)
 
 
