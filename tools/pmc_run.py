@@ -19,7 +19,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 24)
-    ap.add_argument("--workload", default="fullview64", choices=["fullview64", "single64", "fullview6"])
+    ap.add_argument("--workload", default="fullview64",
+                    choices=["fullview64", "single64", "fullview6", "imix_frames"])
+    ap.add_argument("--slot", type=int, default=2240, help="imix_frames: bytes per frame slot (bench.py)")
     ap.add_argument("--ring", type=int, default=None, help="gr_hip_tune ring geometry")
     ap.add_argument("--wg", type=int, default=None, help="gr_hip_tune wg_per_cu")
     ap.add_argument("--stats", type=int, default=None)
@@ -43,6 +45,8 @@ def main():
     else:
         topo = T.config_fullview()
         kw = dict(routes=topo.route_array())
+        if args.workload == "imix_frames":  # whole IMIX frames in mbuf-like slots, as bench.py
+            kw.update(imix=True, stride=args.slot)
     fp = FastPath(0)
     fp.load(topo)
     for k in ("ring", "wg", "stats", "nt"):
@@ -55,13 +59,14 @@ def main():
         frames, meta = S.stream6(n, S.SEED_GPU_BASE, r6[r6["prefixlen"] < 128])
     else:
         frames, meta = S.stream(n, S.SEED_GPU_BASE, **kw)
+    stride = frames.shape[1]
     d_in = torch.from_numpy(frames.reshape(-1)).to(dev)
     d_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
-    d_out = torch.empty_like(d_in)
+    d_out = torch.empty(n * abi.LINE, dtype=torch.uint8, device=dev)
     d_v = torch.empty(n * 8, dtype=torch.uint8, device=dev)
     q = fp.queue(shared_stream(dev))
     for _ in range(args.reps):
-        q.submit(d_in, d_out, d_meta, d_v, n)
+        q.submit(d_in, d_out, d_meta, d_v, n, in_stride=stride, out_stride=abi.LINE)
     torch.cuda.synchronize()
     if args.no_calib:
         return
