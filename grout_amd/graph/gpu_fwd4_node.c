@@ -323,10 +323,14 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 	return delivered;
 }
 
+// A batch spends at least this long on the GPU (launch, PCIe both ways, the
+// kernel's tile latency: ~30 us for 64 packets): no poll before.
+#define REAP_MIN_NS 10000
+
 // The batch on the GPU is done: hand it back now (a poll, no wait).
 static uint32_t reap(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
 	int ready = 0;
-	if (!w->pending || gr_hip_node_pending(w->q, &ready) < 0 || !ready)
+	if (!w->pending || now_ns() - w->pend_ns < REAP_MIN_NS || gr_hip_node_pending(w->q, &ready) < 0 || !ready)
 		return 0;
 	return finish_pending(graph, node, w);
 }
