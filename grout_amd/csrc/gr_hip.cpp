@@ -159,6 +159,7 @@ struct node_slot {
 	uint8_t *lines = nullptr, *out = nullptr;
 	gr_hip_pkt_meta *meta = nullptr;
 	gr_hip_verdict *v = nullptr;
+	void *d_lines = nullptr, *d_out = nullptr, *d_meta = nullptr, *d_v = nullptr; // their device addresses
 	std::vector<uint32_t> pos; // where each mbuf is staged (gr_hip_node_layout)
 	hipEvent_t done = nullptr; // recorded behind the walk's GPU work
 	gr_hip_mbuf *m = nullptr;
@@ -2243,6 +2244,25 @@ static uint32_t node_unfinished(const gr_hip_mbuf *m, uint32_t n, const uint32_t
 // GPU work (gr_hip_node_start); wait for it and hand the walk back with the
 // context's iface / nexthop mirrors (gr_hip_node_finish). With two slots the
 // GPU forwards one walk while the CPU stages the next.
+// Measurement: nanoseconds spent in the parts of gr_hip_node_start, summed
+// over every queue (gr_hip_node_prof).
+static std::atomic<uint64_t> node_prof_ns[GR_HIP_NODE_PROF_COUNT];
+
+static inline uint64_t prof_now() {
+	struct timespec t;
+	clock_gettime(CLOCK_MONOTONIC, &t);
+	return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
+extern "C" int gr_hip_node_prof(uint64_t *out, uint32_t n, int reset) {
+	for (uint32_t k = 0; k < GR_HIP_NODE_PROF_COUNT; k++) {
+		const uint64_t v = reset ? node_prof_ns[k].exchange(0) : node_prof_ns[k].load();
+		if (out != nullptr && k < n)
+			out[k] = v;
+	}
+	return GR_HIP_NODE_PROF_COUNT;
+}
+
 extern "C" int gr_hip_node_start(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst) {
 	if (q == nullptr || (n && m == nullptr))
 		return -EINVAL;
@@ -2253,9 +2273,16 @@ extern "C" int gr_hip_node_start(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint3
 	if (w.pos.size() < n)
 		w.pos.resize(n);
 	uint32_t *pos = w.pos.data();
+	uint64_t t_prof = prof_now();
+	auto lap = [&](int k) {
+		const uint64_t t = prof_now();
+		node_prof_ns[k] += t - t_prof;
+		t_prof = t;
+	};
 	const int staged = gr_hip_node_layout(m, n, burst, pos);
 	if (staged < 0)
 		return staged;
+	lap(GR_HIP_NODE_PROF_LAYOUT);
 	const uint32_t ns = (uint32_t)staged;
 	w.m = m;
 	w.n = n;
@@ -2283,13 +2310,19 @@ extern "C" int gr_hip_node_start(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint3
 		HCK(hipHostMalloc((void **)&w.meta, (size_t)ns * sizeof(gr_hip_pkt_meta), hipHostMallocDefault));
 		HCK(hipHostMalloc((void **)&w.v, (size_t)ns * sizeof(gr_hip_verdict), hipHostMallocDefault));
 		w.cap = ns;
+		// looked up once here, not per walk (hipPointerGetAttributes is slow)
+		if (!host_dev_ptr(w.lines, &w.d_lines) || !host_dev_ptr(w.out, &w.d_out) || !host_dev_ptr(w.meta, &w.d_meta)
+		    || !host_dev_ptr(w.v, &w.d_v))
+			w.d_lines = w.d_out = w.d_meta = w.d_v = nullptr; // not device-accessible: staged copies
 	}
 	if (q->d_pad == nullptr) { // the frame a pad slot points at (frames by address)
 		HCK(hipMalloc((void **)&q->d_pad, GR_HIP_LINE));
 		HCK(hipMemset(q->d_pad, 0, GR_HIP_LINE));
 	}
 	memset(w.v, NODE_V_FILL, (size_t)ns * sizeof(gr_hip_verdict));
+	lap(GR_HIP_NODE_PROF_PREP);
 	std::shared_lock<std::shared_mutex> lk(c->mu); // see gr_hip_fwd4_submit
+	lap(GR_HIP_NODE_PROF_LOCK);
 	uint64_t *ptrs = reinterpret_cast<uint64_t *>(w.lines);
 	w.by_addr = c->node_ptrs && host_dev_ptr_ok(c, m, n, ptrs, pos);
 	int r;
@@ -2305,23 +2338,32 @@ extern "C" int gr_hip_node_start(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint3
 		}
 		if ((r = gr_hip_node_stage(m, n, burst, pos, nullptr, w.meta)) < 0)
 			return r;
-		void *d_ptrs, *d_meta, *d_v;
-		if (!host_dev_ptr(w.lines, &d_ptrs) || !host_dev_ptr(w.meta, &d_meta) || !host_dev_ptr(w.v, &d_v))
+		if (w.d_lines == nullptr)
 			return -EFAULT;
-		gr_hip_batch b = {d_ptrs, nullptr, static_cast<const gr_hip_pkt_meta *>(d_meta),
-				  static_cast<gr_hip_verdict *>(d_v), ns, 0, 0,
+		gr_hip_batch b = {w.d_lines, nullptr, static_cast<const gr_hip_pkt_meta *>(w.d_meta),
+				  static_cast<gr_hip_verdict *>(w.d_v), ns, 0, 0,
 				  GR_HIP_BATCH_F_LINES_ONLY | GR_HIP_BATCH_F_FRAME_PTRS};
-		// after everything already submitted on the queue, like gr_hip_fwd4_host
-		if ((r = launch(q, q->s, &b, true)) < 0)
+		// after everything already submitted on the queue, like gr_hip_fwd4_host;
+		// no timing events (the walk's own completion event is enough)
+		if ((r = launch(q, q->s, &b, false)) < 0)
 			return r;
 		enqueued = true;
 	} else {
 		if ((r = gr_hip_node_stage(m, n, burst, pos, w.lines, w.meta)) < 0)
 			return r;
+		lap(GR_HIP_NODE_PROF_STAGE);
 		// the hand-back writes back at most the first 26 bytes: packed
 		// 32-byte prefixes come back, not whole lines
-		if ((r = host_direct_launch(q, w.lines, w.meta, ns, w.out, GR_HIP_PREFIX, w.v, &enqueued)) < 0)
-			return r;
+		if (c->host_direct && w.d_lines != nullptr) {
+			// zero-copy (see host_direct_launch), on the slot's device addresses
+			gr_hip_batch b = {w.d_lines, w.d_out, static_cast<const gr_hip_pkt_meta *>(w.d_meta),
+					  static_cast<gr_hip_verdict *>(w.d_v), ns, GR_HIP_LINE, GR_HIP_PREFIX,
+					  GR_HIP_BATCH_F_LINES_ONLY | GR_HIP_BATCH_F_PREFIX32};
+			if ((r = launch(q, q->s, &b, false)) < 0)
+				return r;
+			enqueued = true;
+		}
+		lap(GR_HIP_NODE_PROF_LAUNCH);
 		if (!enqueued) { // not device-accessible: staged copies, waited for here
 			lk.unlock(); // gr_hip_fwd4_host takes it itself
 			w.r = gr_hip_fwd4_host_ex(q, w.lines, w.meta, ns, w.out, GR_HIP_PREFIX, w.v);
@@ -2331,6 +2373,7 @@ extern "C" int gr_hip_node_start(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint3
 		HCK(hipEventRecord(w.done, q->s));
 		w.sync = false;
 	}
+	lap(GR_HIP_NODE_PROF_RECORD);
 	// the lock covers the enqueue, not the wait: control-plane writers
 	// (FIB publication) are not held behind the walk's GPU time
 	q->nw_count++;

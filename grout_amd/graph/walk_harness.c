@@ -89,6 +89,16 @@ static struct rte_mbuf *mbuf_at(uint32_t i) {
 	return (struct rte_mbuf *)(H.mem + (size_t)i * GH_MBUF_SZ);
 }
 
+// Whether port_rx leaves each mbuf and frame in the CPU's caches, as a PMD
+// does on a real RX: it writes the mbuf fields from the RX descriptor, and
+// the NIC's DMA lands the frame in the LLC (DDIO). Off: both stay where
+// gh_load left them (cold for large loads).
+static int rx_touch;
+
+void gh_set_rx_touch(int on) {
+	rx_touch = on;
+}
+
 static uint16_t port_rx_process(struct rte_graph *graph, struct rte_node *node, void **objs, uint16_t nb) {
 	(void)objs;
 	(void)nb;
@@ -99,6 +109,12 @@ static uint16_t port_rx_process(struct rte_graph *graph, struct rte_node *node, 
 		struct rte_mbuf *m = mbuf_at(i);
 		const struct gr_hip_pkt_meta *pm = &H.meta_in[i];
 		struct iface_mbuf_data *d = iface_mbuf_data(m);
+		if (rx_touch) {
+			m->pkt_len = pm->pkt_len; // the PMD's descriptor fields
+			m->data_len = pm->pkt_len;
+			m->hash.rss = pm->rss;
+			__builtin_prefetch(rte_pktmbuf_mtod(m, void *), 0, 1); // DDIO: the frame in the LLC
+		}
 		d->iface = iface_from_id(pm->iface);
 		d->vlan_id = pm->vlan_ck & 0xfff;
 		burst[k++] = m;

@@ -684,6 +684,20 @@ int gr_hip_node_finish(gr_hip_queue_t *, struct gr_hip_mbuf **m, uint32_t *n, st
 // GPU work has completed (its finish will not wait).
 int gr_hip_node_pending(gr_hip_queue_t *, int *ready);
 
+// Measurement: nanoseconds gr_hip_node_start spent in each part, summed over
+// every queue of the process since the last reset. out[k] for k < n; returns
+// GR_HIP_NODE_PROF_COUNT.
+enum {
+	GR_HIP_NODE_PROF_LAYOUT, // gr_hip_node_layout
+	GR_HIP_NODE_PROF_PREP, // staging buffers grown, verdicts filled
+	GR_HIP_NODE_PROF_LOCK, // the context lock, shared
+	GR_HIP_NODE_PROF_STAGE, // gr_hip_node_stage
+	GR_HIP_NODE_PROF_LAUNCH, // the kernel launch (host_direct)
+	GR_HIP_NODE_PROF_RECORD, // the walk's completion event
+	GR_HIP_NODE_PROF_COUNT,
+};
+int gr_hip_node_prof(uint64_t *out, uint32_t n, int reset);
+
 #ifdef __cplusplus
 }
 #endif

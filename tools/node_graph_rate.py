@@ -31,9 +31,11 @@ def main():
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--pin", type=int, default=0, help="1: frames by address (node_ptrs)")
     ap.add_argument("--depths", default="1,2")
+    ap.add_argument("--rx-touch", default="0", help="harness port_rx leaves mbuf and frame cached (PMD + DDIO): 0,1")
     args = ap.parse_args()
 
     import test_graph_walk as G  # the harness bindings and the fan-out control plane
+    from grout_amd import abi
     from grout_amd import synth as S
     from grout_amd import topology as T
 
@@ -52,16 +54,23 @@ def main():
     fr, me = S.stream(args.mbufs, S.SEED_GPU_BASE, routes=topo.route_array())
     fr = np.ascontiguousarray(fr)
     me = np.ascontiguousarray(me)
+    L.gh_set_rx_touch.argtypes = [ctypes.c_int]
+    variants = [(int(d), int(t)) for d in args.depths.split(",") for t in args.rx_touch.split(",")]
     for rep in range(args.reps + 1):
-        for depth in (int(d) for d in args.depths.split(",")):
+        for depth, touch in variants:
             assert L.gpu_fwd4_set_depth(depth) == 0
+            L.gh_set_rx_touch(touch)
             assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, len(me)) == 0
             L.gpu_fwd4_prof(1, None)
+            H = abi.hip()
+            H.gr_hip_node_prof(None, 0, 1)
             t0 = time.perf_counter()
             walks = L.gh_run(1 << 24)
             dt = time.perf_counter() - t0
             ph = np.zeros(4, dtype=np.uint64)
             L.gpu_fwd4_prof(0, ph.ctypes.data)
+            lp = np.zeros(6, dtype=np.uint64)
+            H.gr_hip_node_prof(lp.ctypes.data, 6, 1)
             assert walks > 0, walks
             if rep == 0:
                 continue  # warm-up: staging buffers grown, pages touched
@@ -70,9 +79,11 @@ def main():
             names = ["accumulate", "start", "finish", "deliver"]
             per = {k: round(float(v) / len(me), 2) for k, v in zip(names, ph)}
             per["rest_of_walk"] = round(dt * 1e9 / len(me) - sum(per.values()), 2)
-            print(json.dumps({"batch": args.batch, "depth": depth, "mbufs": len(me), "graph_walks": walks,
+            print(json.dumps({"batch": args.batch, "depth": depth, "rx_touch": touch, "mbufs": len(me), "graph_walks": walks,
                               "ms": round(dt * 1e3, 2), "mpps": round(len(me) / dt / 1e6, 1),
                               "ns_per_pkt": per,
+                              "start_ns_per_pkt": {k: round(float(v) / len(me), 2) for k, v in zip(
+                                  ["layout", "prep", "lock", "stage", "launch", "record"], lp)},
                               "mode": "frames by address" if args.pin else "staged lines"}), flush=True)
 
 
