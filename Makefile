@@ -20,7 +20,7 @@ GRAPH_SRC = $(GRAPH)/rte_graph_min.c $(GRAPH)/gr_datapath_min.c $(GRAPH)/gpu_fwd
 GRAPH_HDRS = $(GRAPH)/rte_graph_min.h $(GRAPH)/gr_datapath_min.h $(GRAPH)/gpu_fwd4_node.h include/grout_hip.h
 HDRS = include/grout_hip.h $(CSRC)/fib6.h $(CSRC)/fwd4_kernel.h $(CSRC)/fwd4_dev.h $(CSRC)/fwd4_chain.h $(CSRC)/fib4.h
 
-all: $(LIB_HIP) $(LIB_HOST) $(LIB_ORACLE) $(LIB_GRAPH)
+all: $(LIB_HIP) $(LIB_HOST) $(LIB_ORACLE) $(LIB_GRAPH) tools/libnode_mt.so
 
 $(BUILD)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(BUILD)
@@ -55,6 +55,10 @@ $(LIB_ORACLE): oracle/oracle.c oracle/oracle.h include/grout_hip.h
 # test harness graph; links the HIP library (found next to it at run time).
 $(LIB_GRAPH): $(GRAPH_SRC) $(GRAPH_HDRS) $(LIB_HIP)
 	$(CC) -std=gnu11 $(CFLAGS_HOST) -Iinclude -shared -o $@ $(GRAPH_SRC) -Lgrout_amd -lgrout_hip '-Wl,-rpath,$$ORIGIN'
+
+# measurement tool: the node walk from C threads (tools/node_pipeline.py --driver c)
+tools/libnode_mt.so: tools/node_mt.c include/grout_hip.h $(LIB_HIP)
+	$(CC) -O2 -pthread -fPIC -Wall -Iinclude -shared -o $@ $< -Lgrout_amd -lgrout_hip '-Wl,-rpath,$$ORIGIN/../grout_amd'
 
 # ---- AddressSanitizer + UBSan build of the host code (CPU only) ----------
 # Every host C/C++ source of the libraries and the oracle, built with the ROCm

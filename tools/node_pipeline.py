@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--flush", default="4096,16384,65536")
     ap.add_argument("--mbufs", type=int, default=1 << 20)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--driver", default="python", choices=["python", "c"],
+                    help="c: the threads are C pthreads in tools/libnode_mt.so (no Python between the calls)")
     args = ap.parse_args()
 
     from grout_amd import abi
@@ -68,9 +70,31 @@ def main():
         walk(wk["q"], wk["m"], 1 << 16, 2)  # warm-up: both staging slots grown
         workers.append(wk)
     check = None
+    if args.driver == "c":
+        import ctypes
+        C = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnode_mt.so"))
+        C.node_mt_round.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                    ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
     for flush in (int(x) for x in args.flush.split(",")):
         for k in threads:
             for depth in (1, 2):
+                if args.driver == "c":
+                    qs = (ctypes.c_void_p * k)(*[workers[i]["q"]._h.value for i in range(k)])
+                    ms = (ctypes.c_void_p * k)(*[workers[i]["m"].ctypes.data for i in range(k)])
+                    times = []
+                    for _ in range(args.rounds):
+                        for i in range(k):
+                            workers[i]["m"][:] = workers[i]["mb"]
+                            workers[i]["bufs"][:, :64] = workers[i]["fr"]
+                        sec = ctypes.c_double()
+                        abi.check("node_mt_round", C.node_mt_round(qs, ms, k, n, flush, depth, ctypes.byref(sec)))
+                        times.append(sec.value)
+                    d = float(np.median(times))
+                    print(json.dumps({"driver": "c", "flush_pkts": flush, "threads": k, "depth": depth,
+                                      "mbufs_per_thread": n, "ms_per_round": round(d * 1e3, 2),
+                                      "mpps_aggregate": round(k * n / d / 1e6, 1),
+                                      "mpps_per_thread": round(n / d / 1e6, 1)}), flush=True)
+                    continue
                 bar = threading.Barrier(k + 1)
                 err = []
 
