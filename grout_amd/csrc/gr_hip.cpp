@@ -2304,6 +2304,7 @@ extern "C" int gr_hip_node_start(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint3
 		w.lines = w.out = nullptr;
 		w.meta = nullptr;
 		w.v = nullptr;
+		w.d_lines = w.d_out = w.d_meta = w.d_v = nullptr;
 		w.cap = 0;
 		HCK(hipHostMalloc((void **)&w.lines, (size_t)ns * GR_HIP_LINE, hipHostMallocDefault));
 		HCK(hipHostMalloc((void **)&w.out, (size_t)ns * GR_HIP_PREFIX, hipHostMallocDefault));
