@@ -25,6 +25,11 @@ Scripts (under smoke/ in the reference):
   cross_vrf_forward_test.sh a route whose nexthop is another VRF (xvrf)
   ip_forward_ip6nh_test.sh  IPv4 routes via IPv6 link-local nexthops
   ip_loadbalance_test.sh    an ECMP group of two nexthops
+  ip_fragment_test.sh       a 1280-byte MTU: DF (frag needed) and not (fragment)
+  ipip_encap_test.sh        an IPIP tunnel interface (ipip_output)
+  snat44_test.sh            dynamic SNAT (the CPU's conntrack continuations)
+  dnat44_test.sh            a static DNAT nexthop (dnat44_static)
+  bridge_test.sh            ports in a bridge domain (bridge_input)
 """
 import ipaddress
 
@@ -83,11 +88,12 @@ class Probe:
         return f"{self.script}:{self.line}"
 
 
-def v4(port, src, dst, ttl=64, proto=1, vlan=0, dst_mac=None):
-    # ping: ICMP echo with the default 56-byte payload (98-byte IP packet); traceroute: UDP probe
-    length = 14 + 84 if proto == 1 else 14 + 60
+def v4(port, src, dst, ttl=64, proto=1, vlan=0, dst_mac=None, size=56, df=False):
+    # ping -s size: ICMP echo, 8-byte header + size bytes (default 56: a 98-byte IP
+    # packet); traceroute: UDP probe; df: ping -M do (IP_PMTUDISC_DO)
+    length = 14 + 20 + 8 + size if proto == 1 else 14 + 60
     return S.frame(dst_mac=dst_mac or GR_MAC[port], src_mac=NS_MAC[port], src=src, dst=dst, ttl=ttl,
-                   proto=proto, length=length)
+                   proto=proto, length=length, flags_frag=0x4000 if df else 0)
 
 
 def v6(port, src, dst, hop=64, nh=58, dst_mac=None):
@@ -294,8 +300,133 @@ def ip_loadbalance(resolved):
     return t, pr
 
 
+def ip_fragment(resolved):
+    """smoke/ip_fragment_test.sh: p1's MTU is 1280 (:4). A 1260-byte ping is a
+    1288-byte IP packet: with DF it must fail (ip_error_frag_needed, :20),
+    without DF grout fragments it (ip_fragment, :22); ip_output.c:99-106."""
+    s = "ip_fragment_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 2)
+    t.ifaces[PORT[1]]["mtu"] = 1280  # port_add p1 mtu 1280 (:4)
+    t.add_address(PORT[0], "172.16.0.1/24")  # :5
+    t.add_address(PORT[1], "172.16.1.1/24")  # :6
+    if resolved:
+        neighbour(t, T.VRF_MAIN, PORT[0], "172.16.0.2", NS_MAC[0])
+        neighbour(t, T.VRF_MAIN, PORT[1], "172.16.1.2", NS_MAC[1])
+    pr = [
+        Probe(s, 18, 0, v4(0, "172.16.0.2", "172.16.1.2"), "ip_hold", "port_output", (1, 0, NS_MAC[1])),
+        Probe(s, 20, 0, v4(0, "172.16.0.2", "172.16.1.2", size=1260, df=True), "ip_error_frag_needed"),
+        Probe(s, 22, 0, v4(0, "172.16.0.2", "172.16.1.2", size=1260), "ip_fragment"),
+        # exactly the MTU passes, one byte more does not
+        Probe(s, 22, 0, v4(0, "172.16.0.2", "172.16.1.2", size=1252, df=True), "ip_hold", "port_output",
+              (1, 0, NS_MAC[1])),
+        Probe(s, 22, 0, v4(0, "172.16.0.2", "172.16.1.2", size=1253, df=True), "ip_error_frag_needed"),
+        # the replies come back the other way, on the 1500-byte port
+        Probe(s, 22, 1, v4(1, "172.16.1.2", "172.16.0.2", size=1260), "ip_hold", "port_output", (0, 0, NS_MAC[0])),
+    ]
+    return t, pr
+
+
+def ipip_encap(resolved):
+    """smoke/ipip_encap_test.sh: tun1 is an IPIP interface (local 172.16.1.1,
+    remote 172.16.1.2) holding 10.98.0.1/24 (:6-7). n0's ping to 10.98.0.2
+    leaves ip_output through tun1's type edge, ipip_output (ipip/datapath_out.c:91),
+    whether or not a neighbour is resolved (ip_output.c:110-122); the tunnelled
+    packets n1 sends back are for grout's own 172.16.1.1 (ipip_input on the CPU)."""
+    s = "ipip_encap_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 2)
+    TUN = 30
+    t.add_address(PORT[0], "10.99.0.1/24")  # :4
+    t.add_address(PORT[1], "172.16.1.1/24")  # :5
+    t.add_iface(TUN, "IPIP")  # :6
+    t.add_address(TUN, "10.98.0.1/24")  # :7
+    if resolved:
+        neighbour(t, T.VRF_MAIN, PORT[0], "10.99.0.2", NS_MAC[0])
+        neighbour(t, T.VRF_MAIN, PORT[1], "172.16.1.2", NS_MAC[1])
+    pr = [
+        Probe(s, 20, 0, v4(0, "10.99.0.2", "10.98.0.2"), "ipip_output"),
+        Probe(s, 21, 1, v4(1, "172.16.1.2", "172.16.1.1", proto=4), "ip_input_local"),  # IPIP to grout
+        Probe(s, 20, 0, v4(0, "10.99.0.2", "10.98.0.2", ttl=1), "ip_error_ttl_exceeded"),
+    ]
+    return t, pr
+
+
+def snat44(resolved):
+    """smoke/snat44_test.sh: dynamic SNAT on p0 (:6; GR_IFACE_F_SNAT_DYNAMIC,
+    modules/policy/control/snat44_dynamic.c:39). n1's ping to 172.16.0.2 leaves
+    through p0: the fast path stops where ip_output calls snat44_process
+    (ip_output_snat, run on the CPU); the replies to the SNAT address arrive on
+    p0 and stop where ip_input calls into conntrack (ip_input_local_ct)."""
+    s = "snat44_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 2)
+    t.ifaces[PORT[0]]["flags"] |= abi.IFACE_F_SNAT_DYNAMIC  # :6
+    t.add_address(PORT[0], "172.16.0.1/24")  # :4
+    t.add_address(PORT[1], "10.99.0.1/24")  # :5
+    if resolved:
+        neighbour(t, T.VRF_MAIN, PORT[0], "172.16.0.2", NS_MAC[0])
+        neighbour(t, T.VRF_MAIN, PORT[1], "10.99.0.99", NS_MAC[1])
+    pr = [
+        Probe(s, 20, 1, v4(1, "10.99.0.99", "172.16.0.2"), "ip_output_snat"),
+        Probe(s, 20, 0, v4(0, "172.16.0.2", "172.16.0.1"), "ip_input_local_ct"),
+        Probe(s, 24, 1, v4(1, "10.99.0.99", "172.16.0.2", proto=6), "ip_output_snat"),  # socat TCP
+        Probe(s, 28, 1, v4(1, "10.99.0.99", "172.16.0.2", proto=17), "ip_output_snat"),  # socat UDP
+        # p1 has no SNAT policy: n1's ping to grout's own p1 address stays plain local
+        Probe(s, 20, 1, v4(1, "10.99.0.99", "10.99.0.1"), "ip_input_local"),
+    ]
+    return t, pr
+
+
+def dnat44(resolved):
+    """smoke/dnat44_test.sh: a static DNAT of 172.16.0.99 on p0 (:6): a
+    GR_NH_T_DNAT nexthop and its /32 route in p0's VRF
+    (modules/policy/api/dnat44.c:148-166). n0's ping to 172.16.0.99 leaves
+    ip_input by that nexthop type's edge, dnat44_static."""
+    s = "dnat44_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 2)
+    t.add_address(PORT[0], "172.16.0.1/24")  # :4
+    t.add_address(PORT[1], "10.99.0.1/24")  # :5
+    t.add_route(T.VRF_MAIN, "172.16.0.99/32", t.add_nexthop(PORT[0], nh_type="DNAT"))  # :6
+    if resolved:
+        neighbour(t, T.VRF_MAIN, PORT[0], "172.16.0.2", NS_MAC[0])
+        neighbour(t, T.VRF_MAIN, PORT[1], "10.99.0.99", NS_MAC[1])
+    pr = [
+        Probe(s, 18, 0, v4(0, "172.16.0.2", "172.16.0.99"), "dnat44_static"),
+        # the address next to it is plain connected
+        Probe(s, 18, 0, v4(0, "172.16.0.2", "172.16.0.98"), "ip_hold"),
+    ]
+    return t, pr
+
+
+def bridge(resolved):
+    """smoke/bridge_test.sh: p0..p2 in bridge br0's domain (:5-7): iface_input's
+    mode edge for GR_IFACE_MODE_BRIDGE is bridge_input (bridge_input.c:124),
+    which switches on the CPU."""
+    s = "bridge_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    BR = 40
+    t.add_iface(BR, "BRIDGE", mac=GR_MAC[3])  # :4
+    for p in range(3):
+        t.add_port(PORT[p], p, GR_MAC[p], mode="BRIDGE")  # :5-7 (the domain itself lives on the CPU)
+    t.add_address(BR, "172.16.0.1/24")  # :8
+    pr = [
+        Probe(s, 19, 0, v4(0, "172.16.0.10", "172.16.0.11", dst_mac=NS_MAC[1]), "bridge_input"),
+        Probe(s, 20, 1, v4(1, "172.16.0.11", "172.16.0.12", dst_mac=NS_MAC[2]), "bridge_input"),
+        Probe(s, 32, 0, v4(0, "172.16.0.10", "172.16.0.1", dst_mac=GR_MAC[3]), "bridge_input"),
+        Probe(s, 19, 0, S.frame(dst_mac="ff:ff:ff:ff:ff:ff", src_mac=NS_MAC[0], ethertype=0x0806), "bridge_input"),
+    ]
+    return t, pr
+
+
 SCRIPTS = {f.__name__: f for f in (ip6_forward, vlan_forward, vrf_forward, cross_vrf_forward, ip_forward_ip6nh,
-                                   ip_loadbalance)}
+                                   ip_loadbalance, ip_fragment, ipip_encap, snat44, dnat44, bridge)}
 
 
 # ---------------------------------------------------------------------------
@@ -303,7 +434,8 @@ SCRIPTS = {f.__name__: f for f in (ip6_forward, vlan_forward, vrf_forward, cross
 # ---------------------------------------------------------------------------
 def _pack(probes):
     fr = [p.frame for p in probes]
-    arr, meta = S.pack(fr, stride=128, iface=[PORT[p.port] for p in probes], vlan=[p.vlan for p in probes])
+    stride = max(128, -(-max(len(f) for f in fr) // 64) * 64)  # whole frames: pkt_len bytes readable
+    arr, meta = S.pack(fr, stride=stride, iface=[PORT[p.port] for p in probes], vlan=[p.vlan for p in probes])
     meta["rss"] = [p.rss for p in probes]
     return arr, meta
 
