@@ -30,6 +30,8 @@ Scripts (under smoke/ in the reference):
   snat44_test.sh            dynamic SNAT (the CPU's conntrack continuations)
   dnat44_test.sh            a static DNAT nexthop (dnat44_static)
   bridge_test.sh            ports in a bridge domain (bridge_input)
+  ip6_same_peer_test.sh     a link-local address only on its own link
+  srv6_test.sh              SRv6 encap and local nexthops (sr6_output, sr6_local)
 """
 import ipaddress
 
@@ -425,8 +427,74 @@ def bridge(resolved):
     return t, pr
 
 
+def ip6_same_peer(resolved):
+    """smoke/ip6_same_peer_test.sh: a link-local address is only reachable on
+    its own link (:19: n1's ping to p2's link-local must go unanswered).
+    Link-local routes are scoped to their iface (modules/ip6/control/route.c:150-173):
+    on p1, fe80::/64 is p1's connected prefix, so the packet is held for a
+    neighbour solicitation on p1's link, which nobody answers (ip6_hold in both
+    states)."""
+    s = "ip6_same_peer_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 2)
+    t.add_address6(PORT[0], "fd00:ba4:1::1/64")  # :6
+    t.add_address6(PORT[1], "fd00:ba4:2::1/64")  # :7
+    if resolved:
+        neighbour(t, T.VRF_MAIN, PORT[0], "fd00:ba4:1::2", NS_MAC[0])
+        neighbour(t, T.VRF_MAIN, PORT[1], "fd00:ba4:2::2", NS_MAC[1])
+        neighbour(t, T.VRF_MAIN, PORT[0], eui64_ll(NS_MAC[0]), NS_MAC[0])
+        neighbour(t, T.VRF_MAIN, PORT[1], eui64_ll(NS_MAC[1]), NS_MAC[1])
+    n1_ll, n2_ll = eui64_ll(NS_MAC[0]), eui64_ll(NS_MAC[1])
+    pr = [
+        Probe(s, 17, 0, v6(0, n1_ll, eui64_ll(GR_MAC[0])), "ip6_input_local"),
+        Probe(s, 18, 1, v6(1, n2_ll, eui64_ll(GR_MAC[1])), "ip6_input_local"),
+        Probe(s, 19, 0, v6(0, n1_ll, eui64_ll(GR_MAC[1])), "ip6_hold"),  # p2's link-local, asked on p1
+        Probe(s, 20, 0, v6(0, "fd00:ba4:1::2", "fd00:ba4:2::2"), "ip6_hold", "port_output", (1, 0, NS_MAC[1])),
+        Probe(s, 21, 1, v6(1, "fd00:ba4:2::2", "fd00:ba4:1::2"), "ip6_hold", "port_output", (0, 0, NS_MAC[0])),
+        Probe(s, 22, 0, v6(0, "fd00:ba4:1::2", "fd00:ba4:1::1"), "ip6_input_local"),
+        Probe(s, 23, 1, v6(1, "fd00:ba4:2::2", "fd00:ba4:2::1"), "ip6_input_local"),
+        Probe(s, 24, 0, v6(0, "fd00:ba4:1::2", "fd00:ba4:2::2", hop=1, nh=17), "ip6_error_ttl_exceeded"),
+        Probe(s, 25, 1, v6(1, "fd00:ba4:2::2", "fd00:ba4:1::2", hop=1, nh=17), "ip6_error_ttl_exceeded"),
+    ]
+    return t, pr
+
+
+def srv6(resolved):
+    """smoke/srv6_test.sh: 192.168.0.0/16 via an SRv6 encap nexthop (id 42,
+    :18-19) leaves ip_output by the nexthop type's edge, sr6_output
+    (srv6_output.c:152), after ip_forward; fd00:202:100::/48 via an SRv6 local
+    End.DT4 nexthop (id 666, :27-28) leaves ip6_input by sr6_local; the
+    encapsulated return traffic n1 sends to fd00:202:100:: takes it."""
+    s = "srv6_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 2)
+    t.add_address6(PORT[1], "fd00:102::1/32")  # :5
+    t.add_address(PORT[0], "192.168.61.1/24")  # :6
+    sr = t.add_nexthop(0, nh_type="SR6_OUTPUT", slot=42)  # :18
+    t.add_route(T.VRF_MAIN, "192.168.0.0/16", sr)  # :19
+    gw = t.add_nexthop(PORT[1], "fd00:102::2", NS_MAC[1] if resolved else None)
+    t.add_route6(T.VRF_MAIN, "fd00:202::/32", gw)  # :20
+    loc = t.add_nexthop(0, nh_type="SR6_LOCAL", slot=666)  # :27
+    t.add_route6(T.VRF_MAIN, "fd00:202:100::/48", loc)  # :28
+    if resolved:
+        neighbour(t, T.VRF_MAIN, PORT[0], "192.168.61.2", NS_MAC[0])
+        neighbour(t, T.VRF_MAIN, PORT[1], "fd00:102::2", NS_MAC[1])
+    pr = [
+        Probe(s, 29, 0, v4(0, "192.168.61.2", "192.168.60.1"), "sr6_output"),
+        Probe(s, 29, 0, v4(0, "192.168.61.2", "192.168.60.1", ttl=1), "ip_error_ttl_exceeded"),
+        Probe(s, 29, 1, v6(1, "fd00:102::2", "fd00:202:100::", nh=43), "sr6_local"),  # IPv6 + routing header
+        Probe(s, 30, 1, v6(1, "fd00:102::2", "fd00:202:100::1"), "sr6_local"),
+        # the rest of fd00:202::/32 goes back to n1 by the gateway
+        Probe(s, 30, 1, v6(1, "fd00:102::2", "fd00:202:200::"), "ip6_hold", "port_output", (1, 0, NS_MAC[1])),
+    ]
+    return t, pr
+
+
 SCRIPTS = {f.__name__: f for f in (ip6_forward, vlan_forward, vrf_forward, cross_vrf_forward, ip_forward_ip6nh,
-                                   ip_loadbalance, ip_fragment, ipip_encap, snat44, dnat44, bridge)}
+                                   ip_loadbalance, ip_fragment, ipip_encap, snat44, dnat44, bridge, ip6_same_peer,
+                                   srv6)}
 
 
 # ---------------------------------------------------------------------------
