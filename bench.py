@@ -56,7 +56,7 @@ def parse():
                         "packed 32-byte prefixes, every byte the path changes (GR_HIP_BATCH_F_PREFIX32)")
     p.add_argument("--no-prefix-leg", action="store_true",
                    help="skip the same measurement with packed 32-byte output prefixes (prefix32 in the line)")
-    p.add_argument("--settle-ms", type=float, default=60.0,
+    p.add_argument("--settle-ms", type=float, default=100.0,
                    help="before the --warmup steps of each leg, run the same step untimed for this long: after the "
                         "idle gap of the stream upload the GPU takes ~20-40 launches to reach its steady clock "
                         "(tools/clock_probe.py); the forwarding plane's throughput is its steady-state rate")
