@@ -39,6 +39,8 @@ def parse():
                    help="packets per step per GPU (default 2^24; 2^22 for imix_frames, 8 GiB of 2 KiB slots)")
     p.add_argument("--workload", default="fullview64",
                    choices=["fullview64", "single64", "imix", "imix_frames", "fullview6"])
+    p.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                   help="gr_hip_tune knobs set before the FIB load, e.g. v6_shortcut=1 (repeatable)")
     p.add_argument("--slot", type=int, default=2240,
                    help="imix_frames: bytes per frame slot (2240 = grout's mbuf object: 128 B rte_mbuf + "
                         "64 B priv + 2048 B data room, mempool.c:57-100)")
@@ -111,6 +113,9 @@ def main():
                     "imix_frames": ("config4: IMIX 64/570/1518 synthetic burst, full-view FIB, whole frames "
                                     f"resident in {args.slot}-byte mbuf-like slots")}[args.workload]
     fp = FastPath(local)
+    tune = dict(kv.split("=", 1) for kv in args.tune)
+    for k, v in tune.items():
+        fp.tune(k, int(v))
     fp.load(topo)
     info = fp.fib6_info(T.VRF_MAIN) if args.workload == "fullview6" else fp.fib_info(T.VRF_MAIN)
     log(f"[rank {rank}] topology + FIB loaded in {time.time() - t0:.1f}s: {info}")
@@ -308,6 +313,8 @@ def main():
             "parallelism": f"replicas x{world} (one RX stream + FIB replica per GPU, no collective)"
             + (" [rehearsal: all ranks on one GPU]" if share else ""),
             "forwarded_frac": round(fwd_frac, 6),
+            **({"tune": {k: int(v) for k, v in tune.items()}} if tune else {}),
+            "occupancy_wg_per_cu": fp.tune("occupancy"),
             "placement": (f"calibrated: output lines, then frames = fastest of {args.candidates + 1} allocations each, "
                           "timed over a batch of this workload drawn with another seed (gr_hip_batch_place)"
                           if batch is not None else "plain torch allocations"),

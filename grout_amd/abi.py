@@ -225,6 +225,10 @@ HOST_API = {
     "gr_fib6_skips_used": (_U32, [_P]),
     "gr_fib6_groups_painted": (_U32, [_P]),
     "gr_fib6_n_routes": (_U32, [_P]),
+    "gr_fib6_shortcuts": (_I, [_P, _P, _P, _U32]),
+    "gr_fib6_top": (_P, [_P]),
+    "gr_fib6_groups": (_P, [_P]),
+    "gr_fib6_skips": (_P, [_P]),
 }
 
 

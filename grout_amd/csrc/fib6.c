@@ -496,3 +496,83 @@ uint32_t gr_fib6_max_slot(const gr_fib6_t *f) {
 uint64_t gr_fib6_generation(const gr_fib6_t *f) {
 	return f->generation;
 }
+
+static int cmp_u32(const void *a, const void *b) {
+	const uint32_t x = *(const uint32_t *)a, y = *(const uint32_t *)b;
+	return x < y ? -1 : x > y;
+}
+
+static int cmp_run(const void *a, const void *b) { // (count, key) pairs: count descending, key ascending
+	const uint32_t *x = a, *y = b;
+	if (x[0] != y[0])
+		return x[0] > y[0] ? -1 : 1;
+	return x[1] < y[1] ? -1 : x[1] > y[1];
+}
+
+int gr_fib6_shortcuts(const gr_fib6_t *f, uint32_t *keys, uint32_t *ents, uint32_t max) {
+	if (f == NULL || (max && (keys == NULL || ents == NULL)))
+		return -EINVAL;
+	uint32_t n = 0;
+	uint32_t *k = malloc((size_t)(f->n_routes ? f->n_routes : 1) * sizeof(*k));
+	if (k == NULL)
+		return -ENOMEM;
+	for (uint32_t i = 0; i < f->cap; i++) {
+		const struct rib6_ent *r = &f->ht[i];
+		if (r->used == 1 && r->len >= 32)
+			k[n++] = (uint32_t)r->ip[0] | (uint32_t)r->ip[1] << 8 | (uint32_t)r->ip[2] << 16 | (uint32_t)r->ip[3] << 24;
+	}
+	qsort(k, n, sizeof(*k), cmp_u32);
+	// (routes under the /32, key), busiest first
+	uint32_t *runs = malloc((size_t)(n ? n : 1) * 2 * sizeof(*runs));
+	if (runs == NULL) {
+		free(k);
+		return -ENOMEM;
+	}
+	uint32_t nr = 0;
+	for (uint32_t i = 0; i < n;) {
+		uint32_t j = i;
+		while (j < n && k[j] == k[i])
+			j++;
+		runs[2 * nr] = j - i;
+		runs[2 * nr + 1] = k[i];
+		nr++;
+		i = j;
+	}
+	qsort(runs, nr, 2 * sizeof(*runs), cmp_run);
+	uint32_t out = 0;
+	for (uint32_t i = 0; i < nr && out < max; i++) {
+		const uint32_t key = runs[2 * i + 1];
+		const uint8_t ip[4] = {key & 0xff, (key >> 8) & 0xff, (key >> 16) & 0xff, key >> 24};
+		uint32_t ent = f->top[((uint32_t)ip[0] << 8) | ip[1]];
+		int b = 2;
+		bool ok = true;
+		while (b < 4 && (ent & GR_FIB6_EXT)) {
+			if (ent & GR_FIB6_SKIP) {
+				const struct gr_fib6_skip *s = &f->skips[ent & GR_FIB6_IDX];
+				if (b + s->n > 4) { // compares bytes past the key
+					ok = false;
+					break;
+				}
+				ent = memcmp(ip + b, s->key, s->n) == 0 ? s->child : s->miss;
+				b += s->n;
+			} else if (ent & GR_FIB6_WIDE) {
+				if (b != 2) { // bytes 3 and 4
+					ok = false;
+					break;
+				}
+				ent = f->groups[(size_t)(ent & GR_FIB6_IDX) * GR_FIB6_GROUP + ((uint32_t)ip[2] << 8) + ip[3]];
+				b = 4;
+			} else {
+				ent = f->groups[(size_t)(ent & GR_FIB6_IDX) * GR_FIB6_GROUP + ip[b++]];
+			}
+		}
+		if (!ok || ent == 0)
+			continue;
+		keys[out] = key;
+		ents[out] = ent;
+		out++;
+	}
+	free(runs);
+	free(k);
+	return (int)out;
+}

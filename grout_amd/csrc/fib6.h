@@ -71,6 +71,14 @@ uint32_t gr_fib6_max_slot(const gr_fib6_t *);
 // Build generation: bumps on every repaint that changed the tables.
 uint64_t gr_fib6_generation(const gr_fib6_t *);
 
+// Shortcuts past address bytes 0-3 for the kernel's LDS table: for the /32s
+// holding the most routes (up to max), key = bytes 0-3 (byte 0 in the low
+// bits) and ent = the trie entry the walk reaches after those four bytes
+// (a leaf when the walk ends sooner). /32s whose walk crosses byte 3 in one
+// step (a skip node), or that reach "no route", are left out. Call after
+// gr_fib6_build. Returns the count, or -ENOMEM.
+int gr_fib6_shortcuts(const gr_fib6_t *, uint32_t *keys, uint32_t *ents, uint32_t max);
+
 #ifdef __cplusplus
 }
 #endif

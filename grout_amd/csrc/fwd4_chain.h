@@ -38,6 +38,9 @@ __device__ __forceinline__ kctx make_kctx(const fwd4_params &A, const fwd4_edges
 	P.nhf6 = T->nhf6;
 	P.nhf6_lds = nullptr; // set by the kernel that stages them
 	P.nhf6_n = 0;
+	P.sc_lds = nullptr;
+	P.sc_top = nullptr;
+	P.sc_probes = 0;
 	return P;
 }
 
@@ -377,14 +380,34 @@ __device__ __forceinline__ uint32_t byte_of(const uint32_t (&a)[4], int i) {
 // rte_fib6_lookup (modules/ip6/control/route.c:150-173) in the fib6.h trie of the iface's VRF:
 // key = dst with link-local addresses scoped to the ingress iface
 // (addr6_linklocal_scope, ip6.h:23-36).
-__device__ __forceinline__ uint32_t chain_fib6(const fwd4_rx6 &v, const uint32_t (&dst)[4], uint32_t iface_id) {
+__device__ __forceinline__ uint32_t chain_fib6(const kctx &P, const fwd4_rx6 &v, const uint32_t (&dst)[4],
+					      uint32_t iface_id) {
 	if (v.top == nullptr)
 		return 0;
 	uint32_t key[4] = {dst[0], dst[1], dst[2], dst[3]};
 	if ((key[0] & 0xff) == 0xfe && (key[0] & 0xc000) == 0x8000)
 		key[0] = (key[0] & 0xffff) | ((iface_id >> 8) << 16) | ((iface_id & 0xff) << 24);
-	uint32_t ent = gld(v.top + ((byte_of(key, 0) << 8) | byte_of(key, 1)));
-	int b = 2;
+	uint32_t ent = 0;
+	int b = 0;
+	if (P.sc_probes && v.top == P.sc_top) {
+		// the walk's state after bytes 0-3 for the view's busiest /32s, from LDS:
+		// no per-lane gather for the first levels (gr_fib6_shortcuts)
+		const uint32_t h = FWD4_SC_HASH(key[0]);
+		for (uint32_t i = 0; i < P.sc_probes; i++) {
+			const u2v e = P.sc_lds[(h + i) & (FWD4_SC_SLOTS - 1)];
+			if (e.y == 0)
+				break;
+			if (e.x == key[0]) {
+				ent = e.y;
+				b = 4;
+				break;
+			}
+		}
+	}
+	if (b == 0) {
+		ent = gld(v.top + ((byte_of(key, 0) << 8) | byte_of(key, 1)));
+		b = 2;
+	}
 	while (b < 16 && (ent & 0x80000000u)) {
 		if (ent & GR_FIB6_SKIP) { // skip node: key bytes 0-6, n in byte 7
 			const uint4 k = gld4(v.skips + (ent & GR_FIB6_IDX));
@@ -452,7 +475,7 @@ __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, 
 		return;
 	}
 	const fwd4_rx6 v = {gld(&P.rx6[rx.id].top), gld(&P.rx6[rx.id].groups), gld(&P.rx6[rx.id].skips)};
-	uint32_t slot = chain_fib6(v, dst, rx.id); // ip6_input.c:124-131
+	uint32_t slot = chain_fib6(P, v, dst, rx.id); // ip6_input.c:124-131
 	if (slot == 0 || slot > P.max_nh) {
 		r.edge = GR_HIP_E_IP6_ERROR_DEST_UNREACH;
 		return;

@@ -86,6 +86,7 @@ struct fib4_buf {
 struct fib6_buf {
 	uint32_t *d6 = nullptr;
 	uint32_t groups = 0; // group capacity
+	uint32_t sc_probes = 0; // shortcut table after the skips: FWD4_SC_SLOTS (key, entry); longest probe run
 	uint64_t gen = 0; // fib6 generation it holds
 	bool up = false;
 
@@ -243,6 +244,8 @@ struct gr_hip_ctx {
 	int host_direct; // host path: the kernel reads / writes pinned host memory itself
 	int node_ptrs; // node path: frames in registered memory are handed over by address
 	int tile_order; // 0: workgroup b takes tiles b, b + G, ...; 1: one contiguous run each
+	int v6_sc; // IPv6 /32 shortcuts staged in LDS (fwd4_params.sc), for VRF sc_vrf; 2: staged only
+	uint16_t sc_vrf; // the VRF with the most IPv6 routes among those committed
 	uint32_t spin_max; // ring waits: polls before giving up (0 = the kernel's default)
 	int untimed; // measurements: no HIP events around launches (gr_hip_queue_kernel_ms sees none)
 	uint32_t time_every; // HIP events around every N-th submit of a queue only (0, 1 = every one)
@@ -729,6 +732,8 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->host_direct = 1; // measured 1.9x the staged copies
 	c->node_ptrs = 0; // staged lines: faster than frames by address, more so with several workers
 	c->tile_order = 0;
+	c->v6_sc = 0;
+	c->sc_vrf = 0;
 	c->spin_max = 0;
 	c->untimed = 0;
 	c->time_every = 1;
@@ -1600,6 +1605,11 @@ extern "C" int gr_hip_route6_del(gr_hip_ctx_t *c, uint16_t vrf, uint16_t iface_i
 	return gr_fib6_del(v.rib6, key, len);
 }
 
+static uint32_t *sc_of(const fib6_buf &b) {
+	return reinterpret_cast<uint32_t *>(reinterpret_cast<gr_fib6_skip *>(b.d6 + GR_FIB6_TOP + (size_t)b.groups * GR_FIB6_GROUP)
+					    + b.groups);
+}
+
 // Publish a repainted trie (fib6.h): the first level and the groups and
 // skips in use, written whole into the unpublished copy, then the same flip
 // as gr_hip_fib4_commit.
@@ -1626,7 +1636,7 @@ extern "C" int gr_hip_fib6_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 		if (b.d6 == nullptr) { // sized for the VRF's group capacity once: top, groups, skips
 			const uint32_t cap = gr_fib6_max_groups(v.rib6);
 			HCK(hipMalloc(&b.d6, ((size_t)GR_FIB6_TOP + (size_t)cap * GR_FIB6_GROUP) * sizeof(uint32_t)
-						     + (size_t)cap * sizeof(gr_fib6_skip)));
+						     + (size_t)cap * sizeof(gr_fib6_skip) + FWD4_SC_SLOTS * 8));
 			b.groups = cap;
 		}
 		stager st(c);
@@ -1638,6 +1648,28 @@ extern "C" int gr_hip_fib6_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 			memcpy(st.add(reinterpret_cast<gr_fib6_skip *>(b.d6 + GR_FIB6_TOP + (size_t)b.groups * GR_FIB6_GROUP),
 				      skips),
 			       gr_fib6_skips(v.rib6), (size_t)skips * sizeof(gr_fib6_skip));
+		// the busiest /32s' walk state past byte 3, open addressing at half load
+		uint32_t sk[FWD4_SC_SLOTS / 2], se[FWD4_SC_SLOTS / 2];
+		const int ns = gr_fib6_shortcuts(v.rib6, sk, se, FWD4_SC_SLOTS / 2);
+		if (ns < 0)
+			return ns;
+		uint32_t *img = st.add(sc_of(b), 2 * FWD4_SC_SLOTS);
+		memset(img, 0, FWD4_SC_SLOTS * 8);
+		b.sc_probes = 0;
+		for (int i = 0; i < ns; i++) {
+			uint32_t h = FWD4_SC_HASH(sk[i]), p = 1;
+			while (img[2 * h + 1] != 0) {
+				h = (h + 1) & (FWD4_SC_SLOTS - 1);
+				p++;
+			}
+			img[2 * h] = sk[i];
+			img[2 * h + 1] = se[i];
+			if (p > b.sc_probes)
+				b.sc_probes = p;
+		}
+		if (c->sc_vrf == 0 || c->vrfs[c->sc_vrf].rib6 == nullptr
+		    || gr_fib6_n_routes(v.rib6) >= gr_fib6_n_routes(c->vrfs[c->sc_vrf].rib6))
+			c->sc_vrf = vrf;
 		b.gen = gen;
 		b.up = true;
 		views_follow_published(c, B);
@@ -1814,11 +1846,12 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	A.meta = b->meta;
 	A.verdicts = b->verdicts;
 	A.stats = q->d_stats;
-	A.T = c->d_tables[c->gen]; // the generation published when this launch is enqueued
+	const uint32_t g = c->gen;
+	A.T = c->d_tables[g]; // the generation published when this launch is enqueued
 	// ... whose upload the stream waits for, once per publication (the
 	// host's own streams of gr_hip_fwd4_host at every launch)
 	if (s != q->s || q->seen_serial != c->serial) {
-		HCK(hipStreamWaitEvent(s, c->ready_ev[c->gen], 0));
+		HCK(hipStreamWaitEvent(s, c->ready_ev[g], 0));
 		if (s == q->s)
 			q->seen_serial = c->serial;
 	}
@@ -1838,6 +1871,17 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	// as many as the geometry's LDS leaves room for (IPv6 given up first)
 	uint32_t n4 = c->nh_hi < gr_fwd4_ring_nhf_max() ? c->nh_hi : gr_fwd4_ring_nhf_max();
 	uint32_t n6 = c->v6_routes ? n4 : 0;
+	uint32_t sc = 0; // shortcut table, in 16-byte LDS units
+	if (c->v6_sc && c->v6_routes && c->sc_vrf != 0) {
+		const vrf_fib &v = c->vrfs[c->sc_vrf];
+		const fib6_buf &b = v.b6[v.sel6[g]];
+		if (v.rib6 != nullptr && b.up && b.sc_probes) {
+			A.sc = sc_of(b);
+			A.sc_top = b.d6;
+			A.sc_probes = b.sc_probes | (c->v6_sc == 2 ? 0x80000000u : 0);
+			sc = FWD4_SC_SLOTS / 2;
+		}
+	}
 	int occ;
 	{
 		std::lock_guard<std::mutex> ol(c->occ_mu);
@@ -1854,7 +1898,12 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 				e.occ[v] = gr_fwd4_ring_occupancy(v, cfg, staged);
 			return e;
 		};
-		const gr_hip_ctx::occ_entry *e = &occ_of(n4 + n6);
+		const gr_hip_ctx::occ_entry *e = &occ_of(n4 + n6 + sc);
+		if (e->occ[variant] <= 0 && sc) {
+			sc = 0;
+			A.sc_probes = 0;
+			e = &occ_of(n4 + n6);
+		}
 		if (e->occ[variant] <= 0 && n6) {
 			n6 = 0;
 			e = &occ_of(n4);
@@ -1934,6 +1983,15 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < 0 || value > 2)
 			return -EINVAL;
 		c->tile_order = value;
+	} else if (strcmp(key, "v6_shortcut") == 0) {
+		if (value < 0 || value > 2)
+			return -EINVAL;
+		c->v6_sc = value;
+	} else if (strcmp(key, "v6_shortcut_probes") == 0) { // read: the longest probe run of VRF `value`'s table
+		if (value <= 0 || (uint32_t)value >= c->max_ifaces || c->vrfs[value].rib6 == nullptr
+		    || !c->vrfs[value].uploaded6())
+			return -ENONET;
+		return (int)c->vrfs[value].b6[c->vrfs[value].pub6].sc_probes;
 	} else if (strcmp(key, "host_direct") == 0) {
 		c->host_direct = value != 0;
 	} else if (strcmp(key, "fib_format_of") == 0) { // read: the format VRF `value` is on the device in

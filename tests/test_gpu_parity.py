@@ -590,12 +590,21 @@ def test_tile_orders(fastpath, order):
 
 # ---- IPv6
 
+@pytest.fixture(params=[0, 1], ids=["trie", "shortcut"])
+def v6sc(request, fastpath):
+    """Both IPv6 first-level paths: the trie from the top (gather per level)
+    and the /32 shortcut table staged in LDS (gr_hip_tune "v6_shortcut")."""
+    fastpath.tune("v6_shortcut", request.param)
+    yield request.param
+    fastpath.tune("v6_shortcut", 0)
+
+
 @functools.lru_cache(maxsize=None)
 def _fullview6_big():
     return T.config_fullview6(count=100_000)
 
 
-def test_fullview6_stream(fastpath):
+def test_fullview6_stream(fastpath, v6sc):
     """IPv6 forwarding over a 100k-route IPv6 view, 2^20 packets."""
     t = _fullview6_big()
     fr, me = S.stream6(1 << 20, S.SEED_FULLVIEW6 + 1, t.route6_array())
@@ -605,10 +614,11 @@ def test_fullview6_stream(fastpath):
     assert (g[1]["edge"] == abi.EDGE["port_output"]).mean() > 0.99
     info = fastpath.fib6_info(1)
     assert info["routes"] == len(t.route6_array()) and info["groups_used"] > 20_000  # a deep, path-compressed trie
+    assert 0 < fastpath.tune("v6_shortcut_probes", 1) < 64  # the table is filled, its probe runs short
 
 
 @pytest.mark.parametrize("seed", [1, 2])
-def test_clustered_routes6_stream(fastpath, seed):
+def test_clustered_routes6_stream(fastpath, seed, v6sc):
     """IPv6 forwarding over clustered tables whose tries widen at bytes 2-5
     (scenarios.clustered_routes6: wide groups and widened one-byte skips
     below the first level, the kernel's WIDE branch at several depths)."""
@@ -626,7 +636,7 @@ def test_clustered_routes6_stream(fastpath, seed):
     assert (g[1]["edge"] == abi.EDGE["port_output"]).mean() > 0.9
 
 
-def test_mixed_v4_v6_stream(fastpath):
+def test_mixed_v4_v6_stream(fastpath, v6sc):
     """IPv4 and IPv6 packets interleaved in every wave (divergent chains)."""
     t, _ = SC.corpus_topology()
     rng = np.random.default_rng(46)
@@ -639,7 +649,7 @@ def test_mixed_v4_v6_stream(fastpath):
     compare(oracle.Oracle(t).process(fr, me), run_gpu(fastpath, t, fr, me))
 
 
-def test_live_route6_updates(fastpath):
+def test_live_route6_updates(fastpath, v6sc):
     """route6 add / replace / delete after the first commit, then parity
     (rib6_insert_or_replace / rib6_delete, modules/ip6/control/route.c), one
     commit per kind of change so that the trie's two device copies alternate;

@@ -11,6 +11,7 @@
    limit of ip6_forward, and the IPv6 LPM (oracle hash, brute force and the
    product's trie) against each other.
 """
+import ctypes
 import ipaddress
 
 import numpy as np
@@ -421,4 +422,66 @@ def test_fib6_clustered_rebuilds(seed):
             live[i] = ~live[i]
     if seed != 3:  # seed 3's clusters are too light to widen
         assert _wide_entries(host, f) > 0
+    host.gr_fib6_free(f)
+
+
+def _walk_from(host, f, ip, ent, b):
+    """The rest of the fib6.h walk from (ent, b), as chain_fib6 resumes it."""
+    G = ctypes.cast(host.gr_fib6_groups(f), ctypes.POINTER(ctypes.c_uint32))
+    S = ctypes.cast(host.gr_fib6_skips(f), ctypes.POINTER(ctypes.c_uint8))
+    EXT, SKIP, WIDE, IDX = 0x80000000, 0x40000000, 0x20000000, 0x1FFFFFFF
+    while b < 16 and ent & EXT:
+        if ent & SKIP:
+            k = bytes(S[(ent & IDX) * 16 + i] for i in range(16))
+            n = k[7]
+            match = b + n <= 16 and bytes(ip[b:b + n]) == k[:n]
+            ent = int.from_bytes(k[8:12] if match else k[12:16], "little")
+            b += n
+        elif ent & WIDE:
+            ent = G[(ent & IDX) * 256 + (int(ip[b]) << 8) + int(ip[b + 1])]
+            b += 2
+        else:
+            ent = G[(ent & IDX) * 256 + int(ip[b])]
+            b += 1
+    return 0 if ent & EXT else ent
+
+
+@pytest.mark.parametrize("view", ["fullview6", "clustered"])
+def test_fib6_shortcuts_resume_exact(view):
+    """gr_fib6_shortcuts (the kernel's LDS table past address bytes 0-3):
+    resuming the walk at byte 4 from a /32's shortcut gives the full walk's
+    (and the RIB's) answer, for addresses under the busiest /32s."""
+    import scenarios as SC
+    host = abi.host()
+    if view == "fullview6":
+        r = T.config_fullview6().route6_array()
+    else:
+        r = np.ascontiguousarray(SC.clustered_routes6(3), dtype=abi.ROUTE6_DT)
+        r["nh"] = 1 + np.arange(len(r)) % 97  # nh left to the caller
+    f = _fib6_of(host, r)
+    keys = np.zeros(512, dtype=np.uint32)
+    ents = np.zeros(512, dtype=np.uint32)
+    n = host.gr_fib6_shortcuts(f, keys.ctypes.data, ents.ctypes.data, 512)
+    assert 0 < n <= 512
+    assert len(set(keys[:n].tolist())) == n and (ents[:n] != 0).all()
+    sc = dict(zip(keys[:n].tolist(), ents[:n].tolist()))
+    rng = np.random.default_rng(0x5C)
+    picked = r[rng.integers(0, len(r), 4000)]
+    checked = 0
+    for x in picked:
+        ip = np.ascontiguousarray(x["ip"]).copy()
+        nb = int(x["prefixlen"])
+        host_bits = rng.integers(0, 256, 16, dtype=np.uint8)
+        for i in range(16):  # random host bits under the prefix
+            keep = max(0, min(8, nb - 8 * i))
+            m = (0xFF00 >> keep) & 0xFF
+            ip[i] = (int(ip[i]) & m) | (int(host_bits[i]) & ~m & 0xFF)
+        key = int(ip[0]) | int(ip[1]) << 8 | int(ip[2]) << 16 | int(ip[3]) << 24
+        if key not in sc:
+            continue
+        want = host.gr_fib6_lookup(f, ip.ctypes.data)
+        assert want == host.gr_fib6_lookup_rib(f, ip.ctypes.data)
+        assert _walk_from(host, f, ip, sc[key], 4) == want
+        checked += 1
+    assert checked > 500
     host.gr_fib6_free(f)
