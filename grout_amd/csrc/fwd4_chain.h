@@ -40,7 +40,7 @@ __device__ __forceinline__ kctx make_kctx(const fwd4_params &A, const fwd4_edges
 	P.nhf6_n = 0;
 	P.sc_lds = nullptr;
 	P.sc_top = nullptr;
-	P.sc_probes = 0;
+	P.sc_keys = 0;
 	return P;
 }
 
@@ -389,20 +389,12 @@ __device__ __forceinline__ uint32_t chain_fib6(const kctx &P, const fwd4_rx6 &v,
 		key[0] = (key[0] & 0xffff) | ((iface_id >> 8) << 16) | ((iface_id & 0xff) << 24);
 	uint32_t ent = 0;
 	int b = 0;
-	if (P.sc_probes && v.top == P.sc_top) {
-		// the walk's state after bytes 0-3 for the view's busiest /32s, from LDS:
-		// no per-lane gather for the first levels (gr_fib6_shortcuts)
-		const uint32_t h = FWD4_SC_HASH(key[0]);
-		for (uint32_t i = 0; i < P.sc_probes; i++) {
-			const u2v e = P.sc_lds[(h + i) & (FWD4_SC_SLOTS - 1)];
-			if (e.y == 0)
-				break;
-			if (e.x == key[0]) {
-				ent = e.y;
-				b = 4;
-				break;
-			}
-		}
+	if (P.sc_keys && v.top == P.sc_top) {
+		// the walk's state after bytes 0-3 for the view's busiest /32s, from
+		// one LDS bucket: no per-lane gather for the first levels (gr_fib6_shortcuts)
+		const u4v e = P.sc_lds[FWD4_SC_HASH(key[0])];
+		ent = e.x == key[0] ? e.y : e.z == key[0] ? e.w : 0; // empty pairs hold entry 0
+		b = ent ? 4 : 0;
 	}
 	if (b == 0) {
 		ent = gld(v.top + ((byte_of(key, 0) << 8) | byte_of(key, 1)));

@@ -86,7 +86,7 @@ struct fib4_buf {
 struct fib6_buf {
 	uint32_t *d6 = nullptr;
 	uint32_t groups = 0; // group capacity
-	uint32_t sc_probes = 0; // shortcut table after the skips: FWD4_SC_SLOTS (key, entry); longest probe run
+	uint32_t sc_keys = 0; // shortcut table after the skips: FWD4_SC_BUCKETS x 2 (key, entry); keys placed
 	uint64_t gen = 0; // fib6 generation it holds
 	bool up = false;
 
@@ -1636,7 +1636,7 @@ extern "C" int gr_hip_fib6_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 		if (b.d6 == nullptr) { // sized for the VRF's group capacity once: top, groups, skips
 			const uint32_t cap = gr_fib6_max_groups(v.rib6);
 			HCK(hipMalloc(&b.d6, ((size_t)GR_FIB6_TOP + (size_t)cap * GR_FIB6_GROUP) * sizeof(uint32_t)
-						     + (size_t)cap * sizeof(gr_fib6_skip) + FWD4_SC_SLOTS * 8));
+						     + (size_t)cap * sizeof(gr_fib6_skip) + FWD4_SC_BUCKETS * 16));
 			b.groups = cap;
 		}
 		stager st(c);
@@ -1648,24 +1648,24 @@ extern "C" int gr_hip_fib6_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 			memcpy(st.add(reinterpret_cast<gr_fib6_skip *>(b.d6 + GR_FIB6_TOP + (size_t)b.groups * GR_FIB6_GROUP),
 				      skips),
 			       gr_fib6_skips(v.rib6), (size_t)skips * sizeof(gr_fib6_skip));
-		// the busiest /32s' walk state past byte 3, open addressing at half load
-		uint32_t sk[FWD4_SC_SLOTS / 2], se[FWD4_SC_SLOTS / 2];
-		const int ns = gr_fib6_shortcuts(v.rib6, sk, se, FWD4_SC_SLOTS / 2);
+		// the busiest /32s' walk state past byte 3, two per hash bucket, busiest
+		// first (a key whose bucket is full is left to the trie)
+		uint32_t sk[2 * FWD4_SC_BUCKETS], se[2 * FWD4_SC_BUCKETS];
+		const int ns = gr_fib6_shortcuts(v.rib6, sk, se, 2 * FWD4_SC_BUCKETS);
 		if (ns < 0)
 			return ns;
-		uint32_t *img = st.add(sc_of(b), 2 * FWD4_SC_SLOTS);
-		memset(img, 0, FWD4_SC_SLOTS * 8);
-		b.sc_probes = 0;
+		uint32_t *img = st.add(sc_of(b), 4 * FWD4_SC_BUCKETS);
+		memset(img, 0, FWD4_SC_BUCKETS * 16);
+		b.sc_keys = 0;
 		for (int i = 0; i < ns; i++) {
-			uint32_t h = FWD4_SC_HASH(sk[i]), p = 1;
-			while (img[2 * h + 1] != 0) {
-				h = (h + 1) & (FWD4_SC_SLOTS - 1);
-				p++;
-			}
-			img[2 * h] = sk[i];
-			img[2 * h + 1] = se[i];
-			if (p > b.sc_probes)
-				b.sc_probes = p;
+			uint32_t *k = img + 4 * FWD4_SC_HASH(sk[i]);
+			if (k[1] != 0)
+				k += 2;
+			if (k[1] != 0)
+				continue;
+			k[0] = sk[i];
+			k[1] = se[i];
+			b.sc_keys++;
 		}
 		if (c->sc_vrf == 0 || c->vrfs[c->sc_vrf].rib6 == nullptr
 		    || gr_fib6_n_routes(v.rib6) >= gr_fib6_n_routes(c->vrfs[c->sc_vrf].rib6))
@@ -1875,11 +1875,11 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	if (c->v6_sc && c->v6_routes && c->sc_vrf != 0) {
 		const vrf_fib &v = c->vrfs[c->sc_vrf];
 		const fib6_buf &b = v.b6[v.sel6[g]];
-		if (v.rib6 != nullptr && b.up && b.sc_probes) {
+		if (v.rib6 != nullptr && b.up && b.sc_keys) {
 			A.sc = sc_of(b);
 			A.sc_top = b.d6;
-			A.sc_probes = b.sc_probes | (c->v6_sc == 2 ? 0x80000000u : 0);
-			sc = FWD4_SC_SLOTS / 2;
+			A.sc_keys = b.sc_keys | (c->v6_sc == 2 ? 0x80000000u : 0);
+			sc = FWD4_SC_BUCKETS;
 		}
 	}
 	int occ;
@@ -1901,7 +1901,7 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 		const gr_hip_ctx::occ_entry *e = &occ_of(n4 + n6 + sc);
 		if (e->occ[variant] <= 0 && sc) {
 			sc = 0;
-			A.sc_probes = 0;
+			A.sc_keys = 0;
 			e = &occ_of(n4 + n6);
 		}
 		if (e->occ[variant] <= 0 && n6) {
@@ -1987,11 +1987,11 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < 0 || value > 2)
 			return -EINVAL;
 		c->v6_sc = value;
-	} else if (strcmp(key, "v6_shortcut_probes") == 0) { // read: the longest probe run of VRF `value`'s table
+	} else if (strcmp(key, "v6_shortcuts") == 0) { // read: the keys in VRF `value`'s shortcut table
 		if (value <= 0 || (uint32_t)value >= c->max_ifaces || c->vrfs[value].rib6 == nullptr
 		    || !c->vrfs[value].uploaded6())
 			return -ENONET;
-		return (int)c->vrfs[value].b6[c->vrfs[value].pub6].sc_probes;
+		return (int)c->vrfs[value].b6[c->vrfs[value].pub6].sc_keys;
 	} else if (strcmp(key, "host_direct") == 0) {
 		c->host_direct = value != 0;
 	} else if (strcmp(key, "fib_format_of") == 0) { // read: the format VRF `value` is on the device in
