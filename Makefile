@@ -14,10 +14,10 @@ LIB_HOST = grout_amd/libgrout_host.so
 LIB_ORACLE = oracle/liboracle.so
 LIB_GRAPH = grout_amd/libgrout_graph.so
 GRAPH = grout_amd/graph
-GRAPH_SRC = $(GRAPH)/rte_graph_min.c $(GRAPH)/gr_datapath_min.c $(GRAPH)/gpu_fwd4_node.c $(GRAPH)/gpu_fwd4_cpu_nodes.c \
+GRAPH_SRC = $(GRAPH)/rte_graph_min.c $(GRAPH)/rte_rcu_min.c $(GRAPH)/gr_datapath_min.c $(GRAPH)/gpu_fwd4_node.c $(GRAPH)/gpu_fwd4_cpu_nodes.c \
 	$(GRAPH)/walk_harness.c \
 	$(GRAPH)/graph_selftest.c
-GRAPH_HDRS = $(GRAPH)/rte_graph_min.h $(GRAPH)/gr_datapath_min.h $(GRAPH)/gpu_fwd4_node.h include/grout_hip.h
+GRAPH_HDRS = $(GRAPH)/rte_graph_min.h $(GRAPH)/rte_rcu_min.h $(GRAPH)/gr_datapath_min.h $(GRAPH)/gpu_fwd4_node.h include/grout_hip.h
 HDRS = include/grout_hip.h $(CSRC)/fib6.h $(CSRC)/fwd4_kernel.h $(CSRC)/fwd4_dev.h $(CSRC)/fwd4_chain.h $(CSRC)/fib4.h
 
 all: $(LIB_HIP) $(LIB_HOST) $(LIB_ORACLE) $(LIB_GRAPH) tools/libnode_mt.so
@@ -26,11 +26,11 @@ $(BUILD)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(BUILD)/gr_hip.o: $(CSRC)/gr_hip.cpp $(HDRS)
+$(BUILD)/gr_hip.o: $(CSRC)/gr_hip.cpp $(CSRC)/gr_node_priv.h $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(BUILD)/gr_node.o: $(CSRC)/gr_node.cpp include/grout_hip.h
+$(BUILD)/gr_node.o: $(CSRC)/gr_node.cpp $(CSRC)/gr_node_priv.h include/grout_hip.h
 	@mkdir -p $(BUILD)
 	$(CXX) -O3 -march=x86-64-v3 -fPIC -Wall -Wextra -std=c++17 -c -o $@ $<
 
@@ -54,7 +54,7 @@ $(LIB_ORACLE): oracle/oracle.c oracle/oracle.h include/grout_hip.h
 # The fast path's grout node (C) on the rte_graph / grout stand-ins, with the
 # test harness graph; links the HIP library (found next to it at run time).
 $(LIB_GRAPH): $(GRAPH_SRC) $(GRAPH_HDRS) $(LIB_HIP)
-	$(CC) -std=gnu11 $(CFLAGS_HOST) -Iinclude -shared -o $@ $(GRAPH_SRC) -Lgrout_amd -lgrout_hip '-Wl,-rpath,$$ORIGIN'
+	$(CC) -std=gnu11 $(CFLAGS_HOST) -pthread -Iinclude -shared -o $@ $(GRAPH_SRC) -Lgrout_amd -lgrout_hip '-Wl,-rpath,$$ORIGIN'
 
 # measurement tool: the node walk from C threads (tools/node_pipeline.py --driver c)
 tools/libnode_mt.so: tools/node_mt.c include/grout_hip.h $(LIB_HIP)

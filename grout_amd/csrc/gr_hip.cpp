@@ -15,6 +15,7 @@
 #include "fib4.h"
 #include "fib6.h"
 #include "fwd4_kernel.h"
+#include "gr_node_priv.h"
 
 #include <algorithm>
 #include <atomic>
@@ -191,6 +192,9 @@ struct gr_hip_queue {
 	uint32_t nw_head, nw_count;
 	uint8_t *d_pad; // the zeroed line pad slots of a frames-by-address batch point at
 	uint32_t *h_err, *d_err; // kernel error word (pinned, mapped): a workgroup gave up
+	// per-iface counters of the node walks handed back (gr_hip_node_iface_stats),
+	// counted on the host where grout counts them
+	std::vector<gr_hip_iface_stats> node_if;
 };
 
 struct host_range { // gr_hip_host_register
@@ -232,6 +236,8 @@ struct gr_hip_ctx {
 	uint32_t *d_vlan_keys;
 	uint16_t *d_vlan_vals;
 	uint32_t vlan_cap;
+	std::vector<uint32_t> vlan_keys_h; // host image of the VLAN table (node hand-back counters)
+	std::vector<uint16_t> vlan_vals_h;
 	fwd4_edges edges;
 	fwd4_tables *d_tables[2]; // device copy of what every launch reads, by generation
 	std::vector<gr_hip_queue *> queues;
@@ -968,8 +974,11 @@ static int upload_vlans(gr_hip_ctx *c) {
 		r = h2d(c, c->d_vlan_vals, vals.data(), cap * sizeof(uint16_t));
 	if (r == 0)
 		r = ctl_sync(c); // the vectors go out of scope
-	if (r == 0)
+	if (r == 0) {
+		c->vlan_keys_h = std::move(keys);
+		c->vlan_vals_h = std::move(vals);
 		r = upload_tables(c);
+	}
 	return r;
 }
 
@@ -1766,6 +1775,11 @@ extern "C" int gr_hip_queue_create(gr_hip_ctx_t *c, void *stream, gr_hip_queue_t
 		(void)hipGetLastError();
 		q->d_stats = nullptr;
 	}
+	try {
+		q->node_if.assign(c->max_ifaces, gr_hip_iface_stats{0, 0, 0, 0});
+	} catch (...) {
+		return -ENOMEM; // (not reached in practice: a few tens of KiB)
+	}
 	c->queues.push_back(q);
 	*out = q;
 	return 0;
@@ -1777,11 +1791,27 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 	gr_hip_ctx *c = q->ctx;
 	hipSetDevice(c->dev);
 	hipStreamSynchronize(q->s);
-	for (host_slot &h : q->hs) {
-		if (h.s) {
+	for (host_slot &h : q->hs)
+		if (h.s)
 			hipStreamSynchronize(h.s);
-			hipStreamDestroy(h.s);
+	{
+		// unlink first: a commit running on another thread reaches the
+		// queue's stream and events through this list (quiesce(),
+		// retire_wait(), publish()), under the lock; after this, none can
+		std::lock_guard<std::shared_mutex> l(c->mu);
+		for (size_t i = 0; i < c->queues.size(); i++) {
+			if (c->queues[i] == q) {
+				c->queues.erase(c->queues.begin() + (long)i);
+				break;
+			}
 		}
+	}
+	// a commit may have made its control stream wait on q->retire / q->quiesce
+	// just before the unlink: let that wait resolve before the events go
+	hipStreamSynchronize(c->ctl);
+	for (host_slot &h : q->hs) {
+		if (h.s)
+			hipStreamDestroy(h.s);
 		hipFree(h.in);
 		hipFree(h.out);
 		hipFree(h.meta);
@@ -1807,15 +1837,6 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 	if (q->own_stream)
 		hipStreamDestroy(q->s);
 	(void)hipGetLastError();
-	{
-		std::lock_guard<std::shared_mutex> l(c->mu); // quiesce() and publish() walk the list
-		for (size_t i = 0; i < c->queues.size(); i++) {
-			if (c->queues[i] == q) {
-				c->queues.erase(c->queues.begin() + (long)i);
-				break;
-			}
-		}
-	}
 	delete q;
 	return 0;
 }
@@ -2469,9 +2490,24 @@ extern "C" int gr_hip_node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, ui
 	// nodes, the others are handed back as usual
 	const uint32_t unfinished = node_unfinished(w.m, w.n, w.pos.data(), w.v);
 	std::shared_lock<std::shared_mutex> lk(c->mu); // the hand-back reads the iface and nexthop mirrors
-	r = gr_hip_node_apply(w.m, w.n, w.burst, w.pos.data(), w.by_addr ? nullptr : w.out, GR_HIP_PREFIX, w.v,
-			      c->ifaces.data(), c->max_ifaces, c->nh.data(), (uint32_t)c->nh.size(), stats);
+	const gr_node_vlans vl = {c->vlan_keys_h.data(), c->vlan_vals_h.data(), (uint32_t)c->vlan_keys_h.size()};
+	r = gr_node_apply_ex(w.m, w.n, w.burst, w.pos.data(), w.by_addr ? nullptr : w.out, GR_HIP_PREFIX, w.v,
+			     c->ifaces.data(), c->max_ifaces, c->nh.data(), (uint32_t)c->nh.size(), stats, &vl,
+			     q->node_if.data(), (uint32_t)q->node_if.size());
 	return r < 0 ? r : (int)unfinished;
+}
+
+extern "C" int gr_hip_node_iface_stats(gr_hip_queue_t *q, struct gr_hip_iface_stats *st, uint32_t max, int reset) {
+	if (q == nullptr || (st == nullptr && max))
+		return -EINVAL;
+	const uint32_t m = max < q->node_if.size() ? max : (uint32_t)q->node_if.size();
+	if (m)
+		memcpy(st, q->node_if.data(), (size_t)m * sizeof(*st));
+	if (max > m)
+		memset(st + m, 0, (size_t)(max - m) * sizeof(*st));
+	if (reset)
+		std::fill(q->node_if.begin(), q->node_if.end(), gr_hip_iface_stats{0, 0, 0, 0});
+	return 0;
 }
 
 extern "C" int gr_hip_node_pending(gr_hip_queue_t *q, int *ready) {

@@ -29,7 +29,7 @@
 // sub-interface (iface_input.c:74-86), eth_output clears it
 // (eth_output.c:71), iface_output sets the egress VLAN's id
 // (iface_output.c:81-86).
-#include "../../include/grout_hip.h"
+#include "gr_node_priv.h"
 
 #include <errno.h>
 #include <stddef.h>
@@ -187,6 +187,32 @@ extern "C" int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, uint32
 	return 0;
 }
 
+// The VLAN sub-interface of (parent, vlan_id) in the host image of the
+// context's VLAN table (0: none), vlan_get_iface (iface_input.c:76).
+static inline uint16_t vlan_sub(const struct gr_node_vlans *vl, uint16_t parent, uint16_t vlan_id) {
+	if (vl == nullptr || vl->cap == 0)
+		return 0;
+	const uint32_t key = (((uint32_t)parent << 16) | vlan_id) + 1;
+	for (uint32_t h = (key * 0x9e3779b1u) & (vl->cap - 1);; h = (h + 1) & (vl->cap - 1)) {
+		if (vl->keys[h] == key)
+			return vl->vals[h];
+		if (vl->keys[h] == 0)
+			return 0;
+	}
+}
+
+static inline void count(struct gr_hip_iface_stats *st, uint32_t n_st, uint32_t id, bool tx, uint32_t len) {
+	if (id == 0 || id >= n_st)
+		return;
+	if (tx) {
+		st[id].tx_packets++;
+		st[id].tx_bytes += len;
+	} else {
+		st[id].rx_packets++;
+		st[id].rx_bytes += len;
+	}
+}
+
 extern "C" int gr_hip_node_apply(
 	struct gr_hip_mbuf *m,
 	uint32_t n,
@@ -200,6 +226,27 @@ extern "C" int gr_hip_node_apply(
 	const struct gr_hip_nh *nh,
 	uint32_t n_nh,
 	struct gr_hip_node_stats *stats
+) {
+	return gr_node_apply_ex(m, n, burst, pos, lines, line_stride, verdicts, ifaces, n_ifaces, nh, n_nh, stats,
+				nullptr, nullptr, 0);
+}
+
+extern "C" int gr_node_apply_ex(
+	struct gr_hip_mbuf *m,
+	uint32_t n,
+	uint32_t burst,
+	const uint32_t *pos,
+	const void *lines,
+	uint32_t line_stride,
+	const struct gr_hip_verdict *verdicts,
+	const struct gr_hip_iface *ifaces,
+	uint32_t n_ifaces,
+	const struct gr_hip_nh *nh,
+	uint32_t n_nh,
+	struct gr_hip_node_stats *stats,
+	const struct gr_node_vlans *vlans,
+	struct gr_hip_iface_stats *ifst,
+	uint32_t n_ifst
 ) {
 	if (n == 0)
 		return 0;
@@ -234,6 +281,8 @@ extern "C" int gr_hip_node_apply(
 		struct gr_hip_mbuf &b = m[i];
 		const uint32_t at = pos != nullptr ? pos[i] : i;
 		const struct gr_hip_verdict &v = verdicts[at];
+		const uint32_t len0 = b.pkt_len; // as iface_input / iface_output count it
+		const uint16_t iface0 = b.iface, vlan0 = b.vlan_id; // as port_rx left them
 		// lines NULL: the GPU rewrote the frames in place already
 		const uint8_t *line = L != nullptr ? L + (size_t)at * line_stride : static_cast<const uint8_t *>(b.frame);
 		const bool ip6 = line[12] == 0x86 && line[13] == 0xdd; // RTE_ETHER_TYPE_IPV6
@@ -283,6 +332,25 @@ extern "C" int gr_hip_node_apply(
 						vid = ifaces[oif].vlan_id;
 				}
 				b.vlan_id = vid;
+			}
+			// per-iface counters where grout counts them (rxtx.h:84-117):
+			// iface_input past its admin-down and unknown-VLAN drops
+			// (iface_input.c:93-95), iface_output past its no-parent and
+			// admin-down drops (iface_output.c:103-105)
+			if (ifst != nullptr) {
+				if (v.edge != GR_HIP_E_IFACE_INPUT_ADMIN_DOWN && v.edge != GR_HIP_E_IFACE_INPUT_UNKNOWN_VLAN) {
+					const uint16_t self = demuxed ? vlan_sub(vlans, iface0, vlan0) : b.iface;
+					count(ifst, n_ifst, self, false, len0);
+					if (demuxed)
+						count(ifst, n_ifst, iface0, false, len0);
+				}
+				if (depth == 6 && v.edge != GR_HIP_E_IFACE_OUTPUT_ADMIN_DOWN
+				    && v.edge != GR_HIP_E_IFACE_OUTPUT_VLAN_NO_PARENT && v.nh && v.nh < n_nh && nh != nullptr) {
+					const uint16_t oif = nh[v.nh].iface_id;
+					count(ifst, n_ifst, oif, true, len0);
+					if (v.iface != oif)
+						count(ifst, n_ifst, v.iface, true, len0);
+				}
 			}
 			b.iface = v.iface;
 			b.domain = v.domain;

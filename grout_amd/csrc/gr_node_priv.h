@@ -1,0 +1,43 @@
+// SPDX-License-Identifier: BSD-3-Clause
+//
+// gr_node_priv.h -- what gr_hip.cpp and gr_node.cpp share beyond the C ABI:
+// the node hand-back with the context's VLAN table and per-iface counters.
+#pragma once
+
+#include "../../include/grout_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+// Host image of the context's VLAN sub-interface table (open addressing,
+// key ((parent << 16) | vlan_id) + 1, 0 = empty), the one the kernel probes.
+struct gr_node_vlans {
+	const uint32_t *keys;
+	const uint16_t *vals;
+	uint32_t cap; // power of two, or 0
+};
+
+// gr_hip_node_apply, also adding each packet's rx / tx to ifst[iface id]
+// (n_ifst entries) where grout's iface_input / iface_output count them.
+int gr_node_apply_ex(
+	struct gr_hip_mbuf *m,
+	uint32_t n,
+	uint32_t burst,
+	const uint32_t *pos,
+	const void *lines,
+	uint32_t line_stride,
+	const struct gr_hip_verdict *verdicts,
+	const struct gr_hip_iface *ifaces,
+	uint32_t n_ifaces,
+	const struct gr_hip_nh *nh,
+	uint32_t n_nh,
+	struct gr_hip_node_stats *stats,
+	const struct gr_node_vlans *vlans,
+	struct gr_hip_iface_stats *ifst,
+	uint32_t n_ifst
+);
+
+#ifdef __cplusplus
+}
+#endif

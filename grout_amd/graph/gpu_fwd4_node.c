@@ -28,6 +28,26 @@
 // max_delay when no new burst arrives (rte_graph calls a node only when it
 // holds objects).
 //
+// RCU. A batch's mbufs stay with the node across graph walks (accumulation,
+// then the GPU), and grout's worker reports a QSBR quiescent state every 256
+// walks whatever the node holds (main_loop.c:461-464). So each batch holds a
+// QSBR reader of its own: one of the graph's GPU_FWD4_RCU_PER_GRAPH reader
+// ids goes online when the batch takes its first mbuf (before the GPU reads
+// any mirror for it) and offline at the start of the graph walk after the
+// one that handed the batch back, once grout's nodes behind the edges have
+// processed it. rte_rcu_qsbr_synchronize() in grout's control plane
+// (nexthop_destroy, nexthop.c:505; iface_destroy, iface.c:712) therefore
+// returns only after every batch that may name the object it frees is
+// handed back. The hand-back turns the verdict's iface id and nexthop slot
+// into pointers through the node's own registries (gpu_fwd4_iface_obj_set /
+// _nh_obj_set), which the control plane clears only after that
+// synchronisation, never through grout's iface_from_id, which is cleared
+// before it.
+//
+// Stream limits. rte_graph holds a node's input stream in uint16_t-sized
+// arrays; the node therefore hands at most one batch back per process() call
+// and batches are at most GPU_FWD4_BATCH_MAX packets.
+//
 // Built here against the rte_graph / grout stand-ins (rte_graph_min.h,
 // gr_datapath_min.h); in grout it includes <gr_graph.h>, <gr_mbuf.h>,
 // <gr_module.h> and the DPDK headers instead, with no other change.
@@ -44,7 +64,7 @@ static struct gpu_fwd4_conf conf = {
 	.n_devs = 0, // every visible device
 	.max_ifaces = 1024,
 	.max_nexthops = 1u << 17,
-	.batch = 1u << 16,
+	.batch = GPU_FWD4_BATCH_MAX,
 	.rx_burst = 64,
 	.max_delay_ns = 50000,
 	.depth = 2,
@@ -56,6 +76,7 @@ static struct {
 	int dev;
 	int numa; // the device's NUMA node
 	uint32_t graphs; // worker graphs bound to it
+	int diverged; // a control call failed here only: its graphs punt (FANOUT)
 } gpus[GPU_FWD4_MAX_DEVS];
 static uint32_t n_gpus;
 
@@ -66,7 +87,14 @@ int gpu_fwd4_configure(const struct gpu_fwd4_conf *c) {
 	conf = *c;
 	if (conf.depth == 0)
 		conf.depth = GR_HIP_NODE_DEPTH;
+	if (conf.batch > GPU_FWD4_BATCH_MAX)
+		conf.batch = GPU_FWD4_BATCH_MAX;
 	return 0;
+}
+
+void gpu_fwd4_conf_get(struct gpu_fwd4_conf *c) {
+	if (c != NULL)
+		*c = conf;
 }
 
 int gpu_fwd4_set_depth(uint32_t depth) {
@@ -74,6 +102,57 @@ int gpu_fwd4_set_depth(uint32_t depth) {
 		return -EINVAL;
 	conf.depth = depth; // a graph's next flush switches (finishing what is in flight first)
 	return 0;
+}
+
+int gpu_fwd4_set_batch(uint32_t batch, uint64_t max_delay_ns) {
+	if (batch == 0)
+		return -EINVAL;
+	conf.batch = batch > GPU_FWD4_BATCH_MAX ? GPU_FWD4_BATCH_MAX : batch;
+	conf.max_delay_ns = max_delay_ns;
+	return 0;
+}
+
+// ---- the grout objects verdicts name (see "RCU" above) ---------------------
+static const struct iface **if_obj;
+static uint32_t if_obj_n;
+static const struct nexthop **nh_obj;
+static uint32_t nh_obj_n;
+
+static int obj_table(const void ***t, uint32_t *n, uint32_t want) {
+	if (*t == NULL) {
+		if ((*t = calloc(want, sizeof(void *))) == NULL)
+			return -ENOMEM;
+		*n = want;
+	}
+	return 0;
+}
+
+int gpu_fwd4_iface_obj_set(uint16_t id, const struct iface *i) {
+	int r = obj_table((const void ***)&if_obj, &if_obj_n, conf.max_ifaces);
+	if (r < 0)
+		return r;
+	if (id == 0 || id >= if_obj_n)
+		return -EINVAL;
+	__atomic_store_n(&if_obj[id], i, __ATOMIC_RELEASE);
+	return 0;
+}
+
+int gpu_fwd4_nh_obj_set(uint32_t slot, const struct nexthop *nh) {
+	int r = obj_table((const void ***)&nh_obj, &nh_obj_n, conf.max_nexthops + 1);
+	if (r < 0)
+		return r;
+	if (slot == 0 || slot >= nh_obj_n)
+		return -EINVAL;
+	__atomic_store_n(&nh_obj[slot], nh, __ATOMIC_RELEASE);
+	return 0;
+}
+
+const struct iface *gpu_fwd4_iface_obj(uint16_t id) {
+	return id < if_obj_n ? __atomic_load_n(&if_obj[id], __ATOMIC_ACQUIRE) : NULL;
+}
+
+const struct nexthop *gpu_fwd4_nh_obj(uint32_t slot) {
+	return slot < nh_obj_n ? __atomic_load_n(&nh_obj[slot], __ATOMIC_ACQUIRE) : NULL;
 }
 
 gr_hip_ctx_t *gpu_fwd4_hip_ctx(void) {
@@ -122,12 +201,20 @@ static void gpu_init(struct event_base *ev) {
 
 static void gpu_fini(struct event_base *ev) {
 	(void)ev;
-	while (n_gpus > 0)
+	while (n_gpus > 0) {
 		gr_hip_fini(gpus[--n_gpus].ctx);
+		gpus[n_gpus].diverged = 0;
+	}
+	free(if_obj);
+	free(nh_obj);
+	if_obj = NULL;
+	nh_obj = NULL;
+	if_obj_n = nh_obj_n = 0;
 }
 
 static struct module gpu_module = {
 	.name = "gpu_fwd4",
+	.depends_on = "rcu", // the graphs' QSBR readers (main_loop.c:538-552)
 	.init = gpu_init,
 	.fini = gpu_fini,
 };
@@ -154,8 +241,11 @@ static int pick_gpu(const struct rte_graph *graph) {
 }
 
 // ---- per-graph walk state ----------------------------------------------------
+enum { RD_FREE = 0, RD_HELD, RD_RELEASE };
+
 struct gpu_walk {
 	const struct rte_graph *graph;
+	int slot; // index in walks[]: its QSBR reader ids
 	int gpu; // index in gpus[]
 	gr_hip_queue_t *q;
 	uint32_t n, cap; // the batch accumulating, in buffer `cur`
@@ -166,8 +256,16 @@ struct gpu_walk {
 	int pending; // the other buffer's batch is on the GPU (gr_hip_node_start'ed)
 	uint32_t pend_n; // its size
 	uint64_t pend_ns; // when it was sent
+	// QSBR readers (see "RCU" above): rd[k] is the reader buffer k's batch
+	// holds (-1: none), rstate the state of each of the graph's readers
+	int8_t rd[2];
+	uint8_t rstate[GPU_FWD4_RCU_PER_GRAPH];
 	struct gr_hip_node_stats stats;
+	struct gr_hip_node_stats flushed; // what gpu_fwd4_stats_flush reported already
+	uint32_t node_id[GR_HIP_NODE_COUNT]; // rte_graph ids of the replaced nodes
+	struct gr_hip_iface_stats *ifs; // gpu_fwd4_stats_flush's buffer [conf.max_ifaces]
 	uint64_t gpu_errors; // batches punted because the GPU call failed
+	uint64_t batches, max_batch, stale;
 };
 
 static uint64_t now_ns(void) {
@@ -196,11 +294,10 @@ void gpu_fwd4_prof(int on, uint64_t *out) {
 			prof.ns[k] += now_ns() - prof_t0__;                                        \
 	} while (0)
 
-#define MAX_WALKS 64
-static struct gpu_walk *walks[MAX_WALKS];
+static struct gpu_walk *walks[GPU_FWD4_MAX_GRAPHS];
 
 static struct gpu_walk *walk_of(const struct rte_graph *g) {
-	for (int i = 0; i < MAX_WALKS; i++)
+	for (int i = 0; i < GPU_FWD4_MAX_GRAPHS; i++)
 		if (walks[i] != NULL && walks[i]->graph == g)
 			return walks[i];
 	return NULL;
@@ -208,6 +305,52 @@ static struct gpu_walk *walk_of(const struct rte_graph *g) {
 
 GR_NODE_CTX_TYPE(gpu_fwd4_ctx, { struct gpu_walk *w; });
 
+// ---- RCU: one QSBR reader per batch, from its first mbuf to the walk after
+// its hand-back
+static int rcu_on = 1;
+
+void gpu_fwd4_rcu_readers(int on) {
+	rcu_on = on;
+}
+
+static unsigned reader_id(const struct gpu_walk *w, int r) {
+	return GPU_FWD4_RCU_BASE + (unsigned)w->slot * GPU_FWD4_RCU_PER_GRAPH + (unsigned)r;
+}
+
+// Buffer k's batch takes its first mbuf: a free reader goes online for it.
+static void reader_hold(struct gpu_walk *w, uint32_t k) {
+	if (w->rd[k] >= 0)
+		return;
+	for (int r = 0; r < GPU_FWD4_RCU_PER_GRAPH; r++) {
+		if (w->rstate[r] != RD_FREE)
+			continue;
+		w->rstate[r] = RD_HELD;
+		w->rd[k] = (int8_t)r;
+		if (rcu_on)
+			rte_rcu_qsbr_thread_online(gr_datapath_rcu(), reader_id(w, r));
+		return;
+	}
+	// not reached: two batches held + two released per walk at most
+}
+
+// Buffer k's batch was handed back: its reader goes offline at the next walk.
+static void reader_handed_back(struct gpu_walk *w, uint32_t k) {
+	if (w->rd[k] < 0)
+		return;
+	w->rstate[w->rd[k]] = RD_RELEASE;
+	w->rd[k] = -1;
+}
+
+// A graph walk starts (the flush source node runs first): the batches handed
+// back in earlier walks have been through grout's nodes behind the edges.
+static void readers_release(struct gpu_walk *w) {
+	for (int r = 0; r < GPU_FWD4_RCU_PER_GRAPH; r++) {
+		if (w->rstate[r] != RD_RELEASE)
+			continue;
+		w->rstate[r] = RD_FREE;
+		rte_rcu_qsbr_thread_offline(gr_datapath_rcu(), reader_id(w, r));
+	}
+}
 
 static uint8_t ck_status(uint64_t ol_flags) {
 	switch (ol_flags & RTE_MBUF_F_RX_IP_CKSUM_MASK) {
@@ -224,33 +367,44 @@ static uint8_t ck_status(uint64_t ol_flags) {
 // everywhere; iface_input's vlan_id before eth_input; eth_input's domain and
 // pre-resolved nexthop (NULL), then ip_input's / ip6_input's l3 nexthop over
 // them (l3.h:9 shares the bytes, ip_input.c:156); iface_output's vlan_id for
-// port_output / port_tx (iface_output.c:81-86, port_tx.c:84-118).
-static void hand_back(struct rte_mbuf *m, const struct gr_hip_mbuf *v) {
+// port_output / port_tx (iface_output.c:81-86, port_tx.c:84-118). Returns -1
+// when the iface or nexthop the verdict names is no longer registered (the
+// control plane broke the RCU contract above): the mbuf is then left as it is.
+static int hand_back(struct rte_mbuf *m, const struct gr_hip_mbuf *v) {
+	const struct iface *ifp = gpu_fwd4_iface_obj(v->iface);
+	if (ifp == NULL && v->iface != 0)
+		return -1;
+	const uint8_t *f = v->frame;
+	const int ip6 = f[12] == 0x86 && f[13] == 0xdd;
+	const int node = gr_hip_edge_node(v->edge, v->nh, ip6);
+	const struct nexthop *nh = NULL;
+	if (node != GR_HIP_NODE_IFACE_INPUT && node != GR_HIP_NODE_IFACE_OUTPUT && v->nh != 0
+	    && (nh = gpu_fwd4_nh_obj(v->nh)) == NULL)
+		return -1;
 	m->data_off = v->data_off; // frame bytes were rewritten in place
 	m->data_len = v->data_len;
 	m->pkt_len = v->pkt_len;
 	m->packet_type = v->packet_type;
-	const uint8_t *f = v->frame;
-	const int ip6 = f[12] == 0x86 && f[13] == 0xdd;
-	mbuf_data(m)->iface = iface_from_id(v->iface);
-	switch (gr_hip_edge_node(v->edge, v->nh, ip6)) {
+	mbuf_data(m)->iface = ifp;
+	switch (node) {
 	case GR_HIP_NODE_IFACE_INPUT:
 	case GR_HIP_NODE_IFACE_OUTPUT:
 		iface_mbuf_data(m)->vlan_id = v->vlan_id;
 		break;
 	case GR_HIP_NODE_ETH_OUTPUT:
 		if (v->nh)
-			l3_mbuf_data(m)->nh = gr_nexthop_from_slot(v->nh);
+			l3_mbuf_data(m)->nh = nh;
 		break;
 	default: {
 		struct eth_input_mbuf_data *e = eth_input_mbuf_data(m);
 		e->domain = (eth_domain_t)v->domain;
 		e->nh = NULL;
 		if (v->nh)
-			l3_mbuf_data(m)->nh = gr_nexthop_from_slot(v->nh);
+			l3_mbuf_data(m)->nh = nh;
 		break;
 	}
 	}
+	return 0;
 }
 
 // Enqueue batch buffer k (n mbufs) on the verdict edges; r: what the GPU call
@@ -267,13 +421,17 @@ static void deliver(struct rte_graph *graph, struct rte_node *node, struct gpu_w
 	if (r < 0) {
 		for (uint32_t i = 0; i < n; i++)
 			rte_node_enqueue_x1(graph, node, GR_HIP_E_PUNT, mb[i]);
-		return;
+	} else {
+		for (uint32_t i = 0; i < n; i++) {
+			rte_edge_t e = v[i].edge;
+			if (e != GR_HIP_E_PUNT && hand_back(mb[i], &v[i]) < 0) {
+				w->stale++;
+				e = GR_HIP_E_IP_OUTPUT_ERROR; // a drop node (ip_output.c:187)
+			}
+			rte_node_enqueue_x1(graph, node, e, mb[i]);
+		}
 	}
-	for (uint32_t i = 0; i < n; i++) {
-		if (v[i].edge != GR_HIP_E_PUNT)
-			hand_back(mb[i], &v[i]);
-		rte_node_enqueue_x1(graph, node, v[i].edge, mb[i]);
-	}
+	reader_handed_back(w, k);
 	PROF_ADD(GPU_FWD4_PROF_DELIVER);
 }
 
@@ -294,28 +452,44 @@ static uint32_t finish_pending(struct rte_graph *graph, struct rte_node *node, s
 	return n;
 }
 
-// Send the accumulated batch; returns the mbufs handed back meanwhile.
+static void started(struct gpu_walk *w, uint32_t n) {
+	w->batches++;
+	if (n > w->max_batch)
+		w->max_batch = n;
+}
+
+// Send the accumulated batch; returns the mbufs handed back meanwhile: one
+// batch at most (the accumulated one when synchronous, else the one before),
+// two only when the GPU refuses this one (both then go to grout's CPU nodes
+// and the walk's edges hold at most three batches: still under rte_graph's
+// stream limit).
 static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
 	if (w->n == 0)
 		return 0;
 	const uint32_t k = w->cur, n = w->n;
 	w->n = 0;
 	w->first_ns = 0;
-	if (conf.depth < 2) { // synchronous: finish what an earlier depth left, then this batch
+	if (gpus[w->gpu].diverged) { // not to this GPU: grout's CPU nodes, after the batch before
 		const uint32_t d = finish_pending(graph, node, w);
-		deliver(graph, node, w, k, n, gr_hip_node_process(w->q, w->v[k], n, conf.rx_burst, &w->stats));
+		deliver(graph, node, w, k, n, -ESTALE);
 		return d + n;
+	}
+	if (conf.depth < 2 && !w->pending) { // synchronous
+		started(w, n);
+		deliver(graph, node, w, k, n, gr_hip_node_process(w->q, w->v[k], n, conf.rx_burst, &w->stats));
+		return n;
 	}
 	// stage and send this batch while the previous one may still be on the
 	// GPU, then hand the previous one back: batches leave in arrival order
 	PROF_T0();
 	const int r = gr_hip_node_start(w->q, w->v[k], n, conf.rx_burst);
 	PROF_ADD(GPU_FWD4_PROF_START);
-	uint32_t delivered = finish_pending(graph, node, w);
-	if (r < 0) {
+	const uint32_t delivered = finish_pending(graph, node, w);
+	if (r < 0) { // the GPU did not take it: grout's CPU nodes do (after the one before, in order)
 		deliver(graph, node, w, k, n, r);
 		return delivered + n;
 	}
+	started(w, n);
 	w->pending = 1;
 	w->pend_n = n;
 	w->pend_ns = now_ns();
@@ -338,15 +512,26 @@ static uint32_t reap(struct rte_graph *graph, struct rte_node *node, struct gpu_
 static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node, void **objs, uint16_t nb_objs) {
 	struct gpu_walk *w = gpu_fwd4_ctx(node)->w;
 	PROF_T0();
+	if (gpus[w->gpu].diverged) { // this GPU's mirrors are out of step: grout's CPU nodes
+		if (w->n != 0)
+			flush(graph, node, w); // the packets held first (punted too)
+		else
+			reap(graph, node, w);
+		rte_node_enqueue(graph, node, GR_HIP_E_PUNT, objs, nb_objs);
+		return nb_objs;
+	}
 	uint8_t walk = GR_HIP_MBUF_F_WALK; // this call is one graph walk's iface_input stream
 	for (uint16_t i = 0; i < nb_objs; i++) {
 		struct rte_mbuf *m = objs[i];
-		if (m->nb_segs > 1 || gr_mbuf_is_traced(m)) { // grout's CPU nodes
+		// grout's CPU nodes: multi-segment or traced mbufs; and, never in
+		// practice (a batch starts below conf.batch and a call brings at
+		// most RTE_GRAPH_BURST_SIZE), a full buffer
+		if (m->nb_segs > 1 || gr_mbuf_is_traced(m) || w->n == w->cap) {
 			rte_node_enqueue_x1(graph, node, GR_HIP_E_PUNT, m);
 			continue;
 		}
-		if (w->n == w->cap)
-			flush(graph, node, w);
+		if (w->n == 0)
+			reader_hold(w, w->cur); // before the GPU reads any mirror for this batch
 		const struct iface_mbuf_data *d = iface_mbuf_data(m);
 		w->mbufs[w->cur][w->n] = m;
 		w->v[w->cur][w->n++] = (struct gr_hip_mbuf) {
@@ -378,20 +563,47 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 	return nb_objs;
 }
 
+static void walk_free(struct gpu_walk *w) {
+	for (int k = 0; k < 2; k++) {
+		free(w->mbufs[k]);
+		free(w->v[k]);
+	}
+	free(w->ifs);
+	free(w);
+}
+
+// rte_graph ids of the replaced nodes, by enum gr_hip_node
+static const char *const replaced_names[GR_HIP_NODE_COUNT] = {
+	[GR_HIP_NODE_IFACE_INPUT] = "iface_input",
+	[GR_HIP_NODE_ETH_INPUT] = "eth_input",
+	[GR_HIP_NODE_IP_INPUT] = "ip_input",
+	[GR_HIP_NODE_IP_FORWARD] = "ip_forward",
+	[GR_HIP_NODE_IP_OUTPUT] = "ip_output",
+	[GR_HIP_NODE_ETH_OUTPUT] = "eth_output",
+	[GR_HIP_NODE_IFACE_OUTPUT] = "iface_output",
+	[GR_HIP_NODE_IP6_INPUT] = "ip6_input",
+	[GR_HIP_NODE_IP6_FORWARD] = "ip6_forward",
+	[GR_HIP_NODE_IP6_OUTPUT] = "ip6_output",
+};
+
 static int gpu_fwd4_init(const struct rte_graph *graph, struct rte_node *node) {
 	if (n_gpus == 0)
 		return -ENODEV;
+	if (gr_datapath_rcu() == NULL)
+		return -ENODEV;
 	int slot = 0;
-	while (slot < MAX_WALKS && walks[slot] != NULL)
+	while (slot < GPU_FWD4_MAX_GRAPHS && walks[slot] != NULL)
 		slot++;
-	if (slot == MAX_WALKS)
+	if (slot == GPU_FWD4_MAX_GRAPHS)
 		return -ENOSPC;
 	struct gpu_walk *w = calloc(1, sizeof(*w));
 	if (w == NULL)
 		return -ENOMEM;
 	w->graph = graph;
+	w->slot = slot;
 	w->gpu = pick_gpu(graph);
-	w->cap = conf.batch + RTE_GRAPH_BURST_SIZE;
+	w->cap = GPU_FWD4_BATCH_MAX + RTE_GRAPH_BURST_SIZE; // any batch set_batch allows
+	w->rd[0] = w->rd[1] = -1;
 	int r = 0;
 	for (int k = 0; k < 2; k++) {
 		w->mbufs[k] = calloc(w->cap, sizeof(*w->mbufs[k]));
@@ -399,14 +611,18 @@ static int gpu_fwd4_init(const struct rte_graph *graph, struct rte_node *node) {
 		if (w->mbufs[k] == NULL || w->v[k] == NULL)
 			r = -ENOMEM;
 	}
+	if ((w->ifs = calloc(conf.max_ifaces, sizeof(*w->ifs))) == NULL)
+		r = -ENOMEM;
+	for (int k = 0; k < GR_HIP_NODE_COUNT; k++)
+		w->node_id[k] = rte_node_from_name(replaced_names[k]);
 	if (r == 0)
 		r = gr_hip_queue_create(gpus[w->gpu].ctx, NULL, &w->q);
+	for (int i = 0; r == 0 && i < GPU_FWD4_RCU_PER_GRAPH; i++)
+		r = rte_rcu_qsbr_thread_register(gr_datapath_rcu(), reader_id(w, i)); // offline until a batch holds it
 	if (r < 0) {
-		for (int k = 0; k < 2; k++) {
-			free(w->mbufs[k]);
-			free(w->v[k]);
-		}
-		free(w);
+		if (w->q != NULL)
+			gr_hip_queue_destroy(w->q);
+		walk_free(w);
 		return r;
 	}
 	gpus[w->gpu].graphs++;
@@ -417,24 +633,24 @@ static int gpu_fwd4_init(const struct rte_graph *graph, struct rte_node *node) {
 
 static void gpu_fwd4_fini(const struct rte_graph *graph, struct rte_node *node) {
 	(void)node;
-	for (int i = 0; i < MAX_WALKS; i++) {
+	for (int i = 0; i < GPU_FWD4_MAX_GRAPHS; i++) {
 		struct gpu_walk *w = walks[i];
 		if (w == NULL || w->graph != graph)
 			continue;
 		if (w->pending) // the GPU must be done with its buffers; the mbufs go back to their pool
 			gr_hip_node_finish(w->q, NULL, NULL, NULL);
 		if (w->pending)
-			for (uint32_t i = 0; i < w->pend_n; i++)
-				rte_pktmbuf_free(w->mbufs[w->cur ^ 1][i]);
+			for (uint32_t j = 0; j < w->pend_n; j++)
+				rte_pktmbuf_free(w->mbufs[w->cur ^ 1][j]);
+		for (uint32_t j = 0; j < w->n; j++) // held, never sent
+			rte_pktmbuf_free(w->mbufs[w->cur][j]);
 		gr_hip_queue_destroy(w->q);
+		for (int k = 0; k < GPU_FWD4_RCU_PER_GRAPH; k++) // offline, then gone
+			rte_rcu_qsbr_thread_unregister(gr_datapath_rcu(), reader_id(w, k));
 		if ((uint32_t)w->gpu < n_gpus && gpus[w->gpu].graphs > 0)
 			gpus[w->gpu].graphs--;
-		for (int k = 0; k < 2; k++) {
-			free(w->mbufs[k]);
-			free(w->v[k]);
-		}
-		free(w);
 		walks[i] = NULL;
+		walk_free(w);
 	}
 }
 
@@ -464,11 +680,17 @@ static uint16_t gpu_flush_process(struct rte_graph *graph, struct rte_node *node
 	if (c->w == NULL && (c->w = walk_of(graph)) == NULL)
 		return 0;
 	struct gpu_walk *w = c->w;
-	// same edges as iface_input, same order
-	uint32_t n = reap(graph, node, w);
+	// a new graph walk: what was handed back in the walks before has been
+	// through grout's nodes, those batches' QSBR readers go offline
+	readers_release(w);
+	// same edges as iface_input, same order; one batch handed back at most
+	// (flush() hands back the one still pending, and none is after these)
 	const uint64_t t = now_ns();
+	uint32_t n = 0;
 	if (w->pending && t - w->pend_ns >= conf.max_delay_ns)
-		n += finish_pending(graph, node, w); // waited long enough: wait for the GPU
+		n = finish_pending(graph, node, w); // waited long enough: wait for the GPU
+	else
+		n = reap(graph, node, w);
 	if (w->n != 0 && t - w->first_ns >= conf.max_delay_ns)
 		n += flush(graph, node, w); // pipelined: a later walk of the graph hands it back
 	return (uint16_t)(n > UINT16_MAX ? UINT16_MAX : n);
@@ -505,7 +727,52 @@ int gpu_fwd4_queue_stats(const struct rte_graph *graph, struct gr_hip_iface_stat
 	struct gpu_walk *w = walk_of(graph);
 	if (w == NULL)
 		return -ENOENT;
-	return gr_hip_queue_stats(w->q, stats, max_ifaces, reset);
+	return gr_hip_node_iface_stats(w->q, stats, max_ifaces, reset);
+}
+
+int gpu_fwd4_stats_flush(const struct rte_graph *graph, unsigned lcore_id, gpu_fwd4_node_stat_cb cb, void *cookie) {
+	struct gpu_walk *w = walk_of(graph);
+	if (w == NULL)
+		return -ENOENT;
+	uint64_t total = 0;
+	// iface_input is the node itself: rte_graph counts it
+	for (int k = GR_HIP_NODE_IFACE_INPUT + 1; k < GR_HIP_NODE_COUNT; k++) {
+		const uint64_t p = w->stats.packets[k] - w->flushed.packets[k];
+		const uint64_t c = w->stats.calls[k] - w->flushed.calls[k];
+		if ((p || c) && cb != NULL && w->node_id[k] != RTE_NODE_ID_INVALID)
+			cb(cookie, w->node_id[k], p, c);
+		total += p;
+	}
+	w->flushed = w->stats;
+	if (gr_hip_node_iface_stats(w->q, w->ifs, conf.max_ifaces, 1) == 0) {
+		for (uint32_t i = 1; i < conf.max_ifaces; i++) {
+			const struct gr_hip_iface_stats *d = &w->ifs[i];
+			if ((d->rx_packets | d->tx_packets) == 0)
+				continue;
+			struct iface_stats *st = iface_get_stats((uint16_t)lcore_id, (uint16_t)i);
+			st->rx_packets += d->rx_packets;
+			st->rx_bytes += d->rx_bytes;
+			st->tx_packets += d->tx_packets;
+			st->tx_bytes += d->tx_bytes;
+		}
+	}
+	return (int)(total > INT32_MAX ? INT32_MAX : total);
+}
+
+int gpu_fwd4_walk_info(const struct rte_graph *graph, struct gpu_fwd4_walk_info *info) {
+	struct gpu_walk *w = walk_of(graph);
+	if (w == NULL || info == NULL)
+		return -ENOENT;
+	memset(info, 0, sizeof(*info));
+	info->held = w->n;
+	info->in_flight = (uint32_t)w->pending;
+	info->batches = w->batches;
+	info->max_batch = w->max_batch;
+	info->stale = w->stale;
+	for (int r = 0; r < GPU_FWD4_RCU_PER_GRAPH; r++)
+		info->readers_online += w->rstate[r] != RD_FREE;
+	info->diverged = gpus[w->gpu].diverged;
+	return 0;
 }
 
 int gpu_fwd4_graph_gpu(const struct rte_graph *graph) {
@@ -515,20 +782,45 @@ int gpu_fwd4_graph_gpu(const struct rte_graph *graph) {
 
 // ---- control plane: every change goes to every GPU's context ---------------
 // (grout's control thread calls these from its event handlers, INTEGRATION.md
-// §3; each context is updated under its own quiesce, so a GPU's in-flight
+// §4; each context is updated under its own quiesce, so a GPU's in-flight
 // walks see the old or the new state, never a mix.) The first error is
-// returned; the other contexts still get the change.
+// returned; the other contexts still get the change. A context where the
+// call failed while it succeeded elsewhere, or failed differently, is marked
+// diverged (see gpu_fwd4_node.h).
+static void mark_diverged(const int *rs) {
+	int ok = 0;
+	for (uint32_t i = 0; i < n_gpus; i++)
+		ok |= rs[i] >= 0;
+	for (uint32_t i = 0; i < n_gpus; i++)
+		if (rs[i] < 0 && (ok || rs[i] != rs[0]))
+			__atomic_store_n(&gpus[i].diverged, 1, __ATOMIC_RELEASE);
+}
+
 #define FANOUT(call)                                                                               \
 	do {                                                                                       \
 		int ret__ = n_gpus ? 0 : -ENODEV;                                                  \
+		int rs__[GPU_FWD4_MAX_DEVS];                                                       \
 		for (uint32_t i = 0; i < n_gpus; i++) {                                            \
 			gr_hip_ctx_t *ctx = gpus[i].ctx;                                           \
-			const int r__ = (call);                                                    \
-			if (r__ < 0 && ret__ == 0)                                                 \
-				ret__ = r__;                                                       \
+			rs__[i] = (call);                                                          \
+			if (rs__[i] < 0 && ret__ == 0)                                             \
+				ret__ = rs__[i];                                                   \
 		}                                                                                  \
+		if (ret__ < 0)                                                                     \
+			mark_diverged(rs__);                                                       \
 		return ret__;                                                                      \
 	} while (0)
+
+int gpu_fwd4_diverged(uint32_t i) {
+	return i < n_gpus ? __atomic_load_n(&gpus[i].diverged, __ATOMIC_ACQUIRE) : -ENOENT;
+}
+
+int gpu_fwd4_resync(uint32_t i) {
+	if (i >= n_gpus)
+		return -ENOENT;
+	__atomic_store_n(&gpus[i].diverged, 0, __ATOMIC_RELEASE);
+	return 0;
+}
 
 int gpu_fwd4_iface_set(const struct gr_hip_iface *ifaces, uint32_t n) {
 	FANOUT(gr_hip_iface_set(ctx, ifaces, n));

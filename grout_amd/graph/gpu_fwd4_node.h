@@ -13,6 +13,8 @@ extern "C" {
 #endif
 
 struct rte_graph;
+struct iface;
+struct nexthop;
 
 // next_nodes in enum gr_hip_edge order (include/grout_hip.h)
 #define GPU_FWD4_EDGES                                                                             \
@@ -70,22 +72,47 @@ struct rte_graph;
 
 
 #define GPU_FWD4_MAX_DEVS 16
+#define GPU_FWD4_MAX_GRAPHS 64 // worker graphs (one per worker, worker.c)
+
+// Largest batch a graph accumulates. The node hands at most one batch back
+// per process() call (the node's, and its flush source node's), so one graph
+// walk enqueues at most 2 x GPU_FWD4_BATCH_MAX mbufs plus a few bursts of
+// punts on any one edge: under rte_graph's limit of what a node stream can
+// hold (struct rte_node size / idx are uint16_t, DPDK
+// __rte_node_stream_alloc_size verifies the size), with room to spare.
+// Batches of 16k packets forward as fast as 64k ones.
+#define GPU_FWD4_BATCH_MAX 15360
+
+// QSBR readers of the node (see gpu_fwd4_node.c, "RCU"): each graph holds
+// GPU_FWD4_RCU_PER_GRAPH reader ids from GPU_FWD4_RCU_BASE on, above the
+// workers' lcore ids. grout's rcu module sizes its QSBR variable for
+// RTE_MAX_LCORE + GPU_FWD4_RCU_READERS threads
+// (integration/grout-gpu_fwd4-datapath.patch).
+#define GPU_FWD4_RCU_PER_GRAPH 4
+#define GPU_FWD4_RCU_READERS (GPU_FWD4_MAX_GRAPHS * GPU_FWD4_RCU_PER_GRAPH)
+#define GPU_FWD4_RCU_BASE RTE_MAX_LCORE
 
 struct gpu_fwd4_conf {
 	uint32_t n_devs; // GPUs the module opens, 0 = every visible device
 	int devs[GPU_FWD4_MAX_DEVS]; // their HIP ordinals (the same one twice: two contexts)
 	uint32_t max_ifaces; // gr_hip_init sizes (grout: gr_config)
 	uint32_t max_nexthops;
-	uint32_t batch; // packets accumulated before a GPU walk
+	uint32_t batch; // packets accumulated before a GPU walk (at most GPU_FWD4_BATCH_MAX)
 	uint32_t rx_burst; // port_rx burst size: a shorter burst flushes
 	uint64_t max_delay_ns; // a held packet never waits longer (flush node)
 	uint32_t depth; // batches in flight per graph: 1 = each waited for, 2 = pipelined (0: 2)
 };
 
-// Before module init (grout: from its configuration). 0 or -EINVAL.
+// Before module init (grout: from its configuration). A batch above
+// GPU_FWD4_BATCH_MAX is clamped to it. 0 or -EINVAL.
 int gpu_fwd4_configure(const struct gpu_fwd4_conf *);
+// The configuration in effect (batch clamped).
+void gpu_fwd4_conf_get(struct gpu_fwd4_conf *);
 // Batches in flight per graph (1 or 2), at any time. 0 or -EINVAL.
 int gpu_fwd4_set_depth(uint32_t depth);
+// Batch size and maximum hold time at any time (the next batch of each graph
+// takes them; the batch is clamped to GPU_FWD4_BATCH_MAX). 0 or -EINVAL.
+int gpu_fwd4_set_batch(uint32_t batch, uint64_t max_delay_ns);
 // Measurement: nanoseconds the node spent, per phase, since the last call
 // (then reset); on = 0 stops accumulating. out: GPU_FWD4_PROF_COUNT values.
 enum {
@@ -106,11 +133,64 @@ int gpu_fwd4_graph_gpu(const struct rte_graph *);
 // What rte_graph would have counted for the replaced nodes, and batches the
 // GPU refused (punted whole to grout's CPU nodes). 0 or -ENOENT.
 int gpu_fwd4_node_stats(const struct rte_graph *, struct gr_hip_node_stats *, uint64_t *gpu_errors);
-// The per-iface rx/tx counters of the graph's queue (gr_hip_queue_stats).
+// The per-iface rx/tx counters of the graph's hand-backs not yet folded into
+// grout's iface_stats by gpu_fwd4_stats_flush (gr_hip_node_iface_stats).
 int gpu_fwd4_queue_stats(const struct rte_graph *, struct gr_hip_iface_stats *, uint32_t max_ifaces, int reset);
+
+// grout's housekeeping tick (gr_datapath_loop, main_loop.c:461-475, with
+// integration/grout-gpu_fwd4-datapath.patch): fold what the fast path
+// counted for this worker's graph since the last tick into grout's own
+// statistics, so that `grcli stats` and `grcli interface stats` read as with
+// grout's CPU nodes:
+//   * per replaced node (eth_input, ip_input, ip_forward, ip_output,
+//     eth_output, iface_output, ip6_input, ip6_forward, ip6_output; the
+//     node itself runs as "iface_input" and rte_graph counts it):
+//     cb(cookie, node id, packets, calls) with what rte_graph would have
+//     counted (process() returns, ip_output's rule; one call per graph walk
+//     reaching the node), which the patch adds into the worker's
+//     node_stats as node_stats_callback does (main_loop.c:40-66);
+//   * per iface: rx / tx packets and bytes added into
+//     iface_get_stats(lcore_id, iface) (iface.h:115-118), as
+//     IFACE_STATS_FLUSH does (rxtx.h:107-117).
+// Returns the packets reported to cb, or -ENOENT.
+typedef void (*gpu_fwd4_node_stat_cb)(void *cookie, uint32_t node_id, uint64_t packets, uint64_t calls);
+int gpu_fwd4_stats_flush(const struct rte_graph *, unsigned lcore_id, gpu_fwd4_node_stat_cb cb, void *cookie);
+
+// Per-graph walk state, for tests and measurements.
+struct gpu_fwd4_walk_info {
+	uint32_t held; // mbufs accumulating
+	uint32_t in_flight; // batches started and not handed back
+	uint64_t batches; // batches started
+	uint64_t max_batch; // largest batch started
+	uint64_t stale; // packets whose iface / nexthop was gone at hand-back (dropped)
+	uint32_t readers_online; // the graph's QSBR readers online
+	int diverged; // its GPU's mirrors are out of step: everything goes to grout's CPU nodes
+};
+int gpu_fwd4_walk_info(const struct rte_graph *, struct gpu_fwd4_walk_info *);
+// Tests only: 0 = the node takes no QSBR reader (round 2's behaviour, to
+// show the RCU test fails without them); 1 = default.
+void gpu_fwd4_rcu_readers(int on);
+
+// The grout objects a verdict names, by id / nexthop slot, as the node hands
+// packets back (iface in mbuf_data, l3_mbuf_data.nh). Set them from the
+// control plane's object events (GR_EVENT_IFACE_POST_ADD, NEXTHOP_NEW) and
+// clear them (NULL) only from the events grout pushes after its
+// rte_rcu_qsbr_synchronize (GR_EVENT_IFACE_REMOVE, iface.c:710-719;
+// GR_EVENT_NEXTHOP_DELETE, nexthop.c:505-514): grout itself clears
+// ifaces[id] before it synchronises, and a batch still on the GPU may name
+// the object. 0 or -EINVAL / -ENOMEM.
+int gpu_fwd4_iface_obj_set(uint16_t iface_id, const struct iface *);
+int gpu_fwd4_nh_obj_set(uint32_t slot, const struct nexthop *);
+const struct iface *gpu_fwd4_iface_obj(uint16_t iface_id);
+const struct nexthop *gpu_fwd4_nh_obj(uint32_t slot);
 
 // Control plane, replicated to every context: the gr_hip_* call of the same
 // name on each GPU. 0, or the first -errno (the others are still updated).
+// A context on which a call fails while it succeeds on another (or fails
+// differently) no longer holds the same state: it is marked diverged, and
+// the graphs bound to it hand every packet to grout's CPU nodes (PUNT)
+// until the control plane has replayed its state into that context and
+// calls gpu_fwd4_resync(i).
 int gpu_fwd4_iface_set(const struct gr_hip_iface *, uint32_t n);
 int gpu_fwd4_iface_del(uint16_t iface_id);
 int gpu_fwd4_nh_set(uint32_t first_slot, const struct gr_hip_nh *, uint32_t n);
@@ -129,6 +209,11 @@ int gpu_fwd4_edges_set(int table, uint16_t key, uint8_t edge); // table: GR_HIP_
 int gpu_fwd4_tune(const char *key, int value);
 int gpu_fwd4_host_register(void *ptr, size_t bytes); // grout: each mempool's memory
 int gpu_fwd4_host_unregister(void *ptr);
+// 1 if context i is diverged, 0 if not, -ENOENT.
+int gpu_fwd4_diverged(uint32_t i);
+// Context i holds the control plane's state again (replayed with the
+// gr_hip_* calls on gpu_fwd4_ctx_at(i)): its graphs use the GPU again.
+int gpu_fwd4_resync(uint32_t i);
 
 #ifdef __cplusplus
 }

@@ -4,6 +4,7 @@
 // node infos and their registration pass, parent attachment, the drop
 // node's process(), modules, and the iface / nexthop lookups.
 #include "gr_datapath_min.h"
+#include "gpu_fwd4_node.h"
 
 #include <errno.h>
 #include <stdio.h>
@@ -12,30 +13,67 @@
 struct node_infos node_infos = STAILQ_HEAD_INITIALIZER(node_infos);
 
 #define MAX_IFACES 1024
-#define MAX_SLOTS (1u << 17)
+
+// ---- lcores, RCU, iface counters -------------------------------------------
+static __thread unsigned lcore_of_thread;
+
+unsigned rte_lcore_id(void) {
+	return lcore_of_thread;
+}
+
+void gr_test_lcore_set(unsigned lcore_id) {
+	lcore_of_thread = lcore_id;
+}
+
+static struct iface_stats iface_stats_mem[MAX_IFACES][RTE_MAX_LCORE];
+struct iface_stats (*iface_stats)[RTE_MAX_LCORE] = iface_stats_mem;
+
+static struct rte_rcu_qsbr *rcu;
+
+struct rte_rcu_qsbr *gr_datapath_rcu(void) {
+	return rcu;
+}
+
+// grout's rcu module (main_loop.c:538-552) as the integration patch sizes
+// it: the workers' lcore ids, then the fast path node's readers.
+static void rcu_init(struct event_base *ev) {
+	(void)ev;
+	const uint32_t n = RTE_MAX_LCORE + GPU_FWD4_RCU_READERS;
+	rcu = aligned_alloc(64, (rte_rcu_qsbr_get_memsize(n) + 63) & ~(size_t)63);
+	if (rcu == NULL || rte_rcu_qsbr_init(rcu, n) < 0)
+		abort(); // grout: ABORT("rte_zmalloc(rcu)")
+}
+
+static void rcu_fini(struct event_base *ev) {
+	(void)ev;
+	free(rcu);
+	rcu = NULL;
+}
+
+static struct module rcu_module = {
+	.name = "rcu",
+	.init = rcu_init,
+	.fini = rcu_fini,
+};
+
+RTE_INIT(rcu_module_init) {
+	module_register(&rcu_module);
+}
 
 static const struct iface *ifaces[MAX_IFACES];
-static const struct nexthop **nexthops;
 
 const struct iface *iface_from_id(uint16_t id) {
-	return id < MAX_IFACES ? ifaces[id] : NULL;
+	return id < MAX_IFACES ? __atomic_load_n(&ifaces[id], __ATOMIC_ACQUIRE) : NULL;
 }
 
 void gr_iface_register(struct iface *i) {
 	if (i != NULL && i->id < MAX_IFACES)
-		ifaces[i->id] = i;
+		__atomic_store_n(&ifaces[i->id], i, __ATOMIC_RELEASE);
 }
 
-const struct nexthop *gr_nexthop_from_slot(uint32_t slot) {
-	return (slot < MAX_SLOTS && nexthops != NULL) ? nexthops[slot] : NULL;
-}
-
-void gr_nexthop_register(struct nexthop *nh) {
-	if (nh == NULL || nh->slot >= MAX_SLOTS)
-		return;
-	if (nexthops == NULL && (nexthops = calloc(MAX_SLOTS, sizeof(*nexthops))) == NULL)
-		return;
-	nexthops[nh->slot] = nh;
+void gr_iface_unregister(uint16_t id) {
+	if (id < MAX_IFACES)
+		__atomic_store_n(&ifaces[id], NULL, __ATOMIC_RELEASE);
 }
 
 rte_edge_t gr_node_attach_parent(const char *parent, const char *node) {

@@ -20,6 +20,7 @@
 #pragma once
 
 #include "rte_graph_min.h"
+#include "rte_rcu_min.h"
 
 #include <grout_hip.h>
 #include <stdbool.h>
@@ -88,11 +89,43 @@ static inline const struct nexthop_info_l3 *nexthop_info_l3(const struct nexthop
 	return &nh->l3;
 }
 
-// Registries the control plane fills (grout: iface.c / nexthop.c pools).
+// grout's iface registry (iface.c:459-466: ifaces[id], cleared by
+// iface_destroy before its RCU synchronisation, :710-712). The nexthop
+// objects the fast path names by slot are the node's own registry
+// (gpu_fwd4_nh_obj_set), not grout's.
 const struct iface *iface_from_id(uint16_t id);
 void gr_iface_register(struct iface *);
-const struct nexthop *gr_nexthop_from_slot(uint32_t slot);
-void gr_nexthop_register(struct nexthop *);
+void gr_iface_unregister(uint16_t id);
+
+// ---- lcores, RCU, per-lcore iface counters ---------------------------------
+#define RTE_MAX_LCORE 128
+// The calling thread's lcore id (DPDK rte_lcore_id()); the stand-in's threads
+// set theirs with gr_test_lcore_set (default 0).
+unsigned rte_lcore_id(void);
+void gr_test_lcore_set(unsigned lcore_id);
+
+// The datapath's QSBR variable (main_loop.c:534-536, created by the "rcu"
+// module, :538-543): every worker registers its lcore id as a reader
+// (:408); the fast path's node registers GPU_FWD4_RCU_READERS more
+// (gpu_fwd4_node.h, sized in by integration/grout-gpu_fwd4-datapath.patch).
+struct rte_rcu_qsbr *gr_datapath_rcu(void);
+
+// struct iface_stats and its per-lcore table (iface.h:105-119)
+struct iface_stats {
+	uint64_t rx_packets;
+	uint64_t rx_bytes;
+	uint64_t tx_packets;
+	uint64_t tx_bytes;
+	uint64_t cp_rx_packets;
+	uint64_t cp_rx_bytes;
+	uint64_t cp_tx_packets;
+	uint64_t cp_tx_bytes;
+} __attribute__((aligned(64)));
+
+extern struct iface_stats (*iface_stats)[RTE_MAX_LCORE];
+static inline struct iface_stats *iface_get_stats(uint16_t lcore_id, uint16_t ifid) {
+	return &iface_stats[ifid][lcore_id];
+}
 
 // ---- mbuf private data -----------------------------------------------------
 struct gr_trace_item;

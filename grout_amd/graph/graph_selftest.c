@@ -154,3 +154,68 @@ int gh_graph_selftest(void) {
 	CHECK(rte_graph_destroy(id) == 0 && rte_graph_lookup("st") == NULL);
 	return 0;
 }
+
+// ---- the QSBR stand-in (rte_rcu_min.c) -------------------------------------
+#include <pthread.h>
+#include <unistd.h>
+
+static struct rte_rcu_qsbr *rs_v;
+static volatile int rs_done;
+
+static void *rs_sync(void *arg) {
+	(void)arg;
+	rte_rcu_qsbr_synchronize(rs_v, RTE_QSBR_THRID_INVALID);
+	__atomic_store_n(&rs_done, 1, __ATOMIC_RELEASE);
+	return NULL;
+}
+
+int gh_rcu_selftest(void) {
+	const uint32_t n = 8;
+	rs_v = aligned_alloc(64, (rte_rcu_qsbr_get_memsize(n) + 63) & ~(size_t)63);
+	CHECK(rs_v != NULL && rte_rcu_qsbr_init(rs_v, n) == 0);
+	CHECK(rte_rcu_qsbr_thread_register(rs_v, n) < 0); // ids below max_threads
+	// registered readers start offline: nothing to wait for
+	CHECK(rte_rcu_qsbr_thread_register(rs_v, 1) == 0 && rte_rcu_qsbr_thread_register(rs_v, 2) == 0);
+	CHECK(rs_v->num_threads == 2);
+	uint64_t t = rte_rcu_qsbr_start(rs_v);
+	CHECK(rte_rcu_qsbr_check(rs_v, t, false) == 1);
+	// an online reader holds a writer until it reports quiescent after it started
+	rte_rcu_qsbr_thread_online(rs_v, 1);
+	t = rte_rcu_qsbr_start(rs_v);
+	CHECK(rte_rcu_qsbr_check(rs_v, t, false) == 0);
+	rte_rcu_qsbr_quiescent(rs_v, 1);
+	CHECK(rte_rcu_qsbr_check(rs_v, t, false) == 1);
+	// ... or goes offline
+	t = rte_rcu_qsbr_start(rs_v);
+	CHECK(rte_rcu_qsbr_check(rs_v, t, false) == 0);
+	rte_rcu_qsbr_thread_offline(rs_v, 1);
+	CHECK(rte_rcu_qsbr_check(rs_v, t, false) == 1);
+	// a reader coming online after the writer started holds nothing older
+	t = rte_rcu_qsbr_start(rs_v);
+	rte_rcu_qsbr_thread_online(rs_v, 2);
+	CHECK(rte_rcu_qsbr_check(rs_v, t, false) == 1);
+	// a reader that reported before the token is waited for
+	rte_rcu_qsbr_quiescent(rs_v, 2);
+	t = rte_rcu_qsbr_start(rs_v);
+	CHECK(rte_rcu_qsbr_check(rs_v, t, false) == 0);
+	// synchronize blocks until then, from another thread
+	rs_done = 0;
+	pthread_t th;
+	CHECK(pthread_create(&th, NULL, rs_sync, NULL) == 0);
+	usleep(20000);
+	const int early = __atomic_load_n(&rs_done, __ATOMIC_ACQUIRE);
+	rte_rcu_qsbr_quiescent(rs_v, 2);
+	pthread_join(th, NULL);
+	CHECK(early == 0 && rs_done == 1);
+	// unregistered readers are not waited for, even when they were online
+	t = rte_rcu_qsbr_start(rs_v);
+	CHECK(rte_rcu_qsbr_check(rs_v, t, false) == 0);
+	CHECK(rte_rcu_qsbr_thread_unregister(rs_v, 2) == 0 && rs_v->num_threads == 1);
+	CHECK(rte_rcu_qsbr_check(rs_v, t, false) == 1);
+	// synchronize from a reader reports its own quiescent state first
+	rte_rcu_qsbr_thread_online(rs_v, 1);
+	rte_rcu_qsbr_synchronize(rs_v, 1);
+	free(rs_v);
+	rs_v = NULL;
+	return 0;
+}

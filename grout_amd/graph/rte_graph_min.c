@@ -254,14 +254,19 @@ static void make_pending(struct rte_graph *g, struct rte_node *n) {
 	g->priv->pend_tail = (g->priv->pend_tail + 1) % g->priv->pend_cap;
 }
 
+// A node's stream holds at most UINT16_MAX objects (struct rte_node size /
+// idx are uint16_t; DPDK's __rte_node_stream_alloc_size grows the stream to
+// at most that and verifies it is not already there): more aborts.
 static int grow(struct rte_node *n, uint32_t need) {
 	if (need <= n->size)
 		return 0;
+	if (need > UINT16_MAX)
+		return -ENOSPC;
 	uint32_t sz = n->size;
 	while (sz < need)
 		sz *= 2;
 	if (sz > UINT16_MAX)
-		return -ENOSPC;
+		sz = UINT16_MAX;
 	void **o = realloc(n->objs, sz * sizeof(void *));
 	if (o == NULL)
 		return -ENOMEM;
@@ -282,6 +287,8 @@ static void enqueue(struct rte_graph *g, struct rte_node *node, rte_edge_t next,
 	}
 	memcpy(&to->objs[to->idx], objs, nb * sizeof(void *));
 	to->idx += nb;
+	if (to->idx > to->max_idx)
+		to->max_idx = to->idx;
 	make_pending(g, to);
 }
 

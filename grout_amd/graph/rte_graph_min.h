@@ -170,7 +170,8 @@ struct rte_node {
 	void **objs;
 	rte_node_process_t process;
 	struct rte_node **nodes; // [nb_edges]: next node instances by edge
-	uint64_t total_objs, total_calls, total_packets; // packets = process() returns
+	uint64_t total_objs, total_calls, total_packets; // packets = process() returns (DPDK's objs)
+	uint32_t max_idx; // most objects the node ever held (its stream's high-water mark)
 };
 
 struct rte_graph_param {

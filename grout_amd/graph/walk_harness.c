@@ -21,8 +21,11 @@
 #include "gr_datapath_min.h"
 
 #include <errno.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <time.h>
+#include <unistd.h>
 
 #define GH_PRIV 64
 #define GH_ROOM 2048
@@ -64,7 +67,15 @@ static struct {
 		rte_graph_t gid;
 		struct rte_graph *graph;
 		char name[RTE_GRAPH_NAMESIZE];
+		// the worker's node statistics as grout's housekeeping keeps them
+		// (struct worker_stats node_stats, main_loop.c:40-66), by node id,
+		// and the rte_graph counters already folded in
+		uint64_t *w_packets, *w_batches, *prev_packets, *prev_calls;
 	} graphs[GH_MAX_GRAPHS];
+	uint32_t loop; // walks since the last housekeeping tick (main_loop.c:461)
+	uint8_t *if_dead, *nh_dead; // objects the RCU test's control thread freed
+	uint32_t freed_reads; // grout nodes behind the edges read a freed object
+	uint32_t rec_ip_hold; // recorder id of ip_hold (reads l3_mbuf_data.nh, ip_hold.c:25)
 	int cur; // the graph gh_run / gh_results / stats use
 	char *recorders[GH_MAX_RECORDERS]; // recorder id -> node name
 	uint32_t n_recorders;
@@ -138,9 +149,20 @@ static uint16_t recorder_process(struct rte_graph *graph, struct rte_node *node,
 	for (uint16_t k = 0; k < nb; k++) {
 		const size_t off = (uint8_t *)objs[k] - H.mem;
 		const uint32_t i = (uint32_t)(off / GH_MBUF_SZ);
+		struct rte_mbuf *m = objs[k];
+		// what grout's node here would dereference: the iface everywhere,
+		// ip_hold's nexthop; neither may have been freed (RCU)
+		const struct iface *ifp = mbuf_data(m)->iface;
+		if (ifp != NULL && ifp >= H.ifaces && ifp < H.ifaces + H.max_ifaces && H.if_dead[ifp - H.ifaces])
+			__atomic_fetch_add(&H.freed_reads, 1, __ATOMIC_RELAXED);
+		if (id == H.rec_ip_hold) {
+			const struct nexthop *nh = l3_mbuf_data(m)->nh;
+			if (nh != NULL && nh >= H.nhs && nh <= H.nhs + H.max_nh && H.nh_dead[nh - H.nhs])
+				__atomic_fetch_add(&H.freed_reads, 1, __ATOMIC_RELAXED);
+		}
 		if (i < H.n) {
 			H.edge_of[i] = id;
-			H.seq_of[i] = H.recorded++;
+			__atomic_store_n(&H.seq_of[i], __atomic_fetch_add(&H.recorded, 1, __ATOMIC_ACQ_REL), __ATOMIC_RELAXED);
 		}
 	}
 	return nb;
@@ -177,6 +199,7 @@ static int add_recorder(const char *name) {
 // edge), then those behind the CPU continuation nodes.
 static int register_recorders(void) {
 	const char *roots[] = {"iface_input", "ip_input_local_ct", "ip_output_snat"};
+	H.rec_ip_hold = GR_HIP_E_IP_HOLD;
 	for (unsigned k = 0; k < sizeof(roots) / sizeof(roots[0]); k++) {
 		rte_node_t id = rte_node_from_name(roots[k]);
 		if (id == RTE_NODE_ID_INVALID)
@@ -242,20 +265,33 @@ int gh_init(const int *devs, uint32_t n_devs, uint32_t max_ifaces, uint32_t max_
 	H.max_nh = max_nh;
 	H.ifaces = calloc(max_ifaces, sizeof(*H.ifaces));
 	H.nhs = calloc((size_t)max_nh + 1, sizeof(*H.nhs));
-	if (H.ifaces == NULL || H.nhs == NULL)
+	H.if_dead = calloc(max_ifaces, 1);
+	H.nh_dead = calloc((size_t)max_nh + 1, 1);
+	if (H.ifaces == NULL || H.nhs == NULL || H.if_dead == NULL || H.nh_dead == NULL)
 		return -ENOMEM;
-	for (uint32_t i = 1; i < max_ifaces; i++) { // grout's iface / nexthop objects
-		H.ifaces[i].id = (uint16_t)i;
-		gr_iface_register(&H.ifaces[i]);
-	}
-	for (uint32_t s = 1; s <= max_nh; s++) {
-		H.nhs[s].slot = s;
-		gr_nexthop_register(&H.nhs[s]);
-	}
 	if ((r = gh_register()) < 0)
 		return r;
 	if ((r = gr_modules_init(NULL)) < 0)
 		return r;
+	// grout's iface / nexthop objects, in grout's iface table and in the
+	// node's registries (the control plane's object events)
+	for (uint32_t i = 1; i < max_ifaces; i++) {
+		H.ifaces[i].id = (uint16_t)i;
+		gr_iface_register(&H.ifaces[i]);
+		if ((r = gpu_fwd4_iface_obj_set((uint16_t)i, &H.ifaces[i])) < 0)
+			return r;
+	}
+	for (uint32_t s = 1; s <= max_nh; s++) {
+		H.nhs[s].slot = s;
+		if ((r = gpu_fwd4_nh_obj_set(s, &H.nhs[s])) < 0)
+			return r;
+	}
+	// this thread is the worker of every graph: lcore 0, a QSBR reader
+	// online from its first graph on (main_loop.c:408,441)
+	gr_test_lcore_set(0);
+	if (gr_datapath_rcu() == NULL || rte_rcu_qsbr_thread_register(gr_datapath_rcu(), 0) < 0)
+		return -ENODEV;
+	rte_rcu_qsbr_thread_online(gr_datapath_rcu(), 0);
 	H.inited = 1;
 	return gpu_fwd4_n_ctx() != 0 ? 0 : -ENODEV;
 }
@@ -340,8 +376,24 @@ int gh_graph_create(unsigned cpu, int socket) {
 	H.graphs[k].gid = gid;
 	H.graphs[k].graph = rte_graph_lookup(name);
 	snprintf(H.graphs[k].name, sizeof(H.graphs[k].name), "%s", name);
+	const size_t nn = rte_node_max_count() + 1;
+	H.graphs[k].w_packets = calloc(nn, sizeof(uint64_t));
+	H.graphs[k].w_batches = calloc(nn, sizeof(uint64_t));
+	H.graphs[k].prev_packets = calloc(nn, sizeof(uint64_t));
+	H.graphs[k].prev_calls = calloc(nn, sizeof(uint64_t));
+	if (H.graphs[k].w_packets == NULL || H.graphs[k].w_batches == NULL || H.graphs[k].prev_packets == NULL
+	    || H.graphs[k].prev_calls == NULL)
+		return -ENOMEM;
 	H.cur = k;
 	return k;
+}
+
+static void graph_stats_free(int k) {
+	free(H.graphs[k].w_packets);
+	free(H.graphs[k].w_batches);
+	free(H.graphs[k].prev_packets);
+	free(H.graphs[k].prev_calls);
+	H.graphs[k].w_packets = H.graphs[k].w_batches = H.graphs[k].prev_packets = H.graphs[k].prev_calls = NULL;
 }
 
 int gh_graph_use(int k) {
@@ -365,6 +417,7 @@ int gh_graph_destroy(void) {
 		return -ENOENT;
 	int r = rte_graph_destroy(H.graphs[H.cur].gid);
 	H.graphs[H.cur].graph = NULL;
+	graph_stats_free(H.cur);
 	H.cur = -1;
 	return r;
 }
@@ -411,18 +464,217 @@ int gh_load(const uint8_t *frames, uint32_t stride, const struct gr_hip_pkt_meta
 	return 0;
 }
 
+// grout's housekeeping tick for the current graph, as main_loop.c does it
+// every 256 walks (:461-475) with integration/grout-gpu_fwd4-datapath.patch:
+// the QSBR quiescent report, rte_graph's per-node counters folded into the
+// worker's node statistics (node_stats_callback, :40-66: packets = DPDK's
+// objs, the sum of process() returns; batches = calls), then the fast path's
+// counters for the nodes it replaced and for the ifaces.
+static void gpu_node_stat(void *cookie, uint32_t node_id, uint64_t packets, uint64_t calls) {
+	const int k = (int)(intptr_t)cookie;
+	H.graphs[k].w_packets[node_id] += packets;
+	H.graphs[k].w_batches[node_id] += calls;
+}
+
+static void housekeeping(int k) {
+	rte_rcu_qsbr_quiescent(gr_datapath_rcu(), rte_lcore_id());
+	const rte_node_t nn = rte_node_max_count();
+	for (rte_node_t id = 0; id < nn; id++) {
+		struct rte_node *n = rte_graph_node_get_by_name(H.graphs[k].name, rte_node_id_to_name(id));
+		if (n == NULL)
+			continue;
+		H.graphs[k].w_packets[id] += n->total_packets - H.graphs[k].prev_packets[id];
+		H.graphs[k].w_batches[id] += n->total_calls - H.graphs[k].prev_calls[id];
+		H.graphs[k].prev_packets[id] = n->total_packets;
+		H.graphs[k].prev_calls[id] = n->total_calls;
+	}
+	gpu_fwd4_stats_flush(H.graphs[k].graph, rte_lcore_id(), gpu_node_stat, (void *)(intptr_t)k);
+}
+
+static void walk_once(int k) {
+	rte_graph_walk(H.graphs[k].graph);
+	if (++H.loop == 256) { // HOUSEKEEPING_INTERVAL
+		H.loop = 0;
+		housekeeping(k);
+	}
+}
+
 // Walk the current graph until every injected mbuf reached a recorder, at
-// most max_walks times. Returns the number of walks, or -ETIMEDOUT.
+// most max_walks times, the way gr_datapath_loop does (housekeeping every
+// 256 walks), then one housekeeping tick so that the statistics are whole.
+// Returns the number of walks, or -ETIMEDOUT.
 int gh_run(uint32_t max_walks) {
 	struct rte_graph *g = cur_graph();
 	if (g == NULL)
 		return -ENOENT;
 	for (uint32_t w = 1; w <= max_walks; w++) {
-		rte_graph_walk(g);
-		if (H.recorded == H.n && H.next_rx == H.n)
+		walk_once(H.cur);
+		if (__atomic_load_n(&H.recorded, __ATOMIC_ACQUIRE) == H.n && H.next_rx == H.n) {
+			housekeeping(H.cur);
 			return (int)w;
+		}
 	}
 	return -ETIMEDOUT;
+}
+
+// The worker's node statistics of the current graph for node `name`, as
+// worker_dump_stats reports them (worker.c:502-560): out[0] packets,
+// out[1] batches.
+int gh_worker_stats(const char *name, uint64_t out[2]) {
+	if (H.cur < 0)
+		return -ENOENT;
+	const rte_node_t id = rte_node_from_name(name);
+	if (id == RTE_NODE_ID_INVALID || rte_graph_node_get_by_name(H.graphs[H.cur].name, name) == NULL)
+		return -ENOENT;
+	out[0] = H.graphs[H.cur].w_packets[id];
+	out[1] = H.graphs[H.cur].w_batches[id];
+	return 0;
+}
+
+// `grcli interface stats` for iface `id`: the per-lcore counters summed the
+// way iface_stats_get does (modules/infra/api/stats.c:197-222).
+int gh_iface_stats(uint16_t id, struct gr_hip_iface_stats *out) {
+	if (id >= H.max_ifaces || out == NULL)
+		return -EINVAL;
+	memset(out, 0, sizeof(*out));
+	for (int l = 0; l < RTE_MAX_LCORE; l++) {
+		const struct iface_stats *st = iface_get_stats((uint16_t)l, id);
+		out->rx_packets += st->rx_packets;
+		out->rx_bytes += st->rx_bytes;
+		out->tx_packets += st->tx_packets;
+		out->tx_bytes += st->tx_bytes;
+	}
+	return 0;
+}
+
+// Zero the grout-side statistics (iface_stats of every lcore, the current
+// graph's worker node statistics).
+void gh_stats_reset(void) {
+	for (uint32_t i = 0; i < H.max_ifaces; i++)
+		for (int l = 0; l < RTE_MAX_LCORE; l++)
+			memset(iface_get_stats((uint16_t)l, (uint16_t)i), 0, sizeof(struct iface_stats));
+	if (H.cur >= 0) {
+		const size_t nn = rte_node_max_count() + 1;
+		memset(H.graphs[H.cur].w_packets, 0, nn * sizeof(uint64_t));
+		memset(H.graphs[H.cur].w_batches, 0, nn * sizeof(uint64_t));
+	}
+}
+
+int gh_walk_info(struct gpu_fwd4_walk_info *info) {
+	struct rte_graph *g = cur_graph();
+	return g ? gpu_fwd4_walk_info(g, info) : -ENOENT;
+}
+
+// ---- RCU: grout deletes an object a batch on the GPU names -----------------
+struct gh_rcu_result {
+	uint32_t sync_before_handback; // synchronize had returned before the hand-back
+	uint32_t recorded_at_sync; // mbufs through grout's nodes when synchronize returned
+	uint32_t freed_reads; // grout's nodes read a freed object
+	uint32_t recorded;
+	uint64_t stale; // dropped by the node: the object was gone at hand-back
+	uint64_t sync_us; // synchronize's wait
+	uint32_t walks;
+	uint32_t sync_done;
+};
+
+static struct {
+	uint32_t slot;
+	uint16_t iface_id;
+	uint32_t done, recorded_at_sync;
+	uint64_t sync_us;
+} R;
+
+static uint64_t mono_us(void) {
+	struct timespec t;
+	clock_gettime(CLOCK_MONOTONIC, &t);
+	return (uint64_t)t.tv_sec * 1000000u + (uint64_t)t.tv_nsec / 1000u;
+}
+
+// The control thread: iface_destroy / nexthop_destroy as grout orders them
+// (iface.c:702-725, nexthop.c:493-518): the iface leaves grout's table, the
+// nexthop its id pool; rte_rcu_qsbr_synchronize; then the events that follow
+// it (GR_EVENT_IFACE_REMOVE / NEXTHOP_DELETE: the node's registries), and the
+// objects are freed (marked dead here).
+static void *rcu_control(void *arg) {
+	(void)arg;
+	if (R.iface_id)
+		gr_iface_unregister(R.iface_id);
+	const uint64_t t0 = mono_us();
+	rte_rcu_qsbr_synchronize(gr_datapath_rcu(), RTE_QSBR_THRID_INVALID);
+	R.sync_us = mono_us() - t0;
+	R.recorded_at_sync = __atomic_load_n(&H.recorded, __ATOMIC_ACQUIRE);
+	if (R.iface_id)
+		gpu_fwd4_iface_obj_set(R.iface_id, NULL);
+	if (R.slot)
+		gpu_fwd4_nh_obj_set(R.slot, NULL);
+	if (R.iface_id)
+		H.if_dead[R.iface_id] = 1;
+	if (R.slot)
+		H.nh_dead[R.slot] = 1;
+	__atomic_store_n(&R.done, 1, __ATOMIC_RELEASE);
+	return NULL;
+}
+
+// With the injected stream loaded (gh_load), walk until a batch is on the
+// GPU, then delete nexthop `slot` and iface `iface_id` (0: none) from a
+// control thread while the worker goes on: it reports quiescent, waits
+// hold_ms, then walks until every mbuf is through and the control thread
+// is done. Afterwards the objects are registered again.
+int gh_rcu_delete_test(uint32_t slot, uint16_t iface_id, uint32_t hold_ms, struct gh_rcu_result *res) {
+	if (H.cur < 0 || res == NULL || slot > H.max_nh || iface_id >= H.max_ifaces)
+		return -EINVAL;
+	memset(res, 0, sizeof(*res));
+	memset(&R, 0, sizeof(R));
+	R.slot = slot;
+	R.iface_id = iface_id;
+	H.freed_reads = 0;
+	struct gpu_fwd4_walk_info info;
+	struct gpu_fwd4_walk_info info0;
+	gpu_fwd4_walk_info(H.graphs[H.cur].graph, &info0);
+	uint32_t w = 0;
+	for (;;) { // until the stream's first batch is on the GPU
+		walk_once(H.cur);
+		w++;
+		gpu_fwd4_walk_info(H.graphs[H.cur].graph, &info);
+		if (info.in_flight && info.batches > info0.batches)
+			break;
+		if (H.recorded == H.n || w > 1000000)
+			return -EAGAIN;
+	}
+	pthread_t th;
+	if (pthread_create(&th, NULL, rcu_control, NULL) != 0)
+		return -EAGAIN;
+	rte_rcu_qsbr_quiescent(gr_datapath_rcu(), rte_lcore_id()); // the worker's housekeeping
+	usleep(hold_ms * 1000u);
+	res->sync_before_handback = __atomic_load_n(&R.done, __ATOMIC_ACQUIRE);
+	const uint64_t t_end = mono_us() + 5000000u;
+	while (mono_us() < t_end) {
+		walk_once(H.cur);
+		w++;
+		if (__atomic_load_n(&H.recorded, __ATOMIC_ACQUIRE) == H.n && __atomic_load_n(&R.done, __ATOMIC_ACQUIRE))
+			break;
+	}
+	housekeeping(H.cur);
+	pthread_join(th, NULL);
+	gpu_fwd4_walk_info(H.graphs[H.cur].graph, &info);
+	res->recorded_at_sync = R.recorded_at_sync;
+	res->freed_reads = H.freed_reads;
+	res->recorded = H.recorded;
+	res->stale = info.stale - info0.stale;
+	res->sync_us = R.sync_us;
+	res->walks = w;
+	res->sync_done = R.done;
+	// the objects come back for the next tests
+	if (iface_id) {
+		H.if_dead[iface_id] = 0;
+		gr_iface_register(&H.ifaces[iface_id]);
+		gpu_fwd4_iface_obj_set(iface_id, &H.ifaces[iface_id]);
+	}
+	if (slot) {
+		H.nh_dead[slot] = 0;
+		gpu_fwd4_nh_obj_set(slot, &H.nhs[slot]);
+	}
+	return 0;
 }
 
 // The private area is a union of the nodes' views: a pointer field may hold
@@ -485,14 +737,16 @@ int gh_queue_stats(struct gr_hip_iface_stats *stats, uint32_t max_ifaces, int re
 	return g ? gpu_fwd4_queue_stats(g, stats, max_ifaces, reset) : -ENOENT;
 }
 
-// rte_graph's own counters of a node of the current graph (objs, calls, packets).
-int gh_rte_node_counters(const char *node, uint64_t out[3]) {
+// rte_graph's own counters of a node of the current graph (objects handed
+// in, calls, process() returns, the stream's high-water mark).
+int gh_rte_node_counters(const char *node, uint64_t out[4]) {
 	struct rte_node *n = H.cur >= 0 ? rte_graph_node_get_by_name(H.graphs[H.cur].name, node) : NULL;
 	if (n == NULL)
 		return -ENOENT;
 	out[0] = n->total_objs;
 	out[1] = n->total_calls;
 	out[2] = n->total_packets;
+	out[3] = n->max_idx;
 	return 0;
 }
 
@@ -502,8 +756,11 @@ void gh_fini(void) {
 		if (H.graphs[k].graph != NULL) {
 			rte_graph_destroy(H.graphs[k].gid);
 			H.graphs[k].graph = NULL;
+			graph_stats_free(k);
 		}
 	}
+	if (gr_datapath_rcu() != NULL)
+		rte_rcu_qsbr_thread_unregister(gr_datapath_rcu(), 0);
 	H.cur = -1;
 	gr_modules_fini(NULL);
 	free(H.mem);

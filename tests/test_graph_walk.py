@@ -72,7 +72,63 @@ def lib():
         _lib.gpu_fwd4_set_depth.argtypes = [U32]
         _lib.gh_conn_add.argtypes = [P, P]
         _lib.gh_snat44_static_add.argtypes = [U16, U32, U32]
+        _lib.gh_worker_stats.argtypes = [ctypes.c_char_p, P]
+        _lib.gh_iface_stats.argtypes = [U16, P]
+        _lib.gh_walk_info.argtypes = [P]
+        _lib.gh_rcu_delete_test.argtypes = [U32, U16, U32, P]
+        _lib.gpu_fwd4_set_batch.argtypes = [U32, ctypes.c_uint64]
+        _lib.gpu_fwd4_diverged.argtypes = [U32]
+        _lib.gpu_fwd4_resync.argtypes = [U32]
+        _lib.gpu_fwd4_rcu_readers.argtypes = [ctypes.c_int]
+        _lib.gpu_fwd4_configure.argtypes = [P]
+        _lib.gpu_fwd4_conf_get.argtypes = [P]
+        _lib.gh_graph_selftest.restype = ctypes.c_int
+        _lib.gh_rcu_selftest.restype = ctypes.c_int
     return _lib
+
+
+WALK_INFO_DT = np.dtype([("held", "<u4"), ("in_flight", "<u4"), ("batches", "<u8"), ("max_batch", "<u8"),
+                         ("stale", "<u8"), ("readers_online", "<u4"), ("diverged", "<i4")])
+assert WALK_INFO_DT.itemsize == 40
+RCU_RES_DT = np.dtype([("sync_before_handback", "<u4"), ("recorded_at_sync", "<u4"), ("freed_reads", "<u4"),
+                       ("recorded", "<u4"), ("stale", "<u8"), ("sync_us", "<u8"), ("walks", "<u4"),
+                       ("sync_done", "<u4")])
+assert RCU_RES_DT.itemsize == 40
+CONF_DT = np.dtype([("n_devs", "<u4"), ("devs", "<i4", (16,)), ("max_ifaces", "<u4"), ("max_nexthops", "<u4"),
+                    ("batch", "<u4"), ("rx_burst", "<u4"), ("max_delay_ns", "<u8"), ("depth", "<u4")], align=True)
+assert CONF_DT.itemsize == 104
+BATCH_MAX = 15360  # GPU_FWD4_BATCH_MAX (gpu_fwd4_node.h)
+
+
+def walk_info():
+    w = np.zeros(1, dtype=WALK_INFO_DT)
+    assert lib().gh_walk_info(w.ctypes.data) == 0
+    return w[0]
+
+
+def node_counters(name):
+    """rte_graph's counters of a node of the current graph: objects in,
+    calls, process() returns, the stream's high-water mark."""
+    c = np.zeros(4, dtype=np.uint64)
+    assert lib().gh_rte_node_counters(name.encode(), c.ctypes.data) == 0
+    return c
+
+
+def grout_iface_stats(max_ifaces):
+    """`grcli interface stats` as grout computes it: every lcore's iface_stats
+    summed per iface (stats.c:197-222)."""
+    out = np.zeros(max_ifaces, dtype=abi.STATS_DT)
+    for i in range(max_ifaces):
+        assert lib().gh_iface_stats(i, out[i:i + 1].ctypes.data) == 0
+    return out
+
+
+def grout_node_stats(name):
+    """The worker's node statistics for `name` (packets, batches), as
+    worker_dump_stats reports them."""
+    c = np.zeros(2, dtype=np.uint64)
+    assert lib().gh_worker_stats(name.encode(), c.ctypes.data) == 0
+    return c
 
 
 def rec_name(i):
@@ -92,8 +148,37 @@ def edges_of(name):
 
 def test_runtime_semantics():
     """Registration, dynamic edges, graph creation from patterns (reachable
-    nodes join, dangling edges refused), walk order, stream move, counters."""
+    nodes join, dangling edges refused), walk order, stream move, counters,
+    the stream limit."""
     assert lib().gh_graph_selftest() == 0
+
+
+def test_rcu_qsbr_semantics():
+    """The QSBR stand-in (rte_rcu_min.c) as grout's control plane relies on it:
+    synchronize waits for every online registered reader to report quiescent
+    (or go offline) after it started, and not for offline or unregistered
+    ones; a reader that goes online after the token is not waited for."""
+    assert lib().gh_rcu_selftest() == 0
+
+
+def test_batch_clamped_to_stream_limit():
+    """A batch above GPU_FWD4_BATCH_MAX is clamped, so that the node never
+    hands rte_graph more than its uint16 streams hold (two batches per walk at
+    most, plus bursts of punts)."""
+    L = lib()
+    if L.gh_hip_ctx():
+        pytest.skip("module already initialised in this process")
+    c = np.zeros(1, dtype=CONF_DT)
+    c["max_ifaces"], c["max_nexthops"], c["batch"], c["rx_burst"] = 1024, 1 << 17, 1 << 16, 64
+    c["max_delay_ns"], c["depth"] = 50_000, 2
+    assert L.gpu_fwd4_configure(c.ctypes.data) == 0
+    got = np.zeros(1, dtype=CONF_DT)
+    L.gpu_fwd4_conf_get(got.ctypes.data)
+    assert got["batch"][0] == BATCH_MAX and 2 * BATCH_MAX + 4 * 256 < 0xFFFF
+    assert L.gpu_fwd4_set_batch(1 << 20, 1000) == 0
+    L.gpu_fwd4_conf_get(got.ctypes.data)
+    assert got["batch"][0] == BATCH_MAX and got["max_delay_ns"][0] == 1000
+    assert L.gpu_fwd4_set_batch(0, 1000) < 0
 
 
 def test_node_registration():
@@ -195,12 +280,14 @@ class FanOutPath:
 DEVS = (0, 0)  # two fast-path contexts on the one GPU of the box: two "GPUs"
 
 
-def graph_ctx(devs=DEVS):
+def graph_ctx(devs=DEVS, keep=False):
     """One node module (one fast-path context per entry of devs) and one
-    worker graph (cpu 0, socket 0) per process; graph 0 is the current one."""
+    worker graph (cpu 0, socket 0) per process; graph 0 is the current one
+    (keep: the current graph stays current)."""
     L = lib()
     if "fp" in _gh:
-        assert L.gh_graph_use(0) == 0
+        if not keep:
+            assert L.gh_graph_use(0) == 0
     else:
         d = (ctypes.c_int * len(devs))(*devs)
         r = L.gh_init(ctypes.cast(d, ctypes.c_void_p), len(devs), 1024, 1 << 17, BATCH, BURST, DELAY_NS)
@@ -243,10 +330,11 @@ def stage_of(edges, nh, ip6):
 
 
 def check_walk(topo, fr, me, labels=None):
-    fp = graph_ctx()
+    fp = graph_ctx(keep=True)  # on the current graph
     load(fp, topo)
     L = lib()
     L.gh_queue_stats(None, 0, 1)  # reset the queue's iface counters
+    L.gh_stats_reset()  # and grout's: iface_stats, the worker's node stats
     ns0 = np.zeros(1, dtype=abi.NODE_STATS_DT)
     assert L.gh_node_stats(ns0.ctypes.data, None) == 0
     o_lines, o_v, o_st, want, ns_want = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
@@ -288,13 +376,27 @@ def check_walk(topo, fr, me, labels=None):
     dn = {k: ns[k] - ns0[0][k] for k in ("packets", "calls")}
     assert np.array_equal(dn["packets"], ns_want["packets"]), (dn, ns_want)
     assert np.array_equal(dn["calls"], ns_want["calls"]), (dn, ns_want)
+    # what grout reports (row f2): the per-iface counters the node folded
+    # into grout's per-lcore iface_stats at the housekeeping ticks, summed the
+    # way `grcli interface stats` sums them ...
     qs = np.zeros(fp.max_ifaces, dtype=abi.STATS_DT)
-    assert L.gh_queue_stats(qs.ctypes.data, fp.max_ifaces, 1) == 0
-    assert np.array_equal(qs, o_st)
+    assert L.gh_queue_stats(qs.ctypes.data, fp.max_ifaces, 0) == 0
+    assert not qs["rx_packets"].any() and not qs["tx_packets"].any()  # all folded in
+    gs = grout_iface_stats(fp.max_ifaces)
+    bad = np.nonzero(gs != o_st)[0]
+    assert len(bad) == 0, [(int(i), gs[i], o_st[i]) for i in bad[:4]]
+    # ... and the worker's node statistics (`grcli stats`): the replaced nodes
+    # read as grout's own would, iface_input is the node itself
+    fed = {"eth_output"} if cont.any() else set()  # ip_output_snat feeds grout's eth_output too
+    for k, name in enumerate(abi.NODE_NAMES):
+        if name == "iface_input" or name in fed:
+            continue
+        w = grout_node_stats(name)
+        assert w[0] == ns_want["packets"][k] and w[1] == ns_want["calls"][k], (name, w, ns_want)
+    assert grout_node_stats("iface_input")[0] == len(me)
     # every packet reached the recorder of its edge, counted by rte_graph
     for e in np.unique(got["edge"]):
-        c = np.zeros(3, dtype=np.uint64)
-        assert L.gh_rte_node_counters(rec_name(e).encode(), c.ctypes.data) == 0
+        c = node_counters(rec_name(e))
         assert c[0] >= (got["edge"] == e).sum()
     return got
 
@@ -345,11 +447,9 @@ def test_graph_walk_flush_node(depth):
     t = T.config_single_route()
     n = BATCH + 2 * BURST
     fr, me = S.stream(n, 0xB0D, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
-    c0 = np.zeros(3, dtype=np.uint64)
-    assert lib().gh_rte_node_counters(b"gpu_fwd4_flush", c0.ctypes.data) == 0
+    c0 = node_counters("gpu_fwd4_flush")
     check_walk(t, fr, me)
-    c = np.zeros(3, dtype=np.uint64)
-    assert lib().gh_rte_node_counters(b"gpu_fwd4_flush", c.ctypes.data) == 0
+    c = node_counters("gpu_fwd4_flush")
     assert c[2] - c0[2] >= 2 * BURST  # the flush node handed those packets on
 
 
@@ -445,10 +545,134 @@ def test_graph_walk_cpu_continuations():
     assert (got["eth_type"][1::3] == 0x0008).all() and (got["vtep_af"][1::3] == 0).all()
     assert (got["iface"][1::3] == SC.P3).all() and (got["packet_type"][1::3] == abi.PTYPE_L3_IPV4).all()
     # ip_output's return rule: the SNAT node counted what it sent to eth_output
-    c = np.zeros(3, dtype=np.uint64)
-    assert L.gh_rte_node_counters(b"ip_output_snat", c.ctypes.data) == 0 and c[2] >= 3
+    c = node_counters("ip_output_snat")
+    assert c[2] >= 3
     # no conntrack entry, no rule: ip_input_local, eth_output with the source kept
     L.gh_policy_clear()
     got, lines, _, _ = walk(fr, me)
     assert [rec_name(e) for e in got["edge"]] == ["ip_input_local", "eth_output", "port_output"] * 3
     assert (lines[1::3] == o_lines[1::3]).all()
+
+
+# ---------------------------------------------------------------------------
+# GPU: the node against grout's RCU and rte_graph's stream limits
+# ---------------------------------------------------------------------------
+def _slot_of(topo, ipv4):
+    nh = topo.nh[1:topo.n_nh + 1]
+    return int(np.nonzero((nh["ipv4"] == T.ip4(ipv4)) & (nh["type"] == abi.NH_T["L3"]))[0][0]) + 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("readers", [1, 0], ids=["qsbr_readers", "no_readers"])
+def test_graph_walk_rcu_delete_in_flight(readers):
+    """grout deletes a nexthop and its egress iface while a batch that names
+    both is on the GPU (iface_destroy / nexthop_destroy, iface.c:702-725,
+    nexthop.c:493-518: out of grout's tables, rte_rcu_qsbr_synchronize, then
+    the REMOVE / DELETE events and the free). The worker keeps reporting
+    quiescent (main_loop.c:464). With the node's QSBR readers the
+    synchronisation returns only once the batch has been handed back and
+    through grout's nodes behind the edges, every packet reaches ip_hold with
+    the live nexthop, and nothing freed is read. Without them (round 2's
+    node, the negative control) the synchronisation returns while the batch
+    is still on the GPU, and the hand-back finds the objects gone."""
+    L = lib()
+    fp = graph_ctx()
+    t = T.config_single_route()
+    load(fp, t)
+    gw = _slot_of(t, "172.16.0.2")  # 16.0.0.0/16 via 172.16.0.2, unresolved: ip_hold
+    oif = int(t.nh[gw]["iface_id"])
+    fr, me = S.stream(BATCH, 0xC0C, dst_range=(T.ip4("16.0.0.0"), T.ip4("16.0.255.255")))
+    fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
+    res = np.zeros(1, dtype=RCU_RES_DT)
+    L.gpu_fwd4_rcu_readers(readers)
+    try:
+        assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, len(me)) == 0
+        assert L.gh_rcu_delete_test(gw, oif, 30, res.ctypes.data) == 0
+    finally:
+        L.gpu_fwd4_rcu_readers(1)
+    r = res[0]
+    assert r["sync_done"] == 1 and r["recorded"] == BATCH, r
+    if readers:
+        assert r["sync_before_handback"] == 0, r
+        assert r["recorded_at_sync"] == BATCH, r  # every packet through grout's nodes first
+        assert r["freed_reads"] == 0 and r["stale"] == 0, r
+        out = np.zeros(BATCH, dtype=OUT_DT)
+        lines = np.zeros((BATCH, abi.LINE), dtype=np.uint8)
+        assert L.gh_results(out.ctypes.data, lines.ctypes.data) == BATCH
+        assert (out["edge"] == abi.EDGE["ip_hold"]).all()
+        assert (out["nh"] == gw).all() and (out["iface"] == oif).all()
+        assert walk_info()["readers_online"] <= 2  # released one walk after their hand-back
+    else:
+        assert r["sync_before_handback"] == 1, r
+        assert r["stale"] == BATCH, r  # dropped at hand-back: the objects were gone
+
+
+@pytest.mark.gpu
+def test_graph_walk_full_batches_under_stream_limit():
+    """batch = 65536 with a 10 s hold: the node clamps it to
+    GPU_FWD4_BATCH_MAX, fills whole batches, hands one back per process()
+    call, and no node of the graph ever holds more than two batches plus a
+    burst (rte_graph streams are uint16: the stand-in aborts past 65535, as
+    DPDK's RTE_VERIFY does)."""
+    L = lib()
+    graph_ctx()
+    assert L.gpu_fwd4_set_batch(1 << 16, 10_000_000_000) == 0
+    try:
+        t = T.config_single_route()
+        n = 3 * BATCH_MAX + 1000  # three full batches, then a short RX burst flushes the rest
+        fr, me = S.stream(n, 0xB2A, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+        i0 = walk_info()
+        got = check_walk(t, fr, me)
+        i1 = walk_info()
+    finally:
+        assert L.gpu_fwd4_set_batch(BATCH, DELAY_NS) == 0
+    assert (got["edge"] == abi.EDGE["port_output"]).all()
+    assert i1["max_batch"] == BATCH_MAX
+    assert i1["batches"] - i0["batches"] == 4
+    hw = node_counters("port_output")[3]
+    assert BATCH_MAX <= hw <= 2 * BATCH_MAX + 256, hw
+
+
+@pytest.mark.gpu
+def test_fanout_marks_diverged_context():
+    """A control-plane call that fails on one GPU's context only (here a
+    route into a VRF that context lacks) leaves that context's mirrors out of
+    step: it is marked diverged and the graphs bound to it hand every packet
+    to grout's CPU nodes, until the control plane has replayed the change
+    into it and calls gpu_fwd4_resync(). The other context keeps forwarding."""
+    from grout_amd.fwd import FastPath
+    L = lib()
+    fp = graph_ctx()
+    t = T.config_single_route()
+    load(fp, t)
+    assert L.gh_n_ctx() == 2
+    vrf = 7
+    h0, h1 = FastPath.borrow(L.gh_ctx_at(0)), FastPath.borrow(L.gh_ctx_at(1))
+    h0.fib_create(vrf, 1024)
+    k = L.gh_graph_create(2, 0)  # a worker graph on the least loaded context
+    assert k > 0 and L.gh_graph_gpu() == 1
+    try:
+        r = np.zeros(1, dtype=abi.ROUTE_DT)
+        r[0] = (T.ip4("10.9.0.0"), 16, 0, vrf, _slot_of(t, "172.16.1.2"))
+        L.gpu_fwd4_route4_add.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int]
+        assert L.gpu_fwd4_route4_add(r.ctypes.data, 1, 1) < 0  # -ENONET on context 1 only
+        assert L.gpu_fwd4_diverged(0) == 0 and L.gpu_fwd4_diverged(1) == 1
+        assert walk_info()["diverged"] == 1
+        fr, me = S.stream(3000, 0xD1F, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+        got, _, _, _ = walk(fr, me)
+        assert (got["edge"] == abi.EDGE["punt"]).all()  # iface_input_cpu: grout's CPU nodes
+        # the control plane replays the change into context 1, then resyncs it
+        h1.fib_create(vrf, 1024)
+        h1.route_add(r, replace=True)
+        assert L.gpu_fwd4_resync(1) == 0 and L.gpu_fwd4_diverged(1) == 0
+        got = check_walk(t, fr, me)
+        assert (got["edge"] == abi.EDGE["port_output"]).all()
+    finally:
+        L.gpu_fwd4_resync(1)
+        assert L.gh_graph_destroy() == 0
+        L.gh_graph_use(0)
+        for h in (h0, h1):
+            try:
+                h.fib_destroy(vrf)
+            except Exception:
+                pass

@@ -1,0 +1,48 @@
+# SPDX-License-Identifier: BSD-3-Clause
+"""The changes a grout maintainer makes to grout's own files, as committed
+patches, applied to the reference tree in a dry run:
+
+* integration/grout-iface_input_cpu.patch renames grout's iface_input node to
+  iface_input_cpu (the fast path's PUNT target);
+* integration/grout-gpu_fwd4-datapath.patch makes gr_datapath_loop fold the
+  fast path's counters into grout's statistics at each housekeeping tick
+  (main_loop.c:461-475) and sizes the datapath's QSBR variable for the
+  node's readers (main_loop.c:538-543).
+
+Each patch must apply cleanly, and name only symbols the node's header
+declares."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+PATCHES = ["grout-iface_input_cpu.patch", "grout-gpu_fwd4-datapath.patch"]
+
+
+def _patch_ok(name):
+    return subprocess.run(["patch", "-p1", "--dry-run", "-s", "-d", REF, "-i", os.path.join(ROOT, "integration", name)],
+                          capture_output=True, text=True)
+
+
+@pytest.mark.skipif(not os.path.isdir(REF + "/modules") or shutil.which("patch") is None,
+                    reason="reference tree or patch(1) not available")
+@pytest.mark.parametrize("name", PATCHES)
+def test_patch_applies_to_grout(name):
+    r = _patch_ok(name)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_datapath_patch_names_the_node_api():
+    text = open(os.path.join(ROOT, "integration", "grout-gpu_fwd4-datapath.patch")).read()
+    added = "\n".join(l[1:] for l in text.splitlines() if l.startswith("+") and not l.startswith("+++"))
+    hdr = open(os.path.join(ROOT, "grout_amd", "graph", "gpu_fwd4_node.h")).read()
+    for sym in sorted(set(re.findall(r"\b(gpu_fwd4_\w+|GPU_FWD4_\w+)\b", added))):
+        assert re.search(r"\b%s\b" % sym, hdr), sym
+    # the hook runs at the housekeeping tick, after rte_graph's own counters
+    assert re.search(r"\n \s*rte_graph_cluster_stats_get\(ctx\.stats, false\);\n\+\s*gpu_fwd4_stats_flush\(graph, "
+                     r"rte_lcore_id\(\), gpu_node_stats, &ctx\);", text)
+    assert "RTE_MAX_LCORE + GPU_FWD4_RCU_READERS" in added
