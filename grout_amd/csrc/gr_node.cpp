@@ -115,9 +115,13 @@ extern "C" int gr_hip_edge_node(uint8_t edge, uint32_t nh, int ip6) {
 
 // Walk boundaries of the node's mbufs (include/grout_hip.h,
 // gr_hip_node_layout): a walk starts at m[0], at GR_HIP_MBUF_F_WALK, and
-// `burst` mbufs after the previous start.
+// `burst` mbufs after the previous start. grout's walks hold at most
+// RTE_GRAPH_BURST_SIZE = 256 packets (rx_burst_max / vector_max,
+// modules/infra/control/graph.c:612-650, checked at :619); 64 by default
+// (:88-91).
+#define WALK_MAX 256
 static inline uint32_t walk_burst(uint32_t burst) {
-	return burst == 0 || burst > 64 ? 64 : burst;
+	return burst == 0 ? 64 : burst > WALK_MAX ? WALK_MAX : burst;
 }
 
 static inline bool walk_start(const struct gr_hip_mbuf *m, uint32_t i, uint32_t start, uint32_t burst) {
@@ -135,7 +139,10 @@ extern "C" int gr_hip_node_layout(const struct gr_hip_mbuf *m, uint32_t n, uint3
 		while (e < n && !walk_start(m, e, i, burst))
 			e++;
 		const uint32_t len = e - i;
-		if ((p & 63) + len > 64) // would straddle a tile: start it on the next one
+		// a walk that fits a tile never straddles one (the kernel resolves
+		// eth_output's cache inside a tile); a longer one starts on a tile
+		// (the hand-back resolves it, eth_output_walk)
+		if ((p & 63) + len > 64)
 			p = (p + 63) & ~63u;
 		for (uint32_t k = i; k < e; k++)
 			pos[k] = p++;
@@ -198,6 +205,58 @@ static inline uint16_t vlan_sub(const struct gr_node_vlans *vl, uint16_t parent,
 			return vl->vals[h];
 		if (vl->keys[h] == 0)
 			return 0;
+	}
+}
+
+// eth_output's per-walk source-MAC cache (eth_output.c:37-59) over a walk
+// [a, e) longer than a tile, which the kernel resolved tile by tile: replay
+// it over the whole walk and set each forwarded packet's source MAC (bytes
+// 6-11 of its frame, already handed back) to the cached MAC: its iface's, or
+// zero after a failed lookup of another iface (eth_output_no_mac). eth_output
+// takes ip_output's packets, then ip6_output's, or the other way round when
+// an IPv6 packet reached ip6_input first (rte_graph's pending queue), as the
+// kernel's eth_output_walks does inside a tile.
+static void eth_output_walk(struct gr_hip_mbuf *m, uint32_t a, uint32_t e, const uint32_t *pos,
+			    const struct gr_hip_verdict *verdicts, const int8_t *fam, const struct gr_hip_iface *ifaces,
+			    uint32_t n_ifaces, const struct gr_hip_nh *nh, uint32_t n_nh) {
+	int32_t first4 = -1, first6 = -1;
+	for (uint32_t i = a; i < e; i++) {
+		if (fam[i - a] == 1 && first4 < 0)
+			first4 = (int32_t)i;
+		if (fam[i - a] == 2 && first6 < 0)
+			first6 = (int32_t)i;
+	}
+	const bool six_first = first6 >= 0 && (first4 < 0 || first6 < first4);
+	uint32_t last = GR_HIP_IFACE_ID_UNDEF;
+	bool cleared = false; // the cached source MAC was zeroed
+	for (int pass = 0; pass < 2; pass++) {
+		const int8_t f = (pass == 0) == six_first ? 2 : 1;
+		for (uint32_t i = a; i < e; i++) {
+			if (fam[i - a] != f)
+				continue;
+			const struct gr_hip_verdict &v = verdicts[pos != nullptr ? pos[i] : i];
+			const bool nomac = v.edge == GR_HIP_E_ETH_OUTPUT_NO_MAC;
+			const int node = edge_node(v.edge, v.nh, f == 2);
+			if (!nomac && node != GR_HIP_NODE_IFACE_OUTPUT)
+				continue; // never reached eth_output
+			// priv->iface at eth_output: the nexthop's iface (ip_output.c:91-97)
+			const uint32_t eo = nomac ? v.iface : (v.nh < n_nh && nh != nullptr ? nh[v.nh].iface_id : 0);
+			if (eo != last) {
+				if (nomac) { // iface_get_eth_addr failed: src_mac zeroed, last kept
+					cleared = true;
+					continue;
+				}
+				last = eo;
+				cleared = false;
+			}
+			if (nomac)
+				continue;
+			uint8_t *src = static_cast<uint8_t *>(m[i].frame) + 6;
+			if (cleared)
+				memset(src, 0, 6);
+			else if (eo < n_ifaces && ifaces != nullptr)
+				memcpy(src, ifaces[eo].mac, 6);
+		}
 	}
 }
 
@@ -270,6 +329,8 @@ extern "C" int gr_node_apply_ex(
 	uint32_t ended[2][7] = {}; // packets of the walk that stopped at depth d, per family
 	uint32_t reach[GR_HIP_NODE_COUNT] = {};
 	uint32_t start = 0; // first mbuf of the current graph walk
+	int8_t fam[WALK_MAX]; // per packet of the walk: 1 = entered ip_input, 2 = ip6_input, 0 = neither
+	bool walk_nomac = false; // the walk holds an eth_output_no_mac packet
 	// frames read (the ether type) and written back: prefetch them, the loop
 	// is bound by their cache misses
 	constexpr uint32_t AHEAD = 16;
@@ -290,10 +351,15 @@ extern "C" int gr_node_apply_ex(
 		if (node < -1)
 			return -EINVAL;
 		b.edge = v.edge;
+		if (i - start < WALK_MAX)
+			fam[i - start] = 0;
+		walk_nomac |= v.edge == GR_HIP_E_ETH_OUTPUT_NO_MAC;
 		if (node >= 0) {
 			const int depth = depth_of[ip6][node]; // position of `node` on the packet's path
 			if (depth < 0)
 				return -EINVAL;
+			if (depth >= 2 && i - start < WALK_MAX)
+				fam[i - start] = ip6 ? 2 : 1;
 			ended[ip6][depth]++;
 			// VLAN demux in iface_input: the tag was consumed
 			const bool demuxed = b.vlan_id != 0 && v.edge != GR_HIP_E_IFACE_INPUT_UNKNOWN_VLAN && b.iface < n_ifaces
@@ -357,6 +423,9 @@ extern "C" int gr_node_apply_ex(
 			b.nh = v.nh;
 		}
 		if (i + 1 == n || walk_start(m, i + 1, start, burst)) { // this graph walk ends here
+			if (walk_nomac && i + 1 - start > 64)
+				eth_output_walk(m, start, i + 1, pos, verdicts, fam, ifaces, n_ifaces, nh, n_nh);
+			walk_nomac = false;
 			start = i + 1;
 			if (stats == nullptr)
 				continue;

@@ -263,8 +263,18 @@ class Queue:
         return n, bool(ready.value)
 
     def stats(self, reset=False):
+        """Per-iface counters the queue's kernels accumulated on the device."""
         st = np.zeros(self.fp.max_ifaces, dtype=abi.STATS_DT)
         check("gr_hip_queue_stats", self.lib.gr_hip_queue_stats(self._h, ptr(st), len(st), 1 if reset else 0))
+        return st
+
+    def node_iface_stats(self, reset=False):
+        """Per-iface counters of the node walks handed back, counted on the
+        host where grout counts them (what the grout node folds into grout's
+        iface_stats)."""
+        st = np.zeros(self.fp.max_ifaces, dtype=abi.STATS_DT)
+        check("gr_hip_node_iface_stats", self.lib.gr_hip_node_iface_stats(self._h, ptr(st), len(st),
+                                                                         1 if reset else 0))
         return st
 
     def close(self):

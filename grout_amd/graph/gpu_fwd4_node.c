@@ -104,6 +104,13 @@ int gpu_fwd4_set_depth(uint32_t depth) {
 	return 0;
 }
 
+int gpu_fwd4_set_rx_burst(uint32_t rx_burst) {
+	if (rx_burst == 0 || rx_burst > RTE_GRAPH_BURST_SIZE)
+		return -EINVAL;
+	conf.rx_burst = rx_burst;
+	return 0;
+}
+
 int gpu_fwd4_set_batch(uint32_t batch, uint64_t max_delay_ns) {
 	if (batch == 0)
 		return -EINVAL;
@@ -241,6 +248,12 @@ static int pick_gpu(const struct rte_graph *graph) {
 }
 
 // ---- per-graph walk state ----------------------------------------------------
+// A graph walk is one process() call (its first mbuf carries
+// GR_HIP_MBUF_F_WALK): up to vector_max = 256 packets (graph.c:612-650).
+// The node splits a longer call (several RX queues and other nodes feeding
+// it more) at RTE_GRAPH_BURST_SIZE.
+#define WALK_SPLIT RTE_GRAPH_BURST_SIZE
+
 enum { RD_FREE = 0, RD_HELD, RD_RELEASE };
 
 struct gpu_walk {
@@ -476,13 +489,13 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 	}
 	if (conf.depth < 2 && !w->pending) { // synchronous
 		started(w, n);
-		deliver(graph, node, w, k, n, gr_hip_node_process(w->q, w->v[k], n, conf.rx_burst, &w->stats));
+		deliver(graph, node, w, k, n, gr_hip_node_process(w->q, w->v[k], n, WALK_SPLIT, &w->stats));
 		return n;
 	}
 	// stage and send this batch while the previous one may still be on the
 	// GPU, then hand the previous one back: batches leave in arrival order
 	PROF_T0();
-	const int r = gr_hip_node_start(w->q, w->v[k], n, conf.rx_burst);
+	const int r = gr_hip_node_start(w->q, w->v[k], n, WALK_SPLIT);
 	PROF_ADD(GPU_FWD4_PROF_START);
 	const uint32_t delivered = finish_pending(graph, node, w);
 	if (r < 0) { // the GPU did not take it: grout's CPU nodes do (after the one before, in order)

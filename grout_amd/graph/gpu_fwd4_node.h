@@ -98,7 +98,7 @@ struct gpu_fwd4_conf {
 	uint32_t max_ifaces; // gr_hip_init sizes (grout: gr_config)
 	uint32_t max_nexthops;
 	uint32_t batch; // packets accumulated before a GPU walk (at most GPU_FWD4_BATCH_MAX)
-	uint32_t rx_burst; // port_rx burst size: a shorter burst flushes
+	uint32_t rx_burst; // port_rx burst size (1..256): a shorter burst flushes
 	uint64_t max_delay_ns; // a held packet never waits longer (flush node)
 	uint32_t depth; // batches in flight per graph: 1 = each waited for, 2 = pipelined (0: 2)
 };
@@ -113,6 +113,9 @@ int gpu_fwd4_set_depth(uint32_t depth);
 // Batch size and maximum hold time at any time (the next batch of each graph
 // takes them; the batch is clamped to GPU_FWD4_BATCH_MAX). 0 or -EINVAL.
 int gpu_fwd4_set_batch(uint32_t batch, uint64_t max_delay_ns);
+// The RX burst (grout's rx_burst_max, graph.c:612-650: 1..256): a shorter
+// burst means the RX queue drained, and the node flushes. 0 or -EINVAL.
+int gpu_fwd4_set_rx_burst(uint32_t rx_burst);
 // Measurement: nanoseconds the node spent, per phase, since the last call
 // (then reset); on = 0 stops accumulating. out: GPU_FWD4_PROF_COUNT values.
 enum {

@@ -227,6 +227,14 @@ static int register_recorders(void) {
 	return 0;
 }
 
+// grout's nodes the fast path replaces: they stay in every worker graph
+// (graph_init puts every registered node in base_node_names, graph.c:652-688;
+// worker_graph_new selects them all, :130), idle, and grout's statistics
+// report them under their names (gpu_fwd4_stats_flush). Stand-ins here.
+static const char *const replaced[] = {"eth_input", "ip_input", "ip_forward", "ip_output", "eth_output",
+				       "iface_output", "ip6_input", "ip6_forward", "ip6_output"};
+#define N_REPLACED (sizeof(replaced) / sizeof(replaced[0]))
+
 // Register the graph's nodes (port_rx, grout's node infos, the recorders)
 // without touching the GPU. Idempotent.
 int gh_register(void) {
@@ -238,6 +246,9 @@ int gh_register(void) {
 	int r;
 	if ((r = gr_nodes_register()) < 0 || (r = register_recorders()) < 0)
 		return r;
+	for (unsigned k = 0; k < N_REPLACED; k++)
+		if ((r = add_recorder(replaced[k])) < 0)
+			return r;
 	done = 1;
 	return 0;
 }
@@ -368,8 +379,11 @@ int gh_graph_create(unsigned cpu, int socket) {
 		return -ENOSPC;
 	char name[RTE_GRAPH_NAMESIZE];
 	snprintf(name, sizeof(name), "gr-%04x", (cpu << 1) & 0xffff);
-	const char *patterns[] = {"port_rx", "gpu_fwd4_flush"};
-	struct rte_graph_param prm = {.socket_id = socket, .nb_node_patterns = 2, .node_patterns = patterns};
+	const char *patterns[2 + N_REPLACED] = {"port_rx", "gpu_fwd4_flush"};
+	for (unsigned i = 0; i < N_REPLACED; i++)
+		patterns[2 + i] = replaced[i];
+	struct rte_graph_param prm = {
+		.socket_id = socket, .nb_node_patterns = 2 + N_REPLACED, .node_patterns = patterns};
 	rte_graph_t gid = rte_graph_create(name, &prm);
 	if (gid == RTE_GRAPH_ID_INVALID)
 		return -EINVAL;
@@ -394,6 +408,14 @@ static void graph_stats_free(int k) {
 	free(H.graphs[k].prev_packets);
 	free(H.graphs[k].prev_calls);
 	H.graphs[k].w_packets = H.graphs[k].w_batches = H.graphs[k].prev_packets = H.graphs[k].prev_calls = NULL;
+}
+
+// port_rx's burst (1..256), and the node's (gpu_fwd4_set_rx_burst).
+int gh_set_rx_burst(uint32_t rx_burst) {
+	int r = gpu_fwd4_set_rx_burst(rx_burst);
+	if (r == 0)
+		H.rx_burst = rx_burst;
+	return r;
 }
 
 int gh_graph_use(int k) {

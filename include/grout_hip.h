@@ -618,11 +618,14 @@ struct gr_hip_node_stats {
 int gr_hip_edge_node(uint8_t edge, uint32_t nh, int ip6);
 
 // Graph walks of n mbufs: one starts at m[0], at every mbuf with
-// GR_HIP_MBUF_F_WALK, and `burst` (1..64; 0 = 64) mbufs after the previous
-// start. The staged layout puts mbuf i at pos[i], padding so that no walk
-// straddles a multiple of 64 packets (the kernel resolves eth_output's
-// per-walk cache inside a 64-packet tile, see GR_HIP_META_WALK). Returns
-// the number of staged slots (>= n), or -errno.
+// GR_HIP_MBUF_F_WALK, and `burst` (1..256, grout's rx_burst_max /
+// vector_max limit RTE_GRAPH_BURST_SIZE, graph.c:612-650; 0 = 64) mbufs
+// after the previous start. The staged layout puts mbuf i at pos[i],
+// padding so that no walk of up to 64 packets straddles a multiple of 64
+// (the kernel resolves eth_output's per-walk cache inside a 64-packet tile,
+// see GR_HIP_META_WALK) and a longer walk starts on one (the hand-back
+// resolves the cache over the whole walk). Returns the number of staged
+// slots (>= n), or -errno.
 int gr_hip_node_layout(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, uint32_t *pos);
 
 // Stage n mbufs: the first 64 bytes at each frame (read whatever data_len

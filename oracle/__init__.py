@@ -150,12 +150,14 @@ class Oracle:
                                             abi.BATCH_F_LINES_ONLY if lines_only else 0))
         return out, v, st
 
-    def process_mbufs(self, frames, meta, lines_only=False):
+    def process_mbufs(self, frames, meta, lines_only=False, burst=64):
         """-> (out_lines, verdicts, stats, mbufs, node_stats): process() plus
         the mbuf state at each edge (abi.MBUF_DT, RX data_off 128) and the
         per-node counters. Graph walks as the rte_graph node cuts mbufs
-        (OR_F_MBUF_WALKS): at each abi.META_WALK mark and 64 packets after
-        the previous start."""
+        (OR_F_MBUF_WALKS): at each abi.META_WALK mark and `burst` (1..256)
+        packets after the previous start."""
+        if not 1 <= burst <= 256:
+            raise ValueError("burst")
         frames = np.ascontiguousarray(frames)
         meta = np.ascontiguousarray(meta, dtype=abi.META_DT)
         n = len(meta)
@@ -167,7 +169,8 @@ class Oracle:
         ns = np.zeros(1, dtype=abi.NODE_STATS_DT)
         _ck("or_process_ex", self.L.or_process_ex(self.h, frames.ctypes.data, stride, meta.ctypes.data, n,
                                                   out.ctypes.data, abi.LINE, v.ctypes.data, st.ctypes.data,
-                                                  (abi.BATCH_F_LINES_ONLY if lines_only else 0) | OR_F_MBUF_WALKS,
+                                                  (abi.BATCH_F_LINES_ONLY if lines_only else 0) | OR_F_MBUF_WALKS
+                                                  | ((burst & 0x1FF) << 16),
                                                   mb.ctypes.data,
                                                   ns.ctypes.data))
         return out, v, st, mb, ns[0]

@@ -18,6 +18,7 @@
 #include <unistd.h>
 
 #define OR_BURST 64 // rx_burst_max / vector_max defaults, graph.c:88-91
+#define OR_BURST_MAX 256 // their maximum, RTE_GRAPH_BURST_SIZE (graph.c:619)
 #define OR_HEADROOM 128 // RTE_PKTMBUF_HEADROOM
 #define OR_DATAROOM 2048 // align32pow2(128+14+4+1800), mempool.c:66-68
 #define NEXT GR_HIP_EDGE_CHAIN
@@ -731,7 +732,7 @@ static void mbuf_prepend(struct or_mbuf *m, uint16_t len) { // headroom is alway
 }
 
 struct or_stream {
-	struct or_mbuf *objs[OR_BURST];
+	struct or_mbuf *objs[OR_BURST_MAX];
 	uint16_t n;
 };
 
@@ -1214,7 +1215,7 @@ static void mark(struct or_mbuf **objs, uint16_t n, int node) {
 static void graph_walk(struct or_graph *g, struct or_mbuf **objs, uint16_t n) {
 	mark(objs, n, GR_HIP_NODE_IFACE_INPUT);
 	node_iface_input(g, objs, n);
-	struct or_mbuf *batch[OR_BURST];
+	struct or_mbuf *batch[OR_BURST_MAX];
 	while (g->pend_head != g->pend_tail) {
 		const int node = g->pend[g->pend_head++ % (4 * GR_HIP_NODE_COUNT)];
 		struct or_stream *s = &g->st[node];
@@ -1357,21 +1358,24 @@ int or_process_ex(
 	if (readable > OR_DATAROOM - OR_HEADROOM)
 		readable = OR_DATAROOM - OR_HEADROOM;
 	struct or_graph g = {.t = t, .flags = flags, .readable = readable};
-	struct or_mbuf mb[OR_BURST];
-	struct or_mbuf *objs[OR_BURST];
-	uint8_t *bufs = malloc((size_t)OR_BURST * OR_DATAROOM);
+	uint32_t burst = (flags >> OR_F_BURST_SHIFT) & 0x1ff; // mbuf walks: the walk length cap
+	if (burst == 0 || burst > OR_BURST_MAX)
+		burst = OR_BURST;
+	struct or_mbuf mb[OR_BURST_MAX];
+	struct or_mbuf *objs[OR_BURST_MAX];
+	uint8_t *bufs = malloc((size_t)OR_BURST_MAX * OR_DATAROOM);
 	if (bufs == NULL)
 		return -ENOMEM;
-	memset(bufs, 0, (size_t)OR_BURST * OR_DATAROOM);
-	for (int i = 0; i < OR_BURST; i++)
+	memset(bufs, 0, (size_t)OR_BURST_MAX * OR_DATAROOM);
+	for (int i = 0; i < OR_BURST_MAX; i++)
 		mb[i].buf = bufs + (size_t)i * OR_DATAROOM;
 	const uint8_t *in = in_frames;
 	uint8_t *out = out_lines;
 	for (uint32_t base = 0, k; base < n; base += k) {
-		// this graph walk: up to the next GR_HIP_META_WALK mark, at most 64
-		// packets (graph.c:88-91) and, for a batch (not OR_F_MBUF_WALKS),
-		// never past a multiple of 64 (include/grout_hip.h)
-		uint32_t end = base + OR_BURST;
+		// this graph walk: up to the next GR_HIP_META_WALK mark; for node
+		// mbufs (OR_F_MBUF_WALKS) at most `burst` packets (graph.c:88-91,
+		// 612-650), for a batch never past a multiple of 64 (include/grout_hip.h)
+		uint32_t end = base + burst;
 		if (!(flags & OR_F_MBUF_WALKS))
 			end = (base / OR_BURST + 1) * OR_BURST;
 		if (end > n)

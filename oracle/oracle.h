@@ -78,9 +78,14 @@ uint32_t or_lpm_brute(const or_topo_t *, uint16_t vrf_id, uint32_t ip);
 // Graph walks as a batch defines them (GR_HIP_META_WALK): one starts at
 // packet 0, at each multiple of 64 and at each marked packet.
 // OR_F_MBUF_WALKS (a flags bit): walks as the rte_graph node cuts its mbufs
-// instead (gr_hip_node_layout): at each marked packet and 64 packets after
-// the previous start, wherever that falls.
+// instead (gr_hip_node_layout): at each marked packet and `burst` packets
+// (OR_F_BURST below) after the previous start, wherever that falls.
 #define OR_F_MBUF_WALKS 0x80000000u
+// With OR_F_MBUF_WALKS: a walk is at most OR_F_BURST(b) packets (1..256,
+// grout's rx_burst_max / vector_max, gr_infra.h:446-453, graph.c:612-650);
+// 0 = 64, the default burst (graph.c:88-91).
+#define OR_F_BURST_SHIFT 16
+#define OR_F_BURST(b) ((uint32_t)((b) & 0x1ff) << OR_F_BURST_SHIFT)
 int or_process(
 	or_topo_t *,
 	const void *in_frames,

@@ -387,9 +387,23 @@ ETH_OUTPUT_CACHE_WALKS = [
 ]
 
 
-def eth_output_cache_arrays(stride=STRIDE):
+# Walks longer than a 64-packet tile (grout's rx_burst_max / vector_max go up
+# to 256, graph.c:612-650): the same rule over the whole walk, derived by hand.
+ETH_OUTPUT_CACHE_LONG_WALKS = [
+    ("Z " * 63 + "X Y X", {65}),                      # the failed lookup and its victim in the second tile
+    ("X " + "Z " * 62 + "Y Z X X X", {64}),           # the lookup fails at the tile's end, Z after it is zeroed
+    ("X Y " + "X " * 130, set(range(2, 132))),        # three tiles of zeroed X
+    ("X6 " + "X " * 64 + "Y X X6", {66}),             # ip6_input first: [X6 X6 | X*64 Y X], one zero past a tile
+    ("X Y " + "X " * 254, set(range(2, 256))),        # a whole 256-packet walk
+]
+
+
+def eth_output_cache_arrays(stride=STRIDE, walks=None):
     """frames, meta (abi.META_WALK at each walk start), labels, zero (bool:
-    grout sends the packet with a zero source MAC)."""
+    grout sends the packet with a zero source MAC). walks: (spec, zero set)
+    pairs, ETH_OUTPUT_CACHE_WALKS by default; walks longer than 64 are for
+    node mbuf walks (oracle burst >= their length), not device batches."""
+    walks = ETH_OUTPUT_CACHE_WALKS if walks is None else walks
     fr, f6 = S.frame, S.frame6
     make = {
         "X": lambda k: fr(dst="16.1.7.%d" % (k % 250 + 1)),
@@ -403,9 +417,9 @@ def eth_output_cache_arrays(stride=STRIDE):
     }
     rows, walk, zero, labels = [], [], [], []
     k = 0
-    for w, (spec, z) in enumerate(ETH_OUTPUT_CACHE_WALKS):
+    for w, (spec, z) in enumerate(walks):
         syms = spec.split()
-        while len(rows) % 64 + len(syms) > 64:  # a batch walk never straddles a tile: pad
+        while len(syms) <= 64 and len(rows) % 64 + len(syms) > 64:  # a batch walk never straddles a tile: pad
             rows.append(None)
             walk.append(True)
             zero.append(False)

@@ -76,6 +76,7 @@ def lib():
         _lib.gh_iface_stats.argtypes = [U16, P]
         _lib.gh_walk_info.argtypes = [P]
         _lib.gh_rcu_delete_test.argtypes = [U32, U16, U32, P]
+        _lib.gh_set_rx_burst.argtypes = [U32]
         _lib.gpu_fwd4_set_batch.argtypes = [U32, ctypes.c_uint64]
         _lib.gpu_fwd4_diverged.argtypes = [U32]
         _lib.gpu_fwd4_resync.argtypes = [U32]
@@ -329,7 +330,7 @@ def stage_of(edges, nh, ip6):
     return np.array([L.gr_hip_edge_node(int(e), int(h), int(s)) for e, h, s in zip(edges, nh, ip6)])
 
 
-def check_walk(topo, fr, me, labels=None):
+def check_walk(topo, fr, me, labels=None, burst=BURST):
     fp = graph_ctx(keep=True)  # on the current graph
     load(fp, topo)
     L = lib()
@@ -337,7 +338,7 @@ def check_walk(topo, fr, me, labels=None):
     L.gh_stats_reset()  # and grout's: iface_stats, the worker's node stats
     ns0 = np.zeros(1, dtype=abi.NODE_STATS_DT)
     assert L.gh_node_stats(ns0.ctypes.data, None) == 0
-    o_lines, o_v, o_st, want, ns_want = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
+    o_lines, o_v, o_st, want, ns_want = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True, burst=burst)
     got, lines, ns, _ = walk(fr, me)
     lab = (lambda i: labels[i]) if labels else (lambda i: i)
     # packets handed to a CPU continuation node (conntrack, SNAT) end further
@@ -676,3 +677,30 @@ def test_fanout_marks_diverged_context():
                 h.fib_destroy(vrf)
             except Exception:
                 pass
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("burst", [128, 256])
+def test_graph_walk_long_bursts(burst):
+    """port_rx bursts of 128 and 256 packets (grout's rx_burst_max /
+    vector_max go up to 256, graph.c:612-650): one graph walk per burst, so
+    the node's walks span several 64-packet tiles. eth_output's per-walk
+    source-MAC cache (eth_output.c:37-59), the per-node calls and the iface
+    counters follow grout over whole walks, against the oracle walking the
+    same bursts: the cache walks (long ones included), and a stream."""
+    L = lib()
+    graph_ctx()
+    assert L.gh_set_rx_burst(burst) == 0
+    try:
+        t, _ = SC.corpus_topology()
+        fr, me, lab, _ = SC.eth_output_cache_arrays(walks=SC.ETH_OUTPUT_CACHE_WALKS + SC.ETH_OUTPUT_CACHE_LONG_WALKS)
+        me = me.copy()
+        me["vlan_ck"] &= 0xFFFF ^ abi.META_WALK  # the harness's walks are port_rx's bursts
+        got = check_walk(t, fr, me, lab, burst=burst)
+        assert (got["edge"] == abi.EDGE["eth_output_no_mac"]).sum() >= 10
+        ts = T.config_single_route()
+        fr, me = S.stream(20_011, 0xB0E, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+        got = check_walk(ts, fr, me, burst=burst)
+        assert (got["edge"] == abi.EDGE["port_output"]).all()
+    finally:
+        assert L.gh_set_rx_burst(BURST) == 0

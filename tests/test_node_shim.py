@@ -121,24 +121,89 @@ def test_apply_corpus_matches_oracle_mbufs():
     assert six.sum() > 10 and (m["packet_type"][six] == want["packet_type"][six]).all()
 
 
-@pytest.mark.parametrize("burst", [1, 7, 64])
+@pytest.mark.parametrize("burst", [1, 7, 64, 128, 256])
 def test_node_stats_bursts(burst):
-    """Per-node packets / calls follow grout's rule for any walk size: the
-    oracle walks bursts of 64, so compare at 64 and check the invariants
-    for other sizes."""
+    """Per-node packets / calls follow grout's rule for any walk size up to
+    grout's maximum (rx_burst_max / vector_max <= 256, graph.c:612-650): the
+    oracle walks the same bursts."""
     t, _ = SC.corpus_topology()
     fr, me, _ = SC.corpus_arrays()
-    lines, v, _, _, ns64 = oracle.Oracle(t).process_mbufs(fr, me)
-    _, m = mbufs_for(fr, me)
+    lines, v, _, want, ns_b = oracle.Oracle(t).process_mbufs(fr, me, burst=burst)
+    lines64, _, _, _, ns64 = oracle.Oracle(t).process_mbufs(fr, me)
+    bufs, m = mbufs_for(fr, me)
     ns = apply(m, lines, v, t, burst=burst)
-    assert np.array_equal(ns["packets"], ns64["packets"])  # packets do not depend on the walk size
+    compare_mbufs(m, want, bufs, lines)
+    assert np.array_equal(ns["packets"], ns_b["packets"]) and np.array_equal(ns["calls"], ns_b["calls"])
+    # packets do not depend on the walk size, calls do
+    assert np.array_equal(ns["packets"], ns64["packets"])
     n_walks = -(-len(me) // burst)
     assert (ns["calls"] <= n_walks).all()
-    if burst == 64:
-        assert np.array_equal(ns["calls"], ns64["calls"])
     # ip_output / ip6_output return what they sent to eth_output
     N = {n: i for i, n in enumerate(abi.NODE_NAMES)}
     assert ns["packets"][N["ip_output"]] + ns["packets"][N["ip6_output"]] == ns["packets"][N["eth_output"]]
+
+
+def _vlan_table(topo):
+    """The host image of the context's VLAN table (gr_hip.cpp upload_vlans)."""
+    ifs = topo.ifaces[(topo.ifaces["id"] != 0) & (topo.ifaces["type"] == abi.IFACE_TYPE["VLAN"])]
+    cap = 16
+    while cap < 2 * len(ifs):
+        cap *= 2
+    keys = np.zeros(cap, dtype=np.uint32)
+    vals = np.zeros(cap, dtype=np.uint16)
+    for i in ifs:
+        key = ((int(i["parent_id"]) << 16) | int(i["vlan_id"])) + 1
+        h = (key * 0x9E3779B1) & 0xFFFFFFFF & (cap - 1)
+        while keys[h] not in (0, key):
+            h = (h + 1) & (cap - 1)
+        keys[h], vals[h] = key, i["id"]
+    return keys, vals
+
+
+def apply_counting(m, lines, v, topo, burst=64):
+    """gr_node_apply_ex: the hand-back plus the per-iface counters grout's
+    iface_input / iface_output would have added (what the node folds into
+    grout's iface_stats)."""
+    import ctypes
+    L = ctypes.CDLL(abi.LIB_HIP)
+    keys, vals = _vlan_table(topo)
+    vl = (ctypes.c_void_p * 2)(keys.ctypes.data, vals.ctypes.data)
+    vl_buf = np.zeros(3, dtype=np.uint64)  # struct gr_node_vlans {keys, vals, cap}
+    vl_buf[0], vl_buf[1], vl_buf[2] = vl[0], vl[1], len(keys)
+    st = np.zeros(topo.max_ifaces, dtype=abi.STATS_DT)
+    ns = np.zeros(1, dtype=abi.NODE_STATS_DT)
+    ifaces = np.ascontiguousarray(topo.ifaces)
+    nh = np.ascontiguousarray(topo.nh)
+    lines = np.ascontiguousarray(lines)
+    P, U32 = ctypes.c_void_p, ctypes.c_uint32
+    L.gr_node_apply_ex.argtypes = [P, U32, U32, P, P, U32, P, P, U32, P, U32, P, P, P, U32]
+    abi.check("gr_node_apply_ex", L.gr_node_apply_ex(
+        m.ctypes.data, len(m), burst, None, lines.ctypes.data, abi.LINE, v.ctypes.data, ifaces.ctypes.data,
+        len(ifaces), nh.ctypes.data, len(nh), ns.ctypes.data, vl_buf.ctypes.data, st.ctypes.data, len(st)))
+    return ns[0], st
+
+
+def test_apply_counts_ifaces_where_grout_does():
+    """The hand-back's host-side per-iface counters (rx in iface_input past
+    its admin-down and unknown-VLAN drops, VLAN sub-interface and parent; tx
+    in iface_output past its no-parent and admin-down drops, VLAN and parent)
+    equal the oracle's, over every edge of the corpus and a full-view stream."""
+    t, _ = SC.corpus_topology()
+    fr, me, lab = SC.corpus_arrays()
+    lines, v, st_want, want, _ = oracle.Oracle(t).process_mbufs(fr, me)
+    bufs, m = mbufs_for(fr, me)
+    _, st = apply_counting(m, lines, v, t)
+    compare_mbufs(m, want, bufs, lines, lab)
+    bad = np.nonzero(st != st_want)[0]
+    assert len(bad) == 0, [(int(i), st[i], st_want[i]) for i in bad[:4]]
+    assert st["rx_packets"].sum() > 100 and st["tx_packets"].sum() > 10
+    assert (t.ifaces["type"][np.nonzero(st["tx_packets"])[0]] == abi.IFACE_TYPE["VLAN"]).any()  # VLAN + parent
+    tf = T.config_fullview(count=50_000)
+    fr, me = S.stream(1 << 14, 0xA12, routes=tf.route_array())
+    lines, v, st_want, _, _ = oracle.Oracle(tf).process_mbufs(fr, me)
+    _, m = mbufs_for(fr, me)
+    _, st = apply_counting(m, lines, v, tf)
+    assert np.array_equal(st, st_want)
 
 
 def test_apply_fullview_stream():
@@ -174,6 +239,7 @@ def test_node_process_gpu(fastpath):
         assert np.array_equal(ns["packets"], ns_want["packets"])
         assert np.array_equal(ns["calls"], ns_want["calls"])
         assert np.array_equal(q.stats(), st)  # the iface counters of the same packets
+        assert np.array_equal(q.node_iface_stats(), st)  # and the hand-back's, counted on the host
         q.close()
 
 
