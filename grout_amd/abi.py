@@ -226,7 +226,9 @@ HOST_API = {
     "gr_fib6_skips_used": (_U32, [_P]),
     "gr_fib6_groups_painted": (_U32, [_P]),
     "gr_fib6_n_routes": (_U32, [_P]),
-    "gr_fib6_shortcuts": (_I, [_P, _P, _P, _U32]),
+    "gr_fib6_groups_live": (_U32, [_P]),
+    "gr_fib6_dirty": (_I, [_P, _I, ctypes.POINTER(_P), ctypes.POINTER(_U32)]),
+    "gr_fib6_dirty_clear": (None, [_P]),
     "gr_fib6_top": (_P, [_P]),
     "gr_fib6_groups": (_P, [_P]),
     "gr_fib6_skips": (_P, [_P]),

@@ -1,14 +1,37 @@
 // SPDX-License-Identifier: BSD-3-Clause
 //
 // fib6.c -- the IPv6 RIB of one VRF and the multibit trie the kernel walks
-// (see fib6.h). The RIB is an exact-prefix hash (rib6_insert_or_replace /
-// rib6_delete semantics of modules/ip6/control/route.c:229-345: one nexthop
-// per (prefix, length), replace on request). The trie is repainted from the
-// RIB on commit, routes in ascending prefix length so that a longer prefix
-// always overwrites a shorter one: a route ending in the first level paints
-// its 2^(16-len) entries; a longer route walks (creating groups, each
-// initialised with the entry it replaces, so shorter prefixes stay visible
-// below it) to the group of its last byte and paints 2^(8-k) entries there.
+// (see fib6.h), kept up to date route by route.
+//
+// The RIB is an exact-prefix hash (rib6_insert_or_replace / rib6_delete
+// semantics of modules/ip6/control/route.c:229-345: one nexthop per (prefix,
+// length), replace on request).
+//
+// Three layers, each updated incrementally, the way grout changes its
+// rte_fib6 one route at a time (rte_fib6_add / rte_fib6_delete,
+// modules/ip6/control/route.c:229-345):
+//
+//   1. the plain trie: a first level of 2^16 entries (address bytes 0-1) and
+//      nodes of 256 entries per further byte, every entry a leaf (the
+//      nexthop of the longest matching prefix, with that prefix's length) or
+//      a child node. A route add paints the entries its prefix covers whose
+//      leaf is not longer, a delete repaints the entries it painted with the
+//      next longest covering route (DIR24_8's rule, byte by byte); both mark
+//      the nodes they touch and their ancestors dirty. A node whose entries
+//      all hold one leaf folds back into its parent.
+//   2. compression, recomputed bottom-up for the dirty nodes only: a node
+//      whose entries all hold one leaf is that leaf; all but one, a skip
+//      ("the next bytes equal this key: continue, else this leaf"), merging
+//      a child's skip of the same miss leaf (up to 7 key bytes).
+//   3. the device image (top, 1 KiB group slots, 16-byte skip nodes),
+//      materialised top-down along the dirty paths only, clean subtrees
+//      keeping their slots: a node becomes a group slot, a skip node, or a
+//      wide group of 256 consecutive slots indexed by two bytes when it holds
+//      at least GR_FIB6_WIDE_MIN child groups and no skip (its children then
+//      are its rows), or when it is a one-byte skip over a child heading at
+//      least GR_FIB6_SKIP_WIDE_MIN groups. Every write compares, and the
+//      slots, skips and first-level entries that changed form the dirty
+//      lists a commit uploads (gr_fib6_dirty).
 #include "fib6.h"
 
 #include <errno.h>
@@ -24,20 +47,81 @@ struct rib6_ent {
 	uint32_t nh;
 };
 
+#define NO_NODE UINT32_MAX
+#define REF 0x80000000u // a plain entry holding a child node (index in bits 0-30)
+
+enum { CK_LEAF, CK_SKIP, CK_GROUP }; // compressed kind
+enum { R_NONE, R_STANDALONE, R_ROWS, R_MERGED }; // how the image holds a node
+enum { OBJ_NONE, OBJ_SLOT, OBJ_RUN, OBJ_SKIP }; // what it owns in the image
+
+struct node {
+	uint32_t ent[GR_FIB6_GROUP]; // plain: leaf nexthop (bit 31 clear) or REF | child
+	uint8_t dep[GR_FIB6_GROUP]; // the leaf's prefix length
+	uint32_t parent; // NO_NODE: a first-level entry's child
+	uint32_t pslot; // index in the parent (first-level index when parent is NO_NODE)
+	uint8_t pos; // address byte its entries are indexed by (2..15)
+	uint8_t dirty; // touched (or below a touched node) since the last build
+	uint8_t live;
+	// compression (layer 2)
+	uint8_t ckind;
+	uint8_t sk_n; // CK_SKIP: key bytes
+	uint8_t sk_key[7];
+	uint8_t role, obj;
+	uint16_t n_grp_ch, n_skip_ch; // children of kind CK_GROUP / CK_SKIP
+	uint32_t cval; // CK_LEAF: the leaf; CK_SKIP: the miss leaf
+	uint32_t chain; // CK_SKIP: past the key, a leaf or REF | node (the chain's end)
+	uint32_t merged; // CK_SKIP: the child whose skip this one absorbed, or NO_NODE
+	uint32_t cgroups; // group-kind nodes in its compressed subtree (saturating)
+	// the device image (layer 3)
+	uint32_t obj_idx; // slot, first slot of a run, or skip index
+	uint32_t enc; // R_STANDALONE: the entry that stands for it
+	uint32_t row_at; // R_ROWS: the slot holding its row
+};
+
+struct u32vec {
+	uint32_t *v;
+	uint32_t n, cap;
+};
+
+static int vpush(struct u32vec *a, uint32_t x) {
+	if (a->n == a->cap) {
+		uint32_t c = a->cap ? 2 * a->cap : 256;
+		uint32_t *v = realloc(a->v, (size_t)c * sizeof(*v));
+		if (v == NULL)
+			return -ENOMEM;
+		a->v = v;
+		a->cap = c;
+	}
+	a->v[a->n++] = x;
+	return 0;
+}
+
 struct gr_fib6 {
 	struct rib6_ent *ht;
 	uint32_t cap; // power of two
 	uint32_t n_routes, n_tomb, max_routes;
-	uint32_t *top; // GR_FIB6_TOP
-	uint32_t *groups; // max_groups * GR_FIB6_GROUP
-	uint32_t max_groups, n_groups, n_painted;
-	struct gr_fib6_skip *skips; // max_groups: each replaces at least one group
-	uint32_t n_skips;
-	uint32_t *remap; // max_groups, compaction scratch
-	uint8_t *live; // max_groups
 	uint32_t max_slot;
-	bool dirty;
+	// plain trie
+	uint32_t ptop[GR_FIB6_TOP];
+	uint8_t ptop_dep[GR_FIB6_TOP];
+	struct node *nodes;
+	uint32_t n_nodes_cap, n_nodes_hw, n_nodes_live;
+	struct u32vec node_free;
+	struct u32vec dirty_nodes[16]; // by position
+	struct u32vec dirty_ptop; // first-level entries touched
+	uint8_t *ptop_dirty; // GR_FIB6_TOP flags
+	// the device image: top, group slots, skips (fib6.h encoding)
+	uint32_t top[GR_FIB6_TOP];
+	uint32_t *groups; // max_groups * GR_FIB6_GROUP
+	struct gr_fib6_skip *skips; // max_groups
+	uint32_t max_groups, slot_hw, slots_live, skip_hw, skips_live;
+	struct u32vec slot_free, run_free, skip_free;
+	// what the builds since the last gr_fib6_dirty_clear changed in the image
+	uint8_t *slot_dirty, *skip_dirty, *top_dirty;
+	struct u32vec d_slots, d_skips, d_top;
+	bool all_dirty; // everything (no upload yet)
 	uint64_t generation;
+	uint32_t marks; // image writes of the current build
 };
 
 static void mask6(uint8_t out[16], const uint8_t ip[16], uint8_t len) {
@@ -100,12 +184,15 @@ gr_fib6_t *gr_fib6_new(uint32_t max_routes, uint32_t max_groups) {
 	f->max_routes = max_routes;
 	f->max_groups = max_groups;
 	f->ht = calloc(cap, sizeof(*f->ht));
-	f->top = calloc(GR_FIB6_TOP, sizeof(uint32_t));
-	f->groups = malloc((size_t)max_groups * GR_FIB6_GROUP * sizeof(uint32_t));
-	f->skips = malloc((size_t)max_groups * sizeof(*f->skips));
-	f->remap = malloc((size_t)max_groups * sizeof(uint32_t));
-	f->live = malloc(max_groups);
-	if (!f->ht || !f->top || !f->groups || !f->skips || !f->remap || !f->live) {
+	// zeroed on demand by the OS: only the slots in use are ever touched
+	f->groups = calloc((size_t)max_groups * GR_FIB6_GROUP, sizeof(uint32_t));
+	f->skips = calloc(max_groups, sizeof(*f->skips));
+	f->slot_dirty = calloc(max_groups, 1);
+	f->skip_dirty = calloc(max_groups, 1);
+	f->top_dirty = calloc(GR_FIB6_TOP, 1);
+	f->ptop_dirty = calloc(GR_FIB6_TOP, 1);
+	f->all_dirty = true;
+	if (!f->ht || !f->groups || !f->skips || !f->slot_dirty || !f->skip_dirty || !f->top_dirty || !f->ptop_dirty) {
 		gr_fib6_free(f);
 		return NULL;
 	}
@@ -116,11 +203,23 @@ void gr_fib6_free(gr_fib6_t *f) {
 	if (f == NULL)
 		return;
 	free(f->ht);
-	free(f->top);
+	free(f->nodes);
+	free(f->node_free.v);
+	for (int i = 0; i < 16; i++)
+		free(f->dirty_nodes[i].v);
+	free(f->dirty_ptop.v);
+	free(f->ptop_dirty);
 	free(f->groups);
 	free(f->skips);
-	free(f->remap);
-	free(f->live);
+	free(f->slot_free.v);
+	free(f->run_free.v);
+	free(f->skip_free.v);
+	free(f->slot_dirty);
+	free(f->skip_dirty);
+	free(f->top_dirty);
+	free(f->d_slots.v);
+	free(f->d_skips.v);
+	free(f->d_top.v);
 	free(f);
 }
 
@@ -143,6 +242,209 @@ static int ht_rehash(gr_fib6_t *f) { // drop tombstones
 	return 0;
 }
 
+// ---- layer 1: the plain trie -----------------------------------------------
+
+// Mark node n and its ancestors dirty, and the first-level entry above them.
+static int touch(gr_fib6_t *f, uint32_t n) {
+	while (n != NO_NODE) {
+		struct node *x = &f->nodes[n];
+		if (x->dirty)
+			return 0; // its ancestors are already
+		x->dirty = 1;
+		if (vpush(&f->dirty_nodes[x->pos], n) < 0)
+			return -ENOMEM;
+		if (x->parent == NO_NODE) {
+			n = x->pslot;
+			break;
+		}
+		n = x->parent;
+	}
+	if (!f->ptop_dirty[n]) {
+		f->ptop_dirty[n] = 1;
+		if (vpush(&f->dirty_ptop, n) < 0)
+			return -ENOMEM;
+	}
+	return 0;
+}
+
+static int touch_top(gr_fib6_t *f, uint32_t t) {
+	if (f->ptop_dirty[t])
+		return 0;
+	f->ptop_dirty[t] = 1;
+	return vpush(&f->dirty_ptop, t);
+}
+
+// A node under entry (parent, pslot) at position pos, every entry the leaf
+// (nh, dep) it replaces. Returns its index or NO_NODE.
+static uint32_t node_new(gr_fib6_t *f, uint32_t parent, uint32_t pslot, uint8_t pos, uint32_t nh, uint8_t dep) {
+	uint32_t n;
+	if (f->node_free.n) {
+		n = f->node_free.v[--f->node_free.n];
+	} else {
+		if (f->n_nodes_hw == f->n_nodes_cap) {
+			uint32_t c = f->n_nodes_cap ? 2 * f->n_nodes_cap : 1024;
+			if (c > REF)
+				return NO_NODE;
+			struct node *v = realloc(f->nodes, (size_t)c * sizeof(*v));
+			if (v == NULL)
+				return NO_NODE;
+			f->nodes = v;
+			f->n_nodes_cap = c;
+		}
+		n = f->n_nodes_hw++;
+	}
+	struct node *x = &f->nodes[n];
+	memset(x, 0, sizeof(*x));
+	for (int i = 0; i < GR_FIB6_GROUP; i++)
+		x->ent[i] = nh;
+	memset(x->dep, dep, sizeof(x->dep));
+	x->parent = parent;
+	x->pslot = pslot;
+	x->pos = pos;
+	x->live = 1;
+	x->ckind = CK_LEAF;
+	x->cval = nh;
+	x->merged = NO_NODE;
+	f->n_nodes_live++;
+	return n;
+}
+
+// Paint (nh, len) into entry i of node n when its leaf is not longer; into
+// every entry of a child node the same way (DIR24_8's rule).
+static int paint_entry(gr_fib6_t *f, uint32_t n, int i, uint8_t len, uint32_t nh) {
+	struct node *x = &f->nodes[n];
+	if (x->ent[i] & REF) {
+		const uint32_t c = x->ent[i] & ~REF;
+		for (int j = 0; j < GR_FIB6_GROUP; j++) {
+			int r = paint_entry(f, c, j, len, nh);
+			if (r < 0)
+				return r;
+		}
+		return 0;
+	}
+	if (x->dep[i] > len || (x->dep[i] == len && x->ent[i] == nh))
+		return 0;
+	x->ent[i] = nh;
+	x->dep[i] = len;
+	return touch(f, n);
+}
+
+// Repaint, under entry i of node n, the leaves painted by a prefix of length
+// len with (nh, dep) (a delete: the next longest covering route).
+static int unpaint_entry(gr_fib6_t *f, uint32_t n, int i, uint8_t len, uint32_t nh, uint8_t dep) {
+	struct node *x = &f->nodes[n];
+	if (x->ent[i] & REF) {
+		const uint32_t c = x->ent[i] & ~REF;
+		for (int j = 0; j < GR_FIB6_GROUP; j++) {
+			int r = unpaint_entry(f, c, j, len, nh, dep);
+			if (r < 0)
+				return r;
+		}
+		return 0;
+	}
+	if (x->dep[i] != len)
+		return 0;
+	x->ent[i] = nh;
+	x->dep[i] = dep;
+	return touch(f, n);
+}
+
+// The same at the first level.
+static int paint_top(gr_fib6_t *f, uint32_t t, uint8_t len, uint32_t nh, bool del, uint32_t rnh, uint8_t rdep) {
+	if (f->ptop[t] & REF) {
+		const uint32_t c = f->ptop[t] & ~REF;
+		for (int j = 0; j < GR_FIB6_GROUP; j++) {
+			int r = del ? unpaint_entry(f, c, j, len, rnh, rdep) : paint_entry(f, c, j, len, nh);
+			if (r < 0)
+				return r;
+		}
+		return 0;
+	}
+	if (del) {
+		if (f->ptop_dep[t] != len)
+			return 0;
+		f->ptop[t] = rnh;
+		f->ptop_dep[t] = rdep;
+	} else {
+		if (f->ptop_dep[t] > len || (f->ptop_dep[t] == len && f->ptop[t] == nh))
+			return 0;
+		f->ptop[t] = nh;
+		f->ptop_dep[t] = len;
+	}
+	return touch_top(f, t);
+}
+
+// Apply a route add (del false) or delete (del true, replaced by (rnh,
+// rdep)) of ip/len to the plain trie.
+static int apply(gr_fib6_t *f, const uint8_t ip[16], uint8_t len, uint32_t nh, bool del, uint32_t rnh, uint8_t rdep) {
+	if (len <= 16) {
+		const uint32_t base = ((uint32_t)ip[0] << 8) | ip[1], cnt = 1u << (16 - len);
+		for (uint32_t t = base; t < base + cnt; t++) {
+			int r = paint_top(f, t, len, nh, del, rnh, rdep);
+			if (r < 0)
+				return r;
+		}
+		return 0;
+	}
+	// down to the node of the prefix's last byte, creating nodes on the way
+	// (a delete too: a leaf folded from several prefixes of one length and
+	// nexthop unfolds, and only this prefix's range is repainted)
+	const uint32_t t = ((uint32_t)ip[0] << 8) | ip[1];
+	if (!(f->ptop[t] & REF)) {
+		const uint32_t c = node_new(f, NO_NODE, t, 2, f->ptop[t], f->ptop_dep[t]);
+		if (c == NO_NODE)
+			return -ENOMEM;
+		f->ptop[t] = REF | c;
+		int r = touch(f, c);
+		if (r < 0)
+			return r;
+	}
+	uint32_t n = f->ptop[t] & ~REF;
+	unsigned b = 2;
+	while (len > 8 * (b + 1)) { // the prefix goes past this node's byte
+		struct node *x = &f->nodes[n];
+		const uint32_t i = ip[b];
+		if (!(x->ent[i] & REF)) {
+			const uint32_t c = node_new(f, n, i, (uint8_t)(b + 1), x->ent[i], x->dep[i]);
+			if (c == NO_NODE)
+				return -ENOMEM;
+			x = &f->nodes[n]; // node_new may have moved the array
+			x->ent[i] = REF | c;
+			int r = touch(f, c);
+			if (r < 0)
+				return r;
+		}
+		n = f->nodes[n].ent[i] & ~REF;
+		b++;
+	}
+	const unsigned k = len - 8 * b; // 1..8 bits of byte b
+	const uint32_t base = ip[b] & (0xff00u >> k) & 0xff, cnt = 1u << (8 - k);
+	for (uint32_t i = base; i < base + cnt; i++) {
+		int r = del ? unpaint_entry(f, n, (int)i, len, rnh, rdep) : paint_entry(f, n, (int)i, len, nh);
+		if (r < 0)
+			return r;
+	}
+	return 0;
+}
+
+// The longest route covering ip with a prefix shorter than len: (nh, length),
+// (0, 0) when none.
+static void covering(const gr_fib6_t *f, const uint8_t ip[16], uint8_t len, uint32_t *nh, uint8_t *dep) {
+	for (int l = (int)len - 1; l >= 0; l--) {
+		uint8_t key[16];
+		mask6(key, ip, (uint8_t)l);
+		bool found;
+		const struct rib6_ent *e = ht_find(f, key, (uint8_t)l, &found);
+		if (found) {
+			*nh = e->nh;
+			*dep = (uint8_t)l;
+			return;
+		}
+	}
+	*nh = 0;
+	*dep = 0;
+}
+
 int gr_fib6_add(gr_fib6_t *f, const uint8_t ip[16], uint8_t len, uint32_t nh, int replace) {
 	if (f == NULL || ip == NULL || len > 128 || nh == 0 || nh >= GR_FIB6_EXT)
 		return -EINVAL;
@@ -153,10 +455,9 @@ int gr_fib6_add(gr_fib6_t *f, const uint8_t ip[16], uint8_t len, uint32_t nh, in
 	if (found) {
 		if (!replace)
 			return -EEXIST;
-		if (e->nh != nh) {
-			e->nh = nh;
-			f->dirty = true;
-		}
+		if (e->nh == nh)
+			return 0;
+		e->nh = nh;
 	} else {
 		if (f->n_routes >= f->max_routes || e == NULL)
 			return -ENOSPC;
@@ -167,11 +468,10 @@ int gr_fib6_add(gr_fib6_t *f, const uint8_t ip[16], uint8_t len, uint32_t nh, in
 		e->nh = nh;
 		e->used = 1;
 		f->n_routes++;
-		f->dirty = true;
 	}
 	if (nh > f->max_slot)
 		f->max_slot = nh;
-	return 0;
+	return apply(f, key, len, nh, false, 0, 0);
 }
 
 int gr_fib6_del(gr_fib6_t *f, const uint8_t ip[16], uint8_t len) {
@@ -186,254 +486,416 @@ int gr_fib6_del(gr_fib6_t *f, const uint8_t ip[16], uint8_t len) {
 	e->used = 2;
 	f->n_routes--;
 	f->n_tomb++;
-	f->dirty = true;
 	if (f->n_tomb > f->cap / 4)
 		(void)ht_rehash(f); // a failed rehash only costs probe length
+	uint32_t rnh;
+	uint8_t rdep;
+	covering(f, key, len, &rnh, &rdep);
+	return apply(f, key, len, 0, true, rnh, rdep);
+}
+
+// ---- layer 3 storage: slots, runs of 256 slots, skips ----------------------
+
+static int mark_slot(gr_fib6_t *f, uint32_t s) {
+	f->marks++;
+	if (f->slot_dirty[s])
+		return 0;
+	f->slot_dirty[s] = 1;
+	return vpush(&f->d_slots, s);
+}
+
+static int mark_skip(gr_fib6_t *f, uint32_t k) {
+	f->marks++;
+	if (f->skip_dirty[k])
+		return 0;
+	f->skip_dirty[k] = 1;
+	return vpush(&f->d_skips, k);
+}
+
+static int put_top(gr_fib6_t *f, uint32_t t, uint32_t v) {
+	if (f->top[t] == v)
+		return 0;
+	f->top[t] = v;
+	f->marks++;
+	if (f->top_dirty[t])
+		return 0;
+	f->top_dirty[t] = 1;
+	return vpush(&f->d_top, t);
+}
+
+static inline int put(gr_fib6_t *f, uint32_t s, int i, uint32_t v) {
+	uint32_t *p = &f->groups[(size_t)s * GR_FIB6_GROUP + i];
+	if (*p == v)
+		return 0;
+	*p = v;
+	return mark_slot(f, s);
+}
+
+// A new slot: written whole this build, whatever the image held there.
+static int slot_alloc(gr_fib6_t *f, uint32_t *s) {
+	if (f->slot_free.n) {
+		*s = f->slot_free.v[--f->slot_free.n];
+	} else if (f->slot_hw < f->max_groups) {
+		*s = f->slot_hw++;
+	} else if (f->run_free.n) { // break a free run into single slots
+		const uint32_t w = f->run_free.v[--f->run_free.n];
+		for (uint32_t k = GR_FIB6_GROUP - 1; k >= 1; k--)
+			if (vpush(&f->slot_free, w + k) < 0)
+				return -ENOMEM;
+		*s = w;
+	} else {
+		return -ENOSPC;
+	}
+	f->slots_live++;
+	return mark_slot(f, *s);
+}
+
+static void slot_free(gr_fib6_t *f, uint32_t s) {
+	memset(f->groups + (size_t)s * GR_FIB6_GROUP, 0, GR_FIB6_GROUP * sizeof(uint32_t));
+	f->slots_live--;
+	(void)vpush(&f->slot_free, s); // a failed push only leaks the slot
+}
+
+static bool run_available(const gr_fib6_t *f) {
+	return f->run_free.n || f->slot_hw + GR_FIB6_GROUP <= f->max_groups;
+}
+
+static int run_alloc(gr_fib6_t *f, uint32_t *w) {
+	if (f->run_free.n) {
+		*w = f->run_free.v[--f->run_free.n];
+	} else if (f->slot_hw + GR_FIB6_GROUP <= f->max_groups) {
+		*w = f->slot_hw;
+		f->slot_hw += GR_FIB6_GROUP;
+	} else {
+		return -ENOSPC;
+	}
+	f->slots_live += GR_FIB6_GROUP;
+	for (uint32_t k = 0; k < GR_FIB6_GROUP; k++) {
+		int r = mark_slot(f, *w + k);
+		if (r < 0)
+			return r;
+	}
 	return 0;
 }
 
-static int paint(gr_fib6_t *f, const struct rib6_ent *r) {
-	const uint8_t *ip = r->ip;
-	if (r->len <= 16) {
-		uint32_t base = ((uint32_t)ip[0] << 8) | ip[1];
-		uint32_t cnt = 1u << (16 - r->len);
-		for (uint32_t i = 0; i < cnt; i++)
-			f->top[base + i] = r->nh; // ascending order: never a group yet
-		return 0;
-	}
-	uint32_t *e = &f->top[((uint32_t)ip[0] << 8) | ip[1]];
-	unsigned consumed = 16, b = 2;
-	for (;;) {
-		if (!(*e & GR_FIB6_EXT)) {
-			if (f->n_groups >= f->max_groups)
-				return -ENOSPC;
-			uint32_t g = f->n_groups++;
-			uint32_t *grp = f->groups + (size_t)g * GR_FIB6_GROUP;
-			for (int i = 0; i < GR_FIB6_GROUP; i++)
-				grp[i] = *e;
-			*e = GR_FIB6_EXT | g;
-		}
-		uint32_t *grp = f->groups + (size_t)(*e & ~GR_FIB6_EXT) * GR_FIB6_GROUP;
-		if (r->len <= consumed + 8) {
-			unsigned nb = r->len - consumed;
-			uint32_t base = ip[b], cnt = 1u << (8 - nb);
-			for (uint32_t i = 0; i < cnt; i++)
-				grp[base + i] = r->nh;
-			return 0;
-		}
-		e = &grp[ip[b]];
-		b++;
-		consumed += 8;
-	}
+static void run_free(gr_fib6_t *f, uint32_t w) {
+	memset(f->groups + (size_t)w * GR_FIB6_GROUP, 0, (size_t)GR_FIB6_GROUP * GR_FIB6_GROUP * sizeof(uint32_t));
+	f->slots_live -= GR_FIB6_GROUP;
+	(void)vpush(&f->run_free, w);
 }
 
-// Path compression (bottom-up): a group whose entries all hold one leaf D
-// but for one index x becomes a skip node {key x, child = entry x, miss D};
-// a skip whose child is a skip with the same miss and room in its key
-// absorbs it. Returns the entry that replaces `ent`.
-static uint32_t compress(gr_fib6_t *f, uint32_t ent) {
-	if (!(ent & GR_FIB6_EXT) || (ent & GR_FIB6_SKIP))
-		return ent;
-	uint32_t *grp = f->groups + (size_t)(ent & GR_FIB6_IDX) * GR_FIB6_GROUP;
-	for (int i = 0; i < GR_FIB6_GROUP; i++)
-		grp[i] = compress(f, grp[i]);
+static int skip_alloc(gr_fib6_t *f, uint32_t *k) {
+	if (f->skip_free.n)
+		*k = f->skip_free.v[--f->skip_free.n];
+	else if (f->skip_hw < f->max_groups)
+		*k = f->skip_hw++;
+	else
+		return -ENOSPC;
+	f->skips_live++;
+	return mark_skip(f, *k);
+}
+
+static void skip_free(gr_fib6_t *f, uint32_t k) {
+	memset(&f->skips[k], 0, sizeof(f->skips[k]));
+	f->skips_live--;
+	(void)vpush(&f->skip_free, k);
+}
+
+// Give back what node x owns in the image.
+static void release(gr_fib6_t *f, struct node *x) {
+	switch (x->obj) {
+	case OBJ_SLOT:
+		slot_free(f, x->obj_idx);
+		break;
+	case OBJ_RUN:
+		run_free(f, x->obj_idx);
+		break;
+	case OBJ_SKIP:
+		skip_free(f, x->obj_idx);
+		break;
+	}
+	x->obj = OBJ_NONE;
+}
+
+// ---- layer 2: compression, bottom-up over the dirty nodes ------------------
+
+// The compressed value of entry i of node x: a leaf, or a child node that
+// compresses to a leaf, or REF | child.
+static inline uint32_t cvalue(const gr_fib6_t *f, const struct node *x, int i) {
+	const uint32_t e = x->ent[i];
+	if (!(e & REF))
+		return e;
+	const struct node *c = &f->nodes[e & ~REF];
+	return c->ckind == CK_LEAF ? c->cval : e;
+}
+
+#define CGROUPS_MAX 0x3fffffffu
+
+static void compress_node(gr_fib6_t *f, struct node *x) {
+	uint32_t v0 = cvalue(f, x, 0), v1 = cvalue(f, x, 1), v2 = cvalue(f, x, 2);
 	// the leaf most entries hold: one of the first three
-	uint32_t d = grp[0] == grp[1] || grp[0] == grp[2] ? grp[0] : grp[1];
-	if (d & GR_FIB6_EXT)
-		return ent;
-	int x = -1;
+	const uint32_t d = v0 == v1 || v0 == v2 ? v0 : v1;
+	uint32_t n_grp = 0, n_skip = 0, groups = 0;
+	int x_exc = -1, n_exc = 0;
 	for (int i = 0; i < GR_FIB6_GROUP; i++) {
-		if (grp[i] == d)
-			continue;
-		if (x >= 0)
-			return ent; // two paths leave this group
-		x = i;
-	}
-	if (x < 0)
-		return d; // every entry the same leaf
-	const uint32_t child = grp[x];
-	if ((child & GR_FIB6_SKIP) && (child & GR_FIB6_EXT)) {
-		struct gr_fib6_skip *k = &f->skips[child & GR_FIB6_IDX];
-		if (k->miss == d && k->n < 7) { // prepend x to the child's key
-			memmove(k->key + 1, k->key, k->n);
-			k->key[0] = (uint8_t)x;
-			k->n++;
-			return child;
+		const uint32_t e = x->ent[i];
+		if (e & REF) {
+			const struct node *c = &f->nodes[e & ~REF];
+			n_grp += c->ckind == CK_GROUP;
+			n_skip += c->ckind == CK_SKIP;
+			groups += c->cgroups;
+			if (groups > CGROUPS_MAX)
+				groups = CGROUPS_MAX;
+		}
+		if (cvalue(f, x, i) != d) {
+			x_exc = i;
+			n_exc++;
 		}
 	}
-	struct gr_fib6_skip *k = &f->skips[f->n_skips];
-	memset(k, 0, sizeof(*k));
-	k->key[0] = (uint8_t)x;
-	k->n = 1;
-	k->child = child;
-	k->miss = d;
-	return GR_FIB6_EXT | GR_FIB6_SKIP | f->n_skips++;
-}
-
-static void mark(gr_fib6_t *f, uint32_t ent) {
-	if (!(ent & GR_FIB6_EXT))
-		return;
-	if (ent & GR_FIB6_SKIP) {
-		mark(f, f->skips[ent & GR_FIB6_IDX].child);
+	x->n_grp_ch = (uint16_t)n_grp;
+	x->n_skip_ch = (uint16_t)n_skip;
+	x->merged = NO_NODE;
+	if ((d & REF) || n_exc > 1) {
+		x->ckind = CK_GROUP;
+		x->cgroups = groups + 1 > CGROUPS_MAX ? CGROUPS_MAX : groups + 1;
 		return;
 	}
-	const uint32_t g = ent & GR_FIB6_IDX, slots = (ent & GR_FIB6_WIDE) ? GR_FIB6_GROUP : 1;
-	for (uint32_t s = 0; s < slots; s++)
-		f->live[g + s] = 1;
-	for (uint32_t i = 0; i < slots * GR_FIB6_GROUP; i++)
-		mark(f, f->groups[(size_t)g * GR_FIB6_GROUP + i]);
+	if (n_exc == 0) { // every entry the same leaf
+		x->ckind = CK_LEAF;
+		x->cval = d;
+		x->cgroups = 0;
+		return;
+	}
+	x->ckind = CK_SKIP;
+	x->cval = d;
+	x->sk_key[0] = (uint8_t)x_exc;
+	x->sk_n = 1;
+	const uint32_t e = cvalue(f, x, x_exc);
+	x->chain = e;
+	x->cgroups = 0;
+	if (e & REF) {
+		const uint32_t ci = e & ~REF;
+		const struct node *c = &f->nodes[ci];
+		if (c->ckind == CK_SKIP && c->cval == d && c->sk_n < 7) { // prepend x to the child's key
+			memcpy(x->sk_key + 1, c->sk_key, c->sk_n);
+			x->sk_n = (uint8_t)(c->sk_n + 1);
+			x->chain = c->chain;
+			x->merged = ci;
+		}
+		if (x->chain & REF)
+			x->cgroups = f->nodes[x->chain & ~REF].cgroups;
+	}
 }
 
-static uint32_t relink(const gr_fib6_t *f, uint32_t ent) {
-	// a wide group's slots stay consecutive: all live, packed in order
-	if ((ent & GR_FIB6_EXT) && !(ent & GR_FIB6_SKIP))
-		return (ent & (GR_FIB6_EXT | GR_FIB6_WIDE)) | f->remap[ent & GR_FIB6_IDX];
-	return ent;
+// A node whose entries all hold one leaf (same nexthop, same prefix length)
+// folds into its parent's entry.
+static bool fold(gr_fib6_t *f, uint32_t n) {
+	struct node *x = &f->nodes[n];
+	const uint32_t e0 = x->ent[0];
+	const uint8_t d0 = x->dep[0];
+	if (e0 & REF)
+		return false;
+	for (int i = 1; i < GR_FIB6_GROUP; i++)
+		if (x->ent[i] != e0 || x->dep[i] != d0)
+			return false;
+	if (x->parent == NO_NODE) {
+		f->ptop[x->pslot] = e0;
+		f->ptop_dep[x->pslot] = d0;
+	} else {
+		struct node *p = &f->nodes[x->parent];
+		p->ent[x->pslot] = e0;
+		p->dep[x->pslot] = d0;
+	}
+	release(f, x);
+	x->live = 0;
+	f->n_nodes_live--;
+	(void)vpush(&f->node_free, n);
+	return true;
 }
 
-// Group slots in the subtree of `ent`, counting stops at `cap`.
-static uint32_t subtree_groups(const gr_fib6_t *f, uint32_t ent, uint32_t cap) {
-	if (!(ent & GR_FIB6_EXT))
+// ---- layer 3: materialisation, top-down along the dirty paths --------------
+
+static int standalone(gr_fib6_t *f, uint32_t n, uint32_t *enc);
+
+// The entry standing for plain entry e of a node at position pos - 1, i.e.
+// at position pos.
+static int entry_enc(gr_fib6_t *f, uint32_t e, uint32_t *enc) {
+	if (!(e & REF)) {
+		*enc = e;
 		return 0;
-	if (ent & GR_FIB6_SKIP)
-		return subtree_groups(f, f->skips[ent & GR_FIB6_IDX].child, cap);
-	const uint32_t slots = (ent & GR_FIB6_WIDE) ? GR_FIB6_GROUP : 1;
-	uint32_t n = slots;
-	const uint32_t *e = f->groups + (size_t)(ent & GR_FIB6_IDX) * GR_FIB6_GROUP;
-	for (uint32_t i = 0; i < slots * GR_FIB6_GROUP && n < cap; i++)
-		n += subtree_groups(f, e[i], cap - n);
-	return n;
+	}
+	return standalone(f, e & ~REF, enc);
 }
 
-// Level compression (top-down, entries at byte b): a group whose entries
-// hold at least GR_FIB6_WIDE_MIN child groups and no skip node, at b <= 14,
-// becomes a wide group: entry (x, y) = entry y of child x, or the group's
-// own leaf at x repeated; so does a one-byte skip whose child group heads at
-// least GR_FIB6_SKIP_WIDE_MIN groups. Stops quietly when the group capacity
-// runs out.
-static uint32_t widen(gr_fib6_t *f, uint32_t ent, unsigned b) {
-	if (!(ent & GR_FIB6_EXT) || b >= 16)
-		return ent;
-	if (ent & GR_FIB6_SKIP) {
-		struct gr_fib6_skip *k = &f->skips[ent & GR_FIB6_IDX];
-		// a one-byte skip over a heavy subtree becomes a wide group: row
-		// key = the child group, every other row the miss leaf (the skip's
-		// test and the child's gather in one gather)
-		if (k->n == 1 && b <= 14 && (k->child & GR_FIB6_EXT) && !(k->child & (GR_FIB6_SKIP | GR_FIB6_WIDE))
-		    && f->n_groups + GR_FIB6_GROUP <= f->max_groups
-		    && subtree_groups(f, k->child, GR_FIB6_SKIP_WIDE_MIN) >= GR_FIB6_SKIP_WIDE_MIN) {
-			const uint32_t w = f->n_groups;
-			f->n_groups += GR_FIB6_GROUP;
-			uint32_t *W = f->groups + (size_t)w * GR_FIB6_GROUP;
-			for (uint32_t i = 0; i < GR_FIB6_GROUP * GR_FIB6_GROUP; i++)
-				W[i] = k->miss;
-			uint32_t *row = W + (size_t)k->key[0] * GR_FIB6_GROUP;
-			memcpy(row, f->groups + (size_t)(k->child & GR_FIB6_IDX) * GR_FIB6_GROUP, GR_FIB6_GROUP * sizeof(uint32_t));
-			for (uint32_t i = 0; i < GR_FIB6_GROUP; i++)
-				row[i] = widen(f, row[i], b + 2);
-			return GR_FIB6_EXT | GR_FIB6_WIDE | w;
-		}
-		k->child = widen(f, k->child, b + k->n);
-		return ent;
-	}
-	const uint32_t g = ent & GR_FIB6_IDX;
-	uint32_t n_grp = 0, n_skip = 0;
+// Node n's entries as they stand at its position (a group slot's content,
+// or a row of its parent's wide group) into slot s.
+static int rows_of(gr_fib6_t *f, uint32_t n, uint32_t s) {
 	for (int i = 0; i < GR_FIB6_GROUP; i++) {
-		const uint32_t e = f->groups[(size_t)g * GR_FIB6_GROUP + i];
-		if (e & GR_FIB6_EXT)
-			*((e & GR_FIB6_SKIP) ? &n_skip : &n_grp) += 1;
+		uint32_t v;
+		int r = entry_enc(f, f->nodes[n].ent[i], &v);
+		if (r < 0)
+			return r;
+		if ((r = put(f, s, i, v)) < 0)
+			return r;
 	}
-	if (b <= 14 && n_skip == 0 && n_grp >= GR_FIB6_WIDE_MIN && f->n_groups + GR_FIB6_GROUP <= f->max_groups) {
-		const uint32_t w = f->n_groups;
-		f->n_groups += GR_FIB6_GROUP;
-		const uint32_t *grp = f->groups + (size_t)g * GR_FIB6_GROUP;
-		uint32_t *W = f->groups + (size_t)w * GR_FIB6_GROUP;
-		for (int x = 0; x < GR_FIB6_GROUP; x++) {
-			uint32_t *row = W + (size_t)x * GR_FIB6_GROUP;
-			if (grp[x] & GR_FIB6_EXT)
-				memcpy(row, f->groups + (size_t)(grp[x] & GR_FIB6_IDX) * GR_FIB6_GROUP,
-				       GR_FIB6_GROUP * sizeof(uint32_t));
+	return 0;
+}
+
+static int fill_row(gr_fib6_t *f, uint32_t s, uint32_t leaf) {
+	for (int i = 0; i < GR_FIB6_GROUP; i++) {
+		int r = put(f, s, i, leaf);
+		if (r < 0)
+			return r;
+	}
+	return 0;
+}
+
+// Child node c becomes row s of a wide group.
+static int as_row(gr_fib6_t *f, uint32_t c, uint32_t s) {
+	struct node *x = &f->nodes[c];
+	if (!x->dirty && x->role == R_ROWS && x->row_at == s && !f->slot_dirty[s])
+		return 0; // unchanged (a slot written since the last upload may be a new run)
+	release(f, x);
+	x->role = R_ROWS;
+	x->row_at = s;
+	return rows_of(f, c, s);
+}
+
+static int own(gr_fib6_t *f, struct node *x, int obj, uint32_t *idx) {
+	if (x->obj == obj) {
+		*idx = x->obj_idx;
+		return 0;
+	}
+	release(f, x);
+	int r = obj == OBJ_SLOT ? slot_alloc(f, idx) : obj == OBJ_RUN ? run_alloc(f, idx) : skip_alloc(f, idx);
+	if (r < 0)
+		return r;
+	x->obj = (uint8_t)obj;
+	x->obj_idx = *idx;
+	return 0;
+}
+
+// The entry that stands for node n at its position, its image written.
+static int standalone(gr_fib6_t *f, uint32_t n, uint32_t *enc) {
+	struct node *x = &f->nodes[n];
+	if (!x->dirty && x->role == R_STANDALONE) {
+		*enc = x->enc;
+		return 0;
+	}
+	const unsigned b = x->pos;
+	uint32_t idx, v;
+	int r = 0;
+	if (x->ckind == CK_LEAF) {
+		release(f, x);
+		v = x->cval;
+	} else if (x->ckind == CK_SKIP) {
+		const bool heavy = (x->chain & REF) && f->nodes[x->chain & ~REF].ckind == CK_GROUP
+			&& f->nodes[x->chain & ~REF].cgroups >= GR_FIB6_SKIP_WIDE_MIN;
+		if (x->sk_n == 1 && b <= 14 && heavy && (x->obj == OBJ_RUN || run_available(f))) {
+			// a one-byte skip over a heavy subtree: one wide group, row key =
+			// the child's entries, every other row the miss leaf
+			if ((r = own(f, x, OBJ_RUN, &idx)) < 0)
+				return r;
+			x = &f->nodes[n];
+			const uint32_t key = x->sk_key[0], miss = x->cval, c = x->chain & ~REF;
+			for (uint32_t k = 0; k < GR_FIB6_GROUP && r == 0; k++)
+				r = k == key ? as_row(f, c, idx + k) : fill_row(f, idx + k, miss);
+			if (r < 0)
+				return r;
+			v = GR_FIB6_EXT | GR_FIB6_WIDE | idx;
+		} else {
+			if ((r = own(f, x, OBJ_SKIP, &idx)) < 0)
+				return r;
+			uint32_t child;
+			if ((r = entry_enc(f, f->nodes[n].chain, &child)) < 0)
+				return r;
+			x = &f->nodes[n];
+			struct gr_fib6_skip k;
+			memset(&k, 0, sizeof(k));
+			memcpy(k.key, x->sk_key, x->sk_n);
+			k.n = x->sk_n;
+			k.child = child;
+			k.miss = x->cval;
+			if (memcmp(&f->skips[idx], &k, sizeof(k)) != 0) {
+				f->skips[idx] = k;
+				if ((r = mark_skip(f, idx)) < 0)
+					return r;
+			}
+			v = GR_FIB6_EXT | GR_FIB6_SKIP | idx;
+			// the nodes whose skips this one absorbed own nothing
+			for (uint32_t m = x->merged; m != NO_NODE;) {
+				struct node *y = &f->nodes[m];
+				release(f, y);
+				y->role = R_MERGED;
+				m = y->ckind == CK_SKIP ? y->merged : NO_NODE;
+			}
+		}
+	} else if (b <= 14 && x->n_skip_ch == 0 && x->n_grp_ch >= GR_FIB6_WIDE_MIN && (x->obj == OBJ_RUN || run_available(f))) {
+		// wide: entry (k, y) = entry y of child k, or the leaf at k repeated
+		if ((r = own(f, x, OBJ_RUN, &idx)) < 0)
+			return r;
+		for (uint32_t k = 0; k < GR_FIB6_GROUP && r == 0; k++) {
+			const uint32_t e = f->nodes[n].ent[k];
+			if ((e & REF) && f->nodes[e & ~REF].ckind == CK_GROUP)
+				r = as_row(f, e & ~REF, idx + k);
 			else
-				for (int y = 0; y < GR_FIB6_GROUP; y++)
-					row[y] = grp[x];
+				r = fill_row(f, idx + k, (e & REF) ? f->nodes[e & ~REF].cval : e);
 		}
-		for (uint32_t i = 0; i < GR_FIB6_GROUP * GR_FIB6_GROUP; i++)
-			W[i] = widen(f, W[i], b + 2);
-		return GR_FIB6_EXT | GR_FIB6_WIDE | w;
+		if (r < 0)
+			return r;
+		v = GR_FIB6_EXT | GR_FIB6_WIDE | idx;
+	} else {
+		if ((r = own(f, x, OBJ_SLOT, &idx)) < 0)
+			return r;
+		if ((r = rows_of(f, n, idx)) < 0)
+			return r;
+		v = GR_FIB6_EXT | idx;
 	}
-	for (int i = 0; i < GR_FIB6_GROUP; i++) {
-		uint32_t *e = &f->groups[(size_t)g * GR_FIB6_GROUP + i];
-		*e = widen(f, *e, b + 1);
-	}
-	return ent;
-}
-
-// Pack the groups still referenced to the front.
-static void pack(gr_fib6_t *f) {
-	memset(f->live, 0, f->n_groups);
-	for (uint32_t i = 0; i < GR_FIB6_TOP; i++)
-		mark(f, f->top[i]);
-	uint32_t n = 0;
-	for (uint32_t g = 0; g < f->n_groups; g++)
-		f->remap[g] = f->live[g] ? n++ : UINT32_MAX;
-	for (uint32_t i = 0; i < GR_FIB6_TOP; i++)
-		f->top[i] = relink(f, f->top[i]);
-	for (uint32_t k = 0; k < f->n_skips; k++)
-		f->skips[k].child = relink(f, f->skips[k].child);
-	for (uint32_t g = 0; g < f->n_groups; g++) {
-		if (!f->live[g])
-			continue;
-		uint32_t *src = f->groups + (size_t)g * GR_FIB6_GROUP;
-		uint32_t *dst = f->groups + (size_t)f->remap[g] * GR_FIB6_GROUP; // never above src
-		for (int i = 0; i < GR_FIB6_GROUP; i++)
-			dst[i] = relink(f, src[i]);
-	}
-	f->n_groups = n;
-}
-
-// Path-compress, pack, level-compress, pack again.
-static void compress_all(gr_fib6_t *f) {
-	f->n_painted = f->n_groups;
-	f->n_skips = 0;
-	for (uint32_t i = 0; i < GR_FIB6_TOP; i++)
-		f->top[i] = compress(f, f->top[i]);
-	pack(f);
-	for (uint32_t i = 0; i < GR_FIB6_TOP; i++)
-		f->top[i] = widen(f, f->top[i], 2);
-	pack(f);
+	x = &f->nodes[n];
+	x->role = R_STANDALONE;
+	x->enc = v;
+	*enc = v;
+	return 0;
 }
 
 int gr_fib6_build(gr_fib6_t *f) {
 	if (f == NULL)
 		return -EINVAL;
-	if (!f->dirty)
-		return 0;
-	// counting sort of the live routes by prefix length
-	uint32_t count[130] = {0};
-	for (uint32_t i = 0; i < f->cap; i++)
-		if (f->ht[i].used == 1)
-			count[f->ht[i].len + 1]++;
-	for (int l = 1; l < 130; l++)
-		count[l] += count[l - 1];
-	const struct rib6_ent **order = malloc((size_t)(f->n_routes ? f->n_routes : 1) * sizeof(*order));
-	if (order == NULL)
-		return -ENOMEM;
-	for (uint32_t i = 0; i < f->cap; i++)
-		if (f->ht[i].used == 1)
-			order[count[f->ht[i].len]++] = &f->ht[i];
-	memset(f->top, 0, GR_FIB6_TOP * sizeof(uint32_t));
-	f->n_groups = 0;
-	int ret = 0;
-	for (uint32_t i = 0; i < f->n_routes && ret == 0; i++)
-		ret = paint(f, order[i]);
-	free(order);
-	if (ret < 0)
-		return ret;
-	compress_all(f);
-	f->dirty = false;
-	f->generation++;
-	return 0;
+	const uint32_t marks0 = f->marks;
+	int r = 0;
+	// layer 2: deepest first; nodes that fold away leave their parent dirty
+	for (int pos = 15; pos >= 2; pos--) {
+		struct u32vec *dl = &f->dirty_nodes[pos];
+		for (uint32_t k = 0; k < dl->n; k++) {
+			const uint32_t n = dl->v[k];
+			if (!f->nodes[n].live || fold(f, n))
+				continue;
+			compress_node(f, &f->nodes[n]);
+		}
+	}
+	// layer 3: from the first-level entries above dirty nodes
+	for (uint32_t k = 0; k < f->dirty_ptop.n && r == 0; k++) {
+		const uint32_t t = f->dirty_ptop.v[k];
+		uint32_t v;
+		r = entry_enc(f, f->ptop[t], &v);
+		if (r == 0)
+			r = put_top(f, t, v);
+	}
+	for (int pos = 2; pos < 16; pos++) {
+		struct u32vec *dl = &f->dirty_nodes[pos];
+		for (uint32_t k = 0; k < dl->n; k++)
+			f->nodes[dl->v[k]].dirty = 0;
+		dl->n = 0;
+	}
+	for (uint32_t k = 0; k < f->dirty_ptop.n; k++)
+		f->ptop_dirty[f->dirty_ptop.v[k]] = 0;
+	f->dirty_ptop.n = 0;
+	if (f->marks != marks0)
+		f->generation++;
+	return r;
 }
+
+// ---- lookups and accessors ---------------------------------------------------
 
 uint32_t gr_fib6_lookup(const gr_fib6_t *f, const uint8_t ip[16]) {
 	uint32_t ent = f->top[((uint32_t)ip[0] << 8) | ip[1]];
@@ -473,16 +935,19 @@ const uint32_t *gr_fib6_groups(const gr_fib6_t *f) {
 	return f->groups;
 }
 uint32_t gr_fib6_groups_used(const gr_fib6_t *f) {
-	return f->n_groups;
+	return f->slot_hw;
+}
+uint32_t gr_fib6_groups_live(const gr_fib6_t *f) {
+	return f->slots_live;
 }
 const struct gr_fib6_skip *gr_fib6_skips(const gr_fib6_t *f) {
 	return f->skips;
 }
 uint32_t gr_fib6_skips_used(const gr_fib6_t *f) {
-	return f->n_skips;
+	return f->skip_hw;
 }
 uint32_t gr_fib6_groups_painted(const gr_fib6_t *f) {
-	return f->n_painted;
+	return f->n_nodes_live;
 }
 uint32_t gr_fib6_max_groups(const gr_fib6_t *f) {
 	return f->max_groups;
@@ -497,82 +962,27 @@ uint64_t gr_fib6_generation(const gr_fib6_t *f) {
 	return f->generation;
 }
 
-static int cmp_u32(const void *a, const void *b) {
-	const uint32_t x = *(const uint32_t *)a, y = *(const uint32_t *)b;
-	return x < y ? -1 : x > y;
-}
-
-static int cmp_run(const void *a, const void *b) { // (count, key) pairs: count descending, key ascending
-	const uint32_t *x = a, *y = b;
-	if (x[0] != y[0])
-		return x[0] > y[0] ? -1 : 1;
-	return x[1] < y[1] ? -1 : x[1] > y[1];
-}
-
-int gr_fib6_shortcuts(const gr_fib6_t *f, uint32_t *keys, uint32_t *ents, uint32_t max) {
-	if (f == NULL || (max && (keys == NULL || ents == NULL)))
+int gr_fib6_dirty(const gr_fib6_t *f, int kind, const uint32_t **list, uint32_t *n) {
+	if (f == NULL || list == NULL || n == NULL)
 		return -EINVAL;
-	uint32_t n = 0;
-	uint32_t *k = malloc((size_t)(f->n_routes ? f->n_routes : 1) * sizeof(*k));
-	if (k == NULL)
-		return -ENOMEM;
-	for (uint32_t i = 0; i < f->cap; i++) {
-		const struct rib6_ent *r = &f->ht[i];
-		if (r->used == 1 && r->len >= 32)
-			k[n++] = (uint32_t)r->ip[0] | (uint32_t)r->ip[1] << 8 | (uint32_t)r->ip[2] << 16 | (uint32_t)r->ip[3] << 24;
-	}
-	qsort(k, n, sizeof(*k), cmp_u32);
-	// (routes under the /32, key), busiest first
-	uint32_t *runs = malloc((size_t)(n ? n : 1) * 2 * sizeof(*runs));
-	if (runs == NULL) {
-		free(k);
-		return -ENOMEM;
-	}
-	uint32_t nr = 0;
-	for (uint32_t i = 0; i < n;) {
-		uint32_t j = i;
-		while (j < n && k[j] == k[i])
-			j++;
-		runs[2 * nr] = j - i;
-		runs[2 * nr + 1] = k[i];
-		nr++;
-		i = j;
-	}
-	qsort(runs, nr, 2 * sizeof(*runs), cmp_run);
-	uint32_t out = 0;
-	for (uint32_t i = 0; i < nr && out < max; i++) {
-		const uint32_t key = runs[2 * i + 1];
-		const uint8_t ip[4] = {key & 0xff, (key >> 8) & 0xff, (key >> 16) & 0xff, key >> 24};
-		uint32_t ent = f->top[((uint32_t)ip[0] << 8) | ip[1]];
-		int b = 2;
-		bool ok = true;
-		while (b < 4 && (ent & GR_FIB6_EXT)) {
-			if (ent & GR_FIB6_SKIP) {
-				const struct gr_fib6_skip *s = &f->skips[ent & GR_FIB6_IDX];
-				if (b + s->n > 4) { // compares bytes past the key
-					ok = false;
-					break;
-				}
-				ent = memcmp(ip + b, s->key, s->n) == 0 ? s->child : s->miss;
-				b += s->n;
-			} else if (ent & GR_FIB6_WIDE) {
-				if (b != 2) { // bytes 3 and 4
-					ok = false;
-					break;
-				}
-				ent = f->groups[(size_t)(ent & GR_FIB6_IDX) * GR_FIB6_GROUP + ((uint32_t)ip[2] << 8) + ip[3]];
-				b = 4;
-			} else {
-				ent = f->groups[(size_t)(ent & GR_FIB6_IDX) * GR_FIB6_GROUP + ip[b++]];
-			}
-		}
-		if (!ok || ent == 0)
-			continue;
-		keys[out] = key;
-		ents[out] = ent;
-		out++;
-	}
-	free(runs);
-	free(k);
-	return (int)out;
+	const struct u32vec *v = kind == GR_FIB6_DIRTY_TOP ? &f->d_top
+		: kind == GR_FIB6_DIRTY_SLOTS             ? &f->d_slots
+		: kind == GR_FIB6_DIRTY_SKIPS             ? &f->d_skips
+							  : NULL;
+	if (v == NULL)
+		return -EINVAL;
+	*list = v->v;
+	*n = v->n;
+	return f->all_dirty ? 1 : 0;
+}
+
+void gr_fib6_dirty_clear(gr_fib6_t *f) {
+	for (uint32_t k = 0; k < f->d_top.n; k++)
+		f->top_dirty[f->d_top.v[k]] = 0;
+	for (uint32_t k = 0; k < f->d_slots.n; k++)
+		f->slot_dirty[f->d_slots.v[k]] = 0;
+	for (uint32_t k = 0; k < f->d_skips.n; k++)
+		f->skip_dirty[f->d_skips.v[k]] = 0;
+	f->d_top.n = f->d_slots.n = f->d_skips.n = 0;
+	f->all_dirty = false;
 }

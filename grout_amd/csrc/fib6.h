@@ -51,7 +51,9 @@ void gr_fib6_free(gr_fib6_t *);
 int gr_fib6_add(gr_fib6_t *, const uint8_t ip[16], uint8_t prefixlen, uint32_t nh, int replace);
 // 0 or -ENOENT.
 int gr_fib6_del(gr_fib6_t *, const uint8_t ip[16], uint8_t prefixlen);
-// Repaint the trie if routes changed since the last build: 0 or -ENOSPC.
+// Routes are painted into the plain trie as they are added and deleted; a
+// build brings the image (the tables the kernel walks) up to date along the
+// changed paths only: 0, -ENOSPC (no group slot left) or -ENOMEM.
 int gr_fib6_build(gr_fib6_t *);
 // Longest-prefix match through the painted trie (as the kernel walks it).
 uint32_t gr_fib6_lookup(const gr_fib6_t *, const uint8_t ip[16]);
@@ -63,7 +65,7 @@ const uint32_t *gr_fib6_groups(const gr_fib6_t *);
 uint32_t gr_fib6_groups_used(const gr_fib6_t *);
 const struct gr_fib6_skip *gr_fib6_skips(const gr_fib6_t *);
 uint32_t gr_fib6_skips_used(const gr_fib6_t *);
-// Groups the trie had before path compression (for the record).
+// Nodes of the plain (uncompressed) trie.
 uint32_t gr_fib6_groups_painted(const gr_fib6_t *);
 uint32_t gr_fib6_max_groups(const gr_fib6_t *);
 uint32_t gr_fib6_n_routes(const gr_fib6_t *);
@@ -71,13 +73,17 @@ uint32_t gr_fib6_max_slot(const gr_fib6_t *);
 // Build generation: bumps on every repaint that changed the tables.
 uint64_t gr_fib6_generation(const gr_fib6_t *);
 
-// Shortcuts past address bytes 0-3 for the kernel's LDS table: for the /32s
-// holding the most routes (up to max), key = bytes 0-3 (byte 0 in the low
-// bits) and ent = the trie entry the walk reaches after those four bytes
-// (a leaf when the walk ends sooner). /32s whose walk crosses byte 3 in one
-// step (a skip node), or that reach "no route", are left out. Call after
-// gr_fib6_build. Returns the count, or -ENOMEM.
-int gr_fib6_shortcuts(const gr_fib6_t *, uint32_t *keys, uint32_t *ents, uint32_t max);
+// Slots in use (gr_fib6_groups_used is the high-water mark the image spans).
+uint32_t gr_fib6_groups_live(const gr_fib6_t *);
+
+// What the builds since the last gr_fib6_dirty_clear changed in the image:
+// first-level indexes, group slots (1 KiB each) or skip nodes, in no
+// particular order (a slot or skip once). Returns 1 when everything is to be
+// taken as changed (no clear yet: the first upload), 0, or -EINVAL. A commit
+// uploads them to the device copy it writes, then clears.
+enum { GR_FIB6_DIRTY_TOP, GR_FIB6_DIRTY_SLOTS, GR_FIB6_DIRTY_SKIPS };
+int gr_fib6_dirty(const gr_fib6_t *, int kind, const uint32_t **list, uint32_t *n);
+void gr_fib6_dirty_clear(gr_fib6_t *);
 
 #ifdef __cplusplus
 }

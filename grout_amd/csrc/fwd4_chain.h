@@ -38,9 +38,6 @@ __device__ __forceinline__ kctx make_kctx(const fwd4_params &A, const fwd4_edges
 	P.nhf6 = T->nhf6;
 	P.nhf6_lds = nullptr; // set by the kernel that stages them
 	P.nhf6_n = 0;
-	P.sc_lds = nullptr;
-	P.sc_top = nullptr;
-	P.sc_keys = 0;
 	return P;
 }
 
@@ -387,19 +384,8 @@ __device__ __forceinline__ uint32_t chain_fib6(const kctx &P, const fwd4_rx6 &v,
 	uint32_t key[4] = {dst[0], dst[1], dst[2], dst[3]};
 	if ((key[0] & 0xff) == 0xfe && (key[0] & 0xc000) == 0x8000)
 		key[0] = (key[0] & 0xffff) | ((iface_id >> 8) << 16) | ((iface_id & 0xff) << 24);
-	uint32_t ent = 0;
-	int b = 0;
-	if (P.sc_keys && v.top == P.sc_top) {
-		// the walk's state after bytes 0-3 for the view's busiest /32s, from
-		// one LDS bucket: no per-lane gather for the first levels (gr_fib6_shortcuts)
-		const u4v e = P.sc_lds[FWD4_SC_HASH(key[0])];
-		ent = e.x == key[0] ? e.y : e.z == key[0] ? e.w : 0; // empty pairs hold entry 0
-		b = ent ? 4 : 0;
-	}
-	if (b == 0) {
-		ent = gld(v.top + ((byte_of(key, 0) << 8) | byte_of(key, 1)));
-		b = 2;
-	}
+	uint32_t ent = gld(v.top + ((byte_of(key, 0) << 8) | byte_of(key, 1)));
+	int b = 2;
 	while (b < 16 && (ent & 0x80000000u)) {
 		if (ent & GR_FIB6_SKIP) { // skip node: key bytes 0-6, n in byte 7
 			const uint4 k = gld4(v.skips + (ent & GR_FIB6_IDX));

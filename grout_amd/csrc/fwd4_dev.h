@@ -47,9 +47,6 @@ struct kctx {
 	const fwd4_nhf *nhf6;
 	const __attribute__((address_space(3))) u4v *nhf6_lds; // slots 1..nhf6_n staged in LDS
 	uint32_t nhf6_n;
-	const __attribute__((address_space(3))) u4v *sc_lds; // fwd4_params.sc staged in LDS
-	const uint32_t *sc_top;
-	uint32_t sc_keys;
 };
 
 struct rxv {

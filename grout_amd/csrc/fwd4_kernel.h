@@ -155,19 +155,8 @@ struct fwd4_params {
 	uint32_t order; // 2: XCD x (= b % 8) takes region [x * chunk, (x + 1) * chunk),
 	                // its workgroups interleaved in it (grid % 8 == 0)
 	uint32_t spin_max; // polls before a ring wait gives up (0 = RING_SPIN_MAX)
-	// IPv6 shortcuts past address bytes 0-3 (gr_fib6_shortcuts) of one FIB6
-	// copy, staged in LDS: FWD4_SC_BUCKETS buckets of two (key, entry) pairs,
-	// one 16-byte read per lookup; they apply to lanes whose FIB6 is that copy
-	// (sc_top). sc_keys: keys placed (0: no table).
-	const uint32_t *sc; // [4 * FWD4_SC_BUCKETS]
-	const uint32_t *sc_top;
-	uint32_t sc_keys;
 	uint32_t *err; // set to 1 when a workgroup gave up (host-mapped; may be NULL)
 };
-
-#define FWD4_SC_BITS 9
-#define FWD4_SC_BUCKETS (1u << FWD4_SC_BITS)
-#define FWD4_SC_HASH(key) (((key) * 0x9e3779b1u) >> (32 - FWD4_SC_BITS))
 
 // Kernel variants (bit mask, gr_hip_tune): counters, nontemporal loads and
 // stores of the streamed data.

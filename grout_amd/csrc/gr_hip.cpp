@@ -83,12 +83,10 @@ struct fib4_buf {
 	}
 };
 
-// The same for the IPv6 trie: top[65536], groups, skips (fib6.h).
+// The same for the IPv6 trie: top[65536], group slots, skips (fib6.h).
 struct fib6_buf {
 	uint32_t *d6 = nullptr;
 	uint32_t groups = 0; // group capacity
-	uint32_t sc_keys = 0; // shortcut table after the skips: FWD4_SC_BUCKETS x 2 (key, entry); keys placed
-	uint64_t gen = 0; // fib6 generation it holds
 	bool up = false;
 
 	void free_all() {
@@ -136,11 +134,15 @@ struct vrf_fib {
 		max_slot = 0;
 		num_tbl8 = 0;
 	}
-	// IPv6: fib6.h trie, double-buffered the same way (whole-trie uploads)
+	// IPv6: fib6.h trie, double-buffered the same way: what b6[pub6 ^ 1]
+	// misses of the published image (first-level indexes, group slots, skip
+	// nodes, sorted), or everything
 	gr_fib6_t *rib6 = nullptr;
 	fib6_buf b6[2];
 	int pub6 = 1;
 	uint8_t sel6[2] = {1, 1};
+	std::vector<uint32_t> pend6[3];
+	bool pend6_all = true;
 
 	bool uploaded6() const {
 		return b6[pub6].up;
@@ -250,8 +252,6 @@ struct gr_hip_ctx {
 	int host_direct; // host path: the kernel reads / writes pinned host memory itself
 	int node_ptrs; // node path: frames in registered memory are handed over by address
 	int tile_order; // 0: workgroup b takes tiles b, b + G, ...; 1: one contiguous run each
-	int v6_sc; // IPv6 /32 shortcuts staged in LDS (fwd4_params.sc), for VRF sc_vrf; 2: staged only
-	uint16_t sc_vrf; // the VRF with the most IPv6 routes among those committed
 	uint32_t spin_max; // ring waits: polls before giving up (0 = the kernel's default)
 	int untimed; // measurements: no HIP events around launches (gr_hip_queue_kernel_ms sees none)
 	uint32_t time_every; // HIP events around every N-th submit of a queue only (0, 1 = every one)
@@ -738,8 +738,6 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->host_direct = 1; // measured 1.9x the staged copies
 	c->node_ptrs = 0; // staged lines: faster than frames by address, more so with several workers
 	c->tile_order = 0;
-	c->v6_sc = 0;
-	c->sc_vrf = 0;
 	c->spin_max = 0;
 	c->untimed = 0;
 	c->time_every = 1;
@@ -1577,6 +1575,9 @@ extern "C" int gr_hip_fib6_destroy(gr_hip_ctx_t *c, uint16_t vrf) {
 	v.b6[1].free_all();
 	v.pub6 = 1;
 	v.sel6[0] = v.sel6[1] = 1;
+	for (auto &p : v.pend6)
+		p.clear();
+	v.pend6_all = true;
 	gr_fib6_free(rib6);
 	count_v6(c);
 	return 0;
@@ -1614,14 +1615,35 @@ extern "C" int gr_hip_route6_del(gr_hip_ctx_t *c, uint16_t vrf, uint16_t iface_i
 	return gr_fib6_del(v.rib6, key, len);
 }
 
-static uint32_t *sc_of(const fib6_buf &b) {
-	return reinterpret_cast<uint32_t *>(reinterpret_cast<gr_fib6_skip *>(b.d6 + GR_FIB6_TOP + (size_t)b.groups * GR_FIB6_GROUP)
-					    + b.groups);
+// Sorted, duplicate-free union of two index lists.
+static std::vector<uint32_t> index_union(const std::vector<uint32_t> &a, const std::vector<uint32_t> &b) {
+	std::vector<uint32_t> all(a);
+	all.insert(all.end(), b.begin(), b.end());
+	std::sort(all.begin(), all.end());
+	all.erase(std::unique(all.begin(), all.end()), all.end());
+	return all;
 }
 
-// Publish a repainted trie (fib6.h): the first level and the groups and
-// skips in use, written whole into the unpublished copy, then the same flip
-// as gr_hip_fib4_commit.
+// Stage runs of consecutive indexes of a host array of `unit`-element items
+// into the same places of a device array.
+template <typename E>
+static void stage_runs(stager &st, E *dev, const E *host, size_t unit, const std::vector<uint32_t> &idx) {
+	for (size_t i = 0; i < idx.size();) {
+		size_t j = i + 1;
+		while (j < idx.size() && idx[j] == idx[j - 1] + 1)
+			j++;
+		memcpy(st.add(dev + (size_t)idx[i] * unit, (j - i) * unit), host + (size_t)idx[i] * unit,
+		       (j - i) * unit * sizeof(E));
+		i = j;
+	}
+}
+
+// Publish the VRF's IPv6 trie: bring the host image up to date along the
+// paths the route changes touched (gr_fib6_build), write into the
+// unpublished copy what it misses -- its pending lists (the previous
+// commit's changes) and this commit's: first-level entries, 1 KiB group
+// slots, skip nodes -- then flip like gr_hip_fib4_commit. The first commit
+// into a copy writes it whole.
 extern "C" int gr_hip_fib6_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 	if (c == nullptr || vrf == 0 || vrf >= c->max_ifaces)
 		return -EINVAL;
@@ -1630,72 +1652,84 @@ extern "C" int gr_hip_fib6_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 	vrf_fib &v = c->vrfs[vrf];
 	if (v.rib6 == nullptr)
 		return -ENONET;
+	const uint64_t t0 = now_us();
 	int r = gr_fib6_build(v.rib6);
 	if (r < 0)
 		return r;
-	const uint64_t gen = gr_fib6_generation(v.rib6);
-	if (v.uploaded6() && v.b6[v.pub6].gen == gen)
-		return 0;
+	// this commit's changes
+	std::vector<uint32_t> d[3];
+	bool d_all = false;
+	for (int k = 0; k < 3; k++) {
+		const uint32_t *l = nullptr;
+		uint32_t n = 0;
+		const int all = gr_fib6_dirty(v.rib6, k, &l, &n);
+		if (all < 0)
+			return all;
+		d_all |= all != 0;
+		d[k].assign(l, l + n);
+		std::sort(d[k].begin(), d[k].end());
+	}
+	if (!d_all && d[0].empty() && d[1].empty() && d[2].empty() && v.uploaded6())
+		return 0; // nothing to publish
 	const int w = v.pub6 ^ 1;
 	fib6_buf &b = v.b6[w];
+	const bool full = d_all || v.pend6_all || !b.up;
 	const uint32_t B = c->gen ^ 1;
+	uint64_t t1 = t0;
 	{
 		std::shared_lock<std::shared_mutex> l(c->mu); // submitters go on
-		const uint32_t groups = gr_fib6_groups_used(v.rib6), skips = gr_fib6_skips_used(v.rib6);
-		if (b.d6 == nullptr) { // sized for the VRF's group capacity once: top, groups, skips
+		if (b.d6 == nullptr) { // sized for the VRF's group capacity once: top, group slots, skips
 			const uint32_t cap = gr_fib6_max_groups(v.rib6);
 			HCK(hipMalloc(&b.d6, ((size_t)GR_FIB6_TOP + (size_t)cap * GR_FIB6_GROUP) * sizeof(uint32_t)
-						     + (size_t)cap * sizeof(gr_fib6_skip) + FWD4_SC_BUCKETS * 16));
+						     + (size_t)cap * sizeof(gr_fib6_skip)));
 			b.groups = cap;
 		}
+		gr_fib6_skip *d_skips = reinterpret_cast<gr_fib6_skip *>(b.d6 + GR_FIB6_TOP + (size_t)b.groups * GR_FIB6_GROUP);
 		stager st(c);
-		memcpy(st.add(b.d6, GR_FIB6_TOP), gr_fib6_top(v.rib6), (size_t)GR_FIB6_TOP * sizeof(uint32_t));
-		if (groups)
-			memcpy(st.add(b.d6 + GR_FIB6_TOP, (size_t)groups * GR_FIB6_GROUP), gr_fib6_groups(v.rib6),
-			       (size_t)groups * GR_FIB6_GROUP * sizeof(uint32_t));
-		if (skips)
-			memcpy(st.add(reinterpret_cast<gr_fib6_skip *>(b.d6 + GR_FIB6_TOP + (size_t)b.groups * GR_FIB6_GROUP),
-				      skips),
-			       gr_fib6_skips(v.rib6), (size_t)skips * sizeof(gr_fib6_skip));
-		// the busiest /32s' walk state past byte 3, two per hash bucket, busiest
-		// first (a key whose bucket is full is left to the trie)
-		uint32_t sk[2 * FWD4_SC_BUCKETS], se[2 * FWD4_SC_BUCKETS];
-		const int ns = gr_fib6_shortcuts(v.rib6, sk, se, 2 * FWD4_SC_BUCKETS);
-		if (ns < 0)
-			return ns;
-		uint32_t *img = st.add(sc_of(b), 4 * FWD4_SC_BUCKETS);
-		memset(img, 0, FWD4_SC_BUCKETS * 16);
-		b.sc_keys = 0;
-		for (int i = 0; i < ns; i++) {
-			uint32_t *k = img + 4 * FWD4_SC_HASH(sk[i]);
-			if (k[1] != 0)
-				k += 2;
-			if (k[1] != 0)
-				continue;
-			k[0] = sk[i];
-			k[1] = se[i];
-			b.sc_keys++;
+		if (full) {
+			const uint32_t groups = gr_fib6_groups_used(v.rib6), skips = gr_fib6_skips_used(v.rib6);
+			memcpy(st.add(b.d6, GR_FIB6_TOP), gr_fib6_top(v.rib6), (size_t)GR_FIB6_TOP * sizeof(uint32_t));
+			if (groups)
+				memcpy(st.add(b.d6 + GR_FIB6_TOP, (size_t)groups * GR_FIB6_GROUP), gr_fib6_groups(v.rib6),
+				       (size_t)groups * GR_FIB6_GROUP * sizeof(uint32_t));
+			if (skips)
+				memcpy(st.add(d_skips, skips), gr_fib6_skips(v.rib6), (size_t)skips * sizeof(gr_fib6_skip));
+		} else {
+			stage_runs(st, b.d6, gr_fib6_top(v.rib6), 1, index_union(v.pend6[0], d[0]));
+			stage_runs(st, b.d6 + GR_FIB6_TOP, gr_fib6_groups(v.rib6), GR_FIB6_GROUP, index_union(v.pend6[1], d[1]));
+			stage_runs(st, d_skips, gr_fib6_skips(v.rib6), 1, index_union(v.pend6[2], d[2]));
 		}
-		if (c->sc_vrf == 0 || c->vrfs[c->sc_vrf].rib6 == nullptr
-		    || gr_fib6_n_routes(v.rib6) >= gr_fib6_n_routes(c->vrfs[c->sc_vrf].rib6))
-			c->sc_vrf = vrf;
-		b.gen = gen;
 		b.up = true;
 		views_follow_published(c, B);
 		v.sel6[B] = (uint8_t)w;
 		stage_rx(st, c, B);
+		t1 = now_us();
 		r = retire_wait(c);
 		if (r == 0)
 			r = st.flush();
 		if (r == 0 && hipEventRecord(c->ready_ev[B], c->ctl) != hipSuccess)
 			r = -EIO;
 		if (r != 0) {
-			b.up = false;
+			b.up = false; // half written: rewritten in full next time
 			views_follow_published(c, B);
 			return r;
 		}
 	}
-	return publish(c, B, [&] { v.pub6 = w; });
+	gr_fib6_dirty_clear(v.rib6);
+	const uint64_t t2 = now_us();
+	r = publish(c, B, [&] {
+		const bool old_up = v.b6[v.pub6].up;
+		v.pub6 = w;
+		// the copy just unpublished misses this commit's changes
+		v.pend6_all = d_all || !old_up;
+		for (int k = 0; k < 3; k++)
+			v.pend6[k] = std::move(d[k]);
+	});
+	const uint64_t t3 = now_us();
+	c->commit_us[0].store((uint32_t)(t1 - t0), std::memory_order_relaxed);
+	c->commit_us[1].store((uint32_t)(t2 - t1), std::memory_order_relaxed);
+	c->commit_us[2].store((uint32_t)(t3 - t2), std::memory_order_relaxed);
+	return r;
 }
 
 extern "C" int gr_hip_fib6_lookup_host(gr_hip_ctx_t *c, uint16_t vrf, uint16_t iface_id, const uint8_t ip[16],
@@ -1892,17 +1926,6 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	// as many as the geometry's LDS leaves room for (IPv6 given up first)
 	uint32_t n4 = c->nh_hi < gr_fwd4_ring_nhf_max() ? c->nh_hi : gr_fwd4_ring_nhf_max();
 	uint32_t n6 = c->v6_routes ? n4 : 0;
-	uint32_t sc = 0; // shortcut table, in 16-byte LDS units
-	if (c->v6_sc && c->v6_routes && c->sc_vrf != 0) {
-		const vrf_fib &v = c->vrfs[c->sc_vrf];
-		const fib6_buf &b = v.b6[v.sel6[g]];
-		if (v.rib6 != nullptr && b.up && b.sc_keys) {
-			A.sc = sc_of(b);
-			A.sc_top = b.d6;
-			A.sc_keys = b.sc_keys | (c->v6_sc == 2 ? 0x80000000u : 0);
-			sc = FWD4_SC_BUCKETS;
-		}
-	}
 	int occ;
 	{
 		std::lock_guard<std::mutex> ol(c->occ_mu);
@@ -1919,12 +1942,7 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 				e.occ[v] = gr_fwd4_ring_occupancy(v, cfg, staged);
 			return e;
 		};
-		const gr_hip_ctx::occ_entry *e = &occ_of(n4 + n6 + sc);
-		if (e->occ[variant] <= 0 && sc) {
-			sc = 0;
-			A.sc_keys = 0;
-			e = &occ_of(n4 + n6);
-		}
+		const gr_hip_ctx::occ_entry *e = &occ_of(n4 + n6);
 		if (e->occ[variant] <= 0 && n6) {
 			n6 = 0;
 			e = &occ_of(n4);
@@ -2004,15 +2022,6 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < 0 || value > 2)
 			return -EINVAL;
 		c->tile_order = value;
-	} else if (strcmp(key, "v6_shortcut") == 0) {
-		if (value < 0 || value > 2)
-			return -EINVAL;
-		c->v6_sc = value;
-	} else if (strcmp(key, "v6_shortcuts") == 0) { // read: the keys in VRF `value`'s shortcut table
-		if (value <= 0 || (uint32_t)value >= c->max_ifaces || c->vrfs[value].rib6 == nullptr
-		    || !c->vrfs[value].uploaded6())
-			return -ENONET;
-		return (int)c->vrfs[value].b6[c->vrfs[value].pub6].sc_keys;
 	} else if (strcmp(key, "host_direct") == 0) {
 		c->host_direct = value != 0;
 	} else if (strcmp(key, "fib_format_of") == 0) { // read: the format VRF `value` is on the device in

@@ -590,21 +590,12 @@ def test_tile_orders(fastpath, order):
 
 # ---- IPv6
 
-@pytest.fixture(params=[0, 1], ids=["trie", "shortcut"])
-def v6sc(request, fastpath):
-    """Both IPv6 first-level paths: the trie from the top (gather per level)
-    and the /32 shortcut table staged in LDS (gr_hip_tune "v6_shortcut")."""
-    fastpath.tune("v6_shortcut", request.param)
-    yield request.param
-    fastpath.tune("v6_shortcut", 0)
-
-
 @functools.lru_cache(maxsize=None)
 def _fullview6_big():
     return T.config_fullview6(count=100_000)
 
 
-def test_fullview6_stream(fastpath, v6sc):
+def test_fullview6_stream(fastpath):
     """IPv6 forwarding over a 100k-route IPv6 view, 2^20 packets."""
     t = _fullview6_big()
     fr, me = S.stream6(1 << 20, S.SEED_FULLVIEW6 + 1, t.route6_array())
@@ -614,11 +605,10 @@ def test_fullview6_stream(fastpath, v6sc):
     assert (g[1]["edge"] == abi.EDGE["port_output"]).mean() > 0.99
     info = fastpath.fib6_info(1)
     assert info["routes"] == len(t.route6_array()) and info["groups_used"] > 20_000  # a deep, path-compressed trie
-    assert 300 < fastpath.tune("v6_shortcuts", 1) <= 1024  # most busy /32s find room in a bucket
 
 
 @pytest.mark.parametrize("seed", [1, 2])
-def test_clustered_routes6_stream(fastpath, seed, v6sc):
+def test_clustered_routes6_stream(fastpath, seed):
     """IPv6 forwarding over clustered tables whose tries widen at bytes 2-5
     (scenarios.clustered_routes6: wide groups and widened one-byte skips
     below the first level, the kernel's WIDE branch at several depths)."""
@@ -636,7 +626,7 @@ def test_clustered_routes6_stream(fastpath, seed, v6sc):
     assert (g[1]["edge"] == abi.EDGE["port_output"]).mean() > 0.9
 
 
-def test_mixed_v4_v6_stream(fastpath, v6sc):
+def test_mixed_v4_v6_stream(fastpath):
     """IPv4 and IPv6 packets interleaved in every wave (divergent chains)."""
     t, _ = SC.corpus_topology()
     rng = np.random.default_rng(46)
@@ -649,7 +639,7 @@ def test_mixed_v4_v6_stream(fastpath, v6sc):
     compare(oracle.Oracle(t).process(fr, me), run_gpu(fastpath, t, fr, me))
 
 
-def test_live_route6_updates(fastpath, v6sc):
+def test_live_route6_updates(fastpath):
     """route6 add / replace / delete after the first commit, then parity
     (rib6_insert_or_replace / rib6_delete, modules/ip6/control/route.c), one
     commit per kind of change so that the trie's two device copies alternate;
@@ -688,6 +678,26 @@ def test_live_route6_updates(fastpath, v6sc):
     assert (g[1]["edge"] == abi.EDGE["ip6_error_dest_unreach"]).sum() > 0
     for x in list(r[idx[:20]]) + list(rep[:20]) + list(new[:20]):
         assert fastpath.fib6_lookup(1, bytes(x["ip"])) == o.lpm6(1, bytes(x["ip"]))
+    # then many small commits through both copies (the incremental uploads:
+    # each copy gets the changes it missed, the previous commit's and its own)
+    live = np.ones(len(r), dtype=bool)
+    live[idx[:500]] = False
+    for rnd in range(16):
+        for i in rng.choice(len(r) - 1, 60, replace=False):
+            ip = np.ascontiguousarray(r["ip"][i])
+            pl = int(r["prefixlen"][i])
+            if live[i] and rnd % 3 != 2:
+                fastpath.route6_del(1, bytes(r["ip"][i]), pl)
+                assert o.L.or_route6_del(o.h, 1, 0, ip.ctypes.data, pl) == 0
+                live[i] = False
+            else:
+                x = r[i:i + 1].copy()
+                x["nh"] = T.N_FULLVIEW6_NH // 2 + rng.integers(1, T.N_FULLVIEW6_NH // 2)
+                x["nh"] += int(r["nh"].min()) - 1
+                fastpath.route6_add(x, replace=True)
+                assert o.L.or_route6_add(o.h, x.ctypes.data, 1, 1) == 0
+                live[i] = True
+        commit_and_compare()
     fresh_fastpath_state(fastpath, T.config_single_route())  # drop the modified state
 
 

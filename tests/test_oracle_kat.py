@@ -336,11 +336,12 @@ def _wide_entries(host, f):
     return int(((allv & 0xE0000000) == 0xA0000000).sum())
 
 
-@pytest.mark.parametrize("max_groups", [1 << 16, 300])
+@pytest.mark.parametrize("max_groups", [1 << 16, 200])
 def test_fib6_level_compression(max_groups):
     """Dense /48s (fib_inject -6's largest bucket shape: 2400:0:vvvv:vvvv::/48)
     make wide groups (two bytes per gather) when the group capacity allows,
-    and the trie stays exact either way (300 groups: no room to widen)."""
+    and the trie stays exact either way (200 group slots: no room for the 256
+    slots of a wide group)."""
     host = abi.host()
     n = 40_000
     r = np.zeros(n, dtype=abi.ROUTE6_DT)
@@ -446,42 +447,117 @@ def _walk_from(host, f, ip, ent, b):
     return 0 if ent & EXT else ent
 
 
+def _image(host, f):
+    """The device image of a trie (fib6.h): first level, group slots up to the
+    high-water mark, skip nodes (as u32 quadruples)."""
+    import ctypes
+    _wide_entries(host, f)  # accessor signatures
+    host.gr_fib6_dirty.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                   ctypes.POINTER(ctypes.c_uint32)]
+    host.gr_fib6_dirty.restype = ctypes.c_int
+    ng, ns = host.gr_fib6_groups_used(f), host.gr_fib6_skips_used(f)
+    top = np.ctypeslib.as_array(ctypes.cast(host.gr_fib6_top(f), ctypes.POINTER(ctypes.c_uint32)), shape=(65536,))
+    grp = np.ctypeslib.as_array(ctypes.cast(host.gr_fib6_groups(f), ctypes.POINTER(ctypes.c_uint32)),
+                                shape=(max(ng, 1) * 256,))[:ng * 256].reshape(-1, 256)
+    sk = np.ctypeslib.as_array(ctypes.cast(host.gr_fib6_skips(f), ctypes.POINTER(ctypes.c_uint32)),
+                               shape=(max(ns, 1) * 4,))[:ns * 4].reshape(-1, 4)
+    return top.copy(), grp.copy(), sk.copy()
+
+
+def _dirty(host, f, kind):
+    import ctypes
+    host.gr_fib6_dirty.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                   ctypes.POINTER(ctypes.c_uint32)]
+    host.gr_fib6_dirty.restype = ctypes.c_int
+    host.gr_fib6_dirty_clear.argtypes = [ctypes.c_void_p]
+    p, n = ctypes.c_void_p(), ctypes.c_uint32()
+    all_ = host.gr_fib6_dirty(f, kind, ctypes.byref(p), ctypes.byref(n))
+    assert all_ >= 0
+    v = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint32)), shape=(n.value,)).copy() \
+        if n.value else np.zeros(0, np.uint32)
+    return bool(all_), v
+
+
+def _referenced(top, grp, sk):
+    """Group slots and skip nodes the image reaches from its first level."""
+    slots, skips = set(), set()
+    todo = [top]
+    while todo:
+        e = np.concatenate([np.asarray(x, dtype=np.uint32).ravel() for x in todo])
+        todo = []
+        e = e[(e & 0x80000000) != 0]
+        sk_i = (e[(e & 0x40000000) != 0] & 0x1FFFFFFF).tolist()
+        wide = (e[((e & 0x40000000) == 0) & ((e & 0x20000000) != 0)] & 0x1FFFFFFF).tolist()
+        plain = (e[(e & 0x60000000) == 0] & 0x1FFFFFFF).tolist()
+        new = [s for s in plain if s not in slots] + [w + k for w in wide for k in range(256) if w + k not in slots]
+        slots.update(new)
+        if new:
+            todo.append(grp[np.array(new, dtype=np.int64)])
+        nk = [k for k in sk_i if k not in skips]
+        skips.update(nk)
+        if nk:
+            todo.append(sk[np.array(nk, dtype=np.int64), 2])  # struct gr_fib6_skip: child at byte 8
+    return np.array(sorted(slots), dtype=np.int64), np.array(sorted(skips), dtype=np.int64)
+
+
 @pytest.mark.parametrize("view", ["fullview6", "clustered"])
-def test_fib6_shortcuts_resume_exact(view):
-    """gr_fib6_shortcuts (the kernel's LDS table past address bytes 0-3):
-    resuming the walk at byte 4 from a /32's shortcut gives the full walk's
-    (and the RIB's) answer, for addresses under the busiest /32s."""
+def test_fib6_incremental_publication(view):
+    """Route churn, committed in rounds, as gr_hip_fib6_commit publishes it:
+    two device copies written in turn, each with the changes it missed (the
+    previous commit's dirty lists) and this commit's, never the whole trie.
+    After every commit the copy just written equals the host image on every
+    slot and skip node the image reaches, lookups through the trie equal the
+    RIB's longest match, and a commit of 100 changes touches a small share of
+    the image (the trie is repainted along the changed paths only)."""
     import scenarios as SC
     host = abi.host()
+    rng = np.random.default_rng(0x1C6)
     if view == "fullview6":
-        r = T.config_fullview6().route6_array()
+        r = T.config_fullview6(count=60_000).route6_array()
     else:
-        r = np.ascontiguousarray(SC.clustered_routes6(3), dtype=abi.ROUTE6_DT)
-        r["nh"] = 1 + np.arange(len(r)) % 97  # nh left to the caller
-    f = _fib6_of(host, r)
-    keys = np.zeros(512, dtype=np.uint32)
-    ents = np.zeros(512, dtype=np.uint32)
-    n = host.gr_fib6_shortcuts(f, keys.ctypes.data, ents.ctypes.data, 512)
-    assert 0 < n <= 512
-    assert len(set(keys[:n].tolist())) == n and (ents[:n] != 0).all()
-    sc = dict(zip(keys[:n].tolist(), ents[:n].tolist()))
-    rng = np.random.default_rng(0x5C)
-    picked = r[rng.integers(0, len(r), 4000)]
-    checked = 0
-    for x in picked:
-        ip = np.ascontiguousarray(x["ip"]).copy()
-        nb = int(x["prefixlen"])
-        host_bits = rng.integers(0, 256, 16, dtype=np.uint8)
-        for i in range(16):  # random host bits under the prefix
-            keep = max(0, min(8, nb - 8 * i))
-            m = (0xFF00 >> keep) & 0xFF
-            ip[i] = (int(ip[i]) & m) | (int(host_bits[i]) & ~m & 0xFF)
-        key = int(ip[0]) | int(ip[1]) << 8 | int(ip[2]) << 16 | int(ip[3]) << 24
-        if key not in sc:
-            continue
-        want = host.gr_fib6_lookup(f, ip.ctypes.data)
-        assert want == host.gr_fib6_lookup_rib(f, ip.ctypes.data)
-        assert _walk_from(host, f, ip, sc[key], 4) == want
-        checked += 1
-    assert checked > 500
+        r = np.ascontiguousarray(SC.clustered_routes6(2), dtype=abi.ROUTE6_DT)
+        r["nh"] = 1 + np.arange(len(r)) % 97
+    f = host.gr_fib6_new(len(r) + 16, max(1 << 16, 4 * len(r)))
+    live = rng.random(len(r)) < 0.9
+    for x in r[live]:
+        ip = np.ascontiguousarray(x["ip"])
+        assert host.gr_fib6_add(f, ip.ctypes.data, int(x["prefixlen"]), int(x["nh"]), 0) == 0
+    assert host.gr_fib6_build(f) == 0
+    all0, _ = _dirty(host, f, 1)  # (sets the accessors' signatures)
+    assert all0  # the first upload is whole
+    copies = [_image(host, f), _image(host, f)]  # both written whole
+    pend = (np.zeros(0, np.uint32),) * 3
+    host.gr_fib6_dirty_clear(f)
+    w = 0
+    for rnd in range(12):
+        for i in rng.choice(len(r), 100, replace=False):  # adds, deletes, nexthop changes
+            ip = np.ascontiguousarray(r[i]["ip"])
+            pl = int(r[i]["prefixlen"])
+            if live[i] and rng.random() < 0.5:
+                assert host.gr_fib6_del(f, ip.ctypes.data, pl) == 0
+                live[i] = False
+            else:
+                assert host.gr_fib6_add(f, ip.ctypes.data, pl, int(1 + rng.integers(2000)), 1) == 0
+                live[i] = True
+        assert host.gr_fib6_build(f) == 0
+        top, grp, sk = _image(host, f)
+        d = tuple(_dirty(host, f, k)[1] for k in range(3))  # top, slots, skips
+        assert not _dirty(host, f, 0)[0]
+        w ^= 1
+        ct, cg, cs = copies[w]
+        if len(cg) < len(grp):  # the device copy is sized for the capacity
+            cg = np.concatenate([cg, np.zeros((len(grp) - len(cg), 256), np.uint32)])
+        if len(cs) < len(sk):
+            cs = np.concatenate([cs, np.zeros((len(sk) - len(cs), 4), np.uint32)])
+        ut, us, uk = (np.union1d(a, b).astype(np.int64) for a, b in zip(pend, d))
+        ct[ut], cg[us], cs[uk] = top[ut], grp[us], sk[uk]
+        copies[w] = (ct, cg, cs)
+        pend = d
+        host.gr_fib6_dirty_clear(f)
+        slots, skips = _referenced(top, grp, sk)
+        assert np.array_equal(ct, top)
+        assert np.array_equal(cg[slots], grp[slots]) and np.array_equal(cs[skips], sk[skips])
+        if view == "fullview6":
+            assert len(d[1]) < 0.05 * len(slots), (len(d[1]), len(slots))
+        _fib6_check(host, f, r[live], rng, 3000)
     host.gr_fib6_free(f)
