@@ -1,9 +1,10 @@
 # SPDX-License-Identifier: BSD-3-Clause
-"""FIB load rate and forwarding under route churn (DESIGN.md §4).
+"""FIB load rate and forwarding under route churn (DESIGN.md §6).
 
-1. Load: the 1M-route fib_inject -4 view (smoke/fib_inject.c:245-254 times
-   the injection and prints routes/s) into an empty VRF, one route per
-   gr_hip_route4_add call like fib_inject's one request per route, then one
+1. Load: the 1M-route fib_inject -4 view (--ipv6: fib_inject -6's 200k-route
+   view; smoke/fib_inject.c:245-254 times the injection and prints
+   routes/s) into an empty VRF, one route per gr_hip_route4_add /
+   gr_hip_route6_add call like fib_inject's one request per route, then one
    commit; and again in one batched call. routes/s = routes / (adds + commit).
 2. Churn: the headline batch (2^24 packets over that view) submitted back to
    back for --seconds, without and then with a control thread applying
@@ -11,7 +12,7 @@
    re-adds of random full-view routes, in --period-ms batches, one commit
    per batch). Mpps by wall clock over each window, and the commit latency.
 
-    python tools/fib_churn.py [--seconds 3] [--rate 10000] [--period-ms 10] > out.json
+    python tools/fib_churn.py [--ipv6] [--seconds 3] [--rate 10000] [--period-ms 10] > out.json
 """
 import argparse
 import ctypes
@@ -33,7 +34,9 @@ def main():
     ap.add_argument("--period-ms", type=float, default=10.0, help="one commit per period")
     ap.add_argument("--batch", type=int, default=1 << 24)
     ap.add_argument("--no-per-route", action="store_true")
+    ap.add_argument("--ipv6", action="store_true", help="fib_inject -6's view and an IPv6 stream")
     args = ap.parse_args()
+    v6 = args.ipv6
     import torch
 
     from grout_amd import abi
@@ -41,12 +44,19 @@ def main():
     from grout_amd import topology as T
     from grout_amd.fwd import FastPath, shared_stream
 
-    out = {"tool": "fib_churn"}
-    topo = T.config_fullview()
-    routes = topo.route_array()
-    count = 1_000_000
+    out = {"tool": "fib_churn", "family": "ipv6" if v6 else "ipv4"}
+    if v6:
+        topo = T.config_fullview6()
+        routes = topo.route6_array()
+        count = T.FULLVIEW6_ROUTES
+    else:
+        topo = T.config_fullview()
+        routes = topo.route_array()
+        count = 1_000_000
     view = routes[:count]
     vrf = int(view["vrf_id"][0])
+    add_fn = "gr_hip_route6_add" if v6 else "gr_hip_route4_add"
+    rsize = view.dtype.itemsize
 
     def fresh():
         fp = FastPath(0)
@@ -55,34 +65,53 @@ def main():
         fp.set_reta(topo.reta)
         for v, (mr, nt) in topo.fibs.items():
             fp.fib_create(v, mr, nt)
+        for v, (mr, ng) in topo.fibs6.items():
+            fp.fib6_create(v, mr, ng)
         return fp
+
+    def add(fp, r, replace=False):
+        (fp.route6_add if v6 else fp.route_add)(r, replace=replace)
+
+    def delete(fp, x):
+        if v6:
+            fp.route6_del(vrf, bytes(x["ip"]), int(x["prefixlen"]), int(x["iface_id"]))
+        else:
+            fp.route_del(vrf, int(x["ip"]), int(x["prefixlen"]))
+
+    def commit(fp):
+        (fp.fib6_commit if v6 else fp.fib_commit)(vrf)
 
     # 1. load rates
     if not args.no_per_route:
         fp = fresh()
         L, h = fp.lib, fp.h
         base = view.ctypes.data
+        fn = getattr(L, add_fn)
         t0 = time.perf_counter()
         for i in range(count):
-            r = L.gr_hip_route4_add(h, ctypes.c_void_p(base + 12 * i), 1, 0)
+            r = fn(h, ctypes.c_void_p(base + rsize * i), 1, 0)
             if r:
-                abi.check("gr_hip_route4_add", r)
+                abi.check(add_fn, r)
         t1 = time.perf_counter()
-        fp.fib_commit(vrf)
+        commit(fp)
         t2 = time.perf_counter()
         out["load_per_route"] = {"routes": count, "add_s": round(t1 - t0, 3), "commit_s": round(t2 - t1, 4),
                                  "routes_per_s": round(count / (t2 - t0)),
-                                 "note": "one gr_hip_route4_add per route from Python ctypes, then one commit"}
+                                 "note": "one %s per route from Python ctypes, then one commit" % add_fn}
         print(json.dumps(out["load_per_route"]), file=sys.stderr, flush=True)
         fp.close()
     fp = fresh()
     t0 = time.perf_counter()
-    fp.route_add(view)
+    add(fp, view)
     t1 = time.perf_counter()
-    fp.fib_commit(vrf)
+    commit(fp)
     t2 = time.perf_counter()
-    fp.route_add(routes[count:])  # the address route: the bench topology exactly
-    fp.fib_commit(vrf)
+    if len(routes) > count:
+        add(fp, routes[count:])  # the address route: the bench topology exactly
+    if v6:
+        fp.route_add(topo.route_array())  # the IPv4 routes of the topology
+        fp.fib_commit(vrf)
+    commit(fp)
     t3 = time.perf_counter()
     out["load_batched"] = {"routes": count, "add_s": round(t1 - t0, 3), "commit_s": round(t2 - t1, 4),
                            "routes_per_s": round(count / (t2 - t0)),
@@ -94,7 +123,10 @@ def main():
     # 2. churn
     dev = torch.device("cuda", 0)
     n = args.batch
-    frames, meta = S.stream(n, S.SEED_GPU_BASE, routes=routes)
+    if v6:
+        frames, meta = S.stream6(n, S.SEED_FULLVIEW6, routes[routes["prefixlen"] < 128])
+    else:
+        frames, meta = S.stream(n, S.SEED_GPU_BASE, routes=routes)
     fin = torch.from_numpy(frames.reshape(-1)).to(dev)
     me = torch.from_numpy(meta.view(np.uint8)).to(dev)
     fo = torch.empty(n * abi.LINE, dtype=torch.uint8, device=dev)
@@ -137,17 +169,17 @@ def main():
             rep = view[idx[:k_rep]].copy()
             rep["nh"] = rng.choice(nh_slots, size=k_rep)
             t0 = time.perf_counter()
-            fp.route_add(rep, replace=True)
+            add(fp, rep, replace=True)
             for i in idx[k_rep:]:
-                fp.route_del(vrf, int(view["ip"][i]), int(view["prefixlen"][i]))
+                delete(fp, view[i])
                 live[i] = False
                 deleted.append(i)
             back = [deleted.pop(0) for _ in range(min(k_add, len(deleted) - k_del))] if len(deleted) > k_del else []
             if back:
-                fp.route_add(view[np.array(back)])
+                add(fp, view[np.array(back)])
                 live[np.array(back)] = True
             tc = time.perf_counter()
-            fp.fib_commit(vrf)
+            commit(fp)
             t1 = time.perf_counter()
             lat.append(t1 - t0)
             clat.append(t1 - tc)
@@ -175,7 +207,7 @@ def main():
                                                   np.percentile(np.array(phases), 50, axis=0).round(1).tolist()))})
     out.update({"batch": n, "base": base, "churn": churn, "mpps_ratio": round(churn["mpps"] / base["mpps"], 4),
                 "note": "wall-clock Mpps, submits of 4 launches then a sync, untimed launches; commit latency = "
-                        "route adds/deletes + gr_hip_fib4_commit"})
+                        "route adds/deletes + gr_hip_fib%s_commit" % ("6" if v6 else "4")})
     print(json.dumps(out), flush=True)
     q.close()
     fp.close()
