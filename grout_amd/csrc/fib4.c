@@ -7,7 +7,8 @@
 // direct entry (no more-specific route inside it) or a tbl8 group painted
 // from the trie down to /32. Empty groups are returned to a free list. The
 // result equals a from-scratch longest-prefix-match build, which is what
-// DPDK's dir24_8 maintains incrementally for grout (modules/ip/control/route.c:243,689).
+// DPDK's dir24_8 maintains incrementally for grout (rte_fib_add,
+// modules/ip/control/route.c:243,689).
 #include "fib4.h"
 
 #include <errno.h>

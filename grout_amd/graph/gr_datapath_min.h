@@ -31,7 +31,7 @@ extern "C" {
 #endif
 
 // ---- objects ---------------------------------------------------------------
-// gr_iface_type_t / gr_iface_flags_t (gr_infra.h:18-37), gr_nh_* and
+// gr_iface_type_t / gr_iface_flags_t (gr_infra.h:18-38), gr_nh_* and
 // addr_family_t (gr_nexthop.h:12-40, gr_net_types.h): grout's values.
 typedef uint8_t gr_iface_type_t; // grout: enum : uint8_t (C23)
 enum {

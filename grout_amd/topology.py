@@ -12,7 +12,8 @@ routes exactly as grout's control plane would leave them for the datapath:
 * add_nexthop: a gr_nexthop_info_l3 (gr_nexthop.h:93-105); a MAC makes it
   REACHABLE (l3_nexthop.c:244-250), no address makes it a LINK nexthop
   (l3_nexthop.c:233-238).
-* add_group: GR_NH_T_GROUP with grout's weighted reta (group_nexthop.c:27-56,101-166).
+* add_group: GR_NH_T_GROUP with grout's weighted reta (group_reta_distribute,
+  group_import_info: group_nexthop.c:27-56,101-166).
 * add_route: gr_ip4_route_add_req (modules/ip/api/gr_ip4.h:47-56).
 * IPv6: every VRF also gets a FIB6 (modules/ip6/control/route.c:103-125); an
   IPv6 nexthop address makes an AF_IP6 nexthop; add_address6 mirrors

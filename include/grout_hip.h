@@ -59,14 +59,14 @@ enum {
 	GR_HIP_IFACE_TYPE_COUNT,
 };
 
-// gr_iface_flags_t, gr_infra.h:31-37
+// gr_iface_flags_t, gr_infra.h:31-38
 #define GR_HIP_IFACE_F_UP 0x0001
 #define GR_HIP_IFACE_F_PROMISC 0x0002
 #define GR_HIP_IFACE_F_PACKET_TRACE 0x0004
 #define GR_HIP_IFACE_F_SNAT_STATIC 0x0008
 #define GR_HIP_IFACE_F_SNAT_DYNAMIC 0x0010
 
-// gr_iface_mode_t, gr_infra.h:56-61
+// gr_iface_mode_t, gr_infra.h:56-62
 enum {
 	GR_HIP_IFACE_MODE_VRF = 0,
 	GR_HIP_IFACE_MODE_XC,

@@ -1,6 +1,8 @@
 # SPDX-License-Identifier: BSD-3-Clause
 """Every `file.c:N-M` citation in the repo's sources, tests and docs names
-lines that exist in the mounted reference (or in the repo file it names):
+lines that exist in the mounted reference (or in the repo file it names),
+and those lines hold what the citation talks about (an identifier from its
+clause, or for a smoke script's line the address it configures):
 tools/check_citations.py. Runs where /root/reference is mounted (this
 container), skipped elsewhere; reads the reference as text only."""
 import os

@@ -570,7 +570,7 @@ def test_graph_walk_rcu_delete_in_flight(readers):
     both is on the GPU (iface_destroy / nexthop_destroy, iface.c:702-725,
     nexthop.c:493-518: out of grout's tables, rte_rcu_qsbr_synchronize, then
     the REMOVE / DELETE events and the free). The worker keeps reporting
-    quiescent (main_loop.c:464). With the node's QSBR readers the
+    quiescent (rte_rcu_qsbr_quiescent, main_loop.c:464). With the node's QSBR readers the
     synchronisation returns only once the batch has been handed back and
     through grout's nodes behind the edges, every packet reaches ip_hold with
     the live nexthop, and nothing freed is read. Without them (round 2's

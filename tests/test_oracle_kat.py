@@ -7,7 +7,7 @@
    here the same header follows an Ethernet header addressed to the RX port.
 2. ip_forward's incremental checksum (ip_forward.c:29-32), hand-derived.
 3. The longest-prefix match of both oracle LPMs against brute force.
-4. The five cases of ip6_input's unit test (ip6_input.c:245-318), the hop
+4. The five cases of ip6_input's unit test (ip6_input.c:249-316), the hop
    limit of ip6_forward, and the IPv6 LPM (oracle hash, brute force and the
    product's trie) against each other.
 """
@@ -128,7 +128,7 @@ def test_lpm_vs_brute_force():
         assert o.lpm(1, ip, "dir24") == b
 
 
-# ---- IPv6: the five cases of modules/ip6/datapath/ip6_input.c:245-318
+# ---- IPv6: the five cases of modules/ip6/datapath/ip6_input.c:249-316
 # (ipv6_init_default_mbuf :217-243: version 6, payload 0, next header NONE,
 # hop limit 64, src 0:3:0:3:1:9:8:8, dst 0:3:0:5:2:0:2:4, data_len 40,
 # domain OTHER), restated on frames to a MAC that is not the port's.
@@ -142,23 +142,23 @@ def kat6(**kw):
     return S.frame6(**d)
 
 
-def test_kat6_invalid_version():  # ip6_input.c:245-253
+def test_kat6_invalid_version():  # ip6_input.c:249-258
     assert run(kat_topo(), [kat6(version=5)]) == ["ip6_input_bad_version"]
 
 
-def test_kat6_invalid_src_mcast_addr():  # ip6_input.c:255-266
+def test_kat6_invalid_src_mcast_addr():  # ip6_input.c:260-271
     assert run(kat_topo(), [kat6(src="ffff:ffff:ffff:ffff:ffff:ffff:ffff:ffff")]) == ["ip6_input_bad_addr"]
 
 
-def test_kat6_invalid_dst_unspec_addr():  # ip6_input.c:268-279
+def test_kat6_invalid_dst_unspec_addr():  # ip6_input.c:273-284
     assert run(kat_topo(), [kat6(dst="::")]) == ["ip6_input_bad_addr"]
 
 
-def test_kat6_invalid_dst_mcast_addr():  # ip6_input.c:281-301: scope none, iface-local
+def test_kat6_invalid_dst_mcast_addr():  # ip6_input.c:286-305: scope none, iface-local
     assert run(kat_topo(), [kat6(dst="ff00::1"), kat6(dst="ff01::1")]) == ["ip6_input_bad_addr"] * 2
 
 
-def test_kat6_invalid_mbuf_len():  # ip6_input.c:303-311: data_len = 40 / 2
+def test_kat6_invalid_mbuf_len():  # ip6_input.c:307-316: data_len = 40 / 2
     assert run(kat_topo(), [kat6()], pkt_lens=[14 + 20]) == ["ip6_input_bad_length"]
 
 
@@ -298,13 +298,13 @@ GPU_KATS = [  # (reference test, topology kwargs, frame, pkt_len or None, expect
     ("ip_input.c:337-349", {}, _raw3, None, "ip_input_bad_checksum"),
     ("ip_input.c:351-361", {}, lambda: kat_header(total_len=10), None, "ip_input_bad_length"),
     ("ip_input.c:363-383", dict(snat_dynamic=True, local_nh=True), lambda: kat_header(), None, "ip_input_local_ct"),
-    ("ip6_input.c:245-253", {}, lambda: kat6(version=5), None, "ip6_input_bad_version"),
-    ("ip6_input.c:255-266", {}, lambda: kat6(src="ffff:ffff:ffff:ffff:ffff:ffff:ffff:ffff"), None,
+    ("ip6_input.c:249-258", {}, lambda: kat6(version=5), None, "ip6_input_bad_version"),
+    ("ip6_input.c:260-271", {}, lambda: kat6(src="ffff:ffff:ffff:ffff:ffff:ffff:ffff:ffff"), None,
      "ip6_input_bad_addr"),
-    ("ip6_input.c:268-279", {}, lambda: kat6(dst="::"), None, "ip6_input_bad_addr"),
-    ("ip6_input.c:281-301 scope none", {}, lambda: kat6(dst="ff00::1"), None, "ip6_input_bad_addr"),
-    ("ip6_input.c:281-301 iface-local", {}, lambda: kat6(dst="ff01::1"), None, "ip6_input_bad_addr"),
-    ("ip6_input.c:303-311", {}, lambda: kat6(), 14 + 20, "ip6_input_bad_length"),
+    ("ip6_input.c:273-284", {}, lambda: kat6(dst="::"), None, "ip6_input_bad_addr"),
+    ("ip6_input.c:286-305 scope none", {}, lambda: kat6(dst="ff00::1"), None, "ip6_input_bad_addr"),
+    ("ip6_input.c:286-305 iface-local", {}, lambda: kat6(dst="ff01::1"), None, "ip6_input_bad_addr"),
+    ("ip6_input.c:307-316", {}, lambda: kat6(), 14 + 20, "ip6_input_bad_length"),
 ]
 
 

@@ -32,8 +32,22 @@ Scripts (under smoke/ in the reference):
   bridge_test.sh            ports in a bridge domain (bridge_input)
   ip6_same_peer_test.sh     a link-local address only on its own link
   srv6_test.sh              SRv6 encap and local nexthops (sr6_output, sr6_local)
+  ip_builtin_icmp_test.sh   grout's own pings: the replies, unroutable and unanswered hosts
+  ip6_builtin_icmp_test.sh  the same for IPv6
+  iface_mac_test.sh         secondary MACs: frames for them are another host's
+  nexthop_ageing_test.sh    neighbours REACHABLE, STALE / FAILED, aged out
+  vxlan_test.sh             a VXLAN VTEP, the decapsulated frames back through iface_input
+  bond_active_backup_test.sh frames from the active member with the bond as iface, LACP, bond_output
+  ip_add_del_test.sh        an IPv4 address deleted and added again
+  ip6_add_del_test.sh       an IPv6 address deleted and added again; the port moved to a
+                            VRF, then cross-connected
+
+For the address and ageing scripts, "resolved" names the script's later
+state (the address added again, the neighbours answering again), as each
+function's docstring says.
 """
 import ipaddress
+import os
 
 import numpy as np
 import pytest
@@ -47,6 +61,7 @@ from test_node_shim import RX_DATA_OFF, compare_mbufs, mbufs_for
 GR_MAC = ["02:00:00:00:00:%02x" % p for p in range(4)]  # grout's ports p0..p3
 NS_MAC = ["02:00:00:0a:00:%02x" % n for n in range(4)]  # the namespaces' ends x-p0..x-p3
 PORT = [10, 11, 12, 13]  # iface ids of p0..p3 (1 and 2 are left to the VRF ifaces)
+REF_SMOKE = "/root/reference/smoke"  # read as text by test_probe_lines_are_the_scripts only
 
 
 def eui64_ll(mac):
@@ -80,10 +95,14 @@ class Probe:
     before / after: the edge before and after neighbour resolution; `out`:
     (egress port index, VLAN tag, destination MAC) when it is port_output."""
 
-    def __init__(self, script, line, port, frame, before, after=None, out=None, vlan=0, out_any=None, rss=0):
+    def __init__(self, script, line, port, frame, before, after=None, out=None, vlan=0, out_any=None, rss=0,
+                 iface=None):
         self.script, self.line, self.port, self.frame = script, line, port, frame
         self.before, self.after = before, after if after is not None else before
         self.out, self.out_any, self.vlan, self.rss = out, out_any, vlan, rss
+        # the iface port_rx (or a CPU node going back to iface_input) hands the
+        # frame over with, when it is not the port itself
+        self.iface = iface
 
     @property
     def label(self):
@@ -96,6 +115,11 @@ def v4(port, src, dst, ttl=64, proto=1, vlan=0, dst_mac=None, size=56, df=False)
     length = 14 + 20 + 8 + size if proto == 1 else 14 + 60
     return S.frame(dst_mac=dst_mac or GR_MAC[port], src_mac=NS_MAC[port], src=src, dst=dst, ttl=ttl,
                    proto=proto, length=length, flags_frag=0x4000 if df else 0)
+
+
+def arp(port, dst_mac="ff:ff:ff:ff:ff:ff", src_mac=None):
+    """An ARP frame (a request, broadcast; a reply, to grout's MAC)."""
+    return S.frame(dst_mac=dst_mac, src_mac=src_mac or NS_MAC[port], ethertype=0x0806)
 
 
 def v6(port, src, dst, hop=64, nh=58, dst_mac=None):
@@ -159,7 +183,7 @@ def ip6_forward(resolved):
 def vlan_forward(resolved):
     """smoke/vlan_forward_test.sh: p0.42 and p1.43 over ports p0, p1; the
     namespaces tag their frames (port_rx strips the tag into vlan_id,
-    port_rx.c:225-231, iface_input demuxes it, iface_input.c:64-76)."""
+    port_rx.c:227-232, iface_input demuxes it, iface_input.c:74-86)."""
     s = "vlan_forward_test.sh"
     t = T.Topology()
     t.add_vrf(T.VRF_MAIN)
@@ -182,7 +206,7 @@ def vlan_forward(resolved):
         Probe(s, 27, 0, v4(0, "172.16.0.2", "172.16.0.1"), "ip_input_local", vlan=42),
         # an untagged frame stays on p0 itself, in the same VRF: routed all the same
         Probe(s, 27, 0, v4(0, "172.16.0.2", "172.16.1.2"), "ip_hold", "port_output", (1, 43, NS_MAC[1])),
-        # a tag with no VLAN interface (iface_input.c:70-73)
+        # a tag with no VLAN interface (iface_input.c:80-83)
         Probe(s, 27, 0, v4(0, "172.16.0.2", "172.16.1.2"), "iface_input_unknown_vlan", vlan=44),
     ]
     return t, pr
@@ -303,36 +327,36 @@ def ip_loadbalance(resolved):
 
 
 def ip_fragment(resolved):
-    """smoke/ip_fragment_test.sh: p1's MTU is 1280 (:4). A 1260-byte ping is a
-    1288-byte IP packet: with DF it must fail (ip_error_frag_needed, :20),
-    without DF grout fragments it (ip_fragment, :22); ip_output.c:99-106."""
+    """smoke/ip_fragment_test.sh: p1's MTU is 1280 (:10). A 1260-byte ping is a
+    1288-byte IP packet: with DF it must fail (ip_error_frag_needed, :34),
+    without DF grout fragments it (ip_fragment, :42); ip_output.c:99-106."""
     s = "ip_fragment_test.sh"
     t = T.Topology()
     t.add_vrf(T.VRF_MAIN)
     ports(t, 2)
-    t.ifaces[PORT[1]]["mtu"] = 1280  # port_add p1 mtu 1280 (:4)
-    t.add_address(PORT[0], "172.16.0.1/24")  # :5
-    t.add_address(PORT[1], "172.16.1.1/24")  # :6
+    t.ifaces[PORT[1]]["mtu"] = 1280  # port_add p1 mtu 1280 (:10)
+    t.add_address(PORT[0], "172.16.0.1/24")  # :11
+    t.add_address(PORT[1], "172.16.1.1/24")  # :12
     if resolved:
         neighbour(t, T.VRF_MAIN, PORT[0], "172.16.0.2", NS_MAC[0])
         neighbour(t, T.VRF_MAIN, PORT[1], "172.16.1.2", NS_MAC[1])
     pr = [
-        Probe(s, 18, 0, v4(0, "172.16.0.2", "172.16.1.2"), "ip_hold", "port_output", (1, 0, NS_MAC[1])),
-        Probe(s, 20, 0, v4(0, "172.16.0.2", "172.16.1.2", size=1260, df=True), "ip_error_frag_needed"),
-        Probe(s, 22, 0, v4(0, "172.16.0.2", "172.16.1.2", size=1260), "ip_fragment"),
+        Probe(s, 27, 0, v4(0, "172.16.0.2", "172.16.1.2"), "ip_hold", "port_output", (1, 0, NS_MAC[1])),
+        Probe(s, 34, 0, v4(0, "172.16.0.2", "172.16.1.2", size=1260, df=True), "ip_error_frag_needed"),
+        Probe(s, 42, 0, v4(0, "172.16.0.2", "172.16.1.2", size=1260), "ip_fragment"),
         # exactly the MTU passes, one byte more does not
-        Probe(s, 22, 0, v4(0, "172.16.0.2", "172.16.1.2", size=1252, df=True), "ip_hold", "port_output",
+        Probe(s, 42, 0, v4(0, "172.16.0.2", "172.16.1.2", size=1252, df=True), "ip_hold", "port_output",
               (1, 0, NS_MAC[1])),
-        Probe(s, 22, 0, v4(0, "172.16.0.2", "172.16.1.2", size=1253, df=True), "ip_error_frag_needed"),
+        Probe(s, 42, 0, v4(0, "172.16.0.2", "172.16.1.2", size=1253, df=True), "ip_error_frag_needed"),
         # the replies come back the other way, on the 1500-byte port
-        Probe(s, 22, 1, v4(1, "172.16.1.2", "172.16.0.2", size=1260), "ip_hold", "port_output", (0, 0, NS_MAC[0])),
+        Probe(s, 42, 1, v4(1, "172.16.1.2", "172.16.0.2", size=1260), "ip_hold", "port_output", (0, 0, NS_MAC[0])),
     ]
     return t, pr
 
 
 def ipip_encap(resolved):
     """smoke/ipip_encap_test.sh: tun1 is an IPIP interface (local 172.16.1.1,
-    remote 172.16.1.2) holding 10.98.0.1/24 (:6-7). n0's ping to 10.98.0.2
+    remote 172.16.1.2) holding 10.98.0.1/24 (:11-12). n0's ping to 10.98.0.2
     leaves ip_output through tun1's type edge, ipip_output (ipip/datapath_out.c:91),
     whether or not a neighbour is resolved (ip_output.c:110-122); the tunnelled
     packets n1 sends back are for grout's own 172.16.1.1 (ipip_input on the CPU)."""
@@ -341,23 +365,23 @@ def ipip_encap(resolved):
     t.add_vrf(T.VRF_MAIN)
     ports(t, 2)
     TUN = 30
-    t.add_address(PORT[0], "10.99.0.1/24")  # :4
-    t.add_address(PORT[1], "172.16.1.1/24")  # :5
-    t.add_iface(TUN, "IPIP")  # :6
-    t.add_address(TUN, "10.98.0.1/24")  # :7
+    t.add_address(PORT[0], "10.99.0.1/24")  # :9
+    t.add_address(PORT[1], "172.16.1.1/24")  # :10
+    t.add_iface(TUN, "IPIP")  # :11
+    t.add_address(TUN, "10.98.0.1/24")  # :12
     if resolved:
         neighbour(t, T.VRF_MAIN, PORT[0], "10.99.0.2", NS_MAC[0])
         neighbour(t, T.VRF_MAIN, PORT[1], "172.16.1.2", NS_MAC[1])
     pr = [
-        Probe(s, 20, 0, v4(0, "10.99.0.2", "10.98.0.2"), "ipip_output"),
-        Probe(s, 21, 1, v4(1, "172.16.1.2", "172.16.1.1", proto=4), "ip_input_local"),  # IPIP to grout
-        Probe(s, 20, 0, v4(0, "10.99.0.2", "10.98.0.2", ttl=1), "ip_error_ttl_exceeded"),
+        Probe(s, 27, 0, v4(0, "10.99.0.2", "10.98.0.2"), "ipip_output"),
+        Probe(s, 28, 1, v4(1, "172.16.1.2", "172.16.1.1", proto=4), "ip_input_local"),  # IPIP to grout
+        Probe(s, 27, 0, v4(0, "10.99.0.2", "10.98.0.2", ttl=1), "ip_error_ttl_exceeded"),
     ]
     return t, pr
 
 
 def snat44(resolved):
-    """smoke/snat44_test.sh: dynamic SNAT on p0 (:6; GR_IFACE_F_SNAT_DYNAMIC,
+    """smoke/snat44_test.sh: dynamic SNAT on p0 (:11; GR_IFACE_F_SNAT_DYNAMIC,
     modules/policy/control/snat44_dynamic.c:39). n1's ping to 172.16.0.2 leaves
     through p0: the fast path stops where ip_output calls snat44_process
     (ip_output_snat, run on the CPU); the replies to the SNAT address arrive on
@@ -366,25 +390,25 @@ def snat44(resolved):
     t = T.Topology()
     t.add_vrf(T.VRF_MAIN)
     ports(t, 2)
-    t.ifaces[PORT[0]]["flags"] |= abi.IFACE_F_SNAT_DYNAMIC  # :6
-    t.add_address(PORT[0], "172.16.0.1/24")  # :4
-    t.add_address(PORT[1], "10.99.0.1/24")  # :5
+    t.ifaces[PORT[0]]["flags"] |= abi.IFACE_F_SNAT_DYNAMIC  # :11
+    t.add_address(PORT[0], "172.16.0.1/24")  # :9
+    t.add_address(PORT[1], "10.99.0.1/24")  # :10
     if resolved:
         neighbour(t, T.VRF_MAIN, PORT[0], "172.16.0.2", NS_MAC[0])
         neighbour(t, T.VRF_MAIN, PORT[1], "10.99.0.99", NS_MAC[1])
     pr = [
-        Probe(s, 20, 1, v4(1, "10.99.0.99", "172.16.0.2"), "ip_output_snat"),
-        Probe(s, 20, 0, v4(0, "172.16.0.2", "172.16.0.1"), "ip_input_local_ct"),
-        Probe(s, 24, 1, v4(1, "10.99.0.99", "172.16.0.2", proto=6), "ip_output_snat"),  # socat TCP
-        Probe(s, 28, 1, v4(1, "10.99.0.99", "172.16.0.2", proto=17), "ip_output_snat"),  # socat UDP
+        Probe(s, 27, 1, v4(1, "10.99.0.99", "172.16.0.2"), "ip_output_snat"),
+        Probe(s, 27, 0, v4(0, "172.16.0.2", "172.16.0.1"), "ip_input_local_ct"),
+        Probe(s, 31, 1, v4(1, "10.99.0.99", "172.16.0.2", proto=6), "ip_output_snat"),  # socat TCP
+        Probe(s, 36, 1, v4(1, "10.99.0.99", "172.16.0.2", proto=17), "ip_output_snat"),  # socat UDP
         # p1 has no SNAT policy: n1's ping to grout's own p1 address stays plain local
-        Probe(s, 20, 1, v4(1, "10.99.0.99", "10.99.0.1"), "ip_input_local"),
+        Probe(s, 27, 1, v4(1, "10.99.0.99", "10.99.0.1"), "ip_input_local"),
     ]
     return t, pr
 
 
 def dnat44(resolved):
-    """smoke/dnat44_test.sh: a static DNAT of 172.16.0.99 on p0 (:6): a
+    """smoke/dnat44_test.sh: a static DNAT of 172.16.0.99 on p0 (:11): a
     GR_NH_T_DNAT nexthop and its /32 route in p0's VRF
     (modules/policy/api/dnat44.c:148-166). n0's ping to 172.16.0.99 leaves
     ip_input by that nexthop type's edge, dnat44_static."""
@@ -392,44 +416,44 @@ def dnat44(resolved):
     t = T.Topology()
     t.add_vrf(T.VRF_MAIN)
     ports(t, 2)
-    t.add_address(PORT[0], "172.16.0.1/24")  # :4
-    t.add_address(PORT[1], "10.99.0.1/24")  # :5
-    t.add_route(T.VRF_MAIN, "172.16.0.99/32", t.add_nexthop(PORT[0], nh_type="DNAT"))  # :6
+    t.add_address(PORT[0], "172.16.0.1/24")  # :9
+    t.add_address(PORT[1], "10.99.0.1/24")  # :10
+    t.add_route(T.VRF_MAIN, "172.16.0.99/32", t.add_nexthop(PORT[0], nh_type="DNAT"))  # :11
     if resolved:
         neighbour(t, T.VRF_MAIN, PORT[0], "172.16.0.2", NS_MAC[0])
         neighbour(t, T.VRF_MAIN, PORT[1], "10.99.0.99", NS_MAC[1])
     pr = [
-        Probe(s, 18, 0, v4(0, "172.16.0.2", "172.16.0.99"), "dnat44_static"),
+        Probe(s, 26, 0, v4(0, "172.16.0.2", "172.16.0.99"), "dnat44_static"),
         # the address next to it is plain connected
-        Probe(s, 18, 0, v4(0, "172.16.0.2", "172.16.0.98"), "ip_hold"),
+        Probe(s, 26, 0, v4(0, "172.16.0.2", "172.16.0.98"), "ip_hold"),
     ]
     return t, pr
 
 
 def bridge(resolved):
-    """smoke/bridge_test.sh: p0..p2 in bridge br0's domain (:5-7): iface_input's
+    """smoke/bridge_test.sh: p0..p2 in bridge br0's domain (:9-11): iface_input's
     mode edge for GR_IFACE_MODE_BRIDGE is bridge_input (bridge_input.c:124),
     which switches on the CPU."""
     s = "bridge_test.sh"
     t = T.Topology()
     t.add_vrf(T.VRF_MAIN)
     BR = 40
-    t.add_iface(BR, "BRIDGE", mac=GR_MAC[3])  # :4
+    t.add_iface(BR, "BRIDGE", mac=GR_MAC[3])  # :7
     for p in range(3):
-        t.add_port(PORT[p], p, GR_MAC[p], mode="BRIDGE")  # :5-7 (the domain itself lives on the CPU)
-    t.add_address(BR, "172.16.0.1/24")  # :8
+        t.add_port(PORT[p], p, GR_MAC[p], mode="BRIDGE")  # :9-11 (the domain itself lives on the CPU)
+    t.add_address(BR, "172.16.0.1/24")  # :15
     pr = [
-        Probe(s, 19, 0, v4(0, "172.16.0.10", "172.16.0.11", dst_mac=NS_MAC[1]), "bridge_input"),
-        Probe(s, 20, 1, v4(1, "172.16.0.11", "172.16.0.12", dst_mac=NS_MAC[2]), "bridge_input"),
-        Probe(s, 32, 0, v4(0, "172.16.0.10", "172.16.0.1", dst_mac=GR_MAC[3]), "bridge_input"),
-        Probe(s, 19, 0, S.frame(dst_mac="ff:ff:ff:ff:ff:ff", src_mac=NS_MAC[0], ethertype=0x0806), "bridge_input"),
+        Probe(s, 26, 0, v4(0, "172.16.0.10", "172.16.0.11", dst_mac=NS_MAC[1]), "bridge_input"),
+        Probe(s, 27, 1, v4(1, "172.16.0.11", "172.16.0.12", dst_mac=NS_MAC[2]), "bridge_input"),
+        Probe(s, 42, 0, v4(0, "172.16.0.10", "172.16.0.1", dst_mac=GR_MAC[3]), "bridge_input"),
+        Probe(s, 26, 0, S.frame(dst_mac="ff:ff:ff:ff:ff:ff", src_mac=NS_MAC[0], ethertype=0x0806), "bridge_input"),
     ]
     return t, pr
 
 
 def ip6_same_peer(resolved):
     """smoke/ip6_same_peer_test.sh: a link-local address is only reachable on
-    its own link (:19: n1's ping to p2's link-local must go unanswered).
+    its own link (:24: n1's ping to p2's link-local must go unanswered).
     Link-local routes are scoped to their iface (modules/ip6/control/route.c:150-173):
     on p1, fe80::/64 is p1's connected prefix, so the packet is held for a
     neighbour solicitation on p1's link, which nobody answers (ip6_hold in both
@@ -438,8 +462,8 @@ def ip6_same_peer(resolved):
     t = T.Topology()
     t.add_vrf(T.VRF_MAIN)
     ports(t, 2)
-    t.add_address6(PORT[0], "fd00:ba4:1::1/64")  # :6
-    t.add_address6(PORT[1], "fd00:ba4:2::1/64")  # :7
+    t.add_address6(PORT[0], "fd00:ba4:1::1/64")  # :10
+    t.add_address6(PORT[1], "fd00:ba4:2::1/64")  # :11
     if resolved:
         neighbour(t, T.VRF_MAIN, PORT[0], "fd00:ba4:1::2", NS_MAC[0])
         neighbour(t, T.VRF_MAIN, PORT[1], "fd00:ba4:2::2", NS_MAC[1])
@@ -447,54 +471,348 @@ def ip6_same_peer(resolved):
         neighbour(t, T.VRF_MAIN, PORT[1], eui64_ll(NS_MAC[1]), NS_MAC[1])
     n1_ll, n2_ll = eui64_ll(NS_MAC[0]), eui64_ll(NS_MAC[1])
     pr = [
-        Probe(s, 17, 0, v6(0, n1_ll, eui64_ll(GR_MAC[0])), "ip6_input_local"),
-        Probe(s, 18, 1, v6(1, n2_ll, eui64_ll(GR_MAC[1])), "ip6_input_local"),
-        Probe(s, 19, 0, v6(0, n1_ll, eui64_ll(GR_MAC[1])), "ip6_hold"),  # p2's link-local, asked on p1
-        Probe(s, 20, 0, v6(0, "fd00:ba4:1::2", "fd00:ba4:2::2"), "ip6_hold", "port_output", (1, 0, NS_MAC[1])),
-        Probe(s, 21, 1, v6(1, "fd00:ba4:2::2", "fd00:ba4:1::2"), "ip6_hold", "port_output", (0, 0, NS_MAC[0])),
-        Probe(s, 22, 0, v6(0, "fd00:ba4:1::2", "fd00:ba4:1::1"), "ip6_input_local"),
-        Probe(s, 23, 1, v6(1, "fd00:ba4:2::2", "fd00:ba4:2::1"), "ip6_input_local"),
-        Probe(s, 24, 0, v6(0, "fd00:ba4:1::2", "fd00:ba4:2::2", hop=1, nh=17), "ip6_error_ttl_exceeded"),
-        Probe(s, 25, 1, v6(1, "fd00:ba4:2::2", "fd00:ba4:1::2", hop=1, nh=17), "ip6_error_ttl_exceeded"),
+        Probe(s, 22, 0, v6(0, n1_ll, eui64_ll(GR_MAC[0])), "ip6_input_local"),
+        Probe(s, 23, 1, v6(1, n2_ll, eui64_ll(GR_MAC[1])), "ip6_input_local"),
+        Probe(s, 24, 0, v6(0, n1_ll, eui64_ll(GR_MAC[1])), "ip6_hold"),  # p2's link-local, asked on p1
+        Probe(s, 25, 0, v6(0, "fd00:ba4:1::2", "fd00:ba4:2::2"), "ip6_hold", "port_output", (1, 0, NS_MAC[1])),
+        Probe(s, 26, 1, v6(1, "fd00:ba4:2::2", "fd00:ba4:1::2"), "ip6_hold", "port_output", (0, 0, NS_MAC[0])),
+        Probe(s, 27, 0, v6(0, "fd00:ba4:1::2", "fd00:ba4:1::1"), "ip6_input_local"),
+        Probe(s, 28, 1, v6(1, "fd00:ba4:2::2", "fd00:ba4:2::1"), "ip6_input_local"),
+        Probe(s, 29, 0, v6(0, "fd00:ba4:1::2", "fd00:ba4:2::2", hop=1, nh=17), "ip6_error_ttl_exceeded"),
+        Probe(s, 30, 1, v6(1, "fd00:ba4:2::2", "fd00:ba4:1::2", hop=1, nh=17), "ip6_error_ttl_exceeded"),
     ]
     return t, pr
 
 
 def srv6(resolved):
     """smoke/srv6_test.sh: 192.168.0.0/16 via an SRv6 encap nexthop (id 42,
-    :18-19) leaves ip_output by the nexthop type's edge, sr6_output
+    :43-44) leaves ip_output by the nexthop type's edge, sr6_output
     (srv6_output.c:152), after ip_forward; fd00:202:100::/48 via an SRv6 local
-    End.DT4 nexthop (id 666, :27-28) leaves ip6_input by sr6_local; the
+    End.DT4 nexthop (id 666, :58-59) leaves ip6_input by sr6_local; the
     encapsulated return traffic n1 sends to fd00:202:100:: takes it."""
     s = "srv6_test.sh"
     t = T.Topology()
     t.add_vrf(T.VRF_MAIN)
     ports(t, 2)
-    t.add_address6(PORT[1], "fd00:102::1/32")  # :5
-    t.add_address(PORT[0], "192.168.61.1/24")  # :6
-    sr = t.add_nexthop(0, nh_type="SR6_OUTPUT", slot=42)  # :18
-    t.add_route(T.VRF_MAIN, "192.168.0.0/16", sr)  # :19
+    t.add_address6(PORT[1], "fd00:102::1/32")  # :9
+    t.add_address(PORT[0], "192.168.61.1/24")  # :10
+    sr = t.add_nexthop(0, nh_type="SR6_OUTPUT", slot=42)  # :43
+    t.add_route(T.VRF_MAIN, "192.168.0.0/16", sr)  # :44
     gw = t.add_nexthop(PORT[1], "fd00:102::2", NS_MAC[1] if resolved else None)
-    t.add_route6(T.VRF_MAIN, "fd00:202::/32", gw)  # :20
-    loc = t.add_nexthop(0, nh_type="SR6_LOCAL", slot=666)  # :27
-    t.add_route6(T.VRF_MAIN, "fd00:202:100::/48", loc)  # :28
+    t.add_route6(T.VRF_MAIN, "fd00:202::/32", gw)  # :45
+    loc = t.add_nexthop(0, nh_type="SR6_LOCAL", slot=666)  # :58
+    t.add_route6(T.VRF_MAIN, "fd00:202:100::/48", loc)  # :59
     if resolved:
         neighbour(t, T.VRF_MAIN, PORT[0], "192.168.61.2", NS_MAC[0])
         neighbour(t, T.VRF_MAIN, PORT[1], "fd00:102::2", NS_MAC[1])
     pr = [
-        Probe(s, 29, 0, v4(0, "192.168.61.2", "192.168.60.1"), "sr6_output"),
-        Probe(s, 29, 0, v4(0, "192.168.61.2", "192.168.60.1", ttl=1), "ip_error_ttl_exceeded"),
-        Probe(s, 29, 1, v6(1, "fd00:102::2", "fd00:202:100::", nh=43), "sr6_local"),  # IPv6 + routing header
-        Probe(s, 30, 1, v6(1, "fd00:102::2", "fd00:202:100::1"), "sr6_local"),
+        Probe(s, 62, 0, v4(0, "192.168.61.2", "192.168.60.1"), "sr6_output"),
+        Probe(s, 62, 0, v4(0, "192.168.61.2", "192.168.60.1", ttl=1), "ip_error_ttl_exceeded"),
+        Probe(s, 64, 1, v6(1, "fd00:102::2", "fd00:202:100::", nh=43), "sr6_local"),  # IPv6 + routing header
+        Probe(s, 64, 1, v6(1, "fd00:102::2", "fd00:202:100::1"), "sr6_local"),
         # the rest of fd00:202::/32 goes back to n1 by the gateway
-        Probe(s, 30, 1, v6(1, "fd00:102::2", "fd00:202:200::"), "ip6_hold", "port_output", (1, 0, NS_MAC[1])),
+        Probe(s, 64, 1, v6(1, "fd00:102::2", "fd00:202:200::"), "ip6_hold", "port_output", (1, 0, NS_MAC[1])),
+    ]
+    return t, pr
+
+
+def ip_builtin_icmp(resolved):
+    """smoke/ip_builtin_icmp_test.sh: p0 holds 172.16.2.1/24 and 172.16.0.1/24,
+    p1 172.16.1.1/24 (:9-11). The script's pings and traceroute are grout's
+    own (grcli ping, ip_output on the CPU): what comes back on the wire are
+    the echo replies, ARP replies and ICMP errors for grout's addresses. The
+    two pings that must fail (:30-31) are restated as transit packets from
+    n0: no route to 1.1.1.1 (ip_error_dest_unreach, ip_input.c:147-150) and a
+    host on p1's link nobody answers ARP for (ip_hold in both states)."""
+    s = "ip_builtin_icmp_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 2)
+    t.add_address(PORT[0], "172.16.2.1/24")  # :9
+    t.add_address(PORT[0], "172.16.0.1/24")  # :10
+    t.add_address(PORT[1], "172.16.1.1/24")  # :11
+    if resolved:
+        neighbour(t, T.VRF_MAIN, PORT[0], "172.16.0.2", NS_MAC[0])
+        neighbour(t, T.VRF_MAIN, PORT[1], "172.16.1.2", NS_MAC[1])
+    pr = [
+        # the echo replies to grcli ping (:24-25), to either of p0's addresses
+        Probe(s, 24, 0, v4(0, "172.16.0.2", "172.16.0.1"), "ip_input_local"),
+        Probe(s, 24, 0, v4(0, "172.16.0.2", "172.16.2.1"), "ip_input_local"),
+        Probe(s, 25, 1, v4(1, "172.16.1.2", "172.16.1.1"), "ip_input_local"),
+        # the ARP replies that resolve the pinged hosts
+        Probe(s, 24, 0, arp(0, dst_mac=GR_MAC[0]), "arp_input"),
+        Probe(s, 25, 1, arp(1, dst_mac=GR_MAC[1]), "arp_input"),
+        # :30 no route, :31 nobody answers
+        Probe(s, 30, 0, v4(0, "172.16.0.2", "1.1.1.1"), "ip_error_dest_unreach"),
+        Probe(s, 31, 0, v4(0, "172.16.0.2", "172.16.1.3"), "ip_hold"),
+        # traceroute's answers (:33): ICMP errors from n0, UDP-probe TTL expiry on the way
+        Probe(s, 33, 0, v4(0, "172.16.0.2", "172.16.0.1", proto=1), "ip_input_local"),
+        Probe(s, 33, 0, v4(0, "172.16.0.2", "172.16.1.2", ttl=1, proto=17), "ip_error_ttl_exceeded"),
+        # and n0 reaching n1 through grout once both are resolved
+        Probe(s, 25, 0, v4(0, "172.16.0.2", "172.16.1.2"), "ip_hold", "port_output", (1, 0, NS_MAC[1])),
+    ]
+    return t, pr
+
+
+def ip6_builtin_icmp(resolved):
+    """smoke/ip6_builtin_icmp_test.sh: fd00:ba4::1/64 on p0, fd00:ba4:1::1/64
+    on p1 (:9-10), grcli ping / traceroute of the namespaces (:21-28). The
+    replies come back to grout's addresses; the pings that must fail (:25-26)
+    are restated as transit: fd00:baa::1 has no route
+    (ip6_error_dest_unreach), fd00:ba4:1::3 is never answered (ip6_hold)."""
+    s = "ip6_builtin_icmp_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 2)
+    t.add_address6(PORT[0], "fd00:ba4:0::1/64")  # :9
+    t.add_address6(PORT[1], "fd00:ba4:1::1/64")  # :10
+    if resolved:
+        neighbour(t, T.VRF_MAIN, PORT[0], "fd00:ba4::2", NS_MAC[0])
+        neighbour(t, T.VRF_MAIN, PORT[1], "fd00:ba4:1::2", NS_MAC[1])
+    pr = [
+        Probe(s, 21, 0, v6(0, "fd00:ba4::2", "fd00:ba4::1"), "ip6_input_local"),
+        Probe(s, 22, 1, v6(1, "fd00:ba4:1::2", "fd00:ba4:1::1"), "ip6_input_local"),
+        # the neighbour advertisements, unicast to grout's address
+        Probe(s, 21, 0, v6(0, "fd00:ba4::2", "fd00:ba4::1", hop=255), "ip6_input_local"),
+        Probe(s, 25, 0, v6(0, "fd00:ba4::2", "fd00:baa::1"), "ip6_error_dest_unreach"),
+        Probe(s, 26, 0, v6(0, "fd00:ba4::2", "fd00:ba4:1::3"), "ip6_hold"),
+        Probe(s, 28, 1, v6(1, "fd00:ba4:1::2", "fd00:ba4:1::1", nh=58), "ip6_input_local"),
+        Probe(s, 28, 0, v6(0, "fd00:ba4::2", "fd00:ba4:1::2", hop=1, nh=17), "ip6_error_ttl_exceeded"),
+        # the namespaces reach each other over fd00:ba4::/62 (:18)
+        Probe(s, 22, 0, v6(0, "fd00:ba4::2", "fd00:ba4:1::2"), "ip6_hold", "port_output", (1, 0, NS_MAC[1])),
+        Probe(s, 21, 1, v6(1, "fd00:ba4:1::2", "fd00:ba4::2"), "ip6_hold", "port_output", (0, 0, NS_MAC[0])),
+    ]
+    return t, pr
+
+
+MAC_SECONDARY = ["02:00:00:00:00:01", "02:00:00:00:00:02", "02:00:00:00:00:03"]  # iface_mac_test.sh:11-13
+
+
+def iface_mac(resolved):
+    """smoke/iface_mac_test.sh: secondary MAC addresses on p0 (:16-18, deleted
+    again at :38, :69, :83; resolved = after the deletions). They are the
+    port's receive filter (rte_eth_dev_mac_addr_add, modules/infra/control/port.c);
+    eth_input compares the destination with the iface's one address,
+    iface_get_eth_addr (eth_input.c:62-77): a frame for a secondary MAC is
+    ETH_DOMAIN_OTHER and ip_input / ip6_input drop it as for another host,
+    in both states. The primary MAC is p0's own (:8: no address, so no route)."""
+    s = "iface_mac_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 1)
+    pr = [
+        Probe(s, 16, 0, v4(0, "10.0.0.2", "10.0.0.1", dst_mac=MAC_SECONDARY[0]), "ip_input_other_host"),
+        Probe(s, 17, 0, v4(0, "10.0.0.2", "10.0.0.1", dst_mac=MAC_SECONDARY[1]), "ip_input_other_host"),
+        Probe(s, 18, 0, v6(0, eui64_ll(NS_MAC[0]), eui64_ll(GR_MAC[0]), dst_mac=MAC_SECONDARY[2]),
+              "ip6_input_other_host"),
+        # the primary MAC: no IPv4 address or route on p0, but the link-local address every port gets
+        Probe(s, 8, 0, v4(0, "10.0.0.2", "10.0.0.1"), "ip_error_dest_unreach"),
+        Probe(s, 8, 0, v6(0, eui64_ll(NS_MAC[0]), eui64_ll(GR_MAC[0])), "ip6_input_local"),
+        # ARP to a secondary MAC: eth_input's ether type edge does not look at the domain
+        Probe(s, 16, 0, arp(0, dst_mac=MAC_SECONDARY[0]), "arp_input"),
+    ]
+    return t, pr
+
+
+def nexthop_ageing(resolved):
+    """smoke/nexthop_ageing_test.sh: p0 172.16.0.1/24, p1 172.16.1.1/24
+    (:32-33); the namespaces' pings (:44-45) make grout learn both neighbours
+    (resolved: REACHABLE, and still so after the lifetime expired and the
+    probes were answered, :54-55). With the namespaces' links down the
+    nexthops age out and are destroyed (:69-70; l3_age, l3_nexthop.c:313-360):
+    not resolved, the /32 routes are gone and the connected prefixes' LINK
+    nexthops hold the packets for ARP again (ip_output.c:126-137)."""
+    s = "nexthop_ageing_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 2)
+    t.add_address(PORT[0], "172.16.0.1/24")  # :32
+    t.add_address(PORT[1], "172.16.1.1/24")  # :33
+    if resolved:
+        neighbour(t, T.VRF_MAIN, PORT[0], "172.16.0.2", NS_MAC[0])
+        neighbour(t, T.VRF_MAIN, PORT[1], "172.16.1.2", NS_MAC[1])
+    pr = [
+        Probe(s, 44, 0, v4(0, "172.16.0.2", "172.16.1.2"), "ip_hold", "port_output", (1, 0, NS_MAC[1])),
+        Probe(s, 45, 1, v4(1, "172.16.1.2", "172.16.0.2"), "ip_hold", "port_output", (0, 0, NS_MAC[0])),
+        Probe(s, 44, 0, v4(0, "172.16.0.2", "172.16.0.1"), "ip_input_local"),
+        # the addresses outlive the neighbours (:58-59, :73-74)
+        Probe(s, 58, 0, v4(0, "172.16.0.2", "172.16.0.1"), "ip_input_local"),
+        Probe(s, 59, 1, v4(1, "172.16.1.2", "172.16.1.1"), "ip_input_local"),
+    ]
+    return t, pr
+
+
+def nexthop_ageing_stale(resolved):
+    """smoke/nexthop_ageing_test.sh between :49 and :54: the neighbours'
+    lifetime has expired (REACHABLE -> STALE, l3_nexthop.c:351-354) and the
+    probes are out; a probe left unanswered makes one FAILED
+    (l3_nexthop.c:329-340). Not resolved: 172.16.1.2 STALE and 172.16.0.2
+    FAILED, their /32 routes still in place; ip_output holds packets for
+    any nexthop that is not REACHABLE (ip_output.c:126-137). Resolved: the
+    probes were answered, both REACHABLE again (:54-55)."""
+    s = "nexthop_ageing_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 2)
+    t.add_address(PORT[0], "172.16.0.1/24")  # :32
+    t.add_address(PORT[1], "172.16.1.1/24")  # :33
+    st0 = None if resolved else abi.NH_S["FAILED"]
+    st1 = None if resolved else abi.NH_S["STALE"]
+    n0 = t.add_nexthop(PORT[0], "172.16.0.2", NS_MAC[0], state=st0)
+    t.add_route(T.VRF_MAIN, "172.16.0.2/32", n0)
+    n1 = t.add_nexthop(PORT[1], "172.16.1.2", NS_MAC[1], state=st1)
+    t.add_route(T.VRF_MAIN, "172.16.1.2/32", n1)
+    pr = [
+        Probe(s, 54, 0, v4(0, "172.16.0.2", "172.16.1.2"), "ip_hold", "port_output", (1, 0, NS_MAC[1])),
+        Probe(s, 55, 1, v4(1, "172.16.1.2", "172.16.0.2"), "ip_hold", "port_output", (0, 0, NS_MAC[0])),
+        Probe(s, 54, 1, v4(1, "172.16.1.2", "172.16.0.2", ttl=1), "ip_error_ttl_exceeded"),
+    ]
+    return t, pr
+
+
+def vxlan(resolved):
+    """smoke/vxlan_test.sh: p0 10.0.0.1/24 (:9), bridge br100 (:10) holding
+    192.168.100.1/24 (:14), VXLAN vxlan100 (VNI 100, local 10.0.0.1) in
+    br100's domain (:11). n1's VXLAN packets are UDP 4789 to grout's
+    10.0.0.1: ip_input_local (then l4 and vxlan_input on the CPU). vxlan_input
+    hands the inner frame back to iface_input on vxlan100
+    (vxlan_input.c:96-101, edge "iface_input"), whose mode edge is
+    bridge_input (bridge_input.c:124); bridge_input hands a frame for the
+    bridge's own MAC back to iface_input on br100 (bridge_input.c:85-99),
+    which eth_input and ip_input take as local. A routed packet for a
+    neighbour on br100 leaves by iface_output's type edge for a bridge,
+    bridge_input again (bridge_input.c:125)."""
+    s = "vxlan_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 1)
+    BR, VX = 40, 41
+    BR_MAC = "02:00:00:00:01:00"
+    t.add_address(PORT[0], "10.0.0.1/24")  # :9
+    t.add_iface(BR, "BRIDGE", mac=BR_MAC)  # :10
+    t.add_iface(VX, "VXLAN", mode="BRIDGE")  # :11 (the domain itself lives on the CPU)
+    t.add_address(BR, "192.168.100.1/24")  # :14
+    N1_BR = "02:00:00:0b:00:64"  # n1's br100 (:19, :24)
+    if resolved:
+        neighbour(t, T.VRF_MAIN, PORT[0], "10.0.0.2", NS_MAC[0])
+        neighbour(t, T.VRF_MAIN, BR, "192.168.100.2", N1_BR)
+    inner = v4(0, "192.168.100.2", "192.168.100.1", dst_mac=BR_MAC)
+    inner = inner[:6] + T.mac_bytes(N1_BR) + inner[12:]
+    pr = [
+        # the encapsulated ping (:29): UDP to the VTEP address
+        Probe(s, 29, 0, v4(0, "10.0.0.2", "10.0.0.1", proto=17, size=100), "ip_input_local"),
+        # the inner frames after vxlan_input: n1's ARP request, the ping itself
+        Probe(s, 29, 0, S.frame(dst_mac="ff:ff:ff:ff:ff:ff", src_mac=N1_BR, ethertype=0x0806), "bridge_input",
+              iface=VX),
+        Probe(s, 29, 0, inner, "bridge_input", iface=VX),
+        # ... and bridge_input's hand-back on br100
+        Probe(s, 29, 0, inner, "ip_input_local", iface=BR),
+        # p0's side reaching n1's bridge address through grout
+        Probe(s, 29, 0, v4(0, "10.0.0.2", "192.168.100.2"), "ip_hold", "bridge_input"),
+    ]
+    return t, pr
+
+
+def bond_active_backup(resolved):
+    """smoke/bond_active_backup_test.sh: bond0 (active-backup, :24) over
+    p0..p2 (:26-28) holding 172.16.0.1/24 (:55); its MAC (:35-37) is
+    02:f0:00:b4:44:44. port_rx on the active member hands frames over with the bond
+    as their iface (rx_bond_process, port_rx.c:414-456; get_bond :123-139),
+    LACP frames (ether type 0x8809) with the member itself, whose
+    mode BOND edge is eth_input (lacp_input.c:68) and eth_input's ether type
+    edge lacp_input (:67). Routed packets leaving by bond0 take iface_output's
+    type edge for a bond, bond_output (bond_output.c:250)."""
+    s = "bond_active_backup_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    BOND, BMAC = 50, "02:f0:00:b4:44:44"
+    t.add_iface(BOND, "BOND", mac=BMAC)  # :24, :37
+    for p in range(3):
+        t.add_port(PORT[p], p, GR_MAC[p], mode="BOND")  # :26-28 (the domain lives on the CPU)
+    t.add_address(BOND, "172.16.0.1/24")  # :55
+    if resolved:
+        neighbour(t, T.VRF_MAIN, BOND, "172.16.0.2", NS_MAC[0])
+    lacp = S.frame(dst_mac="01:80:c2:00:00:02", src_mac=NS_MAC[1], ethertype=0x8809)
+    pr = [
+        Probe(s, 59, 1, v4(1, "172.16.0.2", "172.16.0.1", dst_mac=BMAC), "ip_input_local", iface=BOND),
+        Probe(s, 64, 0, v4(0, "172.16.0.2", "172.16.0.1", dst_mac=BMAC), "ip_input_local", iface=BOND),
+        Probe(s, 12, 1, arp(1), "arp_input", iface=BOND),
+        Probe(s, 59, 1, lacp, "lacp_input"),
+        # a frame for a member's own MAC is not the bond's
+        Probe(s, 59, 1, v4(1, "172.16.0.2", "172.16.0.1", dst_mac=GR_MAC[1]), "ip_input_other_host", iface=BOND),
+        # transit back out of bond0 to a neighbour on its link
+        Probe(s, 59, 1, v4(1, "172.16.0.9", "172.16.0.2", dst_mac=BMAC), "ip_hold", "bond_output", iface=BOND),
+    ]
+    return t, pr
+
+
+def ip_add_del(resolved):
+    """smoke/ip_add_del_test.sh: 172.16.0.1/24 on p0 added (:9), deleted
+    (:11) and added again (:13). Not resolved: after the delete, no route is
+    left (ip_error_dest_unreach); resolved: after the second add, the
+    address is local again and its prefix connected (ip_hold)."""
+    s = "ip_add_del_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 1)
+    if resolved:
+        t.add_address(PORT[0], "172.16.0.1/24")  # :13
+    pr = [
+        Probe(s, 11, 0, v4(0, "172.16.0.2", "172.16.0.1"), "ip_error_dest_unreach", "ip_input_local"),
+        Probe(s, 13, 0, v4(0, "172.16.0.2", "172.16.0.3"), "ip_error_dest_unreach", "ip_hold"),
+    ]
+    return t, pr
+
+
+def ip6_add_del(resolved):
+    """smoke/ip6_add_del_test.sh: 2001::1/64 on p0 added (:11), deleted (:13),
+    added again (:15). Not resolved: after the delete; resolved: after the
+    second add. p0's link-local address stays through both."""
+    s = "ip6_add_del_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 1)
+    if resolved:
+        t.add_address6(PORT[0], "2001::1/64")  # :15
+    pr = [
+        Probe(s, 13, 0, v6(0, "2001::2", "2001::1"), "ip6_error_dest_unreach", "ip6_input_local"),
+        Probe(s, 15, 0, v6(0, "2001::2", "2001::3"), "ip6_error_dest_unreach", "ip6_hold"),
+        Probe(s, 14, 0, v6(0, eui64_ll(NS_MAC[0]), eui64_ll(GR_MAC[0])), "ip6_input_local"),
+    ]
+    return t, pr
+
+
+def ip6_add_del_moves(resolved):
+    """smoke/ip6_add_del_test.sh, the moves after :15. Not resolved: p0 set
+    to VRF foo (:18-19): its addresses are flushed and its link-local
+    re-created in foo (GR_EVENT_IFACE_POST_RECONFIG,
+    modules/ip6/control/address.c:469-481), so 2001::1 is gone from both
+    VRFs. Resolved: p0 cross-connected to p1 (:23-25, mode XC): iface_input's
+    mode edge is xconnect (xconnect.c) and p0's addresses are flushed."""
+    s = "ip6_add_del_test.sh"
+    FOO = 2
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    t.add_vrf(FOO)
+    if resolved:
+        t.add_port(PORT[0], 0, GR_MAC[0], mode="XC")  # :24
+        t.add_port(PORT[1], 1, GR_MAC[1], mode="XC")  # :25
+    else:
+        t.add_port(PORT[0], 0, GR_MAC[0], vrf_id=FOO)  # :19
+        t.add_address6(PORT[0], eui64_ll(GR_MAC[0]) + "/64")
+    pr = [
+        Probe(s, 19, 0, v6(0, "2001::2", "2001::1"), "ip6_error_dest_unreach", "xconnect"),
+        Probe(s, 19, 0, v6(0, eui64_ll(NS_MAC[0]), eui64_ll(GR_MAC[0])), "ip6_input_local", "xconnect"),
+        Probe(s, 24, 0, v4(0, "172.16.0.2", "172.16.0.1"), "ip_error_dest_unreach", "xconnect"),
     ]
     return t, pr
 
 
 SCRIPTS = {f.__name__: f for f in (ip6_forward, vlan_forward, vrf_forward, cross_vrf_forward, ip_forward_ip6nh,
                                    ip_loadbalance, ip_fragment, ipip_encap, snat44, dnat44, bridge, ip6_same_peer,
-                                   srv6)}
+                                   srv6, ip_builtin_icmp, ip6_builtin_icmp, iface_mac, nexthop_ageing,
+                                   nexthop_ageing_stale, vxlan, bond_active_backup, ip_add_del, ip6_add_del,
+                                   ip6_add_del_moves)}
 
 
 # ---------------------------------------------------------------------------
@@ -503,7 +821,8 @@ SCRIPTS = {f.__name__: f for f in (ip6_forward, vlan_forward, vrf_forward, cross
 def _pack(probes):
     fr = [p.frame for p in probes]
     stride = max(128, -(-max(len(f) for f in fr) // 64) * 64)  # whole frames: pkt_len bytes readable
-    arr, meta = S.pack(fr, stride=stride, iface=[PORT[p.port] for p in probes], vlan=[p.vlan for p in probes])
+    arr, meta = S.pack(fr, stride=stride, iface=[p.iface or PORT[p.port] for p in probes],
+                       vlan=[p.vlan for p in probes])
     meta["rss"] = [p.rss for p in probes]
     return arr, meta
 
@@ -582,6 +901,25 @@ def test_smoke_script_gpu(fastpath, script, resolved):
         expect_both_members(used, resolved)
     lines_o, _, _, want, _ = oracle.Oracle(t).process_mbufs(fr, me, lines_only=True)
     compare_mbufs(m, want, bufs, lines_o, [p.label for p in probes])
+
+
+TRAFFIC = ("ping", "traceroute", "socat", "tracepath", "route add", "mac add", "address add", "address del", "interface add",
+           "interface set", "check_nexthop", "address show")
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_SMOKE), reason="reference not mounted")
+@pytest.mark.parametrize("script", list(SCRIPTS))
+def test_probe_lines_are_the_scripts(script):
+    """Every probe names the script line whose traffic (or configuration
+    step) it restates: that line exists and sends or configures something."""
+    for resolved in (False, True):
+        _, probes = SCRIPTS[script](resolved)
+        for p in probes:
+            with open(os.path.join(REF_SMOKE, p.script)) as f:
+                lines = f.read().split("\n")
+            assert 1 <= p.line <= len(lines), p.label
+            text = lines[p.line - 1]
+            assert any(w in text for w in TRAFFIC), (p.label, text)
 
 
 def test_group_reta_is_grouts():
