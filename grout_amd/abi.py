@@ -189,6 +189,9 @@ HIP_API = {
     "gr_hip_edge_node": (_I, [_U8, _U32, _I]),
     "gr_hip_node_layout": (_I, [_P, _U32, _U32, _P]),
     "gr_hip_node_stage": (_I, [_P, _U32, _U32, _P, _P, _P]),
+    "gr_hip_node_append": (_I, [_P, _P, _U32, _U32]),
+    "gr_hip_node_send": (_I, [_P, _P, _U32, _U32]),
+    "gr_hip_node_discard": (_I, [_P]),
     "gr_hip_node_apply": (_I, [_P, _U32, _U32, _P, _P, _U32, _P, _P, _U32, _P, _U32, _P]),
     "gr_hip_node_process": (_I, [_P, _P, _U32, _U32, _P]),
     "gr_hip_node_start": (_I, [_P, _P, _U32, _U32]),

@@ -171,6 +171,10 @@ struct node_slot {
 	bool by_addr = false;
 	bool sync = false; // finished at start already (staged copies, or nothing to send)
 	int r = 0; // the GPU call's result when sync
+	// the walk being appended (gr_hip_node_append): views and slots staged so
+	// far, and whether the header lines are (not with "node_ptrs")
+	bool open = false, lines_in = false;
+	uint32_t na = 0, p = 0;
 };
 
 } // namespace
@@ -2351,15 +2355,109 @@ extern "C" int gr_hip_node_prof(uint64_t *out, uint32_t n, int reset) {
 	return GR_HIP_NODE_PROF_COUNT;
 }
 
-extern "C" int gr_hip_node_start(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst) {
+// Pinned staging for ns slots; the first `keep` staged lines and metadata
+// survive (an append growing the walk being staged).
+static int slot_grow(node_slot &w, uint32_t ns, uint32_t keep) {
+	if (ns <= w.cap)
+		return 0;
+	uint32_t cap = w.cap ? w.cap : 1024;
+	while (cap < ns)
+		cap = cap > UINT32_MAX / 2 ? ns : cap * 2;
+	uint8_t *lines = nullptr, *out = nullptr;
+	gr_hip_pkt_meta *meta = nullptr;
+	gr_hip_verdict *v = nullptr;
+	if (hipHostMalloc((void **)&lines, (size_t)cap * GR_HIP_LINE, hipHostMallocDefault) != hipSuccess
+	    || hipHostMalloc((void **)&out, (size_t)cap * GR_HIP_PREFIX, hipHostMallocDefault) != hipSuccess
+	    || hipHostMalloc((void **)&meta, (size_t)cap * sizeof(gr_hip_pkt_meta), hipHostMallocDefault) != hipSuccess
+	    || hipHostMalloc((void **)&v, (size_t)cap * sizeof(gr_hip_verdict), hipHostMallocDefault) != hipSuccess) {
+		(void)hipGetLastError();
+		hipHostFree(lines);
+		hipHostFree(out);
+		hipHostFree(meta);
+		hipHostFree(v);
+		return -ENOMEM;
+	}
+	if (keep) {
+		memcpy(lines, w.lines, (size_t)keep * GR_HIP_LINE);
+		memcpy(meta, w.meta, (size_t)keep * sizeof(gr_hip_pkt_meta));
+	}
+	hipHostFree(w.lines);
+	hipHostFree(w.out);
+	hipHostFree(w.meta);
+	hipHostFree(w.v);
+	w.lines = lines;
+	w.out = out;
+	w.meta = meta;
+	w.v = v;
+	w.cap = cap;
+	// looked up once here, not per walk (hipPointerGetAttributes is slow)
+	if (!host_dev_ptr(w.lines, &w.d_lines) || !host_dev_ptr(w.out, &w.d_out) || !host_dev_ptr(w.meta, &w.d_meta)
+	    || !host_dev_ptr(w.v, &w.d_v))
+		w.d_lines = w.d_out = w.d_meta = w.d_v = nullptr; // not device-accessible: staged copies
+	return 0;
+}
+
+// The slot the next walk is staged into.
+static node_slot &open_slot(gr_hip_queue_t *q) {
+	return q->nw[(q->nw_head + q->nw_count) % GR_HIP_NODE_DEPTH];
+}
+
+extern "C" int gr_hip_node_append(gr_hip_queue_t *q, const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst) {
+	if (q == nullptr || (n && m == nullptr))
+		return -EINVAL;
+	if (q->nw_count == GR_HIP_NODE_DEPTH)
+		return -EBUSY;
+	node_slot &w = open_slot(q);
+	if (!w.open) {
+		w.open = true;
+		w.na = w.p = 0;
+		w.lines_in = !q->ctx->node_ptrs;
+	} else if (n && !(m[0].flags & GR_HIP_MBUF_F_WALK)) {
+		return -EINVAL; // each append is a walk (or walks) of its own
+	}
+	if (n == 0)
+		return (int)w.p;
+	uint64_t t_prof = prof_now();
+	if (w.pos.size() < (size_t)w.na + n)
+		w.pos.resize(std::max<size_t>((size_t)w.na + n, 2 * w.pos.size()));
+	uint32_t *pos = w.pos.data() + w.na;
+	const uint64_t p = gr_node_layout_from(m, n, burst, w.p, pos);
+	if (p > INT32_MAX)
+		return -E2BIG;
+	if (p > w.cap) {
+		hipSetDevice(q->ctx->dev);
+		int r = slot_grow(w, (uint32_t)p, w.p);
+		if (r < 0)
+			return r;
+	}
+	int r = gr_node_stage_from(m, n, burst, pos, w.p, w.lines_in ? w.lines : nullptr, w.meta);
+	if (r < 0)
+		return r;
+	w.na += n;
+	w.p = (uint32_t)p;
+	node_prof_ns[GR_HIP_NODE_PROF_STAGE] += prof_now() - t_prof;
+	return (int)p;
+}
+
+extern "C" int gr_hip_node_discard(gr_hip_queue_t *q) {
+	if (q == nullptr)
+		return -EINVAL;
+	if (q->nw_count < GR_HIP_NODE_DEPTH)
+		open_slot(q).open = false;
+	return 0;
+}
+
+extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst) {
 	if (q == nullptr || (n && m == nullptr))
 		return -EINVAL;
 	if (q->nw_count == GR_HIP_NODE_DEPTH)
 		return -EBUSY;
 	gr_hip_ctx *c = q->ctx;
-	node_slot &w = q->nw[(q->nw_head + q->nw_count) % GR_HIP_NODE_DEPTH];
-	if (w.pos.size() < n)
-		w.pos.resize(n);
+	node_slot &w = open_slot(q);
+	const bool was_open = w.open;
+	w.open = false;
+	if (!(was_open ? w.na == n : n == 0))
+		return -EINVAL; // not what was appended
 	uint32_t *pos = w.pos.data();
 	uint64_t t_prof = prof_now();
 	auto lap = [&](int k) {
@@ -2367,11 +2465,7 @@ extern "C" int gr_hip_node_start(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint3
 		node_prof_ns[k] += t - t_prof;
 		t_prof = t;
 	};
-	const int staged = gr_hip_node_layout(m, n, burst, pos);
-	if (staged < 0)
-		return staged;
-	lap(GR_HIP_NODE_PROF_LAYOUT);
-	const uint32_t ns = (uint32_t)staged;
+	const uint32_t ns = was_open ? w.p : 0;
 	w.m = m;
 	w.n = n;
 	w.ns = ns;
@@ -2384,26 +2478,6 @@ extern "C" int gr_hip_node_start(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint3
 		return 0;
 	}
 	hipSetDevice(c->dev);
-	if (ns > w.cap) {
-		hipHostFree(w.lines);
-		hipHostFree(w.out);
-		hipHostFree(w.meta);
-		hipHostFree(w.v);
-		w.lines = w.out = nullptr;
-		w.meta = nullptr;
-		w.v = nullptr;
-		w.d_lines = w.d_out = w.d_meta = w.d_v = nullptr;
-		w.cap = 0;
-		HCK(hipHostMalloc((void **)&w.lines, (size_t)ns * GR_HIP_LINE, hipHostMallocDefault));
-		HCK(hipHostMalloc((void **)&w.out, (size_t)ns * GR_HIP_PREFIX, hipHostMallocDefault));
-		HCK(hipHostMalloc((void **)&w.meta, (size_t)ns * sizeof(gr_hip_pkt_meta), hipHostMallocDefault));
-		HCK(hipHostMalloc((void **)&w.v, (size_t)ns * sizeof(gr_hip_verdict), hipHostMallocDefault));
-		w.cap = ns;
-		// looked up once here, not per walk (hipPointerGetAttributes is slow)
-		if (!host_dev_ptr(w.lines, &w.d_lines) || !host_dev_ptr(w.out, &w.d_out) || !host_dev_ptr(w.meta, &w.d_meta)
-		    || !host_dev_ptr(w.v, &w.d_v))
-			w.d_lines = w.d_out = w.d_meta = w.d_v = nullptr; // not device-accessible: staged copies
-	}
 	if (q->d_pad == nullptr) { // the frame a pad slot points at (frames by address)
 		HCK(hipMalloc((void **)&q->d_pad, GR_HIP_LINE));
 		HCK(hipMemset(q->d_pad, 0, GR_HIP_LINE));
@@ -2412,10 +2486,10 @@ extern "C" int gr_hip_node_start(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint3
 	lap(GR_HIP_NODE_PROF_PREP);
 	std::shared_lock<std::shared_mutex> lk(c->mu); // see gr_hip_fwd4_submit
 	lap(GR_HIP_NODE_PROF_LOCK);
-	uint64_t *ptrs = reinterpret_cast<uint64_t *>(w.lines);
-	w.by_addr = c->node_ptrs && host_dev_ptr_ok(c, m, n, ptrs, pos);
 	int r;
 	bool enqueued = false;
+	uint64_t *ptrs = reinterpret_cast<uint64_t *>(w.lines);
+	w.by_addr = !w.lines_in && c->node_ptrs && host_dev_ptr_ok(c, m, n, ptrs, pos);
 	if (w.by_addr) {
 		// the frames are device-accessible: hand them over by address, the
 		// kernel reads and rewrites them in place over PCIe
@@ -2425,8 +2499,6 @@ extern "C" int gr_hip_node_start(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint3
 				ptrs[next] = reinterpret_cast<uint64_t>(q->d_pad);
 			next = at + 1;
 		}
-		if ((r = gr_hip_node_stage(m, n, burst, pos, nullptr, w.meta)) < 0)
-			return r;
 		if (w.d_lines == nullptr)
 			return -EFAULT;
 		gr_hip_batch b = {w.d_lines, nullptr, static_cast<const gr_hip_pkt_meta *>(w.d_meta),
@@ -2438,9 +2510,11 @@ extern "C" int gr_hip_node_start(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint3
 			return r;
 		enqueued = true;
 	} else {
-		if ((r = gr_hip_node_stage(m, n, burst, pos, w.lines, w.meta)) < 0)
-			return r;
-		lap(GR_HIP_NODE_PROF_STAGE);
+		if (!w.lines_in) { // "node_ptrs" on, but not every frame is registered: stage the lines now
+			if ((r = gr_node_stage_from(m, n, burst, pos, 0, w.lines, w.meta)) < 0)
+				return r;
+			lap(GR_HIP_NODE_PROF_STAGE);
+		}
 		// the hand-back writes back at most the first 26 bytes: packed
 		// 32-byte prefixes come back, not whole lines
 		if (c->host_direct && w.d_lines != nullptr) {
@@ -2467,6 +2541,20 @@ extern "C" int gr_hip_node_start(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint3
 	// (FIB publication) are not held behind the walk's GPU time
 	q->nw_count++;
 	return 0;
+}
+
+extern "C" int gr_hip_node_start(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst) {
+	if (q == nullptr || (n && m == nullptr))
+		return -EINVAL;
+	if (q->nw_count == GR_HIP_NODE_DEPTH)
+		return -EBUSY;
+	gr_hip_node_discard(q); // the whole walk at once: append it, send it
+	int r = gr_hip_node_append(q, m, n, burst);
+	if (r < 0) {
+		gr_hip_node_discard(q);
+		return r;
+	}
+	return gr_hip_node_send(q, m, n, burst);
 }
 
 extern "C" int gr_hip_node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np,

@@ -128,11 +128,11 @@ static inline bool walk_start(const struct gr_hip_mbuf *m, uint32_t i, uint32_t 
 	return i == 0 || (m[i].flags & GR_HIP_MBUF_F_WALK) || i - start == burst;
 }
 
-extern "C" int gr_hip_node_layout(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, uint32_t *pos) {
-	if (n && (m == nullptr || pos == nullptr))
-		return -EINVAL;
+// The walks of m (m[0] starts one) placed from slot p on; returns the first
+// slot past them.
+extern "C" uint64_t gr_node_layout_from(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, uint64_t p,
+					uint32_t *pos) {
 	burst = walk_burst(burst);
-	uint32_t p = 0;
 	for (uint32_t i = 0; i < n;) {
 		// this walk: [i, e)
 		uint32_t e = i + 1;
@@ -143,30 +143,35 @@ extern "C" int gr_hip_node_layout(const struct gr_hip_mbuf *m, uint32_t n, uint3
 		// eth_output's cache inside a tile); a longer one starts on a tile
 		// (the hand-back resolves it, eth_output_walk)
 		if ((p & 63) + len > 64)
-			p = (p + 63) & ~63u;
+			p = (p + 63) & ~63ull;
 		for (uint32_t k = i; k < e; k++)
-			pos[k] = p++;
+			pos[k] = (uint32_t)p++;
 		i = e;
 	}
+	return p;
+}
+
+extern "C" int gr_hip_node_layout(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, uint32_t *pos) {
+	if (n && (m == nullptr || pos == nullptr))
+		return -EINVAL;
+	const uint64_t p = gr_node_layout_from(m, n, burst, 0, pos);
 	if (p > INT32_MAX)
 		return -E2BIG;
 	return (int)p;
 }
 
-extern "C" int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, const uint32_t *pos,
-				 void *lines, struct gr_hip_pkt_meta *meta) {
-	if (n && (m == nullptr || meta == nullptr))
-		return -EINVAL;
+extern "C" int gr_node_stage_from(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, const uint32_t *pos,
+				  uint32_t next, void *lines, struct gr_hip_pkt_meta *meta) {
 	burst = walk_burst(burst);
 	uint8_t *L = static_cast<uint8_t *>(lines);
 	constexpr uint32_t AHEAD = 16; // frames in flight: staging is bound by their cache misses
 	for (uint32_t i = 0; i < n && i < AHEAD && L != nullptr; i++)
 		__builtin_prefetch(m[i].frame, 0, 0);
-	uint32_t start = 0, next = 0; // next: first slot not yet written
+	uint32_t start = 0; // next: first slot not yet written
 	for (uint32_t i = 0; i < n; i++) {
 		if (i + AHEAD < n && L != nullptr)
 			__builtin_prefetch(m[i + AHEAD].frame, 0, 0);
-		const uint32_t at = pos != nullptr ? pos[i] : i;
+		const uint32_t at = pos != nullptr ? pos[i] : next;
 		for (; next < at; next++) { // a pad slot: punted by the kernel, counted nowhere
 			meta[next] = gr_hip_pkt_meta{0, 0, 0, 0};
 			if (L != nullptr)
@@ -192,6 +197,13 @@ extern "C" int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, uint32
 		meta[at].rss = (uint16_t)m[i].rss;
 	}
 	return 0;
+}
+
+extern "C" int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, const uint32_t *pos,
+				 void *lines, struct gr_hip_pkt_meta *meta) {
+	if (n && (m == nullptr || meta == nullptr))
+		return -EINVAL;
+	return gr_node_stage_from(m, n, burst, pos, 0, lines, meta);
 }
 
 // The VLAN sub-interface of (parent, vlan_id) in the host image of the

@@ -1,7 +1,8 @@
 // SPDX-License-Identifier: BSD-3-Clause
 //
 // gr_node_priv.h -- what gr_hip.cpp and gr_node.cpp share beyond the C ABI:
-// the node hand-back with the context's VLAN table and per-iface counters.
+// the node's staging continued across appends, and its hand-back with the
+// context's VLAN table and per-iface counters.
 #pragma once
 
 #include "../../include/grout_hip.h"
@@ -17,6 +18,14 @@ struct gr_node_vlans {
 	const uint16_t *vals;
 	uint32_t cap; // power of two, or 0
 };
+
+// gr_hip_node_layout continuing at slot p (m[0] starts a walk); returns the
+// first slot past the walks.
+uint64_t gr_node_layout_from(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, uint64_t p, uint32_t *pos);
+// gr_hip_node_stage continuing at slot `next` (the first one not yet
+// written: pad slots from there up to pos[0] are zeroed).
+int gr_node_stage_from(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, const uint32_t *pos, uint32_t next,
+		       void *lines, struct gr_hip_pkt_meta *meta);
 
 // gr_hip_node_apply, also adding each packet's rx / tx to ifst[iface id]
 // (n_ifst entries) where grout's iface_input / iface_output count them.

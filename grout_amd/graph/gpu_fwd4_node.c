@@ -484,18 +484,23 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 	w->first_ns = 0;
 	if (gpus[w->gpu].diverged) { // not to this GPU: grout's CPU nodes, after the batch before
 		const uint32_t d = finish_pending(graph, node, w);
+		gr_hip_node_discard(w->q);
 		deliver(graph, node, w, k, n, -ESTALE);
 		return d + n;
 	}
 	if (conf.depth < 2 && !w->pending) { // synchronous
 		started(w, n);
-		deliver(graph, node, w, k, n, gr_hip_node_process(w->q, w->v[k], n, WALK_SPLIT, &w->stats));
+		int r = gr_hip_node_send(w->q, w->v[k], n, WALK_SPLIT);
+		if (r == 0)
+			r = gr_hip_node_finish(w->q, NULL, NULL, &w->stats);
+		deliver(graph, node, w, k, n, r);
 		return n;
 	}
-	// stage and send this batch while the previous one may still be on the
-	// GPU, then hand the previous one back: batches leave in arrival order
+	// send this batch (staged as it arrived, gpu_fwd4_process) while the
+	// previous one may still be on the GPU, then hand the previous one back:
+	// batches leave in arrival order
 	PROF_T0();
-	const int r = gr_hip_node_start(w->q, w->v[k], n, WALK_SPLIT);
+	const int r = gr_hip_node_send(w->q, w->v[k], n, WALK_SPLIT);
 	PROF_ADD(GPU_FWD4_PROF_START);
 	const uint32_t delivered = finish_pending(graph, node, w);
 	if (r < 0) { // the GPU did not take it: grout's CPU nodes do (after the one before, in order)
@@ -534,6 +539,7 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 		return nb_objs;
 	}
 	uint8_t walk = GR_HIP_MBUF_F_WALK; // this call is one graph walk's iface_input stream
+	const uint32_t n0 = w->n;
 	for (uint16_t i = 0; i < nb_objs; i++) {
 		struct rte_mbuf *m = objs[i];
 		// grout's CPU nodes: multi-segment or traced mbufs; and, never in
@@ -561,6 +567,10 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 		};
 		walk = 0;
 	}
+	// stage this walk now, while its mbufs and frames are in cache (a failure
+	// makes the send refuse the batch: grout's CPU nodes take it, untouched)
+	if (w->n > n0)
+		gr_hip_node_append(w->q, &w->v[w->cur][n0], w->n - n0, WALK_SPLIT);
 	PROF_ADD(GPU_FWD4_PROF_ACCUMULATE);
 	if (w->n == 0) {
 		reap(graph, node, w);

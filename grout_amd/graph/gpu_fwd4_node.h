@@ -119,8 +119,8 @@ int gpu_fwd4_set_rx_burst(uint32_t rx_burst);
 // Measurement: nanoseconds the node spent, per phase, since the last call
 // (then reset); on = 0 stops accumulating. out: GPU_FWD4_PROF_COUNT values.
 enum {
-	GPU_FWD4_PROF_ACCUMULATE, // process(): mbufs into the batch's gr_hip_mbuf views
-	GPU_FWD4_PROF_START, // gr_hip_node_start: layout, staging, launch
+	GPU_FWD4_PROF_ACCUMULATE, // process(): mbufs into the batch's gr_hip_mbuf views, staged (gr_hip_node_append)
+	GPU_FWD4_PROF_START, // gr_hip_node_send: launch
 	GPU_FWD4_PROF_FINISH, // gr_hip_node_finish: wait for the GPU, hand-back onto the views
 	GPU_FWD4_PROF_DELIVER, // the views onto the rte_mbufs + private data, enqueues
 	GPU_FWD4_PROF_COUNT,

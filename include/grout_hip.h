@@ -683,6 +683,23 @@ int gr_hip_node_process(gr_hip_queue_t *, struct gr_hip_mbuf *m, uint32_t n, uin
 #define GR_HIP_NODE_DEPTH 2
 int gr_hip_node_start(gr_hip_queue_t *, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst);
 int gr_hip_node_finish(gr_hip_queue_t *, struct gr_hip_mbuf **m, uint32_t *n, struct gr_hip_node_stats *stats);
+// The start half fused with the node's own pass over its mbufs, so that each
+// rte_mbuf is touched once: the node appends each rte_graph walk's views as
+// the walk brings them (gr_hip_node_append lays them out and stages their
+// header lines and metadata into the queue's open walk slot at once, while
+// the frames are in cache), then sends what it appended (gr_hip_node_send,
+// with m / n = every view appended since the last send, in order: the same
+// pointer the appends read, kept until finish). The layout and the staged
+// bytes are gr_hip_node_start's for the same views, and the walk finishes
+// the same way. Each append after the first of a slot must start with a
+// GR_HIP_MBUF_F_WALK view (-EINVAL otherwise). append returns the slots
+// staged so far, -EBUSY while GR_HIP_NODE_DEPTH walks are in flight; send
+// returns 0, or -EINVAL when m / n are not what was appended (the appended
+// walk is dropped, the views untouched). gr_hip_node_discard drops what was
+// appended and not sent (a walk that will not go to the GPU).
+int gr_hip_node_append(gr_hip_queue_t *, const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst);
+int gr_hip_node_send(gr_hip_queue_t *, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst);
+int gr_hip_node_discard(gr_hip_queue_t *);
 // Walks in flight on the queue; *ready (optional) = 1 when the oldest one's
 // GPU work has completed (its finish will not wait).
 int gr_hip_node_pending(gr_hip_queue_t *, int *ready);
@@ -698,14 +715,14 @@ int gr_hip_node_pending(gr_hip_queue_t *, int *ready);
 // max_ifaces entries, indexed by iface id.
 int gr_hip_node_iface_stats(gr_hip_queue_t *, struct gr_hip_iface_stats *stats, uint32_t max_ifaces, int reset);
 
-// Measurement: nanoseconds gr_hip_node_start spent in each part, summed over
+// Measurement: nanoseconds gr_hip_node_start (append + send) spent in each part, summed over
 // every queue of the process since the last reset. out[k] for k < n; returns
 // GR_HIP_NODE_PROF_COUNT.
 enum {
-	GR_HIP_NODE_PROF_LAYOUT, // gr_hip_node_layout
-	GR_HIP_NODE_PROF_PREP, // staging buffers grown, verdicts filled
+	GR_HIP_NODE_PROF_LAYOUT, // (unused: the layout is part of the staging)
+	GR_HIP_NODE_PROF_PREP, // verdicts filled
 	GR_HIP_NODE_PROF_LOCK, // the context lock, shared
-	GR_HIP_NODE_PROF_STAGE, // gr_hip_node_stage
+	GR_HIP_NODE_PROF_STAGE, // layout + staging (gr_hip_node_append), buffers grown
 	GR_HIP_NODE_PROF_LAUNCH, // the kernel launch (host_direct)
 	GR_HIP_NODE_PROF_RECORD, // the walk's completion event
 	GR_HIP_NODE_PROF_COUNT,

@@ -369,3 +369,66 @@ def test_node_pipelined_walks(fastpath, ptrs):
         if ptrs:
             abi.check("gr_hip_host_unregister", L.gr_hip_host_unregister(fastpath.h, bufs.ctypes.data))
         q.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ptrs", [0, 1])
+def test_node_append_send(fastpath, ptrs):
+    """gr_hip_node_append / _send: the walks of a batch staged one call at a
+    time as they arrive (the grout node's path) end exactly as one
+    gr_hip_node_start of the same views (the oracle's mbufs), walks of every
+    length up to 256 included. A later append whose first view does not
+    start a walk, and a send of other views than were appended, are
+    refused (-EINVAL) and leave the queue usable; discard drops an append."""
+    from golden_util import fresh_fastpath_state
+    topo = T.config_fullview(count=100_000)
+    fr, me = S.stream(30_000, 0xA99E, routes=topo.route_array())
+    fresh_fastpath_state(fastpath, topo)
+    rng = np.random.default_rng(7)
+    cuts = [0]
+    while cuts[-1] < len(fr):
+        cuts.append(min(len(fr), cuts[-1] + int(rng.choice([1, 3, 17, 63, 64, 65, 128, 200, 256]))))
+    walks = list(zip(cuts, cuts[1:]))
+    meta_walk = me.copy()
+    meta_walk["vlan_ck"][[a for a, _ in walks]] |= abi.META_WALK
+    lines, v, st, want, ns_want = oracle.Oracle(topo).process_mbufs(fr, meta_walk, lines_only=True, burst=256)
+    bufs, m = mbufs_for(fr, me)
+    m["flags"][[a for a, _ in walks]] |= abi.MBUF_F_WALK
+    L = fastpath.lib
+    if ptrs:
+        abi.check("gr_hip_host_register", L.gr_hip_host_register(fastpath.h, bufs.ctypes.data, bufs.nbytes))
+    q = fastpath.queue()
+    try:
+        fastpath.tune("node_ptrs", ptrs)
+        # refused appends and sends, then a discarded one
+        assert L.gr_hip_node_append(q._h, m.ctypes.data, 10, 256) > 0
+        assert L.gr_hip_node_append(q._h, m[5:].ctypes.data, 3, 256) == -22  # m[5] starts no walk
+        assert L.gr_hip_node_send(q._h, m.ctypes.data, 11, 256) == -22  # 10 were appended
+        assert q.node_pending()[0] == 0
+        assert L.gr_hip_node_append(q._h, m.ctypes.data, 10, 256) > 0
+        assert L.gr_hip_node_discard(q._h) == 0
+        # the batch, one walk per append, in two halves pipelined
+        half = walks[len(walks) // 2][0]
+        ns_tot = np.zeros(1, dtype=abi.NODE_STATS_DT)[0]
+        for lo, hi in ((0, half), (half, len(m))):
+            part = m[lo:hi]
+            for a, b in walks:
+                if lo <= a < hi:
+                    staged = L.gr_hip_node_append(q._h, part[a - lo:].ctypes.data, b - a, 256)
+                    assert staged >= b - lo, (a, b, staged)
+            abi.check("gr_hip_node_send", L.gr_hip_node_send(q._h, part.ctypes.data, len(part), 256))
+            q._walks.append(part)
+        for _ in range(2):
+            got, ns = q.node_finish()
+            assert q.unfinished == 0
+            ns_tot["packets"] += ns["packets"]
+            ns_tot["calls"] += ns["calls"]
+        compare_mbufs(m, want, bufs, lines)
+        assert np.array_equal(ns_tot["packets"], ns_want["packets"])
+        assert np.array_equal(ns_tot["calls"], ns_want["calls"])
+        assert np.array_equal(q.stats(), st)
+    finally:
+        fastpath.tune("node_ptrs", 0)
+        if ptrs:
+            abi.check("gr_hip_host_unregister", L.gr_hip_host_unregister(fastpath.h, bufs.ctypes.data))
+        q.close()
