@@ -16,8 +16,10 @@
 // Per graph (one per worker, worker.c) the node keeps a walk: the mbufs of
 // successive RX bursts accumulate until a batch is full, an RX burst comes
 // back short (the queue drained: latency matters more than batching) or the
-// oldest packet has waited max_delay; then the batch's header lines are
-// staged and sent to the GPU (gr_hip_node_start), and once the GPU is done
+// oldest packet has waited max_delay. Each process() call's mbufs are
+// staged as they arrive (gr_hip_node_append: header line and metadata into
+// the queue's pinned walk slot while the frames are in cache), the batch is
+// sent to the GPU at the flush (gr_hip_node_send), and once the GPU is done
 // the batch is handed back (gr_hip_node_finish): each mbuf is enqueued on
 // its verdict's edge with grout's private data for that edge. Batches are
 // pipelined two deep ("depth" 2, the default): while the GPU forwards one,

@@ -22,6 +22,7 @@
 
 #include <errno.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <time.h>
@@ -664,9 +665,16 @@ int gh_rcu_delete_test(uint32_t slot, uint16_t iface_id, uint32_t hold_ms, struc
 			return -EAGAIN;
 	}
 	pthread_t th;
+	struct rte_rcu_qsbr *v = gr_datapath_rcu();
+	const uint64_t tok0 = __atomic_load_n(&v->token, __ATOMIC_ACQUIRE);
 	if (pthread_create(&th, NULL, rcu_control, NULL) != 0)
 		return -EAGAIN;
-	rte_rcu_qsbr_quiescent(gr_datapath_rcu(), rte_lcore_id()); // the worker's housekeeping
+	// the worker's housekeeping, once the control thread's synchronize has
+	// started (a quiescent state reported before its token would not count)
+	for (const uint64_t t_max = mono_us() + 1000000u;
+	     __atomic_load_n(&v->token, __ATOMIC_ACQUIRE) == tok0 && mono_us() < t_max;)
+		sched_yield();
+	rte_rcu_qsbr_quiescent(v, rte_lcore_id());
 	usleep(hold_ms * 1000u);
 	res->sync_before_handback = __atomic_load_n(&R.done, __ATOMIC_ACQUIRE);
 	const uint64_t t_end = mono_us() + 5000000u;
