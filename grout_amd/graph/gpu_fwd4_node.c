@@ -15,20 +15,21 @@
 //
 // Per graph (one per worker, worker.c) the node keeps a walk: the mbufs of
 // successive RX bursts accumulate until a batch is full, an RX burst comes
-// back short (the queue drained: latency matters more than batching) or the
-// oldest packet has waited max_delay. Each process() call's mbufs are
-// staged as they arrive (gr_hip_node_append: header line and metadata into
-// the queue's pinned walk slot while the frames are in cache), the batch is
-// sent to the GPU at the flush (gr_hip_node_send), and once the GPU is done
+// back short or a whole graph walk brings none (the queues drained: latency
+// matters more than batching), or the oldest packet has waited max_delay.
+// Each process() call's mbufs are staged as they arrive (gr_hip_node_append:
+// header line and metadata into the queue's pinned walk slot while the
+// frames are in cache), the batch is sent to the GPU at the flush
+// (gr_hip_node_send), and once the GPU is done
 // the batch is handed back (gr_hip_node_finish): each mbuf is enqueued on
 // its verdict's edge with grout's private data for that edge. Batches are
 // pipelined two deep ("depth" 2, the default): while the GPU forwards one,
 // the worker accumulates and stages the next, and hands the one before back
 // as soon as it is done. Batches leave in the order they arrived. A source
 // node, "gpu_fwd4_flush", runs every graph walk: it hands back a batch whose
-// GPU work has completed, and flushes a batch whose packets have waited
-// max_delay when no new burst arrives (rte_graph calls a node only when it
-// holds objects).
+// GPU work has completed, and flushes the batch held when the walk before
+// brought no packet or its oldest packet has waited max_delay (rte_graph
+// calls a node only when it holds objects).
 //
 // RCU. A batch's mbufs stay with the node across graph walks (accumulation,
 // then the GPU), and grout's worker reports a QSBR quiescent state every 256
@@ -281,6 +282,7 @@ struct gpu_walk {
 	struct gr_hip_iface_stats *ifs; // gpu_fwd4_stats_flush's buffer [conf.max_ifaces]
 	uint64_t gpu_errors; // batches punted because the GPU call failed
 	uint64_t batches, max_batch, stale;
+	int rx_seen; // the node took packets since the flush node last ran
 };
 
 static uint64_t now_ns(void) {
@@ -542,6 +544,7 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 	}
 	uint8_t walk = GR_HIP_MBUF_F_WALK; // this call is one graph walk's iface_input stream
 	const uint32_t n0 = w->n;
+	w->rx_seen = 1;
 	for (uint16_t i = 0; i < nb_objs; i++) {
 		struct rte_mbuf *m = objs[i];
 		// grout's CPU nodes: multi-segment or traced mbufs; and, never in
@@ -716,7 +719,11 @@ static uint16_t gpu_flush_process(struct rte_graph *graph, struct rte_node *node
 		n = finish_pending(graph, node, w); // waited long enough: wait for the GPU
 	else
 		n = reap(graph, node, w);
-	if (w->n != 0 && t - w->first_ns >= conf.max_delay_ns)
+	// a whole graph walk brought the node nothing: the RX queues drained,
+	// latency wins over batching (as for a short burst); else max_delay
+	const int idle = !w->rx_seen;
+	w->rx_seen = 0;
+	if (w->n != 0 && (idle || t - w->first_ns >= conf.max_delay_ns))
 		n += flush(graph, node, w); // pipelined: a later walk of the graph hands it back
 	return (uint16_t)(n > UINT16_MAX ? UINT16_MAX : n);
 }

@@ -6,9 +6,13 @@ batches of --batch packets, the GPU forwards them and the node hands every
 mbuf to the recorder node of its edge (walk_harness.c). One worker thread,
 one graph; depth 1 (each batch waited for) against depth 2 (pipelined,
 the default), alternating, --reps times each. Mpps = mbufs / wall time of
-gh_run (one C call: no Python in the loop).
+gh_run (one C call: no Python in the loop). The hold time (--max-delay-us)
+is long enough that --batch sets the flush (full RX bursts never flush
+early): each line reports the batches the node started and the largest.
+--cpu-baseline adds the oracle's C chain on one core over the same stream
+(bench.py's cpu_baseline.single_core_mpps, same box).
 
-    python tools/node_graph_rate.py --batch 16384 > out.jsonl
+    python tools/node_graph_rate.py --batch 16384 --cpu-baseline > out.jsonl
 """
 import argparse
 import ctypes
@@ -32,6 +36,8 @@ def main():
     ap.add_argument("--pin", type=int, default=0, help="1: frames by address (node_ptrs)")
     ap.add_argument("--depths", default="1,2")
     ap.add_argument("--rx-touch", default="0", help="harness port_rx leaves mbuf and frame cached (PMD + DDIO): 0,1")
+    ap.add_argument("--max-delay-us", type=float, default=20_000.0, help="the node's hold time")
+    ap.add_argument("--cpu-baseline", action="store_true")
     args = ap.parse_args()
 
     import test_graph_walk as G  # the harness bindings and the fan-out control plane
@@ -43,7 +49,7 @@ def main():
     L.gpu_fwd4_prof.argtypes = [ctypes.c_int, ctypes.c_void_p]
     L.gpu_fwd4_prof.restype = None
     devs = (ctypes.c_int * 1)(0)
-    r = L.gh_init(ctypes.cast(devs, ctypes.c_void_p), 1, 1024, 1 << 17, args.batch, 64, 50_000)
+    r = L.gh_init(ctypes.cast(devs, ctypes.c_void_p), 1, 1024, 1 << 17, args.batch, 64, int(args.max_delay_us * 1e3))
     assert r == 0, r
     assert L.gh_graph_create(0, 0) == 0
     G._gh["fp"] = fp = G.FanOutPath(L)
@@ -64,9 +70,11 @@ def main():
             L.gpu_fwd4_prof(1, None)
             H = abi.hip()
             H.gr_hip_node_prof(None, 0, 1)
+            wi0 = G.walk_info()
             t0 = time.perf_counter()
             walks = L.gh_run(1 << 24)
             dt = time.perf_counter() - t0
+            wi = G.walk_info()
             ph = np.zeros(4, dtype=np.uint64)
             L.gpu_fwd4_prof(0, ph.ctypes.data)
             lp = np.zeros(6, dtype=np.uint64)
@@ -79,12 +87,23 @@ def main():
             names = ["accumulate", "start", "finish", "deliver"]
             per = {k: round(float(v) / len(me), 2) for k, v in zip(names, ph)}
             per["rest_of_walk"] = round(dt * 1e9 / len(me) - sum(per.values()), 2)
-            print(json.dumps({"batch": args.batch, "depth": depth, "rx_touch": touch, "mbufs": len(me), "graph_walks": walks,
+            print(json.dumps({"batch": args.batch, "max_delay_us": args.max_delay_us, "depth": depth, "rx_touch": touch,
+                              "mbufs": len(me), "graph_walks": walks,
+                              "node_batches": int(wi["batches"] - wi0["batches"]), "max_batch": int(wi["max_batch"]),
                               "ms": round(dt * 1e3, 2), "mpps": round(len(me) / dt / 1e6, 1),
                               "ns_per_pkt": per,
                               "start_ns_per_pkt": {k: round(float(v) / len(me), 2) for k, v in zip(
                                   ["layout", "prep", "lock", "stage", "launch", "record"], lp)},
                               "mode": "frames by address" if args.pin else "staged lines"}), flush=True)
+
+
+    if args.cpu_baseline:
+        import oracle
+        o = oracle.Oracle(topo)
+        m1, _ = o.bench(fr[: 1 << 20].copy(), me[: 1 << 20].copy(), 1, 4_000_000)
+        o.close()
+        print(json.dumps({"cpu_baseline_single_core_mpps": round(m1, 2),
+                          "sample": "oracle C chain, 1 pinned thread, 4M packets of this stream"}), flush=True)
 
 
 if __name__ == "__main__":
