@@ -545,8 +545,20 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 	uint8_t walk = GR_HIP_MBUF_F_WALK; // this call is one graph walk's iface_input stream
 	const uint32_t n0 = w->n;
 	w->rx_seen = 1;
+	// software pipeline over the burst (as DPDK's l3fwd does): each mbuf
+	// PF_MBUF ahead, its frame PF_FRAME ahead, so that their misses overlap
+	// and the staging below finds the frames in cache
+	enum { PF_MBUF = 8, PF_FRAME = 4 };
+	for (uint16_t i = 0; i < nb_objs && i < PF_MBUF; i++)
+		rte_prefetch0(objs[i]);
+	for (uint16_t i = 0; i < nb_objs && i < PF_FRAME; i++)
+		rte_prefetch0(rte_pktmbuf_mtod((struct rte_mbuf *)objs[i], void *));
 	for (uint16_t i = 0; i < nb_objs; i++) {
 		struct rte_mbuf *m = objs[i];
+		if (i + PF_MBUF < nb_objs)
+			rte_prefetch0(objs[i + PF_MBUF]);
+		if (i + PF_FRAME < nb_objs)
+			rte_prefetch0(rte_pktmbuf_mtod((struct rte_mbuf *)objs[i + PF_FRAME], void *));
 		// grout's CPU nodes: multi-segment or traced mbufs; and, never in
 		// practice (a batch starts below conf.batch and a call brings at
 		// most RTE_GRAPH_BURST_SIZE), a full buffer

@@ -72,6 +72,10 @@ struct rte_mbuf {
 _Static_assert(sizeof(struct rte_mbuf) == 128, "rte_mbuf is two cache lines");
 
 #define rte_pktmbuf_mtod(m, t) ((t)((char *)(m)->buf_addr + (m)->data_off))
+// rte_prefetch.h: into every cache level
+static inline void rte_prefetch0(const volatile void *p) {
+	__builtin_prefetch((const void *)p, 0, 3);
+}
 // DPDK puts the mbuf back in m->pool; the stand-in's mbufs belong to the harness
 static inline void rte_pktmbuf_free(struct rte_mbuf *m) {
 	(void)m;

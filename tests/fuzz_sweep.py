@@ -2,7 +2,9 @@
 path against the oracle (whole frames, header lines, in place), one line
 per mismatching seed and a JSON summary at the end.
 
-    python tools/fuzz_sweep.py --seeds 300 [--first 0x10000]
+    python tests/fuzz_sweep.py --seeds 300 [--first 0x10000]
+
+Test infrastructure (it runs the oracle as the checker), so it lives under tests/.
 """
 import argparse
 import json

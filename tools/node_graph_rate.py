@@ -9,10 +9,10 @@ the default), alternating, --reps times each. Mpps = mbufs / wall time of
 gh_run (one C call: no Python in the loop). The hold time (--max-delay-us)
 is long enough that --batch sets the flush (full RX bursts never flush
 early): each line reports the batches the node started and the largest.
---cpu-baseline adds the oracle's C chain on one core over the same stream
-(bench.py's cpu_baseline.single_core_mpps, same box).
+Compare with bench.py's cpu_baseline.single_core_mpps run on the same box
+(the oracle is test infrastructure: only bench.py's baseline leg runs it).
 
-    python tools/node_graph_rate.py --batch 16384 --cpu-baseline > out.jsonl
+    python tools/node_graph_rate.py --batch 16384 > out.jsonl
 """
 import argparse
 import ctypes
@@ -37,7 +37,6 @@ def main():
     ap.add_argument("--depths", default="1,2")
     ap.add_argument("--rx-touch", default="0", help="harness port_rx leaves mbuf and frame cached (PMD + DDIO): 0,1")
     ap.add_argument("--max-delay-us", type=float, default=20_000.0, help="the node's hold time")
-    ap.add_argument("--cpu-baseline", action="store_true")
     args = ap.parse_args()
 
     import test_graph_walk as G  # the harness bindings and the fan-out control plane
@@ -96,14 +95,6 @@ def main():
                                   ["layout", "prep", "lock", "stage", "launch", "record"], lp)},
                               "mode": "frames by address" if args.pin else "staged lines"}), flush=True)
 
-
-    if args.cpu_baseline:
-        import oracle
-        o = oracle.Oracle(topo)
-        m1, _ = o.bench(fr[: 1 << 20].copy(), me[: 1 << 20].copy(), 1, 4_000_000)
-        o.close()
-        print(json.dumps({"cpu_baseline_single_core_mpps": round(m1, 2),
-                          "sample": "oracle C chain, 1 pinned thread, 4M packets of this stream"}), flush=True)
 
 
 if __name__ == "__main__":
