@@ -23,6 +23,8 @@
 #include <errno.h>
 #include <pthread.h>
 #include <sched.h>
+#include <stdint.h>
+#include <sys/mman.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <time.h>
@@ -55,7 +57,9 @@ struct gh_mbuf_out { // per injected mbuf, in injection order
 };
 
 static struct {
-	uint8_t *mem;
+	uint8_t *mem; // the mbufs (mbuf_mem_alloc)
+	void *mem_map;
+	size_t mem_len;
 	uint32_t n, next_rx, recorded;
 	uint32_t rx_burst;
 	const struct gr_hip_pkt_meta *meta_in;
@@ -445,17 +449,42 @@ int gh_graph_destroy(void) {
 	return r;
 }
 
+// The mbufs' memory. DPDK's mempools live in hugepages (EAL), so the
+// stand-in's mbufs are on transparent huge pages: 2 MiB aligned, madvised,
+// zeroed (a page per mbuf would add a TLB miss per packet no grout worker
+// has).
+static void mbuf_mem_free(void) {
+	if (H.mem_map != NULL)
+		munmap(H.mem_map, H.mem_len);
+	H.mem_map = NULL;
+	H.mem = NULL;
+	H.mem_len = 0;
+}
+
+static int mbuf_mem_alloc(size_t bytes) {
+	const size_t huge = (size_t)2 << 20;
+	const size_t len = ((bytes + huge - 1) & ~(huge - 1)) + huge;
+	void *p = mmap(NULL, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+	if (p == MAP_FAILED)
+		return -ENOMEM;
+	uint8_t *a = (uint8_t *)(((uintptr_t)p + huge - 1) & ~(uintptr_t)(huge - 1));
+	(void)madvise(a, len - (size_t)(a - (uint8_t *)p), MADV_HUGEPAGE); // best effort
+	H.mem_map = p;
+	H.mem_len = len;
+	H.mem = a;
+	return 0;
+}
+
 int gh_load(const uint8_t *frames, uint32_t stride, const struct gr_hip_pkt_meta *meta, uint32_t n) {
 	if (stride > GH_ROOM - RTE_PKTMBUF_HEADROOM)
 		return -EINVAL;
 	unpin();
-	free(H.mem);
+	mbuf_mem_free();
 	free(H.edge_of);
 	free(H.seq_of);
-	H.mem = calloc(n ? n : 1, GH_MBUF_SZ);
 	H.edge_of = malloc(n ? n : 1);
 	H.seq_of = calloc(n ? n : 1, sizeof(uint32_t));
-	if (H.mem == NULL || H.edge_of == NULL || H.seq_of == NULL)
+	if (mbuf_mem_alloc((size_t)(n ? n : 1) * GH_MBUF_SZ) < 0 || H.edge_of == NULL || H.seq_of == NULL)
 		return -ENOMEM;
 	memset(H.edge_of, 0xff, n);
 	for (uint32_t i = 0; i < n; i++) {
@@ -793,10 +822,9 @@ void gh_fini(void) {
 		rte_rcu_qsbr_thread_unregister(gr_datapath_rcu(), 0);
 	H.cur = -1;
 	gr_modules_fini(NULL);
-	free(H.mem);
+	mbuf_mem_free();
 	free(H.edge_of);
 	free(H.seq_of);
-	H.mem = NULL;
 	H.edge_of = NULL;
 	H.seq_of = NULL;
 	H.n = 0;
