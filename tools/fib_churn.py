@@ -116,7 +116,7 @@ def main():
     out["load_batched"] = {"routes": count, "add_s": round(t1 - t0, 3), "commit_s": round(t2 - t1, 4),
                            "routes_per_s": round(count / (t2 - t0)),
                            "second_commit_s": round(t3 - t2, 4),
-                           "note": "one gr_hip_route4_add of all routes, then one commit (the first writes one "
+                           "note": "one route add call of all routes (gr_hip_route4_add / gr_hip_route6_add), then one commit (the first writes one "
                                    "copy whole; the second commit writes the other copy whole)"}
     print(json.dumps(out["load_batched"]), file=sys.stderr, flush=True)
 
