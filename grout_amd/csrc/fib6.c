@@ -29,7 +29,12 @@
 //      wide group of 256 consecutive slots indexed by two bytes when it holds
 //      at least GR_FIB6_WIDE_MIN child groups and no skip (its children then
 //      are its rows), or when it is a one-byte skip over a child heading at
-//      least GR_FIB6_SKIP_WIDE_MIN groups. Every write compares, and the
+//      least GR_FIB6_SKIP_WIDE_MIN groups. A wide group's rows keep one entry
+//      per 2^s of the second byte when its children's entries only change at
+//      multiples of 2^s there (their granularity: prefixes that end inside
+//      that byte, as fib_inject's /42, /44 and /46 do): 2^(8-s) slots instead
+//      of 256, so that a route's entry shares its lines with its neighbours'
+//      instead of owning one. Every write compares, and the
 //      slots, skips and first-level entries that changed form the dirty
 //      lists a commit uploads (gr_fib6_dirty).
 #include "fib6.h"
@@ -51,7 +56,7 @@ struct rib6_ent {
 #define REF 0x80000000u // a plain entry holding a child node (index in bits 0-30)
 
 enum { CK_LEAF, CK_SKIP, CK_GROUP }; // compressed kind
-enum { R_NONE, R_STANDALONE, R_ROWS, R_MERGED }; // how the image holds a node
+enum { R_NONE, R_STANDALONE, R_ROWS, R_MERGED, R_RANGE }; // how the image holds a node
 enum { OBJ_NONE, OBJ_SLOT, OBJ_RUN, OBJ_SKIP }; // what it owns in the image
 
 struct node {
@@ -67,6 +72,13 @@ struct node {
 	uint8_t sk_n; // CK_SKIP: key bytes
 	uint8_t sk_key[7];
 	uint8_t role, obj;
+	uint8_t gran; // its entries change only at multiples of 2^gran (0..8): a row may keep 1 per 2^gran
+	uint8_t run_c; // OBJ_RUN: the run's size, 2^run_c slots
+	uint8_t row_s; // R_ROWS: the shift of the wide group holding its row
+	// range shape (leaves only, one run of rs_in over [rs_lo, rs_hi], rs_miss
+	// elsewhere): a parent range group holds it in one 8-byte entry
+	uint8_t rs_ok, rs_lo, rs_hi;
+	uint32_t rs_in, rs_miss;
 	uint16_t n_grp_ch, n_skip_ch; // children of kind CK_GROUP / CK_SKIP
 	uint32_t cval; // CK_LEAF: the leaf; CK_SKIP: the miss leaf
 	uint32_t chain; // CK_SKIP: past the key, a leaf or REF | node (the chain's end)
@@ -75,7 +87,7 @@ struct node {
 	// the device image (layer 3)
 	uint32_t obj_idx; // slot, first slot of a run, or skip index
 	uint32_t enc; // R_STANDALONE: the entry that stands for it
-	uint32_t row_at; // R_ROWS: the slot holding its row
+	uint32_t row_at; // R_ROWS: the first entry of its row in the groups array
 };
 
 struct u32vec {
@@ -115,7 +127,8 @@ struct gr_fib6 {
 	uint32_t *groups; // max_groups * GR_FIB6_GROUP
 	struct gr_fib6_skip *skips; // max_groups
 	uint32_t max_groups, slot_hw, slots_live, skip_hw, skips_live;
-	struct u32vec slot_free, run_free, skip_free;
+	struct u32vec slot_free, skip_free;
+	struct u32vec run_free[9]; // free runs of 2^c slots, c = 1..8
 	// what the builds since the last gr_fib6_dirty_clear changed in the image
 	uint8_t *slot_dirty, *skip_dirty, *top_dirty;
 	struct u32vec d_slots, d_skips, d_top;
@@ -172,7 +185,7 @@ gr_fib6_t *gr_fib6_new(uint32_t max_routes, uint32_t max_groups) {
 		return NULL;
 	if (max_groups == 0)
 		max_groups = 1u << 16;
-	if (max_groups > GR_FIB6_IDX)
+	if (max_groups > GR_FIB6_WIDE_IDX)
 		return NULL;
 	gr_fib6_t *f = calloc(1, sizeof(*f));
 	if (f == NULL)
@@ -212,7 +225,8 @@ void gr_fib6_free(gr_fib6_t *f) {
 	free(f->groups);
 	free(f->skips);
 	free(f->slot_free.v);
-	free(f->run_free.v);
+	for (int c = 0; c < 9; c++)
+		free(f->run_free[c].v);
 	free(f->skip_free.v);
 	free(f->slot_dirty);
 	free(f->skip_dirty);
@@ -531,20 +545,36 @@ static inline int put(gr_fib6_t *f, uint32_t s, int i, uint32_t v) {
 	return mark_slot(f, s);
 }
 
+// A free run of 2^c slots (c = 1..8), splitting a larger free one if need
+// be (its other halves go back to their classes); -ENOSPC when none.
+static int run_pop(gr_fib6_t *f, unsigned c, uint32_t *w) {
+	unsigned k = c;
+	while (k <= 8 && f->run_free[k].n == 0)
+		k++;
+	if (k > 8)
+		return -ENOSPC;
+	const uint32_t x = f->run_free[k].v[--f->run_free[k].n];
+	for (unsigned j = k; j > c; j--)
+		if (vpush(&f->run_free[j - 1], x + (1u << (j - 1))) < 0)
+			return -ENOMEM;
+	*w = x;
+	return 0;
+}
+
 // A new slot: written whole this build, whatever the image held there.
 static int slot_alloc(gr_fib6_t *f, uint32_t *s) {
 	if (f->slot_free.n) {
 		*s = f->slot_free.v[--f->slot_free.n];
 	} else if (f->slot_hw < f->max_groups) {
 		*s = f->slot_hw++;
-	} else if (f->run_free.n) { // break a free run into single slots
-		const uint32_t w = f->run_free.v[--f->run_free.n];
-		for (uint32_t k = GR_FIB6_GROUP - 1; k >= 1; k--)
-			if (vpush(&f->slot_free, w + k) < 0)
-				return -ENOMEM;
-		*s = w;
 	} else {
-		return -ENOSPC;
+		uint32_t w; // break the smallest free run into single slots
+		int r = run_pop(f, 1, &w);
+		if (r < 0)
+			return r;
+		if ((r = vpush(&f->slot_free, w + 1)) < 0)
+			return r;
+		*s = w;
 	}
 	f->slots_live++;
 	return mark_slot(f, *s);
@@ -556,21 +586,26 @@ static void slot_free(gr_fib6_t *f, uint32_t s) {
 	(void)vpush(&f->slot_free, s); // a failed push only leaks the slot
 }
 
-static bool run_available(const gr_fib6_t *f) {
-	return f->run_free.n || f->slot_hw + GR_FIB6_GROUP <= f->max_groups;
+static bool run_available(const gr_fib6_t *f, unsigned c) {
+	for (unsigned k = c; k <= 8; k++)
+		if (f->run_free[k].n)
+			return true;
+	return f->slot_hw + (1u << c) <= f->max_groups;
 }
 
-static int run_alloc(gr_fib6_t *f, uint32_t *w) {
-	if (f->run_free.n) {
-		*w = f->run_free.v[--f->run_free.n];
-	} else if (f->slot_hw + GR_FIB6_GROUP <= f->max_groups) {
+// A run of 2^c consecutive slots (c = 1..8), every slot marked written.
+static int run_alloc(gr_fib6_t *f, unsigned c, uint32_t *w) {
+	const uint32_t len = 1u << c;
+	if (run_pop(f, c, w) == 0) {
+		// from a free run
+	} else if (f->slot_hw + len <= f->max_groups) {
 		*w = f->slot_hw;
-		f->slot_hw += GR_FIB6_GROUP;
+		f->slot_hw += len;
 	} else {
 		return -ENOSPC;
 	}
-	f->slots_live += GR_FIB6_GROUP;
-	for (uint32_t k = 0; k < GR_FIB6_GROUP; k++) {
+	f->slots_live += len;
+	for (uint32_t k = 0; k < len; k++) {
 		int r = mark_slot(f, *w + k);
 		if (r < 0)
 			return r;
@@ -578,10 +613,11 @@ static int run_alloc(gr_fib6_t *f, uint32_t *w) {
 	return 0;
 }
 
-static void run_free(gr_fib6_t *f, uint32_t w) {
-	memset(f->groups + (size_t)w * GR_FIB6_GROUP, 0, (size_t)GR_FIB6_GROUP * GR_FIB6_GROUP * sizeof(uint32_t));
-	f->slots_live -= GR_FIB6_GROUP;
-	(void)vpush(&f->run_free, w);
+static void run_free(gr_fib6_t *f, uint32_t w, unsigned c) {
+	const uint32_t len = 1u << c;
+	memset(f->groups + (size_t)w * GR_FIB6_GROUP, 0, (size_t)len * GR_FIB6_GROUP * sizeof(uint32_t));
+	f->slots_live -= len;
+	(void)vpush(&f->run_free[c], w);
 }
 
 static int skip_alloc(gr_fib6_t *f, uint32_t *k) {
@@ -608,7 +644,7 @@ static void release(gr_fib6_t *f, struct node *x) {
 		slot_free(f, x->obj_idx);
 		break;
 	case OBJ_RUN:
-		run_free(f, x->obj_idx);
+		run_free(f, x->obj_idx, x->run_c);
 		break;
 	case OBJ_SKIP:
 		skip_free(f, x->obj_idx);
@@ -655,6 +691,44 @@ static void compress_node(gr_fib6_t *f, struct node *x) {
 	x->n_grp_ch = (uint16_t)n_grp;
 	x->n_skip_ch = (uint16_t)n_skip;
 	x->merged = NO_NODE;
+	// granularity: the entries (as the image holds them: leaves, or a child
+	// each) change only at multiples of 2^gran
+	unsigned gran = 8;
+	for (int i = 1; i < GR_FIB6_GROUP && gran; i++)
+		if (x->ent[i] != x->ent[i - 1] || (x->ent[i] & REF)) {
+			const unsigned tz = (unsigned)__builtin_ctz((unsigned)i);
+			if (tz < gran)
+				gran = tz;
+		}
+	if (x->ent[0] & REF)
+		gran = 0;
+	x->gran = (uint8_t)gran;
+	// range shape: leaves that fit a range group's entry, V0 .. V1 .. V0
+	// (at most two changes, the outer values equal), or V0 .. V1
+	x->rs_ok = 0;
+	{
+		int nch = 0, ch[2] = {0, 0};
+		bool ok = true;
+		for (int i = 0; i < GR_FIB6_GROUP && ok; i++) {
+			const uint32_t e = x->ent[i];
+			ok = !(e & REF) && e <= GR_FIB6_RANGE_LEAF;
+			if (ok && i && e != x->ent[i - 1]) {
+				if (nch == 2)
+					ok = false;
+				else
+					ch[nch++] = i;
+			}
+		}
+		if (ok && nch == 2 && x->ent[0] != x->ent[GR_FIB6_GROUP - 1])
+			ok = false;
+		if (ok) {
+			x->rs_ok = 1;
+			x->rs_miss = x->ent[0];
+			x->rs_in = nch ? x->ent[ch[0]] : x->ent[0];
+			x->rs_lo = (uint8_t)(nch ? ch[0] : 0);
+			x->rs_hi = (uint8_t)(nch == 2 ? ch[1] - 1 : 255);
+		}
+	}
 	if ((d & REF) || n_exc > 1) {
 		x->ckind = CK_GROUP;
 		x->cgroups = groups + 1 > CGROUPS_MAX ? CGROUPS_MAX : groups + 1;
@@ -727,52 +801,98 @@ static int entry_enc(gr_fib6_t *f, uint32_t e, uint32_t *enc) {
 	return standalone(f, e & ~REF, enc);
 }
 
-// Node n's entries as they stand at its position (a group slot's content,
-// or a row of its parent's wide group) into slot s.
-static int rows_of(gr_fib6_t *f, uint32_t n, uint32_t s) {
-	for (int i = 0; i < GR_FIB6_GROUP; i++) {
+static inline int put_at(gr_fib6_t *f, uint32_t e, uint32_t v) {
+	return put(f, e / GR_FIB6_GROUP, (int)(e % GR_FIB6_GROUP), v);
+}
+
+// Node n's entries as they stand at its position, one per 2^sh (sh <= its
+// granularity), from entry e of the groups array on (a group slot's content
+// with sh 0, or a row of its parent's wide group).
+static int rows_of(gr_fib6_t *f, uint32_t n, uint32_t e, unsigned sh) {
+	for (uint32_t j = 0; j < (GR_FIB6_GROUP >> sh); j++) {
 		uint32_t v;
-		int r = entry_enc(f, f->nodes[n].ent[i], &v);
+		int r = entry_enc(f, f->nodes[n].ent[j << sh], &v);
 		if (r < 0)
 			return r;
-		if ((r = put(f, s, i, v)) < 0)
+		if ((r = put_at(f, e + j, v)) < 0)
 			return r;
 	}
 	return 0;
 }
 
-static int fill_row(gr_fib6_t *f, uint32_t s, uint32_t leaf) {
-	for (int i = 0; i < GR_FIB6_GROUP; i++) {
-		int r = put(f, s, i, leaf);
+static int fill_row(gr_fib6_t *f, uint32_t e, unsigned sh, uint32_t leaf) {
+	for (uint32_t j = 0; j < (GR_FIB6_GROUP >> sh); j++) {
+		int r = put_at(f, e + j, leaf);
 		if (r < 0)
 			return r;
 	}
 	return 0;
 }
 
-// Child node c becomes row s of a wide group.
-static int as_row(gr_fib6_t *f, uint32_t c, uint32_t s) {
+// Child node c becomes the row at entry e of a wide group of shift sh.
+static int as_row(gr_fib6_t *f, uint32_t c, uint32_t e, unsigned sh) {
 	struct node *x = &f->nodes[c];
-	if (!x->dirty && x->role == R_ROWS && x->row_at == s && !f->slot_dirty[s])
+	if (!x->dirty && x->role == R_ROWS && x->row_at == e && x->row_s == sh && !f->slot_dirty[e / GR_FIB6_GROUP])
 		return 0; // unchanged (a slot written since the last upload may be a new run)
 	release(f, x);
 	x->role = R_ROWS;
-	x->row_at = s;
-	return rows_of(f, c, s);
+	x->row_at = e;
+	x->row_s = (uint8_t)sh;
+	return rows_of(f, c, e, sh);
 }
 
-static int own(gr_fib6_t *f, struct node *x, int obj, uint32_t *idx) {
-	if (x->obj == obj) {
+// Node x owns a slot, a skip node or a run of 2^c slots (OBJ_RUN).
+static int own(gr_fib6_t *f, struct node *x, int obj, unsigned c, uint32_t *idx) {
+	if (x->obj == obj && (obj != OBJ_RUN || x->run_c == c)) {
 		*idx = x->obj_idx;
 		return 0;
 	}
 	release(f, x);
-	int r = obj == OBJ_SLOT ? slot_alloc(f, idx) : obj == OBJ_RUN ? run_alloc(f, idx) : skip_alloc(f, idx);
+	int r = obj == OBJ_SLOT ? slot_alloc(f, idx) : obj == OBJ_RUN ? run_alloc(f, c, idx) : skip_alloc(f, idx);
 	if (r < 0)
 		return r;
 	x->obj = (uint8_t)obj;
 	x->obj_idx = *idx;
+	x->run_c = (uint8_t)(obj == OBJ_RUN ? c : 0);
 	return 0;
+}
+
+// A wide entry: run w of shift sh.
+static inline uint32_t wide_enc(uint32_t w, unsigned sh) {
+	return GR_FIB6_EXT | GR_FIB6_WIDE | ((uint32_t)sh << GR_FIB6_WIDE_SHIFT) | w;
+}
+
+// The shift of node x as a wide group: the coarsest granularity all its child
+// groups share (its leaf rows are constant, any shift suits them).
+static unsigned wide_shift(const gr_fib6_t *f, const struct node *x) {
+	unsigned sh = 8;
+	for (int k = 0; k < GR_FIB6_GROUP && sh; k++) {
+		const uint32_t e = x->ent[k];
+		if ((e & REF) && f->nodes[e & ~REF].ckind == CK_GROUP && f->nodes[e & ~REF].gran < sh)
+			sh = f->nodes[e & ~REF].gran;
+	}
+	return sh == 8 ? 0 : sh; // (no child group: not a wide candidate)
+}
+
+// Node x as a range group: a group of leaves and children of range shape,
+// one of them at least (fib6.h).
+static bool range_ok(const gr_fib6_t *f, const struct node *x) {
+	if (x->ckind != CK_GROUP || x->pos > 14)
+		return false;
+	int kids = 0;
+	for (int k = 0; k < GR_FIB6_GROUP; k++) {
+		const uint32_t e = x->ent[k];
+		if (!(e & REF)) {
+			if (e > GR_FIB6_RANGE_LEAF)
+				return false;
+			continue;
+		}
+		const struct node *c = &f->nodes[e & ~REF];
+		if (c->ckind == CK_LEAF ? c->cval > GR_FIB6_RANGE_LEAF : !c->rs_ok)
+			return false;
+		kids += c->ckind != CK_LEAF;
+	}
+	return kids > 0;
 }
 
 // The entry that stands for node n at its position, its image written.
@@ -791,20 +911,23 @@ static int standalone(gr_fib6_t *f, uint32_t n, uint32_t *enc) {
 	} else if (x->ckind == CK_SKIP) {
 		const bool heavy = (x->chain & REF) && f->nodes[x->chain & ~REF].ckind == CK_GROUP
 			&& f->nodes[x->chain & ~REF].cgroups >= GR_FIB6_SKIP_WIDE_MIN;
-		if (x->sk_n == 1 && b <= 14 && heavy && (x->obj == OBJ_RUN || run_available(f))) {
+		const unsigned sh = heavy ? f->nodes[x->chain & ~REF].gran : 0, rc = 8 - sh;
+		if (x->sk_n == 1 && b <= 14 && heavy
+		    && ((x->obj == OBJ_RUN && x->run_c == rc) || run_available(f, rc))) {
 			// a one-byte skip over a heavy subtree: one wide group, row key =
 			// the child's entries, every other row the miss leaf
-			if ((r = own(f, x, OBJ_RUN, &idx)) < 0)
+			if ((r = own(f, x, OBJ_RUN, rc, &idx)) < 0)
 				return r;
 			x = &f->nodes[n];
 			const uint32_t key = x->sk_key[0], miss = x->cval, c = x->chain & ~REF;
+			const uint32_t e0 = idx * GR_FIB6_GROUP, rl = GR_FIB6_GROUP >> sh;
 			for (uint32_t k = 0; k < GR_FIB6_GROUP && r == 0; k++)
-				r = k == key ? as_row(f, c, idx + k) : fill_row(f, idx + k, miss);
+				r = k == key ? as_row(f, c, e0 + k * rl, sh) : fill_row(f, e0 + k * rl, sh, miss);
 			if (r < 0)
 				return r;
-			v = GR_FIB6_EXT | GR_FIB6_WIDE | idx;
+			v = wide_enc(idx, sh);
 		} else {
-			if ((r = own(f, x, OBJ_SKIP, &idx)) < 0)
+			if ((r = own(f, x, OBJ_SKIP, 0, &idx)) < 0)
 				return r;
 			uint32_t child;
 			if ((r = entry_enc(f, f->nodes[n].chain, &child)) < 0)
@@ -830,24 +953,57 @@ static int standalone(gr_fib6_t *f, uint32_t n, uint32_t *enc) {
 				m = y->ckind == CK_SKIP ? y->merged : NO_NODE;
 			}
 		}
-	} else if (b <= 14 && x->n_skip_ch == 0 && x->n_grp_ch >= GR_FIB6_WIDE_MIN && (x->obj == OBJ_RUN || run_available(f))) {
-		// wide: entry (k, y) = entry y of child k, or the leaf at k repeated
-		if ((r = own(f, x, OBJ_RUN, &idx)) < 0)
+	} else if (range_ok(f, x) && ((x->obj == OBJ_RUN && x->run_c == 1) || run_available(f, 1))) {
+		// range group: each entry folds a leaf, or a child's run and miss
+		if ((r = own(f, x, OBJ_RUN, 1, &idx)) < 0)
 			return r;
+		const uint32_t e0 = idx * GR_FIB6_GROUP;
 		for (uint32_t k = 0; k < GR_FIB6_GROUP && r == 0; k++) {
 			const uint32_t e = f->nodes[n].ent[k];
-			if ((e & REF) && f->nodes[e & ~REF].ckind == CK_GROUP)
-				r = as_row(f, e & ~REF, idx + k);
-			else
-				r = fill_row(f, idx + k, (e & REF) ? f->nodes[e & ~REF].cval : e);
+			uint32_t in = e, miss = e, lo = 0, hi = 255;
+			if (e & REF) {
+				struct node *c = &f->nodes[e & ~REF];
+				if (c->ckind == CK_LEAF) {
+					in = miss = c->cval;
+				} else {
+					in = c->rs_in;
+					miss = c->rs_miss;
+					lo = c->rs_lo;
+					hi = c->rs_hi;
+				}
+				release(f, c); // held in this entry, it owns nothing
+				c->role = R_RANGE;
+			}
+			r = put_at(f, e0 + 2 * k, in | lo << 24);
+			if (r == 0)
+				r = put_at(f, e0 + 2 * k + 1, miss | hi << 24);
 		}
 		if (r < 0)
 			return r;
-		v = GR_FIB6_EXT | GR_FIB6_WIDE | idx;
-	} else {
-		if ((r = own(f, x, OBJ_SLOT, &idx)) < 0)
+		x = &f->nodes[n];
+		v = GR_FIB6_EXT | GR_FIB6_RANGE | idx;
+	} else if (b <= 14 && x->n_skip_ch == 0 && x->n_grp_ch >= GR_FIB6_WIDE_MIN
+		   && ((x->obj == OBJ_RUN && x->run_c == 8 - wide_shift(f, x)) || run_available(f, 8 - wide_shift(f, x)))) {
+		// wide: entry (k, y) = entry y of child k, or the leaf at k repeated;
+		// one per 2^sh of y when every child group allows it
+		const unsigned sh = wide_shift(f, x), rc = 8 - sh;
+		if ((r = own(f, x, OBJ_RUN, rc, &idx)) < 0)
 			return r;
-		if ((r = rows_of(f, n, idx)) < 0)
+		const uint32_t e0 = idx * GR_FIB6_GROUP, rl = GR_FIB6_GROUP >> sh;
+		for (uint32_t k = 0; k < GR_FIB6_GROUP && r == 0; k++) {
+			const uint32_t e = f->nodes[n].ent[k];
+			if ((e & REF) && f->nodes[e & ~REF].ckind == CK_GROUP)
+				r = as_row(f, e & ~REF, e0 + k * rl, sh);
+			else
+				r = fill_row(f, e0 + k * rl, sh, (e & REF) ? f->nodes[e & ~REF].cval : e);
+		}
+		if (r < 0)
+			return r;
+		v = wide_enc(idx, sh);
+	} else {
+		if ((r = own(f, x, OBJ_SLOT, 0, &idx)) < 0)
+			return r;
+		if ((r = rows_of(f, n, idx * GR_FIB6_GROUP, 0)) < 0)
 			return r;
 		v = GR_FIB6_EXT | idx;
 	}
@@ -901,13 +1057,20 @@ uint32_t gr_fib6_lookup(const gr_fib6_t *f, const uint8_t ip[16]) {
 	uint32_t ent = f->top[((uint32_t)ip[0] << 8) | ip[1]];
 	int b = 2;
 	while (b < 16 && (ent & GR_FIB6_EXT)) {
-		if (ent & GR_FIB6_SKIP) {
+		if ((ent & GR_FIB6_RANGE) == GR_FIB6_RANGE) {
+			const uint32_t *q = f->groups + (size_t)(ent & GR_FIB6_IDX) * GR_FIB6_GROUP + 2 * ip[b];
+			const uint32_t y = ip[b + 1];
+			ent = y >= (q[0] >> 24) && y <= (q[1] >> 24) ? q[0] & GR_FIB6_RANGE_LEAF : q[1] & GR_FIB6_RANGE_LEAF;
+			b += 2;
+		} else if (ent & GR_FIB6_SKIP) {
 			const struct gr_fib6_skip *k = &f->skips[ent & GR_FIB6_IDX];
 			const bool match = b + k->n <= 16 && memcmp(ip + b, k->key, k->n) == 0;
 			ent = match ? k->child : k->miss;
 			b += k->n;
 		} else if (ent & GR_FIB6_WIDE) {
-			ent = f->groups[(size_t)(ent & GR_FIB6_IDX) * GR_FIB6_GROUP + ((uint32_t)ip[b] << 8) + ip[b + 1]];
+			const unsigned sh = (ent >> GR_FIB6_WIDE_SHIFT) & 7;
+			ent = f->groups[(size_t)(ent & GR_FIB6_WIDE_IDX) * GR_FIB6_GROUP + ((uint32_t)ip[b] << (8 - sh))
+					+ (ip[b + 1] >> sh)];
 			b += 2;
 		} else {
 			ent = f->groups[(size_t)(ent & GR_FIB6_IDX) * GR_FIB6_GROUP + ip[b++]];

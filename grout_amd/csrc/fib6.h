@@ -13,11 +13,23 @@
 // a group whose entries are mostly child groups (and no skip), or a one-byte
 // skip over a heavy subtree with its child group, becomes one wide group of
 // 65536 entries indexed by two bytes, 256 consecutive group slots, one
-// dependent gather instead of two on its paths. Entry encoding
+// dependent gather instead of two on its paths; when its children's entries
+// only change at multiples of 2^s in byte b + 1 (their prefixes end in the
+// top 8 - s bits of that byte), its rows keep one entry per 2^s: 2^(8-s)
+// slots in all, entry (x, y) at x * 2^(8-s) + (y >> s). Entry encoding
 // (u32): bit 31 clear = the nexthop slot of the longest matching prefix (0 =
 // no route, the FIB default_nh, modules/ip6/control/route.c:68); bits 31 and 30 = skip node
-// index in bits 0-28; bits 31 and 29 = wide group (its first slot in bits
-// 0-28); bit 31 alone = group index in bits 0-28.
+// index in bits 0-28; bits 31 and 29 = wide group, its first slot in bits
+// 0-25 and s in bits 26-28; bits 31, 30 and 29 = range group (below), its
+// first slot in bits 0-28; bit 31 alone = group index in bits 0-28.
+//
+// Range group: a node at byte b whose children each hold one run of a leaf
+// in byte b + 1 and another leaf around it (a prefix that ends inside byte
+// b + 1, as fib_inject's /42, /44 and /46 do under their /40s), folded
+// into 256 8-byte entries over two slots: entry x = {in | lo << 24, miss |
+// hi << 24}, the leaf is in when lo <= byte b + 1 <= hi, else miss (a
+// leaf entry of the node: in = miss). One gather ends the walk, and a
+// route's entry shares its line with 15 neighbours instead of owning one.
 #pragma once
 
 #include <stdint.h>
@@ -30,6 +42,10 @@ extern "C" {
 #define GR_FIB6_SKIP 0x40000000u
 #define GR_FIB6_WIDE 0x20000000u
 #define GR_FIB6_IDX 0x1fffffffu
+#define GR_FIB6_WIDE_SHIFT 26 // bits 26-28 of a wide entry: s
+#define GR_FIB6_WIDE_IDX 0x03ffffffu // its first slot
+#define GR_FIB6_RANGE (GR_FIB6_SKIP | GR_FIB6_WIDE) // both bits: a range group
+#define GR_FIB6_RANGE_LEAF 0x00ffffffu // the leaves a range group can hold
 #define GR_FIB6_WIDE_MIN 64 // child groups (of 256 entries) that make a group wide
 #define GR_FIB6_SKIP_WIDE_MIN 16 // groups under a one-byte skip's child that make the pair wide
 

@@ -387,7 +387,12 @@ __device__ __forceinline__ uint32_t chain_fib6(const kctx &P, const fwd4_rx6 &v,
 	uint32_t ent = gld(v.top + ((byte_of(key, 0) << 8) | byte_of(key, 1)));
 	int b = 2;
 	while (b < 16 && (ent & 0x80000000u)) {
-		if (ent & GR_FIB6_SKIP) { // skip node: key bytes 0-6, n in byte 7
+		if ((ent & GR_FIB6_RANGE) == GR_FIB6_RANGE) { // range group: {in | lo << 24, miss | hi << 24} by byte b
+			const u2v q = *(const GR_GLOBAL u2v *)(v.groups + (size_t)(ent & GR_FIB6_IDX) * 256 + 2 * byte_of(key, b));
+			const uint32_t y = byte_of(key, b + 1);
+			ent = (y >= (q.x >> 24) && y <= (q.y >> 24) ? q.x : q.y) & GR_FIB6_RANGE_LEAF;
+			b += 2;
+		} else if (ent & GR_FIB6_SKIP) { // skip node: key bytes 0-6, n in byte 7
 			const uint4 k = gld4(v.skips + (ent & GR_FIB6_IDX));
 			const int n = k.y >> 24;
 			bool match = b + n <= 16;
@@ -395,8 +400,10 @@ __device__ __forceinline__ uint32_t chain_fib6(const kctx &P, const fwd4_rx6 &v,
 				match = byte_of(key, b + i) == ((i < 4 ? k.x >> (8 * i) : k.y >> (8 * (i - 4))) & 0xff);
 			ent = match ? k.z : k.w;
 			b += n;
-		} else if (ent & GR_FIB6_WIDE) { // wide group: bytes b and b + 1 (b <= 14)
-			ent = gld(v.groups + (size_t)(ent & GR_FIB6_IDX) * 256 + (byte_of(key, b) << 8) + byte_of(key, b + 1));
+		} else if (ent & GR_FIB6_WIDE) { // wide group: byte b and the top 8 - s bits of b + 1 (b <= 14)
+			const uint32_t sh = (ent >> GR_FIB6_WIDE_SHIFT) & 7;
+			ent = gld(v.groups + (size_t)(ent & GR_FIB6_WIDE_IDX) * 256 + (byte_of(key, b) << (8 - sh))
+				  + (byte_of(key, b + 1) >> sh));
 			b += 2;
 		} else {
 			ent = gld(v.groups + (size_t)(ent & GR_FIB6_IDX) * 256 + byte_of(key, b));

@@ -432,14 +432,20 @@ def _walk_from(host, f, ip, ent, b):
     S = ctypes.cast(host.gr_fib6_skips(f), ctypes.POINTER(ctypes.c_uint8))
     EXT, SKIP, WIDE, IDX = 0x80000000, 0x40000000, 0x20000000, 0x1FFFFFFF
     while b < 16 and ent & EXT:
-        if ent & SKIP:
+        if ent & SKIP and ent & WIDE:  # range group (fib6.h)
+            q0, q1 = G[(ent & IDX) * 256 + 2 * int(ip[b])], G[(ent & IDX) * 256 + 2 * int(ip[b]) + 1]
+            y = int(ip[b + 1])
+            ent = (q0 if (q0 >> 24) <= y <= (q1 >> 24) else q1) & 0xFFFFFF
+            b += 2
+        elif ent & SKIP:
             k = bytes(S[(ent & IDX) * 16 + i] for i in range(16))
             n = k[7]
             match = b + n <= 16 and bytes(ip[b:b + n]) == k[:n]
             ent = int.from_bytes(k[8:12] if match else k[12:16], "little")
             b += n
         elif ent & WIDE:
-            ent = G[(ent & IDX) * 256 + (int(ip[b]) << 8) + int(ip[b + 1])]
+            sh = (ent >> 26) & 7
+            ent = G[(ent & 0x03FFFFFF) * 256 + (int(ip[b]) << (8 - sh)) + (int(ip[b + 1]) >> sh)]
             b += 2
         else:
             ent = G[(ent & IDX) * 256 + int(ip[b])]
@@ -486,10 +492,15 @@ def _referenced(top, grp, sk):
         e = np.concatenate([np.asarray(x, dtype=np.uint32).ravel() for x in todo])
         todo = []
         e = e[(e & 0x80000000) != 0]
-        sk_i = (e[(e & 0x40000000) != 0] & 0x1FFFFFFF).tolist()
-        wide = (e[((e & 0x40000000) == 0) & ((e & 0x20000000) != 0)] & 0x1FFFFFFF).tolist()
+        kind = e & 0x60000000
+        # range groups: two slots of packed leaves, nothing below them
+        slots.update(w + k for w in (e[kind == 0x60000000] & 0x1FFFFFFF).tolist() for k in (0, 1))
+        sk_i = (e[kind == 0x40000000] & 0x1FFFFFFF).tolist()
+        we = e[kind == 0x20000000]
+        wide = list(zip((we & 0x03FFFFFF).tolist(), ((we >> 26) & 7).tolist()))  # first slot, shift: 2^(8-s) slots
         plain = (e[(e & 0x60000000) == 0] & 0x1FFFFFFF).tolist()
-        new = [s for s in plain if s not in slots] + [w + k for w in wide for k in range(256) if w + k not in slots]
+        new = [s for s in plain if s not in slots] + [w + k for w, sh in wide for k in range(256 >> sh)
+                                                      if w + k not in slots]
         slots.update(new)
         if new:
             todo.append(grp[np.array(new, dtype=np.int64)])
