@@ -604,7 +604,9 @@ def test_fullview6_stream(fastpath):
     compare(o, g)
     assert (g[1]["edge"] == abi.EDGE["port_output"]).mean() > 0.99
     info = fastpath.fib6_info(1)
-    assert info["routes"] == len(t.route6_array()) and info["groups_used"] > 20_000  # a deep, path-compressed trie
+    # a deep trie, compacted: range groups and narrow wide groups (fib6.h) keep
+    # it under 10k group slots (before round 3: over 20k)
+    assert info["routes"] == len(t.route6_array()) and 0 < info["groups_used"] < 10_000, info
 
 
 @pytest.mark.parametrize("seed", [1, 2])
