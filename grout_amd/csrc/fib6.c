@@ -865,6 +865,9 @@ static inline uint32_t wide_enc(uint32_t w, unsigned sh) {
 // The shift of node x as a wide group: the coarsest granularity all its child
 // groups share (its leaf rows are constant, any shift suits them).
 static unsigned wide_shift(const gr_fib6_t *f, const struct node *x) {
+#ifdef FIB6_NO_NARROW // measurement builds (A/B)
+	return 0;
+#endif
 	unsigned sh = 8;
 	for (int k = 0; k < GR_FIB6_GROUP && sh; k++) {
 		const uint32_t e = x->ent[k];
@@ -877,6 +880,9 @@ static unsigned wide_shift(const gr_fib6_t *f, const struct node *x) {
 // Node x as a range group: a group of leaves and children of range shape,
 // one of them at least (fib6.h).
 static bool range_ok(const gr_fib6_t *f, const struct node *x) {
+#ifdef FIB6_NO_RANGE // measurement builds (A/B)
+	return false;
+#endif
 	if (x->ckind != CK_GROUP || x->pos > 14)
 		return false;
 	int kids = 0;
@@ -911,7 +917,11 @@ static int standalone(gr_fib6_t *f, uint32_t n, uint32_t *enc) {
 	} else if (x->ckind == CK_SKIP) {
 		const bool heavy = (x->chain & REF) && f->nodes[x->chain & ~REF].ckind == CK_GROUP
 			&& f->nodes[x->chain & ~REF].cgroups >= GR_FIB6_SKIP_WIDE_MIN;
+#ifdef FIB6_NO_NARROW
+		const unsigned sh = 0, rc = 8;
+#else
 		const unsigned sh = heavy ? f->nodes[x->chain & ~REF].gran : 0, rc = 8 - sh;
+#endif
 		if (x->sk_n == 1 && b <= 14 && heavy
 		    && ((x->obj == OBJ_RUN && x->run_c == rc) || run_available(f, rc))) {
 			// a one-byte skip over a heavy subtree: one wide group, row key =
