@@ -226,3 +226,53 @@ def test_commits_interleaved_across_vrfs(fastpath, fmt):
     finally:
         fastpath.tune("fib_format", 2)
         fresh_fastpath_state(fastpath, T.config_single_route())
+
+
+def test_queue_destroy_during_commits(fastpath):
+    """Queues created, used and destroyed on one thread while another commits
+    in a loop: each publication records every queue's retire event and makes
+    the control stream wait on it, so a queue must leave the context's list
+    (under the exclusive lock, its streams drained) before its events and
+    stream are destroyed (gr_hip_queue_destroy). Every forward stays whole on
+    one FIB state or the other, and nothing errors."""
+    t, nh = SC.corpus_topology()
+    fr, me, _ = SC.corpus_arrays()
+    fresh_fastpath_state(fastpath, T.config_single_route())
+    run_gpu(fastpath, t, fr, me)
+    oa = oracle.Oracle(t, build_dir24=False)
+    lines = np.ascontiguousarray(fr[:, :abi.LINE])  # the host path takes header lines
+    va = oa.process(lines, me, lines_only=True)[1].view("<u8")
+    ob = oracle.Oracle(t, build_dir24=False)
+    for op in TOGGLE_B:
+        r = _route(op[1], nh[op[2]])
+        assert ob.L.or_route_add(ob.h, r.ctypes.data, 1, 1 if op[0] == "rep" else 0) == 0
+    ob.L.or_fib_build(ob.h, 1)
+    vb = ob.process(lines, me, lines_only=True)[1].view("<u8")
+    stop = threading.Event()
+    err, seen = [], []
+
+    def churn():
+        dummy = oracle.Oracle(t, build_dir24=False)
+        state = "A"
+        try:
+            while not stop.is_set():
+                _apply(fastpath, dummy, TOGGLE_B if state == "A" else TOGGLE_A, nh)
+                fastpath.fib_commit(1)
+                state = "B" if state == "A" else "A"
+        except Exception as e:  # pragma: no cover - reported below
+            err.append(e)
+
+    th = threading.Thread(target=churn)
+    th.start()
+    try:
+        for _ in range(60):
+            q = fastpath.queue()  # created, used once, destroyed, while commits run
+            out, v = q.forward_host(lines, np.ascontiguousarray(me))
+            q.close()
+            got = v.view("<u8")
+            seen.append("A" if (got == va).all() else "B" if (got == vb).all() else "mixed")
+    finally:
+        stop.set()
+        th.join()
+    assert not err, err
+    assert "mixed" not in seen, seen

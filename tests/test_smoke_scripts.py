@@ -41,6 +41,7 @@ Scripts (under smoke/ in the reference):
   ip_add_del_test.sh        an IPv4 address deleted and added again
   ip6_add_del_test.sh       an IPv6 address deleted and added again; the port moved to a
                             VRF, then cross-connected
+  srv6_end_x_test.sh        an SRv6 End.X SID (sr6_local) beside plain IPv6 forwarding
 
 For the address and ageing scripts, "resolved" names the script's later
 state (the address added again, the neighbours answering again), as each
@@ -808,11 +809,43 @@ def ip6_add_del_moves(resolved):
     return t, pr
 
 
+def srv6_end_x(resolved):
+    """smoke/srv6_end_x_test.sh: p0, p0-bis, p1 (:40-42) on 2001:db8:61::/64,
+    :62::/64 and :101::/64 (:44-46); an SRv6 local End.X nexthop (id 200,
+    :82) and 5f00:102::100/128 via it (:84). n1 reaches n0 by SRv6-encapsulated
+    packets to that SID (:90-91): ip6_input leaves them by the nexthop type's
+    edge, sr6_local (whose End.X then sends the inner packet on p0-bis, on
+    the CPU), whatever their hop limit (ip6_forward does not run). n0's pings
+    to n1 (:123) are plain IPv6 forwarding from p0 to p1."""
+    s = "srv6_end_x_test.sh"
+    t = T.Topology()
+    t.add_vrf(T.VRF_MAIN)
+    ports(t, 3)
+    t.add_address6(PORT[0], "2001:db8:61::1/64")  # :44
+    t.add_address6(PORT[1], "2001:db8:62::1/64")  # :45
+    t.add_address6(PORT[2], "2001:db8:101::1/64")  # :46
+    endx = t.add_nexthop(PORT[1], nh_type="SR6_LOCAL", slot=200)  # :82
+    t.add_route6(T.VRF_MAIN, "5f00:102::100/128", endx)  # :84
+    if resolved:
+        neighbour(t, T.VRF_MAIN, PORT[0], "2001:db8:61::2", NS_MAC[0])
+        neighbour(t, T.VRF_MAIN, PORT[2], "2001:db8:101::2", NS_MAC[2])
+    pr = [
+        Probe(s, 123, 0, v6(0, "2001:db8:61::2", "2001:db8:101::2"), "ip6_hold", "port_output", (2, 0, NS_MAC[2])),
+        Probe(s, 90, 2, v6(2, "2001:db8:101::2", "5f00:102::100", nh=43), "sr6_local"),
+        Probe(s, 90, 2, v6(2, "2001:db8:101::2", "5f00:102::100", nh=43, hop=1), "sr6_local"),
+        # another SID of 5f00:102::/32, which grout has no route for
+        Probe(s, 92, 2, v6(2, "2001:db8:101::2", "5f00:102::101", nh=43), "ip6_error_dest_unreach"),
+        # n1's replies on the way back, plain IPv6 before its encap route exists
+        Probe(s, 123, 2, v6(2, "2001:db8:101::2", "2001:db8:61::2"), "ip6_hold", "port_output", (0, 0, NS_MAC[0])),
+    ]
+    return t, pr
+
+
 SCRIPTS = {f.__name__: f for f in (ip6_forward, vlan_forward, vrf_forward, cross_vrf_forward, ip_forward_ip6nh,
                                    ip_loadbalance, ip_fragment, ipip_encap, snat44, dnat44, bridge, ip6_same_peer,
                                    srv6, ip_builtin_icmp, ip6_builtin_icmp, iface_mac, nexthop_ageing,
                                    nexthop_ageing_stale, vxlan, bond_active_backup, ip_add_del, ip6_add_del,
-                                   ip6_add_del_moves)}
+                                   ip6_add_del_moves, srv6_end_x)}
 
 
 # ---------------------------------------------------------------------------
@@ -903,7 +936,7 @@ def test_smoke_script_gpu(fastpath, script, resolved):
     compare_mbufs(m, want, bufs, lines_o, [p.label for p in probes])
 
 
-TRAFFIC = ("ping", "traceroute", "socat", "tracepath", "route add", "mac add", "address add", "address del", "interface add",
+TRAFFIC = ("ping", "traceroute", "socat", "tracepath", "route add", "encap seg6", "mac add", "address add", "address del", "interface add",
            "interface set", "check_nexthop", "address show")
 
 
