@@ -394,6 +394,97 @@ def test_fib6_skip_widening(fanout, wide):
     host.gr_fib6_free(f)
 
 
+def _kinds(host, f):
+    """Entries of the image by kind (fib6.h): range groups, wide groups by
+    shift, skips and plain groups referenced from the first level and groups."""
+    import collections
+    top, grp, sk = _image(host, f)
+    slots, _ = _referenced(top, grp, sk)
+    # range groups' own slots hold packed leaves, not entries
+    rg = set()
+    for v in np.concatenate([top, sk[:, 2]] + ([grp[slots].ravel()] if len(slots) else [])):
+        if (int(v) & 0xE0000000) == 0xE0000000:
+            rg.update((int(v) & 0x1FFFFFFF) + k for k in (0, 1))
+    plain_slots = [x for x in slots.tolist() if x not in rg]
+    e = np.concatenate([top, sk[:, 2]] + ([grp[plain_slots].ravel()] if plain_slots else []))
+    e = e[(e & 0x80000000) != 0]
+    c = collections.Counter()
+    for v in e.tolist():
+        k = v & 0x60000000
+        c["range" if k == 0x60000000 else "skip" if k == 0x40000000 else
+          ("wide%d" % ((v >> 26) & 7)) if k == 0x20000000 else "group"] += 1
+    return c
+
+
+def _routes6(rows, plen):
+    r = np.zeros(len(rows), dtype=abi.ROUTE6_DT)
+    for i, b in enumerate(rows):
+        r["ip"][i, :len(b)] = b
+    r["prefixlen"] = plen
+    r["vrf_id"] = 1
+    r["nh"] = 1 + np.arange(len(rows)) % 2000
+    return r
+
+
+def test_fib6_range_groups():
+    """fib_inject's /44 shape (2300:0:vvvv:vv00::/44 under nothing shorter):
+    each byte-4 node's children hold one run of 16 entries in byte 5, so the
+    byte-4 nodes become range groups (8-byte entries, one gather for bytes 4
+    and 5). A /48 added under one /44 breaks its run: that byte-4 node falls
+    back to a plain or wide group, the others stay range groups; deleting it
+    brings the range group back. Lookups equal the RIB's throughout."""
+    host = abi.host()
+    rows = [(0x23, 0, 0, v >> 8, v & 0xFF) for v in range(1, 3000)]
+    r = _routes6(rows, 44)
+    f = _fib6_of(host, r)
+    k0 = _kinds(host, f)
+    assert k0["range"] >= 10, k0
+    rng = np.random.default_rng(70)
+    _fib6_check(host, f, r, rng, 8000)
+    extra = _routes6([(0x23, 0, 0, 5, 7, 0x08)], 48)  # inside 2300:0:5:700::/44's miss range: a new run
+    x = np.ascontiguousarray(extra[0]["ip"])
+    assert host.gr_fib6_add(f, x.ctypes.data, 48, 77, 0) == 0
+    assert host.gr_fib6_build(f) == 0
+    k1 = _kinds(host, f)
+    assert k1["range"] == k0["range"] - 1, (k0, k1)
+    allr = np.concatenate([r, extra])
+    _fib6_check(host, f, allr, rng, 8000)
+    assert host.gr_fib6_del(f, x.ctypes.data, 48) == 0
+    assert host.gr_fib6_build(f) == 0
+    assert _kinds(host, f)["range"] == k0["range"]
+    _fib6_check(host, f, r, rng, 8000)
+    host.gr_fib6_free(f)
+
+
+def test_fib6_narrow_wide_groups():
+    """fib_inject's /36 shape (2100:vvvv:v000::/36: 16 routes per byte-4 node,
+    16 entries each): every child of a byte-3 node changes only at multiples
+    of 16 in byte 4, so the byte-3 wide groups keep one entry per 16 (shift
+    4: 16 slots instead of 256). A /40 under one of them refines that child:
+    its wide group goes back to shift 0; deleting it restores shift 4.
+    Lookups equal the RIB's throughout."""
+    host = abi.host()
+    rows = [(0x21, 0, (v << 4) >> 16 & 0xFF, (v << 4) >> 8 & 0xFF, (v << 4) & 0xFF) for v in range(1, 20000)]
+    r = _routes6(rows, 36)
+    f = _fib6_of(host, r)
+    k0 = _kinds(host, f)
+    assert k0["wide4"] >= 1 and k0["wide0"] == 0, k0
+    rng = np.random.default_rng(71)
+    _fib6_check(host, f, r, rng, 8000)
+    extra = _routes6([(0x21, 0, 0, 0x12, 0x35)], 40)  # a /40 inside 2100:0:123x::/36
+    x = np.ascontiguousarray(extra[0]["ip"])
+    assert host.gr_fib6_add(f, x.ctypes.data, 40, 55, 0) == 0
+    assert host.gr_fib6_build(f) == 0
+    k1 = _kinds(host, f)
+    assert k1["wide0"] >= 1, k1
+    _fib6_check(host, f, np.concatenate([r, extra]), rng, 8000)
+    assert host.gr_fib6_del(f, x.ctypes.data, 40) == 0
+    assert host.gr_fib6_build(f) == 0
+    assert _kinds(host, f) == k0
+    _fib6_check(host, f, r, rng, 8000)
+    host.gr_fib6_free(f)
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_fib6_clustered_rebuilds(seed):
     """Random clusters shaped to trigger both level compressions
