@@ -439,14 +439,24 @@ static void deliver(struct rte_graph *graph, struct rte_node *node, struct gpu_w
 		for (uint32_t i = 0; i < n; i++)
 			rte_node_enqueue_x1(graph, node, GR_HIP_E_PUNT, mb[i]);
 	} else {
+		// runs of one edge go in one rte_node_enqueue (a forwarded stream is
+		// mostly one run to port_output)
+		uint32_t run = 0;
+		rte_edge_t re = 0;
 		for (uint32_t i = 0; i < n; i++) {
 			rte_edge_t e = v[i].edge;
 			if (e != GR_HIP_E_PUNT && hand_back(mb[i], &v[i]) < 0) {
 				w->stale++;
 				e = GR_HIP_E_IP_OUTPUT_ERROR; // a drop node (ip_output.c:187)
 			}
-			rte_node_enqueue_x1(graph, node, e, mb[i]);
+			if (i > run && e != re) { // (a batch is at most GPU_FWD4_BATCH_MAX < UINT16_MAX)
+				rte_node_enqueue(graph, node, re, (void **)&mb[run], (uint16_t)(i - run));
+				run = i;
+			}
+			re = e;
 		}
+		if (n > run)
+			rte_node_enqueue(graph, node, re, (void **)&mb[run], (uint16_t)(n - run));
 	}
 	reader_handed_back(w, k);
 	PROF_ADD(GPU_FWD4_PROF_DELIVER);
