@@ -736,6 +736,105 @@ int gh_rcu_delete_test(uint32_t slot, uint16_t iface_id, uint32_t hold_ms, struc
 	return 0;
 }
 
+// ---- a control plane churning while the worker forwards --------------------
+struct gh_churn_result {
+	uint32_t cycles; // delete / re-add cycles of nexthop a
+	uint32_t commits;
+	uint32_t freed_reads; // grout's nodes read a freed object
+	uint32_t recorded;
+	uint64_t stale; // dropped by the node: the object was gone at hand-back
+	uint32_t walks;
+	uint32_t err; // a control call failed
+};
+
+static struct {
+	struct gr_hip_route4 rt;
+	uint32_t a, b, gap_us;
+	volatile int stop;
+	uint32_t cycles, commits, err;
+} C;
+
+static int route_to(uint32_t slot) {
+	C.rt.nh = slot;
+	int r = gpu_fwd4_route4_add(&C.rt, 1, 1);
+	if (r == 0)
+		r = gpu_fwd4_fib4_commit(C.rt.vrf_id);
+	C.commits += r == 0;
+	return r;
+}
+
+// nexthop_destroy as grout orders it, over and over: the routes leave the
+// nexthop first (nexthop_routes_cleanup: here the route moves to b and is
+// published), then rte_rcu_qsbr_synchronize, then NEXTHOP_DELETE clears the
+// registry and the object is freed (dead); then it comes back (NEXTHOP_NEW)
+// and the route returns to it.
+static void *churn_control(void *arg) {
+	(void)arg;
+	while (!C.stop) {
+		if (route_to(C.b) < 0)
+			C.err++;
+		rte_rcu_qsbr_synchronize(gr_datapath_rcu(), RTE_QSBR_THRID_INVALID);
+		gpu_fwd4_nh_obj_set(C.a, NULL);
+		__atomic_store_n(&H.nh_dead[C.a], 1, __ATOMIC_RELEASE);
+		usleep(C.gap_us);
+		__atomic_store_n(&H.nh_dead[C.a], 0, __ATOMIC_RELEASE);
+		gpu_fwd4_nh_obj_set(C.a, &H.nhs[C.a]);
+		if (route_to(C.a) < 0)
+			C.err++;
+		C.cycles++;
+		usleep(C.gap_us);
+	}
+	return NULL;
+}
+
+// With the injected stream loaded (gh_load) and route (ip, prefixlen, vrf)
+// on nexthop a, walk the whole stream while a control thread cycles nexthop
+// a out and back (churn_control), gap_us between steps. The worker reports
+// quiescent every 256 walks as grout does, and also after every walk with
+// quiesce_each (a worker may: QSBR allows it, main_loop.c:462-463 expects
+// it once workers reclaim; the worst case for a reader held across walks).
+int gh_churn_test(uint32_t ip_be, uint8_t prefixlen, uint16_t vrf_id, uint32_t a, uint32_t b, uint32_t gap_us,
+		  uint32_t quiesce_each, struct gh_churn_result *res) {
+	if (H.cur < 0 || res == NULL || a == 0 || b == 0 || a > H.max_nh || b > H.max_nh)
+		return -EINVAL;
+	memset(res, 0, sizeof(*res));
+	memset(&C, 0, sizeof(C));
+	C.rt = (struct gr_hip_route4) {.ip = ip_be, .prefixlen = prefixlen, .vrf_id = vrf_id, .nh = a};
+	C.a = a;
+	C.b = b;
+	C.gap_us = gap_us;
+	H.freed_reads = 0;
+	struct gpu_fwd4_walk_info info0, info;
+	gpu_fwd4_walk_info(H.graphs[H.cur].graph, &info0);
+	pthread_t th;
+	if (pthread_create(&th, NULL, churn_control, NULL) != 0)
+		return -EAGAIN;
+	uint32_t w = 0;
+	const uint64_t t_end = mono_us() + 20000000u;
+	while (mono_us() < t_end) {
+		walk_once(H.cur);
+		w++;
+		if (quiesce_each)
+			rte_rcu_qsbr_quiescent(gr_datapath_rcu(), rte_lcore_id());
+		if (__atomic_load_n(&H.recorded, __ATOMIC_ACQUIRE) == H.n && H.next_rx == H.n)
+			break;
+	}
+	C.stop = 1;
+	pthread_join(th, NULL);
+	housekeeping(H.cur);
+	gpu_fwd4_walk_info(H.graphs[H.cur].graph, &info);
+	res->cycles = C.cycles;
+	res->commits = C.commits;
+	res->freed_reads = H.freed_reads;
+	res->recorded = H.recorded;
+	res->stale = info.stale - info0.stale;
+	res->walks = w;
+	res->err = C.err;
+	H.nh_dead[a] = 0;
+	gpu_fwd4_nh_obj_set(a, &H.nhs[a]);
+	return 0;
+}
+
 // The private area is a union of the nodes' views: a pointer field may hold
 // another view's bytes, so decode without dereferencing. 0 = NULL,
 // 0xffffffff = not one of the registered objects.

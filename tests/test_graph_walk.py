@@ -76,6 +76,7 @@ def lib():
         _lib.gh_iface_stats.argtypes = [U16, P]
         _lib.gh_walk_info.argtypes = [P]
         _lib.gh_rcu_delete_test.argtypes = [U32, U16, U32, P]
+        _lib.gh_churn_test.argtypes = [U32, ctypes.c_uint8, U16, U32, U32, U32, U32, P]
         _lib.gh_set_rx_burst.argtypes = [U32]
         _lib.gpu_fwd4_set_batch.argtypes = [U32, ctypes.c_uint64]
         _lib.gpu_fwd4_diverged.argtypes = [U32]
@@ -606,6 +607,66 @@ def test_graph_walk_rcu_delete_in_flight(readers):
     else:
         assert r["sync_before_handback"] == 1, r
         assert r["stale"] == BATCH, r  # dropped at hand-back: the objects were gone
+
+
+CHURN_DT = np.dtype([("cycles", "<u4"), ("commits", "<u4"), ("freed_reads", "<u4"), ("recorded", "<u4"),
+                     ("stale", "<u8"), ("walks", "<u4"), ("err", "<u4")])
+assert CHURN_DT.itemsize == 32
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("readers,quiesce_each", [(1, 0), (1, 1), (0, 1)],
+                         ids=["qsbr_readers", "qsbr_readers_quiesce_each_walk", "no_readers_quiesce_each_walk"])
+def test_graph_walk_control_plane_churn(readers, quiesce_each):
+    """A control thread cycles a nexthop out and back while the worker
+    forwards 2^20 packets through it, over and over, as grout's
+    nexthop_destroy orders it: its route moves to another nexthop and is
+    published, rte_rcu_qsbr_synchronize, NEXTHOP_DELETE (the registry entry
+    cleared), the object freed; then it is created again and the route comes
+    back. The worker reports quiescent every 256 walks (and, the worst case
+    for a reader held across walks, after every walk). With the node's QSBR
+    readers every packet reaches ip_hold with one of the two live nexthops,
+    none is dropped stale and nothing freed is read, across hundreds of
+    cycles and commits. Without them (the negative control) synchronize
+    returns while batches naming the nexthop are still on the GPU, and the
+    node drops those packets at hand-back instead (stale > 0)."""
+    L = lib()
+    fp = graph_ctx()
+    t = T.config_single_route()
+    a = t.add_nexthop(T.PORT_IFACE[1], "172.16.1.50")  # unresolved: ip_hold, the nexthop in l3_mbuf_data
+    b = t.add_nexthop(T.PORT_IFACE[1], "172.16.1.51")
+    r = t.route_array()
+    k = int(np.nonzero((r["prefixlen"] == 16) & (r["ip"] == T.ip4("16.1.0.0")))[0][0])
+    t.routes = [r[[i for i in range(len(r)) if i != k]]]
+    t.add_route(T.VRF_MAIN, "16.1.0.0/16", a)
+    load(fp, t)
+    n = 1 << 20
+    fr, me = S.stream(n, 0xC4C, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
+    res = np.zeros(1, dtype=CHURN_DT)
+    L.gpu_fwd4_rcu_readers(readers)
+    try:
+        assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, n) == 0
+        ip_be = int.from_bytes(T.ip4("16.1.0.0").to_bytes(4, "big"), "little")
+        assert L.gh_churn_test(ip_be, 16, T.VRF_MAIN, a, b, 200, quiesce_each, res.ctypes.data) == 0
+    finally:
+        L.gpu_fwd4_rcu_readers(1)
+    c = res[0]
+    assert c["err"] == 0 and c["recorded"] == n and c["cycles"] >= 20, c
+    assert c["freed_reads"] == 0, c  # the registries: nothing freed is ever handed to grout's nodes
+    out = np.zeros(n, dtype=OUT_DT)
+    lines = np.zeros((n, abi.LINE), dtype=np.uint8)
+    assert L.gh_results(out.ctypes.data, lines.ctypes.data) == n
+    dropped = out["edge"] == abi.EDGE["ip_output_error"]
+    assert dropped.sum() == c["stale"], c
+    held = out["edge"] == abi.EDGE["ip_hold"]
+    assert (held | dropped).all()
+    assert np.isin(out["nh"][held], [a, b]).all()
+    if readers:
+        assert c["stale"] == 0, c
+        assert (out["nh"] == a).any() and (out["nh"] == b).any()
+    else:
+        assert c["stale"] > 0, c
 
 
 @pytest.mark.gpu
