@@ -619,15 +619,15 @@ assert CHURN_DT.itemsize == 32
                          ids=["qsbr_readers", "qsbr_readers_quiesce_each_walk", "no_readers_quiesce_each_walk"])
 def test_graph_walk_control_plane_churn(readers, quiesce_each):
     """A control thread cycles a nexthop out and back while the worker
-    forwards 2^20 packets through it, over and over, as grout's
+    forwards 2^21 packets through it, over and over, as grout's
     nexthop_destroy orders it: its route moves to another nexthop and is
     published, rte_rcu_qsbr_synchronize, NEXTHOP_DELETE (the registry entry
     cleared), the object freed; then it is created again and the route comes
     back. The worker reports quiescent every 256 walks (and, the worst case
     for a reader held across walks, after every walk). With the node's QSBR
     readers every packet reaches ip_hold with one of the two live nexthops,
-    none is dropped stale and nothing freed is read, across hundreds of
-    cycles and commits. Without them (the negative control) synchronize
+    none is dropped stale and nothing freed is read, across tens of
+    cycles and their commits. Without them (the negative control) synchronize
     returns while batches naming the nexthop are still on the GPU, and the
     node drops those packets at hand-back instead (stale > 0)."""
     L = lib()
@@ -640,7 +640,7 @@ def test_graph_walk_control_plane_churn(readers, quiesce_each):
     t.routes = [r[[i for i in range(len(r)) if i != k]]]
     t.add_route(T.VRF_MAIN, "16.1.0.0/16", a)
     load(fp, t)
-    n = 1 << 20
+    n = 1 << 21
     fr, me = S.stream(n, 0xC4C, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
     fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
     res = np.zeros(1, dtype=CHURN_DT)
@@ -648,11 +648,11 @@ def test_graph_walk_control_plane_churn(readers, quiesce_each):
     try:
         assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, n) == 0
         ip_be = int.from_bytes(T.ip4("16.1.0.0").to_bytes(4, "big"), "little")
-        assert L.gh_churn_test(ip_be, 16, T.VRF_MAIN, a, b, 200, quiesce_each, res.ctypes.data) == 0
+        assert L.gh_churn_test(ip_be, 16, T.VRF_MAIN, a, b, 50, quiesce_each, res.ctypes.data) == 0
     finally:
         L.gpu_fwd4_rcu_readers(1)
     c = res[0]
-    assert c["err"] == 0 and c["recorded"] == n and c["cycles"] >= 20, c
+    assert c["err"] == 0 and c["recorded"] == n and c["cycles"] >= 10, c
     assert c["freed_reads"] == 0, c  # the registries: nothing freed is ever handed to grout's nodes
     out = np.zeros(n, dtype=OUT_DT)
     lines = np.zeros((n, abi.LINE), dtype=np.uint8)
