@@ -750,7 +750,7 @@ struct gh_churn_result {
 static struct {
 	struct gr_hip_route4 rt;
 	uint32_t a, b, gap_us;
-	volatile int stop;
+	volatile int stop, done;
 	uint32_t cycles, commits, err;
 } C;
 
@@ -784,6 +784,7 @@ static void *churn_control(void *arg) {
 		C.cycles++;
 		usleep(C.gap_us);
 	}
+	__atomic_store_n(&C.done, 1, __ATOMIC_RELEASE);
 	return NULL;
 }
 
@@ -811,15 +812,24 @@ int gh_churn_test(uint32_t ip_be, uint8_t prefixlen, uint16_t vrf_id, uint32_t a
 		return -EAGAIN;
 	uint32_t w = 0;
 	const uint64_t t_end = mono_us() + 20000000u;
-	while (mono_us() < t_end) {
+	// the worker walks until the stream is through and the control thread
+	// has stopped: a synchronize under way waits for the node's readers,
+	// which go offline only as the worker walks
+	while (mono_us() < t_end && !__atomic_load_n(&C.done, __ATOMIC_ACQUIRE)) {
 		walk_once(H.cur);
 		w++;
 		if (quiesce_each)
 			rte_rcu_qsbr_quiescent(gr_datapath_rcu(), rte_lcore_id());
 		if (__atomic_load_n(&H.recorded, __ATOMIC_ACQUIRE) == H.n && H.next_rx == H.n)
-			break;
+			C.stop = 1;
 	}
 	C.stop = 1;
+	if (!__atomic_load_n(&C.done, __ATOMIC_ACQUIRE)) { // the deadline: readers released, the thread can end
+		gpu_fwd4_rcu_readers(0);
+		for (uint32_t k = 0; k < 4; k++)
+			walk_once(H.cur);
+		C.err++;
+	}
 	pthread_join(th, NULL);
 	housekeeping(H.cur);
 	gpu_fwd4_walk_info(H.graphs[H.cur].graph, &info);
