@@ -7,7 +7,11 @@ own queue and 2^20 mbufs of the full-view stream (staged header lines, the
 node's default). Per round every thread resets its mbufs, a barrier, walks
 them all, a barrier; aggregate Mpps = K x mbufs / the median round.
 
-    python tools/node_pipeline.py [--threads 1,4,8] [--flush 4096,16384,65536] > out.jsonl
+    python tools/node_pipeline.py [--threads 1,4,8] [--flush 4096,16384,65536] [--thp] > out.jsonl
+
+--thp puts the data rooms and the gr_hip_mbuf views on transparent huge
+pages, as DPDK's mempools are on hugepages (4 KiB pages cost a TLB miss per
+mbuf).
 """
 import argparse
 import json
@@ -34,6 +38,16 @@ def walk(q, m, flush, depth):
     q.node_finish()
 
 
+def zeros(shape, dtype, thp):
+    if not thp:
+        return np.zeros(shape, dtype=dtype)
+    import mmap
+    nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+    mm = mmap.mmap(-1, nbytes, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+    mm.madvise(mmap.MADV_HUGEPAGE)
+    return np.frombuffer(mm, dtype=dtype).reshape(shape)  # zero-filled; the array keeps the map
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", default="1,4,8")
@@ -42,6 +56,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--driver", default="python", choices=["python", "c"],
                     help="c: the threads are C pthreads in tools/libnode_mt.so (no Python between the calls)")
+    ap.add_argument("--thp", action="store_true", help="mbufs and data rooms on transparent huge pages")
     args = ap.parse_args()
 
     from grout_amd import abi
@@ -57,16 +72,18 @@ def main():
     workers = []
     for w in range(max(threads)):
         fr, me = S.stream(n, S.SEED_GPU_BASE + w, routes=topo.route_array())
-        bufs = np.zeros((n, 256), dtype=np.uint8)  # mbuf data rooms (frame at offset 0)
+        bufs = zeros((n, 256), np.uint8, args.thp)  # mbuf data rooms (frame at offset 0)
         bufs[:, :64] = fr
-        mb = np.zeros(n, dtype=abi.MBUF_DT)
+        mb = zeros(n, abi.MBUF_DT, False)
         mb["frame"] = bufs.ctypes.data + np.arange(n, dtype=np.uint64) * 256
         mb["pkt_len"] = me["pkt_len"]
         mb["data_len"] = me["pkt_len"]
         mb["data_off"] = 128
         mb["rss"] = me["rss"]
         mb["iface"] = me["iface"]
-        wk = {"fr": fr, "bufs": bufs, "mb": mb, "m": mb.copy(), "q": fp.queue()}
+        m = zeros(n, abi.MBUF_DT, args.thp)
+        m[:] = mb
+        wk = {"fr": fr, "bufs": bufs, "mb": mb, "m": m, "q": fp.queue()}
         walk(wk["q"], wk["m"], 1 << 16, 2)  # warm-up: both staging slots grown
         workers.append(wk)
     check = None
@@ -90,7 +107,7 @@ def main():
                         abi.check("node_mt_round", C.node_mt_round(qs, ms, k, n, flush, depth, ctypes.byref(sec)))
                         times.append(sec.value)
                     d = float(np.median(times))
-                    print(json.dumps({"driver": "c", "flush_pkts": flush, "threads": k, "depth": depth,
+                    print(json.dumps({"driver": "c", "thp": args.thp, "flush_pkts": flush, "threads": k, "depth": depth,
                                       "mbufs_per_thread": n, "ms_per_round": round(d * 1e3, 2),
                                       "mpps_aggregate": round(k * n / d / 1e6, 1),
                                       "mpps_per_thread": round(n / d / 1e6, 1)}), flush=True)
@@ -132,7 +149,7 @@ def main():
                     check = got
                 same = bool(np.array_equal(got[0], check[0]) and np.array_equal(got[1], check[1]))
                 d = float(np.median(times))
-                print(json.dumps({"flush_pkts": flush, "threads": k, "depth": depth, "mbufs_per_thread": n,
+                print(json.dumps({"thp": args.thp, "flush_pkts": flush, "threads": k, "depth": depth, "mbufs_per_thread": n,
                                   "ms_per_round": round(d * 1e3, 2), "mpps_aggregate": round(k * n / d / 1e6, 1),
                                   "mpps_per_thread": round(n / d / 1e6, 1), "same_results": same}), flush=True)
     for wk in workers:
