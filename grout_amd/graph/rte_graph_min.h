@@ -76,6 +76,10 @@ _Static_assert(sizeof(struct rte_mbuf) == 128, "rte_mbuf is two cache lines");
 static inline void rte_prefetch0(const volatile void *p) {
 	__builtin_prefetch((const void *)p, 0, 3);
 }
+// rte_prefetch.h: into every cache level, for a write
+static inline void rte_prefetch0_write(const void *p) {
+	__builtin_prefetch(p, 1, 3);
+}
 // DPDK puts the mbuf back in m->pool; the stand-in's mbufs belong to the harness
 static inline void rte_pktmbuf_free(struct rte_mbuf *m) {
 	(void)m;
