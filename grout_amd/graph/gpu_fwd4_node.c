@@ -128,11 +128,13 @@ static uint32_t if_obj_n;
 static const struct nexthop **nh_obj;
 static uint32_t nh_obj_n;
 
+// Allocated at the first set, from the control thread; the size is published
+// after the table (release), and the workers read it first (acquire).
 static int obj_table(const void ***t, uint32_t *n, uint32_t want) {
 	if (*t == NULL) {
 		if ((*t = calloc(want, sizeof(void *))) == NULL)
 			return -ENOMEM;
-		*n = want;
+		__atomic_store_n(n, want, __ATOMIC_RELEASE);
 	}
 	return 0;
 }
@@ -158,11 +160,12 @@ int gpu_fwd4_nh_obj_set(uint32_t slot, const struct nexthop *nh) {
 }
 
 const struct iface *gpu_fwd4_iface_obj(uint16_t id) {
-	return id < if_obj_n ? __atomic_load_n(&if_obj[id], __ATOMIC_ACQUIRE) : NULL;
+	return id < __atomic_load_n(&if_obj_n, __ATOMIC_ACQUIRE) ? __atomic_load_n(&if_obj[id], __ATOMIC_ACQUIRE) : NULL;
 }
 
 const struct nexthop *gpu_fwd4_nh_obj(uint32_t slot) {
-	return slot < nh_obj_n ? __atomic_load_n(&nh_obj[slot], __ATOMIC_ACQUIRE) : NULL;
+	return slot < __atomic_load_n(&nh_obj_n, __ATOMIC_ACQUIRE) ? __atomic_load_n(&nh_obj[slot], __ATOMIC_ACQUIRE)
+								  : NULL;
 }
 
 gr_hip_ctx_t *gpu_fwd4_hip_ctx(void) {
@@ -710,8 +713,11 @@ static void gpu_fwd4_fini(const struct rte_graph *graph, struct rte_node *node) 
 		for (uint32_t j = 0; j < w->n; j++) // held, never sent
 			rte_pktmbuf_free(w->mbufs[w->cur][j]);
 		gr_hip_queue_destroy(w->q);
-		for (int k = 0; k < GPU_FWD4_RCU_PER_GRAPH; k++) // offline, then gone
+		for (int k = 0; k < GPU_FWD4_RCU_PER_GRAPH; k++) { // offline, then gone (rte_rcu_qsbr.h)
+			if (w->rstate[k] != RD_FREE)
+				rte_rcu_qsbr_thread_offline(gr_datapath_rcu(), reader_id(w, k));
 			rte_rcu_qsbr_thread_unregister(gr_datapath_rcu(), reader_id(w, k));
+		}
 		if ((uint32_t)w->gpu < n_gpus && gpus[w->gpu].graphs > 0)
 			gpus[w->gpu].graphs--;
 		walks[i] = NULL;
