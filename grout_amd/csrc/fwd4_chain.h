@@ -387,12 +387,8 @@ __device__ __forceinline__ uint32_t chain_fib6(const kctx &P, const fwd4_rx6 &v,
 	uint32_t ent = gld(v.top + ((byte_of(key, 0) << 8) | byte_of(key, 1)));
 	int b = 2;
 	while (b < 16 && (ent & 0x80000000u)) {
-		if ((ent & GR_FIB6_RANGE) == GR_FIB6_RANGE) { // range group: {in | lo << 24, miss | hi << 24} by byte b
-			const u2v q = *(const GR_GLOBAL u2v *)(v.groups + (size_t)(ent & GR_FIB6_IDX) * 256 + 2 * byte_of(key, b));
-			const uint32_t y = byte_of(key, b + 1);
-			ent = (y >= (q.x >> 24) && y <= (q.y >> 24) ? q.x : q.y) & GR_FIB6_RANGE_LEAF;
-			b += 2;
-		} else if (ent & GR_FIB6_SKIP) { // skip node: key bytes 0-6, n in byte 7
+		const uint32_t kind = ent & GR_FIB6_RANGE;
+		if (kind == GR_FIB6_SKIP) { // skip node: key bytes 0-6, n in byte 7
 			const uint4 k = gld4(v.skips + (ent & GR_FIB6_IDX));
 			const int n = k.y >> 24;
 			bool match = b + n <= 16;
@@ -400,15 +396,23 @@ __device__ __forceinline__ uint32_t chain_fib6(const kctx &P, const fwd4_rx6 &v,
 				match = byte_of(key, b + i) == ((i < 4 ? k.x >> (8 * i) : k.y >> (8 * (i - 4))) & 0xff);
 			ent = match ? k.z : k.w;
 			b += n;
-		} else if (ent & GR_FIB6_WIDE) { // wide group: byte b and the top 8 - s bits of b + 1 (b <= 14)
-			const uint32_t sh = (ent >> GR_FIB6_WIDE_SHIFT) & 7;
-			ent = gld(v.groups + (size_t)(ent & GR_FIB6_WIDE_IDX) * 256 + (byte_of(key, b) << (8 - sh))
-				  + (byte_of(key, b + 1) >> sh));
-			b += 2;
-		} else {
-			ent = gld(v.groups + (size_t)(ent & GR_FIB6_IDX) * 256 + byte_of(key, b));
-			b++;
+			continue;
 		}
+		// the three group kinds in one gather, so that a wave whose lanes sit
+		// in different kinds issues one load per level, not one per kind
+		// (each behind the one before); the 8 bytes at a 4-byte entry read
+		// the next entry too (the groups are followed by the skip nodes)
+		//   range group: entry {in | lo << 24, miss | hi << 24} by byte b
+		//   wide group: byte b and the top 8 - s bits of byte b + 1 (b <= 14)
+		//   plain group: byte b
+		const uint32_t x = byte_of(key, b), y = b < 15 ? byte_of(key, b + 1) : 0;
+		const uint32_t sh = (ent >> GR_FIB6_WIDE_SHIFT) & 7;
+		const size_t off = kind == GR_FIB6_RANGE ? (size_t)(ent & GR_FIB6_IDX) * 256 + 2 * x
+				   : kind == GR_FIB6_WIDE   ? (size_t)(ent & GR_FIB6_WIDE_IDX) * 256 + (x << (8 - sh)) + (y >> sh)
+							    : (size_t)(ent & GR_FIB6_IDX) * 256 + x;
+		const u2a q = *(const GR_GLOBAL u2a *)(v.groups + off);
+		ent = kind == GR_FIB6_RANGE ? (y >= (q.x >> 24) && y <= (q.y >> 24) ? q.x : q.y) & GR_FIB6_RANGE_LEAF : q.x;
+		b += kind == 0 ? 1 : 2;
 	}
 	return (ent & 0x80000000u) ? 0 : ent;
 }

@@ -22,6 +22,8 @@ __device__ __forceinline__ T gld(const T *p) {
 
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+// two dwords at a dword-aligned address (one global_load_dwordx2)
+typedef uint32_t u2a __attribute__((ext_vector_type(2), aligned(4)));
 
 __device__ __forceinline__ uint4 gld4(const void *p) {
 	const u4v v = *(const GR_GLOBAL u4v *)p;
