@@ -374,6 +374,32 @@ __device__ __forceinline__ uint32_t byte_of(const uint32_t (&a)[4], int i) {
 	return (a[i >> 2] >> (8 * (i & 3))) & 0xff;
 }
 
+// The FIB6 view of RX iface `id` (its VRF's trie): through the scalar cache
+// when the active lanes share the iface (a tile from one RX queue), as the
+// IPv4 RX view is, since the trie walk's first gather waits for it.
+__device__ __forceinline__ fwd4_rx6 load_rx6(const kctx &P, uint32_t id) {
+	const uint32_t id0 = __builtin_amdgcn_readfirstlane(id);
+	if (__ballot(id != id0) == 0) {
+		typedef uint32_t u4s __attribute__((ext_vector_type(4)));
+		typedef uint32_t u2s __attribute__((ext_vector_type(2)));
+		const uint64_t a = reinterpret_cast<uint64_t>(P.rx6 + id0);
+		const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)), lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+		const uint64_t p = ((uint64_t)hi << 32) | lo;
+		u4s x;
+		u2s y;
+		asm volatile("s_load_dwordx4 %0, %2, 0x0\n\ts_load_dwordx2 %1, %2, 0x10\n\ts_waitcnt lgkmcnt(0)"
+			     : "=&s"(x), "=&s"(y)
+			     : "s"(p)
+			     : "memory");
+		fwd4_rx6 v;
+		v.top = reinterpret_cast<const uint32_t *>(((uint64_t)x[1] << 32) | x[0]);
+		v.groups = reinterpret_cast<const uint32_t *>(((uint64_t)x[3] << 32) | x[2]);
+		v.skips = reinterpret_cast<const uint4 *>(((uint64_t)y[1] << 32) | y[0]);
+		return v;
+	}
+	return fwd4_rx6{gld(&P.rx6[id].top), gld(&P.rx6[id].groups), gld(&P.rx6[id].skips)};
+}
+
 // rte_fib6_lookup (modules/ip6/control/route.c:150-173) in the fib6.h trie of the iface's VRF:
 // key = dst with link-local addresses scoped to the ingress iface
 // (addr6_linklocal_scope, ip6.h:23-36).
@@ -463,8 +489,7 @@ __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, 
 		r.edge = mc ? GR_HIP_E_IP6_INPUT_LOCAL : GR_HIP_E_IP6_INPUT_OTHER_HOST;
 		return;
 	}
-	const fwd4_rx6 v = {gld(&P.rx6[rx.id].top), gld(&P.rx6[rx.id].groups), gld(&P.rx6[rx.id].skips)};
-	uint32_t slot = chain_fib6(P, v, dst, rx.id); // ip6_input.c:124-131
+	uint32_t slot = chain_fib6(P, load_rx6(P, rx.id), dst, rx.id); // ip6_input.c:124-131
 	if (slot == 0 || slot > P.max_nh) {
 		r.edge = GR_HIP_E_IP6_ERROR_DEST_UNREACH;
 		return;

@@ -745,12 +745,18 @@ struct gh_churn_result {
 	uint64_t stale; // dropped by the node: the object was gone at hand-back
 	uint32_t walks;
 	uint32_t err; // a control call failed
+	// where the race window was: walks that ended with a batch on the GPU
+	// between the move of the route (published) and the registry clear, and
+	// between the clear and the nexthop's return
+	uint32_t inflight_moved;
+	uint32_t inflight_cleared;
 };
 
 static struct {
 	struct gr_hip_route4 rt;
 	uint32_t a, b, gap_us;
 	volatile int stop, done;
+	int phase; // 1: route moved and published, 2: registry entry cleared, 0: otherwise
 	uint32_t cycles, commits, err;
 } C;
 
@@ -773,10 +779,13 @@ static void *churn_control(void *arg) {
 	while (!C.stop) {
 		if (route_to(C.b) < 0)
 			C.err++;
+		__atomic_store_n(&C.phase, 1, __ATOMIC_RELEASE);
 		rte_rcu_qsbr_synchronize(gr_datapath_rcu(), RTE_QSBR_THRID_INVALID);
 		gpu_fwd4_nh_obj_set(C.a, NULL);
 		__atomic_store_n(&H.nh_dead[C.a], 1, __ATOMIC_RELEASE);
+		__atomic_store_n(&C.phase, 2, __ATOMIC_RELEASE);
 		usleep(C.gap_us);
+		__atomic_store_n(&C.phase, 0, __ATOMIC_RELEASE);
 		__atomic_store_n(&H.nh_dead[C.a], 0, __ATOMIC_RELEASE);
 		gpu_fwd4_nh_obj_set(C.a, &H.nhs[C.a]);
 		if (route_to(C.a) < 0)
@@ -785,6 +794,37 @@ static void *churn_control(void *arg) {
 		usleep(C.gap_us);
 	}
 	__atomic_store_n(&C.done, 1, __ATOMIC_RELEASE);
+	return NULL;
+}
+
+// Another worker's load on the graph's GPU during gh_churn_test: batches of
+// gpu_load zeroed packets (each a whole-GPU kernel, as the ring kernel is
+// persistent: ~0.1 ms at 2^22) submitted back to back on a queue of their
+// own, so that the node's batches wait behind them and stay on the GPU
+// across a publication and the synchronize after it, the window an RCU
+// reader must cover. 0: none.
+static uint32_t gpu_load;
+
+void gh_set_gpu_load(uint32_t n) {
+	gpu_load = n;
+}
+
+static void *gpu_load_thread(void *arg) {
+	gr_hip_ctx_t *ctx = arg;
+	gr_hip_queue_t *q = NULL;
+	struct gr_hip_batch b;
+	if (gr_hip_queue_create(ctx, NULL, &q) < 0)
+		return NULL;
+	if (gr_hip_batch_alloc(ctx, gpu_load, GR_HIP_LINE, &b) == 0) {
+		while (!C.stop) {
+			if (gr_hip_fwd4_submit(q, &b) < 0 || gr_hip_fwd4_submit(q, &b) < 0)
+				break;
+			gr_hip_queue_sync(q);
+		}
+		gr_hip_queue_sync(q);
+		gr_hip_batch_free(ctx, &b);
+	}
+	gr_hip_queue_destroy(q);
 	return NULL;
 }
 
@@ -807,9 +847,16 @@ int gh_churn_test(uint32_t ip_be, uint8_t prefixlen, uint16_t vrf_id, uint32_t a
 	H.freed_reads = 0;
 	struct gpu_fwd4_walk_info info0, info;
 	gpu_fwd4_walk_info(H.graphs[H.cur].graph, &info0);
-	pthread_t th;
-	if (pthread_create(&th, NULL, churn_control, NULL) != 0)
+	pthread_t th, lt;
+	const int loaded = gpu_load != 0
+		&& pthread_create(&lt, NULL, gpu_load_thread, gpu_fwd4_ctx_at((uint32_t)gpu_fwd4_graph_gpu(H.graphs[H.cur].graph)))
+			== 0;
+	if (pthread_create(&th, NULL, churn_control, NULL) != 0) {
+		C.stop = 1;
+		if (loaded)
+			pthread_join(lt, NULL);
 		return -EAGAIN;
+	}
 	uint32_t w = 0;
 	const uint64_t t_end = mono_us() + 20000000u;
 	// the worker walks until the stream is through and the control thread
@@ -818,6 +865,12 @@ int gh_churn_test(uint32_t ip_be, uint8_t prefixlen, uint16_t vrf_id, uint32_t a
 	while (mono_us() < t_end && !__atomic_load_n(&C.done, __ATOMIC_ACQUIRE)) {
 		walk_once(H.cur);
 		w++;
+		const int ph = __atomic_load_n(&C.phase, __ATOMIC_ACQUIRE);
+		if (ph != 0) {
+			gpu_fwd4_walk_info(H.graphs[H.cur].graph, &info);
+			if (info.in_flight)
+				*(ph == 1 ? &res->inflight_moved : &res->inflight_cleared) += 1;
+		}
 		if (quiesce_each)
 			rte_rcu_qsbr_quiescent(gr_datapath_rcu(), rte_lcore_id());
 		if (__atomic_load_n(&H.recorded, __ATOMIC_ACQUIRE) == H.n && H.next_rx == H.n)
@@ -831,6 +884,8 @@ int gh_churn_test(uint32_t ip_be, uint8_t prefixlen, uint16_t vrf_id, uint32_t a
 		C.err++;
 	}
 	pthread_join(th, NULL);
+	if (loaded)
+		pthread_join(lt, NULL);
 	housekeeping(H.cur);
 	gpu_fwd4_walk_info(H.graphs[H.cur].graph, &info);
 	res->cycles = C.cycles;

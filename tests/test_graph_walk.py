@@ -79,6 +79,8 @@ def lib():
         _lib.gh_churn_test.argtypes = [U32, ctypes.c_uint8, U16, U32, U32, U32, U32, P]
         _lib.gh_set_rx_burst.argtypes = [U32]
         _lib.gpu_fwd4_set_batch.argtypes = [U32, ctypes.c_uint64]
+        _lib.gh_set_gpu_load.argtypes = [U32]
+        _lib.gh_set_gpu_load.restype = None
         _lib.gpu_fwd4_diverged.argtypes = [U32]
         _lib.gpu_fwd4_resync.argtypes = [U32]
         _lib.gpu_fwd4_rcu_readers.argtypes = [ctypes.c_int]
@@ -587,11 +589,16 @@ def test_graph_walk_rcu_delete_in_flight(readers):
     fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
     res = np.zeros(1, dtype=RCU_RES_DT)
     L.gpu_fwd4_rcu_readers(readers)
+    # the whole stream is one batch: only a full batch is sent (with DELAY_NS
+    # a slow first walk on a fresh process could flush part of it, 2112 of
+    # the 4096 packets, and the rest would start after the synchronize)
+    assert L.gpu_fwd4_set_batch(BATCH, 10_000_000_000) == 0
     try:
         assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, len(me)) == 0
         assert L.gh_rcu_delete_test(gw, oif, 30, res.ctypes.data) == 0
     finally:
         L.gpu_fwd4_rcu_readers(1)
+        assert L.gpu_fwd4_set_batch(BATCH, DELAY_NS) == 0
     r = res[0]
     assert r["sync_done"] == 1 and r["recorded"] == BATCH, r
     if readers:
@@ -609,9 +616,12 @@ def test_graph_walk_rcu_delete_in_flight(readers):
         assert r["stale"] == BATCH, r  # dropped at hand-back: the objects were gone
 
 
+CHURN_BATCH = 256
+CHURN_GPU_LOAD = 1 << 21
 CHURN_DT = np.dtype([("cycles", "<u4"), ("commits", "<u4"), ("freed_reads", "<u4"), ("recorded", "<u4"),
-                     ("stale", "<u8"), ("walks", "<u4"), ("err", "<u4")])
-assert CHURN_DT.itemsize == 32
+                     ("stale", "<u8"), ("walks", "<u4"), ("err", "<u4"), ("inflight_moved", "<u4"),
+                     ("inflight_cleared", "<u4")])
+assert CHURN_DT.itemsize == 40
 
 
 @pytest.mark.gpu
@@ -645,13 +655,24 @@ def test_graph_walk_control_plane_churn(readers, quiesce_each):
     fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
     res = np.zeros(1, dtype=CHURN_DT)
     L.gpu_fwd4_rcu_readers(readers)
+    # batches of 4 RX bursts, sent every few walks, and another queue's
+    # whole-GPU kernels back to back (another worker's load): the node's
+    # batches wait behind them, so one sent before a publication is still on
+    # the GPU when the synchronize after it starts. (With BATCH alone, one
+    # batch every 64 walks on an idle GPU, that window was hit a few times per
+    # run, in some runs never.)
+    assert L.gpu_fwd4_set_batch(CHURN_BATCH, DELAY_NS) == 0
+    L.gh_set_gpu_load(CHURN_GPU_LOAD)
     try:
         assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, n) == 0
         ip_be = int.from_bytes(T.ip4("16.1.0.0").to_bytes(4, "big"), "little")
         assert L.gh_churn_test(ip_be, 16, T.VRF_MAIN, a, b, 50, quiesce_each, res.ctypes.data) == 0
     finally:
         L.gpu_fwd4_rcu_readers(1)
+        L.gh_set_gpu_load(0)
+        assert L.gpu_fwd4_set_batch(BATCH, DELAY_NS) == 0
     c = res[0]
+    print("churn", readers, quiesce_each, c)
     assert c["err"] == 0 and c["recorded"] == n and c["cycles"] >= 10, c
     assert c["freed_reads"] == 0, c  # the registries: nothing freed is ever handed to grout's nodes
     out = np.zeros(n, dtype=OUT_DT)
