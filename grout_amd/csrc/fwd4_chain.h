@@ -38,6 +38,9 @@ __device__ __forceinline__ kctx make_kctx(const fwd4_params &A, const fwd4_edges
 	P.nhf6 = T->nhf6;
 	P.nhf6_lds = nullptr; // set by the kernel that stages them
 	P.nhf6_n = 0;
+	P.top6 = nullptr;
+	P.top6_lds = nullptr;
+	P.top6_n = 0;
 	return P;
 }
 
@@ -410,7 +413,11 @@ __device__ __forceinline__ uint32_t chain_fib6(const kctx &P, const fwd4_rx6 &v,
 	uint32_t key[4] = {dst[0], dst[1], dst[2], dst[3]};
 	if ((key[0] & 0xff) == 0xfe && (key[0] & 0xc000) == 0x8000)
 		key[0] = (key[0] & 0xffff) | ((iface_id >> 8) << 16) | ((iface_id & 0xff) << 24);
-	uint32_t ent = gld(v.top + ((byte_of(key, 0) << 8) | byte_of(key, 1)));
+	// the first level: from LDS where the launch staged it (2000::/4 of the
+	// only IPv6 VRF), else one gather
+	const uint32_t idx = (byte_of(key, 0) << 8) | byte_of(key, 1);
+	const uint32_t k6 = idx - FWD4_TOP6_BASE;
+	uint32_t ent = v.top == P.top6 && k6 < P.top6_n ? P.top6_lds[k6] : gld(v.top + idx);
 	int b = 2;
 	while (b < 16 && (ent & 0x80000000u)) {
 		const uint32_t kind = ent & GR_FIB6_RANGE;

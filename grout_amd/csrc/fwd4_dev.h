@@ -49,6 +49,9 @@ struct kctx {
 	const fwd4_nhf *nhf6;
 	const __attribute__((address_space(3))) u4v *nhf6_lds; // slots 1..nhf6_n staged in LDS
 	uint32_t nhf6_n;
+	const uint32_t *top6; // the trie whose first-level entries FWD4_TOP6_BASE.. are staged
+	const __attribute__((address_space(3))) uint32_t *top6_lds;
+	uint32_t top6_n;
 };
 
 struct rxv {

@@ -150,6 +150,11 @@ struct fwd4_params {
 	uint32_t readable; // frame bytes present per packet (64 or in_stride)
 	uint32_t nhf_lds; // fwd4_ring.hip: fast adjacencies 1..nhf_lds staged in LDS
 	uint32_t nhf6_lds; // and IPv6 fast adjacencies 1..nhf6_lds after them
+	// and the first-level FIB6 entries [FWD4_TOP6_BASE, FWD4_TOP6_BASE + top6_lds)
+	// of top6 (4 bytes each) after those: the trie of the only VRF with IPv6
+	// routes (NULL, 0: none staged)
+	const uint32_t *top6;
+	uint32_t top6_lds;
 	uint32_t chunk; // fwd4_ring.hip: 0 = workgroup b takes tiles b, b + G, ...;
 	                // else the contiguous tiles [b * chunk, (b + 1) * chunk)
 	uint32_t order; // 2: XCD x (= b % 8) takes region [x * chunk, (x + 1) * chunk),
@@ -157,6 +162,11 @@ struct fwd4_params {
 	uint32_t spin_max; // polls before a ring wait gives up (0 = RING_SPIN_MAX)
 	uint32_t *err; // set to 1 when a workgroup gave up (host-mapped; may be NULL)
 };
+
+// First-level FIB6 entries a launch may stage in LDS: 2000::/4 (index =
+// address bytes 0-1), where every global unicast allocation lies today.
+#define FWD4_TOP6_BASE 0x2000u
+#define FWD4_TOP6_MAX 4096u
 
 // Kernel variants (bit mask, gr_hip_tune): counters, nontemporal loads and
 // stores of the streamed data.

@@ -367,6 +367,9 @@ __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params 
 		const uint4 *src6 = reinterpret_cast<const uint4 *>(T->nhf6) + 1;
 		for (uint32_t i = tid; i < A.nhf6_lds; i += C::WAVES * 64)
 			nhf_lds[A.nhf_lds + i] = gld4(src6 + i);
+		uint32_t *top6 = reinterpret_cast<uint32_t *>(nhf_lds + A.nhf_lds + A.nhf6_lds);
+		for (uint32_t i = tid; i < A.top6_lds; i += C::WAVES * 64)
+			top6[i] = gld(A.top6 + FWD4_TOP6_BASE + i);
 	}
 	for (uint32_t i = tid; i < sizeof(fwd4_edges); i += C::WAVES * 64)
 		reinterpret_cast<uint8_t *>(&edges)[i] = reinterpret_cast<const uint8_t *>(&T->edges)[i];
@@ -404,6 +407,9 @@ __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params 
 		kctx P = make_kctx(A, &edges);
 		P.nhf6_lds = (const __attribute__((address_space(3))) u4v *)(nhf_lds + A.nhf_lds);
 		P.nhf6_n = A.nhf6_lds;
+		P.top6 = A.top6;
+		P.top6_lds = (const __attribute__((address_space(3))) uint32_t *)(nhf_lds + A.nhf_lds + A.nhf6_lds);
+		P.top6_n = A.top6_lds;
 		ring_compute<C, STATS, PTRS>(A, P, L, slots, nhf_lds, n_local, wv - C::LOADERS - C::STORERS, lane);
 	}
 
@@ -453,7 +459,7 @@ static const ring_entry ring_ptrs_kernel = {
 // dynamic LDS.
 extern "C" hipError_t gr_fwd4_ring_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant, int cfg) {
 	const ring_entry &e = (variant & FWD4_V_PTRS) ? ring_ptrs_kernel : ring_kernels[(unsigned)cfg % RING_NCFG];
-	const size_t lds = (A->nhf_lds + A->nhf6_lds) * sizeof(fwd4_nhf);
+	const size_t lds = (A->nhf_lds + A->nhf6_lds) * sizeof(fwd4_nhf) + A->top6_lds * sizeof(uint32_t);
 	hipLaunchKernelGGL(e.fn[variant & 3], dim3(grid), dim3(e.threads), lds, s, *A);
 	return hipGetLastError();
 }

@@ -234,6 +234,10 @@ struct gr_hip_ctx {
 	fwd4_nhf *d_nhf6;
 	uint32_t v6_routes; // IPv6 routes on the device, all VRFs (stage nhf6 in LDS when > 0)
 	std::vector<fwd4_rx6> rx6[2]; // IPv6 views and adjacencies (host images)
+	// per generation: the trie every IPv6 RX view points at when they all
+	// point at one (one VRF with IPv6 routes), which launches stage the
+	// 2000::/4 first-level entries of in LDS; NULL otherwise
+	const uint32_t *top6[2];
 	std::vector<fwd4_adj6> adj6;
 	fwd4_rx6 *d_rx6[2];
 	fwd4_adj6 *d_adj6;
@@ -518,6 +522,19 @@ static fwd4_nhf make_nhf6(const fwd4_adj6 &a) {
 	return f;
 }
 
+// The trie all of generation g's IPv6 RX views share (NULL: none, or several).
+static const uint32_t *common_top6(const gr_hip_ctx *c, uint32_t g) {
+	const uint32_t *t = nullptr;
+	for (const fwd4_rx6 &r : c->rx6[g]) {
+		if (r.top == nullptr || r.top == t)
+			continue;
+		if (t != nullptr)
+			return nullptr;
+		t = r.top;
+	}
+	return t;
+}
+
 // Recompute and upload the RX views of generation g (IPv4 and IPv6, every
 // iface) on the control stream; does not wait.
 static int upload_rx(gr_hip_ctx *c, uint32_t g) {
@@ -525,6 +542,7 @@ static int upload_rx(gr_hip_ctx *c, uint32_t g) {
 		c->rx[g][i] = make_rx(c, i, g);
 		c->rx6[g][i] = make_rx6(c, i, g);
 	}
+	c->top6[g] = common_top6(c, g);
 	HCK(hipMemcpyAsync(c->d_rx[g], c->rx[g].data(), sizeof(fwd4_rx) * c->max_ifaces, hipMemcpyHostToDevice, c->ctl));
 	HCK(hipMemcpyAsync(c->d_rx6[g], c->rx6[g].data(), sizeof(fwd4_rx6) * c->max_ifaces, hipMemcpyHostToDevice,
 			   c->ctl));
@@ -689,6 +707,7 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	for (uint32_t g = 0; g < 2; g++) {
 		c->rx[g].assign(max_ifaces, fwd4_rx {});
 		c->rx6[g].assign(max_ifaces, fwd4_rx6 {});
+		c->top6[g] = nullptr;
 	}
 	c->adj.assign((size_t)max_nexthops + 1, fwd4_adj {});
 	c->nhf.assign((size_t)max_nexthops + 1, fwd4_nhf {});
@@ -1182,6 +1201,7 @@ static void stage_rx(stager &st, gr_hip_ctx *c, uint32_t g) {
 		c->rx[g][i] = make_rx(c, i, g);
 		c->rx6[g][i] = make_rx6(c, i, g);
 	}
+	c->top6[g] = common_top6(c, g);
 	memcpy(st.add(c->d_rx[g], c->max_ifaces), c->rx[g].data(), sizeof(fwd4_rx) * c->max_ifaces);
 	memcpy(st.add(c->d_rx6[g], c->max_ifaces), c->rx6[g].data(), sizeof(fwd4_rx6) * c->max_ifaces);
 }
@@ -1930,6 +1950,9 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	// as many as the geometry's LDS leaves room for (IPv6 given up first)
 	uint32_t n4 = c->nh_hi < gr_fwd4_ring_nhf_max() ? c->nh_hi : gr_fwd4_ring_nhf_max();
 	uint32_t n6 = c->v6_routes ? n4 : 0;
+	// and 2000::/4 of the IPv6 trie's first level, when one VRF holds IPv6
+	// routes (given up before the fast adjacencies; in 16-byte units below)
+	uint32_t t6 = c->v6_routes && c->top6[g] != nullptr ? FWD4_TOP6_MAX : 0;
 	int occ;
 	{
 		std::lock_guard<std::mutex> ol(c->occ_mu);
@@ -1946,7 +1969,11 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 				e.occ[v] = gr_fwd4_ring_occupancy(v, cfg, staged);
 			return e;
 		};
-		const gr_hip_ctx::occ_entry *e = &occ_of(n4 + n6);
+		const gr_hip_ctx::occ_entry *e = &occ_of(n4 + n6 + t6 / 4);
+		if (e->occ[variant] <= 0 && t6) {
+			t6 = 0;
+			e = &occ_of(n4 + n6);
+		}
 		if (e->occ[variant] <= 0 && n6) {
 			n6 = 0;
 			e = &occ_of(n4);
@@ -1960,6 +1987,8 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	}
 	A.nhf_lds = n4;
 	A.nhf6_lds = n6;
+	A.top6 = t6 ? c->top6[g] : nullptr;
+	A.top6_lds = t6;
 	uint32_t per_cu = c->wg_per_cu > 0 ? (uint32_t)c->wg_per_cu : RING_WG_PER_CU;
 	if (occ > 0 && per_cu > (uint32_t)occ)
 		per_cu = (uint32_t)occ;
