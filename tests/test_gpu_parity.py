@@ -628,6 +628,51 @@ def test_clustered_routes6_stream(fastpath, seed):
     assert (g[1]["edge"] == abi.EDGE["port_output"]).mean() > 0.9
 
 
+@pytest.mark.parametrize("second_vrf", [False, True], ids=["one_vrf", "two_vrfs"])
+def test_routes6_per_vrf(fastpath, second_vrf):
+    """The first level's 2000::/4 slice is staged in LDS only when one VRF
+    holds IPv6 routes (fwd4_params.top6): packets of a second VRF, whose trie
+    holds the same prefixes on other nexthops, must walk their own VRF's trie
+    (no slice staged), and lookups outside the slice (3000::/4) gather the
+    first level as before. Ingress on p0 (VRF 1) and p3 (VRF 6, or VRF 1;
+    VRFs are ifaces: ids 2-5 are the ports)."""
+    t = T.Topology()
+    t.add_vrf(1, max_routes=1 << 10)
+    for p in range(3):
+        t.add_port(T.PORT_IFACE[p], p, T.PORT_MAC[p])
+    vrf_b = 6 if second_vrf else 1
+    if second_vrf:
+        t.add_vrf(vrf_b, max_routes=1 << 10)
+    t.add_port(T.PORT_IFACE[3], 3, T.PORT_MAC[3], vrf_id=vrf_b)
+    first = T.fullview6_nexthops(t, 64)
+    r = T.fullview6_routes(20_000, 1, first, 32)
+    extra = r.copy()  # the same prefixes under 3000::/4
+    extra["ip"][:, 0] += 0x10
+    both = np.concatenate([r, extra])
+    t.fibs6[1] = (len(both) + 10, 1 << 16)
+    t.add_routes6(both)
+    if second_vrf:
+        rb = both.copy()
+        rb["vrf_id"] = vrf_b
+        rb["nh"] = first + 32 + (np.arange(len(rb)) % 32)
+        t.fibs6[vrf_b] = (len(rb) + 10, 1 << 16)
+        t.add_routes6(rb)
+    n = 1 << 17
+    sel = both[both["prefixlen"] < 128]
+    fa, ma = S.stream6(n, 0x6A01, sel)
+    fb, mb = S.stream6(n, 0x6A02, sel, in_iface=T.PORT_IFACE[3], dst_mac=T.PORT_MAC[3])
+    pick = np.random.default_rng(0x6A03).integers(0, 2, size=n).astype(bool)
+    fr = np.where(pick[:, None], fa, fb)
+    me = np.where(pick, ma, mb)
+    o = oracle.Oracle(t).process(fr, me)
+    g = run_gpu(fastpath, t, fr, me)
+    compare(o, g)
+    assert (g[1]["edge"] == abi.EDGE["port_output"]).mean() > 0.99
+    if second_vrf:  # the two VRFs' nexthops differ: each packet took its own VRF's
+        nh = g[1]["nh"]
+        assert (nh[pick] < first + 32).all() and (nh[~pick] >= first + 32).all()
+
+
 def test_mixed_v4_v6_stream(fastpath):
     """IPv4 and IPv6 packets interleaved in every wave (divergent chains)."""
     t, _ = SC.corpus_topology()
