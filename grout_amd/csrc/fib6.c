@@ -809,7 +809,7 @@ static inline int put_at(gr_fib6_t *f, uint32_t e, uint32_t v) {
 // granularity), from entry e of the groups array on (a group slot's content
 // with sh 0, or a row of its parent's wide group).
 static int rows_of(gr_fib6_t *f, uint32_t n, uint32_t e, unsigned sh) {
-	for (uint32_t j = 0; j < (GR_FIB6_GROUP >> sh); j++) {
+	for (uint32_t j = 0; j < ((uint32_t)GR_FIB6_GROUP >> sh); j++) {
 		uint32_t v;
 		int r = entry_enc(f, f->nodes[n].ent[j << sh], &v);
 		if (r < 0)
@@ -821,7 +821,7 @@ static int rows_of(gr_fib6_t *f, uint32_t n, uint32_t e, unsigned sh) {
 }
 
 static int fill_row(gr_fib6_t *f, uint32_t e, unsigned sh, uint32_t leaf) {
-	for (uint32_t j = 0; j < (GR_FIB6_GROUP >> sh); j++) {
+	for (uint32_t j = 0; j < ((uint32_t)GR_FIB6_GROUP >> sh); j++) {
 		int r = put_at(f, e + j, leaf);
 		if (r < 0)
 			return r;

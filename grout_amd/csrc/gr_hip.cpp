@@ -2603,6 +2603,7 @@ extern "C" int gr_hip_node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, ui
 	if (w.n == 0)
 		return 0;
 	int r = w.r;
+	uint64_t t_prof = prof_now();
 	if (!w.sync) {
 		hipSetDevice(c->dev);
 		HCK(hipEventSynchronize(w.done));
@@ -2612,14 +2613,21 @@ extern "C" int gr_hip_node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, ui
 	}
 	if (r < 0 && r != -ETIMEDOUT)
 		return r;
+	uint64_t t = prof_now();
+	node_prof_ns[GR_HIP_NODE_PROF_FIN_WAIT] += t - t_prof;
 	// packets a kernel that gave up never reached go back to grout's CPU
 	// nodes, the others are handed back as usual
 	const uint32_t unfinished = node_unfinished(w.m, w.n, w.pos.data(), w.v);
-	std::shared_lock<std::shared_mutex> lk(c->mu); // the hand-back reads the iface and nexthop mirrors
-	const gr_node_vlans vl = {c->vlan_keys_h.data(), c->vlan_vals_h.data(), (uint32_t)c->vlan_keys_h.size()};
-	r = gr_node_apply_ex(w.m, w.n, w.burst, w.pos.data(), w.by_addr ? nullptr : w.out, GR_HIP_PREFIX, w.v,
-			     c->ifaces.data(), c->max_ifaces, c->nh.data(), (uint32_t)c->nh.size(), stats, &vl,
-			     q->node_if.data(), (uint32_t)q->node_if.size());
+	t_prof = prof_now();
+	node_prof_ns[GR_HIP_NODE_PROF_FIN_SCAN] += t_prof - t;
+	{
+		std::shared_lock<std::shared_mutex> lk(c->mu); // the hand-back reads the iface and nexthop mirrors
+		const gr_node_vlans vl = {c->vlan_keys_h.data(), c->vlan_vals_h.data(), (uint32_t)c->vlan_keys_h.size()};
+		r = gr_node_apply_ex(w.m, w.n, w.burst, w.pos.data(), w.by_addr ? nullptr : w.out, GR_HIP_PREFIX, w.v,
+				     c->ifaces.data(), c->max_ifaces, c->nh.data(), (uint32_t)c->nh.size(), stats, &vl,
+				     q->node_if.data(), (uint32_t)q->node_if.size());
+	}
+	node_prof_ns[GR_HIP_NODE_PROF_FIN_APPLY] += prof_now() - t_prof;
 	return r < 0 ? r : (int)unfinished;
 }
 

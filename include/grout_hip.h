@@ -715,8 +715,9 @@ int gr_hip_node_pending(gr_hip_queue_t *, int *ready);
 // max_ifaces entries, indexed by iface id.
 int gr_hip_node_iface_stats(gr_hip_queue_t *, struct gr_hip_iface_stats *stats, uint32_t max_ifaces, int reset);
 
-// Measurement: nanoseconds gr_hip_node_start (append + send) spent in each part, summed over
-// every queue of the process since the last reset. out[k] for k < n; returns
+// Measurement: nanoseconds gr_hip_node_start (append + send) and
+// gr_hip_node_finish spent in each part, summed over every queue of the
+// process since the last reset. out[k] for k < n; returns
 // GR_HIP_NODE_PROF_COUNT.
 enum {
 	GR_HIP_NODE_PROF_LAYOUT, // (unused: the layout is part of the staging)
@@ -725,6 +726,9 @@ enum {
 	GR_HIP_NODE_PROF_STAGE, // layout + staging (gr_hip_node_append), buffers grown
 	GR_HIP_NODE_PROF_LAUNCH, // the kernel launch (host_direct)
 	GR_HIP_NODE_PROF_RECORD, // the walk's completion event
+	GR_HIP_NODE_PROF_FIN_WAIT, // finish: the wait for the walk's GPU work and its error check
+	GR_HIP_NODE_PROF_FIN_SCAN, // finish: the pass for packets a kernel that gave up left
+	GR_HIP_NODE_PROF_FIN_APPLY, // finish: the context lock and the hand-back onto the views
 	GR_HIP_NODE_PROF_COUNT,
 };
 int gr_hip_node_prof(uint64_t *out, uint32_t n, int reset);

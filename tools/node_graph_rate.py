@@ -76,8 +76,8 @@ def main():
             wi = G.walk_info()
             ph = np.zeros(4, dtype=np.uint64)
             L.gpu_fwd4_prof(0, ph.ctypes.data)
-            lp = np.zeros(6, dtype=np.uint64)
-            H.gr_hip_node_prof(lp.ctypes.data, 6, 1)
+            lp = np.zeros(9, dtype=np.uint64)
+            H.gr_hip_node_prof(lp.ctypes.data, 9, 1)
             assert walks > 0, walks
             if rep == 0:
                 continue  # warm-up: staging buffers grown, pages touched
@@ -92,7 +92,8 @@ def main():
                               "ms": round(dt * 1e3, 2), "mpps": round(len(me) / dt / 1e6, 1),
                               "ns_per_pkt": per,
                               "start_ns_per_pkt": {k: round(float(v) / len(me), 2) for k, v in zip(
-                                  ["layout", "prep", "lock", "stage", "launch", "record"], lp)},
+                                  ["layout", "prep", "lock", "stage", "launch", "record", "fin_wait", "fin_scan",
+                                   "fin_apply"], lp)},
                               "mode": "frames by address" if args.pin else "staged lines"}), flush=True)
 
 
