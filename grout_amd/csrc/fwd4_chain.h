@@ -496,12 +496,7 @@ __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, 
 		r.edge = mc ? GR_HIP_E_IP6_INPUT_LOCAL : GR_HIP_E_IP6_INPUT_OTHER_HOST;
 		return;
 	}
-	// the trie walk is a chain of dependent loads the wave waits on: issue
-	// them ahead of the streaming waves' (s_setprio; raised for the walk only,
-	// the IPv4 chain and the ring waits keep the default)
-	__builtin_amdgcn_s_setprio(2);
 	uint32_t slot = chain_fib6(P, load_rx6(P, rx.id), dst, rx.id); // ip6_input.c:124-131
-	__builtin_amdgcn_s_setprio(0);
 	if (slot == 0 || slot > P.max_nh) {
 		r.edge = GR_HIP_E_IP6_ERROR_DEST_UNREACH;
 		return;

@@ -314,7 +314,13 @@ __device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds<C, PT
 					}
 				}
 			} else if (head == HEAD_IP6) {
+				// the IPv6 chain (trie walk included) waits on dependent
+				// loads: its wave issues ahead of the streaming waves
+				// (s_setprio) until it leaves it; the IPv4 chain and the ring
+				// waits keep the default (raising them costs IPv4)
+				__builtin_amdgcn_s_setprio(2);
 				chain6(P, R, lane, m, rx, r, data_len);
+				__builtin_amdgcn_s_setprio(0);
 			}
 		}
 		if (__ballot(r.edge == GR_HIP_E_ETH_OUTPUT_NO_MAC) != 0
