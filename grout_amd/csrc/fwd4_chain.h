@@ -18,14 +18,8 @@
 __device__ __forceinline__ kctx make_kctx(const fwd4_params &A, const fwd4_edges *edges) {
 	const fwd4_tables *T = A.T;
 	kctx P;
+	P.T = T;
 	P.rx = T->rx;
-	P.adj = T->adj;
-	P.nhf = T->nhf;
-	P.reta = T->reta;
-	P.vlan_keys = T->vlan_keys;
-	P.vlan_vals = T->vlan_vals;
-	P.reta_cap = T->reta_cap;
-	P.vlan_mask = T->vlan_mask;
 	P.max_ifaces = T->max_ifaces;
 	P.max_nh = T->max_nh;
 	P.readable = A.readable;
@@ -34,8 +28,6 @@ __device__ __forceinline__ kctx make_kctx(const fwd4_params &A, const fwd4_edges
 	P.ip4_edge = type_edge_of(*edges, 0x0008u);
 	P.ip6_edge = type_edge_of(*edges, 0xdd86u);
 	P.rx6 = T->rx6;
-	P.adj6 = T->adj6;
-	P.nhf6 = T->nhf6;
 	P.nhf6_lds = nullptr; // set by the kernel that stages them
 	P.nhf6_n = 0;
 	P.top6 = nullptr;
@@ -256,7 +248,7 @@ __device__ __forceinline__ void chain_tail(const kctx &P, uint8_t *R, uint32_t r
 					  uint4 a, uint4 b) {
 	adjv A = unpack_adj(a, b, uint4{0, 0, 0, 0});
 	if (A.type == GR_HIP_NH_T_GROUP) { // nexthop_group_get_nh, nexthop.h:89-96
-		const uint4 c = gld4(reinterpret_cast<const uint4 *>(P.adj + slot) + 2);
+		const uint4 c = gld4(reinterpret_cast<const uint4 *>(tload(&P.T->adj) + slot) + 2);
 		const uint32_t n_members = c.x & 0xffff, reta_size = c.x >> 16;
 		if (n_members == 1) {
 			slot = c.z;
@@ -264,7 +256,7 @@ __device__ __forceinline__ void chain_tail(const kctx &P, uint8_t *R, uint32_t r
 			slot = 0;
 		} else {
 			uint32_t i = c.y + (m.rss & (reta_size - 1));
-			slot = i < P.reta_cap ? gld(P.reta + i) : 0;
+			slot = i < tload(&P.T->reta_cap) ? gld(tload(&P.T->reta) + i) : 0;
 		}
 		if (slot == 0 || slot > P.max_nh) {
 			r.edge = GR_HIP_E_IP_ERROR_DEST_UNREACH;
@@ -405,23 +397,52 @@ __device__ __forceinline__ fwd4_rx6 load_rx6(const kctx &P, uint32_t id) {
 
 // rte_fib6_lookup (modules/ip6/control/route.c:150-173) in the fib6.h trie of the iface's VRF:
 // key = dst with link-local addresses scoped to the ingress iface
-// (addr6_linklocal_scope, ip6.h:23-36).
-__device__ __forceinline__ uint32_t chain_fib6(const kctx &P, const fwd4_rx6 &v, const uint32_t (&dst)[4],
-					      uint32_t iface_id) {
+// (addr6_linklocal_scope, ip6.h:23-36). chain6 runs it in two parts: the
+// first level and the gather of the level after it before ip6_input's checks
+// (fib6_first), so that they run while that gather is in flight, the rest
+// after them (fib6_rest); a packet the checks stop discards the gather.
+
+// Slot offset in the groups array of the element of entry `ent` (range, wide
+// or plain group) for key byte b (and b + 1 for wide and range groups).
+__device__ __forceinline__ size_t fib6_group_off(uint32_t ent, const uint32_t (&key)[4], int b) {
+	const uint32_t kind = ent & GR_FIB6_RANGE;
+	const uint32_t x = byte_of(key, b), y = b < 15 ? byte_of(key, b + 1) : 0;
+	const uint32_t sh = (ent >> GR_FIB6_WIDE_SHIFT) & 7;
+	return kind == GR_FIB6_RANGE ? (size_t)(ent & GR_FIB6_IDX) * 256 + 2 * x
+	       : kind == GR_FIB6_WIDE ? (size_t)(ent & GR_FIB6_WIDE_IDX) * 256 + (x << (8 - sh)) + (y >> sh)
+				      : (size_t)(ent & GR_FIB6_IDX) * 256 + x;
+}
+
+// The entry the gathered element q gives for entry `ent` of a range, wide or
+// plain group at key byte b; b moves past the bytes it used.
+__device__ __forceinline__ uint32_t fib6_group_next(uint32_t ent, u2a q, const uint32_t (&key)[4], int &b) {
+	const uint32_t kind = ent & GR_FIB6_RANGE;
+	const uint32_t y = b < 15 ? byte_of(key, b + 1) : 0;
+	b += kind == 0 ? 1 : 2;
+	return kind == GR_FIB6_RANGE ? (y >= (q.x >> 24) && y <= (q.y >> 24) ? q.x : q.y) & GR_FIB6_RANGE_LEAF : q.x;
+}
+
+// The scoped key and the first level's entry for it: from LDS where the
+// launch staged it (2000::/4 of the only IPv6 VRF), else one gather. 0 (no
+// route) without a trie.
+__device__ __forceinline__ uint32_t fib6_first(const kctx &P, const fwd4_rx6 &v, const uint32_t (&dst)[4],
+					       uint32_t iface_id, uint32_t (&key)[4]) {
+	for (int i = 0; i < 4; i++)
+		key[i] = dst[i];
 	if (v.top == nullptr)
 		return 0;
-	uint32_t key[4] = {dst[0], dst[1], dst[2], dst[3]};
 	if ((key[0] & 0xff) == 0xfe && (key[0] & 0xc000) == 0x8000)
 		key[0] = (key[0] & 0xffff) | ((iface_id >> 8) << 16) | ((iface_id & 0xff) << 24);
-	// the first level: from LDS where the launch staged it (2000::/4 of the
-	// only IPv6 VRF), else one gather
 	const uint32_t idx = (byte_of(key, 0) << 8) | byte_of(key, 1);
 	const uint32_t k6 = idx - FWD4_TOP6_BASE;
-	uint32_t ent = v.top == P.top6 && k6 < P.top6_n ? P.top6_lds[k6] : gld(v.top + idx);
-	int b = 2;
+	return v.top == P.top6 && k6 < P.top6_n ? P.top6_lds[k6] : gld(v.top + idx);
+}
+
+// The walk from entry `ent` at key byte b to the leaf: the nexthop slot, 0 =
+// no route.
+__device__ __forceinline__ uint32_t fib6_rest(const fwd4_rx6 &v, const uint32_t (&key)[4], uint32_t ent, int b) {
 	while (b < 16 && (ent & 0x80000000u)) {
-		const uint32_t kind = ent & GR_FIB6_RANGE;
-		if (kind == GR_FIB6_SKIP) { // skip node: key bytes 0-6, n in byte 7
+		if ((ent & GR_FIB6_RANGE) == GR_FIB6_SKIP) { // skip node: key bytes 0-6, n in byte 7
 			const uint4 k = gld4(v.skips + (ent & GR_FIB6_IDX));
 			const int n = k.y >> 24;
 			bool match = b + n <= 16;
@@ -438,14 +459,8 @@ __device__ __forceinline__ uint32_t chain_fib6(const kctx &P, const fwd4_rx6 &v,
 		//   range group: entry {in | lo << 24, miss | hi << 24} by byte b
 		//   wide group: byte b and the top 8 - s bits of byte b + 1 (b <= 14)
 		//   plain group: byte b
-		const uint32_t x = byte_of(key, b), y = b < 15 ? byte_of(key, b + 1) : 0;
-		const uint32_t sh = (ent >> GR_FIB6_WIDE_SHIFT) & 7;
-		const size_t off = kind == GR_FIB6_RANGE ? (size_t)(ent & GR_FIB6_IDX) * 256 + 2 * x
-				   : kind == GR_FIB6_WIDE   ? (size_t)(ent & GR_FIB6_WIDE_IDX) * 256 + (x << (8 - sh)) + (y >> sh)
-							    : (size_t)(ent & GR_FIB6_IDX) * 256 + x;
-		const u2a q = *(const GR_GLOBAL u2a *)(v.groups + off);
-		ent = kind == GR_FIB6_RANGE ? (y >= (q.x >> 24) && y <= (q.y >> 24) ? q.x : q.y) & GR_FIB6_RANGE_LEAF : q.x;
-		b += kind == 0 ? 1 : 2;
+		const u2a q = *(const GR_GLOBAL u2a *)(v.groups + fib6_group_off(ent, key, b));
+		ent = fib6_group_next(ent, q, key, b);
 	}
 	return (ent & 0x80000000u) ? 0 : ent;
 }
@@ -474,6 +489,17 @@ __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, 
 		return;
 	}
 	const uint32_t dst[4] = {word_at2(w, 9), word_at2(w, 10), word_at2(w, 11), word_at2(w, 12)};
+	// the trie walk's first level and the gather after it, in flight under
+	// the address checks below, which may discard them (they are
+	// ip6_input.c:77-120)
+	const fwd4_rx6 v6 = load_rx6(P, rx.id);
+	uint32_t key[4];
+	uint32_t ent = fib6_first(P, v6, dst, rx.id, key);
+	int kb = 2; // the key byte ent indexes with
+	const bool pend = (ent & 0x80000000u) && (ent & GR_FIB6_RANGE) != GR_FIB6_SKIP;
+	u2a q = {0, 0};
+	if (pend)
+		q = *(const GR_GLOBAL u2a *)(v6.groups + fib6_group_off(ent, key, kb));
 	const uint32_t src0 = (w[5] >> 16) & 0xff;
 	if (src0 == 0xff || (dst[0] | dst[1] | dst[2] | dst[3]) == 0) { // mcast src, unspec dst, ip6_input.c:77-81
 		r.edge = GR_HIP_E_IP6_INPUT_BAD_ADDR;
@@ -496,7 +522,9 @@ __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, 
 		r.edge = mc ? GR_HIP_E_IP6_INPUT_LOCAL : GR_HIP_E_IP6_INPUT_OTHER_HOST;
 		return;
 	}
-	uint32_t slot = chain_fib6(P, load_rx6(P, rx.id), dst, rx.id); // ip6_input.c:124-131
+	if (pend) // ip6_input.c:124-131
+		ent = fib6_group_next(ent, q, key, kb);
+	uint32_t slot = fib6_rest(v6, key, ent, kb);
 	if (slot == 0 || slot > P.max_nh) {
 		r.edge = GR_HIP_E_IP6_ERROR_DEST_UNREACH;
 		return;
@@ -511,7 +539,7 @@ __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, 
 			const u4v v = P.nhf6_lds[slot - 1];
 			f = uint4{v.x, v.y, v.z, v.w};
 		} else {
-			f = gld4(P.nhf6 + slot);
+			f = gld4(tload(&P.T->nhf6) + slot);
 		}
 		if (f.w >> 16) {
 			r.nh = slot;
@@ -540,10 +568,11 @@ __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, 
 			return;
 		}
 	}
-	const uint4 *ap = reinterpret_cast<const uint4 *>(P.adj6 + slot);
+	const fwd4_adj6 *adj6 = tload(&P.T->adj6);
+	const uint4 *ap = reinterpret_cast<const uint4 *>(adj6 + slot);
 	uint4 a = gld4(ap), b = gld4(ap + 1), c = gld4(ap + 2);
 	if ((a.x & 0xff) == GR_HIP_NH_T_GROUP) { // nexthop_group_get_nh, nexthop.h:89-96
-		const uint4 g = gld4(reinterpret_cast<const uint4 *>(P.adj + slot) + 2);
+		const uint4 g = gld4(reinterpret_cast<const uint4 *>(tload(&P.T->adj) + slot) + 2);
 		const uint32_t n_members = g.x & 0xffff, reta_size = g.x >> 16;
 		if (n_members == 1) {
 			slot = g.z;
@@ -551,13 +580,13 @@ __device__ __forceinline__ void chain6(const kctx &P, uint8_t *R, uint32_t row, 
 			slot = 0;
 		} else {
 			const uint32_t i = g.y + (m.rss & (reta_size - 1));
-			slot = i < P.reta_cap ? gld(P.reta + i) : 0;
+			slot = i < tload(&P.T->reta_cap) ? gld(tload(&P.T->reta) + i) : 0;
 		}
 		if (slot == 0 || slot > P.max_nh) {
 			r.edge = GR_HIP_E_IP6_ERROR_DEST_UNREACH;
 			return;
 		}
-		ap = reinterpret_cast<const uint4 *>(P.adj6 + slot);
+		ap = reinterpret_cast<const uint4 *>(adj6 + slot);
 		a = gld4(ap);
 		b = gld4(ap + 1);
 		c = gld4(ap + 2);
@@ -651,7 +680,7 @@ __device__ bool eth_output_walks(const kctx &P, uint32_t lane, bool live, bool w
 	if (nomac)
 		eo = r.iface;
 	else if (out)
-		eo = fam == 2 ? gld(&P.adj6[r.nh].oif) : gld(&P.adj[r.nh].oif);
+		eo = fam == 2 ? gld(&tload(&P.T->adj6)[r.nh].oif) : gld(&tload(&P.T->adj)[r.nh].oif);
 	const uint64_t E = __ballot(nomac || out), N = __ballot(nomac);
 	const uint64_t F4 = __ballot(live && fam == 1), F6 = __ballot(live && fam == 2);
 	uint64_t starts = __ballot(live && walk_bit) | 1;

@@ -32,21 +32,26 @@ __device__ __forceinline__ uint4 gld4(const void *p) {
 
 // What the chain reads: table pointers (loaded once per workgroup from the
 // device-resident fwd4_tables) and the ether type table, copied into LDS.
+// A field of the launch's table block, through the scalar cache (the block
+// is uniform and read-only for the kernel's life).
+template <typename X>
+__device__ __forceinline__ X tload(const X *p) {
+	return *(const __attribute__((address_space(4))) X *)p;
+}
+
+// What the node chain keeps at hand; the tables only cold paths use (slow
+// adjacencies, ECMP retas, the VLAN table, the global fast adjacencies past
+// the LDS copies) are read from the table block T where they are used, so
+// that the kernel's SGPRs (106, all taken) are not held for them.
 struct kctx {
+	const fwd4_tables *T;
 	const fwd4_rx *rx;
-	const fwd4_adj *adj;
-	const fwd4_nhf *nhf;
-	const uint32_t *reta;
-	const uint32_t *vlan_keys;
-	const uint16_t *vlan_vals;
-	uint32_t reta_cap, vlan_mask, max_ifaces, max_nh, readable;
+	uint32_t max_ifaces, max_nh, readable;
 	const fwd4_edges *edges; // LDS copy
 	uint32_t ip4_edge; // eth_input edges of ether types IPv4 / IPv6 (wave-uniform)
 	uint32_t ip6_edge;
 	const fwd4_rx6 *rx6;
-	const fwd4_adj6 *adj6;
 	gr_hip_iface_stats *stats;
-	const fwd4_nhf *nhf6;
 	const __attribute__((address_space(3))) u4v *nhf6_lds; // slots 1..nhf6_n staged in LDS
 	uint32_t nhf6_n;
 	const uint32_t *top6; // the trie whose first-level entries FWD4_TOP6_BASE.. are staged
@@ -113,24 +118,27 @@ __device__ __forceinline__ adjv unpack_adj(uint4 a, uint4 b, uint4 c) {
 }
 
 __device__ __forceinline__ adjv load_adj(const kctx &P, uint32_t slot) {
-	const uint4 *p = reinterpret_cast<const uint4 *>(P.adj + slot);
+	const uint4 *p = reinterpret_cast<const uint4 *>(tload(&P.T->adj) + slot);
 	return unpack_adj(gld4(p), gld4(p + 1), gld4(p + 2));
 }
 
 // VLAN sub-interface demux, vlan_get_iface (vlan.c:27-34): open addressing
 // on (parent << 16 | vlan) + 1.
 __device__ __forceinline__ uint32_t vlan_lookup(const kctx &P, uint32_t parent, uint32_t vid) {
-	if (P.vlan_keys == nullptr)
+	const uint32_t *keys = tload(&P.T->vlan_keys);
+	if (keys == nullptr)
 		return 0;
+	const uint16_t *vals = tload(&P.T->vlan_vals);
+	const uint32_t mask = tload(&P.T->vlan_mask);
 	uint32_t key = ((parent << 16) | vid) + 1;
-	uint32_t h = (key * 0x9e3779b1u) & P.vlan_mask;
-	for (uint32_t i = 0; i <= P.vlan_mask; i++) {
-		uint32_t k = gld(P.vlan_keys + h);
+	uint32_t h = (key * 0x9e3779b1u) & mask;
+	for (uint32_t i = 0; i <= mask; i++) {
+		uint32_t k = gld(keys + h);
 		if (k == key)
-			return gld(P.vlan_vals + h);
+			return gld(vals + h);
 		if (k == 0)
 			return 0;
-		h = (h + 1) & P.vlan_mask;
+		h = (h + 1) & mask;
 	}
 	return 0;
 }

@@ -305,11 +305,11 @@ __device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds<C, PT
 					r.edge = GR_HIP_E_IP_ERROR_DEST_UNREACH; // NO_ROUTE :150-153
 				} else {
 					// fast adjacency: from LDS for the first slots, else one 16-byte gather
-					const uint4 f = slot <= A.nhf_lds ? nhf_lds[slot - 1] : gld4(P.nhf + slot);
+					const uint4 f = slot <= A.nhf_lds ? nhf_lds[slot - 1] : gld4(tload(&P.T->nhf) + slot);
 					if (f.w >> 16) {
 						fast_tail(R, lane, r, data_len, slot, f);
 					} else {
-						const uint4 *ap = reinterpret_cast<const uint4 *>(P.adj + slot);
+						const uint4 *ap = reinterpret_cast<const uint4 *>(tload(&P.T->adj) + slot);
 						chain_tail(P, R, lane, m, rx.flags, r, dst, data_len, slot, gld4(ap), gld4(ap + 1));
 					}
 				}
