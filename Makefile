@@ -15,9 +15,11 @@ LIB_ORACLE = oracle/liboracle.so
 LIB_GRAPH = grout_amd/libgrout_graph.so
 GRAPH = grout_amd/graph
 GRAPH_SRC = $(GRAPH)/rte_graph_min.c $(GRAPH)/rte_rcu_min.c $(GRAPH)/gr_datapath_min.c $(GRAPH)/gpu_fwd4_node.c $(GRAPH)/gpu_fwd4_cpu_nodes.c \
-	$(GRAPH)/walk_harness.c \
+	$(GRAPH)/gr_control_min.c $(GRAPH)/gpu_fwd4_control.c \
+	$(GRAPH)/walk_harness.c $(GRAPH)/control_harness.c \
 	$(GRAPH)/graph_selftest.c
-GRAPH_HDRS = $(GRAPH)/rte_graph_min.h $(GRAPH)/rte_rcu_min.h $(GRAPH)/gr_datapath_min.h $(GRAPH)/gpu_fwd4_node.h include/grout_hip.h
+GRAPH_HDRS = $(GRAPH)/rte_graph_min.h $(GRAPH)/rte_rcu_min.h $(GRAPH)/gr_datapath_min.h $(GRAPH)/gpu_fwd4_node.h include/grout_hip.h \
+	$(GRAPH)/gr_control_min.h $(GRAPH)/gpu_fwd4_control.h
 HDRS = include/grout_hip.h $(CSRC)/fib6.h $(CSRC)/fwd4_kernel.h $(CSRC)/fwd4_dev.h $(CSRC)/fwd4_chain.h $(CSRC)/fib4.h
 
 all: $(LIB_HIP) $(LIB_HOST) $(LIB_ORACLE) $(LIB_GRAPH) tools/libnode_mt.so

@@ -286,6 +286,7 @@ struct gpu_walk {
 	uint64_t gpu_errors; // batches punted because the GPU call failed
 	uint64_t batches, max_batch, stale;
 	int rx_seen; // the node took packets since the flush node last ran
+	int draining; // gpu_fwd4_drain: hand everything back within the walk
 };
 
 static uint64_t now_ns(void) {
@@ -520,7 +521,7 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 		deliver(graph, node, w, k, n, -ESTALE);
 		return d + n;
 	}
-	if (conf.depth < 2 && !w->pending) { // synchronous
+	if ((conf.depth < 2 || w->draining) && !w->pending) { // synchronous
 		started(w, n);
 		int r = gr_hip_node_send(w->q, w->v[k], n, WALK_SPLIT);
 		if (r == 0)
@@ -624,7 +625,7 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 	const uint64_t t = now_ns();
 	if (w->first_ns == 0)
 		w->first_ns = t;
-	if (w->n >= conf.batch || nb_objs < conf.rx_burst || t - w->first_ns >= conf.max_delay_ns)
+	if (w->draining || w->n >= conf.batch || nb_objs < conf.rx_burst || t - w->first_ns >= conf.max_delay_ns)
 		flush(graph, node, w);
 	else
 		reap(graph, node, w);
@@ -699,19 +700,47 @@ static int gpu_fwd4_init(const struct rte_graph *graph, struct rte_node *node) {
 	return 0;
 }
 
+// mbufs a graph still held when it was destroyed (not drained first)
+static uint64_t fini_freed;
+
+uint64_t gpu_fwd4_fini_freed(void) {
+	return __atomic_load_n(&fini_freed, __ATOMIC_RELAXED);
+}
+
+// Leaving a graph (grout's worker before it switches to a new graph or shuts
+// down, main_loop.c:466-470, with integration/grout-gpu_fwd4-datapath.patch):
+// walk it until the node holds nothing. The walks hand the batch on the GPU
+// back (waiting for it) and send the held one synchronously, as they send
+// whatever RX brings meanwhile; one walk more takes the batches' QSBR readers
+// offline. grout itself holds no packet across graph walks.
+int gpu_fwd4_drain(struct rte_graph *graph) {
+	struct gpu_walk *w = walk_of(graph);
+	if (w == NULL)
+		return -ENOENT;
+	w->draining = 1;
+	for (int k = 0; k < 16 && (w->n != 0 || w->pending); k++)
+		rte_graph_walk(graph);
+	rte_graph_walk(graph); // the readers of the last hand-back go offline
+	w->draining = 0;
+	return (int)(w->n + (w->pending ? w->pend_n : 0));
+}
+
 static void gpu_fwd4_fini(const struct rte_graph *graph, struct rte_node *node) {
 	(void)node;
 	for (int i = 0; i < GPU_FWD4_MAX_GRAPHS; i++) {
 		struct gpu_walk *w = walks[i];
 		if (w == NULL || w->graph != graph)
 			continue;
-		if (w->pending) // the GPU must be done with its buffers; the mbufs go back to their pool
+		// a graph destroyed without gpu_fwd4_drain: its mbufs go back to the
+		// pool, counted (gpu_fwd4_fini_freed)
+		if (w->pending) // the GPU must be done with its buffers
 			gr_hip_node_finish(w->q, NULL, NULL, NULL);
 		if (w->pending)
 			for (uint32_t j = 0; j < w->pend_n; j++)
 				rte_pktmbuf_free(w->mbufs[w->cur ^ 1][j]);
 		for (uint32_t j = 0; j < w->n; j++) // held, never sent
 			rte_pktmbuf_free(w->mbufs[w->cur][j]);
+		__atomic_fetch_add(&fini_freed, w->n + (w->pending ? w->pend_n : 0), __ATOMIC_RELAXED);
 		gr_hip_queue_destroy(w->q);
 		for (int k = 0; k < GPU_FWD4_RCU_PER_GRAPH; k++) { // offline, then gone (rte_rcu_qsbr.h)
 			if (w->rstate[k] != RD_FREE)
@@ -758,15 +787,15 @@ static uint16_t gpu_flush_process(struct rte_graph *graph, struct rte_node *node
 	// (flush() hands back the one still pending, and none is after these)
 	const uint64_t t = now_ns();
 	uint32_t n = 0;
-	if (w->pending && t - w->pend_ns >= conf.max_delay_ns)
-		n = finish_pending(graph, node, w); // waited long enough: wait for the GPU
+	if (w->pending && (w->draining || t - w->pend_ns >= conf.max_delay_ns))
+		n = finish_pending(graph, node, w); // waited long enough (or leaving the graph): wait for the GPU
 	else
 		n = reap(graph, node, w);
 	// a whole graph walk brought the node nothing: the RX queues drained,
 	// latency wins over batching (as for a short burst); else max_delay
 	const int idle = !w->rx_seen;
 	w->rx_seen = 0;
-	if (w->n != 0 && (idle || t - w->first_ns >= conf.max_delay_ns))
+	if (w->n != 0 && (w->draining || idle || t - w->first_ns >= conf.max_delay_ns))
 		n += flush(graph, node, w); // pipelined: a later walk of the graph hands it back
 	return (uint16_t)(n > UINT16_MAX ? UINT16_MAX : n);
 }

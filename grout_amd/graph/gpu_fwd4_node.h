@@ -159,6 +159,18 @@ int gpu_fwd4_queue_stats(const struct rte_graph *, struct gr_hip_iface_stats *, 
 typedef void (*gpu_fwd4_node_stat_cb)(void *cookie, uint32_t node_id, uint64_t packets, uint64_t calls);
 int gpu_fwd4_stats_flush(const struct rte_graph *, unsigned lcore_id, gpu_fwd4_node_stat_cb cb, void *cookie);
 
+// The worker leaves its graph (reconfiguration or shutdown): before it does,
+// grout's gr_datapath_loop calls this on the graph (main_loop.c:466-470,
+// integration/grout-gpu_fwd4-datapath.patch). The node holds up to two
+// batches across graph walks, grout nothing: walks of the graph hand them
+// back through grout's nodes (the batch on the GPU waited for, the held one
+// sent at once) until the node holds nothing. Returns the mbufs still held
+// (0), or -ENOENT for a graph without the node.
+int gpu_fwd4_drain(struct rte_graph *);
+// mbufs freed by the node's fini because a graph was destroyed while it held
+// them (not drained first): counted, never silently.
+uint64_t gpu_fwd4_fini_freed(void);
+
 // Per-graph walk state, for tests and measurements.
 struct gpu_fwd4_walk_info {
 	uint32_t held; // mbufs accumulating

@@ -13,9 +13,12 @@
 //                           graph_init (graph.c:652-688)
 //   modules                 main/module.h:43-49 (struct module, module_register)
 //
-// The objects grout's nodes dereference (struct iface, struct nexthop) are
-// reduced to what the GPU node needs to hand packets back: an id and a
-// nexthop slot. Everything here is written for this repo; in grout the node
+// The objects grout's nodes dereference (struct iface, struct nexthop) have
+// grout's layout: the public base fields, then per-type info
+// (modules/infra/control/iface.h:20-35, nexthop.h:22-96). Nothing in the
+// datapath node reads more than the base fields and the L3 info; the control
+// plane stand-in (gr_control_min.h) and the mirror (gpu_fwd4_control.c) use
+// the rest. Everything here is written for this repo; in grout the node
 // includes grout's real headers instead.
 #pragma once
 
@@ -23,6 +26,7 @@
 #include "rte_rcu_min.h"
 
 #include <grout_hip.h>
+#include <stdalign.h>
 #include <stdbool.h>
 #include <sys/queue.h>
 
@@ -31,8 +35,9 @@ extern "C" {
 #endif
 
 // ---- objects ---------------------------------------------------------------
-// gr_iface_type_t / gr_iface_flags_t (gr_infra.h:18-38), gr_nh_* and
-// addr_family_t (gr_nexthop.h:12-40, gr_net_types.h): grout's values.
+// gr_iface_type_t / gr_iface_flags_t / gr_iface_mode_t (gr_infra.h:18-62),
+// gr_nh_* (gr_nexthop.h:12-82) and addr_family_t (gr_net_types.h): grout's
+// values.
 typedef uint8_t gr_iface_type_t; // grout: enum : uint8_t (C23)
 enum {
 	GR_IFACE_TYPE_UNDEF = 0,
@@ -44,55 +49,191 @@ enum {
 	GR_IFACE_TYPE_BRIDGE,
 	GR_IFACE_TYPE_VXLAN,
 };
+typedef uint8_t gr_iface_mode_t;
+#define GR_IFACE_MODE_VRF GR_HIP_IFACE_MODE_VRF
+#define GR_IFACE_MODE_XC GR_HIP_IFACE_MODE_XC
 #define GR_IFACE_F_UP GR_HIP_IFACE_F_UP
 #define GR_IFACE_F_SNAT_STATIC GR_HIP_IFACE_F_SNAT_STATIC
 #define GR_IFACE_F_SNAT_DYNAMIC GR_HIP_IFACE_F_SNAT_DYNAMIC
+#define GR_IFACE_S_RUNNING 0x0001
+
+// GR_IFACE_ID_UNDEF, GR_VRF_DEFAULT_ID, GR_VRF_ID_UNDEF (gr_infra.h:48-53)
+#define GR_IFACE_ID_UNDEF 0
+#define GR_VRF_DEFAULT_ID 1
+#define GR_VRF_ID_UNDEF GR_IFACE_ID_UNDEF
 typedef uint8_t addr_family_t;
 #define GR_AF_UNSPEC GR_HIP_AF_UNSPEC
 #define GR_AF_IP4 GR_HIP_AF_IP4
 #define GR_AF_IP6 GR_HIP_AF_IP6
 typedef uint8_t gr_nh_type_t;
 #define GR_NH_T_L3 GR_HIP_NH_T_L3
+#define GR_NH_T_BLACKHOLE GR_HIP_NH_T_BLACKHOLE
+#define GR_NH_T_REJECT GR_HIP_NH_T_REJECT
+#define GR_NH_T_GROUP GR_HIP_NH_T_GROUP
+typedef uint8_t gr_nh_state_t;
+#define GR_NH_S_NEW GR_HIP_NH_S_NEW
+#define GR_NH_S_PENDING GR_HIP_NH_S_PENDING
 #define GR_NH_S_REACHABLE GR_HIP_NH_S_REACHABLE
+#define GR_NH_S_STALE GR_HIP_NH_S_STALE
+#define GR_NH_S_FAILED GR_HIP_NH_S_FAILED
+typedef uint8_t gr_nh_flags_t;
 #define GR_NH_F_LOCAL GR_HIP_NH_F_LOCAL
+#define GR_NH_F_GATEWAY GR_HIP_NH_F_GATEWAY
 #define GR_NH_F_LINK GR_HIP_NH_F_LINK
+#define GR_NH_F_MCAST GR_HIP_NH_F_MCAST
+#define GR_NH_F_NEIGH 0x20
+#define NH_LOCAL_ADDR_FLAGS (GR_NH_F_LOCAL | GR_NH_F_LINK) // nexthop.h:185
+typedef uint8_t gr_nh_origin_t;
+#define GR_NH_ORIGIN_UNSPEC 0
+#define GR_NH_ORIGIN_LINK 2
+#define GR_NH_ORIGIN_LEARN 3
+#define GR_NH_ORIGIN_STATIC 4
+#define GR_NH_ORIGIN_ZEBRA 11
+#define GR_NH_ORIGIN_BGP 186
+#define GR_NH_ORIGIN_INTERNAL 255
+#define GR_NH_ID_UNSET 0
 typedef uint32_t ip4_addr_t; // network order
 
-struct iface {
-	uint16_t id;
-	gr_iface_type_t type;
-	uint8_t mode;
-	uint16_t flags;
-	uint16_t mtu;
-	uint16_t vrf_id;
+// __gr_iface_base (gr_infra.h:73-87)
+#define GR_IFACE_BASE_FIELDS                                                                       \
+	uint16_t id;                                                                               \
+	gr_iface_type_t type;                                                                      \
+	gr_iface_mode_t mode;                                                                      \
+	uint16_t flags;                                                                            \
+	uint16_t state;                                                                            \
+	uint16_t mtu;                                                                              \
+	uint16_t vrf_id;                                                                           \
+	uint16_t domain_id;                                                                        \
+	uint32_t speed;
+struct __gr_iface_base {
+	GR_IFACE_BASE_FIELDS
 };
 
-// nexthop_info_l3 (nexthop.h:41-54 over gr_nexthop.h:93-105)
-struct nexthop_info_l3 {
-	uint8_t state;
-	uint8_t flags;
-	addr_family_t af;
-	ip4_addr_t ipv4;
-	uint8_t ipv6[16];
+#define GR_IFACE_INFO_SIZE 64
+struct iface {
+	union { // BASE(__gr_iface_base)
+		struct __gr_iface_base base;
+		struct {
+			GR_IFACE_BASE_FIELDS
+		};
+	};
+	char *name;
+	alignas(void *) uint8_t info[GR_IFACE_INFO_SIZE]; // grout: sized by type
+};
+
+// Per-type iface info (GR_IFACE_INFO, iface.h:37-42): vrf.h:10-16,
+// port.h:17-30, vlan.h:10 over gr_infra.h:105-153.
+struct gr_iface_info_vrf_fib {
+	uint32_t max_routes; // 0 = default
+	uint32_t num_tbl8; // 0 = auto
+};
+struct iface_info_vrf {
+	struct gr_iface_info_vrf_fib ipv4;
+	struct gr_iface_info_vrf_fib ipv6;
+	struct rte_ether_addr mac;
+	uint16_t ref_count;
+};
+struct iface_info_port {
+	uint16_t n_rxq, n_txq, rxq_size, txq_size;
+	struct rte_ether_addr mac;
+	uint16_t port_id;
+};
+struct iface_info_vlan {
+	uint16_t parent_id;
+	uint16_t vlan_id;
 	struct rte_ether_addr mac;
 };
+#define GR_IFACE_INFO_GETTER(type_name)                                                            \
+	static inline struct type_name *type_name(const struct iface *iface) {                     \
+		_Static_assert(sizeof(struct type_name) <= GR_IFACE_INFO_SIZE, #type_name);        \
+		return (struct type_name *)iface->info;                                            \
+	}
+GR_IFACE_INFO_GETTER(iface_info_vrf)
+GR_IFACE_INFO_GETTER(iface_info_port)
+GR_IFACE_INFO_GETTER(iface_info_vlan)
 
-struct nexthop {
-	uint32_t slot; // the dense index the device FIB holds
-	gr_nh_type_t type;
-	uint16_t iface_id;
-	uint16_t vrf_id;
-	struct nexthop_info_l3 l3;
+// struct gr_nexthop_base (gr_nexthop.h:84-90)
+#define GR_NEXTHOP_BASE_FIELDS                                                                     \
+	gr_nh_type_t type;                                                                         \
+	gr_nh_origin_t origin;                                                                     \
+	uint16_t iface_id;                                                                         \
+	uint16_t vrf_id;                                                                           \
+	uint32_t nh_id;
+struct gr_nexthop_base {
+	GR_NEXTHOP_BASE_FIELDS
 };
 
-static inline const struct nexthop_info_l3 *nexthop_info_l3(const struct nexthop *nh) {
-	return &nh->l3;
+// struct gr_nexthop_info_l3 (gr_nexthop.h:93-105)
+#define GR_NEXTHOP_INFO_L3_FIELDS                                                                  \
+	gr_nh_state_t state;                                                                       \
+	gr_nh_flags_t flags;                                                                       \
+	addr_family_t af;                                                                          \
+	uint8_t prefixlen;                                                                         \
+	union {                                                                                    \
+		ip4_addr_t ipv4;                                                                   \
+		uint8_t ipv6[16];                                                                  \
+	};                                                                                         \
+	struct rte_ether_addr mac;
+struct gr_nexthop_info_l3 {
+	GR_NEXTHOP_INFO_L3_FIELDS
+};
+
+// struct nexthop (nexthop.h:22-31): two cache lines
+struct nexthop {
+	union { // BASE(gr_nexthop_base)
+		struct gr_nexthop_base base;
+		struct {
+			GR_NEXTHOP_BASE_FIELDS
+		};
+	};
+	uint32_t ref_count; // number of routes referencing this nexthop
+	alignas(void *) uint8_t info[128 - sizeof(struct gr_nexthop_base) - sizeof(uint32_t)];
+};
+
+// GR_NH_TYPE_INFO(GR_NH_T_L3, nexthop_info_l3, ...) (nexthop.h:43-56)
+struct nexthop_info_l3 {
+	union { // BASE(gr_nexthop_info_l3)
+		struct gr_nexthop_info_l3 base;
+		struct {
+			GR_NEXTHOP_INFO_L3_FIELDS
+		};
+	};
+	uint64_t last_reply;
+	uint64_t last_request;
+	uint8_t ucast_probes;
+	uint8_t bcast_probes;
+	uint16_t held_pkts;
+};
+
+// GR_NH_TYPE_INFO(GR_NH_T_GROUP, nexthop_info_group, ...) (nexthop.h:75-87)
+struct nh_group_member {
+	struct nexthop *nh;
+	uint32_t weight;
+};
+#define MAX_NH_GROUP_RETA_SIZE 4096
+struct nexthop_info_group {
+	uint16_t n_members;
+	uint16_t reta_size; // a power of two
+	struct nexthop *nh; // shortcut when there is a single nexthop in the group
+	struct nh_group_member *members;
+	struct nexthop **reta;
+};
+
+static inline struct nexthop_info_l3 *nexthop_info_l3(const struct nexthop *nh) {
+	_Static_assert(sizeof(struct nexthop_info_l3) <= sizeof(((struct nexthop *)0)->info), "l3 info");
+	return (struct nexthop_info_l3 *)nh->info;
+}
+
+static inline struct nexthop_info_group *nexthop_info_group(const struct nexthop *nh) {
+	_Static_assert(sizeof(struct nexthop_info_group) <= sizeof(((struct nexthop *)0)->info), "group info");
+	return (struct nexthop_info_group *)nh->info;
 }
 
 // grout's iface registry (iface.c:459-466: ifaces[id], cleared by
 // iface_destroy before its RCU synchronisation, :710-712). The nexthop
 // objects the fast path names by slot are the node's own registry
 // (gpu_fwd4_nh_obj_set), not grout's.
+#define GR_MAX_IFACES 1024
 const struct iface *iface_from_id(uint16_t id);
 void gr_iface_register(struct iface *);
 void gr_iface_unregister(uint16_t id);

@@ -17,7 +17,9 @@
 // which node each mbuf reached, in order, and keeps the mbuf.
 // mbufs are built like grout's pool (mempool.c:57-100): 128-byte rte_mbuf,
 // 64-byte private area, 2048-byte data room, frame at headroom 128.
+#include "gpu_fwd4_control.h"
 #include "gpu_fwd4_node.h"
+#include "gr_control_min.h"
 #include "gr_datapath_min.h"
 
 #include <errno.h>
@@ -298,7 +300,6 @@ int gh_init(const int *devs, uint32_t n_devs, uint32_t max_ifaces, uint32_t max_
 			return r;
 	}
 	for (uint32_t s = 1; s <= max_nh; s++) {
-		H.nhs[s].slot = s;
 		if ((r = gpu_fwd4_nh_obj_set(s, &H.nhs[s])) < 0)
 			return r;
 	}
@@ -347,15 +348,18 @@ int gh_set_objects(const struct gr_hip_iface *ifs, uint32_t n_if, const struct g
 			return -EINVAL;
 		const struct gr_hip_nh *s = &nhs[k];
 		struct nexthop *d = &H.nhs[slot];
+		struct nexthop_info_l3 *l3 = nexthop_info_l3(d);
 		d->type = s->type;
 		d->iface_id = s->iface_id;
 		d->vrf_id = s->vrf_id;
-		d->l3.state = s->state;
-		d->l3.flags = s->flags;
-		d->l3.af = s->af;
-		d->l3.ipv4 = s->ipv4;
-		memcpy(d->l3.ipv6, s->ipv6, 16);
-		memcpy(d->l3.mac.addr_bytes, s->mac, 6);
+		l3->state = s->state;
+		l3->flags = s->flags;
+		l3->af = s->af;
+		if (s->af == GR_AF_IP6)
+			memcpy(l3->ipv6, s->ipv6, 16);
+		else
+			l3->ipv4 = s->ipv4;
+		memcpy(l3->mac.addr_bytes, s->mac, 6);
 	}
 	return 0;
 }
@@ -376,14 +380,22 @@ void gh_policy_clear(void) {
 // One worker's graph: what worker_graph_new selects (graph.c:93-145), named
 // after the worker's CPU like grout's ("gr-%04x", (cpu << 1) | index) and
 // created on `socket`. It becomes the current graph.
+static int graph_create(unsigned cpu, unsigned index, int socket);
+
 int gh_graph_create(unsigned cpu, int socket) {
+	return graph_create(cpu, 0, socket);
+}
+
+// grout names a worker's graphs "gr-%04x" with (cpu << 1) | index, the index
+// alternating at each reconfiguration (worker_graph_reload, graph.c:263-290)
+static int graph_create(unsigned cpu, unsigned index, int socket) {
 	int k = 0;
 	while (k < GH_MAX_GRAPHS && H.graphs[k].graph != NULL)
 		k++;
 	if (k == GH_MAX_GRAPHS)
 		return -ENOSPC;
 	char name[RTE_GRAPH_NAMESIZE];
-	snprintf(name, sizeof(name), "gr-%04x", (cpu << 1) & 0xffff);
+	snprintf(name, sizeof(name), "gr-%04x", ((cpu << 1) | (index & 1)) & 0xffff);
 	const char *patterns[2 + N_REPLACED] = {"port_rx", "gpu_fwd4_flush"};
 	for (unsigned i = 0; i < N_REPLACED; i++)
 		patterns[2 + i] = replaced[i];
@@ -549,6 +561,42 @@ static void walk_once(int k) {
 		H.loop = 0;
 		housekeeping(k);
 	}
+}
+
+// The worker while grout's control thread works (control_harness.c): one
+// walk of the current graph (nothing injected is left: the flush node runs,
+// the QSBR readers of the batches handed back go offline) and a quiescent
+// report, as gr_datapath_loop does between bursts (main_loop.c:441-464).
+void gh_walk_idle(void) {
+	if (H.cur >= 0 && H.graphs[H.cur].graph != NULL)
+		walk_once(H.cur);
+	if (H.inited && gr_datapath_rcu() != NULL)
+		rte_rcu_qsbr_quiescent(gr_datapath_rcu(), rte_lcore_id());
+}
+
+int gh_inited(void) {
+	return H.inited;
+}
+
+// The harness's own objects out of grout's iface table and the node's
+// registries (a test that builds its objects through grout's control plane
+// instead, control_harness.c), and back.
+void gh_objects_clear(void) {
+	for (uint32_t i = 1; i < H.max_ifaces; i++) {
+		gr_iface_unregister((uint16_t)i);
+		gpu_fwd4_iface_obj_set((uint16_t)i, NULL);
+	}
+	for (uint32_t s = 1; s <= H.max_nh; s++)
+		gpu_fwd4_nh_obj_set(s, NULL);
+}
+
+void gh_objects_restore(void) {
+	for (uint32_t i = 1; i < H.max_ifaces; i++) {
+		gr_iface_register(&H.ifaces[i]);
+		gpu_fwd4_iface_obj_set((uint16_t)i, &H.ifaces[i]);
+	}
+	for (uint32_t s = 1; s <= H.max_nh; s++)
+		gpu_fwd4_nh_obj_set(s, &H.nhs[s]);
 }
 
 // Walk the current graph until every injected mbuf reached a recorder, at
@@ -906,14 +954,21 @@ int gh_churn_test(uint32_t ip_be, uint8_t prefixlen, uint16_t vrf_id, uint32_t a
 static uint32_t slot_of(const struct nexthop *nh) {
 	if (nh == NULL)
 		return 0;
-	if (nh < H.nhs + 1 || nh > H.nhs + H.max_nh)
-		return 0xffffffffu;
+	if (nh < H.nhs + 1 || nh > H.nhs + H.max_nh) {
+		// grout's nexthops (the control-plane stand-in's pool): the slot the
+		// mirror gave them, looked up by address
+		const uint32_t s = gpu_fwd4_control_nh_slot(nh);
+		return s != 0 ? s : 0xffffffffu;
+	}
 	return (uint32_t)(nh - H.nhs);
 }
 
 static uint32_t iface_id_of(const struct iface *i) {
 	if (i == NULL)
 		return 0;
+	const struct iface *c = gr_test_iface_base(); // grout's ifaces (control-plane stand-in)
+	if (i >= c + 1 && i < c + GR_MAX_IFACES)
+		return (uint32_t)(i - c);
 	if (i < H.ifaces + 1 || i >= H.ifaces + H.max_ifaces)
 		return 0xffff;
 	return (uint32_t)(i - H.ifaces);
@@ -992,4 +1047,50 @@ void gh_fini(void) {
 	H.edge_of = NULL;
 	H.seq_of = NULL;
 	H.n = 0;
+}
+
+// ---- a graph reload while the node holds batches ---------------------------
+struct gh_reload_result {
+	uint32_t held; // mbufs the node held when the worker left the graph
+	uint32_t in_flight; // batches it had on the GPU
+	int32_t left; // gpu_fwd4_drain's return (-1: not called)
+	uint32_t recorded; // mbufs through grout's nodes when the old graph was destroyed
+	uint64_t fini_freed; // mbufs the old graph's fini freed
+	int32_t graph; // the new current graph
+	uint32_t _pad;
+};
+
+// grout's reconfiguration of a worker (worker_graph_reload, graph.c:263-290;
+// gr_datapath_loop, main_loop.c:466-470): the worker walks its graph
+// `walks` times, leaves it at a housekeeping tick (with the datapath patch:
+// gpu_fwd4_drain first, when `drain`), the control plane creates the new
+// graph (the other name index) and destroys the old one. The new graph is
+// the current one afterwards; port_rx goes on with the injected stream.
+int gh_reload_test(uint32_t walks, int drain, struct gh_reload_result *res) {
+	if (H.cur < 0 || res == NULL)
+		return -ENOENT;
+	memset(res, 0, sizeof(*res));
+	const int k = H.cur;
+	for (uint32_t i = 0; i < walks; i++)
+		walk_once(k);
+	struct gpu_fwd4_walk_info info;
+	gpu_fwd4_walk_info(H.graphs[k].graph, &info);
+	res->held = info.held;
+	res->in_flight = info.in_flight;
+	res->left = drain ? gpu_fwd4_drain(H.graphs[k].graph) : -1;
+	housekeeping(k);
+	res->recorded = __atomic_load_n(&H.recorded, __ATOMIC_ACQUIRE);
+	unsigned index = 0;
+	sscanf(H.graphs[k].name, "gr-%x", &index);
+	const int nk = graph_create(index >> 1, (index & 1) ^ 1, 0);
+	if (nk < 0)
+		return nk;
+	const uint64_t f0 = gpu_fwd4_fini_freed();
+	int r = rte_graph_destroy(H.graphs[k].gid);
+	H.graphs[k].graph = NULL;
+	graph_stats_free(k);
+	res->fini_freed = gpu_fwd4_fini_freed() - f0;
+	H.cur = nk;
+	res->graph = nk;
+	return r;
 }

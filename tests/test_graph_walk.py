@@ -333,9 +333,13 @@ def stage_of(edges, nh, ip6):
     return np.array([L.gr_hip_edge_node(int(e), int(h), int(s)) for e, h, s in zip(edges, nh, ip6)])
 
 
-def check_walk(topo, fr, me, labels=None, burst=BURST):
+def check_walk(topo, fr, me, labels=None, burst=BURST, loaded=False):
+    """One walk of (fr, me) through the current graph against the oracle on
+    `topo`. loaded: the contexts already hold topo (a test that built it
+    through grout's control plane and the mirror, test_control_mirror.py)."""
     fp = graph_ctx(keep=True)  # on the current graph
-    load(fp, topo)
+    if not loaded:
+        load(fp, topo)
     L = lib()
     L.gh_queue_stats(None, 0, 1)  # reset the queue's iface counters
     L.gh_stats_reset()  # and grout's: iface_stats, the worker's node stats
@@ -786,3 +790,68 @@ def test_graph_walk_long_bursts(burst):
         assert (got["edge"] == abi.EDGE["port_output"]).all()
     finally:
         assert L.gh_set_rx_burst(BURST) == 0
+
+
+RELOAD_DT = np.dtype([("held", "<u4"), ("in_flight", "<u4"), ("left", "<i4"), ("recorded", "<u4"),
+                      ("fini_freed", "<u8"), ("graph", "<i4"), ("_pad", "<u4")])
+assert RELOAD_DT.itemsize == 32
+
+
+def _reload(walks, drain):
+    res = np.zeros(1, dtype=RELOAD_DT)
+    L = lib()
+    L.gh_reload_test.argtypes = [ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
+    assert L.gh_reload_test(walks, drain, res.ctypes.data) == 0
+    return res[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("drain", [1, 0], ids=["drained", "not_drained"])
+def test_graph_reload_mid_stream(drain):
+    """grout reconfigures a worker mid-stream (worker_graph_reload,
+    graph.c:263-290): the worker leaves its graph at a housekeeping tick
+    (main_loop.c:466-470), the control plane gives it a new graph and
+    destroys the old one. grout's nodes hold nothing across walks; the fast
+    path's node holds the batch it accumulates (and one on the GPU). With
+    the datapath patch the worker drains the node first (gpu_fwd4_drain):
+    every injected mbuf reaches grout's node behind its edge, bit-exact with
+    the oracle, and nothing is freed at the old graph's fini. Without it (the
+    negative control) the held mbufs are freed there -- counted
+    (gpu_fwd4_fini_freed), never handed on."""
+    L = lib()
+    fp = graph_ctx()
+    t = T.config_single_route()
+    load(fp, t)
+    n = 20_000
+    fr, me = S.stream(n, 0xD7A, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
+    _, _, _, want, _ = oracle.Oracle(t).process_mbufs(fr, me, lines_only=True, burst=BURST)
+    walks = 100  # 64 full bursts fill a batch (sent), 36 more are held
+    assert L.gpu_fwd4_set_batch(BATCH, 10_000_000_000) == 0  # no age flush: they stay held
+    try:
+        assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, n) == 0
+        r = _reload(walks, drain)
+        assert r["held"] == walks * BURST - BATCH, r
+        if drain:
+            assert r["left"] == 0 and r["fini_freed"] == 0, r
+            assert r["recorded"] == walks * BURST, r  # all through grout's nodes before the switch
+        else:
+            assert r["fini_freed"] >= r["held"], r
+        w = L.gh_run(1 << 15)  # the new graph goes on with the stream
+        assert (w > 0) if drain else (w < 0), w
+        out = np.zeros(n, dtype=OUT_DT)
+        lines = np.zeros((n, abi.LINE), dtype=np.uint8)
+        assert L.gh_results(out.ctypes.data, lines.ctypes.data) == n
+    finally:
+        assert L.gpu_fwd4_set_batch(BATCH, DELAY_NS) == 0
+        _reload(0, 1)  # back to a graph in slot 0 for the other tests
+        assert L.gh_graph_use(0) == 0
+        _gh["state"]["key"] = None
+    reached = out["edge"] != 0xFF
+    if drain:
+        assert reached.all()
+    else:
+        assert (~reached).sum() == r["fini_freed"], (int((~reached).sum()), r)
+    for f in ("edge", "pkt_len", "data_len", "data_off", "iface", "nh"):
+        assert np.array_equal(out[f][reached], want[f][reached]), f
+    assert (out["edge"][reached] == abi.EDGE["port_output"]).all()
