@@ -1024,6 +1024,28 @@ static int standalone(gr_fib6_t *f, uint32_t n, uint32_t *enc) {
 	return 0;
 }
 
+// A build that stopped part way (no room for a group, a run or a skip, or no
+// memory) has materialised some of the dirty paths and not others, and the
+// nodes it re-owned may have left slots that entries it did not rewrite still
+// name. Nothing of it is published (the commit fails), and the next build
+// redoes all of it: every live node and every first-level entry dirty, the
+// whole image to upload. Routes deleted meanwhile free the room it lacked.
+static int dirty_all(gr_fib6_t *f) {
+	for (uint32_t n = 0; n < f->n_nodes_hw; n++) {
+		struct node *x = &f->nodes[n];
+		if (!x->live || x->dirty)
+			continue;
+		x->dirty = 1;
+		if (vpush(&f->dirty_nodes[x->pos], n) < 0)
+			return -ENOMEM;
+	}
+	for (uint32_t t = 0; t < GR_FIB6_TOP; t++)
+		if (touch_top(f, t) < 0)
+			return -ENOMEM;
+	f->all_dirty = true;
+	return 0;
+}
+
 int gr_fib6_build(gr_fib6_t *f) {
 	if (f == NULL)
 		return -EINVAL;
@@ -1046,6 +1068,10 @@ int gr_fib6_build(gr_fib6_t *f) {
 		r = entry_enc(f, f->ptop[t], &v);
 		if (r == 0)
 			r = put_top(f, t, v);
+	}
+	if (r < 0) { // keep everything dirty: the next build starts over
+		const int e = dirty_all(f);
+		return e < 0 ? e : r;
 	}
 	for (int pos = 2; pos < 16; pos++) {
 		struct u32vec *dl = &f->dirty_nodes[pos];

@@ -261,6 +261,7 @@ struct gr_hip_ctx {
 	int node_ptrs; // node path: frames in registered memory are handed over by address
 	int tile_order; // 0: workgroup b takes tiles b, b + G, ...; 1: one contiguous run each
 	uint32_t spin_max; // ring waits: polls before giving up (0 = the kernel's default)
+	std::atomic<int> fail_appends{0}; // tests: the next N gr_hip_node_append calls fail (-ENOMEM)
 	int untimed; // measurements: no HIP events around launches (gr_hip_queue_kernel_ms sees none)
 	uint32_t time_every; // HIP events around every N-th submit of a queue only (0, 1 = every one)
 	std::vector<host_range> hregs; // registered host memory, by host address
@@ -2047,6 +2048,10 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		c->time_every = (uint32_t)value;
 		for (gr_hip_queue *q : c->queues) // the sampling restarts: submits 0, N, 2N ... from now
 			q->n_submit = 0;
+	} else if (strcmp(key, "fail_appends") == 0) { // tests: the node's staging failure path
+		if (value < 0)
+			return -EINVAL;
+		c->fail_appends.store(value);
 	} else if (strcmp(key, "spin_max") == 0) { // tests: make ring waits give up early
 		if (value < 0)
 			return -EINVAL;
@@ -2446,6 +2451,8 @@ extern "C" int gr_hip_node_append(gr_hip_queue_t *q, const struct gr_hip_mbuf *m
 	}
 	if (n == 0)
 		return (int)w.p;
+	if (q->ctx->fail_appends.load(std::memory_order_relaxed) > 0 && q->ctx->fail_appends.fetch_sub(1) > 0)
+		return -ENOMEM; // as a failed slot_grow: the slot is left as it was
 	uint64_t t_prof = prof_now();
 	if (w.pos.size() < (size_t)w.na + n)
 		w.pos.resize(std::max<size_t>((size_t)w.na + n, 2 * w.pos.size()));

@@ -284,6 +284,7 @@ struct gpu_walk {
 	uint32_t node_id[GR_HIP_NODE_COUNT]; // rte_graph ids of the replaced nodes
 	struct gr_hip_iface_stats *ifs; // gpu_fwd4_stats_flush's buffer [conf.max_ifaces]
 	uint64_t gpu_errors; // batches punted because the GPU call failed
+	uint64_t append_errors; // graph walks punted because they could not be staged
 	uint64_t batches, max_batch, stale;
 	int rx_seen; // the node took packets since the flush node last ran
 	int draining; // gpu_fwd4_drain: hand everything back within the walk
@@ -613,10 +614,17 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 		};
 		walk = 0;
 	}
-	// stage this walk now, while its mbufs and frames are in cache (a failure
-	// makes the send refuse the batch: grout's CPU nodes take it, untouched)
-	if (w->n > n0)
-		gr_hip_node_append(w->q, &w->v[w->cur][n0], w->n - n0, WALK_SPLIT);
+	// stage this walk now, while its mbufs and frames are in cache. A walk
+	// that cannot be staged (no pinned memory for the slot ...; the append
+	// leaves the slot as it was) goes to grout's CPU nodes now, untouched and
+	// counted; the walks before it stay in the batch.
+	if (w->n > n0 && gr_hip_node_append(w->q, &w->v[w->cur][n0], w->n - n0, WALK_SPLIT) < 0) {
+		rte_node_enqueue(graph, node, GR_HIP_E_PUNT, (void **)&w->mbufs[w->cur][n0], (uint16_t)(w->n - n0));
+		w->append_errors++;
+		w->n = n0;
+		if (n0 == 0)
+			reader_handed_back(w, w->cur); // the batch this walk would have started
+	}
 	PROF_ADD(GPU_FWD4_PROF_ACCUMULATE);
 	if (w->n == 0) {
 		reap(graph, node, w);
@@ -876,6 +884,7 @@ int gpu_fwd4_walk_info(const struct rte_graph *graph, struct gpu_fwd4_walk_info 
 	for (int r = 0; r < GPU_FWD4_RCU_PER_GRAPH; r++)
 		info->readers_online += w->rstate[r] != RD_FREE;
 	info->diverged = gpus[w->gpu].diverged;
+	info->append_errors = w->append_errors;
 	return 0;
 }
 

@@ -180,6 +180,7 @@ struct gpu_fwd4_walk_info {
 	uint64_t stale; // packets whose iface / nexthop was gone at hand-back (dropped)
 	uint32_t readers_online; // the graph's QSBR readers online
 	int diverged; // its GPU's mirrors are out of step: everything goes to grout's CPU nodes
+	uint64_t append_errors; // graph walks that could not be staged, punted to grout's CPU nodes
 };
 int gpu_fwd4_walk_info(const struct rte_graph *, struct gpu_fwd4_walk_info *);
 // Tests only: 0 = the node takes no QSBR reader (round 2's behaviour, to

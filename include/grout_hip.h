@@ -477,6 +477,8 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //   "untimed"   1 = no events at all
 //   "spin_max"  polls before a ring wait gives up (0 = default, ~0.4 s):
 //               for tests of the give-up path
+//   "fail_appends" N: the next N gr_hip_node_append calls fail with -ENOMEM
+//               (the slot left as it was): for tests of the node's path
 //   "tile_order" 0 = workgroup b takes 64-packet tiles b, b + G, b + 2G ...
 //               (default), 1 = one contiguous run of tiles per workgroup
 //   "fib_format_of" (read) the format VRF `value`'s FIB is on the device in

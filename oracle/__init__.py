@@ -46,7 +46,7 @@ API = {
     "or_lpm6_brute": (_U32, [_P, _U16, _U16, _P]),
     "or_process": (_I, [_P, _P, _U32, _P, _U32, _P, _U32, _P, _P, _U32]),
     "or_process_ex": (_I, [_P, _P, _U32, _P, _U32, _P, _U32, _P, _P, _U32, _P, _P]),
-    "or_bench": (ctypes.c_double, [_P, _P, _U32, _P, _U32, _I, _U64, ctypes.POINTER(_U64)]),
+    "or_bench": (ctypes.c_double, [_P, _P, _U32, _P, _U32, _I, _U64, _U32, ctypes.POINTER(_U64)]),
 }
 
 OR_F_MBUF_WALKS = 0x80000000  # oracle.h
@@ -175,9 +175,13 @@ class Oracle:
                                                   ns.ctypes.data))
         return out, v, st, mb, ns[0]
 
-    def bench(self, frames, meta, threads, pkts_per_thread):
+    def bench(self, frames, meta, threads, pkts_per_thread, fib_copy=True):
+        """or_bench (oracle.h): aggregate Mpps of `threads` pinned workers after
+        a warm-up pass each; fib_copy: each its own IPv4 FIB copy on THP."""
         fwd = ctypes.c_uint64()
         stride = frames.shape[1]
         mpps = self.L.or_bench(self.h, frames.ctypes.data, stride, meta.ctypes.data, len(meta), threads,
-                               pkts_per_thread, ctypes.byref(fwd))
+                               pkts_per_thread, 1 if fib_copy else 0, ctypes.byref(fwd))
+        if mpps < 0:
+            raise MemoryError("or_bench")
         return mpps, fwd.value

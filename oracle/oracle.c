@@ -1441,11 +1441,95 @@ struct bench_arg {
 	uint32_t stride;
 	const struct gr_hip_pkt_meta *meta;
 	uint32_t n;
+	uint32_t start; // this worker's first packet of the sample
 	uint64_t todo;
 	uint64_t forwarded;
+	uint32_t flags;
 	int cpu;
-	pthread_barrier_t *bar;
+	int err;
+	pthread_barrier_t *ready, *go;
 };
+
+// 2 MiB-aligned anonymous memory advised onto transparent huge pages (grout's
+// rte_fib lives in EAL hugepages); *map / *len: what to munmap.
+static void *thp_alloc(size_t bytes, void **map, size_t *len) {
+	const size_t huge = (size_t)2 << 20;
+	*len = ((bytes + huge - 1) & ~(huge - 1)) + huge;
+	*map = mmap(NULL, *len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+	if (*map == MAP_FAILED)
+		return NULL;
+	void *a = (void *)(((uintptr_t)*map + huge - 1) & ~(uintptr_t)(huge - 1));
+	madvise(a, *len - (size_t)((uint8_t *)a - (uint8_t *)*map), MADV_HUGEPAGE);
+	return a;
+}
+
+// A worker's own copy of the IPv4 FIBs (tbl24 on THP, tbl8), written by the
+// worker itself so that its pages are on its NUMA node; the
+// rest of the topology (ifaces, nexthops, reta, the IPv6 RIB) is shared,
+// read-only.
+struct fib_copies {
+	or_topo_t t;
+	void *maps[GR_HIP_MAX_IFACES];
+	size_t lens[GR_HIP_MAX_IFACES];
+};
+
+static struct fib_copies *fib_copy(const or_topo_t *src) {
+	struct fib_copies *c = calloc(1, sizeof(*c));
+	if (c == NULL)
+		return NULL;
+	c->t = *src;
+	c->t.fibs = calloc(src->max_ifaces, sizeof(struct or_fib));
+	if (c->t.fibs == NULL) {
+		free(c);
+		return NULL;
+	}
+	memcpy(c->t.fibs, src->fibs, src->max_ifaces * sizeof(struct or_fib));
+	for (uint32_t v = 0; v < src->max_ifaces && v < GR_HIP_MAX_IFACES; v++) {
+		const struct or_fib *f = &src->fibs[v];
+		struct or_fib *d = &c->t.fibs[v];
+		d->tbl24 = NULL;
+		d->tbl8 = NULL;
+		if (f->tbl24 != NULL && (d->tbl24 = thp_alloc((size_t)8 << 24, &c->maps[v], &c->lens[v])) != NULL)
+			memcpy(d->tbl24, f->tbl24, (size_t)8 << 24);
+		if (f->tbl8 != NULL && f->num_tbl8 && (d->tbl8 = malloc((size_t)f->num_tbl8 * 256 * 8)) != NULL)
+			memcpy(d->tbl8, f->tbl8, (size_t)f->num_tbl8 * 256 * 8);
+		if ((f->tbl24 != NULL && d->tbl24 == NULL) || (f->tbl8 != NULL && f->num_tbl8 && d->tbl8 == NULL))
+			d->exists = false; // no memory: never looked up (the worker reports it)
+	}
+	return c;
+}
+
+static void fib_copies_free(struct fib_copies *c) {
+	if (c == NULL)
+		return;
+	for (uint32_t v = 0; v < c->t.max_ifaces && v < GR_HIP_MAX_IFACES; v++) {
+		if (c->maps[v] != NULL && c->maps[v] != MAP_FAILED)
+			munmap(c->maps[v], c->lens[v]);
+		free(c->t.fibs[v].tbl8);
+	}
+	free(c->t.fibs);
+	free(c);
+}
+
+// Bursts of OR_BURST from the sample, from `pos` on, wrapping; returns the
+// packets forwarded (port_tx stand-in: net_null).
+static uint64_t bench_run(struct or_graph *g, struct or_mbuf *mb, struct or_mbuf **objs, const struct bench_arg *a,
+			  uint32_t *pos, uint64_t todo) {
+	uint64_t done = 0, fwd = 0;
+	while (done < todo) {
+		for (uint16_t i = 0; i < OR_BURST; i++) {
+			rx_fill(&mb[i], a->frames + (size_t)*pos * a->stride, GR_HIP_LINE, &a->meta[*pos]);
+			objs[i] = &mb[i];
+			if (++*pos == a->n)
+				*pos = 0;
+		}
+		graph_walk(g, objs, OR_BURST);
+		for (uint16_t i = 0; i < OR_BURST; i++)
+			fwd += mb[i].edge == GR_HIP_E_PORT_OUTPUT;
+		done += OR_BURST;
+	}
+	return fwd;
+}
 
 static void *bench_thread(void *p) {
 	struct bench_arg *a = p;
@@ -1455,6 +1539,9 @@ static void *bench_thread(void *p) {
 		CPU_SET(a->cpu, &set);
 		pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
 	}
+	struct fib_copies *own = (a->flags & OR_BENCH_FIB_COPY) ? fib_copy(a->t) : NULL;
+	if ((a->flags & OR_BENCH_FIB_COPY) && own == NULL)
+		a->err = -ENOMEM;
 	// mbuf pool of the worker: OR_BURST mbufs re-filled by the rx stand-in
 	// (the NIC DMA of a ring PMD: the 64-byte header line lands in the mbuf)
 	struct or_mbuf mb[OR_BURST];
@@ -1463,26 +1550,16 @@ static void *bench_thread(void *p) {
 	memset(bufs, 0, (size_t)OR_BURST * OR_DATAROOM);
 	for (int i = 0; i < OR_BURST; i++)
 		mb[i].buf = bufs + (size_t)i * OR_DATAROOM;
-	struct or_graph g = {.t = a->t, .flags = 0, .readable = GR_HIP_LINE};
-	uint64_t done = 0, fwd = 0;
-	uint32_t pos = 0;
-	pthread_barrier_wait(a->bar);
-	while (done < a->todo) {
-		uint16_t k = OR_BURST;
-		for (uint16_t i = 0; i < k; i++) {
-			const struct gr_hip_pkt_meta *md = &a->meta[pos];
-			rx_fill(&mb[i], a->frames + (size_t)pos * a->stride, GR_HIP_LINE, md);
-			objs[i] = &mb[i];
-			if (++pos == a->n)
-				pos = 0;
-		}
-		graph_walk(&g, objs, k);
-		for (uint16_t i = 0; i < k; i++) // port_tx stand-in (net_null)
-			fwd += mb[i].edge == GR_HIP_E_PORT_OUTPUT;
-		done += k;
-	}
-	a->forwarded = fwd;
+	struct or_graph g = {.t = own != NULL ? &own->t : a->t, .flags = 0, .readable = GR_HIP_LINE};
+	// warm-up, untimed: one pass over the whole sample from this worker's
+	// offset (its FIB pages, the nexthops and the sample in its caches / TLB)
+	uint32_t pos = a->start;
+	bench_run(&g, mb, objs, a, &pos, a->n);
+	pthread_barrier_wait(a->ready);
+	pthread_barrier_wait(a->go);
+	a->forwarded = bench_run(&g, mb, objs, a, &pos, a->todo);
 	free(bufs);
+	fib_copies_free(own);
 	return NULL;
 }
 
@@ -1494,14 +1571,16 @@ double or_bench(
 	uint32_t n,
 	int threads,
 	uint64_t pkts_per_thread,
+	uint32_t flags,
 	uint64_t *forwarded
 ) {
 	if (threads < 1 || n == 0)
 		return -1.0;
 	pthread_t th[threads];
 	struct bench_arg args[threads];
-	pthread_barrier_t bar;
-	pthread_barrier_init(&bar, NULL, (unsigned)threads + 1);
+	pthread_barrier_t ready, go;
+	pthread_barrier_init(&ready, NULL, (unsigned)threads + 1);
+	pthread_barrier_init(&go, NULL, (unsigned)threads + 1);
 	int ncpu = (int)sysconf(_SC_NPROCESSORS_ONLN);
 	for (int i = 0; i < threads; i++) {
 		args[i] = (struct bench_arg) {
@@ -1510,25 +1589,33 @@ double or_bench(
 			.stride = in_stride,
 			.meta = meta,
 			.n = n,
-			.todo = pkts_per_thread,
+			.start = (uint32_t)((uint64_t)i * n / (uint64_t)threads), // each worker its own part first
+			.todo = (pkts_per_thread + OR_BURST - 1) / OR_BURST * OR_BURST,
+			.flags = flags,
 			.cpu = threads <= ncpu ? i : -1,
-			.bar = &bar,
+			.ready = &ready,
+			.go = &go,
 		};
-		// each worker starts at its own offset of the stream
 		pthread_create(&th[i], NULL, bench_thread, &args[i]);
 	}
 	struct timespec t0, t1;
-	pthread_barrier_wait(&bar);
+	pthread_barrier_wait(&ready); // every worker has its FIB copy and is warm
 	clock_gettime(CLOCK_MONOTONIC, &t0);
+	pthread_barrier_wait(&go);
 	uint64_t fwd = 0;
+	int err = 0;
 	for (int i = 0; i < threads; i++) {
 		pthread_join(th[i], NULL);
 		fwd += args[i].forwarded;
+		err |= args[i].err;
 	}
 	clock_gettime(CLOCK_MONOTONIC, &t1);
-	pthread_barrier_destroy(&bar);
+	pthread_barrier_destroy(&ready);
+	pthread_barrier_destroy(&go);
 	if (forwarded)
 		*forwarded = fwd;
+	if (err)
+		return -1.0;
 	double s = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
-	return (double)pkts_per_thread * threads / s / 1e6;
+	return (double)args[0].todo * threads / s / 1e6;
 }

@@ -118,9 +118,15 @@ int or_process_ex(
 	struct gr_hip_node_stats *ns
 );
 
-// CPU baseline: `threads` pthreads, each walks its own copy of the packet
-// stream in bursts of 64 until it has processed `pkts_per_thread` packets.
-// Returns the aggregate Mpps (wall clock, CLOCK_MONOTONIC).
+// CPU baseline: `threads` pthreads, one per core, pinned.
+// Worker i starts at packet i * n / threads of the sample and walks it in
+// bursts of 64, wrapping. Each first makes its own copy of the IPv4 FIBs on
+// transparent huge pages (OR_BENCH_FIB_COPY; else all share the topology's,
+// as grout's workers share one rte_fib per VRF) and warms up with one
+// untimed pass over the whole sample; then all start together and each
+// processes pkts_per_thread packets (rounded up to bursts). Returns the
+// aggregate Mpps over the timed part (CLOCK_MONOTONIC), -1 on error.
+#define OR_BENCH_FIB_COPY 0x1
 double or_bench(
 	or_topo_t *,
 	const void *in_frames,
@@ -129,6 +135,7 @@ double or_bench(
 	uint32_t n,
 	int threads,
 	uint64_t pkts_per_thread,
+	uint32_t flags,
 	uint64_t *forwarded
 );
 

@@ -92,8 +92,8 @@ def lib():
 
 
 WALK_INFO_DT = np.dtype([("held", "<u4"), ("in_flight", "<u4"), ("batches", "<u8"), ("max_batch", "<u8"),
-                         ("stale", "<u8"), ("readers_online", "<u4"), ("diverged", "<i4")])
-assert WALK_INFO_DT.itemsize == 40
+                         ("stale", "<u8"), ("readers_online", "<u4"), ("diverged", "<i4"), ("append_errors", "<u8")])
+assert WALK_INFO_DT.itemsize == 48
 RCU_RES_DT = np.dtype([("sync_before_handback", "<u4"), ("recorded_at_sync", "<u4"), ("freed_reads", "<u4"),
                        ("recorded", "<u4"), ("stale", "<u8"), ("sync_us", "<u8"), ("walks", "<u4"),
                        ("sync_done", "<u4")])
@@ -855,3 +855,34 @@ def test_graph_reload_mid_stream(drain):
     for f in ("edge", "pkt_len", "data_len", "data_off", "iface", "nh"):
         assert np.array_equal(out[f][reached], want[f][reached]), f
     assert (out["edge"][reached] == abi.EDGE["port_output"]).all()
+
+
+@pytest.mark.gpu
+def test_graph_walk_append_failure_punts_one_walk():
+    """A graph walk the node cannot stage (gr_hip_node_append fails, e.g. no
+    pinned memory to grow the walk slot; the slot is left as it was) goes to
+    grout's CPU nodes at once (iface_input_cpu), untouched, and is counted
+    (walk_info append_errors). The batch keeps the walks before and after
+    it, which forward bit-exact with the oracle (the whole batch
+    used to be refused at send)."""
+    L = lib()
+    fp = graph_ctx()
+    t = T.config_single_route()
+    load(fp, t)
+    fr, me = S.stream(3000, 0xA9F, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
+    _, _, _, want, _ = oracle.Oracle(t).process_mbufs(fr, me, lines_only=True, burst=BURST)
+    i0 = walk_info()
+    L.gpu_fwd4_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    assert L.gpu_fwd4_tune(b"fail_appends", 1) == 0  # the next append of each context fails
+    try:
+        got, lines, _, _ = walk(fr, me)
+    finally:
+        assert L.gpu_fwd4_tune(b"fail_appends", 0) == 0
+    assert walk_info()["append_errors"] - i0["append_errors"] == 1
+    punt = got["edge"] == abi.EDGE["punt"]
+    assert punt[:BURST].all() and punt.sum() == BURST  # the first walk, whole
+    assert (got["data_off"][punt] == 128).all() and (got["pkt_len"][punt] == me["pkt_len"][punt]).all()
+    assert (lines[punt] == fr[punt, :abi.LINE]).all()  # frames untouched
+    for f in ("edge", "pkt_len", "data_len", "data_off", "iface", "nh"):
+        assert np.array_equal(got[f][~punt], want[f][~punt]), f

@@ -50,6 +50,9 @@ def test_datapath_patch_names_the_node_api():
     assert re.search(r"\n \s*rte_graph_cluster_stats_get\(ctx\.stats, false\);\n\+\s*gpu_fwd4_stats_flush\(graph, "
                      r"rte_lcore_id\(\), gpu_node_stats, &ctx\);", text)
     assert "RTE_MAX_LCORE + GPU_FWD4_RCU_READERS" in added
+    # the node is drained before the worker leaves its graph (reconfiguration, shutdown)
+    assert re.search(r"if \(atomic_load\(&w->shutdown\) \|\| atomic_load\(&w->next_config\) != cur\) \{\n"
+                     r"(\+[^\n]*\n)*\+\s*gpu_fwd4_drain\(graph\);\n \s*worker_active_dec\(\);", text)
 
 
 def _added(name):

@@ -663,3 +663,46 @@ def test_fib6_incremental_publication(view):
             assert len(d[1]) < 0.05 * len(slots), (len(d[1]), len(slots))
         _fib6_check(host, f, r[live], rng, 3000)
     host.gr_fib6_free(f)
+
+
+def test_fib6_build_recovers_from_enospc():
+    """A build that runs out of group slots part way (fib6.c)
+    publishes nothing and leaves the trie to be built again whole: once
+    routes are deleted, the next build succeeds and every lookup equals the
+    RIB's longest match again."""
+    host = abi.host()
+    rng = np.random.default_rng(0xF6E)
+    max_groups = 48
+    f = host.gr_fib6_new(4096, max_groups)
+    routes = []
+    failed = False
+    for i in range(400):  # /40s under distinct first-level entries: each needs groups
+        a = np.zeros(16, dtype=np.uint8)
+        a[0], a[1] = 0x20, 0x01
+        a[2:5] = rng.integers(0, 256, 3, dtype=np.uint8)
+        a[2] = i % 256
+        plen = int(rng.choice([40, 48, 56, 64]))
+        ip = np.ascontiguousarray(a)
+        if host.gr_fib6_add(f, ip.ctypes.data, plen, 1 + i % 7, 0) != 0:
+            continue
+        routes.append((ip, plen))
+        if i % 8 == 7:
+            r = host.gr_fib6_build(f)
+            if r < 0:
+                assert r == -28, r  # -ENOSPC
+                failed = True
+                break
+    assert failed, "the trie never ran out of groups"
+    assert host.gr_fib6_build(f) == -28  # still no room: every path is redone, and fails again
+    # delete routes until it fits
+    while True:
+        ip, plen = routes.pop()
+        assert host.gr_fib6_del(f, ip.ctypes.data, plen) == 0
+        if len(routes) % 4 == 0 and host.gr_fib6_build(f) == 0:
+            break
+    r = np.zeros(len(routes), dtype=abi.ROUTE6_DT)
+    for k, (ip, plen) in enumerate(routes):
+        r[k]["ip"] = ip
+        r[k]["prefixlen"] = plen
+    _fib6_check(host, f, r, rng, 20_000)
+    host.gr_fib6_free(f)
