@@ -1057,7 +1057,7 @@ struct gh_reload_result {
 	uint32_t recorded; // mbufs through grout's nodes when the old graph was destroyed
 	uint64_t fini_freed; // mbufs the old graph's fini freed
 	int32_t graph; // the new current graph
-	uint32_t _pad;
+	uint32_t rx; // mbufs port_rx had delivered by then
 };
 
 // grout's reconfiguration of a worker (worker_graph_reload, graph.c:263-290;
@@ -1080,6 +1080,7 @@ int gh_reload_test(uint32_t walks, int drain, struct gh_reload_result *res) {
 	res->left = drain ? gpu_fwd4_drain(H.graphs[k].graph) : -1;
 	housekeeping(k);
 	res->recorded = __atomic_load_n(&H.recorded, __ATOMIC_ACQUIRE);
+	res->rx = H.next_rx;
 	unsigned index = 0;
 	sscanf(H.graphs[k].name, "gr-%x", &index);
 	const int nk = graph_create(index >> 1, (index & 1) ^ 1, 0);
