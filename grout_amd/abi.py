@@ -196,6 +196,7 @@ HIP_API = {
     "gr_hip_node_process": (_I, [_P, _P, _U32, _U32, _P]),
     "gr_hip_node_start": (_I, [_P, _P, _U32, _U32]),
     "gr_hip_node_finish": (_I, [_P, _P, _P, _P]),
+    "gr_hip_node_finish_mbufs": (_I, [_P, _P, _P, _P, _P, _P]),
     "gr_hip_node_pending": (_I, [_P, _P]),
     "gr_hip_node_iface_stats": (_I, [_P, _P, _U32, _I]),
     "gr_hip_node_prof": (_I, [_P, _U32, _I]),

@@ -2593,8 +2593,8 @@ extern "C" int gr_hip_node_start(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint3
 	return gr_hip_node_send(q, m, n, burst);
 }
 
-extern "C" int gr_hip_node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np,
-				  struct gr_hip_node_stats *stats) {
+static int node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np, struct gr_hip_node_stats *stats,
+		       struct gr_node_direct *direct) {
 	if (q == nullptr)
 		return -EINVAL;
 	if (q->nw_count == 0)
@@ -2632,10 +2632,26 @@ extern "C" int gr_hip_node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, ui
 		const gr_node_vlans vl = {c->vlan_keys_h.data(), c->vlan_vals_h.data(), (uint32_t)c->vlan_keys_h.size()};
 		r = gr_node_apply_ex(w.m, w.n, w.burst, w.pos.data(), w.by_addr ? nullptr : w.out, GR_HIP_PREFIX, w.v,
 				     c->ifaces.data(), c->max_ifaces, c->nh.data(), (uint32_t)c->nh.size(), stats, &vl,
-				     q->node_if.data(), (uint32_t)q->node_if.size());
+				     q->node_if.data(), (uint32_t)q->node_if.size(), direct);
 	}
 	node_prof_ns[GR_HIP_NODE_PROF_FIN_APPLY] += prof_now() - t_prof;
 	return r < 0 ? r : (int)unfinished;
+}
+
+extern "C" int gr_hip_node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np,
+				  struct gr_hip_node_stats *stats) {
+	return node_finish(q, mp, np, stats, nullptr);
+}
+
+extern "C" int gr_hip_node_finish_mbufs(gr_hip_queue_t *q, void *const *mbufs, const struct gr_hip_mbuf_layout *layout,
+					uint8_t *edges, uint32_t *stale, struct gr_hip_node_stats *stats) {
+	if (mbufs == nullptr || layout == nullptr || edges == nullptr)
+		return -EINVAL;
+	gr_node_direct d = {mbufs, layout, edges, 0};
+	const int r = node_finish(q, nullptr, nullptr, stats, &d);
+	if (stale != nullptr)
+		*stale = d.stale;
+	return r;
 }
 
 extern "C" int gr_hip_node_iface_stats(gr_hip_queue_t *q, struct gr_hip_iface_stats *st, uint32_t max, int reset) {

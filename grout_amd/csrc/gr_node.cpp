@@ -284,6 +284,64 @@ static inline void count(struct gr_hip_iface_stats *st, uint32_t n_st, uint32_t 
 	}
 }
 
+static inline void prefetch_for_apply(const struct gr_hip_mbuf *m, uint32_t i, const struct gr_node_direct *d) {
+	__builtin_prefetch(m[i].frame, 1, 0);
+	if (d != nullptr) {
+		const uint8_t *mb = static_cast<const uint8_t *>(d->mbufs[i]);
+		__builtin_prefetch(mb, 1, 0); // data_off .. packet_type: the mbuf's first line
+		__builtin_prefetch(mb + d->lay->priv, 1, 0); // the private data
+	}
+}
+
+template <typename T> static inline void put(uint8_t *base, uint16_t off, T v) {
+	memcpy(base + off, &v, sizeof(v));
+}
+
+static inline const void *reg_get(const void *const *reg, uint32_t n, uint32_t id) {
+	return id < n && reg != nullptr ? __atomic_load_n(&reg[id], __ATOMIC_ACQUIRE) : nullptr;
+}
+
+// One packet's hand-back onto its mbuf (the grout node's private data for
+// the node behind its edge); returns the edge.
+static inline uint8_t to_mbuf(struct gr_node_direct *d, uint32_t i, const struct gr_hip_mbuf &b,
+			      const struct gr_hip_verdict &v, int node) {
+	if (v.edge == GR_HIP_E_PUNT)
+		return GR_HIP_E_PUNT; // grout's CPU iface_input takes it as port_rx left it
+	const struct gr_hip_mbuf_layout &L = *d->lay;
+	const void *ifp = reg_get(L.ifaces, L.n_ifaces, v.iface);
+	const void *nhp = nullptr;
+	if ((ifp == nullptr && v.iface != 0)
+	    || (node != GR_HIP_NODE_IFACE_INPUT && node != GR_HIP_NODE_IFACE_OUTPUT && v.nh != 0
+		&& (nhp = reg_get(L.nh, L.n_nh, v.nh)) == nullptr)) {
+		d->stale++; // an object grout freed: the mbuf stays as it was, a drop node takes it
+		return GR_HIP_E_IP_OUTPUT_ERROR;
+	}
+	uint8_t *mb = static_cast<uint8_t *>(d->mbufs[i]);
+	put<uint16_t>(mb, L.data_off, b.data_off);
+	put<uint16_t>(mb, L.data_len, b.data_len);
+	put<uint32_t>(mb, L.pkt_len, b.pkt_len);
+	put<uint32_t>(mb, L.packet_type, b.packet_type);
+	uint8_t *priv = mb + L.priv;
+	put<const void *>(priv, L.priv_iface, ifp);
+	switch (node) {
+	case GR_HIP_NODE_IFACE_INPUT:
+	case GR_HIP_NODE_IFACE_OUTPUT:
+		put<uint16_t>(priv, L.priv_vlan_id, b.vlan_id);
+		break;
+	case GR_HIP_NODE_ETH_OUTPUT:
+		if (v.nh)
+			put<const void *>(priv, L.priv_l3_nh, nhp);
+		break;
+	default:
+		put<uint32_t>(priv, L.priv_domain, b.domain);
+		put<const void *>(priv, L.priv_eth_nh, nullptr);
+		if (v.nh)
+			put<const void *>(priv, L.priv_l3_nh, nhp);
+		break;
+	}
+	return v.edge;
+}
+
 extern "C" int gr_hip_node_apply(
 	struct gr_hip_mbuf *m,
 	uint32_t n,
@@ -299,7 +357,7 @@ extern "C" int gr_hip_node_apply(
 	struct gr_hip_node_stats *stats
 ) {
 	return gr_node_apply_ex(m, n, burst, pos, lines, line_stride, verdicts, ifaces, n_ifaces, nh, n_nh, stats,
-				nullptr, nullptr, 0);
+				nullptr, nullptr, 0, nullptr);
 }
 
 extern "C" int gr_node_apply_ex(
@@ -317,10 +375,13 @@ extern "C" int gr_node_apply_ex(
 	struct gr_hip_node_stats *stats,
 	const struct gr_node_vlans *vlans,
 	struct gr_hip_iface_stats *ifst,
-	uint32_t n_ifst
+	uint32_t n_ifst,
+	struct gr_node_direct *direct
 ) {
 	if (n == 0)
 		return 0;
+	if (direct != nullptr && (direct->mbufs == nullptr || direct->lay == nullptr || direct->edges == nullptr))
+		return -EINVAL;
 	if (m == nullptr || verdicts == nullptr || (lines != nullptr && line_stride < GR_HIP_PREFIX))
 		return -EINVAL;
 	burst = walk_burst(burst);
@@ -347,11 +408,15 @@ extern "C" int gr_node_apply_ex(
 	// is bound by their cache misses
 	constexpr uint32_t AHEAD = 16;
 	for (uint32_t i = 0; i < n && i < AHEAD; i++)
-		__builtin_prefetch(m[i].frame, 1, 0);
+		prefetch_for_apply(m, i, direct);
 	for (uint32_t i = 0; i < n; i++) {
 		if (i + AHEAD < n)
-			__builtin_prefetch(m[i + AHEAD].frame, 1, 0);
-		struct gr_hip_mbuf &b = m[i];
+			prefetch_for_apply(m, i + AHEAD, direct);
+		// direct: the view is only read, the mbuf gets the result below
+		struct gr_hip_mbuf copy;
+		if (direct != nullptr)
+			copy = m[i];
+		struct gr_hip_mbuf &b = direct != nullptr ? copy : m[i];
 		const uint32_t at = pos != nullptr ? pos[i] : i;
 		const struct gr_hip_verdict &v = verdicts[at];
 		const uint32_t len0 = b.pkt_len; // as iface_input / iface_output count it
@@ -434,6 +499,8 @@ extern "C" int gr_node_apply_ex(
 			b.domain = v.domain;
 			b.nh = v.nh;
 		}
+		if (direct != nullptr)
+			direct->edges[i] = to_mbuf(direct, i, b, v, node);
 		if (i + 1 == n || walk_start(m, i + 1, start, burst)) { // this graph walk ends here
 			if (walk_nomac && i + 1 - start > 64)
 				eth_output_walk(m, start, i + 1, pos, verdicts, fam, ifaces, n_ifaces, nh, n_nh);

@@ -27,8 +27,18 @@ uint64_t gr_node_layout_from(const struct gr_hip_mbuf *m, uint32_t n, uint32_t b
 int gr_node_stage_from(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, const uint32_t *pos, uint32_t next,
 		       void *lines, struct gr_hip_pkt_meta *meta);
 
+// The hand-back straight onto the caller's mbufs (gr_hip_node_finish_mbufs):
+// the views are read, not written; edges[i] and *stale are the outputs.
+struct gr_node_direct {
+	void *const *mbufs;
+	const struct gr_hip_mbuf_layout *lay;
+	uint8_t *edges;
+	uint32_t stale;
+};
+
 // gr_hip_node_apply, also adding each packet's rx / tx to ifst[iface id]
-// (n_ifst entries) where grout's iface_input / iface_output count them.
+// (n_ifst entries) where grout's iface_input / iface_output count them;
+// direct (optional): onto the mbufs instead of the views.
 int gr_node_apply_ex(
 	struct gr_hip_mbuf *m,
 	uint32_t n,
@@ -44,7 +54,8 @@ int gr_node_apply_ex(
 	struct gr_hip_node_stats *stats,
 	const struct gr_node_vlans *vlans,
 	struct gr_hip_iface_stats *ifst,
-	uint32_t n_ifst
+	uint32_t n_ifst,
+	struct gr_node_direct *direct
 );
 
 #ifdef __cplusplus

@@ -59,6 +59,7 @@
 #include "gr_datapath_min.h"
 
 #include <errno.h>
+#include <stddef.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -272,6 +273,7 @@ struct gpu_walk {
 	uint32_t cur;
 	struct rte_mbuf **mbufs[2];
 	struct gr_hip_mbuf *v[2];
+	uint8_t *edges[2]; // each mbuf's edge, as the one-pass hand-back leaves it
 	int pending; // the other buffer's batch is on the GPU (gr_hip_node_start'ed)
 	uint32_t pend_n; // its size
 	uint64_t pend_ns; // when it was sent
@@ -283,6 +285,7 @@ struct gpu_walk {
 	struct gr_hip_node_stats flushed; // what gpu_fwd4_stats_flush reported already
 	uint32_t node_id[GR_HIP_NODE_COUNT]; // rte_graph ids of the replaced nodes
 	struct gr_hip_iface_stats *ifs; // gpu_fwd4_stats_flush's buffer [conf.max_ifaces]
+	struct gr_hip_mbuf_layout lay; // where the hand-back writes in grout's mbufs
 	uint64_t gpu_errors; // batches punted because the GPU call failed
 	uint64_t append_errors; // graph walks punted because they could not be staged
 	uint64_t batches, max_batch, stale;
@@ -385,51 +388,54 @@ static uint8_t ck_status(uint64_t ol_flags) {
 	}
 }
 
-// The private data grout's chain leaves for the node behind `edge`: the iface
-// everywhere; iface_input's vlan_id before eth_input; eth_input's domain and
-// pre-resolved nexthop (NULL), then ip_input's / ip6_input's l3 nexthop over
-// them (l3.h:9 shares the bytes, ip_input.c:156); iface_output's vlan_id for
-// port_output / port_tx (iface_output.c:81-86, port_tx.c:84-118). Returns -1
-// when the iface or nexthop the verdict names is no longer registered (the
-// control plane broke the RCU contract above): the mbuf is then left as it is.
-static int hand_back(struct rte_mbuf *m, const struct gr_hip_mbuf *v) {
-	const struct iface *ifp = gpu_fwd4_iface_obj(v->iface);
-	if (ifp == NULL && v->iface != 0)
-		return -1;
-	const uint8_t *f = v->frame;
-	const int ip6 = f[12] == 0x86 && f[13] == 0xdd;
-	const int node = gr_hip_edge_node(v->edge, v->nh, ip6);
-	const struct nexthop *nh = NULL;
-	if (node != GR_HIP_NODE_IFACE_INPUT && node != GR_HIP_NODE_IFACE_OUTPUT && v->nh != 0
-	    && (nh = gpu_fwd4_nh_obj(v->nh)) == NULL)
-		return -1;
-	m->data_off = v->data_off; // frame bytes were rewritten in place
-	m->data_len = v->data_len;
-	m->pkt_len = v->pkt_len;
-	m->packet_type = v->packet_type;
-	mbuf_data(m)->iface = ifp;
-	switch (node) {
-	case GR_HIP_NODE_IFACE_INPUT:
-	case GR_HIP_NODE_IFACE_OUTPUT:
-		iface_mbuf_data(m)->vlan_id = v->vlan_id;
-		break;
-	case GR_HIP_NODE_ETH_OUTPUT:
-		if (v->nh)
-			l3_mbuf_data(m)->nh = nh;
-		break;
-	default: {
-		struct eth_input_mbuf_data *e = eth_input_mbuf_data(m);
-		e->domain = (eth_domain_t)v->domain;
-		e->nh = NULL;
-		if (v->nh)
-			l3_mbuf_data(m)->nh = nh;
-		break;
-	}
-	}
-	return 0;
+// Where the one-pass hand-back (gr_hip_node_finish_mbufs) writes grout's
+// mbuf fields and the private data grout's chain leaves for the node behind
+// each edge: the iface everywhere; iface_input's vlan_id before eth_input;
+// eth_input's domain and pre-resolved nexthop (NULL), then ip_input's /
+// ip6_input's l3 nexthop over them (l3.h:9 shares the bytes, ip_input.c:156);
+// iface_output's vlan_id for port_output / port_tx (iface_output.c:81-86,
+// port_tx.c:84-118). The verdict's iface id and nexthop slot become pointers
+// through the node's registries (see "RCU" above); a packet whose object is
+// no longer registered (the control plane broke the RCU contract) keeps its
+// mbuf as it was and goes to ip_output_error, counted.
+static void layout_init(struct gr_hip_mbuf_layout *l) {
+	memset(l, 0, sizeof(*l));
+	l->data_off = offsetof(struct rte_mbuf, data_off);
+	l->data_len = offsetof(struct rte_mbuf, data_len);
+	l->pkt_len = offsetof(struct rte_mbuf, pkt_len);
+	l->packet_type = offsetof(struct rte_mbuf, packet_type);
+	l->priv = sizeof(struct rte_mbuf); // rte_mbuf_to_priv
+	l->priv_iface = offsetof(struct mbuf_data, iface);
+	l->priv_vlan_id = offsetof(struct iface_mbuf_data, vlan_id);
+	l->priv_domain = offsetof(struct eth_input_mbuf_data, domain);
+	l->priv_eth_nh = offsetof(struct eth_input_mbuf_data, nh);
+	l->priv_l3_nh = offsetof(struct l3_mbuf_data, nh);
+}
+_Static_assert(sizeof(((struct rte_mbuf *)0)->data_off) == 2 && sizeof(((struct rte_mbuf *)0)->data_len) == 2
+		       && sizeof(((struct rte_mbuf *)0)->pkt_len) == 4 && sizeof(((struct rte_mbuf *)0)->packet_type) == 4
+		       && sizeof(eth_domain_t) == 4,
+	       "the widths gr_hip_mbuf_layout names");
+
+// The registries as they are now (allocated once, at their first set).
+static const struct gr_hip_mbuf_layout *layout_now(struct gpu_walk *w) {
+	w->lay.n_ifaces = __atomic_load_n(&if_obj_n, __ATOMIC_ACQUIRE);
+	w->lay.ifaces = (const void *const *)if_obj;
+	w->lay.n_nh = __atomic_load_n(&nh_obj_n, __ATOMIC_ACQUIRE);
+	w->lay.nh = (const void *const *)nh_obj;
+	return &w->lay;
 }
 
-// Enqueue batch buffer k (n mbufs) on the verdict edges; r: what the GPU call
+// Hand the GPU's oldest batch back onto buffer k's mbufs (one pass: frames,
+// mbuf fields, private data) and return the finish's result.
+static int hand_back(struct gpu_walk *w, uint32_t k) {
+	uint32_t stale = 0;
+	const int r = gr_hip_node_finish_mbufs(w->q, (void *const *)w->mbufs[k], layout_now(w), w->edges[k], &stale,
+					       &w->stats);
+	w->stale += stale;
+	return r;
+}
+
+// Enqueue batch buffer k (n mbufs) on their edges; r: what the GPU call
 // returned (< 0: the GPU could not take them, mbufs untouched: grout's CPU
 // nodes do; > 0: a kernel gave up, the packets it did not reach come back as
 // PUNT with their frames untouched, the others are forwarded as usual).
@@ -437,46 +443,22 @@ static void deliver(struct rte_graph *graph, struct rte_node *node, struct gpu_w
 		    int r) {
 	PROF_T0();
 	struct rte_mbuf **mb = w->mbufs[k];
-	const struct gr_hip_mbuf *v = w->v[k];
 	if (r != 0)
 		w->gpu_errors++;
 	if (r < 0) {
-		for (uint32_t i = 0; i < n; i++)
-			rte_node_enqueue_x1(graph, node, GR_HIP_E_PUNT, mb[i]);
+		rte_node_enqueue(graph, node, GR_HIP_E_PUNT, (void **)mb, (uint16_t)n);
 	} else {
 		// runs of one edge go in one rte_node_enqueue (a forwarded stream is
-		// mostly one run to port_output). hand_back writes each mbuf's first
-		// cache line and its private area and reads its frame's ether type:
-		// the batch was taken in walks long gone, so these lines have left the
-		// core's caches; prefetch them PF_BACK mbufs ahead so that the misses
-		// overlap
-		enum { PF_BACK = 12 };
-		for (uint32_t i = 0; i < n && i < PF_BACK; i++) {
-			rte_prefetch0_write(mb[i]);
-			rte_prefetch0_write(mbuf_data(mb[i]));
-			rte_prefetch0(v[i].frame);
-		}
+		// mostly one run to port_output); a batch is at most
+		// GPU_FWD4_BATCH_MAX < UINT16_MAX
+		const uint8_t *e = w->edges[k];
 		uint32_t run = 0;
-		rte_edge_t re = 0;
-		for (uint32_t i = 0; i < n; i++) {
-			if (i + PF_BACK < n) {
-				rte_prefetch0_write(mb[i + PF_BACK]);
-				rte_prefetch0_write(mbuf_data(mb[i + PF_BACK]));
-				rte_prefetch0(v[i + PF_BACK].frame);
-			}
-			rte_edge_t e = v[i].edge;
-			if (e != GR_HIP_E_PUNT && hand_back(mb[i], &v[i]) < 0) {
-				w->stale++;
-				e = GR_HIP_E_IP_OUTPUT_ERROR; // a drop node (ip_output.c:187)
-			}
-			if (i > run && e != re) { // (a batch is at most GPU_FWD4_BATCH_MAX < UINT16_MAX)
-				rte_node_enqueue(graph, node, re, (void **)&mb[run], (uint16_t)(i - run));
+		for (uint32_t i = 1; i <= n; i++) {
+			if (i == n || e[i] != e[run]) {
+				rte_node_enqueue(graph, node, e[run], (void **)&mb[run], (uint16_t)(i - run));
 				run = i;
 			}
-			re = e;
 		}
-		if (n > run)
-			rte_node_enqueue(graph, node, re, (void **)&mb[run], (uint16_t)(n - run));
 	}
 	reader_handed_back(w, k);
 	PROF_ADD(GPU_FWD4_PROF_DELIVER);
@@ -486,15 +468,11 @@ static void deliver(struct rte_graph *graph, struct rte_node *node, struct gpu_w
 static uint32_t finish_pending(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
 	if (!w->pending)
 		return 0;
-	struct gr_hip_mbuf *vm = NULL;
-	uint32_t n = 0;
+	const uint32_t k = w->cur ^ 1, n = w->pend_n;
 	PROF_T0();
-	const int r = gr_hip_node_finish(w->q, &vm, &n, &w->stats);
+	const int r = hand_back(w, k); // one walk in flight per graph: buffer k's
 	PROF_ADD(GPU_FWD4_PROF_FINISH);
-	const uint32_t k = w->cur ^ 1;
 	w->pending = 0;
-	if (vm != w->v[k]) // cannot happen: one walk in flight per graph, started here
-		return 0;
 	deliver(graph, node, w, k, n, r);
 	return n;
 }
@@ -526,7 +504,7 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 		started(w, n);
 		int r = gr_hip_node_send(w->q, w->v[k], n, WALK_SPLIT);
 		if (r == 0)
-			r = gr_hip_node_finish(w->q, NULL, NULL, &w->stats);
+			r = hand_back(w, k);
 		deliver(graph, node, w, k, n, r);
 		return n;
 	}
@@ -644,6 +622,7 @@ static void walk_free(struct gpu_walk *w) {
 	for (int k = 0; k < 2; k++) {
 		free(w->mbufs[k]);
 		free(w->v[k]);
+		free(w->edges[k]);
 	}
 	free(w->ifs);
 	free(w);
@@ -685,9 +664,11 @@ static int gpu_fwd4_init(const struct rte_graph *graph, struct rte_node *node) {
 	for (int k = 0; k < 2; k++) {
 		w->mbufs[k] = calloc(w->cap, sizeof(*w->mbufs[k]));
 		w->v[k] = calloc(w->cap, sizeof(*w->v[k]));
-		if (w->mbufs[k] == NULL || w->v[k] == NULL)
+		w->edges[k] = calloc(w->cap, 1);
+		if (w->mbufs[k] == NULL || w->v[k] == NULL || w->edges[k] == NULL)
 			r = -ENOMEM;
 	}
+	layout_init(&w->lay);
 	if ((w->ifs = calloc(conf.max_ifaces, sizeof(*w->ifs))) == NULL)
 		r = -ENOMEM;
 	for (int k = 0; k < GR_HIP_NODE_COUNT; k++)

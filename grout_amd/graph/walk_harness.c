@@ -78,7 +78,12 @@ static struct {
 		// (struct worker_stats node_stats, main_loop.c:40-66), by node id,
 		// and the rte_graph counters already folded in
 		uint64_t *w_packets, *w_batches, *prev_packets, *prev_calls;
+		// workers mode (gh_workers_run): this graph's share of the injected
+		// mbufs [rx_next, rx_end) and what reached its recorders
+		uint32_t rx_next, rx_end;
+		uint64_t recorded;
 	} graphs[GH_MAX_GRAPHS];
+	int workers; // gh_workers_run is walking every graph from its own thread
 	uint32_t loop; // walks since the last housekeeping tick (main_loop.c:461)
 	uint8_t *if_dead, *nh_dead; // objects the RCU test's control thread freed
 	uint32_t freed_reads; // grout nodes behind the edges read a freed object
@@ -122,8 +127,14 @@ static uint16_t port_rx_process(struct rte_graph *graph, struct rte_node *node, 
 	(void)nb;
 	uint32_t k = 0;
 	void *burst[RTE_GRAPH_BURST_SIZE];
-	while (k < H.rx_burst && H.next_rx < H.n) {
-		const uint32_t i = H.next_rx++;
+	// workers mode: each graph polls its own part of the mbufs (its RX queue)
+	uint32_t *next = &H.next_rx, end = H.n;
+	if (H.workers && node->ctx[0] != 0) {
+		next = &H.graphs[node->ctx[0] - 1].rx_next;
+		end = H.graphs[node->ctx[0] - 1].rx_end;
+	}
+	while (k < H.rx_burst && *next < end) {
+		const uint32_t i = (*next)++;
 		struct rte_mbuf *m = mbuf_at(i);
 		const struct gr_hip_pkt_meta *pm = &H.meta_in[i];
 		struct iface_mbuf_data *d = iface_mbuf_data(m);
@@ -141,9 +152,19 @@ static uint16_t port_rx_process(struct rte_graph *graph, struct rte_node *node, 
 	return (uint16_t)k;
 }
 
+// ctx[0]: the harness slot of the node's graph + 1 (0: not one of them)
+static int graph_slot_init(const struct rte_graph *graph, struct rte_node *node) {
+	node->ctx[0] = 0;
+	for (int k = 0; k < GH_MAX_GRAPHS; k++)
+		if (strcmp(graph->name, H.graphs[k].name) == 0)
+			node->ctx[0] = (uint8_t)(k + 1);
+	return 0;
+}
+
 static struct rte_node_register port_rx_node = {
 	.name = "port_rx",
 	.flags = RTE_NODE_SOURCE_F,
+	.init = graph_slot_init,
 	.process = port_rx_process,
 	.nb_edges = 1,
 	.next_nodes = {"iface_input"},
@@ -153,6 +174,11 @@ static struct rte_node_register port_rx_node = {
 static uint16_t recorder_process(struct rte_graph *graph, struct rte_node *node, void **objs, uint16_t nb) {
 	(void)graph;
 	const uint8_t id = node->ctx[0];
+	if (H.workers) { // a rate measurement: grout's node behind the edge takes the mbufs, no record
+		if (node->ctx[1] != 0)
+			H.graphs[node->ctx[1] - 1].recorded += nb;
+		return nb;
+	}
 	for (uint16_t k = 0; k < nb; k++) {
 		const size_t off = (uint8_t *)objs[k] - H.mem;
 		const uint32_t i = (uint32_t)(off / GH_MBUF_SZ);
@@ -176,7 +202,8 @@ static uint16_t recorder_process(struct rte_graph *graph, struct rte_node *node,
 }
 
 static int recorder_init(const struct rte_graph *graph, struct rte_node *node) {
-	(void)graph;
+	graph_slot_init(graph, node);
+	node->ctx[1] = node->ctx[0];
 	node->ctx[0] = 0xff;
 	for (uint32_t r = 0; r < H.n_recorders; r++)
 		if (strcmp(H.recorders[r], node->name) == 0)
@@ -401,12 +428,14 @@ static int graph_create(unsigned cpu, unsigned index, int socket) {
 		patterns[2 + i] = replaced[i];
 	struct rte_graph_param prm = {
 		.socket_id = socket, .nb_node_patterns = 2 + N_REPLACED, .node_patterns = patterns};
+	snprintf(H.graphs[k].name, sizeof(H.graphs[k].name), "%s", name); // the nodes' init look it up
 	rte_graph_t gid = rte_graph_create(name, &prm);
-	if (gid == RTE_GRAPH_ID_INVALID)
+	if (gid == RTE_GRAPH_ID_INVALID) {
+		H.graphs[k].name[0] = 0;
 		return -EINVAL;
+	}
 	H.graphs[k].gid = gid;
 	H.graphs[k].graph = rte_graph_lookup(name);
-	snprintf(H.graphs[k].name, sizeof(H.graphs[k].name), "%s", name);
 	const size_t nn = rte_node_max_count() + 1;
 	H.graphs[k].w_packets = calloc(nn, sizeof(uint64_t));
 	H.graphs[k].w_batches = calloc(nn, sizeof(uint64_t));
@@ -420,6 +449,7 @@ static int graph_create(unsigned cpu, unsigned index, int socket) {
 }
 
 static void graph_stats_free(int k) {
+	H.graphs[k].name[0] = 0;
 	free(H.graphs[k].w_packets);
 	free(H.graphs[k].w_batches);
 	free(H.graphs[k].prev_packets);
@@ -1094,4 +1124,80 @@ int gh_reload_test(uint32_t walks, int drain, struct gh_reload_result *res) {
 	H.cur = nk;
 	res->graph = nk;
 	return r;
+}
+
+// ---- several workers, one graph each, on one GPU ----------------------------
+struct gh_workers_arg {
+	int k; // graph slot
+	pthread_barrier_t *bar;
+	uint64_t walks;
+	int err;
+};
+
+static void *worker_thread(void *p) {
+	struct gh_workers_arg *a = p;
+	struct rte_graph *g = H.graphs[a->k].graph;
+	pthread_barrier_wait(a->bar);
+	uint64_t w = 0;
+	const uint64_t want = H.graphs[a->k].rx_end - (H.graphs[a->k].rx_next);
+	for (uint32_t loop = 0; H.graphs[a->k].recorded < want; w++) {
+		rte_graph_walk(g);
+		if (++loop == 256) { // grout's housekeeping tick: the node's statistics fold
+			loop = 0;
+			gpu_fwd4_stats_flush(g, (unsigned)a->k, NULL, NULL); // its own lcore's iface_stats
+		}
+		if (w > (1ull << 32)) {
+			a->err = -ETIMEDOUT;
+			break;
+		}
+	}
+	a->walks = w;
+	pthread_barrier_wait(a->bar);
+	return NULL;
+}
+
+// gr_datapath_loop on `threads` workers at once (worker.c: one graph per
+// worker): graph slots 0 .. threads-1 (gh_graph_create'd), each polling its
+// own contiguous share of the injected mbufs, each walked from its own
+// pthread until everything it received is through its node and handed to
+// the recorders behind (which only count in this mode). Returns 0 and the
+// wall time from the start barrier to the last worker's end, or -errno.
+int gh_workers_run(uint32_t threads, double *seconds, uint64_t *walks) {
+	if (threads == 0 || threads > GH_MAX_GRAPHS || H.n == 0)
+		return -EINVAL;
+	for (uint32_t k = 0; k < threads; k++)
+		if (H.graphs[k].graph == NULL)
+			return -ENOENT;
+	pthread_t th[GH_MAX_GRAPHS];
+	struct gh_workers_arg args[GH_MAX_GRAPHS];
+	pthread_barrier_t bar;
+	pthread_barrier_init(&bar, NULL, threads + 1);
+	for (uint32_t k = 0; k < threads; k++) {
+		H.graphs[k].rx_next = (uint32_t)((uint64_t)H.n * k / threads);
+		H.graphs[k].rx_end = (uint32_t)((uint64_t)H.n * (k + 1) / threads);
+		H.graphs[k].recorded = 0;
+		args[k] = (struct gh_workers_arg) {.k = (int)k, .bar = &bar};
+	}
+	H.workers = 1;
+	for (uint32_t k = 0; k < threads; k++)
+		pthread_create(&th[k], NULL, worker_thread, &args[k]);
+	struct timespec a, b;
+	pthread_barrier_wait(&bar);
+	clock_gettime(CLOCK_MONOTONIC, &a);
+	pthread_barrier_wait(&bar);
+	clock_gettime(CLOCK_MONOTONIC, &b);
+	int err = 0;
+	uint64_t w = 0;
+	for (uint32_t k = 0; k < threads; k++) {
+		pthread_join(th[k], NULL);
+		w += args[k].walks;
+		if (args[k].err && !err)
+			err = args[k].err;
+	}
+	H.workers = 0;
+	pthread_barrier_destroy(&bar);
+	*seconds = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+	if (walks != NULL)
+		*walks = w;
+	return err;
 }

@@ -700,6 +700,40 @@ int gr_hip_node_finish(gr_hip_queue_t *, struct gr_hip_mbuf **m, uint32_t *n, st
 // walk is dropped, the views untouched). gr_hip_node_discard drops what was
 // appended and not sent (a walk that will not go to the GPU).
 int gr_hip_node_append(gr_hip_queue_t *, const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst);
+// Where the hand-back writes in the caller's own mbufs, so that the finish
+// sets them directly instead of the views (one pass over the batch, not
+// two): byte offsets of the fields grout's nodes read in struct rte_mbuf
+// (DPDK rte_mbuf_core.h: data_off and data_len uint16_t, pkt_len and
+// packet_type uint32_t) and in its private area (grout mbuf.h:29-41,
+// rxtx.h:45-48, eth.h:23-36, l3.h:9: iface a pointer, vlan_id uint16_t,
+// domain a 32-bit enum, the nexthops pointers), and the caller's registries
+// that turn a verdict's iface id / nexthop slot into the object pointer the
+// private data holds (read with acquire loads; NULL = no longer registered).
+// No DPDK type crosses the ABI.
+struct gr_hip_mbuf_layout {
+	uint16_t data_off, data_len, pkt_len, packet_type; // in struct rte_mbuf
+	uint16_t priv; // the private area: (char *)m + priv (rte_mbuf_to_priv)
+	uint16_t priv_iface; // mbuf_data.iface
+	uint16_t priv_vlan_id; // iface_mbuf_data.vlan_id
+	uint16_t priv_domain; // eth_input_mbuf_data.domain
+	uint16_t priv_eth_nh; // eth_input_mbuf_data.nh
+	uint16_t priv_l3_nh; // l3_mbuf_data.nh
+	uint32_t n_ifaces, n_nh; // registry sizes
+	const void *const *ifaces; // iface id -> object
+	const void *const *nh; // nexthop slot -> object
+};
+// gr_hip_node_finish handing the oldest walk back straight onto its mbufs:
+// mbufs[i] is the mbuf of view i (the views sent; they are read, not
+// written). Each mbuf gets what gr_hip_node_apply gives its view, in its own
+// fields and private data for the node behind its edge (the iface
+// everywhere; vlan_id before eth_input and past iface_output; eth_input's
+// domain and a NULL nexthop, ip_input's l3 nexthop over them), and
+// edges[i] its edge. A packet whose iface or nexthop is no longer in the
+// registries keeps its mbuf fields and private data and goes to
+// GR_HIP_E_IP_OUTPUT_ERROR, counted in *stale; GR_HIP_E_PUNT: untouched.
+// Returns as gr_hip_node_finish (edges not written on -errno).
+int gr_hip_node_finish_mbufs(gr_hip_queue_t *, void *const *mbufs, const struct gr_hip_mbuf_layout *layout,
+			     uint8_t *edges, uint32_t *stale, struct gr_hip_node_stats *stats);
 int gr_hip_node_send(gr_hip_queue_t *, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst);
 int gr_hip_node_discard(gr_hip_queue_t *);
 // Walks in flight on the queue; *ready (optional) = 1 when the oldest one's

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+# SPDX-License-Identifier: BSD-3-Clause
+"""Several grout workers on one GPU: the fast path's node (gpu_fwd4_node.c)
+in K worker graphs at once, each walked from its own pthread (the walk
+harness's gh_workers_run: one graph per worker as grout's worker.c, each
+polling its own share of the full-view stream like an RX queue, the
+recorders behind the edges only counting). One GPU context, one queue per
+graph. Aggregate Mpps = all mbufs / the wall time of the slowest worker;
+compare with bench.py's cpu_baseline on the same box (16 cores).
+
+    python tools/node_workers.py --threads 1,2,4,8 > out.jsonl
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--threads", default="1,2,4,8")
+    ap.add_argument("--per-thread", type=int, default=1 << 18, help="mbufs per worker")
+    ap.add_argument("--batch", type=int, default=15360)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--rx-touch", type=int, default=1, help="port_rx writes the mbuf and touches the frame (PMD + DDIO)")
+    args = ap.parse_args()
+    threads = [int(x) for x in args.threads.split(",")]
+
+    import test_graph_walk as G  # the harness bindings and the fan-out control plane
+    from grout_amd import abi
+    from grout_amd import synth as S
+    from grout_amd import topology as T
+
+    L = G.lib()
+    L.gh_workers_run.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
+    L.gh_set_rx_touch.argtypes = [ctypes.c_int]
+    devs = (ctypes.c_int * 1)(0)
+    kmax = max(threads)
+    r = L.gh_init(ctypes.cast(devs, ctypes.c_void_p), 1, 1024, 1 << 17, args.batch, 64, 20_000_000)
+    assert r == 0, r
+    for k in range(kmax):
+        assert L.gh_graph_create(k, 0) == k
+    fp = G.FanOutPath(L)
+    topo = T.config_fullview()
+    fp.load(topo)
+    n = kmax * args.per_thread
+    fr, me = S.stream(n, 0x67720002, routes=topo.route_array())
+    fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
+    L.gh_set_pin(0)  # staged header lines: the node's default
+    L.gh_set_rx_touch(args.rx_touch)
+    for k in threads:
+        m = k * args.per_thread
+        assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, m) == 0
+        L.gh_workers_run(k, ctypes.byref(ctypes.c_double()), None)  # warm-up: pages, queues, pinned slots
+        best = []
+        for _ in range(args.reps):
+            assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, m) == 0  # the frames as they came
+            s, w = ctypes.c_double(), ctypes.c_uint64()
+            rr = L.gh_workers_run(k, ctypes.byref(s), ctypes.byref(w))
+            assert rr == 0, rr
+            best.append(s.value)
+        t = float(np.median(best))
+        print(json.dumps({"threads": k, "gpus": 1, "mbufs": m, "batch": args.batch, "rx_touch": args.rx_touch,
+                          "ms": round(t * 1e3, 2), "mpps_aggregate": round(m / t / 1e6, 1),
+                          "mpps_per_worker": round(m / t / 1e6 / k, 1),
+                          "cpu_ns_per_pkt_per_worker": round(t * 1e9 * k / m, 1)}), flush=True)
+    L.gh_fini()
+
+
+if __name__ == "__main__":
+    main()
