@@ -334,6 +334,13 @@ def main():
             "kernel_launches_timed": kcount,
         },
     }
+    if args.workload == "imix_frames":
+        # the frame head is one 64-byte line of a 2 KiB slot: HBM moves it as a
+        # 128-byte granule, so the bytes this layout must move per packet are
+        # 64 more than the algorithmic figure
+        floor = B_PKT + 64
+        result["roofline"]["bytes_per_pkt_granule_floor"] = floor
+        result["roofline"]["frac_at_granule_floor"] = round(n * floor / avg_kernel_s / 1e9 / HBM_PEAK_GBS, 4)
     if plain is not None:
         result["value_plain_placement"] = plain["value"]
         result["plain_placement"] = plain

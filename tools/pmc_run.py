@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 24)
     ap.add_argument("--workload", default="fullview64",
-                    choices=["fullview64", "single64", "fullview6", "imix_frames"])
+                    choices=["fullview64", "single64", "fullview6", "imix", "imix_frames"])
     ap.add_argument("--slot", type=int, default=2240, help="imix_frames: bytes per frame slot (bench.py)")
     ap.add_argument("--ring", type=int, default=None, help="gr_hip_tune ring geometry")
     ap.add_argument("--wg", type=int, default=None, help="gr_hip_tune wg_per_cu")
@@ -47,6 +47,8 @@ def main():
         kw = dict(routes=topo.route_array())
         if args.workload == "imix_frames":  # whole IMIX frames in mbuf-like slots, as bench.py
             kw.update(imix=True, stride=args.slot)
+        elif args.workload == "imix":  # IMIX header lines staged, as bench.py
+            kw.update(imix=True, lines_only=True)
     fp = FastPath(0)
     fp.load(topo)
     for k in ("ring", "wg", "stats", "nt"):
@@ -66,7 +68,8 @@ def main():
     d_v = torch.empty(n * 8, dtype=torch.uint8, device=dev)
     q = fp.queue(shared_stream(dev))
     for _ in range(args.reps):
-        q.submit(d_in, d_out, d_meta, d_v, n, in_stride=stride, out_stride=abi.LINE)
+        q.submit(d_in, d_out, d_meta, d_v, n, in_stride=stride, out_stride=abi.LINE,
+                 lines_only=args.workload == "imix")
     torch.cuda.synchronize()
     if args.no_calib:
         return
