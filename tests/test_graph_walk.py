@@ -854,9 +854,11 @@ def test_graph_reload_mid_stream(drain):
         assert reached.all()
     else:
         assert (~reached).sum() == r["fini_freed"], (int((~reached).sum()), r)
-    for f in ("edge", "pkt_len", "data_len", "data_off", "iface", "nh"):
-        assert np.array_equal(out[f][reached], want[f][reached]), f
+    # every packet leaves on port_output, whose private data is iface_output's
+    # vlan_id (over the l3 nexthop's bytes, check_walk)
     assert (out["edge"][reached] == abi.EDGE["port_output"]).all()
+    for f in ("edge", "pkt_len", "data_len", "data_off", "iface", "vlan_id"):
+        assert np.array_equal(out[f][reached], want[f][reached]), f
 
 
 @pytest.mark.gpu
@@ -886,5 +888,6 @@ def test_graph_walk_append_failure_punts_one_walk():
     assert punt[:BURST].all() and punt.sum() == BURST  # the first walk, whole
     assert (got["data_off"][punt] == 128).all() and (got["pkt_len"][punt] == me["pkt_len"][punt]).all()
     assert (lines[punt] == fr[punt, :abi.LINE]).all()  # frames untouched
-    for f in ("edge", "pkt_len", "data_len", "data_off", "iface", "nh"):
+    assert (got["edge"][~punt] == abi.EDGE["port_output"]).all()  # vlan_id: what port_output reads
+    for f in ("edge", "pkt_len", "data_len", "data_off", "iface", "vlan_id"):
         assert np.array_equal(got[f][~punt], want[f][~punt]), f

@@ -14,6 +14,7 @@
 #   prof[:TAG][=A]    rocprofv3 --kernel-trace --stats of bench.py A -> prof[_TAG]/
 #   pmc:TAG=SET[@A]   rocprofv3 --pmc SET (space separated counters, one pass)
 #                     of tools/pmc_run.py A              -> pmc_TAG/
+#                     (PMC_TIMEOUT seconds, default 120)
 #   run:TAG=CMD       any command (a tools/ script)      -> run_TAG.log
 #
 # e.g. gpurun -- 'bash tools/gpu_session.sh tests smoke bench prof="--steps 20 --warmup 5 --no-cpu-baseline --no-host-path"'
@@ -68,7 +69,7 @@ for step in "$@"; do
 		args=""
 		[ "$set_" != "$arg" ] && args=${arg#*@}
 		rm -rf $OUT/pmc$sfx
-		timeout -s KILL 120 rocprofv3 --pmc $set_ --output-format csv -d $OUT/pmc$sfx -o run -- \
+		timeout -s KILL ${PMC_TIMEOUT:-120} rocprofv3 --pmc $set_ --output-format csv -d $OUT/pmc$sfx -o run -- \
 			python3 tools/pmc_run.py $args > $OUT/pmc$sfx.log 2>&1
 		fatal $? "pmc$sfx"
 		;;
