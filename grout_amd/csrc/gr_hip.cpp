@@ -259,6 +259,7 @@ struct gr_hip_ctx {
 	int ring_cfg; // ring geometry (fwd4_ring.hip ring_cfgN)
 	int host_direct; // host path: the kernel reads / writes pinned host memory itself
 	int node_ptrs; // node path: frames in registered memory are handed over by address
+	int node_nt; // node path: header lines staged with non-temporal stores
 	int tile_order; // 0: workgroup b takes tiles b, b + G, ...; 1: one contiguous run each
 	uint32_t spin_max; // ring waits: polls before giving up (0 = the kernel's default)
 	std::atomic<int> fail_appends{0}; // tests: the next N gr_hip_node_append calls fail (-ENOMEM)
@@ -761,6 +762,7 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->ring_cfg = 2; // 16 waves: 2 loaders, 2 storers, 12 compute, 16 slots
 	c->host_direct = 1; // measured 1.9x the staged copies
 	c->node_ptrs = 0; // staged lines: faster than frames by address, more so with several workers
+	c->node_nt = 0; // cached stores into the walk slot (the A/B in DESIGN.md §6 decides)
 	c->tile_order = 0;
 	c->spin_max = 0;
 	c->untimed = 0;
@@ -2040,6 +2042,8 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		c->fib_fmt = value;
 	} else if (strcmp(key, "node_ptrs") == 0) {
 		c->node_ptrs = value != 0;
+	} else if (strcmp(key, "node_nt") == 0) {
+		c->node_nt = value != 0;
 	} else if (strcmp(key, "untimed") == 0) {
 		c->untimed = value != 0;
 	} else if (strcmp(key, "time_every") == 0) { // sample the launch timing: less event overhead
@@ -2466,7 +2470,7 @@ extern "C" int gr_hip_node_append(gr_hip_queue_t *q, const struct gr_hip_mbuf *m
 		if (r < 0)
 			return r;
 	}
-	int r = gr_node_stage_from(m, n, burst, pos, w.p, w.lines_in ? w.lines : nullptr, w.meta);
+	int r = gr_node_stage_from(m, n, burst, pos, w.p, w.lines_in ? w.lines : nullptr, w.meta, q->ctx->node_nt);
 	if (r < 0)
 		return r;
 	w.na += n;
@@ -2547,7 +2551,7 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 		enqueued = true;
 	} else {
 		if (!w.lines_in) { // "node_ptrs" on, but not every frame is registered: stage the lines now
-			if ((r = gr_node_stage_from(m, n, burst, pos, 0, w.lines, w.meta)) < 0)
+			if ((r = gr_node_stage_from(m, n, burst, pos, 0, w.lines, w.meta, c->node_nt)) < 0)
 				return r;
 			lap(GR_HIP_NODE_PROF_STAGE);
 		}

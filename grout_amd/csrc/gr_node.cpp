@@ -31,6 +31,7 @@
 // (iface_output.c:81-86).
 #include "gr_node_priv.h"
 
+#include <emmintrin.h>
 #include <errno.h>
 #include <stddef.h>
 #include <string.h>
@@ -160,8 +161,21 @@ extern "C" int gr_hip_node_layout(const struct gr_hip_mbuf *m, uint32_t n, uint3
 	return (int)p;
 }
 
+// One 64-byte header line into the slot (64-byte aligned) without reading
+// the slot's line first.
+static inline void line_stream(uint8_t *dst, const void *src) {
+	const __m128i *s = static_cast<const __m128i *>(src);
+	__m128i *d = reinterpret_cast<__m128i *>(dst);
+	const __m128i a = _mm_loadu_si128(s), b = _mm_loadu_si128(s + 1), c = _mm_loadu_si128(s + 2),
+		      e = _mm_loadu_si128(s + 3);
+	_mm_stream_si128(d, a);
+	_mm_stream_si128(d + 1, b);
+	_mm_stream_si128(d + 2, c);
+	_mm_stream_si128(d + 3, e);
+}
+
 extern "C" int gr_node_stage_from(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, const uint32_t *pos,
-				  uint32_t next, void *lines, struct gr_hip_pkt_meta *meta) {
+				  uint32_t next, void *lines, struct gr_hip_pkt_meta *meta, int nt) {
 	burst = walk_burst(burst);
 	uint8_t *L = static_cast<uint8_t *>(lines);
 	constexpr uint32_t AHEAD = 16; // frames in flight: staging is bound by their cache misses
@@ -182,9 +196,14 @@ extern "C" int gr_node_stage_from(const struct gr_hip_mbuf *m, uint32_t n, uint3
 		// IPv4 headers from the data room without a length check (eth_input.c
 		// reads 14 bytes of a shorter frame), and an mbuf's data room always
 		// holds 64 bytes past data_off (mempool.c:66-68)
-		if (m[i].frame == nullptr)
+		if (m[i].frame == nullptr) {
+			if (nt)
+				_mm_sfence();
 			return -EINVAL;
-		if (L != nullptr) // NULL: metadata only (the GPU reads the frames itself)
+		}
+		if (L != nullptr && nt)
+			line_stream(L + (size_t)at * GR_HIP_LINE, m[i].frame);
+		else if (L != nullptr) // NULL: metadata only (the GPU reads the frames itself)
 			memcpy(L + (size_t)at * GR_HIP_LINE, m[i].frame, GR_HIP_LINE);
 		uint16_t vc = (uint16_t)((m[i].vlan_id & 0xfff) | ((m[i].ck & 3) << 12));
 		if (walk_start(m, i, start, burst)) {
@@ -196,6 +215,8 @@ extern "C" int gr_node_stage_from(const struct gr_hip_mbuf *m, uint32_t n, uint3
 		meta[at].pkt_len = (uint16_t)(m[i].pkt_len > 0xffff ? 0xffff : m[i].pkt_len);
 		meta[at].rss = (uint16_t)m[i].rss;
 	}
+	if (nt)
+		_mm_sfence(); // the streamed lines are visible before the launch that reads them
 	return 0;
 }
 
@@ -203,7 +224,7 @@ extern "C" int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, uint32
 				 void *lines, struct gr_hip_pkt_meta *meta) {
 	if (n && (m == nullptr || meta == nullptr))
 		return -EINVAL;
-	return gr_node_stage_from(m, n, burst, pos, 0, lines, meta);
+	return gr_node_stage_from(m, n, burst, pos, 0, lines, meta, 0);
 }
 
 // The VLAN sub-interface of (parent, vlan_id) in the host image of the

@@ -23,9 +23,11 @@ struct gr_node_vlans {
 // first slot past the walks.
 uint64_t gr_node_layout_from(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, uint64_t p, uint32_t *pos);
 // gr_hip_node_stage continuing at slot `next` (the first one not yet
-// written: pad slots from there up to pos[0] are zeroed).
+// written: pad slots from there up to pos[0] are zeroed); nt: the header
+// lines go out with non-temporal stores (no read for ownership of the slot's
+// lines, which only the GPU reads), fenced before the return.
 int gr_node_stage_from(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, const uint32_t *pos, uint32_t next,
-		       void *lines, struct gr_hip_pkt_meta *meta);
+		       void *lines, struct gr_hip_pkt_meta *meta, int nt);
 
 // The hand-back straight onto the caller's mbufs (gr_hip_node_finish_mbufs):
 // the views are read, not written; edges[i] and *stale are the outputs.

@@ -469,6 +469,9 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //   "node_ptrs"  1 = gr_hip_node_process hands registered frames over by
 //               address, 0 = stage header lines (default: faster from one
 //               worker thread up, and much faster with several)
+//   "node_nt"    1 = the node stages header lines into its walk slot with
+//               non-temporal stores (no read for ownership; only the GPU
+//               reads them), 0 = cached stores (default)
 //   "time_every" N: only every N-th submit of a queue gets the HIP event
 //               pair that gr_hip_queue_kernel_ms reads (default 1: all);
 //               each pair costs ~7 us of stream time per launch. Setting
