@@ -479,8 +479,13 @@ extern "C" int gr_node_apply_ex(
 				uint32_t len = b.data_len + (depth < 5 ? 14u : 0u);
 				if (len > 26)
 					len = 26;
-				if (L != nullptr)
-					memcpy(b.frame, line, len);
+				uint8_t *fr = static_cast<uint8_t *>(b.frame);
+				if (L != nullptr && len >= 16) { // two overlapping 16-byte moves, no call
+					memcpy(fr, line, 16);
+					memcpy(fr + len - 16, line + len - 16, 16);
+				} else if (L != nullptr) {
+					memcpy(fr, line, len);
+				}
 			}
 			if (depth <= 4) {
 				if (demuxed)
