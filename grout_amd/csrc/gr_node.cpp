@@ -305,12 +305,21 @@ static inline void count(struct gr_hip_iface_stats *st, uint32_t n_st, uint32_t 
 	}
 }
 
+// The hand-back's prefetch distance and locality (measurement builds
+// override them: tools/apply_cost.py).
+#ifndef GR_NODE_APPLY_AHEAD
+#define GR_NODE_APPLY_AHEAD 16
+#endif
+#ifndef GR_NODE_APPLY_PF_LOC
+#define GR_NODE_APPLY_PF_LOC 0
+#endif
+
 static inline void prefetch_for_apply(const struct gr_hip_mbuf *m, uint32_t i, const struct gr_node_direct *d) {
-	__builtin_prefetch(m[i].frame, 1, 0);
+	__builtin_prefetch(m[i].frame, 1, GR_NODE_APPLY_PF_LOC);
 	if (d != nullptr) {
 		const uint8_t *mb = static_cast<const uint8_t *>(d->mbufs[i]);
-		__builtin_prefetch(mb, 1, 0); // data_off .. packet_type: the mbuf's first line
-		__builtin_prefetch(mb + d->lay->priv, 1, 0); // the private data
+		__builtin_prefetch(mb, 1, GR_NODE_APPLY_PF_LOC); // data_off .. packet_type: the mbuf's first line
+		__builtin_prefetch(mb + d->lay->priv, 1, GR_NODE_APPLY_PF_LOC); // the private data
 	}
 }
 
@@ -427,7 +436,7 @@ extern "C" int gr_node_apply_ex(
 	bool walk_nomac = false; // the walk holds an eth_output_no_mac packet
 	// frames read (the ether type) and written back: prefetch them, the loop
 	// is bound by their cache misses
-	constexpr uint32_t AHEAD = 16;
+	constexpr uint32_t AHEAD = GR_NODE_APPLY_AHEAD;
 	for (uint32_t i = 0; i < n && i < AHEAD; i++)
 		prefetch_for_apply(m, i, direct);
 	for (uint32_t i = 0; i < n; i++) {
