@@ -190,6 +190,7 @@ HIP_API = {
     "gr_hip_node_layout": (_I, [_P, _U32, _U32, _P]),
     "gr_hip_node_stage": (_I, [_P, _U32, _U32, _P, _P, _P]),
     "gr_hip_node_append": (_I, [_P, _P, _U32, _U32]),
+    "gr_hip_node_append_mbufs": (_I, [_P, _P, _U32, _P, _U32]),
     "gr_hip_node_send": (_I, [_P, _P, _U32, _U32]),
     "gr_hip_node_discard": (_I, [_P]),
     "gr_hip_node_apply": (_I, [_P, _U32, _U32, _P, _P, _U32, _P, _P, _U32, _P, _U32, _P]),

@@ -175,6 +175,9 @@ struct node_slot {
 	// far, and whether the header lines are (not with "node_ptrs")
 	bool open = false, lines_in = false;
 	uint32_t na = 0, p = 0;
+	// appended from the mbufs (gr_hip_node_append_mbufs): the views are these
+	bool own = false;
+	std::vector<gr_hip_mbuf> views;
 };
 
 } // namespace
@@ -259,7 +262,6 @@ struct gr_hip_ctx {
 	int ring_cfg; // ring geometry (fwd4_ring.hip ring_cfgN)
 	int host_direct; // host path: the kernel reads / writes pinned host memory itself
 	int node_ptrs; // node path: frames in registered memory are handed over by address
-	int node_nt; // node path: header lines staged with non-temporal stores
 	int tile_order; // 0: workgroup b takes tiles b, b + G, ...; 1: one contiguous run each
 	uint32_t spin_max; // ring waits: polls before giving up (0 = the kernel's default)
 	std::atomic<int> fail_appends{0}; // tests: the next N gr_hip_node_append calls fail (-ENOMEM)
@@ -762,7 +764,6 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->ring_cfg = 2; // 16 waves: 2 loaders, 2 storers, 12 compute, 16 slots
 	c->host_direct = 1; // measured 1.9x the staged copies
 	c->node_ptrs = 0; // staged lines: faster than frames by address, more so with several workers
-	c->node_nt = 0; // cached stores into the walk slot (the A/B in DESIGN.md §6 decides)
 	c->tile_order = 0;
 	c->spin_max = 0;
 	c->untimed = 0;
@@ -2042,8 +2043,6 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		c->fib_fmt = value;
 	} else if (strcmp(key, "node_ptrs") == 0) {
 		c->node_ptrs = value != 0;
-	} else if (strcmp(key, "node_nt") == 0) {
-		c->node_nt = value != 0;
 	} else if (strcmp(key, "untimed") == 0) {
 		c->untimed = value != 0;
 	} else if (strcmp(key, "time_every") == 0) { // sample the launch timing: less event overhead
@@ -2448,10 +2447,11 @@ extern "C" int gr_hip_node_append(gr_hip_queue_t *q, const struct gr_hip_mbuf *m
 	node_slot &w = open_slot(q);
 	if (!w.open) {
 		w.open = true;
+		w.own = false;
 		w.na = w.p = 0;
 		w.lines_in = !q->ctx->node_ptrs;
-	} else if (n && !(m[0].flags & GR_HIP_MBUF_F_WALK)) {
-		return -EINVAL; // each append is a walk (or walks) of its own
+	} else if (w.own || (n && !(m[0].flags & GR_HIP_MBUF_F_WALK))) {
+		return -EINVAL; // each append is a walk (or walks) of its own, of views
 	}
 	if (n == 0)
 		return (int)w.p;
@@ -2470,9 +2470,51 @@ extern "C" int gr_hip_node_append(gr_hip_queue_t *q, const struct gr_hip_mbuf *m
 		if (r < 0)
 			return r;
 	}
-	int r = gr_node_stage_from(m, n, burst, pos, w.p, w.lines_in ? w.lines : nullptr, w.meta, q->ctx->node_nt);
+	int r = gr_node_stage_from(m, n, burst, pos, w.p, w.lines_in ? w.lines : nullptr, w.meta);
 	if (r < 0)
 		return r;
+	w.na += n;
+	w.p = (uint32_t)p;
+	node_prof_ns[GR_HIP_NODE_PROF_STAGE] += prof_now() - t_prof;
+	return (int)p;
+}
+
+extern "C" int gr_hip_node_append_mbufs(gr_hip_queue_t *q, void *const *mbufs, uint32_t n,
+					const struct gr_hip_mbuf_layout *lay, uint32_t burst) {
+	if (q == nullptr || lay == nullptr || (n && mbufs == nullptr))
+		return -EINVAL;
+	if (q->nw_count == GR_HIP_NODE_DEPTH)
+		return -EBUSY;
+	node_slot &w = open_slot(q);
+	if (!w.open) {
+		w.open = true;
+		w.own = true;
+		w.na = w.p = 0;
+		w.lines_in = !q->ctx->node_ptrs;
+	} else if (!w.own) {
+		return -EINVAL; // views were appended to this slot
+	}
+	if (n == 0)
+		return (int)w.p;
+	if (q->ctx->fail_appends.load(std::memory_order_relaxed) > 0 && q->ctx->fail_appends.fetch_sub(1) > 0)
+		return -ENOMEM; // as a failed slot_grow: the slot is left as it was
+	uint64_t t_prof = prof_now();
+	const uint64_t p = gr_node_walk_end(w.p, n, burst); // the cuts do not depend on the mbufs
+	if (p > INT32_MAX)
+		return -E2BIG;
+	if (p > w.cap) {
+		hipSetDevice(q->ctx->dev);
+		int r = slot_grow(w, (uint32_t)p, w.p);
+		if (r < 0)
+			return r;
+	}
+	const size_t need = (size_t)w.na + n;
+	if (w.views.size() < need)
+		w.views.resize(std::max(need, 2 * w.views.size()));
+	if (w.pos.size() < need)
+		w.pos.resize(std::max(need, 2 * w.pos.size()));
+	gr_node_stage_mbufs(mbufs, n, lay, burst, w.p, w.views.data() + w.na, w.pos.data() + w.na,
+			    w.lines_in ? w.lines : nullptr, w.meta);
 	w.na += n;
 	w.p = (uint32_t)p;
 	node_prof_ns[GR_HIP_NODE_PROF_STAGE] += prof_now() - t_prof;
@@ -2488,7 +2530,7 @@ extern "C" int gr_hip_node_discard(gr_hip_queue_t *q) {
 }
 
 extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst) {
-	if (q == nullptr || (n && m == nullptr))
+	if (q == nullptr)
 		return -EINVAL;
 	if (q->nw_count == GR_HIP_NODE_DEPTH)
 		return -EBUSY;
@@ -2496,7 +2538,12 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 	node_slot &w = open_slot(q);
 	const bool was_open = w.open;
 	w.open = false;
-	if (!(was_open ? w.na == n : n == 0))
+	if (was_open && w.own) { // appended from the mbufs: the library's own views
+		if (m != nullptr)
+			return -EINVAL;
+		m = w.views.data();
+	}
+	if ((n && m == nullptr) || !(was_open ? w.na == n : n == 0))
 		return -EINVAL; // not what was appended
 	uint32_t *pos = w.pos.data();
 	uint64_t t_prof = prof_now();
@@ -2551,7 +2598,7 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 		enqueued = true;
 	} else {
 		if (!w.lines_in) { // "node_ptrs" on, but not every frame is registered: stage the lines now
-			if ((r = gr_node_stage_from(m, n, burst, pos, 0, w.lines, w.meta, c->node_nt)) < 0)
+			if ((r = gr_node_stage_from(m, n, burst, pos, 0, w.lines, w.meta)) < 0)
 				return r;
 			lap(GR_HIP_NODE_PROF_STAGE);
 		}

@@ -31,7 +31,6 @@
 // (iface_output.c:81-86).
 #include "gr_node_priv.h"
 
-#include <emmintrin.h>
 #include <errno.h>
 #include <stddef.h>
 #include <string.h>
@@ -161,21 +160,8 @@ extern "C" int gr_hip_node_layout(const struct gr_hip_mbuf *m, uint32_t n, uint3
 	return (int)p;
 }
 
-// One 64-byte header line into the slot (64-byte aligned) without reading
-// the slot's line first.
-static inline void line_stream(uint8_t *dst, const void *src) {
-	const __m128i *s = static_cast<const __m128i *>(src);
-	__m128i *d = reinterpret_cast<__m128i *>(dst);
-	const __m128i a = _mm_loadu_si128(s), b = _mm_loadu_si128(s + 1), c = _mm_loadu_si128(s + 2),
-		      e = _mm_loadu_si128(s + 3);
-	_mm_stream_si128(d, a);
-	_mm_stream_si128(d + 1, b);
-	_mm_stream_si128(d + 2, c);
-	_mm_stream_si128(d + 3, e);
-}
-
 extern "C" int gr_node_stage_from(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, const uint32_t *pos,
-				  uint32_t next, void *lines, struct gr_hip_pkt_meta *meta, int nt) {
+				  uint32_t next, void *lines, struct gr_hip_pkt_meta *meta) {
 	burst = walk_burst(burst);
 	uint8_t *L = static_cast<uint8_t *>(lines);
 	constexpr uint32_t AHEAD = 16; // frames in flight: staging is bound by their cache misses
@@ -196,14 +182,9 @@ extern "C" int gr_node_stage_from(const struct gr_hip_mbuf *m, uint32_t n, uint3
 		// IPv4 headers from the data room without a length check (eth_input.c
 		// reads 14 bytes of a shorter frame), and an mbuf's data room always
 		// holds 64 bytes past data_off (mempool.c:66-68)
-		if (m[i].frame == nullptr) {
-			if (nt)
-				_mm_sfence();
+		if (m[i].frame == nullptr)
 			return -EINVAL;
-		}
-		if (L != nullptr && nt)
-			line_stream(L + (size_t)at * GR_HIP_LINE, m[i].frame);
-		else if (L != nullptr) // NULL: metadata only (the GPU reads the frames itself)
+		if (L != nullptr) // NULL: metadata only (the GPU reads the frames itself)
 			memcpy(L + (size_t)at * GR_HIP_LINE, m[i].frame, GR_HIP_LINE);
 		uint16_t vc = (uint16_t)((m[i].vlan_id & 0xfff) | ((m[i].ck & 3) << 12));
 		if (walk_start(m, i, start, burst)) {
@@ -215,16 +196,91 @@ extern "C" int gr_node_stage_from(const struct gr_hip_mbuf *m, uint32_t n, uint3
 		meta[at].pkt_len = (uint16_t)(m[i].pkt_len > 0xffff ? 0xffff : m[i].pkt_len);
 		meta[at].rss = (uint16_t)m[i].rss;
 	}
-	if (nt)
-		_mm_sfence(); // the streamed lines are visible before the launch that reads them
 	return 0;
+}
+
+// Where a walk of n mbufs appended at slot p ends: cut every `burst` mbufs,
+// each piece placed as gr_node_layout_from places a walk.
+extern "C" uint64_t gr_node_walk_end(uint64_t p, uint32_t n, uint32_t burst) {
+	burst = walk_burst(burst);
+	for (uint32_t i = 0; i < n; i += burst) {
+		const uint32_t len = n - i < burst ? n - i : burst;
+		if ((p & 63) + len > 64)
+			p = (p + 63) & ~63ull;
+		p += len;
+	}
+	return p;
+}
+
+template <typename T> static inline T get(const uint8_t *base, uint16_t off) {
+	T v;
+	memcpy(&v, base + off, sizeof(v));
+	return v;
+}
+
+// gr_hip_node_append_mbufs' one pass over a walk's mbufs (mbufs[0] starts
+// it): each mbuf read through the layout into its view v[i] (what the grout
+// node used to build: rte_pktmbuf_mtod, lengths, packet_type, hash.rss,
+// iface_mbuf_data's iface id and vlan_id, the checksum status), placed from
+// slot p (pos[i]; pads zeroed) as gr_node_layout_from places it, and its
+// header line (lines NULL: none) and metadata staged as gr_node_stage_from
+// stages them. Returns the first slot past the walk.
+extern "C" uint64_t gr_node_stage_mbufs(void *const *mbufs, uint32_t n, const struct gr_hip_mbuf_layout *lay,
+					uint32_t burst, uint64_t p, struct gr_hip_mbuf *v, uint32_t *pos, void *lines,
+					struct gr_hip_pkt_meta *meta) {
+	burst = walk_burst(burst);
+	const struct gr_hip_mbuf_layout &L = *lay;
+	uint8_t *lb = static_cast<uint8_t *>(lines);
+	for (uint32_t i = 0; i < n; i++) {
+		const bool start = i % burst == 0;
+		if (start) {
+			const uint32_t len = n - i < burst ? n - i : burst;
+			if ((p & 63) + len > 64) { // pad to the next tile: punted by the kernel, counted nowhere
+				for (const uint64_t e = (p + 63) & ~63ull; p < e; p++) {
+					meta[p] = gr_hip_pkt_meta{0, 0, 0, 0};
+					if (lb != nullptr)
+						memset(lb + (size_t)p * GR_HIP_LINE, 0, GR_HIP_LINE);
+				}
+			}
+		}
+		const uint8_t *mb = static_cast<const uint8_t *>(mbufs[i]);
+		const uint8_t *priv = mb + L.priv;
+		const uint16_t off = get<uint16_t>(mb, L.data_off);
+		uint8_t *frame = get<uint8_t *>(mb, L.buf_addr) + off;
+		const uint8_t *ifp = get<const uint8_t *>(priv, L.priv_iface);
+		const uint64_t ck = get<uint64_t>(mb, L.ol_flags) & L.ck_mask;
+		struct gr_hip_mbuf &x = v[i];
+		x.frame = frame;
+		x.pkt_len = get<uint32_t>(mb, L.pkt_len);
+		x.data_len = get<uint16_t>(mb, L.data_len);
+		x.data_off = off;
+		x.packet_type = get<uint32_t>(mb, L.packet_type);
+		x.rss = get<uint32_t>(mb, L.rss);
+		x.iface = ifp != nullptr ? get<uint16_t>(ifp, L.iface_id) : 0;
+		x.vlan_id = get<uint16_t>(priv, L.priv_vlan_id);
+		x.ck = ck == L.ck_good ? GR_HIP_CKSUM_GOOD : ck == L.ck_bad ? GR_HIP_CKSUM_BAD : GR_HIP_CKSUM_UNKNOWN;
+		x.edge = 0;
+		x.domain = 0;
+		x.flags = i == 0 ? GR_HIP_MBUF_F_WALK : 0;
+		x.nh = 0;
+		pos[i] = (uint32_t)p;
+		// 64 bytes whatever data_len says (gr_node_stage_from)
+		if (lb != nullptr)
+			memcpy(lb + (size_t)p * GR_HIP_LINE, frame, GR_HIP_LINE);
+		meta[p].iface = x.iface;
+		meta[p].vlan_ck = (uint16_t)((x.vlan_id & 0xfff) | (x.ck << 12) | (start ? GR_HIP_META_WALK : 0));
+		meta[p].pkt_len = (uint16_t)(x.pkt_len > 0xffff ? 0xffff : x.pkt_len);
+		meta[p].rss = (uint16_t)x.rss;
+		p++;
+	}
+	return p;
 }
 
 extern "C" int gr_hip_node_stage(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, const uint32_t *pos,
 				 void *lines, struct gr_hip_pkt_meta *meta) {
 	if (n && (m == nullptr || meta == nullptr))
 		return -EINVAL;
-	return gr_node_stage_from(m, n, burst, pos, 0, lines, meta, 0);
+	return gr_node_stage_from(m, n, burst, pos, 0, lines, meta);
 }
 
 // The VLAN sub-interface of (parent, vlan_id) in the host image of the

@@ -23,11 +23,16 @@ struct gr_node_vlans {
 // first slot past the walks.
 uint64_t gr_node_layout_from(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, uint64_t p, uint32_t *pos);
 // gr_hip_node_stage continuing at slot `next` (the first one not yet
-// written: pad slots from there up to pos[0] are zeroed); nt: the header
-// lines go out with non-temporal stores (no read for ownership of the slot's
-// lines, which only the GPU reads), fenced before the return.
+// written: pad slots from there up to pos[0] are zeroed).
 int gr_node_stage_from(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, const uint32_t *pos, uint32_t next,
-		       void *lines, struct gr_hip_pkt_meta *meta, int nt);
+		       void *lines, struct gr_hip_pkt_meta *meta);
+
+// Where a walk of n mbufs appended at slot p ends (cut every `burst`).
+uint64_t gr_node_walk_end(uint64_t p, uint32_t n, uint32_t burst);
+// gr_hip_node_append_mbufs' pass: views v[], slots pos[], lines and metadata
+// of one walk's mbufs from slot p on; returns the first slot past the walk.
+uint64_t gr_node_stage_mbufs(void *const *mbufs, uint32_t n, const struct gr_hip_mbuf_layout *lay, uint32_t burst,
+			     uint64_t p, struct gr_hip_mbuf *v, uint32_t *pos, void *lines, struct gr_hip_pkt_meta *meta);
 
 // The hand-back straight onto the caller's mbufs (gr_hip_node_finish_mbufs):
 // the views are read, not written; edges[i] and *stale are the outputs.

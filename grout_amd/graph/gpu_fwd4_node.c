@@ -272,7 +272,6 @@ struct gpu_walk {
 	uint64_t first_ns; // arrival of the oldest held packet, 0 = none
 	uint32_t cur;
 	struct rte_mbuf **mbufs[2];
-	struct gr_hip_mbuf *v[2];
 	uint8_t *edges[2]; // each mbuf's edge, as the one-pass hand-back leaves it
 	int pending; // the other buffer's batch is on the GPU (gr_hip_node_start'ed)
 	uint32_t pend_n; // its size
@@ -377,17 +376,6 @@ static void readers_release(struct gpu_walk *w) {
 	}
 }
 
-static uint8_t ck_status(uint64_t ol_flags) {
-	switch (ol_flags & RTE_MBUF_F_RX_IP_CKSUM_MASK) {
-	case RTE_MBUF_F_RX_IP_CKSUM_GOOD:
-		return GR_HIP_CKSUM_GOOD;
-	case RTE_MBUF_F_RX_IP_CKSUM_BAD:
-		return GR_HIP_CKSUM_BAD;
-	default: // UNKNOWN or NONE: ip_input verifies in software (ip_input.c:80-92)
-		return GR_HIP_CKSUM_UNKNOWN;
-	}
-}
-
 // Where the one-pass hand-back (gr_hip_node_finish_mbufs) writes grout's
 // mbuf fields and the private data grout's chain leaves for the node behind
 // each edge: the iface everywhere; iface_input's vlan_id before eth_input;
@@ -410,10 +398,23 @@ static void layout_init(struct gr_hip_mbuf_layout *l) {
 	l->priv_domain = offsetof(struct eth_input_mbuf_data, domain);
 	l->priv_eth_nh = offsetof(struct eth_input_mbuf_data, nh);
 	l->priv_l3_nh = offsetof(struct l3_mbuf_data, nh);
+	// what the staging reads (gr_hip_node_append_mbufs): the frame at
+	// rte_pktmbuf_mtod, hash.rss, the ingress iface's id, and the checksum
+	// status ip_input tests (UNKNOWN or NONE: verified in software,
+	// ip_input.c:80-92)
+	l->buf_addr = offsetof(struct rte_mbuf, buf_addr);
+	l->ol_flags = offsetof(struct rte_mbuf, ol_flags);
+	l->rss = offsetof(struct rte_mbuf, hash.rss);
+	l->iface_id = offsetof(struct iface, id);
+	l->ck_mask = RTE_MBUF_F_RX_IP_CKSUM_MASK;
+	l->ck_good = RTE_MBUF_F_RX_IP_CKSUM_GOOD;
+	l->ck_bad = RTE_MBUF_F_RX_IP_CKSUM_BAD;
 }
 _Static_assert(sizeof(((struct rte_mbuf *)0)->data_off) == 2 && sizeof(((struct rte_mbuf *)0)->data_len) == 2
 		       && sizeof(((struct rte_mbuf *)0)->pkt_len) == 4 && sizeof(((struct rte_mbuf *)0)->packet_type) == 4
-		       && sizeof(eth_domain_t) == 4,
+		       && sizeof(eth_domain_t) == 4 && sizeof(((struct rte_mbuf *)0)->buf_addr) == 8
+		       && sizeof(((struct rte_mbuf *)0)->ol_flags) == 8 && sizeof(((struct rte_mbuf *)0)->hash.rss) == 4
+		       && sizeof(((struct iface *)0)->id) == 2,
 	       "the widths gr_hip_mbuf_layout names");
 
 // The registries as they are now (allocated once, at their first set).
@@ -502,7 +503,7 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 	}
 	if ((conf.depth < 2 || w->draining) && !w->pending) { // synchronous
 		started(w, n);
-		int r = gr_hip_node_send(w->q, w->v[k], n, WALK_SPLIT);
+		int r = gr_hip_node_send(w->q, NULL, n, WALK_SPLIT);
 		if (r == 0)
 			r = hand_back(w, k);
 		deliver(graph, node, w, k, n, r);
@@ -512,7 +513,7 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 	// previous one may still be on the GPU, then hand the previous one back:
 	// batches leave in arrival order
 	PROF_T0();
-	const int r = gr_hip_node_send(w->q, w->v[k], n, WALK_SPLIT);
+	const int r = gr_hip_node_send(w->q, NULL, n, WALK_SPLIT);
 	PROF_ADD(GPU_FWD4_PROF_START);
 	const uint32_t delivered = finish_pending(graph, node, w);
 	if (r < 0) { // the GPU did not take it: grout's CPU nodes do (after the one before, in order)
@@ -550,8 +551,7 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 		rte_node_enqueue(graph, node, GR_HIP_E_PUNT, objs, nb_objs);
 		return nb_objs;
 	}
-	uint8_t walk = GR_HIP_MBUF_F_WALK; // this call is one graph walk's iface_input stream
-	const uint32_t n0 = w->n;
+	const uint32_t n0 = w->n; // this call is one graph walk's iface_input stream
 	w->rx_seen = 1;
 	// software pipeline over the burst (as DPDK's l3fwd does): each mbuf
 	// PF_MBUF ahead, its frame PF_FRAME ahead, so that their misses overlap
@@ -576,27 +576,16 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 		}
 		if (w->n == 0)
 			reader_hold(w, w->cur); // before the GPU reads any mirror for this batch
-		const struct iface_mbuf_data *d = iface_mbuf_data(m);
-		w->mbufs[w->cur][w->n] = m;
-		w->v[w->cur][w->n++] = (struct gr_hip_mbuf) {
-			.frame = rte_pktmbuf_mtod(m, void *),
-			.pkt_len = rte_pktmbuf_pkt_len(m),
-			.data_len = m->data_len,
-			.data_off = m->data_off,
-			.packet_type = m->packet_type,
-			.rss = m->hash.rss,
-			.iface = d->iface != NULL ? d->iface->id : 0,
-			.vlan_id = d->vlan_id,
-			.ck = ck_status(m->ol_flags),
-			.flags = walk,
-		};
-		walk = 0;
+		w->mbufs[w->cur][w->n++] = m;
 	}
-	// stage this walk now, while its mbufs and frames are in cache. A walk
-	// that cannot be staged (no pinned memory for the slot ...; the append
-	// leaves the slot as it was) goes to grout's CPU nodes now, untouched and
+	// stage this walk now, while its mbufs and frames are in cache: the
+	// library reads each mbuf through the layout (frame, lengths, private
+	// data) and stages its header line and metadata in one pass. A walk that
+	// cannot be staged (no pinned memory for the slot ...; the append leaves
+	// the slot as it was) goes to grout's CPU nodes now, untouched and
 	// counted; the walks before it stay in the batch.
-	if (w->n > n0 && gr_hip_node_append(w->q, &w->v[w->cur][n0], w->n - n0, WALK_SPLIT) < 0) {
+	if (w->n > n0
+	    && gr_hip_node_append_mbufs(w->q, (void *const *)&w->mbufs[w->cur][n0], w->n - n0, &w->lay, WALK_SPLIT) < 0) {
 		rte_node_enqueue(graph, node, GR_HIP_E_PUNT, (void **)&w->mbufs[w->cur][n0], (uint16_t)(w->n - n0));
 		w->append_errors++;
 		w->n = n0;
@@ -621,7 +610,6 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 static void walk_free(struct gpu_walk *w) {
 	for (int k = 0; k < 2; k++) {
 		free(w->mbufs[k]);
-		free(w->v[k]);
 		free(w->edges[k]);
 	}
 	free(w->ifs);
@@ -663,9 +651,8 @@ static int gpu_fwd4_init(const struct rte_graph *graph, struct rte_node *node) {
 	int r = 0;
 	for (int k = 0; k < 2; k++) {
 		w->mbufs[k] = calloc(w->cap, sizeof(*w->mbufs[k]));
-		w->v[k] = calloc(w->cap, sizeof(*w->v[k]));
 		w->edges[k] = calloc(w->cap, 1);
-		if (w->mbufs[k] == NULL || w->v[k] == NULL || w->edges[k] == NULL)
+		if (w->mbufs[k] == NULL || w->edges[k] == NULL)
 			r = -ENOMEM;
 	}
 	layout_init(&w->lay);

@@ -469,9 +469,6 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //   "node_ptrs"  1 = gr_hip_node_process hands registered frames over by
 //               address, 0 = stage header lines (default: faster from one
 //               worker thread up, and much faster with several)
-//   "node_nt"    1 = the node stages header lines into its walk slot with
-//               non-temporal stores (no read for ownership; only the GPU
-//               reads them), 0 = cached stores (default)
 //   "time_every" N: only every N-th submit of a queue gets the HIP event
 //               pair that gr_hip_queue_kernel_ms reads (default 1: all);
 //               each pair costs ~7 us of stream time per launch. Setting
@@ -724,7 +721,29 @@ struct gr_hip_mbuf_layout {
 	uint32_t n_ifaces, n_nh; // registry sizes
 	const void *const *ifaces; // iface id -> object
 	const void *const *nh; // nexthop slot -> object
+	// read by gr_hip_node_append_mbufs (staging straight from the mbufs):
+	uint16_t buf_addr; // in struct rte_mbuf (void *): the frame is buf_addr + data_off
+	uint16_t ol_flags; // in struct rte_mbuf (uint64_t)
+	uint16_t rss; // hash.rss in struct rte_mbuf (uint32_t)
+	uint16_t iface_id; // the id (uint16_t) inside the object mbuf_data.iface points to
+	// RTE_MBUF_F_RX_IP_CKSUM_MASK, _GOOD and _BAD (rte_mbuf_core.h): ol_flags
+	// & ck_mask equal to ck_good / ck_bad is GR_HIP_CKSUM_GOOD / _BAD, anything
+	// else GR_HIP_CKSUM_UNKNOWN (ip_input.c:80-92 verifies in software)
+	uint64_t ck_mask, ck_good, ck_bad;
 };
+// gr_hip_node_append without the views: the node passes one rte_graph walk's
+// mbufs (mbufs[0] starts it; it is cut every `burst` mbufs) and the library
+// reads each one through the layout (single segment; frame, lengths,
+// packet_type, rss, checksum status, the iface id and vlan_id from the
+// private data) while it lays the walk out and stages its header line and
+// metadata, in one pass. The views gr_hip_node_send and the finish use are
+// the library's own, built in the same pass: the next gr_hip_node_send on
+// the queue then takes m == NULL and n = every mbuf appended since the last
+// send, and the walk is handed back with gr_hip_node_finish_mbufs (the
+// mbufs array the appends read, kept until then). A slot holds walks
+// appended one way only (-EINVAL otherwise). Returns as gr_hip_node_append.
+int gr_hip_node_append_mbufs(gr_hip_queue_t *, void *const *mbufs, uint32_t n,
+			     const struct gr_hip_mbuf_layout *layout, uint32_t burst);
 // gr_hip_node_finish handing the oldest walk back straight onto its mbufs:
 // mbufs[i] is the mbuf of view i (the views sent; they are read, not
 // written). Each mbuf gets what gr_hip_node_apply gives its view, in its own

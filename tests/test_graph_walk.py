@@ -448,22 +448,6 @@ def test_graph_walk_stream_batches(depth):
 
 
 @pytest.mark.gpu
-def test_graph_walk_nt_staging():
-    """The "node_nt" knob: header lines go into the walk slot with
-    non-temporal stores (fenced before the launch). The same walks, bit-exact
-    with the oracle."""
-    fp = graph_ctx()
-    t = T.config_single_route()
-    fr, me = S.stream(40_000, 0xB0E, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
-    fp.tune("node_nt", 1)
-    try:
-        got = check_walk(t, fr, me)
-    finally:
-        fp.tune("node_nt", 0)
-    assert (got["edge"] == abi.EDGE["port_output"]).all()
-
-
-@pytest.mark.gpu
 def test_graph_walk_flush_node(depth):
     """Full bursts only: the packets behind the last full batch wait for the
     flush source node (max_delay), then leave in order. Pipelined, the source

@@ -192,7 +192,10 @@ _LAYOUT_U16 = ("data_off", "data_len", "pkt_len", "packet_type", "priv", "priv_i
 class Layout(ctypes.Structure):
     """struct gr_hip_mbuf_layout (include/grout_hip.h)"""
     _fields_ = [(k, ctypes.c_uint16) for k in _LAYOUT_U16] + [
-        ("n_ifaces", ctypes.c_uint32), ("n_nh", ctypes.c_uint32), ("ifaces", ctypes.c_void_p), ("nh", ctypes.c_void_p)]
+        ("n_ifaces", ctypes.c_uint32), ("n_nh", ctypes.c_uint32), ("ifaces", ctypes.c_void_p), ("nh", ctypes.c_void_p),
+        ("buf_addr", ctypes.c_uint16), ("ol_flags", ctypes.c_uint16), ("rss", ctypes.c_uint16),
+        ("iface_id", ctypes.c_uint16), ("ck_mask", ctypes.c_uint64), ("ck_good", ctypes.c_uint64),
+        ("ck_bad", ctypes.c_uint64)]
 
 
 class Direct(ctypes.Structure):
@@ -206,6 +209,11 @@ class Direct(ctypes.Structure):
 GROUT_LAYOUT = dict(data_off=16, data_len=40, pkt_len=36, packet_type=32, priv=128, priv_iface=16, priv_vlan_id=24,
                     priv_domain=24, priv_eth_nh=32, priv_l3_nh=24)
 IF_OBJ, NH_OBJ = 0x7F0000001000, 0x7F0000100000  # registry "pointers": base + id
+# what the staging reads: rte_mbuf buf_addr, ol_flags, hash.rss (rte_mbuf_core.h)
+# and RTE_MBUF_F_RX_IP_CKSUM_MASK / _GOOD / _BAD; iface_id: where the fake iface
+# objects below keep their id
+GROUT_STAGE = dict(buf_addr=0, ol_flags=24, rss=44, iface_id=8, ck_mask=(1 << 4) | (1 << 7), ck_good=1 << 7,
+                   ck_bad=1 << 4)
 
 
 def test_apply_onto_mbufs_equals_views():
@@ -273,6 +281,79 @@ def test_apply_onto_mbufs_equals_views():
     assert (mem[:, 254:256] == 0xA5).all()
     # frames: rewritten as the view-based hand-back rewrote them
     assert np.array_equal(bufs2[ok][:, :abi.LINE], bufs[ok][:, :abi.LINE])
+
+
+def test_stage_from_mbufs_equals_views():
+    """gr_hip_node_append_mbufs' one pass (gr_node_stage_mbufs): reading
+    grout's rte_mbufs through the layout gives the views the grout node used
+    to build (frame at buf_addr + data_off, lengths, packet_type, rss, the
+    iface id through mbuf_data.iface, vlan_id, the checksum status from
+    ol_flags), the same placement (walks cut at the burst, pads before a walk
+    that would straddle a tile) and the same staged lines and metadata as
+    gr_hip_node_layout + gr_hip_node_stage on those views, over appends of
+    1 to 300 mbufs."""
+    t, _ = SC.corpus_topology()
+    fr, me, _ = SC.corpus_arrays()
+    keep = ((me["vlan_ck"] >> 12) & 3) != 3  # no ol_flags value gives the corpus's status 3
+    fr, me = np.concatenate([fr[keep]] * 8), np.concatenate([me[keep]] * 8)
+    n = len(me)
+    rng = np.random.default_rng(7)
+    bufs, ref = mbufs_for(fr, me)
+    ref["packet_type"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    ref["rss"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    L, G = GROUT_LAYOUT, GROUT_STAGE
+    mem = np.zeros((n, 256), dtype=np.uint8)
+    U16, U32, U64 = mem.view(np.uint16), mem.view(np.uint32), mem.view(np.uint64)
+    U64[:, G["buf_addr"] // 8] = ref["frame"] - RX_DATA_OFF
+    U16[:, L["data_off"] // 2] = RX_DATA_OFF
+    U16[:, L["data_len"] // 2] = ref["data_len"]
+    U32[:, L["pkt_len"] // 4] = ref["pkt_len"]
+    U32[:, L["packet_type"] // 4] = ref["packet_type"]
+    U32[:, G["rss"] // 4] = ref["rss"]
+    ck_bits = np.array([0, G["ck_bad"], G["ck_good"]], dtype=np.uint64)
+    U64[:, G["ol_flags"] // 8] = ck_bits[ref["ck"]] | np.uint64(1 << 40)  # other flags set too
+    ifobj = np.zeros((t.max_ifaces, 64), dtype=np.uint8)
+    ifobj.view(np.uint16)[:, G["iface_id"] // 2] = np.arange(t.max_ifaces)
+    ifp = np.where(ref["iface"] != 0, ifobj.ctypes.data + 64 * ref["iface"].astype(np.uint64), 0).astype(np.uint64)
+    U64[:, (L["priv"] + L["priv_iface"]) // 8] = ifp
+    U16[:, (L["priv"] + L["priv_vlan_id"]) // 2] = ref["vlan_id"]
+    ptrs = (mem.ctypes.data + np.arange(n, dtype=np.uint64) * 256).astype(np.uint64)
+    lay = Layout(**L, **G, n_ifaces=0, n_nh=0, ifaces=None, nh=None)
+    # appends of 1 .. 300 mbufs; burst 256 cuts the longer ones
+    sizes, i = [], 0
+    while i < n:
+        k = int(min(n - i, rng.choice([1, 3, 7, 40, 64, 65, 100, 256, 300])))
+        sizes.append((i, k))
+        i += k
+    ref["flags"] = 0
+    for i, k in sizes:
+        ref["flags"][i] = abi.MBUF_F_WALK
+    H = abi.hip()
+    pos_ref = np.zeros(n, dtype=np.uint32)
+    end = H.gr_hip_node_layout(ref.ctypes.data, n, 256, pos_ref.ctypes.data)
+    assert end > n  # pads were needed
+    lines_ref = np.full((end, abi.LINE), 0xEE, dtype=np.uint8)
+    meta_ref = np.full(end * abi.META_DT.itemsize, 0xEE, dtype=np.uint8).view(abi.META_DT)
+    abi.check("gr_hip_node_stage", H.gr_hip_node_stage(ref.ctypes.data, n, 256, pos_ref.ctypes.data,
+                                                         lines_ref.ctypes.data, meta_ref.ctypes.data))
+    fn = ctypes.CDLL(abi.LIB_HIP).gr_node_stage_mbufs
+    P = ctypes.c_void_p
+    fn.argtypes = [P, ctypes.c_uint32, P, ctypes.c_uint32, ctypes.c_uint64, P, P, P, P]
+    fn.restype = ctypes.c_uint64
+    v = np.zeros(n, dtype=abi.MBUF_DT)
+    pos = np.zeros(n, dtype=np.uint32)
+    lines = np.full((end, abi.LINE), 0xEE, dtype=np.uint8)
+    meta = np.full(end * abi.META_DT.itemsize, 0xEE, dtype=np.uint8).view(abi.META_DT)
+    p = 0
+    for i, k in sizes:
+        p = fn(ptrs.ctypes.data + 8 * i, k, ctypes.addressof(lay), 256, p, v.ctypes.data + v.itemsize * i,
+               pos.ctypes.data + 4 * i, lines.ctypes.data, meta.ctypes.data)
+    assert p == end
+    for f in ref.dtype.names:
+        assert np.array_equal(v[f], ref[f]), f
+    assert np.array_equal(pos, pos_ref)
+    assert np.array_equal(lines, lines_ref) and np.array_equal(meta, meta_ref)
+    assert ((meta["vlan_ck"] & 0x4000) != 0).sum() == sum(1 + (k - 1) // 256 for _, k in sizes)  # one walk flag per cut
 
 
 def test_apply_counts_ifaces_where_grout_does():

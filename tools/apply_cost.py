@@ -36,7 +36,10 @@ OBJ, FRAME = 2304, 320  # object size (rte_mbuf 128 + priv 64 + headroom 128 + d
 
 class Layout(ctypes.Structure):
     _fields_ = [(k, ctypes.c_uint16) for k in LAYOUT] + [
-        ("n_ifaces", ctypes.c_uint32), ("n_nh", ctypes.c_uint32), ("ifaces", ctypes.c_void_p), ("nh", ctypes.c_void_p)]
+        ("n_ifaces", ctypes.c_uint32), ("n_nh", ctypes.c_uint32), ("ifaces", ctypes.c_void_p), ("nh", ctypes.c_void_p),
+        ("buf_addr", ctypes.c_uint16), ("ol_flags", ctypes.c_uint16), ("rss", ctypes.c_uint16),
+        ("iface_id", ctypes.c_uint16), ("ck_mask", ctypes.c_uint64), ("ck_good", ctypes.c_uint64),
+        ("ck_bad", ctypes.c_uint64)]
 
 
 class Direct(ctypes.Structure):

@@ -36,7 +36,6 @@ def main():
     ap.add_argument("--pin", type=int, default=0, help="1: frames by address (node_ptrs)")
     ap.add_argument("--depths", default="1,2")
     ap.add_argument("--rx-touch", default="0", help="harness port_rx leaves mbuf and frame cached (PMD + DDIO): 0,1")
-    ap.add_argument("--nt", default="0", help="\"node_nt\" knob values to alternate (non-temporal staging): 0,1")
     ap.add_argument("--max-delay-us", type=float, default=20_000.0, help="the node's hold time")
     args = ap.parse_args()
 
@@ -61,11 +60,9 @@ def main():
     fr = np.ascontiguousarray(fr)
     me = np.ascontiguousarray(me)
     L.gh_set_rx_touch.argtypes = [ctypes.c_int]
-    variants = [(int(d), int(t), int(x)) for d in args.depths.split(",") for t in args.rx_touch.split(",")
-                for x in args.nt.split(",")]
+    variants = [(int(d), int(t)) for d in args.depths.split(",") for t in args.rx_touch.split(",")]
     for rep in range(args.reps + 1):
-        for depth, touch, nt in variants:
-            fp.tune("node_nt", nt)
+        for depth, touch in variants:
             assert L.gpu_fwd4_set_depth(depth) == 0
             L.gh_set_rx_touch(touch)
             assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, len(me)) == 0
@@ -89,7 +86,7 @@ def main():
             names = ["accumulate", "start", "finish", "deliver"]
             per = {k: round(float(v) / len(me), 2) for k, v in zip(names, ph)}
             per["rest_of_walk"] = round(dt * 1e9 / len(me) - sum(per.values()), 2)
-            print(json.dumps({"batch": args.batch, "max_delay_us": args.max_delay_us, "depth": depth, "rx_touch": touch, "node_nt": nt,
+            print(json.dumps({"batch": args.batch, "max_delay_us": args.max_delay_us, "depth": depth, "rx_touch": touch,
                               "mbufs": len(me), "graph_walks": walks,
                               "node_batches": int(wi["batches"] - wi0["batches"]), "max_batch": int(wi["max_batch"]),
                               "ms": round(dt * 1e3, 2), "mpps": round(len(me) / dt / 1e6, 1),

@@ -30,7 +30,6 @@ def main():
     ap.add_argument("--batch", type=int, default=15360)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--rx-touch", type=int, default=1, help="port_rx writes the mbuf and touches the frame (PMD + DDIO)")
-    ap.add_argument("--nt", type=int, default=0, help="\"node_nt\": non-temporal staging")
     args = ap.parse_args()
     threads = [int(x) for x in args.threads.split(",")]
 
@@ -51,7 +50,6 @@ def main():
     fp = G.FanOutPath(L)
     topo = T.config_fullview()
     fp.load(topo)
-    fp.tune("node_nt", args.nt)
     n = kmax * args.per_thread
     fr, me = S.stream(n, 0x67720002, routes=topo.route_array())
     fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
@@ -69,7 +67,7 @@ def main():
             assert rr == 0, rr
             best.append(s.value)
         t = float(np.median(best))
-        print(json.dumps({"threads": k, "gpus": 1, "mbufs": m, "batch": args.batch, "rx_touch": args.rx_touch, "node_nt": args.nt,
+        print(json.dumps({"threads": k, "gpus": 1, "mbufs": m, "batch": args.batch, "rx_touch": args.rx_touch,
                           "ms": round(t * 1e3, 2), "mpps_aggregate": round(m / t / 1e6, 1),
                           "mpps_per_worker": round(m / t / 1e6 / k, 1),
                           "cpu_ns_per_pkt_per_worker": round(t * 1e9 * k / m, 1)}), flush=True)
