@@ -428,6 +428,56 @@ static inline uint8_t to_mbuf(struct gr_node_direct *d, uint32_t i, const struct
 	return v.edge;
 }
 
+// The hand-back onto the mbufs of the packet a forwarding plane sees most:
+// forwarded to port_output, untagged on ingress, with lines staged. It is
+// the general loop below specialised for that case (depth 6 of either
+// family: no adj, iface_output's VLAN tag from the nexthop's iface, rx / tx
+// counted where grout counts them, the mbuf and private data as to_mbuf
+// writes them); returns false for any other packet, untouched.
+static inline bool port_output_fast(struct gr_node_direct *d, uint32_t i, const struct gr_hip_mbuf &b,
+				    const struct gr_hip_verdict &v, const uint8_t *line, const struct gr_hip_iface *ifaces,
+				    uint32_t n_ifaces, const struct gr_hip_nh *nh, uint32_t n_nh,
+				    struct gr_hip_iface_stats *ifst, uint32_t n_ifst, bool &ip6) {
+	if (v.edge != GR_HIP_E_PORT_OUTPUT || b.vlan_id != 0 || v.nh == 0 || v.nh >= n_nh || nh == nullptr)
+		return false;
+	ip6 = line[12] == 0x86 && line[13] == 0xdd; // RTE_ETHER_TYPE_IPV6
+	const struct gr_hip_mbuf_layout &L = *d->lay;
+	const void *ifp = reg_get(L.ifaces, L.n_ifaces, v.iface);
+	const uint16_t oif = nh[v.nh].iface_id;
+	if (ifst != nullptr) {
+		count(ifst, n_ifst, b.iface, false, b.pkt_len);
+		count(ifst, n_ifst, oif, true, b.pkt_len);
+		if (v.iface != oif)
+			count(ifst, n_ifst, v.iface, true, b.pkt_len);
+	}
+	if (ifp == nullptr && v.iface != 0) {
+		d->stale++; // see to_mbuf
+		d->edges[i] = GR_HIP_E_IP_OUTPUT_ERROR;
+		return true;
+	}
+	const uint32_t len = b.data_len < 26 ? b.data_len : 26; // bytes 0-25: see the general loop
+	uint8_t *fr = static_cast<uint8_t *>(b.frame);
+	if (len >= 16) {
+		memcpy(fr, line, 16);
+		memcpy(fr + len - 16, line + len - 16, 16);
+	} else {
+		memcpy(fr, line, len);
+	}
+	uint16_t vid = 0;
+	if (oif < n_ifaces && ifaces != nullptr && ifaces[oif].id == oif && ifaces[oif].type == GR_HIP_IFACE_TYPE_VLAN)
+		vid = ifaces[oif].vlan_id;
+	uint8_t *mb = static_cast<uint8_t *>(d->mbufs[i]);
+	put<uint16_t>(mb, L.data_off, b.data_off); // eth_output's prepend undid ip_input's adj
+	put<uint16_t>(mb, L.data_len, b.data_len);
+	put<uint32_t>(mb, L.pkt_len, b.pkt_len);
+	put<uint32_t>(mb, L.packet_type, ip6 ? GR_HIP_PTYPE_L3_IPV6 : GR_HIP_PTYPE_L3_IPV4);
+	uint8_t *priv = mb + L.priv;
+	put<const void *>(priv, L.priv_iface, ifp);
+	put<uint16_t>(priv, L.priv_vlan_id, vid);
+	d->edges[i] = GR_HIP_E_PORT_OUTPUT;
+	return true;
+}
+
 extern "C" int gr_hip_node_apply(
 	struct gr_hip_mbuf *m,
 	uint32_t n,
@@ -498,13 +548,23 @@ extern "C" int gr_node_apply_ex(
 	for (uint32_t i = 0; i < n; i++) {
 		if (i + AHEAD < n)
 			prefetch_for_apply(m, i + AHEAD, direct);
+		const uint32_t at = pos != nullptr ? pos[i] : i;
+		const struct gr_hip_verdict &v = verdicts[at];
+		bool fast6;
+		if (direct != nullptr && L != nullptr
+		    && port_output_fast(direct, i, m[i], v, L + (size_t)at * line_stride, ifaces, n_ifaces, nh, n_nh, ifst,
+					n_ifst, fast6)) {
+			if (i - start < WALK_MAX)
+				fam[i - start] = fast6 ? 2 : 1;
+			ended[fast6][6]++;
+			goto walk_end;
+		}
+		{
 		// direct: the view is only read, the mbuf gets the result below
 		struct gr_hip_mbuf copy;
 		if (direct != nullptr)
 			copy = m[i];
 		struct gr_hip_mbuf &b = direct != nullptr ? copy : m[i];
-		const uint32_t at = pos != nullptr ? pos[i] : i;
-		const struct gr_hip_verdict &v = verdicts[at];
 		const uint32_t len0 = b.pkt_len; // as iface_input / iface_output count it
 		const uint16_t iface0 = b.iface, vlan0 = b.vlan_id; // as port_rx left them
 		// lines NULL: the GPU rewrote the frames in place already
@@ -592,6 +652,8 @@ extern "C" int gr_node_apply_ex(
 		}
 		if (direct != nullptr)
 			direct->edges[i] = to_mbuf(direct, i, b, v, node);
+		}
+	walk_end:
 		if (i + 1 == n || walk_start(m, i + 1, start, burst)) { // this graph walk ends here
 			if (walk_nomac && i + 1 - start > 64)
 				eth_output_walk(m, start, i + 1, pos, verdicts, fam, ifaces, n_ifaces, nh, n_nh);

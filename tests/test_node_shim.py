@@ -227,7 +227,7 @@ def test_apply_onto_mbufs_equals_views():
     fr, me, lab = SC.corpus_arrays()
     lines, v, _, want, _ = oracle.Oracle(t).process_mbufs(fr, me)
     bufs, m_view = mbufs_for(fr, me)
-    apply_counting(m_view, lines, v, t)  # the reference: onto the views
+    ns_view, st_view = apply_counting(m_view, lines, v, t)  # the reference: onto the views
     bufs2, m = mbufs_for(fr, me)
     m0 = m.copy()
     n = len(m)
@@ -248,8 +248,11 @@ def test_apply_onto_mbufs_equals_views():
     lay = Layout(**L, n_ifaces=len(reg_if), n_nh=len(reg_nh), ifaces=reg_if.ctypes.data, nh=reg_nh.ctypes.data)
     edges = np.full(n, 0xEE, dtype=np.uint8)
     d = Direct(mbufs=ptrs.ctypes.data, lay=ctypes.addressof(lay), edges=edges.ctypes.data)
-    apply_counting(m, lines, v, t, direct=ctypes.addressof(d))
+    ns_d, st_d = apply_counting(m, lines, v, t, direct=ctypes.addressof(d))
     assert np.array_equal(m, m0)  # the views: read only
+    # the same per-node and per-iface counters (port_output_fast counts as the general loop)
+    assert np.array_equal(ns_d, ns_view) and np.array_equal(st_d, st_view)
+    assert (v["edge"] == abi.EDGE["port_output"]).sum() > 20
     U16, U32, U64 = mem.view(np.uint16), mem.view(np.uint32), mem.view(np.uint64)
     N = {k: i for i, k in enumerate(abi.NODE_NAMES)}
     six = (lines[:, 12] == 0x86) & (lines[:, 13] == 0xDD)
