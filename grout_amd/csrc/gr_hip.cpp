@@ -177,6 +177,7 @@ struct node_slot {
 	uint32_t na = 0, p = 0;
 	// appended from the mbufs (gr_hip_node_append_mbufs): the views are these
 	bool own = false;
+	bool kcount = false; // its kernel counts the per-iface counters (not the hand-back)
 	std::vector<gr_hip_mbuf> views;
 };
 
@@ -201,9 +202,17 @@ struct gr_hip_queue {
 	uint32_t nw_head, nw_count;
 	uint8_t *d_pad; // the zeroed line pad slots of a frames-by-address batch point at
 	uint32_t *h_err, *d_err; // kernel error word (pinned, mapped): a workgroup gave up
-	// per-iface counters of the node walks handed back (gr_hip_node_iface_stats),
-	// counted on the host where grout counts them
+	// per-iface counters of the node walks handed back (gr_hip_node_iface_stats):
+	// what the kernels counted in d_stats for the walks launched with counters
+	// (folded in through a pinned snapshot of d_stats), and what the host
+	// hand-back counted for the others
 	std::vector<gr_hip_iface_stats> node_if;
+	std::vector<gr_hip_iface_stats> kern_seen; // d_stats totals folded into node_if so far
+	gr_hip_iface_stats *snap = nullptr; // pinned [FWD4_STAT_SHARDS][snap_w] copy of d_stats
+	uint32_t snap_cap = 0, snap_w = 0; // ifaces per shard: allocated, in the copy in flight
+	hipEvent_t snap_ev = nullptr;
+	bool snap_pending = false;
+	uint64_t node_counted = 0, snap_counted = 0; // node walks launched with counters; covered by a snapshot
 };
 
 struct host_range { // gr_hip_host_register
@@ -1839,6 +1848,7 @@ extern "C" int gr_hip_queue_create(gr_hip_ctx_t *c, void *stream, gr_hip_queue_t
 	}
 	try {
 		q->node_if.assign(c->max_ifaces, gr_hip_iface_stats{0, 0, 0, 0});
+		q->kern_seen.assign(c->max_ifaces, gr_hip_iface_stats{0, 0, 0, 0});
 	} catch (...) {
 		return -ENOMEM; // (not reached in practice: a few tens of KiB)
 	}
@@ -1887,6 +1897,9 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 	hipEventDestroy(q->retire);
 	hipEventDestroy(q->sync_ev);
 	hipFree(q->d_stats);
+	if (q->snap_ev != nullptr)
+		hipEventDestroy(q->snap_ev);
+	hipHostFree(q->snap);
 	hipHostFree(q->h_err);
 	for (node_slot &w : q->nw) {
 		hipEventDestroy(w.done);
@@ -2560,6 +2573,7 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 	w.by_addr = false;
 	w.sync = true;
 	w.r = 0;
+	w.kcount = false;
 	if (n == 0) { // nothing to send: finishes at once
 		q->nw_count++;
 		return 0;
@@ -2623,6 +2637,10 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 		HCK(hipEventRecord(w.done, q->s));
 		w.sync = false;
 	}
+	// the kernel counted the walk's packets per iface (launch's "stats" variant)
+	w.kcount = c->stats_on && q->d_stats != nullptr;
+	if (w.kcount)
+		q->node_counted++;
 	lap(GR_HIP_NODE_PROF_RECORD);
 	// the lock covers the enqueue, not the wait: control-plane writers
 	// (FIB publication) are not held behind the walk's GPU time
@@ -2681,9 +2699,11 @@ static int node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np,
 	{
 		std::shared_lock<std::shared_mutex> lk(c->mu); // the hand-back reads the iface and nexthop mirrors
 		const gr_node_vlans vl = {c->vlan_keys_h.data(), c->vlan_vals_h.data(), (uint32_t)c->vlan_keys_h.size()};
+		// the per-iface counters: the kernel's (gr_hip_node_iface_stats folds
+		// them in), or the hand-back's when the kernel ran without them
 		r = gr_node_apply_ex(w.m, w.n, w.burst, w.pos.data(), w.by_addr ? nullptr : w.out, GR_HIP_PREFIX, w.v,
 				     c->ifaces.data(), c->max_ifaces, c->nh.data(), (uint32_t)c->nh.size(), stats, &vl,
-				     q->node_if.data(), (uint32_t)q->node_if.size(), direct);
+				     w.kcount ? nullptr : q->node_if.data(), (uint32_t)q->node_if.size(), direct);
 	}
 	node_prof_ns[GR_HIP_NODE_PROF_FIN_APPLY] += prof_now() - t_prof;
 	return r < 0 ? r : (int)unfinished;
@@ -2705,9 +2725,97 @@ extern "C" int gr_hip_node_finish_mbufs(gr_hip_queue_t *q, void *const *mbufs, c
 	return r;
 }
 
+// The d_stats totals of a complete snapshot (or of `all`, a whole copy
+// [FWD4_STAT_SHARDS][max_ifaces]) folded into node_if: what the kernels
+// counted since the last fold. (gr_hip_queue_stats' reset zeroes d_stats:
+// the totals then restart below what was folded.)
+static void kern_fold(gr_hip_queue_t *q, const gr_hip_iface_stats *all, uint32_t w, uint32_t pitch) {
+	auto since = [](uint64_t now, uint64_t seen) { return now >= seen ? now - seen : now; };
+	for (uint32_t i = 0; i < w; i++) {
+		gr_hip_iface_stats t = {0, 0, 0, 0};
+		for (uint32_t s = 0; s < FWD4_STAT_SHARDS; s++) {
+			const gr_hip_iface_stats &x = all[(size_t)s * pitch + i];
+			t.rx_packets += x.rx_packets;
+			t.rx_bytes += x.rx_bytes;
+			t.tx_packets += x.tx_packets;
+			t.tx_bytes += x.tx_bytes;
+		}
+		gr_hip_iface_stats &seen = q->kern_seen[i], &acc = q->node_if[i];
+		acc.rx_packets += since(t.rx_packets, seen.rx_packets);
+		acc.rx_bytes += since(t.rx_bytes, seen.rx_bytes);
+		acc.tx_packets += since(t.tx_packets, seen.tx_packets);
+		acc.tx_bytes += since(t.tx_bytes, seen.tx_bytes);
+		seen = t;
+	}
+}
+
+// Copy d_stats' first snap_w ifaces of every shard into the pinned snapshot
+// behind the queue's work, and mark it pending.
+static int snap_start(gr_hip_queue_t *q) {
+	gr_hip_ctx *c = q->ctx;
+	std::shared_lock<std::shared_mutex> lk(c->mu); // the iface mirror
+	uint32_t w = 0; // the ifaces in use: ids below the highest one pushed
+	for (uint32_t i = c->max_ifaces; i-- > 1;)
+		if (c->ifaces[i].id != 0) {
+			w = i + 1;
+			break;
+		}
+	if (w == 0)
+		w = 1;
+	if (q->snap_ev == nullptr)
+		HCK(hipEventCreateWithFlags(&q->snap_ev, hipEventDisableTiming));
+	if (w > q->snap_cap) {
+		hipHostFree(q->snap);
+		q->snap = nullptr;
+		q->snap_cap = 0;
+		if (hipHostMalloc((void **)&q->snap, sizeof(gr_hip_iface_stats) * FWD4_STAT_SHARDS * w,
+				  hipHostMallocDefault) != hipSuccess) {
+			(void)hipGetLastError();
+			return -ENOMEM;
+		}
+		q->snap_cap = w;
+	}
+	const size_t row = sizeof(gr_hip_iface_stats);
+	HCK(hipMemcpy2DAsync(q->snap, w * row, q->d_stats, (size_t)c->max_ifaces * row, w * row, FWD4_STAT_SHARDS,
+			     hipMemcpyDeviceToHost, q->s));
+	HCK(hipEventRecord(q->snap_ev, q->s));
+	q->snap_w = w;
+	q->snap_pending = true;
+	q->snap_counted = q->node_counted;
+	return 0;
+}
+
 extern "C" int gr_hip_node_iface_stats(gr_hip_queue_t *q, struct gr_hip_iface_stats *st, uint32_t max, int reset) {
 	if (q == nullptr || (st == nullptr && max))
 		return -EINVAL;
+	// the kernels' counts: a snapshot of d_stats behind the walks launched so
+	// far, folded when it has landed (a poll). With no walk in flight the
+	// counts are final: wait for the snapshot, so that the result is exact
+	// (a housekeeping tick with walks on the GPU reports them at a later one).
+	if (q->d_stats != nullptr && (q->snap_pending || q->snap_counted != q->node_counted)) {
+		const bool idle = q->nw_count == 0;
+		hipSetDevice(q->ctx->dev);
+		for (int pass = 0; pass < 2; pass++) {
+			if (q->snap_pending) {
+				if (idle)
+					HCK(hipEventSynchronize(q->snap_ev));
+				const hipError_t e = idle ? hipSuccess : hipEventQuery(q->snap_ev);
+				if (e == hipSuccess) {
+					kern_fold(q, q->snap, q->snap_w, q->snap_w);
+					q->snap_pending = false;
+				} else if (e != hipErrorNotReady) {
+					return -EIO;
+				}
+				(void)hipGetLastError();
+			}
+			if (q->snap_pending || q->snap_counted == q->node_counted)
+				break;
+			if (const int r = snap_start(q))
+				return r;
+			if (!idle)
+				break; // folded at a later call
+		}
+	}
 	const uint32_t m = max < q->node_if.size() ? max : (uint32_t)q->node_if.size();
 	if (m)
 		memcpy(st, q->node_if.data(), (size_t)m * sizeof(*st));
@@ -2781,8 +2889,17 @@ extern "C" int gr_hip_queue_stats(gr_hip_queue_t *q, struct gr_hip_iface_stats *
 			st[i].tx_bytes += x.tx_bytes;
 		}
 	}
-	if (reset)
+	if (reset) {
+		// node walks' counts not folded yet go to node_if before the zeroing
+		// (a queue of node walks and plain submits at once reports both there)
+		if (q->snap_counted != q->node_counted || q->snap_pending) {
+			kern_fold(q, all.data(), c->max_ifaces, c->max_ifaces);
+			q->snap_pending = false;
+			q->snap_counted = q->node_counted;
+		}
+		std::fill(q->kern_seen.begin(), q->kern_seen.end(), gr_hip_iface_stats{0, 0, 0, 0});
 		HCK(hipMemsetAsync(q->d_stats, 0, all.size() * sizeof(gr_hip_iface_stats), q->s));
+	}
 	return 0;
 }
 

@@ -269,8 +269,8 @@ class Queue:
         return st
 
     def node_iface_stats(self, reset=False):
-        """Per-iface counters of the node walks handed back, counted on the
-        host where grout counts them (what the grout node folds into grout's
+        """Per-iface counters of the node walks (the kernels' counts, or the
+        hand-back's with "stats" off; what the grout node folds into grout's
         iface_stats)."""
         st = np.zeros(self.fp.max_ifaces, dtype=abi.STATS_DT)
         check("gr_hip_node_iface_stats", self.lib.gr_hip_node_iface_stats(self._h, ptr(st), len(st),

@@ -761,16 +761,20 @@ int gr_hip_node_discard(gr_hip_queue_t *);
 // Walks in flight on the queue; *ready (optional) = 1 when the oldest one's
 // GPU work has completed (its finish will not wait).
 int gr_hip_node_pending(gr_hip_queue_t *, int *ready);
-// Per-iface rx / tx counters of the walks handed back on the queue since the
-// last reset, counted on the host during the hand-back where grout counts
-// them: rx in iface_input past its admin-down and unknown-VLAN drops (the
-// VLAN sub-interface and its parent), tx in iface_output past its no-parent
-// and admin-down drops (the egress iface and a VLAN's parent)
-// (modules/infra/datapath/iface_input.c:93-95, iface_output.c:103-105,
-// rxtx.h:84-117). No GPU call: the grout node folds them into grout's
-// per-lcore iface_stats at its housekeeping tick (gpu_fwd4_stats_flush).
-// Call from the thread that drives the queue's walks. `stats` receives
-// max_ifaces entries, indexed by iface id.
+// Per-iface rx / tx counters of the queue's node walks since the last reset,
+// where grout counts them: rx in iface_input past its admin-down and
+// unknown-VLAN drops (the VLAN sub-interface and its parent), tx in
+// iface_output past its no-parent and admin-down drops (the egress iface and
+// a VLAN's parent) (modules/infra/datapath/iface_input.c:93-95,
+// iface_output.c:103-105, rxtx.h:84-117). The kernels count them (the
+// "stats" knob, default on; with it off the hand-back counts them on the
+// host): this call folds in a copy of the queue's device counters taken
+// behind the walks launched so far, without waiting for it while walks are
+// in flight (it lands by a later call), and waiting for it when none is, so
+// that the counts are then exact. The grout node folds the result into
+// grout's per-lcore iface_stats at its housekeeping tick
+// (gpu_fwd4_stats_flush). Call from the thread that drives the queue's
+// walks. `stats` receives max_ifaces entries, indexed by iface id.
 int gr_hip_node_iface_stats(gr_hip_queue_t *, struct gr_hip_iface_stats *stats, uint32_t max_ifaces, int reset);
 
 // Measurement: nanoseconds gr_hip_node_start (append + send) and

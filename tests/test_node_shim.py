@@ -397,26 +397,36 @@ def test_apply_fullview_stream():
 
 
 @pytest.mark.gpu
-def test_node_process_gpu(fastpath):
+@pytest.mark.parametrize("kernel_counters", [1, 0])
+def test_node_process_gpu(fastpath, kernel_counters):
     """The whole node walk on the GPU (stage, fwd4_host, apply) against the
     oracle's mbufs, corpus and a one-route stream. The node stages 64-byte
     header lines, so the oracle runs lines-only: an IPv4 header that does not
-    fit is punted to grout's CPU nodes, mbuf untouched."""
+    fit is punted to grout's CPU nodes, mbuf untouched. The node's per-iface
+    counters are the kernel's (folded in from the queue's device counters),
+    or, with the kernel's counters off ("stats" 0), the hand-back's."""
     from golden_util import fresh_fastpath_state
-    for topo, fr, me, lab in [(SC.corpus_topology()[0],) + tuple(SC.corpus_arrays()),
-                              (T.config_single_route(),) + S.stream(100_003, 0xB0B, dst_range=(
-                                  T.ip4("16.1.0.0"), T.ip4("16.1.255.255"))) + (None,)]:
-        fresh_fastpath_state(fastpath, topo)
-        lines, v, st, want, ns_want = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
-        bufs, m = mbufs_for(fr, me)
-        q = fastpath.queue()
-        ns = q.node_process(m, burst=64)
-        compare_mbufs(m, want, bufs, lines, lab)
-        assert np.array_equal(ns["packets"], ns_want["packets"])
-        assert np.array_equal(ns["calls"], ns_want["calls"])
-        assert np.array_equal(q.stats(), st)  # the iface counters of the same packets
-        assert np.array_equal(q.node_iface_stats(), st)  # and the hand-back's, counted on the host
-        q.close()
+    fastpath.tune("stats", kernel_counters)
+    try:
+        for topo, fr, me, lab in [(SC.corpus_topology()[0],) + tuple(SC.corpus_arrays()),
+                                  (T.config_single_route(),) + S.stream(100_003, 0xB0B, dst_range=(
+                                      T.ip4("16.1.0.0"), T.ip4("16.1.255.255"))) + (None,)]:
+            fresh_fastpath_state(fastpath, topo)
+            lines, v, st, want, ns_want = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
+            bufs, m = mbufs_for(fr, me)
+            q = fastpath.queue()
+            ns = q.node_process(m, burst=64)
+            compare_mbufs(m, want, bufs, lines, lab)
+            assert np.array_equal(ns["packets"], ns_want["packets"])
+            assert np.array_equal(ns["calls"], ns_want["calls"])
+            if kernel_counters:
+                assert np.array_equal(q.stats(), st)  # the iface counters of the same packets
+            else:
+                assert not q.stats()["rx_packets"].any()
+            assert np.array_equal(q.node_iface_stats(), st)  # what the node reports, either way
+            q.close()
+    finally:
+        fastpath.tune("stats", 1)
 
 
 @pytest.mark.gpu
