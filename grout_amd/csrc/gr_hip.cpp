@@ -183,6 +183,10 @@ struct node_slot {
 
 } // namespace
 
+// gr_hip_node_prof's clocks run (the "node_prof" knob): off by default, each
+// read costs tens of nanoseconds per append
+static std::atomic<bool> node_prof_on{false};
+
 struct gr_hip_queue {
 	gr_hip_ctx *ctx;
 	hipStream_t s;
@@ -2056,6 +2060,8 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		c->fib_fmt = value;
 	} else if (strcmp(key, "node_ptrs") == 0) {
 		c->node_ptrs = value != 0;
+	} else if (strcmp(key, "node_prof") == 0) { // process-wide: gr_hip_node_prof's clocks
+		node_prof_on.store(value != 0);
 	} else if (strcmp(key, "untimed") == 0) {
 		c->untimed = value != 0;
 	} else if (strcmp(key, "time_every") == 0) { // sample the launch timing: less event overhead
@@ -2470,7 +2476,8 @@ extern "C" int gr_hip_node_append(gr_hip_queue_t *q, const struct gr_hip_mbuf *m
 		return (int)w.p;
 	if (q->ctx->fail_appends.load(std::memory_order_relaxed) > 0 && q->ctx->fail_appends.fetch_sub(1) > 0)
 		return -ENOMEM; // as a failed slot_grow: the slot is left as it was
-	uint64_t t_prof = prof_now();
+	const bool prof = node_prof_on.load(std::memory_order_relaxed);
+	const uint64_t t_prof = prof ? prof_now() : 0;
 	if (w.pos.size() < (size_t)w.na + n)
 		w.pos.resize(std::max<size_t>((size_t)w.na + n, 2 * w.pos.size()));
 	uint32_t *pos = w.pos.data() + w.na;
@@ -2488,7 +2495,8 @@ extern "C" int gr_hip_node_append(gr_hip_queue_t *q, const struct gr_hip_mbuf *m
 		return r;
 	w.na += n;
 	w.p = (uint32_t)p;
-	node_prof_ns[GR_HIP_NODE_PROF_STAGE] += prof_now() - t_prof;
+	if (prof)
+		node_prof_ns[GR_HIP_NODE_PROF_STAGE] += prof_now() - t_prof;
 	return (int)p;
 }
 
@@ -2511,7 +2519,8 @@ extern "C" int gr_hip_node_append_mbufs(gr_hip_queue_t *q, void *const *mbufs, u
 		return (int)w.p;
 	if (q->ctx->fail_appends.load(std::memory_order_relaxed) > 0 && q->ctx->fail_appends.fetch_sub(1) > 0)
 		return -ENOMEM; // as a failed slot_grow: the slot is left as it was
-	uint64_t t_prof = prof_now();
+	const bool prof = node_prof_on.load(std::memory_order_relaxed);
+	const uint64_t t_prof = prof ? prof_now() : 0;
 	const uint64_t p = gr_node_walk_end(w.p, n, burst); // the cuts do not depend on the mbufs
 	if (p > INT32_MAX)
 		return -E2BIG;
@@ -2530,7 +2539,8 @@ extern "C" int gr_hip_node_append_mbufs(gr_hip_queue_t *q, void *const *mbufs, u
 			    w.lines_in ? w.lines : nullptr, w.meta);
 	w.na += n;
 	w.p = (uint32_t)p;
-	node_prof_ns[GR_HIP_NODE_PROF_STAGE] += prof_now() - t_prof;
+	if (prof)
+		node_prof_ns[GR_HIP_NODE_PROF_STAGE] += prof_now() - t_prof;
 	return (int)p;
 }
 
@@ -2693,7 +2703,7 @@ static int node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np,
 	node_prof_ns[GR_HIP_NODE_PROF_FIN_WAIT] += t - t_prof;
 	// packets a kernel that gave up never reached go back to grout's CPU
 	// nodes, the others are handed back as usual
-	const uint32_t unfinished = node_unfinished(w.m, w.n, w.pos.data(), w.v);
+	const uint32_t unfinished = r == 0 ? 0 : node_unfinished(w.m, w.n, w.pos.data(), w.v); // 0: none gave up
 	t_prof = prof_now();
 	node_prof_ns[GR_HIP_NODE_PROF_FIN_SCAN] += t_prof - t;
 	{

@@ -779,7 +779,9 @@ int gr_hip_node_iface_stats(gr_hip_queue_t *, struct gr_hip_iface_stats *stats, 
 
 // Measurement: nanoseconds gr_hip_node_start (append + send) and
 // gr_hip_node_finish spent in each part, summed over every queue of the
-// process since the last reset. out[k] for k < n; returns
+// process since the last reset, while the clocks run (the "node_prof" knob
+// of gr_hip_tune, process-wide, default off: each clock read costs tens of
+// nanoseconds per append). out[k] for k < n; returns
 // GR_HIP_NODE_PROF_COUNT.
 enum {
 	GR_HIP_NODE_PROF_LAYOUT, // (unused: the layout is part of the staging)

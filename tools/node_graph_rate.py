@@ -65,6 +65,13 @@ def main():
         for depth, touch in variants:
             assert L.gpu_fwd4_set_depth(depth) == 0
             L.gh_set_rx_touch(touch)
+            # the walk as it runs in production: no phase clocks
+            assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, len(me)) == 0
+            t0 = time.perf_counter()
+            assert L.gh_run(1 << 24) > 0
+            dt_plain = time.perf_counter() - t0
+            # the same with the node's and the library's phase clocks
+            fp.tune("node_prof", 1)
             assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, len(me)) == 0
             L.gpu_fwd4_prof(1, None)
             H = abi.hip()
@@ -78,10 +85,11 @@ def main():
             L.gpu_fwd4_prof(0, ph.ctypes.data)
             lp = np.zeros(9, dtype=np.uint64)
             H.gr_hip_node_prof(lp.ctypes.data, 9, 1)
+            fp.tune("node_prof", 0)
             assert walks > 0, walks
             if rep == 0:
                 continue  # warm-up: staging buffers grown, pages touched
-            # ns per packet in each phase of the node (depth 2: start and finish
+            # ns per packet in each phase of the node, clocks on (depth 2: start and finish
             # are the library's halves; depth 1 runs gr_hip_node_process, not split)
             names = ["accumulate", "start", "finish", "deliver"]
             per = {k: round(float(v) / len(me), 2) for k, v in zip(names, ph)}
@@ -90,6 +98,8 @@ def main():
                               "mbufs": len(me), "graph_walks": walks,
                               "node_batches": int(wi["batches"] - wi0["batches"]), "max_batch": int(wi["max_batch"]),
                               "ms": round(dt * 1e3, 2), "mpps": round(len(me) / dt / 1e6, 1),
+                              "mpps_unprofiled": round(len(me) / dt_plain / 1e6, 1),
+                              "ns_per_pkt_unprofiled": round(dt_plain * 1e9 / len(me), 2),
                               "ns_per_pkt": per,
                               "start_ns_per_pkt": {k: round(float(v) / len(me), 2) for k, v in zip(
                                   ["layout", "prep", "lock", "stage", "launch", "record", "fin_wait", "fin_scan",
