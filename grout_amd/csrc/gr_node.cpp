@@ -429,7 +429,8 @@ static inline uint8_t to_mbuf(struct gr_node_direct *d, uint32_t i, const struct
 }
 
 // The hand-back onto the mbufs of the packet a forwarding plane sees most:
-// forwarded to port_output, untagged on ingress, with lines staged. It is
+// forwarded to port_output, untagged on ingress (line: its rewritten header
+// line, or its frame when the GPU rewrote it in place). It is
 // the general loop below specialised for that case (depth 6 of either
 // family: no adj, iface_output's VLAN tag from the nexthop's iface, rx / tx
 // counted where grout counts them, the mbuf and private data as to_mbuf
@@ -455,13 +456,15 @@ static inline bool port_output_fast(struct gr_node_direct *d, uint32_t i, const 
 		d->edges[i] = GR_HIP_E_IP_OUTPUT_ERROR;
 		return true;
 	}
-	const uint32_t len = b.data_len < 26 ? b.data_len : 26; // bytes 0-25: see the general loop
 	uint8_t *fr = static_cast<uint8_t *>(b.frame);
-	if (len >= 16) {
-		memcpy(fr, line, 16);
-		memcpy(fr + len - 16, line + len - 16, 16);
-	} else {
-		memcpy(fr, line, len);
+	if (line != fr) { // else the GPU rewrote the frame in place (frames by address)
+		const uint32_t len = b.data_len < 26 ? b.data_len : 26; // bytes 0-25: see the general loop
+		if (len >= 16) {
+			memcpy(fr, line, 16);
+			memcpy(fr + len - 16, line + len - 16, 16);
+		} else {
+			memcpy(fr, line, len);
+		}
 	}
 	uint16_t vid = 0;
 	if (oif < n_ifaces && ifaces != nullptr && ifaces[oif].id == oif && ifaces[oif].type == GR_HIP_IFACE_TYPE_VLAN)
@@ -551,9 +554,10 @@ extern "C" int gr_node_apply_ex(
 		const uint32_t at = pos != nullptr ? pos[i] : i;
 		const struct gr_hip_verdict &v = verdicts[at];
 		bool fast6;
-		if (direct != nullptr && L != nullptr
-		    && port_output_fast(direct, i, m[i], v, L + (size_t)at * line_stride, ifaces, n_ifaces, nh, n_nh, ifst,
-					n_ifst, fast6)) {
+		if (direct != nullptr
+		    && port_output_fast(direct, i, m[i], v,
+					L != nullptr ? L + (size_t)at * line_stride : static_cast<const uint8_t *>(m[i].frame),
+					ifaces, n_ifaces, nh, n_nh, ifst, n_ifst, fast6)) {
 			if (i - start < WALK_MAX)
 				fam[i - start] = fast6 ? 2 : 1;
 			ended[fast6][6]++;

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--batch", type=int, default=15360)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--rx-touch", type=int, default=1, help="port_rx writes the mbuf and touches the frame (PMD + DDIO)")
+    ap.add_argument("--pin", type=int, default=0, help="1: frames by address (node_ptrs, mbuf memory registered)")
     args = ap.parse_args()
     threads = [int(x) for x in args.threads.split(",")]
 
@@ -53,7 +54,8 @@ def main():
     n = kmax * args.per_thread
     fr, me = S.stream(n, 0x67720002, routes=topo.route_array())
     fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
-    L.gh_set_pin(0)  # staged header lines: the node's default
+    fp.tune("node_ptrs", args.pin)
+    L.gh_set_pin(args.pin)  # 0: staged header lines, the node's default
     L.gh_set_rx_touch(args.rx_touch)
     for k in threads:
         m = k * args.per_thread
@@ -67,7 +69,7 @@ def main():
             assert rr == 0, rr
             best.append(s.value)
         t = float(np.median(best))
-        print(json.dumps({"threads": k, "gpus": 1, "mbufs": m, "batch": args.batch, "rx_touch": args.rx_touch,
+        print(json.dumps({"threads": k, "gpus": 1, "mbufs": m, "batch": args.batch, "rx_touch": args.rx_touch, "mode": "frames by address" if args.pin else "staged lines",
                           "ms": round(t * 1e3, 2), "mpps_aggregate": round(m / t / 1e6, 1),
                           "mpps_per_worker": round(m / t / 1e6 / k, 1),
                           "cpu_ns_per_pkt_per_worker": round(t * 1e9 * k / m, 1)}), flush=True)
