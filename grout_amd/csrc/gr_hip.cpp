@@ -175,10 +175,12 @@ struct node_slot {
 	// far, and whether the header lines are (not with "node_ptrs")
 	bool open = false, lines_in = false;
 	uint32_t na = 0, p = 0;
-	// appended from the mbufs (gr_hip_node_append_mbufs): the views are these
+	// appended from the mbufs (gr_hip_node_append_mbufs): no views; the
+	// mbufs (contiguous over the slot's appends) and the layout they are read with
 	bool own = false;
+	void *const *mb0 = nullptr;
+	const gr_hip_mbuf_layout *lay = nullptr;
 	bool kcount = false; // its kernel counts the per-iface counters (not the hand-back)
-	std::vector<gr_hip_mbuf> views;
 };
 
 } // namespace
@@ -2297,18 +2299,22 @@ static const host_range *hreg_find(const gr_hip_ctx *c, uintptr_t p) {
 
 // Every frame in registered memory and 16-byte aligned: their device
 // addresses into ptrs[pos[i]].
-static bool host_dev_ptr_ok(gr_hip_ctx *c, const gr_hip_mbuf *m, uint32_t n, uint64_t *ptrs, const uint32_t *pos) {
+template <class F> static bool host_dev_ptrs(gr_hip_ctx *c, uint32_t n, F frame, uint64_t *ptrs, const uint32_t *pos) {
 	// the caller holds c->mu
 	if (c->hregs.empty())
 		return false;
 	const host_range *hit = &c->hregs[0];
 	for (uint32_t i = 0; i < n; i++) {
-		const uintptr_t p = reinterpret_cast<uintptr_t>(m[i].frame);
+		const uintptr_t p = reinterpret_cast<uintptr_t>(frame(i));
 		if ((p & 15) || (p - hit->host >= hit->len && (hit = hreg_find(c, p)) == nullptr))
 			return false;
 		ptrs[pos[i]] = hit->dev + (p - hit->host);
 	}
 	return true;
+}
+
+static bool host_dev_ptr_ok(gr_hip_ctx *c, const gr_hip_mbuf *m, uint32_t n, uint64_t *ptrs, const uint32_t *pos) {
+	return host_dev_ptrs(c, n, [m](uint32_t i) { return m[i].frame; }, ptrs, pos);
 }
 
 extern "C" int gr_hip_host_register(gr_hip_ctx_t *c, void *ptr, size_t bytes) {
@@ -2374,13 +2380,13 @@ extern "C" int gr_hip_host_dev_addr(gr_hip_ctx_t *c, const void *ptr, uint64_t *
 // frame is untouched. Those packets go back to grout's CPU nodes (PUNT).
 #define NODE_V_FILL 0xff
 
-static uint32_t node_unfinished(const gr_hip_mbuf *m, uint32_t n, const uint32_t *pos, gr_hip_verdict *v) {
+static uint32_t node_unfinished(const gr_hip_pkt_meta *meta, uint32_t n, const uint32_t *pos, gr_hip_verdict *v) {
 	uint32_t k = 0;
 	for (uint32_t i = 0; i < n; i++) {
 		gr_hip_verdict &x = v[pos[i]];
 		if (x.edge != NODE_V_FILL)
 			continue;
-		x = gr_hip_verdict{GR_HIP_E_PUNT, 0, m[i].iface, 0};
+		x = gr_hip_verdict{GR_HIP_E_PUNT, 0, meta[pos[i]].iface, 0}; // the view's iface, as staged
 		k++;
 	}
 	return k;
@@ -2512,8 +2518,10 @@ extern "C" int gr_hip_node_append_mbufs(gr_hip_queue_t *q, void *const *mbufs, u
 		w.own = true;
 		w.na = w.p = 0;
 		w.lines_in = !q->ctx->node_ptrs;
-	} else if (!w.own) {
-		return -EINVAL; // views were appended to this slot
+		w.mb0 = mbufs;
+		w.lay = lay;
+	} else if (!w.own || mbufs != w.mb0 + w.na || lay != w.lay) {
+		return -EINVAL; // views were appended to this slot, or not the mbufs that follow
 	}
 	if (n == 0)
 		return (int)w.p;
@@ -2531,12 +2539,9 @@ extern "C" int gr_hip_node_append_mbufs(gr_hip_queue_t *q, void *const *mbufs, u
 			return r;
 	}
 	const size_t need = (size_t)w.na + n;
-	if (w.views.size() < need)
-		w.views.resize(std::max(need, 2 * w.views.size()));
 	if (w.pos.size() < need)
 		w.pos.resize(std::max(need, 2 * w.pos.size()));
-	gr_node_stage_mbufs(mbufs, n, lay, burst, w.p, w.views.data() + w.na, w.pos.data() + w.na,
-			    w.lines_in ? w.lines : nullptr, w.meta);
+	gr_node_stage_mbufs(mbufs, n, lay, burst, w.p, w.pos.data() + w.na, w.lines_in ? w.lines : nullptr, w.meta);
 	w.na += n;
 	w.p = (uint32_t)p;
 	if (prof)
@@ -2561,12 +2566,9 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 	node_slot &w = open_slot(q);
 	const bool was_open = w.open;
 	w.open = false;
-	if (was_open && w.own) { // appended from the mbufs: the library's own views
-		if (m != nullptr)
-			return -EINVAL;
-		m = w.views.data();
-	}
-	if ((n && m == nullptr) || !(was_open ? w.na == n : n == 0))
+	const bool own = was_open && w.own; // appended from the mbufs: no views
+	w.own = own;
+	if ((own ? m != nullptr : n && m == nullptr) || !(was_open ? w.na == n : n == 0))
 		return -EINVAL; // not what was appended
 	uint32_t *pos = w.pos.data();
 	uint64_t t_prof = prof_now();
@@ -2600,7 +2602,9 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 	int r;
 	bool enqueued = false;
 	uint64_t *ptrs = reinterpret_cast<uint64_t *>(w.lines);
-	w.by_addr = !w.lines_in && c->node_ptrs && host_dev_ptr_ok(c, m, n, ptrs, pos);
+	auto mbuf_frame = [&w](uint32_t i) { return gr_node_frame(w.mb0[i], w.lay); };
+	w.by_addr = !w.lines_in && c->node_ptrs
+		&& (own ? host_dev_ptrs(c, n, mbuf_frame, ptrs, pos) : host_dev_ptr_ok(c, m, n, ptrs, pos));
 	if (w.by_addr) {
 		// the frames are device-accessible: hand them over by address, the
 		// kernel reads and rewrites them in place over PCIe
@@ -2622,8 +2626,15 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 		enqueued = true;
 	} else {
 		if (!w.lines_in) { // "node_ptrs" on, but not every frame is registered: stage the lines now
-			if ((r = gr_node_stage_from(m, n, burst, pos, 0, w.lines, w.meta)) < 0)
+			if (own) { // the lines only: the metadata is staged
+				for (uint32_t i = 0, next = 0; i < n; next = pos[i] + 1, i++) {
+					for (; next < pos[i]; next++) // a pad slot
+						memset(w.lines + (size_t)next * GR_HIP_LINE, 0, GR_HIP_LINE);
+					memcpy(w.lines + (size_t)pos[i] * GR_HIP_LINE, mbuf_frame(i), GR_HIP_LINE);
+				}
+			} else if ((r = gr_node_stage_from(m, n, burst, pos, 0, w.lines, w.meta)) < 0) {
 				return r;
+			}
 			lap(GR_HIP_NODE_PROF_STAGE);
 		}
 		// the hand-back writes back at most the first 26 bytes: packed
@@ -2689,6 +2700,10 @@ static int node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np,
 	if (w.n == 0)
 		return 0;
 	int r = w.r;
+	if (direct != nullptr)
+		direct->meta = w.own ? w.meta : nullptr; // no views: the hand-back reads the mbufs
+	else if (w.own)
+		return -EINVAL; // appended from the mbufs: gr_hip_node_finish_mbufs hands it back
 	uint64_t t_prof = prof_now();
 	if (!w.sync) {
 		hipSetDevice(c->dev);
@@ -2703,7 +2718,7 @@ static int node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np,
 	node_prof_ns[GR_HIP_NODE_PROF_FIN_WAIT] += t - t_prof;
 	// packets a kernel that gave up never reached go back to grout's CPU
 	// nodes, the others are handed back as usual
-	const uint32_t unfinished = r == 0 ? 0 : node_unfinished(w.m, w.n, w.pos.data(), w.v); // 0: none gave up
+	const uint32_t unfinished = r == 0 ? 0 : node_unfinished(w.meta, w.n, w.pos.data(), w.v); // 0: none gave up
 	t_prof = prof_now();
 	node_prof_ns[GR_HIP_NODE_PROF_FIN_SCAN] += t_prof - t;
 	{
@@ -2728,7 +2743,7 @@ extern "C" int gr_hip_node_finish_mbufs(gr_hip_queue_t *q, void *const *mbufs, c
 					uint8_t *edges, uint32_t *stale, struct gr_hip_node_stats *stats) {
 	if (mbufs == nullptr || layout == nullptr || edges == nullptr)
 		return -EINVAL;
-	gr_node_direct d = {mbufs, layout, edges, 0};
+	gr_node_direct d = {mbufs, layout, edges, 0, nullptr};
 	const int r = node_finish(q, nullptr, nullptr, stats, &d);
 	if (stale != nullptr)
 		*stale = d.stale;

@@ -218,15 +218,21 @@ template <typename T> static inline T get(const uint8_t *base, uint16_t off) {
 	return v;
 }
 
+extern "C" void *gr_node_frame(const void *mbuf, const struct gr_hip_mbuf_layout *lay) {
+	const uint8_t *mb = static_cast<const uint8_t *>(mbuf);
+	return get<uint8_t *>(mb, lay->buf_addr) + get<uint16_t>(mb, lay->data_off);
+}
+
 // gr_hip_node_append_mbufs' one pass over a walk's mbufs (mbufs[0] starts
-// it): each mbuf read through the layout into its view v[i] (what the grout
-// node used to build: rte_pktmbuf_mtod, lengths, packet_type, hash.rss,
-// iface_mbuf_data's iface id and vlan_id, the checksum status), placed from
-// slot p (pos[i]; pads zeroed) as gr_node_layout_from places it, and its
-// header line (lines NULL: none) and metadata staged as gr_node_stage_from
-// stages them. Returns the first slot past the walk.
+// it): each mbuf read through the layout (what the grout node used to put in
+// a view: rte_pktmbuf_mtod, pkt_len, hash.rss, iface_mbuf_data's iface id and
+// vlan_id, the checksum status), placed from slot p (pos[i]; pads zeroed) as
+// gr_node_layout_from places it, and its header line (lines NULL: none) and
+// metadata staged as gr_node_stage_from stages them. No view is written: the
+// hand-back reads the mbufs again (gr_node_direct.meta). Returns the first
+// slot past the walk.
 extern "C" uint64_t gr_node_stage_mbufs(void *const *mbufs, uint32_t n, const struct gr_hip_mbuf_layout *lay,
-					uint32_t burst, uint64_t p, struct gr_hip_mbuf *v, uint32_t *pos, void *lines,
+					uint32_t burst, uint64_t p, uint32_t *pos, void *lines,
 					struct gr_hip_pkt_meta *meta) {
 	burst = walk_burst(burst);
 	const struct gr_hip_mbuf_layout &L = *lay;
@@ -245,32 +251,19 @@ extern "C" uint64_t gr_node_stage_mbufs(void *const *mbufs, uint32_t n, const st
 		}
 		const uint8_t *mb = static_cast<const uint8_t *>(mbufs[i]);
 		const uint8_t *priv = mb + L.priv;
-		const uint16_t off = get<uint16_t>(mb, L.data_off);
-		uint8_t *frame = get<uint8_t *>(mb, L.buf_addr) + off;
 		const uint8_t *ifp = get<const uint8_t *>(priv, L.priv_iface);
 		const uint64_t ck = get<uint64_t>(mb, L.ol_flags) & L.ck_mask;
-		struct gr_hip_mbuf &x = v[i];
-		x.frame = frame;
-		x.pkt_len = get<uint32_t>(mb, L.pkt_len);
-		x.data_len = get<uint16_t>(mb, L.data_len);
-		x.data_off = off;
-		x.packet_type = get<uint32_t>(mb, L.packet_type);
-		x.rss = get<uint32_t>(mb, L.rss);
-		x.iface = ifp != nullptr ? get<uint16_t>(ifp, L.iface_id) : 0;
-		x.vlan_id = get<uint16_t>(priv, L.priv_vlan_id);
-		x.ck = ck == L.ck_good ? GR_HIP_CKSUM_GOOD : ck == L.ck_bad ? GR_HIP_CKSUM_BAD : GR_HIP_CKSUM_UNKNOWN;
-		x.edge = 0;
-		x.domain = 0;
-		x.flags = i == 0 ? GR_HIP_MBUF_F_WALK : 0;
-		x.nh = 0;
+		const uint32_t pkt_len = get<uint32_t>(mb, L.pkt_len);
+		const uint8_t st = ck == L.ck_good ? GR_HIP_CKSUM_GOOD : ck == L.ck_bad ? GR_HIP_CKSUM_BAD : GR_HIP_CKSUM_UNKNOWN;
 		pos[i] = (uint32_t)p;
 		// 64 bytes whatever data_len says (gr_node_stage_from)
 		if (lb != nullptr)
-			memcpy(lb + (size_t)p * GR_HIP_LINE, frame, GR_HIP_LINE);
-		meta[p].iface = x.iface;
-		meta[p].vlan_ck = (uint16_t)((x.vlan_id & 0xfff) | (x.ck << 12) | (start ? GR_HIP_META_WALK : 0));
-		meta[p].pkt_len = (uint16_t)(x.pkt_len > 0xffff ? 0xffff : x.pkt_len);
-		meta[p].rss = (uint16_t)x.rss;
+			memcpy(lb + (size_t)p * GR_HIP_LINE, gr_node_frame(mb, lay), GR_HIP_LINE);
+		meta[p].iface = ifp != nullptr ? get<uint16_t>(ifp, L.iface_id) : 0;
+		meta[p].vlan_ck = (uint16_t)((get<uint16_t>(priv, L.priv_vlan_id) & 0xfff) | (st << 12)
+					     | (start ? GR_HIP_META_WALK : 0));
+		meta[p].pkt_len = (uint16_t)(pkt_len > 0xffff ? 0xffff : pkt_len);
+		meta[p].rss = (uint16_t)get<uint32_t>(mb, L.rss);
 		p++;
 	}
 	return p;
@@ -305,7 +298,7 @@ static inline uint16_t vlan_sub(const struct gr_node_vlans *vl, uint16_t parent,
 // takes ip_output's packets, then ip6_output's, or the other way round when
 // an IPv6 packet reached ip6_input first (rte_graph's pending queue), as the
 // kernel's eth_output_walks does inside a tile.
-static void eth_output_walk(struct gr_hip_mbuf *m, uint32_t a, uint32_t e, const uint32_t *pos,
+static void eth_output_walk(uint8_t *const *wf, uint32_t a, uint32_t e, const uint32_t *pos,
 			    const struct gr_hip_verdict *verdicts, const int8_t *fam, const struct gr_hip_iface *ifaces,
 			    uint32_t n_ifaces, const struct gr_hip_nh *nh, uint32_t n_nh) {
 	int32_t first4 = -1, first6 = -1;
@@ -340,7 +333,7 @@ static void eth_output_walk(struct gr_hip_mbuf *m, uint32_t a, uint32_t e, const
 			}
 			if (nomac)
 				continue;
-			uint8_t *src = static_cast<uint8_t *>(m[i].frame) + 6;
+			uint8_t *src = wf[i - a] + 6; // the walk's frames, wf[0] = packet a's
 			if (cleared)
 				memset(src, 0, 6);
 			else if (eo < n_ifaces && ifaces != nullptr)
@@ -371,7 +364,8 @@ static inline void count(struct gr_hip_iface_stats *st, uint32_t n_st, uint32_t 
 #endif
 
 static inline void prefetch_for_apply(const struct gr_hip_mbuf *m, uint32_t i, const struct gr_node_direct *d) {
-	__builtin_prefetch(m[i].frame, 1, GR_NODE_APPLY_PF_LOC);
+	if (m != nullptr) // else the frame's address is in the mbuf's first line, prefetched below
+		__builtin_prefetch(m[i].frame, 1, GR_NODE_APPLY_PF_LOC);
 	if (d != nullptr) {
 		const uint8_t *mb = static_cast<const uint8_t *>(d->mbufs[i]);
 		__builtin_prefetch(mb, 1, GR_NODE_APPLY_PF_LOC); // data_off .. packet_type: the mbuf's first line
@@ -385,6 +379,27 @@ template <typename T> static inline void put(uint8_t *base, uint16_t off, T v) {
 
 static inline const void *reg_get(const void *const *reg, uint32_t n, uint32_t id) {
 	return id < n && reg != nullptr ? __atomic_load_n(&reg[id], __ATOMIC_ACQUIRE) : nullptr;
+}
+
+// The view of mbuf i as the grout node used to build it (gr_node_stage_mbufs
+// staged the same fields), read before the hand-back writes the mbuf.
+static inline void view_of_mbuf(const struct gr_node_direct *d, uint32_t i, uint32_t at, struct gr_hip_mbuf &b) {
+	const struct gr_hip_mbuf_layout &L = *d->lay;
+	const uint8_t *mb = static_cast<const uint8_t *>(d->mbufs[i]);
+	const uint16_t off = get<uint16_t>(mb, L.data_off);
+	b.frame = get<uint8_t *>(mb, L.buf_addr) + off;
+	b.pkt_len = get<uint32_t>(mb, L.pkt_len);
+	b.data_len = get<uint16_t>(mb, L.data_len);
+	b.data_off = off;
+	b.packet_type = get<uint32_t>(mb, L.packet_type);
+	b.rss = d->meta[at].rss;
+	b.iface = d->meta[at].iface;
+	b.vlan_id = get<uint16_t>(mb + L.priv, L.priv_vlan_id);
+	b.ck = (uint8_t)((d->meta[at].vlan_ck >> 12) & 3);
+	b.edge = 0;
+	b.domain = 0;
+	b.flags = (d->meta[at].vlan_ck & GR_HIP_META_WALK) ? GR_HIP_MBUF_F_WALK : 0;
+	b.nh = 0;
 }
 
 // One packet's hand-back onto its mbuf (the grout node's private data for
@@ -521,7 +536,9 @@ extern "C" int gr_node_apply_ex(
 		return 0;
 	if (direct != nullptr && (direct->mbufs == nullptr || direct->lay == nullptr || direct->edges == nullptr))
 		return -EINVAL;
-	if (m == nullptr || verdicts == nullptr || (lines != nullptr && line_stride < GR_HIP_PREFIX))
+	const bool own = direct != nullptr && direct->meta != nullptr; // no views: read from the mbufs
+	if ((m == nullptr && !own) || (own && pos == nullptr) || verdicts == nullptr
+	    || (lines != nullptr && line_stride < GR_HIP_PREFIX))
 		return -EINVAL;
 	burst = walk_burst(burst);
 	const uint8_t *L = static_cast<const uint8_t *>(lines);
@@ -542,6 +559,7 @@ extern "C" int gr_node_apply_ex(
 	uint32_t reach[GR_HIP_NODE_COUNT] = {};
 	uint32_t start = 0; // first mbuf of the current graph walk
 	int8_t fam[WALK_MAX]; // per packet of the walk: 1 = entered ip_input, 2 = ip6_input, 0 = neither
+	uint8_t *wf[WALK_MAX]; // per packet of the walk: its frame (eth_output_walk)
 	bool walk_nomac = false; // the walk holds an eth_output_no_mac packet
 	// frames read (the ether type) and written back: prefetch them, the loop
 	// is bound by their cache misses
@@ -553,10 +571,20 @@ extern "C" int gr_node_apply_ex(
 			prefetch_for_apply(m, i + AHEAD, direct);
 		const uint32_t at = pos != nullptr ? pos[i] : i;
 		const struct gr_hip_verdict &v = verdicts[at];
+		// direct: the view is only read (own: built from the mbuf before the
+		// hand-back writes it), the mbuf gets the result below
+		struct gr_hip_mbuf copy;
+		if (own)
+			view_of_mbuf(direct, i, at, copy);
+		else if (direct != nullptr)
+			copy = m[i];
+		struct gr_hip_mbuf &b = direct != nullptr ? copy : m[i];
+		if (i - start < WALK_MAX)
+			wf[i - start] = static_cast<uint8_t *>(b.frame);
 		bool fast6;
 		if (direct != nullptr
-		    && port_output_fast(direct, i, m[i], v,
-					L != nullptr ? L + (size_t)at * line_stride : static_cast<const uint8_t *>(m[i].frame),
+		    && port_output_fast(direct, i, b, v,
+					L != nullptr ? L + (size_t)at * line_stride : static_cast<const uint8_t *>(b.frame),
 					ifaces, n_ifaces, nh, n_nh, ifst, n_ifst, fast6)) {
 			if (i - start < WALK_MAX)
 				fam[i - start] = fast6 ? 2 : 1;
@@ -564,11 +592,6 @@ extern "C" int gr_node_apply_ex(
 			goto walk_end;
 		}
 		{
-		// direct: the view is only read, the mbuf gets the result below
-		struct gr_hip_mbuf copy;
-		if (direct != nullptr)
-			copy = m[i];
-		struct gr_hip_mbuf &b = direct != nullptr ? copy : m[i];
 		const uint32_t len0 = b.pkt_len; // as iface_input / iface_output count it
 		const uint16_t iface0 = b.iface, vlan0 = b.vlan_id; // as port_rx left them
 		// lines NULL: the GPU rewrote the frames in place already
@@ -658,9 +681,11 @@ extern "C" int gr_node_apply_ex(
 			direct->edges[i] = to_mbuf(direct, i, b, v, node);
 		}
 	walk_end:
-		if (i + 1 == n || walk_start(m, i + 1, start, burst)) { // this graph walk ends here
+		if (i + 1 == n
+		    || (own ? (direct->meta[pos[i + 1]].vlan_ck & GR_HIP_META_WALK) != 0 || i + 1 - start == burst
+			    : walk_start(m, i + 1, start, burst))) { // this graph walk ends here
 			if (walk_nomac && i + 1 - start > 64)
-				eth_output_walk(m, start, i + 1, pos, verdicts, fam, ifaces, n_ifaces, nh, n_nh);
+				eth_output_walk(wf, start, i + 1, pos, verdicts, fam, ifaces, n_ifaces, nh, n_nh);
 			walk_nomac = false;
 			start = i + 1;
 			if (stats == nullptr)

@@ -29,18 +29,24 @@ int gr_node_stage_from(const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst, 
 
 // Where a walk of n mbufs appended at slot p ends (cut every `burst`).
 uint64_t gr_node_walk_end(uint64_t p, uint32_t n, uint32_t burst);
-// gr_hip_node_append_mbufs' pass: views v[], slots pos[], lines and metadata
-// of one walk's mbufs from slot p on; returns the first slot past the walk.
+// gr_hip_node_append_mbufs' pass: slots pos[], lines and metadata of one
+// walk's mbufs from slot p on; returns the first slot past the walk.
 uint64_t gr_node_stage_mbufs(void *const *mbufs, uint32_t n, const struct gr_hip_mbuf_layout *lay, uint32_t burst,
-			     uint64_t p, struct gr_hip_mbuf *v, uint32_t *pos, void *lines, struct gr_hip_pkt_meta *meta);
+			     uint64_t p, uint32_t *pos, void *lines, struct gr_hip_pkt_meta *meta);
+// rte_pktmbuf_mtod of an mbuf, through the layout.
+void *gr_node_frame(const void *mbuf, const struct gr_hip_mbuf_layout *lay);
 
 // The hand-back straight onto the caller's mbufs (gr_hip_node_finish_mbufs):
 // the views are read, not written; edges[i] and *stale are the outputs.
+// meta non-NULL: no views (the walk was appended from the mbufs): each
+// packet's view is read from its mbuf through lay before the hand-back
+// writes it, with its iface id and walk start from meta[pos[i]].
 struct gr_node_direct {
 	void *const *mbufs;
 	const struct gr_hip_mbuf_layout *lay;
 	uint8_t *edges;
 	uint32_t stale;
+	const struct gr_hip_pkt_meta *meta;
 };
 
 // gr_hip_node_apply, also adding each packet's rx / tx to ifst[iface id]

@@ -731,17 +731,19 @@ struct gr_hip_mbuf_layout {
 	// else GR_HIP_CKSUM_UNKNOWN (ip_input.c:80-92 verifies in software)
 	uint64_t ck_mask, ck_good, ck_bad;
 };
-// gr_hip_node_append without the views: the node passes one rte_graph walk's
+// gr_hip_node_append without views: the node passes one rte_graph walk's
 // mbufs (mbufs[0] starts it; it is cut every `burst` mbufs) and the library
-// reads each one through the layout (single segment; frame, lengths,
-// packet_type, rss, checksum status, the iface id and vlan_id from the
-// private data) while it lays the walk out and stages its header line and
-// metadata, in one pass. The views gr_hip_node_send and the finish use are
-// the library's own, built in the same pass: the next gr_hip_node_send on
-// the queue then takes m == NULL and n = every mbuf appended since the last
-// send, and the walk is handed back with gr_hip_node_finish_mbufs (the
-// mbufs array the appends read, kept until then). A slot holds walks
-// appended one way only (-EINVAL otherwise). Returns as gr_hip_node_append.
+// reads each one through the layout (single segment; the frame at buf_addr +
+// data_off, pkt_len, rss, the checksum status, the iface id and vlan_id from
+// the private data) while it lays the walk out and stages its header line
+// and metadata, in one pass. The appends of one batch pass consecutive parts
+// of one mbufs array, with one layout (-EINVAL otherwise; a slot holds walks
+// appended one way only). The next gr_hip_node_send then takes m == NULL and
+// n = every mbuf appended since the last send, and the batch is handed back
+// with gr_hip_node_finish_mbufs on that array (kept until then): the
+// hand-back reads each mbuf's fields again through the layout before it
+// writes them (gr_hip_node_finish returns -EINVAL for such a batch).
+// Returns as gr_hip_node_append.
 int gr_hip_node_append_mbufs(gr_hip_queue_t *, void *const *mbufs, uint32_t n,
 			     const struct gr_hip_mbuf_layout *layout, uint32_t burst);
 // gr_hip_node_finish handing the oldest walk back straight onto its mbufs:

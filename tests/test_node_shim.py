@@ -162,7 +162,7 @@ def _vlan_table(topo):
     return keys, vals
 
 
-def apply_counting(m, lines, v, topo, burst=64, direct=None):
+def apply_counting(m, lines, v, topo, burst=64, direct=None, pos=None):
     """gr_node_apply_ex: the hand-back plus the per-iface counters grout's
     iface_input / iface_output would have added (what the node folds into
     grout's iface_stats)."""
@@ -179,8 +179,10 @@ def apply_counting(m, lines, v, topo, burst=64, direct=None):
     lines = np.ascontiguousarray(lines)
     P, U32 = ctypes.c_void_p, ctypes.c_uint32
     L.gr_node_apply_ex.argtypes = [P, U32, U32, P, P, U32, P, P, U32, P, U32, P, P, P, U32, P]
+    n = len(v)
     abi.check("gr_node_apply_ex", L.gr_node_apply_ex(
-        m.ctypes.data, len(m), burst, None, lines.ctypes.data, abi.LINE, v.ctypes.data, ifaces.ctypes.data,
+        None if m is None else m.ctypes.data, n, burst, None if pos is None else pos.ctypes.data,
+        lines.ctypes.data, abi.LINE, v.ctypes.data, ifaces.ctypes.data,
         len(ifaces), nh.ctypes.data, len(nh), ns.ctypes.data, vl_buf.ctypes.data, st.ctypes.data, len(st), direct))
     return ns[0], st
 
@@ -201,7 +203,7 @@ class Layout(ctypes.Structure):
 class Direct(ctypes.Structure):
     """struct gr_node_direct (grout_amd/csrc/gr_node_priv.h)"""
     _fields_ = [("mbufs", ctypes.c_void_p), ("lay", ctypes.c_void_p), ("edges", ctypes.c_void_p),
-                ("stale", ctypes.c_uint32)]
+                ("stale", ctypes.c_uint32), ("meta", ctypes.c_void_p)]
 
 
 # grout's rte_mbuf and private-data offsets (DPDK rte_mbuf_core.h; mbuf.h:29-41,
@@ -288,13 +290,12 @@ def test_apply_onto_mbufs_equals_views():
 
 def test_stage_from_mbufs_equals_views():
     """gr_hip_node_append_mbufs' one pass (gr_node_stage_mbufs): reading
-    grout's rte_mbufs through the layout gives the views the grout node used
-    to build (frame at buf_addr + data_off, lengths, packet_type, rss, the
-    iface id through mbuf_data.iface, vlan_id, the checksum status from
-    ol_flags), the same placement (walks cut at the burst, pads before a walk
-    that would straddle a tile) and the same staged lines and metadata as
-    gr_hip_node_layout + gr_hip_node_stage on those views, over appends of
-    1 to 300 mbufs."""
+    grout's rte_mbufs through the layout (frame at buf_addr + data_off,
+    pkt_len, rss, the iface id through mbuf_data.iface, vlan_id, the checksum
+    status from ol_flags) gives the same placement (walks cut at the burst,
+    pads before a walk that would straddle a tile) and the same staged lines
+    and metadata as gr_hip_node_layout + gr_hip_node_stage on the views the
+    grout node used to build, over appends of 1 to 300 mbufs."""
     t, _ = SC.corpus_topology()
     fr, me, _ = SC.corpus_arrays()
     keep = ((me["vlan_ck"] >> 12) & 3) != 3  # no ol_flags value gives the corpus's status 3
@@ -341,22 +342,71 @@ def test_stage_from_mbufs_equals_views():
                                                          lines_ref.ctypes.data, meta_ref.ctypes.data))
     fn = ctypes.CDLL(abi.LIB_HIP).gr_node_stage_mbufs
     P = ctypes.c_void_p
-    fn.argtypes = [P, ctypes.c_uint32, P, ctypes.c_uint32, ctypes.c_uint64, P, P, P, P]
+    fn.argtypes = [P, ctypes.c_uint32, P, ctypes.c_uint32, ctypes.c_uint64, P, P, P]
     fn.restype = ctypes.c_uint64
-    v = np.zeros(n, dtype=abi.MBUF_DT)
     pos = np.zeros(n, dtype=np.uint32)
     lines = np.full((end, abi.LINE), 0xEE, dtype=np.uint8)
     meta = np.full(end * abi.META_DT.itemsize, 0xEE, dtype=np.uint8).view(abi.META_DT)
     p = 0
     for i, k in sizes:
-        p = fn(ptrs.ctypes.data + 8 * i, k, ctypes.addressof(lay), 256, p, v.ctypes.data + v.itemsize * i,
-               pos.ctypes.data + 4 * i, lines.ctypes.data, meta.ctypes.data)
+        p = fn(ptrs.ctypes.data + 8 * i, k, ctypes.addressof(lay), 256, p, pos.ctypes.data + 4 * i,
+               lines.ctypes.data, meta.ctypes.data)
     assert p == end
-    for f in ref.dtype.names:
-        assert np.array_equal(v[f], ref[f]), f
     assert np.array_equal(pos, pos_ref)
     assert np.array_equal(lines, lines_ref) and np.array_equal(meta, meta_ref)
     assert ((meta["vlan_ck"] & 0x4000) != 0).sum() == sum(1 + (k - 1) // 256 for _, k in sizes)  # one walk flag per cut
+
+
+def test_apply_onto_mbufs_without_views():
+    """The hand-back of a batch appended from the mbufs (no views: each
+    packet's fields read from its rte_mbuf through the layout, its iface id
+    and walk starts from the staged metadata) leaves every mbuf, private
+    area, frame, edge and counter exactly as the hand-back driven by the
+    views does, over every edge of the corpus in walks of 64."""
+    t, _ = SC.corpus_topology()
+    fr, me, _ = SC.corpus_arrays()
+    keep = ((me["vlan_ck"] >> 12) & 3) != 3
+    fr, me = np.concatenate([fr[keep]] * 4), np.concatenate([me[keep]] * 4)
+    n = len(me)
+    lines, v, _, _, _ = oracle.Oracle(t).process_mbufs(fr, me)
+    L, G = GROUT_LAYOUT, GROUT_STAGE
+    ifobj = np.zeros((t.max_ifaces, 64), dtype=np.uint8)
+    ifobj.view(np.uint16)[:, G["iface_id"] // 2] = np.arange(t.max_ifaces)
+    reg_if = np.zeros(t.max_ifaces, dtype=np.uint64)
+    live = t.ifaces["id"] != 0
+    reg_if[live] = IF_OBJ + np.nonzero(live)[0]
+    reg_nh = (NH_OBJ + np.arange(len(t.nh), dtype=np.uint64)).astype(np.uint64)
+    reg_nh[0] = 0
+    lay = Layout(**L, **G, n_ifaces=len(reg_if), n_nh=len(reg_nh), ifaces=reg_if.ctypes.data, nh=reg_nh.ctypes.data)
+    H = abi.hip()
+    res = []
+    for own in (False, True):
+        bufs, m = mbufs_for(fr, me)  # the frames at RX, each run its own copy
+        m["flags"][::64] = abi.MBUF_F_WALK
+        mem = np.zeros((n, 256), dtype=np.uint8)
+        U16, U32, U64 = mem.view(np.uint16), mem.view(np.uint32), mem.view(np.uint64)
+        U64[:, G["buf_addr"] // 8] = m["frame"] - RX_DATA_OFF
+        U16[:, L["data_off"] // 2] = RX_DATA_OFF
+        U16[:, L["data_len"] // 2] = m["data_len"]
+        U32[:, L["pkt_len"] // 4] = m["pkt_len"]
+        U16[:, (L["priv"] + L["priv_vlan_id"]) // 2] = m["vlan_id"]
+        ptrs = (mem.ctypes.data + np.arange(n, dtype=np.uint64) * 256).astype(np.uint64)
+        pos = np.arange(n, dtype=np.uint32)  # walks of 64 on tiles: no pads
+        meta = np.zeros(n, dtype=abi.META_DT)
+        abi.check("gr_hip_node_stage", H.gr_hip_node_stage(m.ctypes.data, n, 64, pos.ctypes.data, None,
+                                                             meta.ctypes.data))
+        edges = np.full(n, 0xEE, dtype=np.uint8)
+        d = Direct(mbufs=ptrs.ctypes.data, lay=ctypes.addressof(lay), edges=edges.ctypes.data,
+                   meta=meta.ctypes.data if own else None)
+        ns, st = apply_counting(None if own else m, lines, v, t, direct=ctypes.addressof(d), pos=pos)
+        res.append((mem.copy(), bufs.copy(), edges.copy(), ns, st, d.stale))
+    (mem0, b0, e0, ns0, st0, s0), (mem1, b1, e1, ns1, st1, s1) = res
+    assert np.array_equal(e0, e1) and (e0 != 0xEE).all()
+    assert np.array_equal(mem0[:, 16:48], mem1[:, 16:48])  # data_off .. data_len, packet_type
+    assert np.array_equal(mem0[:, 128:192], mem1[:, 128:192])  # the private area
+    assert np.array_equal(b0[:, :abi.LINE], b1[:, :abi.LINE])  # the frames
+    assert np.array_equal(ns0, ns1) and np.array_equal(st0, st1) and s0 == s1
+    assert len(set(e0.tolist())) > 20
 
 
 def test_apply_counts_ifaces_where_grout_does():

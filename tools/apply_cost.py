@@ -44,7 +44,7 @@ class Layout(ctypes.Structure):
 
 class Direct(ctypes.Structure):
     _fields_ = [("mbufs", ctypes.c_void_p), ("lay", ctypes.c_void_p), ("edges", ctypes.c_void_p),
-                ("stale", ctypes.c_uint32)]
+                ("stale", ctypes.c_uint32), ("meta", ctypes.c_void_p)]
 
 
 def main():
