@@ -485,9 +485,11 @@ static inline bool port_output_fast(struct gr_node_direct *d, uint32_t i, const 
 	if (oif < n_ifaces && ifaces != nullptr && ifaces[oif].id == oif && ifaces[oif].type == GR_HIP_IFACE_TYPE_VLAN)
 		vid = ifaces[oif].vlan_id;
 	uint8_t *mb = static_cast<uint8_t *>(d->mbufs[i]);
-	put<uint16_t>(mb, L.data_off, b.data_off); // eth_output's prepend undid ip_input's adj
-	put<uint16_t>(mb, L.data_len, b.data_len);
-	put<uint32_t>(mb, L.pkt_len, b.pkt_len);
+	if (d->meta == nullptr) { // the view's lengths (read from this mbuf otherwise: unchanged)
+		put<uint16_t>(mb, L.data_off, b.data_off); // eth_output's prepend undid ip_input's adj
+		put<uint16_t>(mb, L.data_len, b.data_len);
+		put<uint32_t>(mb, L.pkt_len, b.pkt_len);
+	}
 	put<uint32_t>(mb, L.packet_type, ip6 ? GR_HIP_PTYPE_L3_IPV6 : GR_HIP_PTYPE_L3_IPV4);
 	uint8_t *priv = mb + L.priv;
 	put<const void *>(priv, L.priv_iface, ifp);
