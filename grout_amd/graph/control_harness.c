@@ -33,17 +33,25 @@ struct call {
 	int done;
 };
 
+// One control call is one turn of grout's control loop: its timers (the
+// mirror's publication) fire when it ends.
+static int control_turn(int (*fn)(void *), void *arg) {
+	const int r = fn(arg);
+	gr_test_event_loop_turn();
+	return r;
+}
+
 static void *control_thread(void *p) {
 	struct call *c = p;
 	gr_test_lcore_set(RTE_MAX_LCORE - 1); // not a worker's lcore
-	c->ret = c->fn(c->arg);
+	c->ret = control_turn(c->fn, c->arg);
 	__atomic_store_n(&c->done, 1, __ATOMIC_RELEASE);
 	return NULL;
 }
 
 static int on_control(int (*fn)(void *), void *arg) {
 	if (!gh_inited())
-		return fn(arg);
+		return control_turn(fn, arg);
 	struct call c = {.fn = fn, .arg = arg};
 	pthread_t th;
 	if (pthread_create(&th, NULL, control_thread, &c) != 0)
@@ -273,6 +281,33 @@ int gc_route4_add(uint16_t vrf_id, uint32_t ip_be, uint8_t prefixlen, uint32_t g
 	memcpy(a.gw, &gw_be, 4);
 	return on_control(do_route4_add, &a);
 }
+// count routes of /prefixlen from ip (host order steps) via nexthop nh_id, in
+// one control turn, as FRR's bulk installs reach grout
+struct a_many {
+	uint16_t vrf_id;
+	uint32_t ip_host;
+	uint8_t prefixlen;
+	uint32_t count, nh_id;
+	uint8_t origin;
+};
+static int do_route4_add_many(void *p) {
+	const struct a_many *a = p;
+	const uint32_t step = a->prefixlen ? 1u << (32 - a->prefixlen) : 0;
+	for (uint32_t k = 0; k < a->count; k++) {
+		const uint32_t ip = __builtin_bswap32(a->ip_host + k * step);
+		const int r = route4_add(a->vrf_id, ip, a->prefixlen, 0, a->nh_id, a->origin, 0);
+		if (r < 0)
+			return r;
+	}
+	return 0;
+}
+int gc_route4_add_many(uint16_t vrf_id, uint32_t ip_be, uint8_t prefixlen, uint32_t count, uint32_t nh_id,
+		       uint8_t origin) {
+	struct a_many a = {.vrf_id = vrf_id, .ip_host = __builtin_bswap32(ip_be), .prefixlen = prefixlen,
+			   .count = count, .nh_id = nh_id, .origin = origin};
+	return on_control(do_route4_add_many, &a);
+}
+
 int gc_route4_del(uint16_t vrf_id, uint32_t ip_be, uint8_t prefixlen, int missing_ok) {
 	struct a_l3 a = {.vrf_id = vrf_id, .prefixlen = prefixlen, .flag = missing_ok};
 	IP4(a, ip_be);

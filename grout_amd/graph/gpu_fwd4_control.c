@@ -19,6 +19,7 @@
 #include <errno.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/time.h>
 
 // ---- a small open-addressing hash: fixed-size keys -> uint32 ---------------
 struct ht {
@@ -164,8 +165,16 @@ static struct {
 	uint32_t n_r6, cap_r6;
 	struct ht k6;
 	struct fib_conf *fibs; // [max_ifaces] by VRF id
+	// route changes applied to every context's RIB and not yet published
+	// (see "publication" below)
+	uint8_t *dirty4, *dirty6; // [max_ifaces] by VRF id
+	uint32_t pending;
+	struct event *flush_ev;
+	int flush_armed;
 	struct gpu_fwd4_control_stats st;
 } M;
+
+static struct event_base *ev_base; // the control thread's (gpu_fwd4_control_attach)
 
 static void note(int r) {
 	// no GPU context at all (CPU tests): the shadow alone is kept
@@ -189,8 +198,10 @@ static int ready(void) {
 	M.if_seen = calloc(M.max_ifaces, 1);
 	M.if_removing = calloc(M.max_ifaces, 1);
 	M.fibs = calloc(M.max_ifaces, sizeof(*M.fibs));
+	M.dirty4 = calloc(M.max_ifaces, 1);
+	M.dirty6 = calloc(M.max_ifaces, 1);
 	if (M.free_slots == NULL || M.nh == NULL || M.ifs == NULL || M.if_live == NULL || M.if_seen == NULL
-	    || M.if_removing == NULL || M.fibs == NULL) {
+	    || M.if_removing == NULL || M.fibs == NULL || M.dirty4 == NULL || M.dirty6 == NULL) {
 		gpu_fwd4_control_reset();
 		return -ENOMEM;
 	}
@@ -214,7 +225,15 @@ void gpu_fwd4_control_reset(void) {
 	free(M.r4);
 	free(M.r6);
 	free(M.fibs);
+	free(M.dirty4);
+	free(M.dirty6);
+	if (M.flush_ev != NULL)
+		event_free(M.flush_ev);
 	memset(&M, 0, sizeof(M));
+}
+
+void gpu_fwd4_control_attach(struct event_base *ev) {
+	ev_base = ev;
 }
 
 // ---- nexthop slots ---------------------------------------------------------
@@ -399,11 +418,70 @@ static uint32_t mask4(uint32_t ip_be, uint8_t plen) {
 static void commit4(uint16_t vrf_id) {
 	note(gpu_fwd4_fib4_commit(vrf_id));
 	M.st.commits++;
+	M.dirty4[vrf_id] = 0;
 }
 
 static void commit6(uint16_t vrf_id) {
 	note(gpu_fwd4_fib6_commit(vrf_id));
 	M.st.commits++;
+	M.dirty6[vrf_id] = 0;
+}
+
+// ---- publication -------------------------------------------------------------
+// Each route event reaches every context's RIB at once; publishing it (a
+// commit: the changed tbl24 ranges / trie paths uploaded into the unpublished
+// copy and the copies flipped) waits until the control thread's
+// event loop comes round (a timer of PUBLISH_DELAY_US), PUBLISH_BATCH changes
+// have gathered, or grout is about to wait for the datapath before freeing a
+// nexthop (GR_EVENT_NEXTHOP_PRE_DELETE, pushed by nexthop_destroy before its
+// rte_rcu_qsbr_synchronize; an iface's removal destroys its nexthops the same
+// way). So a full view loaded by FRR is published in a few hundred commits, not
+// one per route, and a deleted route is still off every GPU before grout's
+// synchronize for its nexthop starts: no batch started after it can name the
+// nexthop's slot, which the slot's next owner may reuse.
+#define PUBLISH_BATCH 4096
+#define PUBLISH_DELAY_US 200
+
+void gpu_fwd4_control_flush(void) {
+	if (M.flush_armed) {
+		evtimer_del(M.flush_ev);
+		M.flush_armed = 0;
+	}
+	if (M.pending == 0)
+		return;
+	for (uint32_t v = 0; v < M.max_ifaces; v++) {
+		if (M.dirty4[v])
+			commit4((uint16_t)v);
+		if (M.dirty6[v])
+			commit6((uint16_t)v);
+	}
+	M.pending = 0;
+}
+
+static void publish_cb(int fd, short what, void *arg) {
+	(void)fd;
+	(void)what;
+	(void)arg;
+	M.flush_armed = 0;
+	gpu_fwd4_control_flush();
+}
+
+static void route_changed(uint16_t vrf_id, int ip6) {
+	(ip6 ? M.dirty6 : M.dirty4)[vrf_id] = 1;
+	if (++M.pending >= PUBLISH_BATCH) {
+		gpu_fwd4_control_flush();
+		return;
+	}
+	if (M.flush_armed)
+		return;
+	if (M.flush_ev == NULL)
+		M.flush_ev = evtimer_new(ev_base, publish_cb, NULL);
+	const struct timeval tv = {.tv_sec = 0, .tv_usec = PUBLISH_DELAY_US};
+	if (M.flush_ev == NULL || evtimer_add(M.flush_ev, &tv) < 0) {
+		gpu_fwd4_control_flush(); // no timer: publish now
+		return;
+	}
+	M.flush_armed = 1;
 }
 
 static void shadow_route4(const struct gr_hip_route4 *rt, int add) {
@@ -458,7 +536,7 @@ static void on_route4(uint32_t ev, const void *obj) {
 		note(gpu_fwd4_route4_del(rt.vrf_id, rt.ip, rt.prefixlen));
 		shadow_route4(&rt, 0);
 	}
-	commit4(r->vrf_id);
+	route_changed(r->vrf_id, 0);
 }
 
 static bool ip6_is_linklocal(const uint8_t a[16]) {
@@ -539,7 +617,7 @@ static void on_route6(uint32_t ev, const void *obj) {
 		note(gpu_fwd4_route6_del(rt.vrf_id, rt.iface_id, rt.ip, rt.prefixlen));
 		shadow_route6(&rt, 0);
 	}
-	commit6(r->vrf_id);
+	route_changed(r->vrf_id, 1);
 }
 
 // ---- ifaces ------------------------------------------------------------------
@@ -577,6 +655,7 @@ static void fib_create(uint16_t vrf_id, const struct iface_info_vrf *v) {
 
 static void fib_destroy(uint16_t vrf_id) {
 	struct fib_conf *f = &M.fibs[vrf_id];
+	M.dirty4[vrf_id] = M.dirty6[vrf_id] = 0; // nothing left to publish there
 	if (f->on4)
 		note(gpu_fwd4_fib4_destroy(vrf_id));
 	if (f->on6)
@@ -634,6 +713,8 @@ static void on_iface(uint32_t ev, const void *obj) {
 			push_iface(i);
 		break;
 	case GR_EVENT_IFACE_PRE_REMOVE: // the iface leaves the GPUs with grout's ifaces[] (iface.c:702-712)
+		M.st.presync += M.pending != 0;
+		gpu_fwd4_control_flush(); // before grout's synchronize (see "publication")
 		M.if_removing[i->id] = 1;
 		M.if_live[i->id] = 0;
 		memset(&M.ifs[i->id], 0, sizeof(M.ifs[i->id]));
@@ -659,6 +740,10 @@ static void dispatch(uint32_t ev, const void *obj) {
 	case GR_EVENT_NEXTHOP_UPDATE:
 	case GR_EVENT_NEXTHOP_DELETE:
 		on_nexthop(ev, obj);
+		break;
+	case GR_EVENT_NEXTHOP_PRE_DELETE: // grout waits for the datapath next: publish first
+		M.st.presync += M.pending != 0;
+		gpu_fwd4_control_flush();
 		break;
 	case GR_EVENT_IP_ROUTE_ADD:
 	case GR_EVENT_IP_ROUTE_DEL:
@@ -700,6 +785,7 @@ RTE_INIT(gpu_fwd4_control_init) {
 		event_subscribe(obj_evs[k], on_event);
 		event_subscribe_internal(obj_evs[k], on_internal_event);
 	}
+	event_subscribe_internal(GR_EVENT_NEXTHOP_PRE_DELETE, on_internal_event);
 }
 
 // ---- queries -------------------------------------------------------------------
@@ -737,8 +823,10 @@ int gpu_fwd4_control_routes6(struct gr_hip_route6 *out, uint32_t max) {
 }
 
 void gpu_fwd4_control_stats(struct gpu_fwd4_control_stats *st) {
-	if (st != NULL)
+	if (st != NULL) {
 		*st = M.st;
+		st->pending = M.pending;
+	}
 }
 
 // ---- replay into one context -------------------------------------------------

@@ -57,6 +57,8 @@ struct gpu_fwd4_control_stats {
 	uint32_t slots_used; // nexthop slots held
 	uint32_t reta_used; // reta entries held
 	uint32_t routes4, routes6;
+	uint32_t pending; // route changes in every context's RIB, not yet published
+	uint64_t presync; // publications grout's wait for the datapath forced (see "publication")
 };
 void gpu_fwd4_control_stats(struct gpu_fwd4_control_stats *);
 
@@ -67,6 +69,14 @@ int gpu_fwd4_control_replay(uint32_t i);
 
 // Tests: forget everything (the contexts' state is the caller's to reset).
 void gpu_fwd4_control_reset(void);
+
+// Route changes are published in batches (gpu_fwd4_control.c,
+// "publication"): a timer on the control thread's event base, which the
+// module's init passes here, publishes what the event loop's turn gathered.
+struct event_base;
+void gpu_fwd4_control_attach(struct event_base *ev);
+// Publish every route change gathered so far, now (every VRF's FIBs).
+void gpu_fwd4_control_flush(void);
 
 #ifdef __cplusplus
 }

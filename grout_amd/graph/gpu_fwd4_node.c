@@ -55,6 +55,7 @@
 // gr_datapath_min.h); in grout it includes <gr_graph.h>, <gr_mbuf.h>,
 // <gr_module.h> and the DPDK headers instead, with no other change.
 #include "gpu_fwd4_node.h"
+#include "gpu_fwd4_control.h"
 
 #include "gr_datapath_min.h"
 
@@ -185,7 +186,7 @@ gr_hip_ctx_t *gpu_fwd4_ctx_at(uint32_t i) {
 static void gpu_fini(struct event_base *ev);
 
 static void gpu_init(struct event_base *ev) {
-	(void)ev;
+	gpu_fwd4_control_attach(ev); // the mirror's publication timer
 	int devs[GPU_FWD4_MAX_DEVS];
 	uint32_t n = conf.n_devs;
 	if (n == 0) { // every visible device

@@ -55,6 +55,64 @@ static void rcu_sync(void) {
 		rte_rcu_qsbr_synchronize(gr_datapath_rcu(), RTE_QSBR_THRID_INVALID);
 }
 
+// ---- libevent timers ---------------------------------------------------------
+struct event {
+	void (*cb)(int, short, void *);
+	void *arg;
+	int pending;
+	struct event *next;
+};
+static struct event *timers;
+
+struct event *event_new(struct event_base *base, int fd, short what, void (*cb)(int, short, void *), void *arg) {
+	(void)base;
+	(void)fd;
+	(void)what;
+	struct event *e = calloc(1, sizeof(*e));
+	if (e == NULL)
+		return NULL;
+	e->cb = cb;
+	e->arg = arg;
+	e->next = timers;
+	timers = e;
+	return e;
+}
+
+int event_add(struct event *ev, const struct timeval *tv) {
+	(void)tv;
+	ev->pending = 1;
+	return 0;
+}
+
+int event_del(struct event *ev) {
+	ev->pending = 0;
+	return 0;
+}
+
+void event_free(struct event *ev) {
+	for (struct event **p = &timers; *p != NULL; p = &(*p)->next)
+		if (*p == ev) {
+			*p = ev->next;
+			break;
+		}
+	free(ev);
+}
+
+void gr_test_event_loop_turn(void) {
+	for (int round = 0; round < 16; round++) { // a callback may add a timer again
+		int fired = 0;
+		for (struct event *e = timers; e != NULL; e = e->next)
+			if (e->pending) {
+				e->pending = 0;
+				e->cb(-1, 0x01 /* EV_TIMEOUT */, e->arg);
+				fired = 1;
+				break; // the list may have changed
+			}
+		if (!fired)
+			return;
+	}
+}
+
 // ---- events (main/event.c:25-67) -------------------------------------------
 #define MAX_SUBS 128
 static struct {
@@ -667,6 +725,7 @@ static void nexthop_destroy(struct nexthop *nh) {
 	nh_hashed[pool_index(nh)] = false;
 	nexthop_iter(remove_group_member_cb, nh);
 	nexthop_id_put(nh);
+	event_push_internal(GR_EVENT_NEXTHOP_PRE_DELETE, nh); // patch
 	rcu_sync();
 	if (nh->origin != GR_NH_ORIGIN_INTERNAL)
 		event_push(GR_EVENT_NEXTHOP_DELETE, nh);

@@ -71,11 +71,31 @@ void event_push(uint32_t ev_type, const void *obj);
 // delivered only to callbacks registered with event_subscribe_internal.
 void event_subscribe_internal(uint32_t ev_type, event_sub_cb_t callback);
 void event_push_internal(uint32_t ev_type, const void *obj);
+// nexthop_destroy pushes it on the internal channel before it waits for the
+// datapath (the patch defines it in modules/infra/control/nexthop.h): a
+// subscriber that holds FIB changes back publishes them first.
+#define GR_EVENT_NEXTHOP_PRE_DELETE GR_MSG_TYPE(GR_INFRA_MODULE, 0x30ff)
 // Tests: the event counters zeroed; events pushed (public, internal) since.
 void gr_test_events_reset(void);
 // Tests: 0 = grout without the patch (event_push_internal does nothing).
 void gr_test_internal_events(int on);
 void gr_test_events_count(uint64_t *pub, uint64_t *internal);
+
+// ---- the control thread's event loop: libevent's timers (in grout, libevent
+// itself on the event base modules get at init) -------------------------------
+struct event;
+struct timeval;
+struct event *event_new(struct event_base *base, int fd, short what, void (*cb)(int, short, void *), void *arg);
+int event_add(struct event *ev, const struct timeval *tv);
+int event_del(struct event *ev);
+void event_free(struct event *ev);
+#define evtimer_new(b, cb, arg) event_new((b), -1, 0, (cb), (arg))
+#define evtimer_add(ev, tv) event_add((ev), (tv))
+#define evtimer_del(ev) event_del(ev)
+// Tests: one turn of the control thread's loop ends (each harness control
+// call is one): every pending timer fires. Time is not modelled: a turn is
+// taken to outlast any timer's delay.
+void gr_test_event_loop_turn(void);
 
 // route4_event / route6_event (modules/ip/control/route.c:205-210,
 // modules/ip6/control/route.c:222-227), moved into ip4.h / ip6.h by the

@@ -44,8 +44,8 @@ P, U8, U16, U32, I = ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint16, ctypes.c_
 
 STATS_DT = np.dtype([("events", "<u8"), ("internal", "<u8"), ("commits", "<u8"), ("errors", "<u8"),
                      ("first_error", "<i4"), ("slots_used", "<u4"), ("reta_used", "<u4"), ("routes4", "<u4"),
-                     ("routes6", "<u4"), ("_pad", "<u4")])
-assert STATS_DT.itemsize == 56
+                     ("routes6", "<u4"), ("pending", "<u4"), ("presync", "<u8")])
+assert STATS_DT.itemsize == 64
 
 ORIGIN_STATIC, ORIGIN_LINK, ORIGIN_LEARN, ORIGIN_INTERNAL = 4, 2, 3, 255
 NH_F_NEIGH = 0x20
@@ -73,6 +73,7 @@ def lib():
             "gc_addr6_add": (I, [U16, P, U8]), "gc_addr6_del": (I, [U16, P, U8]),
             "gc_route4_add": (I, [U16, U32, U8, U32, U32, U8, I]), "gc_route4_del": (I, [U16, U32, U8, I]),
             "gc_route6_add": (I, [U16, P, U8, P, U32, U8, I]), "gc_route6_del": (I, [U16, P, U8, I]),
+            "gc_route4_add_many": (I, [U16, U32, U8, U32, U32, U8]),
             "gc_arp": (I, [U16, U32, P]), "gc_ndp": (I, [U16, P, P]),
             "gc_resolve4": (I, [U16, U32]), "gc_age4": (I, [U16, U32, U32, U32]),
             "gc_nh_add_l3": (I, [U32, U16, U32, P, U8, I]), "gc_nh_add_type": (I, [U32, U8, U16, U8]),
@@ -276,6 +277,36 @@ def test_mirror_follows_grout_sequences(control):
     # the learned neighbour: INTERNAL objects, only on the patch's channel
     assert ev[1] >= 4 + 1, ev
     assert stats()["internal"] == ev[1]
+
+
+def test_mirror_publishes_route_changes_in_batches(control):
+    """Route events reach every context's RIB at once and are published in
+    batches (gpu_fwd4_control.c, "publication"): when the control loop's turn
+    ends, or every 4096 changes. A full view FRR installs in one burst then
+    costs a few hundred commits, not one per route. grout's wait for the
+    datapath before it frees a nexthop (nexthop_destroy's synchronize, after
+    the pre-delete event the patch pushes) publishes first, so a route deleted
+    with its nexthop is off every GPU before the synchronize starts."""
+    L = control
+    build_base()
+    st0 = stats()
+    assert st0["pending"] == 0
+    # one turn: 10,000 /24s via nexthop 100 (4096 + 4096 published on the way, the rest at the turn's end)
+    ok(L.gc_route4_add_many(VRF, be("20.0.0.0"), 24, 10_000, 100, ORIGIN_STATIC))
+    st1 = stats()
+    assert st1["commits"] - st0["commits"] == 3 and st1["pending"] == 0, (st0, st1)
+    assert st1["routes4"] - st0["routes4"] == 10_000
+    # a single route: published at its turn's end
+    ok(L.gc_route4_add(VRF, be("21.0.0.0"), 8, 0, 101, ORIGIN_STATIC, 0))
+    st2 = stats()
+    assert st2["commits"] - st1["commits"] == 1 and st2["pending"] == 0
+    # nexthop 100 deleted through the API: its 10,000 routes go (route events,
+    # held), then nexthop_destroy's pre-delete publishes them before its
+    # synchronize; nothing is left for the turn's end
+    ok(L.gc_nh_del(100, 0))
+    st3 = stats()
+    assert st3["presync"] - st2["presync"] >= 1, (st2, st3)
+    assert st3["pending"] == 0 and st3["routes4"] == st2["routes4"] - 10_000  # the group keeps its route
 
 
 def test_mirror_without_the_patch_misses_internal_objects(control):

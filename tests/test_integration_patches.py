@@ -68,12 +68,19 @@ def test_control_patch_feeds_the_mirror():
     pushed = set(re.findall(r"event_push_internal\((GR_EVENT_\w+)", added))
     assert pushed == {"GR_EVENT_NEXTHOP_NEW", "GR_EVENT_NEXTHOP_UPDATE", "GR_EVENT_NEXTHOP_DELETE",
                       "GR_EVENT_IP_ROUTE_ADD", "GR_EVENT_IP_ROUTE_DEL", "GR_EVENT_IP6_ROUTE_ADD",
-                      "GR_EVENT_IP6_ROUTE_DEL"}, pushed
+                      "GR_EVENT_IP6_ROUTE_DEL", "GR_EVENT_NEXTHOP_PRE_DELETE"}, pushed
     mirror = open(os.path.join(ROOT, "grout_amd", "graph", "gpu_fwd4_control.c")).read()
     subs = mirror[mirror.index("obj_evs[] = {"):]
     subs = subs[:subs.index("};")]
-    assert pushed <= set(re.findall(r"GR_EVENT_\w+", subs))
     assert "event_subscribe_internal(obj_evs[k]" in mirror
+    subscribed = set(re.findall(r"GR_EVENT_\w+", subs)) | set(
+        re.findall(r"event_subscribe_internal\((GR_EVENT_\w+)", mirror))
+    assert pushed <= subscribed, pushed - subscribed
+    # the pre-delete event, before nexthop_destroy's synchronize, in the patch and the stand-in
+    nh_hunk = text[text.index("+++ b/modules/infra/control/nexthop.c"):]
+    assert nh_hunk.index("event_push_internal(GR_EVENT_NEXTHOP_PRE_DELETE") < nh_hunk.index(
+        "rte_rcu_qsbr_synchronize(gr_datapath_rcu()")
+    assert "#define GR_EVENT_NEXTHOP_PRE_DELETE GR_MSG_TYPE(GR_INFRA_MODULE, 0x30ff)" in added
     stand_in = open(os.path.join(ROOT, "grout_amd", "graph", "gr_control_min.c")).read()
     assert pushed <= set(re.findall(r"event_push_internal\((GR_EVENT_\w+)", stand_in))
     # the internal channel's API and the event objects as the patch declares them
