@@ -23,9 +23,11 @@
 // index for the struct nexthop * grout's FIB holds (route.c:124-145); the slot
 // is taken at the nexthop's first event and given back at its DELETE, which
 // grout pushes after rte_rcu_qsbr_synchronize (modules/infra/control/nexthop.c:505-513), when no
-// batch can name it any more. Every route change is published at once
-// (gpu_fwd4_fib4_commit), so the route is gone from every GPU before grout's
-// synchronize for its nexthop starts.
+// batch can name it any more. Route changes are published in batches
+// (gpu_fwd4_fib4_commit at the control loop turn's end, every 4096 changes,
+// and at GR_EVENT_NEXTHOP_PRE_DELETE, which the patch pushes before
+// nexthop_destroy's synchronize), so a route is gone from every GPU before
+// grout's synchronize for its nexthop starts.
 #pragma once
 
 #include <grout_hip.h>
