@@ -25,6 +25,19 @@ sys.path.insert(0, ROOT)
 
 # algorithmic HBM bytes per packet: line in, metadata in, one
 # FIB entry (2 or 4 bytes by device format), line out, verdict out
+def host_cpus():
+    """The CPUs the CPU baseline may use: the process's cpuset, and the
+    cgroup's CPU-time quota (cgroup v2 cpu.max) when one is set: a box's 16
+    cores are a share of a larger host, which is why the baseline varies by box."""
+    out = {"allowed": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()}
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        out["quota_cpus"] = None if quota == "max" else round(int(quota) / int(period), 2)
+    except (OSError, ValueError):
+        out["quota_cpus"] = None
+    return out
+
+
 def b_pkt(fib_entry_bytes, out_bytes=64):
     return 64 + 8 + fib_entry_bytes + out_bytes + 8
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
@@ -415,6 +428,7 @@ def main():
             "single_core_mpps": round(m1, 2),
             "per_core_mpps": round(mS / threads, 2),
             "fib_copy_mpps": round(mN, 2),
+            "host_cpus": host_cpus(),
             "sample": (f"oracle C restatement of grout's node chain (bursts of 64, "
                        f"{'per-length prefix hash LPM6' if args.workload == 'fullview6' else 'DIR24_8 8-byte entries'}), "
                        f"{threads} pinned threads on one shared FIB (grout's layout: one rte_fib per VRF), "

@@ -1581,7 +1581,15 @@ double or_bench(
 	pthread_barrier_t ready, go;
 	pthread_barrier_init(&ready, NULL, (unsigned)threads + 1);
 	pthread_barrier_init(&go, NULL, (unsigned)threads + 1);
-	int ncpu = (int)sysconf(_SC_NPROCESSORS_ONLN);
+	// the CPUs this process may run on (a container's cpuset), in order:
+	// worker i is pinned to the i-th of them when there are enough
+	cpu_set_t allowed;
+	int cpus[CPU_SETSIZE], ncpu = 0;
+	if (sched_getaffinity(0, sizeof(allowed), &allowed) == 0) {
+		for (int c = 0; c < CPU_SETSIZE; c++)
+			if (CPU_ISSET(c, &allowed))
+				cpus[ncpu++] = c;
+	}
 	for (int i = 0; i < threads; i++) {
 		args[i] = (struct bench_arg) {
 			.t = t,
@@ -1592,7 +1600,7 @@ double or_bench(
 			.start = (uint32_t)((uint64_t)i * n / (uint64_t)threads), // each worker its own part first
 			.todo = (pkts_per_thread + OR_BURST - 1) / OR_BURST * OR_BURST,
 			.flags = flags,
-			.cpu = threads <= ncpu ? i : -1,
+			.cpu = threads <= ncpu ? cpus[i] : -1,
 			.ready = &ready,
 			.go = &go,
 		};

@@ -18,6 +18,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import oracle  # noqa: E402  (test infrastructure: the CPU baseline only)
+from bench import host_cpus  # noqa: E402
 from grout_amd import synth as S  # noqa: E402
 from grout_amd import topology as T  # noqa: E402
 
@@ -40,7 +41,7 @@ def main():
         print(json.dumps({"rep": rep, "single_core_mpps": round(m1, 2), "cores": threads,
                           "fib_copy_mpps": round(mN, 2), "fib_copy_per_core": round(mN / threads, 2),
                           "shared_fib_mpps": round(mS, 2), "shared_fib_per_core": round(mS / threads, 2),
-                          "wall_s": round(time.time() - t0, 1)}), flush=True)
+                          "host_cpus": host_cpus(), "wall_s": round(time.time() - t0, 1)}), flush=True)
     o.close()
 
 
