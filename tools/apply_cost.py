@@ -8,7 +8,9 @@ no GPU wait: the verdicts and header lines come from one GPU pass over the
 stream (gr_hip_fwd4_host) before the clocks start. The mbufs (rte_mbuf,
 private area, frame: 2304-byte objects) sit on transparent huge pages, as
 DPDK's mempools sit on hugepages. Variants on one library: with and without
-the per-iface and per-node counters, so that each part's share shows.
+the per-iface and per-node counters, so that each part's share shows, and
+with the frames taken as already rewritten (lines NULL: what the hand-back
+would cost if the GPU wrote its prefixes into the frames itself).
 Compare library builds by running this once per build, alternating
 (--lib build/ab/<name>.so; tools/ab_libs.sh's pattern).
 
@@ -115,7 +117,7 @@ def main():
 
     m0 = m.copy()
 
-    def apply_pass(ifst, stats, direct=True):
+    def apply_pass(ifst, stats, direct=True, in_place=False):
         t = 0.0
         for s in starts:
             if not direct:  # the views are written: each pass starts from the RX state
@@ -123,7 +125,7 @@ def main():
             d = Direct(mbufs=int(ptrs.ctypes.data) + 8 * s, lay=ctypes.addressof(lay), edges=edges.ctypes.data)
             t0 = time.perf_counter()
             r = L.gr_node_apply_ex(int(m.ctypes.data) + m.itemsize * s, B, 64, None,
-                                   int(out32.ctypes.data) + abi.PREFIX * s, abi.PREFIX,
+                                   None if in_place else int(out32.ctypes.data) + abi.PREFIX * s, abi.PREFIX,
                                    int(v.ctypes.data) + v.itemsize * s, ifaces.ctypes.data, len(ifaces),
                                    nh.ctypes.data, len(nh), ns.ctypes.data if stats else None, vl.ctypes.data,
                                    st.ctypes.data if ifst else None, len(st),
@@ -143,13 +145,13 @@ def main():
         return t * 1e9 / (len(starts) * B)
 
     variants = {"apply": (1, 1, True), "apply_no_iface_counters": (0, 1, True), "apply_no_counters": (0, 0, True),
-                "apply_onto_views": (1, 1, False)}
+                "apply_onto_views": (1, 1, False), "apply_frames_rewritten_by_gpu": (0, 1, True, True)}
     apply_pass(1, 1)  # warm-up: pages, code
     res = {k: [] for k in variants}
     res["stage"] = []
     for _ in range(args.reps):
-        for k, (a, b, c) in variants.items():
-            res[k].append(apply_pass(a, b, c))
+        for k, v in variants.items():
+            res[k].append(apply_pass(*v))
         res["stage"].append(stage_pass())
     fwd = float((v["edge"] == abi.EDGE["port_output"]).mean())
     print(json.dumps({"lib": os.path.relpath(abi.LIB_HIP, ROOT), "pkts": len(starts) * B, "batch": B,
