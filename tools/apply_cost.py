@@ -150,8 +150,8 @@ def main():
     res = {k: [] for k in variants}
     res["stage"] = []
     for _ in range(args.reps):
-        for k, v in variants.items():
-            res[k].append(apply_pass(*v))
+        for k, a in variants.items():
+            res[k].append(apply_pass(*a))
         res["stage"].append(stage_pass())
     fwd = float((v["edge"] == abi.EDGE["port_output"]).mean())
     print(json.dumps({"lib": os.path.relpath(abi.LIB_HIP, ROOT), "pkts": len(starts) * B, "batch": B,
