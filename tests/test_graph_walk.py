@@ -410,11 +410,18 @@ def check_walk(topo, fr, me, labels=None, burst=BURST, loaded=False):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pin", [1, 0])
-def test_graph_walk_corpus(pin):
-    """Every edge. pin 1: the mbuf memory is registered, frames go to the GPU
-    by address and come back rewritten in place; pin 0: header lines staged."""
+@pytest.mark.parametrize("pin,ptrs", [(1, 0), (0, 0), (1, 1), (0, 1)],
+                         ids=["registered_staged", "staged", "by_address", "by_address_unregistered"])
+def test_graph_walk_corpus(pin, ptrs):
+    """Every edge. pin 1: the mbuf memory is registered with the contexts;
+    ptrs ("node_ptrs") 1: registered frames go to the GPU by address and come
+    back rewritten in place (the node appends the mbufs themselves: their
+    device addresses are taken through the layout at send), and with the
+    memory not registered the lines are staged at send instead, from the
+    mbufs; ptrs 0: header lines staged as the walks arrive (the default)."""
     lib().gh_set_pin(pin)
+    fp = graph_ctx()
+    fp.tune("node_ptrs", ptrs)
     t, _ = SC.corpus_topology()
     fr, me, lab = SC.corpus_arrays()
     # ol_flags has no value for the corpus's out-of-range status 3 ("ol 3")
@@ -424,6 +431,7 @@ def test_graph_walk_corpus(pin):
         got = check_walk(t, fr, me, lab)
     finally:
         lib().gh_set_pin(1)
+        fp.tune("node_ptrs", 0)
     assert len(set(got["edge"])) > 20
 
 
