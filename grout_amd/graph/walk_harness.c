@@ -122,6 +122,14 @@ void gh_set_rx_touch(int on) {
 	rx_touch = on;
 }
 
+// Measurement: port_rx hands its bursts straight to port_output, past the
+// node (the harness's own cost per packet, without the fast path).
+static int null_node;
+
+void gh_set_null_node(int on) {
+	null_node = on;
+}
+
 static uint16_t port_rx_process(struct rte_graph *graph, struct rte_node *node, void **objs, uint16_t nb) {
 	(void)objs;
 	(void)nb;
@@ -148,7 +156,7 @@ static uint16_t port_rx_process(struct rte_graph *graph, struct rte_node *node, 
 		d->vlan_id = pm->vlan_ck & 0xfff;
 		burst[k++] = m;
 	}
-	rte_node_enqueue(graph, node, 0, burst, (uint16_t)k);
+	rte_node_enqueue(graph, node, null_node ? 1 : 0, burst, (uint16_t)k);
 	return (uint16_t)k;
 }
 
@@ -166,8 +174,8 @@ static struct rte_node_register port_rx_node = {
 	.flags = RTE_NODE_SOURCE_F,
 	.init = graph_slot_init,
 	.process = port_rx_process,
-	.nb_edges = 1,
-	.next_nodes = {"iface_input"},
+	.nb_edges = 2,
+	.next_nodes = {"iface_input", "port_output"},
 };
 
 // a recorder's ctx holds its recorder id

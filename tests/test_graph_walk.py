@@ -191,7 +191,9 @@ def test_node_registration():
     want = ["iface_input_cpu"] + abi.EDGE_NAMES[1:]  # PUNT: grout's stock iface_input, renamed
     assert edges_of("iface_input") == want
     assert edges_of("gpu_fwd4_flush") == want
-    assert edges_of("port_rx") == ["iface_input"]
+    # port_rx (the harness's stand-in) feeds iface_input; port_output only in the
+    # harness-alone measurement (gh_set_null_node)
+    assert edges_of("port_rx") == ["iface_input", "port_output"]
     # the CPU continuation nodes and where they go (ip_input.c:20-32, ip_output.c:21-30)
     assert edges_of("ip_input_local_ct") == ["ip_input_local", "dnat44_dynamic"]
     snat = edges_of("ip_output_snat")

@@ -57,19 +57,33 @@ def main():
     fp.tune("node_ptrs", args.pin)
     L.gh_set_pin(args.pin)  # 0: staged header lines, the node's default
     L.gh_set_rx_touch(args.rx_touch)
+    L.gh_set_null_node.argtypes = [ctypes.c_int]
+
+    def run(k, m, null):
+        L.gh_set_null_node(null)
+        try:
+            assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, m) == 0
+            L.gh_workers_run(k, ctypes.byref(ctypes.c_double()), None)  # warm-up: pages, queues, pinned slots
+            best = []
+            for _ in range(args.reps):
+                assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, m) == 0  # the frames as they came
+                s, w = ctypes.c_double(), ctypes.c_uint64()
+                rr = L.gh_workers_run(k, ctypes.byref(s), ctypes.byref(w))
+                assert rr == 0, rr
+                best.append(s.value)
+            return float(np.median(best))
+        finally:
+            L.gh_set_null_node(0)
+
     for k in threads:
         m = k * args.per_thread
-        assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, m) == 0
-        L.gh_workers_run(k, ctypes.byref(ctypes.c_double()), None)  # warm-up: pages, queues, pinned slots
-        best = []
-        for _ in range(args.reps):
-            assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, m) == 0  # the frames as they came
-            s, w = ctypes.c_double(), ctypes.c_uint64()
-            rr = L.gh_workers_run(k, ctypes.byref(s), ctypes.byref(w))
-            assert rr == 0, rr
-            best.append(s.value)
-        t = float(np.median(best))
-        print(json.dumps({"threads": k, "gpus": 1, "mbufs": m, "batch": args.batch, "rx_touch": args.rx_touch, "mode": "frames by address" if args.pin else "staged lines",
+        t = run(k, m, 0)
+        # the same walks with port_rx handing its bursts straight to port_output:
+        # the harness's own cost, which the node's walk pays too
+        t0 = run(k, m, 1)
+        print(json.dumps({"threads": k, "gpus": 1, "mbufs": m, "batch": args.batch, "rx_touch": args.rx_touch,
+                          "harness_alone_mpps": round(m / t0 / 1e6, 1),
+                          "node_ns_per_pkt_per_worker": round((t - t0) * 1e9 * k / m, 1), "mode": "frames by address" if args.pin else "staged lines",
                           "ms": round(t * 1e3, 2), "mpps_aggregate": round(m / t / 1e6, 1),
                           "mpps_per_worker": round(m / t / 1e6 / k, 1),
                           "cpu_ns_per_pkt_per_worker": round(t * 1e9 * k / m, 1)}), flush=True)
