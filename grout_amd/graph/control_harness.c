@@ -332,6 +332,28 @@ int gc_arp(uint16_t iface_id, uint32_t sip_be, const uint8_t *mac) {
 	memcpy(a.mac, mac, 6);
 	return on_control(do_arp, &a);
 }
+// count neighbours from sip (host-order steps) learned in one control turn,
+// as an ARP storm reaches grout
+struct a_arps {
+	uint16_t iface_id;
+	uint32_t ip_host, count;
+	uint8_t mac[6];
+};
+static int do_arp_many(void *p) {
+	const struct a_arps *a = p;
+	for (uint32_t k = 0; k < a->count; k++) {
+		const int r = arp_probe_input(a->iface_id, __builtin_bswap32(a->ip_host + k), &MAC(a->mac));
+		if (r < 0)
+			return r;
+	}
+	return 0;
+}
+int gc_arp_many(uint16_t iface_id, uint32_t sip_be, uint32_t count, const uint8_t *mac) {
+	struct a_arps a = {.iface_id = iface_id, .ip_host = __builtin_bswap32(sip_be), .count = count};
+	memcpy(a.mac, mac, 6);
+	return on_control(do_arp_many, &a);
+}
+
 int gc_ndp(uint16_t iface_id, const uint8_t *ip, const uint8_t *mac) {
 	struct a_l3 a = {.iface_id = iface_id};
 	memcpy(a.ip, ip, 16);

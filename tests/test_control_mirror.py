@@ -74,6 +74,7 @@ def lib():
             "gc_route4_add": (I, [U16, U32, U8, U32, U32, U8, I]), "gc_route4_del": (I, [U16, U32, U8, I]),
             "gc_route6_add": (I, [U16, P, U8, P, U32, U8, I]), "gc_route6_del": (I, [U16, P, U8, I]),
             "gc_route4_add_many": (I, [U16, U32, U8, U32, U32, U8]),
+            "gc_arp_many": (I, [U16, U32, U32, P]),
             "gc_arp": (I, [U16, U32, P]), "gc_ndp": (I, [U16, P, P]),
             "gc_resolve4": (I, [U16, U32]), "gc_age4": (I, [U16, U32, U32, U32]),
             "gc_nh_add_l3": (I, [U32, U16, U32, P, U8, I]), "gc_nh_add_type": (I, [U32, U8, U16, U8]),
@@ -623,6 +624,16 @@ def test_control_bulk_routes_walk(mirrored):
     fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
     g = walk_check(w, fr, me, ["bulk"] * len(me))["bulk"]
     assert edges(g) == ["port_output"] and (g["iface"] == PORTS[3]).all()
+    # an ARP storm: 2,000 neighbours learned in one turn (each a LEARN nexthop,
+    # pushed at once, and its INTERNAL /32, published with the turn)
+    s0 = stats()
+    t0 = time.perf_counter()
+    ok(L.gc_arp_many(PORTS[2], be("10.9.0.1"), 2000, mac(NEIGH_MAC)))
+    dt = time.perf_counter() - t0
+    s1 = stats()
+    assert s1["slots_used"] - s0["slots_used"] == 2000 and s1["routes4"] - s0["routes4"] == 2000
+    assert s1["commits"] - s0["commits"] == 1 and s1["errors"] == 0, (s0, s1)
+    print(f"2000 neighbours in one turn: {dt:.3f} s ({dt / 2000 * 1e6:.0f} us each)")
     # their nexthop deleted through the API: the routes go first, published before the synchronize
     p0 = stats()["presync"]
     ok(L.gc_nh_del(100, 0))
