@@ -168,6 +168,8 @@ static struct {
 	// route changes applied to every context's RIB and not yet published
 	// (see "publication" below)
 	uint8_t *dirty4, *dirty6; // [max_ifaces] by VRF id
+	uint32_t *nh_dirty, n_nh_dirty; // L3 nexthop slots whose mirror waits for the publication
+	uint8_t *nh_is_dirty; // [max_nh + 1]
 	uint32_t pending;
 	struct event *flush_ev;
 	int flush_armed;
@@ -200,8 +202,11 @@ static int ready(void) {
 	M.fibs = calloc(M.max_ifaces, sizeof(*M.fibs));
 	M.dirty4 = calloc(M.max_ifaces, 1);
 	M.dirty6 = calloc(M.max_ifaces, 1);
+	M.nh_dirty = calloc(M.max_nh + 1, sizeof(uint32_t));
+	M.nh_is_dirty = calloc(M.max_nh + 1, 1);
 	if (M.free_slots == NULL || M.nh == NULL || M.ifs == NULL || M.if_live == NULL || M.if_seen == NULL
-	    || M.if_removing == NULL || M.fibs == NULL || M.dirty4 == NULL || M.dirty6 == NULL) {
+	    || M.if_removing == NULL || M.fibs == NULL || M.dirty4 == NULL || M.dirty6 == NULL || M.nh_dirty == NULL
+	    || M.nh_is_dirty == NULL) {
 		gpu_fwd4_control_reset();
 		return -ENOMEM;
 	}
@@ -227,6 +232,8 @@ void gpu_fwd4_control_reset(void) {
 	free(M.fibs);
 	free(M.dirty4);
 	free(M.dirty6);
+	free(M.nh_dirty);
+	free(M.nh_is_dirty);
 	if (M.flush_ev != NULL)
 		event_free(M.flush_ev);
 	memset(&M, 0, sizeof(M));
@@ -333,7 +340,12 @@ static void reta_free(uint32_t off, uint32_t len) {
 // struct nexthop (nexthop.h:22-96) -> struct gr_hip_nh. A group's reta
 // (struct nexthop *[reta_size], group_nexthop.c:27-56) becomes slots in a
 // range of the contexts' reta table; the range is kept while the size is.
+static void nh_changed(uint32_t slot);
+static void nh_flush(void);
+
 static int push_nh(uint32_t slot, const struct nexthop *nh) {
+	if (nh->type != GR_NH_T_L3)
+		nh_flush(); // the slots a group or a type nexthop may name are on every GPU first
 	struct gr_hip_nh o;
 	memset(&o, 0, sizeof(o));
 	o.type = nh->type;
@@ -372,8 +384,11 @@ static int push_nh(uint32_t slot, const struct nexthop *nh) {
 			o.reta_off = new_off;
 		}
 	}
-	note(r = gpu_fwd4_nh_set(slot, &o, 1));
 	M.nh[slot] = o;
+	if (nh->type == GR_NH_T_L3)
+		nh_changed(slot); // published before any route or group naming it (see "publication")
+	else
+		note(r = gpu_fwd4_nh_set(slot, &o, 1));
 	// the old range goes once the nexthop no longer names it
 	if (old.type == GR_NH_T_GROUP && old.n_members > 1 && old.reta_size > 0
 	    && !(new_len == old.reta_size && new_off == old.reta_off))
@@ -400,7 +415,7 @@ static void on_nexthop(uint32_t ev, const void *obj) {
 			return;
 		const struct gr_hip_nh old = M.nh[slot];
 		memset(&M.nh[slot], 0, sizeof(M.nh[slot]));
-		note(gpu_fwd4_nh_set(slot, &M.nh[slot], 1));
+		nh_changed(slot); // no route names it since grout's synchronize
 		note(gpu_fwd4_nh_obj_set(slot, NULL));
 		if (old.type == GR_NH_T_GROUP && old.n_members > 1)
 			reta_free(old.reta_off, old.reta_size);
@@ -442,6 +457,28 @@ static void commit6(uint16_t vrf_id) {
 #define PUBLISH_BATCH 4096
 #define PUBLISH_DELAY_US 200
 
+static int cmp_u32(const void *a, const void *b) {
+	const uint32_t x = *(const uint32_t *)a, y = *(const uint32_t *)b;
+	return x < y ? -1 : x > y;
+}
+
+// The L3 nexthops changed since the last publication onto every GPU, one
+// call per run of consecutive slots (a burst of learned neighbours takes
+// consecutive slots).
+static void nh_flush(void) {
+	if (M.n_nh_dirty == 0)
+		return;
+	qsort(M.nh_dirty, M.n_nh_dirty, sizeof(uint32_t), cmp_u32);
+	for (uint32_t i = 0, j; i < M.n_nh_dirty; i = j) {
+		for (j = i + 1; j < M.n_nh_dirty && M.nh_dirty[j] == M.nh_dirty[j - 1] + 1; j++)
+			;
+		note(gpu_fwd4_nh_set(M.nh_dirty[i], &M.nh[M.nh_dirty[i]], j - i));
+	}
+	for (uint32_t i = 0; i < M.n_nh_dirty; i++)
+		M.nh_is_dirty[M.nh_dirty[i]] = 0;
+	M.n_nh_dirty = 0;
+}
+
 void gpu_fwd4_control_flush(void) {
 	if (M.flush_armed) {
 		evtimer_del(M.flush_ev);
@@ -449,6 +486,7 @@ void gpu_fwd4_control_flush(void) {
 	}
 	if (M.pending == 0)
 		return;
+	nh_flush(); // before the routes that may name them
 	for (uint32_t v = 0; v < M.max_ifaces; v++) {
 		if (M.dirty4[v])
 			commit4((uint16_t)v);
@@ -466,8 +504,7 @@ static void publish_cb(int fd, short what, void *arg) {
 	gpu_fwd4_control_flush();
 }
 
-static void route_changed(uint16_t vrf_id, int ip6) {
-	(ip6 ? M.dirty6 : M.dirty4)[vrf_id] = 1;
+static void publish_later(void) {
 	if (++M.pending >= PUBLISH_BATCH) {
 		gpu_fwd4_control_flush();
 		return;
@@ -482,6 +519,19 @@ static void route_changed(uint16_t vrf_id, int ip6) {
 		return;
 	}
 	M.flush_armed = 1;
+}
+
+static void route_changed(uint16_t vrf_id, int ip6) {
+	(ip6 ? M.dirty6 : M.dirty4)[vrf_id] = 1;
+	publish_later();
+}
+
+static void nh_changed(uint32_t slot) {
+	if (!M.nh_is_dirty[slot]) {
+		M.nh_is_dirty[slot] = 1;
+		M.nh_dirty[M.n_nh_dirty++] = slot;
+	}
+	publish_later();
 }
 
 static void shadow_route4(const struct gr_hip_route4 *rt, int add) {
