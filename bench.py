@@ -38,6 +38,38 @@ def host_cpus():
     return out
 
 
+def _cpu_sysfs(cpu, leaf):
+    try:
+        return open(f"/sys/devices/system/cpu/cpu{cpu}/{leaf}").read().strip()
+    except OSError:
+        return None
+
+
+def cpu_placement(n, policy="spread"):
+    """CPUs for n pinned workers, or None (the i-th allowed CPU each).
+    "spread": one hardware thread per physical core, the cores taken round
+    robin over the L3 domains (a Zen CCD: 8 cores, one L3 and one link to
+    memory), socket by socket; a grout deployment spreads its lcores the same
+    way. None when the topology is unreadable or has fewer cores than n."""
+    if policy != "spread" or not hasattr(os, "sched_getaffinity"):
+        return None
+    domains = {}
+    for c in sorted(os.sched_getaffinity(0)):
+        sib = _cpu_sysfs(c, "topology/thread_siblings_list")
+        if sib is None:
+            return None
+        first = int(sib.replace("-", ",").split(",")[0])
+        if first != c:
+            continue  # an SMT sibling of a core already listed
+        pkg = _cpu_sysfs(c, "topology/physical_package_id") or "0"
+        l3 = _cpu_sysfs(c, "cache/index3/id") or pkg
+        domains.setdefault((int(pkg), int(l3)), []).append(c)
+    order, lists = [], [domains[k] for k in sorted(domains)]
+    for i in range(max((len(x) for x in lists), default=0)):
+        order += [x[i] for x in lists if i < len(x)]
+    return order[:n] if len(order) >= n else None
+
+
 def b_pkt(fib_entry_bytes, out_bytes=64):
     return 64 + 8 + fib_entry_bytes + out_bytes + 8
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak

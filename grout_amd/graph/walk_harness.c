@@ -17,6 +17,8 @@
 // which node each mbuf reached, in order, and keeps the mbuf.
 // mbufs are built like grout's pool (mempool.c:57-100): 128-byte rte_mbuf,
 // 64-byte private area, 2048-byte data room, frame at headroom 128.
+#define _GNU_SOURCE // pthread_setaffinity_np, CPU_SET
+
 #include "gpu_fwd4_control.h"
 #include "gpu_fwd4_node.h"
 #include "gr_control_min.h"
@@ -82,8 +84,17 @@ static struct {
 		// mbufs [rx_next, rx_end) and what reached its recorders
 		uint32_t rx_next, rx_end;
 		uint64_t recorded;
+		// recycle mode: the worker's mempool, a stack of free mbuf indices;
+		// rx_next .. rx_end count the passes over its share rx_start + [0, share)
+		uint32_t *free_mb, n_free;
+		uint32_t rx_start, share;
 	} graphs[GH_MAX_GRAPHS];
+	const uint8_t *frames_in; // gh_load's stream (recycle mode refills the mbufs from it)
+	uint32_t stride_in;
+	uint32_t recycle; // workers mode: mbufs per worker's pool (0: every packet its own mbuf)
+	uint32_t passes; // recycle mode: times each worker goes over its share of the stream
 	int workers; // gh_workers_run is walking every graph from its own thread
+	int lcores[GH_MAX_GRAPHS], n_lcores; // workers mode: worker k pinned to lcores[k] (k < n_lcores)
 	uint32_t loop; // walks since the last housekeeping tick (main_loop.c:461)
 	uint8_t *if_dead, *nh_dead; // objects the RCU test's control thread freed
 	uint32_t freed_reads; // grout nodes behind the edges read a freed object
@@ -130,6 +141,29 @@ void gh_set_null_node(int on) {
 	null_node = on;
 }
 
+// Workers mode: each worker's packets through a pool of `pool` mbufs of its
+// own, refilled from the loaded stream as they come back from the recorders
+// (a mempool and its per-lcore cache), instead of one mbuf per packet, going
+// `passes` times over its share of the stream. pool 0: off.
+void gh_set_recycle(uint32_t pool, uint32_t passes) {
+	H.recycle = pool;
+	H.passes = passes ? passes : 1;
+}
+
+// Workers mode: worker k pinned to cpus[k], as grout pins each worker to its
+// lcore. n 0: the scheduler places them.
+int gh_set_lcores(const int *cpus, int n) {
+	if (n < 0 || n > GH_MAX_GRAPHS)
+		return -EINVAL;
+	for (int k = 0; k < n; k++) {
+		if (cpus[k] < 0 || cpus[k] >= CPU_SETSIZE)
+			return -EINVAL;
+		H.lcores[k] = cpus[k];
+	}
+	H.n_lcores = n;
+	return 0;
+}
+
 static uint16_t port_rx_process(struct rte_graph *graph, struct rte_node *node, void **objs, uint16_t nb) {
 	(void)objs;
 	(void)nb;
@@ -140,6 +174,33 @@ static uint16_t port_rx_process(struct rte_graph *graph, struct rte_node *node, 
 	if (H.workers && node->ctx[0] != 0) {
 		next = &H.graphs[node->ctx[0] - 1].rx_next;
 		end = H.graphs[node->ctx[0] - 1].rx_end;
+	}
+	if (H.workers && H.recycle && node->ctx[0] != 0) {
+		// recycle mode: each packet of the worker's share of the stream into
+		// an mbuf of its pool, as a PMD refills its RX ring from a mempool
+		// (the NIC's DMA writes the frame, DDIO lands it in the LLC)
+		__typeof__(&H.graphs[0]) G = &H.graphs[node->ctx[0] - 1];
+		while (k < H.rx_burst && G->rx_next < G->rx_end && G->n_free > 0) {
+			const uint32_t i = G->rx_start + (G->rx_next++ - G->rx_start) % G->share;
+			struct rte_mbuf *m = mbuf_at(G->free_mb[--G->n_free]);
+			const struct gr_hip_pkt_meta *pm = &H.meta_in[i];
+			m->data_off = RTE_PKTMBUF_HEADROOM;
+			m->pkt_len = pm->pkt_len;
+			m->data_len = pm->pkt_len;
+			m->packet_type = 0;
+			m->hash.rss = pm->rss;
+			const uint32_t ck = (pm->vlan_ck >> 12) & 3;
+			m->ol_flags = ck == GR_HIP_CKSUM_BAD ? RTE_MBUF_F_RX_IP_CKSUM_BAD
+				: ck == GR_HIP_CKSUM_GOOD    ? RTE_MBUF_F_RX_IP_CKSUM_GOOD
+							     : RTE_MBUF_F_RX_IP_CKSUM_UNKNOWN;
+			memcpy(rte_pktmbuf_mtod(m, uint8_t *), H.frames_in + (size_t)i * H.stride_in, H.stride_in);
+			struct iface_mbuf_data *d = iface_mbuf_data(m);
+			d->iface = iface_from_id(pm->iface);
+			d->vlan_id = pm->vlan_ck & 0xfff;
+			burst[k++] = m;
+		}
+		rte_node_enqueue(graph, node, null_node ? 1 : 0, burst, (uint16_t)k);
+		return (uint16_t)k;
 	}
 	while (k < H.rx_burst && *next < end) {
 		const uint32_t i = (*next)++;
@@ -183,8 +244,13 @@ static uint16_t recorder_process(struct rte_graph *graph, struct rte_node *node,
 	(void)graph;
 	const uint8_t id = node->ctx[0];
 	if (H.workers) { // a rate measurement: grout's node behind the edge takes the mbufs, no record
-		if (node->ctx[1] != 0)
-			H.graphs[node->ctx[1] - 1].recorded += nb;
+		if (node->ctx[1] != 0) {
+			__typeof__(&H.graphs[0]) G = &H.graphs[node->ctx[1] - 1];
+			G->recorded += nb;
+			if (H.recycle) // back to the worker's mempool (port_tx's completion, a drop node's free)
+				for (uint16_t k = 0; k < nb; k++)
+					G->free_mb[G->n_free++] = (uint32_t)(((uint8_t *)objs[k] - H.mem) / GH_MBUF_SZ);
+		}
 		return nb;
 	}
 	for (uint16_t k = 0; k < nb; k++) {
@@ -557,6 +623,8 @@ int gh_load(const uint8_t *frames, uint32_t stride, const struct gr_hip_pkt_meta
 	H.next_rx = 0;
 	H.recorded = 0;
 	H.meta_in = meta;
+	H.frames_in = frames; // the caller keeps it while it walks (recycle mode)
+	H.stride_in = stride;
 	if (H.pin && n && gpu_fwd4_n_ctx() != 0) {
 		int r = gpu_fwd4_host_register(H.mem, (size_t)n * GH_MBUF_SZ);
 		if (r < 0)
@@ -1137,6 +1205,7 @@ int gh_reload_test(uint32_t walks, int drain, struct gh_reload_result *res) {
 // ---- several workers, one graph each, on one GPU ----------------------------
 struct gh_workers_arg {
 	int k; // graph slot
+	int cpu; // -1: not pinned
 	pthread_barrier_t *bar;
 	uint64_t walks;
 	int err;
@@ -1145,6 +1214,12 @@ struct gh_workers_arg {
 static void *worker_thread(void *p) {
 	struct gh_workers_arg *a = p;
 	struct rte_graph *g = H.graphs[a->k].graph;
+	if (a->cpu >= 0) { // grout's worker on its lcore (worker.c: the thread's affinity)
+		cpu_set_t set;
+		CPU_ZERO(&set);
+		CPU_SET(a->cpu, &set);
+		pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+	}
 	pthread_barrier_wait(a->bar);
 	uint64_t w = 0;
 	const uint64_t want = H.graphs[a->k].rx_end - (H.graphs[a->k].rx_next);
@@ -1178,14 +1253,34 @@ int gh_workers_run(uint32_t threads, double *seconds, uint64_t *walks) {
 			return -ENOENT;
 	pthread_t th[GH_MAX_GRAPHS];
 	struct gh_workers_arg args[GH_MAX_GRAPHS];
+	if (H.recycle && ((uint64_t)H.recycle * threads > H.n || (uint64_t)H.n * H.passes > UINT32_MAX))
+		return -EINVAL; // the pools are carved out of the loaded mbufs
 	pthread_barrier_t bar;
-	pthread_barrier_init(&bar, NULL, threads + 1);
 	for (uint32_t k = 0; k < threads; k++) {
 		H.graphs[k].rx_next = (uint32_t)((uint64_t)H.n * k / threads);
 		H.graphs[k].rx_end = (uint32_t)((uint64_t)H.n * (k + 1) / threads);
 		H.graphs[k].recorded = 0;
-		args[k] = (struct gh_workers_arg) {.k = (int)k, .bar = &bar};
+		if (H.recycle) {
+			H.graphs[k].free_mb = malloc(H.recycle * sizeof(uint32_t));
+			if (H.graphs[k].free_mb == NULL) {
+				for (uint32_t j = 0; j < k; j++) {
+					free(H.graphs[j].free_mb);
+					H.graphs[j].free_mb = NULL;
+				}
+				return -ENOMEM;
+			}
+			for (uint32_t j = 0; j < H.recycle; j++) // popped from the top: lowest index first
+				H.graphs[k].free_mb[j] = k * H.recycle + (H.recycle - 1 - j);
+			H.graphs[k].n_free = H.recycle;
+			H.graphs[k].rx_start = H.graphs[k].rx_next;
+			H.graphs[k].share = H.graphs[k].rx_end - H.graphs[k].rx_next;
+			H.graphs[k].rx_end = H.graphs[k].rx_next + H.graphs[k].share * H.passes;
+		}
+		args[k] = (struct gh_workers_arg) {.k = (int)k, .cpu = -1, .bar = &bar};
 	}
+	for (uint32_t k = 0; k < threads && (int)k < H.n_lcores; k++)
+		args[k].cpu = H.lcores[k];
+	pthread_barrier_init(&bar, NULL, threads + 1);
 	H.workers = 1;
 	for (uint32_t k = 0; k < threads; k++)
 		pthread_create(&th[k], NULL, worker_thread, &args[k]);
@@ -1204,6 +1299,11 @@ int gh_workers_run(uint32_t threads, double *seconds, uint64_t *walks) {
 	}
 	H.workers = 0;
 	pthread_barrier_destroy(&bar);
+	for (uint32_t k = 0; k < threads; k++) {
+		free(H.graphs[k].free_mb);
+		H.graphs[k].free_mb = NULL;
+		H.graphs[k].n_free = 0;
+	}
 	*seconds = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
 	if (walks != NULL)
 		*walks = w;

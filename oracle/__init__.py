@@ -175,11 +175,16 @@ class Oracle:
                                                   ns.ctypes.data))
         return out, v, st, mb, ns[0]
 
-    def bench(self, frames, meta, threads, pkts_per_thread, fib_copy=True):
+    def bench(self, frames, meta, threads, pkts_per_thread, fib_copy=True, cpus=None):
         """or_bench (oracle.h): aggregate Mpps of `threads` pinned workers after
-        a warm-up pass each; fib_copy: each its own IPv4 FIB copy on THP."""
+        a warm-up pass each; fib_copy: each its own IPv4 FIB copy on THP;
+        cpus: worker i on cpus[i] (default: the i-th CPU the process may use)."""
         fwd = ctypes.c_uint64()
         stride = frames.shape[1]
+        c = list(cpus or [])
+        arr = (ctypes.c_int * max(1, len(c)))(*c)
+        if self.L.or_bench_set_cpus(arr, len(c)) != 0:
+            raise ValueError(f"or_bench_set_cpus {c}")
         mpps = self.L.or_bench(self.h, frames.ctypes.data, stride, meta.ctypes.data, len(meta), threads,
                                pkts_per_thread, 1 if fib_copy else 0, ctypes.byref(fwd))
         if mpps < 0:

@@ -1563,6 +1563,20 @@ static void *bench_thread(void *p) {
 	return NULL;
 }
 
+static int bench_cpus[CPU_SETSIZE], bench_ncpus;
+
+int or_bench_set_cpus(const int *cpus, int n) {
+	if (n < 0 || n > CPU_SETSIZE)
+		return -1;
+	for (int i = 0; i < n; i++)
+		if (cpus[i] < 0 || cpus[i] >= CPU_SETSIZE)
+			return -1;
+	if (n > 0)
+		memcpy(bench_cpus, cpus, sizeof(int) * (size_t)n);
+	bench_ncpus = n;
+	return 0;
+}
+
 double or_bench(
 	or_topo_t *t,
 	const void *in_frames,
@@ -1581,11 +1595,15 @@ double or_bench(
 	pthread_barrier_t ready, go;
 	pthread_barrier_init(&ready, NULL, (unsigned)threads + 1);
 	pthread_barrier_init(&go, NULL, (unsigned)threads + 1);
-	// the CPUs this process may run on (a container's cpuset), in order:
-	// worker i is pinned to the i-th of them when there are enough
+	// the CPUs this process may run on (a container's cpuset), in order, or
+	// the placement or_bench_set_cpus gave: worker i is pinned to the i-th of
+	// them when there are enough
 	cpu_set_t allowed;
 	int cpus[CPU_SETSIZE], ncpu = 0;
-	if (sched_getaffinity(0, sizeof(allowed), &allowed) == 0) {
+	if (bench_ncpus > 0) {
+		memcpy(cpus, bench_cpus, sizeof(int) * (size_t)bench_ncpus);
+		ncpu = bench_ncpus;
+	} else if (sched_getaffinity(0, sizeof(allowed), &allowed) == 0) {
 		for (int c = 0; c < CPU_SETSIZE; c++)
 			if (CPU_ISSET(c, &allowed))
 				cpus[ncpu++] = c;

@@ -127,6 +127,10 @@ int or_process_ex(
 // processes pkts_per_thread packets (rounded up to bursts). Returns the
 // aggregate Mpps over the timed part (CLOCK_MONOTONIC), -1 on error.
 #define OR_BENCH_FIB_COPY 0x1
+// or_bench_set_cpus: worker i of later or_bench runs pinned to cpus[i] (a
+// placement, e.g. one core per L3 domain) instead of the i-th allowed CPU;
+// n = 0 goes back to that. 0, or -1 when a CPU is out of range.
+int or_bench_set_cpus(const int *cpus, int n);
 double or_bench(
 	or_topo_t *,
 	const void *in_frames,

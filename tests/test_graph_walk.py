@@ -14,6 +14,7 @@ registration (edge names in enum order) and its refusal to join a graph
 without the GPU module. GPU: whole walks against the oracle's mbuf-level
 chain (oracle.c process_mbufs, lines-only: the node stages 64-byte lines)."""
 import ctypes
+import errno
 import os
 
 import numpy as np
@@ -504,6 +505,65 @@ def test_graph_walk_two_gpus():
             h = FastPath.borrow(L.gh_ctx_at(i))
             assert h.fib_lookup(1, dst) == nh_new
         _gh["state"]["key"] = None  # the topology changed under fresh_fastpath_state: reload
+    finally:
+        assert L.gh_graph_use(1) == 0
+        assert L.gh_graph_destroy() == 0
+        L.gh_graph_use(0)
+
+
+@pytest.mark.gpu
+def test_graph_workers_recycled_mbufs():
+    """The workers mode tools/node_workers.py measures: two worker graphs
+    walked from their own threads at once, each over its share of the
+    stream. With gh_set_recycle every worker's packets go through a small
+    mempool of its own (port_rx refills an mbuf from the stream when the
+    recorder behind the edge gives it back, as port_tx frees them), a pool
+    smaller than a batch included (the flush node sends partial batches):
+    every edge takes the same number of packets as with one mbuf per packet,
+    and `passes` times as many when each worker goes over its share again."""
+    L = lib()
+    L.gh_workers_run.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
+    L.gh_set_recycle.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+    L.gh_set_recycle.restype = None
+    fp = graph_ctx()
+    t = T.config_fullview(count=20_000)
+    load(fp, t)
+    assert L.gh_graph_create(1, 0) == 1
+    fr, me = S.stream(3 * BATCH + 777, 0xB1F, routes=t.route_array())
+    fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
+    names = [rec_name(e) for e in range(abi.E_COUNT)]
+
+    def edge_counts():
+        c = np.zeros(abi.E_COUNT, dtype=np.int64)
+        for g in (0, 1):
+            assert L.gh_graph_use(g) == 0
+            c += [int(node_counters(x)[0]) for x in names]
+        return c
+
+    def run(pool, passes=1):
+        L.gh_set_recycle(pool, passes)
+        try:
+            assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, len(me)) == 0
+            c0 = edge_counts()
+            s, w = ctypes.c_double(), ctypes.c_uint64()
+            assert L.gh_workers_run(2, ctypes.byref(s), ctypes.byref(w)) == 0
+            assert s.value > 0 and w.value > 0
+            return edge_counts() - c0
+        finally:
+            L.gh_set_recycle(0, 1)
+
+    try:
+        want = run(0)
+        assert want.sum() == len(me) and want[abi.EDGE["port_output"]] > 0.9 * len(me)
+        for pool in (len(me) // 2, 1000):  # a batch and a half, a quarter batch
+            got = run(pool)
+            assert (got == want).all(), (pool, got, want)
+        assert (run(1000, passes=3) == 3 * want).all()  # each share three times over
+        L.gh_set_recycle(len(me), 1)  # two pools of the whole stream: more mbufs than loaded
+        try:
+            assert L.gh_workers_run(2, None, None) == -errno.EINVAL
+        finally:
+            L.gh_set_recycle(0, 1)
     finally:
         assert L.gh_graph_use(1) == 0
         assert L.gh_graph_destroy() == 0

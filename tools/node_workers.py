@@ -31,6 +31,11 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--rx-touch", type=int, default=1, help="port_rx writes the mbuf and touches the frame (PMD + DDIO)")
     ap.add_argument("--pin", type=int, default=0, help="1: frames by address (node_ptrs, mbuf memory registered)")
+    ap.add_argument("--recycle", type=int, default=0,
+                    help="mbufs per worker's pool (a mempool: port_rx refills them from the stream); 0: one per packet")
+    ap.add_argument("--passes", type=int, default=1, help="with --recycle: times each worker goes over its share")
+    ap.add_argument("--lcores", default="none", choices=["none", "allowed", "spread"],
+                    help="worker placement: the scheduler's, the k-th allowed CPU, or bench.cpu_placement's spread")
     args = ap.parse_args()
     threads = [int(x) for x in args.threads.split(",")]
 
@@ -58,12 +63,28 @@ def main():
     L.gh_set_pin(args.pin)  # 0: staged header lines, the node's default
     L.gh_set_rx_touch(args.rx_touch)
     L.gh_set_null_node.argtypes = [ctypes.c_int]
+    L.gh_set_recycle.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+    L.gh_set_recycle.restype = None
+    L.gh_set_recycle(args.recycle, args.passes)
+    from bench import cpu_placement
+
+    def place(k):
+        cpus = []
+        if args.lcores == "allowed":
+            cpus = sorted(os.sched_getaffinity(0))[:k]
+        elif args.lcores == "spread":
+            cpus = cpu_placement(k) or []
+        arr = (ctypes.c_int * max(1, len(cpus)))(*cpus)
+        assert L.gh_set_lcores(arr, len(cpus)) == 0
+        return cpus
+    per = args.passes if args.recycle else 1  # packets through each worker: its share, `passes` times
 
     def run(k, m, null):
         L.gh_set_null_node(null)
         try:
             assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, m) == 0
-            L.gh_workers_run(k, ctypes.byref(ctypes.c_double()), None)  # warm-up: pages, queues, pinned slots
+            rr = L.gh_workers_run(k, ctypes.byref(ctypes.c_double()), None)  # warm-up: pages, queues, pinned slots
+            assert rr == 0, rr
             best = []
             for _ in range(args.reps):
                 assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, m) == 0  # the frames as they came
@@ -76,14 +97,17 @@ def main():
             L.gh_set_null_node(0)
 
     for k in threads:
+        cpus = place(k)
         m = k * args.per_thread
         t = run(k, m, 0)
         # the same walks with port_rx handing its bursts straight to port_output:
         # the harness's own cost, which the node's walk pays too
         t0 = run(k, m, 1)
-        print(json.dumps({"threads": k, "gpus": 1, "mbufs": m, "batch": args.batch, "rx_touch": args.rx_touch,
+        m_loaded, m = m, m * per
+        print(json.dumps({"threads": k, "gpus": 1, "packets": m, "batch": args.batch, "rx_touch": args.rx_touch,
                           "harness_alone_mpps": round(m / t0 / 1e6, 1),
                           "node_ns_per_pkt_per_worker": round((t - t0) * 1e9 * k / m, 1), "mode": "frames by address" if args.pin else "staged lines",
+                          "recycle": args.recycle, "passes": per, "lcores": args.lcores, "cpus": cpus, "mbufs_loaded": m_loaded,
                           "ms": round(t * 1e3, 2), "mpps_aggregate": round(m / t / 1e6, 1),
                           "mpps_per_worker": round(m / t / 1e6 / k, 1),
                           "cpu_ns_per_pkt_per_worker": round(t * 1e9 * k / m, 1)}), flush=True)
