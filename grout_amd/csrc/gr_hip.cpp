@@ -189,7 +189,9 @@ struct node_slot {
 // read costs tens of nanoseconds per append
 static std::atomic<bool> node_prof_on{false};
 
-struct gr_hip_queue {
+// a worker's own: on whole 128-byte line pairs, none shared with another
+// worker's queue (the node writes its slots at every append)
+struct alignas(128) gr_hip_queue {
 	gr_hip_ctx *ctx;
 	hipStream_t s;
 	bool own_stream;

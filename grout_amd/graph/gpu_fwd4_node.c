@@ -641,9 +641,13 @@ static int gpu_fwd4_init(const struct rte_graph *graph, struct rte_node *node) {
 		slot++;
 	if (slot == GPU_FWD4_MAX_GRAPHS)
 		return -ENOSPC;
-	struct gpu_walk *w = calloc(1, sizeof(*w));
+	// the worker's own lines (grout: rte_zmalloc, cache-aligned): no line the
+	// walk writes shared with another worker's
+	const size_t wsz = (sizeof(struct gpu_walk) + 127) / 128 * 128;
+	struct gpu_walk *w = aligned_alloc(128, wsz);
 	if (w == NULL)
 		return -ENOMEM;
+	memset(w, 0, wsz);
 	w->graph = graph;
 	w->slot = slot;
 	w->gpu = pick_gpu(graph);

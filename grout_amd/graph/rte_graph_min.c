@@ -23,6 +23,20 @@ struct node_def {
 	rte_edge_t nb_edges;
 };
 
+// A graph's memory is its worker's alone (DPDK allocates each graph in one
+// cache-aligned memzone, graph_populate.c): every allocation of a graph on
+// whole 128-byte line pairs, so that no line a walk writes (node counters,
+// object arrays, the pending list) is shared with another worker's graph.
+#define GRAPH_LINE 128
+
+static void *graph_zalloc(size_t n) {
+	const size_t sz = (n + GRAPH_LINE - 1) / GRAPH_LINE * GRAPH_LINE;
+	void *p = aligned_alloc(GRAPH_LINE, sz ? sz : GRAPH_LINE);
+	if (p != NULL)
+		memset(p, 0, sz ? sz : GRAPH_LINE);
+	return p;
+}
+
 static struct node_def defs[MAX_NODES];
 static rte_node_t n_defs;
 
@@ -134,7 +148,7 @@ static void graph_free(struct rte_graph *g) {
 static int add_node(struct rte_graph *g, rte_node_t id) {
 	if (g->priv->inst_of[id] >= 0)
 		return 0;
-	struct rte_node *n = calloc(1, sizeof(*n));
+	struct rte_node *n = graph_zalloc(sizeof(*n));
 	if (n == NULL)
 		return -ENOMEM;
 	g->priv->inst_of[id] = (int32_t)g->priv->n_nodes;
@@ -144,7 +158,7 @@ static int add_node(struct rte_graph *g, rte_node_t id) {
 	n->id = id;
 	n->process = d->process;
 	n->size = RTE_GRAPH_BURST_SIZE;
-	n->objs = calloc(n->size, sizeof(void *));
+	n->objs = graph_zalloc(n->size * sizeof(void *));
 	if (n->objs == NULL)
 		return -ENOMEM;
 	for (rte_edge_t e = 0; e < d->nb_edges; e++) { // every reachable node joins
@@ -166,20 +180,20 @@ rte_graph_t rte_graph_create(const char *name, struct rte_graph_param *prm) {
 		id++;
 	if (id == MAX_GRAPHS)
 		return RTE_GRAPH_ID_INVALID;
-	struct rte_graph *g = calloc(1, sizeof(*g));
+	struct rte_graph *g = graph_zalloc(sizeof(*g));
 	if (g == NULL)
 		return RTE_GRAPH_ID_INVALID;
-	if ((g->priv = calloc(1, sizeof(*g->priv))) == NULL) {
+	if ((g->priv = graph_zalloc(sizeof(*g->priv))) == NULL) {
 		free(g);
 		return RTE_GRAPH_ID_INVALID;
 	}
 	snprintf(g->name, sizeof(g->name), "%s", name);
 	g->id = id;
 	g->socket = prm->socket_id;
-	g->priv->nodes = calloc(MAX_NODES, sizeof(*g->priv->nodes));
-	g->priv->inst_of = malloc(MAX_NODES * sizeof(*g->priv->inst_of));
+	g->priv->nodes = graph_zalloc(MAX_NODES * sizeof(*g->priv->nodes));
+	g->priv->inst_of = graph_zalloc(MAX_NODES * sizeof(*g->priv->inst_of));
 	g->priv->pend_cap = MAX_NODES + 1;
-	g->priv->pending = calloc(g->priv->pend_cap, sizeof(*g->priv->pending));
+	g->priv->pending = graph_zalloc(g->priv->pend_cap * sizeof(*g->priv->pending));
 	if (g->priv->nodes == NULL || g->priv->inst_of == NULL || g->priv->pending == NULL)
 		goto fail;
 	for (uint32_t i = 0; i < MAX_NODES; i++)
@@ -201,7 +215,7 @@ rte_graph_t rte_graph_create(const char *name, struct rte_graph_param *prm) {
 		struct rte_node *n = g->priv->nodes[i];
 		const struct node_def *d = &defs[n->id];
 		n->nb_edges = d->nb_edges;
-		n->nodes = calloc(d->nb_edges ? d->nb_edges : 1, sizeof(*n->nodes));
+		n->nodes = graph_zalloc((d->nb_edges ? d->nb_edges : 1) * sizeof(*n->nodes));
 		if (n->nodes == NULL)
 			goto fail;
 		for (rte_edge_t e = 0; e < d->nb_edges; e++)
@@ -267,9 +281,11 @@ static int grow(struct rte_node *n, uint32_t need) {
 		sz *= 2;
 	if (sz > UINT16_MAX)
 		sz = UINT16_MAX;
-	void **o = realloc(n->objs, sz * sizeof(void *));
+	void **o = graph_zalloc(sz * sizeof(void *));
 	if (o == NULL)
 		return -ENOMEM;
+	memcpy(o, n->objs, n->idx * sizeof(void *));
+	free(n->objs);
 	n->objs = o;
 	n->size = (uint16_t)sz;
 	return 0;

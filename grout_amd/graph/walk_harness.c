@@ -37,7 +37,7 @@
 #define GH_PRIV 64
 #define GH_ROOM 2048
 #define GH_MBUF_SZ (sizeof(struct rte_mbuf) + GH_PRIV + GH_ROOM)
-#define GH_MAX_GRAPHS 8
+#define GH_MAX_GRAPHS 16
 #define GH_MAX_RECORDERS 128
 
 struct gh_mbuf_out { // per injected mbuf, in injection order
@@ -73,7 +73,7 @@ static struct {
 	struct nexthop *nhs;
 	uint32_t max_ifaces, max_nh;
 	struct {
-		rte_graph_t gid;
+		_Alignas(128) rte_graph_t gid; // each worker's on lines of its own
 		struct rte_graph *graph;
 		char name[RTE_GRAPH_NAMESIZE];
 		// the worker's node statistics as grout's housekeeping keeps them

@@ -5,10 +5,18 @@ in K worker graphs at once, each walked from its own pthread (the walk
 harness's gh_workers_run: one graph per worker as grout's worker.c, each
 polling its own share of the full-view stream like an RX queue, the
 recorders behind the edges only counting). One GPU context, one queue per
-graph. Aggregate Mpps = all mbufs / the wall time of the slowest worker;
+graph. Aggregate Mpps = all packets / the wall time of the slowest worker;
 compare with bench.py's cpu_baseline on the same box (16 cores).
 
-    python tools/node_workers.py --threads 1,2,4,8 > out.jsonl
+--recycle P: each worker's packets go through a pool of P mbufs of its own
+(a mempool: port_rx refills an mbuf from the stream when the recorder gives
+it back), --passes times over its share, instead of one mbuf per packet.
+--lcores spread: worker k pinned to bench.cpu_placement's k-th core (one
+core per L3 domain in turn), as a deployment places its lcores. The node's
+cost is the median over --reps back-to-back pairs of (node run - harness-
+alone run): the host's other tenants move both alike.
+
+    python tools/node_workers.py --threads 1,4,8,16 --recycle 65536 --passes 8 --lcores spread
 """
 import argparse
 import ctypes
@@ -28,7 +36,7 @@ def main():
     ap.add_argument("--threads", default="1,2,4,8")
     ap.add_argument("--per-thread", type=int, default=1 << 18, help="mbufs per worker")
     ap.add_argument("--batch", type=int, default=15360)
-    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rx-touch", type=int, default=1, help="port_rx writes the mbuf and touches the frame (PMD + DDIO)")
     ap.add_argument("--pin", type=int, default=0, help="1: frames by address (node_ptrs, mbuf memory registered)")
     ap.add_argument("--recycle", type=int, default=0,
@@ -79,34 +87,36 @@ def main():
         return cpus
     per = args.passes if args.recycle else 1  # packets through each worker: its share, `passes` times
 
-    def run(k, m, null):
+    def once(k, m, null):
         L.gh_set_null_node(null)
         try:
-            assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, m) == 0
-            rr = L.gh_workers_run(k, ctypes.byref(ctypes.c_double()), None)  # warm-up: pages, queues, pinned slots
+            assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, m) == 0  # the frames as they came
+            s, w = ctypes.c_double(), ctypes.c_uint64()
+            rr = L.gh_workers_run(k, ctypes.byref(s), ctypes.byref(w))
             assert rr == 0, rr
-            best = []
-            for _ in range(args.reps):
-                assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, m) == 0  # the frames as they came
-                s, w = ctypes.c_double(), ctypes.c_uint64()
-                rr = L.gh_workers_run(k, ctypes.byref(s), ctypes.byref(w))
-                assert rr == 0, rr
-                best.append(s.value)
-            return float(np.median(best))
+            return s.value
         finally:
             L.gh_set_null_node(0)
+
+    def run(k, m):
+        """(node, harness alone) wall times, medians over --reps pairs run
+        back to back: the host's other tenants move both alike."""
+        once(k, m, 0)  # warm-up: pages, queues, pinned slots
+        once(k, m, 1)
+        pairs = [(once(k, m, 0), once(k, m, 1)) for _ in range(args.reps)]
+        return float(np.median([p[0] for p in pairs])), float(np.median([p[1] for p in pairs])), \
+            float(np.median([p[0] - p[1] for p in pairs]))
 
     for k in threads:
         cpus = place(k)
         m = k * args.per_thread
-        t = run(k, m, 0)
-        # the same walks with port_rx handing its bursts straight to port_output:
-        # the harness's own cost, which the node's walk pays too
-        t0 = run(k, m, 1)
+        # t0: the same walks with port_rx handing its bursts straight to
+        # port_output: the harness's own cost, which the node's walk pays too
+        t, t0, dt = run(k, m)
         m_loaded, m = m, m * per
         print(json.dumps({"threads": k, "gpus": 1, "packets": m, "batch": args.batch, "rx_touch": args.rx_touch,
                           "harness_alone_mpps": round(m / t0 / 1e6, 1),
-                          "node_ns_per_pkt_per_worker": round((t - t0) * 1e9 * k / m, 1), "mode": "frames by address" if args.pin else "staged lines",
+                          "node_ns_per_pkt_per_worker": round(dt * 1e9 * k / m, 1), "mode": "frames by address" if args.pin else "staged lines",
                           "recycle": args.recycle, "passes": per, "lcores": args.lcores, "cpus": cpus, "mbufs_loaded": m_loaded,
                           "ms": round(t * 1e3, 2), "mpps_aggregate": round(m / t / 1e6, 1),
                           "mpps_per_worker": round(m / t / 1e6 / k, 1),
