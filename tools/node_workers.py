@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--recycle", type=int, default=0,
                     help="mbufs per worker's pool (a mempool: port_rx refills them from the stream); 0: one per packet")
     ap.add_argument("--passes", type=int, default=1, help="with --recycle: times each worker goes over its share")
+    ap.add_argument("--prof", type=int, default=0,
+                    help="1: one more node run per line with the node's and the library's phase clocks (1 worker only)")
     ap.add_argument("--lcores", default="none", choices=["none", "allowed", "spread"],
                     help="worker placement: the scheduler's, the k-th allowed CPU, or bench.cpu_placement's spread")
     args = ap.parse_args()
@@ -55,6 +57,8 @@ def main():
     L = G.lib()
     L.gh_workers_run.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
     L.gh_set_rx_touch.argtypes = [ctypes.c_int]
+    L.gpu_fwd4_prof.argtypes = [ctypes.c_int, ctypes.c_void_p]
+    L.gpu_fwd4_prof.restype = None
     devs = (ctypes.c_int * 1)(0)
     kmax = max(threads)
     r = L.gh_init(ctypes.cast(devs, ctypes.c_void_p), 1, 1024, 1 << 17, args.batch, 64, 20_000_000)
@@ -113,6 +117,22 @@ def main():
         # t0: the same walks with port_rx handing its bursts straight to
         # port_output: the harness's own cost, which the node's walk pays too
         t, t0, dt = run(k, m)
+        prof = None
+        if args.prof and k == 1:  # the clocks are process-wide: one worker
+            fp.tune("node_prof", 1)
+            L.gpu_fwd4_prof(1, None)
+            H = abi.hip()
+            H.gr_hip_node_prof(None, 0, 1)
+            once(k, m, 0)
+            ph = np.zeros(4, dtype=np.uint64)
+            L.gpu_fwd4_prof(0, ph.ctypes.data)
+            lp = np.zeros(9, dtype=np.uint64)
+            H.gr_hip_node_prof(lp.ctypes.data, 9, 1)
+            fp.tune("node_prof", 0)
+            pk = m * per
+            prof = {"node": {a: round(float(v) / pk, 2) for a, v in zip(["accumulate", "start", "finish", "deliver"], ph)},
+                    "library": {a: round(float(v) / pk, 2) for a, v in zip(
+                        ["layout", "prep", "lock", "stage", "launch", "record", "fin_wait", "fin_scan", "fin_apply"], lp)}}
         m_loaded, m = m, m * per
         print(json.dumps({"threads": k, "gpus": 1, "packets": m, "batch": args.batch, "rx_touch": args.rx_touch,
                           "harness_alone_mpps": round(m / t0 / 1e6, 1),
@@ -120,7 +140,8 @@ def main():
                           "recycle": args.recycle, "passes": per, "lcores": args.lcores, "cpus": cpus, "mbufs_loaded": m_loaded,
                           "ms": round(t * 1e3, 2), "mpps_aggregate": round(m / t / 1e6, 1),
                           "mpps_per_worker": round(m / t / 1e6 / k, 1),
-                          "cpu_ns_per_pkt_per_worker": round(t * 1e9 * k / m, 1)}), flush=True)
+                          "cpu_ns_per_pkt_per_worker": round(t * 1e9 * k / m, 1),
+                          "prof_ns_per_pkt": prof}), flush=True)
     L.gh_fini()
 
 
