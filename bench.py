@@ -50,8 +50,10 @@ def cpu_placement(n, policy="spread"):
     "spread": one hardware thread per physical core, the cores taken round
     robin over the L3 domains (a Zen CCD: 8 cores, one L3 and one link to
     memory), socket by socket; a grout deployment spreads its lcores the same
-    way. None when the topology is unreadable or has fewer cores than n."""
-    if policy != "spread" or not hasattr(os, "sched_getaffinity"):
+    way. "socket": the same over the L3 domains of one socket (the first
+    allowed CPU's: the workers' staging memory and the GPU's link stay on
+    it). None when the topology is unreadable or has fewer cores than n."""
+    if policy not in ("spread", "socket") or not hasattr(os, "sched_getaffinity"):
         return None
     domains = {}
     for c in sorted(os.sched_getaffinity(0)):
@@ -64,6 +66,9 @@ def cpu_placement(n, policy="spread"):
         pkg = _cpu_sysfs(c, "topology/physical_package_id") or "0"
         l3 = _cpu_sysfs(c, "cache/index3/id") or pkg
         domains.setdefault((int(pkg), int(l3)), []).append(c)
+    if policy == "socket" and domains:
+        first = min(domains)[0]
+        domains = {k: v for k, v in domains.items() if k[0] == first}
     order, lists = [], [domains[k] for k in sorted(domains)]
     for i in range(max((len(x) for x in lists), default=0)):
         order += [x[i] for x in lists if i < len(x)]

@@ -44,7 +44,7 @@ def main():
     ap.add_argument("--passes", type=int, default=1, help="with --recycle: times each worker goes over its share")
     ap.add_argument("--prof", type=int, default=0,
                     help="1: one more node run per line with the node's and the library's phase clocks (1 worker only)")
-    ap.add_argument("--lcores", default="none", choices=["none", "allowed", "spread"],
+    ap.add_argument("--lcores", default="none", choices=["none", "allowed", "spread", "socket"],
                     help="worker placement: the scheduler's, the k-th allowed CPU, or bench.cpu_placement's spread")
     args = ap.parse_args()
     threads = [int(x) for x in args.threads.split(",")]
@@ -84,8 +84,8 @@ def main():
         cpus = []
         if args.lcores == "allowed":
             cpus = sorted(os.sched_getaffinity(0))[:k]
-        elif args.lcores == "spread":
-            cpus = cpu_placement(k) or []
+        elif args.lcores in ("spread", "socket"):
+            cpus = cpu_placement(k, args.lcores) or []
         arr = (ctypes.c_int * max(1, len(cpus)))(*cpus)
         assert L.gh_set_lcores(arr, len(cpus)) == 0
         return cpus
