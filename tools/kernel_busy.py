@@ -1,17 +1,19 @@
 #!/usr/bin/env python3
 # SPDX-License-Identifier: BSD-3-Clause
 """How busy the GPU was during each burst of kernels in a rocprofv3 kernel
-trace (`--kernel-trace`, the *_kernel_trace.csv): kernels are grouped into
+trace (`--kernel-trace`: the *_kernel_trace.csv, or the *_results.db that
+ROCm 7's rocprofv3 writes by default): kernels are grouped into
 runs separated by more than --gap-ms of idle GPU, and each run reports its
 span, the time at least one kernel was running (the union of the kernels'
 intervals), that as a fraction of the span, the summed kernel time (above
 the union when kernels of several queues overlap) and the mean kernel.
 
-    python tools/kernel_busy.py gpurun_out/prof_w16/.../w16_kernel_trace.csv
+    python tools/kernel_busy.py gpurun_out/prof_w16/w16_results.db --kernel gr_fwd4_ring
 """
 import argparse
 import csv
 import json
+import sqlite3
 
 
 def runs(intervals, gap_ns):
@@ -45,10 +47,16 @@ def main():
     ap.add_argument("--kernel", default="", help="only kernels whose name contains this")
     a = ap.parse_args()
     iv = []
-    with open(a.trace, newline="") as f:
-        for row in csv.DictReader(f):
-            if a.kernel in row["Kernel_Name"]:
-                iv.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
+    if a.trace.endswith(".db"):
+        db = sqlite3.connect(a.trace)
+        for name, s, e in db.execute("select name, start, end from kernels"):
+            if a.kernel in name:
+                iv.append((int(s), int(e)))
+    else:
+        with open(a.trace, newline="") as f:
+            for row in csv.DictReader(f):
+                if a.kernel in row["Kernel_Name"]:
+                    iv.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
     for k, r in enumerate(runs(iv, a.gap_ms * 1e6)):
         span = max(e for _, e in r) - min(s for s, _ in r)
         busy = union(r)
