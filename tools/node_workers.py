@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--recycle", type=int, default=0,
                     help="mbufs per worker's pool (a mempool: port_rx refills them from the stream); 0: one per packet")
     ap.add_argument("--passes", type=int, default=1, help="with --recycle: times each worker goes over its share")
+    ap.add_argument("--ring-cfg", type=int, default=-1, help="the \"ring\" knob (kernel geometry, fwd4_ring.hip ring_cfgN); -1: the default")
+    ap.add_argument("--wg-per-cu", type=int, default=-1, help="the \"wg_per_cu\" knob; -1: the default")
     ap.add_argument("--prof", type=int, default=0,
                     help="1: one more node run per line with the node's and the library's phase clocks (1 worker only)")
     ap.add_argument("--lcores", default="none", choices=["none", "allowed", "spread", "socket"],
@@ -72,6 +74,10 @@ def main():
     fr, me = S.stream(n, 0x67720002, routes=topo.route_array())
     fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
     fp.tune("node_ptrs", args.pin)
+    if args.ring_cfg >= 0:
+        fp.tune("ring", args.ring_cfg)
+    if args.wg_per_cu >= 0:
+        fp.tune("wg_per_cu", args.wg_per_cu)
     L.gh_set_pin(args.pin)  # 0: staged header lines, the node's default
     L.gh_set_rx_touch(args.rx_touch)
     L.gh_set_null_node.argtypes = [ctypes.c_int]
@@ -137,7 +143,7 @@ def main():
         print(json.dumps({"threads": k, "gpus": 1, "packets": m, "batch": args.batch, "rx_touch": args.rx_touch,
                           "harness_alone_mpps": round(m / t0 / 1e6, 1),
                           "node_ns_per_pkt_per_worker": round(dt * 1e9 * k / m, 1), "mode": "frames by address" if args.pin else "staged lines",
-                          "recycle": args.recycle, "passes": per, "lcores": args.lcores, "cpus": cpus, "mbufs_loaded": m_loaded,
+                          "recycle": args.recycle, "passes": per, "lcores": args.lcores, "cpus": cpus, "ring_cfg": args.ring_cfg, "wg_per_cu": args.wg_per_cu, "mbufs_loaded": m_loaded,
                           "ms": round(t * 1e3, 2), "mpps_aggregate": round(m / t / 1e6, 1),
                           "mpps_per_worker": round(m / t / 1e6 / k, 1),
                           "cpu_ns_per_pkt_per_worker": round(t * 1e9 * k / m, 1),
