@@ -2402,7 +2402,25 @@ static uint32_t node_unfinished(const gr_hip_pkt_meta *meta, uint32_t n, const u
 // GPU forwards one walk while the CPU stages the next.
 // Measurement: nanoseconds spent in the parts of gr_hip_node_start, summed
 // over every queue (gr_hip_node_prof).
-static std::atomic<uint64_t> node_prof_ns[GR_HIP_NODE_PROF_COUNT];
+// Each thread's own cell (no line shared between workers), summed when read.
+struct alignas(128) node_prof_cell {
+	std::atomic<uint64_t> ns[GR_HIP_NODE_PROF_COUNT]; // one writer: the cell's thread
+	void add(int k, uint64_t d) {
+		ns[k].store(ns[k].load(std::memory_order_relaxed) + d, std::memory_order_relaxed);
+	}
+};
+static std::mutex node_prof_mu;
+static std::vector<node_prof_cell *> node_prof_cells; // kept for the process's life (a few per worker thread)
+
+static node_prof_cell &node_prof_ns() {
+	thread_local node_prof_cell *cell = nullptr;
+	if (cell == nullptr) {
+		cell = new node_prof_cell();
+		std::lock_guard<std::mutex> l(node_prof_mu);
+		node_prof_cells.push_back(cell);
+	}
+	return *cell;
+}
 
 static inline uint64_t prof_now() {
 	struct timespec t;
@@ -2411,8 +2429,11 @@ static inline uint64_t prof_now() {
 }
 
 extern "C" int gr_hip_node_prof(uint64_t *out, uint32_t n, int reset) {
+	std::lock_guard<std::mutex> l(node_prof_mu);
 	for (uint32_t k = 0; k < GR_HIP_NODE_PROF_COUNT; k++) {
-		const uint64_t v = reset ? node_prof_ns[k].exchange(0) : node_prof_ns[k].load();
+		uint64_t v = 0;
+		for (node_prof_cell *c : node_prof_cells)
+			v += reset ? c->ns[k].exchange(0) : c->ns[k].load();
 		if (out != nullptr && k < n)
 			out[k] = v;
 	}
@@ -2504,7 +2525,7 @@ extern "C" int gr_hip_node_append(gr_hip_queue_t *q, const struct gr_hip_mbuf *m
 	w.na += n;
 	w.p = (uint32_t)p;
 	if (prof)
-		node_prof_ns[GR_HIP_NODE_PROF_STAGE] += prof_now() - t_prof;
+		node_prof_ns().add(GR_HIP_NODE_PROF_STAGE, prof_now() - t_prof);
 	return (int)p;
 }
 
@@ -2547,7 +2568,7 @@ extern "C" int gr_hip_node_append_mbufs(gr_hip_queue_t *q, void *const *mbufs, u
 	w.na += n;
 	w.p = (uint32_t)p;
 	if (prof)
-		node_prof_ns[GR_HIP_NODE_PROF_STAGE] += prof_now() - t_prof;
+		node_prof_ns().add(GR_HIP_NODE_PROF_STAGE, prof_now() - t_prof);
 	return (int)p;
 }
 
@@ -2576,7 +2597,7 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 	uint64_t t_prof = prof_now();
 	auto lap = [&](int k) {
 		const uint64_t t = prof_now();
-		node_prof_ns[k] += t - t_prof;
+		node_prof_ns().add(k, t - t_prof);
 		t_prof = t;
 	};
 	const uint32_t ns = was_open ? w.p : 0;
@@ -2717,12 +2738,12 @@ static int node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np,
 	if (r < 0 && r != -ETIMEDOUT)
 		return r;
 	uint64_t t = prof_now();
-	node_prof_ns[GR_HIP_NODE_PROF_FIN_WAIT] += t - t_prof;
+	node_prof_ns().add(GR_HIP_NODE_PROF_FIN_WAIT, t - t_prof);
 	// packets a kernel that gave up never reached go back to grout's CPU
 	// nodes, the others are handed back as usual
 	const uint32_t unfinished = r == 0 ? 0 : node_unfinished(w.meta, w.n, w.pos.data(), w.v); // 0: none gave up
 	t_prof = prof_now();
-	node_prof_ns[GR_HIP_NODE_PROF_FIN_SCAN] += t_prof - t;
+	node_prof_ns().add(GR_HIP_NODE_PROF_FIN_SCAN, t_prof - t);
 	{
 		std::shared_lock<std::shared_mutex> lk(c->mu); // the hand-back reads the iface and nexthop mirrors
 		const gr_node_vlans vl = {c->vlan_keys_h.data(), c->vlan_vals_h.data(), (uint32_t)c->vlan_keys_h.size()};
@@ -2732,7 +2753,7 @@ static int node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np,
 				     c->ifaces.data(), c->max_ifaces, c->nh.data(), (uint32_t)c->nh.size(), stats, &vl,
 				     w.kcount ? nullptr : q->node_if.data(), (uint32_t)q->node_if.size(), direct);
 	}
-	node_prof_ns[GR_HIP_NODE_PROF_FIN_APPLY] += prof_now() - t_prof;
+	node_prof_ns().add(GR_HIP_NODE_PROF_FIN_APPLY, prof_now() - t_prof);
 	return r < 0 ? r : (int)unfinished;
 }
 

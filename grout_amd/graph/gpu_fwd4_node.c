@@ -265,6 +265,7 @@ static int pick_gpu(const struct rte_graph *graph) {
 enum { RD_FREE = 0, RD_HELD, RD_RELEASE };
 
 struct gpu_walk {
+	uint64_t prof_ns[GPU_FWD4_PROF_COUNT]; // gpu_fwd4_prof's clocks, this worker's
 	const struct rte_graph *graph;
 	int slot; // index in walks[]: its QSBR reader ids
 	int gpu; // index in gpus[]
@@ -299,27 +300,32 @@ static uint64_t now_ns(void) {
 	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
 
-// Where a worker's time goes (gpu_fwd4_prof): accumulated only while on.
-static struct {
-	int on;
-	uint64_t ns[GPU_FWD4_PROF_COUNT];
-} prof;
+// Where the workers' time goes (gpu_fwd4_prof): accumulated only while on,
+// each worker's in its own gpu_walk (no line shared between workers),
+// summed over the graphs when read.
+static int prof_on;
 
-void gpu_fwd4_prof(int on, uint64_t *out) {
-	if (out != NULL)
-		memcpy(out, prof.ns, sizeof(prof.ns));
-	memset(prof.ns, 0, sizeof(prof.ns));
-	prof.on = on;
-}
-
-#define PROF_T0() const uint64_t prof_t0__ = prof.on ? now_ns() : 0
+#define PROF_T0() const uint64_t prof_t0__ = prof_on ? now_ns() : 0
 #define PROF_ADD(k)                                                                                \
 	do {                                                                                       \
-		if (prof.on)                                                                       \
-			prof.ns[k] += now_ns() - prof_t0__;                                        \
+		if (prof_on)                                                                       \
+			w->prof_ns[k] += now_ns() - prof_t0__;                                     \
 	} while (0)
 
 static struct gpu_walk *walks[GPU_FWD4_MAX_GRAPHS];
+
+void gpu_fwd4_prof(int on, uint64_t *out) {
+	if (out != NULL)
+		memset(out, 0, GPU_FWD4_PROF_COUNT * sizeof(uint64_t));
+	for (int i = 0; i < GPU_FWD4_MAX_GRAPHS; i++) {
+		if (walks[i] == NULL)
+			continue;
+		for (int k = 0; out != NULL && k < GPU_FWD4_PROF_COUNT; k++)
+			out[k] += walks[i]->prof_ns[k];
+		memset(walks[i]->prof_ns, 0, sizeof(walks[i]->prof_ns));
+	}
+	prof_on = on;
+}
 
 static struct gpu_walk *walk_of(const struct rte_graph *g) {
 	for (int i = 0; i < GPU_FWD4_MAX_GRAPHS; i++)
@@ -536,7 +542,12 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 // The batch on the GPU is done: hand it back now (a poll, no wait).
 static uint32_t reap(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
 	int ready = 0;
-	if (!w->pending || now_ns() - w->pend_ns < REAP_MIN_NS || gr_hip_node_pending(w->q, &ready) < 0 || !ready)
+	if (!w->pending || now_ns() - w->pend_ns < REAP_MIN_NS)
+		return 0;
+	PROF_T0();
+	const int r = gr_hip_node_pending(w->q, &ready);
+	PROF_ADD(GPU_FWD4_PROF_POLL);
+	if (r < 0 || !ready)
 		return 0;
 	return finish_pending(graph, node, w);
 }
@@ -760,6 +771,7 @@ static uint16_t gpu_flush_process(struct rte_graph *graph, struct rte_node *node
 	struct gpu_flush_ctx *c = gpu_flush_ctx(node);
 	if (c->w == NULL && (c->w = walk_of(graph)) == NULL)
 		return 0;
+	PROF_T0();
 	struct gpu_walk *w = c->w;
 	// a new graph walk: what was handed back in the walks before has been
 	// through grout's nodes, those batches' QSBR readers go offline
@@ -778,6 +790,7 @@ static uint16_t gpu_flush_process(struct rte_graph *graph, struct rte_node *node
 	w->rx_seen = 0;
 	if (w->n != 0 && (w->draining || idle || t - w->first_ns >= conf.max_delay_ns))
 		n += flush(graph, node, w); // pipelined: a later walk of the graph hands it back
+	PROF_ADD(GPU_FWD4_PROF_FLUSH_NODE);
 	return (uint16_t)(n > UINT16_MAX ? UINT16_MAX : n);
 }
 

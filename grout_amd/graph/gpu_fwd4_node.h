@@ -123,6 +123,8 @@ enum {
 	GPU_FWD4_PROF_START, // gr_hip_node_send: launch
 	GPU_FWD4_PROF_FINISH, // gr_hip_node_finish: wait for the GPU, hand-back onto the views
 	GPU_FWD4_PROF_DELIVER, // the views onto the rte_mbufs + private data, enqueues
+	GPU_FWD4_PROF_POLL, // the completion poll of the batch on the GPU (gr_hip_node_pending)
+	GPU_FWD4_PROF_FLUSH_NODE, // the flush source node's whole call (its hand-backs and flushes included)
 	GPU_FWD4_PROF_COUNT,
 };
 void gpu_fwd4_prof(int on, uint64_t *out);

@@ -81,7 +81,7 @@ def main():
             walks = L.gh_run(1 << 24)
             dt = time.perf_counter() - t0
             wi = G.walk_info()
-            ph = np.zeros(4, dtype=np.uint64)
+            ph = np.zeros(6, dtype=np.uint64)  # GPU_FWD4_PROF_COUNT
             L.gpu_fwd4_prof(0, ph.ctypes.data)
             lp = np.zeros(9, dtype=np.uint64)
             H.gr_hip_node_prof(lp.ctypes.data, 9, 1)
@@ -91,9 +91,10 @@ def main():
                 continue  # warm-up: staging buffers grown, pages touched
             # ns per packet in each phase of the node, clocks on (depth 2: start and finish
             # are the library's halves; depth 1 runs gr_hip_node_process, not split)
-            names = ["accumulate", "start", "finish", "deliver"]
+            names = ["accumulate", "start", "finish", "deliver", "poll", "flush_node"]
             per = {k: round(float(v) / len(me), 2) for k, v in zip(names, ph)}
-            per["rest_of_walk"] = round(dt * 1e9 / len(me) - sum(per.values()), 2)
+            # poll and flush_node overlap the four phases (the flush node's hand-backs and flushes)
+            per["rest_of_walk"] = round(dt * 1e9 / len(me) - sum(per[k] for k in names[:4]), 2)
             print(json.dumps({"batch": args.batch, "max_delay_us": args.max_delay_us, "depth": depth, "rx_touch": touch,
                               "mbufs": len(me), "graph_walks": walks,
                               "node_batches": int(wi["batches"] - wi0["batches"]), "max_batch": int(wi["max_batch"]),

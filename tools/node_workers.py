@@ -45,7 +45,7 @@ def main():
     ap.add_argument("--ring-cfg", type=int, default=-1, help="the \"ring\" knob (kernel geometry, fwd4_ring.hip ring_cfgN); -1: the default")
     ap.add_argument("--wg-per-cu", type=int, default=-1, help="the \"wg_per_cu\" knob; -1: the default")
     ap.add_argument("--prof", type=int, default=0,
-                    help="1: one more node run per line with the node's and the library's phase clocks (1 worker only)")
+                    help="1: one more node run per line with the node's and the library's phase clocks")
     ap.add_argument("--lcores", default="none", choices=["none", "allowed", "spread", "socket"],
                     help="worker placement: the scheduler's, the k-th allowed CPU, or bench.cpu_placement's spread")
     args = ap.parse_args()
@@ -124,19 +124,19 @@ def main():
         # port_output: the harness's own cost, which the node's walk pays too
         t, t0, dt = run(k, m)
         prof = None
-        if args.prof and k == 1:  # the clocks are process-wide: one worker
+        if args.prof:  # every worker's clocks add into the same counters
             fp.tune("node_prof", 1)
             L.gpu_fwd4_prof(1, None)
             H = abi.hip()
             H.gr_hip_node_prof(None, 0, 1)
             once(k, m, 0)
-            ph = np.zeros(4, dtype=np.uint64)
+            ph = np.zeros(6, dtype=np.uint64)  # GPU_FWD4_PROF_COUNT
             L.gpu_fwd4_prof(0, ph.ctypes.data)
             lp = np.zeros(9, dtype=np.uint64)
             H.gr_hip_node_prof(lp.ctypes.data, 9, 1)
             fp.tune("node_prof", 0)
-            pk = m * per
-            prof = {"node": {a: round(float(v) / pk, 2) for a, v in zip(["accumulate", "start", "finish", "deliver"], ph)},
+            pk = m * per  # the clocks add up every worker's time: ns of a worker per packet it takes
+            prof = {"node": {a: round(float(v) / pk, 2) for a, v in zip(["accumulate", "start", "finish", "deliver", "poll", "flush_node"], ph)},
                     "library": {a: round(float(v) / pk, 2) for a, v in zip(
                         ["layout", "prep", "lock", "stage", "launch", "record", "fin_wait", "fin_scan", "fin_apply"], lp)}}
         m_loaded, m = m, m * per
