@@ -278,6 +278,7 @@ struct gpu_walk {
 	int pending; // the other buffer's batch is on the GPU (gr_hip_node_start'ed)
 	uint32_t pend_n; // its size
 	uint64_t pend_ns; // when it was sent
+	uint64_t gpu_ns; // how long the last batches took to come back (a moving average), 0: none yet
 	// QSBR readers (see "RCU" above): rd[k] is the reader buffer k's batch
 	// holds (-1: none), rstate the state of each of the graph's readers
 	int8_t rd[2];
@@ -472,6 +473,21 @@ static void deliver(struct rte_graph *graph, struct rte_node *node, struct gpu_w
 	PROF_ADD(GPU_FWD4_PROF_DELIVER);
 }
 
+// The batch on the GPU is done (or the poll failed: finish_pending reports
+// it): polled like a worker polls its RX queues, the time it took noted for
+// reap's first poll.
+static void poll_until_ready(struct gpu_walk *w) {
+	if (!w->pending)
+		return;
+	PROF_T0();
+	for (int ready = 0; !ready;)
+		if (gr_hip_node_pending(w->q, &ready) <= 0) // an error, or nothing in flight after all
+			break;
+	PROF_ADD(GPU_FWD4_PROF_POLL);
+	const uint64_t waited = now_ns() - w->pend_ns;
+	w->gpu_ns = w->gpu_ns ? (w->gpu_ns * 7 + waited) / 8 : waited;
+}
+
 // Wait for the batch on the GPU and hand it back. Returns its size.
 static uint32_t finish_pending(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
 	if (!w->pending)
@@ -522,6 +538,7 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 	PROF_T0();
 	const int r = gr_hip_node_send(w->q, NULL, n, WALK_SPLIT);
 	PROF_ADD(GPU_FWD4_PROF_START);
+	poll_until_ready(w); // a worker polls; a blocking wait would sleep on the GPU's interrupt
 	const uint32_t delivered = finish_pending(graph, node, w);
 	if (r < 0) { // the GPU did not take it: grout's CPU nodes do (after the one before, in order)
 		deliver(graph, node, w, k, n, r);
@@ -537,18 +554,24 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 
 // A batch spends at least this long on the GPU (launch, PCIe both ways, the
 // kernel's tile latency: ~30 us for 64 packets): no poll before.
+// Nor before 3/4 of what the last batches took: each poll is a runtime call
+// (hipEventQuery), whose locks every worker of the process shares.
 #define REAP_MIN_NS 10000
 
 // The batch on the GPU is done: hand it back now (a poll, no wait).
 static uint32_t reap(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
 	int ready = 0;
-	if (!w->pending || now_ns() - w->pend_ns < REAP_MIN_NS)
+	if (!w->pending)
+		return 0;
+	const uint64_t t = now_ns(), waited = t - w->pend_ns;
+	if (waited < REAP_MIN_NS || waited < w->gpu_ns / 4 * 3)
 		return 0;
 	PROF_T0();
 	const int r = gr_hip_node_pending(w->q, &ready);
 	PROF_ADD(GPU_FWD4_PROF_POLL);
 	if (r < 0 || !ready)
 		return 0;
+	w->gpu_ns = w->gpu_ns ? (w->gpu_ns * 7 + waited) / 8 : waited; // an upper bound: polled late
 	return finish_pending(graph, node, w);
 }
 
