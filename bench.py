@@ -7,10 +7,14 @@ synthetic packets already resident in HBM (default 2^24 packets, 64-byte
 slots): iface_input .. iface_output for every packet, header lines written
 out of place so every step sees the same input. Multi-GPU runs are replicas
 (one independent RX stream and FIB replica per GPU, no collective on the data
-path; torch.distributed is used only for the barrier and the max-over-ranks
-clock), so scaling is weak.
+path; torch.distributed over gloo is used only for the barrier, the
+max-over-ranks clock and the per-rank report), so scaling is weak.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
+
+--gpus N > 1 without a launcher: this process starts N fresh rank processes
+itself (grout_amd.replicas.spawn) before any GPU call and exits with their
+status. Under torch.distributed.run, WORLD_SIZE must equal --gpus.
 """
 import argparse
 import json
@@ -125,6 +129,18 @@ def log(*a):
 
 def main():
     args = parse()
+    from grout_amd import replicas
+
+    # N GPUs = N replicas, one process each. Without a launcher the parent
+    # starts them itself, before anything here touches a GPU, and exits with
+    # their status; under one (torch.distributed.run) the world must be --gpus
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(replicas.spawn(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        log(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}: one rank per GPU, the two must agree")
+        sys.exit(2)
+
     import torch
 
     from grout_amd import abi
@@ -132,17 +148,20 @@ def main():
     from grout_amd import topology as T
     from grout_amd.fwd import FastPath, shared_stream
 
-    from grout_amd.replicas import Replicas
-
     # GR_BENCH_SHARE_GPU=1: a rehearsal of the N>1 path on a one-GPU box,
-    # every rank on device 0 and gloo for the barrier and the clock (RCCL
-    # refuses two ranks on one GPU); the driver's runs never set it
+    # every rank on device 0; the driver's runs never set it. Barrier, clock
+    # and report go over gloo either way (no collective on the data path)
     share = os.environ.get("GR_BENCH_SHARE_GPU") == "1"
-    rep = Replicas("gloo" if share else "nccl")
+    rep = replicas.Replicas("gloo")
     world, rank = rep.world, rep.rank
     local = 0 if share else rep.local
+    if local >= torch.cuda.device_count():
+        log(f"bench.py: rank {rank} wants device {local}, {torch.cuda.device_count()} visible")
+        sys.exit(2)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    gpu_numa = abi.hip().gr_hip_device_numa_node(local)
+    bound = replicas.bind_to_numa(gpu_numa)  # this rank's host threads on its GPU's socket
 
     # ---- control plane: topology + FIB replica on this GPU
     t0 = time.time()
@@ -257,6 +276,7 @@ def main():
         for _ in range(steps):
             step()
         torch.cuda.synchronize()
+        own = time.perf_counter() - t0  # this replica's own clock
         rep.barrier()
         el = time.perf_counter() - t0
         q.sync()
@@ -265,9 +285,11 @@ def main():
         timed = sum(1 for i in range(warmup, warmup + steps) if i % every == 0)
         ms, cnt = q.kernel_ms(timed)
         fp.tune("time_every", 1)
+        measure.own = own
         return rep.max_over_ranks(el), ms, cnt
 
     tmax, kern_ms, kcount = measure((d_in, d_out, d_meta, d_v), args.steps, args.warmup)
+    own_s = measure.own
 
     if batch is not None:
         vh = np.empty(n, dtype=abi.VERDICT_DT)
@@ -338,6 +360,19 @@ def main():
                            "changed bytes as whole lines"}
         del x_in, x_meta, x_out, x_v
 
+    # every replica's own figures, next to the whole-job line: its GPU, the
+    # NUMA node of its GPU and of the CPU it ran on, its own clock and kernel
+    props = torch.cuda.get_device_properties(local)
+    pci = None
+    if hasattr(props, "pci_bus_id"):
+        pci = f"{getattr(props, 'pci_domain_id', 0):04x}:{props.pci_bus_id:02x}:{getattr(props, 'pci_device_id', 0):02x}"
+    mine = {"rank": rank, "device": local, "pci": pci, "gpu_numa": gpu_numa, "cpu_numa": replicas.cpu_numa_node(),
+            "bound_to_gpu_numa": bound is not None, "mpps": round(n * args.steps / own_s / 1e6, 1),
+            "ms_per_step": round(own_s / args.steps * 1e3, 4), "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "forwarded_frac": round(fwd_frac, 6),
+            **({"kernel_ms_avg_plain": plain["kernel_ms_avg"]} if plain is not None else {})}
+    ranks = rep.gather_objects(mine)
+
     result = {
         "metric": "Mpps IPv4 forward, 64B pkts, ~1M-route FIB (device-resident), 1/8 GPU",
         "value": round(value, 1),
@@ -394,6 +429,13 @@ def main():
     if plain is not None:
         result["value_plain_placement"] = plain["value"]
         result["plain_placement"] = plain
+        # the conservative figure: the same kernel on plain torch allocations
+        if plain["kernel_ms_avg"]:
+            result["roofline"]["frac_plain"] = round(n * B_PKT / (plain["kernel_ms_avg"] / 1e3) / 1e9 / HBM_PEAK_GBS,
+                                                     4)
+        result["roofline"]["kernel_ms_avg_plain"] = plain["kernel_ms_avg"]
+    if world > 1:
+        result["ranks"] = ranks
     if pfx_leg is not None:
         result["prefix32"] = pfx_leg
     if args.workload == "fullview6":
