@@ -12,17 +12,29 @@ BUILD = build
 LIB_HIP = grout_amd/libgrout_hip.so
 LIB_HOST = grout_amd/libgrout_host.so
 LIB_ORACLE = oracle/liboracle.so
-LIB_GRAPH = grout_amd/libgrout_graph.so
-GRAPH = grout_amd/graph
-GRAPH_SRC = $(GRAPH)/rte_graph_min.c $(GRAPH)/rte_rcu_min.c $(GRAPH)/gr_datapath_min.c $(GRAPH)/gpu_fwd4_node.c $(GRAPH)/gpu_fwd4_cpu_nodes.c \
-	$(GRAPH)/gr_control_min.c $(GRAPH)/gpu_fwd4_control.c \
-	$(GRAPH)/walk_harness.c $(GRAPH)/control_harness.c \
-	$(GRAPH)/graph_selftest.c
-GRAPH_HDRS = $(GRAPH)/rte_graph_min.h $(GRAPH)/rte_rcu_min.h $(GRAPH)/gr_datapath_min.h $(GRAPH)/gpu_fwd4_node.h include/grout_hip.h \
-	$(GRAPH)/gr_control_min.h $(GRAPH)/gpu_fwd4_control.h
+# The grout module (what grout builds in modules/gpu):
+# the node, the control-plane mirror, the CPU continuation nodes. It includes
+# grout's and DPDK's headers by name; here the include path leads those names
+# to the test stand-ins, and the library leaves grout's / DPDK's symbols
+# undefined (the stand-in library that loads it provides them).
+MOD = grout_amd/module
+LIB_MOD = grout_amd/libgrout_gpu_fwd4.so
+MOD_SRC = $(MOD)/gpu_fwd4_node.c $(MOD)/gpu_fwd4_control.c $(MOD)/gpu_fwd4_cpu_nodes.c
+MOD_HDRS = $(MOD)/gpu_fwd4_node.h $(MOD)/gpu_fwd4_control.h include/grout_hip.h
+# Test infrastructure: the rte_graph / grout stand-ins and the walk and
+# control harnesses, linked against the module library.
+STANDIN = tests/standin
+LIB_STANDIN = $(STANDIN)/libgrout_standin.so
+STANDIN_SRC = $(STANDIN)/rte_graph_min.c $(STANDIN)/rte_rcu_min.c $(STANDIN)/gr_datapath_min.c \
+	$(STANDIN)/gr_control_min.c $(STANDIN)/walk_harness.c $(STANDIN)/control_harness.c $(STANDIN)/graph_selftest.c
+STANDIN_HDRS = $(wildcard $(STANDIN)/include/*.h $(STANDIN)/include/event2/*.h)
+MOD_INC = -Iinclude -I$(MOD) -I$(STANDIN)/include
+# grout's C flags (its meson.build) for the module's sources
+MOD_CFLAGS = -std=gnu2x -D_GNU_SOURCE -DALLOW_EXPERIMENTAL_API -fms-extensions -Wmissing-prototypes -Wstrict-aliasing=2 \
+	-fstrict-aliasing
 HDRS = include/grout_hip.h $(CSRC)/fib6.h $(CSRC)/fwd4_kernel.h $(CSRC)/fwd4_dev.h $(CSRC)/fwd4_chain.h $(CSRC)/fib4.h
 
-all: $(LIB_HIP) $(LIB_HOST) $(LIB_ORACLE) $(LIB_GRAPH) tools/libnode_mt.so
+all: $(LIB_HIP) $(LIB_HOST) $(LIB_ORACLE) $(LIB_MOD) $(LIB_STANDIN) tools/libnode_mt.so
 
 $(BUILD)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(BUILD)
@@ -53,10 +65,13 @@ $(LIB_HOST): $(CSRC)/fib4.c $(CSRC)/fib6.c $(CSRC)/synth.c $(CSRC)/fib4.h $(CSRC
 $(LIB_ORACLE): oracle/oracle.c oracle/oracle.h include/grout_hip.h
 	$(CC) $(CFLAGS_HOST) -pthread -shared -o $@ oracle/oracle.c
 
-# The fast path's grout node (C) on the rte_graph / grout stand-ins, with the
-# test harness graph; links the HIP library (found next to it at run time).
-$(LIB_GRAPH): $(GRAPH_SRC) $(GRAPH_HDRS) $(LIB_HIP)
-	$(CC) -std=gnu11 $(CFLAGS_HOST) -pthread -Iinclude -shared -o $@ $(GRAPH_SRC) -Lgrout_amd -lgrout_hip '-Wl,-rpath,$$ORIGIN'
+# links the HIP library (found next to it at run time)
+$(LIB_MOD): $(MOD_SRC) $(MOD_HDRS) $(STANDIN_HDRS) $(LIB_HIP)
+	$(CC) $(MOD_CFLAGS) $(CFLAGS_HOST) -pthread $(MOD_INC) -shared -o $@ $(MOD_SRC) -Lgrout_amd -lgrout_hip '-Wl,-rpath,$$ORIGIN'
+
+$(LIB_STANDIN): $(STANDIN_SRC) $(STANDIN_HDRS) $(MOD_HDRS) $(LIB_MOD)
+	$(CC) -std=gnu11 $(CFLAGS_HOST) -pthread $(MOD_INC) -shared -o $@ $(STANDIN_SRC) -Lgrout_amd -lgrout_gpu_fwd4 -lgrout_hip \
+		'-Wl,-rpath,$$ORIGIN/../../grout_amd'
 
 # measurement tool: the node walk from C threads (tools/node_pipeline.py --driver c)
 tools/libnode_mt.so: tools/node_mt.c include/grout_hip.h $(LIB_HIP)
@@ -97,10 +112,14 @@ $(ASAN_DIR)/liboracle.so: oracle/oracle.c oracle/oracle.h include/grout_hip.h
 
 # globals not instrumented here: the identical edge-name literals of the node
 # sources end up registered twice at one merged address (a false ODR report)
-$(ASAN_DIR)/libgrout_graph.so: $(GRAPH_SRC) $(GRAPH_HDRS) $(ASAN_DIR)/libgrout_hip.so
-	$(SAN_C) -mllvm -asan-globals=0 -std=gnu11 -Iinclude -shared -o $@ $(GRAPH_SRC) -L$(ASAN_DIR) -lgrout_hip '-Wl,-rpath,$$ORIGIN'
+$(ASAN_DIR)/libgrout_gpu_fwd4.so: $(MOD_SRC) $(MOD_HDRS) $(STANDIN_HDRS) $(ASAN_DIR)/libgrout_hip.so
+	$(SAN_C) -mllvm -asan-globals=0 -std=gnu11 $(MOD_INC) -shared -o $@ $(MOD_SRC) -L$(ASAN_DIR) -lgrout_hip '-Wl,-rpath,$$ORIGIN'
 
-asan: $(ASAN_DIR)/libgrout_hip.so $(ASAN_DIR)/libgrout_host.so $(ASAN_DIR)/liboracle.so $(ASAN_DIR)/libgrout_graph.so
+$(ASAN_DIR)/libgrout_standin.so: $(STANDIN_SRC) $(STANDIN_HDRS) $(MOD_HDRS) $(ASAN_DIR)/libgrout_gpu_fwd4.so
+	$(SAN_C) -mllvm -asan-globals=0 -std=gnu11 $(MOD_INC) -shared -o $@ $(STANDIN_SRC) -L$(ASAN_DIR) -lgrout_gpu_fwd4 \
+		-lgrout_hip '-Wl,-rpath,$$ORIGIN'
+
+asan: $(ASAN_DIR)/libgrout_hip.so $(ASAN_DIR)/libgrout_host.so $(ASAN_DIR)/liboracle.so $(ASAN_DIR)/libgrout_standin.so
 
 # the CPU suite on the sanitized libraries (GR_LIBDIR: abi.py / oracle load from there)
 asan-test: asan
@@ -108,6 +127,6 @@ asan-test: asan
 		UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 python -m pytest tests -x -q -m "not gpu" -p no:cacheprovider
 
 clean:
-	rm -rf $(BUILD) $(LIB_HIP) $(LIB_HOST) $(LIB_ORACLE) $(LIB_GRAPH)
+	rm -rf $(BUILD) $(LIB_HIP) $(LIB_HOST) $(LIB_ORACLE) $(LIB_MOD) $(LIB_STANDIN) grout_amd/libgrout_graph.so
 
 .PHONY: all clean asan asan-test

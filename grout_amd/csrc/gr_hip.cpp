@@ -2725,8 +2725,6 @@ static int node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np,
 	int r = w.r;
 	if (direct != nullptr)
 		direct->meta = w.own ? w.meta : nullptr; // no views: the hand-back reads the mbufs
-	else if (w.own)
-		return -EINVAL; // appended from the mbufs: gr_hip_node_finish_mbufs hands it back
 	uint64_t t_prof = prof_now();
 	if (!w.sync) {
 		hipSetDevice(c->dev);
@@ -2735,6 +2733,12 @@ static int node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np,
 		// walk a give-up hit is read from the verdicts below
 		r = q_check(q);
 	}
+	// appended from the mbufs: gr_hip_node_finish_mbufs hands it back. Refused
+	// only once the GPU is done with it (above): a caller that drops the walk
+	// here (a graph destroyed with a batch in flight) frees its mbufs next,
+	// whose frames the kernel may be rewriting in place
+	if (direct == nullptr && w.own)
+		return -EINVAL;
 	if (r < 0 && r != -ETIMEDOUT)
 		return r;
 	uint64_t t = prof_now();

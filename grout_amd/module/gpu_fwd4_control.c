@@ -8,13 +8,25 @@
 // mirror also keeps what it pushed (a shadow), which serves the slot and
 // reta bookkeeping, the tests, and the replay into a context that diverged.
 //
-// Built here against the control-plane stand-in (gr_control_min.h); in grout
-// it includes <event.h>, "iface.h", "nexthop.h", "ip4.h", "ip6.h" and "vrf.h"
-// (with integration/grout-gpu_fwd4-control.patch applied) instead.
+// It includes grout's headers by their names (ip4.h / ip6.h / event.h / nexthop.h
+// with integration/grout-gpu_fwd4-control.patch applied); here the include path
+// leads them to the test stand-ins (tests/standin/include).
 #include "gpu_fwd4_control.h"
 
 #include "gpu_fwd4_node.h"
-#include "gr_control_min.h"
+
+#include "event.h"
+#include "iface.h"
+#include "ip4.h"
+#include "ip6.h"
+#include "nexthop.h"
+#include "port.h"
+#include "vlan.h"
+#include "vrf.h"
+
+#include <event2/event.h>
+#include <rte_common.h>
+#include <rte_ether.h>
 
 #include <errno.h>
 #include <stdlib.h>
@@ -177,6 +189,7 @@ static struct {
 } M;
 
 static struct event_base *ev_base; // the control thread's (gpu_fwd4_control_attach)
+static void publish_cb(int fd, short what, void *arg);
 
 static void note(int r) {
 	// no GPU context at all (CPU tests): the shadow alone is kept
@@ -239,8 +252,21 @@ void gpu_fwd4_control_reset(void) {
 	memset(&M, 0, sizeof(M));
 }
 
+// The publication timer lives on the control thread's event base: created
+// here when the module's init passes it (and on first use after a reset),
+// rebuilt when the base changes. With no base (events before the module's
+// init) every change is published at once, counted in no_timer.
 void gpu_fwd4_control_attach(struct event_base *ev) {
+	if (ev == ev_base && (M.flush_ev != NULL || ev == NULL))
+		return;
+	if (M.flush_ev != NULL) { // on the old loop: publish what it waited for, then move
+		gpu_fwd4_control_flush();
+		event_free(M.flush_ev);
+		M.flush_ev = NULL;
+	}
 	ev_base = ev;
+	if (ev != NULL)
+		M.flush_ev = evtimer_new(ev, publish_cb, NULL);
 }
 
 // ---- nexthop slots ---------------------------------------------------------
@@ -430,13 +456,23 @@ static uint32_t mask4(uint32_t ip_be, uint8_t plen) {
 	return __builtin_bswap32(plen ? h & (0xffffffffu << (32 - plen)) : 0);
 }
 
+// A publication while L3 nexthop changes still wait for theirs may put on the
+// GPUs a route naming a slot whose mirror is stale (slots are reused): every
+// caller flushes the nexthops first (nh_flush), counted here if one did not.
+static void commit_check(void) {
+	if (M.n_nh_dirty != 0)
+		M.st.unordered++;
+}
+
 static void commit4(uint16_t vrf_id) {
+	commit_check();
 	note(gpu_fwd4_fib4_commit(vrf_id));
 	M.st.commits++;
 	M.dirty4[vrf_id] = 0;
 }
 
 static void commit6(uint16_t vrf_id) {
+	commit_check();
 	note(gpu_fwd4_fib6_commit(vrf_id));
 	M.st.commits++;
 	M.dirty6[vrf_id] = 0;
@@ -511,10 +547,11 @@ static void publish_later(void) {
 	}
 	if (M.flush_armed)
 		return;
-	if (M.flush_ev == NULL)
+	if (M.flush_ev == NULL && ev_base != NULL)
 		M.flush_ev = evtimer_new(ev_base, publish_cb, NULL);
 	const struct timeval tv = {.tv_sec = 0, .tv_usec = PUBLISH_DELAY_US};
 	if (M.flush_ev == NULL || evtimer_add(M.flush_ev, &tv) < 0) {
+		M.st.no_timer++;
 		gpu_fwd4_control_flush(); // no timer: publish now
 		return;
 	}
@@ -713,8 +750,11 @@ static void fib_destroy(uint16_t vrf_id) {
 	memset(f, 0, sizeof(*f));
 }
 
-// Every route of a VRF again, into its (re-created) FIBs, and published.
+// Every route of a VRF again, into its (re-created) FIBs, and published:
+// the L3 nexthops waiting for the next publication first, as for any other
+// (the routes may name their slots).
 static void fib_refill(uint16_t vrf_id) {
+	nh_flush();
 	for (uint32_t i = 0; i < M.n_r4; i++)
 		if (M.r4[i].vrf_id == vrf_id)
 			note(gpu_fwd4_route4_add(&M.r4[i], 1, 1));

@@ -61,6 +61,8 @@ struct gpu_fwd4_control_stats {
 	uint32_t routes4, routes6;
 	uint32_t pending; // route changes in every context's RIB, not yet published
 	uint64_t presync; // publications grout's wait for the datapath forced (see "publication")
+	uint64_t unordered; // publications made while L3 nexthop changes were unpublished (0: never)
+	uint64_t no_timer; // changes published at once: no timer on an event base (before attach)
 };
 void gpu_fwd4_control_stats(struct gpu_fwd4_control_stats *);
 

@@ -17,11 +17,26 @@
 // Both receive mbufs in the state grout's chain leaves them there (the GPU
 // node's hand-back: data_off past the Ethernet header, the ingress iface or
 // the egress iface in mbuf_data, l3_mbuf_data.nh, TTL and checksum already
-// rewritten by ip_forward). Built here against the grout / DPDK stand-ins;
-// in grout they include ip4_datapath.h, conntrack.h and nat_datapath.h.
+// rewritten by ip_forward). grout's and DPDK's headers by their names (the
+// test stand-ins here, tests/standin/include).
 #include "gpu_fwd4_node.h"
 
-#include "gr_datapath_min.h"
+#include "conntrack.h"
+#include "eth.h"
+#include "graph.h"
+#include "iface.h"
+#include "l3.h"
+#include "mbuf.h"
+#include "nat_datapath.h"
+#include "nexthop.h"
+
+#include <rte_byteorder.h>
+#include <rte_ether.h>
+#include <rte_graph_worker.h>
+#include <rte_ip.h>
+#include <rte_mbuf.h>
+
+#include <string.h>
 
 // ---- ip_input_local_ct ------------------------------------------------------
 enum {

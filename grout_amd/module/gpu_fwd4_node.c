@@ -51,13 +51,28 @@
 // arrays; the node therefore hands at most one batch back per process() call
 // and batches are at most GPU_FWD4_BATCH_MAX packets.
 //
-// Built here against the rte_graph / grout stand-ins (rte_graph_min.h,
-// gr_datapath_min.h); in grout it includes <gr_graph.h>, <gr_mbuf.h>,
-// <gr_module.h> and the DPDK headers instead, with no other change.
+// It includes grout's and DPDK's headers by their names and builds unchanged
+// in grout (modules/gpu, integration/grout-gpu_module-build.patch) and here,
+// where the include path leads those names to the test stand-ins
+// (tests/standin/include).
 #include "gpu_fwd4_node.h"
 #include "gpu_fwd4_control.h"
 
-#include "gr_datapath_min.h"
+#include "datapath.h"
+#include "eth.h"
+#include "graph.h"
+#include "iface.h"
+#include "l3.h"
+#include "mbuf.h"
+#include "module.h"
+#include "rcu.h"
+#include "rxtx.h"
+
+#include <rte_common.h>
+#include <rte_graph.h>
+#include <rte_graph_worker.h>
+#include <rte_mbuf.h>
+#include <rte_rcu_qsbr.h>
 
 #include <errno.h>
 #include <stddef.h>
@@ -125,9 +140,10 @@ int gpu_fwd4_set_batch(uint32_t batch, uint64_t max_delay_ns) {
 }
 
 // ---- the grout objects verdicts name (see "RCU" above) ---------------------
-static const struct iface **if_obj;
+// (object pointers kept as const void *: the one table allocator serves both)
+static const void **if_obj;
 static uint32_t if_obj_n;
-static const struct nexthop **nh_obj;
+static const void **nh_obj;
 static uint32_t nh_obj_n;
 
 // Allocated at the first set, from the control thread; the size is published
@@ -142,7 +158,7 @@ static int obj_table(const void ***t, uint32_t *n, uint32_t want) {
 }
 
 int gpu_fwd4_iface_obj_set(uint16_t id, const struct iface *i) {
-	int r = obj_table((const void ***)&if_obj, &if_obj_n, conf.max_ifaces);
+	int r = obj_table(&if_obj, &if_obj_n, conf.max_ifaces);
 	if (r < 0)
 		return r;
 	if (id == 0 || id >= if_obj_n)
@@ -152,7 +168,7 @@ int gpu_fwd4_iface_obj_set(uint16_t id, const struct iface *i) {
 }
 
 int gpu_fwd4_nh_obj_set(uint32_t slot, const struct nexthop *nh) {
-	int r = obj_table((const void ***)&nh_obj, &nh_obj_n, conf.max_nexthops + 1);
+	int r = obj_table(&nh_obj, &nh_obj_n, conf.max_nexthops + 1);
 	if (r < 0)
 		return r;
 	if (slot == 0 || slot >= nh_obj_n)
@@ -162,12 +178,14 @@ int gpu_fwd4_nh_obj_set(uint32_t slot, const struct nexthop *nh) {
 }
 
 const struct iface *gpu_fwd4_iface_obj(uint16_t id) {
-	return id < __atomic_load_n(&if_obj_n, __ATOMIC_ACQUIRE) ? __atomic_load_n(&if_obj[id], __ATOMIC_ACQUIRE) : NULL;
+	return id < __atomic_load_n(&if_obj_n, __ATOMIC_ACQUIRE) ? (const struct iface *)__atomic_load_n(&if_obj[id], __ATOMIC_ACQUIRE)
+								  : NULL;
 }
 
 const struct nexthop *gpu_fwd4_nh_obj(uint32_t slot) {
-	return slot < __atomic_load_n(&nh_obj_n, __ATOMIC_ACQUIRE) ? __atomic_load_n(&nh_obj[slot], __ATOMIC_ACQUIRE)
-								  : NULL;
+	return slot < __atomic_load_n(&nh_obj_n, __ATOMIC_ACQUIRE)
+		? (const struct nexthop *)__atomic_load_n(&nh_obj[slot], __ATOMIC_ACQUIRE)
+		: NULL;
 }
 
 gr_hip_ctx_t *gpu_fwd4_hip_ctx(void) {
@@ -234,8 +252,21 @@ static struct module gpu_module = {
 	.fini = gpu_fini,
 };
 
+// grout's worker loop calls these (datapath.h's hooks, which
+// integration/grout-gpu_fwd4-datapath.patch adds to main_loop.c): the drain
+// before a worker leaves its graph, the statistics fold at each housekeeping
+// tick, and the QSBR reader ids of the node's batches (see "RCU" above),
+// which the rcu module's init sizes in.
+static struct gr_datapath_hooks gpu_hooks = {
+	.name = "gpu_fwd4",
+	.rcu_readers = GPU_FWD4_RCU_READERS,
+	.graph_leave = gpu_fwd4_drain,
+	.stats_flush = gpu_fwd4_stats_flush,
+};
+
 RTE_INIT(gpu_module_init) {
 	module_register(&gpu_module);
+	gr_datapath_hooks_register(&gpu_hooks); // before the rcu module's init reads the readers
 }
 
 // The GPU a worker graph runs on: one on the graph's NUMA socket (any GPU if
@@ -292,8 +323,15 @@ struct gpu_walk {
 	uint64_t append_errors; // graph walks punted because they could not be staged
 	uint64_t batches, max_batch, stale;
 	int rx_seen; // the node took packets since the flush node last ran
-	int draining; // gpu_fwd4_drain: hand everything back within the walk
+	int draining; // gpu_fwd4_drain: DRAIN_HAND_BACK or DRAIN_LEAVE (0: not draining)
+	uint64_t handed; // batches handed back (delivered onto their edges)
+	uint64_t drain_punted; // mbufs a drain in DRAIN_LEAVE mode sent to grout's CPU nodes
 };
+
+// gpu_fwd4_drain's modes: hand every batch back within the walk (the held one
+// sent and waited for at once), or leave the GPU: the batch on it handed back,
+// what is held or arrives sent to grout's CPU nodes (PUNT), untouched.
+enum { DRAIN_HAND_BACK = 1, DRAIN_LEAVE = 2 };
 
 static uint64_t now_ns(void) {
 	struct timespec ts;
@@ -346,7 +384,7 @@ void gpu_fwd4_rcu_readers(int on) {
 }
 
 static unsigned reader_id(const struct gpu_walk *w, int r) {
-	return GPU_FWD4_RCU_BASE + (unsigned)w->slot * GPU_FWD4_RCU_PER_GRAPH + (unsigned)r;
+	return gpu_hooks.rcu_base + (unsigned)w->slot * GPU_FWD4_RCU_PER_GRAPH + (unsigned)r;
 }
 
 // Buffer k's batch takes its first mbuf: a free reader goes online for it.
@@ -428,9 +466,9 @@ _Static_assert(sizeof(((struct rte_mbuf *)0)->data_off) == 2 && sizeof(((struct 
 // The registries as they are now (allocated once, at their first set).
 static const struct gr_hip_mbuf_layout *layout_now(struct gpu_walk *w) {
 	w->lay.n_ifaces = __atomic_load_n(&if_obj_n, __ATOMIC_ACQUIRE);
-	w->lay.ifaces = (const void *const *)if_obj;
+	w->lay.ifaces = if_obj;
 	w->lay.n_nh = __atomic_load_n(&nh_obj_n, __ATOMIC_ACQUIRE);
-	w->lay.nh = (const void *const *)nh_obj;
+	w->lay.nh = nh_obj;
 	return &w->lay;
 }
 
@@ -470,6 +508,7 @@ static void deliver(struct rte_graph *graph, struct rte_node *node, struct gpu_w
 		}
 	}
 	reader_handed_back(w, k);
+	w->handed++;
 	PROF_ADD(GPU_FWD4_PROF_DELIVER);
 }
 
@@ -575,9 +614,34 @@ static uint32_t reap(struct rte_graph *graph, struct rte_node *node, struct gpu_
 	return finish_pending(graph, node, w);
 }
 
+// gpu_fwd4_drain past its bound (DRAIN_LEAVE): the batch on the GPU is
+// waited for and handed back; the held one (staged, not sent: its frames and
+// mbufs untouched) goes to grout's CPU nodes, after it in arrival order.
+// Returns the mbufs handed back or sent on.
+static uint32_t leave(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
+	uint32_t n = finish_pending(graph, node, w);
+	if (w->n != 0) {
+		const uint32_t k = w->cur, held = w->n;
+		gr_hip_node_discard(w->q);
+		w->n = 0;
+		w->first_ns = 0;
+		rte_node_enqueue(graph, node, GR_HIP_E_PUNT, (void **)w->mbufs[k], (uint16_t)held);
+		reader_handed_back(w, k);
+		w->drain_punted += held;
+		n += held;
+	}
+	return n;
+}
+
 static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node, void **objs, uint16_t nb_objs) {
 	struct gpu_walk *w = gpu_fwd4_ctx(node)->w;
 	PROF_T0();
+	if (w->draining == DRAIN_LEAVE) { // the worker leaves the graph: nothing more for the GPU
+		leave(graph, node, w);
+		rte_node_enqueue(graph, node, GR_HIP_E_PUNT, objs, nb_objs);
+		w->drain_punted += nb_objs;
+		return nb_objs;
+	}
 	if (gpus[w->gpu].diverged) { // this GPU's mirrors are out of step: grout's CPU nodes
 		if (w->n != 0)
 			flush(graph, node, w); // the packets held first (punted too)
@@ -722,22 +786,47 @@ uint64_t gpu_fwd4_fini_freed(void) {
 	return __atomic_load_n(&fini_freed, __ATOMIC_RELAXED);
 }
 
+// Batches a drain may hand back: -1 = those the node holds when it starts +
+// DRAIN_EXTRA (what RX brings during its walks), else this many
+// (gpu_fwd4_set_drain_bound).
+#define DRAIN_EXTRA 2
+static int32_t drain_bound = -1;
+
+int gpu_fwd4_set_drain_bound(int32_t batches) {
+	drain_bound = batches < 0 ? -1 : batches;
+	return 0;
+}
+
 // Leaving a graph (grout's worker before it switches to a new graph or shuts
-// down, main_loop.c:466-470, with integration/grout-gpu_fwd4-datapath.patch):
-// walk it until the node holds nothing. The walks hand the batch on the GPU
-// back (waiting for it) and send the held one synchronously, as they send
-// whatever RX brings meanwhile; one walk more takes the batches' QSBR readers
-// offline. grout itself holds no packet across graph walks.
+// down: the graph_leave hook, main_loop.c:466-470 with
+// integration/grout-gpu_fwd4-datapath.patch). grout itself holds no packet
+// across graph walks; the node holds up to two batches. Walks of the graph in
+// DRAIN_HAND_BACK mode hand the batch on the GPU back (waiting for it) and
+// send the held one, and whatever RX brings meanwhile, synchronously: one walk
+// normally leaves nothing held. The walks are bounded by batches handed back,
+// not by walks: once the batches held at the start and DRAIN_EXTRA more are
+// back (gpu_fwd4_set_drain_bound), one walk in DRAIN_LEAVE mode hands back the batch on the GPU and sends
+// what is still held, and what RX brings in that walk, to grout's CPU nodes
+// (PUNT, untouched: forwarded by iface_input_cpu, counted there). Every
+// hand-back went through grout's nodes within its walk, so the batches' QSBR
+// readers go offline here. Returns the mbufs sent to grout's CPU nodes in
+// DRAIN_LEAVE mode (0 normally), or -ENOENT.
 int gpu_fwd4_drain(struct rte_graph *graph) {
 	struct gpu_walk *w = walk_of(graph);
 	if (w == NULL)
 		return -ENOENT;
-	w->draining = 1;
-	for (int k = 0; k < 16 && (w->n != 0 || w->pending); k++)
+	const uint64_t h0 = w->handed, p0 = w->drain_punted;
+	const uint64_t bound = drain_bound >= 0 ? (uint64_t)drain_bound : (w->n != 0) + (uint64_t)w->pending + DRAIN_EXTRA;
+	w->draining = DRAIN_HAND_BACK;
+	while ((w->n != 0 || w->pending) && w->handed - h0 < bound)
 		rte_graph_walk(graph);
-	rte_graph_walk(graph); // the readers of the last hand-back go offline
+	if (w->n != 0 || w->pending) {
+		w->draining = DRAIN_LEAVE;
+		rte_graph_walk(graph);
+	}
 	w->draining = 0;
-	return (int)(w->n + (w->pending ? w->pend_n : 0));
+	readers_release(w);
+	return (int)(w->drain_punted - p0);
 }
 
 static void gpu_fwd4_fini(const struct rte_graph *graph, struct rte_node *node) {
@@ -747,8 +836,11 @@ static void gpu_fwd4_fini(const struct rte_graph *graph, struct rte_node *node) 
 		if (w == NULL || w->graph != graph)
 			continue;
 		// a graph destroyed without gpu_fwd4_drain: its mbufs go back to the
-		// pool, counted (gpu_fwd4_fini_freed)
-		if (w->pending) // the GPU must be done with its buffers
+		// pool, counted (gpu_fwd4_fini_freed). The batch on the GPU is
+		// dropped from the queue only once the GPU is done with its frames
+		// (gr_hip_node_finish waits before it refuses a batch appended from
+		// the mbufs)
+		if (w->pending)
 			gr_hip_node_finish(w->q, NULL, NULL, NULL);
 		if (w->pending)
 			for (uint32_t j = 0; j < w->pend_n; j++)
@@ -799,6 +891,10 @@ static uint16_t gpu_flush_process(struct rte_graph *graph, struct rte_node *node
 	// a new graph walk: what was handed back in the walks before has been
 	// through grout's nodes, those batches' QSBR readers go offline
 	readers_release(w);
+	if (w->draining == DRAIN_LEAVE) {
+		const uint32_t n = leave(graph, node, w);
+		return (uint16_t)(n > UINT16_MAX ? UINT16_MAX : n);
+	}
 	// same edges as iface_input, same order; one batch handed back at most
 	// (flush() hands back the one still pending, and none is after these)
 	const uint64_t t = now_ns();
@@ -894,6 +990,8 @@ int gpu_fwd4_walk_info(const struct rte_graph *graph, struct gpu_fwd4_walk_info 
 		info->readers_online += w->rstate[r] != RD_FREE;
 	info->diverged = gpus[w->gpu].diverged;
 	info->append_errors = w->append_errors;
+	info->handed = w->handed;
+	info->drain_punted = w->drain_punted;
 	return 0;
 }
 

@@ -84,13 +84,12 @@ struct nexthop;
 #define GPU_FWD4_BATCH_MAX 15360
 
 // QSBR readers of the node (see gpu_fwd4_node.c, "RCU"): each graph holds
-// GPU_FWD4_RCU_PER_GRAPH reader ids from GPU_FWD4_RCU_BASE on, above the
-// workers' lcore ids. grout's rcu module sizes its QSBR variable for
-// RTE_MAX_LCORE + GPU_FWD4_RCU_READERS threads
+// GPU_FWD4_RCU_PER_GRAPH reader ids, above the workers' lcore ids. The module
+// asks for GPU_FWD4_RCU_READERS of them through its datapath hooks, and grout's
+// rcu module sizes its QSBR variable for them
 // (integration/grout-gpu_fwd4-datapath.patch).
 #define GPU_FWD4_RCU_PER_GRAPH 4
 #define GPU_FWD4_RCU_READERS (GPU_FWD4_MAX_GRAPHS * GPU_FWD4_RCU_PER_GRAPH)
-#define GPU_FWD4_RCU_BASE RTE_MAX_LCORE
 
 struct gpu_fwd4_conf {
 	uint32_t n_devs; // GPUs the module opens, 0 = every visible device
@@ -142,8 +141,9 @@ int gpu_fwd4_node_stats(const struct rte_graph *, struct gr_hip_node_stats *, ui
 // grout's iface_stats by gpu_fwd4_stats_flush (gr_hip_node_iface_stats).
 int gpu_fwd4_queue_stats(const struct rte_graph *, struct gr_hip_iface_stats *, uint32_t max_ifaces, int reset);
 
-// grout's housekeeping tick (gr_datapath_loop, main_loop.c:461-475, with
-// integration/grout-gpu_fwd4-datapath.patch): fold what the fast path
+// grout's housekeeping tick (gr_datapath_loop, main_loop.c:461-475, through
+// the stats_flush hook integration/grout-gpu_fwd4-datapath.patch adds, which
+// the module registers): fold what the fast path
 // counted for this worker's graph since the last tick into grout's own
 // statistics, so that `grcli stats` and `grcli interface stats` read as with
 // grout's CPU nodes:
@@ -162,13 +162,22 @@ typedef void (*gpu_fwd4_node_stat_cb)(void *cookie, uint32_t node_id, uint64_t p
 int gpu_fwd4_stats_flush(const struct rte_graph *, unsigned lcore_id, gpu_fwd4_node_stat_cb cb, void *cookie);
 
 // The worker leaves its graph (reconfiguration or shutdown): before it does,
-// grout's gr_datapath_loop calls this on the graph (main_loop.c:466-470,
+// grout's gr_datapath_loop calls this on the graph (the graph_leave hook the
+// module registers, main_loop.c:466-470 with
 // integration/grout-gpu_fwd4-datapath.patch). The node holds up to two
 // batches across graph walks, grout nothing: walks of the graph hand them
 // back through grout's nodes (the batch on the GPU waited for, the held one
-// sent at once) until the node holds nothing. Returns the mbufs still held
-// (0), or -ENOENT for a graph without the node.
+// sent at once), bounded by batches handed back (those held at the start +
+// 2, or gpu_fwd4_set_drain_bound's); past the bound the held mbufs,
+// and those RX brings in the last walk, go to grout's CPU nodes (PUNT). The
+// node then holds nothing and its QSBR readers are offline. Returns the mbufs
+// sent to grout's CPU nodes that way (0 normally), or -ENOENT for a graph
+// without the node.
 int gpu_fwd4_drain(struct rte_graph *);
+// Batches a drain may hand back before it sends the rest to grout's CPU
+// nodes: -1 (the default) = those held when it starts + 2; tests set 0 to
+// take that way at once. 0.
+int gpu_fwd4_set_drain_bound(int32_t batches);
 // mbufs freed by the node's fini because a graph was destroyed while it held
 // them (not drained first): counted, never silently.
 uint64_t gpu_fwd4_fini_freed(void);
@@ -183,6 +192,8 @@ struct gpu_fwd4_walk_info {
 	uint32_t readers_online; // the graph's QSBR readers online
 	int diverged; // its GPU's mirrors are out of step: everything goes to grout's CPU nodes
 	uint64_t append_errors; // graph walks that could not be staged, punted to grout's CPU nodes
+	uint64_t handed; // batches handed back onto their edges
+	uint64_t drain_punted; // mbufs drains sent to grout's CPU nodes (DRAIN_LEAVE)
 };
 int gpu_fwd4_walk_info(const struct rte_graph *, struct gpu_fwd4_walk_info *);
 // Tests only: 0 = the node takes no QSBR reader (round 2's behaviour, to

@@ -742,7 +742,8 @@ struct gr_hip_mbuf_layout {
 // n = every mbuf appended since the last send, and the batch is handed back
 // with gr_hip_node_finish_mbufs on that array (kept until then): the
 // hand-back reads each mbuf's fields again through the layout before it
-// writes them (gr_hip_node_finish returns -EINVAL for such a batch).
+// writes them (gr_hip_node_finish drops such a batch with -EINVAL, after
+// waiting for its GPU work: the caller may free the mbufs then).
 // Returns as gr_hip_node_append.
 int gr_hip_node_append_mbufs(gr_hip_queue_t *, void *const *mbufs, uint32_t n,
 			     const struct gr_hip_mbuf_layout *layout, uint32_t burst);

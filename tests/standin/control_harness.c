@@ -72,6 +72,16 @@ int gc_begin(void) {
 		gh_objects_clear();
 	gpu_fwd4_control_reset();
 	gr_test_events_reset();
+	// without the module (CPU tests) the mirror still gets the control
+	// thread's event base, as the module's init passes it
+	gpu_fwd4_control_attach(gr_test_event_base());
+	return 0;
+}
+
+// Tests: the mirror's event base taken away (events before the module's
+// init: no timer) or given back.
+int gc_attach(int on) {
+	gpu_fwd4_control_attach(on ? gr_test_event_base() : NULL);
 	return 0;
 }
 
@@ -149,6 +159,34 @@ int gc_vlan_add(uint16_t id, uint16_t parent_id, uint16_t vlan_id, const uint8_t
 static int do_iface_up(void *p) {
 	struct a_iface *a = p;
 	return iface_set_up_down(iface_from_id_rw(a->id), a->up);
+}
+
+// One control-loop turn: a neighbour learned by ARP on `iface_id` (its L3
+// nexthop waits for the next publication of the mirror), then the VRF's FIBs
+// resized (grout migrates its routes; the mirror refills new device FIBs and
+// publishes them). max_routes 0: that family unchanged.
+struct a_vrf_resize {
+	uint16_t vrf_id, iface_id;
+	uint32_t ip_be;
+	const uint8_t *mac;
+	struct gr_iface_info_vrf_fib v4, v6;
+};
+
+static int do_arp_vrf_resize(void *p) {
+	struct a_vrf_resize *a = p;
+	int r = 0;
+	if (a->mac != NULL)
+		r = arp_probe_input(a->iface_id, a->ip_be, (const struct rte_ether_addr *)a->mac);
+	if (r < 0)
+		return r;
+	return iface_vrf_reconfig_fib(iface_from_id_rw(a->vrf_id), &a->v4, &a->v6);
+}
+
+int gc_arp_vrf_resize(uint16_t vrf_id, uint16_t iface_id, uint32_t ip_be, const uint8_t *mac, uint32_t max_routes,
+		      uint32_t max_routes6) {
+	struct a_vrf_resize a = {.vrf_id = vrf_id, .iface_id = iface_id, .ip_be = ip_be, .mac = mac,
+				 .v4 = {max_routes, 0}, .v6 = {max_routes6, 0}};
+	return on_control(do_arp_vrf_resize, &a);
 }
 
 int gc_iface_up(uint16_t id, int up) {

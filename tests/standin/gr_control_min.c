@@ -57,6 +57,7 @@ static void rcu_sync(void) {
 
 // ---- libevent timers ---------------------------------------------------------
 struct event {
+	struct event_base *base;
 	void (*cb)(int, short, void *);
 	void *arg;
 	int pending;
@@ -65,12 +66,12 @@ struct event {
 static struct event *timers;
 
 struct event *event_new(struct event_base *base, int fd, short what, void (*cb)(int, short, void *), void *arg) {
-	(void)base;
 	(void)fd;
 	(void)what;
 	struct event *e = calloc(1, sizeof(*e));
 	if (e == NULL)
 		return NULL;
+	e->base = base;
 	e->cb = cb;
 	e->arg = arg;
 	e->next = timers;
@@ -80,6 +81,8 @@ struct event *event_new(struct event_base *base, int fd, short what, void (*cb)(
 
 int event_add(struct event *ev, const struct timeval *tv) {
 	(void)tv;
+	if (ev->base == NULL)
+		return -1; // libevent: no event_base set
 	ev->pending = 1;
 	return 0;
 }
@@ -96,6 +99,11 @@ void event_free(struct event *ev) {
 			break;
 		}
 	free(ev);
+}
+
+struct event_base *gr_test_event_base(void) {
+	static char base; // opaque: only its address is used
+	return (struct event_base *)&base;
 }
 
 void gr_test_event_loop_turn(void) {
@@ -310,6 +318,41 @@ struct iface *iface_create(const struct gr_iface *conf, const void *api_info) {
 }
 
 // iface_set_up_down, the generic path (iface.c:632-654)
+// iface_reconfig (iface.c:325-420) of a VRF's FIB sizes (GR_VRF_SET_FIB,
+// vrf.c:315-357): per address family a non-zero max_routes replaces the size
+// (and resets num_tbl8 unless one is given too), a non-zero num_tbl8 replaces
+// that; an unchanged family is skipped; fib4_reconfig / fib6_reconfig fill
+// the defaults (route.c:740-748) and migrate the routes (the stand-in's RIB is
+// a list: nothing to move). Then GR_EVENT_IFACE_POST_RECONFIG (iface.c:420).
+int iface_vrf_reconfig_fib(struct iface *iface, const struct gr_iface_info_vrf_fib *v4,
+			   const struct gr_iface_info_vrf_fib *v6) {
+	if (iface == NULL || iface->type != GR_IFACE_TYPE_VRF)
+		return errno_set(EINVAL);
+	struct iface_info_vrf *vrf = iface_info_vrf(iface);
+	const struct gr_iface_info_vrf_fib *api[2] = {v4, v6};
+	struct gr_iface_info_vrf_fib *conf[2] = {&vrf->ipv4, &vrf->ipv6};
+	for (int af = 0; af < 2; af++) {
+		if (api[af] == NULL || (api[af]->max_routes == 0 && api[af]->num_tbl8 == 0))
+			continue;
+		const struct gr_iface_info_vrf_fib old = *conf[af];
+		if (api[af]->max_routes) {
+			conf[af]->max_routes = api[af]->max_routes;
+			if (!api[af]->num_tbl8)
+				conf[af]->num_tbl8 = 0;
+		}
+		if (api[af]->num_tbl8)
+			conf[af]->num_tbl8 = api[af]->num_tbl8;
+		if (conf[af]->max_routes == old.max_routes && conf[af]->num_tbl8 == old.num_tbl8)
+			continue;
+		if (!conf[af]->max_routes)
+			conf[af]->max_routes = max_routes_default;
+		if (af == 0 && !conf[af]->num_tbl8)
+			conf[af]->num_tbl8 = fib4_auto_tbl8(conf[af]->max_routes);
+	}
+	event_push(GR_EVENT_IFACE_POST_RECONFIG, iface);
+	return 0;
+}
+
 int iface_set_up_down(struct iface *iface, bool up) {
 	if (iface == NULL)
 		return errno_set(EINVAL);

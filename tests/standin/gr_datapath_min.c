@@ -4,7 +4,6 @@
 // node infos and their registration pass, parent attachment, the drop
 // node's process(), modules, and the iface / nexthop lookups.
 #include "gr_datapath_min.h"
-#include "gpu_fwd4_node.h"
 
 #include <errno.h>
 #include <stdio.h>
@@ -34,11 +33,46 @@ struct rte_rcu_qsbr *gr_datapath_rcu(void) {
 	return rcu;
 }
 
+// ---- datapath hooks (the datapath patch's main_loop.c) -----------------------
+static STAILQ_HEAD(, gr_datapath_hooks) hooks = STAILQ_HEAD_INITIALIZER(hooks);
+static uint32_t hooks_readers;
+
+void gr_datapath_hooks_register(struct gr_datapath_hooks *h) {
+	h->rcu_base = RTE_MAX_LCORE + hooks_readers;
+	hooks_readers += h->rcu_readers;
+	STAILQ_INSERT_TAIL(&hooks, h, next);
+}
+
+uint32_t gr_datapath_hooks_readers(void) {
+	return hooks_readers;
+}
+
+int gr_datapath_hooks_graph_leave(struct rte_graph *graph) {
+	struct gr_datapath_hooks *h;
+	int ret = 0;
+	STAILQ_FOREACH(h, &hooks, next) {
+		const int n = h->graph_leave != NULL ? h->graph_leave(graph) : 0;
+		if (n < 0 && ret >= 0)
+			ret = n;
+		else if (n > 0 && ret >= 0)
+			ret += n;
+	}
+	return ret;
+}
+
+void gr_datapath_hooks_stats_flush(const struct rte_graph *graph, unsigned lcore_id, gr_node_stats_cb_t cb,
+				   void *cookie) {
+	struct gr_datapath_hooks *h;
+	STAILQ_FOREACH(h, &hooks, next)
+		if (h->stats_flush != NULL)
+			h->stats_flush(graph, lcore_id, cb, cookie);
+}
+
 // grout's rcu module (main_loop.c:538-552) as the integration patch sizes
-// it: the workers' lcore ids, then the fast path node's readers.
+// it: the workers' lcore ids, then the hooks' readers.
 static void rcu_init(struct event_base *ev) {
 	(void)ev;
-	const uint32_t n = RTE_MAX_LCORE + GPU_FWD4_RCU_READERS;
+	const uint32_t n = RTE_MAX_LCORE + hooks_readers;
 	rcu = aligned_alloc(64, (rte_rcu_qsbr_get_memsize(n) + 63) & ~(size_t)63);
 	if (rcu == NULL || rte_rcu_qsbr_init(rcu, n) < 0)
 		abort(); // grout: ABORT("rte_zmalloc(rcu)")

@@ -96,6 +96,10 @@ void event_free(struct event *ev);
 // call is one): every pending timer fires. Time is not modelled: a turn is
 // taken to outlast any timer's delay.
 void gr_test_event_loop_turn(void);
+// The control thread's event base the harness gives modules at init (grout:
+// its libevent base). An event made without one cannot be added (libevent's
+// event_add: "event has no event_base set", -1).
+struct event_base *gr_test_event_base(void);
 
 // route4_event / route6_event (modules/ip/control/route.c:205-210,
 // modules/ip6/control/route.c:222-227), moved into ip4.h / ip6.h by the
@@ -170,6 +174,9 @@ struct iface *iface_create(const struct gr_iface *conf, const void *api_info);
 int iface_destroy(struct iface *);
 int iface_set_up_down(struct iface *, bool up);
 int iface_set_eth_addr(struct iface *, const struct rte_ether_addr *);
+// iface_reconfig of a VRF's FIB sizes (GR_VRF_SET_FIB): NULL or zero sizes leave a family as it is.
+int iface_vrf_reconfig_fib(struct iface *, const struct gr_iface_info_vrf_fib *v4,
+			   const struct gr_iface_info_vrf_fib *v6);
 int iface_get_eth_addr(const struct iface *, struct rte_ether_addr *);
 struct iface *iface_from_id_rw(uint16_t id);
 // The stand-in's iface storage (ids index it), for the harness's decoding.

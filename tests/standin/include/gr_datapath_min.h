@@ -247,8 +247,8 @@ void gr_test_lcore_set(unsigned lcore_id);
 
 // The datapath's QSBR variable (main_loop.c:534-536, created by the "rcu"
 // module, :538-543): every worker registers its lcore id as a reader
-// (:408); the fast path's node registers GPU_FWD4_RCU_READERS more
-// (gpu_fwd4_node.h, sized in by integration/grout-gpu_fwd4-datapath.patch).
+// (:408); the datapath hooks' modules register theirs above (sized in by
+// integration/grout-gpu_fwd4-datapath.patch, see "datapath hooks" below).
 struct rte_rcu_qsbr *gr_datapath_rcu(void);
 
 // struct iface_stats and its per-lcore table (iface.h:105-119)
@@ -422,6 +422,41 @@ rte_edge_t gr_node_attach_parent(const char *parent, const char *node);
 // graph_init's registration pass (graph.c:652-688): register every node of
 // node_infos with rte_graph, then run their register callbacks. 0 or -errno.
 int gr_nodes_register(void);
+
+// ---- datapath hooks ----------------------------------------------------------
+// What integration/grout-gpu_fwd4-datapath.patch adds to grout's
+// modules/infra/datapath/datapath.h and main_loop.c: a module whose nodes hold
+// packets across graph walks, or count for nodes that do not run themselves,
+// registers hooks (at constructor time, before the "rcu" module's init) that
+// gr_datapath_loop calls. Without such a module grout runs as before.
+typedef void (*gr_node_stats_cb_t)(void *cookie, uint32_t node_id, uint64_t packets, uint64_t calls);
+
+struct gr_datapath_hooks {
+	const char *name;
+	// QSBR reader ids the module's nodes use above the workers' lcore ids;
+	// rcu_base, the first of them, is set by gr_datapath_hooks_register
+	uint32_t rcu_readers;
+	uint32_t rcu_base;
+	// the worker is about to leave `graph` (reconfiguration, shutdown): hand
+	// back through the graph what its nodes hold. Returns the mbufs that went
+	// to a drop node instead (counted there), or -errno.
+	int (*graph_leave)(struct rte_graph *graph);
+	// the housekeeping tick, after rte_graph's own counters: cb once per node
+	// with what it counted since the last tick
+	int (*stats_flush)(const struct rte_graph *graph, unsigned lcore_id, gr_node_stats_cb_t cb, void *cookie);
+	STAILQ_ENTRY(gr_datapath_hooks) next;
+};
+
+void gr_datapath_hooks_register(struct gr_datapath_hooks *);
+// The QSBR reader ids the hooks registered (the patched rcu_init sizes its
+// variable for RTE_MAX_LCORE + this).
+uint32_t gr_datapath_hooks_readers(void);
+// What the patched gr_datapath_loop does, for the harness's worker loop:
+// every hook's graph_leave (the sum of their returns, the first -errno wins),
+// every hook's stats_flush.
+int gr_datapath_hooks_graph_leave(struct rte_graph *graph);
+void gr_datapath_hooks_stats_flush(const struct rte_graph *graph, unsigned lcore_id, gr_node_stats_cb_t cb,
+				   void *cookie);
 
 // ---- modules ---------------------------------------------------------------
 struct event_base;

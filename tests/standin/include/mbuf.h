@@ -1,0 +1,7 @@
+// SPDX-License-Identifier: BSD-3-Clause
+// Test stand-in under the name of modules/infra/datapath/mbuf.h: GR_MBUF_PRIV_DATA_TYPE, mbuf_data, gr_mbuf_is_traced.
+// The module files (grout_amd/module/) include grout's and DPDK's headers by
+// their names; here those names lead to the stand-ins, in grout to the real ones.
+#pragma once
+
+#include "gr_datapath_min.h"

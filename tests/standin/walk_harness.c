@@ -390,7 +390,7 @@ int gh_init(const int *devs, uint32_t n_devs, uint32_t max_ifaces, uint32_t max_
 		return -ENOMEM;
 	if ((r = gh_register()) < 0)
 		return r;
-	if ((r = gr_modules_init(NULL)) < 0)
+	if ((r = gr_modules_init(gr_test_event_base())) < 0)
 		return r;
 	// grout's iface / nexthop objects, in grout's iface table and in the
 	// node's registries (the control plane's object events)
@@ -638,8 +638,9 @@ int gh_load(const uint8_t *frames, uint32_t stride, const struct gr_hip_pkt_meta
 // every 256 walks (:461-475) with integration/grout-gpu_fwd4-datapath.patch:
 // the QSBR quiescent report, rte_graph's per-node counters folded into the
 // worker's node statistics (node_stats_callback, :40-66: packets = DPDK's
-// objs, the sum of process() returns; batches = calls), then the fast path's
-// counters for the nodes it replaced and for the ifaces.
+// objs, the sum of process() returns; batches = calls), then every datapath
+// hook's stats_flush (the fast path module's: its counters for the nodes it
+// replaced and for the ifaces).
 static void gpu_node_stat(void *cookie, uint32_t node_id, uint64_t packets, uint64_t calls) {
 	const int k = (int)(intptr_t)cookie;
 	H.graphs[k].w_packets[node_id] += packets;
@@ -658,7 +659,7 @@ static void housekeeping(int k) {
 		H.graphs[k].prev_packets[id] = n->total_packets;
 		H.graphs[k].prev_calls[id] = n->total_calls;
 	}
-	gpu_fwd4_stats_flush(H.graphs[k].graph, rte_lcore_id(), gpu_node_stat, (void *)(intptr_t)k);
+	gr_datapath_hooks_stats_flush(H.graphs[k].graph, rte_lcore_id(), gpu_node_stat, (void *)(intptr_t)k);
 }
 
 static void walk_once(int k) {
@@ -1146,7 +1147,7 @@ void gh_fini(void) {
 	if (gr_datapath_rcu() != NULL)
 		rte_rcu_qsbr_thread_unregister(gr_datapath_rcu(), 0);
 	H.cur = -1;
-	gr_modules_fini(NULL);
+	gr_modules_fini(gr_test_event_base());
 	mbuf_mem_free();
 	free(H.edge_of);
 	free(H.seq_of);
@@ -1159,17 +1160,21 @@ void gh_fini(void) {
 struct gh_reload_result {
 	uint32_t held; // mbufs the node held when the worker left the graph
 	uint32_t in_flight; // batches it had on the GPU
-	int32_t left; // gpu_fwd4_drain's return (-1: not called)
+	int32_t left; // the graph_leave hooks' return: mbufs the drain sent to grout's CPU nodes (-1: not called)
 	uint32_t recorded; // mbufs through grout's nodes when the old graph was destroyed
 	uint64_t fini_freed; // mbufs the old graph's fini freed
 	int32_t graph; // the new current graph
 	uint32_t rx; // mbufs port_rx had delivered by then
+	uint32_t readers_online; // the node's QSBR readers online after the drain
+	uint32_t held_after; // mbufs the node held after it
+	uint32_t in_flight_after;
+	uint32_t _pad;
 };
 
 // grout's reconfiguration of a worker (worker_graph_reload, graph.c:263-290;
 // gr_datapath_loop, main_loop.c:466-470): the worker walks its graph
 // `walks` times, leaves it at a housekeeping tick (with the datapath patch:
-// gpu_fwd4_drain first, when `drain`), the control plane creates the new
+// the graph_leave hooks first, the node's gpu_fwd4_drain, when `drain`), the control plane creates the new
 // graph (the other name index) and destroys the old one. The new graph is
 // the current one afterwards; port_rx goes on with the injected stream.
 int gh_reload_test(uint32_t walks, int drain, struct gh_reload_result *res) {
@@ -1183,7 +1188,11 @@ int gh_reload_test(uint32_t walks, int drain, struct gh_reload_result *res) {
 	gpu_fwd4_walk_info(H.graphs[k].graph, &info);
 	res->held = info.held;
 	res->in_flight = info.in_flight;
-	res->left = drain ? gpu_fwd4_drain(H.graphs[k].graph) : -1;
+	res->left = drain ? gr_datapath_hooks_graph_leave(H.graphs[k].graph) : -1;
+	gpu_fwd4_walk_info(H.graphs[k].graph, &info);
+	res->readers_online = info.readers_online;
+	res->held_after = info.held;
+	res->in_flight_after = info.in_flight;
 	housekeeping(k);
 	res->recorded = __atomic_load_n(&H.recorded, __ATOMIC_ACQUIRE);
 	res->rx = H.next_rx;
@@ -1227,7 +1236,7 @@ static void *worker_thread(void *p) {
 		rte_graph_walk(g);
 		if (++loop == 256) { // grout's housekeeping tick: the node's statistics fold
 			loop = 0;
-			gpu_fwd4_stats_flush(g, (unsigned)a->k, NULL, NULL); // its own lcore's iface_stats
+			gr_datapath_hooks_stats_flush(g, (unsigned)a->k, NULL, NULL); // its own lcore's iface_stats
 		}
 		if (w > (1ull << 32)) {
 			a->err = -ETIMEDOUT;

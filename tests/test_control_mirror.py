@@ -44,8 +44,9 @@ P, U8, U16, U32, I = ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint16, ctypes.c_
 
 STATS_DT = np.dtype([("events", "<u8"), ("internal", "<u8"), ("commits", "<u8"), ("errors", "<u8"),
                      ("first_error", "<i4"), ("slots_used", "<u4"), ("reta_used", "<u4"), ("routes4", "<u4"),
-                     ("routes6", "<u4"), ("pending", "<u4"), ("presync", "<u8")])
-assert STATS_DT.itemsize == 64
+                     ("routes6", "<u4"), ("pending", "<u4"), ("presync", "<u8"), ("unordered", "<u8"),
+                     ("no_timer", "<u8")])
+assert STATS_DT.itemsize == 80
 
 ORIGIN_STATIC, ORIGIN_LINK, ORIGIN_LEARN, ORIGIN_INTERNAL = 4, 2, 3, 255
 NH_F_NEIGH = 0x20
@@ -87,6 +88,7 @@ def lib():
             "gpu_fwd4_control_reta": (I, [U32, P, U32]), "gpu_fwd4_control_routes4": (I, [P, U32]),
             "gpu_fwd4_control_routes6": (I, [P, U32]), "gpu_fwd4_control_stats": (None, [P]),
             "gpu_fwd4_control_replay": (I, [U32]),
+            "gc_arp_vrf_resize": (I, [U16, U16, U32, P, U32, U32]), "gc_attach": (I, [I]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -308,6 +310,50 @@ def test_mirror_publishes_route_changes_in_batches(control):
     st3 = stats()
     assert st3["presync"] - st2["presync"] >= 1, (st2, st3)
     assert st3["pending"] == 0 and st3["routes4"] == st2["routes4"] - 10_000  # the group keeps its route
+
+
+def test_mirror_vrf_resize_publishes_nexthops_first(control):
+    """A VRF's FIBs resized (iface_reconfig with GR_VRF_SET_FIB, vrf.c:315-357:
+    grout migrates its routes, the mirror refills new device FIBs and
+    publishes them) in the same control-loop turn as a neighbour learned by
+    ARP, whose L3 nexthop is still waiting for the next publication: the
+    refill publishes the nexthops before the routes that may name them (slots
+    are reused: a stale slot could carry a deleted neighbour's MAC). No
+    publication is ever made with L3 nexthop changes pending (unordered 0)."""
+    L = control
+    build_base()
+    w = Want()
+    want_base(w)
+    st0 = stats()
+    ok(L.gc_arp_vrf_resize(VRF, PORTS[2], be("172.16.2.9"), mac(HOST3_MAC), 1 << 17, 1 << 17))
+    st1 = stats()
+    assert st1["errors"] == 0 and st1["unordered"] == 0, st1
+    assert st1["commits"] - st0["commits"] >= 2 and st1["pending"] == 0, (st0, st1)  # the refill's v4 + v6
+    h = w.l3(L.gc_slot4(VRF, be("172.16.2.9")), 2, "172.16.2.9", HOST3_MAC, abi.NH_S["REACHABLE"], NH_F_NEIGH)
+    w.route("172.16.2.9/32", h)
+    check_shadow(w)
+    # an unchanged size is not a reconfiguration of the FIBs: nothing refilled
+    ok(L.gc_arp_vrf_resize(VRF, PORTS[2], be("172.16.2.9"), None, 1 << 17, 0))
+    assert stats()["commits"] == st1["commits"]
+
+
+def test_mirror_timer_follows_the_event_base(control):
+    """Route events before the module's init attaches the control thread's
+    event base have no publication timer: each change is published at once,
+    counted (no_timer). Once a base is attached the timer is made on it and
+    the changes of one turn are published together again."""
+    L = control
+    build_base()
+    ok(L.gc_attach(0))
+    st0 = stats()
+    ok(L.gc_route4_add_many(VRF, be("20.0.0.0"), 24, 10, 100, ORIGIN_STATIC))
+    st1 = stats()
+    assert st1["no_timer"] - st0["no_timer"] == 10 and st1["commits"] - st0["commits"] == 10, (st0, st1)
+    ok(L.gc_attach(1))
+    ok(L.gc_route4_add_many(VRF, be("21.0.0.0"), 24, 10, 100, ORIGIN_STATIC))
+    st2 = stats()
+    assert st2["no_timer"] == st1["no_timer"] and st2["commits"] - st1["commits"] == 1, (st1, st2)
+    assert st2["errors"] == 0 and st2["unordered"] == 0
 
 
 def test_mirror_without_the_patch_misses_internal_objects(control):
@@ -644,6 +690,31 @@ def test_control_bulk_routes_walk(mirrored):
     grp["n_members"], grp["single"] = 1, sl["m101"]
     g = walk_check(w, fr, me, ["bulk"] * len(me))["bulk"]
     assert edges(g) == ["ip_error_dest_unreach"]
+
+
+@pytest.mark.gpu
+def test_control_vrf_resize_walk(mirrored):
+    """The VRF's FIBs resized in the turn a neighbour is learned: the GPUs'
+    new FIBs hold every route and the neighbour's nexthop is published with
+    them; walks to it and to the base corpus forward bit-exact."""
+    L = mirrored
+    w = Want()
+    sl = want_base(w)
+    sl.update(want_v6(w))
+    ok(L.gc_arp_vrf_resize(VRF, PORTS[2], be("172.16.2.9"), mac(HOST3_MAC), 1 << 17, 1 << 17))
+    assert stats()["unordered"] == 0 and stats()["errors"] == 0
+    h = w.l3(L.gc_slot4(VRF, be("172.16.2.9")), 2, "172.16.2.9", HOST3_MAC, abi.NH_S["REACHABLE"], NH_F_NEIGH)
+    w.route("172.16.2.9/32", h)
+    check_shadow(w)
+    fr, me, labs = corpus()
+    g = walk_check(w, fr, me, labs)
+    assert edges(g["gw"]) == ["port_output"] and edges(g["group"]) == ["port_output"]
+    r = np.zeros(1, dtype=abi.ROUTE_DT)
+    r["ip"], r["prefixlen"], r["vrf_id"], r["nh"] = T.ip4("172.16.2.9"), 32, VRF, h
+    fr, me = S.stream(4096, 0xB19, routes=r, in_iface=PORTS[0], dst_mac=T.PORT_MAC[0])
+    fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
+    g = walk_check(w, fr, me, ["host"] * len(me))["host"]
+    assert edges(g) == ["port_output"] and (g["iface"] == PORTS[2]).all()
 
 
 @pytest.mark.gpu

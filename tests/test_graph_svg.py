@@ -82,7 +82,7 @@ def test_verdict_edges_name_grout_nodes():
 
 
 def test_node_edges_match_the_fixture():
-    """The compiled node's next nodes (libgrout_graph.so) carry those names."""
+    """The compiled node's next nodes (libgrout_gpu_fwd4.so, loaded by the stand-in library) carry those names."""
     from test_graph_walk import edges_of, lib
     assert lib().gh_register() == 0
     got = edges_of("iface_input")

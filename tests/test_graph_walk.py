@@ -1,12 +1,14 @@
 # SPDX-License-Identifier: BSD-3-Clause
-"""The fast path as a grout node in an rte_graph walk (grout_amd/graph/).
+"""The fast path as a grout node in an rte_graph walk (grout_amd/module/).
 
 gpu_fwd4_node.c is the node a grout maintainer compiles into grout: it is
 registered as "iface_input" through grout's node-info surface, its next
 nodes are the verdict edges, and it hands each mbuf to its edge with the
-private data grout's chain leaves there. Here it is compiled against the
-rte_graph / grout stand-ins (rte_graph_min.h, gr_datapath_min.h) and walked in
-a worker-shaped graph: port_rx (bursts of 64) -> iface_input -> recorder
+private data grout's chain leaves there. Here the module library
+(libgrout_gpu_fwd4.so) is compiled against the rte_graph / grout stand-ins
+under grout's header names (tests/standin/include) and loaded by the
+stand-in library (tests/standin/libgrout_standin.so), which walks it in a
+worker-shaped graph: port_rx (bursts of 64) -> iface_input -> recorder
 nodes named after every edge (walk_harness.c).
 
 CPU: the stand-in runtime's semantics (graph_selftest.c), the node's
@@ -26,7 +28,9 @@ from grout_amd import abi
 from grout_amd import synth as S
 from grout_amd import topology as T
 
-LIB = os.path.join(os.path.dirname(abi.LIB_HIP), "libgrout_graph.so")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "tests", "standin", "libgrout_standin.so")  # test infrastructure: the stand-ins + harness
+LIB_MODULE = os.path.join(os.path.dirname(abi.LIB_HIP), "libgrout_gpu_fwd4.so")  # the module (product)
 
 OUT_DT = np.dtype([("pkt_len", "<u4"), ("data_len", "<u2"), ("data_off", "<u2"), ("packet_type", "<u4"),
                    ("iface", "<u2"), ("vlan_id", "<u2"), ("edge", "u1"), ("domain", "u1"), ("conn", "<u2"),
@@ -93,8 +97,9 @@ def lib():
 
 
 WALK_INFO_DT = np.dtype([("held", "<u4"), ("in_flight", "<u4"), ("batches", "<u8"), ("max_batch", "<u8"),
-                         ("stale", "<u8"), ("readers_online", "<u4"), ("diverged", "<i4"), ("append_errors", "<u8")])
-assert WALK_INFO_DT.itemsize == 48
+                         ("stale", "<u8"), ("readers_online", "<u4"), ("diverged", "<i4"), ("append_errors", "<u8"),
+                         ("handed", "<u8"), ("drain_punted", "<u8")])
+assert WALK_INFO_DT.itemsize == 64
 RCU_RES_DT = np.dtype([("sync_before_handback", "<u4"), ("recorded_at_sync", "<u4"), ("freed_reads", "<u4"),
                        ("recorded", "<u4"), ("stale", "<u8"), ("sync_us", "<u8"), ("walks", "<u4"),
                        ("sync_done", "<u4")])
@@ -863,8 +868,9 @@ def test_graph_walk_long_bursts(burst):
 
 
 RELOAD_DT = np.dtype([("held", "<u4"), ("in_flight", "<u4"), ("left", "<i4"), ("recorded", "<u4"),
-                      ("fini_freed", "<u8"), ("graph", "<i4"), ("rx", "<u4")])
-assert RELOAD_DT.itemsize == 32
+                      ("fini_freed", "<u8"), ("graph", "<i4"), ("rx", "<u4"), ("readers_online", "<u4"),
+                      ("held_after", "<u4"), ("in_flight_after", "<u4"), ("_pad", "<u4")])
+assert RELOAD_DT.itemsize == 48
 
 
 def _reload(walks, drain):
@@ -876,18 +882,23 @@ def _reload(walks, drain):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("drain", [1, 0], ids=["drained", "not_drained"])
-def test_graph_reload_mid_stream(drain):
+@pytest.mark.parametrize("mode", ["drained", "drained_leave", "not_drained"])
+def test_graph_reload_mid_stream(mode):
     """grout reconfigures a worker mid-stream (worker_graph_reload,
     graph.c:263-290): the worker leaves its graph at a housekeeping tick
     (main_loop.c:466-470), the control plane gives it a new graph and
     destroys the old one. grout's nodes hold nothing across walks; the fast
     path's node holds the batch it accumulates (and one on the GPU). With
-    the datapath patch the worker drains the node first (gpu_fwd4_drain):
+    the datapath patch the worker runs the datapath hooks' graph_leave first
+    (the module's gpu_fwd4_drain), while port_rx keeps delivering the stream:
     every injected mbuf reaches grout's node behind its edge, bit-exact with
-    the oracle, and nothing is freed at the old graph's fini. Without it (the
-    negative control) the held mbufs are freed there -- counted
-    (gpu_fwd4_fini_freed), never handed on."""
+    the oracle, nothing is held or freed at the old graph's fini, and the
+    node's QSBR readers are all offline. drained_leave: the drain's bound on
+    batches handed back set to 0, so that it leaves the GPU at once: the
+    batch on the GPU is handed back, the held batch and what RX brings in
+    that walk go to grout's CPU nodes (iface_input_cpu) untouched, counted in
+    the drain's return. Without the drain (the negative control) the held
+    mbufs are freed at fini -- counted (gpu_fwd4_fini_freed), never handed on."""
     L = lib()
     fp = graph_ctx()
     t = T.config_single_route()
@@ -897,16 +908,26 @@ def test_graph_reload_mid_stream(drain):
     fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
     _, _, _, want, _ = oracle.Oracle(t).process_mbufs(fr, me, lines_only=True, burst=BURST)
     walks = 100  # 64 full bursts fill a batch (sent), 36 more are held
+    drain = mode != "not_drained"
+    L.gpu_fwd4_set_drain_bound.argtypes = [ctypes.c_int32]
     assert L.gpu_fwd4_set_batch(BATCH, 10_000_000_000) == 0  # no age flush: they stay held
     try:
         assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, n) == 0
+        if mode == "drained_leave":
+            assert L.gpu_fwd4_set_drain_bound(0) == 0
         r = _reload(walks, drain)
-        assert r["held"] == walks * BURST - BATCH, r
+        assert L.gpu_fwd4_set_drain_bound(-1) == 0
+        assert r["held"] == walks * BURST - BATCH and r["in_flight"] == 1, r
         if drain:
-            assert r["left"] == 0 and r["fini_freed"] == 0, r
-            # everything port_rx delivered (the drain's walks polled RX too) is
-            # through grout's nodes before the switch
-            assert r["recorded"] == r["rx"] >= walks * BURST, r
+            assert r["fini_freed"] == 0 and r["held_after"] == 0 and r["in_flight_after"] == 0, r
+            assert r["readers_online"] == 0, r  # the drain released the batches' QSBR readers
+            # RX kept delivering through the drain, and everything it delivered
+            # is through grout's nodes before the switch
+            assert r["recorded"] == r["rx"] > walks * BURST, r
+            if mode == "drained":
+                assert r["left"] == 0, r
+            else:  # the held batch + the drain walk's burst, to iface_input_cpu
+                assert r["left"] == r["held"] + (r["rx"] - walks * BURST), r
         else:
             assert r["fini_freed"] >= r["held"], r
         w = L.gh_run(1 << 15)  # the new graph goes on with the stream
@@ -915,6 +936,7 @@ def test_graph_reload_mid_stream(drain):
         lines = np.zeros((n, abi.LINE), dtype=np.uint8)
         assert L.gh_results(out.ctypes.data, lines.ctypes.data) == n
     finally:
+        L.gpu_fwd4_set_drain_bound(-1)
         assert L.gpu_fwd4_set_batch(BATCH, DELAY_NS) == 0
         _reload(0, 1)  # back to a graph in slot 0 for the other tests
         assert L.gh_graph_use(0) == 0
@@ -924,11 +946,21 @@ def test_graph_reload_mid_stream(drain):
         assert reached.all()
     else:
         assert (~reached).sum() == r["fini_freed"], (int((~reached).sum()), r)
-    # every packet leaves on port_output, whose private data is iface_output's
-    # vlan_id (over the l3 nexthop's bytes, check_walk)
-    assert (out["edge"][reached] == abi.EDGE["port_output"]).all()
+    punt = out["edge"] == abi.EDGE["punt"]
+    if mode == "drained_leave":
+        # the held mbufs and the drain walk's burst: right after the batch on the GPU
+        lo = BATCH
+        assert np.array_equal(np.nonzero(punt)[0], np.arange(lo, lo + r["left"]))
+        assert (out["data_off"][punt] == 128).all()  # as port_rx left them
+        assert np.array_equal(lines[punt], fr[punt][:, :abi.LINE])  # frames untouched
+    else:
+        assert not punt.any()
+    fwd = reached & ~punt
+    # every other packet leaves on port_output, whose private data is
+    # iface_output's vlan_id (over the l3 nexthop's bytes, check_walk)
+    assert (out["edge"][fwd] == abi.EDGE["port_output"]).all()
     for f in ("edge", "pkt_len", "data_len", "data_off", "iface", "vlan_id"):
-        assert np.array_equal(out[f][reached], want[f][reached]), f
+        assert np.array_equal(out[f][fwd], want[f][fwd]), f
 
 
 @pytest.mark.gpu

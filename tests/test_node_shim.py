@@ -668,3 +668,52 @@ def test_node_append_send(fastpath, ptrs):
         if ptrs:
             abi.check("gr_hip_host_unregister", L.gr_hip_host_unregister(fastpath.h, bufs.ctypes.data))
         q.close()
+
+
+@pytest.mark.gpu
+def test_finish_drop_waits_for_the_gpu(fastpath):
+    """gr_hip_node_finish on a batch appended from the mbufs drops it with
+    -EINVAL (gr_hip_node_finish_mbufs hands such a batch back), but only once
+    the GPU is done with it: gpu_fwd4_fini calls it on a graph destroyed with
+    a batch in flight and frees the mbufs next, while the kernel rewrites
+    registered frames in place. Every forwarded frame is therefore already
+    rewritten when the call returns."""
+    from golden_util import fresh_fastpath_state
+    topo = T.config_single_route()
+    n = 1 << 18
+    fr, me = S.stream(n, 0xF1A1, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    fresh_fastpath_state(fastpath, topo)
+    lines, v, _, _, _ = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
+    bufs, m = mbufs_for(fr, me)
+    orig = bufs[:, :abi.LINE].copy()
+    L_, G = GROUT_LAYOUT, GROUT_STAGE
+    mem = np.zeros((n, 256), dtype=np.uint8)
+    U16, U32, U64 = mem.view(np.uint16), mem.view(np.uint32), mem.view(np.uint64)
+    U64[:, G["buf_addr"] // 8] = m["frame"] - RX_DATA_OFF
+    U16[:, L_["data_off"] // 2] = RX_DATA_OFF
+    U16[:, L_["data_len"] // 2] = m["data_len"]
+    U32[:, L_["pkt_len"] // 4] = m["pkt_len"]
+    U32[:, G["rss"] // 4] = m["rss"]
+    ifobj = np.zeros((topo.max_ifaces, 64), dtype=np.uint8)
+    ifobj.view(np.uint16)[:, G["iface_id"] // 2] = np.arange(topo.max_ifaces)
+    U64[:, (L_["priv"] + L_["priv_iface"]) // 8] = ifobj.ctypes.data + 64 * m["iface"].astype(np.uint64)
+    ptrs = (mem.ctypes.data + np.arange(n, dtype=np.uint64) * 256).astype(np.uint64)
+    lay = Layout(**L_, **G, n_ifaces=0, n_nh=0, ifaces=None, nh=None)
+    L = fastpath.lib
+    abi.check("gr_hip_host_register", L.gr_hip_host_register(fastpath.h, bufs.ctypes.data, bufs.nbytes))
+    q = fastpath.queue()
+    try:
+        fastpath.tune("node_ptrs", 1)  # frames by address: the kernel rewrites them over PCIe
+        assert L.gr_hip_node_append_mbufs(q._h, ptrs.ctypes.data, n, ctypes.addressof(lay), 256) >= n
+        abi.check("gr_hip_node_send", L.gr_hip_node_send(q._h, None, n, 256))
+        assert L.gr_hip_node_finish(q._h, None, None, None) == -22  # -EINVAL: not handed back ...
+        after = bufs[:, :abi.LINE].copy()  # ... but the GPU is done with the frames
+        assert q.node_pending()[0] == 0
+    finally:
+        fastpath.tune("node_ptrs", 0)
+        q.close()
+        abi.check("gr_hip_host_unregister", L.gr_hip_host_unregister(fastpath.h, bufs.ctypes.data))
+    fwd = v["edge"] == abi.EDGE["port_output"]
+    assert fwd.all()
+    assert not np.array_equal(after, orig)
+    assert np.array_equal(after, lines)

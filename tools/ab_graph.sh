@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B prebuilt builds of one library on one box, through
 # tools/node_graph_rate.py (ARGS: its options): LIB=graph (default) swaps
-# libgrout_graph.so (the grout node + walk harness), LIB=hip libgrout_hip.so,
+# tests/standin/libgrout_standin.so (the walk harness + the module library), LIB=hip libgrout_hip.so,
 # with build/ab/<LIB>_<name>.so for each name in LIBS (default "old new"),
 # alternating processes.
 cd "$(dirname "$0")/.."

@@ -35,7 +35,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = "/root/reference"
 
 SCAN = [
-    "include", "grout_amd/csrc", "grout_amd/graph", "grout_amd", "oracle", "tests", "bench.py",
+    "include", "grout_amd/csrc", "grout_amd/module", "tests/standin", "grout_amd", "oracle", "tests", "bench.py",
     "DESIGN.md", "INTEGRATION.md", "__graft_entry__.py",
 ]
 EXT = (".c", ".h", ".cpp", ".hip", ".py", ".md")
