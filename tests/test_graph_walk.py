@@ -917,7 +917,7 @@ def test_graph_reload_mid_stream(mode):
             assert L.gpu_fwd4_set_drain_bound(0) == 0
         r = _reload(walks, drain)
         assert L.gpu_fwd4_set_drain_bound(-1) == 0
-        assert r["held"] == walks * BURST - BATCH and r["in_flight"] == 1, r
+        assert r["held"] == walks * BURST - BATCH and r["in_flight"] <= 1, r  # the sent batch may be back already
         if drain:
             assert r["fini_freed"] == 0 and r["held_after"] == 0 and r["in_flight_after"] == 0, r
             assert r["readers_online"] == 0, r  # the drain released the batches' QSBR readers
