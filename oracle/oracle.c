@@ -1338,6 +1338,50 @@ int or_process(
 	return or_process_ex(t, in_frames, in_stride, meta, n, out_lines, out_stride, v, stats, flags, NULL, NULL);
 }
 
+// One graph walk over frames in place (test measurement: the walk harness's
+// "chain" node, tests/standin/walk_harness.c, runs grout's CPU chain on its
+// own mbufs for the like-for-like comparison with the GPU node). mb[i].buf
+// is set so that MTOD is frames[i]: the chain reads and rewrites each frame
+// where it lies, as grout's nodes rewrite an mbuf's data. mo[i]: the mbuf
+// state at the packet's edge (data_off relative to 128, as or_process_ex).
+int or_walk_frames(
+	const or_topo_t *t,
+	uint8_t *const *frames,
+	uint32_t readable,
+	const struct gr_hip_pkt_meta *meta,
+	uint16_t n,
+	struct gr_hip_mbuf *mo
+) {
+	if (n > OR_BURST_MAX || (n && (frames == NULL || meta == NULL || mo == NULL)))
+		return -EINVAL;
+	struct or_graph g = {.t = t, .flags = 0, .readable = readable};
+	struct or_mbuf mb[OR_BURST_MAX];
+	struct or_mbuf *objs[OR_BURST_MAX];
+	for (uint16_t i = 0; i < n; i++) {
+		const struct gr_hip_pkt_meta *md = &meta[i];
+		mb[i].buf = frames[i] - OR_HEADROOM;
+		rx_fill(&mb[i], frames[i], 0, md);
+		objs[i] = &mb[i];
+	}
+	graph_walk(&g, objs, n);
+	for (uint16_t i = 0; i < n; i++) {
+		const struct or_mbuf *m = &mb[i];
+		const struct gr_hip_pkt_meta *md = &meta[i];
+		const bool punt = m->edge == GR_HIP_E_PUNT;
+		struct gr_hip_mbuf *b = &mo[i];
+		b->pkt_len = punt ? md->pkt_len : m->pkt_len;
+		b->data_len = (uint16_t)(punt ? md->pkt_len : m->data_len);
+		b->data_off = (uint16_t)(punt ? OR_HEADROOM : m->data_off);
+		b->packet_type = punt ? 0 : m->packet_type;
+		b->iface = punt ? md->iface : m->iface;
+		b->vlan_id = punt ? (md->vlan_ck & 0xfff) : m->vlan_id;
+		b->edge = m->edge;
+		b->domain = punt ? 0 : m->domain;
+		b->nh = punt ? 0 : m->l3_nh;
+	}
+	return 0;
+}
+
 int or_process_ex(
 	or_topo_t *t,
 	const void *in_frames,

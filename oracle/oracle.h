@@ -118,6 +118,14 @@ int or_process_ex(
 	struct gr_hip_node_stats *ns
 );
 
+// One graph walk of the chain over n <= 256 packets whose frames lie in
+// place (frames[i]: the Ethernet header, `readable` bytes), rewritten there
+// as grout's nodes rewrite an mbuf's data. mo[i]: the mbuf state at the
+// packet's edge (fields as or_process_ex; frame untouched). For the walk
+// harness's CPU chain node (tests/standin/walk_harness.c). 0 or -EINVAL.
+int or_walk_frames(const or_topo_t *, uint8_t *const *frames, uint32_t readable, const struct gr_hip_pkt_meta *meta,
+		   uint16_t n, struct gr_hip_mbuf *mo);
+
 // CPU baseline: `threads` pthreads, one per core, pinned.
 // Worker i starts at packet i * n / threads of the sample and walks it in
 // bursts of 64, wrapping. Each first makes its own copy of the IPv4 FIBs on

@@ -37,7 +37,7 @@
 #define GH_PRIV 64
 #define GH_ROOM 2048
 #define GH_MBUF_SZ (sizeof(struct rte_mbuf) + GH_PRIV + GH_ROOM)
-#define GH_MAX_GRAPHS 16
+#define GH_MAX_GRAPHS 40
 #define GH_MAX_RECORDERS 128
 
 struct gh_mbuf_out { // per injected mbuf, in injection order
@@ -88,12 +88,15 @@ static struct {
 		// rx_next .. rx_end count the passes over its share rx_start + [0, share)
 		uint32_t *free_mb, n_free;
 		uint32_t rx_start, share;
+		// latency mode: the worker's histogram of TSC cycles from port_rx to a recorder
+		uint64_t *lat;
 	} graphs[GH_MAX_GRAPHS];
 	const uint8_t *frames_in; // gh_load's stream (recycle mode refills the mbufs from it)
 	uint32_t stride_in;
 	uint32_t recycle; // workers mode: mbufs per worker's pool (0: every packet its own mbuf)
 	uint32_t passes; // recycle mode: times each worker goes over its share of the stream
 	int workers; // gh_workers_run is walking every graph from its own thread
+	uint32_t wk0; // gh_workers_run's worker k walks graph slot wk0 + k
 	int lcores[GH_MAX_GRAPHS], n_lcores; // workers mode: worker k pinned to lcores[k] (k < n_lcores)
 	uint32_t loop; // walks since the last housekeeping tick (main_loop.c:461)
 	uint8_t *if_dead, *nh_dead; // objects the RCU test's control thread freed
@@ -150,6 +153,15 @@ void gh_set_recycle(uint32_t pool, uint32_t passes) {
 	H.passes = passes ? passes : 1;
 }
 
+// Workers mode: worker k walks graph slot slot0 + k (e.g. the chain graphs
+// created after the GPU node's).
+int gh_workers_first(uint32_t slot0) {
+	if (slot0 >= GH_MAX_GRAPHS)
+		return -EINVAL;
+	H.wk0 = slot0;
+	return 0;
+}
+
 // Workers mode: worker k pinned to cpus[k], as grout pins each worker to its
 // lcore. n 0: the scheduler places them.
 int gh_set_lcores(const int *cpus, int n) {
@@ -164,11 +176,47 @@ int gh_set_lcores(const int *cpus, int n) {
 	return 0;
 }
 
+// ---- latency: each packet's time from port_rx to the recorder behind its edge
+// Workers mode with gh_set_latency(1): port_rx stamps every mbuf of a burst
+// with one TSC read (in the mbuf's second cache line, where DPDK keeps its
+// dynamic fields, e.g. the RX timestamp), the recorders read the TSC once per
+// call and count each packet's cycles in the worker's log histogram:
+// GH_LAT_SUB buckets per power of two. Off by default: the throughput runs
+// pay none of it.
+#define GH_LAT_SUB 16
+#define GH_LAT_BUCKETS (64 * GH_LAT_SUB)
+static int lat_on;
+static double tsc_per_ns; // measured over the last gh_workers_run
+
+static inline uint64_t tsc(void) {
+	return __builtin_ia32_rdtsc();
+}
+
+static inline unsigned lat_bucket(uint64_t d) {
+	if (d < GH_LAT_SUB)
+		return (unsigned)d;
+	const unsigned e = 63u - (unsigned)__builtin_clzll(d); // >= 4
+	return e * GH_LAT_SUB + (unsigned)((d >> (e - 4)) & (GH_LAT_SUB - 1));
+}
+
+void gh_set_latency(int on) {
+	lat_on = on;
+}
+
+// The bucket's lower edge, in cycles (for the test's percentiles).
+uint64_t gh_lat_bucket_floor(uint32_t b) {
+	if (b < GH_LAT_SUB)
+		return b;
+	const unsigned e = b / GH_LAT_SUB, f = b % GH_LAT_SUB;
+	return (1ull << e) | ((uint64_t)f << (e - 4));
+}
+
 static uint16_t port_rx_process(struct rte_graph *graph, struct rte_node *node, void **objs, uint16_t nb) {
 	(void)objs;
 	(void)nb;
 	uint32_t k = 0;
 	void *burst[RTE_GRAPH_BURST_SIZE];
+	const uint64_t stamp = lat_on ? tsc() : 0;
 	// workers mode: each graph polls its own part of the mbufs (its RX queue)
 	uint32_t *next = &H.next_rx, end = H.n;
 	if (H.workers && node->ctx[0] != 0) {
@@ -197,6 +245,8 @@ static uint16_t port_rx_process(struct rte_graph *graph, struct rte_node *node, 
 			struct iface_mbuf_data *d = iface_mbuf_data(m);
 			d->iface = iface_from_id(pm->iface);
 			d->vlan_id = pm->vlan_ck & 0xfff;
+			if (lat_on)
+				m->_rest[0] = stamp;
 			burst[k++] = m;
 		}
 		rte_node_enqueue(graph, node, null_node ? 1 : 0, burst, (uint16_t)k);
@@ -215,6 +265,8 @@ static uint16_t port_rx_process(struct rte_graph *graph, struct rte_node *node, 
 		}
 		d->iface = iface_from_id(pm->iface);
 		d->vlan_id = pm->vlan_ck & 0xfff;
+		if (lat_on)
+			m->_rest[0] = stamp;
 		burst[k++] = m;
 	}
 	rte_node_enqueue(graph, node, null_node ? 1 : 0, burst, (uint16_t)k);
@@ -239,6 +291,98 @@ static struct rte_node_register port_rx_node = {
 	.next_nodes = {"iface_input", "port_output"},
 };
 
+// ---- grout's CPU chain in the same harness (like-for-like measurement) -----
+// A "chain" graph (gh_graph_create_chain) is the GPU node's worker graph with
+// grout's own node chain in its place: port_rx_chain (port_rx's code, the same
+// mempools, lcores and recorders) hands its bursts to cpu_chain, which runs
+// the oracle's restatement of grout's nodes iface_input .. iface_output
+// (or_walk_frames, reached through the pointer gh_set_chain is given: this
+// library links nothing of the oracle) on the mbufs in place, writes grout's
+// mbuf fields and private data for each packet's edge as grout's nodes leave
+// them, and enqueues runs of one edge on the same edges as the GPU node.
+// Test infrastructure only (tests/perf_node_chain.py).
+typedef int (*gh_chain_fn)(const void *topo, uint8_t *const *frames, uint32_t readable,
+			   const struct gr_hip_pkt_meta *meta, uint16_t n, struct gr_hip_mbuf *mo);
+static gh_chain_fn chain_fn;
+static const void *chain_topo;
+
+void gh_set_chain(void *fn, const void *topo) {
+	chain_fn = (gh_chain_fn)fn;
+	chain_topo = topo;
+}
+
+#pragma GCC diagnostic push
+#pragma GCC diagnostic ignored "-Wmaybe-uninitialized" // frames / meta: filled for every i < nb
+static uint16_t cpu_chain_process(struct rte_graph *graph, struct rte_node *node, void **objs, uint16_t nb) {
+	uint8_t *frames[RTE_GRAPH_BURST_SIZE];
+	struct gr_hip_pkt_meta meta[RTE_GRAPH_BURST_SIZE];
+	struct gr_hip_mbuf mo[RTE_GRAPH_BURST_SIZE];
+	uint8_t edge[RTE_GRAPH_BURST_SIZE];
+	if (nb == 0)
+		return 0;
+	if (chain_fn == NULL) {
+		rte_node_enqueue(graph, node, GR_HIP_E_PUNT, objs, nb);
+		return nb;
+	}
+	for (uint16_t i = 0; i < nb; i++) { // what grout's nodes read of each mbuf
+		struct rte_mbuf *m = objs[i];
+		const struct iface_mbuf_data *d = iface_mbuf_data(m);
+		const uint64_t ck = m->ol_flags & RTE_MBUF_F_RX_IP_CKSUM_MASK;
+		frames[i] = rte_pktmbuf_mtod(m, uint8_t *);
+		meta[i].iface = d->iface != NULL ? d->iface->id : 0;
+		meta[i].pkt_len = (uint16_t)m->pkt_len;
+		meta[i].rss = m->hash.rss;
+		meta[i].vlan_ck = (uint16_t)((d->vlan_id & 0xfff)
+			| ((ck == RTE_MBUF_F_RX_IP_CKSUM_GOOD ? GR_HIP_CKSUM_GOOD
+			    : ck == RTE_MBUF_F_RX_IP_CKSUM_BAD ? GR_HIP_CKSUM_BAD : GR_HIP_CKSUM_UNKNOWN) << 12));
+	}
+	chain_fn(chain_topo, frames, GH_ROOM - RTE_PKTMBUF_HEADROOM, meta, nb, mo);
+	for (uint16_t i = 0; i < nb; i++) { // grout's mbuf fields and private data at the edge
+		struct rte_mbuf *m = objs[i];
+		const struct gr_hip_mbuf *o = &mo[i];
+		edge[i] = o->edge;
+		if (o->edge == GR_HIP_E_PUNT)
+			continue;
+		m->data_off = (uint16_t)(m->data_off + o->data_off - RTE_PKTMBUF_HEADROOM);
+		m->data_len = o->data_len;
+		m->pkt_len = o->pkt_len;
+		m->packet_type = o->packet_type;
+		struct iface_mbuf_data *d = iface_mbuf_data(m);
+		d->iface = iface_from_id(o->iface);
+		if (o->edge == GR_HIP_E_PORT_OUTPUT)
+			d->vlan_id = o->vlan_id; // iface_output's, for port_tx
+		else if (o->nh != 0)
+			l3_mbuf_data(m)->nh = o->nh <= H.max_nh ? &H.nhs[o->nh] : NULL;
+		else
+			eth_input_mbuf_data(m)->domain = o->domain;
+	}
+	for (uint16_t i = 1, run = 0; i <= nb; i++) {
+		if (i == nb || edge[i] != edge[run]) {
+			rte_node_enqueue(graph, node, edge[run], &objs[run], (uint16_t)(i - run));
+			run = i;
+		}
+	}
+	return nb;
+}
+
+#pragma GCC diagnostic pop
+
+static struct rte_node_register cpu_chain_node = {
+	.name = "cpu_chain",
+	.process = cpu_chain_process,
+	.nb_edges = GR_HIP_E_COUNT,
+	.next_nodes = {GPU_FWD4_EDGES},
+};
+
+static struct rte_node_register port_rx_chain_node = {
+	.name = "port_rx_chain",
+	.flags = RTE_NODE_SOURCE_F,
+	.init = graph_slot_init,
+	.process = port_rx_process,
+	.nb_edges = 2,
+	.next_nodes = {"cpu_chain", "port_output"},
+};
+
 // a recorder's ctx holds its recorder id
 static uint16_t recorder_process(struct rte_graph *graph, struct rte_node *node, void **objs, uint16_t nb) {
 	(void)graph;
@@ -247,6 +391,11 @@ static uint16_t recorder_process(struct rte_graph *graph, struct rte_node *node,
 		if (node->ctx[1] != 0) {
 			__typeof__(&H.graphs[0]) G = &H.graphs[node->ctx[1] - 1];
 			G->recorded += nb;
+			if (lat_on && G->lat != NULL) {
+				const uint64_t now = tsc();
+				for (uint16_t k = 0; k < nb; k++)
+					G->lat[lat_bucket(now - ((struct rte_mbuf *)objs[k])->_rest[0])]++;
+			}
 			if (H.recycle) // back to the worker's mempool (port_tx's completion, a drop node's free)
 				for (uint16_t k = 0; k < nb; k++)
 					G->free_mb[G->n_free++] = (uint32_t)(((uint8_t *)objs[k] - H.mem) / GH_MBUF_SZ);
@@ -354,6 +503,10 @@ int gh_register(void) {
 	int r;
 	if ((r = gr_nodes_register()) < 0 || (r = register_recorders()) < 0)
 		return r;
+	// the chain graphs' nodes (after the recorders: cpu_chain's edges are theirs)
+	if (__rte_node_register(&cpu_chain_node) == RTE_NODE_ID_INVALID
+	    || __rte_node_register(&port_rx_chain_node) == RTE_NODE_ID_INVALID)
+		return -EEXIST;
 	for (unsigned k = 0; k < N_REPLACED; k++)
 		if ((r = add_recorder(replaced[k])) < 0)
 			return r;
@@ -482,9 +635,19 @@ void gh_policy_clear(void) {
 // after the worker's CPU like grout's ("gr-%04x", (cpu << 1) | index) and
 // created on `socket`. It becomes the current graph.
 static int graph_create(unsigned cpu, unsigned index, int socket);
+static int graph_chain; // the next graph_create makes a chain graph
 
 int gh_graph_create(unsigned cpu, int socket) {
 	return graph_create(cpu, 0, socket);
+}
+
+// A worker graph with grout's CPU chain in place of the GPU node (see
+// cpu_chain above); the other index of the worker's names.
+int gh_graph_create_chain(unsigned cpu, int socket) {
+	graph_chain = 1;
+	const int k = graph_create(cpu, 1, socket);
+	graph_chain = 0;
+	return k;
 }
 
 // grout names a worker's graphs "gr-%04x" with (cpu << 1) | index, the index
@@ -497,7 +660,8 @@ static int graph_create(unsigned cpu, unsigned index, int socket) {
 		return -ENOSPC;
 	char name[RTE_GRAPH_NAMESIZE];
 	snprintf(name, sizeof(name), "gr-%04x", ((cpu << 1) | (index & 1)) & 0xffff);
-	const char *patterns[2 + N_REPLACED] = {"port_rx", "gpu_fwd4_flush"};
+	const char *patterns[2 + N_REPLACED] = {graph_chain ? "port_rx_chain" : "port_rx",
+						graph_chain ? "cpu_chain" : "gpu_fwd4_flush"};
 	for (unsigned i = 0; i < N_REPLACED; i++)
 		patterns[2 + i] = replaced[i];
 	struct rte_graph_param prm = {
@@ -1255,10 +1419,10 @@ static void *worker_thread(void *p) {
 // the recorders behind (which only count in this mode). Returns 0 and the
 // wall time from the start barrier to the last worker's end, or -errno.
 int gh_workers_run(uint32_t threads, double *seconds, uint64_t *walks) {
-	if (threads == 0 || threads > GH_MAX_GRAPHS || H.n == 0)
+	if (threads == 0 || H.wk0 + threads > GH_MAX_GRAPHS || H.n == 0)
 		return -EINVAL;
 	for (uint32_t k = 0; k < threads; k++)
-		if (H.graphs[k].graph == NULL)
+		if (H.graphs[H.wk0 + k].graph == NULL)
 			return -ENOENT;
 	pthread_t th[GH_MAX_GRAPHS];
 	struct gh_workers_arg args[GH_MAX_GRAPHS];
@@ -1266,29 +1430,33 @@ int gh_workers_run(uint32_t threads, double *seconds, uint64_t *walks) {
 		return -EINVAL; // the pools are carved out of the loaded mbufs
 	pthread_barrier_t bar;
 	for (uint32_t k = 0; k < threads; k++) {
-		H.graphs[k].rx_next = (uint32_t)((uint64_t)H.n * k / threads);
-		H.graphs[k].rx_end = (uint32_t)((uint64_t)H.n * (k + 1) / threads);
-		H.graphs[k].recorded = 0;
+		H.graphs[H.wk0 + k].rx_next = (uint32_t)((uint64_t)H.n * k / threads);
+		H.graphs[H.wk0 + k].rx_end = (uint32_t)((uint64_t)H.n * (k + 1) / threads);
+		H.graphs[H.wk0 + k].recorded = 0;
 		if (H.recycle) {
-			H.graphs[k].free_mb = malloc(H.recycle * sizeof(uint32_t));
-			if (H.graphs[k].free_mb == NULL) {
+			H.graphs[H.wk0 + k].free_mb = malloc(H.recycle * sizeof(uint32_t));
+			if (H.graphs[H.wk0 + k].free_mb == NULL) {
 				for (uint32_t j = 0; j < k; j++) {
-					free(H.graphs[j].free_mb);
-					H.graphs[j].free_mb = NULL;
+					free(H.graphs[H.wk0 + j].free_mb);
+					H.graphs[H.wk0 + j].free_mb = NULL;
 				}
 				return -ENOMEM;
 			}
 			for (uint32_t j = 0; j < H.recycle; j++) // popped from the top: lowest index first
-				H.graphs[k].free_mb[j] = k * H.recycle + (H.recycle - 1 - j);
-			H.graphs[k].n_free = H.recycle;
-			H.graphs[k].rx_start = H.graphs[k].rx_next;
-			H.graphs[k].share = H.graphs[k].rx_end - H.graphs[k].rx_next;
-			H.graphs[k].rx_end = H.graphs[k].rx_next + H.graphs[k].share * H.passes;
+				H.graphs[H.wk0 + k].free_mb[j] = k * H.recycle + (H.recycle - 1 - j);
+			H.graphs[H.wk0 + k].n_free = H.recycle;
+			H.graphs[H.wk0 + k].rx_start = H.graphs[H.wk0 + k].rx_next;
+			H.graphs[H.wk0 + k].share = H.graphs[H.wk0 + k].rx_end - H.graphs[H.wk0 + k].rx_next;
+			H.graphs[H.wk0 + k].rx_end = H.graphs[H.wk0 + k].rx_next + H.graphs[H.wk0 + k].share * H.passes;
 		}
-		args[k] = (struct gh_workers_arg) {.k = (int)k, .cpu = -1, .bar = &bar};
+		args[k] = (struct gh_workers_arg) {.k = (int)(H.wk0 + k), .cpu = -1, .bar = &bar};
 	}
 	for (uint32_t k = 0; k < threads && (int)k < H.n_lcores; k++)
 		args[k].cpu = H.lcores[k];
+	for (uint32_t k = 0; k < threads; k++) {
+		free(H.graphs[H.wk0 + k].lat);
+		H.graphs[H.wk0 + k].lat = lat_on ? calloc(GH_LAT_BUCKETS, sizeof(uint64_t)) : NULL;
+	}
 	pthread_barrier_init(&bar, NULL, threads + 1);
 	H.workers = 1;
 	for (uint32_t k = 0; k < threads; k++)
@@ -1296,7 +1464,9 @@ int gh_workers_run(uint32_t threads, double *seconds, uint64_t *walks) {
 	struct timespec a, b;
 	pthread_barrier_wait(&bar);
 	clock_gettime(CLOCK_MONOTONIC, &a);
+	const uint64_t tsc_a = tsc();
 	pthread_barrier_wait(&bar);
+	const uint64_t tsc_b = tsc();
 	clock_gettime(CLOCK_MONOTONIC, &b);
 	int err = 0;
 	uint64_t w = 0;
@@ -1309,12 +1479,29 @@ int gh_workers_run(uint32_t threads, double *seconds, uint64_t *walks) {
 	H.workers = 0;
 	pthread_barrier_destroy(&bar);
 	for (uint32_t k = 0; k < threads; k++) {
-		free(H.graphs[k].free_mb);
-		H.graphs[k].free_mb = NULL;
-		H.graphs[k].n_free = 0;
+		free(H.graphs[H.wk0 + k].free_mb);
+		H.graphs[H.wk0 + k].free_mb = NULL;
+		H.graphs[H.wk0 + k].n_free = 0;
 	}
 	*seconds = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+	if (*seconds > 0)
+		tsc_per_ns = (double)(tsc_b - tsc_a) / (*seconds * 1e9);
 	if (walks != NULL)
 		*walks = w;
 	return err;
+}
+
+// Latency mode: the last gh_workers_run's histogram, summed over its workers
+// (GH_LAT_BUCKETS counts of TSC cycles, gh_lat_bucket_floor gives each
+// bucket's lower edge), and the TSC's rate over that run (cycles per ns).
+int gh_latency(uint64_t *hist, uint32_t n, double *cycles_per_ns) {
+	if (hist == NULL || n < GH_LAT_BUCKETS)
+		return -EINVAL;
+	memset(hist, 0, GH_LAT_BUCKETS * sizeof(uint64_t));
+	for (int k = 0; k < GH_MAX_GRAPHS; k++)
+		for (uint32_t b = 0; H.graphs[k].lat != NULL && b < GH_LAT_BUCKETS; b++)
+			hist[b] += H.graphs[k].lat[b];
+	if (cycles_per_ns != NULL)
+		*cycles_per_ns = tsc_per_ns;
+	return GH_LAT_BUCKETS;
 }

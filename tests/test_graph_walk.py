@@ -993,3 +993,19 @@ def test_graph_walk_append_failure_punts_one_walk():
     assert (got["edge"][~punt] == abi.EDGE["port_output"]).all()  # vlan_id: what port_output reads
     for f in ("edge", "pkt_len", "data_len", "data_off", "iface", "vlan_id"):
         assert np.array_equal(got[f][~punt], want[f][~punt]), f
+
+
+def test_chain_graph_matches_oracle():
+    """The like-for-like measurement's CPU side (tests/perf_node_chain.py):
+    a worker graph with grout's CPU chain in the GPU node's place (the
+    harness's cpu_chain node over the oracle's or_walk_frames) leaves every
+    mbuf of the exception corpus and of a full-view stream -- edge, lengths,
+    data_off, packet_type, egress iface, frame bytes -- as the oracle's
+    mbuf-level chain does. Run in a process of its own: it initialises the
+    harness without a GPU."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "perf_node_chain.py"), "--check"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert '"check": "ok"' in r.stdout
