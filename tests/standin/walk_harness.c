@@ -1453,10 +1453,12 @@ int gh_workers_run(uint32_t threads, double *seconds, uint64_t *walks) {
 	}
 	for (uint32_t k = 0; k < threads && (int)k < H.n_lcores; k++)
 		args[k].cpu = H.lcores[k];
-	for (uint32_t k = 0; k < threads; k++) {
-		free(H.graphs[H.wk0 + k].lat);
-		H.graphs[H.wk0 + k].lat = lat_on ? calloc(GH_LAT_BUCKETS, sizeof(uint64_t)) : NULL;
+	for (int g = 0; g < GH_MAX_GRAPHS; g++) { // this run's histograms only
+		free(H.graphs[g].lat);
+		H.graphs[g].lat = NULL;
 	}
+	for (uint32_t k = 0; k < threads && lat_on; k++)
+		H.graphs[H.wk0 + k].lat = calloc(GH_LAT_BUCKETS, sizeof(uint64_t));
 	pthread_barrier_init(&bar, NULL, threads + 1);
 	H.workers = 1;
 	for (uint32_t k = 0; k < threads; k++)
