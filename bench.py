@@ -486,34 +486,43 @@ def main():
     # (SURVEY.md §8d): pinned workers on one shared FIB (grout's layout: one
     # rte_fib per VRF for every worker), each starting at its own offset of
     # the sample, each warmed up by one untimed pass over the whole sample
-    # before the timed part; beside it the same with a FIB copy per worker on
-    # THP (slower on the boxes measured: 16 tables of 128 MiB leave L3)
+    # before the timed part. The single-core leg is the 16-core leg's worker 0
+    # alone: same CPU, offset, warm-up, shared FIB and packet count, in the
+    # same call; beside them the 16 workers with a FIB copy each on THP
+    # (slower on the boxes measured: 16 tables of 128 MiB leave L3)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import oracle
         o = oracle.Oracle(topo)
         cf, cm = frames[: 1 << 20].copy(), meta[: 1 << 20].copy()
-        m0, _ = o.bench(cf, cm, 1, 1 << 20)  # calibration, sizes the timed parts
-        single_s = min(2.0, args.cpu_seconds / 3)
-        m1, _ = o.bench(cf, cm, 1, max(1 << 20, int(m0 * 1e6 * single_s)))
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        per_thread = max(1 << 20, int(m1 * 1e6 * args.cpu_seconds))
-        mS, _ = o.bench(cf, cm, threads, per_thread, fib_copy=False)
-        mN, _ = o.bench(cf, cm, threads, per_thread)
+        allowed = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
+        cpus = allowed[:threads] if len(allowed) >= threads else None  # worker i on the i-th allowed CPU
+        m0, _ = o.bench(cf, cm, 1, 1 << 20, fib_copy=False, cpus=cpus[:1] if cpus else None)  # sizes the timed parts
+        per_thread = max(1 << 20, int(m0 * 1e6 * args.cpu_seconds))
+        m1, _ = o.bench(cf, cm, 1, per_thread, fib_copy=False, cpus=cpus[:1] if cpus else None)
+        mS, _ = o.bench(cf, cm, threads, per_thread, fib_copy=False, cpus=cpus)
+        m1b, _ = o.bench(cf, cm, 1, per_thread, fib_copy=False, cpus=cpus[:1] if cpus else None)  # after, same CPU
+        mN, _ = o.bench(cf, cm, threads, per_thread, cpus=cpus)
+        single = (m1 + m1b) / 2
         result["cpu_baseline"] = {
             "value": round(mS, 2),
             "unit": "Mpps",
             "cores": threads,
             "kind": "port",
-            "single_core_mpps": round(m1, 2),
+            "single_core_mpps": round(single, 2),
+            "single_core_mpps_before_after": [round(m1, 2), round(m1b, 2)],
             "per_core_mpps": round(mS / threads, 2),
+            "per_core_over_single": round(mS / threads / single, 3),
             "fib_copy_mpps": round(mN, 2),
+            "cpus": cpus,
             "host_cpus": host_cpus(),
             "sample": (f"oracle C restatement of grout's node chain (bursts of 64, "
                        f"{'per-length prefix hash LPM6' if args.workload == 'fullview6' else 'DIR24_8 8-byte entries'}), "
                        f"{threads} pinned threads on one shared FIB (grout's layout: one rte_fib per VRF), "
                        f"each starting at its own offset of the same 1M-packet prefix of this stream, warmed up "
-                       f"by one pass over it, then {per_thread} packets each timed; fib_copy_mpps: the same with "
-                       f"a FIB copy per thread on THP"),
+                       f"by one pass over it, then {per_thread} packets each timed; single_core_mpps: worker 0 "
+                       f"alone (same CPU, offset, warm-up, shared FIB, packets), before and after the "
+                       f"{threads}-core leg; fib_copy_mpps: the {threads} workers with a FIB copy each on THP"),
         }
         o.close()
 

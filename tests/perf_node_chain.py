@@ -118,6 +118,9 @@ def main():
     ap.add_argument("--threads", default="1,8,16")
     ap.add_argument("--per-thread", type=int, default=1 << 18, help="mbufs loaded per worker")
     ap.add_argument("--batch", type=int, default=15360)
+    ap.add_argument("--batches", default=None,
+                    help="GPU node batch sizes to sweep at each K (gpu_fwd4_set_batch), e.g. 1024,4096,15360; "
+                         "the chain and the harness alone are measured once per K")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--recycle", type=int, default=65536, help="mbufs per worker's pool (0: one per packet)")
     ap.add_argument("--passes", type=int, default=8, help="with --recycle: passes over each worker's share")
@@ -211,7 +214,10 @@ def main():
             L.gh_workers_first(0)
 
     out = open(args.out, "a") if args.out else None
-    for k in threads:
+    L.gpu_fwd4_set_batch.argtypes = [ctypes.c_uint32, ctypes.c_uint64]
+    batches = [int(x) for x in args.batches.split(",")] if args.batches else [args.batch]
+    for k, batch in [(k, b) for k in threads for b in batches]:
+        assert L.gpu_fwd4_set_batch(batch, 20_000_000) == 0
         cpus = place(k)
         m = k * args.per_thread
         pk = m * per
@@ -228,7 +234,7 @@ def main():
             assert int(hist.sum()) == pk, (mode, int(hist.sum()), pk)
             lat[mode] = percentiles(hist.astype(np.float64), cpn, floor)
         line = {"threads": k, "packets": pk, "lcores": args.lcores, "cpus": cpus, "recycle": args.recycle,
-                "passes": per, "batch": args.batch, "reps": args.reps,
+                "passes": per, "batch": batch, "reps": args.reps,
                 "workload": "config3 full view (fib_inject 1M routes), 64 B, seeded stream 0x67720002"}
         for mode in ("gpu", "chain"):
             line[mode] = {"mpps": round(pk / med[mode] / 1e6, 1),
