@@ -323,6 +323,22 @@ def main():
         except (OSError, ValueError, AttributeError):
             traffic, traffic_src = None, None
 
+    # the same measurement on gr_hip_batch_alloc's buffers without placement
+    # (physically contiguous allocations, "alloc_contig"): what a deployment
+    # gets with no timing at start-up, in the same run
+    contig = None
+    if batch is not None and not args.no_plain:
+        cb = fp.batch_alloc(n, in_stride)
+        h2d(cb.in_frames, frames)
+        h2d(cb.meta, meta)
+        torch.cuda.synchronize()
+        ct, cms, ccnt = measure((cb.in_frames, cb.out_lines, cb.meta, cb.verdicts), args.steps, args.warmup)
+        contig = {"value": round(rep.aggregate_mpps(n, args.steps, ct), 1),
+                  "ms_per_step": round(ct / args.steps * 1e3, 4),
+                  "kernel_ms_avg": round(cms / max(ccnt, 1), 4),
+                  "note": "gr_hip_batch_alloc buffers (physically contiguous), no placement timing"}
+        fp.batch_free(cb)
+
     # the same measurement on plain torch allocations of the same stream:
     # the placement's share of `value`, in the same run
     plain = None
@@ -400,8 +416,9 @@ def main():
             "forwarded_frac": round(fwd_frac, 6),
             **({"tune": {k: int(v) for k, v in tune.items()}} if tune else {}),
             "occupancy_wg_per_cu": fp.tune("occupancy"),
-            "placement": (f"calibrated: output lines, then frames = fastest of {args.candidates + 1} allocations each, "
-                          "timed over a batch of this workload drawn with another seed (gr_hip_batch_place)"
+            "placement": (f"calibrated: output lines, then frames = fastest of {args.candidates + 1} physically "
+                          "contiguous allocations each (gr_hip_batch_alloc), timed over a batch of this workload drawn "
+                          "with another seed (gr_hip_batch_place)"
                           if batch is not None else "plain torch allocations"),
             "output": ("packed 32-byte header prefixes (every byte the path changes; GR_HIP_BATCH_F_PREFIX32)"
                        if prefix32 else "whole 64-byte header lines"),
@@ -434,6 +451,11 @@ def main():
             result["roofline"]["frac_plain"] = round(n * B_PKT / (plain["kernel_ms_avg"] / 1e3) / 1e9 / HBM_PEAK_GBS,
                                                      4)
         result["roofline"]["kernel_ms_avg_plain"] = plain["kernel_ms_avg"]
+    if contig is not None:
+        result["contiguous_unplaced"] = contig
+        if contig["kernel_ms_avg"]:
+            result["roofline"]["frac_contiguous_unplaced"] = round(
+                n * B_PKT / (contig["kernel_ms_avg"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
     if world > 1:
         result["ranks"] = ranks
     if pfx_leg is not None:

@@ -280,6 +280,7 @@ struct gr_hip_ctx {
 	int host_direct; // host path: the kernel reads / writes pinned host memory itself
 	int node_ptrs; // node path: frames in registered memory are handed over by address
 	int tile_order; // 0: workgroup b takes tiles b, b + G, ...; 1: one contiguous run each
+	int alloc_contig; // large device arrays physically contiguous first (dev_alloc), default 1
 	uint32_t spin_max; // ring waits: polls before giving up (0 = the kernel's default)
 	std::atomic<int> fail_appends{0}; // tests: the next N gr_hip_node_append calls fail (-ENOMEM)
 	int untimed; // measurements: no HIP events around launches (gr_hip_queue_kernel_ms sees none)
@@ -785,6 +786,7 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->spin_max = 0;
 	c->untimed = 0;
 	c->time_every = 1;
+	c->alloc_contig = 1;
 	for (int v = 0; v < 8; v++)
 		c->occ_ring[v] = gr_fwd4_ring_occupancy(v, 0, 0);
 	c->occ_n = 0;
@@ -1347,11 +1349,23 @@ static void stage_groups(stager &st, E *dev, const uint32_t *t8, const std::vect
 	}
 }
 
-#ifdef FIB_ALLOC_FLAGS // measurement builds: FIB arrays from hipExtMallocWithFlags
-#define fib_malloc(p, sz) hipExtMallocWithFlags((void **)(p), (sz), FIB_ALLOC_FLAGS)
-#else
-#define fib_malloc(p, sz) hipMalloc((p), (sz))
-#endif
+// Large device arrays (the FIB tables, batch buffers and their placement
+// candidates) are asked of the driver physically contiguous first
+// (hipDeviceMallocContiguous), which maps them with large fragments: the
+// kernel's streams and gathers then translate fast whatever pages they land
+// on. Plain allocations are placed at random in that respect, and a slow
+// pairing of frames and output lines stalls on address translation (the
+// L1 TLB's in-flight limit: TCP_UTCL1_STALL_INFLIGHT_MAX, DESIGN.md §6
+// "placement"). hipMalloc when the driver cannot (or "alloc_contig" 0).
+static hipError_t dev_alloc(const gr_hip_ctx *c, void **p, size_t sz) {
+	if (c->alloc_contig) {
+		if (hipExtMallocWithFlags(p, sz, hipDeviceMallocContiguous) == hipSuccess)
+			return hipSuccess;
+		(void)hipGetLastError();
+	}
+	return hipMalloc(p, sz);
+}
+#define fib_malloc(p, sz) dev_alloc(c, (void **)(p), (sz))
 
 // Allocate the device arrays copy `b` needs in format `fmt`.
 static int fib4_buf_alloc(gr_hip_ctx *c, fib4_buf &b, int fmt, uint32_t num_tbl8) {
@@ -1360,12 +1374,11 @@ static int fib4_buf_alloc(gr_hip_ctx *c, fib4_buf &b, int fmt, uint32_t num_tbl8
 	if (fmt == FIB_FMT_24_W2 && b.d24_16 == nullptr)
 		HCK(fib_malloc(&b.d24_16, sizeof(uint16_t) * GR_FIB4_TBL24_ENTRIES));
 	if (fmt == FIB_FMT_16_8_8 && b.d16 == nullptr) // top + the worst case of one chunk per /16
-		HCK(hipMalloc(&b.d16, sizeof(uint32_t) * 65536 + sizeof(uint16_t) * 256 * 65536));
+		HCK(fib_malloc(&b.d16, sizeof(uint32_t) * 65536 + sizeof(uint16_t) * 256 * 65536));
 	if (fmt == FIB_FMT_24 && b.d24 == nullptr) {
-		HCK(hipMalloc(&b.d24, sizeof(uint32_t) * GR_FIB4_TBL24_ENTRIES));
-		HCK(hipMalloc(&b.d8, sizeof(uint32_t) * 256 * (size_t)num_tbl8));
+		HCK(fib_malloc(&b.d24, sizeof(uint32_t) * GR_FIB4_TBL24_ENTRIES));
+		HCK(fib_malloc(&b.d8, sizeof(uint32_t) * 256 * (size_t)num_tbl8));
 	}
-	(void)c;
 	return 0;
 }
 
@@ -1725,8 +1738,8 @@ extern "C" int gr_hip_fib6_commit(gr_hip_ctx_t *c, uint16_t vrf) {
 		std::shared_lock<std::shared_mutex> l(c->mu); // submitters go on
 		if (b.d6 == nullptr) { // sized for the VRF's group capacity once: top, group slots, skips
 			const uint32_t cap = gr_fib6_max_groups(v.rib6);
-			HCK(hipMalloc(&b.d6, ((size_t)GR_FIB6_TOP + (size_t)cap * GR_FIB6_GROUP) * sizeof(uint32_t)
-						     + (size_t)cap * sizeof(gr_fib6_skip)));
+			HCK(fib_malloc(&b.d6, ((size_t)GR_FIB6_TOP + (size_t)cap * GR_FIB6_GROUP) * sizeof(uint32_t)
+						      + (size_t)cap * sizeof(gr_fib6_skip)));
 			b.groups = cap;
 		}
 		gr_fib6_skip *d_skips = reinterpret_cast<gr_fib6_skip *>(b.d6 + GR_FIB6_TOP + (size_t)b.groups * GR_FIB6_GROUP);
@@ -2082,6 +2095,8 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < 0)
 			return -EINVAL;
 		c->spin_max = (uint32_t)value;
+	} else if (strcmp(key, "alloc_contig") == 0) { // later allocations only
+		c->alloc_contig = value != 0;
 	} else if (strcmp(key, "tile_order") == 0) {
 		if (value < 0 || value > 2)
 			return -EINVAL;
@@ -2981,7 +2996,7 @@ extern "C" int gr_hip_batch_alloc(gr_hip_ctx_t *c, uint32_t n, uint32_t in_strid
 	const size_t sizes[4] = {(size_t)n * in_stride, (size_t)n * GR_HIP_LINE, (size_t)n * 8, (size_t)n * 8};
 	void *p[4] = {nullptr, nullptr, nullptr, nullptr};
 	for (int k = 0; k < 4; k++)
-		if (hipMalloc(&p[k], sizes[k]) != hipSuccess || hipMemset(p[k], 0, sizes[k]) != hipSuccess) {
+		if (dev_alloc(c, &p[k], sizes[k]) != hipSuccess || hipMemset(p[k], 0, sizes[k]) != hipSuccess) {
 			(void)hipGetLastError();
 			for (void *q : p)
 				if (q)
@@ -3013,11 +3028,11 @@ static int place_time(gr_hip_queue *q, const gr_hip_batch &t, float *ms) {
 
 // Up to `candidates` more device buffers of `bytes` each (fewer when memory
 // runs short), after `cur`.
-static std::vector<void *> place_alloc(void *cur, size_t bytes, uint32_t candidates) {
+static std::vector<void *> place_alloc(const gr_hip_ctx *c, void *cur, size_t bytes, uint32_t candidates) {
 	std::vector<void *> v{cur};
 	for (uint32_t k = 0; k < candidates; k++) {
 		void *o = nullptr;
-		if (hipMalloc(&o, bytes) != hipSuccess) {
+		if (dev_alloc(c, &o, bytes) != hipSuccess) {
 			(void)hipGetLastError();
 			break;
 		}
@@ -3048,7 +3063,7 @@ extern "C" int gr_hip_batch_place(gr_hip_ctx_t *c, gr_hip_batch *b, uint32_t can
 	q->d_stats = nullptr;
 	q->always_timed = true; // "untimed" / "time_every" do not apply to the probes
 	// 1. the output lines: candidates against the current buffer
-	std::vector<void *> outs = place_alloc(b->out_lines, (size_t)b->n * b->out_stride, candidates);
+	std::vector<void *> outs = place_alloc(c, b->out_lines, (size_t)b->n * b->out_stride, candidates);
 	size_t pick = 0;
 	float best = 0;
 	for (size_t k = 0; k < outs.size() && r == 0; k++) {
@@ -3066,7 +3081,7 @@ extern "C" int gr_hip_batch_place(gr_hip_ctx_t *c, gr_hip_batch *b, uint32_t can
 	std::vector<void *> ins{const_cast<void *>(b->in_frames)};
 	size_t pick_in = 0;
 	if (r == 0) {
-		ins = place_alloc(const_cast<void *>(b->in_frames), in_b, candidates);
+		ins = place_alloc(c, const_cast<void *>(b->in_frames), in_b, candidates);
 		for (size_t k = 1; k < ins.size() && r == 0; k++) {
 			if (hipMemcpyAsync(ins[k], b->in_frames, in_b, hipMemcpyDeviceToDevice, q->s) != hipSuccess) {
 				(void)hipGetLastError();

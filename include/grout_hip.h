@@ -479,6 +479,12 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               for tests of the give-up path
 //   "fail_appends" N: the next N gr_hip_node_append calls fail with -ENOMEM
 //               (the slot left as it was): for tests of the node's path
+//   "alloc_contig" 1 = the large device arrays allocated from then on (FIB
+//               tables, gr_hip_batch_alloc's buffers and gr_hip_batch_place's
+//               candidates) are asked for physically contiguous first
+//               (hipDeviceMallocContiguous: large fragments, fast address
+//               translation for the kernel's streams and gathers), hipMalloc
+//               when that fails (default); 0 = hipMalloc always
 //   "tile_order" 0 = workgroup b takes 64-packet tiles b, b + G, b + 2G ...
 //               (default), 1 = one contiguous run of tiles per workgroup
 //   "fib_format_of" (read) the format VRF `value`'s FIB is on the device in
