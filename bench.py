@@ -42,6 +42,16 @@ def host_cpus():
     return out
 
 
+def cgroup_cpu_stat():
+    """The cgroup's CPU accounting (cgroup v2 cpu.stat): with a CPU-time quota
+    (cpu.max), `throttled_usec` grows when the process's threads together
+    exceed it, which slows busy pinned workers whatever their CPUs."""
+    try:
+        return {k: int(v) for k, v in (l.split() for l in open("/sys/fs/cgroup/cpu.stat"))}
+    except (OSError, ValueError):
+        return {}
+
+
 def _cpu_sysfs(cpu, leaf):
     try:
         return open(f"/sys/devices/system/cpu/cpu{cpu}/{leaf}").read().strip()
@@ -522,7 +532,11 @@ def main():
         m0, _ = o.bench(cf, cm, 1, 1 << 20, fib_copy=False, cpus=cpus[:1] if cpus else None)  # sizes the timed parts
         per_thread = max(1 << 20, int(m0 * 1e6 * args.cpu_seconds))
         m1, _ = o.bench(cf, cm, 1, per_thread, fib_copy=False, cpus=cpus[:1] if cpus else None)
+        cs0 = cgroup_cpu_stat()
+        tS = time.perf_counter()
         mS, _ = o.bench(cf, cm, threads, per_thread, fib_copy=False, cpus=cpus)
+        tS = time.perf_counter() - tS
+        cs1 = cgroup_cpu_stat()
         m1b, _ = o.bench(cf, cm, 1, per_thread, fib_copy=False, cpus=cpus[:1] if cpus else None)  # after, same CPU
         mN, _ = o.bench(cf, cm, threads, per_thread, cpus=cpus)
         single = (m1 + m1b) / 2
@@ -536,6 +550,13 @@ def main():
             "per_core_mpps": round(mS / threads, 2),
             "per_core_over_single": round(mS / threads / single, 3),
             "fib_copy_mpps": round(mN, 2),
+            # the cgroup's CPU-time quota over the multi-core leg: throttled
+            # time is time the pinned workers were stopped by the quota, not
+            # slowed by their own work (the process has other threads too)
+            "quota_throttled_ms": round((cs1.get("throttled_usec", 0) - cs0.get("throttled_usec", 0)) / 1e3, 1)
+            if cs0 and cs1 else None,
+            "quota_throttled_periods": (cs1.get("nr_throttled", 0) - cs0.get("nr_throttled", 0)) if cs0 and cs1 else None,
+            "multi_core_leg_s": round(tS, 2),
             "cpus": cpus,
             "host_cpus": host_cpus(),
             "sample": (f"oracle C restatement of grout's node chain (bursts of 64, "

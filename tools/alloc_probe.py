@@ -34,6 +34,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--batch", type=int, default=1 << 24)
     ap.add_argument("--kinds", default="torch,malloc,contig,contig+in")
+    ap.add_argument("--fib-contig", default="1", help="FIB tables contiguous (the \"alloc_contig\" knob at load), "
+                    "e.g. 0,1: one context each, interleaved")
+    ap.add_argument("--rounds", type=int, default=1, help="passes over every (fib, kind)")
     a = ap.parse_args()
     import torch
 
@@ -49,16 +52,20 @@ def main():
     hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
 
     dev = torch.device("cuda", 0)
-    fp = FastPath(0)
     topo = T.config_fullview()
-    fp.load(topo)
+    fps = {}
+    for fc in [int(x) for x in a.fib_contig.split(",")]:
+        fps[fc] = FastPath(0)
+        fps[fc].tune("alloc_contig", fc)
+        fps[fc].load(topo)
     n = a.batch
     frames, meta = S.stream(n, 0x67721000, routes=topo.route_array())
     t_in = torch.from_numpy(frames.reshape(-1)).to(dev)
     d_meta = torch.from_numpy(meta.view(np.uint8)).to(dev)
     d_v = torch.empty(n * 8, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
-    q = fp.queue(shared_stream(dev))
+    stream = shared_stream(dev)
+    qs = {fc: f.queue(stream) for fc, f in fps.items()}
 
     def alloc(kind, size):
         if kind == "torch":
@@ -71,7 +78,7 @@ def main():
             raise MemoryError(f"{kind}: hip error {r}")
         return p.value, p
 
-    def timed(d_in, d_out):
+    def timed(q, d_in, d_out):
         for _ in range(a.warm):
             q.submit(d_in, d_out, d_meta, d_v, n)
         q.sync()
@@ -81,7 +88,8 @@ def main():
         ms, cnt = q.kernel_ms(a.steps)
         return ms / max(cnt, 1)
 
-    for kind in a.kinds.split(","):
+    for _, fc, kind in [(r, fc, k) for r in range(a.rounds) for fc in fps for k in a.kinds.split(",")]:
+        q = qs[fc]
         base, _, in_too = kind.partition("+")
         keep = []
         d_in = t_in.data_ptr()
@@ -93,16 +101,17 @@ def main():
         for _ in range(a.cands):
             d_out, h = alloc(base, n * abi.LINE)
             keep.append(h)
-            res.append(round(timed(d_in, d_out), 4))
-        print(json.dumps({"kind": kind, "kernel_ms": res, "min": min(res), "median": float(np.median(res)),
+            res.append(round(timed(q, d_in, d_out), 4))
+        print(json.dumps({"fib_contig": fc, "kind": kind, "kernel_ms": res, "min": min(res), "median": float(np.median(res)),
                           "max": max(res), "spread": round(max(res) / min(res), 3)}), flush=True)
         for h in keep:
             if isinstance(h, ctypes.c_void_p):
                 hip.hipFree(h)
         del keep
         torch.cuda.synchronize()
-    q.close()
-    fp.close()
+    for fc in fps:
+        qs[fc].close()
+        fps[fc].close()
 
 
 if __name__ == "__main__":
