@@ -141,6 +141,10 @@ __device__ __forceinline__ uint32_t tile_of(const fwd4_params &A, uint32_t k) {
 		const uint32_t x = blockIdx.x & 7, l = blockIdx.x >> 3, per = gridDim.x >> 3;
 		return x * A.chunk + l + k * per;
 	}
+	if (A.order == 3) { // runs of A.chunk tiles: the grid's window moves as in order 0,
+		const uint32_t j = k / A.chunk; // each CU's tiles come in contiguous runs
+		return (j * gridDim.x + blockIdx.x) * A.chunk + (k - j * A.chunk);
+	}
 	return A.chunk ? blockIdx.x * A.chunk + k : blockIdx.x + k * gridDim.x;
 }
 
@@ -401,6 +405,9 @@ __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params 
 		const uint32_t x = blockIdx.x & 7, l = blockIdx.x >> 3, per = gridDim.x >> 3;
 		const uint32_t lo = x * A.chunk + l, hi = min((x + 1) * A.chunk, n_tiles);
 		n_local = lo < hi ? (hi - 1 - lo) / per + 1 : 0;
+	} else if (A.order == 3) {
+		const uint32_t S = gridDim.x * A.chunk, r = n_tiles % S, b0 = blockIdx.x * A.chunk;
+		n_local = n_tiles / S * A.chunk + (r > b0 ? min(A.chunk, r - b0) : 0);
 	} else if (A.chunk)
 		n_local = blockIdx.x * A.chunk < n_tiles ? min(A.chunk, n_tiles - blockIdx.x * A.chunk) : 0;
 	else

@@ -279,7 +279,9 @@ struct gr_hip_ctx {
 	int ring_cfg; // ring geometry (fwd4_ring.hip ring_cfgN)
 	int host_direct; // host path: the kernel reads / writes pinned host memory itself
 	int node_ptrs; // node path: frames in registered memory are handed over by address
-	int tile_order; // 0: workgroup b takes tiles b, b + G, ...; 1: one contiguous run each
+	int tile_order; // 0: workgroup b takes tiles b, b + G, ...; 1: one contiguous run each;
+	                // 2: one region per XCD; 3: runs of tile_run tiles interleaved
+	uint32_t tile_run; // tiles per run of tile order 3
 	int alloc_contig; // large device arrays physically contiguous first (dev_alloc), default 1
 	uint32_t spin_max; // ring waits: polls before giving up (0 = the kernel's default)
 	std::atomic<int> fail_appends{0}; // tests: the next N gr_hip_node_append calls fail (-ENOMEM)
@@ -783,6 +785,7 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->host_direct = 1; // measured 1.9x the staged copies
 	c->node_ptrs = 0; // staged lines: faster than frames by address, more so with several workers
 	c->tile_order = 0;
+	c->tile_run = 16;
 	c->spin_max = 0;
 	c->untimed = 0;
 	c->time_every = 1;
@@ -2043,6 +2046,8 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 		A.chunk = (tiles + 7) / 8;
 	else if (c->tile_order == 2)
 		A.order = 0;
+	if (c->tile_order == 3)
+		A.chunk = c->tile_run;
 	// every `time_every`-th submit of the queue carries the event pair
 	// (counted over every submit that could be timed, whatever the knobs)
 	if (timed && !q->always_timed) {
@@ -2098,9 +2103,13 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 	} else if (strcmp(key, "alloc_contig") == 0) { // later allocations only
 		c->alloc_contig = value != 0;
 	} else if (strcmp(key, "tile_order") == 0) {
-		if (value < 0 || value > 2)
+		if (value < 0 || value > 3)
 			return -EINVAL;
 		c->tile_order = value;
+	} else if (strcmp(key, "tile_run") == 0) {
+		if (value < 1 || value > 4096)
+			return -EINVAL;
+		c->tile_run = (uint32_t)value;
 	} else if (strcmp(key, "host_direct") == 0) {
 		c->host_direct = value != 0;
 	} else if (strcmp(key, "fib_format_of") == 0) { // read: the format VRF `value` is on the device in

@@ -486,7 +486,10 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               translation for the kernel's streams and gathers), hipMalloc
 //               when that fails (default); 0 = hipMalloc always
 //   "tile_order" 0 = workgroup b takes 64-packet tiles b, b + G, b + 2G ...
-//               (default), 1 = one contiguous run of tiles per workgroup
+//               (default), 1 = one contiguous run of tiles per workgroup,
+//               2 = one region per XCD, its workgroups interleaved in it,
+//               3 = runs of "tile_run" tiles (default 16), run j of
+//               workgroup b being run j * G + b
 //   "fib_format_of" (read) the format VRF `value`'s FIB is on the device in
 //   "occupancy" (read) resident workgroups per CU of the current variant
 //   "commit_us_stage" / "commit_us_enqueue" / "commit_us_publish" (read) the last

@@ -574,18 +574,21 @@ def test_ring_geometries(fastpath, cfg):
         fastpath.tune("wg_per_cu", 0)
 
 
-@pytest.mark.parametrize("order", [1, 2])
-def test_tile_orders(fastpath, order):
+@pytest.mark.parametrize("order,run", [(1, 16), (2, 16), (3, 16), (3, 5)])
+def test_tile_orders(fastpath, order, run):
     """The other tile orders (one contiguous run per workgroup; one region per
-    XCD) cover every tile exactly once, ragged sizes included, bit-exact."""
+    XCD; interleaved runs of `run` tiles) cover every tile exactly once, ragged
+    sizes included, bit-exact."""
     tf = _fullview()
     fr, me = S.stream(1 << 20, 0x7110 + order, routes=tf.route_array())
     fastpath.tune("tile_order", order)
+    fastpath.tune("tile_run", run)
     try:
         for n in (1 << 20, 64 * 1000 + 17, 64 * 257 + 1, 63, 1):
             compare(oracle.Oracle(tf).process(fr[:n], me[:n]), run_gpu(fastpath, tf, fr[:n], me[:n]))
     finally:
         fastpath.tune("tile_order", 0)
+        fastpath.tune("tile_run", 16)
 
 
 # ---- IPv6

@@ -12,7 +12,7 @@ kinds torch (the bench's plain leg), hipMalloc, hipExtMallocWithFlags
 (hipDeviceMallocContiguous); and the input itself of that kind too ("+in").
 One JSON line per kind: every candidate's kernel ms, min / median / max.
 
-    python3 tools/alloc_probe.py [--cands 8] [--kinds torch,malloc,contig,contig+in]
+    python3 tools/alloc_probe.py [--cands 8] [--kinds torch,malloc,contig,contig+in] [--orders 0,1,2]
 """
 import argparse
 import ctypes
@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--fib-contig", default="1", help="FIB tables contiguous (the \"alloc_contig\" knob at load), "
                     "e.g. 0,1: one context each, interleaved")
     ap.add_argument("--rounds", type=int, default=1, help="passes over every (fib, kind)")
+    ap.add_argument("--orders", default="0", help="tile orders (the \"tile_order\" knob), e.g. 0,1,2,3:16 (order 3 with "
+                    "runs of 16 tiles): every candidate "
+                    "timed under each")
     a = ap.parse_args()
     import torch
 
@@ -78,7 +81,18 @@ def main():
             raise MemoryError(f"{kind}: hip error {r}")
         return p.value, p
 
-    def timed(q, d_in, d_out):
+    orders = a.orders.split(",")  # "3:16" = tile order 3, runs of 16 tiles
+
+    def timed(q, fp, d_in, d_out):
+        res = []
+        for o in orders:
+            order, _, run = o.partition(":")
+            fp.tune("tile_order", int(order))
+            fp.tune("tile_run", int(run or 16))
+            res.append(timed1(q, d_in, d_out))
+        return res
+
+    def timed1(q, d_in, d_out):
         for _ in range(a.warm):
             q.submit(d_in, d_out, d_meta, d_v, n)
         q.sync()
@@ -101,9 +115,11 @@ def main():
         for _ in range(a.cands):
             d_out, h = alloc(base, n * abi.LINE)
             keep.append(h)
-            res.append(round(timed(q, d_in, d_out), 4))
-        print(json.dumps({"fib_contig": fc, "kind": kind, "kernel_ms": res, "min": min(res), "median": float(np.median(res)),
-                          "max": max(res), "spread": round(max(res) / min(res), 3)}), flush=True)
+            res.append(timed(q, fps[fc], d_in, d_out))
+        for i, o in enumerate(orders):
+            r = [round(x[i], 4) for x in res]
+            print(json.dumps({"fib_contig": fc, "kind": kind, "tile_order": o, "kernel_ms": r, "min": min(r),
+                              "median": float(np.median(r)), "max": max(r), "spread": round(max(r) / min(r), 3)}), flush=True)
         for h in keep:
             if isinstance(h, ctypes.c_void_p):
                 hip.hipFree(h)
