@@ -518,7 +518,9 @@ def main():
     # (SURVEY.md §8d): pinned workers on one shared FIB (grout's layout: one
     # rte_fib per VRF for every worker), each starting at its own offset of
     # the sample, each warmed up by one untimed pass over the whole sample
-    # before the timed part. The single-core leg is the 16-core leg's worker 0
+    # before the timed part, one core per L3 domain in turn (cpu_placement);
+    # the same leg packed on the first allowed CPUs beside it. The single-core
+    # leg is the 16-core leg's worker 0
     # alone: same CPU, offset, warm-up, shared FIB and packet count, in the
     # same call; beside them the 16 workers with a FIB copy each on THP
     # (slower on the boxes measured: 16 tables of 128 MiB leave L3)
@@ -528,18 +530,27 @@ def main():
         cf, cm = frames[: 1 << 20].copy(), meta[: 1 << 20].copy()
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         allowed = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
-        cpus = allowed[:threads] if len(allowed) >= threads else None  # worker i on the i-th allowed CPU
-        m0, _ = o.bench(cf, cm, 1, 1 << 20, fib_copy=False, cpus=cpus[:1] if cpus else None)  # sizes the timed parts
+        packed = allowed[:threads] if len(allowed) >= threads else None  # worker i on the i-th allowed CPU
+        spread = cpu_placement(threads, "spread")  # one core per L3 domain in turn
+        cpus = spread or packed
+        one = cpus[:1] if cpus else None
+        m0, _ = o.bench(cf, cm, 1, 1 << 20, fib_copy=False, cpus=one)  # sizes the timed parts
         per_thread = max(1 << 20, int(m0 * 1e6 * args.cpu_seconds))
-        m1, _ = o.bench(cf, cm, 1, per_thread, fib_copy=False, cpus=cpus[:1] if cpus else None)
+        m1, _ = o.bench(cf, cm, 1, per_thread, fib_copy=False, cpus=one)
         cs0 = cgroup_cpu_stat()
         tS = time.perf_counter()
         mS, _ = o.bench(cf, cm, threads, per_thread, fib_copy=False, cpus=cpus)
         tS = time.perf_counter() - tS
         cs1 = cgroup_cpu_stat()
-        m1b, _ = o.bench(cf, cm, 1, per_thread, fib_copy=False, cpus=cpus[:1] if cpus else None)  # after, same CPU
+        m1b, _ = o.bench(cf, cm, 1, per_thread, fib_copy=False, cpus=one)  # after, same CPU
+        mP = None
+        if spread and packed and spread != packed:  # the same leg on the first allowed CPUs
+            mP, _ = o.bench(cf, cm, threads, per_thread, fib_copy=False, cpus=packed)
         mN, _ = o.bench(cf, cm, threads, per_thread, cpus=cpus)
         single = (m1 + m1b) / 2
+
+        def l3_domains(cs):
+            return len({_cpu_sysfs(c, "cache/index3/id") for c in cs}) if cs else None
         result["cpu_baseline"] = {
             "value": round(mS, 2),
             "unit": "Mpps",
@@ -549,6 +560,12 @@ def main():
             "single_core_mpps_before_after": [round(m1, 2), round(m1b, 2)],
             "per_core_mpps": round(mS / threads, 2),
             "per_core_over_single": round(mS / threads / single, 3),
+            "l3_domains": l3_domains(cpus),
+            # the same workers packed on the first allowed CPUs (fewer L3
+            # domains: they share each CCD's L3 and its link to memory)
+            "packed_mpps": round(mP, 2) if mP is not None else None,
+            "packed_per_core_over_single": round(mP / threads / single, 3) if mP is not None else None,
+            "packed_l3_domains": l3_domains(packed) if mP is not None else None,
             "fib_copy_mpps": round(mN, 2),
             # the cgroup's CPU-time quota over the multi-core leg: throttled
             # time is time the pinned workers were stopped by the quota, not
@@ -561,11 +578,13 @@ def main():
             "host_cpus": host_cpus(),
             "sample": (f"oracle C restatement of grout's node chain (bursts of 64, "
                        f"{'per-length prefix hash LPM6' if args.workload == 'fullview6' else 'DIR24_8 8-byte entries'}), "
-                       f"{threads} pinned threads on one shared FIB (grout's layout: one rte_fib per VRF), "
+                       f"{threads} pinned threads (one core per L3 domain in turn, as grout spreads its lcores) "
+                       f"on one shared FIB (grout's layout: one rte_fib per VRF), "
                        f"each starting at its own offset of the same 1M-packet prefix of this stream, warmed up "
                        f"by one pass over it, then {per_thread} packets each timed; single_core_mpps: worker 0 "
                        f"alone (same CPU, offset, warm-up, shared FIB, packets), before and after the "
-                       f"{threads}-core leg; fib_copy_mpps: the {threads} workers with a FIB copy each on THP"),
+                       f"{threads}-core leg; packed_mpps: the same leg on the first {threads} allowed CPUs; "
+                       f"fib_copy_mpps: the {threads} workers with a FIB copy each on THP"),
         }
         o.close()
 
