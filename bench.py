@@ -111,7 +111,7 @@ def parse():
     p.add_argument("--placement", default="calibrated", choices=["calibrated", "plain"],
                    help="calibrated: batch buffers from gr_hip_batch_alloc, output lines re-placed by gr_hip_batch_place over "
                         "--candidates allocations; plain: torch allocations")
-    p.add_argument("--candidates", type=int, default=6)
+    p.add_argument("--candidates", type=int, default=8)
     p.add_argument("--no-plain", action="store_true",
                    help="skip the same measurement on plain torch allocations (value_plain_placement)")
     p.add_argument("--time-every", type=int, default=4,
@@ -426,9 +426,9 @@ def main():
             "forwarded_frac": round(fwd_frac, 6),
             **({"tune": {k: int(v) for k, v in tune.items()}} if tune else {}),
             "occupancy_wg_per_cu": fp.tune("occupancy"),
-            "placement": (f"calibrated: output lines, then frames = fastest of {args.candidates + 1} physically "
-                          "contiguous allocations each (gr_hip_batch_alloc), timed over a batch of this workload drawn "
-                          "with another seed (gr_hip_batch_place)"
+            "placement": (f"calibrated: output lines, then frames = fastest of {args.candidates + 1} allocations "
+                          "each (gr_hip_batch_alloc's, then plain and physically contiguous in turn), timed over a "
+                          "batch of this workload drawn with another seed (gr_hip_batch_place)"
                           if batch is not None else "plain torch allocations"),
             "output": ("packed 32-byte header prefixes (every byte the path changes; GR_HIP_BATCH_F_PREFIX32)"
                        if prefix32 else "whole 64-byte header lines"),

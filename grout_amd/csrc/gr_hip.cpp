@@ -3023,25 +3023,29 @@ extern "C" int gr_hip_batch_alloc(gr_hip_ctx_t *c, uint32_t n, uint32_t in_strid
 	return 0;
 }
 
-// Kernel time of batch t on the probe queue q: 2 warm-up launches, 4 timed.
-static int place_time(gr_hip_queue *q, const gr_hip_batch &t, float *ms) {
-	for (int i = 0; i < 6; i++) {
+// Kernel time of batch t on the probe queue q: 3 warm-up launches, 6 timed
+// (the first `warm` extra launches bring the clock up before any probe).
+static int place_time(gr_hip_queue *q, const gr_hip_batch &t, float *ms, int warm = 0) {
+	constexpr int TIMED = 6;
+	for (int i = 0; i < warm + 3 + TIMED; i++) {
 		const int r = gr_hip_fwd4_submit(q, &t);
 		if (r)
 			return r;
 	}
-	uint32_t cnt = 0;
-	const int r = gr_hip_queue_kernel_ms(q, 4, ms, &cnt);
-	return r ? r : cnt == 4 ? 0 : -EIO; // the probes must all be timed
+	uint32_t cnt = 0; // the last TIMED launches
+	const int r = gr_hip_queue_kernel_ms(q, TIMED, ms, &cnt);
+	return r ? r : cnt == TIMED ? 0 : -EIO; // the probes must all be timed
 }
 
 // Up to `candidates` more device buffers of `bytes` each (fewer when memory
-// runs short), after `cur`.
+// runs short), after `cur`. With "alloc_contig" the candidates alternate
+// between plain and physically contiguous allocations: which kind lands in
+// the fast translation class differs from box to box.
 static std::vector<void *> place_alloc(const gr_hip_ctx *c, void *cur, size_t bytes, uint32_t candidates) {
 	std::vector<void *> v{cur};
 	for (uint32_t k = 0; k < candidates; k++) {
 		void *o = nullptr;
-		if (dev_alloc(c, &o, bytes) != hipSuccess) {
+		if ((c->alloc_contig && k % 2 == 0 ? hipMalloc(&o, bytes) : dev_alloc(c, &o, bytes)) != hipSuccess) {
 			(void)hipGetLastError();
 			break;
 		}
@@ -3079,7 +3083,7 @@ extern "C" int gr_hip_batch_place(gr_hip_ctx_t *c, gr_hip_batch *b, uint32_t can
 		gr_hip_batch t = *b;
 		t.out_lines = outs[k];
 		float ms = 0;
-		if ((r = place_time(q, t, &ms)) == 0 && (k == 0 || ms < best)) {
+		if ((r = place_time(q, t, &ms, k == 0 ? 32 : 0)) == 0 && (k == 0 || ms < best)) {
 			best = ms;
 			pick = k;
 		}

@@ -543,10 +543,11 @@ int gr_hip_memcpy_d2h(gr_hip_ctx_t *, void *dst, const void *src, size_t bytes);
 // (n * in_stride bytes), output lines (n * 64), metadata and verdicts, all
 // zeroed; fills *b (flags 0, out_stride 64). Free with gr_hip_batch_free.
 int gr_hip_batch_alloc(gr_hip_ctx_t *, uint32_t n, uint32_t in_stride, struct gr_hip_batch *b);
-// Where the output lines' HBM pages lie relative to the frames' changes the
-// kernel's time by up to ~20 % (concurrent reads and writes that collide in
-// the memory channels). With the batch's frames and metadata in
-// place, this allocates `candidates` more output-line buffers, times each
+// Which HBM pages back the frames and the output lines changes the kernel's
+// time by up to ~15 %: some regions of an allocation translate slowly (the
+// L1 TLB sits at its in-flight limit). With the batch's
+// frames and metadata in place, this allocates `candidates` more output-line
+// buffers (plain and, with "alloc_contig", physically contiguous in turn), times each
 // (and the current one) over the batch on a private queue without counters
 // and keeps the fastest; then `candidates` more frame buffers, each holding a
 // copy of the frames, timed against the lines kept, and keeps the fastest
