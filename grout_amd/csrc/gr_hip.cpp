@@ -36,11 +36,16 @@ extern "C" int gr_fwd4_ring_ncfg(void);
 #define RING_WG_PER_CU 2 // default workgroups per CU of the ring kernel (measured)
 
 
+// GR_HIP_TRACE_ERRORS=1 in the environment: each failing HIP call named on
+// stderr (file:line, the call, HIP's error string) before it is returned
 #define HCK(expr)                                                                                  \
 	do {                                                                                       \
 		hipError_t e__ = (expr);                                                           \
 		if (e__ != hipSuccess) {                                                           \
 			(void)hipGetLastError();                                                   \
+			if (getenv("GR_HIP_TRACE_ERRORS"))                                         \
+				fprintf(stderr, "gr_hip: %s:%d: %s: %s\n", __FILE__, __LINE__, #expr, \
+					hipGetErrorString(e__));                                   \
 			return e__ == hipErrorOutOfMemory ? -ENOMEM : -EIO;                        \
 		}                                                                                  \
 	} while (0)

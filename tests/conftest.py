@@ -8,6 +8,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+# a failing HIP call inside libgrout_hip.so names itself on stderr (captured
+# with the failing test's output)
+os.environ.setdefault("GR_HIP_TRACE_ERRORS", "1")
 
 
 def pytest_configure(config):
