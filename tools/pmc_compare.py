@@ -15,7 +15,9 @@ import sys
 def main():
     root = sys.argv[1]
     out = collections.OrderedDict()
-    for wl in sorted(os.listdir(root), key=lambda x: (x != "single64", x)):
+    def order(x):  # single64 first, spans by size, then the rest
+        return (x != "single64", not x.startswith("span"), int(x[4:]) if x[4:].isdigit() else 0, x)
+    for wl in sorted(os.listdir(root), key=order):
         if not os.path.isdir(os.path.join(root, wl)):
             continue
         c, durs = {}, []

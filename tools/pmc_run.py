@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--stats", type=int, default=None)
     ap.add_argument("--nt", type=int, default=None)
     ap.add_argument("--no-calib", action="store_true")
+    ap.add_argument("--span-bits", type=int, default=None,
+                    help="fullview64 with destinations uniform in an aligned 2^N-address range (from 16.0.0.0 when "
+                         "N <= 28, else from 0.0.0.0): the FIB lookups touch 2^(N-8) x 2 bytes of tbl24")
     args = ap.parse_args()
     import torch
 
@@ -45,6 +48,9 @@ def main():
     else:
         topo = T.config_fullview()
         kw = dict(routes=topo.route_array())
+        if args.span_bits is not None:
+            lo = 0x10000000 if args.span_bits <= 28 else 0
+            kw = dict(dst_range=(lo, lo + (1 << args.span_bits) - 1))
         if args.workload == "imix_frames":  # whole IMIX frames in mbuf-like slots, as bench.py
             kw.update(imix=True, stride=args.slot)
         elif args.workload == "imix":  # IMIX header lines staged, as bench.py
