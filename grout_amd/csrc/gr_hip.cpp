@@ -284,6 +284,7 @@ struct gr_hip_ctx {
 	int ring_cfg; // ring geometry (fwd4_ring.hip ring_cfgN)
 	int host_direct; // host path: the kernel reads / writes pinned host memory itself
 	int node_ptrs; // node path: frames in registered memory are handed over by address
+	uint32_t stage_min_tiles; // fast adjacencies staged in LDS only from this many tiles per workgroup
 	int tile_order; // 0: workgroup b takes tiles b, b + G, ...; 1: one contiguous run each;
 	                // 2: one region per XCD; 3: runs of tile_run tiles interleaved
 	uint32_t tile_run; // tiles per run of tile order 3
@@ -791,6 +792,7 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->node_ptrs = 0; // staged lines: faster than frames by address, more so with several workers
 	c->tile_order = 0;
 	c->tile_run = 16;
+	c->stage_min_tiles = 4;
 	c->spin_max = 0;
 	c->untimed = 0;
 	c->time_every = 1;
@@ -1999,6 +2001,15 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	// and 2000::/4 of the IPv6 trie's first level, when one VRF holds IPv6
 	// routes (given up before the fast adjacencies; in 16-byte units below)
 	uint32_t t6 = c->v6_routes && c->top6[g] != nullptr ? FWD4_TOP6_MAX : 0;
+	// a launch too small to give each workgroup "stage_min_tiles" tiles reads
+	// the adjacencies from the global tables: staging 32 KiB per workgroup
+	// for a tile or two only adds to a small batch's latency
+	{
+		const uint32_t per = c->wg_per_cu > 0 ? (uint32_t)c->wg_per_cu : RING_WG_PER_CU;
+		const uint32_t g0 = (uint32_t)c->n_cu * per;
+		if ((uint64_t)tiles < (uint64_t)g0 * c->stage_min_tiles)
+			n4 = n6 = t6 = 0;
+	}
 	int occ;
 	{
 		std::lock_guard<std::mutex> ol(c->occ_mu);
@@ -2111,6 +2122,10 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < 0 || value > 3)
 			return -EINVAL;
 		c->tile_order = value;
+	} else if (strcmp(key, "stage_min_tiles") == 0) {
+		if (value < 0)
+			return -EINVAL;
+		c->stage_min_tiles = (uint32_t)value;
 	} else if (strcmp(key, "tile_run") == 0) {
 		if (value < 1 || value > 4096)
 			return -EINVAL;

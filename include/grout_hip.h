@@ -490,6 +490,10 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               2 = one region per XCD, its workgroups interleaved in it,
 //               3 = runs of "tile_run" tiles (default 16), run j of
 //               workgroup b being run j * G + b
+//   "stage_min_tiles" the fast adjacencies (and IPv6 first-level slice) are
+//               staged in each workgroup's LDS only when the launch gives every
+//               workgroup at least this many 64-packet tiles (default 4);
+//               smaller launches read them from the global tables
 //   "fib_format_of" (read) the format VRF `value`'s FIB is on the device in
 //   "occupancy" (read) resident workgroups per CU of the current variant
 //   "commit_us_stage" / "commit_us_enqueue" / "commit_us_publish" (read) the last

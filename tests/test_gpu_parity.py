@@ -591,6 +591,21 @@ def test_tile_orders(fastpath, order, run):
         fastpath.tune("tile_run", 16)
 
 
+@pytest.mark.parametrize("stage_min", [0, 1 << 20])
+def test_adjacency_staging_threshold(fastpath, stage_min):
+    """Fast adjacencies staged in LDS (stage_min_tiles 0: always) or read
+    from the global tables (a threshold no launch reaches): the same
+    results, bit-exact, large and ragged batches."""
+    tf = _fullview()
+    fr, me = S.stream(1 << 18, 0x57A6, routes=tf.route_array())
+    fastpath.tune("stage_min_tiles", stage_min)
+    try:
+        for n in (1 << 18, 64 * 300 + 9, 1024, 1):
+            compare(oracle.Oracle(tf).process(fr[:n], me[:n]), run_gpu(fastpath, tf, fr[:n], me[:n]))
+    finally:
+        fastpath.tune("stage_min_tiles", 4)
+
+
 # ---- IPv6
 
 @functools.lru_cache(maxsize=None)

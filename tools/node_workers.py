@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--wg-per-cu", type=int, default=-1, help="the \"wg_per_cu\" knob; -1: the default")
     ap.add_argument("--prof", type=int, default=0,
                     help="1: one more node run per line with the node's and the library's phase clocks")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE", help="gr_hip_tune knobs (repeatable)")
     ap.add_argument("--lcores", default="none", choices=["none", "allowed", "spread", "socket"],
                     help="worker placement: the scheduler's, the k-th allowed CPU, or bench.cpu_placement's spread")
     args = ap.parse_args()
@@ -78,6 +79,9 @@ def main():
         fp.tune("ring", args.ring_cfg)
     if args.wg_per_cu >= 0:
         fp.tune("wg_per_cu", args.wg_per_cu)
+    for kv in args.tune:
+        k, v = kv.split("=")
+        fp.tune(k, int(v))
     L.gh_set_pin(args.pin)  # 0: staged header lines, the node's default
     L.gh_set_rx_touch(args.rx_touch)
     L.gh_set_null_node.argtypes = [ctypes.c_int]
@@ -143,7 +147,7 @@ def main():
         print(json.dumps({"threads": k, "gpus": 1, "packets": m, "batch": args.batch, "rx_touch": args.rx_touch,
                           "harness_alone_mpps": round(m / t0 / 1e6, 1),
                           "node_ns_per_pkt_per_worker": round(dt * 1e9 * k / m, 1), "mode": "frames by address" if args.pin else "staged lines",
-                          "recycle": args.recycle, "passes": per, "lcores": args.lcores, "cpus": cpus, "ring_cfg": args.ring_cfg, "wg_per_cu": args.wg_per_cu, "mbufs_loaded": m_loaded,
+                          "recycle": args.recycle, "passes": per, "lcores": args.lcores, "cpus": cpus, "ring_cfg": args.ring_cfg, "wg_per_cu": args.wg_per_cu, "tune": args.tune, "mbufs_loaded": m_loaded,
                           "ms": round(t * 1e3, 2), "mpps_aggregate": round(m / t / 1e6, 1),
                           "mpps_per_worker": round(m / t / 1e6 / k, 1),
                           "cpu_ns_per_pkt_per_worker": round(t * 1e9 * k / m, 1),
