@@ -158,9 +158,37 @@ struct fwd4_params {
 	uint32_t chunk; // fwd4_ring.hip: 0 = workgroup b takes tiles b, b + G, ...;
 	                // else the contiguous tiles [b * chunk, (b + 1) * chunk)
 	uint32_t order; // 2: XCD x (= b % 8) takes region [x * chunk, (x + 1) * chunk),
-	                // its workgroups interleaved in it (grid % 8 == 0)
+	                // its workgroups interleaved in it (grid % 8 == 0);
+	                // 3: runs of `chunk` tiles, run j of workgroup b = run j * G + b
 	uint32_t spin_max; // polls before a ring wait gives up (0 = RING_SPIN_MAX)
 	uint32_t *err; // set to 1 when a workgroup gave up (host-mapped; may be NULL)
+	// the resident kernel (gr_fwd4_resident): the workgroup's index and count in
+	// the tile order (wgs 0: blockIdx / gridDim), and whether `in` holds frame
+	// addresses (GR_HIP_BATCH_F_FRAME_PTRS)
+	uint32_t wg0, wgs;
+	uint32_t ptrs;
+	uint32_t _pad;
+};
+
+// The resident kernel's batches: ring r of a context holds `ndesc`
+// descriptors in pinned host memory; the host writes A, then `seq` (release);
+// the kernel's workgroup r takes them in seq order (1, 2, ...), runs each,
+// and stores its seq into done[r * stride] (release, system scope).
+struct __attribute__((aligned(64))) fwd4_res_desc {
+	uint64_t seq;
+	uint64_t _pad[7];
+	struct fwd4_params A;
+};
+
+struct fwd4_res_params {
+	struct fwd4_res_desc *descs; // [rings][ndesc], host memory
+	uint64_t *done; // [rings * stride], host memory
+	uint64_t *exited; // [rings * stride], host memory: launch_id once ring r's workgroup has left
+	uint32_t *stop; // host memory: nonzero = every workgroup leaves after its batch
+	uint64_t lifetime; // s_memrealtime ticks (100 MHz): a workgroup idle past it sets *stop
+	uint64_t launch_id;
+	uint32_t ndesc;
+	uint32_t stride; // uint64_t per ring in done / exited
 };
 
 // First-level FIB6 entries a launch may stage in LDS: 2000::/4 (index =

@@ -135,17 +135,44 @@ __device__ __forceinline__ bool flag_wait(L_t &L, const uint32_t *f, uint32_t wa
 	}
 }
 
+// This workgroup's index and the workgroup count in the tile order: the
+// launch's, or the resident kernel's per-batch ones (fwd4_params.wgs).
+__device__ __forceinline__ uint32_t wg_id(const fwd4_params &A) {
+	return A.wgs ? A.wg0 : blockIdx.x;
+}
+__device__ __forceinline__ uint32_t wg_count(const fwd4_params &A) {
+	return A.wgs ? A.wgs : gridDim.x;
+}
+
 // Tile k of this workgroup (see fwd4_params.chunk).
 __device__ __forceinline__ uint32_t tile_of(const fwd4_params &A, uint32_t k) {
+	const uint32_t b = wg_id(A), G = wg_count(A);
 	if (A.order == 2) { // XCD x = b % 8 interleaves its workgroups over region x
-		const uint32_t x = blockIdx.x & 7, l = blockIdx.x >> 3, per = gridDim.x >> 3;
+		const uint32_t x = b & 7, l = b >> 3, per = G >> 3;
 		return x * A.chunk + l + k * per;
 	}
 	if (A.order == 3) { // runs of A.chunk tiles: the grid's window moves as in order 0,
 		const uint32_t j = k / A.chunk; // each CU's tiles come in contiguous runs
-		return (j * gridDim.x + blockIdx.x) * A.chunk + (k - j * A.chunk);
+		return (j * G + b) * A.chunk + (k - j * A.chunk);
 	}
-	return A.chunk ? blockIdx.x * A.chunk + k : blockIdx.x + k * gridDim.x;
+	return A.chunk ? b * A.chunk + k : b + k * G;
+}
+
+// How many tiles this workgroup takes (tile_of's k ranges over [0, that)).
+__device__ __forceinline__ uint32_t local_tiles(const fwd4_params &A) {
+	const uint32_t n_tiles = (A.n + 63) >> 6, b = wg_id(A), G = wg_count(A);
+	if (A.order == 2) {
+		const uint32_t x = b & 7, l = b >> 3, per = G >> 3;
+		const uint32_t lo = x * A.chunk + l, hi = min((x + 1) * A.chunk, n_tiles);
+		return lo < hi ? (hi - 1 - lo) / per + 1 : 0;
+	}
+	if (A.order == 3) {
+		const uint32_t S = G * A.chunk, r = n_tiles % S, b0 = b * A.chunk;
+		return n_tiles / S * A.chunk + (r > b0 ? min(A.chunk, r - b0) : 0);
+	}
+	if (A.chunk)
+		return b * A.chunk < n_tiles ? min(A.chunk, n_tiles - b * A.chunk) : 0;
+	return b < n_tiles ? (n_tiles - 1 - b) / G + 1 : 0;
 }
 
 // Frame pointers of tile t, one per lane (rows past the batch repeat its last
@@ -165,8 +192,8 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
 // reads), so that the counted vmcnt waits below stay exact. In PTRS mode a
 // loader also loads the next tile's frame pointers ahead (one more load per
 // tile, issued before the tile's DMA, which only makes the waits longer).
-template <class C, bool NT, bool PTRS>
-__device__ void ring_loader(const fwd4_params &A, ring_lds<C, PTRS> &L, uint32_t n_local, uint32_t j, uint32_t lane) {
+template <class C, bool NT, bool PTRS, class LT>
+__device__ void ring_loader(const fwd4_params &A, LT &L, uint32_t n_local, uint32_t j, uint32_t lane) {
 	const uint32_t prow = lane >> 2;
 	const uint32_t pchunk = (lane & 3) ^ ((lane >> 4) & 3); // chunk this lane lands in slot lane & 3
 	uint32_t pub = j; // oldest of this loader's tiles not yet published
@@ -226,8 +253,8 @@ __device__ void ring_loader(const fwd4_params &A, ring_lds<C, PTRS> &L, uint32_t
 			flag_set(&L.ready[pub % C::SLOTS], pub + 1);
 }
 
-template <class C, bool NT, bool PTRS>
-__device__ void ring_storer(const fwd4_params &A, ring_lds<C, PTRS> &L, uint32_t n_local, uint32_t j, uint32_t lane) {
+template <class C, bool NT, bool PTRS, class LT>
+__device__ void ring_storer(const fwd4_params &A, LT &L, uint32_t n_local, uint32_t j, uint32_t lane) {
 	const uint32_t prow = lane >> 2, part = lane & 3;
 	const uint32_t pslot = (part ^ ((lane >> 4) & 3)) << 4;
 	const bool prefix = A.out_stride == GR_HIP_PREFIX; // packed 32-byte prefixes (whole lines are >= 64)
@@ -269,8 +296,8 @@ __device__ void ring_storer(const fwd4_params &A, ring_lds<C, PTRS> &L, uint32_t
 	}
 }
 
-template <class C, bool STATS, bool PTRS>
-__device__ void ring_compute(const fwd4_params &A, const kctx &P, ring_lds<C, PTRS> &L, stat_slot *slots,
+template <class C, bool STATS, bool PTRS, class LT>
+__device__ void ring_compute(const fwd4_params &A, const kctx &P, LT &L, stat_slot *slots,
 			     const uint4 *nhf_lds, uint32_t n_local, uint32_t c, uint32_t lane) {
 	for (uint32_t k = c; k < n_local; k += C::COMPUTE) {
 		const uint32_t s = k % C::SLOTS;
@@ -399,19 +426,7 @@ __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params 
 	}
 	__syncthreads();
 
-	const uint32_t n_tiles = (A.n + 63) >> 6;
-	uint32_t n_local;
-	if (A.order == 2) {
-		const uint32_t x = blockIdx.x & 7, l = blockIdx.x >> 3, per = gridDim.x >> 3;
-		const uint32_t lo = x * A.chunk + l, hi = min((x + 1) * A.chunk, n_tiles);
-		n_local = lo < hi ? (hi - 1 - lo) / per + 1 : 0;
-	} else if (A.order == 3) {
-		const uint32_t S = gridDim.x * A.chunk, r = n_tiles % S, b0 = blockIdx.x * A.chunk;
-		n_local = n_tiles / S * A.chunk + (r > b0 ? min(A.chunk, r - b0) : 0);
-	} else if (A.chunk)
-		n_local = blockIdx.x * A.chunk < n_tiles ? min(A.chunk, n_tiles - blockIdx.x * A.chunk) : 0;
-	else
-		n_local = blockIdx.x < n_tiles ? (n_tiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+	const uint32_t n_local = local_tiles(A);
 	if (wv < C::LOADERS) {
 		ring_loader<C, NT, PTRS>(A, L, n_local, wv, lane);
 	} else if (wv < C::LOADERS + C::STORERS) {
@@ -442,6 +457,122 @@ __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params 
 		ring_trace[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 	}
 #endif
+}
+
+// ---- the resident kernel ----------------------------------------------------
+// One long-lived launch per context (gr_hip.cpp, knob "resident"): workgroup
+// r serves descriptor ring r (fwd4_res_desc in pinned host memory). It waits
+// for the ring's next seq, copies that batch's fwd4_params into LDS, runs the
+// three roles over the whole batch as one workgroup (tile order 0, wgs 1),
+// makes the batch's writes visible to the host and stores the seq into
+// done[r]. No launch and no hardware queue per batch: what small host batches
+// pay otherwise. A workgroup idle past its lifetime sets
+// *stop, and every workgroup leaves at *stop (host's or that one's) after the
+// batch it is running (its waits are bounded as in a launch), so the grid
+// always drains; each then marks its ring's exited word. Counters are the
+// hand-back's (no STATS variant), adjacencies are read from the global
+// tables (nothing staged).
+typedef ring_cfg2 ring_cfg_res;
+
+__device__ __forceinline__ uint64_t sys_load64(const uint64_t *p) {
+	return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void __launch_bounds__(ring_cfg_res::WAVES * 64) gr_fwd4_resident(const fwd4_res_params R) {
+	typedef ring_cfg_res C;
+	__shared__ __attribute__((aligned(16))) ring_lds<C, true> L;
+	__shared__ __attribute__((aligned(16))) fwd4_params A;
+	__shared__ fwd4_edges edges;
+	__shared__ uint64_t seq_s;
+	__shared__ uint32_t go;
+	const uint32_t tid = threadIdx.x, lane = tid & 63;
+	const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+	uint64_t *done = R.done + (size_t)blockIdx.x * R.stride;
+	const fwd4_res_desc *ring = R.descs + (size_t)blockIdx.x * R.ndesc;
+	const uint64_t until = __builtin_amdgcn_s_memrealtime() + R.lifetime;
+	if (tid == 0)
+		seq_s = sys_load64(done) + 1; // a relaunch resumes after the last batch done
+	for (;;) {
+		if (tid == 0) {
+			const uint64_t want = seq_s;
+			const fwd4_res_desc *d = ring + want % R.ndesc;
+			uint32_t g = 0;
+			for (;;) {
+				if (__hip_atomic_load(R.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
+					break; // every workgroup leaves: the host relaunches once all have
+				if (sys_load64(&d->seq) == want) {
+					g = 1;
+					break;
+				}
+				if (__builtin_amdgcn_s_memrealtime() > until) { // idle past the lifetime
+					__hip_atomic_store(R.stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+					break;
+				}
+				__builtin_amdgcn_s_sleep(8);
+			}
+			go = g;
+		}
+		__syncthreads();
+		if (!go)
+			break;
+		{ // the batch's parameters, from host memory
+			const uint32_t *src = reinterpret_cast<const uint32_t *>(&ring[seq_s % R.ndesc].A);
+			uint32_t *dst = reinterpret_cast<uint32_t *>(&A);
+			for (uint32_t i = tid; i < sizeof(fwd4_params) / 4; i += C::WAVES * 64)
+				dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+		}
+		__syncthreads();
+		// the edge table of the generation this batch names
+		for (uint32_t i = tid; i < sizeof(fwd4_edges); i += C::WAVES * 64)
+			reinterpret_cast<uint8_t *>(&edges)[i] = reinterpret_cast<const uint8_t *>(&A.T->edges)[i];
+		if (tid < C::SLOTS) {
+			L.ready[tid] = 0;
+			L.done[tid] = 0;
+			L.free_[tid] = 0;
+		}
+		if (tid == 0) {
+			L.abort = 0;
+			L.spin_max = A.spin_max ? A.spin_max : RING_SPIN_MAX;
+		}
+		__syncthreads();
+		const uint32_t n_local = local_tiles(A);
+		const bool ptrs = A.ptrs != 0;
+		if (wv < C::LOADERS) {
+			if (ptrs)
+				ring_loader<C, false, true>(A, L, n_local, wv, lane);
+			else
+				ring_loader<C, false, false>(A, L, n_local, wv, lane);
+		} else if (wv < C::LOADERS + C::STORERS) {
+			if (ptrs)
+				ring_storer<C, false, true>(A, L, n_local, wv - C::LOADERS, lane);
+			else
+				ring_storer<C, false, false>(A, L, n_local, wv - C::LOADERS, lane);
+		} else {
+			const kctx P = make_kctx(A, &edges);
+			if (ptrs)
+				ring_compute<C, false, true>(A, P, L, nullptr, nullptr, n_local, wv - C::LOADERS - C::STORERS, lane);
+			else
+				ring_compute<C, false, false>(A, P, L, nullptr, nullptr, n_local, wv - C::LOADERS - C::STORERS, lane);
+		}
+		wait_vmcnt<0>(); // this wave's stores of the batch are done
+		__syncthreads();
+		if (tid == 0) {
+			if (L.abort && A.err != nullptr)
+				__hip_atomic_store(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			// release at system scope: the batch's lines and verdicts before its seq
+			__hip_atomic_store(done, seq_s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+			seq_s++;
+		}
+		__syncthreads();
+	}
+	if (tid == 0) // this ring's workgroup is gone: the host may relaunch once every ring's is
+		__hip_atomic_store(R.exited + (size_t)blockIdx.x * R.stride, R.launch_id, __ATOMIC_RELEASE,
+				   __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+extern "C" hipError_t gr_fwd4_resident_launch(const fwd4_res_params *R, uint32_t rings, hipStream_t s) {
+	hipLaunchKernelGGL(gr_fwd4_resident, dim3(rings), dim3(ring_cfg_res::WAVES * 64), 0, s, *R);
+	return hipGetLastError();
 }
 
 typedef void (*fwd4_rfn)(const fwd4_params);

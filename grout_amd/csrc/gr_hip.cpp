@@ -31,6 +31,7 @@
 
 extern "C" hipError_t gr_fwd4_ring_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant, int cfg);
 extern "C" int gr_fwd4_ring_occupancy(int variant, int cfg, uint32_t nhf_lds);
+extern "C" hipError_t gr_fwd4_resident_launch(const fwd4_res_params *R, uint32_t rings, hipStream_t s);
 extern "C" uint32_t gr_fwd4_ring_nhf_max(void);
 extern "C" int gr_fwd4_ring_ncfg(void);
 #define RING_WG_PER_CU 2 // default workgroups per CU of the ring kernel (measured)
@@ -186,6 +187,8 @@ struct node_slot {
 	void *const *mb0 = nullptr;
 	const gr_hip_mbuf_layout *lay = nullptr;
 	bool kcount = false; // its kernel counts the per-iface counters (not the hand-back)
+	bool resident = false; // posted to the resident kernel (res_post): done at res_seq
+	uint64_t res_seq = 0;
 };
 
 } // namespace
@@ -226,6 +229,9 @@ struct alignas(128) gr_hip_queue {
 	hipEvent_t snap_ev = nullptr;
 	bool snap_pending = false;
 	uint64_t node_counted = 0, snap_counted = 0; // node walks launched with counters; covered by a snapshot
+	int ring = -1; // the resident kernel's ring this queue posts to (-1: none yet)
+	uint64_t res_seq = 0; // the last seq posted on it
+	uint64_t res_retire = 0; // posted before the last FIB publication (retire_wait)
 };
 
 struct host_range { // gr_hip_host_register
@@ -294,6 +300,23 @@ struct gr_hip_ctx {
 	int untimed; // measurements: no HIP events around launches (gr_hip_queue_kernel_ms sees none)
 	uint32_t time_every; // HIP events around every N-th submit of a queue only (0, 1 = every one)
 	std::vector<host_range> hregs; // registered host memory, by host address
+	// the resident kernel (knob "resident", see res_post): descriptor rings,
+	// done and exited words (pinned host memory), its stream and launch state
+	int res_on;
+	uint32_t res_rings; // workgroups of a launch = rings (knob "resident_rings")
+	uint32_t res_ms; // lifetime of an idle workgroup (knob "resident_ms")
+	fwd4_res_desc *res_desc;
+	uint64_t *res_done, *res_exited;
+	uint32_t *res_stop;
+	fwd4_res_desc *res_desc_d; // their device addresses
+	uint64_t *res_done_d, *res_exited_d;
+	uint32_t *res_stop_d;
+	hipStream_t res_s;
+	hipEvent_t res_ev;
+	std::atomic<bool> res_live; // launched, and not yet seen to have left
+	uint64_t res_launch; // id of the last launch (0: none)
+	std::vector<uint8_t> res_taken; // rings held by a queue
+	std::mutex res_mu;
 	// FIB publication (see retire_wait): two pinned staging buffers used in
 	// turn by the commits (fib_mu), each with the event of its last upload,
 	// and per generation the event of the upload that made it complete
@@ -319,10 +342,15 @@ struct gr_hip_ctx {
 // ---------------------------------------------------------------------------
 
 // Make the control stream wait for everything submitted on every queue.
+static int res_wait(gr_hip_queue *q, uint64_t seq);
+static void res_free(gr_hip_ctx *c);
+
 static int quiesce(gr_hip_ctx *c) {
 	for (gr_hip_queue *q : c->queues) {
 		HCK(hipEventRecord(q->quiesce, q->s));
 		HCK(hipStreamWaitEvent(c->ctl, q->quiesce, 0));
+		if (const int r = res_wait(q, q->res_seq)) // its resident batches: on the host
+			return r;
 	}
 	return 0;
 }
@@ -793,6 +821,9 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->tile_order = 0;
 	c->tile_run = 16;
 	c->stage_min_tiles = 4;
+	c->res_on = 0;
+	c->res_rings = 16;
+	c->res_ms = 50;
 	c->spin_max = 0;
 	c->untimed = 0;
 	c->time_every = 1;
@@ -817,6 +848,7 @@ extern "C" int gr_hip_fini(gr_hip_ctx_t *c) {
 	hipSetDevice(c->dev);
 	while (!c->queues.empty())
 		gr_hip_queue_destroy(c->queues.back());
+	res_free(c);
 	if (c->ctl)
 		hipStreamSynchronize(c->ctl); // the last commits' uploads
 	for (const host_range &r : c->hregs)
@@ -1146,6 +1178,12 @@ extern "C" int gr_hip_reta_set(gr_hip_ctx_t *c, uint32_t first, const uint32_t *
 // returns once the work is enqueued. Route adds and deletes only touch the
 // host RIB (fib_mu).
 
+static uint64_t now_ns_host() {
+	struct timespec t;
+	clock_gettime(CLOCK_MONOTONIC, &t);
+	return (uint64_t)t.tv_sec * 1000000000u + (uint64_t)t.tv_nsec;
+}
+
 static uint64_t now_us() {
 	struct timespec t;
 	clock_gettime(CLOCK_MONOTONIC, &t);
@@ -1155,8 +1193,11 @@ static uint64_t now_us() {
 // Wait, on the control stream, for every launch submitted before the last
 // publication.
 static int retire_wait(gr_hip_ctx *c) {
-	for (gr_hip_queue *q : c->queues)
+	for (gr_hip_queue *q : c->queues) {
 		HCK(hipStreamWaitEvent(c->ctl, q->retire, 0));
+		if (const int r = res_wait(q, q->res_retire)) // resident batches posted before it: on the host
+			return r;
+	}
 	return 0;
 }
 
@@ -1180,8 +1221,10 @@ static int publish(gr_hip_ctx *c, uint32_t g, F then) {
 	c->serial++;
 	then();
 	count_v6(c);
-	for (gr_hip_queue *q : c->queues)
+	for (gr_hip_queue *q : c->queues) {
 		HCK(hipEventRecord(q->retire, q->s));
+		q->res_retire = q->res_seq;
+	}
 	return 0;
 }
 
@@ -1897,6 +1940,11 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 	for (host_slot &h : q->hs)
 		if (h.s)
 			hipStreamSynchronize(h.s);
+	if (q->ring >= 0) {
+		res_wait(q, q->res_seq); // its resident batches, then the ring is free again
+		std::lock_guard<std::mutex> rl(c->res_mu);
+		c->res_taken[(size_t)q->ring] = 0;
+	}
 	{
 		// unlink first: a commit running on another thread reaches the
 		// queue's stream and events through this list (quiesce(),
@@ -2080,6 +2128,200 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 	return 0;
 }
 
+// ---------------------------------------------------------------------------
+// the resident kernel (knob "resident"; fwd4_ring.hip gr_fwd4_resident)
+// ---------------------------------------------------------------------------
+// A queue's node batches go to the context's resident kernel instead of a
+// launch each: the batch's fwd4_params into the next descriptor of the
+// queue's ring (pinned host memory), then its seq. The kernel's workgroup for
+// that ring runs it and stores the seq into the ring's done word once the
+// results are in host memory; the node polls that word (a load, no runtime
+// call, no hardware queue held per batch: DESIGN.md §6.3). A workgroup idle
+// past the lifetime sets the stop word and all leave after their batch;
+// whoever then finds a batch waiting launches the kernel again, once every
+// ring's exited word carries the last launch's id, so that one workgroup at
+// most ever serves a ring. Posts wait for the FIB generation's upload on the
+// host (launches make their stream wait); commits and quiesce wait, on the
+// host, for the batches posted before them (retire_wait, quiesce).
+#define RES_NDESC 4 // descriptors per ring (GR_HIP_NODE_DEPTH batches in flight at most)
+#define RES_STRIDE 8 // uint64_t per ring in the done / exited words: a 64-byte line each
+#define RES_WAIT_NS (10ull * 1000000000ull) // a batch not done after this: -ETIMEDOUT
+
+static uint64_t res_word(const uint64_t *w, int ring) {
+	return __atomic_load_n(w + (size_t)ring * RES_STRIDE, __ATOMIC_ACQUIRE);
+}
+
+static void res_free(gr_hip_ctx *c) {
+	if (c->res_live && c->res_stop != nullptr) {
+		__atomic_store_n(c->res_stop, 1u, __ATOMIC_RELEASE);
+		hipEventSynchronize(c->res_ev); // every workgroup leaves after its batch
+		c->res_live = false;
+	}
+	if (c->res_ev != nullptr)
+		hipEventDestroy(c->res_ev);
+	if (c->res_s != nullptr)
+		hipStreamDestroy(c->res_s);
+	hipHostFree(c->res_desc);
+	hipHostFree(c->res_done);
+	hipHostFree(c->res_exited);
+	hipHostFree(c->res_stop);
+	c->res_ev = nullptr;
+	c->res_s = nullptr;
+	c->res_desc = nullptr;
+	c->res_done = c->res_exited = nullptr;
+	c->res_stop = nullptr;
+	(void)hipGetLastError();
+}
+
+// The rings, their words and the kernel's stream, on first use (res_mu held).
+static int res_setup(gr_hip_ctx *c) {
+	if (c->res_desc != nullptr)
+		return 0;
+	const size_t nd = sizeof(fwd4_res_desc) * c->res_rings * RES_NDESC;
+	const size_t nw = sizeof(uint64_t) * c->res_rings * RES_STRIDE;
+	const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+	int least = 0, greatest = 0;
+	hipDeviceGetStreamPriorityRange(&least, &greatest);
+	if (hipHostMalloc(reinterpret_cast<void **>(&c->res_desc), nd, fl) != hipSuccess
+	    || hipHostMalloc(reinterpret_cast<void **>(&c->res_done), nw, fl) != hipSuccess
+	    || hipHostMalloc(reinterpret_cast<void **>(&c->res_exited), nw, fl) != hipSuccess
+	    || hipHostMalloc(reinterpret_cast<void **>(&c->res_stop), 64, fl) != hipSuccess
+	    || hipHostGetDevicePointer(reinterpret_cast<void **>(&c->res_desc_d), c->res_desc, 0) != hipSuccess
+	    || hipHostGetDevicePointer(reinterpret_cast<void **>(&c->res_done_d), c->res_done, 0) != hipSuccess
+	    || hipHostGetDevicePointer(reinterpret_cast<void **>(&c->res_exited_d), c->res_exited, 0) != hipSuccess
+	    || hipHostGetDevicePointer(reinterpret_cast<void **>(&c->res_stop_d), c->res_stop, 0) != hipSuccess
+	    // its own priority: a hardware queue of its own, not shared with the
+	    // streams whose work would wait behind a resident launch
+	    || hipStreamCreateWithPriority(&c->res_s, hipStreamNonBlocking, greatest) != hipSuccess
+	    || hipEventCreateWithFlags(&c->res_ev, hipEventDisableTiming) != hipSuccess) {
+		(void)hipGetLastError();
+		res_free(c);
+		return -ENOMEM;
+	}
+	memset(c->res_desc, 0, nd);
+	memset(c->res_done, 0, nw);
+	memset(c->res_exited, 0, nw);
+	*c->res_stop = 0;
+	c->res_taken.assign(c->res_rings, 0);
+	return 0;
+}
+
+// Launch the kernel when none runs (res_mu held). A launch that is leaving
+// (stop set) is relaunched only once all its workgroups have left.
+static int res_ensure(gr_hip_ctx *c) {
+	if (c->res_live) {
+		if (__atomic_load_n(c->res_stop, __ATOMIC_ACQUIRE) == 0)
+			return 0;
+		for (uint32_t r = 0; r < c->res_rings; r++)
+			if (res_word(c->res_exited, (int)r) != c->res_launch)
+				return 0; // still leaving: a later poll relaunches
+		c->res_live = false;
+	}
+	__atomic_store_n(c->res_stop, 0u, __ATOMIC_RELEASE);
+	fwd4_res_params R{};
+	R.descs = c->res_desc_d;
+	R.done = c->res_done_d;
+	R.exited = c->res_exited_d;
+	R.stop = c->res_stop_d;
+	R.lifetime = (uint64_t)c->res_ms * 100000u; // s_memrealtime: 100 MHz
+	R.launch_id = ++c->res_launch;
+	R.ndesc = RES_NDESC;
+	R.stride = RES_STRIDE;
+	HCK(gr_fwd4_resident_launch(&R, c->res_rings, c->res_s));
+	HCK(hipEventRecord(c->res_ev, c->res_s));
+	c->res_live = true;
+	return 0;
+}
+
+// A waiting batch and a kernel that left: launch it again.
+static int res_kick(gr_hip_ctx *c) {
+	if (!__atomic_load_n(c->res_stop, __ATOMIC_ACQUIRE) && c->res_live)
+		return 0;
+	std::lock_guard<std::mutex> l(c->res_mu);
+	return res_ensure(c);
+}
+
+// A ring for queue q, on its first resident batch: false when none is free.
+static bool res_take(gr_hip_queue *q) {
+	if (q->ring >= 0)
+		return true;
+	gr_hip_ctx *c = q->ctx;
+	std::lock_guard<std::mutex> l(c->res_mu);
+	if (res_setup(c) != 0)
+		return false;
+	for (uint32_t r = 0; r < c->res_rings; r++) {
+		if (!c->res_taken[r]) {
+			c->res_taken[r] = 1;
+			q->ring = (int)r;
+			q->res_seq = q->res_retire = res_word(c->res_done, (int)r); // the ring's numbering goes on
+			return true;
+		}
+	}
+	return false;
+}
+
+static bool res_is_done(const gr_hip_queue *q, uint64_t seq) {
+	return res_word(q->ctx->res_done, q->ring) >= seq;
+}
+
+// Wait, on the host, until the ring's batch `seq` is done.
+static int res_wait(gr_hip_queue *q, uint64_t seq) {
+	if (q->ring < 0 || res_is_done(q, seq))
+		return 0;
+	gr_hip_ctx *c = q->ctx;
+	const uint64_t t0 = now_ns_host();
+	for (uint32_t spin = 1; !res_is_done(q, seq); spin++) {
+		if ((spin & 1023) == 0) {
+			if (const int r = res_kick(c))
+				return r;
+			const hipError_t e = hipEventQuery(c->res_ev);
+			if (e != hipSuccess && e != hipErrorNotReady) {
+				(void)hipGetLastError();
+				return -EIO;
+			}
+			if (now_ns_host() - t0 > RES_WAIT_NS)
+				return -ETIMEDOUT;
+		}
+		__builtin_ia32_pause();
+	}
+	return 0;
+}
+
+// Post batch b (device addresses) on q's ring; c->mu held shared.
+static int res_post(gr_hip_queue *q, const gr_hip_batch *b) {
+	gr_hip_ctx *c = q->ctx;
+	const uint32_t g = c->gen;
+	if (q->seen_serial != c->serial) { // the generation's upload (launch(): a stream wait)
+		HCK(hipEventSynchronize(c->ready_ev[g]));
+		q->seen_serial = c->serial;
+	}
+	const uint64_t seq = q->res_seq + 1;
+	if (seq > res_word(c->res_done, q->ring) + RES_NDESC)
+		return -EBUSY; // (not reached: GR_HIP_NODE_DEPTH < RES_NDESC)
+	fwd4_params A{};
+	A.in = static_cast<const uint8_t *>(b->in_frames);
+	A.out = static_cast<uint8_t *>(b->out_lines);
+	A.meta = b->meta;
+	A.verdicts = b->verdicts;
+	A.T = c->d_tables[g];
+	A.n = b->n;
+	A.in_stride = b->in_stride;
+	A.out_stride = b->out_stride;
+	A.readable = (b->flags & GR_HIP_BATCH_F_LINES_ONLY) ? GR_HIP_LINE
+		: (b->flags & GR_HIP_BATCH_F_FRAME_PTRS)    ? UINT32_MAX
+							    : b->in_stride;
+	A.spin_max = c->spin_max;
+	A.err = q->d_err;
+	A.wg0 = 0;
+	A.wgs = 1; // the ring's one workgroup takes every tile
+	A.ptrs = (b->flags & GR_HIP_BATCH_F_FRAME_PTRS) ? 1 : 0;
+	fwd4_res_desc &d = c->res_desc[(size_t)q->ring * RES_NDESC + seq % RES_NDESC];
+	memcpy(&d.A, &A, sizeof(A));
+	__atomic_store_n(&d.seq, seq, __ATOMIC_RELEASE); // after A
+	q->res_seq = seq;
+	return res_kick(c);
+}
+
 extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 	if (c == nullptr || key == nullptr)
 		return -EINVAL;
@@ -2122,6 +2364,18 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < 0 || value > 3)
 			return -EINVAL;
 		c->tile_order = value;
+	} else if (strcmp(key, "resident") == 0) { // node batches through the resident kernel (res_post)
+		c->res_on = value != 0;
+	} else if (strcmp(key, "resident_rings") == 0) { // before the first resident batch only
+		if (value < 1 || value > 256 || c->res_desc != nullptr)
+			return -EINVAL;
+		c->res_rings = (uint32_t)value;
+	} else if (strcmp(key, "resident_ms") == 0) {
+		if (value < 1 || value > 10000)
+			return -EINVAL;
+		c->res_ms = (uint32_t)value;
+	} else if (strcmp(key, "resident_launches") == 0) { // read
+		return (int)c->res_launch;
 	} else if (strcmp(key, "stage_min_tiles") == 0) {
 		if (value < 0)
 			return -EINVAL;
@@ -2653,6 +2907,7 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 	w.sync = true;
 	w.r = 0;
 	w.kcount = false;
+	w.resident = false;
 	if (n == 0) { // nothing to send: finishes at once
 		q->nw_count++;
 		return 0;
@@ -2688,8 +2943,14 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 				  GR_HIP_BATCH_F_LINES_ONLY | GR_HIP_BATCH_F_FRAME_PTRS};
 		// after everything already submitted on the queue, like gr_hip_fwd4_host;
 		// no timing events (the walk's own completion event is enough)
-		if ((r = launch(q, q->s, &b, false)) < 0)
+		if (c->res_on && res_take(q)) {
+			if ((r = res_post(q, &b)) < 0)
+				return r;
+			w.resident = true;
+			w.res_seq = q->res_seq;
+		} else if ((r = launch(q, q->s, &b, false)) < 0) {
 			return r;
+		}
 		enqueued = true;
 	} else {
 		if (!w.lines_in) { // "node_ptrs" on, but not every frame is registered: stage the lines now
@@ -2711,8 +2972,14 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 			gr_hip_batch b = {w.d_lines, w.d_out, static_cast<const gr_hip_pkt_meta *>(w.d_meta),
 					  static_cast<gr_hip_verdict *>(w.d_v), ns, GR_HIP_LINE, GR_HIP_PREFIX,
 					  GR_HIP_BATCH_F_LINES_ONLY | GR_HIP_BATCH_F_PREFIX32};
-			if ((r = launch(q, q->s, &b, false)) < 0)
+			if (c->res_on && res_take(q)) {
+				if ((r = res_post(q, &b)) < 0)
+					return r;
+				w.resident = true;
+				w.res_seq = q->res_seq;
+			} else if ((r = launch(q, q->s, &b, false)) < 0) {
 				return r;
+			}
 			enqueued = true;
 		}
 		lap(GR_HIP_NODE_PROF_LAUNCH);
@@ -2722,11 +2989,13 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 		}
 	}
 	if (enqueued) {
-		HCK(hipEventRecord(w.done, q->s));
+		if (!w.resident)
+			HCK(hipEventRecord(w.done, q->s));
 		w.sync = false;
 	}
-	// the kernel counted the walk's packets per iface (launch's "stats" variant)
-	w.kcount = c->stats_on && q->d_stats != nullptr;
+	// the kernel counted the walk's packets per iface (launch's "stats" variant;
+	// the resident kernel counts none: the hand-back does)
+	w.kcount = c->stats_on && q->d_stats != nullptr && !w.resident;
 	if (w.kcount)
 		q->node_counted++;
 	lap(GR_HIP_NODE_PROF_RECORD);
@@ -2770,7 +3039,10 @@ static int node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np,
 	if (direct != nullptr)
 		direct->meta = w.own ? w.meta : nullptr; // no views: the hand-back reads the mbufs
 	uint64_t t_prof = prof_now();
-	if (!w.sync) {
+	if (!w.sync && w.resident) {
+		if ((r = res_wait(q, w.res_seq)) == 0)
+			r = q_check(q);
+	} else if (!w.sync) {
 		hipSetDevice(c->dev);
 		HCK(hipEventSynchronize(w.done));
 		// the queue's error word covers every kernel in flight on it: which
@@ -2931,6 +3203,11 @@ extern "C" int gr_hip_node_pending(gr_hip_queue_t *q, int *ready) {
 			const node_slot &w = q->nw[q->nw_head];
 			if (w.sync) {
 				*ready = 1;
+			} else if (w.resident) { // a load of the ring's done word; a kernel that left is relaunched
+				if (res_is_done(q, w.res_seq))
+					*ready = 1;
+				else if (const int r = res_kick(q->ctx))
+					return r;
 			} else {
 				hipSetDevice(q->ctx->dev);
 				const hipError_t e = hipEventQuery(w.done);

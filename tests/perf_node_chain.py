@@ -126,6 +126,8 @@ def main():
     ap.add_argument("--passes", type=int, default=8, help="with --recycle: passes over each worker's share")
     ap.add_argument("--lcores", default="spread", choices=["none", "allowed", "spread", "socket"])
     ap.add_argument("--out", default=None, help="also append the lines to this JSONL file")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="gr_hip_tune knobs of the GPU node's contexts, e.g. resident=1 (repeatable)")
     args = ap.parse_args()
 
     import test_graph_walk as G
@@ -165,6 +167,9 @@ def main():
     fp = G.FanOutPath(L)
     topo = T.config_fullview()
     fp.load(topo)
+    for kv in args.tune:
+        k, v = kv.split("=")
+        fp.tune(k, int(v))
     ifs = np.ascontiguousarray(topo.ifaces[topo.ifaces["id"] != 0])
     nh = np.ascontiguousarray(topo.nh[1:topo.n_nh + 1])
     assert L.gh_set_objects(ifs.ctypes.data, len(ifs), nh.ctypes.data, 1, len(nh)) == 0
@@ -234,7 +239,7 @@ def main():
             assert int(hist.sum()) == pk, (mode, int(hist.sum()), pk)
             lat[mode] = percentiles(hist.astype(np.float64), cpn, floor)
         line = {"threads": k, "packets": pk, "lcores": args.lcores, "cpus": cpus, "recycle": args.recycle,
-                "passes": per, "batch": batch, "reps": args.reps,
+                "passes": per, "batch": batch, "reps": args.reps, "tune": args.tune,
                 "workload": "config3 full view (fib_inject 1M routes), 64 B, seeded stream 0x67720002"}
         for mode in ("gpu", "chain"):
             line[mode] = {"mpps": round(pk / med[mode] / 1e6, 1),

@@ -1,0 +1,219 @@
+# SPDX-License-Identifier: BSD-3-Clause
+"""The resident kernel (knob "resident", fwd4_ring.hip gr_fwd4_resident):
+node batches posted to descriptor rings in pinned host memory and taken by a
+long-lived kernel instead of a launch each (gr_hip.cpp res_post). Every test
+here is a node test of test_node_shim.py / test_graph_walk.py run through it:
+the same mbufs, lines, verdicts and counters as the oracle (the counters are
+the hand-back's: the resident kernel counts none), plus what is its own: a
+kernel that left (lifetime over) is relaunched and resumes the ring, a kernel
+that gives up hands back what it did not reach, FIB publications and quiesce
+wait for the batches posted before them."""
+import time
+
+import numpy as np
+import pytest
+
+import oracle
+from grout_amd import abi
+from grout_amd import synth as S
+from grout_amd import topology as T
+from test_node_shim import compare_mbufs, mbufs_for
+
+
+@pytest.fixture
+def resident(fastpath):
+    assert fastpath.tune("resident", 1) == 0
+    yield fastpath
+    fastpath.tune("resident", 0)
+    fastpath.tune("resident_ms", 50)
+
+
+def _pipelined(fp, q, m, cuts):
+    """Walks [cuts[i], cuts[i+1]) started two at a time, finished in order."""
+    parts = [m[a:b] for a, b in zip(cuts, cuts[1:])]
+    tot = np.zeros(1, dtype=abi.NODE_STATS_DT)[0]
+    q.node_start(parts[0])
+    for k in range(1, len(parts) + 1):
+        if k < len(parts):
+            q.node_start(parts[k])
+        got, ns = q.node_finish()
+        assert got is parts[k - 1] and q.unfinished == 0
+        tot["packets"] += ns["packets"]
+        tot["calls"] += ns["calls"]
+    return tot
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ptrs", [0, 1], ids=["staged", "by_address"])
+def test_resident_pipelined_walks(resident, ptrs):
+    """Walks pipelined two deep through the resident kernel end as the oracle
+    leaves them: mbufs, frames, node and per-iface counters."""
+    from golden_util import fresh_fastpath_state
+    fp = resident
+    topo = T.config_fullview(count=100_000)
+    fr, me = S.stream(50_000, 0xD1F, routes=topo.route_array())
+    fresh_fastpath_state(fp, topo)
+    lines, v, st, want, ns_want = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
+    bufs, m = mbufs_for(fr, me)
+    L = fp.lib
+    if ptrs:
+        abi.check("gr_hip_host_register", L.gr_hip_host_register(fp.h, bufs.ctypes.data, bufs.nbytes))
+    q = fp.queue()
+    try:
+        fp.tune("node_ptrs", ptrs)
+        launches0 = fp.tune("resident_launches")
+        tot = _pipelined(fp, q, m, [0, 64, 64 * 100, 64 * 101, 64 * 400, 64 * 401 + 64, len(m)])
+        compare_mbufs(m, want, bufs, lines)
+        assert np.array_equal(tot["packets"], ns_want["packets"])
+        assert np.array_equal(tot["calls"], ns_want["calls"])
+        assert np.array_equal(q.node_iface_stats(), st)
+        assert not q.stats()["rx_packets"].any()  # nothing counted by a kernel
+        assert fp.tune("resident_launches") >= max(launches0, 1)
+    finally:
+        fp.tune("node_ptrs", 0)
+        if ptrs:
+            abi.check("gr_hip_host_unregister", L.gr_hip_host_unregister(fp.h, bufs.ctypes.data))
+        q.close()
+
+
+@pytest.mark.gpu
+def test_resident_relaunch(resident):
+    """A 2 ms lifetime: between walks the idle kernel leaves; the next batch
+    launches it again and its workgroup resumes the ring after the last seq
+    done. Every walk is still the oracle's."""
+    from golden_util import fresh_fastpath_state
+    fp = resident
+    assert fp.tune("resident_ms", 2) == 0
+    topo = T.config_fullview(count=50_000)
+    fr, me = S.stream(8 * 3000, 0xD20, routes=topo.route_array())
+    fresh_fastpath_state(fp, topo)
+    lines, v, st, want, ns_want = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
+    bufs, m = mbufs_for(fr, me)
+    q = fp.queue()
+    try:
+        l0 = fp.tune("resident_launches")
+        for k in range(8):
+            part = m[k * 3000:(k + 1) * 3000]
+            q.node_start(part)
+            got, _ = q.node_finish()
+            assert got is part and q.unfinished == 0
+            time.sleep(0.02)  # idle past the lifetime: the kernel leaves
+        compare_mbufs(m, want, bufs, lines)
+        assert np.array_equal(q.node_iface_stats(), st)
+        assert fp.tune("resident_launches") - l0 >= 4  # relaunched (at most once per walk)
+    finally:
+        q.close()
+
+
+@pytest.mark.gpu
+def test_resident_give_up_hands_back(resident):
+    """A resident kernel that gives up (spin_max 1) reports it once (the
+    queue's error word), and the node hands back what it finished and punts
+    the rest untouched, as after a launch."""
+    from golden_util import fresh_fastpath_state
+    fp = resident
+    topo = T.config_single_route()
+    n = 1 << 16
+    fr, me = S.stream(n, 0xD21, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    fresh_fastpath_state(fp, topo)
+    lines, v, st, want, _ = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
+    bufs, m = mbufs_for(fr, me)
+    orig_bufs, orig_m = bufs.copy(), m.copy()
+    q = fp.queue()
+    try:
+        assert fp.tune("spin_max", 1) == 0
+        q.node_start(m)
+        q.node_finish()
+    finally:
+        fp.tune("spin_max", 0)
+    punt = m["edge"] == abi.EDGE["punt"]
+    assert q.unfinished == punt.sum()
+    assert np.array_equal(bufs[punt], orig_bufs[punt])
+    orig_m["edge"] = abi.EDGE["punt"]
+    assert np.array_equal(m[punt], orig_m[punt])
+    done = ~punt
+    compare_mbufs(m[done], want[done], bufs[done], lines[done])
+    # the queue goes on: a normal walk after it
+    q.node_start(m[:0])
+    q.node_finish()
+    q.close()
+
+
+@pytest.mark.gpu
+def test_resident_route_change_between_walks(resident):
+    """A route committed while the queue's ring holds a batch: the batch
+    posted before the commit reads the old FIB whole (the commit waits, on
+    the host, for batches posted before the previous publication before it
+    rewrites that copy), the walk after it the new one."""
+    import copy
+    from golden_util import fresh_fastpath_state
+    fp = resident
+    topo = T.config_fullview(count=20_000)
+    fr, me = S.stream(20_000, 0xD22, routes=topo.route_array())
+    fresh_fastpath_state(fp, topo)
+    dst = int.from_bytes(bytes(fr[0, 30:34]), "big")
+    nh_new = int(topo.route_array()["nh"][1])
+    r = np.zeros(1, dtype=abi.ROUTE_DT)
+    r[0] = (dst, 32, 0, 1, nh_new)
+    topo2 = copy.deepcopy(topo)
+    topo2.routes.append(r)
+    lines_a, _, _, want_a, _ = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
+    lines_b, _, _, want_b, _ = oracle.Oracle(topo2).process_mbufs(fr, me, lines_only=True)
+    assert not np.array_equal(lines_a, lines_b)  # the new route changes some packets
+    bufs_a, m_a = mbufs_for(fr, me)
+    bufs_b, m_b = mbufs_for(fr, me)
+    q = fp.queue()
+    try:
+        q.node_start(m_a)  # on the GPU across the commit below
+        fp.route_add(r, replace=True)
+        fp.fib_commit(1)
+        got, _ = q.node_finish()
+        assert got is m_a and q.unfinished == 0
+        compare_mbufs(m_a, want_a, bufs_a, lines_a)
+        q.node_start(m_b)
+        got, _ = q.node_finish()
+        assert got is m_b and q.unfinished == 0
+        compare_mbufs(m_b, want_b, bufs_b, lines_b)
+    finally:
+        q.close()
+        import golden_util
+        golden_util._loaded["key"] = None  # the FIB changed under fresh_fastpath_state: reload next time
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ptrs", [0, 1], ids=["staged", "by_address"])
+def test_resident_graph_walk_corpus(ptrs):
+    """Every edge, in whole rte_graph walks of the grout module's node, its
+    batches through the resident kernel: grout's mbufs, node statistics and
+    folded per-iface counters as the oracle's."""
+    import test_graph_walk as G
+    import scenarios as SC
+    G.lib().gh_set_pin(1)
+    fp = G.graph_ctx()
+    fp.tune("resident", 1)
+    fp.tune("node_ptrs", ptrs)
+    t, _ = SC.corpus_topology()
+    fr, me, lab = SC.corpus_arrays()
+    keep = ((me["vlan_ck"] >> 12) & 3) != 3
+    fr, me, lab = fr[keep], me[keep], [x for x, k in zip(lab, keep) if k]
+    try:
+        got = G.check_walk(t, fr, me, lab)
+    finally:
+        fp.tune("node_ptrs", 0)
+        fp.tune("resident", 0)
+    assert len(set(got["edge"])) > 20
+
+
+@pytest.mark.gpu
+def test_resident_graph_control_plane_churn():
+    """test_graph_walk's control-plane churn (nexthops and routes changed
+    between and during walks, quiesce on every change) with the batches on the
+    resident kernel: quiesce and the FIB publications wait for them."""
+    import test_graph_walk as G
+    fp = G.graph_ctx()
+    fp.tune("resident", 1)
+    try:
+        G.test_graph_walk_control_plane_churn(1, 1)
+        G.test_graph_walk_stream_batches(2)
+    finally:
+        fp.tune("resident", 0)
