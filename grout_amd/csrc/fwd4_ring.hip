@@ -463,9 +463,9 @@ __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params 
 // One long-lived launch per context (gr_hip.cpp, knob "resident"): workgroup
 // r serves descriptor ring r (fwd4_res_desc in pinned host memory). It waits
 // for the ring's next seq, copies that batch's fwd4_params into LDS, runs the
-// three roles over the whole batch as one workgroup (tile order 0, wgs 1),
-// makes the batch's writes visible to the host and stores the seq into
-// done[r]. No launch and no hardware queue per batch: what small host batches
+// three roles over its share of the batch's tiles (tile order 0 over the
+// queue's rings: wg0 of wgs), makes those writes visible to the host and
+// stores the seq into done[r]. No launch and no hardware queue per batch: what small host batches
 // pay otherwise. A workgroup idle past its lifetime sets
 // *stop, and every workgroup leaves at *stop (host's or that one's) after the
 // batch it is running (its waits are bounded as in a launch), so the grid

@@ -229,7 +229,14 @@ struct alignas(128) gr_hip_queue {
 	hipEvent_t snap_ev = nullptr;
 	bool snap_pending = false;
 	uint64_t node_counted = 0, snap_counted = 0; // node walks launched with counters; covered by a snapshot
-	int ring = -1; // the resident kernel's ring this queue posts to (-1: none yet)
+	// gr_hip_fwd4_host on pageable memory: the queue's own pinned copies
+	// (grown on demand), which the CPU fills and drains around the pinned path
+	uint8_t *pg_lines = nullptr, *pg_out = nullptr;
+	gr_hip_pkt_meta *pg_meta = nullptr;
+	gr_hip_verdict *pg_v = nullptr;
+	uint32_t pg_cap = 0;
+	int ring = -1; // the first of the resident kernel's res_w rings this queue posts to (-1: none yet)
+	uint32_t res_w = 0; // how many (the context's res_w when they were taken)
 	uint64_t res_seq = 0; // the last seq posted on it
 	uint64_t res_retire = 0; // posted before the last FIB publication (retire_wait)
 };
@@ -304,6 +311,7 @@ struct gr_hip_ctx {
 	// done and exited words (pinned host memory), its stream and launch state
 	int res_on;
 	uint32_t res_rings; // workgroups of a launch = rings (knob "resident_rings")
+	uint32_t res_w; // rings (workgroups) per queue: each batch split over them (knob "resident_wgs")
 	uint32_t res_ms; // lifetime of an idle workgroup (knob "resident_ms")
 	fwd4_res_desc *res_desc;
 	uint64_t *res_done, *res_exited;
@@ -822,7 +830,8 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->tile_run = 16;
 	c->stage_min_tiles = 4;
 	c->res_on = 0;
-	c->res_rings = 16;
+	c->res_rings = 32; // 16 queues (worker graphs) of 2 rings
+	c->res_w = 2; // measured: DESIGN.md §6.3
 	c->res_ms = 50;
 	c->spin_max = 0;
 	c->untimed = 0;
@@ -1943,7 +1952,8 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 	if (q->ring >= 0) {
 		res_wait(q, q->res_seq); // its resident batches, then the ring is free again
 		std::lock_guard<std::mutex> rl(c->res_mu);
-		c->res_taken[(size_t)q->ring] = 0;
+		for (uint32_t j = 0; j < q->res_w; j++)
+			c->res_taken[(size_t)q->ring + j] = 0;
 	}
 	{
 		// unlink first: a commit running on another thread reaches the
@@ -1980,6 +1990,10 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 		hipEventDestroy(q->snap_ev);
 	hipHostFree(q->snap);
 	hipHostFree(q->h_err);
+	hipHostFree(q->pg_lines);
+	hipHostFree(q->pg_out);
+	hipHostFree(q->pg_meta);
+	hipHostFree(q->pg_v);
 	for (node_slot &w : q->nw) {
 		hipEventDestroy(w.done);
 		hipHostFree(w.lines);
@@ -2132,17 +2146,19 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 // the resident kernel (knob "resident"; fwd4_ring.hip gr_fwd4_resident)
 // ---------------------------------------------------------------------------
 // A queue's node batches go to the context's resident kernel instead of a
-// launch each: the batch's fwd4_params into the next descriptor of the
-// queue's ring (pinned host memory), then its seq. The kernel's workgroup for
-// that ring runs it and stores the seq into the ring's done word once the
-// results are in host memory; the node polls that word (a load, no runtime
-// call, no hardware queue held per batch: DESIGN.md §6.3). A workgroup idle
-// past the lifetime sets the stop word and all leave after their batch;
-// whoever then finds a batch waiting launches the kernel again, once every
-// ring's exited word carries the last launch's id, so that one workgroup at
-// most ever serves a ring. Posts wait for the FIB generation's upload on the
-// host (launches make their stream wait); commits and quiesce wait, on the
-// host, for the batches posted before them (retire_wait, quiesce).
+// launch each. The queue holds res_w rings (descriptors in pinned host
+// memory); each batch's fwd4_params go into the next descriptor of every one
+// of them, then its seq, workgroup j of the W taking tiles j, j + W, ... The
+// kernel's workgroup for a ring stores the seq into the ring's done word once
+// its tiles' results are in host memory; the batch is done when all W are
+// (the node polls those words: loads, no runtime call, no hardware queue held
+// per batch: DESIGN.md §6.3). A workgroup idle past the lifetime sets the
+// stop word and all leave after their batch; whoever then finds a batch
+// waiting launches the kernel again, once every ring's exited word carries
+// the last launch's id, so that one workgroup at most ever serves a ring.
+// Posts wait for the FIB generation's upload on the host (launches make their
+// stream wait); commits and quiesce wait, on the host, for the batches posted
+// before them (retire_wait, quiesce).
 #define RES_NDESC 4 // descriptors per ring (GR_HIP_NODE_DEPTH batches in flight at most)
 #define RES_STRIDE 8 // uint64_t per ring in the done / exited words: a 64-byte line each
 #define RES_WAIT_NS (10ull * 1000000000ull) // a batch not done after this: -ETIMEDOUT
@@ -2249,11 +2265,15 @@ static bool res_take(gr_hip_queue *q) {
 	std::lock_guard<std::mutex> l(c->res_mu);
 	if (res_setup(c) != 0)
 		return false;
-	for (uint32_t r = 0; r < c->res_rings; r++) {
+	const uint32_t W = c->res_w;
+	for (uint32_t r = 0; r + W <= c->res_rings; r += W) { // W consecutive rings, in groups of W
 		if (!c->res_taken[r]) {
-			c->res_taken[r] = 1;
+			for (uint32_t j = 0; j < W; j++)
+				c->res_taken[r + j] = 1;
 			q->ring = (int)r;
-			q->res_seq = q->res_retire = res_word(c->res_done, (int)r); // the ring's numbering goes on
+			q->res_w = W;
+			// the rings' numbering goes on (every batch is posted to all W: same seq)
+			q->res_seq = q->res_retire = res_word(c->res_done, (int)r);
 			return true;
 		}
 	}
@@ -2261,7 +2281,10 @@ static bool res_take(gr_hip_queue *q) {
 }
 
 static bool res_is_done(const gr_hip_queue *q, uint64_t seq) {
-	return res_word(q->ctx->res_done, q->ring) >= seq;
+	for (uint32_t j = 0; j < q->res_w; j++)
+		if (res_word(q->ctx->res_done, q->ring + (int)j) < seq)
+			return false;
+	return true;
 }
 
 // Wait, on the host, until the ring's batch `seq` is done.
@@ -2296,8 +2319,9 @@ static int res_post(gr_hip_queue *q, const gr_hip_batch *b) {
 		q->seen_serial = c->serial;
 	}
 	const uint64_t seq = q->res_seq + 1;
-	if (seq > res_word(c->res_done, q->ring) + RES_NDESC)
-		return -EBUSY; // (not reached: GR_HIP_NODE_DEPTH < RES_NDESC)
+	for (uint32_t j = 0; j < q->res_w; j++)
+		if (seq > res_word(c->res_done, q->ring + (int)j) + RES_NDESC)
+			return -EBUSY; // (not reached: GR_HIP_NODE_DEPTH < RES_NDESC)
 	fwd4_params A{};
 	A.in = static_cast<const uint8_t *>(b->in_frames);
 	A.out = static_cast<uint8_t *>(b->out_lines);
@@ -2312,12 +2336,14 @@ static int res_post(gr_hip_queue *q, const gr_hip_batch *b) {
 							    : b->in_stride;
 	A.spin_max = c->spin_max;
 	A.err = q->d_err;
-	A.wg0 = 0;
-	A.wgs = 1; // the ring's one workgroup takes every tile
+	A.wgs = q->res_w; // the batch split over the queue's rings: workgroup j takes tiles j, j + W, ...
 	A.ptrs = (b->flags & GR_HIP_BATCH_F_FRAME_PTRS) ? 1 : 0;
-	fwd4_res_desc &d = c->res_desc[(size_t)q->ring * RES_NDESC + seq % RES_NDESC];
-	memcpy(&d.A, &A, sizeof(A));
-	__atomic_store_n(&d.seq, seq, __ATOMIC_RELEASE); // after A
+	for (uint32_t j = 0; j < q->res_w; j++) {
+		A.wg0 = j;
+		fwd4_res_desc &d = c->res_desc[(size_t)(q->ring + (int)j) * RES_NDESC + seq % RES_NDESC];
+		memcpy(&d.A, &A, sizeof(A));
+		__atomic_store_n(&d.seq, seq, __ATOMIC_RELEASE); // after A
+	}
 	q->res_seq = seq;
 	return res_kick(c);
 }
@@ -2370,6 +2396,10 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < 1 || value > 256 || c->res_desc != nullptr)
 			return -EINVAL;
 		c->res_rings = (uint32_t)value;
+	} else if (strcmp(key, "resident_wgs") == 0) { // for queues that take their rings from then on
+		if (value < 1 || value > 64)
+			return -EINVAL;
+		c->res_w = (uint32_t)value;
 	} else if (strcmp(key, "resident_ms") == 0) {
 		if (value < 1 || value > 10000)
 			return -EINVAL;
@@ -2517,6 +2547,51 @@ static int host_direct_launch(gr_hip_queue *q, const void *lines, const gr_hip_p
 	return r;
 }
 
+// Pageable host memory: through the queue's own pinned copies, in chunks,
+// the CPU copying in and out around the pinned path. Pageable pointers never
+// reach the runtime's asynchronous copies (a pageable copy once reported an
+// illegal address after earlier tests had registered and unregistered host
+// memory: DESIGN.md §4).
+#define PG_CHUNK (1u << 20)
+static int host_pageable(gr_hip_queue *q, const void *lines, const gr_hip_pkt_meta *meta, uint32_t n,
+			 void *out_lines, uint32_t out_stride, gr_hip_verdict *verdicts) {
+	const uint32_t cap = n < PG_CHUNK ? n : PG_CHUNK;
+	if (q->pg_cap < cap) {
+		hipHostFree(q->pg_lines);
+		hipHostFree(q->pg_out);
+		hipHostFree(q->pg_meta);
+		hipHostFree(q->pg_v);
+		q->pg_lines = q->pg_out = nullptr;
+		q->pg_meta = nullptr;
+		q->pg_v = nullptr;
+		q->pg_cap = 0;
+		if (hipHostMalloc(reinterpret_cast<void **>(&q->pg_lines), (size_t)cap * GR_HIP_LINE, hipHostMallocDefault) != hipSuccess
+		    || hipHostMalloc(reinterpret_cast<void **>(&q->pg_out), (size_t)cap * GR_HIP_LINE, hipHostMallocDefault) != hipSuccess
+		    || hipHostMalloc(reinterpret_cast<void **>(&q->pg_meta), (size_t)cap * sizeof(gr_hip_pkt_meta), hipHostMallocDefault) != hipSuccess
+		    || hipHostMalloc(reinterpret_cast<void **>(&q->pg_v), (size_t)cap * sizeof(gr_hip_verdict), hipHostMallocDefault) != hipSuccess) {
+			(void)hipGetLastError();
+			return -ENOMEM;
+		}
+		q->pg_cap = cap;
+	}
+	const uint8_t *in = static_cast<const uint8_t *>(lines);
+	uint8_t *out = static_cast<uint8_t *>(out_lines);
+	int r = 0;
+	for (uint32_t off = 0; off < n; off += cap) {
+		const uint32_t cnt = n - off < cap ? n - off : cap;
+		memcpy(q->pg_lines, in + (size_t)off * GR_HIP_LINE, (size_t)cnt * GR_HIP_LINE);
+		memcpy(q->pg_meta, meta + off, (size_t)cnt * sizeof(*meta));
+		const int e = gr_hip_fwd4_host_ex(q, q->pg_lines, q->pg_meta, cnt, q->pg_out, out_stride, q->pg_v);
+		if (e < 0 && e != -ETIMEDOUT)
+			return e;
+		if (e == -ETIMEDOUT) // verdicts of packets never reached read back as 0xff: reported once
+			r = e;
+		memcpy(out + (size_t)off * out_stride, q->pg_out, (size_t)cnt * out_stride);
+		memcpy(verdicts + off, q->pg_v, (size_t)cnt * sizeof(*verdicts));
+	}
+	return r;
+}
+
 extern "C" int gr_hip_fwd4_host_ex(
 	gr_hip_queue_t *q,
 	const void *lines,
@@ -2535,6 +2610,10 @@ extern "C" int gr_hip_fwd4_host_ex(
 	const uint32_t oflags = out_stride == GR_HIP_PREFIX ? GR_HIP_BATCH_F_PREFIX32 : 0;
 	gr_hip_ctx *c = q->ctx;
 	hipSetDevice(c->dev);
+	void *dp;
+	if (!host_dev_ptr(lines, &dp) || !host_dev_ptr(meta, &dp) || !host_dev_ptr(out_lines, &dp)
+	    || !host_dev_ptr(verdicts, &dp))
+		return host_pageable(q, lines, meta, n, out_lines, out_stride, verdicts);
 	std::shared_lock<std::shared_mutex> l(c->mu); // see gr_hip_fwd4_submit
 	bool direct = false;
 	if (const int r = host_direct_launch(q, lines, meta, n, out_lines, out_stride, verdicts, &direct); r < 0)

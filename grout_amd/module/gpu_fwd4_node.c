@@ -223,6 +223,7 @@ static void gpu_init(struct event_base *ev) {
 			gpu_fini(NULL); // all or nothing: the nodes' init then fails
 			return;
 		}
+		gr_hip_tune(c, "resident", conf.launch_per_batch ? 0 : 1);
 		const int numa = gr_hip_device_numa_node(devs[i]);
 		gpus[n_gpus].ctx = c;
 		gpus[n_gpus].dev = devs[i];

@@ -100,6 +100,10 @@ struct gpu_fwd4_conf {
 	uint32_t rx_burst; // port_rx burst size (1..256): a shorter burst flushes
 	uint64_t max_delay_ns; // a held packet never waits longer (flush node)
 	uint32_t depth; // batches in flight per graph: 1 = each waited for, 2 = pipelined (0: 2)
+	// 0 (the default): each GPU's batches go to its resident kernel (gr_hip
+	// knob "resident": descriptor rings, no launch per batch); 1: one launch
+	// per batch
+	uint32_t launch_per_batch;
 };
 
 // Before module init (grout: from its configuration). A batch above

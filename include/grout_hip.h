@@ -490,6 +490,20 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               2 = one region per XCD, its workgroups interleaved in it,
 //               3 = runs of "tile_run" tiles (default 16), run j of
 //               workgroup b being run j * G + b
+//   "resident"  1 = node batches (gr_hip_node_send) go to the context's
+//               resident kernel: one long-lived launch whose workgroups take
+//               batches from per-queue descriptor rings in pinned host memory,
+//               completion polled as a memory word (no launch, no runtime call,
+//               no hardware queue per batch); per-iface counters are then the
+//               hand-back's. 0 = one launch per batch (default; the grout
+//               module turns it on unless gpu_fwd4_conf.launch_per_batch)
+//   "resident_wgs" rings (workgroups) per queue, each batch split over them
+//               (default 2; queues taking their rings from then on)
+//   "resident_rings" rings in all = workgroups of the resident launch
+//               (default 32; before the first resident batch only)
+//   "resident_ms" an idle workgroup leaves after this long, all with it; the
+//               next batch launches the kernel again (default 50)
+//   "resident_launches" (read) resident launches so far
 //   "stage_min_tiles" the fast adjacencies (and IPv6 first-level slice) are
 //               staged in each workgroup's LDS only when the launch gives every
 //               workgroup at least this many 64-packet tiles (default 4);

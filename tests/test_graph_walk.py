@@ -742,12 +742,18 @@ def test_graph_walk_control_plane_churn(readers, quiesce_each):
     # run, in some runs never.)
     assert L.gpu_fwd4_set_batch(CHURN_BATCH, DELAY_NS) == 0
     L.gh_set_gpu_load(CHURN_GPU_LOAD)
+    if not readers:
+        # the negative control needs batches that wait behind the other
+        # queue's kernels: one launch per batch (the resident kernel's batches
+        # do not queue behind launches, so its window is rarely hit)
+        fp.tune("resident", 0)
     try:
         assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, n) == 0
         ip_be = int.from_bytes(T.ip4("16.1.0.0").to_bytes(4, "big"), "little")
         assert L.gh_churn_test(ip_be, 16, T.VRF_MAIN, a, b, 50, quiesce_each, res.ctypes.data) == 0
     finally:
         L.gpu_fwd4_rcu_readers(1)
+        fp.tune("resident", 1)  # the module's default
         L.gh_set_gpu_load(0)
         assert L.gpu_fwd4_set_batch(BATCH, DELAY_NS) == 0
     c = res[0]

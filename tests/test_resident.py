@@ -190,7 +190,7 @@ def test_resident_graph_walk_corpus(ptrs):
     import scenarios as SC
     G.lib().gh_set_pin(1)
     fp = G.graph_ctx()
-    fp.tune("resident", 1)
+    fp.tune("resident", 1)  # the module's default
     fp.tune("node_ptrs", ptrs)
     t, _ = SC.corpus_topology()
     fr, me, lab = SC.corpus_arrays()
@@ -200,7 +200,6 @@ def test_resident_graph_walk_corpus(ptrs):
         got = G.check_walk(t, fr, me, lab)
     finally:
         fp.tune("node_ptrs", 0)
-        fp.tune("resident", 0)
     assert len(set(got["edge"])) > 20
 
 
@@ -211,9 +210,6 @@ def test_resident_graph_control_plane_churn():
     resident kernel: quiesce and the FIB publications wait for them."""
     import test_graph_walk as G
     fp = G.graph_ctx()
-    fp.tune("resident", 1)
-    try:
-        G.test_graph_walk_control_plane_churn(1, 1)
-        G.test_graph_walk_stream_batches(2)
-    finally:
-        fp.tune("resident", 0)
+    fp.tune("resident", 1)  # the module's default
+    G.test_graph_walk_control_plane_churn(1, 1)
+    G.test_graph_walk_stream_batches(2)
