@@ -174,8 +174,9 @@ struct fwd4_params {
 // descriptors in pinned host memory; the host writes A, then `seq` (release);
 // the kernel's workgroup r takes them in seq order (1, 2, ...), runs each,
 // and stores its seq into done[r * stride] (release, system scope).
+#define FWD4_RES_EMPTY (1ull << 63) // in fwd4_res_desc.seq: none of the batch's tiles are this ring's
 struct __attribute__((aligned(64))) fwd4_res_desc {
-	uint64_t seq;
+	uint64_t seq; // | FWD4_RES_EMPTY
 	uint64_t _pad[7];
 	struct fwd4_params A;
 };
@@ -185,10 +186,13 @@ struct fwd4_res_params {
 	uint64_t *done; // [rings * stride], host memory
 	uint64_t *exited; // [rings * stride], host memory: launch_id once ring r's workgroup has left
 	uint32_t *stop; // host memory: nonzero = every workgroup leaves after its batch
+	const uint32_t *taken; // host memory [rings]: 0 = no queue holds ring r, its workgroup leaves at once
 	uint64_t lifetime; // s_memrealtime ticks (100 MHz): a workgroup idle past it sets *stop
 	uint64_t launch_id;
 	uint32_t ndesc;
 	uint32_t stride; // uint64_t per ring in done / exited
+	uint32_t nap_max; // idle polls back off up to this many s_sleep(8) between reads (1: none)
+	uint32_t _pad;
 };
 
 // First-level FIB6 entries a launch may stage in LDS: 2000::/4 (index =

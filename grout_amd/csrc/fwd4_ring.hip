@@ -160,6 +160,8 @@ __device__ __forceinline__ uint32_t tile_of(const fwd4_params &A, uint32_t k) {
 
 // How many tiles this workgroup takes (tile_of's k ranges over [0, that)).
 __device__ __forceinline__ uint32_t local_tiles(const fwd4_params &A) {
+	if (A.wgs && A.wg0 >= A.wgs)
+		return 0; // a resident ring beyond the batch's split: its seq only
 	const uint32_t n_tiles = (A.n + 63) >> 6, b = wg_id(A), G = wg_count(A);
 	if (A.order == 2) {
 		const uint32_t x = b & 7, l = b >> 3, per = G >> 3;
@@ -490,8 +492,19 @@ __global__ void __launch_bounds__(ring_cfg_res::WAVES * 64) gr_fwd4_resident(con
 	uint64_t *done = R.done + (size_t)blockIdx.x * R.stride;
 	const fwd4_res_desc *ring = R.descs + (size_t)blockIdx.x * R.ndesc;
 	const uint64_t until = __builtin_amdgcn_s_memrealtime() + R.lifetime;
-	if (tid == 0)
+	if (tid == 0) {
 		seq_s = sys_load64(done) + 1; // a relaunch resumes after the last batch done
+		go = __hip_atomic_load(R.taken + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+	}
+	__syncthreads();
+	if (go == 0) { // no queue holds this ring: nothing to poll (a queue taking it relaunches)
+		if (tid == 0)
+			__hip_atomic_store(R.exited + (size_t)blockIdx.x * R.stride, R.launch_id, __ATOMIC_RELEASE,
+					   __HIP_MEMORY_SCOPE_SYSTEM);
+		return;
+	}
+	__syncthreads(); // every wave has read go
+	uint32_t nap = 1; // idle polls back off (each one is a read over PCIe)
 	for (;;) {
 		if (tid == 0) {
 			const uint64_t want = seq_s;
@@ -500,21 +513,33 @@ __global__ void __launch_bounds__(ring_cfg_res::WAVES * 64) gr_fwd4_resident(con
 			for (;;) {
 				if (__hip_atomic_load(R.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
 					break; // every workgroup leaves: the host relaunches once all have
-				if (sys_load64(&d->seq) == want) {
-					g = 1;
+				const uint64_t w = sys_load64(&d->seq);
+				if ((w & ~FWD4_RES_EMPTY) == want) {
+					g = (w & FWD4_RES_EMPTY) ? 2 : 1;
 					break;
 				}
 				if (__builtin_amdgcn_s_memrealtime() > until) { // idle past the lifetime
 					__hip_atomic_store(R.stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 					break;
 				}
-				__builtin_amdgcn_s_sleep(8);
+				for (uint32_t i = 0; i < nap; i++)
+					__builtin_amdgcn_s_sleep(8);
+				nap = nap * 2 < R.nap_max ? nap * 2 : R.nap_max;
+			}
+			if (g == 2) { // no tiles of this batch here: its seq only
+				__hip_atomic_store(done, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+				seq_s = want + 1;
 			}
 			go = g;
 		}
 		__syncthreads();
-		if (!go)
+		const uint32_t gv = go;
+		__syncthreads(); // every wave has read go before thread 0 writes the next one
+		if (gv == 2)
+			continue;
+		if (!gv)
 			break;
+		nap = 1;
 		{ // the batch's parameters, from host memory
 			const uint32_t *src = reinterpret_cast<const uint32_t *>(&ring[seq_s % R.ndesc].A);
 			uint32_t *dst = reinterpret_cast<uint32_t *>(&A);

@@ -313,12 +313,14 @@ struct gr_hip_ctx {
 	uint32_t res_rings; // workgroups of a launch = rings (knob "resident_rings")
 	uint32_t res_w; // rings (workgroups) per queue: each batch split over them (knob "resident_wgs")
 	uint32_t res_ms; // lifetime of an idle workgroup (knob "resident_ms")
+	uint32_t res_nap; // idle poll backoff ceiling, in s_sleep(8) units (knob "resident_nap")
 	fwd4_res_desc *res_desc;
 	uint64_t *res_done, *res_exited;
 	uint32_t *res_stop;
+	uint32_t *res_taken_h; // [res_rings]: rings held by a queue, as the kernel reads it
 	fwd4_res_desc *res_desc_d; // their device addresses
 	uint64_t *res_done_d, *res_exited_d;
-	uint32_t *res_stop_d;
+	uint32_t *res_stop_d, *res_taken_d;
 	hipStream_t res_s;
 	hipEvent_t res_ev;
 	std::atomic<bool> res_live; // launched, and not yet seen to have left
@@ -830,9 +832,10 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->tile_run = 16;
 	c->stage_min_tiles = 4;
 	c->res_on = 0;
-	c->res_rings = 32; // 16 queues (worker graphs) of 2 rings
-	c->res_w = 2; // measured: DESIGN.md §6.3
+	c->res_rings = 64; // 32 queues (worker graphs) of 2 rings; workgroups of rings no queue holds leave at once
+	c->res_w = 2; // a batch uses up to 2 of them, 32 tiles each (measured: DESIGN.md §6.3)
 	c->res_ms = 50;
+	c->res_nap = 1;
 	c->spin_max = 0;
 	c->untimed = 0;
 	c->time_every = 1;
@@ -1952,8 +1955,10 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 	if (q->ring >= 0) {
 		res_wait(q, q->res_seq); // its resident batches, then the ring is free again
 		std::lock_guard<std::mutex> rl(c->res_mu);
-		for (uint32_t j = 0; j < q->res_w; j++)
+		for (uint32_t j = 0; j < q->res_w; j++) {
 			c->res_taken[(size_t)q->ring + j] = 0;
+			__atomic_store_n(c->res_taken_h + q->ring + j, 0u, __ATOMIC_RELEASE);
+		}
 	}
 	{
 		// unlink first: a commit running on another thread reaches the
@@ -2148,7 +2153,8 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 // A queue's node batches go to the context's resident kernel instead of a
 // launch each. The queue holds res_w rings (descriptors in pinned host
 // memory); each batch's fwd4_params go into the next descriptor of every one
-// of them, then its seq, workgroup j of the W taking tiles j, j + W, ... The
+// of them, then its seq: the batch split over k of them (RES_TILES_PER_WG
+// tiles each), workgroup j < k taking tiles j, j + k, ..., the others none. The
 // kernel's workgroup for a ring stores the seq into the ring's done word once
 // its tiles' results are in host memory; the batch is done when all W are
 // (the node polls those words: loads, no runtime call, no hardware queue held
@@ -2162,6 +2168,7 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 #define RES_NDESC 4 // descriptors per ring (GR_HIP_NODE_DEPTH batches in flight at most)
 #define RES_STRIDE 8 // uint64_t per ring in the done / exited words: a 64-byte line each
 #define RES_WAIT_NS (10ull * 1000000000ull) // a batch not done after this: -ETIMEDOUT
+#define RES_TILES_PER_WG 32 // tiles per workgroup a batch is split into (up to the queue's rings)
 
 static uint64_t res_word(const uint64_t *w, int ring) {
 	return __atomic_load_n(w + (size_t)ring * RES_STRIDE, __ATOMIC_ACQUIRE);
@@ -2181,6 +2188,8 @@ static void res_free(gr_hip_ctx *c) {
 	hipHostFree(c->res_done);
 	hipHostFree(c->res_exited);
 	hipHostFree(c->res_stop);
+	hipHostFree(c->res_taken_h);
+	c->res_taken_h = nullptr;
 	c->res_ev = nullptr;
 	c->res_s = nullptr;
 	c->res_desc = nullptr;
@@ -2202,6 +2211,8 @@ static int res_setup(gr_hip_ctx *c) {
 	    || hipHostMalloc(reinterpret_cast<void **>(&c->res_done), nw, fl) != hipSuccess
 	    || hipHostMalloc(reinterpret_cast<void **>(&c->res_exited), nw, fl) != hipSuccess
 	    || hipHostMalloc(reinterpret_cast<void **>(&c->res_stop), 64, fl) != hipSuccess
+	    || hipHostMalloc(reinterpret_cast<void **>(&c->res_taken_h), sizeof(uint32_t) * c->res_rings, fl) != hipSuccess
+	    || hipHostGetDevicePointer(reinterpret_cast<void **>(&c->res_taken_d), c->res_taken_h, 0) != hipSuccess
 	    || hipHostGetDevicePointer(reinterpret_cast<void **>(&c->res_desc_d), c->res_desc, 0) != hipSuccess
 	    || hipHostGetDevicePointer(reinterpret_cast<void **>(&c->res_done_d), c->res_done, 0) != hipSuccess
 	    || hipHostGetDevicePointer(reinterpret_cast<void **>(&c->res_exited_d), c->res_exited, 0) != hipSuccess
@@ -2217,6 +2228,7 @@ static int res_setup(gr_hip_ctx *c) {
 	memset(c->res_desc, 0, nd);
 	memset(c->res_done, 0, nw);
 	memset(c->res_exited, 0, nw);
+	memset(c->res_taken_h, 0, sizeof(uint32_t) * c->res_rings);
 	*c->res_stop = 0;
 	c->res_taken.assign(c->res_rings, 0);
 	return 0;
@@ -2239,10 +2251,12 @@ static int res_ensure(gr_hip_ctx *c) {
 	R.done = c->res_done_d;
 	R.exited = c->res_exited_d;
 	R.stop = c->res_stop_d;
+	R.taken = c->res_taken_d;
 	R.lifetime = (uint64_t)c->res_ms * 100000u; // s_memrealtime: 100 MHz
 	R.launch_id = ++c->res_launch;
 	R.ndesc = RES_NDESC;
 	R.stride = RES_STRIDE;
+	R.nap_max = c->res_nap;
 	HCK(gr_fwd4_resident_launch(&R, c->res_rings, c->res_s));
 	HCK(hipEventRecord(c->res_ev, c->res_s));
 	c->res_live = true;
@@ -2268,8 +2282,14 @@ static bool res_take(gr_hip_queue *q) {
 	const uint32_t W = c->res_w;
 	for (uint32_t r = 0; r + W <= c->res_rings; r += W) { // W consecutive rings, in groups of W
 		if (!c->res_taken[r]) {
-			for (uint32_t j = 0; j < W; j++)
+			for (uint32_t j = 0; j < W; j++) {
 				c->res_taken[r + j] = 1;
+				__atomic_store_n(c->res_taken_h + r + j, 1u, __ATOMIC_RELEASE);
+			}
+			// a live launch's workgroups for these rings left at once: it
+			// leaves, and the next batch launches one that serves them
+			if (c->res_live)
+				__atomic_store_n(c->res_stop, 1u, __ATOMIC_RELEASE);
 			q->ring = (int)r;
 			q->res_w = W;
 			// the rings' numbering goes on (every batch is posted to all W: same seq)
@@ -2336,11 +2356,20 @@ static int res_post(gr_hip_queue *q, const gr_hip_batch *b) {
 							    : b->in_stride;
 	A.spin_max = c->spin_max;
 	A.err = q->d_err;
-	A.wgs = q->res_w; // the batch split over the queue's rings: workgroup j takes tiles j, j + W, ...
+	// the batch split over k of the queue's W rings, RES_TILES_PER_WG tiles
+	// each (workgroup j < k takes tiles j, j + k, ...); the others get the
+	// descriptor with no tiles, so that every ring's seq moves on together
+	const uint32_t tiles = (b->n + 63) / 64;
+	uint32_t k = (tiles + RES_TILES_PER_WG - 1) / RES_TILES_PER_WG;
+	A.wgs = k < 1 ? 1 : k > q->res_w ? q->res_w : k;
 	A.ptrs = (b->flags & GR_HIP_BATCH_F_FRAME_PTRS) ? 1 : 0;
 	for (uint32_t j = 0; j < q->res_w; j++) {
-		A.wg0 = j;
 		fwd4_res_desc &d = c->res_desc[(size_t)(q->ring + (int)j) * RES_NDESC + seq % RES_NDESC];
+		if (j >= A.wgs) { // none of its tiles: the workgroup stores the seq without reading A
+			__atomic_store_n(&d.seq, seq | FWD4_RES_EMPTY, __ATOMIC_RELEASE);
+			continue;
+		}
+		A.wg0 = j;
 		memcpy(&d.A, &A, sizeof(A));
 		__atomic_store_n(&d.seq, seq, __ATOMIC_RELEASE); // after A
 	}
@@ -2400,6 +2429,10 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < 1 || value > 64)
 			return -EINVAL;
 		c->res_w = (uint32_t)value;
+	} else if (strcmp(key, "resident_nap") == 0) { // the next launch
+		if (value < 1 || value > 64)
+			return -EINVAL;
+		c->res_nap = (uint32_t)value;
 	} else if (strcmp(key, "resident_ms") == 0) {
 		if (value < 1 || value > 10000)
 			return -EINVAL;

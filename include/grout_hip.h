@@ -497,10 +497,14 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               no hardware queue per batch); per-iface counters are then the
 //               hand-back's. 0 = one launch per batch (default; the grout
 //               module turns it on unless gpu_fwd4_conf.launch_per_batch)
-//   "resident_wgs" rings (workgroups) per queue, each batch split over them
-//               (default 2; queues taking their rings from then on)
-//   "resident_rings" rings in all = workgroups of the resident launch
-//               (default 32; before the first resident batch only)
+//   "resident_wgs" rings (workgroups) per queue: a batch is split over up to
+//               that many, 32 tiles (2048 packets) each (default 2; queues
+//               taking their rings from then on)
+//   "resident_rings" rings in all (default 64: 32 queues; before the first
+//               resident batch only); the workgroups of rings no queue holds
+//               leave at once
+//   "resident_nap" idle polls back off up to this many s_sleep(8) between
+//               reads of a ring (default 1: none; the next launch)
 //   "resident_ms" an idle workgroup leaves after this long, all with it; the
 //               next batch launches the kernel again (default 50)
 //   "resident_launches" (read) resident launches so far

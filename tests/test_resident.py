@@ -106,6 +106,37 @@ def test_resident_relaunch(resident):
 
 
 @pytest.mark.gpu
+def test_resident_queue_joins_a_live_kernel(resident):
+    """A queue that takes its rings while the kernel runs (the workgroups of
+    rings nobody held left at once) makes it leave; its first batch launches
+    one that serves it, and the first queue's batches go on through it."""
+    from golden_util import fresh_fastpath_state
+    fp = resident
+    topo = T.config_fullview(count=50_000)
+    fr, me = S.stream(4 * 5000, 0xD23, routes=topo.route_array())
+    fresh_fastpath_state(fp, topo)
+    lines, v, st, want, _ = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
+    bufs, m = mbufs_for(fr, me)
+    q1 = fp.queue()
+    q2 = None
+    try:
+        q1.node_start(m[:5000])
+        q1.node_finish()
+        l0 = fp.tune("resident_launches")
+        q2 = fp.queue()
+        for q, part in ((q2, m[5000:10000]), (q1, m[10000:15000]), (q2, m[15000:])):
+            q.node_start(part)
+            got, _ = q.node_finish()
+            assert got is part and q.unfinished == 0
+        assert fp.tune("resident_launches") > l0  # relaunched for q2's rings
+        compare_mbufs(m, want, bufs, lines)
+    finally:
+        q1.close()
+        if q2 is not None:
+            q2.close()
+
+
+@pytest.mark.gpu
 def test_resident_give_up_hands_back(resident):
     """A resident kernel that gives up (spin_max 1) reports it once (the
     queue's error word), and the node hands back what it finished and punts
