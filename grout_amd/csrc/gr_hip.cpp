@@ -2861,10 +2861,14 @@ static int slot_grow(node_slot &w, uint32_t ns, uint32_t keep) {
 	uint8_t *lines = nullptr, *out = nullptr;
 	gr_hip_pkt_meta *meta = nullptr;
 	gr_hip_verdict *v = nullptr;
-	if (hipHostMalloc((void **)&lines, (size_t)cap * GR_HIP_LINE, hipHostMallocDefault) != hipSuccess
-	    || hipHostMalloc((void **)&out, (size_t)cap * GR_HIP_PREFIX, hipHostMallocDefault) != hipSuccess
-	    || hipHostMalloc((void **)&meta, (size_t)cap * sizeof(gr_hip_pkt_meta), hipHostMallocDefault) != hipSuccess
-	    || hipHostMalloc((void **)&v, (size_t)cap * sizeof(gr_hip_verdict), hipHostMallocDefault) != hipSuccess) {
+	// fine-grained (coherent): the resident kernel reads a slot while it runs,
+	// past any kernel boundary, which is the only point where coarse-grained
+	// host memory is made coherent (its frame pointers read stale otherwise)
+	const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+	if (hipHostMalloc((void **)&lines, (size_t)cap * GR_HIP_LINE, fl) != hipSuccess
+	    || hipHostMalloc((void **)&out, (size_t)cap * GR_HIP_PREFIX, fl) != hipSuccess
+	    || hipHostMalloc((void **)&meta, (size_t)cap * sizeof(gr_hip_pkt_meta), fl) != hipSuccess
+	    || hipHostMalloc((void **)&v, (size_t)cap * sizeof(gr_hip_verdict), fl) != hipSuccess) {
 		(void)hipGetLastError();
 		hipHostFree(lines);
 		hipHostFree(out);
