@@ -186,12 +186,13 @@ struct fwd4_res_params {
 	uint64_t *done; // [rings * stride], host memory
 	uint64_t *exited; // [rings * stride], host memory: launch_id once ring r's workgroup has left
 	uint32_t *stop; // host memory: nonzero = every workgroup leaves after its batch
-	const uint32_t *taken; // host memory [rings]: 0 = no queue holds ring r, its workgroup leaves at once
+	const uint32_t *taken; // host memory [rings]: 0 = no queue holds ring r (its workgroup leaves at
+	                       // once), 1 = a queue's first ring, 2 = one of its helpers (polls backed off)
 	uint64_t lifetime; // s_memrealtime ticks (100 MHz): a workgroup idle past it sets *stop
 	uint64_t launch_id;
 	uint32_t ndesc;
 	uint32_t stride; // uint64_t per ring in done / exited
-	uint32_t nap_max; // idle polls back off up to this many s_sleep(8) between reads (1: none)
+	uint32_t nap_max; // helper rings' idle polls back off up to this many s_sleep(8) between reads
 	uint32_t _pad;
 };
 

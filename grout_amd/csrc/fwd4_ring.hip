@@ -503,6 +503,9 @@ __global__ void __launch_bounds__(ring_cfg_res::WAVES * 64) gr_fwd4_resident(con
 					   __HIP_MEMORY_SCOPE_SYSTEM);
 		return;
 	}
+	// a queue's first ring polls at full rate; its helper rings (taken 2: only
+	// batches of more than 32 tiles reach them) back off to R.nap_max
+	const uint32_t nap_max = go == 2 ? R.nap_max : 1;
 	__syncthreads(); // every wave has read go
 	uint32_t nap = 1; // idle polls back off (each one is a read over PCIe)
 	for (;;) {
@@ -524,7 +527,7 @@ __global__ void __launch_bounds__(ring_cfg_res::WAVES * 64) gr_fwd4_resident(con
 				}
 				for (uint32_t i = 0; i < nap; i++)
 					__builtin_amdgcn_s_sleep(8);
-				nap = nap * 2 < R.nap_max ? nap * 2 : R.nap_max;
+				nap = nap * 2 < nap_max ? nap * 2 : nap_max;
 			}
 			if (g == 2) { // no tiles of this batch here: its seq only
 				__hip_atomic_store(done, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

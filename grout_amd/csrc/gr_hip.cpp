@@ -835,7 +835,7 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->res_rings = 64; // 32 queues (worker graphs) of 2 rings; workgroups of rings no queue holds leave at once
 	c->res_w = 2; // a batch uses up to 2 of them, 32 tiles each (measured: DESIGN.md §6.3)
 	c->res_ms = 50;
-	c->res_nap = 1;
+	c->res_nap = 16;
 	c->spin_max = 0;
 	c->untimed = 0;
 	c->time_every = 1;
@@ -2282,9 +2282,9 @@ static bool res_take(gr_hip_queue *q) {
 	const uint32_t W = c->res_w;
 	for (uint32_t r = 0; r + W <= c->res_rings; r += W) { // W consecutive rings, in groups of W
 		if (!c->res_taken[r]) {
-			for (uint32_t j = 0; j < W; j++) {
+			for (uint32_t j = 0; j < W; j++) { // 1: the queue's first ring, 2: a helper
 				c->res_taken[r + j] = 1;
-				__atomic_store_n(c->res_taken_h + r + j, 1u, __ATOMIC_RELEASE);
+				__atomic_store_n(c->res_taken_h + r + j, j == 0 ? 1u : 2u, __ATOMIC_RELEASE);
 			}
 			// a live launch's workgroups for these rings left at once: it
 			// leaves, and the next batch launches one that serves them

@@ -503,8 +503,9 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //   "resident_rings" rings in all (default 64: 32 queues; before the first
 //               resident batch only); the workgroups of rings no queue holds
 //               leave at once
-//   "resident_nap" idle polls back off up to this many s_sleep(8) between
-//               reads of a ring (default 1: none; the next launch)
+//   "resident_nap" a queue's helper rings (all but its first) back off their
+//               idle polls up to this many s_sleep(8) between reads (default
+//               16; the next launch)
 //   "resident_ms" an idle workgroup leaves after this long, all with it; the
 //               next batch launches the kernel again (default 50)
 //   "resident_launches" (read) resident launches so far
