@@ -174,9 +174,8 @@ struct fwd4_params {
 // descriptors in pinned host memory; the host writes A, then `seq` (release);
 // the kernel's workgroup r takes them in seq order (1, 2, ...), runs each,
 // and stores its seq into done[r * stride] (release, system scope).
-#define FWD4_RES_EMPTY (1ull << 63) // in fwd4_res_desc.seq: none of the batch's tiles are this ring's
 struct __attribute__((aligned(64))) fwd4_res_desc {
-	uint64_t seq; // | FWD4_RES_EMPTY
+	uint64_t seq;
 	uint64_t _pad[7];
 	struct fwd4_params A;
 };

@@ -516,9 +516,8 @@ __global__ void __launch_bounds__(ring_cfg_res::WAVES * 64) gr_fwd4_resident(con
 			for (;;) {
 				if (__hip_atomic_load(R.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
 					break; // every workgroup leaves: the host relaunches once all have
-				const uint64_t w = sys_load64(&d->seq);
-				if ((w & ~FWD4_RES_EMPTY) == want) {
-					g = (w & FWD4_RES_EMPTY) ? 2 : 1;
+				if (sys_load64(&d->seq) == want) {
+					g = 1;
 					break;
 				}
 				if (__builtin_amdgcn_s_memrealtime() > until) { // idle past the lifetime
@@ -529,17 +528,11 @@ __global__ void __launch_bounds__(ring_cfg_res::WAVES * 64) gr_fwd4_resident(con
 					__builtin_amdgcn_s_sleep(8);
 				nap = nap * 2 < nap_max ? nap * 2 : nap_max;
 			}
-			if (g == 2) { // no tiles of this batch here: its seq only
-				__hip_atomic_store(done, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-				seq_s = want + 1;
-			}
 			go = g;
 		}
 		__syncthreads();
 		const uint32_t gv = go;
 		__syncthreads(); // every wave has read go before thread 0 writes the next one
-		if (gv == 2)
-			continue;
 		if (!gv)
 			break;
 		nap = 1;

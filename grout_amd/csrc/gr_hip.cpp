@@ -162,6 +162,14 @@ struct host_slot {
 	gr_hip_verdict *v = nullptr;
 };
 
+// What the resident kernel must have done (res_post): seq[j] on ring j of the
+// queue's rings, j < k (each ring numbers its own batches).
+#define RES_WMAX 8
+struct res_mark {
+	uint64_t seq[RES_WMAX] = {};
+	uint32_t k = 0;
+};
+
 // One rte_graph node walk (gr_hip_node_start .. gr_hip_node_finish): its
 // pinned staging, grown on demand, and the walk in flight.
 struct node_slot {
@@ -187,8 +195,8 @@ struct node_slot {
 	void *const *mb0 = nullptr;
 	const gr_hip_mbuf_layout *lay = nullptr;
 	bool kcount = false; // its kernel counts the per-iface counters (not the hand-back)
-	bool resident = false; // posted to the resident kernel (res_post): done at res_seq
-	uint64_t res_seq = 0;
+	bool resident = false; // posted to the resident kernel (res_post): done at `res`
+	res_mark res;
 };
 
 } // namespace
@@ -237,8 +245,8 @@ struct alignas(128) gr_hip_queue {
 	uint32_t pg_cap = 0;
 	int ring = -1; // the first of the resident kernel's res_w rings this queue posts to (-1: none yet)
 	uint32_t res_w = 0; // how many (the context's res_w when they were taken)
-	uint64_t res_seq = 0; // the last seq posted on it
-	uint64_t res_retire = 0; // posted before the last FIB publication (retire_wait)
+	res_mark res_posted; // the last seq posted on each of its rings
+	res_mark res_retire; // posted before the last FIB publication (retire_wait)
 };
 
 struct host_range { // gr_hip_host_register
@@ -352,14 +360,14 @@ struct gr_hip_ctx {
 // ---------------------------------------------------------------------------
 
 // Make the control stream wait for everything submitted on every queue.
-static int res_wait(gr_hip_queue *q, uint64_t seq);
+static int res_wait(gr_hip_queue *q, const res_mark &m);
 static void res_free(gr_hip_ctx *c);
 
 static int quiesce(gr_hip_ctx *c) {
 	for (gr_hip_queue *q : c->queues) {
 		HCK(hipEventRecord(q->quiesce, q->s));
 		HCK(hipStreamWaitEvent(c->ctl, q->quiesce, 0));
-		if (const int r = res_wait(q, q->res_seq)) // its resident batches: on the host
+		if (const int r = res_wait(q, q->res_posted)) // its resident batches: on the host
 			return r;
 	}
 	return 0;
@@ -832,8 +840,8 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->tile_run = 16;
 	c->stage_min_tiles = 4;
 	c->res_on = 0;
-	c->res_rings = 64; // 32 queues (worker graphs) of 2 rings; workgroups of rings no queue holds leave at once
-	c->res_w = 2; // a batch uses up to 2 of them, 32 tiles each (measured: DESIGN.md §6.3)
+	c->res_rings = 128; // 32 queues (worker graphs) of 4 rings; workgroups of rings no queue holds leave at once
+	c->res_w = 4; // a batch uses up to 4 of them, 32 tiles each (measured: DESIGN.md §3.3)
 	c->res_ms = 50;
 	c->res_nap = 16;
 	c->spin_max = 0;
@@ -1235,7 +1243,7 @@ static int publish(gr_hip_ctx *c, uint32_t g, F then) {
 	count_v6(c);
 	for (gr_hip_queue *q : c->queues) {
 		HCK(hipEventRecord(q->retire, q->s));
-		q->res_retire = q->res_seq;
+		q->res_retire = q->res_posted;
 	}
 	return 0;
 }
@@ -1953,7 +1961,7 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 		if (h.s)
 			hipStreamSynchronize(h.s);
 	if (q->ring >= 0) {
-		res_wait(q, q->res_seq); // its resident batches, then the ring is free again
+		res_wait(q, q->res_posted); // its resident batches, then the rings are free again
 		std::lock_guard<std::mutex> rl(c->res_mu);
 		for (uint32_t j = 0; j < q->res_w; j++) {
 			c->res_taken[(size_t)q->ring + j] = 0;
@@ -2152,14 +2160,14 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 // ---------------------------------------------------------------------------
 // A queue's node batches go to the context's resident kernel instead of a
 // launch each. The queue holds res_w rings (descriptors in pinned host
-// memory); each batch's fwd4_params go into the next descriptor of every one
-// of them, then its seq: the batch split over k of them (RES_TILES_PER_WG
-// tiles each), workgroup j < k taking tiles j, j + k, ..., the others none. The
-// kernel's workgroup for a ring stores the seq into the ring's done word once
-// its tiles' results are in host memory; the batch is done when all W are
-// (the node polls those words: loads, no runtime call, no hardware queue held
-// per batch: DESIGN.md §6.3). A workgroup idle past the lifetime sets the
-// stop word and all leave after their batch; whoever then finds a batch
+// memory), each numbering its own batches; a batch goes to k of them
+// (RES_TILES_PER_WG tiles each): its fwd4_params into each one's next
+// descriptor, then that ring's seq, workgroup j < k taking tiles j, j + k, ...
+// The kernel's workgroup for a ring stores the seq into the ring's done word
+// once its tiles' results are in host memory; the batch is done when all k
+// are (the node polls those words: loads, no runtime call, no hardware queue
+// held per batch: DESIGN.md §6.3). A workgroup idle past the lifetime sets
+// the stop word and all leave after their batch; whoever then finds a batch
 // waiting launches the kernel again, once every ring's exited word carries
 // the last launch's id, so that one workgroup at most ever serves a ring.
 // Posts wait for the FIB generation's upload on the host (launches make their
@@ -2292,28 +2300,30 @@ static bool res_take(gr_hip_queue *q) {
 				__atomic_store_n(c->res_stop, 1u, __ATOMIC_RELEASE);
 			q->ring = (int)r;
 			q->res_w = W;
-			// the rings' numbering goes on (every batch is posted to all W: same seq)
-			q->res_seq = q->res_retire = res_word(c->res_done, (int)r);
+			q->res_posted.k = W; // each ring's numbering goes on
+			for (uint32_t j = 0; j < W; j++)
+				q->res_posted.seq[j] = res_word(c->res_done, (int)(r + j));
+			q->res_retire = q->res_posted;
 			return true;
 		}
 	}
 	return false;
 }
 
-static bool res_is_done(const gr_hip_queue *q, uint64_t seq) {
-	for (uint32_t j = 0; j < q->res_w; j++)
-		if (res_word(q->ctx->res_done, q->ring + (int)j) < seq)
+static bool res_is_done(const gr_hip_queue *q, const res_mark &m) {
+	for (uint32_t j = 0; j < m.k; j++)
+		if (res_word(q->ctx->res_done, q->ring + (int)j) < m.seq[j])
 			return false;
 	return true;
 }
 
 // Wait, on the host, until the ring's batch `seq` is done.
-static int res_wait(gr_hip_queue *q, uint64_t seq) {
-	if (q->ring < 0 || res_is_done(q, seq))
+static int res_wait(gr_hip_queue *q, const res_mark &m) {
+	if (q->ring < 0 || res_is_done(q, m))
 		return 0;
 	gr_hip_ctx *c = q->ctx;
 	const uint64_t t0 = now_ns_host();
-	for (uint32_t spin = 1; !res_is_done(q, seq); spin++) {
+	for (uint32_t spin = 1; !res_is_done(q, m); spin++) {
 		if ((spin & 1023) == 0) {
 			if (const int r = res_kick(c))
 				return r;
@@ -2330,17 +2340,21 @@ static int res_wait(gr_hip_queue *q, uint64_t seq) {
 	return 0;
 }
 
-// Post batch b (device addresses) on q's ring; c->mu held shared.
-static int res_post(gr_hip_queue *q, const gr_hip_batch *b) {
+// Post batch b (device addresses) on k of q's rings (RES_TILES_PER_WG tiles
+// each, workgroup j < k taking tiles j, j + k, ...); *m receives what must be
+// done for it. c->mu held shared.
+static int res_post(gr_hip_queue *q, const gr_hip_batch *b, res_mark *m) {
 	gr_hip_ctx *c = q->ctx;
 	const uint32_t g = c->gen;
 	if (q->seen_serial != c->serial) { // the generation's upload (launch(): a stream wait)
 		HCK(hipEventSynchronize(c->ready_ev[g]));
 		q->seen_serial = c->serial;
 	}
-	const uint64_t seq = q->res_seq + 1;
-	for (uint32_t j = 0; j < q->res_w; j++)
-		if (seq > res_word(c->res_done, q->ring + (int)j) + RES_NDESC)
+	const uint32_t tiles = (b->n + 63) / 64;
+	uint32_t k = (tiles + RES_TILES_PER_WG - 1) / RES_TILES_PER_WG;
+	k = k < 1 ? 1 : k > q->res_w ? q->res_w : k;
+	for (uint32_t j = 0; j < k; j++)
+		if (q->res_posted.seq[j] + 1 > res_word(c->res_done, q->ring + (int)j) + RES_NDESC)
 			return -EBUSY; // (not reached: GR_HIP_NODE_DEPTH < RES_NDESC)
 	fwd4_params A{};
 	A.in = static_cast<const uint8_t *>(b->in_frames);
@@ -2356,24 +2370,18 @@ static int res_post(gr_hip_queue *q, const gr_hip_batch *b) {
 							    : b->in_stride;
 	A.spin_max = c->spin_max;
 	A.err = q->d_err;
-	// the batch split over k of the queue's W rings, RES_TILES_PER_WG tiles
-	// each (workgroup j < k takes tiles j, j + k, ...); the others get the
-	// descriptor with no tiles, so that every ring's seq moves on together
-	const uint32_t tiles = (b->n + 63) / 64;
-	uint32_t k = (tiles + RES_TILES_PER_WG - 1) / RES_TILES_PER_WG;
-	A.wgs = k < 1 ? 1 : k > q->res_w ? q->res_w : k;
+	A.wgs = k;
 	A.ptrs = (b->flags & GR_HIP_BATCH_F_FRAME_PTRS) ? 1 : 0;
-	for (uint32_t j = 0; j < q->res_w; j++) {
+	m->k = k;
+	for (uint32_t j = 0; j < k; j++) {
+		const uint64_t seq = q->res_posted.seq[j] + 1;
 		fwd4_res_desc &d = c->res_desc[(size_t)(q->ring + (int)j) * RES_NDESC + seq % RES_NDESC];
-		if (j >= A.wgs) { // none of its tiles: the workgroup stores the seq without reading A
-			__atomic_store_n(&d.seq, seq | FWD4_RES_EMPTY, __ATOMIC_RELEASE);
-			continue;
-		}
 		A.wg0 = j;
 		memcpy(&d.A, &A, sizeof(A));
 		__atomic_store_n(&d.seq, seq, __ATOMIC_RELEASE); // after A
+		q->res_posted.seq[j] = seq;
+		m->seq[j] = seq;
 	}
-	q->res_seq = seq;
 	return res_kick(c);
 }
 
@@ -2426,7 +2434,7 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 			return -EINVAL;
 		c->res_rings = (uint32_t)value;
 	} else if (strcmp(key, "resident_wgs") == 0) { // for queues that take their rings from then on
-		if (value < 1 || value > 64)
+		if (value < 1 || value > RES_WMAX)
 			return -EINVAL;
 		c->res_w = (uint32_t)value;
 	} else if (strcmp(key, "resident_nap") == 0) { // the next launch
@@ -3060,10 +3068,9 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 		// after everything already submitted on the queue, like gr_hip_fwd4_host;
 		// no timing events (the walk's own completion event is enough)
 		if (c->res_on && res_take(q)) {
-			if ((r = res_post(q, &b)) < 0)
+			if ((r = res_post(q, &b, &w.res)) < 0)
 				return r;
 			w.resident = true;
-			w.res_seq = q->res_seq;
 		} else if ((r = launch(q, q->s, &b, false)) < 0) {
 			return r;
 		}
@@ -3089,10 +3096,9 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 					  static_cast<gr_hip_verdict *>(w.d_v), ns, GR_HIP_LINE, GR_HIP_PREFIX,
 					  GR_HIP_BATCH_F_LINES_ONLY | GR_HIP_BATCH_F_PREFIX32};
 			if (c->res_on && res_take(q)) {
-				if ((r = res_post(q, &b)) < 0)
+				if ((r = res_post(q, &b, &w.res)) < 0)
 					return r;
 				w.resident = true;
-				w.res_seq = q->res_seq;
 			} else if ((r = launch(q, q->s, &b, false)) < 0) {
 				return r;
 			}
@@ -3156,7 +3162,7 @@ static int node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np,
 		direct->meta = w.own ? w.meta : nullptr; // no views: the hand-back reads the mbufs
 	uint64_t t_prof = prof_now();
 	if (!w.sync && w.resident) {
-		if ((r = res_wait(q, w.res_seq)) == 0)
+		if ((r = res_wait(q, w.res)) == 0)
 			r = q_check(q);
 	} else if (!w.sync) {
 		hipSetDevice(c->dev);
@@ -3320,7 +3326,7 @@ extern "C" int gr_hip_node_pending(gr_hip_queue_t *q, int *ready) {
 			if (w.sync) {
 				*ready = 1;
 			} else if (w.resident) { // a load of the ring's done word; a kernel that left is relaunched
-				if (res_is_done(q, w.res_seq))
+				if (res_is_done(q, w.res))
 					*ready = 1;
 				else if (const int r = res_kick(q->ctx))
 					return r;

@@ -497,10 +497,10 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               no hardware queue per batch); per-iface counters are then the
 //               hand-back's. 0 = one launch per batch (default; the grout
 //               module turns it on unless gpu_fwd4_conf.launch_per_batch)
-//   "resident_wgs" rings (workgroups) per queue: a batch is split over up to
-//               that many, 32 tiles (2048 packets) each (default 2; queues
-//               taking their rings from then on)
-//   "resident_rings" rings in all (default 64: 32 queues; before the first
+//   "resident_wgs" rings (workgroups) per queue, 1..8: a batch is split over
+//               up to that many, 32 tiles (2048 packets) each (default 4;
+//               queues taking their rings from then on)
+//   "resident_rings" rings in all (default 128: 32 queues; before the first
 //               resident batch only); the workgroups of rings no queue holds
 //               leave at once
 //   "resident_nap" a queue's helper rings (all but its first) back off their
