@@ -718,7 +718,10 @@ def test_graph_walk_control_plane_churn(readers, quiesce_each):
     none is dropped stale and nothing freed is read, across tens of
     cycles and their commits. Without them (the negative control) synchronize
     returns while batches naming the nexthop are still on the GPU, and the
-    node drops those packets at hand-back instead (stale > 0)."""
+    node drops those packets at hand-back instead (stale > 0); the registry
+    check at hand-back cannot close the window in which the nexthop is freed
+    right after it, so a few freed reads may happen too (round 5: 8 in one run,
+    0 in the others) -- what the readers are for."""
     L = lib()
     fp = graph_ctx()
     t = T.config_single_route()
@@ -759,7 +762,8 @@ def test_graph_walk_control_plane_churn(readers, quiesce_each):
     c = res[0]
     print("churn", readers, quiesce_each, c)
     assert c["err"] == 0 and c["recorded"] == n and c["cycles"] >= 10, c
-    assert c["freed_reads"] == 0, c  # the registries: nothing freed is ever handed to grout's nodes
+    if readers:  # nothing freed is ever handed to grout's nodes
+        assert c["freed_reads"] == 0, c
     out = np.zeros(n, dtype=OUT_DT)
     lines = np.zeros((n, abi.LINE), dtype=np.uint8)
     assert L.gh_results(out.ctypes.data, lines.ctypes.data) == n
