@@ -322,6 +322,7 @@ struct gr_hip_ctx {
 	uint32_t res_w; // rings (workgroups) per queue: each batch split over them (knob "resident_wgs")
 	uint32_t res_ms; // lifetime of an idle workgroup (knob "resident_ms")
 	uint32_t res_nap; // idle poll backoff ceiling, in s_sleep(8) units (knob "resident_nap")
+	uint32_t res_tiles; // tiles per workgroup a batch is split into, up to the queue's rings (knob "resident_tiles")
 	fwd4_res_desc *res_desc;
 	uint64_t *res_done, *res_exited;
 	uint32_t *res_stop;
@@ -844,6 +845,7 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->res_w = 4; // a batch uses up to 4 of them, 32 tiles each (measured: DESIGN.md §3.3)
 	c->res_ms = 50;
 	c->res_nap = 16;
+	c->res_tiles = 8; // RES_TILES_PER_WG (measured: DESIGN.md §3.3)
 	c->spin_max = 0;
 	c->untimed = 0;
 	c->time_every = 1;
@@ -2176,7 +2178,7 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 #define RES_NDESC 4 // descriptors per ring (GR_HIP_NODE_DEPTH batches in flight at most)
 #define RES_STRIDE 8 // uint64_t per ring in the done / exited words: a 64-byte line each
 #define RES_WAIT_NS (10ull * 1000000000ull) // a batch not done after this: -ETIMEDOUT
-#define RES_TILES_PER_WG 32 // tiles per workgroup a batch is split into (up to the queue's rings)
+#define RES_TILES_PER_WG 8 // default tiles per workgroup a batch is split into (knob "resident_tiles")
 
 static uint64_t res_word(const uint64_t *w, int ring) {
 	return __atomic_load_n(w + (size_t)ring * RES_STRIDE, __ATOMIC_ACQUIRE);
@@ -2351,7 +2353,7 @@ static int res_post(gr_hip_queue *q, const gr_hip_batch *b, res_mark *m) {
 		q->seen_serial = c->serial;
 	}
 	const uint32_t tiles = (b->n + 63) / 64;
-	uint32_t k = (tiles + RES_TILES_PER_WG - 1) / RES_TILES_PER_WG;
+	uint32_t k = (tiles + c->res_tiles - 1) / c->res_tiles;
 	k = k < 1 ? 1 : k > q->res_w ? q->res_w : k;
 	for (uint32_t j = 0; j < k; j++)
 		if (q->res_posted.seq[j] + 1 > res_word(c->res_done, q->ring + (int)j) + RES_NDESC)
@@ -2437,6 +2439,10 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < 1 || value > RES_WMAX)
 			return -EINVAL;
 		c->res_w = (uint32_t)value;
+	} else if (strcmp(key, "resident_tiles") == 0) {
+		if (value < 1)
+			return -EINVAL;
+		c->res_tiles = (uint32_t)value;
 	} else if (strcmp(key, "resident_nap") == 0) { // the next launch
 		if (value < 1 || value > 64)
 			return -EINVAL;

@@ -498,8 +498,10 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               hand-back's. 0 = one launch per batch (default; the grout
 //               module turns it on unless gpu_fwd4_conf.launch_per_batch)
 //   "resident_wgs" rings (workgroups) per queue, 1..8: a batch is split over
-//               up to that many, 32 tiles (2048 packets) each (default 4;
+//               up to that many, "resident_tiles" tiles each (default 4;
 //               queues taking their rings from then on)
+//   "resident_tiles" 64-packet tiles per workgroup a batch is split into
+//               (default 8)
 //   "resident_rings" rings in all (default 128: 32 queues; before the first
 //               resident batch only); the workgroups of rings no queue holds
 //               leave at once
