@@ -2291,7 +2291,12 @@ static bool res_take(gr_hip_queue *q) {
 		return false;
 	const uint32_t W = c->res_w;
 	for (uint32_t r = 0; r + W <= c->res_rings; r += W) { // W consecutive rings, in groups of W
-		if (!c->res_taken[r]) {
+		// all W free: queues that took theirs under another "resident_wgs"
+		// hold groups of another size
+		bool free = true;
+		for (uint32_t j = 0; j < W && free; j++)
+			free = !c->res_taken[r + j];
+		if (free) {
 			for (uint32_t j = 0; j < W; j++) { // 1: the queue's first ring, 2: a helper
 				c->res_taken[r + j] = 1;
 				__atomic_store_n(c->res_taken_h + r + j, j == 0 ? 1u : 2u, __ATOMIC_RELEASE);

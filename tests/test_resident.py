@@ -244,3 +244,89 @@ def test_resident_graph_control_plane_churn():
     fp.tune("resident", 1)  # the module's default
     G.test_graph_walk_control_plane_churn(1, 1)
     G.test_graph_walk_stream_batches(2)
+
+
+@pytest.fixture
+def knobs(resident):
+    """The split knobs back at their defaults after the test."""
+    yield resident
+    resident.tune("resident_wgs", 4)
+    resident.tune("resident_tiles", 8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wgs,tiles", [(1, 8), (2, 1), (3, 2), (8, 1), (8, 1000)])
+def test_resident_split_knobs(knobs, wgs, tiles):
+    """Ragged batches (1 to 15360 packets) split over every number of rings
+    the knobs allow, one workgroup per `tiles` tiles up to the queue's `wgs`
+    rings: each walk as the oracle's."""
+    from golden_util import fresh_fastpath_state
+    fp = knobs
+    assert fp.tune("resident_wgs", wgs) == 0 and fp.tune("resident_tiles", tiles) == 0
+    topo = T.config_fullview(count=50_000)
+    sizes = [1, 63, 64, 65, 129, 640, 1000, 4097, 15360]
+    fr, me = S.stream(sum(sizes), 0xD30 + wgs, routes=topo.route_array())
+    fresh_fastpath_state(fp, topo)
+    lines, v, st, want, ns_want = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
+    bufs, m = mbufs_for(fr, me)
+    q = fp.queue()
+    try:
+        tot = _pipelined(fp, q, m, list(np.cumsum([0] + sizes)))
+        compare_mbufs(m, want, bufs, lines)
+        assert np.array_equal(tot["packets"], ns_want["packets"])
+        assert np.array_equal(q.node_iface_stats(), st)
+        assert not q.stats()["rx_packets"].any()  # every batch went to the resident kernel
+    finally:
+        q.close()
+
+
+@pytest.mark.gpu
+def test_resident_rings_run_out(knobs):
+    """A queue takes its rings on its first batch, as many as "resident_wgs"
+    says then: groups of different sizes side by side (a group is taken only
+    whole and free); once no group of the current size is free, a queue's
+    batches get a launch each (its kernel counters show it), and a queue
+    closed hands its rings back. Every walk, on every queue, sequential or
+    all queues in flight at once, is the oracle's."""
+    from golden_util import fresh_fastpath_state
+    fp = knobs
+    topo = T.config_fullview(count=50_000)
+    per = 2000
+    fr, me = S.stream(per * 40, 0xD31, routes=topo.route_array())
+    fresh_fastpath_state(fp, topo)
+    lines, v, st, want, _ = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
+    bufs, m = mbufs_for(fr, me)
+    parts = [m[i * per:(i + 1) * per] for i in range(40)]
+
+    def walk(q, part):
+        q.node_start(part)
+        got, _ = q.node_finish()
+        assert got is part and q.unfinished == 0
+
+    qs = []
+    try:
+        # of 128 rings: 0-3 (groups of 4), 8-15 (of 8: 0-7 is not free), 18-20
+        # (of 3: 3-5, 6-8, 9-11, 12-14 and 15-17 are not), then 24-31, 32-39,
+        # ..., 120-127 (13 groups of 8); 3 more queues find none
+        for i, w in enumerate([4, 8, 3] + [8] * 16):
+            assert fp.tune("resident_wgs", w) == 0
+            qs.append(fp.queue())
+            walk(qs[i], parts[i])
+        launched = [i for i, q in enumerate(qs) if q.stats()["rx_packets"].any()]
+        assert launched == [16, 17, 18]
+        for i, q in enumerate(qs):  # all 19 queues in flight at once
+            q.node_start(parts[19 + i])
+        for i, q in enumerate(qs):
+            got, _ = q.node_finish()
+            assert got is parts[19 + i] and q.unfinished == 0
+        compare_mbufs(m[:per * 38], want[:per * 38], bufs[:per * 38], lines[:per * 38])
+        assert all(qs[i].stats()["rx_packets"].sum() == 2 * per for i in launched)
+        # rings 0-3 handed back: with 4-7, never taken, a group of 8 again
+        qs[0].close()
+        qs[0] = fp.queue()
+        walk(qs[0], parts[38])
+        assert not qs[0].stats()["rx_packets"].any()
+        compare_mbufs(parts[38], want[per * 38:per * 39], bufs[per * 38:per * 39], lines[per * 38:per * 39])
+    finally:
+        for q in qs:
+            q.close()
