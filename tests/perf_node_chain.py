@@ -128,6 +128,9 @@ def main():
     ap.add_argument("--out", default=None, help="also append the lines to this JSONL file")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="gr_hip_tune knobs of the GPU node's contexts, e.g. resident=1 (repeatable)")
+    ap.add_argument("--alt", action="append", default=[], metavar="KEY=VALUE/BACK",
+                    help="also run the GPU node with knob KEY at VALUE (gpu_alt), interleaved with the other "
+                         "modes in every rep, KEY set back to BACK after each run, e.g. resident=0/1 (repeatable)")
     args = ap.parse_args()
 
     import test_graph_walk as G
@@ -170,6 +173,8 @@ def main():
     for kv in args.tune:
         k, v = kv.split("=")
         fp.tune(k, int(v))
+    alt = [(kv.split("=")[0], int(kv.split("=")[1].split("/")[0])) for kv in args.alt]
+    alt_back = [(kv.split("=")[0], int(kv.split("/")[1])) for kv in args.alt]
     ifs = np.ascontiguousarray(topo.ifaces[topo.ifaces["id"] != 0])
     nh = np.ascontiguousarray(topo.nh[1:topo.n_nh + 1])
     assert L.gh_set_objects(ifs.ctypes.data, len(ifs), nh.ctypes.data, 1, len(nh)) == 0
@@ -201,6 +206,8 @@ def main():
         assert L.gh_workers_first(kmax if mode == "chain" else 0) == 0
         L.gh_set_null_node(1 if mode == "alone" else 0)
         L.gh_set_latency(1 if lat else 0)
+        for key, v in (alt if mode == "gpu_alt" else []):
+            fp.tune(key, v)
         try:
             assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, m) == 0
             s, w = ctypes.c_double(), ctypes.c_uint64()
@@ -214,6 +221,8 @@ def main():
                 hist = (hist, cpn.value)
             return s.value, hist
         finally:
+            for key, v in (alt_back if mode == "gpu_alt" else []):
+                fp.tune(key, v)
             L.gh_set_null_node(0)
             L.gh_set_latency(0)
             L.gh_workers_first(0)
@@ -226,22 +235,23 @@ def main():
         cpus = place(k)
         m = k * args.per_thread
         pk = m * per
-        for mode in ("gpu", "chain", "alone"):  # warm-up: pages, queues, pinned slots, FIB in cache
+        gmodes = ("gpu", "gpu_alt") if alt else ("gpu",)
+        for mode in gmodes + ("chain", "alone"):  # warm-up: pages, queues, pinned slots, FIB in cache
             once(k, m, mode)
-        t = {"gpu": [], "chain": [], "alone": []}
+        t = {mode: [] for mode in gmodes + ("chain", "alone")}
         for _ in range(args.reps):
             for mode in t:
                 t[mode].append(once(k, m, mode)[0])
         med = {mode: float(np.median(v)) for mode, v in t.items()}
         lat = {}
-        for mode in ("gpu", "chain"):
+        for mode in gmodes + ("chain",):
             _, (hist, cpn) = once(k, m, mode, lat=True)
             assert int(hist.sum()) == pk, (mode, int(hist.sum()), pk)
             lat[mode] = percentiles(hist.astype(np.float64), cpn, floor)
         line = {"threads": k, "packets": pk, "lcores": args.lcores, "cpus": cpus, "recycle": args.recycle,
-                "passes": per, "batch": batch, "reps": args.reps, "tune": args.tune,
+                "passes": per, "batch": batch, "reps": args.reps, "tune": args.tune, "alt": args.alt,
                 "workload": "config3 full view (fib_inject 1M routes), 64 B, seeded stream 0x67720002"}
-        for mode in ("gpu", "chain"):
+        for mode in gmodes + ("chain",):
             line[mode] = {"mpps": round(pk / med[mode] / 1e6, 1),
                           "cpu_ns_per_pkt_per_worker": round(med[mode] * 1e9 * k / pk, 1),
                           "walk_ns_per_pkt_per_worker": round((med[mode] - med["alone"]) * 1e9 * k / pk, 1),
@@ -249,6 +259,8 @@ def main():
         line["harness_alone"] = {"mpps": round(pk / med["alone"] / 1e6, 1),
                                  "cpu_ns_per_pkt_per_worker": round(med["alone"] * 1e9 * k / pk, 1)}
         line["gpu_over_chain"] = round(med["chain"] / med["gpu"], 3)
+        if alt:
+            line["gpu_over_gpu_alt"] = round(med["gpu_alt"] / med["gpu"], 3)
         s = json.dumps(line)
         print(s, flush=True)
         if out:
