@@ -173,10 +173,14 @@ struct fwd4_params {
 // The resident kernel's batches: ring r of a context holds `ndesc`
 // descriptors in pinned host memory; the host writes A, then `seq` (release);
 // the kernel's workgroup r takes them in seq order (1, 2, ...), runs each,
-// and stores its seq into done[r * stride] (release, system scope).
+// and stores its seq into done[r * stride] (release, system scope). A batch
+// split over k rings of a queue is posted to its helpers (rings r+1 .. r+k-1)
+// first, then to its first ring r, whose descriptor names the helpers' seqs:
+// the first ring's workgroup wakes them through device memory (wake[]), so
+// that only first rings poll host memory.
 struct __attribute__((aligned(64))) fwd4_res_desc {
 	uint64_t seq;
-	uint64_t _pad[7];
+	uint64_t helper_seq[7]; // first ring: the seq of this batch on ring r + 1 + j, j < A.wgs - 1
 	struct fwd4_params A;
 };
 
@@ -185,13 +189,14 @@ struct fwd4_res_params {
 	uint64_t *done; // [rings * stride], host memory
 	uint64_t *exited; // [rings * stride], host memory: launch_id once ring r's workgroup has left
 	uint32_t *stop; // host memory: nonzero = every workgroup leaves after its batch
+	uint64_t *wake; // [rings * stride], device memory: the last helper seq a first ring woke ring r for
 	const uint32_t *taken; // host memory [rings]: 0 = no queue holds ring r (its workgroup leaves at
 	                       // once), 1 = a queue's first ring, 2 = one of its helpers (polls backed off)
 	uint64_t lifetime; // s_memrealtime ticks (100 MHz): a workgroup idle past it sets *stop
 	uint64_t launch_id;
 	uint32_t ndesc;
 	uint32_t stride; // uint64_t per ring in done / exited
-	uint32_t nap_max; // helper rings' idle polls back off up to this many s_sleep(8) between reads
+	uint32_t nap_max; // helper rings' idle polls (device memory) back off up to this many s_sleep(8)
 	uint32_t _pad;
 };
 

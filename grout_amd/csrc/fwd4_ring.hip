@@ -503,20 +503,32 @@ __global__ void __launch_bounds__(ring_cfg_res::WAVES * 64) gr_fwd4_resident(con
 					   __HIP_MEMORY_SCOPE_SYSTEM);
 		return;
 	}
-	// a queue's first ring polls at full rate; its helper rings (taken 2: only
-	// batches of more than 32 tiles reach them) back off to R.nap_max
-	const uint32_t nap_max = go == 2 ? R.nap_max : 1;
+	// a queue's first ring polls its descriptor in host memory at full rate;
+	// its helper rings (taken 2: batches of more than 8 tiles reach them) poll
+	// their wake word in device memory, which the first ring's workgroup
+	// writes when it takes a batch split over them, backed off to R.nap_max,
+	// and read the stop word over PCIe only every 16th poll
+	const bool helper = go == 2;
+	const uint32_t nap_max = helper ? R.nap_max : 1;
+	const uint32_t stop_every = helper ? 15u : 3u; // mask
+	const uint64_t *wake = R.wake + (size_t)blockIdx.x * R.stride;
 	__syncthreads(); // every wave has read go
-	uint32_t nap = 1; // idle polls back off (each one is a read over PCIe)
+	uint32_t nap = 1; // idle polls back off
 	for (;;) {
 		if (tid == 0) {
 			const uint64_t want = seq_s;
 			const fwd4_res_desc *d = ring + want % R.ndesc;
 			uint32_t g = 0;
-			for (;;) {
-				if (__hip_atomic_load(R.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
+			for (uint32_t poll = 0;; poll++) {
+				if ((poll & stop_every) == 0
+				    && __hip_atomic_load(R.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
 					break; // every workgroup leaves: the host relaunches once all have
-				if (sys_load64(&d->seq) == want) {
+				// relaxed polls (they bypass the caches; an acquire would invalidate
+				// this XCD's L2 on every poll, which idle rings then do all the
+				// time), one acquire fence once the batch is there
+				if ((!helper || __hip_atomic_load(wake, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want)
+				    && __hip_atomic_load(&d->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == want) {
+					__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 					g = 1;
 					break;
 				}
@@ -543,6 +555,15 @@ __global__ void __launch_bounds__(ring_cfg_res::WAVES * 64) gr_fwd4_resident(con
 				dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 		}
 		__syncthreads();
+		if (!helper && tid > 0 && tid < A.wgs && blockIdx.x + tid < gridDim.x) { // wake the helpers it is split over
+			// relaxed both: the helper acquires its own descriptor's seq before
+			// it reads it, so nothing here needs ordering (and a release would
+			// write back this XCD's L2)
+			const uint64_t hs = __hip_atomic_load(&ring[seq_s % R.ndesc].helper_seq[tid - 1], __ATOMIC_RELAXED,
+							      __HIP_MEMORY_SCOPE_SYSTEM);
+			__hip_atomic_store(R.wake + (size_t)(blockIdx.x + tid) * R.stride, hs, __ATOMIC_RELAXED,
+					   __HIP_MEMORY_SCOPE_AGENT);
+		}
 		// the edge table of the generation this batch names
 		for (uint32_t i = tid; i < sizeof(fwd4_edges); i += C::WAVES * 64)
 			reinterpret_cast<uint8_t *>(&edges)[i] = reinterpret_cast<const uint8_t *>(&A.T->edges)[i];

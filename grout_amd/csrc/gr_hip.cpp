@@ -327,6 +327,7 @@ struct gr_hip_ctx {
 	uint64_t *res_done, *res_exited;
 	uint32_t *res_stop;
 	uint32_t *res_taken_h; // [res_rings]: rings held by a queue, as the kernel reads it
+	uint64_t *res_wake_d = nullptr; // [res_rings * RES_STRIDE], device memory: helpers' wake words
 	fwd4_res_desc *res_desc_d; // their device addresses
 	uint64_t *res_done_d, *res_exited_d;
 	uint32_t *res_stop_d, *res_taken_d;
@@ -2199,6 +2200,8 @@ static void res_free(gr_hip_ctx *c) {
 	hipHostFree(c->res_exited);
 	hipHostFree(c->res_stop);
 	hipHostFree(c->res_taken_h);
+	hipFree(c->res_wake_d);
+	c->res_wake_d = nullptr;
 	c->res_taken_h = nullptr;
 	c->res_ev = nullptr;
 	c->res_s = nullptr;
@@ -2227,10 +2230,14 @@ static int res_setup(gr_hip_ctx *c) {
 	    || hipHostGetDevicePointer(reinterpret_cast<void **>(&c->res_done_d), c->res_done, 0) != hipSuccess
 	    || hipHostGetDevicePointer(reinterpret_cast<void **>(&c->res_exited_d), c->res_exited, 0) != hipSuccess
 	    || hipHostGetDevicePointer(reinterpret_cast<void **>(&c->res_stop_d), c->res_stop, 0) != hipSuccess
+	    || hipMalloc(reinterpret_cast<void **>(&c->res_wake_d), nw) != hipSuccess
 	    // its own priority: a hardware queue of its own, not shared with the
 	    // streams whose work would wait behind a resident launch
 	    || hipStreamCreateWithPriority(&c->res_s, hipStreamNonBlocking, greatest) != hipSuccess
-	    || hipEventCreateWithFlags(&c->res_ev, hipEventDisableTiming) != hipSuccess) {
+	    || hipEventCreateWithFlags(&c->res_ev, hipEventDisableTiming) != hipSuccess
+	    // before the first launch, on its stream (no device-wide sync: another
+	    // context's resident kernel may be running on this device)
+	    || hipMemsetAsync(c->res_wake_d, 0, nw, c->res_s) != hipSuccess) {
 		(void)hipGetLastError();
 		res_free(c);
 		return -ENOMEM;
@@ -2261,6 +2268,7 @@ static int res_ensure(gr_hip_ctx *c) {
 	R.done = c->res_done_d;
 	R.exited = c->res_exited_d;
 	R.stop = c->res_stop_d;
+	R.wake = c->res_wake_d;
 	R.taken = c->res_taken_d;
 	R.lifetime = (uint64_t)c->res_ms * 100000u; // s_memrealtime: 100 MHz
 	R.launch_id = ++c->res_launch;
@@ -2380,11 +2388,15 @@ static int res_post(gr_hip_queue *q, const gr_hip_batch *b, res_mark *m) {
 	A.wgs = k;
 	A.ptrs = (b->flags & GR_HIP_BATCH_F_FRAME_PTRS) ? 1 : 0;
 	m->k = k;
-	for (uint32_t j = 0; j < k; j++) {
+	// the helpers first: the first ring's workgroup wakes them (fwd4_res_desc)
+	for (uint32_t j = k; j-- > 0;) {
 		const uint64_t seq = q->res_posted.seq[j] + 1;
 		fwd4_res_desc &d = c->res_desc[(size_t)(q->ring + (int)j) * RES_NDESC + seq % RES_NDESC];
 		A.wg0 = j;
 		memcpy(&d.A, &A, sizeof(A));
+		if (j == 0)
+			for (uint32_t h = 1; h < k; h++)
+				d.helper_seq[h - 1] = m->seq[h];
 		__atomic_store_n(&d.seq, seq, __ATOMIC_RELEASE); // after A
 		q->res_posted.seq[j] = seq;
 		m->seq[j] = seq;

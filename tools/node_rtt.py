@@ -28,7 +28,8 @@ def main():
     ap.add_argument("--iters", type=int, default=300)
     ap.add_argument("--warm", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=2)
-    ap.add_argument("--tiles", default="32", help="resident_tiles settings to compare, e.g. 8,32")
+    ap.add_argument("--tiles", default="8", help="resident_tiles settings to compare, e.g. 8,32")
+    ap.add_argument("--wgs", default="4", help="resident_wgs (rings per queue) settings to compare, e.g. 4,8")
     a = ap.parse_args()
     from golden_util import fresh_fastpath_state
     from grout_amd import synth as S
@@ -43,10 +44,11 @@ def main():
     fr, me = S.stream(max(sizes), 0x277, routes=topo.route_array())
     res = {}
     for _ in range(a.rounds):
-        for resident in [0] + [int(t) for t in a.tiles.split(",")]:  # 0: a launch per batch
-            fp.tune("resident", 1 if resident else 0)
+        for resident, wgs in [(0, 0)] + [(int(t), int(w)) for t in a.tiles.split(",") for w in a.wgs.split(",")]:
+            fp.tune("resident", 1 if resident else 0)  # 0: a launch per batch
             if resident:
                 fp.tune("resident_tiles", resident)
+                fp.tune("resident_wgs", wgs)
             q = fp.queue()
             for n in sizes:
                 times = []
@@ -57,10 +59,11 @@ def main():
                     q.node_finish()
                     if i >= a.warm:
                         times.append(time.perf_counter() - t)
-                res.setdefault((resident, n), []).append(float(np.median(times)) * 1e6)
+                res.setdefault((resident, wgs, n), []).append(float(np.median(times)) * 1e6)
             q.close()
-    for (resident, n), v in sorted(res.items()):
-        print(json.dumps({"resident_tiles": resident, "packets": n, "rtt_us_median": round(float(np.median(v)), 1),
+    for (resident, wgs, n), v in sorted(res.items()):
+        print(json.dumps({"resident_tiles": resident, "resident_wgs": wgs, "packets": n,
+                          "rtt_us_median": round(float(np.median(v)), 1),
                           "rounds": [round(x, 1) for x in v]}), flush=True)
     fp.tune("resident", 0)
     fp.close()
