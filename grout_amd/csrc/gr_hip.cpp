@@ -245,6 +245,7 @@ struct alignas(128) gr_hip_queue {
 	uint32_t pg_cap = 0;
 	int ring = -1; // the first of the resident kernel's res_w rings this queue posts to (-1: none yet)
 	uint32_t res_w = 0; // how many (the context's res_w when they were taken)
+	uint32_t res_inflight = 0; // its resident batches posted and not yet finished
 	res_mark res_posted; // the last seq posted on each of its rings
 	res_mark res_retire; // posted before the last FIB publication (retire_wait)
 };
@@ -323,6 +324,9 @@ struct gr_hip_ctx {
 	uint32_t res_ms; // lifetime of an idle workgroup (knob "resident_ms")
 	uint32_t res_nap; // idle poll backoff ceiling, in s_sleep(8) units (knob "resident_nap")
 	uint32_t res_tiles; // tiles per workgroup a batch is split into, up to the queue's rings (knob "resident_tiles")
+	uint32_t res_split = 0; // at most this many of a queue's rings per batch (0: all; knob "resident_split")
+	uint32_t res_budget = 0; // workgroups the busy queues' batches are split over together (knob "resident_budget"; 0: no cap)
+	std::atomic<uint32_t> res_busy{0}; // queues with resident batches in flight
 	fwd4_res_desc *res_desc;
 	uint64_t *res_done, *res_exited;
 	uint32_t *res_stop;
@@ -1965,6 +1969,8 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 			hipStreamSynchronize(h.s);
 	if (q->ring >= 0) {
 		res_wait(q, q->res_posted); // its resident batches, then the rings are free again
+		if (q->res_inflight > 0)
+			c->res_busy.fetch_sub(1, std::memory_order_relaxed);
 		std::lock_guard<std::mutex> rl(c->res_mu);
 		for (uint32_t j = 0; j < q->res_w; j++) {
 			c->res_taken[(size_t)q->ring + j] = 0;
@@ -2368,6 +2374,13 @@ static int res_post(gr_hip_queue *q, const gr_hip_batch *b, res_mark *m) {
 	const uint32_t tiles = (b->n + 63) / 64;
 	uint32_t k = (tiles + c->res_tiles - 1) / c->res_tiles;
 	k = k < 1 ? 1 : k > q->res_w ? q->res_w : k;
+	if (c->res_split != 0 && k > c->res_split)
+		k = c->res_split;
+	if (c->res_budget != 0) { // busy GPU: fewer workgroups per batch
+		const uint32_t busy = c->res_busy.load(std::memory_order_relaxed) + (q->res_inflight == 0 ? 1 : 0);
+		const uint32_t cap = c->res_budget / busy;
+		k = k > cap ? (cap < 1 ? 1 : cap) : k;
+	}
 	for (uint32_t j = 0; j < k; j++)
 		if (q->res_posted.seq[j] + 1 > res_word(c->res_done, q->ring + (int)j) + RES_NDESC)
 			return -EBUSY; // (not reached: GR_HIP_NODE_DEPTH < RES_NDESC)
@@ -2401,6 +2414,8 @@ static int res_post(gr_hip_queue *q, const gr_hip_batch *b, res_mark *m) {
 		q->res_posted.seq[j] = seq;
 		m->seq[j] = seq;
 	}
+	if (q->res_inflight++ == 0)
+		c->res_busy.fetch_add(1, std::memory_order_relaxed);
 	return res_kick(c);
 }
 
@@ -2460,6 +2475,14 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < 1)
 			return -EINVAL;
 		c->res_tiles = (uint32_t)value;
+	} else if (strcmp(key, "resident_budget") == 0) { // the next batches of every queue; 0: off
+		if (value < 0)
+			return -EINVAL;
+		c->res_budget = (uint32_t)value;
+	} else if (strcmp(key, "resident_split") == 0) { // the next batches of every queue
+		if (value < 0 || value > RES_WMAX)
+			return -EINVAL;
+		c->res_split = (uint32_t)value;
 	} else if (strcmp(key, "resident_nap") == 0) { // the next launch
 		if (value < 1 || value > 64)
 			return -EINVAL;
@@ -2470,6 +2493,8 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		c->res_ms = (uint32_t)value;
 	} else if (strcmp(key, "resident_launches") == 0) { // read
 		return (int)c->res_launch;
+	} else if (strcmp(key, "resident_busy") == 0) { // read: queues with resident batches in flight
+		return (int)c->res_busy.load();
 	} else if (strcmp(key, "stage_min_tiles") == 0) {
 		if (value < 0)
 			return -EINVAL;
@@ -3187,6 +3212,8 @@ static int node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np,
 	if (!w.sync && w.resident) {
 		if ((r = res_wait(q, w.res)) == 0)
 			r = q_check(q);
+		if (q->res_inflight > 0 && --q->res_inflight == 0)
+			c->res_busy.fetch_sub(1, std::memory_order_relaxed);
 	} else if (!w.sync) {
 		hipSetDevice(c->dev);
 		HCK(hipEventSynchronize(w.done));

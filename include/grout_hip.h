@@ -502,12 +502,21 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               queues taking their rings from then on)
 //   "resident_tiles" 64-packet tiles per workgroup a batch is split into
 //               (default 8)
+//   "resident_split" at most this many of a queue's rings per batch, from the
+//               next batch on (default 0: all of them)
+//   "resident_budget" workgroups the batches of all busy queues (queues with
+//               resident batches in flight) are split over together: a batch
+//               takes at most budget / busy rings, at least 1 (32: a lone
+//               worker's batch up to its 4 rings, 16 busy workers' 2 each);
+//               0 = no cap (default: the gain under load is within the host's
+//               noise). "resident_busy" (read): busy queues now
 //   "resident_rings" rings in all (default 128: 32 queues; before the first
 //               resident batch only); the workgroups of rings no queue holds
 //               leave at once
-//   "resident_nap" a queue's helper rings (all but its first) back off their
-//               idle polls up to this many s_sleep(8) between reads (default
-//               16; the next launch)
+//   "resident_nap" a queue's helper rings (all but its first: they poll a
+//               wake word in device memory that the first ring's workgroup
+//               writes) back off their idle polls up to this many s_sleep(8)
+//               between reads (default 16; the next launch)
 //   "resident_ms" an idle workgroup leaves after this long, all with it; the
 //               next batch launches the kernel again (default 50)
 //   "resident_launches" (read) resident launches so far

@@ -252,17 +252,23 @@ def knobs(resident):
     yield resident
     resident.tune("resident_wgs", 4)
     resident.tune("resident_tiles", 8)
+    resident.tune("resident_split", 0)
+    resident.tune("resident_budget", 0)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wgs,tiles", [(1, 8), (2, 1), (3, 2), (8, 1), (8, 1000)])
-def test_resident_split_knobs(knobs, wgs, tiles):
+@pytest.mark.parametrize("wgs,tiles,split,budget", [(1, 8, 0, 32), (2, 1, 0, 32), (3, 2, 0, 32), (8, 1, 0, 0),
+                                                   (8, 1000, 0, 32), (8, 1, 5, 0), (8, 1, 0, 3), (4, 8, 0, 1)])
+def test_resident_split_knobs(knobs, wgs, tiles, split, budget):
     """Ragged batches (1 to 15360 packets) split over every number of rings
     the knobs allow, one workgroup per `tiles` tiles up to the queue's `wgs`
-    rings: each walk as the oracle's."""
+    rings, at most `split`, at most `budget` over the busy queues (here one,
+    two batches in flight): each walk as the oracle's, and the queue no longer
+    busy after its last."""
     from golden_util import fresh_fastpath_state
     fp = knobs
     assert fp.tune("resident_wgs", wgs) == 0 and fp.tune("resident_tiles", tiles) == 0
+    assert fp.tune("resident_split", split) == 0 and fp.tune("resident_budget", budget) == 0
     topo = T.config_fullview(count=50_000)
     sizes = [1, 63, 64, 65, 129, 640, 1000, 4097, 15360]
     fr, me = S.stream(sum(sizes), 0xD30 + wgs, routes=topo.route_array())
@@ -276,6 +282,7 @@ def test_resident_split_knobs(knobs, wgs, tiles):
         assert np.array_equal(tot["packets"], ns_want["packets"])
         assert np.array_equal(q.node_iface_stats(), st)
         assert not q.stats()["rx_packets"].any()  # every batch went to the resident kernel
+        assert fp.tune("resident_busy") == 0
     finally:
         q.close()
 
@@ -320,6 +327,7 @@ def test_resident_rings_run_out(knobs):
             got, _ = q.node_finish()
             assert got is parts[19 + i] and q.unfinished == 0
         compare_mbufs(m[:per * 38], want[:per * 38], bufs[:per * 38], lines[:per * 38])
+        assert fp.tune("resident_busy") == 0
         assert all(qs[i].stats()["rx_packets"].sum() == 2 * per for i in launched)
         # rings 0-3 handed back: with 4-7, never taken, a group of 8 again
         qs[0].close()
