@@ -190,9 +190,11 @@ struct fwd4_res_params {
 	uint64_t *exited; // [rings * stride], host memory: launch_id once ring r's workgroup has left
 	uint32_t *stop; // host memory: nonzero = every workgroup leaves after its batch
 	uint64_t *wake; // [rings * stride], device memory: the last helper seq a first ring woke ring r for
+	uint64_t *active; // device memory: s_memrealtime when a workgroup last finished a batch
 	const uint32_t *taken; // host memory [rings]: 0 = no queue holds ring r (its workgroup leaves at
 	                       // once), 1 = a queue's first ring, 2 = one of its helpers (polls backed off)
-	uint64_t lifetime; // s_memrealtime ticks (100 MHz): a workgroup idle past it sets *stop
+	uint64_t lifetime; // s_memrealtime ticks (100 MHz): a first ring idle past it, with no batch
+	                   // finished anywhere for as long (*active), sets *stop
 	uint64_t launch_id;
 	uint32_t ndesc;
 	uint32_t stride; // uint64_t per ring in done / exited

@@ -491,7 +491,7 @@ __global__ void __launch_bounds__(ring_cfg_res::WAVES * 64) gr_fwd4_resident(con
 	const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
 	uint64_t *done = R.done + (size_t)blockIdx.x * R.stride;
 	const fwd4_res_desc *ring = R.descs + (size_t)blockIdx.x * R.ndesc;
-	const uint64_t until = __builtin_amdgcn_s_memrealtime() + R.lifetime;
+	uint64_t idle_since = __builtin_amdgcn_s_memrealtime(); // thread 0's: its last batch done
 	if (tid == 0) {
 		seq_s = sys_load64(done) + 1; // a relaunch resumes after the last batch done
 		go = __hip_atomic_load(R.taken + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -532,9 +532,18 @@ __global__ void __launch_bounds__(ring_cfg_res::WAVES * 64) gr_fwd4_resident(con
 					g = 1;
 					break;
 				}
-				if (__builtin_amdgcn_s_memrealtime() > until) { // idle past the lifetime
-					__hip_atomic_store(R.stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-					break;
+				// idle past the lifetime, and so is every ring (the last batch
+				// any workgroup finished, *R.active): the kernel leaves. Helpers
+				// leave with the first rings, never of their own accord
+				const uint64_t now = __builtin_amdgcn_s_memrealtime();
+				if (!helper && now - idle_since > R.lifetime) {
+					const uint64_t act = __hip_atomic_load(R.active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					if (act > now || now - act <= R.lifetime) {
+						idle_since = act > now ? now : act; // another ring is busy: look again later
+					} else {
+						__hip_atomic_store(R.stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+						break;
+					}
 				}
 				for (uint32_t i = 0; i < nap; i++)
 					__builtin_amdgcn_s_sleep(8);
@@ -604,6 +613,8 @@ __global__ void __launch_bounds__(ring_cfg_res::WAVES * 64) gr_fwd4_resident(con
 			// release at system scope: the batch's lines and verdicts before its seq
 			__hip_atomic_store(done, seq_s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 			seq_s++;
+			idle_since = __builtin_amdgcn_s_memrealtime();
+			__hip_atomic_store(R.active, idle_since, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		}
 		__syncthreads();
 	}

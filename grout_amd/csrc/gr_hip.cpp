@@ -2175,8 +2175,8 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 // The kernel's workgroup for a ring stores the seq into the ring's done word
 // once its tiles' results are in host memory; the batch is done when all k
 // are (the node polls those words: loads, no runtime call, no hardware queue
-// held per batch: DESIGN.md §6.3). A workgroup idle past the lifetime sets
-// the stop word and all leave after their batch; whoever then finds a batch
+// held per batch: DESIGN.md §6.3). Once no ring has finished a batch for the
+// lifetime, a first ring sets the stop word and all leave after their batch; whoever then finds a batch
 // waiting launches the kernel again, once every ring's exited word carries
 // the last launch's id, so that one workgroup at most ever serves a ring.
 // Posts wait for the FIB generation's upload on the host (launches make their
@@ -2236,14 +2236,14 @@ static int res_setup(gr_hip_ctx *c) {
 	    || hipHostGetDevicePointer(reinterpret_cast<void **>(&c->res_done_d), c->res_done, 0) != hipSuccess
 	    || hipHostGetDevicePointer(reinterpret_cast<void **>(&c->res_exited_d), c->res_exited, 0) != hipSuccess
 	    || hipHostGetDevicePointer(reinterpret_cast<void **>(&c->res_stop_d), c->res_stop, 0) != hipSuccess
-	    || hipMalloc(reinterpret_cast<void **>(&c->res_wake_d), nw) != hipSuccess
+	    || hipMalloc(reinterpret_cast<void **>(&c->res_wake_d), nw + 64) != hipSuccess // + the active word
 	    // its own priority: a hardware queue of its own, not shared with the
 	    // streams whose work would wait behind a resident launch
 	    || hipStreamCreateWithPriority(&c->res_s, hipStreamNonBlocking, greatest) != hipSuccess
 	    || hipEventCreateWithFlags(&c->res_ev, hipEventDisableTiming) != hipSuccess
 	    // before the first launch, on its stream (no device-wide sync: another
 	    // context's resident kernel may be running on this device)
-	    || hipMemsetAsync(c->res_wake_d, 0, nw, c->res_s) != hipSuccess) {
+	    || hipMemsetAsync(c->res_wake_d, 0, nw + 64, c->res_s) != hipSuccess) {
 		(void)hipGetLastError();
 		res_free(c);
 		return -ENOMEM;
@@ -2275,6 +2275,7 @@ static int res_ensure(gr_hip_ctx *c) {
 	R.exited = c->res_exited_d;
 	R.stop = c->res_stop_d;
 	R.wake = c->res_wake_d;
+	R.active = c->res_wake_d + (size_t)c->res_rings * RES_STRIDE;
 	R.taken = c->res_taken_d;
 	R.lifetime = (uint64_t)c->res_ms * 100000u; // s_memrealtime: 100 MHz
 	R.launch_id = ++c->res_launch;

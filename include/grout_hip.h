@@ -517,8 +517,8 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               wake word in device memory that the first ring's workgroup
 //               writes) back off their idle polls up to this many s_sleep(8)
 //               between reads (default 16; the next launch)
-//   "resident_ms" an idle workgroup leaves after this long, all with it; the
-//               next batch launches the kernel again (default 50)
+//   "resident_ms" the kernel leaves once no ring has finished a batch for this
+//               long; the next batch launches it again (default 50)
 //   "resident_launches" (read) resident launches so far
 //   "stage_min_tiles" the fast adjacencies (and IPv6 first-level slice) are
 //               staged in each workgroup's LDS only when the launch gives every

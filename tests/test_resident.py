@@ -338,3 +338,49 @@ def test_resident_rings_run_out(knobs):
     finally:
         for q in qs:
             q.close()
+
+
+@pytest.mark.gpu
+def test_resident_lifetime_is_idleness(resident):
+    """The kernel leaves when no ring has finished a batch for the lifetime,
+    not when one ring has been idle that long: a queue that holds its rings
+    and posts nothing does not make the kernel leave under another queue's
+    steady walks (no relaunch over ten lifetimes of them); once all are
+    idle, it leaves and the next batch launches it again."""
+    from golden_util import fresh_fastpath_state
+    fp = resident
+    assert fp.tune("resident_ms", 50) == 0
+    topo = T.config_fullview(count=50_000)
+    per = 4096
+    fr, me = S.stream(per * 8, 0xD32, routes=topo.route_array())
+    fresh_fastpath_state(fp, topo)
+    lines, v, st, want, _ = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
+    q1, q2 = fp.queue(), fp.queue()
+    try:
+        bufs, m = mbufs_for(fr[:per], me[:per])
+        q2.node_start(m)  # q2 takes its rings, then stays idle
+        q2.node_finish()
+        q1.node_start(m)
+        q1.node_finish()
+        l0 = fp.tune("resident_launches")
+        t0 = time.perf_counter()
+        k = 0
+        while time.perf_counter() - t0 < 0.5:  # ten lifetimes of steady walks on q1
+            i = k % 8
+            bufs, m = mbufs_for(fr[i * per:(i + 1) * per], me[i * per:(i + 1) * per])
+            q1.node_start(m)
+            got, _ = q1.node_finish()
+            assert got is m and q1.unfinished == 0
+            compare_mbufs(m, want[i * per:(i + 1) * per], bufs, lines[i * per:(i + 1) * per])
+            k += 1
+        assert k > 20
+        assert fp.tune("resident_launches") == l0  # q2's idle first ring did not stop it
+        time.sleep(0.25)  # all idle: it leaves
+        bufs, m = mbufs_for(fr[:per], me[:per])
+        q2.node_start(m)
+        q2.node_finish()
+        compare_mbufs(m, want[:per], bufs, lines[:per])
+        assert fp.tune("resident_launches") == l0 + 1
+    finally:
+        q1.close()
+        q2.close()
