@@ -124,6 +124,13 @@ int gpu_fwd4_set_depth(uint32_t depth) {
 	return 0;
 }
 
+int gpu_fwd4_set_launch_per_batch(int on) {
+	conf.launch_per_batch = on ? 1 : 0;
+	for (uint32_t i = 0; i < n_gpus; i++)
+		gr_hip_tune(gpus[i].ctx, "resident", on ? 0 : 1);
+	return 0;
+}
+
 int gpu_fwd4_set_rx_burst(uint32_t rx_burst) {
 	if (rx_burst == 0 || rx_burst > RTE_GRAPH_BURST_SIZE)
 		return -EINVAL;
@@ -592,10 +599,11 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 	return delivered;
 }
 
-// A batch spends at least this long on the GPU (launch, PCIe both ways, the
-// kernel's tile latency: ~30 us for 64 packets): no poll before.
-// Nor before 3/4 of what the last batches took: each poll is a runtime call
-// (hipEventQuery), whose locks every worker of the process shares.
+// A batch spends at least this long on the GPU (PCIe both ways, the kernel's
+// tile latency: ~12 us for 64 packets resident): no poll before.
+// With a launch per batch, nor before 3/4 of what the last batches took: each
+// poll is then a runtime call (hipEventQuery), whose locks every worker of the
+// process shares; with the resident kernel a poll is a load of a done word.
 #define REAP_MIN_NS 10000
 
 // The batch on the GPU is done: hand it back now (a poll, no wait).
@@ -604,7 +612,7 @@ static uint32_t reap(struct rte_graph *graph, struct rte_node *node, struct gpu_
 	if (!w->pending)
 		return 0;
 	const uint64_t t = now_ns(), waited = t - w->pend_ns;
-	if (waited < REAP_MIN_NS || waited < w->gpu_ns / 4 * 3)
+	if (waited < REAP_MIN_NS || (conf.launch_per_batch && waited < w->gpu_ns / 4 * 3))
 		return 0;
 	PROF_T0();
 	const int r = gr_hip_node_pending(w->q, &ready);

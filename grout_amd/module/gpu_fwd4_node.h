@@ -113,6 +113,9 @@ int gpu_fwd4_configure(const struct gpu_fwd4_conf *);
 void gpu_fwd4_conf_get(struct gpu_fwd4_conf *);
 // Batches in flight per graph (1 or 2), at any time. 0 or -EINVAL.
 int gpu_fwd4_set_depth(uint32_t depth);
+// 1: one launch per batch; 0: batches posted to the resident kernel (the
+// default, gpu_fwd4_conf.launch_per_batch), on every GPU from the next batch
+int gpu_fwd4_set_launch_per_batch(int on);
 // Batch size and maximum hold time at any time (the next batch of each graph
 // takes them; the batch is clamped to GPU_FWD4_BATCH_MAX). 0 or -EINVAL.
 int gpu_fwd4_set_batch(uint32_t batch, uint64_t max_delay_ns);

@@ -127,7 +127,7 @@ def main():
     ap.add_argument("--lcores", default="spread", choices=["none", "allowed", "spread", "socket"])
     ap.add_argument("--out", default=None, help="also append the lines to this JSONL file")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
-                    help="gr_hip_tune knobs of the GPU node's contexts, e.g. resident=1 (repeatable)")
+                    help="gr_hip_tune knobs of the GPU node's contexts, e.g. resident=1, or launch_per_batch (the module's) (repeatable)")
     ap.add_argument("--alt", action="append", default=[], metavar="KEY=VALUE/BACK",
                     help="also run the GPU node with knob KEY at VALUE (gpu_alt), interleaved with the other "
                          "modes in every rep, KEY set back to BACK after each run, e.g. resident=0/1 (repeatable)")
@@ -170,9 +170,19 @@ def main():
     fp = G.FanOutPath(L)
     topo = T.config_fullview()
     fp.load(topo)
+    L.gpu_fwd4_set_launch_per_batch.argtypes = [ctypes.c_int]
+
+    def set_knob(key, v):
+        """launch_per_batch: the module's own (gpu_fwd4_set_launch_per_batch);
+        else a gr_hip_tune knob of every context."""
+        if key == "launch_per_batch":
+            assert L.gpu_fwd4_set_launch_per_batch(v) == 0
+        else:
+            fp.tune(key, v)
+
     for kv in args.tune:
         k, v = kv.split("=")
-        fp.tune(k, int(v))
+        set_knob(k, int(v))
     alt = [(kv.split("=")[0], int(kv.split("=")[1].split("/")[0])) for kv in args.alt]
     alt_back = [(kv.split("=")[0], int(kv.split("/")[1])) for kv in args.alt]
     ifs = np.ascontiguousarray(topo.ifaces[topo.ifaces["id"] != 0])
@@ -207,7 +217,7 @@ def main():
         L.gh_set_null_node(1 if mode == "alone" else 0)
         L.gh_set_latency(1 if lat else 0)
         for key, v in (alt if mode == "gpu_alt" else []):
-            fp.tune(key, v)
+            set_knob(key, v)
         try:
             assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, m) == 0
             s, w = ctypes.c_double(), ctypes.c_uint64()
@@ -222,7 +232,7 @@ def main():
             return s.value, hist
         finally:
             for key, v in (alt_back if mode == "gpu_alt" else []):
-                fp.tune(key, v)
+                set_knob(key, v)
             L.gh_set_null_node(0)
             L.gh_set_latency(0)
             L.gh_workers_first(0)
