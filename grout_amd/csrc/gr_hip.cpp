@@ -325,7 +325,7 @@ struct gr_hip_ctx {
 	uint32_t res_nap; // idle poll backoff ceiling, in s_sleep(8) units (knob "resident_nap")
 	uint32_t res_tiles; // tiles per workgroup a batch is split into, up to the queue's rings (knob "resident_tiles")
 	uint32_t res_split = 0; // at most this many of a queue's rings per batch (0: all; knob "resident_split")
-	uint32_t res_budget = 0; // workgroups the busy queues' batches are split over together (knob "resident_budget"; 0: no cap)
+	uint32_t res_budget = 32; // workgroups the busy queues' batches are split over together (knob "resident_budget"; 0: no cap)
 	std::atomic<uint32_t> res_busy{0}; // queues with resident batches in flight
 	fwd4_res_desc *res_desc;
 	uint64_t *res_done, *res_exited;
@@ -846,8 +846,8 @@ extern "C" int gr_hip_init(int dev, uint32_t max_ifaces, uint32_t max_nexthops, 
 	c->tile_run = 16;
 	c->stage_min_tiles = 4;
 	c->res_on = 0;
-	c->res_rings = 128; // 32 queues (worker graphs) of 4 rings; workgroups of rings no queue holds leave at once
-	c->res_w = 4; // a batch uses up to 4 of them, 32 tiles each (measured: DESIGN.md §3.3)
+	c->res_rings = 256; // 32 queues (worker graphs) of 8 rings; workgroups of rings no queue holds leave at once
+	c->res_w = 8; // a batch uses up to 8 of them, fewer when many queues are busy (res_budget)
 	c->res_ms = 50;
 	c->res_nap = 16;
 	c->res_tiles = 8; // RES_TILES_PER_WG (measured: DESIGN.md §3.3)
@@ -2494,6 +2494,8 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		c->res_ms = (uint32_t)value;
 	} else if (strcmp(key, "resident_launches") == 0) { // read
 		return (int)c->res_launch;
+	} else if (strcmp(key, "resident_ring_count") == 0) { // read: "resident_rings"
+		return (int)c->res_rings;
 	} else if (strcmp(key, "resident_busy") == 0) { // read: queues with resident batches in flight
 		return (int)c->res_busy.load();
 	} else if (strcmp(key, "stage_min_tiles") == 0) {

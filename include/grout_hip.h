@@ -498,7 +498,7 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               hand-back's. 0 = one launch per batch (default; the grout
 //               module turns it on unless gpu_fwd4_conf.launch_per_batch)
 //   "resident_wgs" rings (workgroups) per queue, 1..8: a batch is split over
-//               up to that many, "resident_tiles" tiles each (default 4;
+//               up to that many, "resident_tiles" tiles each (default 8;
 //               queues taking their rings from then on)
 //   "resident_tiles" 64-packet tiles per workgroup a batch is split into
 //               (default 8)
@@ -506,13 +506,13 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               next batch on (default 0: all of them)
 //   "resident_budget" workgroups the batches of all busy queues (queues with
 //               resident batches in flight) are split over together: a batch
-//               takes at most budget / busy rings, at least 1 (32: a lone
-//               worker's batch up to its 4 rings, 16 busy workers' 2 each);
-//               0 = no cap (default: the gain under load is within the host's
-//               noise). "resident_busy" (read): busy queues now
-//   "resident_rings" rings in all (default 128: 32 queues; before the first
-//               resident batch only); the workgroups of rings no queue holds
-//               leave at once
+//               takes at most budget / busy rings, at least 1 (default 32: a
+//               lone worker's batch up to its 8 rings, 8 busy workers' 4 each,
+//               16 busy workers' 2); 0 = no cap. "resident_busy" (read): busy
+//               queues now
+//   "resident_rings" rings in all (default 256: 32 queues; before the first
+//               resident batch only; "resident_ring_count" reads it); the
+//               workgroups of rings no queue holds leave at once
 //   "resident_nap" a queue's helper rings (all but its first: they poll a
 //               wake word in device memory that the first ring's workgroup
 //               writes) back off their idle polls up to this many s_sleep(8)

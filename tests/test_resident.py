@@ -250,10 +250,10 @@ def test_resident_graph_control_plane_churn():
 def knobs(resident):
     """The split knobs back at their defaults after the test."""
     yield resident
-    resident.tune("resident_wgs", 4)
+    resident.tune("resident_wgs", 8)
     resident.tune("resident_tiles", 8)
     resident.tune("resident_split", 0)
-    resident.tune("resident_budget", 0)
+    resident.tune("resident_budget", 32)
 
 
 @pytest.mark.gpu
@@ -298,12 +298,12 @@ def test_resident_rings_run_out(knobs):
     from golden_util import fresh_fastpath_state
     fp = knobs
     topo = T.config_fullview(count=50_000)
-    per = 2000
-    fr, me = S.stream(per * 40, 0xD31, routes=topo.route_array())
+    per = 1000
+    fr, me = S.stream(per * 80, 0xD31, routes=topo.route_array())
     fresh_fastpath_state(fp, topo)
     lines, v, st, want, _ = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
     bufs, m = mbufs_for(fr, me)
-    parts = [m[i * per:(i + 1) * per] for i in range(40)]
+    parts = [m[i * per:(i + 1) * per] for i in range(80)]
 
     def walk(q, part):
         q.node_start(part)
@@ -311,30 +311,35 @@ def test_resident_rings_run_out(knobs):
         assert got is part and q.unfinished == 0
 
     qs = []
+    rings = fp.tune("resident_ring_count")
+    assert rings >= 32 and rings % 8 == 0
+    g8 = (rings - 24) // 8
     try:
-        # of 128 rings: 0-3 (groups of 4), 8-15 (of 8: 0-7 is not free), 18-20
+        # of R rings: 0-3 (groups of 4), 8-15 (of 8: 0-7 is not free), 18-20
         # (of 3: 3-5, 6-8, 9-11, 12-14 and 15-17 are not), then 24-31, 32-39,
-        # ..., 120-127 (13 groups of 8); 3 more queues find none
-        for i, w in enumerate([4, 8, 3] + [8] * 16):
+        # ..., R-8 - R-1 ((R - 24) / 8 groups of 8); 3 more queues find none
+        for i, w in enumerate([4, 8, 3] + [8] * (g8 + 3)):
             assert fp.tune("resident_wgs", w) == 0
             qs.append(fp.queue())
             walk(qs[i], parts[i])
         launched = [i for i, q in enumerate(qs) if q.stats()["rx_packets"].any()]
-        assert launched == [16, 17, 18]
-        for i, q in enumerate(qs):  # all 19 queues in flight at once
-            q.node_start(parts[19 + i])
+        assert launched == [3 + g8, 4 + g8, 5 + g8]
+        nq = len(qs)
+        for i, q in enumerate(qs):  # every queue in flight at once
+            q.node_start(parts[nq + i])
         for i, q in enumerate(qs):
             got, _ = q.node_finish()
-            assert got is parts[19 + i] and q.unfinished == 0
-        compare_mbufs(m[:per * 38], want[:per * 38], bufs[:per * 38], lines[:per * 38])
+            assert got is parts[nq + i] and q.unfinished == 0
+        compare_mbufs(m[:per * 2 * nq], want[:per * 2 * nq], bufs[:per * 2 * nq], lines[:per * 2 * nq])
         assert fp.tune("resident_busy") == 0
         assert all(qs[i].stats()["rx_packets"].sum() == 2 * per for i in launched)
         # rings 0-3 handed back: with 4-7, never taken, a group of 8 again
         qs[0].close()
         qs[0] = fp.queue()
-        walk(qs[0], parts[38])
+        x = 2 * nq
+        walk(qs[0], parts[x])
         assert not qs[0].stats()["rx_packets"].any()
-        compare_mbufs(parts[38], want[per * 38:per * 39], bufs[per * 38:per * 39], lines[per * 38:per * 39])
+        compare_mbufs(parts[x], want[per * x:per * (x + 1)], bufs[per * x:per * (x + 1)], lines[per * x:per * (x + 1)])
     finally:
         for q in qs:
             q.close()
