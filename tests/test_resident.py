@@ -379,13 +379,17 @@ def test_resident_lifetime_is_idleness(resident):
             compare_mbufs(m, want[i * per:(i + 1) * per], bufs, lines[i * per:(i + 1) * per])
             k += 1
         assert k > 20
-        assert fp.tune("resident_launches") == l0  # q2's idle first ring did not stop it
+        # q2's idle first ring did not stop it (a kernel stopped by one idle ring
+        # would relaunch about ten times here; up to two allows for host stalls
+        # of a lifetime between walks on a busy box)
+        l1 = fp.tune("resident_launches")
+        assert l1 - l0 <= 2
         time.sleep(0.25)  # all idle: it leaves
         bufs, m = mbufs_for(fr[:per], me[:per])
         q2.node_start(m)
         q2.node_finish()
         compare_mbufs(m, want[:per], bufs, lines[:per])
-        assert fp.tune("resident_launches") == l0 + 1
+        assert fp.tune("resident_launches") == l1 + 1
     finally:
         q1.close()
         q2.close()
