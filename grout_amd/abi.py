@@ -174,6 +174,7 @@ HIP_API = {
     "gr_hip_fwd4_host": (_I, [_P, _P, _P, _U32, _P, _P]),
     "gr_hip_fwd4_host_ex": (_I, [_P, _P, _P, _U32, _P, _U32, _P]),
     "gr_hip_queue_stats": (_I, [_P, _P, _U32, _I]),
+    "gr_hip_queue_stats_shards": (_I, [_P, _P, _U32, _I]),
     "gr_hip_host_alloc": (_I, [_P, ctypes.c_size_t, PP]),
     "gr_hip_host_free": (_I, [_P, _P]),
     "gr_hip_dev_alloc": (_I, [_P, ctypes.c_size_t, PP]),

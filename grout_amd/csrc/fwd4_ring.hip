@@ -564,14 +564,18 @@ __global__ void __launch_bounds__(ring_cfg_res::WAVES * 64) gr_fwd4_resident(con
 				dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 		}
 		__syncthreads();
-		if (!helper && tid > 0 && tid < A.wgs && blockIdx.x + tid < gridDim.x) { // wake the helpers it is split over
+		// wake the helpers it is split over: only as the batch's first ring
+		// (wg0 0; a workgroup that took its role under an older grouping of the
+		// rings may hold a helper's descriptor, whose helper_seq are zeros), and
+		// by a max, so that no wake word ever goes back
+		if (!helper && A.wg0 == 0 && tid > 0 && tid < A.wgs && blockIdx.x + tid < gridDim.x) {
 			// relaxed both: the helper acquires its own descriptor's seq before
 			// it reads it, so nothing here needs ordering (and a release would
 			// write back this XCD's L2)
 			const uint64_t hs = __hip_atomic_load(&ring[seq_s % R.ndesc].helper_seq[tid - 1], __ATOMIC_RELAXED,
 							      __HIP_MEMORY_SCOPE_SYSTEM);
-			__hip_atomic_store(R.wake + (size_t)(blockIdx.x + tid) * R.stride, hs, __ATOMIC_RELAXED,
-					   __HIP_MEMORY_SCOPE_AGENT);
+			__hip_atomic_fetch_max(R.wake + (size_t)(blockIdx.x + tid) * R.stride, hs, __ATOMIC_RELAXED,
+					       __HIP_MEMORY_SCOPE_AGENT);
 		}
 		// the edge table of the generation this batch names
 		for (uint32_t i = tid; i < sizeof(fwd4_edges); i += C::WAVES * 64)
@@ -625,6 +629,48 @@ __global__ void __launch_bounds__(ring_cfg_res::WAVES * 64) gr_fwd4_resident(con
 
 extern "C" hipError_t gr_fwd4_resident_launch(const fwd4_res_params *R, uint32_t rings, hipStream_t s) {
 	hipLaunchKernelGGL(gr_fwd4_resident, dim3(rings), dim3(ring_cfg_res::WAVES * 64), 0, s, *R);
+	return hipGetLastError();
+}
+
+// Resident workgroups per CU (its static LDS decides): how many rings a device
+// can serve at once (gr_hip.cpp res_take).
+extern "C" int gr_fwd4_resident_occupancy(void) {
+	int b = 0;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gr_fwd4_resident, ring_cfg_res::WAVES * 64, 0) != hipSuccess) {
+		(void)hipGetLastError();
+		return 0;
+	}
+	return b;
+}
+
+// ---- the per-iface counters, read at the memory side -----------------------
+// The kernels add to the counters with agent-scope atomics, which execute at
+// the memory side and leave no line in any XCD's L2; a plain read (a copy, a
+// memset's zeroes) may meet a line another XCD's L2 still holds from before.
+// So the host reads them, and resets them, through this kernel only: one
+// agent-scope atomic per 8-byte counter (fetch-add 0, or exchange with 0 to
+// read and reset at once: nothing counted in between is lost), each value
+// stored at system scope into pinned host memory. d: [rows][pitch] counters
+// of 4 u64, of which the first w of each row; out: [rows][w] of 4 u64.
+__global__ void __launch_bounds__(256) gr_stats_collect(unsigned long long *d, unsigned long long *out, uint32_t w,
+							uint32_t pitch, uint32_t rows, int reset) {
+	const uint32_t i = blockIdx.x * 256 + threadIdx.x, per = w * 4;
+	if (i >= per * rows)
+		return;
+	const uint32_t r = i / per, k = i % per;
+	GR_GLOBAL unsigned long long *p = (GR_GLOBAL unsigned long long *)(d + (size_t)r * pitch * 4 + k);
+	const unsigned long long v = reset ? __hip_atomic_exchange(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+					   : __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	__hip_atomic_store(out + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+extern "C" hipError_t gr_stats_collect_launch(void *d, void *out, uint32_t w, uint32_t pitch, uint32_t rows, int reset,
+					      hipStream_t s) {
+	const uint32_t n = w * 4 * rows;
+	if (n == 0)
+		return hipSuccess;
+	hipLaunchKernelGGL(gr_stats_collect, dim3((n + 255) / 256), dim3(256), 0, s, static_cast<unsigned long long *>(d),
+			   static_cast<unsigned long long *>(out), w, pitch, rows, reset);
 	return hipGetLastError();
 }
 

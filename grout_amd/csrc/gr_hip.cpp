@@ -25,6 +25,7 @@
 #include <new>
 #include <stdio.h>
 #include <time.h>
+#include <unistd.h>
 #include <stdlib.h>
 #include <string.h>
 #include <vector>
@@ -32,7 +33,10 @@
 extern "C" hipError_t gr_fwd4_ring_launch(const fwd4_params *A, uint32_t grid, hipStream_t s, int variant, int cfg);
 extern "C" int gr_fwd4_ring_occupancy(int variant, int cfg, uint32_t nhf_lds);
 extern "C" hipError_t gr_fwd4_resident_launch(const fwd4_res_params *R, uint32_t rings, hipStream_t s);
+extern "C" hipError_t gr_stats_collect_launch(void *d, void *out, uint32_t w, uint32_t pitch, uint32_t rows, int reset,
+					      hipStream_t s);
 extern "C" uint32_t gr_fwd4_ring_nhf_max(void);
+extern "C" int gr_fwd4_resident_occupancy(void);
 extern "C" int gr_fwd4_ring_ncfg(void);
 #define RING_WG_PER_CU 2 // default workgroups per CU of the ring kernel (measured)
 
@@ -197,6 +201,7 @@ struct node_slot {
 	bool kcount = false; // its kernel counts the per-iface counters (not the hand-back)
 	bool resident = false; // posted to the resident kernel (res_post): done at `res`
 	res_mark res;
+	uint64_t t_post = 0; // when it was posted (host ns): its deadline starts there
 };
 
 } // namespace
@@ -233,7 +238,12 @@ struct alignas(128) gr_hip_queue {
 	std::vector<gr_hip_iface_stats> node_if;
 	std::vector<gr_hip_iface_stats> kern_seen; // d_stats totals folded into node_if so far
 	gr_hip_iface_stats *snap = nullptr; // pinned [FWD4_STAT_SHARDS][snap_w] copy of d_stats
+	void *snap_d = nullptr; // its device address (gr_stats_collect writes it)
 	uint32_t snap_cap = 0, snap_w = 0; // ifaces per shard: allocated, in the copy in flight
+	// gr_hip_queue_stats' read of every shard (pinned, as snap)
+	gr_hip_iface_stats *rd = nullptr;
+	void *rd_d = nullptr;
+	uint32_t rd_cap = 0;
 	hipEvent_t snap_ev = nullptr;
 	bool snap_pending = false;
 	uint64_t node_counted = 0, snap_counted = 0; // node walks launched with counters; covered by a snapshot
@@ -248,13 +258,70 @@ struct alignas(128) gr_hip_queue {
 	uint32_t res_inflight = 0; // its resident batches posted and not yet finished
 	res_mark res_posted; // the last seq posted on each of its rings
 	res_mark res_retire; // posted before the last FIB publication (retire_wait)
+	// per ring of the queue: the last seq res_cancel retired unrun (read
+	// without res_mu by the worker's node_finish)
+	uint64_t res_cancelled[RES_WMAX] = {};
+	// a resident batch the kernel would neither finish nor leave (res_cancel):
+	// the GPU may still write the queue's node slots, so nothing of them is
+	// used or freed again; every later node call fails (the node punts)
+	bool dead = false;
+	uint32_t res_polls = 0; // gr_hip_node_pending's polls of resident batches
 };
 
 struct host_range { // gr_hip_host_register
 	uintptr_t host, dev;
 	size_t len;
-	bool ours; // registered by us (hipHostUnregister on the way out)
+	bool ours; // holds a reference on a registration of ours (hreg_global)
 };
+
+// hipHostRegister is process-wide: the runtime knows one registration of a
+// range, whichever context asked. Every context that registers a range holds
+// a reference here, and the last one out unregisters it, after waiting on the
+// host for its own queues (gr_hip_host_unregister). Without the count, context
+// A's unregister left context B's registry holding a device address the
+// runtime no longer mapped (tools/hostreg_probe.py: B's address unchanged
+// after A's hipHostUnregister, the runtime's attributes already "unregistered").
+struct hreg_global {
+	uintptr_t host, dev;
+	size_t len;
+	uint32_t refs;
+};
+static std::mutex g_hreg_mu;
+static std::vector<hreg_global> g_hregs;
+
+#define RES_MAX_DEV 64
+// Rings held by queues, per device, over every context of the process: a
+// resident launch's workgroups must all be co-resident (one per CU at its LDS
+// size), or a ring no CU ever runs stalls its queue's batches (res_take).
+static std::atomic<uint32_t> g_res_held[RES_MAX_DEV];
+
+// The registration of ours that holds [p, p + len), or null (g_hreg_mu held).
+static hreg_global *hreg_global_find(uintptr_t p, size_t len) {
+	for (hreg_global &g : g_hregs)
+		if (p >= g.host && p - g.host <= g.len && len <= g.len - (p - g.host))
+			return &g;
+	return nullptr;
+}
+
+// Drop a reference taken by gr_hip_host_register; the last unregisters.
+static int hreg_global_put(uintptr_t p, size_t len) {
+	std::lock_guard<std::mutex> gl(g_hreg_mu);
+	for (size_t i = 0; i < g_hregs.size(); i++) {
+		hreg_global &g = g_hregs[i];
+		if (!(p >= g.host && p - g.host <= g.len && len <= g.len - (p - g.host)))
+			continue;
+		if (--g.refs == 0) {
+			const hipError_t e = hipHostUnregister(reinterpret_cast<void *>(g.host));
+			g_hregs.erase(g_hregs.begin() + (long)i);
+			if (e != hipSuccess) {
+				(void)hipGetLastError();
+				return -EIO;
+			}
+		}
+		return 0;
+	}
+	return -ENOENT;
+}
 
 struct gr_hip_ctx {
 	int dev;
@@ -315,6 +382,9 @@ struct gr_hip_ctx {
 	std::atomic<int> fail_appends{0}; // tests: the next N gr_hip_node_append calls fail (-ENOMEM)
 	int untimed; // measurements: no HIP events around launches (gr_hip_queue_kernel_ms sees none)
 	uint32_t time_every; // HIP events around every N-th submit of a queue only (0, 1 = every one)
+	int stats_copy; // gr_hip_queue_stats reads with a copy and resets with a memset (measurement only)
+	int sync_check; // debugging: the host path waits after each step it enqueues and names a failing one
+	std::atomic<int> host_path_last{-1}; // the path the last gr_hip_fwd4_host(_ex) took (GR_HIP_HOST_PATH_*)
 	std::vector<host_range> hregs; // registered host memory, by host address
 	// the resident kernel (knob "resident", see res_post): descriptor rings,
 	// done and exited words (pinned host memory), its stream and launch state
@@ -341,6 +411,13 @@ struct gr_hip_ctx {
 	uint64_t res_launch; // id of the last launch (0: none)
 	std::vector<uint8_t> res_taken; // rings held by a queue
 	std::mutex res_mu;
+	uint32_t res_wait_ms = 500; // a resident batch not done after this is cancelled (knob "resident_wait_ms")
+	uint32_t res_cap = 0; // rings this device can hold co-resident (res_setup; device-wide, g_res_held)
+	uint32_t res_reserve_cu = 0; // CUs left to other kernels (knob "resident_reserve_cu")
+	uint32_t res_held = 0; // rings this context's queues hold (counted in g_res_held)
+	bool res_dead = false; // a launch that would not leave: no resident batch any more, its words never freed
+	bool res_hold = false; // tests: no (re)launch while set (a kernel that stopped serving its rings)
+	std::atomic<uint32_t> res_cancels{0}; // batches res_cancel retired unrun (knob read "resident_cancels")
 	// FIB publication (see retire_wait): two pinned staging buffers used in
 	// turn by the commits (fib_mu), each with the event of its last upload,
 	// and per generation the event of the upload that made it complete
@@ -368,6 +445,7 @@ struct gr_hip_ctx {
 // Make the control stream wait for everything submitted on every queue.
 static int res_wait(gr_hip_queue *q, const res_mark &m);
 static void res_free(gr_hip_ctx *c);
+static uint64_t now_ns_host();
 
 static int quiesce(gr_hip_ctx *c) {
 	for (gr_hip_queue *q : c->queues) {
@@ -878,9 +956,10 @@ extern "C" int gr_hip_fini(gr_hip_ctx_t *c) {
 	res_free(c);
 	if (c->ctl)
 		hipStreamSynchronize(c->ctl); // the last commits' uploads
+	// (every queue is gone: nothing of this context reads them any more)
 	for (const host_range &r : c->hregs)
 		if (r.ours)
-			hipHostUnregister(reinterpret_cast<void *>(r.host));
+			hreg_global_put(r.host, r.len);
 	c->hregs.clear();
 	for (vrf_fib &v : c->vrfs) {
 		gr_fib4_free(v.rib);
@@ -1968,13 +2047,17 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 		if (h.s)
 			hipStreamSynchronize(h.s);
 	if (q->ring >= 0) {
-		res_wait(q, q->res_posted); // its resident batches, then the rings are free again
+		res_wait(q, q->res_posted); // its resident batches (retired past the deadline), then the rings are free again
 		if (q->res_inflight > 0)
 			c->res_busy.fetch_sub(1, std::memory_order_relaxed);
 		std::lock_guard<std::mutex> rl(c->res_mu);
-		for (uint32_t j = 0; j < q->res_w; j++) {
-			c->res_taken[(size_t)q->ring + j] = 0;
-			__atomic_store_n(c->res_taken_h + q->ring + j, 0u, __ATOMIC_RELEASE);
+		if (!c->res_dead) {
+			for (uint32_t j = 0; j < q->res_w; j++) {
+				c->res_taken[(size_t)q->ring + j] = 0;
+				__atomic_store_n(c->res_taken_h + q->ring + j, 0u, __ATOMIC_RELEASE);
+			}
+			g_res_held[c->dev].fetch_sub(q->res_w);
+			c->res_held -= q->res_w;
 		}
 	}
 	{
@@ -2011,6 +2094,7 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 	if (q->snap_ev != nullptr)
 		hipEventDestroy(q->snap_ev);
 	hipHostFree(q->snap);
+	hipHostFree(q->rd);
 	hipHostFree(q->h_err);
 	hipHostFree(q->pg_lines);
 	hipHostFree(q->pg_out);
@@ -2018,6 +2102,8 @@ extern "C" int gr_hip_queue_destroy(gr_hip_queue_t *q) {
 	hipHostFree(q->pg_v);
 	for (node_slot &w : q->nw) {
 		hipEventDestroy(w.done);
+		if (q->dead) // a resident launch that would not leave may still write them: leaked
+			continue;
 		hipHostFree(w.lines);
 		hipHostFree(w.out);
 		hipHostFree(w.meta);
@@ -2184,18 +2270,50 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 // before them (retire_wait, quiesce).
 #define RES_NDESC 4 // descriptors per ring (GR_HIP_NODE_DEPTH batches in flight at most)
 #define RES_STRIDE 8 // uint64_t per ring in the done / exited words: a 64-byte line each
-#define RES_WAIT_NS (10ull * 1000000000ull) // a batch not done after this: -ETIMEDOUT
 #define RES_TILES_PER_WG 8 // default tiles per workgroup a batch is split into (knob "resident_tiles")
+#define RES_LEAVE_NS (500ull * 1000000ull) // a launch told to stop has left within this, or is stuck
 
 static uint64_t res_word(const uint64_t *w, int ring) {
 	return __atomic_load_n(w + (size_t)ring * RES_STRIDE, __ATOMIC_ACQUIRE);
 }
 
+// Tell the live launch to stop and wait, bounded, until it is gone: every
+// workgroup leaves after the batch it is running (whose waits are bounded).
+// 0: gone (or faulted: it touches nothing more); -EDEADLK: still running
+// past RES_LEAVE_NS (a workgroup no CU runs, or one that does not return).
+static int res_leave(gr_hip_ctx *c) {
+	if (!c->res_live)
+		return 0;
+	__atomic_store_n(c->res_stop, 1u, __ATOMIC_RELEASE);
+	const uint64_t t0 = now_ns_host();
+	for (uint32_t spin = 0;; spin++) {
+		const hipError_t e = hipEventQuery(c->res_ev);
+		if (e == hipSuccess || e != hipErrorNotReady) {
+			(void)hipGetLastError();
+			break;
+		}
+		if (now_ns_host() - t0 > RES_LEAVE_NS)
+			return -EDEADLK;
+		if (spin > 64)
+			usleep(20);
+	}
+	c->res_live = false;
+	return 0;
+}
+
 static void res_free(gr_hip_ctx *c) {
-	if (c->res_live && c->res_stop != nullptr) {
-		__atomic_store_n(c->res_stop, 1u, __ATOMIC_RELEASE);
-		hipEventSynchronize(c->res_ev); // every workgroup leaves after its batch
-		c->res_live = false;
+	if (c->res_live && c->res_stop != nullptr && res_leave(c) != 0) {
+		// still running: its rings and words stay allocated (leaked), the
+		// kernel may still read and write them
+		c->res_dead = true;
+		c->res_desc = nullptr;
+		c->res_done = c->res_exited = nullptr;
+		c->res_stop = nullptr;
+		c->res_taken_h = nullptr;
+		c->res_wake_d = nullptr;
+		c->res_ev = nullptr;
+		c->res_s = nullptr;
+		return;
 	}
 	if (c->res_ev != nullptr)
 		hipEventDestroy(c->res_ev);
@@ -2254,12 +2372,22 @@ static int res_setup(gr_hip_ctx *c) {
 	memset(c->res_taken_h, 0, sizeof(uint32_t) * c->res_rings);
 	*c->res_stop = 0;
 	c->res_taken.assign(c->res_rings, 0);
+	// how many rings the device runs at once: workgroups per CU at the
+	// kernel's LDS size, times the CUs not reserved for other kernels
+	const int occ = gr_fwd4_resident_occupancy();
+	const int cus = c->n_cu - (int)c->res_reserve_cu;
+	c->res_cap = occ > 0 && cus > 0 ? (uint32_t)(occ * cus) : 0;
 	return 0;
 }
 
 // Launch the kernel when none runs (res_mu held). A launch that is leaving
 // (stop set) is relaunched only once all its workgroups have left.
 static int res_ensure(gr_hip_ctx *c) {
+	if (c->res_hold) { // tests: the kernel stops serving its rings
+		if (c->res_live)
+			__atomic_store_n(c->res_stop, 1u, __ATOMIC_RELEASE);
+		return 0;
+	}
 	if (c->res_live) {
 		if (__atomic_load_n(c->res_stop, __ATOMIC_ACQUIRE) == 0)
 			return 0;
@@ -2305,7 +2433,19 @@ static bool res_take(gr_hip_queue *q) {
 	if (res_setup(c) != 0)
 		return false;
 	const uint32_t W = c->res_w;
-	for (uint32_t r = 0; r + W <= c->res_rings; r += W) { // W consecutive rings, in groups of W
+	if (c->res_dead || (uint32_t)c->dev >= RES_MAX_DEV)
+		return false;
+	// co-residency: the device's rings held, over every context, stay within
+	// what its CUs run at once; past that the queue launches per batch
+	std::atomic<uint32_t> &held = g_res_held[c->dev];
+	for (uint32_t h = held.load(); ;) {
+		if (h + W > c->res_cap)
+			return false;
+		if (held.compare_exchange_weak(h, h + W))
+			break;
+	}
+	bool got = false;
+	for (uint32_t r = 0; r + W <= c->res_rings && !got; r += W) { // W consecutive rings, in groups of W
 		// all W free: queues that took theirs under another "resident_wgs"
 		// hold groups of another size
 		bool free = true;
@@ -2326,10 +2466,15 @@ static bool res_take(gr_hip_queue *q) {
 			for (uint32_t j = 0; j < W; j++)
 				q->res_posted.seq[j] = res_word(c->res_done, (int)(r + j));
 			q->res_retire = q->res_posted;
-			return true;
+			for (uint32_t j = 0; j < RES_WMAX; j++)
+				q->res_cancelled[j] = 0;
+			c->res_held += W;
+			got = true;
 		}
 	}
-	return false;
+	if (!got)
+		held.fetch_sub(W);
+	return got;
 }
 
 static bool res_is_done(const gr_hip_queue *q, const res_mark &m) {
@@ -2339,27 +2484,82 @@ static bool res_is_done(const gr_hip_queue *q, const res_mark &m) {
 	return true;
 }
 
-// Wait, on the host, until the ring's batch `seq` is done.
-static int res_wait(gr_hip_queue *q, const res_mark &m) {
+// Whether res_cancel retired any of m's descriptors unrun.
+static bool res_was_cancelled(const gr_hip_queue *q, const res_mark &m) {
+	for (uint32_t j = 0; j < m.k; j++)
+		if (__atomic_load_n(&q->res_cancelled[j], __ATOMIC_ACQUIRE) >= m.seq[j])
+			return true;
+	return false;
+}
+
+// A batch past its deadline, or a launch that faulted (res_mu not held):
+// make sure no workgroup ever runs it. The live launch is told to stop and
+// waited for (res_leave); its workgroups finish the batch each is running,
+// so once it is gone a ring whose done word is still below m's seq never
+// started m there. Those descriptors are retired (seq cleared, the done word
+// moved on by the host, so that a relaunch resumes after them) and recorded
+// in res_cancelled: the walk's verdicts still hold the fill value there and
+// its packets go back to grout's CPU nodes untouched. A launch that does not
+// leave makes the context's resident kernel dead: -EDEADLK, and the caller
+// must neither reuse nor free what the batch names (the node marks the queue
+// dead). Returns 0 (m done after all), -ETIMEDOUT (retired), -EDEADLK.
+static int res_cancel(gr_hip_queue *q, const res_mark &m) {
+	gr_hip_ctx *c = q->ctx;
+	std::lock_guard<std::mutex> l(c->res_mu);
+	if (res_is_done(q, m))
+		return 0;
+	if (res_leave(c) != 0) {
+		c->res_dead = true;
+		q->dead = true;
+		return -EDEADLK;
+	}
+	if (res_is_done(q, m))
+		return 0; // it ran before the launch left
+	for (uint32_t j = 0; j < m.k; j++) {
+		const int ring = q->ring + (int)j;
+		const uint64_t d = res_word(c->res_done, ring);
+		if (d >= m.seq[j])
+			continue;
+		for (uint64_t sq = d + 1; sq <= m.seq[j]; sq++) {
+			fwd4_res_desc &dd = c->res_desc[(size_t)ring * RES_NDESC + sq % RES_NDESC];
+			if (__atomic_load_n(&dd.seq, __ATOMIC_ACQUIRE) == sq)
+				__atomic_store_n(&dd.seq, 0ull, __ATOMIC_RELEASE);
+		}
+		__atomic_store_n(&q->res_cancelled[j], m.seq[j], __ATOMIC_RELEASE);
+		__atomic_store_n(c->res_done + (size_t)ring * RES_STRIDE, m.seq[j], __ATOMIC_RELEASE);
+	}
+	c->res_cancels.fetch_add(1);
+	return -ETIMEDOUT;
+}
+
+// Wait, on the host, until batch m is done: past `deadline` (host ns), or
+// when the launch faulted, res_cancel decides (0, -ETIMEDOUT, -EDEADLK).
+static int res_wait(gr_hip_queue *q, const res_mark &m, uint64_t deadline) {
 	if (q->ring < 0 || res_is_done(q, m))
 		return 0;
 	gr_hip_ctx *c = q->ctx;
-	const uint64_t t0 = now_ns_host();
+	if (c->res_dead)
+		return res_was_cancelled(q, m) ? -ETIMEDOUT : -EDEADLK;
 	for (uint32_t spin = 1; !res_is_done(q, m); spin++) {
 		if ((spin & 1023) == 0) {
-			if (const int r = res_kick(c))
-				return r;
+			if (res_kick(c) != 0)
+				return res_cancel(q, m);
 			const hipError_t e = hipEventQuery(c->res_ev);
 			if (e != hipSuccess && e != hipErrorNotReady) {
 				(void)hipGetLastError();
-				return -EIO;
+				const int r = res_cancel(q, m); // the faulted launch touches nothing more
+				return r == -ETIMEDOUT ? -EIO : r;
 			}
-			if (now_ns_host() - t0 > RES_WAIT_NS)
-				return -ETIMEDOUT;
+			if (now_ns_host() > deadline)
+				return res_cancel(q, m);
 		}
 		__builtin_ia32_pause();
 	}
 	return 0;
+}
+
+static int res_wait(gr_hip_queue *q, const res_mark &m) {
+	return res_wait(q, m, now_ns_host() + (uint64_t)q->ctx->res_wait_ms * 1000000ull);
 }
 
 // Post batch b (device addresses) on k of q's rings (RES_TILES_PER_WG tiles
@@ -2367,6 +2567,8 @@ static int res_wait(gr_hip_queue *q, const res_mark &m) {
 // done for it. c->mu held shared.
 static int res_post(gr_hip_queue *q, const gr_hip_batch *b, res_mark *m) {
 	gr_hip_ctx *c = q->ctx;
+	if (c->res_dead || q->dead)
+		return -EIO;
 	const uint32_t g = c->gen;
 	if (q->seen_serial != c->serial) { // the generation's upload (launch(): a stream wait)
 		HCK(hipEventSynchronize(c->ready_ev[g]));
@@ -2408,6 +2610,10 @@ static int res_post(gr_hip_queue *q, const gr_hip_batch *b, res_mark *m) {
 		fwd4_res_desc &d = c->res_desc[(size_t)(q->ring + (int)j) * RES_NDESC + seq % RES_NDESC];
 		A.wg0 = j;
 		memcpy(&d.A, &A, sizeof(A));
+		// the first ring's names its helpers' seqs; a helper's, none (a
+		// workgroup that still holds the first ring's role from an older
+		// grouping reads zeros here, which the kernel's max ignores)
+		memset(d.helper_seq, 0, sizeof(d.helper_seq));
 		if (j == 0)
 			for (uint32_t h = 1; h < k; h++)
 				d.helper_seq[h - 1] = m->seq[h];
@@ -2442,6 +2648,12 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		node_prof_on.store(value != 0);
 	} else if (strcmp(key, "untimed") == 0) {
 		c->untimed = value != 0;
+	} else if (strcmp(key, "stats_copy") == 0) { // measurement: the counters read as in round 5
+		c->stats_copy = value != 0;
+	} else if (strcmp(key, "sync_check") == 0) { // debugging: host path steps waited for one by one
+		c->sync_check = value != 0;
+	} else if (strcmp(key, "host_path_last") == 0) { // read: 0 direct, 1 staged copies, 2 pageable
+		return c->host_path_last.load();
 	} else if (strcmp(key, "time_every") == 0) { // sample the launch timing: less event overhead
 		if (value < 0 || value > 1024)
 			return -EINVAL;
@@ -2488,6 +2700,27 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < 1 || value > 64)
 			return -EINVAL;
 		c->res_nap = (uint32_t)value;
+	} else if (strcmp(key, "resident_wait_ms") == 0) { // a resident batch's deadline, from its post
+		if (value < 1 || value > 60000)
+			return -EINVAL;
+		c->res_wait_ms = (uint32_t)value;
+	} else if (strcmp(key, "resident_reserve_cu") == 0) { // before the first resident batch only
+		if (value < 0 || value >= c->n_cu || c->res_desc != nullptr)
+			return -EINVAL;
+		c->res_reserve_cu = (uint32_t)value;
+	} else if (strcmp(key, "resident_cap") == 0) { // read: rings the device holds co-resident (0: not set up)
+		return (int)c->res_cap;
+	} else if (strcmp(key, "resident_held") == 0) { // read: rings held on this device, every context
+		return (uint32_t)c->dev < RES_MAX_DEV ? (int)g_res_held[c->dev].load() : 0;
+	} else if (strcmp(key, "resident_cancels") == 0) { // read: batches retired unrun past their deadline
+		return (int)c->res_cancels.load();
+	} else if (strcmp(key, "resident_dead") == 0) { // read: a launch would not leave (no resident batches since)
+		return c->res_dead ? 1 : 0;
+	} else if (strcmp(key, "resident_hold") == 0) { // tests: the live launch leaves and is not relaunched (1) or is again (0)
+		std::lock_guard<std::mutex> rl(c->res_mu);
+		c->res_hold = value != 0;
+		if (c->res_hold && c->res_live)
+			__atomic_store_n(c->res_stop, 1u, __ATOMIC_RELEASE);
 	} else if (strcmp(key, "resident_ms") == 0) {
 		if (value < 1 || value > 10000)
 			return -EINVAL;
@@ -2617,6 +2850,22 @@ extern "C" int gr_hip_queue_kernel_ms(gr_hip_queue_t *q, uint32_t n, float *ms, 
 	return 0;
 }
 
+// Knob "sync_check" (debugging): the host path waits for each step it has
+// just enqueued on stream s, and a failing one is named on stderr (an
+// asynchronous error otherwise surfaces at whatever call comes next: round 5's
+// illegal address was reported by a copy).
+#define SYNC_CHECK(c, s, what)                                                                    \
+	do {                                                                                       \
+		if ((c)->sync_check) {                                                             \
+			const hipError_t e__ = hipStreamSynchronize(s);                            \
+			if (e__ != hipSuccess) {                                                   \
+				(void)hipGetLastError();                                           \
+				fprintf(stderr, "gr_hip: sync_check: %s: %s\n", what, hipGetErrorString(e__)); \
+				return -EIO;                                                       \
+			}                                                                          \
+		}                                                                                  \
+	} while (0)
+
 // Zero-copy host batch (the context's "host_direct"): the kernel's loaders
 // and storers move the lines over PCIe themselves, both directions at once,
 // no staging copies. Enqueues the launch on the queue's stream and sets
@@ -2636,6 +2885,8 @@ static int host_direct_launch(gr_hip_queue *q, const void *lines, const gr_hip_p
 			  n, GR_HIP_LINE, out_stride, GR_HIP_BATCH_F_LINES_ONLY | oflags};
 	const int r = launch(q, q->s, &b, true);
 	*direct = r == 0;
+	if (r == 0)
+		SYNC_CHECK(q->ctx, q->s, "direct launch");
 	return r;
 }
 
@@ -2704,12 +2955,16 @@ extern "C" int gr_hip_fwd4_host_ex(
 	hipSetDevice(c->dev);
 	void *dp;
 	if (!host_dev_ptr(lines, &dp) || !host_dev_ptr(meta, &dp) || !host_dev_ptr(out_lines, &dp)
-	    || !host_dev_ptr(verdicts, &dp))
-		return host_pageable(q, lines, meta, n, out_lines, out_stride, verdicts);
+	    || !host_dev_ptr(verdicts, &dp)) {
+		const int r = host_pageable(q, lines, meta, n, out_lines, out_stride, verdicts);
+		c->host_path_last.store(GR_HIP_HOST_PATH_PAGEABLE);
+		return r;
+	}
 	std::shared_lock<std::shared_mutex> l(c->mu); // see gr_hip_fwd4_submit
 	bool direct = false;
 	if (const int r = host_direct_launch(q, lines, meta, n, out_lines, out_stride, verdicts, &direct); r < 0)
 		return r;
+	c->host_path_last.store(direct ? GR_HIP_HOST_PATH_DIRECT : GR_HIP_HOST_PATH_STAGED);
 	if (direct) {
 		l.unlock(); // enqueued: the wait needs no lock (see gr_hip_node_start)
 		if (const int e_ = host_wait(q, q->s))
@@ -2737,16 +2992,22 @@ extern "C" int gr_hip_fwd4_host_ex(
 		uint32_t cnt = n - off < HOST_CHUNK ? n - off : HOST_CHUNK;
 		HCK(hipMemcpyAsync(h.in, in + (size_t)off * GR_HIP_LINE, (size_t)cnt * GR_HIP_LINE,
 				   hipMemcpyHostToDevice, h.s));
+		SYNC_CHECK(c, h.s, "lines H2D");
 		HCK(hipMemcpyAsync(h.meta, meta + off, (size_t)cnt * sizeof(*meta), hipMemcpyHostToDevice, h.s));
+		SYNC_CHECK(c, h.s, "meta H2D");
 		// verdicts of packets a kernel that gave up never reached read back as 0xff
 		HCK(hipMemsetAsync(h.v, 0xff, (size_t)cnt * sizeof(*verdicts), h.s));
+		SYNC_CHECK(c, h.s, "verdict fill");
 		gr_hip_batch b = {h.in, h.out, h.meta, h.v, cnt, GR_HIP_LINE, out_stride, GR_HIP_BATCH_F_LINES_ONLY | oflags};
 		int r = launch(q, h.s, &b, false);
 		if (r < 0)
 			return r;
+		SYNC_CHECK(c, h.s, "staged launch");
 		HCK(hipMemcpyAsync(out + (size_t)off * out_stride, h.out, (size_t)cnt * out_stride,
 				   hipMemcpyDeviceToHost, h.s));
+		SYNC_CHECK(c, h.s, "lines D2H");
 		HCK(hipMemcpyAsync(verdicts + off, h.v, (size_t)cnt * sizeof(*verdicts), hipMemcpyDeviceToHost, h.s));
+		SYNC_CHECK(c, h.s, "verdicts D2H");
 	}
 	for (host_slot &h : q->hs) {
 		if (const int e_ = host_wait(q, h.s))
@@ -2799,7 +3060,13 @@ extern "C" int gr_hip_host_register(gr_hip_ctx_t *c, void *ptr, size_t bytes) {
 			return -EEXIST;
 	host_range r = {p, 0, bytes, false};
 	void *dp = nullptr;
-	if (host_dev_ptr(ptr, &dp)) { // already pinned (hipHostMalloc, torch pin_memory)
+	std::lock_guard<std::mutex> gl(g_hreg_mu);
+	if (hreg_global_find(p, bytes) != nullptr) { // registered by us for another context
+		hreg_global *g = hreg_global_find(p, bytes);
+		g->refs++;
+		r.dev = g->dev + (p - g->host);
+		r.ours = true;
+	} else if (host_dev_ptr(ptr, &dp)) { // pinned by someone else (hipHostMalloc, torch pin_memory)
 		r.dev = reinterpret_cast<uintptr_t>(dp);
 	} else {
 		HCK(hipHostRegister(ptr, bytes, hipHostRegisterMapped));
@@ -2810,6 +3077,7 @@ extern "C" int gr_hip_host_register(gr_hip_ctx_t *c, void *ptr, size_t bytes) {
 		}
 		r.dev = reinterpret_cast<uintptr_t>(dp);
 		r.ours = true;
+		g_hregs.push_back({p, r.dev, bytes, 1});
 	}
 	c->hregs.push_back(r);
 	return 0;
@@ -2823,13 +3091,18 @@ extern "C" int gr_hip_host_unregister(gr_hip_ctx_t *c, void *ptr) {
 	for (size_t i = 0; i < c->hregs.size(); i++) {
 		if (c->hregs[i].host != reinterpret_cast<uintptr_t>(ptr))
 			continue;
-		int r = quiesce(c); // no kernel may still read it
-		if (r != 0)
+		// no kernel of this context may still read it: quiesce() orders the
+		// control stream after every queue's work (and waits for resident
+		// batches on the host); the host then waits for that stream, before
+		// the runtime unmaps the range (an unmapped range read by a kernel
+		// still running is an illegal address)
+		if (const int r = quiesce(c))
 			return r;
-		if (c->hregs[i].ours)
-			HCK(hipHostUnregister(ptr));
+		if (const int r = ctl_sync(c))
+			return r;
+		const host_range hr = c->hregs[i];
 		c->hregs.erase(c->hregs.begin() + (long)i);
-		return 0;
+		return hr.ours ? hreg_global_put(hr.host, hr.len) : 0;
 	}
 	return -ENOENT;
 }
@@ -3056,6 +3329,8 @@ extern "C" int gr_hip_node_discard(gr_hip_queue_t *q) {
 extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst) {
 	if (q == nullptr)
 		return -EINVAL;
+	if (q->dead)
+		return -EIO; // (res_cancel) its slots may still be written by the GPU
 	if (q->nw_count == GR_HIP_NODE_DEPTH)
 		return -EBUSY;
 	gr_hip_ctx *c = q->ctx;
@@ -3119,6 +3394,7 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 		// after everything already submitted on the queue, like gr_hip_fwd4_host;
 		// no timing events (the walk's own completion event is enough)
 		if (c->res_on && res_take(q)) {
+			w.t_post = now_ns_host();
 			if ((r = res_post(q, &b, &w.res)) < 0)
 				return r;
 			w.resident = true;
@@ -3147,6 +3423,7 @@ extern "C" int gr_hip_node_send(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uint32
 					  static_cast<gr_hip_verdict *>(w.d_v), ns, GR_HIP_LINE, GR_HIP_PREFIX,
 					  GR_HIP_BATCH_F_LINES_ONLY | GR_HIP_BATCH_F_PREFIX32};
 			if (c->res_on && res_take(q)) {
+				w.t_post = now_ns_host();
 				if ((r = res_post(q, &b, &w.res)) < 0)
 					return r;
 				w.resident = true;
@@ -3213,10 +3490,19 @@ static int node_finish(gr_hip_queue_t *q, struct gr_hip_mbuf **mp, uint32_t *np,
 		direct->meta = w.own ? w.meta : nullptr; // no views: the hand-back reads the mbufs
 	uint64_t t_prof = prof_now();
 	if (!w.sync && w.resident) {
-		if ((r = res_wait(q, w.res)) == 0)
-			r = q_check(q);
+		r = res_wait(q, w.res, w.t_post + (uint64_t)c->res_wait_ms * 1000000ull);
 		if (q->res_inflight > 0 && --q->res_inflight == 0)
 			c->res_busy.fetch_sub(1, std::memory_order_relaxed);
+		if (r == -EDEADLK)
+			return r; // the GPU may still run it: nothing of the walk is touched (q->dead)
+		// retired unrun (here or by a control-plane wait), or the launch
+		// faulted: what was not reached is punted, like a give-up
+		if (r == 0 && res_was_cancelled(q, w.res))
+			r = -ETIMEDOUT;
+		if (r == -EIO)
+			r = -ETIMEDOUT;
+		if (r == 0)
+			r = q_check(q);
 	} else if (!w.sync) {
 		hipSetDevice(c->dev);
 		HCK(hipEventSynchronize(w.done));
@@ -3292,8 +3578,31 @@ static void kern_fold(gr_hip_queue_t *q, const gr_hip_iface_stats *all, uint32_t
 	}
 }
 
+// A pinned, coherent, device-mapped buffer of at least `n` counter entries
+// (gr_stats_collect's destination), grown on demand.
+static int stats_buf(gr_hip_iface_stats **h, void **d, uint32_t *cap, uint32_t n) {
+	if (*cap >= n)
+		return 0;
+	hipHostFree(*h);
+	*h = nullptr;
+	*d = nullptr;
+	*cap = 0;
+	if (hipHostMalloc(reinterpret_cast<void **>(h), sizeof(gr_hip_iface_stats) * n,
+			  hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess
+	    || hipHostGetDevicePointer(d, *h, 0) != hipSuccess) {
+		(void)hipGetLastError();
+		hipHostFree(*h);
+		*h = nullptr;
+		*d = nullptr;
+		return -ENOMEM;
+	}
+	*cap = n;
+	return 0;
+}
+
 // Copy d_stats' first snap_w ifaces of every shard into the pinned snapshot
-// behind the queue's work, and mark it pending.
+// behind the queue's work (gr_stats_collect: read at the memory side), and
+// mark it pending.
 static int snap_start(gr_hip_queue_t *q) {
 	gr_hip_ctx *c = q->ctx;
 	std::shared_lock<std::shared_mutex> lk(c->mu); // the iface mirror
@@ -3307,20 +3616,11 @@ static int snap_start(gr_hip_queue_t *q) {
 		w = 1;
 	if (q->snap_ev == nullptr)
 		HCK(hipEventCreateWithFlags(&q->snap_ev, hipEventDisableTiming));
-	if (w > q->snap_cap) {
-		hipHostFree(q->snap);
-		q->snap = nullptr;
-		q->snap_cap = 0;
-		if (hipHostMalloc((void **)&q->snap, sizeof(gr_hip_iface_stats) * FWD4_STAT_SHARDS * w,
-				  hipHostMallocDefault) != hipSuccess) {
-			(void)hipGetLastError();
-			return -ENOMEM;
-		}
-		q->snap_cap = w;
-	}
-	const size_t row = sizeof(gr_hip_iface_stats);
-	HCK(hipMemcpy2DAsync(q->snap, w * row, q->d_stats, (size_t)c->max_ifaces * row, w * row, FWD4_STAT_SHARDS,
-			     hipMemcpyDeviceToHost, q->s));
+	uint32_t cap = q->snap_cap * FWD4_STAT_SHARDS;
+	if (const int r = stats_buf(&q->snap, &q->snap_d, &cap, w * FWD4_STAT_SHARDS))
+		return q->snap_cap = 0, r;
+	q->snap_cap = cap / FWD4_STAT_SHARDS;
+	HCK(gr_stats_collect_launch(q->d_stats, q->snap_d, w, c->max_ifaces, FWD4_STAT_SHARDS, 0, q->s));
 	HCK(hipEventRecord(q->snap_ev, q->s));
 	q->snap_w = w;
 	q->snap_pending = true;
@@ -3379,10 +3679,22 @@ extern "C" int gr_hip_node_pending(gr_hip_queue_t *q, int *ready) {
 			if (w.sync) {
 				*ready = 1;
 			} else if (w.resident) { // a load of the ring's done word; a kernel that left is relaunched
-				if (res_is_done(q, w.res))
+				gr_hip_ctx *c = q->ctx;
+				if (res_is_done(q, w.res)) {
 					*ready = 1;
-				else if (const int r = res_kick(q->ctx))
-					return r;
+				} else if (c->res_dead || res_kick(c) != 0) {
+					return -EIO; // node_finish sorts it out (res_wait, res_cancel)
+				} else if ((++q->res_polls & 255) == 0) {
+					// bounded like res_wait: past the batch's deadline, or a
+					// launch that faulted, node_finish cancels it
+					const hipError_t e = hipEventQuery(c->res_ev);
+					if (e != hipSuccess && e != hipErrorNotReady) {
+						(void)hipGetLastError();
+						return -EIO;
+					}
+					if (now_ns_host() - w.t_post > (uint64_t)c->res_wait_ms * 1000000ull)
+						return -ETIMEDOUT;
+				}
 			} else {
 				hipSetDevice(q->ctx->dev);
 				const hipError_t e = hipEventQuery(w.done);
@@ -3411,42 +3723,77 @@ extern "C" int gr_hip_node_process(gr_hip_queue_t *q, struct gr_hip_mbuf *m, uin
 	return gr_hip_node_finish(q, nullptr, nullptr, stats);
 }
 
-extern "C" int gr_hip_queue_stats(gr_hip_queue_t *q, struct gr_hip_iface_stats *st, uint32_t max, int reset) {
-	if (q == nullptr || (st == nullptr && max))
-		return -EINVAL;
+// Every shard's counters of every iface into q->rd ([FWD4_STAT_SHARDS][max_ifaces]),
+// behind all the queue's work, read at the memory side (gr_stats_collect; with
+// `reset` zeroed by the same atomics: no memset whose zeroes an XCD's L2 might
+// hold). Node walks' counts not folded yet go to node_if first.
+static int stats_collect_all(gr_hip_queue *q, bool reset) {
 	gr_hip_ctx *c = q->ctx;
 	if (q->d_stats == nullptr)
 		return -ENOMEM;
 	hipSetDevice(c->dev);
-	std::vector<gr_hip_iface_stats> all((size_t)FWD4_STAT_SHARDS * c->max_ifaces);
 	if (const int e_ = host_wait(q, q->s))
 		return e_;
 	for (host_slot &h : q->hs)
 		if (h.s)
 			if (const int e_ = host_wait(q, h.s))
 				return e_;
-	HCK(hipMemcpy(all.data(), q->d_stats, all.size() * sizeof(gr_hip_iface_stats), hipMemcpyDeviceToHost));
-	uint32_t m = max < c->max_ifaces ? max : c->max_ifaces;
-	memset(st, 0, (size_t)max * sizeof(*st));
-	for (uint32_t s = 0; s < FWD4_STAT_SHARDS; s++) {
-		for (uint32_t i = 0; i < m; i++) {
-			const gr_hip_iface_stats &x = all[(size_t)s * c->max_ifaces + i];
-			st[i].rx_packets += x.rx_packets;
-			st[i].rx_bytes += x.rx_bytes;
-			st[i].tx_packets += x.tx_packets;
-			st[i].tx_bytes += x.tx_bytes;
-		}
+	if (const int r = stats_buf(&q->rd, &q->rd_d, &q->rd_cap, FWD4_STAT_SHARDS * c->max_ifaces))
+		return r;
+	const size_t bytes = sizeof(gr_hip_iface_stats) * FWD4_STAT_SHARDS * c->max_ifaces;
+	if (c->stats_copy) { // measurement only (tools/stats_read_probe.py): round 5's copy and memset
+		HCK(hipMemcpy(q->rd, q->d_stats, bytes, hipMemcpyDeviceToHost));
+		if (reset)
+			HCK(hipMemsetAsync(q->d_stats, 0, bytes, q->s));
+	} else {
+		HCK(gr_stats_collect_launch(q->d_stats, q->rd_d, c->max_ifaces, c->max_ifaces, FWD4_STAT_SHARDS,
+					    reset ? 1 : 0, q->s));
+		if (const int e_ = host_wait(q, q->s))
+			return e_;
 	}
 	if (reset) {
 		// node walks' counts not folded yet go to node_if before the zeroing
 		// (a queue of node walks and plain submits at once reports both there)
 		if (q->snap_counted != q->node_counted || q->snap_pending) {
-			kern_fold(q, all.data(), c->max_ifaces, c->max_ifaces);
+			kern_fold(q, q->rd, c->max_ifaces, c->max_ifaces);
 			q->snap_pending = false;
 			q->snap_counted = q->node_counted;
 		}
 		std::fill(q->kern_seen.begin(), q->kern_seen.end(), gr_hip_iface_stats{0, 0, 0, 0});
-		HCK(hipMemsetAsync(q->d_stats, 0, all.size() * sizeof(gr_hip_iface_stats), q->s));
+	}
+	return 0;
+}
+
+extern "C" int gr_hip_queue_stats_shards(gr_hip_queue_t *q, struct gr_hip_iface_stats *st, uint32_t w, int reset) {
+	if (q == nullptr || (st == nullptr && w))
+		return -EINVAL;
+	if (const int r = stats_collect_all(q, reset != 0))
+		return r;
+	const uint32_t mi = q->ctx->max_ifaces, m = w < mi ? w : mi;
+	for (uint32_t s = 0; s < FWD4_STAT_SHARDS; s++) {
+		memcpy(st + (size_t)s * w, q->rd + (size_t)s * mi, (size_t)m * sizeof(*st));
+		if (w > m)
+			memset(st + (size_t)s * w + m, 0, (size_t)(w - m) * sizeof(*st));
+	}
+	return FWD4_STAT_SHARDS;
+}
+
+extern "C" int gr_hip_queue_stats(gr_hip_queue_t *q, struct gr_hip_iface_stats *st, uint32_t max, int reset) {
+	if (q == nullptr || (st == nullptr && max))
+		return -EINVAL;
+	gr_hip_ctx *c = q->ctx;
+	if (const int r = stats_collect_all(q, reset != 0))
+		return r;
+	uint32_t m = max < c->max_ifaces ? max : c->max_ifaces;
+	memset(st, 0, (size_t)max * sizeof(*st));
+	for (uint32_t s = 0; s < FWD4_STAT_SHARDS; s++) {
+		for (uint32_t i = 0; i < m; i++) {
+			const gr_hip_iface_stats &x = q->rd[(size_t)s * c->max_ifaces + i];
+			st[i].rx_packets += x.rx_packets;
+			st[i].rx_bytes += x.rx_bytes;
+			st[i].tx_packets += x.tx_packets;
+			st[i].tx_bytes += x.tx_bytes;
+		}
 	}
 	return 0;
 }

@@ -268,6 +268,13 @@ class Queue:
         check("gr_hip_queue_stats", self.lib.gr_hip_queue_stats(self._h, ptr(st), len(st), 1 if reset else 0))
         return st
 
+    def stats_shards(self, w, reset=False):
+        """The same counters per shard, (64, w) of abi.STATS_DT: workgroup b of
+        a launch counts into shard b % 64 (gr_hip_queue_stats_shards)."""
+        st = np.zeros(64 * w, dtype=abi.STATS_DT)
+        check("gr_hip_queue_stats_shards", self.lib.gr_hip_queue_stats_shards(self._h, ptr(st), w, 1 if reset else 0))
+        return st.reshape(64, w)
+
     def node_iface_stats(self, reset=False):
         """Per-iface counters of the node walks (the kernels' counts, or the
         hand-back's with "stats" off; what the grout node folds into grout's

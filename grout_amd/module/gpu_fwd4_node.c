@@ -270,6 +270,7 @@ static struct gr_datapath_hooks gpu_hooks = {
 	.rcu_readers = GPU_FWD4_RCU_READERS,
 	.graph_leave = gpu_fwd4_drain,
 	.stats_flush = gpu_fwd4_stats_flush,
+	.holding = gpu_fwd4_holding,
 };
 
 RTE_INIT(gpu_module_init) {
@@ -334,6 +335,10 @@ struct gpu_walk {
 	int draining; // gpu_fwd4_drain: DRAIN_HAND_BACK or DRAIN_LEAVE (0: not draining)
 	uint64_t handed; // batches handed back (delivered onto their edges)
 	uint64_t drain_punted; // mbufs a drain in DRAIN_LEAVE mode sent to grout's CPU nodes
+	// mbufs of a batch the GPU would neither finish nor give up (the fast
+	// path's -EDEADLK: its resident kernel did not leave): never handed on,
+	// since the GPU may still rewrite their frames; the GPU is marked diverged
+	uint64_t stranded;
 };
 
 // gpu_fwd4_drain's modes: hand every batch back within the walk (the held one
@@ -535,7 +540,12 @@ static void poll_until_ready(struct gpu_walk *w) {
 	w->gpu_ns = w->gpu_ns ? (w->gpu_ns * 7 + waited) / 8 : waited;
 }
 
-// Wait for the batch on the GPU and hand it back. Returns its size.
+// Wait for the batch on the GPU and hand it back. Returns its size. The
+// fast path bounds the wait: past the batch's deadline it retires what the
+// GPU did not run, and the hand-back punts those packets, untouched, to
+// grout's CPU nodes (counted in gpu_errors). Only when the GPU would not let
+// go of the batch (-EDEADLK) are its mbufs kept: stranded, never handed on,
+// and the GPU marked diverged (its graphs punt from then on).
 static uint32_t finish_pending(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
 	if (!w->pending)
 		return 0;
@@ -544,6 +554,13 @@ static uint32_t finish_pending(struct rte_graph *graph, struct rte_node *node, s
 	const int r = hand_back(w, k); // one walk in flight per graph: buffer k's
 	PROF_ADD(GPU_FWD4_PROF_FINISH);
 	w->pending = 0;
+	if (r == -EDEADLK) {
+		w->stranded += n;
+		w->gpu_errors++;
+		reader_handed_back(w, k);
+		__atomic_store_n(&gpus[w->gpu].diverged, 1, __ATOMIC_RELEASE);
+		return 0;
+	}
 	deliver(graph, node, w, k, n, r);
 	return n;
 }
@@ -576,6 +593,13 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 		int r = gr_hip_node_send(w->q, NULL, n, WALK_SPLIT);
 		if (r == 0)
 			r = hand_back(w, k);
+		if (r == -EDEADLK) { // stranded: see finish_pending
+			w->stranded += n;
+			w->gpu_errors++;
+			reader_handed_back(w, k);
+			__atomic_store_n(&gpus[w->gpu].diverged, 1, __ATOMIC_RELEASE);
+			return 0;
+		}
 		deliver(graph, node, w, k, n, r);
 		return n;
 	}
@@ -617,7 +641,9 @@ static uint32_t reap(struct rte_graph *graph, struct rte_node *node, struct gpu_
 	PROF_T0();
 	const int r = gr_hip_node_pending(w->q, &ready);
 	PROF_ADD(GPU_FWD4_PROF_POLL);
-	if (r < 0 || !ready)
+	if (r < 0) // past its deadline, or the GPU failed: the finish decides (bounded)
+		return finish_pending(graph, node, w);
+	if (!ready)
 		return 0;
 	w->gpu_ns = w->gpu_ns ? (w->gpu_ns * 7 + waited) / 8 : waited; // an upper bound: polled late
 	return finish_pending(graph, node, w);
@@ -1001,7 +1027,18 @@ int gpu_fwd4_walk_info(const struct rte_graph *graph, struct gpu_fwd4_walk_info 
 	info->append_errors = w->append_errors;
 	info->handed = w->handed;
 	info->drain_punted = w->drain_punted;
+	info->stranded = w->stranded;
 	return 0;
+}
+
+uint64_t gpu_fwd4_holding(const struct rte_graph *graph) {
+	const struct gpu_walk *w = walk_of(graph);
+	if (w == NULL)
+		return 0;
+	uint64_t held = w->n + (w->pending ? w->pend_n : 0);
+	for (int r = 0; r < GPU_FWD4_RCU_PER_GRAPH; r++)
+		held += w->rstate[r] != RD_FREE; // offline at the next walk's flush node
+	return held;
 }
 
 int gpu_fwd4_graph_gpu(const struct rte_graph *graph) {

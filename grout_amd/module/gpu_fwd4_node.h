@@ -185,6 +185,14 @@ int gpu_fwd4_drain(struct rte_graph *);
 // nodes: -1 (the default) = those held when it starts + 2; tests set 0 to
 // take that way at once. 0.
 int gpu_fwd4_set_drain_bound(int32_t batches);
+// grout's housekeeping tick asks every datapath hook what it holds (the
+// holding hook integration/grout-gpu_fwd4-datapath.patch adds): the mbufs the
+// node holds in `graph` (accumulating, and the batch on the GPU) plus its
+// QSBR readers still online (they go offline at the next walk). While it is
+// not 0, grout's worker neither micro-sleeps nor blocks on its RX interrupts
+// (main_loop.c:478-508): the flush node's walks hand the batches back, and
+// the readers go offline, before the worker idles. 0 for another graph.
+uint64_t gpu_fwd4_holding(const struct rte_graph *);
 // mbufs freed by the node's fini because a graph was destroyed while it held
 // them (not drained first): counted, never silently.
 uint64_t gpu_fwd4_fini_freed(void);
@@ -201,6 +209,7 @@ struct gpu_fwd4_walk_info {
 	uint64_t append_errors; // graph walks that could not be staged, punted to grout's CPU nodes
 	uint64_t handed; // batches handed back onto their edges
 	uint64_t drain_punted; // mbufs drains sent to grout's CPU nodes (DRAIN_LEAVE)
+	uint64_t stranded; // mbufs of batches the GPU would not let go of (never handed on)
 };
 int gpu_fwd4_walk_info(const struct rte_graph *, struct gpu_fwd4_walk_info *);
 // Tests only: 0 = the node takes no QSBR reader (round 2's behaviour, to

@@ -526,6 +526,11 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //               smaller launches read them from the global tables
 //   "fib_format_of" (read) the format VRF `value`'s FIB is on the device in
 //   "occupancy" (read) resident workgroups per CU of the current variant
+//   "host_path_last" (read) GR_HIP_HOST_PATH_* of the last gr_hip_fwd4_host(_ex)
+//   "sync_check" debugging: the host path waits after every step it enqueues
+//       and names a failing step on stderr (-EIO)
+//   "stats_copy" measurement only: counters read by a copy and reset by a
+//       memset, as before round 6 (tools/stats_read_probe.py)
 //   "commit_us_stage" / "commit_us_enqueue" / "commit_us_publish" (read) the last
 //       gr_hip_fib4_commit's phases in microseconds: host staging, the
 //       enqueue under the shared lock, the flip under the exclusive lock
@@ -548,6 +553,14 @@ int gr_hip_fwd4_host(
 	void *out_lines,
 	struct gr_hip_verdict *verdicts
 );
+// Which of the three ways the last call took (gr_hip_tune "host_path_last"):
+// every buffer device-accessible pinned memory and "host_direct" on (the
+// kernel over PCIe), pinned with "host_direct" off (runtime copies through
+// device staging), or any buffer pageable (the CPU copies it through the
+// queue's own pinned buffers: pageable pointers never reach the runtime).
+#define GR_HIP_HOST_PATH_DIRECT 0
+#define GR_HIP_HOST_PATH_STAGED 1
+#define GR_HIP_HOST_PATH_PAGEABLE 2
 // The same with the output stride chosen: GR_HIP_LINE (64, whole lines, as
 // gr_hip_fwd4_host) or GR_HIP_PREFIX (32: packed prefixes holding every byte
 // the path changes, GR_HIP_BATCH_F_PREFIX32; less PCIe traffic back).
@@ -564,6 +577,13 @@ int gr_hip_fwd4_host_ex(
 // Per-iface counters accumulated by the queue's kernels (rx in iface_input,
 // tx in iface_output). `stats` receives max_ifaces entries.
 int gr_hip_queue_stats(gr_hip_queue_t *, struct gr_hip_iface_stats *stats, uint32_t max_ifaces, int reset);
+// The same counters before they are summed: `stats` receives 64 shards of
+// `w` ifaces ([shard][w]; a workgroup b of a launch counts into shard b % 64).
+// Returns the number of shards. Diagnostics (which workgroups counted what);
+// grout's counters need only gr_hip_queue_stats / gr_hip_node_iface_stats.
+// Both read the device counters at the memory side (one agent-scope atomic
+// per counter, reset by exchange), never with a plain copy or memset.
+int gr_hip_queue_stats_shards(gr_hip_queue_t *, struct gr_hip_iface_stats *stats, uint32_t w, int reset);
 
 // Device / pinned host memory helpers for C callers without a framework
 // allocator (pinned buffers make gr_hip_fwd4_host copies asynchronous).

@@ -68,6 +68,15 @@ void gr_datapath_hooks_stats_flush(const struct rte_graph *graph, unsigned lcore
 			h->stats_flush(graph, lcore_id, cb, cookie);
 }
 
+uint64_t gr_datapath_hooks_holding(const struct rte_graph *graph) {
+	struct gr_datapath_hooks *h;
+	uint64_t held = 0;
+	STAILQ_FOREACH(h, &hooks, next)
+		if (h->holding != NULL)
+			held += h->holding(graph);
+	return held;
+}
+
 // grout's rcu module (main_loop.c:538-552) as the integration patch sizes
 // it: the workers' lcore ids, then the hooks' readers.
 static void rcu_init(struct event_base *ev) {

@@ -444,6 +444,11 @@ struct gr_datapath_hooks {
 	// the housekeeping tick, after rte_graph's own counters: cb once per node
 	// with what it counted since the last tick
 	int (*stats_flush)(const struct rte_graph *graph, unsigned lcore_id, gr_node_stats_cb_t cb, void *cookie);
+	// what the module's nodes still hold in `graph` (packets accumulating or
+	// on a device, and QSBR readers of theirs online), read at the
+	// housekeeping tick: while it is not 0 the worker neither sleeps nor
+	// blocks on RX interrupts
+	uint64_t (*holding)(const struct rte_graph *graph);
 	STAILQ_ENTRY(gr_datapath_hooks) next;
 };
 
@@ -457,6 +462,8 @@ uint32_t gr_datapath_hooks_readers(void);
 int gr_datapath_hooks_graph_leave(struct rte_graph *graph);
 void gr_datapath_hooks_stats_flush(const struct rte_graph *graph, unsigned lcore_id, gr_node_stats_cb_t cb,
 				   void *cookie);
+// every hook's holding, summed (the patched loop's `held`)
+uint64_t gr_datapath_hooks_holding(const struct rte_graph *graph);
 
 // ---- modules ---------------------------------------------------------------
 struct event_base;

@@ -805,14 +805,20 @@ int gh_load(const uint8_t *frames, uint32_t stride, const struct gr_hip_pkt_meta
 // objs, the sum of process() returns; batches = calls), then every datapath
 // hook's stats_flush (the fast path module's: its counters for the nodes it
 // replaced and for the ifaces).
+static uint64_t window_count; // the tick's ctx.last_count: packets any node counted in the window
+
 static void gpu_node_stat(void *cookie, uint32_t node_id, uint64_t packets, uint64_t calls) {
 	const int k = (int)(intptr_t)cookie;
 	H.graphs[k].w_packets[node_id] += packets;
 	H.graphs[k].w_batches[node_id] += calls;
+	window_count += packets; // hook_node_stats: ctx->last_count += packets
 }
 
-static void housekeeping(int k) {
+// Returns what grout's tick finds in ctx.last_count: the packets the graph's
+// nodes (and the hooks, for the nodes they replaced) counted in the window.
+static uint64_t housekeeping(int k) {
 	rte_rcu_qsbr_quiescent(gr_datapath_rcu(), rte_lcore_id());
+	window_count = 0;
 	const rte_node_t nn = rte_node_max_count();
 	for (rte_node_t id = 0; id < nn; id++) {
 		struct rte_node *n = rte_graph_node_get_by_name(H.graphs[k].name, rte_node_id_to_name(id));
@@ -820,10 +826,12 @@ static void housekeeping(int k) {
 			continue;
 		H.graphs[k].w_packets[id] += n->total_packets - H.graphs[k].prev_packets[id];
 		H.graphs[k].w_batches[id] += n->total_calls - H.graphs[k].prev_calls[id];
+		window_count += n->total_packets - H.graphs[k].prev_packets[id];
 		H.graphs[k].prev_packets[id] = n->total_packets;
 		H.graphs[k].prev_calls[id] = n->total_calls;
 	}
 	gr_datapath_hooks_stats_flush(H.graphs[k].graph, rte_lcore_id(), gpu_node_stat, (void *)(intptr_t)k);
+	return window_count;
 }
 
 static void walk_once(int k) {
@@ -1052,6 +1060,135 @@ int gh_rcu_delete_test(uint32_t slot, uint16_t iface_id, uint32_t hold_ms, struc
 		H.nh_dead[slot] = 0;
 		gpu_fwd4_nh_obj_set(slot, &H.nhs[slot]);
 	}
+	return 0;
+}
+
+// ---- grout's worker loop when RX goes quiet -----------------------------------
+// gr_datapath_loop's housekeeping (main_loop.c:461-527) with the datapath
+// patch: every 256 walks the tick folds the counters (ctx.last_count) and
+// sums what the hooks hold; a window with neither counts as idle. Micro-sleep
+// mode (max_sleep_us > 0, no adaptive IRQ): each idle window sleeps 1 us
+// longer, up to max_sleep_us (port.c:833-878 sets it). Adaptive-IRQ mode:
+// after two idle windows the worker arms its RX interrupts and, with no RX
+// pending, takes its QSBR reader offline and blocks (adaptive_irq_wait,
+// :202-314); here the block is a wait of block_ms on a control thread that
+// runs rte_rcu_qsbr_synchronize meanwhile (grout's route or nexthop delete,
+// route.c:764), and the test ends. The loaded stream is one burst followed by
+// silence: port_rx delivers it, then nothing.
+struct gh_loop_result {
+	uint32_t walks; // graph walks
+	uint32_t windows; // housekeeping ticks
+	uint32_t sleeps; // micro-sleeps taken
+	uint32_t sleeps_held; // ... of them while a hook held packets (counted with ignore_holding)
+	uint32_t busy_held; // ticks busy only because a hook held packets
+	uint32_t blocked; // the adaptive-IRQ stand-in blocked
+	uint32_t recorded_at_block; // mbufs through grout's nodes when the worker blocked (or stopped)
+	uint64_t held_at_block; // what the hooks held then
+	uint32_t readers_online_at_block; // the node's QSBR readers online then
+	uint32_t sync_returned; // the control thread's synchronize returned while the worker was blocked
+	uint64_t sync_us;
+	uint64_t elapsed_us;
+	uint32_t recorded; // at the end
+};
+
+static struct {
+	volatile int done;
+	uint64_t us;
+} LS;
+
+static void *loop_sync(void *arg) {
+	(void)arg;
+	const uint64_t t0 = mono_us();
+	rte_rcu_qsbr_synchronize(gr_datapath_rcu(), RTE_QSBR_THRID_INVALID);
+	LS.us = mono_us() - t0;
+	__atomic_store_n(&LS.done, 1, __ATOMIC_RELEASE);
+	return NULL;
+}
+
+// ignore_holding: the loop as grout runs it without the holding hook (for the
+// test that shows what goes wrong then). idle_windows: micro-sleep mode stops
+// after that many idle ticks in a row once everything is through.
+int gh_loop_test(uint32_t max_sleep_us, int adaptive_irq, int ignore_holding, uint32_t block_ms,
+		 uint32_t idle_windows, uint32_t max_walks, struct gh_loop_result *res) {
+	struct rte_graph *g = cur_graph();
+	if (g == NULL || res == NULL)
+		return -ENOENT;
+	memset(res, 0, sizeof(*res));
+	const uint64_t t0 = mono_us();
+	uint32_t loop = 0, sleep = 0, airq_empty = 0, idle_run = 0;
+	struct rte_rcu_qsbr *v = gr_datapath_rcu();
+	for (uint32_t w = 0; w < max_walks; w++) {
+		rte_graph_walk(g);
+		res->walks++;
+		if (++loop < 256)
+			continue;
+		loop = 0;
+		res->windows++;
+		const uint64_t last_count = housekeeping(H.cur);
+		const uint64_t hold = gr_datapath_hooks_holding(g);
+		const uint64_t held = ignore_holding ? 0 : hold;
+		if (last_count == 0 && hold && !ignore_holding)
+			res->busy_held++;
+		if (adaptive_irq) {
+			if (last_count == 0 && held == 0 && ++airq_empty >= 2) { // ADAPTIVE_IRQ_EMPTY_WINDOWS
+				airq_empty = 0;
+				if (H.next_rx < H.n) // rte_eth_rx_queue_count() > 0: poll on
+					continue;
+				// rte_rcu_qsbr_thread_offline, then the epoll wait
+				struct gpu_fwd4_walk_info info;
+				gpu_fwd4_walk_info(g, &info);
+				res->blocked = 1;
+				res->recorded_at_block = __atomic_load_n(&H.recorded, __ATOMIC_ACQUIRE);
+				res->held_at_block = hold;
+				res->readers_online_at_block = info.readers_online;
+				rte_rcu_qsbr_thread_offline(v, rte_lcore_id());
+				memset(&LS, 0, sizeof(LS));
+				pthread_t th;
+				if (pthread_create(&th, NULL, loop_sync, NULL) != 0)
+					return -EAGAIN;
+				for (const uint64_t t_end = mono_us() + (uint64_t)block_ms * 1000u;
+				     !__atomic_load_n(&LS.done, __ATOMIC_ACQUIRE) && mono_us() < t_end;)
+					usleep(100);
+				res->sync_returned = __atomic_load_n(&LS.done, __ATOMIC_ACQUIRE);
+				res->sync_us = LS.us;
+				// the wakeup (a reconfig kick here): back online, and the
+				// node's readers (if any were left online) are released by
+				// walks until the synchronize is through
+				rte_rcu_qsbr_thread_online(v, rte_lcore_id());
+				for (const uint64_t t_end = mono_us() + 5000000u;
+				     !__atomic_load_n(&LS.done, __ATOMIC_ACQUIRE) && mono_us() < t_end;) {
+					rte_graph_walk(g);
+					rte_rcu_qsbr_quiescent(v, rte_lcore_id());
+				}
+				pthread_join(th, NULL);
+				break;
+			}
+			if (last_count || held)
+				airq_empty = 0;
+		} else {
+			if (last_count == 0 && held == 0 && max_sleep_us > 0) {
+				sleep = sleep >= max_sleep_us ? max_sleep_us : sleep + 1;
+				usleep(sleep);
+				res->sleeps++;
+				if (hold)
+					res->sleeps_held++;
+			} else {
+				sleep = 0;
+			}
+			const int through = __atomic_load_n(&H.recorded, __ATOMIC_ACQUIRE) == H.n && H.next_rx == H.n;
+			idle_run = through && last_count == 0 && held == 0 ? idle_run + 1 : 0;
+			if (idle_run >= idle_windows) {
+				struct gpu_fwd4_walk_info info;
+				gpu_fwd4_walk_info(g, &info);
+				res->recorded_at_block = __atomic_load_n(&H.recorded, __ATOMIC_ACQUIRE);
+				res->held_at_block = hold;
+				res->readers_online_at_block = info.readers_online;
+				break;
+			}
+		}
+	}
+	res->elapsed_us = mono_us() - t0;
+	res->recorded = __atomic_load_n(&H.recorded, __ATOMIC_ACQUIRE);
 	return 0;
 }
 

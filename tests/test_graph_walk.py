@@ -83,6 +83,8 @@ def lib():
         _lib.gh_rcu_delete_test.argtypes = [U32, U16, U32, P]
         _lib.gh_churn_test.argtypes = [U32, ctypes.c_uint8, U16, U32, U32, U32, U32, P]
         _lib.gh_set_rx_burst.argtypes = [U32]
+        _lib.gh_loop_test.argtypes = [U32, ctypes.c_int, ctypes.c_int, U32, U32, U32, P]
+        _lib.gpu_fwd4_holding.restype = ctypes.c_uint64
         _lib.gpu_fwd4_set_batch.argtypes = [U32, ctypes.c_uint64]
         _lib.gh_set_gpu_load.argtypes = [U32]
         _lib.gh_set_gpu_load.restype = None
@@ -98,8 +100,12 @@ def lib():
 
 WALK_INFO_DT = np.dtype([("held", "<u4"), ("in_flight", "<u4"), ("batches", "<u8"), ("max_batch", "<u8"),
                          ("stale", "<u8"), ("readers_online", "<u4"), ("diverged", "<i4"), ("append_errors", "<u8"),
-                         ("handed", "<u8"), ("drain_punted", "<u8")])
-assert WALK_INFO_DT.itemsize == 64
+                         ("handed", "<u8"), ("drain_punted", "<u8"), ("stranded", "<u8")])
+assert WALK_INFO_DT.itemsize == 72
+LOOP_RES_DT = np.dtype([("walks", "<u4"), ("windows", "<u4"), ("sleeps", "<u4"), ("sleeps_held", "<u4"),
+                        ("busy_held", "<u4"), ("blocked", "<u4"), ("recorded_at_block", "<u4"),
+                        ("held_at_block", "<u8"), ("readers_online_at_block", "<u4"), ("sync_returned", "<u4"),
+                        ("sync_us", "<u8"), ("elapsed_us", "<u8"), ("recorded", "<u4")], align=True)
 RCU_RES_DT = np.dtype([("sync_before_handback", "<u4"), ("recorded_at_sync", "<u4"), ("freed_reads", "<u4"),
                        ("recorded", "<u4"), ("stale", "<u8"), ("sync_us", "<u8"), ("walks", "<u4"),
                        ("sync_done", "<u4")])
@@ -1019,3 +1025,158 @@ def test_chain_graph_matches_oracle():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     assert '"check": "ok"' in r.stdout
+
+
+# ---------------------------------------------------------------------------
+# grout's idle logic: the worker sleeps or blocks only when the node holds
+# nothing (the holding hook, integration/grout-gpu_fwd4-datapath.patch)
+# ---------------------------------------------------------------------------
+def _loop(max_sleep_us=0, adaptive=0, ignore_holding=0, block_ms=1000, idle_windows=4, max_walks=50_000_000):
+    r = np.zeros(1, dtype=LOOP_RES_DT)
+    assert lib().gh_loop_test(max_sleep_us, adaptive, ignore_holding, block_ms, idle_windows, max_walks,
+                              r.ctypes.data) == 0
+    return r[0]
+
+
+def _burst_then_silence(n=BATCH_MAX + 1000, seed=0x1D1E):
+    """One burst of n packets (a full batch and a held remainder), then RX
+    quiet; the oracle's edges for them."""
+    fp = graph_ctx()
+    t = T.config_single_route()
+    load(fp, t)
+    fr, me = S.stream(n, seed, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
+    want = oracle.Oracle(t).process_mbufs(fr, me, lines_only=True, burst=BURST)[3]
+    L = lib()
+    assert L.gpu_fwd4_set_batch(BATCH_MAX, 50_000) == 0  # a held packet waits 50 us at most
+    assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, n) == 0
+    return fp, n, want
+
+
+def _results(n):
+    out = np.zeros(n, dtype=OUT_DT)
+    lines = np.zeros((n, abi.LINE), dtype=np.uint8)
+    assert lib().gh_results(out.ctypes.data, lines.ctypes.data) == n
+    return out
+
+
+def _restore_batch():
+    assert lib().gpu_fwd4_set_batch(BATCH, DELAY_NS) == 0
+
+
+@pytest.mark.gpu
+def test_idle_loop_adaptive_irq_blocks_only_when_nothing_held():
+    """Adaptive-IRQ mode (main_loop.c:478-497): one burst, then silence. Two
+    idle windows come long before the GPU hands the 15360-packet batch back;
+    with the holding hook those windows are busy, and by the time the worker
+    blocks every mbuf is through grout's nodes (bit-exact with the oracle),
+    the node's QSBR readers are offline, and a control thread's
+    rte_rcu_qsbr_synchronize returns while the worker is blocked."""
+    fp, n, want = _burst_then_silence()
+    try:
+        r = _loop(adaptive=1, block_ms=2000)
+    finally:
+        _restore_batch()
+    assert r["blocked"] == 1, r
+    assert r["recorded_at_block"] == n and r["held_at_block"] == 0, r
+    assert r["readers_online_at_block"] == 0, r
+    assert r["sync_returned"] == 1, r
+    assert r["busy_held"] > 0, r  # windows with nothing counted, the batch on the GPU
+    got = _results(n)
+    assert np.array_equal(got["edge"], want["edge"]) and np.array_equal(got["iface"], want["iface"])
+
+
+@pytest.mark.gpu
+def test_idle_loop_without_holding_blocks_with_a_batch_on_the_gpu():
+    """The same loop as grout runs it without the hook (the negative
+    control): the resident kernel held back (knob "resident_hold") keeps the
+    batch on the GPU, the worker blocks after two idle windows with the batch
+    and its QSBR reader online, and the synchronize does not return while it
+    is blocked. After the wakeup the batch's deadline ("resident_wait_ms")
+    retires it: its packets go to grout's CPU nodes and the synchronize
+    returns."""
+    fp, n, _ = _burst_then_silence(seed=0x1D1F)
+    fp.tune("resident_wait_ms", 400)
+    fp.tune("resident_hold", 1)
+    try:
+        r = _loop(adaptive=1, ignore_holding=1, block_ms=100)
+    finally:
+        fp.tune("resident_hold", 0)
+        fp.tune("resident_wait_ms", 500)
+        _restore_batch()
+    assert r["blocked"] == 1, r
+    assert r["recorded_at_block"] < n and r["held_at_block"] > 0, r
+    assert r["readers_online_at_block"] > 0, r
+    assert r["sync_returned"] == 0, r
+    assert lib().gh_run(1 << 20) > 0  # everything through after the wakeup
+    assert walk_info()["readers_online"] == 0
+
+
+@pytest.mark.gpu
+def test_idle_loop_resident_deadline_punts_and_counts():
+    """A resident kernel that stops serving its rings (knob "resident_hold":
+    it leaves and is not relaunched): the node's walks return, the batch is
+    retired at its deadline ("resident_wait_ms", measured from the post) and
+    every one of its mbufs goes to grout's CPU nodes (iface_input_cpu)
+    untouched, counted in the node's gpu_errors and the library's
+    "resident_cancels"; then the worker idles and blocks with nothing held.
+    Afterwards the kernel is launched again and the GPU forwards as before."""
+    fp, n, want = _burst_then_silence(seed=0x1D20)
+    L = lib()
+    hip = abi.hip()
+    ctx = L.gh_hip_ctx()
+    c0 = hip.gr_hip_tune(ctx, b"resident_cancels", 0)
+    err0 = ctypes.c_uint64()
+    assert L.gh_node_stats(None, ctypes.byref(err0)) == 0
+    fp.tune("resident_wait_ms", 200)
+    fp.tune("resident_hold", 1)
+    try:
+        r = _loop(adaptive=1, block_ms=2000)
+    finally:
+        fp.tune("resident_hold", 0)
+        fp.tune("resident_wait_ms", 500)
+        _restore_batch()
+    assert r["blocked"] == 1 and r["recorded_at_block"] == n, r
+    assert r["readers_online_at_block"] == 0 and r["sync_returned"] == 1, r
+    assert 200_000 <= r["elapsed_us"] < 3_000_000, r  # past the deadline, well within grout's 5 s
+    got = _results(n)
+    punt = got["edge"] == abi.EDGE["punt"]
+    assert punt.sum() >= BATCH_MAX, int(punt.sum())  # the retired batch, untouched
+    ok = ~punt
+    assert np.array_equal(got["edge"][ok], want["edge"][ok])
+    assert (got["data_off"][punt] == 128).all()  # as port_rx left them (RTE_PKTMBUF_HEADROOM)
+    err = ctypes.c_uint64()
+    assert L.gh_node_stats(None, ctypes.byref(err)) == 0
+    assert err.value > err0.value
+    assert hip.gr_hip_tune(ctx, b"resident_cancels", 0) > c0
+    assert walk_info()["stranded"] == 0
+    # the kernel serves batches again
+    check_walk(T.config_single_route(), *S.stream(5000, 0x1D21, dst_range=(T.ip4("16.1.0.0"),
+                                                                          T.ip4("16.1.255.255"))))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ignore_holding", [0, 1], ids=["holding", "no_holding"])
+def test_idle_loop_micro_sleep(ignore_holding):
+    """Micro-sleep mode (main_loop.c:499-509, max_sleep_us from port.c:833-878):
+    with the hook no window sleeps while the node holds packets; without it
+    (the batch kept on the GPU by "resident_hold" until its deadline) the
+    worker sleeps with the batch held."""
+    fp, n, want = _burst_then_silence(seed=0x1D22 + ignore_holding)
+    if ignore_holding:
+        fp.tune("resident_wait_ms", 200)
+        fp.tune("resident_hold", 1)
+    try:
+        r = _loop(max_sleep_us=20, ignore_holding=ignore_holding, idle_windows=8)
+    finally:
+        fp.tune("resident_hold", 0)
+        fp.tune("resident_wait_ms", 500)
+        _restore_batch()
+    assert r["recorded"] == n, r
+    if ignore_holding:
+        assert r["sleeps_held"] > 0, r
+    else:
+        assert r["sleeps_held"] == 0 and r["busy_held"] > 0, r
+        assert r["readers_online_at_block"] == 0, r
+        got = _results(n)
+        assert np.array_equal(got["edge"], want["edge"])

@@ -96,10 +96,18 @@ def test_datapath_patch_adds_hooks_not_module_calls():
     assert re.search(r"if \(atomic_load\(&w->shutdown\) \|\| atomic_load\(&w->next_config\) != cur\) \{\n"
                      r"(\+[^\n]*\n)*\+\s*int n = hook->graph_leave \? hook->graph_leave\(graph\) : 0;\n"
                      r"(\+[^\n]*\n)* \s*worker_active_dec\(\);", text)
-    # stats_flush at the housekeeping tick, right after rte_graph's own counters
-    assert re.search(r"\n \s*rte_graph_cluster_stats_get\(ctx\.stats, false\);\n\+\s*STAILQ_FOREACH \(hook, "
-                     r"&datapath_hooks, next\)\n\+\s*if \(hook->stats_flush != NULL\)\n\+\s*hook->stats_flush\(graph, "
-                     r"rte_lcore_id\(\), hook_node_stats, &ctx\);", text)
+    # stats_flush at the housekeeping tick, right after rte_graph's own counters,
+    # and what the hooks' nodes hold summed there
+    assert re.search(r"\n \s*rte_graph_cluster_stats_get\(ctx\.stats, false\);\n\+\s*held = 0;\n\+\s*STAILQ_FOREACH "
+                     r"\(hook, &datapath_hooks, next\) \{\n\+\s*if \(hook->stats_flush != NULL\)\n\+\s*hook->stats_flush\("
+                     r"graph, rte_lcore_id\(\), hook_node_stats, &ctx\);\n(\+[^\n]*\n)*\+\s*held \+= "
+                     r"hook->holding\(graph\);", text)
+    # a window whose nodes hold packets is not idle: no micro-sleep, no block
+    # on RX interrupts (main_loop.c:478-508)
+    assert re.search(r"\n\+\s*if \(ctx\.last_count == 0 && held == 0\n \s*&& \+\+airq_empty >= "
+                     r"ADAPTIVE_IRQ_EMPTY_WINDOWS\) \{", text)
+    assert re.search(r"\n\+\s*if \(ctx\.last_count \|\| held\)\n \s*airq_empty = 0;", text)
+    assert re.search(r"\n\+\s*if \(ctx\.last_count == 0 && held == 0 && max_sleep_us > 0\) \{", text)
     assert "const uint32_t readers = RTE_MAX_LCORE + hooks_rcu_readers;" in added
     body = re.search(r"struct gr_datapath_hooks \{(.*?)\};", added, re.S).group(1)
     mine = re.search(r"struct gr_datapath_hooks \{(.*?)\};", open(os.path.join(STANDIN_INC, "gr_datapath_min.h")).read(),
@@ -110,6 +118,7 @@ def test_datapath_patch_adds_hooks_not_module_calls():
     node = open(os.path.join(MOD, "gpu_fwd4_node.c")).read()
     assert "gr_datapath_hooks_register(&gpu_hooks);" in node
     assert ".graph_leave = gpu_fwd4_drain," in node and ".stats_flush = gpu_fwd4_stats_flush," in node
+    assert ".holding = gpu_fwd4_holding," in node
 
 
 def _quoted_includes(path):
