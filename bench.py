@@ -171,6 +171,9 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     gpu_numa = abi.hip().gr_hip_device_numa_node(local)
+    # the CPUs this process may use before the rank binds to its GPU's socket:
+    # the CPU baseline gets them back (a box's whole share, not one socket's)
+    own_cpus = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
     bound = replicas.bind_to_numa(gpu_numa)  # this rank's host threads on its GPU's socket
 
     # ---- control plane: topology + FIB replica on this GPU
@@ -475,8 +478,18 @@ def main():
     elif args.workload != "fullview64":
         result["metric"] = result["metric"] + f" [non-headline workload: {args.workload}]"
 
+    # every rank's GPU legs are done: after this barrier rank 0 alone goes on,
+    # with the host-memory path on its own GPU and the CPU baseline on the
+    # host's cores (N > 1 lines carry both too; the other ranks are idle)
+    rep.barrier()
+    if rank != 0:
+        q.close()
+        fp.close()
+        rep.close()
+        return
+
     # ---- host-memory path (PCIe-inclusive): reported, never `value`
-    if rank == 0 and world == 1 and not args.no_host_path:
+    if not args.no_host_path:
         hn = min(n, 1 << 23)
         lines = torch.from_numpy(np.ascontiguousarray(frames[:hn, :abi.LINE]).reshape(-1)).pin_memory()
         hmeta = torch.from_numpy(meta[:hn].view(np.uint8)).pin_memory()
@@ -524,8 +537,10 @@ def main():
     # alone: same CPU, offset, warm-up, shared FIB and packet count, in the
     # same call; beside them the 16 workers with a FIB copy each on THP
     # (slower on the boxes measured: 16 tables of 128 MiB leave L3)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if not args.no_cpu_baseline:
         import oracle
+        if own_cpus is not None:  # unbound: the box's whole CPU share (cpu_placement picks from it)
+            os.sched_setaffinity(0, own_cpus)
         o = oracle.Oracle(topo)
         cf, cm = frames[: 1 << 20].copy(), meta[: 1 << 20].copy()
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
@@ -582,6 +597,7 @@ def main():
             "multi_core_leg_s": round(tS, 2),
             "cpus": cpus,
             "host_cpus": host_cpus(),
+            "ranks_idle": world - 1,  # the other replicas had finished (final barrier)
             "sample": (f"oracle C restatement of grout's node chain (bursts of 64, "
                        f"{'per-length prefix hash LPM6' if args.workload == 'fullview6' else 'DIR24_8 8-byte entries'}), "
                        f"{threads} pinned threads on one shared FIB (grout's layout: one rte_fib per VRF), "
@@ -594,8 +610,7 @@ def main():
         }
         o.close()
 
-    if rank == 0:
-        print(json.dumps(result), flush=True)
+    print(json.dumps(result), flush=True)
     q.close()
     fp.close()
     rep.close()

@@ -195,16 +195,18 @@ def test_bench_two_ranks_on_the_gpu():
 def test_bench_spawns_two_ranks_on_the_gpu():
     """The driver's N>1 command without a launcher: bench.py --gpus 2 starts
     both ranks itself on config 3 (full view); one line, n_gpus 2, both
-    ranks' own rates and kernel times."""
+    ranks' own rates and kernel times, and -- after the final barrier, rank
+    0 alone -- the PCIe-inclusive host path and the CPU baseline (a short
+    sample here), as on the driver's N>1 lines."""
     import json
     import subprocess
     import sys
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["GR_BENCH_SHARE_GPU"] = "1"
     cmd = [sys.executable, "bench.py", "--gpus", "2", "--workload", "fullview64", "--batch", str(1 << 22),
-           "--steps", "8", "--warmup", "2", "--settle-ms", "20", "--no-prefix-leg", "--no-cpu-baseline",
-           "--no-host-path"]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+           "--steps", "8", "--warmup", "2", "--settle-ms", "20", "--no-prefix-leg", "--cpu-seconds", "0.3",
+           "--cpu-threads", "4"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [x for x in r.stdout.splitlines() if x.strip()]
     assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]  # only the line on stdout
@@ -212,3 +214,5 @@ def test_bench_spawns_two_ranks_on_the_gpu():
     assert d["n_gpus"] == 2 and [x["rank"] for x in d["ranks"]] == [0, 1]
     assert all(x["mpps"] > 0 and x["kernel_ms_avg"] > 0 and x["forwarded_frac"] > 0.999 for x in d["ranks"])
     assert "frac_plain" in d["roofline"]
+    assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["cores"] == 4 and d["cpu_baseline"]["ranks_idle"] == 1
+    assert d["host_path"]["mpps"] > 0

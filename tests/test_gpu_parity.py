@@ -112,6 +112,20 @@ def test_fullview_full_size(fastpath, inplace):
     assert (g[1]["edge"] == abi.EDGE["port_output"]).mean() > 0.99
 
 
+@pytest.mark.parametrize("g", range(8))
+def test_config5_per_gpu_streams(fastpath, g):
+    """BASELINE config 5's inputs: the RX stream of GPU g of the 8-GPU node
+    (seed 0x67721000 + g; what bench.py --gpus 8's rank g
+    forwards), 2^22 packets over the 1M-route view, forwarded on this GPU:
+    bit-exact with the oracle, counters included."""
+    t = _fullview()
+    fr, me = S.stream(1 << 22, S.SEED_GPU_BASE + g, routes=t.route_array())
+    o = oracle.Oracle(t).process(fr, me)
+    got = run_gpu(fastpath, t, fr, me)
+    compare(o, got)
+    assert (got[1]["edge"] == abi.EDGE["port_output"]).mean() > 0.99
+
+
 def test_fullview_random_dst(fastpath):
     """Uniformly random destinations: misses, tbl8 hits, /32s."""
     t = _fullview()
