@@ -65,7 +65,7 @@ struct event {
 };
 static struct event *timers;
 
-struct event *event_new(struct event_base *base, int fd, short what, void (*cb)(int, short, void *), void *arg) {
+struct event *event_new(struct event_base *base, evutil_socket_t fd, short what, event_callback_fn cb, void *arg) {
 	(void)fd;
 	(void)what;
 	struct event *e = calloc(1, sizeof(*e));

@@ -312,7 +312,7 @@ static rte_be16_t cksum_update32(rte_be16_t cksum, uint32_t from, uint32_t to) {
 // snat44_process with static rules only: a packet whose source has a rule
 // on the egress iface gets the translated source, its IPv4 checksum and a
 // non-zero UDP checksum updated (FINAL); anything else CONTINUEs.
-nat_verdict_t snat44_process(const struct iface *iface, struct rte_mbuf *m) {
+nat_verdict_t gr_standin_snat44_process(const struct iface *iface, struct rte_mbuf *m) {
 	if (!(iface->flags & GR_IFACE_F_SNAT_STATIC))
 		return NAT_VERDICT_CONTINUE;
 	struct rte_ipv4_hdr *ip = rte_pktmbuf_mtod(m, struct rte_ipv4_hdr *);

@@ -85,7 +85,9 @@ void gr_test_events_count(uint64_t *pub, uint64_t *internal);
 // itself on the event base modules get at init) -------------------------------
 struct event;
 struct timeval;
-struct event *event_new(struct event_base *base, int fd, short what, void (*cb)(int, short, void *), void *arg);
+typedef int evutil_socket_t; // libevent's, on POSIX (event2/util.h)
+typedef void (*event_callback_fn)(evutil_socket_t, short, void *); // event2/event.h
+struct event *event_new(struct event_base *base, evutil_socket_t fd, short what, event_callback_fn cb, void *arg);
 int event_add(struct event *ev, const struct timeval *tv);
 int event_del(struct event *ev);
 void event_free(struct event *ev);

@@ -218,13 +218,27 @@ rte_edge_t rte_node_edge_get(rte_node_t id, char *next_nodes[]);
 rte_graph_t rte_graph_create(const char *name, struct rte_graph_param *prm);
 int rte_graph_destroy(rte_graph_t id);
 struct rte_graph *rte_graph_lookup(const char *name);
-void rte_graph_walk(struct rte_graph *graph);
+// DPDK's rte_graph_walk, rte_node_enqueue and rte_node_enqueue_x1 are static
+// inline (rte_graph_worker.h, rte_graph_worker_common.h): so are these, over
+// the stand-in's walk and enqueue
+void rte_standin_graph_walk(struct rte_graph *graph);
+static inline void rte_graph_walk(struct rte_graph *graph) {
+	rte_standin_graph_walk(graph);
+}
 // The instance of node `name` in `graph` (NULL if absent); for counters.
 struct rte_node *rte_graph_node_get_by_name(const char *graph, const char *name);
 
 // Worker API (rte_graph_worker_common.h)
-void rte_node_enqueue_x1(struct rte_graph *graph, struct rte_node *node, rte_edge_t next, void *obj);
-void rte_node_enqueue(struct rte_graph *graph, struct rte_node *node, rte_edge_t next, void **objs, uint16_t nb_objs);
+void rte_standin_node_enqueue_x1(struct rte_graph *graph, struct rte_node *node, rte_edge_t next, void *obj);
+void rte_standin_node_enqueue(struct rte_graph *graph, struct rte_node *node, rte_edge_t next, void **objs,
+			      uint16_t nb_objs);
+static inline void rte_node_enqueue_x1(struct rte_graph *graph, struct rte_node *node, rte_edge_t next, void *obj) {
+	rte_standin_node_enqueue_x1(graph, node, next, obj);
+}
+static inline void rte_node_enqueue(struct rte_graph *graph, struct rte_node *node, rte_edge_t next, void **objs,
+				    uint16_t nb_objs) {
+	rte_standin_node_enqueue(graph, node, next, objs, nb_objs);
+}
 void rte_node_next_stream_move(struct rte_graph *graph, struct rte_node *src, rte_edge_t next);
 
 #define RTE_INIT(fn)                                                                               \

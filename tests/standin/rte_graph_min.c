@@ -308,11 +308,11 @@ static void enqueue(struct rte_graph *g, struct rte_node *node, rte_edge_t next,
 	make_pending(g, to);
 }
 
-void rte_node_enqueue_x1(struct rte_graph *graph, struct rte_node *node, rte_edge_t next, void *obj) {
+void rte_standin_node_enqueue_x1(struct rte_graph *graph, struct rte_node *node, rte_edge_t next, void *obj) {
 	enqueue(graph, node, next, &obj, 1);
 }
 
-void rte_node_enqueue(struct rte_graph *graph, struct rte_node *node, rte_edge_t next, void **objs,
+void rte_standin_node_enqueue(struct rte_graph *graph, struct rte_node *node, rte_edge_t next, void **objs,
 		      uint16_t nb_objs) {
 	if (nb_objs)
 		enqueue(graph, node, next, objs, nb_objs);
@@ -336,7 +336,7 @@ static void run(struct rte_graph *g, struct rte_node *n) {
 	n->total_packets += ret;
 }
 
-void rte_graph_walk(struct rte_graph *g) {
+void rte_standin_graph_walk(struct rte_graph *g) {
 	for (uint32_t i = 0; i < g->priv->n_nodes; i++) { // sources first
 		struct rte_node *n = g->priv->nodes[i];
 		if (defs[n->id].flags & RTE_NODE_SOURCE_F) {

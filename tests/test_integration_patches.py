@@ -213,7 +213,7 @@ def test_module_library_exports_its_api_only():
     syms = [l.split()[-1] for l in out.splitlines() if l.strip()]
     assert syms and all(x.startswith("gpu_fwd4_") for x in syms), [x for x in syms if not x.startswith("gpu_fwd4_")]
     und = subprocess.run(["nm", "-D", "--undefined-only", lib], capture_output=True, text=True, check=True).stdout
-    assert "rte_node_enqueue" in und and "module_register" in und  # grout's / DPDK's, left undefined
+    assert "rte_node_from_name" in und and "module_register" in und  # grout's / DPDK's, left undefined
 
 
 def _added(name):
@@ -257,3 +257,128 @@ def test_control_patch_feeds_the_mirror():
     # every INTERNAL-origin branch grout has for these events now pushes internally
     for f in ("modules/infra/control/nexthop.c", "modules/ip/control/route.c", "modules/ip6/control/route.c"):
         assert "+++ b/" + f in text, f
+
+
+# ---- the stand-ins' prototypes against grout's and DPDK's ---------------------
+# What the module calls that grout declares, and where (grout's tree, or the
+# lines an integration patch adds).
+GROUT_PROTOS = {
+    "event_subscribe": "main/event.h",
+    "event_subscribe_internal": "grout-gpu_fwd4-control.patch",
+    "gr_conn_lookup": "modules/policy/control/conntrack.h",
+    "gr_conn_parse_key": "modules/policy/control/conntrack.h",
+    "gr_datapath_hooks_register": "grout-gpu_fwd4-datapath.patch",
+    "gr_datapath_rcu": "modules/infra/datapath/rcu.h",
+    "gr_mbuf_is_traced": "modules/infra/datapath/mbuf.h",
+    "iface_get_eth_addr": "modules/infra/control/iface.h",
+    "iface_get_stats": "modules/infra/control/iface.h",
+    "module_register": "main/module.h",
+    "snat44_process": "modules/policy/datapath/nat_datapath.h",
+}
+# DPDK 25.11 (subprojects/dpdk-25.11.wrap) and libevent 2.1 are not in the
+# reference tree: their published prototypes, restated (inline?, return, params)
+EXTERNAL_PROTOS = {
+    "rte_graph_walk": (True, "void", ["struct rte_graph *"]),
+    "rte_node_enqueue": (True, "void", ["struct rte_graph *", "struct rte_node *", "rte_edge_t", "void * *",
+                                        "uint16_t"]),
+    "rte_node_enqueue_x1": (True, "void", ["struct rte_graph *", "struct rte_node *", "rte_edge_t", "void *"]),
+    "rte_node_from_name": (False, "rte_node_t", ["const char *"]),
+    "rte_pktmbuf_free": (True, "void", ["struct rte_mbuf *"]),
+    "rte_prefetch0": (True, "void", ["const volatile void *"]),
+    "rte_rcu_qsbr_thread_online": (True, "void", ["struct rte_rcu_qsbr *", "unsigned int"]),
+    "rte_rcu_qsbr_thread_offline": (True, "void", ["struct rte_rcu_qsbr *", "unsigned int"]),
+    "rte_rcu_qsbr_thread_register": (False, "int", ["struct rte_rcu_qsbr *", "unsigned int"]),
+    "rte_rcu_qsbr_thread_unregister": (False, "int", ["struct rte_rcu_qsbr *", "unsigned int"]),
+    "event_new": (False, "struct event *", ["struct event_base *", "evutil_socket_t", "short", "event_callback_fn",
+                                            "void *"]),
+    "event_add": (False, "int", ["struct event *", "const struct timeval *"]),
+    "event_del": (False, "int", ["struct event *"]),
+    "event_free": (False, "void", ["struct event *"]),
+}
+_QUAL = {"const", "volatile", "struct", "enum", "union", "signed", "unsigned", "restrict"}
+_STORAGE = {"static", "inline", "extern", "__rte_always_inline", "__rte_experimental"}
+
+
+def _c_strip(text):
+    text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+    return re.sub(r"//[^\n]*", " ", text)
+
+
+def _c_type(tokens):
+    return " ".join(tokens)
+
+
+def _c_param(p):
+    toks = re.findall(r"\w+|\*", p)
+    if len(toks) > 1 and re.match(r"\w+$", toks[-1]) and any(t == "*" or t not in _QUAL for t in toks[:-1]):
+        toks = toks[:-1]  # the parameter's name
+    return _c_type(toks)
+
+
+def _c_proto(text, name):
+    """(inline, return type, parameter types) of `name`'s declaration or
+    definition in C text, or None."""
+    m = re.search(r"^([ \t\w\*]*?)\b%s\s*\(([^()]*)\)\s*[;{]" % re.escape(name), _c_strip(text), re.M)
+    if m is None:
+        return None
+    pre = re.findall(r"\w+|\*", m.group(1))
+    inline = any(t in ("inline", "__rte_always_inline") for t in pre)
+    ret = _c_type([t for t in pre if t not in _STORAGE])
+    params = [_c_param(p) for p in m.group(2).split(",") if p.strip()]
+    return inline, ret, params if params != ["void"] else []
+
+
+def _module_calls():
+    txt = _c_strip("".join(open(os.path.join(MOD, f)).read() for f in MODULE_SRC))
+    return set(re.findall(r"\b([a-z_]\w*)\s*\(", txt))
+
+
+def _standin_proto(name):
+    for dp, _, fs in os.walk(STANDIN_INC):
+        for f in sorted(fs):
+            p = _c_proto(open(os.path.join(dp, f)).read(), name)
+            if p is not None:
+                return p
+    return None
+
+
+def test_standin_prototypes_parse():
+    """The prototype reader on the forms grout writes (names or none, const
+    typedefs, pointers, static inline, a declaration over several lines)."""
+    assert _c_proto("static inline struct iface_stats *iface_get_stats(uint16_t lcore_id, uint16_t ifid) {",
+                    "iface_get_stats") == (True, "struct iface_stats *", ["uint16_t", "uint16_t"])
+    assert _c_proto("bool gr_conn_parse_key(\n\tconst struct iface *,\n\tconst addr_family_t,\n"
+                    "\tconst struct rte_mbuf *,\n\tstruct conn_key *\n);", "gr_conn_parse_key") == (
+        False, "bool", ["const struct iface *", "const addr_family_t", "const struct rte_mbuf *", "struct conn_key *"])
+    assert _c_proto("struct rte_rcu_qsbr *gr_datapath_rcu(void);", "gr_datapath_rcu") == (
+        False, "struct rte_rcu_qsbr *", [])
+
+
+def test_standin_prototypes_match_grouts():
+    """Every function the module calls that grout declares has, in the
+    stand-ins it is compiled against here, grout's prototype: the same return
+    type, parameter types, and static inline or not (iface.h:117-119,
+    nat_datapath.h:57-67, conntrack.h:50-56, ...); every DPDK or libevent
+    function it calls, the published prototype (EXTERNAL_PROTOS). A mismatch
+    would otherwise surface only when a grout maintainer builds the module."""
+    calls = _module_calls()
+    for name, where in sorted(GROUT_PROTOS.items()):
+        assert name in calls, name  # the table lists only what the module uses
+        mine = _standin_proto(name)
+        assert mine is not None, name
+        if where.endswith(".patch"):
+            theirs = _c_proto(_added(where)[1], name)
+        elif os.path.isdir(REF + "/modules"):
+            theirs = _c_proto(open(os.path.join(REF, where)).read(), name)
+        else:
+            continue  # the reference tree is not mounted: nothing to compare with
+        assert theirs is not None, (name, where)
+        assert mine == theirs, (name, where, mine, theirs)
+    for name, want in sorted(EXTERNAL_PROTOS.items()):
+        mine = _standin_proto(name)
+        assert mine is not None, name
+        assert mine == want, (name, mine, want)
+    # every DPDK / libevent function the module calls is in the table
+    ext = {c for c in calls if c.startswith(("rte_", "event_"))} - set(GROUT_PROTOS)
+    ext -= {"rte_pktmbuf_mtod"}  # a macro in DPDK and here
+    assert ext <= set(EXTERNAL_PROTOS), ext - set(EXTERNAL_PROTOS)
