@@ -339,6 +339,13 @@ struct gpu_walk {
 	// path's -EDEADLK: its resident kernel did not leave): never handed on,
 	// since the GPU may still rewrite their frames; the GPU is marked diverged
 	uint64_t stranded;
+	// latency budget (conf.latency_budget_ns): the batch cap in effect, the
+	// arrival of the oldest packet of the batch on the GPU, and what the
+	// batches' oldest packets took, arrival to hand-back (a moving average)
+	uint32_t lcap;
+	uint64_t pend_first_ns;
+	uint64_t lat_ns;
+	uint64_t over_budget;
 };
 
 // gpu_fwd4_drain's modes: hand every batch back within the walk (the held one
@@ -384,6 +391,14 @@ static struct gpu_walk *walk_of(const struct rte_graph *g) {
 		if (walks[i] != NULL && walks[i]->graph == g)
 			return walks[i];
 	return NULL;
+}
+
+int gpu_fwd4_set_latency_budget(uint64_t budget_ns) {
+	conf.latency_budget_ns = budget_ns; // each graph's cap restarts at its next batch
+	for (int i = 0; i < GPU_FWD4_MAX_GRAPHS; i++)
+		if (walks[i] != NULL)
+			walks[i]->lcap = 0;
+	return 0;
 }
 
 GR_NODE_CTX_TYPE(gpu_fwd4_ctx, { struct gpu_walk *w; });
@@ -540,6 +555,43 @@ static void poll_until_ready(struct gpu_walk *w) {
 	w->gpu_ns = w->gpu_ns ? (w->gpu_ns * 7 + waited) / 8 : waited;
 }
 
+// What the batch accumulating may hold, and how long its oldest packet may
+// wait before it is sent: conf's, or under a latency budget the graph's cap
+// and the budget less the GPU's round trip (a quarter of the budget at least).
+static uint32_t batch_cap(struct gpu_walk *w) {
+	if (conf.latency_budget_ns == 0)
+		return conf.batch;
+	if (w->lcap == 0 || w->lcap > conf.batch)
+		w->lcap = conf.batch < 1024 ? conf.batch : 1024;
+	return w->lcap;
+}
+
+static uint64_t hold_max(const struct gpu_walk *w) {
+	const uint64_t b = conf.latency_budget_ns;
+	if (b == 0)
+		return conf.max_delay_ns;
+	const uint64_t h = w->gpu_ns + b / 4 < b ? b - w->gpu_ns : b / 4;
+	return h < conf.max_delay_ns ? h : conf.max_delay_ns;
+}
+
+// A batch came back: its oldest packet took `lat` from its arrival. Under a
+// budget the cap shrinks by a quarter past it, and grows by an eighth (64 at
+// least) while full batches come back within 3/5 of it.
+static void budget_update(struct gpu_walk *w, uint64_t lat, uint32_t n) {
+	w->lat_ns = w->lat_ns ? (w->lat_ns * 7 + lat) / 8 : lat;
+	const uint64_t b = conf.latency_budget_ns;
+	if (b == 0)
+		return;
+	const uint32_t cap = batch_cap(w);
+	if (lat > b) {
+		w->over_budget++;
+		w->lcap = cap - cap / 4 > 64 ? cap - cap / 4 : 64;
+	} else if (lat * 5 < b * 3 && n >= cap - cap / 8) {
+		const uint32_t up = cap / 8 > 64 ? cap / 8 : 64;
+		w->lcap = cap + up < conf.batch ? cap + up : conf.batch;
+	}
+}
+
 // Wait for the batch on the GPU and hand it back. Returns its size. The
 // fast path bounds the wait: past the batch's deadline it retires what the
 // GPU did not run, and the hand-back punts those packets, untouched, to
@@ -554,6 +606,7 @@ static uint32_t finish_pending(struct rte_graph *graph, struct rte_node *node, s
 	const int r = hand_back(w, k); // one walk in flight per graph: buffer k's
 	PROF_ADD(GPU_FWD4_PROF_FINISH);
 	w->pending = 0;
+	budget_update(w, now_ns() - w->pend_first_ns, n);
 	if (r == -EDEADLK) {
 		w->stranded += n;
 		w->gpu_errors++;
@@ -580,6 +633,7 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 	if (w->n == 0)
 		return 0;
 	const uint32_t k = w->cur, n = w->n;
+	const uint64_t first = w->first_ns;
 	w->n = 0;
 	w->first_ns = 0;
 	if (gpus[w->gpu].diverged) { // not to this GPU: grout's CPU nodes, after the batch before
@@ -619,6 +673,7 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 	w->pending = 1;
 	w->pend_n = n;
 	w->pend_ns = now_ns();
+	w->pend_first_ns = first ? first : w->pend_ns;
 	w->cur = k ^ 1;
 	return delivered;
 }
@@ -734,7 +789,7 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 	const uint64_t t = now_ns();
 	if (w->first_ns == 0)
 		w->first_ns = t;
-	if (w->draining || w->n >= conf.batch || nb_objs < conf.rx_burst || t - w->first_ns >= conf.max_delay_ns)
+	if (w->draining || w->n >= batch_cap(w) || nb_objs < conf.rx_burst || t - w->first_ns >= hold_max(w))
 		flush(graph, node, w);
 	else
 		reap(graph, node, w);
@@ -934,7 +989,7 @@ static uint16_t gpu_flush_process(struct rte_graph *graph, struct rte_node *node
 	// (flush() hands back the one still pending, and none is after these)
 	const uint64_t t = now_ns();
 	uint32_t n = 0;
-	if (w->pending && (w->draining || t - w->pend_ns >= conf.max_delay_ns))
+	if (w->pending && (w->draining || t - w->pend_ns >= hold_max(w)))
 		n = finish_pending(graph, node, w); // waited long enough (or leaving the graph): wait for the GPU
 	else
 		n = reap(graph, node, w);
@@ -942,7 +997,7 @@ static uint16_t gpu_flush_process(struct rte_graph *graph, struct rte_node *node
 	// latency wins over batching (as for a short burst); else max_delay
 	const int idle = !w->rx_seen;
 	w->rx_seen = 0;
-	if (w->n != 0 && (w->draining || idle || t - w->first_ns >= conf.max_delay_ns))
+	if (w->n != 0 && (w->draining || idle || t - w->first_ns >= hold_max(w)))
 		n += flush(graph, node, w); // pipelined: a later walk of the graph hands it back
 	PROF_ADD(GPU_FWD4_PROF_FLUSH_NODE);
 	return (uint16_t)(n > UINT16_MAX ? UINT16_MAX : n);
@@ -1028,6 +1083,9 @@ int gpu_fwd4_walk_info(const struct rte_graph *graph, struct gpu_fwd4_walk_info 
 	info->handed = w->handed;
 	info->drain_punted = w->drain_punted;
 	info->stranded = w->stranded;
+	info->batch_cap = batch_cap(w);
+	info->lat_ns = w->lat_ns;
+	info->over_budget = w->over_budget;
 	return 0;
 }
 

@@ -104,6 +104,14 @@ struct gpu_fwd4_conf {
 	// knob "resident": descriptor rings, no launch per batch); 1: one launch
 	// per batch
 	uint32_t launch_per_batch;
+	// 0 (the default): batches of `batch` packets, held `max_delay_ns` at
+	// most. Otherwise a latency budget for a packet from its arrival at the
+	// node to its hand-back onto its edge: each graph sizes its batches so
+	// that its batches' oldest packets come back within it (a batch cap
+	// shrunk by a quarter when one does not, grown by an eighth while they
+	// come back within 3/5 of it), and holds a packet at most the budget
+	// less the GPU's measured round trip (a quarter of it at least)
+	uint64_t latency_budget_ns;
 };
 
 // Before module init (grout: from its configuration). A batch above
@@ -119,6 +127,8 @@ int gpu_fwd4_set_launch_per_batch(int on);
 // Batch size and maximum hold time at any time (the next batch of each graph
 // takes them; the batch is clamped to GPU_FWD4_BATCH_MAX). 0 or -EINVAL.
 int gpu_fwd4_set_batch(uint32_t batch, uint64_t max_delay_ns);
+// The latency budget (gpu_fwd4_conf.latency_budget_ns; 0: off), at any time.
+int gpu_fwd4_set_latency_budget(uint64_t budget_ns);
 // The RX burst (grout's rx_burst_max, graph.c:612-650: 1..256): a shorter
 // burst means the RX queue drained, and the node flushes. 0 or -EINVAL.
 int gpu_fwd4_set_rx_burst(uint32_t rx_burst);
@@ -210,6 +220,9 @@ struct gpu_fwd4_walk_info {
 	uint64_t handed; // batches handed back onto their edges
 	uint64_t drain_punted; // mbufs drains sent to grout's CPU nodes (DRAIN_LEAVE)
 	uint64_t stranded; // mbufs of batches the GPU would not let go of (never handed on)
+	uint32_t batch_cap; // the batch size in effect (latency budget: the graph's cap)
+	uint64_t lat_ns; // moving average of the batches' oldest packet, arrival to hand-back
+	uint64_t over_budget; // batches whose oldest packet came back past the latency budget
 };
 int gpu_fwd4_walk_info(const struct rte_graph *, struct gpu_fwd4_walk_info *);
 // Tests only: 0 = the node takes no QSBR reader (round 2's behaviour, to

@@ -122,6 +122,9 @@ def main():
                     help="GPU node batch sizes to sweep at each K (gpu_fwd4_set_batch), e.g. 1024,4096,15360; "
                          "the chain and the harness alone are measured once per K")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--budget-us", type=float, default=0,
+                    help="the GPU node's latency budget (gpu_fwd4_set_latency_budget): batches sized so that their "
+                         "oldest packet comes back within it; --batch is then the largest batch")
     ap.add_argument("--recycle", type=int, default=65536, help="mbufs per worker's pool (0: one per packet)")
     ap.add_argument("--passes", type=int, default=8, help="with --recycle: passes over each worker's share")
     ap.add_argument("--lcores", default="spread", choices=["none", "allowed", "spread", "socket"])
@@ -148,7 +151,9 @@ def main():
                             ("gh_workers_run", ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(ctypes.c_double),
                                                               ctypes.POINTER(ctypes.c_uint64)]),
                             ("gh_set_rx_touch", None, [ctypes.c_int]), ("gh_set_null_node", None, [ctypes.c_int]),
-                            ("gh_set_recycle", None, [ctypes.c_uint32, ctypes.c_uint32])]:
+                            ("gh_set_recycle", None, [ctypes.c_uint32, ctypes.c_uint32]),
+                            ("gh_walk_info_at", ctypes.c_int, [ctypes.c_int, ctypes.c_void_p]),
+                            ("gpu_fwd4_set_latency_budget", ctypes.c_int, [ctypes.c_uint64])]:
         f = getattr(L, name)
         f.restype, f.argtypes = res, argt
 
@@ -240,6 +245,7 @@ def main():
     out = open(args.out, "a") if args.out else None
     L.gpu_fwd4_set_batch.argtypes = [ctypes.c_uint32, ctypes.c_uint64]
     batches = [int(x) for x in args.batches.split(",")] if args.batches else [args.batch]
+    assert L.gpu_fwd4_set_latency_budget(int(args.budget_us * 1e3)) == 0
     for k, batch in [(k, b) for k in threads for b in batches]:
         assert L.gpu_fwd4_set_batch(batch, 20_000_000) == 0
         cpus = place(k)
@@ -254,12 +260,21 @@ def main():
                 t[mode].append(once(k, m, mode)[0])
         med = {mode: float(np.median(v)) for mode, v in t.items()}
         lat = {}
+        caps = {}
         for mode in gmodes + ("chain",):
             _, (hist, cpn) = once(k, m, mode, lat=True)
             assert int(hist.sum()) == pk, (mode, int(hist.sum()), pk)
             lat[mode] = percentiles(hist.astype(np.float64), cpn, floor)
+            if mode != "chain" and args.budget_us:  # each worker graph's batch cap where the run left it
+                wi = np.zeros(1, dtype=G.WALK_INFO_DT)
+                cs = []
+                for g in range(k):
+                    assert L.gh_walk_info_at(g, wi.ctypes.data) == 0
+                    cs.append(int(wi[0]["batch_cap"]))
+                caps[mode] = cs
         line = {"threads": k, "packets": pk, "lcores": args.lcores, "cpus": cpus, "recycle": args.recycle,
                 "passes": per, "batch": batch, "reps": args.reps, "tune": args.tune, "alt": args.alt,
+                **({"budget_us": args.budget_us, "batch_caps": caps} if args.budget_us else {}),
                 "workload": "config3 full view (fib_inject 1M routes), 64 B, seeded stream 0x67720002"}
         for mode in gmodes + ("chain",):
             line[mode] = {"mpps": round(pk / med[mode] / 1e6, 1),

@@ -944,6 +944,13 @@ int gh_walk_info(struct gpu_fwd4_walk_info *info) {
 	return g ? gpu_fwd4_walk_info(g, info) : -ENOENT;
 }
 
+// The same for graph slot k (workers mode: worker k's graph).
+int gh_walk_info_at(int k, struct gpu_fwd4_walk_info *info) {
+	if (k < 0 || k >= GH_MAX_GRAPHS || H.graphs[k].graph == NULL)
+		return -ENOENT;
+	return gpu_fwd4_walk_info(H.graphs[k].graph, info);
+}
+
 // ---- RCU: grout deletes an object a batch on the GPU names -----------------
 struct gh_rcu_result {
 	uint32_t sync_before_handback; // synchronize had returned before the hand-back

@@ -100,8 +100,9 @@ def lib():
 
 WALK_INFO_DT = np.dtype([("held", "<u4"), ("in_flight", "<u4"), ("batches", "<u8"), ("max_batch", "<u8"),
                          ("stale", "<u8"), ("readers_online", "<u4"), ("diverged", "<i4"), ("append_errors", "<u8"),
-                         ("handed", "<u8"), ("drain_punted", "<u8"), ("stranded", "<u8")])
-assert WALK_INFO_DT.itemsize == 72
+                         ("handed", "<u8"), ("drain_punted", "<u8"), ("stranded", "<u8"), ("batch_cap", "<u4"),
+                         ("lat_ns", "<u8"), ("over_budget", "<u8")], align=True)
+assert WALK_INFO_DT.itemsize == 96
 LOOP_RES_DT = np.dtype([("walks", "<u4"), ("windows", "<u4"), ("sleeps", "<u4"), ("sleeps_held", "<u4"),
                         ("busy_held", "<u4"), ("blocked", "<u4"), ("recorded_at_block", "<u4"),
                         ("held_at_block", "<u8"), ("readers_online_at_block", "<u4"), ("sync_returned", "<u4"),
@@ -111,8 +112,9 @@ RCU_RES_DT = np.dtype([("sync_before_handback", "<u4"), ("recorded_at_sync", "<u
                        ("sync_done", "<u4")])
 assert RCU_RES_DT.itemsize == 40
 CONF_DT = np.dtype([("n_devs", "<u4"), ("devs", "<i4", (16,)), ("max_ifaces", "<u4"), ("max_nexthops", "<u4"),
-                    ("batch", "<u4"), ("rx_burst", "<u4"), ("max_delay_ns", "<u8"), ("depth", "<u4")], align=True)
-assert CONF_DT.itemsize == 104
+                    ("batch", "<u4"), ("rx_burst", "<u4"), ("max_delay_ns", "<u8"), ("depth", "<u4"),
+                    ("launch_per_batch", "<u4"), ("latency_budget_ns", "<u8")], align=True)
+assert CONF_DT.itemsize == 112
 BATCH_MAX = 15360  # GPU_FWD4_BATCH_MAX (gpu_fwd4_node.h)
 
 
@@ -1180,3 +1182,28 @@ def test_idle_loop_micro_sleep(ignore_holding):
         assert r["readers_online_at_block"] == 0, r
         got = _results(n)
         assert np.array_equal(got["edge"], want["edge"])
+
+
+@pytest.mark.gpu
+def test_latency_budget_sizes_batches():
+    """gpu_fwd4_set_latency_budget: under a 100 us budget the graph's batches
+    are sized by what their oldest packets took (arrival to hand-back), not by
+    the 15360 of gpu_fwd4_set_batch: the cap stays within a few thousand
+    packets, and the walk is bit-exact with the oracle as ever."""
+    L = lib()
+    L.gpu_fwd4_set_latency_budget.argtypes = [ctypes.c_uint64]
+    fp = graph_ctx()
+    t = T.config_single_route()
+    fr, me = S.stream(8 * BATCH_MAX, 0x1A7B, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    assert L.gpu_fwd4_set_batch(BATCH_MAX, 20_000_000) == 0
+    assert L.gpu_fwd4_set_latency_budget(100_000) == 0
+    try:
+        i0 = walk_info()
+        check_walk(t, fr, me)
+        i1 = walk_info()
+    finally:
+        assert L.gpu_fwd4_set_latency_budget(0) == 0
+        _restore_batch()
+    assert 64 <= i1["batch_cap"] <= 4096, i1
+    assert i1["max_batch"] <= 4096 + BURST or i1["batches"] - i0["batches"] >= len(me) // 4096, i1
+    assert 0 < i1["lat_ns"], i1
