@@ -291,10 +291,13 @@ def test_resident_split_knobs(knobs, wgs, tiles, split, budget):
 def test_resident_rings_run_out(knobs):
     """A queue takes its rings on its first batch, as many as "resident_wgs"
     says then: groups of different sizes side by side (a group is taken only
-    whole and free); once no group of the current size is free, a queue's
+    whole and free), and only while the device's CUs can hold every ring that
+    queues of any context hold at once ("resident_cap", "resident_held": the
+    graph-walk tests' module contexts on the same GPU hold some). Once no
+    group of the current size is free, or the device is full, a queue's
     batches get a launch each (its kernel counters show it), and a queue
-    closed hands its rings back. Every walk, on every queue, sequential or
-    all queues in flight at once, is the oracle's."""
+    closed hands its rings back. Every walk, on every queue, sequential or all
+    queues in flight at once, is the oracle's."""
     from golden_util import fresh_fastpath_state
     fp = knobs
     topo = T.config_fullview(count=50_000)
@@ -314,16 +317,43 @@ def test_resident_rings_run_out(knobs):
     rings = fp.tune("resident_ring_count")
     assert rings >= 32 and rings % 8 == 0
     g8 = (rings - 24) // 8
+    # the library's rule, simulated: first free aligned group of w in this
+    # context, and the device's held rings + w within its cap
+    taken = [False] * rings
+    sim = {"held": None, "cap": None}
+
+    def take(w):
+        if sim["held"] + w > sim["cap"]:
+            return -1
+        for r in range(0, rings - w + 1, w):
+            if not any(taken[r:r + w]):
+                taken[r:r + w] = [True] * w
+                sim["held"] += w
+                return r
+        return -1
+
     try:
         # of R rings: 0-3 (groups of 4), 8-15 (of 8: 0-7 is not free), 18-20
         # (of 3: 3-5, 6-8, 9-11, 12-14 and 15-17 are not), then 24-31, 32-39,
         # ..., R-8 - R-1 ((R - 24) / 8 groups of 8); 3 more queues find none
+        # (fewer get rings when the device holds others' already)
+        got_ring = []
         for i, w in enumerate([4, 8, 3] + [8] * (g8 + 3)):
             assert fp.tune("resident_wgs", w) == 0
+            if i == 0:
+                held0 = fp.tune("resident_held")
             qs.append(fp.queue())
             walk(qs[i], parts[i])
+            if i == 0:  # the rings are set up by now
+                sim["cap"] = fp.tune("resident_cap")
+                sim["held"] = held0
+                assert sim["cap"] > 0 and held0 + 4 <= sim["cap"], (held0, sim)
+            got_ring.append(take(w))
+        assert fp.tune("resident_held") == sim["held"], sim
         launched = [i for i, q in enumerate(qs) if q.stats()["rx_packets"].any()]
-        assert launched == [3 + g8, 4 + g8, 5 + g8]
+        assert launched == [i for i, r in enumerate(got_ring) if r < 0], (launched, got_ring, sim)
+        if held0 == 0:  # the device to itself: the layout of the comment above
+            assert launched == [3 + g8, 4 + g8, 5 + g8]
         nq = len(qs)
         for i, q in enumerate(qs):  # every queue in flight at once
             q.node_start(parts[nq + i])
@@ -334,11 +364,17 @@ def test_resident_rings_run_out(knobs):
         assert fp.tune("resident_busy") == 0
         assert all(qs[i].stats()["rx_packets"].sum() == 2 * per for i in launched)
         # rings 0-3 handed back: with 4-7, never taken, a group of 8 again
+        # (if the device has room for 8 more)
         qs[0].close()
+        taken[0:4] = [False] * 4
+        sim["held"] -= 4
         qs[0] = fp.queue()
         x = 2 * nq
         walk(qs[0], parts[x])
-        assert not qs[0].stats()["rx_packets"].any()
+        r0 = take(8)
+        assert bool(qs[0].stats()["rx_packets"].any()) == (r0 < 0), (r0, sim)
+        if sim["held"] - 8 + 8 <= sim["cap"] and r0 >= 0:
+            assert r0 == 0
         compare_mbufs(parts[x], want[per * x:per * (x + 1)], bufs[per * x:per * (x + 1)], lines[per * x:per * (x + 1)])
     finally:
         for q in qs:
