@@ -153,6 +153,7 @@ def main():
                             ("gh_set_rx_touch", None, [ctypes.c_int]), ("gh_set_null_node", None, [ctypes.c_int]),
                             ("gh_set_recycle", None, [ctypes.c_uint32, ctypes.c_uint32]),
                             ("gh_walk_info_at", ctypes.c_int, [ctypes.c_int, ctypes.c_void_p]),
+                            ("gh_node_stats_at", ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
                             ("gpu_fwd4_set_latency_budget", ctypes.c_int, [ctypes.c_uint64])]:
         f = getattr(L, name)
         f.restype, f.argtypes = res, argt
@@ -260,21 +261,28 @@ def main():
                 t[mode].append(once(k, m, mode)[0])
         med = {mode: float(np.median(v)) for mode, v in t.items()}
         lat = {}
-        caps = {}
+        caps, health = {}, {}
         for mode in gmodes + ("chain",):
             _, (hist, cpn) = once(k, m, mode, lat=True)
             assert int(hist.sum()) == pk, (mode, int(hist.sum()), pk)
             lat[mode] = percentiles(hist.astype(np.float64), cpn, floor)
-            if mode != "chain" and args.budget_us:  # each worker graph's batch cap where the run left it
+            if mode != "chain":  # each worker graph's batch cap where the run left it, and what went wrong
                 wi = np.zeros(1, dtype=G.WALK_INFO_DT)
-                cs = []
+                cs, over, errs = [], 0, 0
                 for g in range(k):
                     assert L.gh_walk_info_at(g, wi.ctypes.data) == 0
                     cs.append(int(wi[0]["batch_cap"]))
+                    over += int(wi[0]["over_budget"])
+                    e = ctypes.c_uint64()
+                    assert L.gh_node_stats_at(g, None, ctypes.byref(e)) == 0
+                    errs += e.value
                 caps[mode] = cs
+                health[mode] = {"over_budget_batches": over, "gpu_errors": errs,
+                                "resident_cancels": abi.hip().gr_hip_tune(L.gh_hip_ctx(), b"resident_cancels", 0)}
         line = {"threads": k, "packets": pk, "lcores": args.lcores, "cpus": cpus, "recycle": args.recycle,
                 "passes": per, "batch": batch, "reps": args.reps, "tune": args.tune, "alt": args.alt,
                 **({"budget_us": args.budget_us, "batch_caps": caps} if args.budget_us else {}),
+                "gpu_health": health,
                 "workload": "config3 full view (fib_inject 1M routes), 64 B, seeded stream 0x67720002"}
         for mode in gmodes + ("chain",):
             line[mode] = {"mpps": round(pk / med[mode] / 1e6, 1),

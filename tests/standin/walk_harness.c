@@ -944,6 +944,13 @@ int gh_walk_info(struct gpu_fwd4_walk_info *info) {
 	return g ? gpu_fwd4_walk_info(g, info) : -ENOENT;
 }
 
+// gpu_fwd4_node_stats of graph slot k.
+int gh_node_stats_at(int k, struct gr_hip_node_stats *stats, uint64_t *gpu_errors) {
+	if (k < 0 || k >= GH_MAX_GRAPHS || H.graphs[k].graph == NULL)
+		return -ENOENT;
+	return gpu_fwd4_node_stats(H.graphs[k].graph, stats, gpu_errors);
+}
+
 // The same for graph slot k (workers mode: worker k's graph).
 int gh_walk_info_at(int k, struct gpu_fwd4_walk_info *info) {
 	if (k < 0 || k >= GH_MAX_GRAPHS || H.graphs[k].graph == NULL)
