@@ -989,7 +989,9 @@ static uint16_t gpu_flush_process(struct rte_graph *graph, struct rte_node *node
 	// (flush() hands back the one still pending, and none is after these)
 	const uint64_t t = now_ns();
 	uint32_t n = 0;
-	if (w->pending && (w->draining || t - w->pend_ns >= hold_max(w)))
+	// (conf's delay, also under a latency budget: the batch on the GPU is
+	// reaped as soon as it is back, and a wait here would stall RX)
+	if (w->pending && (w->draining || t - w->pend_ns >= conf.max_delay_ns))
 		n = finish_pending(graph, node, w); // waited long enough (or leaving the graph): wait for the GPU
 	else
 		n = reap(graph, node, w);
