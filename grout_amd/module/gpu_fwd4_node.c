@@ -343,6 +343,7 @@ struct gpu_walk {
 	// arrival of the oldest packet of the batch on the GPU, and what the
 	// batches' oldest packets took, arrival to hand-back (a moving average)
 	uint32_t lcap;
+	uint64_t rtt_ns; // the batches' round trips, send to back (a moving average of those sampled)
 	uint64_t pend_first_ns;
 	uint64_t lat_ns;
 	uint64_t over_budget;
@@ -547,17 +548,22 @@ static void poll_until_ready(struct gpu_walk *w) {
 	if (!w->pending)
 		return;
 	PROF_T0();
-	for (int ready = 0; !ready;)
+	int polls = 0;
+	for (int ready = 0; !ready; polls++)
 		if (gr_hip_node_pending(w->q, &ready) <= 0) // an error, or nothing in flight after all
 			break;
 	PROF_ADD(GPU_FWD4_PROF_POLL);
 	const uint64_t waited = now_ns() - w->pend_ns;
 	w->gpu_ns = w->gpu_ns ? (w->gpu_ns * 7 + waited) / 8 : waited;
+	if (polls > 1) // it came back just now: its round trip (else it was back before: no sample)
+		w->rtt_ns = w->rtt_ns ? (w->rtt_ns * 7 + waited) / 8 : waited;
 }
 
 // What the batch accumulating may hold, and how long its oldest packet may
 // wait before it is sent: conf's, or under a latency budget the graph's cap
-// and the budget less the GPU's round trip (a quarter of the budget at least).
+// and the budget less the GPU's round trip (a quarter of the budget at least;
+// the round trip sampled when a batch comes back while polled, not when the
+// next batch's fill outlasted it).
 static uint32_t batch_cap(struct gpu_walk *w) {
 	if (conf.latency_budget_ns == 0)
 		return conf.batch;
@@ -570,26 +576,28 @@ static uint64_t hold_max(const struct gpu_walk *w) {
 	const uint64_t b = conf.latency_budget_ns;
 	if (b == 0)
 		return conf.max_delay_ns;
-	const uint64_t h = w->gpu_ns + b / 4 < b ? b - w->gpu_ns : b / 4;
+	const uint64_t h = w->rtt_ns + b / 4 < b ? b - w->rtt_ns : b / 4;
 	return h < conf.max_delay_ns ? h : conf.max_delay_ns;
 }
 
 // A batch came back: its oldest packet took `lat` from its arrival. Under a
-// budget the cap shrinks by a quarter past it, and grows by an eighth (64 at
-// least) while full batches come back within 3/5 of it.
+// budget the cap follows the moving average of those times: down by an eighth
+// while it is above 4/5 of the budget, up by an eighth (64 at least) while it
+// is below 11/20 and full batches come back. One late batch (a host stall,
+// another worker's burst on the GPU) moves it little: every worker keeps
+// batches of about the same size, and the slowest one sets the pace.
 static void budget_update(struct gpu_walk *w, uint64_t lat, uint32_t n) {
 	w->lat_ns = w->lat_ns ? (w->lat_ns * 7 + lat) / 8 : lat;
 	const uint64_t b = conf.latency_budget_ns;
 	if (b == 0)
 		return;
-	const uint32_t cap = batch_cap(w);
-	if (lat > b) {
+	if (lat > b)
 		w->over_budget++;
-		w->lcap = cap - cap / 4 > 64 ? cap - cap / 4 : 64;
-	} else if (lat * 5 < b * 3 && n >= cap - cap / 8) {
-		const uint32_t up = cap / 8 > 64 ? cap / 8 : 64;
-		w->lcap = cap + up < conf.batch ? cap + up : conf.batch;
-	}
+	const uint32_t cap = batch_cap(w), step = cap / 8 > 64 ? cap / 8 : 64;
+	if (w->lat_ns * 5 > b * 4)
+		w->lcap = cap > step + 64 ? cap - step : 64;
+	else if (w->lat_ns * 20 < b * 11 && n >= cap - cap / 8)
+		w->lcap = cap + step < conf.batch ? cap + step : conf.batch;
 }
 
 // Wait for the batch on the GPU and hand it back. Returns its size. The
@@ -701,6 +709,7 @@ static uint32_t reap(struct rte_graph *graph, struct rte_node *node, struct gpu_
 	if (!ready)
 		return 0;
 	w->gpu_ns = w->gpu_ns ? (w->gpu_ns * 7 + waited) / 8 : waited; // an upper bound: polled late
+	w->rtt_ns = w->rtt_ns ? (w->rtt_ns * 7 + waited) / 8 : waited;
 	return finish_pending(graph, node, w);
 }
 

@@ -107,10 +107,11 @@ struct gpu_fwd4_conf {
 	// 0 (the default): batches of `batch` packets, held `max_delay_ns` at
 	// most. Otherwise a latency budget for a packet from its arrival at the
 	// node to its hand-back onto its edge: each graph sizes its batches so
-	// that its batches' oldest packets come back within it (a batch cap
-	// shrunk by a quarter when one does not, grown by an eighth while they
-	// come back within 3/5 of it), and holds a packet at most the budget
-	// less the GPU's measured round trip (a quarter of it at least)
+	// that its batches' oldest packets come back within it (a batch cap that
+	// follows the moving average of those times: an eighth down while it is
+	// above 4/5 of the budget, an eighth up while below 11/20 of it), and
+	// holds a packet at most the budget less the GPU's measured round trip
+	// (a quarter of the budget at least)
 	uint64_t latency_budget_ns;
 };
 
