@@ -413,7 +413,10 @@ struct gr_hip_ctx {
 	std::mutex res_mu;
 	uint32_t res_wait_ms = 500; // a resident batch not done after this is cancelled (knob "resident_wait_ms")
 	uint32_t res_cap = 0; // rings this device can hold co-resident (res_setup; device-wide, g_res_held)
-	uint32_t res_reserve_cu = 0; // CUs left to other kernels (knob "resident_reserve_cu")
+	// CUs no ring may take (knob "resident_reserve_cu"): a queue that finds no
+	// ring launches per batch, and its launches need CUs the resident kernel
+	// does not hold for its lifetime after the last batch
+	uint32_t res_reserve_cu = 16;
 	uint32_t res_held = 0; // rings this context's queues hold (counted in g_res_held)
 	bool res_dead = false; // a launch that would not leave: no resident batch any more, its words never freed
 	bool res_hold = false; // tests: no (re)launch while set (a kernel that stopped serving its rings)

@@ -520,6 +520,21 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //   "resident_ms" the kernel leaves once no ring has finished a batch for this
 //               long; the next batch launches it again (default 50)
 //   "resident_launches" (read) resident launches so far
+//   "resident_wait_ms" a resident batch not done this long after its post
+//               (default 500) is cancelled: the kernel is stopped, what it did
+//               not start is retired and handed back as not reached (the node
+//               punts it); a kernel that does not leave makes the context's
+//               resident path dead (-EDEADLK, nothing of the batch reused)
+//   "resident_reserve_cu" CUs no ring may take (default 16; before the first
+//               resident batch): a queue finds rings only while every ring
+//               held on the device, over all contexts, fits the other CUs at
+//               the kernel's occupancy, else it launches per batch
+//   "resident_cap" / "resident_held" (read) those rings: the device's cap,
+//               and what the queues of every context hold
+//   "resident_cancels" (read) batches cancelled past their deadline
+//   "resident_dead" (read) 1 once a kernel would not leave
+//   "resident_hold" tests: 1 = the kernel leaves and is not launched again
+//               (its batches reach their deadline), 0 = back to normal
 //   "stage_min_tiles" the fast adjacencies (and IPv6 first-level slice) are
 //               staged in each workgroup's LDS only when the launch gives every
 //               workgroup at least this many 64-packet tiles (default 4);
