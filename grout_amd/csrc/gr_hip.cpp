@@ -3239,6 +3239,8 @@ static node_slot &open_slot(gr_hip_queue_t *q) {
 extern "C" int gr_hip_node_append(gr_hip_queue_t *q, const struct gr_hip_mbuf *m, uint32_t n, uint32_t burst) {
 	if (q == nullptr || (n && m == nullptr))
 		return -EINVAL;
+	if (q->dead)
+		return -EIO; // (res_cancel) its slots may still be written by the GPU
 	if (q->nw_count == GR_HIP_NODE_DEPTH)
 		return -EBUSY;
 	node_slot &w = open_slot(q);
@@ -3282,6 +3284,8 @@ extern "C" int gr_hip_node_append_mbufs(gr_hip_queue_t *q, void *const *mbufs, u
 					const struct gr_hip_mbuf_layout *lay, uint32_t burst) {
 	if (q == nullptr || lay == nullptr || (n && mbufs == nullptr))
 		return -EINVAL;
+	if (q->dead)
+		return -EIO; // (res_cancel) its slots may still be written by the GPU
 	if (q->nw_count == GR_HIP_NODE_DEPTH)
 		return -EBUSY;
 	node_slot &w = open_slot(q);
