@@ -420,6 +420,7 @@ struct gr_hip_ctx {
 	uint32_t res_held = 0; // rings this context's queues hold (counted in g_res_held)
 	bool res_dead = false; // a launch that would not leave: no resident batch any more, its words never freed
 	bool res_hold = false; // tests: no (re)launch while set (a kernel that stopped serving its rings)
+	bool res_leave_fail = false; // tests: res_leave reports a launch that would not leave
 	std::atomic<uint32_t> res_cancels{0}; // batches res_cancel retired unrun (knob read "resident_cancels")
 	// FIB publication (see retire_wait): two pinned staging buffers used in
 	// turn by the commits (fib_mu), each with the event of its last upload,
@@ -2285,6 +2286,8 @@ static uint64_t res_word(const uint64_t *w, int ring) {
 // 0: gone (or faulted: it touches nothing more); -EDEADLK: still running
 // past RES_LEAVE_NS (a workgroup no CU runs, or one that does not return).
 static int res_leave(gr_hip_ctx *c) {
+	if (c->res_leave_fail) // tests: as if a workgroup never left (the kernel itself is stopped by "resident_hold")
+		return -EDEADLK;
 	if (!c->res_live)
 		return 0;
 	__atomic_store_n(c->res_stop, 1u, __ATOMIC_RELEASE);
@@ -2724,6 +2727,8 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		c->res_hold = value != 0;
 		if (c->res_hold && c->res_live)
 			__atomic_store_n(c->res_stop, 1u, __ATOMIC_RELEASE);
+	} else if (strcmp(key, "resident_leave_fail") == 0) { // tests: the -EDEADLK path (with "resident_hold")
+		c->res_leave_fail = value != 0;
 	} else if (strcmp(key, "resident_ms") == 0) {
 		if (value < 1 || value > 10000)
 			return -EINVAL;

@@ -429,3 +429,58 @@ def test_resident_lifetime_is_idleness(resident):
     finally:
         q1.close()
         q2.close()
+
+
+@pytest.mark.gpu
+def test_resident_deadline_and_dead_context():
+    """The library's side of a resident batch past its deadline, on a context
+    of its own. With the kernel stopped ("resident_hold") the walk's finish
+    returns after "resident_wait_ms" with every packet not reached handed back
+    as PUNT, its frame untouched (the batch's descriptors retired: nothing
+    runs it later), counted in "resident_cancels"; released, the same queue
+    forwards as the oracle's again. When the kernel would not even leave
+    ("resident_leave_fail" stands for a workgroup no CU runs), the finish
+    returns -EDEADLK without handing the walk back, the queue refuses every
+    later walk (-EIO) and the context reports its resident path dead."""
+    import errno
+    from golden_util import fresh_fastpath_state
+    from grout_amd.fwd import FastPath
+    topo = T.config_fullview(count=50_000)
+    fr, me = S.stream(4096, 0xDEAD, routes=topo.route_array())
+    lines, v, st, want, _ = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
+    fp = FastPath(0)
+    try:
+        fresh_fastpath_state(fp, topo, {})
+        assert fp.tune("resident", 1) == 0 and fp.tune("resident_wait_ms", 100) == 0
+        q = fp.queue()
+        bufs, m = mbufs_for(fr, me)
+        q.node_start(m)
+        q.node_finish()  # the queue takes its rings, the kernel runs
+        compare_mbufs(m, want, bufs, lines)
+        fp.tune("resident_hold", 1)
+        bufs, m = mbufs_for(fr, me)
+        t0 = time.perf_counter()
+        q.node_start(m)
+        got, _ = q.node_finish()
+        dt = time.perf_counter() - t0
+        assert 0.09 <= dt < 2.0, dt
+        assert q.unfinished == len(m)  # every packet: the kernel never started the batch
+        assert (m["edge"] == abi.EDGE["punt"]).all() and (m["data_off"] == 128).all()
+        assert np.array_equal(bufs[:, :abi.LINE], fr[:, :abi.LINE])  # frames untouched
+        assert fp.tune("resident_cancels") == 1 and fp.tune("resident_dead") == 0
+        fp.tune("resident_hold", 0)
+        bufs, m = mbufs_for(fr, me)
+        q.node_start(m)
+        q.node_finish()
+        compare_mbufs(m, want, bufs, lines)
+        # the kernel would not leave
+        fp.tune("resident_hold", 1)
+        fp.tune("resident_leave_fail", 1)
+        bufs, m = mbufs_for(fr, me)
+        q.node_start(m)
+        r = fp.lib.gr_hip_node_finish(q._h, None, None, None)
+        assert r == -errno.EDEADLK, r
+        assert fp.tune("resident_dead") == 1
+        assert fp.lib.gr_hip_node_start(q._h, m.ctypes.data, len(m), 64) == -errno.EIO
+    finally:
+        fp.close()  # (the kernel has left: "resident_hold"; its rings are leaked, as for a real one)
