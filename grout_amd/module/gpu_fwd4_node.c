@@ -582,8 +582,8 @@ static uint64_t hold_max(const struct gpu_walk *w) {
 
 // A batch came back: its oldest packet took `lat` from its arrival. Under a
 // budget the cap follows the moving average of those times: down by an eighth
-// while it is above 4/5 of the budget, up by an eighth (64 at least) while it
-// is below 11/20 and full batches come back. One late batch (a host stall,
+// while it is above 17/20 of the budget, up by an eighth (64 at least) while it
+// is below 13/20 and full batches come back. One late batch (a host stall,
 // another worker's burst on the GPU) moves it little: every worker keeps
 // batches of about the same size, and the slowest one sets the pace.
 static void budget_update(struct gpu_walk *w, uint64_t lat, uint32_t n) {
@@ -594,9 +594,9 @@ static void budget_update(struct gpu_walk *w, uint64_t lat, uint32_t n) {
 	if (lat > b)
 		w->over_budget++;
 	const uint32_t cap = batch_cap(w), step = cap / 8 > 64 ? cap / 8 : 64;
-	if (w->lat_ns * 5 > b * 4)
+	if (w->lat_ns * 20 > b * 17)
 		w->lcap = cap > step + 64 ? cap - step : 64;
-	else if (w->lat_ns * 20 < b * 11 && n >= cap - cap / 8)
+	else if (w->lat_ns * 20 < b * 13 && n >= cap - cap / 8)
 		w->lcap = cap + step < conf.batch ? cap + step : conf.batch;
 }
 

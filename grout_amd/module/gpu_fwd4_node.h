@@ -109,7 +109,7 @@ struct gpu_fwd4_conf {
 	// node to its hand-back onto its edge: each graph sizes its batches so
 	// that its batches' oldest packets come back within it (a batch cap that
 	// follows the moving average of those times: an eighth down while it is
-	// above 4/5 of the budget, an eighth up while below 11/20 of it), and
+	// above 17/20 of the budget, an eighth up while below 13/20 of it), and
 	// holds a packet at most the budget less the GPU's measured round trip
 	// (a quarter of the budget at least)
 	uint64_t latency_budget_ns;
