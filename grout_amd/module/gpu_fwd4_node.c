@@ -939,14 +939,20 @@ static void gpu_fwd4_fini(const struct rte_graph *graph, struct rte_node *node) 
 		// dropped from the queue only once the GPU is done with its frames
 		// (gr_hip_node_finish waits before it refuses a batch appended from
 		// the mbufs)
-		if (w->pending)
-			gr_hip_node_finish(w->q, NULL, NULL, NULL);
-		if (w->pending)
+		// (a GPU that would not let go of it, -EDEADLK: its mbufs stay
+		// stranded, never freed, since the GPU may still write their frames)
+		const int fr = w->pending ? gr_hip_node_finish(w->q, NULL, NULL, NULL) : 0;
+		uint64_t freed = w->n;
+		if (w->pending && fr != -EDEADLK) {
 			for (uint32_t j = 0; j < w->pend_n; j++)
 				rte_pktmbuf_free(w->mbufs[w->cur ^ 1][j]);
+			freed += w->pend_n;
+		} else if (w->pending) {
+			w->stranded += w->pend_n;
+		}
 		for (uint32_t j = 0; j < w->n; j++) // held, never sent
 			rte_pktmbuf_free(w->mbufs[w->cur][j]);
-		__atomic_fetch_add(&fini_freed, w->n + (w->pending ? w->pend_n : 0), __ATOMIC_RELAXED);
+		__atomic_fetch_add(&fini_freed, freed, __ATOMIC_RELAXED);
 		gr_hip_queue_destroy(w->q);
 		for (int k = 0; k < GPU_FWD4_RCU_PER_GRAPH; k++) { // offline, then gone (rte_rcu_qsbr.h)
 			if (w->rstate[k] != RD_FREE)
