@@ -57,7 +57,9 @@ typedef ring_cfg<16, 2, 2, 16, 8> ring_cfg8;
 typedef ring_cfg<14, 1, 1, 8, 8> ring_cfg9;
 typedef ring_cfg<14, 2, 2, 8, 4> ring_cfg10;
 typedef ring_cfg<12, 1, 1, 8, 8> ring_cfg11;
-#define RING_NCFG 12
+// geometry 2 with lanes [0, SG) of each FIB gather through the scalar cache
+// (fib_tbl24_split): 12, 13, 14 = SG 16, 32, 64
+#define RING_NCFG 15
 
 template <class C, bool PTRS>
 struct ring_lds {
@@ -298,7 +300,48 @@ __device__ void ring_storer(const fwd4_params &A, LT &L, uint32_t n_local, uint3
 	}
 }
 
-template <class C, bool STATS, bool PTRS, class LT>
+// The tbl24 gather of a wave's IPv4 lanes (chain_fib's first load, 4-byte
+// DIR24_8 of one VRF), SG of them through the scalar cache. A vector gather
+// of 64 unrelated destinations is 64 L1 tag lookups and translations, and the
+// addresser stalls on the L1's translations in flight (DESIGN.md §6.1:
+// TCP_UTCL1_STALL_INFLIGHT_MAX); lanes [0, SG) go through the scalar cache
+// instead, which has its own translation path: one readlane and one scalar
+// load per lane, all issued before the vector gather of the other lanes and
+// waited for together. Wave-uniform control flow only. Returns true for the
+// lanes whose entry is in `ent` (the others call chain_fib). The scalar cache
+// is not invalidated by anything but a launch, so only gr_fwd4_ring uses this
+// (the resident kernel sees FIB updates between its batches).
+template <int SG>
+__device__ __forceinline__ bool fib_tbl24_split(const rxv &rx, uint32_t dst, bool want, uint32_t lane, uint32_t &ent) {
+	want = want && rx.tbl24 != nullptr && (rx.flags & (FWD4_RX_FIB16 | FWD4_RX_FIB24W2)) == 0;
+	const uint64_t wm = __ballot(want);
+	if (wm == 0)
+		return false;
+	const uint32_t f = (uint32_t)__builtin_ctzll(wm);
+	const uint64_t tb = reinterpret_cast<uint64_t>(rx.tbl24);
+	const uint32_t blo = __builtin_amdgcn_readlane((uint32_t)tb, f);
+	const uint32_t bhi = __builtin_amdgcn_readlane((uint32_t)(tb >> 32), f);
+	want = want && (uint32_t)tb == blo && (uint32_t)(tb >> 32) == bhi; // the first lane's VRF
+	const uint32_t idx = want ? __builtin_bswap32(dst) >> 8 : 0; // entry 0 for the others: a harmless read
+	const __attribute__((address_space(4))) uint32_t *base =
+		(const __attribute__((address_space(4))) uint32_t *)(((uint64_t)bhi << 32) | blo);
+	uint32_t sv[SG];
+#pragma unroll
+	for (int i = 0; i < SG; i++)
+		sv[i] = base[(uint32_t)__builtin_amdgcn_readlane(idx, i)];
+	uint32_t v = 0, w = 0;
+	if (want && lane >= (uint32_t)SG)
+		v = gld(rx.tbl24 + idx);
+	// into their own register, so that waiting for the scalar loads does not
+	// wait for the vector gather too
+#pragma unroll
+	for (int i = 0; i < SG; i++)
+		asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(w) : "s"(sv[i]), "i"(i));
+	ent = lane < (uint32_t)SG ? w : v;
+	return want;
+}
+
+template <class C, bool STATS, bool PTRS, int SG = 0, class LT>
 __device__ void ring_compute(const fwd4_params &A, const kctx &P, LT &L, stat_slot *slots,
 			     const uint4 *nhf_lds, uint32_t n_local, uint32_t c, uint32_t lane) {
 	for (uint32_t k = c; k < n_local; k += C::COMPUTE) {
@@ -326,14 +369,28 @@ __device__ void ring_compute(const fwd4_params &A, const kctx &P, LT &L, stat_sl
 
 		result r = {GR_HIP_E_PUNT, 0, m.iface, 0, 0, 0, 0, 0};
 		uint32_t fam = 0; // the packet entered ip_input (1) / ip6_input (2)
+		uint32_t dst = 0, data_len = 0;
+		int head = HEAD_DONE;
 		if (live) {
-			uint32_t dst = 0, data_len = 0;
 			const uint8_t *frame = PTRS ? reinterpret_cast<const uint8_t *>(L.ptrs[s][lane])
 						    : A.in + (size_t)(base + lane) * A.in_stride;
-			const int head = chain_head(P, R, lane, m, rx, r, dst, data_len, frame);
+			head = chain_head(P, R, lane, m, rx, r, dst, data_len, frame);
 			fam = head == HEAD_IN4 || head == HEAD_IP4 ? 1 : head == HEAD_IP6 ? 2 : 0;
+		}
+		uint32_t ent = 0;
+		bool got = false;
+		if constexpr (SG > 0)
+			got = fib_tbl24_split<SG>(rx, dst, head == HEAD_IP4, lane, ent);
+		if (live) {
 			if (head == HEAD_IP4) {
-				const uint32_t slot = chain_fib(rx, dst);
+				uint32_t slot;
+				if (got) { // chain_fib's tbl8 step
+					slot = ent;
+					if (ent & 0x80000000u)
+						slot = gld(rx.tbl8 + (size_t)(ent & 0x7fffffffu) * 256 + (__builtin_bswap32(dst) & 0xff));
+				} else {
+					slot = chain_fib(rx, dst);
+				}
 				if (slot == 0 || slot > P.max_nh) {
 					r.edge = GR_HIP_E_IP_ERROR_DEST_UNREACH; // NO_ROUTE :150-153
 				} else {
@@ -385,7 +442,7 @@ extern "C" int gr_fwd4_ring_trace(uint64_t *out, uint32_t n) {
 }
 #endif
 
-template <class C, bool STATS, bool NT, bool PTRS = false>
+template <class C, bool STATS, bool NT, bool PTRS = false, int SG = 0>
 __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params A) {
 #ifdef RING_TRACE
 	if (threadIdx.x == 0 && blockIdx.x < RING_TRACE_MAX)
@@ -440,7 +497,7 @@ __global__ void __launch_bounds__(C::WAVES * 64) gr_fwd4_ring(const fwd4_params 
 		P.top6 = A.top6;
 		P.top6_lds = (const __attribute__((address_space(3))) uint32_t *)(nhf_lds + A.nhf_lds + A.nhf6_lds);
 		P.top6_n = A.top6_lds;
-		ring_compute<C, STATS, PTRS>(A, P, L, slots, nhf_lds, n_local, wv - C::LOADERS - C::STORERS, lane);
+		ring_compute<C, STATS, PTRS, SG>(A, P, L, slots, nhf_lds, n_local, wv - C::LOADERS - C::STORERS, lane);
 	}
 
 	__syncthreads(); // every role has left its loop (each wait is bounded)
@@ -679,13 +736,15 @@ struct ring_entry {
 	fwd4_rfn fn[4]; // by FWD4_V_STATS | FWD4_V_NT
 	uint32_t threads;
 };
-#define RING_ENTRY(C) {{gr_fwd4_ring<C, false, false>, gr_fwd4_ring<C, true, false>, gr_fwd4_ring<C, false, true>, \
-			 gr_fwd4_ring<C, true, true>}, C::WAVES * 64}
+#define RING_ENTRY_SG(C, SG) {{gr_fwd4_ring<C, false, false, false, SG>, gr_fwd4_ring<C, true, false, false, SG>, \
+			 gr_fwd4_ring<C, false, true, false, SG>, gr_fwd4_ring<C, true, true, false, SG>}, C::WAVES * 64}
+#define RING_ENTRY(C) RING_ENTRY_SG(C, 0)
 static const ring_entry ring_kernels[RING_NCFG] = {
 	RING_ENTRY(ring_cfg0), RING_ENTRY(ring_cfg1), RING_ENTRY(ring_cfg2),
 	RING_ENTRY(ring_cfg3), RING_ENTRY(ring_cfg4), RING_ENTRY(ring_cfg5),
 	RING_ENTRY(ring_cfg6), RING_ENTRY(ring_cfg7), RING_ENTRY(ring_cfg8),
 	RING_ENTRY(ring_cfg9), RING_ENTRY(ring_cfg10), RING_ENTRY(ring_cfg11),
+	RING_ENTRY_SG(ring_cfg2, 16), RING_ENTRY_SG(ring_cfg2, 32), RING_ENTRY_SG(ring_cfg2, 64),
 };
 
 // Frame-pointer batches (GR_HIP_BATCH_F_FRAME_PTRS) run on geometry 2, the

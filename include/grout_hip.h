@@ -452,7 +452,10 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 
 // Tuning knobs, for measurements (A/B in one process). Keys:
 //   "ring"      geometry of the ring kernel (loaders / storers / slots /
-//               tiles in flight), 0..11; default 2
+//               tiles in flight), 0..11; default 2;
+//               12..14: geometry 2 with the 4-byte tbl24 gathers of 16 / 32
+//               / 64 lanes through the scalar cache (measured slower,
+//               DESIGN.md §6.1)
 //   "stats"     1 = per-iface counters (default; grout always counts), 0 = off
 //   "nt"        1 = nontemporal loads / stores of the streamed data (default)
 //   "wg_per_cu" 0 = default grid (2 workgroups per CU, fewer if LDS

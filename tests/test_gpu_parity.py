@@ -575,11 +575,13 @@ def test_high_slots_fall_back_to_4byte_fib(fastpath):
     assert g[1]["nh"].min() >= first and g[1]["nh"].max() > (1 << 15)
 
 
-@pytest.mark.parametrize("cfg", range(12))
-def test_ring_geometries(fastpath, cfg):
+@pytest.mark.parametrize("cfg,fmt", [(c, 2) for c in range(12)] + [(c, f) for c in (12, 13, 14) for f in (0, 2, 1)])
+def test_ring_geometries(fastpath, cfg, fmt):
     """Every ring geometry (loaders / storers / slots / tiles in flight) of
     fwd4_ring.hip forwards bit-exact; wg_per_cu 1 makes each workgroup walk
-    its ring many times round."""
+    its ring many times round. Geometries 12-14 gather the 4-byte DIR24_8
+    entries of some lanes through the scalar cache (fib_tbl24_split): they
+    run in every FIB format, 4-byte first (the only one they split)."""
     t, _ = SC.corpus_topology()
     fr, me, lab = SC.corpus_arrays()
     tf = _fullview()
@@ -588,14 +590,18 @@ def test_ring_geometries(fastpath, cfg):
     o2 = oracle.Oracle(tf).process(fr2, me2)
     fastpath.tune("ring", cfg)
     fastpath.tune("wg_per_cu", 1)
+    fastpath.tune("fib_format", fmt)
     try:
         compare(o1, run_gpu(fastpath, t, fr, me), lab)
         compare(o2, run_gpu(fastpath, tf, fr2, me2))
+        assert fastpath.tune("fib_format_of", 1) == fmt
         n = 64 * 1000 + 17  # ragged last tile; some workgroups get one tile more than others
         compare(oracle.Oracle(tf).process(fr2[:n], me2[:n]), run_gpu(fastpath, tf, fr2[:n], me2[:n]))
     finally:
         fastpath.tune("ring", 2)  # the default geometry
         fastpath.tune("wg_per_cu", 0)
+        fastpath.tune("fib_format", 2)
+        fresh_fastpath_state(fastpath, T.config_single_route())
 
 
 @pytest.mark.parametrize("order,run", [(1, 16), (2, 16), (3, 16), (3, 5)])

@@ -17,6 +17,7 @@ groups=(
   "TCP_UTCL1_TRANSLATION_MISS_sum TCP_CLIENT_UTCL1_INFLIGHT_sum TCP_UTCL1_STALL_INFLIGHT_MAX_sum TCP_UTCL1_STALL_MULTI_MISS_sum"
   "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_LATENCY_sum TCP_TCC_WRITE_REQ_sum"
   "TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum TCC_LATENCY_FIFO_FULL_sum TCP_PENDING_STALL_CYCLES_sum"
+  "SQ_INSTS_SMEM SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES"
 )
 for item in "$@"; do
   IFS=: read -r label wl extra <<< "$item"

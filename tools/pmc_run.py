@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--wg", type=int, default=None, help="gr_hip_tune wg_per_cu")
     ap.add_argument("--stats", type=int, default=None)
     ap.add_argument("--nt", type=int, default=None)
+    ap.add_argument("--fib-format", type=int, default=None, help="gr_hip_tune fib_format (0: 4-byte DIR24_8)")
     ap.add_argument("--no-calib", action="store_true")
     ap.add_argument("--span-bits", type=int, default=None,
                     help="fullview64 with destinations uniform in an aligned 2^N-address range (from 16.0.0.0 when "
@@ -56,6 +57,8 @@ def main():
         elif args.workload == "imix":  # IMIX header lines staged, as bench.py
             kw.update(imix=True, lines_only=True)
     fp = FastPath(0)
+    if args.fib_format is not None:
+        fp.tune("fib_format", args.fib_format)
     fp.load(topo)
     for k in ("ring", "wg", "stats", "nt"):
         v = getattr(args, k)
