@@ -369,48 +369,64 @@ __device__ void ring_compute(const fwd4_params &A, const kctx &P, LT &L, stat_sl
 
 		result r = {GR_HIP_E_PUNT, 0, m.iface, 0, 0, 0, 0, 0};
 		uint32_t fam = 0; // the packet entered ip_input (1) / ip6_input (2)
-		uint32_t dst = 0, data_len = 0;
-		int head = HEAD_DONE;
-		if (live) {
-			const uint8_t *frame = PTRS ? reinterpret_cast<const uint8_t *>(L.ptrs[s][lane])
-						    : A.in + (size_t)(base + lane) * A.in_stride;
-			head = chain_head(P, R, lane, m, rx, r, dst, data_len, frame);
-			fam = head == HEAD_IN4 || head == HEAD_IP4 ? 1 : head == HEAD_IP6 ? 2 : 0;
-		}
-		uint32_t ent = 0;
-		bool got = false;
-		if constexpr (SG > 0)
-			got = fib_tbl24_split<SG>(rx, dst, head == HEAD_IP4, lane, ent);
-		if (live) {
-			if (head == HEAD_IP4) {
-				uint32_t slot;
-				if (got) { // chain_fib's tbl8 step
-					slot = ent;
-					if (ent & 0x80000000u)
+		// from the FIB's nexthop slot to the verdict
+		auto tail4 = [&](uint32_t slot, uint32_t dst, uint32_t data_len) {
+			if (slot == 0 || slot > P.max_nh) {
+				r.edge = GR_HIP_E_IP_ERROR_DEST_UNREACH; // NO_ROUTE :150-153
+			} else {
+				// fast adjacency: from LDS for the first slots, else one 16-byte gather
+				const uint4 f = slot <= A.nhf_lds ? nhf_lds[slot - 1] : gld4(tload(&P.T->nhf) + slot);
+				if (f.w >> 16) {
+					fast_tail(R, lane, r, data_len, slot, f);
+				} else {
+					const uint4 *ap = reinterpret_cast<const uint4 *>(tload(&P.T->adj) + slot);
+					chain_tail(P, R, lane, m, rx.flags, r, dst, data_len, slot, gld4(ap), gld4(ap + 1));
+				}
+			}
+		};
+		// the IPv6 chain (trie walk included) waits on dependent loads: its
+		// wave issues ahead of the streaming waves (s_setprio) until it leaves
+		// it; the IPv4 chain and the ring waits keep the default (raising them
+		// costs IPv4)
+		auto tail6 = [&](uint32_t data_len) {
+			__builtin_amdgcn_s_setprio(2);
+			chain6(P, R, lane, m, rx, r, data_len);
+			__builtin_amdgcn_s_setprio(0);
+		};
+		if constexpr (SG == 0) {
+			if (live) {
+				uint32_t dst = 0, data_len = 0;
+				const uint8_t *frame = PTRS ? reinterpret_cast<const uint8_t *>(L.ptrs[s][lane])
+							    : A.in + (size_t)(base + lane) * A.in_stride;
+				const int head = chain_head(P, R, lane, m, rx, r, dst, data_len, frame);
+				fam = head == HEAD_IN4 || head == HEAD_IP4 ? 1 : head == HEAD_IP6 ? 2 : 0;
+				if (head == HEAD_IP4)
+					tail4(chain_fib(rx, dst), dst, data_len);
+				else if (head == HEAD_IP6)
+					tail6(data_len);
+			}
+		} else { // the tbl24 gathers wave-wide, between the head and the tails
+			uint32_t dst = 0, data_len = 0;
+			int head = HEAD_DONE;
+			if (live) {
+				const uint8_t *frame = PTRS ? reinterpret_cast<const uint8_t *>(L.ptrs[s][lane])
+							    : A.in + (size_t)(base + lane) * A.in_stride;
+				head = chain_head(P, R, lane, m, rx, r, dst, data_len, frame);
+				fam = head == HEAD_IN4 || head == HEAD_IP4 ? 1 : head == HEAD_IP6 ? 2 : 0;
+			}
+			uint32_t ent = 0;
+			const bool got = fib_tbl24_split<SG>(rx, dst, head == HEAD_IP4, lane, ent);
+			if (live) {
+				if (head == HEAD_IP4) {
+					uint32_t slot = ent; // chain_fib's tbl8 step, or all of it
+					if (!got)
+						slot = chain_fib(rx, dst);
+					else if (ent & 0x80000000u)
 						slot = gld(rx.tbl8 + (size_t)(ent & 0x7fffffffu) * 256 + (__builtin_bswap32(dst) & 0xff));
-				} else {
-					slot = chain_fib(rx, dst);
+					tail4(slot, dst, data_len);
+				} else if (head == HEAD_IP6) {
+					tail6(data_len);
 				}
-				if (slot == 0 || slot > P.max_nh) {
-					r.edge = GR_HIP_E_IP_ERROR_DEST_UNREACH; // NO_ROUTE :150-153
-				} else {
-					// fast adjacency: from LDS for the first slots, else one 16-byte gather
-					const uint4 f = slot <= A.nhf_lds ? nhf_lds[slot - 1] : gld4(tload(&P.T->nhf) + slot);
-					if (f.w >> 16) {
-						fast_tail(R, lane, r, data_len, slot, f);
-					} else {
-						const uint4 *ap = reinterpret_cast<const uint4 *>(tload(&P.T->adj) + slot);
-						chain_tail(P, R, lane, m, rx.flags, r, dst, data_len, slot, gld4(ap), gld4(ap + 1));
-					}
-				}
-			} else if (head == HEAD_IP6) {
-				// the IPv6 chain (trie walk included) waits on dependent
-				// loads: its wave issues ahead of the streaming waves
-				// (s_setprio) until it leaves it; the IPv4 chain and the ring
-				// waits keep the default (raising them costs IPv4)
-				__builtin_amdgcn_s_setprio(2);
-				chain6(P, R, lane, m, rx, r, data_len);
-				__builtin_amdgcn_s_setprio(0);
 			}
 		}
 		if (__ballot(r.edge == GR_HIP_E_ETH_OUTPUT_NO_MAC) != 0
