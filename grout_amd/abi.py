@@ -104,6 +104,7 @@ PTYPE_L3_IPV4, PTYPE_L3_IPV6 = 0x10, 0x40  # DPDK rte_mbuf_ptype.h
 BATCH_F_FRAME_PTRS = 0x2
 BATCH_F_PREFIX32 = 0x4  # out_lines: packed 32-byte prefixes (every byte the path changes)
 PREFIX = 32
+NODE_DEPTH = 4  # GR_HIP_NODE_DEPTH: node walks in flight per queue
 
 
 class Batch(ctypes.Structure):

@@ -2272,7 +2272,8 @@ static int launch(gr_hip_queue *q, hipStream_t s, const gr_hip_batch *b, bool ti
 // Posts wait for the FIB generation's upload on the host (launches make their
 // stream wait); commits and quiesce wait, on the host, for the batches posted
 // before them (retire_wait, quiesce).
-#define RES_NDESC 4 // descriptors per ring (GR_HIP_NODE_DEPTH batches in flight at most)
+#define RES_NDESC 8 // descriptors per ring (GR_HIP_NODE_DEPTH batches in flight at most)
+static_assert(GR_HIP_NODE_DEPTH < RES_NDESC, "a ring's batches in flight fit its descriptors");
 #define RES_STRIDE 8 // uint64_t per ring in the done / exited words: a 64-byte line each
 #define RES_TILES_PER_WG 8 // default tiles per workgroup a batch is split into (knob "resident_tiles")
 #define RES_LEAVE_NS (500ull * 1000000ull) // a launch told to stop has left within this, or is stuck

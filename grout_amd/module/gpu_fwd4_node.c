@@ -25,7 +25,10 @@
 // its verdict's edge with grout's private data for that edge. Batches are
 // pipelined two deep ("depth" 2, the default): while the GPU forwards one,
 // the worker accumulates and stages the next, and hands the one before back
-// as soon as it is done. Batches leave in the order they arrived. A source
+// as soon as it is done; deeper (up to GR_HIP_NODE_DEPTH), depth - 1 batches
+// are on the GPU while the next accumulates, so that a worker whose batches
+// take longer on the GPU than to fill (small batches under a latency budget,
+// many workers) keeps filling. Batches leave in the order they arrived. A source
 // node, "gpu_fwd4_flush", runs every graph walk: it hands back a batch whose
 // GPU work has completed, and flushes the batch held when the walk before
 // brought no packet or its oldest packet has waited max_delay (rte_graph
@@ -49,7 +52,9 @@
 //
 // Stream limits. rte_graph holds a node's input stream in uint16_t-sized
 // arrays; the node therefore hands at most one batch back per process() call
-// and batches are at most GPU_FWD4_BATCH_MAX packets.
+// (all those on the GPU only on the way out: a drain leaving the graph, a GPU
+// marked diverged, GR_HIP_NODE_DEPTH x GPU_FWD4_BATCH_MAX < UINT16_MAX) and
+// batches are at most GPU_FWD4_BATCH_MAX packets.
 //
 // It includes grout's and DPDK's headers by their names and builds unchanged
 // in grout (modules/gpu, integration/grout-gpu_module-build.patch) and here,
@@ -106,7 +111,7 @@ int gpu_fwd4_configure(const struct gpu_fwd4_conf *c) {
 		return -EINVAL;
 	conf = *c;
 	if (conf.depth == 0)
-		conf.depth = GR_HIP_NODE_DEPTH;
+		conf.depth = 2;
 	if (conf.batch > GPU_FWD4_BATCH_MAX)
 		conf.batch = GPU_FWD4_BATCH_MAX;
 	return 0;
@@ -302,6 +307,12 @@ static int pick_gpu(const struct rte_graph *graph) {
 // it more) at RTE_GRAPH_BURST_SIZE.
 #define WALK_SPLIT RTE_GRAPH_BURST_SIZE
 
+// Batch buffers per graph: the library's walk slots (conf.depth of them in use)
+#define WALK_BUFS GR_HIP_NODE_DEPTH
+_Static_assert(GPU_FWD4_RCU_PER_GRAPH >= 2 * WALK_BUFS, "a reader per batch held, and per batch handed back in a walk");
+_Static_assert((uint64_t)WALK_BUFS * GPU_FWD4_BATCH_MAX + RTE_GRAPH_BURST_SIZE <= UINT16_MAX,
+	       "every batch handed back in one walk fits rte_graph's stream");
+
 enum { RD_FREE = 0, RD_HELD, RD_RELEASE };
 
 struct gpu_walk {
@@ -312,16 +323,18 @@ struct gpu_walk {
 	gr_hip_queue_t *q;
 	uint32_t n, cap; // the batch accumulating, in buffer `cur`
 	uint64_t first_ns; // arrival of the oldest held packet, 0 = none
-	uint32_t cur;
-	struct rte_mbuf **mbufs[2];
-	uint8_t *edges[2]; // each mbuf's edge, as the one-pass hand-back leaves it
-	int pending; // the other buffer's batch is on the GPU (gr_hip_node_start'ed)
-	uint32_t pend_n; // its size
-	uint64_t pend_ns; // when it was sent
+	// batch buffers, a ring: the npend batches on the GPU (sent, oldest in
+	// `head`) and after them the one accumulating, cur = (head + npend) % WALK_BUFS
+	uint32_t cur, head, npend;
+	struct rte_mbuf **mbufs[WALK_BUFS];
+	uint8_t *edges[WALK_BUFS]; // each mbuf's edge, as the one-pass hand-back leaves it
+	uint32_t pend_n[WALK_BUFS]; // a batch on the GPU: its size,
+	uint64_t pend_ns[WALK_BUFS]; // when it was sent,
+	uint64_t pend_first_ns[WALK_BUFS]; // and when its oldest packet arrived
 	uint64_t gpu_ns; // how long the last batches took to come back (a moving average), 0: none yet
 	// QSBR readers (see "RCU" above): rd[k] is the reader buffer k's batch
 	// holds (-1: none), rstate the state of each of the graph's readers
-	int8_t rd[2];
+	int8_t rd[WALK_BUFS];
 	uint8_t rstate[GPU_FWD4_RCU_PER_GRAPH];
 	struct gr_hip_node_stats stats;
 	struct gr_hip_node_stats flushed; // what gpu_fwd4_stats_flush reported already
@@ -344,7 +357,6 @@ struct gpu_walk {
 	// batches' oldest packets took, arrival to hand-back (a moving average)
 	uint32_t lcap;
 	uint64_t rtt_ns; // the batches' round trips, send to back (a moving average of those sampled)
-	uint64_t pend_first_ns;
 	uint64_t lat_ns;
 	uint64_t over_budget;
 };
@@ -429,7 +441,7 @@ static void reader_hold(struct gpu_walk *w, uint32_t k) {
 			rte_rcu_qsbr_thread_online(gr_datapath_rcu(), reader_id(w, r));
 		return;
 	}
-	// not reached: two batches held + two released per walk at most
+	// not reached: WALK_BUFS batches held + as many released per walk at most
 }
 
 // Buffer k's batch was handed back: its reader goes offline at the next walk.
@@ -541,11 +553,11 @@ static void deliver(struct rte_graph *graph, struct rte_node *node, struct gpu_w
 	PROF_ADD(GPU_FWD4_PROF_DELIVER);
 }
 
-// The batch on the GPU is done (or the poll failed: finish_pending reports
-// it): polled like a worker polls its RX queues, the time it took noted for
-// reap's first poll.
+// The oldest batch on the GPU is done (or the poll failed: finish_oldest
+// reports it): polled like a worker polls its RX queues, the time it took
+// noted for reap's first poll.
 static void poll_until_ready(struct gpu_walk *w) {
-	if (!w->pending)
+	if (w->npend == 0)
 		return;
 	PROF_T0();
 	int polls = 0;
@@ -553,7 +565,7 @@ static void poll_until_ready(struct gpu_walk *w) {
 		if (gr_hip_node_pending(w->q, &ready) <= 0) // an error, or nothing in flight after all
 			break;
 	PROF_ADD(GPU_FWD4_PROF_POLL);
-	const uint64_t waited = now_ns() - w->pend_ns;
+	const uint64_t waited = now_ns() - w->pend_ns[w->head];
 	w->gpu_ns = w->gpu_ns ? (w->gpu_ns * 7 + waited) / 8 : waited;
 	if (polls > 1) // it came back just now: its round trip (else it was back before: no sample)
 		w->rtt_ns = w->rtt_ns ? (w->rtt_ns * 7 + waited) / 8 : waited;
@@ -600,21 +612,22 @@ static void budget_update(struct gpu_walk *w, uint64_t lat, uint32_t n) {
 		w->lcap = cap + step < conf.batch ? cap + step : conf.batch;
 }
 
-// Wait for the batch on the GPU and hand it back. Returns its size. The
-// fast path bounds the wait: past the batch's deadline it retires what the
-// GPU did not run, and the hand-back punts those packets, untouched, to
+// Wait for the oldest batch on the GPU and hand it back. Returns its size.
+// The fast path bounds the wait: past the batch's deadline it retires what
+// the GPU did not run, and the hand-back punts those packets, untouched, to
 // grout's CPU nodes (counted in gpu_errors). Only when the GPU would not let
 // go of the batch (-EDEADLK) are its mbufs kept: stranded, never handed on,
 // and the GPU marked diverged (its graphs punt from then on).
-static uint32_t finish_pending(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
-	if (!w->pending)
+static uint32_t finish_oldest(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
+	if (w->npend == 0)
 		return 0;
-	const uint32_t k = w->cur ^ 1, n = w->pend_n;
+	const uint32_t k = w->head, n = w->pend_n[k];
 	PROF_T0();
-	const int r = hand_back(w, k); // one walk in flight per graph: buffer k's
+	const int r = hand_back(w, k); // the library's oldest walk: buffer k's
 	PROF_ADD(GPU_FWD4_PROF_FINISH);
-	w->pending = 0;
-	budget_update(w, now_ns() - w->pend_first_ns, n);
+	w->head = (k + 1) % WALK_BUFS;
+	w->npend--;
+	budget_update(w, now_ns() - w->pend_first_ns[k], n);
 	if (r == -EDEADLK) {
 		w->stranded += n;
 		w->gpu_errors++;
@@ -626,6 +639,14 @@ static uint32_t finish_pending(struct rte_graph *graph, struct rte_node *node, s
 	return n;
 }
 
+// Every batch on the GPU, oldest first (leaving the graph, a GPU diverged).
+static uint32_t finish_all(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
+	uint32_t n = 0;
+	while (w->npend != 0)
+		n += finish_oldest(graph, node, w);
+	return n;
+}
+
 static void started(struct gpu_walk *w, uint32_t n) {
 	w->batches++;
 	if (n > w->max_batch)
@@ -633,10 +654,10 @@ static void started(struct gpu_walk *w, uint32_t n) {
 }
 
 // Send the accumulated batch; returns the mbufs handed back meanwhile: one
-// batch at most (the accumulated one when synchronous, else the one before),
-// two only when the GPU refuses this one (both then go to grout's CPU nodes
-// and the walk's edges hold at most three batches: still under rte_graph's
-// stream limit).
+// batch at most (the accumulated one when synchronous, else the oldest on the
+// GPU once depth - 1 are there, or once it is done), two only when the GPU
+// refuses this one (both then go to grout's CPU nodes and the walk's edges
+// hold at most three batches: still under rte_graph's stream limit).
 static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
 	if (w->n == 0)
 		return 0;
@@ -644,18 +665,19 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 	const uint64_t first = w->first_ns;
 	w->n = 0;
 	w->first_ns = 0;
-	if (gpus[w->gpu].diverged) { // not to this GPU: grout's CPU nodes, after the batch before
-		const uint32_t d = finish_pending(graph, node, w);
+	if (gpus[w->gpu].diverged) { // not to this GPU: grout's CPU nodes, after the batches before
+		const uint32_t d = finish_all(graph, node, w);
 		gr_hip_node_discard(w->q);
 		deliver(graph, node, w, k, n, -ESTALE);
+		w->cur = (w->head + w->npend) % WALK_BUFS;
 		return d + n;
 	}
-	if ((conf.depth < 2 || w->draining) && !w->pending) { // synchronous
+	if ((conf.depth < 2 || w->draining) && w->npend == 0) { // synchronous
 		started(w, n);
 		int r = gr_hip_node_send(w->q, NULL, n, WALK_SPLIT);
 		if (r == 0)
 			r = hand_back(w, k);
-		if (r == -EDEADLK) { // stranded: see finish_pending
+		if (r == -EDEADLK) { // stranded: see finish_oldest
 			w->stranded += n;
 			w->gpu_errors++;
 			reader_handed_back(w, k);
@@ -666,23 +688,34 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 		return n;
 	}
 	// send this batch (staged as it arrived, gpu_fwd4_process) while the
-	// previous one may still be on the GPU, then hand the previous one back:
-	// batches leave in arrival order
+	// ones before may still be on the GPU; with depth - 1 of them there (one
+	// for depth 1 and during a drain), hand the oldest back, waiting for it,
+	// else only if it is done: batches leave in arrival order
 	PROF_T0();
 	const int r = gr_hip_node_send(w->q, NULL, n, WALK_SPLIT);
 	PROF_ADD(GPU_FWD4_PROF_START);
-	poll_until_ready(w); // a worker polls; a blocking wait would sleep on the GPU's interrupt
-	const uint32_t delivered = finish_pending(graph, node, w);
-	if (r < 0) { // the GPU did not take it: grout's CPU nodes do (after the one before, in order)
+	const uint32_t room = conf.depth > 2 && !w->draining ? conf.depth - 1 : 1;
+	uint32_t delivered = 0;
+	if (r < 0 || w->npend >= room) {
+		poll_until_ready(w); // a worker polls; a blocking wait would sleep on the GPU's interrupt
+		delivered = finish_oldest(graph, node, w);
+	} else if (w->npend != 0) {
+		int ready = 0;
+		if (gr_hip_node_pending(w->q, &ready) > 0 && ready)
+			delivered = finish_oldest(graph, node, w);
+	}
+	if (r < 0) { // the GPU did not take it: grout's CPU nodes do, after the batches before
+		delivered += finish_all(graph, node, w);
 		deliver(graph, node, w, k, n, r);
+		w->cur = (w->head + w->npend) % WALK_BUFS;
 		return delivered + n;
 	}
 	started(w, n);
-	w->pending = 1;
-	w->pend_n = n;
-	w->pend_ns = now_ns();
-	w->pend_first_ns = first ? first : w->pend_ns;
-	w->cur = k ^ 1;
+	w->pend_n[k] = n;
+	w->pend_ns[k] = now_ns();
+	w->pend_first_ns[k] = first ? first : w->pend_ns[k];
+	w->npend++;
+	w->cur = (w->head + w->npend) % WALK_BUFS;
 	return delivered;
 }
 
@@ -693,32 +726,32 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 // process shares; with the resident kernel a poll is a load of a done word.
 #define REAP_MIN_NS 10000
 
-// The batch on the GPU is done: hand it back now (a poll, no wait).
+// The oldest batch on the GPU is done: hand it back now (a poll, no wait).
 static uint32_t reap(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
 	int ready = 0;
-	if (!w->pending)
+	if (w->npend == 0)
 		return 0;
-	const uint64_t t = now_ns(), waited = t - w->pend_ns;
+	const uint64_t t = now_ns(), waited = t - w->pend_ns[w->head];
 	if (waited < REAP_MIN_NS || (conf.launch_per_batch && waited < w->gpu_ns / 4 * 3))
 		return 0;
 	PROF_T0();
 	const int r = gr_hip_node_pending(w->q, &ready);
 	PROF_ADD(GPU_FWD4_PROF_POLL);
 	if (r < 0) // past its deadline, or the GPU failed: the finish decides (bounded)
-		return finish_pending(graph, node, w);
+		return finish_oldest(graph, node, w);
 	if (!ready)
 		return 0;
 	w->gpu_ns = w->gpu_ns ? (w->gpu_ns * 7 + waited) / 8 : waited; // an upper bound: polled late
 	w->rtt_ns = w->rtt_ns ? (w->rtt_ns * 7 + waited) / 8 : waited;
-	return finish_pending(graph, node, w);
+	return finish_oldest(graph, node, w);
 }
 
-// gpu_fwd4_drain past its bound (DRAIN_LEAVE): the batch on the GPU is
+// gpu_fwd4_drain past its bound (DRAIN_LEAVE): the batches on the GPU are
 // waited for and handed back; the held one (staged, not sent: its frames and
-// mbufs untouched) goes to grout's CPU nodes, after it in arrival order.
+// mbufs untouched) goes to grout's CPU nodes, after them in arrival order.
 // Returns the mbufs handed back or sent on.
 static uint32_t leave(struct rte_graph *graph, struct rte_node *node, struct gpu_walk *w) {
-	uint32_t n = finish_pending(graph, node, w);
+	uint32_t n = finish_all(graph, node, w);
 	if (w->n != 0) {
 		const uint32_t k = w->cur, held = w->n;
 		gr_hip_node_discard(w->q);
@@ -806,7 +839,7 @@ static uint16_t gpu_fwd4_process(struct rte_graph *graph, struct rte_node *node,
 }
 
 static void walk_free(struct gpu_walk *w) {
-	for (int k = 0; k < 2; k++) {
+	for (int k = 0; k < WALK_BUFS; k++) {
 		free(w->mbufs[k]);
 		free(w->edges[k]);
 	}
@@ -849,9 +882,9 @@ static int gpu_fwd4_init(const struct rte_graph *graph, struct rte_node *node) {
 	w->slot = slot;
 	w->gpu = pick_gpu(graph);
 	w->cap = GPU_FWD4_BATCH_MAX + RTE_GRAPH_BURST_SIZE; // any batch set_batch allows
-	w->rd[0] = w->rd[1] = -1;
 	int r = 0;
-	for (int k = 0; k < 2; k++) {
+	for (int k = 0; k < WALK_BUFS; k++) {
+		w->rd[k] = -1;
 		w->mbufs[k] = calloc(w->cap, sizeof(*w->mbufs[k]));
 		w->edges[k] = calloc(w->cap, 1);
 		if (w->mbufs[k] == NULL || w->edges[k] == NULL)
@@ -915,11 +948,11 @@ int gpu_fwd4_drain(struct rte_graph *graph) {
 	if (w == NULL)
 		return -ENOENT;
 	const uint64_t h0 = w->handed, p0 = w->drain_punted;
-	const uint64_t bound = drain_bound >= 0 ? (uint64_t)drain_bound : (w->n != 0) + (uint64_t)w->pending + DRAIN_EXTRA;
+	const uint64_t bound = drain_bound >= 0 ? (uint64_t)drain_bound : (w->n != 0) + (uint64_t)w->npend + DRAIN_EXTRA;
 	w->draining = DRAIN_HAND_BACK;
-	while ((w->n != 0 || w->pending) && w->handed - h0 < bound)
+	while ((w->n != 0 || w->npend != 0) && w->handed - h0 < bound)
 		rte_graph_walk(graph);
-	if (w->n != 0 || w->pending) {
+	if (w->n != 0 || w->npend != 0) {
 		w->draining = DRAIN_LEAVE;
 		rte_graph_walk(graph);
 	}
@@ -941,14 +974,16 @@ static void gpu_fwd4_fini(const struct rte_graph *graph, struct rte_node *node) 
 		// the mbufs)
 		// (a GPU that would not let go of it, -EDEADLK: its mbufs stay
 		// stranded, never freed, since the GPU may still write their frames)
-		const int fr = w->pending ? gr_hip_node_finish(w->q, NULL, NULL, NULL) : 0;
 		uint64_t freed = w->n;
-		if (w->pending && fr != -EDEADLK) {
-			for (uint32_t j = 0; j < w->pend_n; j++)
-				rte_pktmbuf_free(w->mbufs[w->cur ^ 1][j]);
-			freed += w->pend_n;
-		} else if (w->pending) {
-			w->stranded += w->pend_n;
+		for (; w->npend != 0; w->npend--, w->head = (w->head + 1) % WALK_BUFS) { // oldest first
+			const uint32_t k = w->head;
+			if (gr_hip_node_finish(w->q, NULL, NULL, NULL) == -EDEADLK) {
+				w->stranded += w->pend_n[k];
+				continue;
+			}
+			for (uint32_t j = 0; j < w->pend_n[k]; j++)
+				rte_pktmbuf_free(w->mbufs[k][j]);
+			freed += w->pend_n[k];
 		}
 		for (uint32_t j = 0; j < w->n; j++) // held, never sent
 			rte_pktmbuf_free(w->mbufs[w->cur][j]);
@@ -1001,13 +1036,13 @@ static uint16_t gpu_flush_process(struct rte_graph *graph, struct rte_node *node
 		return (uint16_t)(n > UINT16_MAX ? UINT16_MAX : n);
 	}
 	// same edges as iface_input, same order; one batch handed back at most
-	// (flush() hands back the one still pending, and none is after these)
+	// (flush() hands back one more at most, and none is after these)
 	const uint64_t t = now_ns();
 	uint32_t n = 0;
 	// (conf's delay, also under a latency budget: the batch on the GPU is
 	// reaped as soon as it is back, and a wait here would stall RX)
-	if (w->pending && (w->draining || t - w->pend_ns >= conf.max_delay_ns))
-		n = finish_pending(graph, node, w); // waited long enough (or leaving the graph): wait for the GPU
+	if (w->npend != 0 && (w->draining || t - w->pend_ns[w->head] >= conf.max_delay_ns))
+		n = finish_oldest(graph, node, w); // waited long enough (or leaving the graph): wait for the GPU
 	else
 		n = reap(graph, node, w);
 	// a whole graph walk brought the node nothing: the RX queues drained,
@@ -1089,7 +1124,7 @@ int gpu_fwd4_walk_info(const struct rte_graph *graph, struct gpu_fwd4_walk_info 
 		return -ENOENT;
 	memset(info, 0, sizeof(*info));
 	info->held = w->n;
-	info->in_flight = (uint32_t)w->pending;
+	info->in_flight = w->npend;
 	info->batches = w->batches;
 	info->max_batch = w->max_batch;
 	info->stale = w->stale;
@@ -1110,7 +1145,9 @@ uint64_t gpu_fwd4_holding(const struct rte_graph *graph) {
 	const struct gpu_walk *w = walk_of(graph);
 	if (w == NULL)
 		return 0;
-	uint64_t held = w->n + (w->pending ? w->pend_n : 0);
+	uint64_t held = w->n;
+	for (uint32_t i = 0; i < w->npend; i++)
+		held += w->pend_n[(w->head + i) % WALK_BUFS];
 	for (int r = 0; r < GPU_FWD4_RCU_PER_GRAPH; r++)
 		held += w->rstate[r] != RD_FREE; // offline at the next walk's flush node
 	return held;

@@ -77,7 +77,9 @@ struct nexthop;
 // Largest batch a graph accumulates. The node hands at most one batch back
 // per process() call (the node's, and its flush source node's), so one graph
 // walk enqueues at most 2 x GPU_FWD4_BATCH_MAX mbufs plus a few bursts of
-// punts on any one edge: under rte_graph's limit of what a node stream can
+// punts on any one edge (every batch the graph holds, GR_HIP_NODE_DEPTH of
+// them, only on the way out: a drain leaving the graph, a GPU marked
+// diverged): under rte_graph's limit of what a node stream can
 // hold (struct rte_node size / idx are uint16_t, DPDK
 // __rte_node_stream_alloc_size verifies the size), with room to spare.
 // Batches of 16k packets forward as fast as 64k ones.
@@ -88,7 +90,7 @@ struct nexthop;
 // asks for GPU_FWD4_RCU_READERS of them through its datapath hooks, and grout's
 // rcu module sizes its QSBR variable for them
 // (integration/grout-gpu_fwd4-datapath.patch).
-#define GPU_FWD4_RCU_PER_GRAPH 4
+#define GPU_FWD4_RCU_PER_GRAPH 8 // 2 x GR_HIP_NODE_DEPTH: batches held, batches handed back in a walk
 #define GPU_FWD4_RCU_READERS (GPU_FWD4_MAX_GRAPHS * GPU_FWD4_RCU_PER_GRAPH)
 
 struct gpu_fwd4_conf {
@@ -99,7 +101,10 @@ struct gpu_fwd4_conf {
 	uint32_t batch; // packets accumulated before a GPU walk (at most GPU_FWD4_BATCH_MAX)
 	uint32_t rx_burst; // port_rx burst size (1..256): a shorter burst flushes
 	uint64_t max_delay_ns; // a held packet never waits longer (flush node)
-	uint32_t depth; // batches in flight per graph: 1 = each waited for, 2 = pipelined (0: 2)
+	// batches in flight per graph (1 .. GR_HIP_NODE_DEPTH): 1 = each waited
+	// for, 2 = one on the GPU while the next accumulates (0: 2, the default),
+	// d = d - 1 on the GPU while the next accumulates
+	uint32_t depth;
 	// 0 (the default): each GPU's batches go to its resident kernel (gr_hip
 	// knob "resident": descriptor rings, no launch per batch); 1: one launch
 	// per batch

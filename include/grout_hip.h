@@ -764,7 +764,10 @@ int gr_hip_node_process(gr_hip_queue_t *, struct gr_hip_mbuf *m, uint32_t n, uin
 // the queue until their finish, which reports them in *m / *n. Walks finish
 // in start order. gr_hip_node_process is start + finish and returns -EBUSY
 // while walks are in flight.
-#define GR_HIP_NODE_DEPTH 2
+// (4: the grout node keeps up to depth - 1 batches on the GPU while it
+// accumulates the next, gpu_fwd4_conf.depth; a walk slot's pinned staging
+// is allocated at its first use)
+#define GR_HIP_NODE_DEPTH 4
 int gr_hip_node_start(gr_hip_queue_t *, struct gr_hip_mbuf *m, uint32_t n, uint32_t burst);
 int gr_hip_node_finish(gr_hip_queue_t *, struct gr_hip_mbuf **m, uint32_t *n, struct gr_hip_node_stats *stats);
 // The start half fused with the node's own pass over its mbufs, so that each

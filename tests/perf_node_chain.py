@@ -177,12 +177,15 @@ def main():
     topo = T.config_fullview()
     fp.load(topo)
     L.gpu_fwd4_set_launch_per_batch.argtypes = [ctypes.c_int]
+    L.gpu_fwd4_set_depth.argtypes = [ctypes.c_uint32]
 
     def set_knob(key, v):
-        """launch_per_batch: the module's own (gpu_fwd4_set_launch_per_batch);
-        else a gr_hip_tune knob of every context."""
+        """launch_per_batch, depth: the module's own (gpu_fwd4_set_launch_per_batch,
+        gpu_fwd4_set_depth); else a gr_hip_tune knob of every context."""
         if key == "launch_per_batch":
             assert L.gpu_fwd4_set_launch_per_batch(v) == 0
+        elif key == "depth":
+            assert L.gpu_fwd4_set_depth(v) == 0
         else:
             fp.tune(key, v)
 

@@ -453,9 +453,10 @@ def test_graph_walk_corpus(pin, ptrs):
     assert len(set(got["edge"])) > 20
 
 
-@pytest.fixture(params=[2, 1], ids=["pipelined", "depth1"])
+@pytest.fixture(params=[2, 1, 3, 4], ids=["pipelined", "depth1", "depth3", "depth4"])
 def depth(request):
-    """Batches in flight per graph: 2 (the default) or 1 (each waited for)."""
+    """Batches in flight per graph: 2 (the default), 1 (each waited for), or
+    3 and 4 (two and three on the GPU while the next accumulates)."""
     graph_ctx()
     assert lib().gpu_fwd4_set_depth(request.param) == 0
     yield request.param
@@ -984,6 +985,77 @@ def test_graph_reload_mid_stream(mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["drained", "drained_leave", "not_drained"])
+def test_graph_reload_deep_pipeline(mode):
+    """The reload above with depth 4 and 512-packet batches: up to three
+    batches on the GPU and one accumulating when the worker leaves its graph.
+    Drained, every mbuf reaches grout's node behind its edge in RX order,
+    bit-exact, nothing held or freed, no QSBR reader online; drained_leave,
+    every batch on the GPU is handed back first (oldest first), then the held
+    one and the drain walk's burst go to grout's CPU nodes untouched, right
+    after them; not drained, fini frees (and counts) the held and the
+    in-flight mbufs, after the GPU is done with them."""
+    L = lib()
+    fp = graph_ctx()
+    t = T.config_single_route()
+    load(fp, t)
+    n, batch, walks = 20_000, 512, 100
+    fr, me = S.stream(n, 0xD7B, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    fr, me = np.ascontiguousarray(fr), np.ascontiguousarray(me, dtype=abi.META_DT)
+    _, _, _, want, _ = oracle.Oracle(t).process_mbufs(fr, me, lines_only=True, burst=BURST)
+    sent = walks * BURST // batch * batch  # 12 full batches sent, 256 packets held
+    drain = mode != "not_drained"
+    L.gpu_fwd4_set_drain_bound.argtypes = [ctypes.c_int32]
+    assert L.gpu_fwd4_set_depth(4) == 0
+    assert L.gpu_fwd4_set_batch(batch, 10_000_000_000) == 0  # no age flush: the rest stays held
+    try:
+        assert L.gh_load(fr.ctypes.data, fr.shape[1], me.ctypes.data, n) == 0
+        if mode == "drained_leave":
+            assert L.gpu_fwd4_set_drain_bound(0) == 0
+        r = _reload(walks, drain)
+        assert L.gpu_fwd4_set_drain_bound(-1) == 0
+        assert r["held"] == walks * BURST - sent and r["in_flight"] <= 3, r
+        if drain:
+            assert r["fini_freed"] == 0 and r["held_after"] == 0 and r["in_flight_after"] == 0, r
+            assert r["readers_online"] == 0, r
+            assert r["recorded"] == r["rx"] > walks * BURST, r
+            if mode == "drained":
+                assert r["left"] == 0, r
+            else:
+                assert r["left"] == r["held"] + (r["rx"] - walks * BURST), r
+        else:
+            assert r["fini_freed"] == r["held"] + r["in_flight"] * batch, r  # held + every batch on the GPU
+        w = L.gh_run(1 << 15)
+        assert (w > 0) if drain else (w < 0), w
+        out = np.zeros(n, dtype=OUT_DT)
+        lines = np.zeros((n, abi.LINE), dtype=np.uint8)
+        assert L.gh_results(out.ctypes.data, lines.ctypes.data) == n
+    finally:
+        L.gpu_fwd4_set_drain_bound(-1)
+        assert L.gpu_fwd4_set_depth(2) == 0
+        assert L.gpu_fwd4_set_batch(BATCH, DELAY_NS) == 0
+        _reload(0, 1)
+        assert L.gh_graph_use(0) == 0
+        _gh["state"]["key"] = None
+    reached = out["edge"] != 0xFF
+    if drain:
+        assert reached.all()
+    else:
+        assert (~reached).sum() == r["fini_freed"], (int((~reached).sum()), r)
+    punt = out["edge"] == abi.EDGE["punt"]
+    if mode == "drained_leave":
+        assert np.array_equal(np.nonzero(punt)[0], np.arange(sent, sent + r["left"]))
+        assert (out["data_off"][punt] == 128).all()
+        assert np.array_equal(lines[punt], fr[punt][:, :abi.LINE])
+    else:
+        assert not punt.any()
+    fwd = reached & ~punt
+    assert (out["edge"][fwd] == abi.EDGE["port_output"]).all()
+    for f in ("edge", "pkt_len", "data_len", "data_off", "iface", "vlan_id"):
+        assert np.array_equal(out[f][fwd], want[f][fwd]), f
+
+
+@pytest.mark.gpu
 def test_graph_walk_append_failure_punts_one_walk():
     """A graph walk the node cannot stage (gr_hip_node_append fails, e.g. no
     pinned memory to grow the walk slot; the slot is left as it was) goes to
@@ -1100,6 +1172,30 @@ def test_idle_loop_adaptive_irq_blocks_only_when_nothing_held():
 
 
 @pytest.mark.gpu
+def test_idle_loop_deep_pipeline():
+    """The adaptive-IRQ loop with depth 4 and 2048-packet batches: when RX
+    goes quiet up to three batches are on the GPU and one accumulating; the
+    holding hook counts them all, so the worker blocks only once every mbuf
+    is through grout's nodes, bit-exact and in order, and every QSBR reader
+    is offline."""
+    L = lib()
+    fp, n, want = _burst_then_silence(n=8 * 2048 + 100, seed=0x1D23)
+    assert L.gpu_fwd4_set_depth(4) == 0
+    assert L.gpu_fwd4_set_batch(2048, 20_000_000) == 0
+    try:
+        r = _loop(adaptive=1, block_ms=2000)
+    finally:
+        assert L.gpu_fwd4_set_depth(2) == 0
+        _restore_batch()
+    assert r["blocked"] == 1, r
+    assert r["recorded_at_block"] == n and r["held_at_block"] == 0, r
+    assert r["readers_online_at_block"] == 0 and r["sync_returned"] == 1, r
+    got = _results(n)
+    assert np.array_equal(got["edge"], want["edge"])
+    assert np.array_equal(got["iface"], want["iface"])
+
+
+@pytest.mark.gpu
 def test_idle_loop_without_holding_blocks_with_a_batch_on_the_gpu():
     """The same loop as grout runs it without the hook (the negative
     control): the resident kernel held back (knob "resident_hold") keeps the
@@ -1197,12 +1293,16 @@ def test_idle_loop_micro_sleep(ignore_holding):
 
 
 @pytest.mark.gpu
-def test_latency_budget_sizes_batches():
+@pytest.mark.parametrize("depth", [2, 3], ids=["depth2", "depth3"])
+def test_latency_budget_sizes_batches(depth):
     """gpu_fwd4_set_latency_budget: under a 100 us budget the graph's batches
     are sized by what their oldest packets took (arrival to hand-back), not by
     the 15360 of gpu_fwd4_set_batch: the cap stays within a few thousand
-    packets, and the walk is bit-exact with the oracle as ever."""
+    packets, and the walk is bit-exact with the oracle as ever (also with two
+    batches on the GPU while the next accumulates)."""
     L = lib()
+    graph_ctx()
+    assert L.gpu_fwd4_set_depth(depth) == 0
     L.gpu_fwd4_set_latency_budget.argtypes = [ctypes.c_uint64]
     fp = graph_ctx()
     t = T.config_single_route()
@@ -1215,6 +1315,7 @@ def test_latency_budget_sizes_batches():
         i1 = walk_info()
     finally:
         assert L.gpu_fwd4_set_latency_budget(0) == 0
+        assert L.gpu_fwd4_set_depth(2) == 0
         _restore_batch()
     assert 64 <= i1["batch_cap"] <= 4096, i1
     assert i1["max_batch"] <= 4096 + BURST or i1["batches"] - i0["batches"] >= len(me) // 4096, i1

@@ -557,8 +557,9 @@ def test_node_pipelined_walks(fastpath, ptrs):
     """gr_hip_node_start / _finish: walk i+1 is staged and sent while walk i
     is on the GPU, and walks finish in start order; every walk ends exactly
     as gr_hip_node_process leaves it (the oracle's mbufs), counters included.
-    A third walk in flight is refused (-EBUSY), and so is node_process while
-    walks are in flight; finishing with none in flight is -ENOENT."""
+    Past GR_HIP_NODE_DEPTH walks in flight a start is refused (-EBUSY), and
+    so is node_process while walks are in flight; finishing with none in
+    flight is -ENOENT."""
     from golden_util import fresh_fastpath_state
     topo = T.config_fullview(count=100_000)
     fr, me = S.stream(50_000, 0xB1F, routes=topo.route_array())
@@ -575,21 +576,28 @@ def test_node_pipelined_walks(fastpath, ptrs):
         cuts = [0, 64 * 100, 64 * 101, 64 * 400, 64 * 401 + 64, len(m)]
         parts = [m[a:b] for a, b in zip(cuts, cuts[1:])]
         total = np.zeros(1, dtype=abi.NODE_STATS_DT)[0]
-        q.node_start(parts[0])
-        assert q.node_pending()[0] == 1
-        for k in range(1, len(parts)):
+        D = abi.NODE_DEPTH
+        assert len(parts) > D
+        for k in range(D):  # the queue full: D walks in flight
             q.node_start(parts[k])
-            assert q.node_pending()[0] == 2
-            assert L.gr_hip_node_start(q._h, parts[k].ctypes.data, len(parts[k]), 64) == -16  # -EBUSY
-            assert L.gr_hip_node_process(q._h, parts[k].ctypes.data, len(parts[k]), 64, None) == -16
+            assert q.node_pending()[0] == k + 1
+        assert L.gr_hip_node_start(q._h, parts[D].ctypes.data, len(parts[D]), 64) == -16  # -EBUSY
+        assert L.gr_hip_node_process(q._h, parts[D].ctypes.data, len(parts[D]), 64, None) == -16
+        done = 0
+        for k in range(D, len(parts)):  # one out, one in: still D in flight
             got, ns = q.node_finish()
-            assert got is parts[k - 1] and q.unfinished == 0
+            assert got is parts[done] and q.unfinished == 0
+            done += 1
             total["packets"] += ns["packets"]
             total["calls"] += ns["calls"]
-        got, ns = q.node_finish()
-        assert got is parts[-1]
-        total["packets"] += ns["packets"]
-        total["calls"] += ns["calls"]
+            q.node_start(parts[k])
+            assert q.node_pending()[0] == D
+        while done < len(parts):
+            got, ns = q.node_finish()
+            assert got is parts[done]
+            done += 1
+            total["packets"] += ns["packets"]
+            total["calls"] += ns["calls"]
         assert q.node_pending() == (0, False)
         assert L.gr_hip_node_finish(q._h, None, None, None) == -2  # -ENOENT
         compare_mbufs(m, want, bufs, lines)
