@@ -266,6 +266,7 @@ struct alignas(128) gr_hip_queue {
 	// used or freed again; every later node call fails (the node punts)
 	bool dead = false;
 	uint32_t res_polls = 0; // gr_hip_node_pending's polls of resident batches
+	uint32_t res_rot = 0; // the helper ring the last rotated batch went to (knob "resident_rotate")
 };
 
 struct host_range { // gr_hip_host_register
@@ -396,6 +397,11 @@ struct gr_hip_ctx {
 	uint32_t res_tiles; // tiles per workgroup a batch is split into, up to the queue's rings (knob "resident_tiles")
 	uint32_t res_split = 0; // at most this many of a queue's rings per batch (0: all; knob "resident_split")
 	uint32_t res_budget = 32; // workgroups the busy queues' batches are split over together (knob "resident_budget"; 0: no cap)
+	// a one-ring batch posted while the queue has others in flight runs on
+	// the queue's next helper ring, its first ring only waking that one
+	// (knob "resident_rotate", off by default; the grout node sets it when
+	// more than one batch per graph is on the GPU, gpu_fwd4_conf.depth > 2)
+	bool res_rotate = false;
 	std::atomic<uint32_t> res_busy{0}; // queues with resident batches in flight
 	fwd4_res_desc *res_desc;
 	uint64_t *res_done, *res_exited;
@@ -2591,8 +2597,19 @@ static int res_post(gr_hip_queue *q, const gr_hip_batch *b, res_mark *m) {
 		const uint32_t cap = c->res_budget / busy;
 		k = k > cap ? (cap < 1 ? 1 : cap) : k;
 	}
-	for (uint32_t j = 0; j < k; j++)
-		if (q->res_posted.seq[j] + 1 > res_word(c->res_done, q->ring + (int)j) + RES_NDESC)
+	// a one-ring batch behind others of the queue: on helper ring h, so that
+	// it does not wait for them on the first ring, which only wakes h (an
+	// empty share of its own; rings 1 .. h-1 are waited for at their last
+	// posted batch, older ones, which leave before this one anyway)
+	uint32_t h = 0;
+	if (k == 1 && c->res_rotate && q->res_inflight > 0 && q->res_w > 1) {
+		q->res_rot = q->res_rot % (q->res_w - 1) + 1; // 1 .. res_w - 1 in turn
+		h = q->res_rot;
+	}
+	const uint32_t kpost = h ? h + 1 : k; // rings the batch's mark covers
+	for (uint32_t j = 0; j < kpost; j++)
+		if ((j == 0 || j == kpost - 1 || !h)
+		    && q->res_posted.seq[j] + 1 > res_word(c->res_done, q->ring + (int)j) + RES_NDESC)
 			return -EBUSY; // (not reached: GR_HIP_NODE_DEPTH < RES_NDESC)
 	fwd4_params A{};
 	A.in = static_cast<const uint8_t *>(b->in_frames);
@@ -2610,6 +2627,35 @@ static int res_post(gr_hip_queue *q, const gr_hip_batch *b, res_mark *m) {
 	A.err = q->d_err;
 	A.wgs = k;
 	A.ptrs = (b->flags & GR_HIP_BATCH_F_FRAME_PTRS) ? 1 : 0;
+	if (h) {
+		m->k = kpost;
+		for (uint32_t j = 1; j < h; j++)
+			m->seq[j] = q->res_posted.seq[j];
+		// ring h: the whole batch, as a batch of one ring
+		const uint64_t sh = q->res_posted.seq[h] + 1;
+		fwd4_res_desc &dh = c->res_desc[(size_t)(q->ring + (int)h) * RES_NDESC + sh % RES_NDESC];
+		A.wg0 = 0;
+		A.wgs = 1;
+		memcpy(&dh.A, &A, sizeof(A));
+		memset(dh.helper_seq, 0, sizeof(dh.helper_seq));
+		__atomic_store_n(&dh.seq, sh, __ATOMIC_RELEASE); // after A
+		q->res_posted.seq[h] = sh;
+		m->seq[h] = sh;
+		// the first ring: no tile of its own, wakes ring h for it
+		const uint64_t s0 = q->res_posted.seq[0] + 1;
+		fwd4_res_desc &d0 = c->res_desc[(size_t)q->ring * RES_NDESC + s0 % RES_NDESC];
+		A.n = 0;
+		A.wgs = h + 1;
+		memcpy(&d0.A, &A, sizeof(A));
+		memset(d0.helper_seq, 0, sizeof(d0.helper_seq));
+		d0.helper_seq[h - 1] = sh;
+		__atomic_store_n(&d0.seq, s0, __ATOMIC_RELEASE);
+		q->res_posted.seq[0] = s0;
+		m->seq[0] = s0;
+		if (q->res_inflight++ == 0)
+			c->res_busy.fetch_add(1, std::memory_order_relaxed);
+		return res_kick(c);
+	}
 	m->k = k;
 	// the helpers first: the first ring's workgroup wakes them (fwd4_res_desc)
 	for (uint32_t j = k; j-- > 0;) {
@@ -2707,6 +2753,8 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		if (value < 1 || value > 64)
 			return -EINVAL;
 		c->res_nap = (uint32_t)value;
+	} else if (strcmp(key, "resident_rotate") == 0) { // one-ring batches behind others go to the helper rings in turn
+		c->res_rotate = value != 0;
 	} else if (strcmp(key, "resident_wait_ms") == 0) { // a resident batch's deadline, from its post
 		if (value < 1 || value > 60000)
 			return -EINVAL;

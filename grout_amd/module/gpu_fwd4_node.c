@@ -126,6 +126,8 @@ int gpu_fwd4_set_depth(uint32_t depth) {
 	if (depth == 0 || depth > GR_HIP_NODE_DEPTH)
 		return -EINVAL;
 	conf.depth = depth; // a graph's next flush switches (finishing what is in flight first)
+	for (uint32_t i = 0; i < n_gpus; i++)
+		gr_hip_tune(gpus[i].ctx, "resident_rotate", depth > 2);
 	return 0;
 }
 
@@ -236,6 +238,9 @@ static void gpu_init(struct event_base *ev) {
 			return;
 		}
 		gr_hip_tune(c, "resident", conf.launch_per_batch ? 0 : 1);
+		// more than one batch per graph on the GPU: a queue's one-ring batches
+		// run on its rings in turn, not one after the other on its first
+		gr_hip_tune(c, "resident_rotate", conf.depth > 2);
 		const int numa = gr_hip_device_numa_node(devs[i]);
 		gpus[n_gpus].ctx = c;
 		gpus[n_gpus].dev = devs[i];

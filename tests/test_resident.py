@@ -287,6 +287,58 @@ def test_resident_split_knobs(knobs, wgs, tiles, split, budget):
         q.close()
 
 
+def _deep(q, m, cuts, depth):
+    """Walks [cuts[i], cuts[i+1]) with `depth` of them in flight, finished in order."""
+    parts = [m[a:b] for a, b in zip(cuts, cuts[1:])]
+    tot = np.zeros(1, dtype=abi.NODE_STATS_DT)[0]
+    done = 0
+    for k in range(len(parts) + depth):
+        if k >= depth or k >= len(parts):
+            if done < len(parts):
+                got, ns = q.node_finish()
+                assert got is parts[done] and q.unfinished == 0
+                tot["packets"] += ns["packets"]
+                tot["calls"] += ns["calls"]
+                done += 1
+        if k < len(parts):
+            q.node_start(parts[k])
+    assert done == len(parts)
+    return tot
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wgs,budget", [(8, 32), (3, 32), (8, 2)])
+def test_resident_rotate(knobs, wgs, budget):
+    """Knob "resident_rotate" (the grout node's depth > 2): a batch of one
+    ring posted while others of its queue are in flight runs on the queue's
+    next helper ring, the first ring only waking it. Ragged batches, up to
+    GR_HIP_NODE_DEPTH in flight, rotated over the helpers (and split as
+    usual when large): every walk as the oracle's, in start order, and the
+    queue idle after its last."""
+    from golden_util import fresh_fastpath_state
+    fp = knobs
+    assert fp.tune("resident_wgs", wgs) == 0 and fp.tune("resident_budget", budget) == 0
+    assert fp.tune("resident_rotate", 1) == 0
+    topo = T.config_fullview(count=50_000)
+    sizes = [1, 63, 64, 65, 129, 512, 300, 64, 2000, 511, 7, 4097, 128, 256, 15360, 64, 64, 64, 1000, 33]
+    fr, me = S.stream(sum(sizes), 0xD40 + wgs, routes=topo.route_array())
+    fresh_fastpath_state(fp, topo)
+    lines, v, st, want, ns_want = oracle.Oracle(topo).process_mbufs(fr, me, lines_only=True)
+    bufs, m = mbufs_for(fr, me)
+    q = fp.queue()
+    try:
+        tot = _deep(q, m, list(np.cumsum([0] + sizes)), abi.NODE_DEPTH)
+        compare_mbufs(m, want, bufs, lines)
+        assert np.array_equal(tot["packets"], ns_want["packets"])
+        assert np.array_equal(tot["calls"], ns_want["calls"])
+        assert np.array_equal(q.node_iface_stats(), st)
+        assert not q.stats()["rx_packets"].any()  # every batch went to the resident kernel
+        assert fp.tune("resident_busy") == 0
+    finally:
+        fp.tune("resident_rotate", 0)
+        q.close()
+
+
 @pytest.mark.gpu
 def test_resident_rings_run_out(knobs):
     """A queue takes its rings on its first batch, as many as "resident_wgs"
