@@ -2755,6 +2755,8 @@ extern "C" int gr_hip_tune(gr_hip_ctx_t *c, const char *key, int value) {
 		c->res_nap = (uint32_t)value;
 	} else if (strcmp(key, "resident_rotate") == 0) { // one-ring batches behind others go to the helper rings in turn
 		c->res_rotate = value != 0;
+	} else if (strcmp(key, "resident_rotating") == 0) { // read: "resident_rotate"
+		return c->res_rotate ? 1 : 0;
 	} else if (strcmp(key, "resident_wait_ms") == 0) { // a resident batch's deadline, from its post
 		if (value < 1 || value > 60000)
 			return -EINVAL;

@@ -92,7 +92,7 @@ static struct gpu_fwd4_conf conf = {
 	.batch = GPU_FWD4_BATCH_MAX,
 	.rx_burst = 64,
 	.max_delay_ns = 50000,
-	.depth = 2,
+	.depth = 0, // from the latency budget (depth_now)
 };
 
 // One fast-path context per GPU; the worker graphs are spread over them.
@@ -110,8 +110,6 @@ int gpu_fwd4_configure(const struct gpu_fwd4_conf *c) {
 	    || c->depth > GR_HIP_NODE_DEPTH)
 		return -EINVAL;
 	conf = *c;
-	if (conf.depth == 0)
-		conf.depth = 2;
 	if (conf.batch > GPU_FWD4_BATCH_MAX)
 		conf.batch = GPU_FWD4_BATCH_MAX;
 	return 0;
@@ -122,12 +120,32 @@ void gpu_fwd4_conf_get(struct gpu_fwd4_conf *c) {
 		*c = conf;
 }
 
+// Budgets up to this get the deepest pipeline when conf.depth is 0 (DESIGN.md
+// §6.3: at 50 us, 1.2-2.3x depth 2 at 8 and 16 workers; at 100 us little
+// gain and a p99 past the budget at 16 workers)
+#define DEPTH_AUTO_BUDGET_NS 75000
+
+// The depth in effect: conf's, or with conf.depth 0 (the default) 2, and
+// GR_HIP_NODE_DEPTH under a latency budget of DEPTH_AUTO_BUDGET_NS or less.
+static uint32_t depth_now(void) {
+	if (conf.depth != 0)
+		return conf.depth;
+	const uint64_t b = conf.latency_budget_ns;
+	return b != 0 && b <= DEPTH_AUTO_BUDGET_NS ? GR_HIP_NODE_DEPTH : 2;
+}
+
+// More than one batch per graph on the GPU: a queue's one-ring batches run
+// on its rings in turn, not one after the other on its first ("resident_rotate").
+static void rotate_sync(void) {
+	for (uint32_t i = 0; i < n_gpus; i++)
+		gr_hip_tune(gpus[i].ctx, "resident_rotate", depth_now() > 2);
+}
+
 int gpu_fwd4_set_depth(uint32_t depth) {
-	if (depth == 0 || depth > GR_HIP_NODE_DEPTH)
+	if (depth > GR_HIP_NODE_DEPTH)
 		return -EINVAL;
 	conf.depth = depth; // a graph's next flush switches (finishing what is in flight first)
-	for (uint32_t i = 0; i < n_gpus; i++)
-		gr_hip_tune(gpus[i].ctx, "resident_rotate", depth > 2);
+	rotate_sync();
 	return 0;
 }
 
@@ -238,9 +256,7 @@ static void gpu_init(struct event_base *ev) {
 			return;
 		}
 		gr_hip_tune(c, "resident", conf.launch_per_batch ? 0 : 1);
-		// more than one batch per graph on the GPU: a queue's one-ring batches
-		// run on its rings in turn, not one after the other on its first
-		gr_hip_tune(c, "resident_rotate", conf.depth > 2);
+		gr_hip_tune(c, "resident_rotate", depth_now() > 2); // (rotate_sync)
 		const int numa = gr_hip_device_numa_node(devs[i]);
 		gpus[n_gpus].ctx = c;
 		gpus[n_gpus].dev = devs[i];
@@ -416,6 +432,7 @@ int gpu_fwd4_set_latency_budget(uint64_t budget_ns) {
 	for (int i = 0; i < GPU_FWD4_MAX_GRAPHS; i++)
 		if (walks[i] != NULL)
 			walks[i]->lcap = 0;
+	rotate_sync(); // the depth may follow the budget
 	return 0;
 }
 
@@ -677,7 +694,8 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 		w->cur = (w->head + w->npend) % WALK_BUFS;
 		return d + n;
 	}
-	if ((conf.depth < 2 || w->draining) && w->npend == 0) { // synchronous
+	const uint32_t depth = depth_now();
+	if ((depth < 2 || w->draining) && w->npend == 0) { // synchronous
 		started(w, n);
 		int r = gr_hip_node_send(w->q, NULL, n, WALK_SPLIT);
 		if (r == 0)
@@ -699,7 +717,7 @@ static uint32_t flush(struct rte_graph *graph, struct rte_node *node, struct gpu
 	PROF_T0();
 	const int r = gr_hip_node_send(w->q, NULL, n, WALK_SPLIT);
 	PROF_ADD(GPU_FWD4_PROF_START);
-	const uint32_t room = conf.depth > 2 && !w->draining ? conf.depth - 1 : 1;
+	const uint32_t room = depth > 2 && !w->draining ? depth - 1 : 1;
 	uint32_t delivered = 0;
 	if (r < 0 || w->npend >= room) {
 		poll_until_ready(w); // a worker polls; a blocking wait would sleep on the GPU's interrupt
@@ -1143,6 +1161,7 @@ int gpu_fwd4_walk_info(const struct rte_graph *graph, struct gpu_fwd4_walk_info 
 	info->batch_cap = batch_cap(w);
 	info->lat_ns = w->lat_ns;
 	info->over_budget = w->over_budget;
+	info->depth = depth_now();
 	return 0;
 }
 

@@ -102,8 +102,9 @@ struct gpu_fwd4_conf {
 	uint32_t rx_burst; // port_rx burst size (1..256): a shorter burst flushes
 	uint64_t max_delay_ns; // a held packet never waits longer (flush node)
 	// batches in flight per graph (1 .. GR_HIP_NODE_DEPTH): 1 = each waited
-	// for, 2 = one on the GPU while the next accumulates (0: 2, the default),
-	// d = d - 1 on the GPU while the next accumulates
+	// for, 2 = one on the GPU while the next accumulates, d = d - 1 on the
+	// GPU while the next accumulates; 0 (the default): 2, and
+	// GR_HIP_NODE_DEPTH under a latency budget of 75 us or less
 	uint32_t depth;
 	// 0 (the default): each GPU's batches go to its resident kernel (gr_hip
 	// knob "resident": descriptor rings, no launch per batch); 1: one launch
@@ -125,7 +126,8 @@ struct gpu_fwd4_conf {
 int gpu_fwd4_configure(const struct gpu_fwd4_conf *);
 // The configuration in effect (batch clamped).
 void gpu_fwd4_conf_get(struct gpu_fwd4_conf *);
-// Batches in flight per graph (1 or 2), at any time. 0 or -EINVAL.
+// Batches in flight per graph (1 .. GR_HIP_NODE_DEPTH; 0: from the latency
+// budget, gpu_fwd4_conf.depth), at any time. 0 or -EINVAL.
 int gpu_fwd4_set_depth(uint32_t depth);
 // 1: one launch per batch; 0: batches posted to the resident kernel (the
 // default, gpu_fwd4_conf.launch_per_batch), on every GPU from the next batch
@@ -229,6 +231,7 @@ struct gpu_fwd4_walk_info {
 	uint32_t batch_cap; // the batch size in effect (latency budget: the graph's cap)
 	uint64_t lat_ns; // moving average of the batches' oldest packet, arrival to hand-back
 	uint64_t over_budget; // batches whose oldest packet came back past the latency budget
+	uint32_t depth; // the depth in effect (gpu_fwd4_conf.depth, or the one the budget picked)
 };
 int gpu_fwd4_walk_info(const struct rte_graph *, struct gpu_fwd4_walk_info *);
 // Tests only: 0 = the node takes no QSBR reader (round 2's behaviour, to

@@ -101,8 +101,8 @@ def lib():
 WALK_INFO_DT = np.dtype([("held", "<u4"), ("in_flight", "<u4"), ("batches", "<u8"), ("max_batch", "<u8"),
                          ("stale", "<u8"), ("readers_online", "<u4"), ("diverged", "<i4"), ("append_errors", "<u8"),
                          ("handed", "<u8"), ("drain_punted", "<u8"), ("stranded", "<u8"), ("batch_cap", "<u4"),
-                         ("lat_ns", "<u8"), ("over_budget", "<u8")], align=True)
-assert WALK_INFO_DT.itemsize == 96
+                         ("lat_ns", "<u8"), ("over_budget", "<u8"), ("depth", "<u4")], align=True)
+assert WALK_INFO_DT.itemsize == 104
 LOOP_RES_DT = np.dtype([("walks", "<u4"), ("windows", "<u4"), ("sleeps", "<u4"), ("sleeps_held", "<u4"),
                         ("busy_held", "<u4"), ("blocked", "<u4"), ("recorded_at_block", "<u4"),
                         ("held_at_block", "<u8"), ("readers_online_at_block", "<u4"), ("sync_returned", "<u4"),
@@ -460,7 +460,7 @@ def depth(request):
     graph_ctx()
     assert lib().gpu_fwd4_set_depth(request.param) == 0
     yield request.param
-    lib().gpu_fwd4_set_depth(2)
+    lib().gpu_fwd4_set_depth(0)  # the default: from the budget
 
 
 @pytest.mark.gpu
@@ -1032,7 +1032,7 @@ def test_graph_reload_deep_pipeline(mode):
         assert L.gh_results(out.ctypes.data, lines.ctypes.data) == n
     finally:
         L.gpu_fwd4_set_drain_bound(-1)
-        assert L.gpu_fwd4_set_depth(2) == 0
+        assert L.gpu_fwd4_set_depth(0) == 0
         assert L.gpu_fwd4_set_batch(BATCH, DELAY_NS) == 0
         _reload(0, 1)
         assert L.gh_graph_use(0) == 0
@@ -1185,7 +1185,7 @@ def test_idle_loop_deep_pipeline():
     try:
         r = _loop(adaptive=1, block_ms=2000)
     finally:
-        assert L.gpu_fwd4_set_depth(2) == 0
+        assert L.gpu_fwd4_set_depth(0) == 0
         _restore_batch()
     assert r["blocked"] == 1, r
     assert r["recorded_at_block"] == n and r["held_at_block"] == 0, r
@@ -1293,6 +1293,37 @@ def test_idle_loop_micro_sleep(ignore_holding):
 
 
 @pytest.mark.gpu
+def test_latency_budget_picks_the_depth():
+    """gpu_fwd4_conf.depth 0 (the default): two batches per graph in flight,
+    and GR_HIP_NODE_DEPTH under a latency budget of 75 us or less, with the
+    resident kernel's ring rotation on; a depth set by hand
+    wins. Bit-exact walks either way."""
+    L = lib()
+    L.gpu_fwd4_set_latency_budget.argtypes = [ctypes.c_uint64]
+    fp = graph_ctx()
+    t = T.config_single_route()
+    fr, me = S.stream(3 * BATCH_MAX, 0x1A7C, dst_range=(T.ip4("16.1.0.0"), T.ip4("16.1.255.255")))
+    hip, ctx = abi.hip(), L.gh_hip_ctx()
+    assert L.gpu_fwd4_set_depth(0) == 0
+    try:
+        assert walk_info()["depth"] == 2 and hip.gr_hip_tune(ctx, b"resident_rotating", 0) == 0
+        assert L.gpu_fwd4_set_batch(BATCH_MAX, 20_000_000) == 0
+        assert L.gpu_fwd4_set_latency_budget(50_000) == 0
+        assert walk_info()["depth"] == abi.NODE_DEPTH and hip.gr_hip_tune(ctx, b"resident_rotating", 0) == 1
+        check_walk(t, fr, me)
+        assert walk_info()["batch_cap"] < BATCH_MAX
+        assert L.gpu_fwd4_set_depth(2) == 0  # by hand: no longer the budget's
+        assert walk_info()["depth"] == 2 and hip.gr_hip_tune(ctx, b"resident_rotating", 0) == 0
+        assert L.gpu_fwd4_set_depth(0) == 0
+        assert L.gpu_fwd4_set_latency_budget(100_000) == 0
+        assert walk_info()["depth"] == 2 and hip.gr_hip_tune(ctx, b"resident_rotating", 0) == 0
+    finally:
+        assert L.gpu_fwd4_set_latency_budget(0) == 0
+        assert L.gpu_fwd4_set_depth(0) == 0
+        _restore_batch()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("depth", [2, 3], ids=["depth2", "depth3"])
 def test_latency_budget_sizes_batches(depth):
     """gpu_fwd4_set_latency_budget: under a 100 us budget the graph's batches
@@ -1315,7 +1346,7 @@ def test_latency_budget_sizes_batches(depth):
         i1 = walk_info()
     finally:
         assert L.gpu_fwd4_set_latency_budget(0) == 0
-        assert L.gpu_fwd4_set_depth(2) == 0
+        assert L.gpu_fwd4_set_depth(0) == 0
         _restore_batch()
     assert 64 <= i1["batch_cap"] <= 4096, i1
     assert i1["max_batch"] <= 4096 + BURST or i1["batches"] - i0["batches"] >= len(me) // 4096, i1
