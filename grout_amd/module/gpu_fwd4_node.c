@@ -617,8 +617,7 @@ static uint64_t hold_max(const struct gpu_walk *w) {
 // A batch came back: its oldest packet took `lat` from its arrival. Under a
 // budget the cap follows the moving average of those times: down by an eighth
 // while it is above 17/20 of the budget, up by an eighth (64 at least) while it
-// is below 13/20 and full batches come back (14/20 and 10/20 with more than
-// one batch on the GPU, whose tail is longer: DESIGN.md §6.3). One late batch (a host stall,
+// is below 13/20 and full batches come back. One late batch (a host stall,
 // another worker's burst on the GPU) moves it little: every worker keeps
 // batches of about the same size, and the slowest one sets the pace.
 static void budget_update(struct gpu_walk *w, uint64_t lat, uint32_t n) {
@@ -629,10 +628,9 @@ static void budget_update(struct gpu_walk *w, uint64_t lat, uint32_t n) {
 	if (lat > b)
 		w->over_budget++;
 	const uint32_t cap = batch_cap(w), step = cap / 8 > 64 ? cap / 8 : 64;
-	const uint64_t hi = depth_now() > 2 ? 14 : 17, lo = hi - 4; // twentieths of the budget
-	if (w->lat_ns * 20 > b * hi)
+	if (w->lat_ns * 20 > b * 17)
 		w->lcap = cap > step + 64 ? cap - step : 64;
-	else if (w->lat_ns * 20 < b * lo && n >= cap - cap / 8)
+	else if (w->lat_ns * 20 < b * 13 && n >= cap - cap / 8)
 		w->lcap = cap + step < conf.batch ? cap + step : conf.batch;
 }
 
