@@ -2597,18 +2597,20 @@ static int res_post(gr_hip_queue *q, const gr_hip_batch *b, res_mark *m) {
 		const uint32_t cap = c->res_budget / busy;
 		k = k > cap ? (cap < 1 ? 1 : cap) : k;
 	}
-	// a one-ring batch behind others of the queue: on helper ring h, so that
-	// it does not wait for them on the first ring, which only wakes h (an
-	// empty share of its own; rings 1 .. h-1 are waited for at their last
-	// posted batch, older ones, which leave before this one anyway)
+	// a batch of k rings behind others of the queue: on helper rings h ..
+	// h + k - 1, so that it does not wait for them on the first ring(s),
+	// which only wakes those (an empty share of its own; rings 1 .. h-1 are
+	// waited for at their last posted batch, older ones, which leave before
+	// this one anyway). h goes round 1 .. res_w - k.
 	uint32_t h = 0;
-	if (k == 1 && c->res_rotate && q->res_inflight > 0 && q->res_w > 1) {
-		q->res_rot = q->res_rot % (q->res_w - 1) + 1; // 1 .. res_w - 1 in turn
+	if (c->res_rotate && q->res_inflight > 0 && k < q->res_w) {
+		const uint32_t span = q->res_w - k; // first rings of a group of k among the helpers
+		q->res_rot = q->res_rot % span + 1;
 		h = q->res_rot;
 	}
-	const uint32_t kpost = h ? h + 1 : k; // rings the batch's mark covers
+	const uint32_t kpost = h ? h + k : k; // rings the batch's mark covers
 	for (uint32_t j = 0; j < kpost; j++)
-		if ((j == 0 || j == kpost - 1 || !h)
+		if ((!h || j == 0 || j >= h)
 		    && q->res_posted.seq[j] + 1 > res_word(c->res_done, q->ring + (int)j) + RES_NDESC)
 			return -EBUSY; // (not reached: GR_HIP_NODE_DEPTH < RES_NDESC)
 	fwd4_params A{};
@@ -2631,24 +2633,31 @@ static int res_post(gr_hip_queue *q, const gr_hip_batch *b, res_mark *m) {
 		m->k = kpost;
 		for (uint32_t j = 1; j < h; j++)
 			m->seq[j] = q->res_posted.seq[j];
-		// ring h: the whole batch, as a batch of one ring
-		const uint64_t sh = q->res_posted.seq[h] + 1;
-		fwd4_res_desc &dh = c->res_desc[(size_t)(q->ring + (int)h) * RES_NDESC + sh % RES_NDESC];
-		A.wg0 = 0;
-		A.wgs = 1;
-		memcpy(&dh.A, &A, sizeof(A));
-		memset(dh.helper_seq, 0, sizeof(dh.helper_seq));
-		__atomic_store_n(&dh.seq, sh, __ATOMIC_RELEASE); // after A
-		q->res_posted.seq[h] = sh;
-		m->seq[h] = sh;
-		// the first ring: no tile of its own, wakes ring h for it
+		// rings h .. h + k - 1: the batch split over k rings, workgroup j
+		// taking tiles j, j + k, ... (helpers wake no one)
+		uint64_t sh[RES_WMAX] = {};
+		for (uint32_t j = 0; j < k; j++) {
+			const uint32_t r = h + j;
+			sh[j] = q->res_posted.seq[r] + 1;
+			fwd4_res_desc &dh = c->res_desc[(size_t)(q->ring + (int)r) * RES_NDESC + sh[j] % RES_NDESC];
+			A.wg0 = j;
+			A.wgs = k;
+			memcpy(&dh.A, &A, sizeof(A));
+			memset(dh.helper_seq, 0, sizeof(dh.helper_seq));
+			__atomic_store_n(&dh.seq, sh[j], __ATOMIC_RELEASE); // after A
+			q->res_posted.seq[r] = sh[j];
+			m->seq[r] = sh[j];
+		}
+		// the first ring: no tile of its own, wakes rings h .. h + k - 1 for it
 		const uint64_t s0 = q->res_posted.seq[0] + 1;
 		fwd4_res_desc &d0 = c->res_desc[(size_t)q->ring * RES_NDESC + s0 % RES_NDESC];
 		A.n = 0;
-		A.wgs = h + 1;
+		A.wg0 = 0;
+		A.wgs = h + k;
 		memcpy(&d0.A, &A, sizeof(A));
 		memset(d0.helper_seq, 0, sizeof(d0.helper_seq));
-		d0.helper_seq[h - 1] = sh;
+		for (uint32_t j = 0; j < k; j++)
+			d0.helper_seq[h + j - 1] = sh[j];
 		__atomic_store_n(&d0.seq, s0, __ATOMIC_RELEASE);
 		q->res_posted.seq[0] = s0;
 		m->seq[0] = s0;
