@@ -523,9 +523,10 @@ int gr_hip_queue_kernel_ms(gr_hip_queue_t *, uint32_t n, float *ms, uint32_t *co
 //   "resident_ms" the kernel leaves once no ring has finished a batch for this
 //               long; the next batch launches it again (default 50)
 //   "resident_launches" (read) resident launches so far
-//   "resident_rotate" 1 = a batch of one ring posted while other batches of
-//               its queue are in flight runs on the queue's next helper ring
-//               in turn, its first ring only waking that one (default 0; the
+//   "resident_rotate" 1 = a batch of k rings posted while other batches of
+//               its queue are in flight runs on the queue's helper rings
+//               h .. h + k - 1, h in turn, its first ring only waking them
+//               (default 0; the
 //               grout module sets it when more than one batch per graph is on
 //               the GPU); "resident_rotating" (read) the setting
 //   "resident_wait_ms" a resident batch not done this long after its post

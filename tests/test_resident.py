@@ -309,12 +309,12 @@ def _deep(q, m, cuts, depth):
 @pytest.mark.gpu
 @pytest.mark.parametrize("wgs,budget", [(8, 32), (3, 32), (8, 2)])
 def test_resident_rotate(knobs, wgs, budget):
-    """Knob "resident_rotate" (the grout node's depth > 2): a batch of one
-    ring posted while others of its queue are in flight runs on the queue's
-    next helper ring, the first ring only waking it. Ragged batches, up to
-    GR_HIP_NODE_DEPTH in flight, rotated over the helpers (and split as
-    usual when large): every walk as the oracle's, in start order, and the
-    queue idle after its last."""
+    """Knob "resident_rotate" (the grout node's depth > 2): a batch of k
+    rings posted while others of its queue are in flight runs on a group of
+    k helper rings in turn, the first ring only waking them. Ragged batches,
+    up to GR_HIP_NODE_DEPTH in flight, rotated over the helpers (those using
+    every ring as usual): every walk as the oracle's, in start order, and
+    the queue idle after its last."""
     from golden_util import fresh_fastpath_state
     fp = knobs
     assert fp.tune("resident_wgs", wgs) == 0 and fp.tune("resident_budget", budget) == 0
