@@ -955,12 +955,12 @@ int gpu_fwd4_set_drain_bound(int32_t batches) {
 // Leaving a graph (grout's worker before it switches to a new graph or shuts
 // down: the graph_leave hook, main_loop.c:466-470 with
 // integration/grout-gpu_fwd4-datapath.patch). grout itself holds no packet
-// across graph walks; the node holds up to two batches. Walks of the graph in
-// DRAIN_HAND_BACK mode hand the batch on the GPU back (waiting for it) and
+// across graph walks; the node holds up to `depth` batches. Walks of the graph in
+// DRAIN_HAND_BACK mode hand the batches on the GPU back (waiting for them) and
 // send the held one, and whatever RX brings meanwhile, synchronously: one walk
 // normally leaves nothing held. The walks are bounded by batches handed back,
 // not by walks: once the batches held at the start and DRAIN_EXTRA more are
-// back (gpu_fwd4_set_drain_bound), one walk in DRAIN_LEAVE mode hands back the batch on the GPU and sends
+// back (gpu_fwd4_set_drain_bound), one walk in DRAIN_LEAVE mode hands back the batches on the GPU and sends
 // what is still held, and what RX brings in that walk, to grout's CPU nodes
 // (PUNT, untouched: forwarded by iface_input_cpu, counted there). Every
 // hand-back went through grout's nodes within its walk, so the batches' QSBR
@@ -991,7 +991,7 @@ static void gpu_fwd4_fini(const struct rte_graph *graph, struct rte_node *node) 
 		if (w == NULL || w->graph != graph)
 			continue;
 		// a graph destroyed without gpu_fwd4_drain: its mbufs go back to the
-		// pool, counted (gpu_fwd4_fini_freed). The batch on the GPU is
+		// pool, counted (gpu_fwd4_fini_freed). A batch on the GPU is
 		// dropped from the queue only once the GPU is done with its frames
 		// (gr_hip_node_finish waits before it refuses a batch appended from
 		// the mbufs)
@@ -1062,7 +1062,7 @@ static uint16_t gpu_flush_process(struct rte_graph *graph, struct rte_node *node
 	// (flush() hands back one more at most, and none is after these)
 	const uint64_t t = now_ns();
 	uint32_t n = 0;
-	// (conf's delay, also under a latency budget: the batch on the GPU is
+	// (conf's delay, also under a latency budget: the oldest batch on the GPU is
 	// reaped as soon as it is back, and a wait here would stall RX)
 	if (w->npend != 0 && (w->draining || t - w->pend_ns[w->head] >= conf.max_delay_ns))
 		n = finish_oldest(graph, node, w); // waited long enough (or leaving the graph): wait for the GPU

@@ -147,7 +147,7 @@ enum {
 	GPU_FWD4_PROF_START, // gr_hip_node_send: launch
 	GPU_FWD4_PROF_FINISH, // gr_hip_node_finish: wait for the GPU, hand-back onto the views
 	GPU_FWD4_PROF_DELIVER, // the views onto the rte_mbufs + private data, enqueues
-	GPU_FWD4_PROF_POLL, // the completion poll of the batch on the GPU (gr_hip_node_pending)
+	GPU_FWD4_PROF_POLL, // the completion poll of the oldest batch on the GPU (gr_hip_node_pending)
 	GPU_FWD4_PROF_FLUSH_NODE, // the flush source node's whole call (its hand-backs and flushes included)
 	GPU_FWD4_PROF_COUNT,
 };
@@ -191,7 +191,7 @@ int gpu_fwd4_stats_flush(const struct rte_graph *, unsigned lcore_id, gpu_fwd4_n
 // module registers, main_loop.c:466-470 with
 // integration/grout-gpu_fwd4-datapath.patch). The node holds up to two
 // batches across graph walks, grout nothing: walks of the graph hand them
-// back through grout's nodes (the batch on the GPU waited for, the held one
+// back through grout's nodes (the batches on the GPU waited for, the held one
 // sent at once), bounded by batches handed back (those held at the start +
 // 2, or gpu_fwd4_set_drain_bound's); past the bound the held mbufs,
 // and those RX brings in the last walk, go to grout's CPU nodes (PUNT). The
@@ -205,7 +205,7 @@ int gpu_fwd4_drain(struct rte_graph *);
 int gpu_fwd4_set_drain_bound(int32_t batches);
 // grout's housekeeping tick asks every datapath hook what it holds (the
 // holding hook integration/grout-gpu_fwd4-datapath.patch adds): the mbufs the
-// node holds in `graph` (accumulating, and the batch on the GPU) plus its
+// node holds in `graph` (accumulating, and the batches on the GPU) plus its
 // QSBR readers still online (they go offline at the next walk). While it is
 // not 0, grout's worker neither micro-sleeps nor blocks on its RX interrupts
 // (main_loop.c:478-508): the flush node's walks hand the batches back, and
